@@ -1,0 +1,181 @@
+/*
+ * mrec.h -- C ABI of libmrec.so, the MI355X (gfx950) embedding-lookup +
+ * feature-interaction hot path.
+ *
+ * The reference (Troublem1/PyTorchRec) is pure Python; its hot path is the ATen
+ * op sites listed in SURVEY.md §2b, reached from IModel.train_step
+ * (torchrec/model/IModel.py:116-125).  Each entry point below names the
+ * reference interface it replaces.  The Python side (pytorchrec_amd/_mrec.py)
+ * binds these with ctypes; INTEGRATION.md shows the binding.
+ *
+ * Conventions (all entry points):
+ *   - Every buffer is a caller-owned device pointer (torch caching allocator).
+ *     The library keeps no pointer past return and allocates nothing; scratch
+ *     is passed in as a workspace sized by a *_workspace_size query.
+ *   - Arrays documented as HOST are read during the call only.
+ *   - Work is enqueued on `stream` (a hipStream_t); no call synchronises the
+ *     device, so every call is safe inside hipStreamBeginCapture (hipGraphs).
+ *   - Return value is an mrec_status; on error mrec_last_error() (thread-local)
+ *     describes it.  No C++ exception crosses the ABI.
+ *   - Out-of-range ids never fault: the kernel substitutes a zero row (forward)
+ *     or skips the lookup (backward) and sets *d_oob_flag (device int32, may be
+ *     NULL) to 1.  The Python wrapper turns the flag into IndexError in its
+ *     checked mode, matching nn.Embedding.
+ */
+#ifndef MREC_H
+#define MREC_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define MREC_ABI_VERSION 1
+#define MREC_MAX_TABLES 64      /* tables per table bank / per call */
+#define MREC_BWD_MAX_BATCH 16384 /* lookups per table per plan/apply call */
+
+typedef enum {
+  MREC_OK = 0,
+  MREC_EINVAL = 1, /* bad argument (null pointer, size, dtype combination) */
+  MREC_EOOB = 2,   /* reserved: host-detected out-of-range id */
+  MREC_EHIP = 3,   /* HIP runtime error (launch failure, ...) */
+  MREC_ERCCL = 4,  /* reserved for RCCL errors */
+  MREC_ENOSPC = 5  /* workspace too small */
+} mrec_status;
+
+typedef enum { MREC_F32 = 0, MREC_BF16 = 1, MREC_I32 = 2, MREC_I64 = 3 } mrec_dtype;
+
+typedef void *mrec_stream; /* hipStream_t */
+
+/*
+ * A table bank: F embedding tables packed row-wise into one device buffer
+ * [total_rows, row_stride] of `dtype`.  Table f occupies rows
+ * [row_offset[f], row_offset[f] + rows[f]).  Row r holds the embedding
+ * v[0..dim) and, when has_w, the first-order weight w at column `dim`
+ * (SURVEY.md §7 hard part 1: "[v(16) | w | pad]").  row_stride*sizeof(dtype)
+ * must be a power of two in [16, 256] bytes (64 B for bf16 D=16 + w).
+ * Replaces F x torch.nn.Embedding(rows_f, dim) (+ Embedding(rows_f, 1) biases)
+ * built in IModel._init_weights (FunkSVD.py:39-41, SVDPP.py:36-42).
+ */
+typedef struct {
+  void *data;                 /* device */
+  const int64_t *row_offset;  /* HOST [n_tables] */
+  const int64_t *rows;        /* HOST [n_tables] */
+  int32_t n_tables;
+  int32_t dim;
+  int32_t row_stride; /* elements */
+  int32_t has_w;
+  mrec_dtype dtype; /* MREC_F32 or MREC_BF16 */
+} mrec_table_bank;
+
+/*
+ * Per-field categorical ids: field f of sample b is at
+ * field_ptr[f][b * stride] (int32 or int64).  field_ptr is a HOST array of
+ * n_tables device pointers, so the batch dict's per-feature tensors
+ * (CategoricalColumnWithIdentity.get_feature_data, .py:20-22) are read in place
+ * and a stacked [B, F] tensor is field_ptr[f] = base + f, stride = F.
+ */
+typedef struct {
+  const void *const *field_ptr; /* HOST [n_tables] of device pointers */
+  mrec_dtype dtype;             /* MREC_I32 or MREC_I64 */
+  int64_t stride;               /* elements between samples */
+} mrec_ids;
+
+int mrec_abi_version(void);
+const char *mrec_last_error(void);
+
+/* ------------------------------------------------------------------------- */
+/* Forward                                                                   */
+/* ------------------------------------------------------------------------- */
+
+/*
+ * Multi-table gather: out[b, f*dim + d] = bank[row_offset[f] + id[f][b], d]
+ * (bit-exact copy when out_dtype == bank dtype; bf16->f32 widening is exact).
+ * Row stride of `out` is out_ld elements.  If w_out != NULL (bank must have_w)
+ * w_out[b*n_tables + f] = w (fp32).
+ * Replaces nn.Embedding forward = aten::embedding -> index_select
+ * (FunkSVD.py:47-48, NCF.py:62-65).
+ */
+mrec_status mrec_emb_gather_fwd(const mrec_table_bank *bank, const mrec_ids *ids, int64_t batch,
+                                void *out, mrec_dtype out_dtype, int64_t out_ld, float *w_out,
+                                int32_t *d_oob_flag, mrec_stream stream);
+
+/* flags for mrec_interact_fwd */
+#define MREC_INTERACT_FM2 1         /* add 1/2 sum_d[(sum_f v)^2 - sum_f v^2] */
+#define MREC_INTERACT_FIRST_ORDER 2 /* add sum_f w[id_f] (bank must have_w) */
+
+/*
+ * Fused gather + interaction + deep-input builder, one wave per sample, the
+ * per-sample [F, D] block held in registers and reduced with wave shuffles:
+ *   x0[b, :]   = [ v_0 .. v_{F-1} (F*dim) | dense[b, 0..n_dense) | 0 .. ]   (x0_cols wide)
+ *   logit[b]   = bias + dense[b].dense_w + (FM2 ? fm2(v) : 0) + (FIRST_ORDER ? sum_f w : 0)
+ *   fm_sum[b,:] = sum_f v_f   (fp32, saved for the backward; may be NULL)
+ * x0 may be NULL (pure FM, config C1); dense/dense_w may be NULL when n_dense==0;
+ * bias is a device float[1] (may be NULL = 0).  x0_dtype F32 or BF16.
+ * Replaces: nn.Embedding gathers + torch.cat + the FM mul/sum + bias
+ * embeddings (FunkSVD.py:47-51, SVDPP.py:57-66, NCF.py:62-70).
+ */
+mrec_status mrec_interact_fwd(const mrec_table_bank *bank, const mrec_ids *ids, int64_t batch,
+                              const float *dense, int32_t n_dense, int64_t dense_ld,
+                              const float *dense_w, const float *bias, int32_t flags, void *x0,
+                              mrec_dtype x0_dtype, int64_t x0_ld, int32_t x0_cols, float *logit,
+                              float *fm_sum, int32_t *d_oob_flag, mrec_stream stream);
+
+/*
+ * Standalone FM second order on a dense [B, F, D] fp32 tensor (row-major),
+ * y[b] = 1/2 sum_d[(sum_f v)^2 - sum_f v^2]; bwd dv = dy[b] (S_d - v_fd).
+ * FunkSVD.py:51 is the F = 2 case.
+ */
+mrec_status mrec_fm2_fwd(const float *v, int64_t batch, int32_t fields, int32_t dim, float *y,
+                         mrec_stream stream);
+mrec_status mrec_fm2_bwd(const float *v, const float *dy, int64_t batch, int32_t fields,
+                         int32_t dim, float *dv, mrec_stream stream);
+
+/* ------------------------------------------------------------------------- */
+/* Backward: embedding scatter-add                                           */
+/* ------------------------------------------------------------------------- */
+
+typedef enum {
+  MREC_BWD_DENSE_GRAD = 0, /* grad[row] += sum g  (grad laid out like the bank, dtype of bank;
+                              caller zero-fills; == aten::embedding_dense_backward) */
+  MREC_BWD_SGD = 1,        /* bank[row] -= lr * sum g, round-to-nearest-even */
+  MREC_BWD_SGD_SR = 2      /* bank[row] -= lr * sum g, stochastic rounding (bf16 banks) */
+} mrec_bwd_mode;
+
+/*
+ * Bytes of workspace mrec_emb_bwd needs for `batch` lookups per table.
+ */
+size_t mrec_emb_bwd_workspace_size(int32_t n_tables, int64_t batch);
+
+/*
+ * Deterministic sorted-segment plan: per table, the lookups are sorted by
+ * (id, sample) in LDS and segmented by unique row.  Depends only on the ids, so
+ * it can run on a side stream as soon as the batch is resident.
+ */
+mrec_status mrec_emb_bwd_plan(const mrec_table_bank *bank, const mrec_ids *ids, int64_t batch,
+                              void *workspace, size_t ws_bytes, int32_t *d_oob_flag,
+                              mrec_stream stream);
+
+/*
+ * Gradient sources of lookup (b, f) (each may be NULL = 0):
+ *   g_v[d] = dx[b, f*dim + d]                                (dx: F32/BF16, row stride dx_ld)
+ *          + dfm[b] * (fm_sum[b, d] - v[b, f*dim + d])      (FM2 backward; v read from x0)
+ *   g_w    = dw[b]                                          (first-order backward)
+ * Segment sums are fp32 in ascending sample order (bitwise reproducible), then
+ * applied per unique row as `mode` says.  `seed` drives stochastic rounding.
+ * Replaces aten::embedding_dense_backward + the dense optimizer step
+ * (IModel.py:120-124).
+ */
+mrec_status mrec_emb_bwd_apply(const mrec_table_bank *bank, int64_t batch, const void *workspace,
+                               size_t ws_bytes, const void *dx, mrec_dtype dx_dtype, int64_t dx_ld,
+                               const float *dfm, const float *fm_sum, const void *x0,
+                               mrec_dtype x0_dtype, int64_t x0_ld, const float *dw,
+                               mrec_bwd_mode mode, float lr, uint64_t seed, void *grad,
+                               mrec_stream stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* MREC_H */

@@ -1,0 +1,208 @@
+"""ctypes binding of libmrec.so (the C ABI declared in include/mrec.h).
+
+The library is built in-tree (``pytorchrec_amd/lib/libmrec.so``, see
+``pytorchrec_amd/build.py``).  There is deliberately no fallback: any op that
+runs on a GPU tensor goes through this library, and if the library is missing
+the call raises ``MrecUnavailable`` instead of silently running something else.
+
+``torch`` must be imported before the library is loaded so that the HIP runtime
+torch ships (SONAME libamdhip64.so.7) is the one libmrec binds to — one runtime
+per process, shared streams and device pointers.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+import threading
+
+import torch  # noqa: F401  (must precede the dlopen, see module docstring)
+
+LIB_DIR = os.path.join(os.path.dirname(os.path.abspath(__file__)), "lib")
+LIB_PATH = os.path.join(LIB_DIR, "libmrec.so")
+
+ABI_VERSION = 1
+MAX_TABLES = 64
+BWD_MAX_BATCH = 16384
+
+# mrec_status
+OK, EINVAL, EOOB, EHIP, ERCCL, ENOSPC = range(6)
+# mrec_dtype
+F32, BF16, I32, I64 = 0, 1, 2, 3
+# interact flags
+INTERACT_FM2 = 1
+INTERACT_FIRST_ORDER = 2
+# bwd modes
+BWD_DENSE_GRAD, BWD_SGD, BWD_SGD_SR = 0, 1, 2
+
+_STATUS_NAMES = {OK: "MREC_OK", EINVAL: "MREC_EINVAL", EOOB: "MREC_EOOB", EHIP: "MREC_EHIP",
+                 ERCCL: "MREC_ERCCL", ENOSPC: "MREC_ENOSPC"}
+
+
+class MrecUnavailable(RuntimeError):
+    """libmrec.so is missing or unloadable: the HIP path cannot run."""
+
+
+class MrecError(RuntimeError):
+    def __init__(self, fn, status, msg):
+        super().__init__(f"{fn} failed: {_STATUS_NAMES.get(status, status)}: {msg}")
+        self.status = status
+
+
+class TableBank(ctypes.Structure):
+    _fields_ = [("data", ctypes.c_void_p),
+                ("row_offset", ctypes.POINTER(ctypes.c_int64)),
+                ("rows", ctypes.POINTER(ctypes.c_int64)),
+                ("n_tables", ctypes.c_int32),
+                ("dim", ctypes.c_int32),
+                ("row_stride", ctypes.c_int32),
+                ("has_w", ctypes.c_int32),
+                ("dtype", ctypes.c_int)]
+
+
+class Ids(ctypes.Structure):
+    _fields_ = [("field_ptr", ctypes.POINTER(ctypes.c_void_p)),
+                ("dtype", ctypes.c_int),
+                ("stride", ctypes.c_int64)]
+
+
+_vp = ctypes.c_void_p
+_i32 = ctypes.c_int32
+_i64 = ctypes.c_int64
+_f32 = ctypes.c_float
+_fp = ctypes.POINTER(ctypes.c_float)
+_bank_p = ctypes.POINTER(TableBank)
+_ids_p = ctypes.POINTER(Ids)
+
+# name -> (restype, argtypes); the set the header declares (checked by tests)
+SIGNATURES = {
+    "mrec_abi_version": (ctypes.c_int, []),
+    "mrec_last_error": (ctypes.c_char_p, []),
+    "mrec_emb_gather_fwd": (ctypes.c_int, [_bank_p, _ids_p, _i64, _vp, ctypes.c_int, _i64, _vp,
+                                           _vp, _vp]),
+    "mrec_interact_fwd": (ctypes.c_int, [_bank_p, _ids_p, _i64, _vp, _i32, _i64, _vp, _vp, _i32,
+                                         _vp, ctypes.c_int, _i64, _i32, _vp, _vp, _vp, _vp]),
+    "mrec_fm2_fwd": (ctypes.c_int, [_vp, _i64, _i32, _i32, _vp, _vp]),
+    "mrec_fm2_bwd": (ctypes.c_int, [_vp, _vp, _i64, _i32, _i32, _vp, _vp]),
+    "mrec_emb_bwd_workspace_size": (ctypes.c_size_t, [_i32, _i64]),
+    "mrec_emb_bwd_plan": (ctypes.c_int, [_bank_p, _ids_p, _i64, _vp, ctypes.c_size_t, _vp, _vp]),
+    "mrec_emb_bwd_apply": (ctypes.c_int, [_bank_p, _i64, _vp, ctypes.c_size_t, _vp, ctypes.c_int,
+                                          _i64, _vp, _vp, _vp, ctypes.c_int, _i64, _vp,
+                                          ctypes.c_int, _f32, ctypes.c_uint64, _vp, _vp]),
+}
+
+_lib = None
+_lock = threading.Lock()
+
+
+def lib():
+    """Load (once) and return the ctypes handle; raise MrecUnavailable if absent."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    with _lock:
+        if _lib is not None:
+            return _lib
+        if not os.path.exists(LIB_PATH):
+            raise MrecUnavailable(
+                f"{LIB_PATH} not found: build it with `python -c 'import __graft_entry__ as g; "
+                f"g.build()'` (hipcc --offload-arch=gfx950). There is no CPU fallback.")
+        try:
+            handle = ctypes.CDLL(LIB_PATH, mode=ctypes.RTLD_GLOBAL)
+        except OSError as e:
+            raise MrecUnavailable(f"cannot load {LIB_PATH}: {e}") from e
+        for name, (res, args) in SIGNATURES.items():
+            fn = getattr(handle, name)
+            fn.restype = res
+            fn.argtypes = args
+        v = handle.mrec_abi_version()
+        if v != ABI_VERSION:
+            raise MrecUnavailable(f"libmrec ABI {v} != expected {ABI_VERSION}; rebuild it")
+        _lib = handle
+        return _lib
+
+
+def available() -> bool:
+    try:
+        lib()
+        return True
+    except MrecUnavailable:
+        return False
+
+
+def check(fn_name: str, status: int):
+    if status != OK:
+        msg = lib().mrec_last_error()
+        raise MrecError(fn_name, status, msg.decode() if msg else "")
+
+
+def call(fn_name: str, *args):
+    check(fn_name, getattr(lib(), fn_name)(*args))
+
+
+def stream_handle(device=None) -> int:
+    return torch.cuda.current_stream(device).cuda_stream
+
+
+def dtype_code(t: torch.dtype) -> int:
+    if t == torch.float32:
+        return F32
+    if t == torch.bfloat16:
+        return BF16
+    if t == torch.int32:
+        return I32
+    if t == torch.int64:
+        return I64
+    raise TypeError(f"unsupported dtype for libmrec: {t}")
+
+
+def ptr(t) -> int | None:
+    return None if t is None else t.data_ptr()
+
+
+class BankDesc:
+    """Keeps the ctypes TableBank and its host arrays alive."""
+
+    def __init__(self, weight: torch.Tensor, row_offset, rows, dim: int, has_w: bool):
+        n = len(rows)
+        if n > MAX_TABLES:
+            raise ValueError(f"at most {MAX_TABLES} tables per bank")
+        self._off = (ctypes.c_int64 * n)(*[int(x) for x in row_offset])
+        self._rows = (ctypes.c_int64 * n)(*[int(x) for x in rows])
+        self.weight = weight
+        self.struct = TableBank(weight.data_ptr(), self._off, self._rows, n, int(dim),
+                                int(weight.shape[1]), int(bool(has_w)), dtype_code(weight.dtype))
+
+    def ref(self):
+        self.struct.data = self.weight.data_ptr()
+        return ctypes.byref(self.struct)
+
+
+class IdsDesc:
+    """Per-field id tensors (each [B] contiguous, or columns of a [B, F] tensor)."""
+
+    def __init__(self, fields, stacked: torch.Tensor | None = None):
+        if stacked is not None:
+            n = stacked.shape[1]
+            base = stacked.data_ptr()
+            es = stacked.element_size()
+            self.tensors = [stacked]
+            ptrs = [base + f * es for f in range(n)]
+            stride = stacked.stride(0)
+            dt = stacked.dtype
+            if stacked.stride(1) != 1:
+                raise ValueError("stacked ids must be contiguous along fields")
+        else:
+            self.tensors = list(fields)
+            n = len(self.tensors)
+            dt = self.tensors[0].dtype
+            for t in self.tensors:
+                if t.dtype != dt or t.dim() != 1 or (t.numel() > 1 and t.stride(0) != 1):
+                    raise ValueError("per-field ids must be 1-D contiguous tensors of one dtype")
+            ptrs = [t.data_ptr() for t in self.tensors]
+            stride = 1
+        self._ptrs = (ctypes.c_void_p * n)(*ptrs)
+        self.struct = Ids(ctypes.cast(self._ptrs, ctypes.POINTER(ctypes.c_void_p)),
+                          dtype_code(dt), int(stride))
+
+    def ref(self):
+        return ctypes.byref(self.struct)

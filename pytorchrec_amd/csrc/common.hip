@@ -1,0 +1,77 @@
+// Host-side helpers and the ABI identity functions of libmrec.
+#include "common.h"
+
+namespace mrec {
+
+static thread_local std::string g_last_error;
+
+void set_error(const std::string &msg) { g_last_error = msg; }
+
+mrec_status launch_status(const char *what) {
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess) {
+    set_error(std::string(what) + ": " + hipGetErrorString(e));
+    return MREC_EHIP;
+  }
+  return MREC_OK;
+}
+
+static bool pow2(int64_t x) { return x > 0 && (x & (x - 1)) == 0; }
+
+mrec_status make_bank_args(const mrec_table_bank *bank, BankArgs *out, int *elem_bytes,
+                           int *lanes_per_row) {
+  MREC_CHECK_ARG(bank != nullptr, "bank is NULL");
+  MREC_CHECK_ARG(bank->data != nullptr, "bank->data is NULL");
+  MREC_CHECK_ARG(bank->row_offset != nullptr && bank->rows != nullptr,
+                 "bank->row_offset/rows is NULL");
+  MREC_CHECK_ARG(bank->n_tables >= 1 && bank->n_tables <= MREC_MAX_TABLES,
+                 "n_tables out of [1, MREC_MAX_TABLES]");
+  MREC_CHECK_ARG(bank->dtype == MREC_F32 || bank->dtype == MREC_BF16, "bank dtype must be F32/BF16");
+  const int eb = bank->dtype == MREC_F32 ? 4 : 2;
+  const int epl = 16 / eb;
+  MREC_CHECK_ARG(bank->dim >= epl && bank->dim % epl == 0,
+                 "dim must be a positive multiple of 16 bytes' worth of elements");
+  MREC_CHECK_ARG(bank->row_stride >= bank->dim + (bank->has_w ? 1 : 0), "row_stride too small");
+  const int64_t row_bytes = static_cast<int64_t>(bank->row_stride) * eb;
+  MREC_CHECK_ARG(pow2(row_bytes) && row_bytes >= 16 && row_bytes <= 256,
+                 "row_stride*elem_size must be a power of two in [16, 256] bytes");
+  MREC_CHECK_ARG((reinterpret_cast<uintptr_t>(bank->data) & 15) == 0, "bank->data not 16B aligned");
+  out->data = static_cast<char *>(bank->data);
+  for (int f = 0; f < bank->n_tables; ++f) {
+    MREC_CHECK_ARG(bank->row_offset[f] >= 0 && bank->rows[f] >= 0, "negative row_offset/rows");
+    out->row_offset[f] = bank->row_offset[f];
+    out->rows[f] = bank->rows[f];
+  }
+  for (int f = bank->n_tables; f < MREC_MAX_TABLES; ++f) out->row_offset[f] = out->rows[f] = 0;
+  out->n_tables = bank->n_tables;
+  out->dim = bank->dim;
+  out->row_stride = bank->row_stride;
+  out->has_w = bank->has_w ? 1 : 0;
+  *elem_bytes = eb;
+  *lanes_per_row = static_cast<int>(row_bytes / 16);
+  return MREC_OK;
+}
+
+mrec_status make_ids_args(const mrec_ids *ids, int n_tables, IdsArgs *out) {
+  MREC_CHECK_ARG(ids != nullptr && ids->field_ptr != nullptr, "ids / ids->field_ptr is NULL");
+  MREC_CHECK_ARG(ids->dtype == MREC_I32 || ids->dtype == MREC_I64, "ids dtype must be I32/I64");
+  MREC_CHECK_ARG(ids->stride >= 1, "ids stride must be >= 1");
+  for (int f = 0; f < n_tables; ++f) {
+    MREC_CHECK_ARG(ids->field_ptr[f] != nullptr, "ids field pointer is NULL");
+    out->ptr[f] = ids->field_ptr[f];
+  }
+  for (int f = n_tables; f < MREC_MAX_TABLES; ++f) out->ptr[f] = nullptr;
+  out->stride = ids->stride;
+  out->is64 = ids->dtype == MREC_I64 ? 1 : 0;
+  return MREC_OK;
+}
+
+}  // namespace mrec
+
+extern "C" {
+
+int mrec_abi_version(void) { return MREC_ABI_VERSION; }
+
+const char *mrec_last_error(void) { return mrec::g_last_error.c_str(); }
+
+}  // extern "C"

@@ -1,0 +1,379 @@
+// Forward kernels: multi-table gather, fused gather + FM + first-order + deep
+// input builder, standalone FM2.
+//
+// Row access: a table row is 16..256 bytes (a power of two), read by a "worker"
+// of LPR = row_bytes/16 consecutive lanes with one 16-byte load each, so one
+// wave-instruction reads 64/LPR whole rows, each as one contiguous request.
+#include "common.h"
+
+namespace mrec {
+
+// ---------------------------------------------------------------------------
+// plain gather: worker per (b, f) lookup
+// ---------------------------------------------------------------------------
+template <typename T, typename O, int LPR>
+__global__ __launch_bounds__(256) void gather_kernel(BankArgs bank, IdsArgs ids, int64_t B,
+                                                     O *__restrict__ out, int64_t out_ld,
+                                                     float *__restrict__ w_out,
+                                                     int32_t *__restrict__ oob) {
+  constexpr int EPL = Vec<T>::EPL;
+  constexpr int WPB = 256 / LPR;
+  const int F = bank.n_tables;
+  const int64_t g = static_cast<int64_t>(blockIdx.x) * WPB + threadIdx.x / LPR;
+  const int l = threadIdx.x % LPR;
+  if (g >= B * F) return;
+  const int64_t b = g / F;
+  const int f = static_cast<int>(g - b * F);
+  const int64_t id = load_id(ids, f, b);
+  const bool ok = id >= 0 && id < bank.rows[f];
+  uint4 raw = make_uint4(0, 0, 0, 0);
+  if (ok) {
+    const T *row = reinterpret_cast<const T *>(bank.data) +
+                   (bank.row_offset[f] + id) * static_cast<int64_t>(bank.row_stride);
+    raw = *reinterpret_cast<const uint4 *>(row + l * EPL);
+  } else if (l == 0 && oob) {
+    *oob = 1;
+  }
+  const int D = bank.dim;
+  const int e0 = l * EPL;
+  if (e0 + EPL <= D) {
+    O *dst = out + b * out_ld + static_cast<int64_t>(f) * D + e0;
+    if constexpr (sizeof(O) == sizeof(T)) {
+      *reinterpret_cast<uint4 *>(dst) = raw;  // bit copy
+    } else {
+      float v[EPL];
+      Vec<T>::to_f32(raw, v);
+      if constexpr (sizeof(O) == 4) {  // widen bf16 -> f32 (exact)
+#pragma unroll
+        for (int j = 0; j < EPL; j += 4)
+          *reinterpret_cast<float4 *>(dst + j) = make_float4(v[j], v[j + 1], v[j + 2], v[j + 3]);
+      } else {  // narrow f32 -> bf16 (RNE)
+        *reinterpret_cast<uint2 *>(dst) = make_uint2(pack_bf16x2(v[0], v[1]), pack_bf16x2(v[2], v[3]));
+      }
+    }
+  } else if (w_out && bank.has_w && e0 == D) {
+    float v[EPL];
+    Vec<T>::to_f32(raw, v);
+    w_out[b * F + f] = v[0];
+  }
+}
+
+// ---------------------------------------------------------------------------
+// fused interaction: one wave per sample
+// ---------------------------------------------------------------------------
+template <typename T, int LPR, bool X0_BF16>
+__global__ __launch_bounds__(256) void interact_kernel(
+    BankArgs bank, IdsArgs ids, int64_t B, const float *__restrict__ dense, int n_dense,
+    int64_t dense_ld, const float *__restrict__ dense_w, const float *__restrict__ bias, int flags,
+    void *__restrict__ x0v, int64_t x0_ld, int x0_cols, float *__restrict__ logit,
+    float *__restrict__ fm_sum, int32_t *__restrict__ oob) {
+  constexpr int EPL = Vec<T>::EPL;
+  constexpr int WPW = 64 / LPR;                             // rows per wave-instruction
+  constexpr int MAXIT = (MREC_MAX_TABLES + WPW - 1) / WPW;  // field iterations
+  const int lane = threadIdx.x & 63;
+  const int64_t b = static_cast<int64_t>(blockIdx.x) * 4 + (threadIdx.x >> 6);
+  if (b >= B) return;
+  const int worker = lane / LPR;
+  const int l = lane % LPR;
+  const int e0 = l * EPL;
+  const int F = bank.n_tables;
+  const int D = bank.dim;
+  const bool v_lane = e0 + EPL <= D;
+  const bool w_lane = bank.has_w && e0 == D;
+
+  // phase 1: issue every row load of this sample before consuming any
+  uint4 raw[MAXIT];
+#pragma unroll
+  for (int it = 0; it < MAXIT; ++it) {
+    raw[it] = make_uint4(0, 0, 0, 0);
+    const int f = it * WPW + worker;
+    if (it * WPW < F && f < F) {
+      const int64_t id = load_id(ids, f, b);
+      if (id >= 0 && id < bank.rows[f]) {
+        const T *row = reinterpret_cast<const T *>(bank.data) +
+                       (bank.row_offset[f] + id) * static_cast<int64_t>(bank.row_stride);
+        raw[it] = *reinterpret_cast<const uint4 *>(row + e0);
+      } else if (l == 0 && oob) {
+        *oob = 1;
+      }
+    }
+  }
+
+  // phase 2: per-lane sums over this lane's fields + deep-input write
+  float s[EPL], q[EPL];
+#pragma unroll
+  for (int j = 0; j < EPL; ++j) s[j] = q[j] = 0.f;
+  float wsum = 0.f;
+#pragma unroll
+  for (int it = 0; it < MAXIT; ++it) {
+    const int f = it * WPW + worker;
+    if (it * WPW >= F || f >= F) continue;
+    float v[EPL];
+    Vec<T>::to_f32(raw[it], v);
+    if (v_lane) {
+#pragma unroll
+      for (int j = 0; j < EPL; ++j) {
+        s[j] += v[j];
+        q[j] = fmaf(v[j], v[j], q[j]);
+      }
+      if (x0v) {
+        const int64_t o = b * x0_ld + static_cast<int64_t>(f) * D + e0;
+        if constexpr (X0_BF16) {
+          uint16_t *dst = static_cast<uint16_t *>(x0v) + o;
+          if constexpr (sizeof(T) == 2) {
+            *reinterpret_cast<uint4 *>(dst) = raw[it];
+          } else {
+            *reinterpret_cast<uint2 *>(dst) =
+                make_uint2(pack_bf16x2(v[0], v[1]), pack_bf16x2(v[2], v[3]));
+          }
+        } else {
+          float *dst = static_cast<float *>(x0v) + o;
+#pragma unroll
+          for (int j = 0; j < EPL; j += 4)
+            *reinterpret_cast<float4 *>(dst + j) = make_float4(v[j], v[j + 1], v[j + 2], v[j + 3]);
+        }
+      }
+    } else if (w_lane) {
+      wsum += v[0];
+    }
+  }
+
+  // reduce over workers (lanes with equal l)
+#pragma unroll
+  for (int off = LPR; off < 64; off <<= 1) {
+#pragma unroll
+    for (int j = 0; j < EPL; ++j) {
+      s[j] += __shfl_xor(s[j], off);
+      q[j] += __shfl_xor(q[j], off);
+    }
+    wsum += __shfl_xor(wsum, off);
+  }
+  float fm = 0.f;
+  if (v_lane) {
+#pragma unroll
+    for (int j = 0; j < EPL; ++j) fm += s[j] * s[j] - q[j];
+  }
+#pragma unroll
+  for (int off = 1; off < LPR; off <<= 1) {
+    fm += __shfl_xor(fm, off);
+    wsum += __shfl_xor(wsum, off);
+  }
+  if (fm_sum && worker == 0 && v_lane) {
+    float *dst = fm_sum + b * D + e0;
+#pragma unroll
+    for (int j = 0; j < EPL; j += 4)
+      *reinterpret_cast<float4 *>(dst + j) = make_float4(s[j], s[j + 1], s[j + 2], s[j + 3]);
+  }
+
+  // dense features: first-order dot + copy into x0, zero the pad columns
+  float ds = 0.f;
+  for (int j = lane; j < n_dense; j += 64) ds = fmaf(dense[b * dense_ld + j], dense_w[j], ds);
+#pragma unroll
+  for (int off = 1; off < 64; off <<= 1) ds += __shfl_xor(ds, off);
+  if (x0v) {
+    const int base = F * D;
+    for (int c = base + lane; c < x0_cols; c += 64) {
+      const float x = (c - base < n_dense) ? dense[b * dense_ld + (c - base)] : 0.f;
+      if constexpr (X0_BF16)
+        static_cast<uint16_t *>(x0v)[b * x0_ld + c] = f32_to_bf16_rne(x);
+      else
+        static_cast<float *>(x0v)[b * x0_ld + c] = x;
+    }
+  }
+  if (lane == 0 && logit) {
+    float y = (bias ? bias[0] : 0.f) + ds;
+    if (flags & MREC_INTERACT_FM2) y += 0.5f * fm;
+    if (flags & MREC_INTERACT_FIRST_ORDER) y += wsum;
+    logit[b] = y;
+  }
+}
+
+// ---------------------------------------------------------------------------
+// standalone FM2 on [B, F, D] fp32: one wave per sample, lanes over d
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void fm2_fwd_kernel(const float *__restrict__ v, int64_t B,
+                                                      int F, int D, float *__restrict__ y) {
+  const int lane = threadIdx.x & 63;
+  const int64_t b = static_cast<int64_t>(blockIdx.x) * 4 + (threadIdx.x >> 6);
+  if (b >= B) return;
+  const float *vb = v + b * F * D;
+  float acc = 0.f;
+  for (int d = lane; d < D; d += 64) {
+    float s = 0.f, q = 0.f;
+    for (int f = 0; f < F; ++f) {
+      const float x = vb[f * D + d];
+      s += x;
+      q = fmaf(x, x, q);
+    }
+    acc += s * s - q;
+  }
+#pragma unroll
+  for (int off = 1; off < 64; off <<= 1) acc += __shfl_xor(acc, off);
+  if (lane == 0) y[b] = 0.5f * acc;
+}
+
+__global__ __launch_bounds__(256) void fm2_bwd_kernel(const float *__restrict__ v,
+                                                      const float *__restrict__ dy, int64_t B,
+                                                      int F, int D, float *__restrict__ dv) {
+  const int lane = threadIdx.x & 63;
+  const int64_t b = static_cast<int64_t>(blockIdx.x) * 4 + (threadIdx.x >> 6);
+  if (b >= B) return;
+  const float *vb = v + b * F * D;
+  float *gb = dv + b * F * D;
+  const float g = dy[b];
+  for (int d = lane; d < D; d += 64) {
+    float s = 0.f;
+    for (int f = 0; f < F; ++f) s += vb[f * D + d];
+    for (int f = 0; f < F; ++f) gb[f * D + d] = g * (s - vb[f * D + d]);
+  }
+}
+
+// ---------------------------------------------------------------------------
+// dispatch helpers
+// ---------------------------------------------------------------------------
+template <typename T, typename O>
+static void launch_gather(int lpr, const BankArgs &ba, const IdsArgs &ia, int64_t B, void *out,
+                          int64_t out_ld, float *w_out, int32_t *oob, hipStream_t s) {
+  const int64_t work = B * ba.n_tables;
+  const int wpb = 256 / lpr;
+  const dim3 grid(static_cast<unsigned>((work + wpb - 1) / wpb));
+  O *o = static_cast<O *>(out);
+  switch (lpr) {
+    case 1: gather_kernel<T, O, 1><<<grid, 256, 0, s>>>(ba, ia, B, o, out_ld, w_out, oob); break;
+    case 2: gather_kernel<T, O, 2><<<grid, 256, 0, s>>>(ba, ia, B, o, out_ld, w_out, oob); break;
+    case 4: gather_kernel<T, O, 4><<<grid, 256, 0, s>>>(ba, ia, B, o, out_ld, w_out, oob); break;
+    case 8: gather_kernel<T, O, 8><<<grid, 256, 0, s>>>(ba, ia, B, o, out_ld, w_out, oob); break;
+    default: gather_kernel<T, O, 16><<<grid, 256, 0, s>>>(ba, ia, B, o, out_ld, w_out, oob); break;
+  }
+}
+
+template <typename T, bool XB>
+static void launch_interact(int lpr, const BankArgs &ba, const IdsArgs &ia, int64_t B,
+                            const float *dense, int n_dense, int64_t dense_ld, const float *dense_w,
+                            const float *bias, int flags, void *x0, int64_t x0_ld, int x0_cols,
+                            float *logit, float *fm_sum, int32_t *oob, hipStream_t s) {
+  const dim3 grid(static_cast<unsigned>((B + 3) / 4));
+#define MREC_IK(L)                                                                          \
+  interact_kernel<T, L, XB><<<grid, 256, 0, s>>>(ba, ia, B, dense, n_dense, dense_ld, dense_w, \
+                                                 bias, flags, x0, x0_ld, x0_cols, logit,       \
+                                                 fm_sum, oob)
+  switch (lpr) {
+    case 1: MREC_IK(1); break;
+    case 2: MREC_IK(2); break;
+    case 4: MREC_IK(4); break;
+    case 8: MREC_IK(8); break;
+    default: MREC_IK(16); break;
+  }
+#undef MREC_IK
+}
+
+}  // namespace mrec
+
+using namespace mrec;
+
+extern "C" {
+
+mrec_status mrec_emb_gather_fwd(const mrec_table_bank *bank, const mrec_ids *ids, int64_t batch,
+                                void *out, mrec_dtype out_dtype, int64_t out_ld, float *w_out,
+                                int32_t *d_oob_flag, mrec_stream stream) {
+  BankArgs ba;
+  IdsArgs ia;
+  int eb, lpr;
+  mrec_status st = make_bank_args(bank, &ba, &eb, &lpr);
+  if (st != MREC_OK) return st;
+  if ((st = make_ids_args(ids, ba.n_tables, &ia)) != MREC_OK) return st;
+  MREC_CHECK_ARG(batch >= 0, "batch < 0");
+  MREC_CHECK_ARG(out != nullptr, "out is NULL");
+  MREC_CHECK_ARG(out_dtype == MREC_F32 || out_dtype == MREC_BF16, "out dtype must be F32/BF16");
+  const int ob = out_dtype == MREC_F32 ? 4 : 2;
+  MREC_CHECK_ARG(out_ld >= static_cast<int64_t>(ba.n_tables) * ba.dim, "out_ld < n_tables*dim");
+  MREC_CHECK_ARG((reinterpret_cast<uintptr_t>(out) & 15) == 0 && (out_ld * ob) % 16 == 0 &&
+                     (ba.dim * ob) % 16 == 0,
+                 "out must be 16B aligned with 16B-multiple rows");
+  MREC_CHECK_ARG(w_out == nullptr || ba.has_w, "w_out requested but bank has no w column");
+  if (batch == 0) return MREC_OK;
+  hipStream_t s = static_cast<hipStream_t>(stream);
+  if (bank->dtype == MREC_BF16) {
+    if (out_dtype == MREC_BF16)
+      launch_gather<uint16_t, uint16_t>(lpr, ba, ia, batch, out, out_ld, w_out, d_oob_flag, s);
+    else
+      launch_gather<uint16_t, float>(lpr, ba, ia, batch, out, out_ld, w_out, d_oob_flag, s);
+  } else {
+    if (out_dtype == MREC_BF16)
+      launch_gather<float, uint16_t>(lpr, ba, ia, batch, out, out_ld, w_out, d_oob_flag, s);
+    else
+      launch_gather<float, float>(lpr, ba, ia, batch, out, out_ld, w_out, d_oob_flag, s);
+  }
+  return launch_status("mrec_emb_gather_fwd");
+}
+
+mrec_status mrec_interact_fwd(const mrec_table_bank *bank, const mrec_ids *ids, int64_t batch,
+                              const float *dense, int32_t n_dense, int64_t dense_ld,
+                              const float *dense_w, const float *bias, int32_t flags, void *x0,
+                              mrec_dtype x0_dtype, int64_t x0_ld, int32_t x0_cols, float *logit,
+                              float *fm_sum, int32_t *d_oob_flag, mrec_stream stream) {
+  BankArgs ba;
+  IdsArgs ia;
+  int eb, lpr;
+  mrec_status st = make_bank_args(bank, &ba, &eb, &lpr);
+  if (st != MREC_OK) return st;
+  if ((st = make_ids_args(ids, ba.n_tables, &ia)) != MREC_OK) return st;
+  MREC_CHECK_ARG(batch >= 0, "batch < 0");
+  MREC_CHECK_ARG(n_dense >= 0, "n_dense < 0");
+  MREC_CHECK_ARG(n_dense == 0 || (dense != nullptr && dense_w != nullptr && dense_ld >= n_dense),
+                 "dense/dense_w NULL or dense_ld < n_dense");
+  MREC_CHECK_ARG(!(flags & MREC_INTERACT_FIRST_ORDER) || ba.has_w,
+                 "FIRST_ORDER requested but bank has no w column");
+  if (x0) {
+    MREC_CHECK_ARG(x0_dtype == MREC_F32 || x0_dtype == MREC_BF16, "x0 dtype must be F32/BF16");
+    const int xb = x0_dtype == MREC_F32 ? 4 : 2;
+    MREC_CHECK_ARG(x0_cols >= ba.n_tables * ba.dim + n_dense && x0_ld >= x0_cols,
+                   "x0_cols < F*dim + n_dense or x0_ld < x0_cols");
+    MREC_CHECK_ARG((reinterpret_cast<uintptr_t>(x0) & 15) == 0 && (x0_ld * xb) % 16 == 0 &&
+                       (ba.dim * xb) % 16 == 0,
+                   "x0 must be 16B aligned with 16B-multiple rows");
+  }
+  MREC_CHECK_ARG(fm_sum == nullptr || (reinterpret_cast<uintptr_t>(fm_sum) & 15) == 0,
+                 "fm_sum not 16B aligned");
+  if (batch == 0) return MREC_OK;
+  hipStream_t s = static_cast<hipStream_t>(stream);
+  const bool xb16 = x0 && x0_dtype == MREC_BF16;
+  if (bank->dtype == MREC_BF16) {
+    if (xb16)
+      launch_interact<uint16_t, true>(lpr, ba, ia, batch, dense, n_dense, dense_ld, dense_w, bias,
+                                      flags, x0, x0_ld, x0_cols, logit, fm_sum, d_oob_flag, s);
+    else
+      launch_interact<uint16_t, false>(lpr, ba, ia, batch, dense, n_dense, dense_ld, dense_w, bias,
+                                       flags, x0, x0_ld, x0_cols, logit, fm_sum, d_oob_flag, s);
+  } else {
+    if (xb16)
+      launch_interact<float, true>(lpr, ba, ia, batch, dense, n_dense, dense_ld, dense_w, bias,
+                                   flags, x0, x0_ld, x0_cols, logit, fm_sum, d_oob_flag, s);
+    else
+      launch_interact<float, false>(lpr, ba, ia, batch, dense, n_dense, dense_ld, dense_w, bias,
+                                    flags, x0, x0_ld, x0_cols, logit, fm_sum, d_oob_flag, s);
+  }
+  return launch_status("mrec_interact_fwd");
+}
+
+mrec_status mrec_fm2_fwd(const float *v, int64_t batch, int32_t fields, int32_t dim, float *y,
+                         mrec_stream stream) {
+  MREC_CHECK_ARG(v != nullptr && y != nullptr, "NULL pointer");
+  MREC_CHECK_ARG(batch >= 0 && fields >= 1 && dim >= 1, "bad shape");
+  if (batch == 0) return MREC_OK;
+  fm2_fwd_kernel<<<dim3(static_cast<unsigned>((batch + 3) / 4)), 256, 0,
+                   static_cast<hipStream_t>(stream)>>>(v, batch, fields, dim, y);
+  return launch_status("mrec_fm2_fwd");
+}
+
+mrec_status mrec_fm2_bwd(const float *v, const float *dy, int64_t batch, int32_t fields,
+                         int32_t dim, float *dv, mrec_stream stream) {
+  MREC_CHECK_ARG(v != nullptr && dy != nullptr && dv != nullptr, "NULL pointer");
+  MREC_CHECK_ARG(batch >= 0 && fields >= 1 && dim >= 1, "bad shape");
+  if (batch == 0) return MREC_OK;
+  fm2_bwd_kernel<<<dim3(static_cast<unsigned>((batch + 3) / 4)), 256, 0,
+                   static_cast<hipStream_t>(stream)>>>(v, dy, batch, fields, dim, dv);
+  return launch_status("mrec_fm2_bwd");
+}
+
+}  // extern "C"

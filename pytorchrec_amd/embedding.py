@@ -1,0 +1,419 @@
+"""Embedding bank: F categorical tables packed for the MI355X hot path.
+
+``EmbeddingBank`` replaces the F ``torch.nn.Embedding`` tables (plus the
+``Embedding(rows, 1)`` first-order biases) that a reference model builds in
+``IModel._init_weights`` (torchrec/model/FunkSVD.py:39-41, SVDPP.py:36-42).  All
+tables live in ONE parameter ``weight`` of shape [total_rows, row_stride]:
+
+    row r of table f  ->  weight[row_offset[f] + r] = [ v(dim) | w | pad ]
+
+with the row padded to a power-of-two byte width (64 B for bf16 dim 16 + w) so
+each lookup is one aligned, coalesced request (DESIGN.md §Data layout).
+
+The autograd functions here are the only way the models touch the tables on a
+GPU: they call libmrec (``_mrec``) and raise if it is missing.  On a CPU device
+(config C1, the reference's own CPU path) the same math runs as plain torch
+index_select / index_add (``cpu_path``) — an explicit device dispatch, never a
+fallback for a GPU tensor.
+
+Update modes (``EmbeddingBank.update``):
+  "dense"     backward materialises the dense table gradient exactly like
+              ``aten::embedding_dense_backward`` so any torch optimizer works
+              (reference semantics, IModel.py:120-124);
+  "sgd"       the backward applies row-sparse SGD in place (identical to dense
+              SGD without momentum / weight decay), the gradient never exists;
+              ``IModel.compile`` switches to it when the compiled optimizer is
+              plain SGD (SURVEY.md §7 hard part 5).
+"""
+from __future__ import annotations
+
+from typing import List, Optional, Sequence
+
+import torch
+
+from pytorchrec_amd import _mrec, cpu_path
+
+
+def _row_stride(dim: int, has_w: bool, dtype: torch.dtype) -> int:
+    es = torch.tensor([], dtype=dtype).element_size()
+    need = (dim + (1 if has_w else 0)) * es
+    b = 16
+    while b < need:
+        b *= 2
+    if b > 256:
+        raise ValueError(f"row of {need} bytes exceeds 256 B (dim too large for one bank row)")
+    return b // es
+
+
+class EmbeddingBank(torch.nn.Module):
+    """F embedding tables (+ optional first-order weight column) in one tensor.
+
+    ``category_nums[f]`` rows for table f (``CategoricalColumn.category_num``,
+    CategoricalColumn.py:9-14).  ``weight`` is initialised by the host model's
+    ``IModel._reset_weights`` (normal(0, 0.01), IModel.py:61-68): the class name
+    contains "Embedding" so the reference's type-name match applies to it.
+    """
+
+    def __init__(self, category_nums: Sequence[int], dim: int, with_first_order: bool = False,
+                 dtype: torch.dtype = torch.float32, update: str = "dense", device=None):
+        super().__init__()
+        if len(category_nums) < 1:
+            raise ValueError("need at least one table")
+        if update not in ("dense", "sgd"):
+            raise ValueError(f"update must be 'dense' or 'sgd', got {update!r}")
+        es = torch.tensor([], dtype=dtype).element_size()
+        if dim <= 0 or (dim * es) % 16:
+            raise ValueError(f"dim*{es}B must be a positive multiple of 16 bytes (dim={dim})")
+        self.category_nums = [int(n) for n in category_nums]
+        self.dim = int(dim)
+        self.has_w = bool(with_first_order)
+        self.row_stride = _row_stride(self.dim, self.has_w, dtype)
+        offs, acc = [], 0
+        for n in self.category_nums:
+            offs.append(acc)
+            acc += n
+        self.row_offset = offs
+        self.total_rows = acc
+        self.weight = torch.nn.Parameter(
+            torch.empty(acc, self.row_stride, dtype=dtype, device=device),
+            requires_grad=(update == "dense"))
+        self.update = update
+        self.sgd_lr: Optional[float] = None
+        self.sgd_group = None  # optimizer param group the fused SGD lr is read from
+        self.stochastic_rounding = dtype == torch.bfloat16
+        self.check_ids = True  # raise IndexError on out-of-range ids (syncs once per call)
+        self._seed = 0x5eed
+        self._desc = None
+
+    @property
+    def n_tables(self) -> int:
+        return len(self.category_nums)
+
+    # -- optimizer integration -------------------------------------------------
+    def use_fused_sgd(self, lr: float, group=None):
+        self.update = "sgd"
+        self.sgd_lr = float(lr)
+        self.sgd_group = group
+        self.weight.requires_grad_(False)
+
+    def use_dense_grad(self):
+        self.update = "dense"
+        self.weight.requires_grad_(True)
+
+    def current_lr(self) -> float:
+        if self.sgd_group is not None:
+            return float(self.sgd_group["lr"])
+        if self.sgd_lr is None:
+            raise RuntimeError("fused SGD update without a learning rate")
+        return self.sgd_lr
+
+    def next_seed(self) -> int:
+        self._seed = (self._seed * 6364136223846793005 + 1442695040888963407) & (2 ** 64 - 1)
+        return self._seed
+
+    # -- table views (for checkpoints / tests) ----------------------------------
+    def table(self, f: int) -> torch.Tensor:
+        o = self.row_offset[f]
+        return self.weight[o:o + self.category_nums[f], :self.dim]
+
+    def first_order(self, f: int) -> torch.Tensor:
+        if not self.has_w:
+            raise ValueError("bank has no first-order column")
+        o = self.row_offset[f]
+        return self.weight[o:o + self.category_nums[f], self.dim]
+
+    def desc(self) -> _mrec.BankDesc:
+        if self._desc is None or self._desc.weight is not self.weight:
+            self._desc = _mrec.BankDesc(self.weight, self.row_offset, self.category_nums,
+                                        self.dim, self.has_w)
+        return self._desc
+
+    def extra_repr(self) -> str:
+        return (f"tables={self.n_tables}, rows={self.total_rows}, dim={self.dim}, "
+                f"first_order={self.has_w}, row_stride={self.row_stride}, "
+                f"dtype={self.weight.dtype}, update={self.update}")
+
+
+# ----------------------------------------------------------------------------
+# helpers
+# ----------------------------------------------------------------------------
+
+
+def _oob_flag(bank: EmbeddingBank, device) -> Optional[torch.Tensor]:
+    return torch.zeros(1, dtype=torch.int32, device=device) if bank.check_ids else None
+
+
+def _raise_if_oob(flag: Optional[torch.Tensor]):
+    if flag is not None and int(flag.item()) != 0:
+        raise IndexError("index out of range in self")
+
+
+def _ids_desc(ids: Sequence[torch.Tensor], start: int = 0, count: Optional[int] = None):
+    if start == 0 and count is None:
+        return _mrec.IdsDesc(ids)
+    return _mrec.IdsDesc([t[start:start + count] for t in ids])
+
+
+def _plan(bank: EmbeddingBank, ids, start: int, count: int, flag):
+    n = bank.n_tables
+    ws_bytes = _mrec.lib().mrec_emb_bwd_workspace_size(n, count)
+    ws = torch.empty(ws_bytes, dtype=torch.uint8, device=bank.weight.device)
+    idd = _ids_desc(ids, start, count) if (start or count != ids[0].shape[0]) else _ids_desc(ids)
+    _mrec.call("mrec_emb_bwd_plan", bank.desc().ref(), idd.ref(), count, ws.data_ptr(), ws_bytes,
+               _mrec.ptr(flag), _mrec.stream_handle())
+    return ws, ws_bytes
+
+
+def _apply(bank: EmbeddingBank, ws, ws_bytes, count, dx=None, dfm=None, fm_sum=None, x0=None,
+           dw=None, grad=None):
+    """Run the fused backward for lookups [0, count) described by ``ws``; the
+    per-sample tensors must already be sliced to the same chunk."""
+    if bank.update == "sgd":
+        mode = _mrec.BWD_SGD_SR if (bank.stochastic_rounding and
+                                    bank.weight.dtype == torch.bfloat16) else _mrec.BWD_SGD
+        lr = bank.current_lr()
+    else:
+        mode, lr = _mrec.BWD_DENSE_GRAD, 0.0
+    dx_dt = _mrec.dtype_code(dx.dtype) if dx is not None else _mrec.F32
+    x0_dt = _mrec.dtype_code(x0.dtype) if x0 is not None else _mrec.F32
+    _mrec.call("mrec_emb_bwd_apply", bank.desc().ref(), count, ws.data_ptr(), ws_bytes,
+               _mrec.ptr(dx), dx_dt, dx.stride(0) if dx is not None else 0,
+               _mrec.ptr(dfm), _mrec.ptr(fm_sum), _mrec.ptr(x0), x0_dt,
+               x0.stride(0) if x0 is not None else 0, _mrec.ptr(dw), mode, float(lr),
+               bank.next_seed(), _mrec.ptr(grad), _mrec.stream_handle())
+
+
+def _chunks(batch: int):
+    step = _mrec.BWD_MAX_BATCH
+    return [(s, min(step, batch - s)) for s in range(0, batch, step)] or [(0, 0)]
+
+
+def _backward_into_bank(bank: EmbeddingBank, ids, batch, plan_ws, dx=None, dfm=None,
+                        fm_sum=None, x0=None, dw=None):
+    """Shared backward: returns the dense grad (dense mode) or None (fused SGD)."""
+    grad = None
+    if bank.update == "dense":
+        grad = torch.zeros_like(bank.weight)
+    if plan_ws is not None:
+        ws, wsb = plan_ws
+        _apply(bank, ws, wsb, batch, dx, dfm, fm_sum, x0, dw, grad)
+        return grad
+    for s, c in _chunks(batch):
+        if c == 0:
+            continue
+        ws, wsb = _plan(bank, ids, s, c, None)
+        sl = (lambda t: None if t is None else t[s:s + c])
+        _apply(bank, ws, wsb, c, sl(dx), sl(dfm), sl(fm_sum), sl(x0), sl(dw), grad)
+    return grad
+
+
+def _needs_backward(bank: EmbeddingBank) -> bool:
+    return torch.is_grad_enabled() and (bank.update == "sgd" or bank.weight.requires_grad)
+
+
+# ----------------------------------------------------------------------------
+# autograd: plain multi-table gather  (nn.Embedding x F)
+# ----------------------------------------------------------------------------
+
+
+class _GatherFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, weight, trigger, bank: EmbeddingBank, ids: List[torch.Tensor], out_dtype,
+                want_w: bool):
+        B = ids[0].shape[0]
+        F, D = bank.n_tables, bank.dim
+        dev = weight.device
+        out = torch.empty(B, F * D, dtype=out_dtype, device=dev)
+        w_out = torch.empty(B, F, dtype=torch.float32, device=dev) if want_w else None
+        flag = _oob_flag(bank, dev)
+        if B:
+            _mrec.call("mrec_emb_gather_fwd", bank.desc().ref(), _ids_desc(ids).ref(), B,
+                       out.data_ptr(), _mrec.dtype_code(out_dtype), out.stride(0),
+                       _mrec.ptr(w_out), _mrec.ptr(flag), _mrec.stream_handle())
+        plan_ws = None
+        if _needs_backward(bank) and 0 < B <= _mrec.BWD_MAX_BATCH:
+            plan_ws = _plan(bank, ids, 0, B, None)
+        _raise_if_oob(flag)
+        ctx.bank, ctx.ids, ctx.B, ctx.plan_ws = bank, ids, B, plan_ws
+        if want_w:
+            return out, w_out
+        return out
+
+    @staticmethod
+    def backward(ctx, dout, dw_out=None):
+        bank = ctx.bank
+        dx = dout.contiguous() if dout is not None else None
+        dw = None
+        if dw_out is not None:
+            if bank.n_tables != 1:
+                raise NotImplementedError("first-order grads through gather need one table "
+                                          "per call; use interact() for multi-field models")
+            dw = dw_out.reshape(-1).contiguous().float()
+        grad = _backward_into_bank(bank, ctx.ids, ctx.B, ctx.plan_ws, dx=dx, dw=dw)
+        return grad, None, None, None, None, None
+
+
+def gather(bank: EmbeddingBank, ids: Sequence[torch.Tensor], out_dtype=None, with_w=False):
+    """out[b, f*D:(f+1)*D] = table_f[ids[f][b]] — F ``nn.Embedding`` lookups.
+
+    Returns [B, F*D] (and [B, F] first-order weights if ``with_w``).
+    """
+    ids = list(ids)
+    if len(ids) != bank.n_tables:
+        raise ValueError(f"expected {bank.n_tables} id tensors, got {len(ids)}")
+    out_dtype = out_dtype or bank.weight.dtype
+    if not bank.weight.is_cuda:
+        return cpu_path.gather(bank, ids, out_dtype, with_w)
+    trigger = _trigger(bank)
+    return _GatherFn.apply(bank.weight, trigger, bank, ids, out_dtype, with_w)
+
+
+_TRIGGERS = {}
+
+
+def _trigger(bank: EmbeddingBank):
+    """A 0-element leaf that requires grad, so autograd calls our backward even when
+    the bank itself is updated in place (fused SGD, weight.requires_grad False)."""
+    if bank.update != "sgd" or not torch.is_grad_enabled():
+        return None
+    t = _TRIGGERS.get(bank.weight.device)
+    if t is None:
+        t = torch.zeros(0, device=bank.weight.device, requires_grad=True)
+        _TRIGGERS[bank.weight.device] = t
+    return t
+
+
+# ----------------------------------------------------------------------------
+# autograd: fused gather + FM2 + first order + deep-input builder
+# ----------------------------------------------------------------------------
+
+
+class _InteractFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, weight, dense_w, bias, trigger, bank: EmbeddingBank, ids, dense, fm2: bool,
+                first_order: bool, x0_cols: int, x0_dtype):
+        B = ids[0].shape[0]
+        dev = weight.device
+        n_dense = 0 if dense is None else dense.shape[1]
+        flags = (_mrec.INTERACT_FM2 if fm2 else 0) | (_mrec.INTERACT_FIRST_ORDER if first_order else 0)
+        x0 = None
+        if x0_cols:
+            x0 = torch.empty(B, x0_cols, dtype=x0_dtype, device=dev)
+        logit = torch.empty(B, dtype=torch.float32, device=dev)
+        fm_sum = torch.empty(B, bank.dim, dtype=torch.float32, device=dev) if fm2 else None
+        flag = _oob_flag(bank, dev)
+        if B:
+            _mrec.call("mrec_interact_fwd", bank.desc().ref(), _ids_desc(ids).ref(), B,
+                       _mrec.ptr(dense), n_dense, dense.stride(0) if dense is not None else 0,
+                       _mrec.ptr(dense_w), _mrec.ptr(bias), flags, _mrec.ptr(x0),
+                       _mrec.dtype_code(x0_dtype), x0.stride(0) if x0 is not None else 0,
+                       int(x0_cols), logit.data_ptr(), _mrec.ptr(fm_sum), _mrec.ptr(flag),
+                       _mrec.stream_handle())
+        plan_ws = None
+        if _needs_backward(bank) and 0 < B <= _mrec.BWD_MAX_BATCH:
+            plan_ws = _plan(bank, ids, 0, B, None)
+        _raise_if_oob(flag)
+        ctx.bank, ctx.ids, ctx.B, ctx.plan_ws = bank, ids, B, plan_ws
+        ctx.fm2, ctx.first_order = fm2, first_order
+        ctx.save_for_backward(x0, fm_sum, dense)
+        ctx.has_dense_w = dense_w is not None
+        ctx.has_bias = bias is not None
+        if x0 is None:
+            return logit
+        return x0, logit
+
+    @staticmethod
+    def backward(ctx, *grads):
+        if len(grads) == 2:
+            dx0, dlogit = grads
+        else:
+            dx0, dlogit = None, grads[0]
+        x0, fm_sum, dense = ctx.saved_tensors
+        bank = ctx.bank
+        if dlogit is not None:
+            dlogit = dlogit.contiguous().float()
+        dfm = dlogit if (ctx.fm2 and dlogit is not None) else None
+        dw = dlogit if (ctx.first_order and dlogit is not None) else None
+        if dx0 is not None:
+            dx0 = dx0.contiguous()
+        grad = None
+        if bank.update == "sgd" or bank.weight.requires_grad:
+            grad = _backward_into_bank(bank, ctx.ids, ctx.B, ctx.plan_ws, dx=dx0, dfm=dfm,
+                                       fm_sum=fm_sum, x0=x0 if dfm is not None else None, dw=dw)
+        g_dense_w = g_bias = None
+        if dlogit is not None:
+            if ctx.has_dense_w and dense is not None:
+                g_dense_w = dense.t().float() @ dlogit
+            if ctx.has_bias:
+                g_bias = dlogit.sum().reshape(1)
+        return grad, g_dense_w, g_bias, None, None, None, None, None, None, None, None
+
+
+def interact(bank: EmbeddingBank, ids: Sequence[torch.Tensor], dense: Optional[torch.Tensor] = None,
+             dense_w: Optional[torch.Tensor] = None, bias: Optional[torch.Tensor] = None,
+             fm2: bool = True, first_order: bool = True, x0_cols: int = 0,
+             x0_dtype: torch.dtype = torch.bfloat16):
+    """Fused DeepFM/FM/DCN input stage (see include/mrec.h ``mrec_interact_fwd``).
+
+    Returns ``logit`` [B] (bias + dense.dense_w + FM2 + sum_f w) when ``x0_cols`` is 0,
+    else ``(x0 [B, x0_cols], logit)`` with x0 = [v_0..v_{F-1} | dense | 0-pad].
+    """
+    ids = list(ids)
+    if len(ids) != bank.n_tables:
+        raise ValueError(f"expected {bank.n_tables} id tensors, got {len(ids)}")
+    if first_order and not bank.has_w:
+        raise ValueError("first_order needs a bank built with_first_order=True")
+    if dense is not None:
+        dense = dense.contiguous().float()
+        if dense_w is None:
+            raise ValueError("dense features need dense_w")
+    if not bank.weight.is_cuda:
+        return cpu_path.interact(bank, ids, dense, dense_w, bias, fm2, first_order, x0_cols,
+                                 x0_dtype)
+    trigger = _trigger(bank)
+    return _InteractFn.apply(bank.weight, dense_w, bias, trigger, bank, ids, dense, fm2,
+                             first_order, int(x0_cols), x0_dtype)
+
+
+def fm2_dense(v: torch.Tensor) -> torch.Tensor:
+    """FM second order of a dense [B, F, D] fp32 tensor (HIP on GPU)."""
+    return _Fm2Fn.apply(v) if v.is_cuda else cpu_path.fm2(v)
+
+
+class _Fm2Fn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, v):
+        v = v.contiguous().float()
+        B, F, D = v.shape
+        y = torch.empty(B, dtype=torch.float32, device=v.device)
+        _mrec.call("mrec_fm2_fwd", v.data_ptr(), B, F, D, y.data_ptr(), _mrec.stream_handle())
+        ctx.save_for_backward(v)
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        (v,) = ctx.saved_tensors
+        B, F, D = v.shape
+        dv = torch.empty_like(v)
+        dy = dy.contiguous().float()
+        _mrec.call("mrec_fm2_bwd", v.data_ptr(), dy.data_ptr(), B, F, D, dv.data_ptr(),
+                   _mrec.stream_handle())
+        return dv
+
+
+def init_bank_(bank: EmbeddingBank, std: float = 0.01, generator=None, chunk_rows: int = 1 << 24):
+    """normal(0, std) init in row chunks (IModel._reset_weights_fn, IModel.py:67-68);
+    chunked so multi-GB banks never need a second full-size temporary."""
+    with torch.no_grad():
+        w = bank.weight
+        for s in range(0, w.shape[0], chunk_rows):
+            w[s:s + chunk_rows].normal_(0.0, std, generator=generator)
+    return bank
+
+
+def rows_to_bytes(bank: EmbeddingBank) -> int:
+    return bank.weight.numel() * bank.weight.element_size()
+
+
+__all__ = ["EmbeddingBank", "gather", "interact", "fm2_dense", "init_bank_", "rows_to_bytes"]
+

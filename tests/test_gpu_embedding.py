@@ -1,0 +1,309 @@
+"""GPU parity of the embedding kernels (libmrec via ctypes) against the CPU
+oracle (oracle/ref.py) and the reference's golden vectors.
+
+Bars (north_star): index gather bit-exact; fp interaction within 1e-5 relative
+with the magnitude-aware denominator of SURVEY.md §7 hard part 3; scatter-add
+gradients within fp32 reordering tolerance of the fp64 oracle.
+"""
+import numpy as np
+import pytest
+import torch
+
+from conftest import golden
+from oracle import ref
+
+pytestmark = pytest.mark.gpu
+
+
+def _bank(category_nums, dim, has_w, dtype, update="dense", device="cuda"):
+    from pytorchrec_amd import _mrec
+    from pytorchrec_amd.embedding import EmbeddingBank
+    assert _mrec.available(), "libmrec.so must be built and loadable on the GPU box"
+    b = EmbeddingBank(category_nums, dim, with_first_order=has_w, dtype=dtype, update=update,
+                      device=device)
+    return b
+
+
+def _fill(bank, tables, ws=None):
+    """Write per-table numpy values (fp32 or bf16 bits) into the bank."""
+    with torch.no_grad():
+        bank.weight.zero_()
+        for f, t in enumerate(tables):
+            o = bank.row_offset[f]
+            if t.dtype == np.uint16:
+                tt = torch.from_numpy(t.view(np.int16)).view(torch.bfloat16)
+            else:
+                tt = torch.from_numpy(t).to(bank.weight.dtype)
+            bank.weight[o:o + t.shape[0], :bank.dim] = tt.to(bank.weight.device)
+            if ws is not None:
+                bank.weight[o:o + t.shape[0], bank.dim] = torch.from_numpy(ws[f]).to(
+                    bank.weight.device, bank.weight.dtype)
+
+
+def _bits(t):
+    t = t.detach().cpu()
+    if t.dtype == torch.bfloat16:
+        return t.view(torch.int16).numpy().view(np.uint16)
+    return t.numpy().view(np.uint32)
+
+
+def _wbits(a):
+    return a if a.dtype == np.uint16 else np.ascontiguousarray(a, np.float32).view(np.uint32)
+
+
+def _ids_with_edges(rng, rows, B):
+    ids = rng.integers(0, rows, B)
+    ids[:4] = [0, rows - 1, 0, rows - 1]
+    ids[4:8] = ids[8:12]
+    return ids
+
+
+def _rand_tables(rng, nums, dim, dtype):
+    tabs = [(rng.standard_normal((n, dim)) * 0.5).astype(np.float32) for n in nums]
+    if dtype == torch.bfloat16:
+        tabs = [ref.f32_to_bf16_bits(t) for t in tabs]
+    return tabs
+
+
+def _as_f32(t):
+    return ref.bf16_bits_to_f32(t) if t.dtype == np.uint16 else t
+
+
+# ---------------------------------------------------------------------------
+# gather
+# ---------------------------------------------------------------------------
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+def test_gather_golden_g1_bit_exact(gpu, dtype):
+    from pytorchrec_amd.embedding import gather
+    g = golden("g1_gather.npz")
+    table = g["table"] if dtype == torch.float32 else g["table_bf16"]
+    want = g["out"] if dtype == torch.float32 else g["out_bf16"]
+    bank = _bank([table.shape[0]], table.shape[1], False, dtype)
+    _fill(bank, [table])
+    ids = torch.from_numpy(g["ids"]).to(gpu)  # int64, as .long() gives
+    out = gather(bank, [ids])
+    assert np.array_equal(_bits(out), _wbits(want))
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("id_dtype", [torch.int32, torch.int64])
+def test_gather_multi_table_bit_exact(gpu, dtype, id_dtype):
+    from pytorchrec_amd.embedding import gather
+    rng = np.random.default_rng(3)
+    nums = [int(x) for x in rng.integers(2, 3000, 26)]
+    nums[0] = 1  # a one-row table
+    D, B = 16, 1000
+    tabs = _rand_tables(rng, nums, D, dtype)
+    wts = [rng.standard_normal(n).astype(np.float32) for n in nums]
+    bank = _bank(nums, D, True, dtype)
+    _fill(bank, tabs, wts)
+    ids_np = np.stack([_ids_with_edges(rng, n, B) for n in nums], 1)
+    ids = [torch.from_numpy(ids_np[:, f]).to(gpu, id_dtype) for f in range(26)]
+    out, w = gather(bank, ids, with_w=True)
+    want = ref.multi_table_gather(tabs, ids_np).reshape(B, -1)
+    assert np.array_equal(_bits(out), _wbits(want))
+    wq = [(_as_f32(ref.f32_to_bf16_bits(x)) if dtype == torch.bfloat16 else x) for x in wts]
+    want_w = np.stack([wq[f][ids_np[:, f]] for f in range(26)], 1)
+    assert np.array_equal(w.detach().cpu().numpy(), want_w)
+    # widened / narrowed outputs
+    out32 = gather(bank, ids, out_dtype=torch.float32)
+    assert np.array_equal(out32.detach().cpu().numpy(), _as_f32(want) if want.dtype == np.uint16 else want)
+
+
+def test_gather_out_of_range_raises_index_error(gpu):
+    from pytorchrec_amd.embedding import gather
+    bank = _bank([10, 20], 8, False, torch.float32)
+    _fill(bank, [np.ones((10, 8), np.float32), np.ones((20, 8), np.float32)])
+    good = torch.tensor([0, 9], device=gpu)
+    with pytest.raises(IndexError):
+        gather(bank, [good, torch.tensor([0, 20], device=gpu)])
+    with pytest.raises(IndexError):
+        gather(bank, [torch.tensor([-1, 0], device=gpu), good])
+    out = gather(bank, [good, torch.tensor([19, 0], device=gpu)])
+    assert torch.all(out == 1)
+
+
+def test_gather_empty_batch(gpu):
+    from pytorchrec_amd.embedding import gather
+    bank = _bank([10], 8, False, torch.float32)
+    out = gather(bank, [torch.empty(0, dtype=torch.int64, device=gpu)])
+    assert out.shape == (0, 8)
+
+
+# ---------------------------------------------------------------------------
+# fused interaction
+# ---------------------------------------------------------------------------
+
+def _fm_tol_ok(got, v, want, rtol=1e-5):
+    den = np.abs(want) + ref.fm2_magnitude(v)
+    return np.all(np.abs(got - want) <= rtol * den + 1e-12), np.max(np.abs(got - want) / den)
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+def test_interact_deepfm_stage(gpu, dtype):
+    from pytorchrec_amd.embedding import interact
+    rng = np.random.default_rng(5)
+    nums = [int(x) for x in rng.integers(50, 5000, 26)]
+    D, B, ND = 16, 777, 13
+    tabs = _rand_tables(rng, nums, D, dtype)
+    wts = [(rng.standard_normal(n) * 0.3).astype(np.float32) for n in nums]
+    bank = _bank(nums, D, True, dtype)
+    _fill(bank, tabs, wts)
+    ids_np = np.stack([_ids_with_edges(rng, n, B) for n in nums], 1)
+    ids = [torch.from_numpy(ids_np[:, f].astype(np.int32)).to(gpu) for f in range(26)]
+    dense = rng.random((B, ND)).astype(np.float32)
+    dense_w = (rng.standard_normal(ND) * 0.1).astype(np.float32)
+    bias = np.array([0.25], np.float32)
+    x0, logit = interact(bank, ids, torch.from_numpy(dense).to(gpu),
+                         torch.from_numpy(dense_w).to(gpu), torch.from_numpy(bias).to(gpu),
+                         fm2=True, first_order=True, x0_cols=448, x0_dtype=torch.bfloat16)
+    v = _as_f32(ref.multi_table_gather(tabs, ids_np))  # exactly what the kernel reads
+    wq = [(_as_f32(ref.f32_to_bf16_bits(x)) if dtype == torch.bfloat16 else x) for x in wts]
+    w_g = np.stack([wq[f][ids_np[:, f]] for f in range(26)], 1)
+    want = ref.fm2(v) + ref.first_order(w_g, dense, dense_w, bias[0])
+    ok, worst = _fm_tol_ok(logit.detach().cpu().numpy().astype(np.float64), v, want)
+    assert ok, worst
+    # x0 = [v | dense | 0]: embeddings bit-exact in bf16, dense RNE-rounded, pad zero
+    x0n = _bits(x0)
+    want_v = ref.f32_to_bf16_bits(v.reshape(B, -1))
+    assert np.array_equal(x0n[:, :26 * D], want_v)
+    assert np.array_equal(x0n[:, 26 * D:26 * D + ND], ref.f32_to_bf16_bits(dense))
+    assert np.all(x0n[:, 26 * D + ND:] == 0)
+
+
+def test_interact_fm_equals_funksvd_golden_g3(gpu):
+    """FM over {uid, iid} == FunkSVD.forward (FunkSVD.py:51) — SURVEY G3."""
+    from pytorchrec_amd.embedding import interact
+    g = golden("g3_funksvd.npz")
+    D = g["u_table"].shape[1]
+    bank = _bank([g["u_table"].shape[0], g["i_table"].shape[0]], D, False, torch.float32)
+    _fill(bank, [g["u_table"], g["i_table"]])
+    ids = [torch.from_numpy(g["uid"]).to(gpu), torch.from_numpy(g["iid"]).to(gpu)]
+    logit = interact(bank, ids, fm2=True, first_order=False)
+    np.testing.assert_allclose(logit.detach().cpu().numpy(), g["prediction"], rtol=1e-5, atol=1e-9)
+
+
+# ---------------------------------------------------------------------------
+# backward
+# ---------------------------------------------------------------------------
+
+def test_dense_grad_golden_g2(gpu):
+    from pytorchrec_amd.embedding import gather
+    g = golden("g2_dense_grad.npz")
+    g1 = golden("g1_gather.npz")
+    rows = int(g["rows"])
+    bank = _bank([rows], g["dy"].shape[1], False, torch.float32, update="dense")
+    _fill(bank, [g1["table"]])
+    out = gather(bank, [torch.from_numpy(g["ids"]).to(gpu)])
+    out.backward(torch.from_numpy(g["dy"]).to(gpu))
+    got = bank.weight.grad[:, :bank.dim].detach().cpu().numpy()
+    np.testing.assert_allclose(got, g["grad"], rtol=1e-6, atol=1e-7)
+    untouched = np.setdiff1d(np.arange(rows), g["ids"])
+    assert np.all(got[untouched] == 0)
+
+
+@pytest.mark.parametrize("zipf", [False, True])
+def test_fused_sgd_f32_matches_oracle(gpu, zipf):
+    """Row-sparse SGD through the interact backward (dx from the MLP, FM2 and
+    first-order grads) == dense SGD on the oracle's dense gradient."""
+    from pytorchrec_amd.embedding import interact
+    rng = np.random.default_rng(7 + zipf)
+    nums = [300, 40, 1, 5000]
+    D, B, F = 16, 3000, 4
+    tabs = _rand_tables(rng, nums, D, torch.float32)
+    wts = [(rng.standard_normal(n) * 0.3).astype(np.float32) for n in nums]
+    bank = _bank(nums, D, True, torch.float32, update="sgd")
+    bank.use_fused_sgd(lr=0.05)
+    _fill(bank, tabs, wts)
+    before = bank.weight.detach().clone()
+    if zipf:
+        ids_np = np.stack([np.minimum(rng.zipf(1.05, B) - 1, n - 1) for n in nums], 1)
+    else:
+        ids_np = np.stack([rng.integers(0, n, B) for n in nums], 1)
+    ids = [torch.from_numpy(ids_np[:, f]).to(gpu) for f in range(F)]
+    bias = torch.zeros(1, device=gpu, requires_grad=True)
+    x0, logit = interact(bank, ids, bias=bias, fm2=True, first_order=True, x0_cols=F * D,
+                         x0_dtype=torch.float32)
+    dx0 = rng.standard_normal((B, F * D)).astype(np.float32)
+    dlogit = rng.standard_normal(B).astype(np.float32)
+    torch.autograd.backward([x0, logit], [torch.from_numpy(dx0).to(gpu),
+                                          torch.from_numpy(dlogit).to(gpu)])
+    v = ref.multi_table_gather(tabs, ids_np).astype(np.float64)
+    gv = dx0.reshape(B, F, D) + ref.fm2_bwd(v, dlogit)
+    after = bank.weight.detach().cpu().numpy().astype(np.float64)
+    for f in range(F):
+        o, n = bank.row_offset[f], nums[f]
+        want = ref.sgd_rows(tabs[f], ids_np[:, f], gv[:, f], 0.05)
+        want_w = ref.sgd_rows(wts[f][:, None], ids_np[:, f], dlogit[:, None], 0.05)[:, 0]
+        got = after[o:o + n]
+        scale = np.abs(tabs[f]).max() + 0.05 * np.abs(ref.dense_grad(n, ids_np[:, f], np.abs(gv[:, f]))).max()
+        np.testing.assert_allclose(got[:, :D], want, rtol=0, atol=2e-6 * scale)
+        np.testing.assert_allclose(got[:, D], want_w, rtol=0, atol=2e-6 * (1 + np.abs(want_w).max()))
+        untouched = np.setdiff1d(np.arange(n), ids_np[:, f])
+        assert torch.equal(bank.weight[o + untouched].cpu(), before[o + untouched].cpu())
+    assert bias.grad is not None and abs(float(bias.grad) - dlogit.sum()) < 1e-3
+
+
+def test_fused_sgd_bf16_stochastic_rounding_within_one_ulp(gpu):
+    from pytorchrec_amd.embedding import gather
+    rng = np.random.default_rng(11)
+    nums = [2000, 2000]
+    D, B = 16, 4096
+    tabs = _rand_tables(rng, nums, D, torch.bfloat16)
+    bank = _bank(nums, D, False, torch.bfloat16, update="sgd")
+    bank.use_fused_sgd(lr=0.1)
+    _fill(bank, tabs)
+    ids_np = np.stack([np.minimum(rng.zipf(1.2, B) - 1, n - 1) for n in nums], 1)
+    ids = [torch.from_numpy(ids_np[:, f]).to(gpu) for f in range(2)]
+    out = gather(bank, ids, out_dtype=torch.float32)
+    dy = (rng.standard_normal((B, 2 * D)) * 0.01).astype(np.float32)
+    out.backward(torch.from_numpy(dy).to(gpu))
+    after = _bits(bank.weight)
+    for f in range(2):
+        o, n = bank.row_offset[f], nums[f]
+        want = ref.sgd_rows(_as_f32(tabs[f]), ids_np[:, f], dy[:, f * D:(f + 1) * D], 0.1)
+        got = ref.bf16_bits_to_f32(after[o:o + n, :D]).astype(np.float64)
+        assert np.all(np.abs(got - want) <= ref.bf16_ulp(want) * 1.0001)
+
+
+def test_plan_handles_all_duplicates_and_single_row(gpu):
+    """Every lookup hits row 0 (one segment of length B, the hot-row path)."""
+    from pytorchrec_amd.embedding import gather
+    bank = _bank([3], 8, False, torch.float32, update="dense")
+    _fill(bank, [np.zeros((3, 8), np.float32)])
+    B = 5000
+    out = gather(bank, [torch.zeros(B, dtype=torch.int64, device=gpu)])
+    dy = torch.ones(B, 8, device=gpu)
+    out.backward(dy)
+    g = bank.weight.grad[:, :8].detach().cpu().numpy()
+    assert np.all(g[0] == B) and np.all(g[1:] == 0)
+
+
+def test_backward_large_batch_is_chunked(gpu):
+    """B > MREC_BWD_MAX_BATCH runs as sequential plan/apply chunks."""
+    from pytorchrec_amd.embedding import gather
+    rng = np.random.default_rng(13)
+    B = 40000
+    bank = _bank([700], 8, False, torch.float32, update="dense")
+    _fill(bank, [rng.standard_normal((700, 8)).astype(np.float32)])
+    ids_np = rng.integers(0, 700, B)
+    out = gather(bank, [torch.from_numpy(ids_np).to(gpu)])
+    dy = rng.standard_normal((B, 8)).astype(np.float32)
+    out.backward(torch.from_numpy(dy).to(gpu))
+    want = ref.dense_grad(700, ids_np, dy)
+    np.testing.assert_allclose(bank.weight.grad[:, :8].detach().cpu().numpy(), want, rtol=1e-5,
+                               atol=1e-5 * np.abs(want).max())
+
+
+def test_fm2_dense_kernel(gpu):
+    from pytorchrec_amd.embedding import fm2_dense
+    rng = np.random.default_rng(17)
+    v = rng.standard_normal((300, 13, 24)).astype(np.float32)
+    vt = torch.from_numpy(v).to(gpu).requires_grad_()
+    y = fm2_dense(vt)
+    ok, worst = _fm_tol_ok(y.detach().cpu().numpy().astype(np.float64), v, ref.fm2(v))
+    assert ok, worst
+    dy = rng.standard_normal(300).astype(np.float32)
+    y.backward(torch.from_numpy(dy).to(gpu))
+    np.testing.assert_allclose(vt.grad.detach().cpu().numpy(), ref.fm2_bwd(v, dy), rtol=1e-5, atol=1e-5)

@@ -1,0 +1,309 @@
+#!/usr/bin/env python
+"""DeepFM Criteo-shaped train-step throughput on MI355X (BASELINE.json metric).
+
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--model deepfm|dcnv2|din]
+
+One step = one full training step (interact fwd -> MLP fwd -> BCE -> MLP bwd ->
+embedding sorted-segment backward with the SGD update fused -> SGD on the dense
+params) over one synthetic Criteo-shaped batch that is already
+resident in HBM.  The step is captured once in a HIP graph and replayed; before
+each replay the next of 4 pre-generated batches is copied into the graph's input
+buffer (one D2D copy, inside the timed region).
+
+For N > 1 the driver launches one process per GPU (torch.distributed.run); each
+rank trains on its own 4096 samples (weak scaling) and the MAX elapsed time over
+ranks is reported.  Rank 0 prints ONE JSON line.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import statistics
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+if ROOT not in sys.path:
+    sys.path.insert(0, ROOT)
+
+import torch  # noqa: E402
+
+CRITEO_FIELDS = 26
+CRITEO_DENSE = 13
+CRITEO_ROWS = 38462  # ceil(1,000,000 / 26), SURVEY.md §8(d) C2
+HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md chip table (spec)
+
+
+def parse():
+    p = argparse.ArgumentParser()
+    p.add_argument("--gpus", type=int, default=1)
+    p.add_argument("--steps", type=int, default=50)
+    p.add_argument("--warmup", type=int, default=10)
+    p.add_argument("--model", default="deepfm", choices=["deepfm", "dcnv2", "din"])
+    p.add_argument("--batch", type=int, default=4096)
+    p.add_argument("--rows-per-table", type=int, default=CRITEO_ROWS)
+    p.add_argument("--zipf", type=float, default=0.0, help="Zipf alpha for ids (0 = uniform)")
+    p.add_argument("--lr", type=float, default=1e-2)
+    p.add_argument("--no-graph", action="store_true")
+    p.add_argument("--no-cpu-baseline", action="store_true")
+    p.add_argument("--cpu-seconds", type=float, default=12.0)
+    p.add_argument("--no-roofline", action="store_true")
+    return p.parse_args()
+
+
+# ----------------------------------------------------------------------------
+# workload
+# ----------------------------------------------------------------------------
+
+def build_deepfm(args, device):
+    from pytorchrec_amd.feature_column import CategoricalColumnWithIdentity, NumericColumn
+    from pytorchrec_amd.model import DeepFM
+    sparse = [CategoricalColumnWithIdentity(args.rows_per_table, f"c_c_C{f + 1}")
+              for f in range(CRITEO_FIELDS)]
+    dense = [NumericColumn(f"c_n_I{j + 1}") for j in range(CRITEO_DENSE)]
+    label = CategoricalColumnWithIdentity(2, "label")
+    model = DeepFM(sparse, dense, label, emb_size=16, layers=(400, 400, 400), dropout=0.0,
+                   emb_dtype=torch.bfloat16, device=device, random_seed=2020)
+    return model, sparse, dense, label
+
+
+def make_batch_buffer(args, sparse, seed, device):
+    """One contiguous byte buffer per batch: ids [F, B] int32 | dense [B, 13] f32 |
+    label [B] f32; returns (buffer, views-builder)."""
+    B, F = args.batch, len(sparse)
+    g = torch.Generator(device="cpu").manual_seed(seed)
+    if args.zipf > 0:
+        import numpy as np
+        rng = np.random.default_rng(seed + 1)
+        ids = torch.from_numpy(np.stack([np.minimum(rng.zipf(args.zipf, B) - 1, c.category_num - 1)
+                                         for c in sparse]).astype("int32"))
+    else:
+        ids = torch.stack([torch.randint(0, c.category_num, (B,), generator=g, dtype=torch.int32)
+                           for c in sparse])
+    dense = torch.rand(B, CRITEO_DENSE, generator=torch.Generator().manual_seed(seed + 2))
+    label = (torch.rand(B, generator=torch.Generator().manual_seed(seed + 3)) < 0.25).float()
+    parts = [ids.reshape(-1).view(torch.uint8), dense.reshape(-1).view(torch.uint8),
+             label.view(torch.uint8)]
+    return torch.cat(parts).to(device)
+
+
+def batch_views(buf, args, sparse, dense_cols, label_col):
+    B, F = args.batch, len(sparse)
+    n_ids = F * B * 4
+    n_dense = B * CRITEO_DENSE * 4
+    ids = buf[:n_ids].view(torch.int32).view(F, B)
+    dense = buf[n_ids:n_ids + n_dense].view(torch.float32).view(B, CRITEO_DENSE)
+    label = buf[n_ids + n_dense:n_ids + n_dense + B * 4].view(torch.float32)
+    data = {c.feature_name: ids[f] for f, c in enumerate(sparse)}
+    data["__dense__"] = dense
+    data[label_col.feature_name] = label
+    return data
+
+
+# ----------------------------------------------------------------------------
+# per-kernel roofline (HIP events on the launch stream, eager back-to-back launches)
+# ----------------------------------------------------------------------------
+
+def time_launches(fn, reps=50):
+    s = torch.cuda.current_stream()
+    fn()
+    e0 = torch.cuda.Event(enable_timing=True)
+    e1 = torch.cuda.Event(enable_timing=True)
+    e0.record(s)
+    for _ in range(reps):
+        fn()
+    e1.record(s)
+    e1.synchronize()
+    return e0.elapsed_time(e1) / reps * 1e-3  # seconds per launch
+
+
+def kernel_rooflines(model, data, args):
+    """Average duration of each HBM-bound embedding kernel, launched exactly as the
+    train step launches it, and its algorithmic bytes."""
+    from pytorchrec_amd import _mrec, embedding as E
+    bank = model.embeddings
+    B, F, D = args.batch, bank.n_tables, bank.dim
+    ids = model._ids(data)
+    dense = model._dense(data)
+    out = {}
+    with torch.no_grad():
+        def fwd():
+            E._InteractFn.forward(_Ctx(), bank.weight, model.dense_weight, model.global_bias, None,
+                                  bank, ids, dense, True, True, model.x0_cols, torch.bfloat16)
+        # bytes/sample: ids F*4 + useful row bytes F*(D+1)*2 + dense 13*4 + x0 write
+        # x0_cols*2 + logit 4 + fm_sum D*4
+        fwd_bytes = F * 4 + F * (D + 1) * 2 + CRITEO_DENSE * 4 + model.x0_cols * 2 + 4 + D * 4
+        t = time_launches(fwd)
+        out["mrec_interact_fwd"] = (t, fwd_bytes * B)
+
+        ws, wsb = E._plan(bank, ids, 0, B, None)
+
+        def plan():
+            E._plan(bank, ids, 0, B, None)
+        t = time_launches(plan)
+        out["mrec_emb_bwd_plan"] = (t, (F * 4 + F * 12) * B)
+
+        x0, logit = E._InteractFn.forward(_Ctx(), bank.weight, model.dense_weight,
+                                          model.global_bias, None, bank, ids, dense, True, True,
+                                          model.x0_cols, torch.bfloat16)
+        fm_sum = torch.zeros(B, D, device=x0.device)
+        dx0 = torch.zeros_like(x0)
+        dl = torch.zeros(B, device=x0.device)
+
+        def apply():
+            E._apply(bank, ws, wsb, B, dx=dx0, dfm=dl, fm_sum=fm_sum, x0=x0, dw=dl)
+        t = time_launches(apply)
+        # per lookup: perm 4 + dx D*2 + v re-read D*2 + row read+write 2*(D+1)*2;
+        # per sample: fm_sum D*4 + dlogit 4
+        apply_bytes = F * (4 + D * 2 + D * 2 + 2 * (D + 1) * 2) + D * 4 + 4
+        out["mrec_emb_bwd_apply"] = (t, apply_bytes * B)
+    return out
+
+
+class _Ctx:
+    """Stand-in autograd ctx for calling Function.forward directly."""
+    def save_for_backward(self, *a):
+        pass
+
+
+# ----------------------------------------------------------------------------
+# CPU baseline (oracle restatement of the reference path; rank 0, N = 1 only)
+# ----------------------------------------------------------------------------
+
+def cpu_baseline(args):
+    from oracle.models import RefDeepFM, criteo_batch, sgd_train_step
+    threads = min(16, os.cpu_count() or 1)
+    torch.set_num_threads(threads)
+    nums = [args.rows_per_table] * CRITEO_FIELDS
+    m = RefDeepFM(nums, CRITEO_DENSE, 16, (400, 400, 400))
+    opt = torch.optim.SGD(m.parameters(), lr=args.lr)
+    ids, dense, label = criteo_batch(nums, args.batch, seed=0, zipf=args.zipf)
+    for _ in range(3):
+        sgd_train_step(m, opt, ids, dense, label)
+    ts, t_end = [], time.perf_counter() + args.cpu_seconds
+    while (time.perf_counter() < t_end and len(ts) < 20) or len(ts) < 3:
+        t = time.perf_counter()
+        sgd_train_step(m, opt, ids, dense, label)
+        ts.append(time.perf_counter() - t)
+    med = statistics.median(ts)
+    return {"value": round(args.batch / med, 1), "unit": "samples/s", "cores": threads,
+            "kind": "port",
+            "sample": (f"{len(ts)} timed steps (median, after 3 warm-up) of the fp32 torch-CPU "
+                       f"restatement of the reference path (26 nn.Embedding + 26 Embedding(rows,1), "
+                       f"MLP 429-400-400-400-1, BCE, dense-grad SGD) at B={args.batch}, "
+                       f"{args.rows_per_table} rows/table; {threads} threads"),
+            "ms_per_step": round(med * 1e3, 3)}
+
+
+# ----------------------------------------------------------------------------
+
+def main():
+    args = parse()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        import torch.distributed as dist
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    device = torch.device("cuda", local)
+    torch.cuda.set_device(device)
+
+    if args.model != "deepfm":
+        raise SystemExit("only --model deepfm is wired into bench.py this round")
+    model, sparse, dense_cols, label_col = build_deepfm(args, device)
+    model.compile(torch.optim.SGD(model.get_parameters(), lr=args.lr),
+                  torch.nn.BCEWithLogitsLoss(), [], device)
+    for bank in model.embedding_banks():
+        bank.check_ids = False  # no host sync inside the captured step
+    assert model.embeddings.update == "sgd", "SGD must fuse into the embedding backward"
+
+    bufs = [make_batch_buffer(args, sparse, 1000 * rank + s, device) for s in range(4)]
+    static = bufs[0].clone()
+    data = batch_views(static, args, sparse, dense_cols, label_col)
+
+    def step():
+        return model.train_step(data)["loss"]
+
+    if args.no_graph:
+        def run(i):
+            static.copy_(bufs[i % 4])
+            step()
+    else:
+        s = torch.cuda.Stream()
+        s.wait_stream(torch.cuda.current_stream())
+        with torch.cuda.stream(s):
+            for _ in range(3):
+                step()
+        torch.cuda.current_stream().wait_stream(s)
+        graph = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(graph):
+            step()
+
+        def run(i):
+            static.copy_(bufs[i % 4])
+            graph.replay()
+
+    for i in range(args.warmup):
+        run(i)
+
+    def barrier():
+        if world > 1:
+            torch.distributed.barrier()
+        torch.cuda.synchronize()
+
+    barrier()
+    t0 = time.perf_counter()
+    for i in range(args.steps):
+        run(i)
+    barrier()
+    elapsed = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([elapsed], device=device, dtype=torch.float64)
+        torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX)
+        elapsed = float(t)
+
+    samples = args.batch * world * args.steps
+    result = {
+        "metric": "samples/sec DeepFM Criteo-shaped batch 4096 per GPU (train step)",
+        "value": round(samples / elapsed, 1),
+        "unit": "samples/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": round(elapsed / args.steps * 1e3, 4),
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "bf16",
+        "data": "synthetic (Criteo-shaped: uniform ids seed 0, U[0,1) dense, Bernoulli(0.25) labels)"
+                + (f", zipf {args.zipf}" if args.zipf else ""),
+        "config": {"workload": "DeepFM Criteo-shaped (C2): 26 sparse x %d rows, D=16 bf16 tables "
+                               "with packed first-order weight, 13 dense, MLP 400-400-400, BCE, "
+                               "SGD lr %g (fused row-sparse update)" % (args.rows_per_table, args.lr),
+                   "global_batch": args.batch * world, "batch_per_gpu": args.batch,
+                   "parallelism": f"dp{world}" if world > 1 else "single",
+                   "hip_graph": not args.no_graph},
+    }
+    if rank == 0 and not args.no_roofline:
+        ks = kernel_rooflines(model, data, args)
+        name, (t, nbytes) = max(ks.items(), key=lambda kv: kv[1][0])
+        ach = nbytes / t / 1e9
+        result["roofline"] = {"bound": "hbm", "kernel": name, "achieved": round(ach, 1),
+                              "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                              "frac": round(ach / HBM_PEAK_GBS, 4), "traffic": None,
+                              "avg_us": round(t * 1e6, 3), "bytes_per_launch": nbytes}
+        result["roofline_kernels"] = {k: {"avg_us": round(v[0] * 1e6, 3), "bytes": v[1],
+                                          "GB/s": round(v[1] / v[0] / 1e9, 1)}
+                                      for k, v in ks.items()}
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        result["cpu_baseline"] = cpu_baseline(args)
+    if rank == 0:
+        print(json.dumps(result), flush=True)
+    if world > 1:
+        torch.distributed.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -34,7 +34,7 @@ extern "C" {
 
 #define MREC_ABI_VERSION 1
 #define MREC_MAX_TABLES 64      /* tables per table bank / per call */
-#define MREC_BWD_MAX_BATCH 16384 /* lookups per table per plan/apply call */
+#define MREC_BWD_MAX_BATCH 8192  /* lookups per table per plan/apply call */
 
 typedef enum {
   MREC_OK = 0,
@@ -112,7 +112,8 @@ mrec_status mrec_emb_gather_fwd(const mrec_table_bank *bank, const mrec_ids *ids
  *   x0[b, :]   = [ v_0 .. v_{F-1} (F*dim) | dense[b, 0..n_dense) | 0 .. ]   (x0_cols wide)
  *   logit[b]   = bias + dense[b].dense_w + (FM2 ? fm2(v) : 0) + (FIRST_ORDER ? sum_f w : 0)
  *   fm_sum[b,:] = sum_f v_f   (fp32, saved for the backward; may be NULL)
- * x0 may be NULL (pure FM, config C1); dense/dense_w may be NULL when n_dense==0;
+ * x0 may be NULL (pure FM, config C1); dense may be NULL when n_dense==0, dense_w
+ * NULL drops the dense first-order term (DCN-v2 feeds dense only to x0);
  * bias is a device float[1] (may be NULL = 0).  x0_dtype F32 or BF16.
  * Replaces: nn.Embedding gathers + torch.cat + the FM mul/sum + bias
  * embeddings (FunkSVD.py:47-51, SVDPP.py:57-66, NCF.py:62-70).
@@ -152,11 +153,13 @@ size_t mrec_emb_bwd_workspace_size(int32_t n_tables, int64_t batch);
 /*
  * Deterministic sorted-segment plan: per table, the lookups are sorted by
  * (id, sample) in LDS and segmented by unique row.  Depends only on the ids, so
- * it can run on a side stream as soon as the batch is resident.
+ * it can run on a side stream as soon as the batch is resident.  If d_step
+ * (device uint64, may be NULL) is given the plan increments it once, so a graph
+ * replayed step after step still draws fresh stochastic-rounding bits.
  */
 mrec_status mrec_emb_bwd_plan(const mrec_table_bank *bank, const mrec_ids *ids, int64_t batch,
                               void *workspace, size_t ws_bytes, int32_t *d_oob_flag,
-                              mrec_stream stream);
+                              uint64_t *d_step, mrec_stream stream);
 
 /*
  * Gradient sources of lookup (b, f) (each may be NULL = 0):
@@ -164,7 +167,8 @@ mrec_status mrec_emb_bwd_plan(const mrec_table_bank *bank, const mrec_ids *ids, 
  *          + dfm[b] * (fm_sum[b, d] - v[b, f*dim + d])      (FM2 backward; v read from x0)
  *   g_w    = dw[b]                                          (first-order backward)
  * Segment sums are fp32 in ascending sample order (bitwise reproducible), then
- * applied per unique row as `mode` says.  `seed` drives stochastic rounding.
+ * applied per unique row as `mode` says.  Stochastic rounding draws its bits from
+ * hash(seed + *d_step, row, column) (d_step may be NULL = 0).
  * Replaces aten::embedding_dense_backward + the dense optimizer step
  * (IModel.py:120-124).
  */
@@ -172,8 +176,64 @@ mrec_status mrec_emb_bwd_apply(const mrec_table_bank *bank, int64_t batch, const
                                size_t ws_bytes, const void *dx, mrec_dtype dx_dtype, int64_t dx_ld,
                                const float *dfm, const float *fm_sum, const void *x0,
                                mrec_dtype x0_dtype, int64_t x0_ld, const float *dw,
-                               mrec_bwd_mode mode, float lr, uint64_t seed, void *grad,
-                               mrec_stream stream);
+                               mrec_bwd_mode mode, float lr, uint64_t seed,
+                               const uint64_t *d_step, void *grad, mrec_stream stream);
+
+/* ------------------------------------------------------------------------- */
+/* Dense towers: MFMA bf16 GEMM with fused epilogues                          */
+/* ------------------------------------------------------------------------- */
+
+typedef enum {
+  MREC_LAYOUT_ROW = 0, /* element (i, k) at ptr[i*ld + k]  (k contiguous)   */
+  MREC_LAYOUT_COL = 1  /* element (i, k) at ptr[k*ld + i]  (i contiguous)   */
+} mrec_layout;
+
+typedef struct {
+  const void *ptr; /* device */
+  mrec_dtype dtype;
+  mrec_layout layout;
+  int64_t ld; /* elements */
+} mrec_operand;
+
+#define MREC_ACT_NONE 0
+#define MREC_ACT_RELU 1
+#define MREC_AMOD_NONE 0
+#define MREC_AMOD_RELU_MASK 1 /* A(m,k) *= (mod(m,k) > 0): ReLU backward */
+#define MREC_AMOD_MUL 2       /* A(m,k) *= mod(m,k):      DCN dz = g * x0  */
+
+/* v = acc + bias[n]; aux[m,n] = v; v = act(v); v *= mul[m,n]; v += add[m,n]; C = v.
+ * Every pointer may be NULL (term skipped); mul/add/aux are bf16 [M, ld]. */
+typedef struct {
+  const float *bias;
+  int32_t act;
+  const void *mul;
+  int64_t ld_mul;
+  const void *add;
+  int64_t ld_add;
+  void *aux;
+  int64_t ld_aux;
+} mrec_epilogue;
+
+size_t mrec_gemm_workspace_size(int64_t M, int64_t N, int32_t split_k);
+
+/*
+ * C[M, N'] = epi( sum_k A'(m, k) B(k, n) ),  A' = A modified by a_mod (bf16,
+ * A's layout) as a_mod_kind says.  A bf16; B bf16 or fp32 (converted while
+ * staging — the fp32 master weights are read directly); fp32 accumulation on
+ * v_mfma_f32_16x16x32_bf16.  B(k, n) for layout ROW is ptr[n*ld + k] (nn.Linear's
+ * [out, in] weight), for COL ptr[k*ld + n].  b_ones_col == N appends a column of
+ * ones to B (N' = N + 1), so C[:, N] = sum_k A'(m, k): the bias gradient of a
+ * weight-gradient GEMM.  B(k, n) = 0 for b_cols <= n < N (b_cols <= N), so the
+ * gradient of a zero-padded input comes out zero-padded.  split_k > 1 reduces fp32
+ * slabs in fixed order (deterministic) through `workspace`.
+ * Replaces nn.Linear forward/backward = aten::addmm / mm and the ReLU
+ * (Dense.py:20-24, MLP.py:22-23; SURVEY.md §2b MLP row).
+ */
+mrec_status mrec_gemm(int64_t M, int64_t N, int64_t K, const mrec_operand *A,
+                      const mrec_operand *B, const mrec_operand *a_mod, int32_t a_mod_kind,
+                      int64_t b_ones_col, int64_t b_cols, const mrec_epilogue *epi, void *C,
+                      mrec_dtype c_dtype, int64_t ldc, int32_t split_k, void *workspace,
+                      size_t ws_bytes, mrec_stream stream);
 
 #ifdef __cplusplus
 }

@@ -1,0 +1,121 @@
+"""torch-CPU restatement of the reference training path for the CTR models
+(TEST INFRASTRUCTURE ONLY: checker + bench.py's cpu_baseline leg).
+
+Built exactly from the reference's primitives, the way a PyTorchRec user would
+write these models on the reference:
+  * one ``torch.nn.Embedding(rows_f, D)`` per field (FunkSVD.py:39-41) and one
+    ``Embedding(rows_f, 1)`` first-order bias per field (SVDPP.py:40-41), dense
+    gradients (``sparse=False``) -> ``aten::embedding_dense_backward``;
+  * reference ``MLP`` semantics: Linear -> ReLU per layer (MLP.py:8-23, Dense.py);
+  * init normal(0, 0.01) (IModel._reset_weights_fn, IModel.py:61-68);
+  * step = forward -> BCEWithLogits -> zero_grad -> backward -> SGD.step over ALL
+    parameters, i.e. ``IModel.train_step`` (IModel.py:116-125).
+
+``dtype=torch.float64`` gives the model-level parity oracle; float32 is the CPU
+baseline (SURVEY.md §8(d) "CPU baseline").
+"""
+from __future__ import annotations
+
+from typing import List, Sequence
+
+import torch
+from torch import nn
+
+
+def _reset(m):
+    if isinstance(m, (nn.Linear, nn.Embedding)):
+        nn.init.normal_(m.weight, 0.0, 0.01)
+        if isinstance(m, nn.Linear) and m.bias is not None:
+            nn.init.normal_(m.bias, 0.0, 0.01)
+
+
+def _mlp(units: Sequence[int]) -> nn.Sequential:
+    layers = []
+    for a, b in zip(units[:-1], units[1:]):
+        layers += [nn.Linear(a, b), nn.ReLU()]
+    return nn.Sequential(*layers)
+
+
+class RefDeepFM(nn.Module):
+    """DeepFM the reference way.  ``deep=False`` gives FM (config C1)."""
+
+    def __init__(self, category_nums: List[int], n_dense: int, emb_size: int = 16,
+                 layers=(400, 400, 400), deep: bool = True, dtype=torch.float32, seed: int = 2020):
+        super().__init__()
+        torch.manual_seed(seed)
+        self.F, self.D, self.n_dense = len(category_nums), emb_size, n_dense
+        self.emb = nn.ModuleList([nn.Embedding(n, emb_size) for n in category_nums])
+        self.w1 = nn.ModuleList([nn.Embedding(n, 1) for n in category_nums])
+        self.dense_w = nn.Linear(n_dense, 1, bias=False) if n_dense else None
+        self.global_bias = nn.Parameter(torch.zeros(1))
+        self.deep = deep
+        if deep:
+            self.mlp = _mlp([self.F * emb_size + n_dense, *layers])
+            self.out = nn.Linear(layers[-1], 1)
+        self.apply(_reset)
+        self.to(dtype)
+
+    def forward(self, ids: torch.Tensor, dense: torch.Tensor | None):
+        """ids [B, F] int64, dense [B, n_dense] -> logits [B]."""
+        v = torch.stack([e(ids[:, f]) for f, e in enumerate(self.emb)], 1)  # [B, F, D]
+        s = v.sum(1)
+        logit = 0.5 * (s * s - (v * v).sum(1)).sum(-1)
+        logit = logit + torch.cat([w(ids[:, f]) for f, w in enumerate(self.w1)], 1).sum(1)
+        logit = logit + self.global_bias
+        if self.dense_w is not None:
+            logit = logit + self.dense_w(dense).squeeze(-1)
+        if self.deep:
+            x0 = torch.cat([v.reshape(v.shape[0], -1)] + ([dense] if self.n_dense else []), 1)
+            logit = logit + self.out(self.mlp(x0)).squeeze(-1)
+        return logit
+
+
+class RefDCNv2(nn.Module):
+    """Stacked DCN-v2 the reference way (cross layers = nn.Linear(d, d))."""
+
+    def __init__(self, category_nums: List[int], n_dense: int, emb_size=16, n_cross=3,
+                 layers=(400, 400), dtype=torch.float32, seed=2020):
+        super().__init__()
+        torch.manual_seed(seed)
+        self.emb = nn.ModuleList([nn.Embedding(n, emb_size) for n in category_nums])
+        d = len(category_nums) * emb_size + n_dense
+        self.cross = nn.ModuleList([nn.Linear(d, d) for _ in range(n_cross)])
+        self.mlp = _mlp([d, *layers])
+        self.out = nn.Linear(layers[-1], 1)
+        self.apply(_reset)
+        self.to(dtype)
+
+    def forward(self, ids, dense):
+        v = torch.cat([e(ids[:, f]) for f, e in enumerate(self.emb)], 1)
+        x0 = torch.cat([v, dense], 1) if dense is not None else v
+        x = x0
+        for c in self.cross:
+            x = x0 * c(x) + x
+        return self.out(self.mlp(x)).squeeze(-1)
+
+
+def sgd_train_step(model: nn.Module, opt: torch.optim.Optimizer, ids, dense, label):
+    """``IModel.train_step`` (IModel.py:116-125) with BCEWithLogitsLoss."""
+    logit = model(ids, dense)
+    loss = torch.nn.functional.binary_cross_entropy_with_logits(logit, label.to(logit.dtype))
+    opt.zero_grad()
+    loss.backward()
+    opt.step()
+    return loss
+
+
+def criteo_batch(category_nums, batch: int, n_dense: int = 13, seed: int = 0, zipf: float = 0.0,
+                 label_rate: float = 0.25):
+    """SURVEY.md §8(d) synthetic Criteo-shaped batch: ids uniform (seed 0) or Zipf
+    (seed 1), dense U[0,1) (seed 2), labels Bernoulli(0.25) (seed 3)."""
+    import numpy as np
+    F = len(category_nums)
+    rng = np.random.default_rng(seed)
+    if zipf:
+        ids = np.stack([np.minimum(rng.zipf(zipf, batch) - 1, n - 1) for n in category_nums], 1)
+    else:
+        ids = np.stack([rng.integers(0, n, batch) for n in category_nums], 1)
+    dense = np.random.default_rng(seed + 2).random((batch, n_dense), dtype=np.float32)
+    label = (np.random.default_rng(seed + 3).random(batch) < label_rate).astype(np.float32)
+    return (torch.from_numpy(ids.astype(np.int64)), torch.from_numpy(dense),
+            torch.from_numpy(label))

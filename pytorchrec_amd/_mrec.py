@@ -22,7 +22,7 @@ LIB_PATH = os.path.join(LIB_DIR, "libmrec.so")
 
 ABI_VERSION = 1
 MAX_TABLES = 64
-BWD_MAX_BATCH = 16384
+BWD_MAX_BATCH = 8192
 
 # mrec_status
 OK, EINVAL, EOOB, EHIP, ERCCL, ENOSPC = range(6)
@@ -65,6 +65,22 @@ class Ids(ctypes.Structure):
                 ("stride", ctypes.c_int64)]
 
 
+class Operand(ctypes.Structure):
+    _fields_ = [("ptr", ctypes.c_void_p), ("dtype", ctypes.c_int), ("layout", ctypes.c_int),
+                ("ld", ctypes.c_int64)]
+
+
+class Epilogue(ctypes.Structure):
+    _fields_ = [("bias", ctypes.c_void_p), ("act", ctypes.c_int32),
+                ("mul", ctypes.c_void_p), ("ld_mul", ctypes.c_int64),
+                ("add", ctypes.c_void_p), ("ld_add", ctypes.c_int64),
+                ("aux", ctypes.c_void_p), ("ld_aux", ctypes.c_int64)]
+
+
+LAYOUT_ROW, LAYOUT_COL = 0, 1
+ACT_NONE, ACT_RELU = 0, 1
+AMOD_NONE, AMOD_RELU_MASK, AMOD_MUL = 0, 1, 2
+
 _vp = ctypes.c_void_p
 _i32 = ctypes.c_int32
 _i64 = ctypes.c_int64
@@ -72,6 +88,8 @@ _f32 = ctypes.c_float
 _fp = ctypes.POINTER(ctypes.c_float)
 _bank_p = ctypes.POINTER(TableBank)
 _ids_p = ctypes.POINTER(Ids)
+_op_p = ctypes.POINTER(Operand)
+_epi_p = ctypes.POINTER(Epilogue)
 
 # name -> (restype, argtypes); the set the header declares (checked by tests)
 SIGNATURES = {
@@ -84,10 +102,14 @@ SIGNATURES = {
     "mrec_fm2_fwd": (ctypes.c_int, [_vp, _i64, _i32, _i32, _vp, _vp]),
     "mrec_fm2_bwd": (ctypes.c_int, [_vp, _vp, _i64, _i32, _i32, _vp, _vp]),
     "mrec_emb_bwd_workspace_size": (ctypes.c_size_t, [_i32, _i64]),
-    "mrec_emb_bwd_plan": (ctypes.c_int, [_bank_p, _ids_p, _i64, _vp, ctypes.c_size_t, _vp, _vp]),
+    "mrec_emb_bwd_plan": (ctypes.c_int, [_bank_p, _ids_p, _i64, _vp, ctypes.c_size_t, _vp, _vp,
+                                         _vp]),
     "mrec_emb_bwd_apply": (ctypes.c_int, [_bank_p, _i64, _vp, ctypes.c_size_t, _vp, ctypes.c_int,
                                           _i64, _vp, _vp, _vp, ctypes.c_int, _i64, _vp,
-                                          ctypes.c_int, _f32, ctypes.c_uint64, _vp, _vp]),
+                                          ctypes.c_int, _f32, ctypes.c_uint64, _vp, _vp, _vp]),
+    "mrec_gemm_workspace_size": (ctypes.c_size_t, [_i64, _i64, _i32]),
+    "mrec_gemm": (ctypes.c_int, [_i64, _i64, _i64, _op_p, _op_p, _op_p, _i32, _i64, _i64, _epi_p,
+                                 _vp, ctypes.c_int, _i64, _i32, _vp, ctypes.c_size_t, _vp]),
 }
 
 _lib = None

@@ -68,7 +68,7 @@ def interact(bank, ids, dense: Optional[torch.Tensor], dense_w, bias, use_fm2: b
     logit = torch.zeros(B, dtype=torch.float32)
     if bias is not None:
         logit = logit + bias.float()
-    if dense is not None:
+    if dense is not None and dense_w is not None:
         logit = logit + dense.float() @ dense_w.float()
     if use_fm2:
         logit = logit + fm2(v)

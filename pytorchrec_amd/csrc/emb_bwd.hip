@@ -1,8 +1,8 @@
 // Embedding backward: deterministic sorted-segment scatter-add with a fused
 // row-sparse update.
 //
-// plan  : one 1024-thread workgroup per table sorts its (id, sample) keys with
-//         an LDS bitonic network (<= 16384 keys, 128 KiB of LDS), then emits the
+// plan  : one 1024-thread workgroup per table sorts its ids with a stable LDS
+//         radix sort (<= 8192 keys, 4-bit digits), then emits the
 //         permutation, the unique rows and their segment starts.  Depends only on
 //         the ids, so it can overlap the MLP forward on a side stream.
 // apply : one LPR-lane worker per unique row sums the per-lookup gradients of
@@ -15,7 +15,7 @@
 namespace mrec {
 
 constexpr int kPlanThreads = 1024;
-constexpr int kMaxPlanKeys = 16384;
+constexpr int kMaxPlanKeys = 8192;
 constexpr int kShortSeg = 16;
 
 struct TableWs {  // per-table workspace view
@@ -45,98 +45,155 @@ __host__ __device__ inline TableWs table_ws(const void *ws, int f, int64_t batch
 }
 
 // ---------------------------------------------------------------------------
-// plan
+// plan: stable LSD radix sort of the table's ids in LDS
 // ---------------------------------------------------------------------------
-__global__ __launch_bounds__(kPlanThreads) void plan_kernel(BankArgs bank, IdsArgs ids, int64_t B,
-                                                            int NP, void *ws,
-                                                            int32_t *__restrict__ oob) {
-  __shared__ uint64_t keys[kMaxPlanKeys];
-  __shared__ int32_t wsum[kPlanThreads / 64 + 1];
-  __shared__ int32_t s_nvalid;
-  const int f = blockIdx.x;
-  const int tid = threadIdx.x;
-  const int64_t rows = bank.rows[f];
-  if (tid == 0) s_nvalid = 0;
-  for (int i = tid; i < NP; i += kPlanThreads) {
-    uint64_t key = ~0ull;
-    if (i < B) {
-      const int64_t id = load_id(ids, f, i);
-      if (id >= 0 && id < rows) {
-        key = (static_cast<uint64_t>(id) << 32) | static_cast<uint32_t>(i);
-      } else {
-        key = (0xffffffffull << 32) | static_cast<uint32_t>(i);
-        if (oob) *oob = 1;
-      }
-    }
-    keys[i] = key;
+// Element i (= sample b, ascending) sits in "round" r = i / 1024, lane t = i % 1024,
+// so a wave's 64 lanes hold 64 consecutive elements and the (round, wave) groups
+// are in element order.  Each 4-bit pass ranks an element inside its wave with
+// 4 ballots (lanes with the same digit), writes per-(digit, group) counts in
+// digit-major order, and one block scan of that array gives every element's
+// destination: digit base + earlier groups with that digit + rank in wave.
+// Stability makes equal ids keep ascending b, so segments come out in the
+// reference's accumulation order.  Invalid ids (out of range, padding) get the
+// key `rows`, one past every valid id, and therefore sort last.
+constexpr int kRadixBits = 4;
+constexpr int kDigits = 1 << kRadixBits;
+constexpr int kMaxRounds = kMaxPlanKeys / kPlanThreads;  // 8
+constexpr int kMaxGroups = kMaxRounds * (kPlanThreads / 64);  // 128
+
+__device__ __forceinline__ uint64_t digit_peers(uint32_t d) {
+  uint64_t m = ~0ull;
+#pragma unroll
+  for (int k = 0; k < kRadixBits; ++k) {
+    const uint64_t bk = __ballot((d >> k) & 1u);
+    m &= ((d >> k) & 1u) ? bk : ~bk;
   }
-  __syncthreads();
-  // bitonic network, ascending; every thread owns NP/2/threads comparators
-  for (int k = 2; k <= NP; k <<= 1) {
-    for (int j = k >> 1; j > 0; j >>= 1) {
-      for (int p = tid; p < (NP >> 1); p += kPlanThreads) {
-        const int i = 2 * j * (p / j) + (p % j);
-        const int ix = i + j;
-        const uint64_t a = keys[i], c = keys[ix];
-        const bool up = (i & k) == 0;
-        if ((a > c) == up) {
-          keys[i] = c;
-          keys[ix] = a;
-        }
-      }
-      __syncthreads();
-    }
-  }
-  // segment heads: contiguous chunk per thread, block exclusive scan of counts
-  const int chunk = (NP + kPlanThreads - 1) / kPlanThreads;
-  const int lo = tid * chunk;
-  const int hi = min(lo + chunk, NP);
-  int cnt = 0;
-  for (int i = lo; i < hi; ++i) {
-    const uint32_t id = static_cast<uint32_t>(keys[i] >> 32);
-    const bool valid = id != 0xffffffffu;
-    if (valid && (i == 0 || static_cast<uint32_t>(keys[i - 1] >> 32) != id)) ++cnt;
-    if (valid && (i + 1 == NP || static_cast<uint32_t>(keys[i + 1] >> 32) == 0xffffffffu))
-      s_nvalid = i + 1;  // exactly one writer: the last valid position
-  }
-  const int lane = tid & 63, wid = tid >> 6;
-  int incl = cnt;
+  return m;
+}
+
+// block-wide exclusive scan of n <= 2*kPlanThreads uint32 values in place
+__device__ void block_exclusive_scan(uint32_t *a, int n, uint32_t *wtot, uint32_t *total) {
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int i0 = 2 * tid;
+  const uint32_t v0 = i0 < n ? a[i0] : 0u;
+  const uint32_t v1 = i0 + 1 < n ? a[i0 + 1] : 0u;
+  uint32_t incl = v0 + v1;
 #pragma unroll
   for (int off = 1; off < 64; off <<= 1) {
-    const int t = __shfl_up(incl, off);
+    const uint32_t t = __shfl_up(incl, off);
     if (lane >= off) incl += t;
   }
-  if (lane == 63) wsum[wid] = incl;
+  if (lane == 63) wtot[wid] = incl;
   __syncthreads();
-  if (tid == 0) {
-    int run = 0;
-    for (int w = 0; w < kPlanThreads / 64; ++w) {
-      const int t = wsum[w];
-      wsum[w] = run;
-      run += t;
+  if (wid == 0) {
+    uint32_t w = lane < kPlanThreads / 64 ? wtot[lane] : 0u;
+    uint32_t wi = w;
+#pragma unroll
+    for (int off = 1; off < 64; off <<= 1) {
+      const uint32_t t = __shfl_up(wi, off);
+      if (lane >= off) wi += t;
     }
-    wsum[kPlanThreads / 64] = run;
+    if (lane < kPlanThreads / 64) wtot[lane] = wi - w;
+    if (lane == kPlanThreads / 64 - 1 && total) *total = wi;
   }
   __syncthreads();
-  int u = wsum[wid] + incl - cnt;  // exclusive prefix
-  TableWs t = table_ws(ws, f, B);
-  const int nvalid = s_nvalid;
+  const uint32_t ex = wtot[wid] + incl - v0 - v1;
+  if (i0 < n) a[i0] = ex;
+  if (i0 + 1 < n) a[i0 + 1] = ex + v0;
+  __syncthreads();
+}
+
+__global__ __launch_bounds__(kPlanThreads) void plan_kernel(BankArgs bank, IdsArgs ids, int64_t B,
+                                                            int rounds, void *ws,
+                                                            int32_t *__restrict__ oob,
+                                                            uint64_t *__restrict__ d_step) {
+  __shared__ uint32_t keyA[kMaxPlanKeys], keyB[kMaxPlanKeys];
+  __shared__ uint16_t payA[kMaxPlanKeys], payB[kMaxPlanKeys];
+  __shared__ uint32_t hist[kDigits * kMaxGroups];
+  __shared__ uint32_t wtot[kPlanThreads / 64];
+  __shared__ uint32_t s_total;
+  __shared__ int32_t s_nvalid;
+  const int f = blockIdx.x;
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const uint32_t rows = static_cast<uint32_t>(bank.rows[f]);
+  const int N = rounds * kPlanThreads;
+  const int G = rounds * (kPlanThreads / 64);
+  for (int i = tid; i < N; i += kPlanThreads) {
+    uint32_t key = rows;  // invalid / padding
+    if (i < B) {
+      const int64_t id = load_id(ids, f, i);
+      if (id >= 0 && id < static_cast<int64_t>(rows)) {
+        key = static_cast<uint32_t>(id);
+      } else if (oob) {
+        *oob = 1;
+      }
+    }
+    keyA[i] = key;
+    payA[i] = static_cast<uint16_t>(i);
+  }
+  if (tid == 0) s_nvalid = 0;
+  const int bits = 32 - __clz(rows);  // covers every key value 0..rows
+  const int passes = (bits + kRadixBits - 1) / kRadixBits;
+  uint32_t *kin = keyA, *kout = keyB;
+  uint16_t *pin = payA, *pout = payB;
+  const uint64_t lt = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
+  __syncthreads();
+  for (int p = 0; p < passes; ++p) {
+    const int sh = p * kRadixBits;
+    for (int i = tid; i < kDigits * G; i += kPlanThreads) hist[i] = 0u;
+    __syncthreads();
+    for (int r = 0; r < rounds; ++r) {
+      const uint32_t d = (kin[r * kPlanThreads + tid] >> sh) & (kDigits - 1);
+      const uint64_t m = digit_peers(d);
+      if ((m & lt) == 0) hist[d * G + r * (kPlanThreads / 64) + wid] = __popcll(m);
+    }
+    __syncthreads();
+    block_exclusive_scan(hist, kDigits * G, wtot, nullptr);
+    for (int r = 0; r < rounds; ++r) {
+      const int i = r * kPlanThreads + tid;
+      const uint32_t key = kin[i];
+      const uint32_t d = (key >> sh) & (kDigits - 1);
+      const uint64_t m = digit_peers(d);
+      const uint32_t dst = hist[d * G + r * (kPlanThreads / 64) + wid] + __popcll(m & lt);
+      kout[dst] = key;
+      pout[dst] = pin[i];
+    }
+    __syncthreads();
+    uint32_t *tk = kin; kin = kout; kout = tk;
+    uint16_t *tp = pin; pin = pout; pout = tp;
+  }
+  // segments: head flags over the sorted valid prefix, block scan of per-thread counts
+  const int chunk = (N + kPlanThreads - 1) / kPlanThreads;
+  const int lo = tid * chunk;
+  const int hi = min(lo + chunk, N);
+  uint32_t cnt = 0;
   for (int i = lo; i < hi; ++i) {
-    const uint64_t key = keys[i];
-    const uint32_t id = static_cast<uint32_t>(key >> 32);
-    if (id == 0xffffffffu) break;
-    t.perm[i] = static_cast<int32_t>(key & 0xffffffffu);
-    if (i == 0 || static_cast<uint32_t>(keys[i - 1] >> 32) != id) {
+    const uint32_t k = kin[i];
+    if (k < rows && (i == 0 || kin[i - 1] != k)) ++cnt;
+  }
+  hist[tid] = cnt;
+  __syncthreads();
+  block_exclusive_scan(hist, kPlanThreads, wtot, &s_total);
+  uint32_t u = hist[tid];
+  TableWs t = table_ws(ws, f, B);
+  for (int i = lo; i < hi; ++i) {
+    const uint32_t k = kin[i];
+    if (k >= rows) break;
+    t.perm[i] = pin[i];
+    if (i == 0 || kin[i - 1] != k) {
       t.seg[u] = i;
-      t.uniq[u] = static_cast<int32_t>(id);
+      t.uniq[u] = static_cast<int32_t>(k);
       ++u;
     }
+    if (i + 1 == N || kin[i + 1] >= rows) s_nvalid = i + 1;  // the one last valid element
   }
+  __syncthreads();
   if (tid == 0) {
-    const int nu = wsum[kPlanThreads / 64];
+    const int nu = static_cast<int>(s_total);
     t.hdr[0] = nu;
-    t.hdr[1] = nvalid;
-    t.seg[nu] = nvalid;
+    t.hdr[1] = s_nvalid;
+    t.seg[nu] = s_nvalid;
+    if (d_step && f == 0) *d_step += 1;
   }
 }
 
@@ -156,6 +213,7 @@ struct ApplyArgs {
   int mode;
   float lr;
   uint64_t seed;
+  const uint64_t *d_step;
   void *grad;
 };
 
@@ -266,6 +324,7 @@ __device__ __forceinline__ void apply_row(const BankArgs &bank, const ApplyArgs 
 template <typename T, int LPR>
 __global__ __launch_bounds__(256) void apply_kernel(BankArgs bank, int64_t B, const void *ws,
                                                     ApplyArgs a) {
+  if (a.d_step) a.seed += *a.d_step * 0x9e3779b97f4a7c15ull;
   constexpr int EPL = Vec<T>::EPL;
   constexpr int WPB = 256 / LPR;
   __shared__ int32_t long_list[WPB];
@@ -356,7 +415,7 @@ size_t mrec_emb_bwd_workspace_size(int32_t n_tables, int64_t batch) {
 
 mrec_status mrec_emb_bwd_plan(const mrec_table_bank *bank, const mrec_ids *ids, int64_t batch,
                               void *workspace, size_t ws_bytes, int32_t *d_oob_flag,
-                              mrec_stream stream) {
+                              uint64_t *d_step, mrec_stream stream) {
   BankArgs ba;
   IdsArgs ia;
   int eb, lpr;
@@ -371,11 +430,9 @@ mrec_status mrec_emb_bwd_plan(const mrec_table_bank *bank, const mrec_ids *ids, 
   }
   for (int f = 0; f < ba.n_tables; ++f)
     MREC_CHECK_ARG(ba.rows[f] < (int64_t(1) << 31), "rows per table must be < 2^31");
-  int np = 1;
-  while (np < batch) np <<= 1;
-  if (np < 2) np = 2;
+  const int rounds = static_cast<int>((batch + kPlanThreads - 1) / kPlanThreads);
   plan_kernel<<<dim3(ba.n_tables), kPlanThreads, 0, static_cast<hipStream_t>(stream)>>>(
-      ba, ia, batch, np, workspace, d_oob_flag);
+      ba, ia, batch, rounds < 1 ? 1 : rounds, workspace, d_oob_flag, d_step);
   return launch_status("mrec_emb_bwd_plan");
 }
 
@@ -383,8 +440,8 @@ mrec_status mrec_emb_bwd_apply(const mrec_table_bank *bank, int64_t batch, const
                                size_t ws_bytes, const void *dx, mrec_dtype dx_dtype, int64_t dx_ld,
                                const float *dfm, const float *fm_sum, const void *x0,
                                mrec_dtype x0_dtype, int64_t x0_ld, const float *dw,
-                               mrec_bwd_mode mode, float lr, uint64_t seed, void *grad,
-                               mrec_stream stream) {
+                               mrec_bwd_mode mode, float lr, uint64_t seed,
+                               const uint64_t *d_step, void *grad, mrec_stream stream) {
   BankArgs ba;
   int eb, lpr;
   mrec_status st = make_bank_args(bank, &ba, &eb, &lpr);
@@ -430,6 +487,7 @@ mrec_status mrec_emb_bwd_apply(const mrec_table_bank *bank, int64_t batch, const
   a.mode = mode;
   a.lr = lr;
   a.seed = seed;
+  a.d_step = d_step;
   a.grad = grad;
   hipStream_t s = static_cast<hipStream_t>(stream);
   const int wpb = 256 / lpr;

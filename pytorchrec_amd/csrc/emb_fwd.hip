@@ -167,7 +167,8 @@ __global__ __launch_bounds__(256) void interact_kernel(
 
   // dense features: first-order dot + copy into x0, zero the pad columns
   float ds = 0.f;
-  for (int j = lane; j < n_dense; j += 64) ds = fmaf(dense[b * dense_ld + j], dense_w[j], ds);
+  if (dense_w)
+    for (int j = lane; j < n_dense; j += 64) ds = fmaf(dense[b * dense_ld + j], dense_w[j], ds);
 #pragma unroll
   for (int off = 1; off < 64; off <<= 1) ds += __shfl_xor(ds, off);
   if (x0v) {
@@ -320,8 +321,8 @@ mrec_status mrec_interact_fwd(const mrec_table_bank *bank, const mrec_ids *ids, 
   if ((st = make_ids_args(ids, ba.n_tables, &ia)) != MREC_OK) return st;
   MREC_CHECK_ARG(batch >= 0, "batch < 0");
   MREC_CHECK_ARG(n_dense >= 0, "n_dense < 0");
-  MREC_CHECK_ARG(n_dense == 0 || (dense != nullptr && dense_w != nullptr && dense_ld >= n_dense),
-                 "dense/dense_w NULL or dense_ld < n_dense");
+  MREC_CHECK_ARG(n_dense == 0 || (dense != nullptr && dense_ld >= n_dense),
+                 "dense NULL or dense_ld < n_dense");
   MREC_CHECK_ARG(!(flags & MREC_INTERACT_FIRST_ORDER) || ba.has_w,
                  "FIRST_ORDER requested but bank has no w column");
   if (x0) {

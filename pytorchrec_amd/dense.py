@@ -1,0 +1,207 @@
+"""Dense-tower ops: Linear(+bias)(+ReLU), DCN-v2 cross, DIN attention pooling.
+
+One seam for the model code.  On a GPU they run on libmrec's MFMA bf16 GEMM
+(``mrec_gemm``: fp32 accumulation, bias / ReLU / DCN epilogues fused, the fp32
+master weights converted to bf16 while staging, ReLU' and ``g * x0`` applied
+while staging the backward operand, the bias gradient carried as an extra ones
+column of the weight-gradient GEMM).  On a CPU device (config C1) they are the
+reference's fp32 torch ops.
+
+Activation tensors are [M, N] views of [M, round8(N)] bf16 buffers so every
+row starts 16-byte aligned.
+"""
+from __future__ import annotations
+
+import ctypes
+from typing import Optional
+
+import torch
+import torch.nn.functional as F
+
+from pytorchrec_amd import _mrec
+
+_BF16 = torch.bfloat16
+
+
+def _r8(n: int) -> int:
+    return (n + 7) // 8 * 8
+
+
+def _alloc(M: int, N: int, dtype, device) -> torch.Tensor:
+    return torch.empty(M, _r8(N), dtype=dtype, device=device)[:, :N]
+
+
+def _op(t: torch.Tensor, layout: int) -> _mrec.Operand:
+    if t.dim() != 2 or t.stride(1) != 1:
+        raise ValueError("GEMM operands must be 2-D with unit inner stride")
+    return _mrec.Operand(t.data_ptr(), _mrec.dtype_code(t.dtype), layout, t.stride(0))
+
+
+def _split_for(M: int, N: int, K: int) -> int:
+    """Split-K so that a small-output, long-K GEMM (weight gradients) fills the chip."""
+    tiles = ((M + 63) // 64) * ((N + 63) // 64)
+    s = 1
+    while tiles * s < 256 and K // (s * 2) >= 256 and s < 16:
+        s *= 2
+    return s
+
+
+def gemm(A, a_layout, B, b_layout, M, N, K, *, a_mod=None, a_mod_kind=0, ones_col=False,
+         b_cols=None, bias=None, act=0, mul=None, add=None, aux=None, out=None,
+         out_dtype=_BF16, split_k=None):
+    """C[M, N(+1)] = epi(A'[M, K] @ B[K, N]) on libmrec (see include/mrec.h mrec_gemm)."""
+    dev = A.device
+    ncols = N + 1 if ones_col else N
+    if out is None:
+        out = _alloc(M, ncols, out_dtype, dev)
+    if split_k is None:
+        split_k = _split_for(M, ncols, K)
+    ws_bytes = _mrec.lib().mrec_gemm_workspace_size(M, N, split_k)
+    ws = torch.empty(ws_bytes, dtype=torch.uint8, device=dev) if ws_bytes else None
+    epi = _mrec.Epilogue(_mrec.ptr(bias), act, _mrec.ptr(mul), mul.stride(0) if mul is not None else 0,
+                         _mrec.ptr(add), add.stride(0) if add is not None else 0,
+                         _mrec.ptr(aux), aux.stride(0) if aux is not None else 0)
+    a_op, b_op = _op(A, a_layout), _op(B, b_layout)
+    m_op = _op(a_mod, a_layout) if a_mod is not None else None
+    _mrec.call("mrec_gemm", M, N, K, ctypes.byref(a_op), ctypes.byref(b_op),
+               ctypes.byref(m_op) if m_op is not None else None, a_mod_kind,
+               N if ones_col else -1, N if b_cols is None else b_cols, ctypes.byref(epi),
+               out.data_ptr(), _mrec.dtype_code(out.dtype), out.stride(0), split_k,
+               _mrec.ptr(ws), ws_bytes, _mrec.stream_handle())
+    return out
+
+
+def _bf16_rows(t: torch.Tensor) -> torch.Tensor:
+    if t.dtype != _BF16:
+        t = t.to(_BF16)
+    if t.stride(-1) != 1:
+        t = t.contiguous()
+    return t
+
+
+def _weight_f32(w: torch.Tensor) -> torch.Tensor:
+    w = w.detach()
+    if w.dtype != torch.float32:
+        w = w.float()
+    return w if w.stride(1) == 1 else w.contiguous()
+
+
+class _LinearFn(torch.autograd.Function):
+    """y = act(x[:, :K] W^T + b) with W [N, K] fp32 (nn.Linear layout)."""
+
+    @staticmethod
+    def forward(ctx, x, weight, bias, relu: bool, out_dtype):
+        x = _bf16_rows(x)
+        M, K_x = x.shape
+        N, K = weight.shape
+        W = _weight_f32(weight)
+        b = bias.detach().float().contiguous() if bias is not None else None
+        y = gemm(x, _mrec.LAYOUT_ROW, W, _mrec.LAYOUT_ROW, M, N, K, bias=b,
+                 act=_mrec.ACT_RELU if relu else _mrec.ACT_NONE, out_dtype=out_dtype)
+        ctx.save_for_backward(x, W, y if relu else None)
+        ctx.relu, ctx.has_bias, ctx.K_x = relu, bias is not None, K_x
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        x, W, y = ctx.saved_tensors
+        M, K_x = x.shape
+        N, K = W.shape
+        dy = _bf16_rows(dy)
+        mod_kind = _mrec.AMOD_RELU_MASK if ctx.relu else _mrec.AMOD_NONE
+        dx = dW = db = None
+        if ctx.needs_input_grad[0]:
+            # dx[m, k] = sum_n dZ[m, n] W[n, k]; B(k'=n, col=k) = W[n*ld + k] -> COL
+            dx = gemm(dy, _mrec.LAYOUT_ROW, W, _mrec.LAYOUT_COL, M, K_x, N, a_mod=y,
+                      a_mod_kind=mod_kind, b_cols=K, out_dtype=_BF16)
+        if ctx.needs_input_grad[1] or ctx.needs_input_grad[2]:
+            # dW[n, k] = sum_m dZ[m, n] x[m, k]: A(i=n, red=m) = dy[m*ld + n] -> COL,
+            # B(red=m, col=k) = x[m*ld + k] -> COL; ones column -> db
+            g = gemm(dy, _mrec.LAYOUT_COL, x, _mrec.LAYOUT_COL, N, K, M, a_mod=y,
+                     a_mod_kind=mod_kind, ones_col=ctx.has_bias, out_dtype=torch.float32)
+            dW = g[:, :K]
+            db = g[:, K] if ctx.has_bias else None
+        return dx, dW, db, None, None
+
+
+def linear(x: torch.Tensor, weight: torch.Tensor, bias: Optional[torch.Tensor],
+           act: Optional[str] = None, out_dtype=_BF16) -> torch.Tensor:
+    """y = act(x W^T + b), W stored [out, in] like nn.Linear (Dense.py:12).  x may
+    carry zero pad columns beyond in_features; they are ignored (and get a zero
+    gradient)."""
+    if not x.is_cuda:
+        k = weight.shape[1]
+        xx = x[:, :k] if x.shape[1] > k else x
+        y = F.linear(xx.float(), weight.float(), None if bias is None else bias.float())
+        return torch.relu(y) if act == "relu" else y
+    return _LinearFn.apply(x, weight, bias, act == "relu", out_dtype)
+
+
+class _CrossFn(torch.autograd.Function):
+    """DCN-v2 layer x_{l+1} = x0 * (x_l W^T + b) + x_l (one GEMM, epilogue fused;
+    z = x_l W^T + b kept for the backward)."""
+
+    @staticmethod
+    def forward(ctx, x0, xl, weight, bias):
+        x0, xl = _bf16_rows(x0), _bf16_rows(xl)
+        M = xl.shape[0]
+        d = weight.shape[0]
+        W = _weight_f32(weight)
+        b = bias.detach().float().contiguous() if bias is not None else None
+        z = _alloc(M, d, _BF16, xl.device)
+        out = gemm(xl, _mrec.LAYOUT_ROW, W, _mrec.LAYOUT_ROW, M, d, d, bias=b, mul=x0, add=xl,
+                   aux=z)
+        ctx.save_for_backward(x0, xl, W, z)
+        ctx.has_bias = bias is not None
+        ctx.shapes = (x0.shape, xl.shape)
+        return out
+
+    @staticmethod
+    def backward(ctx, g):
+        x0, xl, W, z = ctx.saved_tensors
+        g = _bf16_rows(g)
+        M = g.shape[0]
+        d = W.shape[0]
+        # dz = g * x0 (applied while staging A); dx_l = dz W + g; dW = dz^T x_l; db = sum dz
+        dxl = gemm(g, _mrec.LAYOUT_ROW, W, _mrec.LAYOUT_COL, M, xl.shape[1], d, a_mod=x0,
+                   a_mod_kind=_mrec.AMOD_MUL, b_cols=d, add=_pad_cols(g, xl.shape[1]))
+        gw = gemm(g, _mrec.LAYOUT_COL, xl, _mrec.LAYOUT_COL, d, d, M, a_mod=x0,
+                  a_mod_kind=_mrec.AMOD_MUL, ones_col=ctx.has_bias, out_dtype=torch.float32)
+        dx0 = (g.float() * z.float()).to(_BF16)
+        if x0.shape[1] > d:
+            dx0 = F.pad(dx0, (0, x0.shape[1] - d))
+        return dx0, dxl, gw[:, :d], (gw[:, d] if ctx.has_bias else None)
+
+
+def _pad_cols(t: torch.Tensor, n: int) -> torch.Tensor:
+    if t.shape[1] == n:
+        return t
+    out = torch.zeros(t.shape[0], _r8(n), dtype=t.dtype, device=t.device)[:, :n]
+    out[:, :t.shape[1]] = t
+    return out
+
+
+def cross(x0: torch.Tensor, xl: torch.Tensor, weight: torch.Tensor,
+          bias: Optional[torch.Tensor]) -> torch.Tensor:
+    """DCN-v2 cross layer x_{l+1} = x0 * (W x_l + b) + x_l."""
+    d = weight.shape[1]
+    if not xl.is_cuda:
+        x0c = x0[:, :d].float()
+        xlc = xl[:, :d].float()
+        return x0c * F.linear(xlc, weight.float(), None if bias is None else bias.float()) + xlc
+    return _CrossFn.apply(x0, xl, weight, bias)
+
+
+def din_attention(q: torch.Tensor, k: torch.Tensor, valid: torch.Tensor, att_mlp,
+                  att_out: torch.nn.Linear):
+    """DIN target attention: s_j = att_out(att_mlp([q, k_j, q-k_j, q*k_j]));
+    a = softmax over valid j (invalid -> -inf, SASRec.py:26-29); u = sum_j a_j k_j.
+    q [B, E], k [B, L, E], valid [B, L] bool -> u [B, E] (fp32)."""
+    B, L, E = k.shape
+    qb = q.unsqueeze(1).expand(B, L, E).to(k.dtype)
+    feat = torch.cat([qb, k, qb - k, qb * k], dim=-1).reshape(B * L, 4 * E)
+    h = att_mlp(feat)
+    s = linear(h, att_out.weight, att_out.bias, out_dtype=torch.float32).float().reshape(B, L)
+    s = s.masked_fill(~valid, float("-inf"))
+    a = torch.softmax(s, dim=-1)
+    return (a.unsqueeze(-1) * k.float()).sum(1)

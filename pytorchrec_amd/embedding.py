@@ -84,6 +84,7 @@ class EmbeddingBank(torch.nn.Module):
         self.check_ids = True  # raise IndexError on out-of-range ids (syncs once per call)
         self._seed = 0x5eed
         self._desc = None
+        self._step = None  # device uint64 counter (SR bits stay fresh under graph replay)
 
     @property
     def n_tables(self) -> int:
@@ -106,6 +107,11 @@ class EmbeddingBank(torch.nn.Module):
         if self.sgd_lr is None:
             raise RuntimeError("fused SGD update without a learning rate")
         return self.sgd_lr
+
+    def step_counter(self) -> torch.Tensor:
+        if self._step is None or self._step.device != self.weight.device:
+            self._step = torch.zeros(1, dtype=torch.int64, device=self.weight.device)
+        return self._step
 
     def next_seed(self) -> int:
         self._seed = (self._seed * 6364136223846793005 + 1442695040888963407) & (2 ** 64 - 1)
@@ -160,7 +166,7 @@ def _plan(bank: EmbeddingBank, ids, start: int, count: int, flag):
     ws = torch.empty(ws_bytes, dtype=torch.uint8, device=bank.weight.device)
     idd = _ids_desc(ids, start, count) if (start or count != ids[0].shape[0]) else _ids_desc(ids)
     _mrec.call("mrec_emb_bwd_plan", bank.desc().ref(), idd.ref(), count, ws.data_ptr(), ws_bytes,
-               _mrec.ptr(flag), _mrec.stream_handle())
+               _mrec.ptr(flag), bank.step_counter().data_ptr(), _mrec.stream_handle())
     return ws, ws_bytes
 
 
@@ -180,7 +186,8 @@ def _apply(bank: EmbeddingBank, ws, ws_bytes, count, dx=None, dfm=None, fm_sum=N
                _mrec.ptr(dx), dx_dt, dx.stride(0) if dx is not None else 0,
                _mrec.ptr(dfm), _mrec.ptr(fm_sum), _mrec.ptr(x0), x0_dt,
                x0.stride(0) if x0 is not None else 0, _mrec.ptr(dw), mode, float(lr),
-               bank.next_seed(), _mrec.ptr(grad), _mrec.stream_handle())
+               bank.next_seed(), bank.step_counter().data_ptr(), _mrec.ptr(grad),
+               _mrec.stream_handle())
 
 
 def _chunks(batch: int):
@@ -365,8 +372,6 @@ def interact(bank: EmbeddingBank, ids: Sequence[torch.Tensor], dense: Optional[t
         raise ValueError("first_order needs a bank built with_first_order=True")
     if dense is not None:
         dense = dense.contiguous().float()
-        if dense_w is None:
-            raise ValueError("dense features need dense_w")
     if not bank.weight.is_cuda:
         return cpu_path.interact(bank, ids, dense, dense_w, bias, fm2, first_order, x0_cols,
                                  x0_dtype)

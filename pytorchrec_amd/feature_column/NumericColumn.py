@@ -1,0 +1,46 @@
+"""Numeric column (torchrec/feature_column/NumericColumn.py:14-53)."""
+from typing import Any, Dict
+
+from torch import Tensor
+
+from pytorchrec_amd.feature_column.DenseColumn import DenseColumn
+from pytorchrec_amd.feature_column.NormalizationMode import NormalizationMode
+
+
+class NumericColumn(DenseColumn):
+    """A float feature with optional max-min or z-score normalisation."""
+
+    def __init__(self, feature_name: str, min_value: float = 0.0, max_value: float = 1.0,
+                 mean_value: float = 0.0, std_value: float = 1.0):
+        super().__init__()
+        self.feature_name = feature_name
+        self.min_value = min_value
+        self.max_value = max_value
+        self.mean_value = mean_value
+        self.std_value = std_value
+
+    def get_feature_data(self, batch: Dict[str, Any],
+                         normalization_mode: NormalizationMode = NormalizationMode.NOP) -> Tensor:
+        x = batch[self.feature_name].float()
+        if normalization_mode == NormalizationMode.NOP:
+            return x
+        if normalization_mode == NormalizationMode.MAX_MIN:
+            return (x - self.min_value) / (self.max_value - self.min_value)
+        if normalization_mode == NormalizationMode.Z_SCORE:
+            return (x - self.mean_value) / self.std_value
+        raise Exception("NormalizationMode is wrong!")
+
+    @staticmethod
+    def from_series(feature_name: str, series):
+        from pandas.api import types
+        assert types.is_numeric_dtype(series), series.dtypes
+        return NumericColumn(feature_name=feature_name, min_value=series.min(),
+                             max_value=series.max(), mean_value=series.mean(),
+                             std_value=series.std())
+
+    def __str__(self):
+        s = (f"name: {self.feature_name}, min: {self.min_value}, max: {self.max_value}, "
+             f"mean: {self.mean_value}, std: {self.std_value}")
+        for key, value in self.get_info().items():
+            s += f", {key}: {value}"
+        return s

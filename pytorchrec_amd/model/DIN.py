@@ -1,0 +1,99 @@
+"""DIN — Deep Interest Network with target-attention pooling (config C4).
+
+Absent from the reference; built from its idioms:
+  * padded history ``pos_his`` [B, L] with 0 = PAD, tail-padded
+    (interaction_history_list.py:17-29); validity = his_id > 0 with position 0
+    forced valid (``get_valid_his_index``, torchrec/model/utils.py:5-10);
+  * masked softmax with -inf on invalid keys (SASRec.py:26-29) — this build uses
+    the softmax variant of DIN (the official-code form) and documents it;
+  * item and category tables shared between the target and the history;
+  * attention unit = reference ``MLP`` over [q, k, q-k, q*k] + ``Linear(h, 1)``;
+    top = ``MLP`` over [q, u] + ``Linear(last, 1)``.
+"""
+from __future__ import annotations
+
+from typing import Any, Dict, List, Optional
+
+import torch
+from torch import Tensor
+from torch.nn import Linear
+
+from pytorchrec_amd import dense as dense_ops
+from pytorchrec_amd.embedding import EmbeddingBank, gather
+from pytorchrec_amd.feature_column import CategoricalColumn
+from pytorchrec_amd.model.DeepFM import _parse_layers
+from pytorchrec_amd.model.IModel import IModel
+from pytorchrec_amd.model.layer.MLP import MLP
+from pytorchrec_amd.utils.argument import ArgumentDescription
+
+
+class DIN(IModel):
+    @classmethod
+    def get_argument_descriptions(cls) -> List[ArgumentDescription]:
+        return [
+            ArgumentDescription(name="emb_size", type_=int, help_info="embedding dim",
+                                default_value=16, lower_closed_bound=1),
+            ArgumentDescription(name="att_layers", type_=str, help_info="attention MLP widths",
+                                default_value="80,40"),
+            ArgumentDescription(name="layers", type_=str, help_info="top MLP widths",
+                                default_value="200,80"),
+        ]
+
+    @classmethod
+    def check_argument_values(cls, arguments: Dict[str, Any]) -> None:
+        super().check_argument_values(arguments)
+
+    def __init__(self, iid_column: CategoricalColumn, cid_column: CategoricalColumn,
+                 his_column: CategoricalColumn, his_cate_column: CategoricalColumn,
+                 label_column=None, emb_size: int = 16, att_layers=(80, 40), layers=(200, 80),
+                 dropout: float = 0.0, emb_dtype: torch.dtype = torch.float32, device=None,
+                 **kwargs):
+        self.iid_column = iid_column
+        self.cid_column = cid_column
+        self.his_column = his_column
+        self.his_cate_column = his_cate_column
+        self.label_column = label_column
+        self.emb_size = int(emb_size)
+        self.att_layers = _parse_layers(att_layers)
+        self.layers = _parse_layers(layers)
+        self.dropout = float(dropout)
+        self.emb_dtype = emb_dtype
+        self.build_device = torch.device(device) if device is not None else None
+        super().__init__(**kwargs)
+
+    def _init_weights(self):
+        dev = self.build_device
+        D = self.emb_size
+        self.embeddings = EmbeddingBank([self.iid_column.category_num,
+                                         self.cid_column.category_num], D,
+                                        with_first_order=False, dtype=self.emb_dtype, device=dev)
+        E = 2 * D
+        self.att_mlp = MLP(4 * E, self.att_layers, "relu", 0.0)
+        self.att_out = Linear(self.att_layers[-1], 1)
+        self.mlp = MLP(2 * E, self.layers, "relu", self.dropout)
+        self.prediction = Linear(self.layers[-1], 1)
+        if dev is not None:
+            for m in (self.att_mlp, self.att_out, self.mlp, self.prediction):
+                m.to(dev)
+
+    def forward(self, data: Dict[str, Tensor]):
+        bank = self.embeddings
+        on_gpu = bank.weight.is_cuda
+        act_dtype = torch.bfloat16 if on_gpu else torch.float32
+        q = gather(bank, [self.iid_column.get_feature_ids(data),
+                          self.cid_column.get_feature_ids(data)], out_dtype=act_dtype)
+        his = self.his_column.get_feature_ids(data)
+        hcat = self.his_cate_column.get_feature_ids(data)
+        B, L = his.shape
+        k = gather(bank, [his.reshape(-1), hcat.reshape(-1)], out_dtype=act_dtype)
+        k = k.reshape(B, L, -1)
+        valid = his > 0
+        valid[:, 0] = True
+        u = dense_ops.din_attention(q, k, valid, self.att_mlp, self.att_out)
+        h = self.mlp(torch.cat([q.float(), u], dim=-1).to(act_dtype))
+        logit = dense_ops.linear(h, self.prediction.weight, self.prediction.bias,
+                                 out_dtype=torch.float32)
+        target = None
+        if self.label_column is not None and self.label_column.feature_name in data:
+            target = data[self.label_column.feature_name].float()
+        return logit.reshape(-1).float(), target

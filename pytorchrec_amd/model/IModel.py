@@ -1,0 +1,214 @@
+"""Model runtime base — mirror of ``torchrec.model.IModel``
+(torchrec/model/IModel.py:34-321), the caller of the hot path.
+
+Kept from the reference, same names / argument meaning / errors:
+  * ``__init__(random_seed)``: seed -> ``_init_weights()`` -> ``_reset_weights()``
+    (normal(0, 0.01) for every module whose type name contains "Linear" or
+    "Embedding"; IModel.py:37-68) — so subclasses store their columns and
+    hyper-parameters BEFORE calling ``super().__init__``;
+  * ``get_parameters`` (bias params get weight_decay 0, IModel.py:83-92);
+  * ``compile`` type checks raising ``ValueError`` (IModel.py:94-114);
+  * ``train_step`` = to_device -> forward -> loss -> zero_grad -> backward -> step
+    (IModel.py:116-125);
+  * ``fit`` / ``evaluate`` / ``predict`` loops, ``save_weights`` / ``load_weights``,
+    ``save_best_weights`` / ``load_best_weights``; ``RuntimeError`` before compile.
+
+MI355X additions (documented deviations):
+  * ``compile`` fuses the embedding update into the backward when the optimizer
+    is plain SGD (no momentum / weight decay / nesterov on the bank's group):
+    identical arithmetic to dense SGD, but no full-table gradient exists
+    (SURVEY.md §7 hard part 5).  Any other optimizer gets the dense gradient.
+  * ``predict`` calls ``predict_step`` (the reference calls a missing
+    ``evaluate_step`` at IModel.py:300 and cannot run).
+  * metrics may be any callables ``metric(prediction, target) -> float`` with a
+    ``name``; the reference's ranking metrics are out of scope.
+"""
+from __future__ import annotations
+
+import copy
+import pickle
+from abc import ABC, abstractmethod
+from typing import Dict, List, Optional
+
+import numpy as np
+import torch
+from torch.nn import Module
+from torch.nn.modules.loss import _Loss  # noqa
+from torch.optim.optimizer import Optimizer
+
+from pytorchrec_amd.utils.argument import IWithArguments
+from pytorchrec_amd.utils.data_structure import tensor_to_device
+from pytorchrec_amd.utils.global_utils import set_torch_seed
+
+
+class IModel(Module, IWithArguments, ABC):
+    """Model interface: ``forward(data: Dict[str, Tensor]) -> (prediction, target)``."""
+
+    def __init__(self, random_seed: int = 2020, **kwargs):  # noqa
+        set_torch_seed(random_seed)
+        super().__init__()
+        self.stop_training = False
+        self.best_state_dict = None
+        self.history: Optional[list] = None
+        self._is_compiled = False
+        self.compiled_optimizers: Optional[Optimizer] = None
+        self.compiled_loss: Optional[_Loss] = None
+        self.compiled_metrics: Optional[list] = None
+        self.compiled_device: Optional[torch.device] = None
+        self._init_weights()
+        self._reset_weights()
+
+    @abstractmethod
+    def _init_weights(self):
+        pass
+
+    @staticmethod
+    def _reset_weights_fn(m):
+        if "Linear" in str(type(m)):
+            torch.nn.init.normal_(m.weight, mean=0.0, std=0.01)
+            if m.bias is not None:
+                torch.nn.init.normal_(m.bias, mean=0.0, std=0.01)
+        elif "Embedding" in str(type(m)):
+            with torch.no_grad():
+                torch.nn.init.normal_(m.weight, mean=0.0, std=0.01)
+
+    def _reset_weights(self):
+        self.apply(self._reset_weights_fn)
+
+    # -- checkpoints (IModel.py:73-81, 314-321) --------------------------------
+    def load_weights(self, filepath: str, device: torch.device):
+        state_dict = torch.load(filepath, map_location=device, weights_only=True)
+        self.load_state_dict(state_dict)
+        self.to(device)
+
+    def save_weights(self, filepath: str):
+        torch.save(self.state_dict(), filepath, pickle_protocol=pickle.HIGHEST_PROTOCOL)
+
+    def save_best_weights(self):
+        self.best_state_dict = copy.deepcopy(tensor_to_device(self.state_dict(), torch.device("cpu")))
+
+    def load_best_weights(self):
+        assert self.best_state_dict is not None
+        self.load_state_dict(self.best_state_dict)
+        self.to(self.compiled_device)
+
+    def get_parameters(self):
+        weight_p, bias_p = [], []
+        for name, p in filter(lambda x: x[1].requires_grad, self.named_parameters()):
+            (bias_p if "bias" in name else weight_p).append(p)
+        return [{"params": weight_p}, {"params": bias_p, "weight_decay": 0.0}]
+
+    # -- compile ----------------------------------------------------------------
+    def compile(self, optimizer: Optimizer, loss: _Loss, metrics: List, device: torch.device):
+        if not isinstance(optimizer, Optimizer):
+            raise ValueError(f"optimizer参数不合法: {optimizer}")
+        if not isinstance(loss, _Loss):
+            raise ValueError(f"loss参数不合法: {loss}")
+        if not isinstance(metrics, list) or not all(callable(m) for m in metrics):
+            raise ValueError(f"metrics参数不合法: {metrics}")
+        if not isinstance(device, torch.device):
+            raise ValueError(f"device参数不合法: {device}")
+        self.compiled_optimizers = optimizer
+        self.compiled_loss = loss
+        self.compiled_metrics = metrics
+        self.compiled_device = device
+        self.to(device)
+        self._configure_embedding_update(optimizer)
+        self._is_compiled = True
+
+    def embedding_banks(self):
+        from pytorchrec_amd.embedding import EmbeddingBank
+        return [m for m in self.modules() if isinstance(m, EmbeddingBank)]
+
+    def _configure_embedding_update(self, optimizer: Optimizer):
+        """Fuse the table update into the backward when that is exactly dense SGD."""
+        for bank in self.embedding_banks():
+            group = None
+            for g in optimizer.param_groups:
+                if any(p is bank.weight for p in g["params"]):
+                    group = g
+            plain_sgd = (isinstance(optimizer, torch.optim.SGD) and group is not None
+                         and group.get("momentum", 0) == 0 and group.get("weight_decay", 0) == 0
+                         and not group.get("nesterov", False) and not group.get("maximize", False))
+            if plain_sgd:
+                bank.use_fused_sgd(group["lr"], group)
+            elif group is not None or bank.update != "sgd":
+                bank.use_dense_grad()
+
+    # -- steps ------------------------------------------------------------------
+    def train_step(self, data: Dict):
+        self.train()
+        data = tensor_to_device(data, self.compiled_device)
+        prediction, target = self(data)
+        loss = self.compiled_loss(prediction, target)
+        self.compiled_optimizers.zero_grad()
+        loss.backward()
+        self.compiled_optimizers.step(closure=None)
+        return {"loss": loss}
+
+    def test_step(self, data):
+        self.eval()
+        data = tensor_to_device(data, self.compiled_device)
+        prediction, target = self(data)
+        return prediction, target
+
+    def predict_step(self, data):
+        self.eval()
+        data = tensor_to_device(data, self.compiled_device)
+        prediction, _ = self(data)
+        return prediction
+
+    def _loader(self, dataset, batch_size, shuffle=False, workers=0, drop_last=False):
+        from torch.utils.data import DataLoader
+        return DataLoader(dataset=dataset, batch_size=batch_size, shuffle=shuffle,
+                          num_workers=workers, drop_last=drop_last)
+
+    def fit(self, dataset, batch_size: int, epochs: int, dev_dataset=None, train_mode=None,
+            verbose: int = 1, callbacks=None, shuffle: bool = True, workers: int = 0,
+            drop_last: bool = False, dev_batch_size: Optional[int] = None, dev_freq: int = 1):
+        """Epoch loop of IModel.py:127-209 without the (out-of-scope) callback
+        framework: per-epoch logs are appended to ``self.history``."""
+        self._assert_compile_was_called()
+        self.stop_training = False
+        self.history = []
+        for epoch in range(epochs):
+            if hasattr(dataset, "train_neg_sample") and train_mode is not None and \
+                    str(getattr(train_mode, "value", train_mode)) == "pair_wise":
+                dataset.train_neg_sample()
+            logs = {}
+            for data in self._loader(dataset, batch_size, shuffle, workers, drop_last):
+                logs = self.train_step(data)
+            epoch_logs = {k: float(v) for k, v in logs.items()}
+            if dev_dataset is not None and (epoch + 1) % dev_freq == 0:
+                epoch_logs.update(self.evaluate(dev_dataset, dev_batch_size or batch_size,
+                                                verbose=verbose, workers=workers))
+            self.history.append(epoch_logs)
+            if verbose:
+                print(f"epoch {epoch + 1}/{epochs}: " +
+                      ", ".join(f"{k}={v:.5f}" for k, v in epoch_logs.items()))
+            if self.stop_training:
+                break
+        return self.history
+
+    @torch.no_grad()
+    def evaluate(self, dataset, batch_size: int, verbose: int = 1, callbacks=None, workers: int = 0):
+        self._assert_compile_was_called()
+        preds, targets = [], []
+        for data in self._loader(dataset, batch_size, workers=workers):
+            p, t = self.test_step(data)
+            preds.append(p.detach().float().cpu().numpy())
+            targets.append(t.detach().float().cpu().numpy())
+        predictions = np.concatenate(preds) if preds else np.zeros(0)
+        target = np.concatenate(targets) if targets else np.zeros(0)
+        return {getattr(m, "name", type(m).__name__): float(m(predictions, target))
+                for m in self.compiled_metrics}
+
+    @torch.no_grad()
+    def predict(self, dataset, batch_size: int, verbose: int = 0, callbacks=None, workers: int = 0):
+        preds = [self.predict_step(d).detach().float().cpu().numpy()
+                 for d in self._loader(dataset, batch_size, workers=workers)]
+        return np.concatenate(preds) if preds else np.zeros(0)
+
+    def _assert_compile_was_called(self):
+        if not self._is_compiled:
+            raise RuntimeError("训练/测试前必须编译模型")

@@ -1,0 +1,191 @@
+"""GPU numerics of the MFMA GEMM (libmrec mrec_gemm) and the dense-tower layers
+built on it, against plain torch fp64/fp32 references of the same op on the same
+bf16-rounded operands.
+
+Tolerance: operands are bf16, accumulation fp32 (error ~1e-6 * sum|a*b|), the
+output is rounded once to bf16 (<= 1 ulp = 2^-8 relative) — so the check is
+|got - ref| <= 2^-8 * |ref| + 1e-5 * sum_k |a_k b_k| (+1e-30).
+"""
+import numpy as np
+import pytest
+import torch
+
+from conftest import golden
+from oracle import ref
+
+pytestmark = pytest.mark.gpu
+
+
+def _bf(x):
+    return x.to(torch.bfloat16).to(torch.float64)
+
+
+def _close(got, want, mag, out_bf16=True):
+    got = got.double().cpu()
+    want = want.double().cpu()
+    mag = mag.double().cpu()
+    tol = (2.0 ** -8 if out_bf16 else 1e-6) * want.abs() + 1e-5 * mag + 1e-30
+    bad = (got - want).abs() > tol
+    return (~bad).all().item(), ((got - want).abs() / tol).max().item()
+
+
+@pytest.mark.parametrize("shape", [(300, 77, 93), (4096, 400, 429), (64, 1, 400), (1, 5, 7)])
+def test_gemm_forward_bias_relu(gpu, shape):
+    from pytorchrec_amd import dense as D, _mrec
+    M, N, K = shape
+    g = torch.Generator().manual_seed(M + N + K)
+    x = torch.randn(M, K, generator=g).to(gpu).to(torch.bfloat16)
+    W = (torch.randn(N, K, generator=g) * 0.1).to(gpu)
+    b = (torch.randn(N, generator=g) * 0.1).to(gpu)
+    xp = torch.zeros(M, D._r8(K), dtype=torch.bfloat16, device=gpu)[:, :K]
+    xp.copy_(x)
+    y = D.gemm(xp, _mrec.LAYOUT_ROW, W, _mrec.LAYOUT_ROW, M, N, K, bias=b, act=_mrec.ACT_RELU)
+    want = torch.relu(_bf(x) @ _bf(W).T + b.double())
+    mag = _bf(x).abs() @ _bf(W).abs().T + b.double().abs()
+    ok, worst = _close(y, want, mag)
+    assert ok, worst
+
+
+@pytest.mark.parametrize("split_k", [1, 4, 8])
+def test_gemm_weight_grad_col_col_ones_column(gpu, split_k):
+    """dW = dZ^T x and db = sum_m dZ via the ones column; dZ = dy * (y > 0)."""
+    from pytorchrec_amd import dense as D, _mrec
+    M, N, K = 1000, 70, 45
+    g = torch.Generator().manual_seed(5)
+    dy = torch.randn(M, N, generator=g).to(torch.bfloat16).to(gpu)
+    y = torch.randn(M, N, generator=g).to(torch.bfloat16).to(gpu)
+    x = torch.randn(M, K, generator=g).to(torch.bfloat16).to(gpu)
+    out = D.gemm(dy, _mrec.LAYOUT_COL, x, _mrec.LAYOUT_COL, N, K, M, a_mod=y,
+                 a_mod_kind=_mrec.AMOD_RELU_MASK, ones_col=True, out_dtype=torch.float32,
+                 split_k=split_k)
+    dz = _bf(dy) * (y.double() > 0)
+    want_w = dz.T @ _bf(x)
+    want_b = dz.sum(0)
+    ok, worst = _close(out[:, :K], want_w, dz.abs().T @ _bf(x).abs(), out_bf16=False)
+    assert ok, worst
+    ok, worst = _close(out[:, K], want_b, dz.abs().sum(0), out_bf16=False)
+    assert ok, worst
+
+
+def test_gemm_input_grad_row_col_with_zero_pad(gpu):
+    """dx = dZ W with W fp32 [N, K] read as a COL operand; columns >= K of the
+    padded output are exactly zero."""
+    from pytorchrec_amd import dense as D, _mrec
+    M, N, K, KX = 513, 400, 429, 432
+    g = torch.Generator().manual_seed(9)
+    dy = torch.randn(M, N, generator=g).to(torch.bfloat16).to(gpu)
+    y = torch.randn(M, N, generator=g).to(torch.bfloat16).to(gpu)
+    W = (torch.randn(N, K, generator=g) * 0.05).to(gpu)
+    dx = D.gemm(dy, _mrec.LAYOUT_ROW, W, _mrec.LAYOUT_COL, M, KX, N, a_mod=y,
+                a_mod_kind=_mrec.AMOD_RELU_MASK, b_cols=K)
+    dz = _bf(dy) * (y.double() > 0)
+    want = dz @ _bf(W)
+    ok, worst = _close(dx[:, :K], want, dz.abs() @ _bf(W).abs())
+    assert ok, worst
+    assert torch.all(dx[:, K:] == 0)
+
+
+def test_mlp_matches_reference_golden_g6(gpu):
+    """Reference MLP (golden G6 from torchrec.model.layer.MLP) through our MLP on
+    the GPU: forward and all gradients, bf16 tolerance."""
+    from pytorchrec_amd.model.layer import MLP
+    gd = golden("g6_mlp.npz")
+    n = int(gd["n_layers"])
+    units = [gd["W0"].shape[1]] + [gd[f"W{i}"].shape[0] for i in range(n)]
+    mlp = MLP(units[0], units[1:], "relu", 0.0).to(gpu)
+    lins = [m for m in mlp.modules() if isinstance(m, torch.nn.Linear)]
+    with torch.no_grad():
+        for i, m in enumerate(lins):
+            m.weight.copy_(torch.from_numpy(gd[f"W{i}"]))
+            m.bias.copy_(torch.from_numpy(gd[f"b{i}"]))
+    x = torch.from_numpy(gd["x"]).to(gpu).requires_grad_()
+    y = mlp(x)
+    y.backward(torch.from_numpy(gd["dout"]).to(gpu).to(y.dtype))
+    # bf16 activations: compare against the golden fp32 values with bf16-level tolerance
+    for got, want in [(y.float(), gd["y"]), (x.grad.float(), gd["dx"])] + \
+            [(m.weight.grad, gd[f"dW{i}"]) for i, m in enumerate(lins)] + \
+            [(m.bias.grad, gd[f"db{i}"]) for i, m in enumerate(lins)]:
+        g_ = got.detach().cpu().numpy()
+        np.testing.assert_allclose(g_, want, rtol=3e-2, atol=3e-2 * np.abs(want).max())
+
+
+def test_dcn_cross_forward_backward(gpu):
+    from pytorchrec_amd import dense as D
+    rng = np.random.default_rng(21)
+    M, d = 256, 45
+    x0 = torch.from_numpy(rng.standard_normal((M, d)).astype(np.float32)).to(torch.bfloat16)
+    W = [torch.from_numpy((rng.standard_normal((d, d)) * 0.1).astype(np.float32)) for _ in range(3)]
+    b = [torch.from_numpy((rng.standard_normal(d) * 0.1).astype(np.float32)) for _ in range(3)]
+    Wg = [w.to(gpu).requires_grad_() for w in W]
+    bg = [v.to(gpu).requires_grad_() for v in b]
+    x0g = x0.to(gpu).requires_grad_()
+    x = x0g
+    for i in range(3):
+        x = D.cross(x0g, x, Wg[i], bg[i])
+    dout = rng.standard_normal((M, d)).astype(np.float32)
+    x.backward(torch.from_numpy(dout).to(gpu).to(x.dtype))
+    layers = [(w.numpy(), v.numpy()) for w, v in zip(W, b)]
+    x0n = x0.float().numpy()
+    xs, zs = ref.dcn_cross_fwd(x0n, layers)
+    dx0, grads = ref.dcn_cross_bwd(xs, zs, layers, ref.bf16_round(dout))
+    np.testing.assert_allclose(x.detach().float().cpu().numpy(), xs[-1], rtol=0.05,
+                               atol=0.05 * np.abs(xs[-1]).max())
+    np.testing.assert_allclose(x0g.grad.float().cpu().numpy(), dx0, rtol=0.05,
+                               atol=0.05 * np.abs(dx0).max())
+    for i in range(3):
+        np.testing.assert_allclose(Wg[i].grad.cpu().numpy(), grads[i][0], rtol=0.05,
+                                   atol=0.05 * np.abs(grads[i][0]).max())
+        np.testing.assert_allclose(bg[i].grad.cpu().numpy(), grads[i][1], rtol=0.05,
+                                   atol=0.05 * np.abs(grads[i][1]).max())
+
+
+def test_deepfm_train_step_matches_oracle_model(gpu):
+    """One DeepFM train step on the GPU (fp32 tables, bf16 MLP) vs the oracle's
+    reference-path model (fp64) from identical weights: loss and updated tables."""
+    import torch.nn as nn
+    from oracle.models import RefDeepFM, criteo_batch, sgd_train_step
+    from pytorchrec_amd.feature_column import CategoricalColumnWithIdentity, NumericColumn
+    from pytorchrec_amd.model import DeepFM
+    nums = [50, 80, 3, 200, 17, 64]
+    F, ND, B = len(nums), 5, 512
+    sparse = [CategoricalColumnWithIdentity(n, f"c{f}") for f, n in enumerate(nums)]
+    dense = [NumericColumn(f"d{j}") for j in range(ND)]
+    lab = CategoricalColumnWithIdentity(2, "label")
+    m = DeepFM(sparse, dense, lab, emb_size=16, layers=(64, 32), device=gpu, random_seed=3)
+    with torch.no_grad():  # larger init so the MLP contributes visibly
+        for p in m.mlp.parameters():
+            p.mul_(10)
+    r = RefDeepFM(nums, ND, 16, (64, 32), dtype=torch.float64)
+    with torch.no_grad():
+        for f in range(F):
+            r.emb[f].weight.copy_(m.embeddings.table(f).double().cpu())
+            r.w1[f].weight.copy_(m.embeddings.first_order(f).double().cpu()[:, None])
+        r.dense_w.weight.copy_(m.dense_weight.double().cpu()[None])
+        r.global_bias.copy_(m.global_bias.double().cpu())
+        ml = [x for x in m.mlp.modules() if isinstance(x, nn.Linear)] + [m.prediction]
+        rl = [x for x in r.mlp.modules() if isinstance(x, nn.Linear)] + [r.out]
+        for a, b_ in zip(ml, rl):
+            b_.weight.copy_(a.weight.double().cpu())
+            b_.bias.copy_(a.bias.double().cpu())
+    ids, dn, label = criteo_batch(nums, B, n_dense=ND, seed=4)
+    data = {c.feature_name: ids[:, f].to(gpu) for f, c in enumerate(sparse)}
+    data.update({c.feature_name: dn[:, j].to(gpu) for j, c in enumerate(dense)})
+    data["label"] = label.to(gpu)
+    lr = 0.5
+    before = [r.emb[f].weight.detach().clone() for f in range(F)]
+    before_w = [r.w1[f].weight.detach()[:, 0].clone() for f in range(F)]
+    m.compile(torch.optim.SGD(m.get_parameters(), lr=lr), torch.nn.BCEWithLogitsLoss(), [], gpu)
+    assert m.embeddings.update == "sgd"
+    loss = float(m.train_step(data)["loss"])
+    ropt = torch.optim.SGD(r.parameters(), lr=lr)
+    rloss = float(sgd_train_step(r, ropt, ids, dn.double(), label))
+    assert abs(loss - rloss) < 2e-3 * max(1.0, abs(rloss)), (loss, rloss)
+    # compare the UPDATES (after - before): bf16 MLP -> a few % relative
+    for f in range(F):
+        d_got = m.embeddings.table(f).detach().double().cpu() - before[f]
+        d_want = r.emb[f].weight.detach() - before[f]
+        scale = float(d_want.abs().max()) + 1e-12
+        assert float((d_got - d_want).abs().max()) <= 0.05 * scale, f
+        dw_got = m.embeddings.first_order(f).detach().double().cpu() - before_w[f]
+        dw_want = r.w1[f].weight.detach()[:, 0] - before_w[f]
+        assert float((dw_got - dw_want).abs().max()) <= 0.02 * (float(dw_want.abs().max()) + 1e-12)

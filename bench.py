@@ -105,16 +105,26 @@ def batch_views(buf, args, sparse, dense_cols, label_col):
 # per-kernel roofline (HIP events on the launch stream, eager back-to-back launches)
 # ----------------------------------------------------------------------------
 
-def time_launches(fn, reps=50):
-    s = torch.cuda.current_stream()
-    fn()
-    e0 = torch.cuda.Event(enable_timing=True)
-    e1 = torch.cuda.Event(enable_timing=True)
-    e0.record(s)
-    for _ in range(reps):
+def time_launches(fn, reps=100):
+    """Average device time of one launch of ``fn``: ``reps`` back-to-back launches
+    captured in a HIP graph (no host launch overhead), bracketed by HIP events on
+    the stream the kernels run on."""
+    s = torch.cuda.Stream()
+    s.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(s):
         fn()
-    e1.record(s)
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g, stream=s):
+            for _ in range(reps):
+                fn()
+        g.replay()
+        e0 = torch.cuda.Event(enable_timing=True)
+        e1 = torch.cuda.Event(enable_timing=True)
+        e0.record(s)
+        g.replay()
+        e1.record(s)
     e1.synchronize()
+    torch.cuda.current_stream().wait_stream(s)
     return e0.elapsed_time(e1) / reps * 1e-3  # seconds per launch
 
 
@@ -138,6 +148,7 @@ def kernel_rooflines(model, data, args):
         out["mrec_interact_fwd"] = (t, fwd_bytes * B)
 
         ws, wsb = E._plan(bank, ids, 0, B, None)
+        torch.cuda.synchronize()
 
         def plan():
             E._plan(bank, ids, 0, B, None)
@@ -213,8 +224,9 @@ def main():
     if args.model != "deepfm":
         raise SystemExit("only --model deepfm is wired into bench.py this round")
     model, sparse, dense_cols, label_col = build_deepfm(args, device)
-    model.compile(torch.optim.SGD(model.get_parameters(), lr=args.lr),
-                  torch.nn.BCEWithLogitsLoss(), [], device)
+    from pytorchrec_amd.loss import BCEWithLogitsLoss
+    model.compile(torch.optim.SGD(model.get_parameters(), lr=args.lr), BCEWithLogitsLoss(), [],
+                  device)
     for bank in model.embedding_banks():
         bank.check_ids = False  # no host sync inside the captured step
     assert model.embeddings.update == "sgd", "SGD must fuse into the embedding backward"

@@ -202,7 +202,8 @@ typedef struct {
 #define MREC_AMOD_MUL 2       /* A(m,k) *= mod(m,k):      DCN dz = g * x0  */
 
 /* v = acc + bias[n]; aux[m,n] = v; v = act(v); v *= mul[m,n]; v += add[m,n]; C = v.
- * Every pointer may be NULL (term skipped); mul/add/aux are bf16 [M, ld]. */
+ * Every pointer may be NULL (term skipped); mul/add/aux are bf16 [M, ld].  With
+ * b_ones_col the extra column (the row sums of A') goes to ones_out (fp32 [M]). */
 typedef struct {
   const float *bias;
   int32_t act;
@@ -212,20 +213,24 @@ typedef struct {
   int64_t ld_add;
   void *aux;
   int64_t ld_aux;
+  float *ones_out;
 } mrec_epilogue;
 
-size_t mrec_gemm_workspace_size(int64_t M, int64_t N, int32_t split_k);
+size_t mrec_gemm_workspace_size(int64_t M, int64_t N, int64_t K, int32_t split_k);
 
 /*
- * C[M, N'] = epi( sum_k A'(m, k) B(k, n) ),  A' = A modified by a_mod (bf16,
- * A's layout) as a_mod_kind says.  A bf16; B bf16 or fp32 (converted while
- * staging — the fp32 master weights are read directly); fp32 accumulation on
- * v_mfma_f32_16x16x32_bf16.  B(k, n) for layout ROW is ptr[n*ld + k] (nn.Linear's
- * [out, in] weight), for COL ptr[k*ld + n].  b_ones_col == N appends a column of
- * ones to B (N' = N + 1), so C[:, N] = sum_k A'(m, k): the bias gradient of a
+ * C[M, N] = epi( sum_k A'(m, k) B(k, n) ),  A' = A modified by a_mod (bf16,
+ * A's layout) as a_mod_kind says.  A and B bf16 (fp32 weights go through
+ * mrec_weight_prep), fp32 accumulation on v_mfma_f32_16x16x32_bf16.  Each
+ * workgroup stages a K slab of <= 448 into LDS in one phase (every load in
+ * flight at once); K is split over max(split_k, ceil(K/448)) workgroups.
+ * B(k, n) for layout ROW is ptr[n*ld + k] (nn.Linear's [out, in] weight), for
+ * COL ptr[k*ld + n].  b_ones_col == N appends a column of
+ * ones to B, so epi->ones_out[m] = sum_k A'(m, k): the bias gradient of a
  * weight-gradient GEMM.  B(k, n) = 0 for b_cols <= n < N (b_cols <= N), so the
- * gradient of a zero-padded input comes out zero-padded.  split_k > 1 reduces fp32
- * slabs in fixed order (deterministic) through `workspace`.
+ * gradient of a zero-padded input comes out zero-padded.  With more than one K
+ * slab the fp32 partials are reduced in fixed order (deterministic) through
+ * `workspace` (mrec_gemm_workspace_size bytes).
  * Replaces nn.Linear forward/backward = aten::addmm / mm and the ReLU
  * (Dense.py:20-24, MLP.py:22-23; SURVEY.md §2b MLP row).
  */
@@ -234,6 +239,51 @@ mrec_status mrec_gemm(int64_t M, int64_t N, int64_t K, const mrec_operand *A,
                       int64_t b_ones_col, int64_t b_cols, const mrec_epilogue *epi, void *C,
                       mrec_dtype c_dtype, int64_t ldc, int32_t split_k, void *workspace,
                       size_t ws_bytes, mrec_stream stream);
+
+/*
+ * fp32 [N, K] weight (row stride ldw) -> bf16 images for the GEMMs: `row`
+ * [N, ldr] (B operand of the forward) and/or `tr` = W^T [K, ldt] (B operand of the
+ * input-gradient GEMM); pad columns are zero.  One launch per weight per step
+ * keeps the fp32 master weights as the optimizer's parameters.
+ */
+mrec_status mrec_weight_prep(const float *W, int64_t N, int64_t K, int64_t ldw, void *row,
+                             int64_t ldr, void *tr, int64_t ldt, mrec_stream stream);
+
+/* ------------------------------------------------------------------------- */
+/* CTR head and loss                                                          */
+/* ------------------------------------------------------------------------- */
+
+/*
+ * z[b] = base[b] + bias[0] + h[b, :H] . w   (h bf16 rows, 16-B aligned; w fp32 [H];
+ * base/bias may be NULL).  The deep tower's Linear(H, 1) (NCF.py:51, 74) fused
+ * with the sum of the wide/FM logit.
+ */
+mrec_status mrec_head_fwd(const void *h, int64_t ldh, int64_t batch, int32_t H, const float *w,
+                          const float *bias, const float *base, float *z, mrec_stream stream);
+/* dh[b, :] = dz[b] * w  (bf16, pad columns up to ldh zeroed) */
+mrec_status mrec_head_bwd(const float *dz, const float *w, int64_t batch, int32_t H, void *dh,
+                          int64_t ldh, mrec_stream stream);
+
+/*
+ * torch.nn.BCEWithLogitsLoss (mean): *loss = mean(max(z,0) - z y + log1p(exp(-|z|)))
+ * (fixed-order reduction); backward dz = g[0] (sigmoid(z) - y) / B (g may be NULL = 1).
+ * The CTR loss the reference lacks (losses.py:8-12 has BPR/Top1/MSE only).
+ */
+mrec_status mrec_bce_fwd(const float *z, const float *y, int64_t batch, float *loss,
+                         mrec_stream stream);
+mrec_status mrec_bce_bwd(const float *z, const float *y, int64_t batch, const float *g, float *dz,
+                         mrec_stream stream);
+
+/*
+ * out[c] = sum_b s[b] X[b, c] for c < C, and *total = sum_b s[b] (if total != NULL):
+ * the gradients of a small Linear / bias fed by per-sample scalars (dense
+ * first-order weights, global bias, Linear(H, 1)).  Deterministic two-pass
+ * reduction through `workspace` (mrec_colsum_workspace_size(C) bytes).
+ */
+size_t mrec_colsum_workspace_size(int64_t C);
+mrec_status mrec_colsum(const float *s, const void *X, mrec_dtype x_dtype, int64_t ldx,
+                        int64_t batch, int64_t C, float *out, float *total, void *workspace,
+                        size_t ws_bytes, mrec_stream stream);
 
 #ifdef __cplusplus
 }

@@ -38,45 +38,62 @@ def _op(t: torch.Tensor, layout: int) -> _mrec.Operand:
 
 
 def _split_for(M: int, N: int, K: int) -> int:
-    """Split-K so that a small-output, long-K GEMM (weight gradients) fills the chip."""
+    """K slabs per output tile: at least ceil(K / 448) (the library enforces it),
+    more while a small-output long-K GEMM (weight gradients) leaves CUs idle."""
     tiles = ((M + 63) // 64) * ((N + 63) // 64)
-    s = 1
-    while tiles * s < 256 and K // (s * 2) >= 256 and s < 16:
-        s *= 2
+    s = max(1, -(-K // 448))
+    while tiles * s < 256 and K // (s + 1) >= 128 and s < 64:
+        s += 1
     return s
 
 
-def gemm(A, a_layout, B, b_layout, M, N, K, *, a_mod=None, a_mod_kind=0, ones_col=False,
+def gemm(A, a_layout, B, b_layout, M, N, K, *, a_mod=None, a_mod_kind=0, ones_out=None,
          b_cols=None, bias=None, act=0, mul=None, add=None, aux=None, out=None,
          out_dtype=_BF16, split_k=None):
-    """C[M, N(+1)] = epi(A'[M, K] @ B[K, N]) on libmrec (see include/mrec.h mrec_gemm)."""
+    """C[M, N] = epi(A'[M, K] @ B[K, N]) on libmrec (see include/mrec.h mrec_gemm).
+    ``ones_out`` (fp32 [M]) receives sum_k A'(m, k) through an appended ones column."""
     dev = A.device
-    ncols = N + 1 if ones_col else N
     if out is None:
-        out = _alloc(M, ncols, out_dtype, dev)
+        out = _alloc(M, N, out_dtype, dev)
     if split_k is None:
-        split_k = _split_for(M, ncols, K)
-    ws_bytes = _mrec.lib().mrec_gemm_workspace_size(M, N, split_k)
+        split_k = _split_for(M, N + (ones_out is not None), K)
+    ws_bytes = _mrec.lib().mrec_gemm_workspace_size(M, N, K, split_k)
     ws = torch.empty(ws_bytes, dtype=torch.uint8, device=dev) if ws_bytes else None
     epi = _mrec.Epilogue(_mrec.ptr(bias), act, _mrec.ptr(mul), mul.stride(0) if mul is not None else 0,
                          _mrec.ptr(add), add.stride(0) if add is not None else 0,
-                         _mrec.ptr(aux), aux.stride(0) if aux is not None else 0)
+                         _mrec.ptr(aux), aux.stride(0) if aux is not None else 0,
+                         _mrec.ptr(ones_out))
     a_op, b_op = _op(A, a_layout), _op(B, b_layout)
     m_op = _op(a_mod, a_layout) if a_mod is not None else None
     _mrec.call("mrec_gemm", M, N, K, ctypes.byref(a_op), ctypes.byref(b_op),
                ctypes.byref(m_op) if m_op is not None else None, a_mod_kind,
-               N if ones_col else -1, N if b_cols is None else b_cols, ctypes.byref(epi),
-               out.data_ptr(), _mrec.dtype_code(out.dtype), out.stride(0), split_k,
-               _mrec.ptr(ws), ws_bytes, _mrec.stream_handle())
+               N if ones_out is not None else -1, N if b_cols is None else b_cols,
+               ctypes.byref(epi), out.data_ptr(), _mrec.dtype_code(out.dtype), out.stride(0),
+               split_k, _mrec.ptr(ws), ws_bytes, _mrec.stream_handle())
     return out
 
 
+def weight_prep(W: torch.Tensor, row: bool = True, tr: bool = True):
+    """bf16 images of an fp32 [N, K] weight: row [N, r8(K)] and W^T [K, r8(N)]."""
+    W = _weight_f32(W)
+    N, K = W.shape
+    wr = torch.empty(N, _r8(K), dtype=_BF16, device=W.device) if row else None
+    wt = torch.empty(K, _r8(N), dtype=_BF16, device=W.device) if tr else None
+    _mrec.call("mrec_weight_prep", W.data_ptr(), N, K, W.stride(0), _mrec.ptr(wr),
+               wr.stride(0) if wr is not None else 0, _mrec.ptr(wt),
+               wt.stride(0) if wt is not None else 0, _mrec.stream_handle())
+    return wr, wt
+
+
 def _bf16_rows(t: torch.Tensor) -> torch.Tensor:
-    if t.dtype != _BF16:
-        t = t.to(_BF16)
-    if t.stride(-1) != 1:
-        t = t.contiguous()
-    return t
+    """bf16 [M, N] with 16-byte aligned rows (what mrec_gemm requires); copies into
+    an r8-padded buffer only when the input is not already laid out that way."""
+    if (t.dtype == _BF16 and t.stride(-1) == 1 and t.stride(0) % 8 == 0
+            and t.data_ptr() % 16 == 0):
+        return t
+    out = _alloc(t.shape[0], t.shape[1], _BF16, t.device)
+    out.copy_(t)
+    return out
 
 
 def _weight_f32(w: torch.Tensor) -> torch.Tensor:
@@ -94,33 +111,34 @@ class _LinearFn(torch.autograd.Function):
         x = _bf16_rows(x)
         M, K_x = x.shape
         N, K = weight.shape
-        W = _weight_f32(weight)
+        need_dx = ctx.needs_input_grad[0]
+        wr, wt = weight_prep(weight, row=True, tr=need_dx)
         b = bias.detach().float().contiguous() if bias is not None else None
-        y = gemm(x, _mrec.LAYOUT_ROW, W, _mrec.LAYOUT_ROW, M, N, K, bias=b,
+        y = gemm(x, _mrec.LAYOUT_ROW, wr[:, :K], _mrec.LAYOUT_ROW, M, N, K, bias=b,
                  act=_mrec.ACT_RELU if relu else _mrec.ACT_NONE, out_dtype=out_dtype)
-        ctx.save_for_backward(x, W, y if relu else None)
-        ctx.relu, ctx.has_bias, ctx.K_x = relu, bias is not None, K_x
+        ctx.save_for_backward(x, wt, y if relu else None)
+        ctx.relu, ctx.has_bias, ctx.NK = relu, bias is not None, (N, K)
         return y
 
     @staticmethod
     def backward(ctx, dy):
-        x, W, y = ctx.saved_tensors
+        x, wt, y = ctx.saved_tensors
         M, K_x = x.shape
-        N, K = W.shape
+        N, K = ctx.NK
         dy = _bf16_rows(dy)
         mod_kind = _mrec.AMOD_RELU_MASK if ctx.relu else _mrec.AMOD_NONE
         dx = dW = db = None
         if ctx.needs_input_grad[0]:
-            # dx[m, k] = sum_n dZ[m, n] W[n, k]; B(k'=n, col=k) = W[n*ld + k] -> COL
-            dx = gemm(dy, _mrec.LAYOUT_ROW, W, _mrec.LAYOUT_COL, M, K_x, N, a_mod=y,
+            # dx[m, k] = sum_n dZ[m, n] W[n, k]; B(k'=n, col=k) = W^T[k*ld + n] -> ROW
+            dx = gemm(dy, _mrec.LAYOUT_ROW, wt, _mrec.LAYOUT_ROW, M, K_x, N, a_mod=y,
                       a_mod_kind=mod_kind, b_cols=K, out_dtype=_BF16)
         if ctx.needs_input_grad[1] or ctx.needs_input_grad[2]:
             # dW[n, k] = sum_m dZ[m, n] x[m, k]: A(i=n, red=m) = dy[m*ld + n] -> COL,
             # B(red=m, col=k) = x[m*ld + k] -> COL; ones column -> db
-            g = gemm(dy, _mrec.LAYOUT_COL, x, _mrec.LAYOUT_COL, N, K, M, a_mod=y,
-                     a_mod_kind=mod_kind, ones_col=ctx.has_bias, out_dtype=torch.float32)
-            dW = g[:, :K]
-            db = g[:, K] if ctx.has_bias else None
+            dW = torch.empty(N, K, dtype=torch.float32, device=dy.device)
+            db = torch.empty(N, dtype=torch.float32, device=dy.device) if ctx.has_bias else None
+            gemm(dy, _mrec.LAYOUT_COL, x, _mrec.LAYOUT_COL, N, K, M, a_mod=y,
+                 a_mod_kind=mod_kind, ones_out=db, out=dW)
         return dx, dW, db, None, None
 
 
@@ -146,31 +164,32 @@ class _CrossFn(torch.autograd.Function):
         x0, xl = _bf16_rows(x0), _bf16_rows(xl)
         M = xl.shape[0]
         d = weight.shape[0]
-        W = _weight_f32(weight)
+        wr, wt = weight_prep(weight)
         b = bias.detach().float().contiguous() if bias is not None else None
         z = _alloc(M, d, _BF16, xl.device)
-        out = gemm(xl, _mrec.LAYOUT_ROW, W, _mrec.LAYOUT_ROW, M, d, d, bias=b, mul=x0, add=xl,
-                   aux=z)
-        ctx.save_for_backward(x0, xl, W, z)
+        out = gemm(xl, _mrec.LAYOUT_ROW, wr[:, :d], _mrec.LAYOUT_ROW, M, d, d, bias=b, mul=x0,
+                   add=xl, aux=z)
+        ctx.save_for_backward(x0, xl, wt, z)
         ctx.has_bias = bias is not None
-        ctx.shapes = (x0.shape, xl.shape)
         return out
 
     @staticmethod
     def backward(ctx, g):
-        x0, xl, W, z = ctx.saved_tensors
+        x0, xl, wt, z = ctx.saved_tensors
         g = _bf16_rows(g)
         M = g.shape[0]
-        d = W.shape[0]
+        d = z.shape[1]
         # dz = g * x0 (applied while staging A); dx_l = dz W + g; dW = dz^T x_l; db = sum dz
-        dxl = gemm(g, _mrec.LAYOUT_ROW, W, _mrec.LAYOUT_COL, M, xl.shape[1], d, a_mod=x0,
+        dxl = gemm(g, _mrec.LAYOUT_ROW, wt, _mrec.LAYOUT_ROW, M, xl.shape[1], d, a_mod=x0,
                    a_mod_kind=_mrec.AMOD_MUL, b_cols=d, add=_pad_cols(g, xl.shape[1]))
-        gw = gemm(g, _mrec.LAYOUT_COL, xl, _mrec.LAYOUT_COL, d, d, M, a_mod=x0,
-                  a_mod_kind=_mrec.AMOD_MUL, ones_col=ctx.has_bias, out_dtype=torch.float32)
+        dW = torch.empty(d, d, dtype=torch.float32, device=g.device)
+        db = torch.empty(d, dtype=torch.float32, device=g.device) if ctx.has_bias else None
+        gemm(g, _mrec.LAYOUT_COL, xl, _mrec.LAYOUT_COL, d, d, M, a_mod=x0,
+             a_mod_kind=_mrec.AMOD_MUL, ones_out=db, out=dW)
         dx0 = (g.float() * z.float()).to(_BF16)
         if x0.shape[1] > d:
             dx0 = F.pad(dx0, (0, x0.shape[1] - d))
-        return dx0, dxl, gw[:, :d], (gw[:, d] if ctx.has_bias else None)
+        return dx0, dxl, dW, db
 
 
 def _pad_cols(t: torch.Tensor, n: int) -> torch.Tensor:
@@ -205,3 +224,62 @@ def din_attention(q: torch.Tensor, k: torch.Tensor, valid: torch.Tensor, att_mlp
     s = s.masked_fill(~valid, float("-inf"))
     a = torch.softmax(s, dim=-1)
     return (a.unsqueeze(-1) * k.float()).sum(1)
+
+
+def colsum(s: torch.Tensor, X: Optional[torch.Tensor], want_total: bool = True):
+    """(sum_b s[b] X[b, :], sum_b s[b]) with libmrec's deterministic column sum."""
+    s = s.contiguous().float()
+    C = 0 if X is None else X.shape[1]
+    dev = s.device
+    out = torch.empty(C, dtype=torch.float32, device=dev)
+    tot = torch.empty(1, dtype=torch.float32, device=dev) if want_total else None
+    wsb = _mrec.lib().mrec_colsum_workspace_size(C)
+    ws = torch.empty(wsb, dtype=torch.uint8, device=dev)
+    if X is not None and X.stride(1) != 1:
+        X = X.contiguous()
+    _mrec.call("mrec_colsum", s.data_ptr(), _mrec.ptr(X),
+               _mrec.dtype_code(X.dtype) if X is not None else _mrec.F32,
+               X.stride(0) if X is not None else 0, s.shape[0], C, out.data_ptr(), _mrec.ptr(tot),
+               ws.data_ptr(), wsb, _mrec.stream_handle())
+    return out, tot
+
+
+class _HeadFn(torch.autograd.Function):
+    """z = base + h W^T + b for a Linear(H, 1) output layer (fp32 z [B])."""
+
+    @staticmethod
+    def forward(ctx, h, weight, bias, base):
+        h = _bf16_rows(h)
+        B, H = h.shape
+        w = _weight_f32(weight).reshape(-1)
+        b = bias.detach().float() if bias is not None else None
+        base_c = base.detach().float().contiguous() if base is not None else None
+        z = torch.empty(B, dtype=torch.float32, device=h.device)
+        _mrec.call("mrec_head_fwd", h.data_ptr(), h.stride(0), B, H, w.data_ptr(), _mrec.ptr(b),
+                   _mrec.ptr(base_c), z.data_ptr(), _mrec.stream_handle())
+        ctx.save_for_backward(h, w)
+        ctx.has_bias, ctx.has_base = bias is not None, base is not None
+        return z
+
+    @staticmethod
+    def backward(ctx, dz):
+        h, w = ctx.saved_tensors
+        B, H = h.shape
+        dz = dz.contiguous().float()
+        dh = None
+        if ctx.needs_input_grad[0]:
+            dh = _alloc(B, H, _BF16, dz.device)
+            _mrec.call("mrec_head_bwd", dz.data_ptr(), w.data_ptr(), B, H, dh.data_ptr(),
+                       dh.stride(0), _mrec.stream_handle())
+        dW, db = colsum(dz, h, want_total=ctx.has_bias)
+        return dh, dW.reshape(1, H), db, (dz if ctx.has_base else None)
+
+
+def head(h: torch.Tensor, weight: torch.Tensor, bias: Optional[torch.Tensor],
+         base: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """Logit of a Linear(H, 1) output layer plus an optional per-sample base logit
+    (the FM / wide part): z = base + h W^T + b, fp32 [B]."""
+    if not h.is_cuda:
+        z = F.linear(h.float(), weight.float(), None if bias is None else bias.float()).reshape(-1)
+        return z if base is None else z + base.float()
+    return _HeadFn.apply(h, weight, bias, base)

@@ -170,6 +170,39 @@ def _plan(bank: EmbeddingBank, ids, start: int, count: int, flag):
     return ws, ws_bytes
 
 
+_SIDE = {}
+
+
+def _side_stream(device) -> torch.cuda.Stream:
+    st = _SIDE.get(device)
+    if st is None:
+        st = torch.cuda.Stream(device=device)
+        _SIDE[device] = st
+    return st
+
+
+class _AsyncPlan:
+    """The sorted-segment plan launched on a side stream: it depends only on the
+    ids, so it runs concurrently with the interaction kernel and the MLP forward;
+    the backward waits on its event before the apply kernel."""
+
+    def __init__(self, bank: EmbeddingBank, ids, batch: int):
+        cur = torch.cuda.current_stream(bank.weight.device)
+        side = _side_stream(bank.weight.device)
+        side.wait_stream(cur)
+        with torch.cuda.stream(side):
+            self.ws, self.ws_bytes = _plan(bank, ids, 0, batch, None)
+            self.event = torch.cuda.Event()
+            self.event.record(side)
+        self.ws.record_stream(cur)
+        for t in ids:
+            t.record_stream(side)
+
+    def get(self):
+        torch.cuda.current_stream(self.ws.device).wait_event(self.event)
+        return self.ws, self.ws_bytes
+
+
 def _apply(bank: EmbeddingBank, ws, ws_bytes, count, dx=None, dfm=None, fm_sum=None, x0=None,
            dw=None, grad=None):
     """Run the fused backward for lookups [0, count) described by ``ws``; the
@@ -202,7 +235,7 @@ def _backward_into_bank(bank: EmbeddingBank, ids, batch, plan_ws, dx=None, dfm=N
     if bank.update == "dense":
         grad = torch.zeros_like(bank.weight)
     if plan_ws is not None:
-        ws, wsb = plan_ws
+        ws, wsb = plan_ws.get() if isinstance(plan_ws, _AsyncPlan) else plan_ws
         _apply(bank, ws, wsb, batch, dx, dfm, fm_sum, x0, dw, grad)
         return grad
     for s, c in _chunks(batch):
@@ -239,7 +272,7 @@ class _GatherFn(torch.autograd.Function):
                        _mrec.ptr(w_out), _mrec.ptr(flag), _mrec.stream_handle())
         plan_ws = None
         if _needs_backward(bank) and 0 < B <= _mrec.BWD_MAX_BATCH:
-            plan_ws = _plan(bank, ids, 0, B, None)
+            plan_ws = _AsyncPlan(bank, ids, B)
         _raise_if_oob(flag)
         ctx.bank, ctx.ids, ctx.B, ctx.plan_ws = bank, ids, B, plan_ws
         if want_w:
@@ -318,7 +351,7 @@ class _InteractFn(torch.autograd.Function):
                        _mrec.stream_handle())
         plan_ws = None
         if _needs_backward(bank) and 0 < B <= _mrec.BWD_MAX_BATCH:
-            plan_ws = _plan(bank, ids, 0, B, None)
+            plan_ws = _AsyncPlan(bank, ids, B)
         _raise_if_oob(flag)
         ctx.bank, ctx.ids, ctx.B, ctx.plan_ws = bank, ids, B, plan_ws
         ctx.fm2, ctx.first_order = fm2, first_order
@@ -348,11 +381,12 @@ class _InteractFn(torch.autograd.Function):
             grad = _backward_into_bank(bank, ctx.ids, ctx.B, ctx.plan_ws, dx=dx0, dfm=dfm,
                                        fm_sum=fm_sum, x0=x0 if dfm is not None else None, dw=dw)
         g_dense_w = g_bias = None
-        if dlogit is not None:
-            if ctx.has_dense_w and dense is not None:
-                g_dense_w = dense.t().float() @ dlogit
-            if ctx.has_bias:
-                g_bias = dlogit.sum().reshape(1)
+        if dlogit is not None and (ctx.has_dense_w or ctx.has_bias):
+            from pytorchrec_amd.dense import colsum
+            X = dense if (ctx.has_dense_w and dense is not None) else None
+            gw, gb = colsum(dlogit, X, want_total=ctx.has_bias)
+            g_dense_w = gw if X is not None else None
+            g_bias = gb
         return grad, g_dense_w, g_bias, None, None, None, None, None, None, None, None
 
 

@@ -75,6 +75,4 @@ class DCNv2(_CTRBase):
         for layer in self.cross:
             x = dense_ops.cross(x0, x, layer.weight, layer.bias)
         h = self.mlp(x)
-        logit = dense_ops.linear(h, self.prediction.weight, self.prediction.bias,
-                                 out_dtype=torch.float32)
-        return logit.reshape(-1).float(), self._target(data)
+        return dense_ops.head(h, self.prediction.weight, self.prediction.bias), self._target(data)

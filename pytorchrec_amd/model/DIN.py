@@ -91,8 +91,7 @@ class DIN(IModel):
         valid[:, 0] = True
         u = dense_ops.din_attention(q, k, valid, self.att_mlp, self.att_out)
         h = self.mlp(torch.cat([q.float(), u], dim=-1).to(act_dtype))
-        logit = dense_ops.linear(h, self.prediction.weight, self.prediction.bias,
-                                 out_dtype=torch.float32)
+        logit = dense_ops.head(h, self.prediction.weight, self.prediction.bias)
         target = None
         if self.label_column is not None and self.label_column.feature_name in data:
             target = data[self.label_column.feature_name].float()

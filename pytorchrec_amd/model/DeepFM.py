@@ -159,6 +159,5 @@ class DeepFM(_CTRBase):
                              self.dense_weight, self.global_bias, fm2=True, first_order=True,
                              x0_cols=self.x0_cols, x0_dtype=self._x0_dtype())
         h = self.mlp(x0)
-        deep = dense_ops.linear(h, self.prediction.weight, self.prediction.bias,
-                               out_dtype=torch.float32)
-        return logit + deep.reshape(-1).float(), self._target(data)
+        prediction = dense_ops.head(h, self.prediction.weight, self.prediction.bias, base=logit)
+        return prediction, self._target(data)

@@ -29,7 +29,8 @@ def _close(got, want, mag, out_bf16=True):
     return (~bad).all().item(), ((got - want).abs() / tol).max().item()
 
 
-@pytest.mark.parametrize("shape", [(300, 77, 93), (4096, 400, 429), (64, 1, 400), (1, 5, 7)])
+@pytest.mark.parametrize("shape", [(300, 77, 93), (4096, 400, 429), (64, 1, 400), (1, 5, 7),
+                                   (200, 96, 1000)])
 def test_gemm_forward_bias_relu(gpu, shape):
     from pytorchrec_amd import dense as D, _mrec
     M, N, K = shape
@@ -39,14 +40,16 @@ def test_gemm_forward_bias_relu(gpu, shape):
     b = (torch.randn(N, generator=g) * 0.1).to(gpu)
     xp = torch.zeros(M, D._r8(K), dtype=torch.bfloat16, device=gpu)[:, :K]
     xp.copy_(x)
-    y = D.gemm(xp, _mrec.LAYOUT_ROW, W, _mrec.LAYOUT_ROW, M, N, K, bias=b, act=_mrec.ACT_RELU)
+    wr, _ = D.weight_prep(W, tr=False)
+    y = D.gemm(xp, _mrec.LAYOUT_ROW, wr[:, :K], _mrec.LAYOUT_ROW, M, N, K, bias=b,
+               act=_mrec.ACT_RELU)
     want = torch.relu(_bf(x) @ _bf(W).T + b.double())
     mag = _bf(x).abs() @ _bf(W).abs().T + b.double().abs()
     ok, worst = _close(y, want, mag)
     assert ok, worst
 
 
-@pytest.mark.parametrize("split_k", [1, 4, 8])
+@pytest.mark.parametrize("split_k", [1, 4, 13])
 def test_gemm_weight_grad_col_col_ones_column(gpu, split_k):
     """dW = dZ^T x and db = sum_m dZ via the ones column; dZ = dy * (y > 0)."""
     from pytorchrec_amd import dense as D, _mrec
@@ -55,15 +58,17 @@ def test_gemm_weight_grad_col_col_ones_column(gpu, split_k):
     dy = torch.randn(M, N, generator=g).to(torch.bfloat16).to(gpu)
     y = torch.randn(M, N, generator=g).to(torch.bfloat16).to(gpu)
     x = torch.randn(M, K, generator=g).to(torch.bfloat16).to(gpu)
+    dy, y, x = D._bf16_rows(dy), D._bf16_rows(y), D._bf16_rows(x)  # 16-B aligned rows
+    db = torch.empty(N, dtype=torch.float32, device=gpu)
     out = D.gemm(dy, _mrec.LAYOUT_COL, x, _mrec.LAYOUT_COL, N, K, M, a_mod=y,
-                 a_mod_kind=_mrec.AMOD_RELU_MASK, ones_col=True, out_dtype=torch.float32,
+                 a_mod_kind=_mrec.AMOD_RELU_MASK, ones_out=db, out_dtype=torch.float32,
                  split_k=split_k)
     dz = _bf(dy) * (y.double() > 0)
     want_w = dz.T @ _bf(x)
     want_b = dz.sum(0)
     ok, worst = _close(out[:, :K], want_w, dz.abs().T @ _bf(x).abs(), out_bf16=False)
     assert ok, worst
-    ok, worst = _close(out[:, K], want_b, dz.abs().sum(0), out_bf16=False)
+    ok, worst = _close(db, want_b, dz.abs().sum(0), out_bf16=False)
     assert ok, worst
 
 
@@ -76,8 +81,13 @@ def test_gemm_input_grad_row_col_with_zero_pad(gpu):
     dy = torch.randn(M, N, generator=g).to(torch.bfloat16).to(gpu)
     y = torch.randn(M, N, generator=g).to(torch.bfloat16).to(gpu)
     W = (torch.randn(N, K, generator=g) * 0.05).to(gpu)
-    dx = D.gemm(dy, _mrec.LAYOUT_ROW, W, _mrec.LAYOUT_COL, M, KX, N, a_mod=y,
+    wr, wt = D.weight_prep(W)
+    # B(k'=n, col=k) = W[n, k]: the row image read as COL, or W^T read as ROW
+    dx = D.gemm(dy, _mrec.LAYOUT_ROW, wr, _mrec.LAYOUT_COL, M, KX, N, a_mod=y,
                 a_mod_kind=_mrec.AMOD_RELU_MASK, b_cols=K)
+    dx2 = D.gemm(dy, _mrec.LAYOUT_ROW, wt, _mrec.LAYOUT_ROW, M, KX, N, a_mod=y,
+                 a_mod_kind=_mrec.AMOD_RELU_MASK, b_cols=K)
+    assert torch.equal(dx, dx2)
     dz = _bf(dy) * (y.double() > 0)
     want = dz @ _bf(W)
     ok, worst = _close(dx[:, :K], want, dz.abs() @ _bf(W).abs())

@@ -1,0 +1,89 @@
+"""Microbenchmark of libmrec's MFMA GEMM on the DeepFM MLP shapes (B = 4096).
+
+    python tools/bench_gemm.py [--reps 200] [--only fwd|dx|dw]
+
+Prints per-shape average kernel time (HIP events around back-to-back launches on
+one stream, graph-captured to strip host overhead) and, for reference, torch's
+own matmul (hipBLASLt) on the same shape.
+"""
+import argparse
+import os
+import sys
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+import torch  # noqa: E402
+
+from pytorchrec_amd import _mrec, dense as D  # noqa: E402
+
+
+def timed(fn, reps):
+    s = torch.cuda.Stream()
+    s.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(s):
+        fn()
+    torch.cuda.current_stream().wait_stream(s)
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g):
+        for _ in range(10):
+            fn()
+    g.replay()
+    torch.cuda.synchronize()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    for _ in range(reps // 10):
+        g.replay()
+    e1.record()
+    e1.synchronize()
+    return e0.elapsed_time(e1) * 1e3 / (reps // 10 * 10)
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--reps", type=int, default=200)
+    ap.add_argument("--only", default="")
+    a = ap.parse_args()
+    dev = torch.device("cuda:0")
+    M, N, K = 4096, 400, 429
+    x = D._alloc(M, 432, torch.bfloat16, dev)
+    x.normal_()
+    W = torch.randn(N, K, device=dev) * 0.05
+    b = torch.randn(N, device=dev) * 0.05
+    wr, wt = D.weight_prep(W)
+    y = D._alloc(M, N, torch.bfloat16, dev)
+    y.normal_()
+    dy = D._alloc(M, N, torch.bfloat16, dev)
+    dy.normal_()
+    dW = torch.empty(N, K, device=dev)
+    db = torch.empty(N, device=dev)
+    flop = 2 * M * N * K
+    cases = {
+        "fwd": lambda: D.gemm(x, _mrec.LAYOUT_ROW, wr[:, :K], _mrec.LAYOUT_ROW, M, N, K, bias=b,
+                              act=_mrec.ACT_RELU, out=y),
+        "dx": lambda: D.gemm(dy, _mrec.LAYOUT_ROW, wt, _mrec.LAYOUT_ROW, M, 432, N, a_mod=y,
+                             a_mod_kind=_mrec.AMOD_RELU_MASK, b_cols=K),
+        "dw": lambda: D.gemm(dy, _mrec.LAYOUT_COL, x, _mrec.LAYOUT_COL, N, K, M, a_mod=y,
+                             a_mod_kind=_mrec.AMOD_RELU_MASK, ones_out=db, out=dW),
+        "prep": lambda: D.weight_prep(W),
+    }
+    xb = x[:, :K].contiguous()
+    wb = W.to(torch.bfloat16)
+    dyb = dy.contiguous()
+    ref = {
+        "fwd": lambda: torch.nn.functional.linear(xb, wb),
+        "dx": lambda: dyb @ wb,
+        "dw": lambda: dyb.t() @ xb,
+    }
+    for name, fn in cases.items():
+        if a.only and name != a.only:
+            continue
+        t = timed(fn, a.reps)
+        line = f"{name:5s} mrec {t:8.2f} us  {flop / t / 1e6:8.1f} TFLOP/s"
+        if name in ref:
+            tr = timed(ref[name], a.reps)
+            line += f"   | torch/hipBLASLt {tr:8.2f} us"
+        print(line, flush=True)
+
+
+if __name__ == "__main__":
+    main()

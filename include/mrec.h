@@ -197,13 +197,13 @@ typedef struct {
 
 #define MREC_ACT_NONE 0
 #define MREC_ACT_RELU 1
-#define MREC_AMOD_NONE 0
-#define MREC_AMOD_RELU_MASK 1 /* A(m,k) *= (mod(m,k) > 0): ReLU backward */
-#define MREC_AMOD_MUL 2       /* A(m,k) *= mod(m,k):      DCN dz = g * x0  */
 
-/* v = acc + bias[n]; aux[m,n] = v; v = act(v); v *= mul[m,n]; v += add[m,n]; C = v.
- * Every pointer may be NULL (term skipped); mul/add/aux are bf16 [M, ld].  With
- * b_ones_col the extra column (the row sums of A') goes to ones_out (fp32 [M]). */
+/* v = acc + bias[n]; aux[m,n] = v; v = act(v); v *= mul[m,n]; v += add[m,n];
+ * v = (mask[m,n] > 0) ? v : 0; C = v.  Every pointer may be NULL (term skipped);
+ * mul/add/aux/mask are bf16 [M, ld].  `mask` applies the ReLU' of the layer that
+ * produced this GEMM's *output* operand, so a backward GEMM emits the next
+ * layer's pre-activation gradient directly.  With b_ones_col the extra column (the
+ * row sums of A) goes to ones_out (fp32 [M]). */
 typedef struct {
   const float *bias;
   int32_t act;
@@ -213,32 +213,35 @@ typedef struct {
   int64_t ld_add;
   void *aux;
   int64_t ld_aux;
+  const void *mask;
+  int64_t ld_mask;
   float *ones_out;
 } mrec_epilogue;
 
 size_t mrec_gemm_workspace_size(int64_t M, int64_t N, int64_t K, int32_t split_k);
 
 /*
- * C[M, N] = epi( sum_k A'(m, k) B(k, n) ),  A' = A modified by a_mod (bf16,
- * A's layout) as a_mod_kind says.  A and B bf16 (fp32 weights go through
- * mrec_weight_prep), fp32 accumulation on v_mfma_f32_16x16x32_bf16.  Each
- * workgroup stages a K slab of <= 448 into LDS in one phase (every load in
- * flight at once); K is split over max(split_k, ceil(K/448)) workgroups.
- * B(k, n) for layout ROW is ptr[n*ld + k] (nn.Linear's [out, in] weight), for
- * COL ptr[k*ld + n].  b_ones_col == N appends a column of
- * ones to B, so epi->ones_out[m] = sum_k A'(m, k): the bias gradient of a
- * weight-gradient GEMM.  B(k, n) = 0 for b_cols <= n < N (b_cols <= N), so the
- * gradient of a zero-padded input comes out zero-padded.  With more than one K
- * slab the fp32 partials are reduced in fixed order (deterministic) through
- * `workspace` (mrec_gemm_workspace_size bytes).
+ * C[M, N] = epi( sum_k A(m, k) B(k, n) ), A and B bf16 with 16-byte aligned rows
+ * (fp32 weights go through mrec_weight_prep), fp32 accumulation on
+ * v_mfma_f32_16x16x32_bf16.  Each 256-thread workgroup computes a 64x64 tile over
+ * a K slab of <= 448: both operand slabs are brought into LDS by
+ * global_load_lds_dwordx4 (LDS-DMA, swizzled images, no register staging), COL
+ * operands are read back with ds_read_b64_tr_b16; K is split over
+ * max(split_k, ceil(K/448)) workgroups, partials reduced in fixed order
+ * (deterministic) through `workspace` (mrec_gemm_workspace_size bytes).
+ * Layout ROW: element (i, k) at ptr[i*ld + k]; COL: at ptr[k*ld + i] (for B, i is
+ * the output column n; nn.Linear's [out, in] weight is B in ROW layout).
+ * b_ones_col == N appends a column of ones to B, so epi->ones_out[m] = sum_k A(m, k):
+ * the bias gradient of a weight-gradient GEMM.  B(k, n) = 0 for b_cols <= n < N.
+ * Operand pad elements between K (or the valid rows) and the next multiple of 8 must
+ * be zero; C's pad columns up to min(ldc, round8(N)) are written as zero.
  * Replaces nn.Linear forward/backward = aten::addmm / mm and the ReLU
  * (Dense.py:20-24, MLP.py:22-23; SURVEY.md §2b MLP row).
  */
 mrec_status mrec_gemm(int64_t M, int64_t N, int64_t K, const mrec_operand *A,
-                      const mrec_operand *B, const mrec_operand *a_mod, int32_t a_mod_kind,
-                      int64_t b_ones_col, int64_t b_cols, const mrec_epilogue *epi, void *C,
-                      mrec_dtype c_dtype, int64_t ldc, int32_t split_k, void *workspace,
-                      size_t ws_bytes, mrec_stream stream);
+                      const mrec_operand *B, int64_t b_ones_col, int64_t b_cols,
+                      const mrec_epilogue *epi, void *C, mrec_dtype c_dtype, int64_t ldc,
+                      int32_t split_k, void *workspace, size_t ws_bytes, mrec_stream stream);
 
 /*
  * fp32 [N, K] weight (row stride ldw) -> bf16 images for the GEMMs: `row`
@@ -260,9 +263,12 @@ mrec_status mrec_weight_prep(const float *W, int64_t N, int64_t K, int64_t ldw, 
  */
 mrec_status mrec_head_fwd(const void *h, int64_t ldh, int64_t batch, int32_t H, const float *w,
                           const float *bias, const float *base, float *z, mrec_stream stream);
-/* dh[b, :] = dz[b] * w  (bf16, pad columns up to ldh zeroed) */
-mrec_status mrec_head_bwd(const float *dz, const float *w, int64_t batch, int32_t H, void *dh,
-                          int64_t ldh, mrec_stream stream);
+/* dh[b, :] = dz[b] * w  (bf16, pad columns up to ldh zeroed); with `mask` (bf16
+ * [batch, ld_mask], may be NULL) dh[b, h] = 0 where mask[b, h] <= 0: the ReLU' of
+ * the layer that produced h, so dh is that layer's pre-activation gradient. */
+mrec_status mrec_head_bwd(const float *dz, const float *w, int64_t batch, int32_t H,
+                          const void *mask, int64_t ld_mask, void *dh, int64_t ldh,
+                          mrec_stream stream);
 
 /*
  * torch.nn.BCEWithLogitsLoss (mean): *loss = mean(max(z,0) - z y + log1p(exp(-|z|)))

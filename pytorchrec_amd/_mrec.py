@@ -75,12 +75,12 @@ class Epilogue(ctypes.Structure):
                 ("mul", ctypes.c_void_p), ("ld_mul", ctypes.c_int64),
                 ("add", ctypes.c_void_p), ("ld_add", ctypes.c_int64),
                 ("aux", ctypes.c_void_p), ("ld_aux", ctypes.c_int64),
+                ("mask", ctypes.c_void_p), ("ld_mask", ctypes.c_int64),
                 ("ones_out", ctypes.c_void_p)]
 
 
 LAYOUT_ROW, LAYOUT_COL = 0, 1
 ACT_NONE, ACT_RELU = 0, 1
-AMOD_NONE, AMOD_RELU_MASK, AMOD_MUL = 0, 1, 2
 
 _vp = ctypes.c_void_p
 _i32 = ctypes.c_int32
@@ -109,11 +109,11 @@ SIGNATURES = {
                                           _i64, _vp, _vp, _vp, ctypes.c_int, _i64, _vp,
                                           ctypes.c_int, _f32, ctypes.c_uint64, _vp, _vp, _vp]),
     "mrec_gemm_workspace_size": (ctypes.c_size_t, [_i64, _i64, _i64, _i32]),
-    "mrec_gemm": (ctypes.c_int, [_i64, _i64, _i64, _op_p, _op_p, _op_p, _i32, _i64, _i64, _epi_p,
+    "mrec_gemm": (ctypes.c_int, [_i64, _i64, _i64, _op_p, _op_p, _i64, _i64, _epi_p,
                                  _vp, ctypes.c_int, _i64, _i32, _vp, ctypes.c_size_t, _vp]),
     "mrec_weight_prep": (ctypes.c_int, [_vp, _i64, _i64, _i64, _vp, _i64, _vp, _i64, _vp]),
     "mrec_head_fwd": (ctypes.c_int, [_vp, _i64, _i64, _i32, _vp, _vp, _vp, _vp, _vp]),
-    "mrec_head_bwd": (ctypes.c_int, [_vp, _vp, _i64, _i32, _vp, _i64, _vp]),
+    "mrec_head_bwd": (ctypes.c_int, [_vp, _vp, _i64, _i32, _vp, _i64, _vp, _i64, _vp]),
     "mrec_bce_fwd": (ctypes.c_int, [_vp, _vp, _i64, _vp, _vp]),
     "mrec_bce_bwd": (ctypes.c_int, [_vp, _vp, _i64, _vp, _vp, _vp]),
     "mrec_colsum_workspace_size": (ctypes.c_size_t, [_i64]),

@@ -1,27 +1,30 @@
 // MFMA bf16 GEMM for the dense towers (MLP, DCN-v2 cross, DIN attention unit).
 //
-//   C[m, n] = epi( sum_k A'(m, k) * B(k, n) )
+//   C[m, n] = epi( sum_k A(m, k) * B(k, n) ),  A, B bf16, fp32 accumulation
 //
-// A'(m, k) = A(m, k) [* (Amod(m, k) > 0) | * Amod(m, k)]   (ReLU' mask / dz = g*x0)
-// Operands are ROW (k contiguous) or COL (m / n contiguous); B may be fp32 (read
-// and converted while staging) or bf16.  Everything is staged into LDS as
-// [row][k] images (COL operands transposed on the way in, 8x8 blocks per thread)
-// and consumed by v_mfma_f32_16x16x32_bf16 with fp32 accumulation.  Output tile
-// 64x64 per 256-thread workgroup, 4 waves in 2x2, each wave 2x2 MFMA tiles.
+// Operands are ROW (k contiguous) or COL (m / n contiguous).  One 256-thread
+// workgroup computes a 64x64 output tile over a K slab of <= 448 (4 waves in 2x2,
+// each wave 2x2 v_mfma_f32_16x16x32_bf16 tiles).  The slab is moved into LDS with
+// global_load_lds_dwordx4 (LDS-DMA: no VGPR staging, no per-element VALU), in
+// 64-wide k groups that are all put in flight at once; the MFMA loop consumes group
+// g as soon as its DMA has landed (s_waitcnt vmcnt + barrier), so the copy of the
+// later groups overlaps the math on the earlier ones.
 //
-// Two schedules:
-//  * panel  (K <= 448, the MLP / cross / attention shapes): the whole K extent of
-//    the A row panel and the B column panel is loaded into LDS in ONE phase with
-//    every load in flight at once, then the block runs K/32 MFMA steps out of LDS
-//    with no further global traffic.  At these small K the per-tile load latency,
-//    not the MFMA rate, is what a K-loop pays; this pays it once.
-//  * stream (long K: weight gradients reduce over the batch): BK = 64 tiles,
-//    double-buffered, the next tile's loads issued before the current MFMAs;
-//    split-K over workgroups with a fixed-order fp32 slab reduction.
+// LDS images (per operand, per k group of 64: 64 rows x 64 k = 8 KiB):
+//   ROW: [row][8 slots of 16 B], chunk c (8 k) of row r in slot c ^ (r & 7) — the
+//        XOR swizzle is applied to the per-lane DMA *source* address (the DMA
+//        destination is lane-linear), so fragment reads are bank-conflict free;
+//   COL: [k/8][row/16][8 k][16 rows] 256-B blocks, read back transposed with
+//        ds_read_b64_tr_b16 straight into MFMA operand layout.
+// Pieces outside the operand (rows >= ilim, k >= kend) are DMA'd from a zero page;
+// a 16-B piece straddling the last valid k (or row, for COL) reads the operand's
+// pad elements, which must be zero (every buffer libmrec writes is zero-padded).
 //
-// Epilogue: v = acc + bias[n]; aux = v; v = relu(v); v *= mul; v += add; C = v.
+// Epilogue (through LDS, 8 columns per 16-B store):
+//   v = acc + bias[n]; aux = v; v = relu(v); v *= mul; v += add; v = mask>0 ? v : 0.
 // b_ones_col = N appends a ones column to B: column N of the product is the row
-// sum of A' (the bias gradient) and is written to `ones_out` (fp32 [M]).
+// sum of A (the bias gradient) and goes to `ones_out` (fp32 [M]).  Split-K partial
+// tiles go to a workspace and are reduced in fixed order (deterministic).
 #include <algorithm>
 
 #include "common.h"
@@ -30,334 +33,379 @@ namespace mrec {
 
 constexpr int BM = 64, BN = 64;
 constexpr int GEMM_THREADS = 256;
-constexpr int PANEL_KMAX = 448;
-constexpr int PANEL_LD = PANEL_KMAX + 8;  // 912 B rows: 16 rows of a ds_read_b128 group hit distinct banks
+constexpr int KG = 64;                 // k per staging group
+constexpr int SLAB_KMAX = 448;         // k per workgroup: 2 x 7 groups x 8 KiB = 112 KiB LDS
+constexpr int GROUP_ELEMS = 64 * KG;   // one operand's group image (bf16 elements)
+constexpr int TLD = BN + 4;            // fp32 row stride of the C tile staged in LDS
 
 typedef short bf16x8 __attribute__((ext_vector_type(8)));
 typedef float f32x4 __attribute__((ext_vector_type(4)));
+typedef short v4s __attribute__((ext_vector_type(4)));
+typedef __attribute__((address_space(3))) v4s lds_v4s;
 
 struct GemmArgs {
   int64_t M, N, K;
-  const void *A;
+  const uint16_t *A;
   int64_t lda;
-  int a_col;
-  const void *amod;
-  int64_t ld_amod;
-  int amod_kind;  // 0 none, 1 relu mask, 2 multiply
-  const void *B;
+  const uint16_t *B;
   int64_t ldb;
-  int b_col;
   int64_t b_ones_col;
   int64_t b_cols;
   const float *bias;
   int act;
-  const void *mul;
+  const uint16_t *mul;
   int64_t ld_mul;
-  const void *add;
+  const uint16_t *add;
   int64_t ld_add;
-  void *aux;
+  uint16_t *aux;
   int64_t ld_aux;
+  const uint16_t *mask;
+  int64_t ld_mask;
   void *C;
   int64_t ldc;
   int c_f32;
+  int vec;         // C / aux / mul / add / mask rows 16-B aligned: 16-B epilogue stores
+  int64_t pad_to;  // columns [N, pad_to) of C are written as 0
   float *ones_out;
-  int a_vec, amod_vec, b_vec;
   int split_k;
   int64_t k_per_split;
   float *ws;
+  int64_t ldws;    // row stride of a split-K partial slab (round8(ncols))
 };
 
 __device__ __forceinline__ float bf(uint16_t h) { return __uint_as_float(uint32_t(h) << 16); }
 
-// ---- slab staging --------------------------------------------------------
-// A workgroup stages a [64 rows][klen] slab of A and of B (klen <= 448) into
-// LDS [row][k] images.  Every thread first issues ALL of its 16-byte loads for
-// the slab (registers are the staging buffer: up to 16 per operand, plus 16 for
-// the A modifier), then applies the modifier / 8x8 transpose and writes LDS.
-//   ROW operand: 8 threads per row, 32 rows per pass, 2 passes, <= 7 chunks per pass
-//   COL operand: unit = 8x8 block (8 k rows x 8 rows), 8 * kc units, <= 2 per
-//                thread, 8 loads each
-constexpr int ROW_UNITS = 14;  // 2 passes x 7 chunks (56 chunks = 448 per row / 8 threads)
-constexpr int COL_UNITS = 2;   // ceil(8 * 56 / 256)
-constexpr int MAX_LOADS = 16;
+__device__ __attribute__((aligned(64))) uint4 g_zero_page[64];
 
-__device__ __forceinline__ uint16_t h16(const uint4 &w, int j) {
-  const uint32_t x = (j < 2) ? w.x : (j < 4) ? w.y : (j < 6) ? w.z : w.w;
-  return uint16_t((j & 1) ? (x >> 16) : (x & 0xffffu));
+// s_waitcnt vmcnt(n) with expcnt / lgkmcnt left unconstrained (gfx9 encoding)
+template <int N>
+__device__ __forceinline__ void wait_vmcnt() {
+  __builtin_amdgcn_s_waitcnt((N & 15) | ((N >> 4) << 14) | (7 << 4) | (15 << 8));
 }
-
-__device__ __forceinline__ uint4 mod16(int kind, const uint4 &a, const uint4 &m) {
-  uint16_t t[8];
-#pragma unroll
-  for (int j = 0; j < 8; ++j) {
-    const uint16_t av = h16(a, j), mv = h16(m, j);
-    t[j] = (kind == 1) ? ((mv != 0 && !(mv & 0x8000u)) ? av : uint16_t(0))
-                       : f32_to_bf16_rne(bf(av) * bf(mv));
+__device__ __forceinline__ void wait_vmcnt_dyn(int n) {
+  switch (n) {
+    case 0: wait_vmcnt<0>(); break;
+    case 4: wait_vmcnt<4>(); break;
+    case 8: wait_vmcnt<8>(); break;
+    case 12: wait_vmcnt<12>(); break;
+    case 16: wait_vmcnt<16>(); break;
+    case 20: wait_vmcnt<20>(); break;
+    case 24: wait_vmcnt<24>(); break;
+    default: wait_vmcnt<0>(); break;
   }
-  return make_uint4(uint32_t(t[0]) | (uint32_t(t[1]) << 16), uint32_t(t[2]) | (uint32_t(t[3]) << 16),
-                    uint32_t(t[4]) | (uint32_t(t[5]) << 16), uint32_t(t[6]) | (uint32_t(t[7]) << 16));
 }
 
-// Operand view: element (i, k) of the GEMM operand (i = output row for A, output
-// column for B) lives at ptr[i*ld + k] (ROW) or ptr[k*ld + i] (COL).
-struct OpView {
-  const uint16_t *p;
-  int64_t ld;
-  int64_t ilim;  // valid i (rows of A = M; columns of B = b_cols)
-  bool vec;
-};
-
+// Per-lane DMA source walker for one operand.  Every wave issues 2 instructions per
+// k group (pieces t = wave and wave + 4 of the group's 8), each moving 1 KiB.
 template <bool COL>
-struct Stager {
-  static constexpr int NL = COL ? COL_UNITS * 8 : ROW_UNITS;
-  uint4 r[NL];
+struct DmaSrc {
+  const uint16_t *p[2];  // source of this lane's piece for group 0
+  bool iok[2];           // row (ROW) / row-chunk (COL) inside the operand
+  int kofs[2];           // this lane's k offset within a group
+  int64_t step;          // elements between consecutive groups
 
-  // Issue every load of this thread for slab rows [i0, i0+64), k in [k0, k0+klen):
-  // unconditional 16-B loads from clamped addresses — no branch, no wait between
-  // them; out-of-range elements are zeroed in mask().  Rows are 16-B aligned with
-  // ld a multiple of 8 (checked on the host), so a chunk never leaves its row.
-  __device__ __forceinline__ void issue(const OpView &v, int64_t i0, int64_t k0, int klen,
-                                        int64_t kend) {
-    const int tid = threadIdx.x;
-    const int kc = klen / 8;
-    if constexpr (!COL) {
-      // 8 threads per row (128 contiguous bytes per row per instruction), 32 rows
-      // per pass, 2 passes; chunk j of a thread is k8 = (8j + q) * 8
-      const int q = tid & 7;
+  __device__ __forceinline__ DmaSrc(const uint16_t *base, int64_t ld, int64_t ilim, int64_t i0,
+                                    int64_t k0, int wave, int lane) {
 #pragma unroll
-      for (int p = 0; p < 2; ++p) {
-        const int64_t i = i0 + (tid >> 3) + 32 * p;
-        const uint16_t *rowp = v.p + (i < v.ilim ? i : 0) * v.ld + k0;
-#pragma unroll
-        for (int j = 0; j < ROW_UNITS / 2; ++j) {
-          const int ch = 8 * j + q;
-          const bool ok = ch < kc && i < v.ilim && k0 + ch * 8 < kend;
-          r[p * (ROW_UNITS / 2) + j] =
-              *reinterpret_cast<const uint4 *>(ok ? rowp + ch * 8 : v.p);
-        }
+    for (int u = 0; u < 2; ++u) {
+      const int t = wave + 4 * u;
+      int64_t i, k;
+      if constexpr (!COL) {
+        const int rr = lane >> 3;
+        i = i0 + t * 8 + rr;
+        k = ((lane & 7) ^ rr) * 8;
+      } else {
+        i = i0 + (lane >> 4) * 16 + (lane & 1) * 8;
+        k = t * 8 + ((lane & 15) >> 1);
       }
-    } else {
-#pragma unroll
-      for (int u = 0; u < COL_UNITS; ++u) {
-        const int c = tid + u * GEMM_THREADS;
-        const int rb = c & 7, k8 = (c >> 3) * 8;
-        const int64_t i = i0 + rb * 8;
-#pragma unroll
-        for (int j = 0; j < 8; ++j) {
-          const int64_t k = k0 + k8 + j;
-          const bool ok = c < 8 * kc && k < kend && i < v.ilim;
-          r[u * 8 + j] = *reinterpret_cast<const uint4 *>(v.p + (ok ? k * v.ld + i : 0));
-        }
-      }
+      iok[u] = i < ilim;
+      kofs[u] = static_cast<int>(k);
+      p[u] = COL ? base + (k0 + k) * ld + i : base + i * ld + (k0 + k);
     }
+    step = COL ? KG * ld : KG;
   }
-
-  // zero every element outside [0, ilim) x [k0, kend) (after the loads landed);
-  // branch-free word selects so the compiler never drains the load queue early
-  __device__ __forceinline__ static uint4 keep_first(const uint4 &x, int keep) {
-    uint32_t w[4] = {x.x, x.y, x.z, x.w};
+  // issue group `kg` (k range [k0 + 64 kg, ...), valid below kend - k0) into img
+  __device__ __forceinline__ void issue(int kg, int64_t krel_end, uint16_t *gimg, int wave) const {
+    const uint16_t *zero = reinterpret_cast<const uint16_t *>(g_zero_page);
 #pragma unroll
-    for (int q = 0; q < 4; ++q) {
-      const uint32_t lo = (2 * q < keep) ? 0x0000ffffu : 0u;
-      const uint32_t hi = (2 * q + 1 < keep) ? 0xffff0000u : 0u;
-      w[q] &= (lo | hi);
-    }
-    return make_uint4(w[0], w[1], w[2], w[3]);
-  }
-  __device__ __forceinline__ void mask(const OpView &v, int64_t i0, int64_t k0, int klen,
-                                       int64_t kend) {
-    const int tid = threadIdx.x;
-    const int kc = klen / 8;
-    if constexpr (!COL) {
-      const int q = tid & 7;
-#pragma unroll
-      for (int p = 0; p < 2; ++p) {
-        const int64_t i = i0 + (tid >> 3) + 32 * p;
-#pragma unroll
-        for (int j = 0; j < ROW_UNITS / 2; ++j) {
-          const int ch = 8 * j + q;
-          const int64_t k = k0 + ch * 8;
-          const bool ok = ch < kc && i < v.ilim && k < kend;
-          const int keep = ok ? static_cast<int>(min<int64_t>(8, kend - k)) : 0;
-          r[p * (ROW_UNITS / 2) + j] = keep_first(r[p * (ROW_UNITS / 2) + j], keep);
-        }
-      }
-    } else {
-#pragma unroll
-      for (int u = 0; u < COL_UNITS; ++u) {
-        const int c = tid + u * GEMM_THREADS;
-        const int rb = c & 7, k8 = (c >> 3) * 8;
-        const int64_t i = i0 + rb * 8;
-        const int keep_i = static_cast<int>(min<int64_t>(8, max<int64_t>(0, v.ilim - i)));
-#pragma unroll
-        for (int j = 0; j < 8; ++j) {
-          const bool ok = c < 8 * kc && k0 + k8 + j < kend;
-          r[u * 8 + j] = keep_first(r[u * 8 + j], ok ? keep_i : 0);
-        }
-      }
-    }
-  }
-
-  __device__ __forceinline__ void apply(int kind, const Stager &m) {
-#pragma unroll
-    for (int u = 0; u < NL; ++u) r[u] = mod16(kind, r[u], m.r[u]);
-  }
-
-  // write the staged registers into the [64][ld] LDS image
-  __device__ __forceinline__ void commit(uint16_t *S, int ld, int klen) const {
-    const int tid = threadIdx.x;
-    const int kc = klen / 8;
-    if constexpr (!COL) {
-      const int q = tid & 7;
-#pragma unroll
-      for (int p = 0; p < 2; ++p) {
-        uint16_t *rowS = S + ((tid >> 3) + 32 * p) * ld;
-#pragma unroll
-        for (int j = 0; j < ROW_UNITS / 2; ++j) {
-          const int ch = 8 * j + q;
-          if (ch < kc) *reinterpret_cast<uint4 *>(rowS + ch * 8) = r[p * (ROW_UNITS / 2) + j];
-        }
-      }
-    } else {
-#pragma unroll
-      for (int u = 0; u < COL_UNITS; ++u) {
-        const int c = tid + u * GEMM_THREADS;
-        if (c < 8 * kc) {
-          const int rb = c & 7, k8 = (c >> 3) * 8;
-#pragma unroll
-          for (int jn = 0; jn < 8; ++jn) {  // row rb*8+jn gets k8..k8+7 = column jn of the block
-            uint16_t t[8];
-#pragma unroll
-            for (int jk = 0; jk < 8; ++jk) t[jk] = h16(r[u * 8 + jk], jn);
-            *reinterpret_cast<uint4 *>(S + (rb * 8 + jn) * ld + k8) =
-                make_uint4(uint32_t(t[0]) | (uint32_t(t[1]) << 16),
-                           uint32_t(t[2]) | (uint32_t(t[3]) << 16),
-                           uint32_t(t[4]) | (uint32_t(t[5]) << 16),
-                           uint32_t(t[6]) | (uint32_t(t[7]) << 16));
-          }
-        }
-      }
+    for (int u = 0; u < 2; ++u) {
+      const bool ok = iok[u] && (kg * KG + kofs[u]) < krel_end;
+      const uint16_t *src = ok ? p[u] + kg * step : zero;
+      __builtin_amdgcn_global_load_lds(src, gimg + (wave + 4 * u) * 512, 16, 0, 0);
     }
   }
 };
 
+// write 1.0 into tile column `col` of the B image for k < kvalid (the ones column)
+template <bool COL>
+__device__ __forceinline__ void ones_column(uint16_t *img, int col, int klen, int kvalid) {
+  for (int k = threadIdx.x; k < klen; k += GEMM_THREADS) {
+    const uint16_t v = k < kvalid ? uint16_t(0x3f80) : uint16_t(0);
+    if constexpr (!COL) {
+      const int c = k >> 3;
+      img[(c >> 3) * GROUP_ELEMS + col * KG + (((c & 7) ^ (col & 7)) << 3) + (k & 7)] = v;
+    } else {
+      img[(k >> 3) * 512 + (col >> 4) * 128 + (k & 7) * 16 + (col & 15)] = v;
+    }
+  }
+}
+
+// scalar epilogue of one element (split-K reduce and unaligned outputs)
 __device__ __forceinline__ void epilogue_elem(const GemmArgs &g, int64_t m, int64_t n, float acc) {
   if (n == g.b_ones_col) {
     if (g.ones_out) g.ones_out[m] = acc;
+    if (n < g.pad_to) {
+      if (g.c_f32)
+        static_cast<float *>(g.C)[m * g.ldc + n] = 0.f;
+      else
+        static_cast<uint16_t *>(g.C)[m * g.ldc + n] = 0;
+    }
+    return;
+  }
+  if (n >= g.N) {
+    if (n < g.pad_to) {
+      if (g.c_f32)
+        static_cast<float *>(g.C)[m * g.ldc + n] = 0.f;
+      else
+        static_cast<uint16_t *>(g.C)[m * g.ldc + n] = 0;
+    }
     return;
   }
   float v = acc + (g.bias ? g.bias[n] : 0.f);
-  if (g.aux) static_cast<uint16_t *>(g.aux)[m * g.ld_aux + n] = f32_to_bf16_rne(v);
+  if (g.aux) g.aux[m * g.ld_aux + n] = f32_to_bf16_rne(v);
   if (g.act == 1) v = fmaxf(v, 0.f);
-  if (g.mul) v *= bf(static_cast<const uint16_t *>(g.mul)[m * g.ld_mul + n]);
-  if (g.add) v += bf(static_cast<const uint16_t *>(g.add)[m * g.ld_add + n]);
+  if (g.mul) v *= bf(g.mul[m * g.ld_mul + n]);
+  if (g.add) v += bf(g.add[m * g.ld_add + n]);
+  if (g.mask) {
+    const uint16_t mv = g.mask[m * g.ld_mask + n];
+    if (mv == 0 || (mv & 0x8000u)) v = 0.f;
+  }
   if (g.c_f32)
     static_cast<float *>(g.C)[m * g.ldc + n] = v;
   else
     static_cast<uint16_t *>(g.C)[m * g.ldc + n] = f32_to_bf16_rne(v);
 }
 
-__device__ __forceinline__ void mfma_step(const uint16_t *As, const uint16_t *Bs, int ld, int k,
-                                          int wm, int wn, int lane, f32x4 (&acc)[2][2]) {
-  const int fr = lane & 15, fk = k + (lane >> 4) * 8;
-  bf16x8 a[2], b[2];
+__device__ __forceinline__ void unpack8(const uint4 r, float (&f)[8]) {
+  const uint32_t w[4] = {r.x, r.y, r.z, r.w};
 #pragma unroll
-  for (int i = 0; i < 2; ++i)
-    a[i] = *reinterpret_cast<const bf16x8 *>(As + (wm * 32 + i * 16 + fr) * ld + fk);
-#pragma unroll
-  for (int j = 0; j < 2; ++j)
-    b[j] = *reinterpret_cast<const bf16x8 *>(Bs + (wn * 32 + j * 16 + fr) * ld + fk);
-#pragma unroll
-  for (int i = 0; i < 2; ++i)
-#pragma unroll
-    for (int j = 0; j < 2; ++j)
-      acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[i], b[j], acc[i][j], 0, 0, 0);
+  for (int j = 0; j < 4; ++j) {
+    f[2 * j] = __uint_as_float(w[j] << 16);
+    f[2 * j + 1] = __uint_as_float(w[j] & 0xffff0000u);
+  }
 }
 
-__device__ __forceinline__ void write_tile(const GemmArgs &g, int64_t m0, int64_t n0, int wm,
-                                           int wn, int lane, const f32x4 (&acc)[2][2]) {
-  const int64_t ncols = g.b_ones_col >= 0 ? g.b_ones_col + 1 : g.N;
+// 16-B epilogue of columns [n, n + 8) of row m (n % 8 == 0, n < max(N + ones, pad_to))
+__device__ __forceinline__ void epilogue_chunk(const GemmArgs &g, int64_t m, int64_t n,
+                                               float (&v)[8]) {
+  if (g.b_ones_col >= n && g.b_ones_col < n + 8 && g.ones_out) {
+    float o = 0.f;
 #pragma unroll
-  for (int i = 0; i < 2; ++i) {
+    for (int j = 0; j < 8; ++j)
+      if (n + j == g.b_ones_col) o = v[j];
+    g.ones_out[m] = o;
+  }
+  if (!g.vec) {
 #pragma unroll
-    for (int j = 0; j < 2; ++j) {
-      const int64_t n = n0 + wn * 32 + j * 16 + (lane & 15);
+    for (int j = 0; j < 8; ++j)
+      if (n + j < g.N || n + j < g.pad_to) epilogue_elem(g, m, n + j, v[j]);
+    return;
+  }
+  if (n >= g.N && n >= g.pad_to) return;
+  const int cnt = static_cast<int>(min<int64_t>(8, max<int64_t>(0, g.N - n)));
+  if (g.bias) {
 #pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int64_t m = m0 + wm * 32 + i * 16 + (lane >> 4) * 4 + r;
-        if (m < g.M && n < ncols) {
-          if (g.split_k > 1)
-            g.ws[(static_cast<int64_t>(blockIdx.z) * g.M + m) * ncols + n] = acc[i][j][r];
-          else
-            epilogue_elem(g, m, n, acc[i][j][r]);
-        }
-      }
-    }
+    for (int j = 0; j < 8; ++j) v[j] += j < cnt ? g.bias[n + j] : 0.f;
+  }
+#pragma unroll
+  for (int j = 0; j < 8; ++j) v[j] = j < cnt ? v[j] : 0.f;
+  if (g.aux)
+    *reinterpret_cast<uint4 *>(g.aux + m * g.ld_aux + n) =
+        make_uint4(pack_bf16x2(v[0], v[1]), pack_bf16x2(v[2], v[3]), pack_bf16x2(v[4], v[5]),
+                   pack_bf16x2(v[6], v[7]));
+  if (g.act == 1) {
+#pragma unroll
+    for (int j = 0; j < 8; ++j) v[j] = fmaxf(v[j], 0.f);
+  }
+  if (g.mul) {
+    float t[8];
+    unpack8(*reinterpret_cast<const uint4 *>(g.mul + m * g.ld_mul + n), t);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) v[j] *= t[j];
+  }
+  if (g.add) {
+    float t[8];
+    unpack8(*reinterpret_cast<const uint4 *>(g.add + m * g.ld_add + n), t);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) v[j] += t[j];
+  }
+  if (g.mask) {
+    float t[8];
+    unpack8(*reinterpret_cast<const uint4 *>(g.mask + m * g.ld_mask + n), t);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) v[j] = t[j] > 0.f ? v[j] : 0.f;
+  }
+#pragma unroll
+  for (int j = 0; j < 8; ++j) v[j] = j < cnt ? v[j] : 0.f;
+  if (n >= g.pad_to && n < g.N) return;  // (cannot happen: pad_to >= N when vec)
+  if (g.c_f32) {
+    float *c = static_cast<float *>(g.C) + m * g.ldc + n;
+    *reinterpret_cast<float4 *>(c) = make_float4(v[0], v[1], v[2], v[3]);
+    *reinterpret_cast<float4 *>(c + 4) = make_float4(v[4], v[5], v[6], v[7]);
+  } else {
+    *reinterpret_cast<uint4 *>(static_cast<uint16_t *>(g.C) + m * g.ldc + n) =
+        make_uint4(pack_bf16x2(v[0], v[1]), pack_bf16x2(v[2], v[3]), pack_bf16x2(v[4], v[5]),
+                   pack_bf16x2(v[6], v[7]));
   }
 }
 
 // ---------------------------------------------------------------------------
-// slab kernel: one K slab (<= 448) per workgroup, staged in one phase
+// the kernel
 // ---------------------------------------------------------------------------
-template <bool A_COL, bool B_COL, bool AMOD>
-__global__ __launch_bounds__(GEMM_THREADS) void gemm_slab_kernel(GemmArgs g) {
+template <bool A_COL, bool B_COL>
+__global__ __launch_bounds__(GEMM_THREADS) void gemm_dma_kernel(GemmArgs g) {
   extern __shared__ __attribute__((aligned(16))) uint16_t smem[];
+  const int64_t kb = static_cast<int64_t>(blockIdx.z) * g.k_per_split;
+  const int64_t ke = min(g.K, kb + g.k_per_split);
+  const int64_t krel = ke > kb ? ke - kb : 0;
+  const int nkg = static_cast<int>((krel + KG - 1) / KG);
   uint16_t *As = smem;
-  uint16_t *Bs = smem + BM * PANEL_LD;
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  uint16_t *Bs = smem + nkg * GROUP_ELEMS;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int wm = wave >> 1, wn = wave & 1;
   const int64_t m0 = static_cast<int64_t>(blockIdx.y) * BM;
   const int64_t n0 = static_cast<int64_t>(blockIdx.x) * BN;
-  const int64_t kb = static_cast<int64_t>(blockIdx.z) * g.k_per_split;
-  const int64_t ke = min(g.K, kb + g.k_per_split);
-  const int klen = ke > kb ? static_cast<int>((ke - kb + 31) / 32 * 32) : 0;
-  const OpView va{static_cast<const uint16_t *>(g.A), g.lda, g.M, static_cast<bool>(g.a_vec)};
-  const OpView vb{static_cast<const uint16_t *>(g.B), g.ldb, g.b_cols, static_cast<bool>(g.b_vec)};
+
   {
-    Stager<A_COL> sa;
-    Stager<B_COL> sb;
-    sa.issue(va, m0, kb, klen, ke);
-    sb.issue(vb, n0, kb, klen, ke);
-    if constexpr (AMOD) {
-      const OpView vm{static_cast<const uint16_t *>(g.amod), g.ld_amod, g.M,
-                      static_cast<bool>(g.amod_vec)};
-      Stager<A_COL> sm;
-      sm.issue(vm, m0, kb, klen, ke);
-      sa.mask(va, m0, kb, klen, ke);
-      sa.apply(g.amod_kind, sm);  // masked-out A elements are 0 whatever the modifier
-    } else {
-      sa.mask(va, m0, kb, klen, ke);
-    }
-    sb.mask(vb, n0, kb, klen, ke);
-    sa.commit(As, PANEL_LD, klen);
-    sb.commit(Bs, PANEL_LD, klen);
-    if (g.b_ones_col >= 0 && n0 <= g.b_ones_col && g.b_ones_col < n0 + BN) {
-      __syncthreads();  // the commit above wrote zeros into this row (uniform branch)
-      // the appended ones column of B: row (b_ones_col - n0) of the B image = 1 for k < ke
-      const int rowo = static_cast<int>(g.b_ones_col - n0);
-      for (int k = tid; k < klen; k += GEMM_THREADS)
-        Bs[rowo * PANEL_LD + k] = (kb + k < ke) ? uint16_t(0x3f80) : uint16_t(0);
+    const DmaSrc<A_COL> da(g.A, g.lda, g.M, m0, kb, wave, lane);
+    const DmaSrc<B_COL> db(g.B, g.ldb, g.b_cols, n0, kb, wave, lane);
+    for (int kg = 0; kg < nkg; ++kg) {
+      da.issue(kg, krel, As + kg * GROUP_ELEMS, wave);
+      db.issue(kg, krel, Bs + kg * GROUP_ELEMS, wave);
     }
   }
-  __syncthreads();
+  const bool ones_here = g.b_ones_col >= n0 && g.b_ones_col < n0 + BN;  // uniform
+  if (ones_here) {
+    wait_vmcnt<0>();
+    __syncthreads();
+    ones_column<B_COL>(Bs, static_cast<int>(g.b_ones_col - n0), nkg * KG, static_cast<int>(krel));
+    __syncthreads();
+  }
+
+  // per-lane fragment offsets within a group image, for the group's two k steps
+  const int g4 = lane >> 4, l15 = lane & 15;
+  int aoff[2], boff[2];
+#pragma unroll
+  for (int s = 0; s < 2; ++s) {
+    if constexpr (!A_COL)
+      aoff[s] = (wm * 32 + l15) * KG + ((((s * 4 + g4) ^ (lane & 7))) << 3);
+    else
+      aoff[s] = (s * 4 + g4) * 512 + (wm * 32 >> 4) * 128 + (l15 >> 2) * 16 + 4 * (l15 & 3);
+    if constexpr (!B_COL)
+      boff[s] = (wn * 32 + l15) * KG + ((((s * 4 + g4) ^ (lane & 7))) << 3);
+    else
+      boff[s] = (s * 4 + g4) * 512 + (wn * 32 >> 4) * 128 + (l15 >> 2) * 16 + 4 * (l15 & 3);
+  }
+
   f32x4 acc[2][2];
 #pragma unroll
   for (int i = 0; i < 2; ++i)
 #pragma unroll
     for (int j = 0; j < 2; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-  for (int k = 0; k < klen; k += 32) mfma_step(As, Bs, PANEL_LD, k, wm, wn, lane, acc);
-  write_tile(g, m0, n0, wm, wn, lane, acc);
+
+  for (int kg = 0; kg < nkg; ++kg) {
+    // this wave's DMAs of groups <= kg have landed; the barrier makes that true for
+    // every wave.  A bare s_barrier (with a compiler memory clobber): __syncthreads'
+    // release fence would wait for vmcnt(0), i.e. for the whole slab.
+    if (!ones_here) wait_vmcnt_dyn(4 * (nkg - 1 - kg));
+    asm volatile("s_barrier" ::: "memory");
+    const uint16_t *ag = As + kg * GROUP_ELEMS, *bg = Bs + kg * GROUP_ELEMS;
+#pragma unroll
+    for (int s = 0; s < 2; ++s) {
+      bf16x8 a[2], b[2];
+#pragma unroll
+      for (int i = 0; i < 2; ++i) {
+        if constexpr (!A_COL) {
+          a[i] = *reinterpret_cast<const bf16x8 *>(ag + aoff[s] + i * 16 * KG);
+        } else {
+          const uint16_t *q = ag + aoff[s] + i * 128;
+          const v4s lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4s *)(q));
+          const v4s hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4s *)(q + 64));
+          a[i] = bf16x8{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+        }
+        if constexpr (!B_COL) {
+          b[i] = *reinterpret_cast<const bf16x8 *>(bg + boff[s] + i * 16 * KG);
+        } else {
+          const uint16_t *q = bg + boff[s] + i * 128;
+          const v4s lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4s *)(q));
+          const v4s hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4s *)(q + 64));
+          b[i] = bf16x8{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+        }
+      }
+#pragma unroll
+      for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[i], b[j], acc[i][j], 0, 0, 0);
+    }
+  }
+
+  // ---- epilogue: C tile -> LDS (fp32) -> 8-column chunks ----
+  __syncthreads();
+  float *T = reinterpret_cast<float *>(smem);
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+      for (int r = 0; r < 4; ++r)
+        T[(wm * 32 + i * 16 + g4 * 4 + r) * TLD + wn * 32 + j * 16 + l15] = acc[i][j][r];
+  __syncthreads();
+  const int row = tid >> 2;
+  const int64_t m = m0 + row;
+  if (m >= g.M) return;
+  const int64_t ncols = g.b_ones_col >= 0 ? g.b_ones_col + 1 : g.N;
+#pragma unroll
+  for (int h = 0; h < 2; ++h) {
+    const int c = (tid & 3) * 16 + h * 8;
+    const int64_t n = n0 + c;
+    float v[8];
+    const float4 x0 = *reinterpret_cast<const float4 *>(T + row * TLD + c);
+    const float4 x1 = *reinterpret_cast<const float4 *>(T + row * TLD + c + 4);
+    v[0] = x0.x; v[1] = x0.y; v[2] = x0.z; v[3] = x0.w;
+    v[4] = x1.x; v[5] = x1.y; v[6] = x1.z; v[7] = x1.w;
+    if (g.split_k > 1) {
+      if (n < ncols) {
+        float *w = g.ws + (static_cast<int64_t>(blockIdx.z) * g.M + m) * g.ldws + n;
+        *reinterpret_cast<float4 *>(w) = x0;
+        *reinterpret_cast<float4 *>(w + 4) = x1;
+      }
+    } else if (n < ncols || n < g.pad_to) {
+      epilogue_chunk(g, m, n, v);
+    }
+  }
 }
 
-// fixed-order reduction of split-K partial slabs + epilogue
+// fixed-order reduction of the split-K partial slabs + epilogue (4 columns / thread)
 __global__ __launch_bounds__(256) void splitk_reduce_kernel(GemmArgs g) {
   const int64_t ncols = g.b_ones_col >= 0 ? g.b_ones_col + 1 : g.N;
-  const int64_t total = g.M * ncols;
+  const int64_t q = g.ldws / 4;
+  const int64_t total = g.M * q;
+  const int64_t slab = g.M * g.ldws;
   for (int64_t i = static_cast<int64_t>(blockIdx.x) * 256 + threadIdx.x; i < total;
        i += static_cast<int64_t>(gridDim.x) * 256) {
-    float s = 0.f;
-    for (int z = 0; z < g.split_k; ++z) s += g.ws[z * total + i];
-    epilogue_elem(g, i / ncols, i % ncols, s);
+    const int64_t m = i / q, n = (i - m * q) * 4;
+    if (n >= ncols && n >= g.pad_to) continue;
+    float4 s = *reinterpret_cast<const float4 *>(g.ws + m * g.ldws + n);
+    for (int z = 1; z < g.split_k; ++z) {
+      const float4 t = *reinterpret_cast<const float4 *>(g.ws + z * slab + m * g.ldws + n);
+      s.x += t.x; s.y += t.y; s.z += t.z; s.w += t.w;
+    }
+    const float e[4] = {s.x, s.y, s.z, s.w};
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+      if (n + j < ncols || n + j < g.pad_to) epilogue_elem(g, m, n + j, e[j]);
   }
 }
 
@@ -391,29 +439,31 @@ static bool aligned16(const void *p, int64_t ld, int es) {
   return p && (reinterpret_cast<uintptr_t>(p) & 15) == 0 && (ld * es) % 16 == 0;
 }
 
-// K slab per workgroup (multiple of 32, <= PANEL_KMAX) and the resulting split count
+// K slab per workgroup (multiple of 64, <= SLAB_KMAX) and the resulting split count
 static void plan_split(int64_t K, int32_t split_req, int64_t *kps, int32_t *splits) {
   int64_t s = split_req < 1 ? 1 : split_req;
-  int64_t k = ((K + s - 1) / s + 31) / 32 * 32;
-  if (k > PANEL_KMAX) {
-    s = (K + PANEL_KMAX - 1) / PANEL_KMAX;
-    k = ((K + s - 1) / s + 31) / 32 * 32;
+  int64_t k = ((K + s - 1) / s + KG - 1) / KG * KG;
+  if (k > SLAB_KMAX) {
+    s = (K + SLAB_KMAX - 1) / SLAB_KMAX;
+    k = ((K + s - 1) / s + KG - 1) / KG * KG;
   }
-  if (k < 32) k = 32;
+  if (k < KG) k = KG;
   *kps = k;
   *splits = static_cast<int32_t>(K > 0 ? (K + k - 1) / k : 1);
 }
 
-template <bool AC, bool BC, bool AM>
-static void launch_slab(const GemmArgs &g, dim3 grid, hipStream_t s) {
+template <bool AC, bool BC>
+static void launch_dma(const GemmArgs &g, dim3 grid, hipStream_t s) {
   static bool attr = false;
-  const size_t lds = 2 * static_cast<size_t>(BM) * PANEL_LD * sizeof(uint16_t);
+  const size_t lds = std::max<size_t>(2 * 64 * static_cast<size_t>(g.k_per_split) * sizeof(uint16_t),
+                                      BM * TLD * sizeof(float));
   if (!attr) {
-    (void)hipFuncSetAttribute(reinterpret_cast<const void *>(gemm_slab_kernel<AC, BC, AM>),
-                              hipFuncAttributeMaxDynamicSharedMemorySize, static_cast<int>(lds));
+    (void)hipFuncSetAttribute(reinterpret_cast<const void *>(gemm_dma_kernel<AC, BC>),
+                              hipFuncAttributeMaxDynamicSharedMemorySize,
+                              2 * 64 * SLAB_KMAX * static_cast<int>(sizeof(uint16_t)));
     attr = true;
   }
-  gemm_slab_kernel<AC, BC, AM><<<grid, GEMM_THREADS, lds, s>>>(g);
+  gemm_dma_kernel<AC, BC><<<grid, GEMM_THREADS, lds, s>>>(g);
 }
 
 }  // namespace mrec
@@ -427,23 +477,21 @@ size_t mrec_gemm_workspace_size(int64_t M, int64_t N, int64_t K, int32_t split_k
   int32_t splits;
   plan_split(K, split_k, &kps, &splits);
   if (splits <= 1) return 0;
-  return static_cast<size_t>(splits) * static_cast<size_t>(M) * static_cast<size_t>(N + 1) * 4;
+  return static_cast<size_t>(splits) * static_cast<size_t>(M) *
+         static_cast<size_t>((N + 1 + 7) / 8 * 8) * 4;
 }
 
 mrec_status mrec_gemm(int64_t M, int64_t N, int64_t K, const mrec_operand *A,
-                      const mrec_operand *B, const mrec_operand *a_mod, int32_t a_mod_kind,
-                      int64_t b_ones_col, int64_t b_cols, const mrec_epilogue *epi, void *C,
-                      mrec_dtype c_dtype, int64_t ldc, int32_t split_k, void *workspace,
-                      size_t ws_bytes, mrec_stream stream) {
+                      const mrec_operand *B, int64_t b_ones_col, int64_t b_cols,
+                      const mrec_epilogue *epi, void *C, mrec_dtype c_dtype, int64_t ldc,
+                      int32_t split_k, void *workspace, size_t ws_bytes, mrec_stream stream) {
   MREC_CHECK_ARG(M >= 0 && N >= 0 && K >= 0, "negative size");
   MREC_CHECK_ARG(A && A->ptr && B && B->ptr && C, "NULL operand");
   MREC_CHECK_ARG(A->dtype == MREC_BF16 && B->dtype == MREC_BF16,
                  "A and B must be bf16 (prepare fp32 weights with mrec_weight_prep)");
+  MREC_CHECK_ARG(aligned16(A->ptr, A->ld, 2) && aligned16(B->ptr, B->ld, 2),
+                 "A/B rows must be 16-byte aligned (pointer % 16 == 0, ld % 8 == 0)");
   MREC_CHECK_ARG(c_dtype == MREC_BF16 || c_dtype == MREC_F32, "C must be bf16 or f32");
-  MREC_CHECK_ARG(a_mod_kind >= 0 && a_mod_kind <= 2, "bad a_mod_kind");
-  MREC_CHECK_ARG(a_mod_kind == 0 || (a_mod && a_mod->ptr && a_mod->dtype == MREC_BF16 &&
-                                     a_mod->layout == A->layout),
-                 "a_mod must be bf16 with A's layout");
   MREC_CHECK_ARG(b_ones_col < 0 || b_ones_col == N, "b_ones_col must be -1 or N");
   MREC_CHECK_ARG(b_cols >= 0 && b_cols <= N, "b_cols must be in [0, N]");
   MREC_CHECK_ARG(split_k >= 1 && split_k <= 64, "split_k out of [1, 64]");
@@ -462,55 +510,51 @@ mrec_status mrec_gemm(int64_t M, int64_t N, int64_t K, const mrec_operand *A,
   g.M = M;
   g.N = N;
   g.K = K;
-  g.A = A->ptr;
+  g.A = static_cast<const uint16_t *>(A->ptr);
   g.lda = A->ld;
-  g.a_col = A->layout == MREC_LAYOUT_COL;
-  g.amod = a_mod_kind ? a_mod->ptr : nullptr;
-  g.ld_amod = a_mod_kind ? a_mod->ld : 0;
-  g.amod_kind = a_mod_kind;
-  g.B = B->ptr;
+  g.B = static_cast<const uint16_t *>(B->ptr);
   g.ldb = B->ld;
-  g.b_col = B->layout == MREC_LAYOUT_COL;
+  const bool a_col = A->layout == MREC_LAYOUT_COL, b_col = B->layout == MREC_LAYOUT_COL;
   g.b_ones_col = b_ones_col;
   g.b_cols = b_cols;
   if (epi) {
     g.bias = epi->bias;
     g.act = epi->act;
-    g.mul = epi->mul;
+    g.mul = static_cast<const uint16_t *>(epi->mul);
     g.ld_mul = epi->ld_mul;
-    g.add = epi->add;
+    g.add = static_cast<const uint16_t *>(epi->add);
     g.ld_add = epi->ld_add;
-    g.aux = epi->aux;
+    g.aux = static_cast<uint16_t *>(epi->aux);
     g.ld_aux = epi->ld_aux;
+    g.mask = static_cast<const uint16_t *>(epi->mask);
+    g.ld_mask = epi->ld_mask;
     g.ones_out = epi->ones_out;
   }
   g.C = C;
   g.ldc = ldc;
   g.c_f32 = c_dtype == MREC_F32;
-  g.a_vec = aligned16(g.A, g.lda, 2);
-  g.amod_vec = g.amod ? aligned16(g.amod, g.ld_amod, 2) : 1;
-  g.b_vec = aligned16(g.B, g.ldb, 2);
-  MREC_CHECK_ARG(g.a_vec && g.b_vec && g.amod_vec,
-                 "A/B/a_mod rows must be 16-byte aligned (pointer % 16 == 0, ld % 8 == 0)");
+  g.pad_to = std::min<int64_t>(ldc, (N + 7) / 8 * 8);
+  g.ldws = (ncols + 7) / 8 * 8;
+  g.vec = aligned16(C, ldc, g.c_f32 ? 4 : 2) && (!g.mul || aligned16(g.mul, g.ld_mul, 2)) &&
+          (!g.add || aligned16(g.add, g.ld_add, 2)) && (!g.aux || aligned16(g.aux, g.ld_aux, 2)) &&
+          (!g.mask || aligned16(g.mask, g.ld_mask, 2));
   g.ws = static_cast<float *>(workspace);
   g.split_k = splits;
   g.k_per_split = kps;
   hipStream_t s = static_cast<hipStream_t>(stream);
   const dim3 grid(static_cast<unsigned>((ncols + BN - 1) / BN),
                   static_cast<unsigned>((M + BM - 1) / BM), static_cast<unsigned>(splits));
-  const bool am = a_mod_kind != 0;
-  if (!g.a_col && !g.b_col) {
-    am ? launch_slab<false, false, true>(g, grid, s) : launch_slab<false, false, false>(g, grid, s);
-  } else if (!g.a_col && g.b_col) {
-    am ? launch_slab<false, true, true>(g, grid, s) : launch_slab<false, true, false>(g, grid, s);
-  } else if (g.a_col && !g.b_col) {
-    am ? launch_slab<true, false, true>(g, grid, s) : launch_slab<true, false, false>(g, grid, s);
-  } else {
-    am ? launch_slab<true, true, true>(g, grid, s) : launch_slab<true, true, false>(g, grid, s);
-  }
+  if (!a_col && !b_col)
+    launch_dma<false, false>(g, grid, s);
+  else if (!a_col && b_col)
+    launch_dma<false, true>(g, grid, s);
+  else if (a_col && !b_col)
+    launch_dma<true, false>(g, grid, s);
+  else
+    launch_dma<true, true>(g, grid, s);
   mrec_status st = launch_status("mrec_gemm");
   if (st != MREC_OK || splits == 1) return st;
-  const int64_t total = M * ncols;
+  const int64_t total = M * (g.ldws / 4);
   const unsigned rb = static_cast<unsigned>(std::min<int64_t>((total + 255) / 256, 2048));
   splitk_reduce_kernel<<<rb, 256, 0, s>>>(g);
   return launch_status("mrec_gemm(split-k reduce)");

@@ -37,10 +37,13 @@ __global__ __launch_bounds__(256) void head_fwd_kernel(const uint16_t *__restric
   if (lane == 0) z[b] = acc + (bias ? bias[0] : 0.f) + (base ? base[b] : 0.f);
 }
 
-// dh[b, h] = dz[b] * w[h]  (bf16 out, row stride ldh; pad columns up to ldh zeroed)
+// dh[b, h] = dz[b] * w[h] (* relu'(mask[b, h]))  (bf16 out, row stride ldh; pad
+// columns up to ldh zeroed)
 __global__ __launch_bounds__(256) void head_bwd_kernel(const float *__restrict__ dz,
                                                        const float *__restrict__ w, int64_t B, int H,
-                                                       uint16_t *__restrict__ dh, int64_t ldh) {
+                                                       const uint16_t *__restrict__ mask,
+                                                       int64_t ld_mask, uint16_t *__restrict__ dh,
+                                                       int64_t ldh) {
   const int64_t n8 = ldh / 8;
   const int64_t total = B * n8;
   for (int64_t i = static_cast<int64_t>(blockIdx.x) * 256 + threadIdx.x; i < total;
@@ -51,6 +54,15 @@ __global__ __launch_bounds__(256) void head_bwd_kernel(const float *__restrict__
     float v[8];
 #pragma unroll
     for (int j = 0; j < 8; ++j) v[j] = (c + j < H) ? g * w[c + j] : 0.f;
+    if (mask) {
+      const uint4 mv = *reinterpret_cast<const uint4 *>(mask + b * ld_mask + c);
+      const uint32_t mw[4] = {mv.x, mv.y, mv.z, mv.w};
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const uint32_t h = (mw[j >> 1] >> ((j & 1) * 16)) & 0xffffu;
+        if (h == 0 || (h & 0x8000u)) v[j] = 0.f;
+      }
+    }
     *reinterpret_cast<uint4 *>(dh + b * ldh + c) =
         make_uint4(pack_bf16x2(v[0], v[1]), pack_bf16x2(v[2], v[3]), pack_bf16x2(v[4], v[5]),
                    pack_bf16x2(v[6], v[7]));
@@ -161,16 +173,21 @@ mrec_status mrec_head_fwd(const void *h, int64_t ldh, int64_t batch, int32_t H, 
   return launch_status("mrec_head_fwd");
 }
 
-mrec_status mrec_head_bwd(const float *dz, const float *w, int64_t batch, int32_t H, void *dh,
-                          int64_t ldh, mrec_stream stream) {
+mrec_status mrec_head_bwd(const float *dz, const float *w, int64_t batch, int32_t H,
+                          const void *mask, int64_t ld_mask, void *dh, int64_t ldh,
+                          mrec_stream stream) {
   MREC_CHECK_ARG(dz && w && dh, "NULL pointer");
   MREC_CHECK_ARG(batch >= 0 && H >= 1 && ldh >= H && ldh % 8 == 0, "bad shape");
   MREC_CHECK_ARG((reinterpret_cast<uintptr_t>(dh) & 15) == 0, "dh must be 16-byte aligned");
+  MREC_CHECK_ARG(!mask || ((reinterpret_cast<uintptr_t>(mask) & 15) == 0 && ld_mask % 8 == 0 &&
+                           ld_mask >= (H + 7) / 8 * 8),
+                 "mask rows must be 16-byte aligned and cover round8(H) columns");
   if (batch == 0) return MREC_OK;
   const int64_t total = batch * (ldh / 8);
   const unsigned g = static_cast<unsigned>(std::min<int64_t>((total + 255) / 256, 4096));
   head_bwd_kernel<<<g, 256, 0, static_cast<hipStream_t>(stream)>>>(
-      dz, w, batch, H, static_cast<uint16_t *>(dh), ldh);
+      dz, w, batch, H, static_cast<const uint16_t *>(mask), ld_mask, static_cast<uint16_t *>(dh),
+      ldh);
   return launch_status("mrec_head_bwd");
 }
 

@@ -2,9 +2,16 @@
 
 One seam for the model code.  On a GPU they run on libmrec's MFMA bf16 GEMM
 (``mrec_gemm``: fp32 accumulation, bias / ReLU / DCN epilogues fused, the fp32
-master weights converted to bf16 while staging, ReLU' and ``g * x0`` applied
-while staging the backward operand, the bias gradient carried as an extra ones
-column of the weight-gradient GEMM).  On a CPU device (config C1) they are the
+master weights converted to bf16 by one small prep kernel, the bias gradient
+carried as an extra ones column of the weight-gradient GEMM).
+
+ReLU' is applied by the *consumer* of a ReLU output: the backward GEMM (or head
+kernel) that produces d(relu output) masks it in its epilogue and stamps the
+gradient tensor (``_MASK_TAG`` = (mask data_ptr, version)); the producing layer
+skips its own masking only when the stamp on the incoming gradient is intact.
+Autograd accumulation of several consumers' gradients bumps the version, so the
+producer then masks itself (masking is idempotent) — correct in every graph,
+free in the MLP chain.  On a CPU device (config C1) they are the
 reference's fp32 torch ops.
 
 Activation tensors are [M, N] views of [M, round8(N)] bf16 buffers so every
@@ -47,11 +54,29 @@ def _split_for(M: int, N: int, K: int) -> int:
     return s
 
 
-def gemm(A, a_layout, B, b_layout, M, N, K, *, a_mod=None, a_mod_kind=0, ones_out=None,
-         b_cols=None, bias=None, act=0, mul=None, add=None, aux=None, out=None,
-         out_dtype=_BF16, split_k=None):
-    """C[M, N] = epi(A'[M, K] @ B[K, N]) on libmrec (see include/mrec.h mrec_gemm).
-    ``ones_out`` (fp32 [M]) receives sum_k A'(m, k) through an appended ones column."""
+_MASK_TAG = "_mrec_relu_masked"
+_RELU_OUT = "_mrec_relu_out"
+
+
+def _stamp(grad: torch.Tensor, mask_src: torch.Tensor) -> torch.Tensor:
+    setattr(grad, _MASK_TAG, (mask_src.data_ptr(), grad._version))
+    return grad
+
+
+def _premasked(grad: torch.Tensor, y_ptr: int) -> bool:
+    t = getattr(grad, _MASK_TAG, None)
+    return t is not None and t[0] == y_ptr and t[1] == grad._version
+
+
+def _is_relu_out(x: torch.Tensor) -> bool:
+    return getattr(x, _RELU_OUT, False) and x.is_cuda
+
+
+def gemm(A, a_layout, B, b_layout, M, N, K, *, ones_out=None, b_cols=None, bias=None, act=0,
+         mul=None, add=None, aux=None, mask=None, out=None, out_dtype=_BF16, split_k=None):
+    """C[M, N] = epi(A[M, K] @ B[K, N]) on libmrec (see include/mrec.h mrec_gemm).
+    ``ones_out`` (fp32 [M]) receives sum_k A(m, k) through an appended ones column;
+    ``mask`` ([M, N] bf16) zeroes outputs where mask <= 0 (ReLU')."""
     dev = A.device
     if out is None:
         out = _alloc(M, N, out_dtype, dev)
@@ -62,11 +87,10 @@ def gemm(A, a_layout, B, b_layout, M, N, K, *, a_mod=None, a_mod_kind=0, ones_ou
     epi = _mrec.Epilogue(_mrec.ptr(bias), act, _mrec.ptr(mul), mul.stride(0) if mul is not None else 0,
                          _mrec.ptr(add), add.stride(0) if add is not None else 0,
                          _mrec.ptr(aux), aux.stride(0) if aux is not None else 0,
+                         _mrec.ptr(mask), mask.stride(0) if mask is not None else 0,
                          _mrec.ptr(ones_out))
     a_op, b_op = _op(A, a_layout), _op(B, b_layout)
-    m_op = _op(a_mod, a_layout) if a_mod is not None else None
     _mrec.call("mrec_gemm", M, N, K, ctypes.byref(a_op), ctypes.byref(b_op),
-               ctypes.byref(m_op) if m_op is not None else None, a_mod_kind,
                N if ones_out is not None else -1, N if b_cols is None else b_cols,
                ctypes.byref(epi), out.data_ptr(), _mrec.dtype_code(out.dtype), out.stride(0),
                split_k, _mrec.ptr(ws), ws_bytes, _mrec.stream_handle())
@@ -104,10 +128,11 @@ def _weight_f32(w: torch.Tensor) -> torch.Tensor:
 
 
 class _LinearFn(torch.autograd.Function):
-    """y = act(x[:, :K] W^T + b) with W [N, K] fp32 (nn.Linear layout)."""
+    """y = act(x[:, :K] W^T + b) with W [N, K] fp32 (nn.Linear layout).
+    x_relu: x is a ReLU output, so dx is masked by x in the dx GEMM's epilogue."""
 
     @staticmethod
-    def forward(ctx, x, weight, bias, relu: bool, out_dtype):
+    def forward(ctx, x, weight, bias, relu: bool, out_dtype, x_relu: bool):
         x = _bf16_rows(x)
         M, K_x = x.shape
         N, K = weight.shape
@@ -117,7 +142,8 @@ class _LinearFn(torch.autograd.Function):
         y = gemm(x, _mrec.LAYOUT_ROW, wr[:, :K], _mrec.LAYOUT_ROW, M, N, K, bias=b,
                  act=_mrec.ACT_RELU if relu else _mrec.ACT_NONE, out_dtype=out_dtype)
         ctx.save_for_backward(x, wt, y if relu else None)
-        ctx.relu, ctx.has_bias, ctx.NK = relu, bias is not None, (N, K)
+        ctx.relu, ctx.has_bias, ctx.NK, ctx.x_relu = relu, bias is not None, (N, K), x_relu
+        ctx.y_ptr = y.data_ptr()
         return y
 
     @staticmethod
@@ -125,21 +151,23 @@ class _LinearFn(torch.autograd.Function):
         x, wt, y = ctx.saved_tensors
         M, K_x = x.shape
         N, K = ctx.NK
+        if ctx.relu and not _premasked(dy, ctx.y_ptr):
+            dy = torch.where(y > 0, dy.to(y.dtype), torch.zeros((), dtype=y.dtype, device=y.device))
         dy = _bf16_rows(dy)
-        mod_kind = _mrec.AMOD_RELU_MASK if ctx.relu else _mrec.AMOD_NONE
         dx = dW = db = None
         if ctx.needs_input_grad[0]:
             # dx[m, k] = sum_n dZ[m, n] W[n, k]; B(k'=n, col=k) = W^T[k*ld + n] -> ROW
-            dx = gemm(dy, _mrec.LAYOUT_ROW, wt, _mrec.LAYOUT_ROW, M, K_x, N, a_mod=y,
-                      a_mod_kind=mod_kind, b_cols=K, out_dtype=_BF16)
+            dx = gemm(dy, _mrec.LAYOUT_ROW, wt, _mrec.LAYOUT_ROW, M, K_x, N, b_cols=K,
+                      mask=x if ctx.x_relu else None, out_dtype=_BF16)
+            if ctx.x_relu:
+                _stamp(dx, x)
         if ctx.needs_input_grad[1] or ctx.needs_input_grad[2]:
             # dW[n, k] = sum_m dZ[m, n] x[m, k]: A(i=n, red=m) = dy[m*ld + n] -> COL,
             # B(red=m, col=k) = x[m*ld + k] -> COL; ones column -> db
             dW = torch.empty(N, K, dtype=torch.float32, device=dy.device)
             db = torch.empty(N, dtype=torch.float32, device=dy.device) if ctx.has_bias else None
-            gemm(dy, _mrec.LAYOUT_COL, x, _mrec.LAYOUT_COL, N, K, M, a_mod=y,
-                 a_mod_kind=mod_kind, ones_out=db, out=dW)
-        return dx, dW, db, None, None
+            gemm(dy, _mrec.LAYOUT_COL, x, _mrec.LAYOUT_COL, N, K, M, ones_out=db, out=dW)
+        return dx, dW, db, None, None, None
 
 
 def linear(x: torch.Tensor, weight: torch.Tensor, bias: Optional[torch.Tensor],
@@ -152,7 +180,10 @@ def linear(x: torch.Tensor, weight: torch.Tensor, bias: Optional[torch.Tensor],
         xx = x[:, :k] if x.shape[1] > k else x
         y = F.linear(xx.float(), weight.float(), None if bias is None else bias.float())
         return torch.relu(y) if act == "relu" else y
-    return _LinearFn.apply(x, weight, bias, act == "relu", out_dtype)
+    y = _LinearFn.apply(x, weight, bias, act == "relu", out_dtype, _is_relu_out(x))
+    if act == "relu":
+        setattr(y, _RELU_OUT, True)
+    return y
 
 
 class _CrossFn(torch.autograd.Function):
@@ -179,13 +210,16 @@ class _CrossFn(torch.autograd.Function):
         g = _bf16_rows(g)
         M = g.shape[0]
         d = z.shape[1]
-        # dz = g * x0 (applied while staging A); dx_l = dz W + g; dW = dz^T x_l; db = sum dz
-        dxl = gemm(g, _mrec.LAYOUT_ROW, wt, _mrec.LAYOUT_ROW, M, xl.shape[1], d, a_mod=x0,
-                   a_mod_kind=_mrec.AMOD_MUL, b_cols=d, add=_pad_cols(g, xl.shape[1]))
+        # dz = g * x0; dx_l = dz W + g; dW = dz^T x_l; db = sum dz
+        dz = _alloc(M, d, _BF16, g.device)
+        torch.mul(g[:, :d], x0[:, :d], out=dz)
+        if dz.stride(0) > d:
+            dz.as_strided((M, dz.stride(0) - d), (dz.stride(0), 1), d).zero_()
+        dxl = gemm(dz, _mrec.LAYOUT_ROW, wt, _mrec.LAYOUT_ROW, M, xl.shape[1], d, b_cols=d,
+                   add=_pad_cols(g, xl.shape[1]))
         dW = torch.empty(d, d, dtype=torch.float32, device=g.device)
         db = torch.empty(d, dtype=torch.float32, device=g.device) if ctx.has_bias else None
-        gemm(g, _mrec.LAYOUT_COL, xl, _mrec.LAYOUT_COL, d, d, M, a_mod=x0,
-             a_mod_kind=_mrec.AMOD_MUL, ones_out=db, out=dW)
+        gemm(dz, _mrec.LAYOUT_COL, xl, _mrec.LAYOUT_COL, d, d, M, ones_out=db, out=dW)
         dx0 = (g.float() * z.float()).to(_BF16)
         if x0.shape[1] > d:
             dx0 = F.pad(dx0, (0, x0.shape[1] - d))
@@ -248,7 +282,7 @@ class _HeadFn(torch.autograd.Function):
     """z = base + h W^T + b for a Linear(H, 1) output layer (fp32 z [B])."""
 
     @staticmethod
-    def forward(ctx, h, weight, bias, base):
+    def forward(ctx, h, weight, bias, base, h_relu: bool):
         h = _bf16_rows(h)
         B, H = h.shape
         w = _weight_f32(weight).reshape(-1)
@@ -258,7 +292,7 @@ class _HeadFn(torch.autograd.Function):
         _mrec.call("mrec_head_fwd", h.data_ptr(), h.stride(0), B, H, w.data_ptr(), _mrec.ptr(b),
                    _mrec.ptr(base_c), z.data_ptr(), _mrec.stream_handle())
         ctx.save_for_backward(h, w)
-        ctx.has_bias, ctx.has_base = bias is not None, base is not None
+        ctx.has_bias, ctx.has_base, ctx.h_relu = bias is not None, base is not None, h_relu
         return z
 
     @staticmethod
@@ -269,10 +303,13 @@ class _HeadFn(torch.autograd.Function):
         dh = None
         if ctx.needs_input_grad[0]:
             dh = _alloc(B, H, _BF16, dz.device)
-            _mrec.call("mrec_head_bwd", dz.data_ptr(), w.data_ptr(), B, H, dh.data_ptr(),
+            _mrec.call("mrec_head_bwd", dz.data_ptr(), w.data_ptr(), B, H,
+                       h.data_ptr() if ctx.h_relu else None, h.stride(0), dh.data_ptr(),
                        dh.stride(0), _mrec.stream_handle())
+            if ctx.h_relu:
+                _stamp(dh, h)
         dW, db = colsum(dz, h, want_total=ctx.has_bias)
-        return dh, dW.reshape(1, H), db, (dz if ctx.has_base else None)
+        return dh, dW.reshape(1, H), db, (dz if ctx.has_base else None), None
 
 
 def head(h: torch.Tensor, weight: torch.Tensor, bias: Optional[torch.Tensor],
@@ -282,4 +319,4 @@ def head(h: torch.Tensor, weight: torch.Tensor, bias: Optional[torch.Tensor],
     if not h.is_cuda:
         z = F.linear(h.float(), weight.float(), None if bias is None else bias.float()).reshape(-1)
         return z if base is None else z + base.float()
-    return _HeadFn.apply(h, weight, bias, base)
+    return _HeadFn.apply(h, weight, bias, base, _is_relu_out(h))

@@ -51,19 +51,17 @@ def test_gemm_forward_bias_relu(gpu, shape):
 
 @pytest.mark.parametrize("split_k", [1, 4, 13])
 def test_gemm_weight_grad_col_col_ones_column(gpu, split_k):
-    """dW = dZ^T x and db = sum_m dZ via the ones column; dZ = dy * (y > 0)."""
+    """dW = dZ^T x and db = sum_m dZ via the ones column."""
     from pytorchrec_amd import dense as D, _mrec
     M, N, K = 1000, 70, 45
     g = torch.Generator().manual_seed(5)
     dy = torch.randn(M, N, generator=g).to(torch.bfloat16).to(gpu)
-    y = torch.randn(M, N, generator=g).to(torch.bfloat16).to(gpu)
     x = torch.randn(M, K, generator=g).to(torch.bfloat16).to(gpu)
-    dy, y, x = D._bf16_rows(dy), D._bf16_rows(y), D._bf16_rows(x)  # 16-B aligned rows
+    dy, x = D._bf16_rows(dy), D._bf16_rows(x)  # 16-B aligned rows
     db = torch.empty(N, dtype=torch.float32, device=gpu)
-    out = D.gemm(dy, _mrec.LAYOUT_COL, x, _mrec.LAYOUT_COL, N, K, M, a_mod=y,
-                 a_mod_kind=_mrec.AMOD_RELU_MASK, ones_out=db, out_dtype=torch.float32,
-                 split_k=split_k)
-    dz = _bf(dy) * (y.double() > 0)
+    out = D.gemm(dy, _mrec.LAYOUT_COL, x, _mrec.LAYOUT_COL, N, K, M, ones_out=db,
+                 out_dtype=torch.float32, split_k=split_k)
+    dz = _bf(dy)
     want_w = dz.T @ _bf(x)
     want_b = dz.sum(0)
     ok, worst = _close(out[:, :K], want_w, dz.abs().T @ _bf(x).abs(), out_bf16=False)
@@ -72,27 +70,73 @@ def test_gemm_weight_grad_col_col_ones_column(gpu, split_k):
     assert ok, worst
 
 
-def test_gemm_input_grad_row_col_with_zero_pad(gpu):
-    """dx = dZ W with W fp32 [N, K] read as a COL operand; columns >= K of the
-    padded output are exactly zero."""
+@pytest.mark.parametrize("masked", [False, True])
+def test_gemm_input_grad_row_col_with_zero_pad(gpu, masked):
+    """dx = dZ W with W fp32 [N, K] read as a COL operand (== W^T read as ROW);
+    columns >= K of the padded output are exactly zero; with an epilogue mask the
+    output is zero wherever the mask (a ReLU output) is <= 0."""
     from pytorchrec_amd import dense as D, _mrec
     M, N, K, KX = 513, 400, 429, 432
     g = torch.Generator().manual_seed(9)
-    dy = torch.randn(M, N, generator=g).to(torch.bfloat16).to(gpu)
-    y = torch.randn(M, N, generator=g).to(torch.bfloat16).to(gpu)
+    dy = D._bf16_rows(torch.randn(M, N, generator=g).to(torch.bfloat16).to(gpu))
     W = (torch.randn(N, K, generator=g) * 0.05).to(gpu)
+    mask = D._alloc(M, KX, torch.bfloat16, gpu)
+    mask.copy_(torch.relu(torch.randn(M, KX, generator=g)).to(torch.bfloat16))
+    mask[:, :3] = -0.0  # negative zero is not > 0
     wr, wt = D.weight_prep(W)
+    mk = mask if masked else None
     # B(k'=n, col=k) = W[n, k]: the row image read as COL, or W^T read as ROW
-    dx = D.gemm(dy, _mrec.LAYOUT_ROW, wr, _mrec.LAYOUT_COL, M, KX, N, a_mod=y,
-                a_mod_kind=_mrec.AMOD_RELU_MASK, b_cols=K)
-    dx2 = D.gemm(dy, _mrec.LAYOUT_ROW, wt, _mrec.LAYOUT_ROW, M, KX, N, a_mod=y,
-                 a_mod_kind=_mrec.AMOD_RELU_MASK, b_cols=K)
+    dx = D.gemm(dy, _mrec.LAYOUT_ROW, wr, _mrec.LAYOUT_COL, M, KX, N, b_cols=K, mask=mk)
+    dx2 = D.gemm(dy, _mrec.LAYOUT_ROW, wt, _mrec.LAYOUT_ROW, M, KX, N, b_cols=K, mask=mk)
     assert torch.equal(dx, dx2)
-    dz = _bf(dy) * (y.double() > 0)
-    want = dz @ _bf(W)
-    ok, worst = _close(dx[:, :K], want, dz.abs() @ _bf(W).abs())
+    want = _bf(dy) @ _bf(W)
+    mag = _bf(dy).abs() @ _bf(W).abs()
+    if masked:
+        keep = mask[:, :K].double() > 0
+        assert torch.all(dx[:, :K][~keep] == 0)
+        want = want * keep
+    ok, worst = _close(dx[:, :K], want, mag)
     assert ok, worst
     assert torch.all(dx[:, K:] == 0)
+
+
+def test_relu_output_consumed_twice_matches_torch(gpu):
+    """A ReLU output feeding two consumers: the gradients accumulate in autograd,
+    which voids the consumer's pre-mask stamp, so the producer masks itself."""
+    from pytorchrec_amd import dense as D
+    g = torch.Generator().manual_seed(3)
+    M, K, H = 384, 96, 64
+    x = torch.randn(M, K, generator=g)
+    W1, b1 = torch.randn(H, K, generator=g) * 0.1, torch.randn(H, generator=g) * 0.1
+    W2, W3 = torch.randn(8, H, generator=g) * 0.1, torch.randn(1, H, generator=g) * 0.1
+    ps = [t.to(gpu).requires_grad_() for t in (W1, b1, W2, W3)]
+    y = D.linear(x.to(gpu).to(torch.bfloat16), ps[0], ps[1], act="relu")
+    out = D.linear(y, ps[2], None).float().sum(1) + D.head(y, ps[3], None)
+    out.sum().backward()
+    rs = [t.double().requires_grad_() for t in (W1, b1, W2, W3)]
+    # forward on the bf16-rounded weight (what the GEMM multiplies) so no ReLU flips
+    w1 = rs[0] + (_bf(W1) - W1.double())
+    yr = torch.relu(_bf(x) @ w1.T + rs[1])
+    ((yr @ rs[2].T).sum(1) + (yr @ rs[3].T).reshape(-1)).sum().backward()
+    for got, want in zip(ps, rs):
+        np.testing.assert_allclose(got.grad.double().cpu().numpy(), want.grad.numpy(),
+                                   rtol=3e-2, atol=3e-2 * want.grad.abs().max().item())
+
+
+def test_head_backward_mask(gpu):
+    from pytorchrec_amd import _mrec, dense as D
+    g = torch.Generator().manual_seed(4)
+    B, H = 1000, 45
+    h = D._alloc(B, H, torch.bfloat16, gpu)
+    h.copy_(torch.randn(B, H, generator=g).to(torch.bfloat16))
+    dz = torch.randn(B, generator=g).to(gpu)
+    w = torch.randn(H, generator=g).to(gpu)
+    dh = D._alloc(B, H, torch.bfloat16, gpu)
+    _mrec.call("mrec_head_bwd", dz.data_ptr(), w.data_ptr(), B, H, h.data_ptr(), h.stride(0),
+               dh.data_ptr(), dh.stride(0), _mrec.stream_handle())
+    want = (dz[:, None] * w[None, :]) * (h.float() > 0)
+    assert torch.equal(dh, want.to(torch.bfloat16))
+    assert torch.all(dh.as_strided((B, dh.stride(0)), (dh.stride(0), 1))[:, H:] == 0)
 
 
 def test_mlp_matches_reference_golden_g6(gpu):

@@ -60,10 +60,10 @@ def main():
     cases = {
         "fwd": lambda: D.gemm(x, _mrec.LAYOUT_ROW, wr[:, :K], _mrec.LAYOUT_ROW, M, N, K, bias=b,
                               act=_mrec.ACT_RELU, out=y),
-        "dx": lambda: D.gemm(dy, _mrec.LAYOUT_ROW, wt, _mrec.LAYOUT_ROW, M, 432, N, a_mod=y,
-                             a_mod_kind=_mrec.AMOD_RELU_MASK, b_cols=K),
-        "dw": lambda: D.gemm(dy, _mrec.LAYOUT_COL, x, _mrec.LAYOUT_COL, N, K, M, a_mod=y,
-                             a_mod_kind=_mrec.AMOD_RELU_MASK, ones_out=db, out=dW),
+        "dx": lambda: D.gemm(dy, _mrec.LAYOUT_ROW, wt, _mrec.LAYOUT_ROW, M, 432, N, b_cols=K,
+                             mask=x),
+        "dw": lambda: D.gemm(dy, _mrec.LAYOUT_COL, x, _mrec.LAYOUT_COL, N, K, M, ones_out=db,
+                             out=dW),
         "prep": lambda: D.weight_prep(W),
     }
     xb = x[:, :K].contiguous()

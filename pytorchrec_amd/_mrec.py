@@ -20,7 +20,7 @@ import torch  # noqa: F401  (must precede the dlopen, see module docstring)
 LIB_DIR = os.path.join(os.path.dirname(os.path.abspath(__file__)), "lib")
 LIB_PATH = os.path.join(LIB_DIR, "libmrec.so")
 
-ABI_VERSION = 1
+ABI_VERSION = 2
 MAX_TABLES = 64
 BWD_MAX_BATCH = 8192
 

@@ -32,7 +32,7 @@
 extern "C" {
 #endif
 
-#define MREC_ABI_VERSION 2
+#define MREC_ABI_VERSION 3
 #define MREC_MAX_TABLES 64      /* tables per table bank / per call */
 #define MREC_BWD_MAX_BATCH 8192  /* lookups per table per plan/apply call */
 
@@ -81,6 +81,12 @@ typedef struct {
   const void *const *field_ptr; /* HOST [n_tables] of device pointers */
   mrec_dtype dtype;             /* MREC_I32 or MREC_I64 */
   int64_t stride;               /* elements between samples */
+  /* chunked addressing (0 = off): element b of a field sits at
+   * field_ptr[f][(b / chunk) * chunk_stride + b % chunk] — the owner-side view of
+   * an all-to-all receive buffer [source][table][slot] (see mrec_shard_*) */
+  int64_t chunk;
+  int64_t chunk_stride;
+  int32_t pad_negative; /* negative ids are padding slots: skipped, never flagged OOB */
 } mrec_ids;
 
 int mrec_abi_version(void);
@@ -178,6 +184,70 @@ mrec_status mrec_emb_bwd_apply(const mrec_table_bank *bank, int64_t batch, const
                                mrec_dtype x0_dtype, int64_t x0_ld, const float *dw,
                                mrec_bwd_mode mode, float lr, uint64_t seed,
                                const uint64_t *d_step, void *grad, mrec_stream stream);
+
+/*
+ * mrec_emb_bwd_apply with the per-lookup gradient rows given directly instead of
+ * derived from dx / dfm / dw (those must be NULL when g_occ is set): lookup b of
+ * table f contributes g_occ[idx * g_ld + 0 .. dim(+1)), idx = b when chunk == 0,
+ * else (b / chunk) * chunk_stride + f * chunk + b % chunk — the receive buffer of
+ * mrec_shard_lookup_grad rows after the reverse all-to-all (fp32, g_ld % 4 == 0).
+ * The owner side of a row-sharded table (SURVEY.md §8e backward).
+ */
+mrec_status mrec_emb_bwd_apply_given(const mrec_table_bank *bank, int64_t batch,
+                                     const void *workspace, size_t ws_bytes, const void *dx,
+                                     mrec_dtype dx_dtype, int64_t dx_ld, const float *dfm,
+                                     const float *fm_sum, const void *x0, mrec_dtype x0_dtype,
+                                     int64_t x0_ld, const float *dw, const float *g_occ,
+                                     int64_t g_ld, int64_t chunk, int64_t chunk_stride,
+                                     mrec_bwd_mode mode, float lr, uint64_t seed,
+                                     const uint64_t *d_step, void *grad, mrec_stream stream);
+
+/* ------------------------------------------------------------------------- */
+/* Row-sharded tables (one process per GPU, W = world size)                   */
+/* ------------------------------------------------------------------------- */
+/*
+ * Table f is split cyclically: id i lives on rank i % W as local row i / W.  Every
+ * exchange buffer has W equal parts of [n_tables][cap] slots (fixed capacity per
+ * (owner, table)), so the all-to-alls are equal-split, need no host sync and can be
+ * captured in a HIP graph.  Padding slots hold -1.  The reference has no sharding;
+ * this replaces the dense nn.Embedding of IModel._init_weights (FunkSVD.py:39-41)
+ * when a table does not fit, or should not be replicated on, one GPU.
+ */
+
+/*
+ * Sender side, forward.  For each table f and sample b (ascending, stable):
+ * owner = id % W, slot = rank of (b) among this table's ids with that owner;
+ *   send_ids[(owner * n_tables + f) * cap + slot] = id / W
+ *   pos[f * batch + b] = (owner * n_tables + f) * cap + slot
+ * Unused slots get -1.  An id outside [0, rows[f]) sets *d_oob_flag and gets
+ * pos = -1; a slot >= cap sets *d_overflow (the caller must raise) and pos = -1.
+ * One 1024-thread workgroup per table; requires (W + 1) * ceil(batch/64) <= 2048.
+ */
+mrec_status mrec_shard_bucketize(const mrec_ids *ids, int32_t n_tables, const int64_t *rows,
+                                 int64_t batch, int32_t world, int32_t cap, int32_t *send_ids,
+                                 int32_t *pos, int32_t *d_overflow, int32_t *d_oob_flag,
+                                 mrec_stream stream);
+
+/*
+ * Owner side, forward: rows_out[j, :] = local bank row of recv_ids[j] (table
+ * f = (j / cap) % n_tables), whole row_stride elements, zeros for padding (-1) or
+ * an out-of-shard id.  recv_ids / rows_out have world * n_tables * cap entries.
+ */
+mrec_status mrec_shard_gather(const mrec_table_bank *local, const int32_t *recv_ids,
+                              int32_t world, int32_t cap, void *rows_out, mrec_stream stream);
+
+/*
+ * Sender side, backward: the gradient row of every lookup, written where its
+ * embedding row came from (g_out[pos[f*batch+b] * g_ld + ...], fp32):
+ *   g[d] = dx[b, f*dim + d] + dfm[b] * (fm_sum[b, d] - x0[b, f*dim + d]),  g[dim] = dw[b]
+ * (same terms and NULL rules as mrec_emb_bwd_apply); lookups with pos < 0 skipped.
+ */
+mrec_status mrec_shard_lookup_grad(int64_t batch, int32_t n_tables, int32_t dim, int32_t has_w,
+                                   const int32_t *pos, const void *dx, mrec_dtype dx_dtype,
+                                   int64_t dx_ld, const float *dfm, const float *fm_sum,
+                                   const void *x0, mrec_dtype x0_dtype, int64_t x0_ld,
+                                   const float *dw, float *g_out, int64_t g_ld,
+                                   mrec_stream stream);
 
 /* ------------------------------------------------------------------------- */
 /* Dense towers: MFMA bf16 GEMM with fused epilogues                          */

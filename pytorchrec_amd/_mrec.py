@@ -20,7 +20,7 @@ import torch  # noqa: F401  (must precede the dlopen, see module docstring)
 LIB_DIR = os.path.join(os.path.dirname(os.path.abspath(__file__)), "lib")
 LIB_PATH = os.path.join(LIB_DIR, "libmrec.so")
 
-ABI_VERSION = 2
+ABI_VERSION = 3
 MAX_TABLES = 64
 BWD_MAX_BATCH = 8192
 
@@ -62,7 +62,10 @@ class TableBank(ctypes.Structure):
 class Ids(ctypes.Structure):
     _fields_ = [("field_ptr", ctypes.POINTER(ctypes.c_void_p)),
                 ("dtype", ctypes.c_int),
-                ("stride", ctypes.c_int64)]
+                ("stride", ctypes.c_int64),
+                ("chunk", ctypes.c_int64),
+                ("chunk_stride", ctypes.c_int64),
+                ("pad_negative", ctypes.c_int32)]
 
 
 class Operand(ctypes.Structure):
@@ -108,6 +111,16 @@ SIGNATURES = {
     "mrec_emb_bwd_apply": (ctypes.c_int, [_bank_p, _i64, _vp, ctypes.c_size_t, _vp, ctypes.c_int,
                                           _i64, _vp, _vp, _vp, ctypes.c_int, _i64, _vp,
                                           ctypes.c_int, _f32, ctypes.c_uint64, _vp, _vp, _vp]),
+    "mrec_emb_bwd_apply_given": (ctypes.c_int, [_bank_p, _i64, _vp, ctypes.c_size_t, _vp,
+                                                ctypes.c_int, _i64, _vp, _vp, _vp, ctypes.c_int,
+                                                _i64, _vp, _vp, _i64, _i64, _i64, ctypes.c_int,
+                                                _f32, ctypes.c_uint64, _vp, _vp, _vp]),
+    "mrec_shard_bucketize": (ctypes.c_int, [_ids_p, _i32, ctypes.POINTER(ctypes.c_int64), _i64,
+                                            _i32, _i32, _vp, _vp, _vp, _vp, _vp]),
+    "mrec_shard_gather": (ctypes.c_int, [_bank_p, _vp, _i32, _i32, _vp, _vp]),
+    "mrec_shard_lookup_grad": (ctypes.c_int, [_i64, _i32, _i32, _i32, _vp, _vp, ctypes.c_int,
+                                              _i64, _vp, _vp, _vp, ctypes.c_int, _i64, _vp, _vp,
+                                              _i64, _vp]),
     "mrec_gemm_workspace_size": (ctypes.c_size_t, [_i64, _i64, _i64, _i32]),
     "mrec_gemm": (ctypes.c_int, [_i64, _i64, _i64, _op_p, _op_p, _i64, _i64, _epi_p,
                                  _vp, ctypes.c_int, _i64, _i32, _vp, ctypes.c_size_t, _vp]),
@@ -211,7 +224,8 @@ class BankDesc:
 class IdsDesc:
     """Per-field id tensors (each [B] contiguous, or columns of a [B, F] tensor)."""
 
-    def __init__(self, fields, stacked: torch.Tensor | None = None):
+    def __init__(self, fields, stacked: torch.Tensor | None = None, chunk: int = 0,
+                 chunk_stride: int = 0, pad_negative: bool = False):
         if stacked is not None:
             n = stacked.shape[1]
             base = stacked.data_ptr()
@@ -233,7 +247,17 @@ class IdsDesc:
             stride = 1
         self._ptrs = (ctypes.c_void_p * n)(*ptrs)
         self.struct = Ids(ctypes.cast(self._ptrs, ctypes.POINTER(ctypes.c_void_p)),
-                          dtype_code(dt), int(stride))
+                          dtype_code(dt), int(stride), int(chunk), int(chunk_stride),
+                          int(bool(pad_negative)))
+
+    @classmethod
+    def exchange_view(cls, buf: torch.Tensor, n_tables: int, cap: int):
+        """Owner-side view of a receive buffer [W][n_tables][cap] (int32, -1 = pad):
+        table f's W*cap entries at buf[f*cap + (i // cap) * n_tables*cap + i % cap]."""
+        flat = buf.reshape(-1)
+        d = cls([flat[f * cap:] for f in range(n_tables)], chunk=cap,
+                chunk_stride=n_tables * cap, pad_negative=True)
+        return d
 
     def ref(self):
         return ctypes.byref(self.struct)

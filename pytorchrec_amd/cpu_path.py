@@ -63,7 +63,15 @@ def interact(bank, ids, dense: Optional[torch.Tensor], dense_w, bias, use_fm2: b
     w = _weight(bank)
     rows = _rows(bank, ids)
     g = [w.index_select(0, r) for r in rows]
-    v = torch.stack([x[:, :bank.dim] for x in g], dim=1).float()  # [B, F, D]
+    return interact_rows(g, bank.dim, dense, dense_w, bias, use_fm2, first_order, x0_cols,
+                         x0_dtype)
+
+
+def interact_rows(g: List[torch.Tensor], dim: int, dense: Optional[torch.Tensor], dense_w, bias,
+                  use_fm2: bool, first_order: bool, x0_cols: int, x0_dtype):
+    """The interaction on already-gathered rows g[f] = [B, >= dim(+1)] (also the
+    row-sharded CPU path, whose rows arrive through the exchange)."""
+    v = torch.stack([x[:, :dim] for x in g], dim=1).float()  # [B, F, D]
     B = v.shape[0]
     logit = torch.zeros(B, dtype=torch.float32)
     if bias is not None:
@@ -73,7 +81,7 @@ def interact(bank, ids, dense: Optional[torch.Tensor], dense_w, bias, use_fm2: b
     if use_fm2:
         logit = logit + fm2(v)
     if first_order:
-        logit = logit + torch.stack([x[:, bank.dim] for x in g], dim=1).float().sum(1)
+        logit = logit + torch.stack([x[:, dim] for x in g], dim=1).float().sum(1)
     if not x0_cols:
         return logit
     parts = [v.reshape(B, -1)]

@@ -41,7 +41,10 @@ struct BankArgs {
 struct IdsArgs {
   const void *ptr[MREC_MAX_TABLES];
   int64_t stride;
+  int64_t chunk;         // 0: element b at b * stride
+  int64_t chunk_stride;  // else at (b / chunk) * chunk_stride + b % chunk
   int32_t is64;
+  int32_t pad_negative;
 };
 
 mrec_status make_bank_args(const mrec_table_bank *bank, BankArgs *out, int *elem_bytes,
@@ -83,7 +86,7 @@ __device__ __forceinline__ uint32_t hash3(uint64_t seed, uint64_t row, uint32_t 
 }
 
 __device__ __forceinline__ int64_t load_id(const IdsArgs &ids, int f, int64_t b) {
-  const int64_t off = b * ids.stride;
+  const int64_t off = ids.chunk ? (b / ids.chunk) * ids.chunk_stride + b % ids.chunk : b * ids.stride;
   if (ids.is64) return static_cast<const int64_t *>(ids.ptr[f])[off];
   return static_cast<int64_t>(static_cast<const int32_t *>(ids.ptr[f])[off]);
 }

@@ -61,8 +61,14 @@ mrec_status make_ids_args(const mrec_ids *ids, int n_tables, IdsArgs *out) {
     out->ptr[f] = ids->field_ptr[f];
   }
   for (int f = n_tables; f < MREC_MAX_TABLES; ++f) out->ptr[f] = nullptr;
+  MREC_CHECK_ARG(ids->chunk >= 0 && (ids->chunk == 0 || ids->chunk_stride >= ids->chunk),
+                 "ids chunk / chunk_stride invalid");
+  MREC_CHECK_ARG(ids->chunk == 0 || ids->stride == 1, "chunked ids need stride 1");
   out->stride = ids->stride;
+  out->chunk = ids->chunk;
+  out->chunk_stride = ids->chunk_stride;
   out->is64 = ids->dtype == MREC_I64 ? 1 : 0;
+  out->pad_negative = ids->pad_negative ? 1 : 0;
   return MREC_OK;
 }
 

@@ -124,7 +124,7 @@ __global__ __launch_bounds__(kPlanThreads) void plan_kernel(BankArgs bank, IdsAr
       const int64_t id = load_id(ids, f, i);
       if (id >= 0 && id < static_cast<int64_t>(rows)) {
         key = static_cast<uint32_t>(id);
-      } else if (oob) {
+      } else if (oob && !(ids.pad_negative && id < 0)) {
         *oob = 1;
       }
     }
@@ -215,6 +215,12 @@ struct ApplyArgs {
   uint64_t seed;
   const uint64_t *d_step;
   void *grad;
+  // per-lookup gradient rows given directly (owner side of a sharded table):
+  // lookup b of table f -> g_occ[idx * g_ld + e], idx = chunked(b) + f * chunk
+  const float *g_occ;
+  int64_t g_ld;
+  int64_t chunk;
+  int64_t chunk_stride;
 };
 
 template <int EPL>
@@ -246,16 +252,31 @@ __device__ __forceinline__ void load_bf16xN(const uint16_t *p, float *v) {
 template <int EPL>
 __device__ __forceinline__ void add_lookup_grad(const ApplyArgs &a, int64_t b, int f, int D,
                                                 int e0, bool v_lane, bool w_lane, float *acc) {
+  if (a.g_occ) {
+    const int64_t idx = a.chunk ? (b / a.chunk) * a.chunk_stride + f * a.chunk + b % a.chunk : b;
+    const float *g = a.g_occ + idx * a.g_ld;
+    if (v_lane) {
+      float t[EPL];
+      load_f32xN<EPL>(g + e0, t);
+#pragma unroll
+      for (int j = 0; j < EPL; ++j) acc[j] += t[j];
+    } else if (w_lane) {
+      acc[0] += g[D];
+    }
+    return;
+  }
   if (v_lane) {
+    // per-lookup gradient first, then one add into the segment sum: the same
+    // arithmetic as mrec_shard_lookup_grad, so sharded and unsharded updates agree
     const int64_t col = static_cast<int64_t>(f) * D + e0;
     float g[EPL];
+#pragma unroll
+    for (int j = 0; j < EPL; ++j) g[j] = 0.f;
     if (a.dx) {
       if (a.dx_bf16)
         load_bf16xN<EPL>(static_cast<const uint16_t *>(a.dx) + b * a.dx_ld + col, g);
       else
         load_f32xN<EPL>(static_cast<const float *>(a.dx) + b * a.dx_ld + col, g);
-#pragma unroll
-      for (int j = 0; j < EPL; ++j) acc[j] += g[j];
     }
     if (a.dfm) {
       const float c = a.dfm[b];
@@ -266,8 +287,10 @@ __device__ __forceinline__ void add_lookup_grad(const ApplyArgs &a, int64_t b, i
       else
         load_f32xN<EPL>(static_cast<const float *>(a.x0) + b * a.x0_ld + col, v);
 #pragma unroll
-      for (int j = 0; j < EPL; ++j) acc[j] = fmaf(c, s[j] - v[j], acc[j]);
+      for (int j = 0; j < EPL; ++j) g[j] = fmaf(c, s[j] - v[j], g[j]);
     }
+#pragma unroll
+    for (int j = 0; j < EPL; ++j) acc[j] += g[j];
   } else if (w_lane && a.dw) {
     acc[0] += a.dw[b];
   }
@@ -442,6 +465,19 @@ mrec_status mrec_emb_bwd_apply(const mrec_table_bank *bank, int64_t batch, const
                                mrec_dtype x0_dtype, int64_t x0_ld, const float *dw,
                                mrec_bwd_mode mode, float lr, uint64_t seed,
                                const uint64_t *d_step, void *grad, mrec_stream stream) {
+  return mrec_emb_bwd_apply_given(bank, batch, workspace, ws_bytes, dx, dx_dtype, dx_ld, dfm,
+                                  fm_sum, x0, x0_dtype, x0_ld, dw, nullptr, 0, 0, 0, mode, lr,
+                                  seed, d_step, grad, stream);
+}
+
+mrec_status mrec_emb_bwd_apply_given(const mrec_table_bank *bank, int64_t batch,
+                                     const void *workspace, size_t ws_bytes, const void *dx,
+                                     mrec_dtype dx_dtype, int64_t dx_ld, const float *dfm,
+                                     const float *fm_sum, const void *x0, mrec_dtype x0_dtype,
+                                     int64_t x0_ld, const float *dw, const float *g_occ,
+                                     int64_t g_ld, int64_t chunk, int64_t chunk_stride,
+                                     mrec_bwd_mode mode, float lr, uint64_t seed,
+                                     const uint64_t *d_step, void *grad, mrec_stream stream) {
   BankArgs ba;
   int eb, lpr;
   mrec_status st = make_bank_args(bank, &ba, &eb, &lpr);
@@ -473,6 +509,13 @@ mrec_status mrec_emb_bwd_apply(const mrec_table_bank *bank, int64_t batch, const
                    "x0/fm_sum must be 16B aligned with 16B-multiple rows");
   }
   MREC_CHECK_ARG(dw == nullptr || ba.has_w, "dw given but bank has no w column");
+  if (g_occ) {
+    MREC_CHECK_ARG(!dx && !dfm && !dw, "g_occ excludes dx / dfm / dw");
+    MREC_CHECK_ARG(g_ld >= D + (ba.has_w ? 1 : 0) && g_ld % 4 == 0 &&
+                       (reinterpret_cast<uintptr_t>(g_occ) & 15) == 0,
+                   "g_occ rows must be 16B aligned, g_ld >= dim + has_w, g_ld % 4 == 0");
+    MREC_CHECK_ARG(chunk >= 0 && (chunk == 0 || chunk_stride >= F * chunk), "bad chunk");
+  }
   if (batch == 0) return MREC_OK;
   ApplyArgs a;
   a.dx = dx;
@@ -489,6 +532,10 @@ mrec_status mrec_emb_bwd_apply(const mrec_table_bank *bank, int64_t batch, const
   a.seed = seed;
   a.d_step = d_step;
   a.grad = grad;
+  a.g_occ = g_occ;
+  a.g_ld = g_ld;
+  a.chunk = chunk;
+  a.chunk_stride = chunk_stride;
   hipStream_t s = static_cast<hipStream_t>(stream);
   const int wpb = 256 / lpr;
   const dim3 grid(static_cast<unsigned>((batch + wpb - 1) / wpb), static_cast<unsigned>(F));

@@ -181,26 +181,31 @@ def _side_stream(device) -> torch.cuda.Stream:
     return st
 
 
-class _AsyncPlan:
-    """The sorted-segment plan launched on a side stream: it depends only on the
+class _AsyncPlanBase:
+    """A sorted-segment plan launched on a side stream: it depends only on the
     ids, so it runs concurrently with the interaction kernel and the MLP forward;
     the backward waits on its event before the apply kernel."""
 
-    def __init__(self, bank: EmbeddingBank, ids, batch: int):
-        cur = torch.cuda.current_stream(bank.weight.device)
-        side = _side_stream(bank.weight.device)
+    def __init__(self, device, launch, inputs):
+        cur = torch.cuda.current_stream(device)
+        side = _side_stream(device)
         side.wait_stream(cur)
         with torch.cuda.stream(side):
-            self.ws, self.ws_bytes = _plan(bank, ids, 0, batch, None)
+            self.ws, self.ws_bytes = launch()
             self.event = torch.cuda.Event()
             self.event.record(side)
         self.ws.record_stream(cur)
-        for t in ids:
+        for t in inputs:
             t.record_stream(side)
 
     def get(self):
         torch.cuda.current_stream(self.ws.device).wait_event(self.event)
         return self.ws, self.ws_bytes
+
+
+class _AsyncPlan(_AsyncPlanBase):
+    def __init__(self, bank: EmbeddingBank, ids, batch: int):
+        super().__init__(bank.weight.device, lambda: _plan(bank, ids, 0, batch, None), ids)
 
 
 def _apply(bank: EmbeddingBank, ws, ws_bytes, count, dx=None, dfm=None, fm_sum=None, x0=None,
@@ -406,6 +411,10 @@ def interact(bank: EmbeddingBank, ids: Sequence[torch.Tensor], dense: Optional[t
         raise ValueError("first_order needs a bank built with_first_order=True")
     if dense is not None:
         dense = dense.contiguous().float()
+    from pytorchrec_amd.sharding import ShardedEmbeddingBank, sharded_interact
+    if isinstance(bank, ShardedEmbeddingBank):
+        return sharded_interact(bank, ids, dense, dense_w, bias, fm2, first_order, int(x0_cols),
+                                x0_dtype)
     if not bank.weight.is_cuda:
         return cpu_path.interact(bank, ids, dense, dense_w, bias, fm2, first_order, x0_cols,
                                  x0_dtype)

@@ -16,7 +16,8 @@ from torch import Tensor
 from torch.nn import Linear, ModuleList
 
 from pytorchrec_amd import dense as dense_ops
-from pytorchrec_amd.embedding import EmbeddingBank, interact
+from pytorchrec_amd.embedding import interact
+from pytorchrec_amd.sharding import make_bank
 from pytorchrec_amd.feature_column import CategoricalColumn, NumericColumn
 from pytorchrec_amd.model.DeepFM import _CTRBase, _parse_layers, _round_up
 from pytorchrec_amd.model.layer.MLP import MLP
@@ -56,7 +57,7 @@ class DCNv2(_CTRBase):
     def _init_weights(self):
         dev = self.build_device
         F, D, n = len(self.sparse_columns), self.emb_size, len(self.dense_columns)
-        self.embeddings = EmbeddingBank([c.category_num for c in self.sparse_columns], D,
+        self.embeddings = make_bank([c.category_num for c in self.sparse_columns], D,
                                         with_first_order=False, dtype=self.emb_dtype, device=dev)
         self.deep_in = F * D + n
         self.x0_cols = _round_up(self.deep_in, 8)

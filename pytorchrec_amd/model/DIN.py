@@ -19,7 +19,8 @@ from torch import Tensor
 from torch.nn import Linear
 
 from pytorchrec_amd import dense as dense_ops
-from pytorchrec_amd.embedding import EmbeddingBank, gather
+from pytorchrec_amd.embedding import gather
+from pytorchrec_amd.sharding import make_bank
 from pytorchrec_amd.feature_column import CategoricalColumn
 from pytorchrec_amd.model.DeepFM import _parse_layers
 from pytorchrec_amd.model.IModel import IModel
@@ -64,7 +65,7 @@ class DIN(IModel):
     def _init_weights(self):
         dev = self.build_device
         D = self.emb_size
-        self.embeddings = EmbeddingBank([self.iid_column.category_num,
+        self.embeddings = make_bank([self.iid_column.category_num,
                                          self.cid_column.category_num], D,
                                         with_first_order=False, dtype=self.emb_dtype, device=dev)
         E = 2 * D

@@ -26,7 +26,8 @@ from torch import Tensor
 from torch.nn import Linear, Parameter
 
 from pytorchrec_amd import dense as dense_ops
-from pytorchrec_amd.embedding import EmbeddingBank, interact
+from pytorchrec_amd.embedding import interact
+from pytorchrec_amd.sharding import make_bank
 from pytorchrec_amd.feature_column import CategoricalColumn, NumericColumn
 from pytorchrec_amd.model.IModel import IModel
 from pytorchrec_amd.model.layer.MLP import MLP
@@ -98,7 +99,7 @@ class FM(_CTRBase):
         super().__init__(**kwargs)
 
     def _init_weights(self):
-        self.embeddings = EmbeddingBank([c.category_num for c in self.sparse_columns],
+        self.embeddings = make_bank([c.category_num for c in self.sparse_columns],
                                         self.emb_size, with_first_order=True,
                                         dtype=self.emb_dtype, device=self.build_device)
         n = len(self.dense_columns)
@@ -142,7 +143,7 @@ class DeepFM(_CTRBase):
     def _init_weights(self):
         dev = self.build_device
         F, D, n = len(self.sparse_columns), self.emb_size, len(self.dense_columns)
-        self.embeddings = EmbeddingBank([c.category_num for c in self.sparse_columns], D,
+        self.embeddings = make_bank([c.category_num for c in self.sparse_columns], D,
                                         with_first_order=True, dtype=self.emb_dtype, device=dev)
         self.dense_weight = Parameter(torch.randn(n, device=dev) * 0.01) if n else None
         self.global_bias = Parameter(torch.zeros(1, device=dev))

@@ -122,7 +122,16 @@ class IModel(Module, IWithArguments, ABC):
 
     def _configure_embedding_update(self, optimizer: Optimizer):
         """Fuse the table update into the backward when that is exactly dense SGD."""
+        from pytorchrec_amd.sharding import ShardedEmbeddingBank
         for bank in self.embedding_banks():
+            if isinstance(bank, ShardedEmbeddingBank):
+                g0 = optimizer.param_groups[0]
+                if not (isinstance(optimizer, torch.optim.SGD) and g0.get("momentum", 0) == 0
+                        and not g0.get("nesterov", False) and not g0.get("maximize", False)):
+                    raise NotImplementedError("row-sharded tables train with the fused SGD "
+                                              "update only (torch.optim.SGD, no momentum)")
+                bank.use_fused_sgd(g0["lr"], g0)
+                continue
             group = None
             for g in optimizer.param_groups:
                 if any(p is bank.weight for p in g["params"]):
@@ -135,6 +144,36 @@ class IModel(Module, IWithArguments, ABC):
             elif group is not None or bank.update != "sgd":
                 bank.use_dense_grad()
 
+    # -- data parallel (one process per GPU) ------------------------
+    def distribute(self, comm):
+        """Make this replica data-parallel over ``comm`` (a sharding.ShardComm):
+        rank 0's dense parameters are broadcast now, and every train_step averages
+        the dense gradients over the ranks (one flat all-reduce) before the
+        optimizer step.  Row-sharded tables exchange rows themselves."""
+        self.dp_comm = comm
+        with torch.no_grad():
+            for p in self._dp_params():
+                comm.broadcast_(p.data)
+        return self
+
+    def _dp_params(self):
+        from pytorchrec_amd.sharding import ShardedEmbeddingBank
+        sharded = {id(b.weight) for b in self.embedding_banks()
+                   if isinstance(b, ShardedEmbeddingBank)}
+        return [p for p in self.parameters() if p.requires_grad and id(p) not in sharded]
+
+    def _allreduce_dense_grads(self):
+        params = [p for p in self._dp_params() if p.grad is not None]
+        if not params:
+            return
+        flat = torch.cat([p.grad.reshape(-1) for p in params])
+        self.dp_comm.allreduce_mean_(flat)
+        o = 0
+        for p in params:
+            n = p.grad.numel()
+            p.grad.copy_(flat[o:o + n].view_as(p.grad))
+            o += n
+
     # -- steps ------------------------------------------------------------------
     def train_step(self, data: Dict):
         self.train()
@@ -143,6 +182,8 @@ class IModel(Module, IWithArguments, ABC):
         loss = self.compiled_loss(prediction, target)
         self.compiled_optimizers.zero_grad()
         loss.backward()
+        if getattr(self, "dp_comm", None) is not None and self.dp_comm.world > 1:
+            self._allreduce_dense_grads()
         self.compiled_optimizers.step(closure=None)
         return {"loss": loss}
 

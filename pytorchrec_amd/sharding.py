@@ -1,0 +1,438 @@
+"""Row-sharded embedding tables across the GPUs of a node.
+
+One process per GPU.  Table f is split cyclically: global id ``i`` lives on rank
+``i % W`` as local row ``i // W`` (cyclic, so Zipf-hot rows spread over owners).
+The dense tower stays data-parallel.  One training step of a sharded bank:
+
+  sender  bucketize ids by owner into fixed-capacity slots   mrec_shard_bucketize
+          all_to_all ids                                     (equal split, RCCL)
+  owner   gather the requested rows                          mrec_shard_gather
+          all_to_all rows back                               (equal split)
+  sender  interaction on the received rows                   mrec_interact_fwd
+  ---- backward ----
+  sender  per-lookup gradient rows into the same slots       mrec_shard_lookup_grad
+          all_to_all gradients to the owners                 (equal split)
+  owner   sorted-segment plan over the received ids          mrec_emb_bwd_plan (chunked view)
+          fixed-order segment sums + fused SGD               mrec_emb_bwd_apply_given
+
+Every exchange buffer is ``[W][n_tables][cap]`` slots, so all collectives are
+equal-split: no host sync, capturable in a HIP graph.  A slot overflow (more than
+``cap`` ids of one table for one owner in a rank's batch) is flagged on the
+device and raised, never dropped silently.  The loss is the mean over each rank's
+batch, so the global objective is the mean of the ranks' losses: dense gradients
+are all-reduced and averaged, and owners scale the summed row gradients by 1/W.
+
+The reference has no sharding (it keeps one dense ``nn.Embedding`` per field,
+FunkSVD.py:39-41); the per-field semantics (gather, duplicate-summing backward,
+SGD) are unchanged.  The same protocol runs on CPU tensors over ``gloo`` (the
+multi-process tests), with torch ops in place of the kernels.
+"""
+from __future__ import annotations
+
+import contextlib
+import ctypes
+from typing import List, Optional, Sequence
+
+import torch
+import torch.distributed as dist
+
+from pytorchrec_amd import _mrec
+from pytorchrec_amd.embedding import EmbeddingBank, _AsyncPlanBase, _side_stream, _trigger
+
+
+# ----------------------------------------------------------------------------
+# communicator
+# ----------------------------------------------------------------------------
+
+
+class ShardComm:
+    """Equal-split all-to-all and mean all-reduce on a ``torch.distributed`` group
+    (RCCL for GPU tensors, gloo for CPU tensors).  ``world == 1`` needs no group."""
+
+    def __init__(self, group=None, world: Optional[int] = None, rank: Optional[int] = None):
+        self.group = group
+        if world is None:
+            world = dist.get_world_size(group) if dist.is_initialized() else 1
+        if rank is None:
+            rank = dist.get_rank(group) if dist.is_initialized() else 0
+        self.world, self.rank = int(world), int(rank)
+
+    def exchange(self, send: torch.Tensor) -> torch.Tensor:
+        """``out[s]`` = part ``rank`` of rank s's ``send`` (dim 0 split in W equal parts)."""
+        if self.world == 1:
+            return send
+        send = send.contiguous()
+        out = torch.empty_like(send)
+        dist.all_to_all_single(out, send, group=self.group)
+        return out
+
+    def allreduce_mean_(self, flat: torch.Tensor) -> torch.Tensor:
+        if self.world > 1:
+            dist.all_reduce(flat, group=self.group)
+            flat.div_(self.world)
+        return flat
+
+    def broadcast_(self, t: torch.Tensor, src: int = 0) -> torch.Tensor:
+        if self.world > 1:
+            dist.broadcast(t, src, group=self.group)
+        return t
+
+
+def default_cap(batch: int, world: int) -> int:
+    """Slots per (owner, table): every id fits at W <= 2; at larger W twice the
+    uniform share (hot Zipf owners reach ~1.6x at W = 8), bounded so the owner's
+    per-table plan stays within MREC_BWD_MAX_BATCH keys."""
+    cap = min(int(batch), _mrec.BWD_MAX_BATCH // int(world))
+    return max(1, cap)
+
+
+# ----------------------------------------------------------------------------
+# the sharded bank
+# ----------------------------------------------------------------------------
+
+
+class ShardedEmbeddingBank(EmbeddingBank):
+    """This rank's shard of F row-sharded tables (same row layout as EmbeddingBank).
+
+    ``category_nums`` are the GLOBAL row counts; local table f holds rows
+    ``rank, rank + W, ...`` of global table f.  The update is always the fused
+    row-sparse SGD (the table gradient never exists)."""
+
+    def __init__(self, category_nums: Sequence[int], dim: int, comm: ShardComm,
+                 with_first_order: bool = False, dtype: torch.dtype = torch.float32,
+                 cap: Optional[int] = None, max_batch: int = 4096, device=None):
+        W, r = comm.world, comm.rank
+        local = [(int(n) - r + W - 1) // W if int(n) > r else 0 for n in category_nums]
+        super().__init__([max(n, 0) for n in local], dim, with_first_order, dtype,
+                         update="sgd", device=device)
+        self.global_rows = [int(n) for n in category_nums]
+        self.comm = comm
+        self.world, self.rank = W, r
+        self.cap = int(cap) if cap is not None else default_cap(max_batch, W)
+        if W * self.cap > _mrec.BWD_MAX_BATCH:
+            raise ValueError(f"world * cap = {W * self.cap} exceeds MREC_BWD_MAX_BATCH")
+        self._flags = None  # device int32 [2] = {overflow, oob}, sticky until checked
+        self._global_rows_arr = (ctypes.c_int64 * len(self.global_rows))(*self.global_rows)
+
+    @property
+    def g_ld(self) -> int:
+        return (self.dim + (1 if self.has_w else 0) + 3) // 4 * 4
+
+    def flags(self) -> torch.Tensor:
+        if self._flags is None or self._flags.device != self.weight.device:
+            self._flags = torch.zeros(2, dtype=torch.int32, device=self.weight.device)
+        return self._flags
+
+    def check_flags(self):
+        """Raise if any exchange since the last check overflowed its slots or saw an
+        out-of-range id (syncs once)."""
+        f = self.flags()
+        ov, oob = (int(x) for x in f.tolist())
+        f.zero_()
+        if ov:  # (overflowed lookups also read slot -1, which sets the OOB flag)
+            raise RuntimeError(f"row-sharded exchange overflow: more than cap={self.cap} ids of "
+                               "one table for one owner in a batch; raise cap")
+        if oob:
+            raise IndexError("index out of range in self")
+
+    # -- global <-> shard ------------------------------------------------------
+    @torch.no_grad()
+    def load_global_(self, tables: Sequence[torch.Tensor]):
+        """Fill the shard from full global tables (each [rows_f, >= dim(+1)])."""
+        for f, t in enumerate(tables):
+            n = self.category_nums[f]
+            if n == 0:
+                continue
+            src = t[self.rank::self.world]
+            o = self.row_offset[f]
+            cols = self.dim + (1 if self.has_w else 0)
+            self.weight[o:o + n, :cols].copy_(src[:, :cols].to(self.weight.dtype))
+        return self
+
+    def local_rows_of(self, f: int) -> torch.Tensor:
+        """Global ids of this shard's rows of table f."""
+        return torch.arange(self.rank, self.global_rows[f], self.world)
+
+    def extra_repr(self) -> str:
+        return super().extra_repr() + f", world={self.world}, rank={self.rank}, cap={self.cap}"
+
+
+_ACTIVE: List[tuple] = []
+
+
+@contextlib.contextmanager
+def sharded_tables(comm: ShardComm, cap: Optional[int] = None, max_batch: int = 4096):
+    """Models built inside this context get ``ShardedEmbeddingBank`` tables
+    (no rank ever materialises a full table)."""
+    _ACTIVE.append((comm, cap, max_batch))
+    try:
+        yield
+    finally:
+        _ACTIVE.pop()
+
+
+def make_bank(category_nums, dim, with_first_order=False, dtype=torch.float32, device=None):
+    """EmbeddingBank factory used by the models' ``_init_weights``."""
+    if _ACTIVE:
+        comm, cap, max_batch = _ACTIVE[-1]
+        return ShardedEmbeddingBank(category_nums, dim, comm, with_first_order, dtype, cap,
+                                    max_batch, device)
+    return EmbeddingBank(category_nums, dim, with_first_order=with_first_order, dtype=dtype,
+                         device=device)
+
+
+# ----------------------------------------------------------------------------
+# GPU phases (each one libmrec call; usable on their own, e.g. to drive several
+# simulated ranks in one process)
+# ----------------------------------------------------------------------------
+
+
+def shard_bucketize(bank: ShardedEmbeddingBank, ids: Sequence[torch.Tensor]):
+    """-> (send_ids [W, F, cap] int32, pos [F, B] int32)."""
+    F, W, cap = bank.n_tables, bank.world, bank.cap
+    B = ids[0].shape[0]
+    dev = bank.weight.device
+    send = torch.empty(W, F, cap, dtype=torch.int32, device=dev)
+    pos = torch.empty(F, B, dtype=torch.int32, device=dev)
+    fl = bank.flags()
+    _mrec.call("mrec_shard_bucketize", _mrec.IdsDesc(ids).ref(), F, bank._global_rows_arr, B, W,
+               cap, send.data_ptr(), pos.data_ptr(), fl.data_ptr(), fl.data_ptr() + 4,
+               _mrec.stream_handle())
+    return send, pos
+
+
+def shard_gather(bank: ShardedEmbeddingBank, recv_ids: torch.Tensor) -> torch.Tensor:
+    """Owner: rows of the received ids -> [W*F*cap, row_stride] (bank dtype)."""
+    n = recv_ids.numel()
+    out = torch.empty(n, bank.row_stride, dtype=bank.weight.dtype, device=bank.weight.device)
+    _mrec.call("mrec_shard_gather", bank.desc().ref(), recv_ids.data_ptr(), bank.world, bank.cap,
+               out.data_ptr(), _mrec.stream_handle())
+    return out
+
+
+def remote_desc(bank: ShardedEmbeddingBank, rows_recv: torch.Tensor) -> _mrec.BankDesc:
+    """The received rows seen as a bank: F tables over the same buffer, each table's
+    'id' being the slot index (pos)."""
+    F = bank.n_tables
+    n = rows_recv.shape[0]
+    return _mrec.BankDesc(rows_recv, [0] * F, [n] * F, bank.dim, bank.has_w)
+
+
+def shard_interact(bank: ShardedEmbeddingBank, rows_recv: torch.Tensor, pos: torch.Tensor,
+                   dense, dense_w, bias, fm2: bool, first_order: bool, x0_cols: int, x0_dtype):
+    """Sender: mrec_interact_fwd over the received rows (ids = slots) ->
+    (x0 or None, logit, fm_sum or None)."""
+    B = pos.shape[1]
+    dev = bank.weight.device
+    rdesc = remote_desc(bank, rows_recv)
+    n_dense = 0 if dense is None else dense.shape[1]
+    flags = (_mrec.INTERACT_FM2 if fm2 else 0) | (_mrec.INTERACT_FIRST_ORDER if first_order else 0)
+    x0 = torch.empty(B, x0_cols, dtype=x0_dtype, device=dev) if x0_cols else None
+    logit = torch.empty(B, dtype=torch.float32, device=dev)
+    fm_sum = torch.empty(B, bank.dim, dtype=torch.float32, device=dev) if fm2 else None
+    fl = bank.flags()
+    if B:
+        _mrec.call("mrec_interact_fwd", rdesc.ref(),
+                   _mrec.IdsDesc([pos[f] for f in range(bank.n_tables)]).ref(), B,
+                   _mrec.ptr(dense), n_dense, dense.stride(0) if dense is not None else 0,
+                   _mrec.ptr(dense_w), _mrec.ptr(bias), flags, _mrec.ptr(x0),
+                   _mrec.dtype_code(x0_dtype), x0.stride(0) if x0 is not None else 0,
+                   int(x0_cols), logit.data_ptr(), _mrec.ptr(fm_sum), fl.data_ptr() + 4,
+                   _mrec.stream_handle())
+    return x0, logit, fm_sum
+
+
+def owner_plan(bank: ShardedEmbeddingBank, recv_ids: torch.Tensor):
+    """Sorted-segment plan of the owner's received ids (padding skipped)."""
+    F, W, cap = bank.n_tables, bank.world, bank.cap
+    n = W * cap
+    wsb = _mrec.lib().mrec_emb_bwd_workspace_size(F, n)
+    ws = torch.empty(wsb, dtype=torch.uint8, device=bank.weight.device)
+    desc = _mrec.IdsDesc.exchange_view(recv_ids, F, cap)
+    fl = bank.flags()
+    _mrec.call("mrec_emb_bwd_plan", bank.desc().ref(), desc.ref(), n, ws.data_ptr(), wsb,
+               fl.data_ptr() + 4, bank.step_counter().data_ptr(), _mrec.stream_handle())
+    return ws, wsb
+
+
+class _AsyncOwnerPlan(_AsyncPlanBase):
+    def __init__(self, bank: ShardedEmbeddingBank, recv_ids: torch.Tensor):
+        super().__init__(bank.weight.device, lambda: owner_plan(bank, recv_ids), [recv_ids])
+
+
+def shard_lookup_grad(bank: ShardedEmbeddingBank, pos: torch.Tensor, batch: int, dx=None,
+                      dfm=None, fm_sum=None, x0=None, dw=None) -> torch.Tensor:
+    """Sender: per-lookup gradient rows at their slots -> [W*F*cap, g_ld] fp32."""
+    F, W, cap = bank.n_tables, bank.world, bank.cap
+    g = torch.empty(W * F * cap, bank.g_ld, dtype=torch.float32, device=bank.weight.device)
+    _mrec.call("mrec_shard_lookup_grad", batch, F, bank.dim, int(bank.has_w), pos.data_ptr(),
+               _mrec.ptr(dx), _mrec.dtype_code(dx.dtype) if dx is not None else _mrec.F32,
+               dx.stride(0) if dx is not None else 0, _mrec.ptr(dfm), _mrec.ptr(fm_sum),
+               _mrec.ptr(x0), _mrec.dtype_code(x0.dtype) if x0 is not None else _mrec.F32,
+               x0.stride(0) if x0 is not None else 0, _mrec.ptr(dw), g.data_ptr(), g.shape[1],
+               _mrec.stream_handle())
+    return g
+
+
+def owner_apply(bank: ShardedEmbeddingBank, plan, g_recv: torch.Tensor, lr: float):
+    """Owner: fixed-order segment sums of the received gradient rows + SGD(lr)."""
+    ws, wsb = plan
+    F, W, cap = bank.n_tables, bank.world, bank.cap
+    mode = _mrec.BWD_SGD_SR if (bank.stochastic_rounding and
+                                bank.weight.dtype == torch.bfloat16) else _mrec.BWD_SGD
+    _mrec.call("mrec_emb_bwd_apply_given", bank.desc().ref(), W * cap, ws.data_ptr(), wsb,
+               None, _mrec.F32, 0, None, None, None, _mrec.F32, 0, None, g_recv.data_ptr(),
+               g_recv.shape[1], cap, F * cap, mode, float(lr), bank.next_seed(),
+               bank.step_counter().data_ptr(), None, _mrec.stream_handle())
+
+
+# ----------------------------------------------------------------------------
+# autograd (GPU)
+# ----------------------------------------------------------------------------
+
+
+class _ShardedInteractFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, dense_w, bias, trigger, bank: ShardedEmbeddingBank, ids, dense, fm2: bool,
+                first_order: bool, x0_cols: int, x0_dtype):
+        B = ids[0].shape[0]
+        dev = bank.weight.device
+        comm = bank.comm
+        send_ids, pos = shard_bucketize(bank, ids)
+        recv_ids = comm.exchange(send_ids)
+        plan = _AsyncOwnerPlan(bank, recv_ids) if trigger is not None else None
+        rows_recv = comm.exchange(shard_gather(bank, recv_ids))
+        x0, logit, fm_sum = shard_interact(bank, rows_recv, pos, dense, dense_w, bias, fm2,
+                                           first_order, x0_cols, x0_dtype)
+        if bank.check_ids:
+            bank.check_flags()
+        ctx.bank, ctx.B, ctx.plan = bank, B, plan
+        ctx.fm2, ctx.first_order = fm2, first_order
+        ctx.has_dense_w, ctx.has_bias = dense_w is not None, bias is not None
+        ctx.save_for_backward(x0, fm_sum, dense, pos)
+        if x0 is None:
+            return logit
+        return x0, logit
+
+    @staticmethod
+    def backward(ctx, *grads):
+        if len(grads) == 2:
+            dx0, dlogit = grads
+        else:
+            dx0, dlogit = None, grads[0]
+        x0, fm_sum, dense, pos = ctx.saved_tensors
+        bank = ctx.bank
+        if dlogit is not None:
+            dlogit = dlogit.contiguous().float()
+        dfm = dlogit if (ctx.fm2 and dlogit is not None) else None
+        dw = dlogit if (ctx.first_order and dlogit is not None) else None
+        if dx0 is not None:
+            dx0 = dx0.contiguous()
+        if ctx.plan is not None:
+            g_send = shard_lookup_grad(bank, pos, ctx.B, dx=dx0, dfm=dfm, fm_sum=fm_sum,
+                                       x0=x0 if dfm is not None else None, dw=dw)
+            g_recv = bank.comm.exchange(g_send)
+            owner_apply(bank, ctx.plan.get(), g_recv, bank.current_lr() / bank.world)
+        g_dense_w = g_bias = None
+        if dlogit is not None and (ctx.has_dense_w or ctx.has_bias):
+            from pytorchrec_amd.dense import colsum
+            X = dense if (ctx.has_dense_w and dense is not None) else None
+            gw, gb = colsum(dlogit, X, want_total=ctx.has_bias)
+            g_dense_w = gw if X is not None else None
+            g_bias = gb
+        return g_dense_w, g_bias, None, None, None, None, None, None, None, None
+
+
+# ----------------------------------------------------------------------------
+# CPU restatement of the same protocol (gloo; the multi-process tests)
+# ----------------------------------------------------------------------------
+
+
+def cpu_bucketize(bank: ShardedEmbeddingBank, ids: Sequence[torch.Tensor]):
+    F, W, cap = bank.n_tables, bank.world, bank.cap
+    B = ids[0].shape[0]
+    send = torch.full((W, F, cap), -1, dtype=torch.int32)
+    pos = torch.empty(F, B, dtype=torch.int32)
+    for f, t in enumerate(ids):
+        t = t.long()
+        if t.numel() and (int(t.min()) < 0 or int(t.max()) >= bank.global_rows[f]):
+            raise IndexError("index out of range in self")
+        owner = t % W
+        order = torch.argsort(owner, stable=True)
+        counts = torch.bincount(owner, minlength=W)
+        starts = torch.cumsum(counts, 0) - counts
+        slot = torch.empty(B, dtype=torch.long)
+        slot[order] = torch.arange(B) - starts[owner[order]]
+        if B and int(slot.max()) >= cap:
+            raise RuntimeError(f"row-sharded exchange overflow: more than cap={cap} ids of one "
+                               "table for one owner in a batch; raise cap")
+        send[owner, f, slot] = (t // W).to(torch.int32)
+        pos[f] = ((owner * F + f) * cap + slot).to(torch.int32)
+    return send, pos
+
+
+def _cpu_owner_rows(bank: ShardedEmbeddingBank, recv: torch.Tensor) -> torch.Tensor:
+    F, cap = bank.n_tables, bank.cap
+    flat = recv.reshape(-1).long()
+    f_of = (torch.arange(flat.numel()) // cap) % F
+    offs = torch.tensor(bank.row_offset, dtype=torch.long)[f_of]
+    valid = flat >= 0
+    rows = torch.zeros(flat.numel(), bank.row_stride, dtype=bank.weight.dtype)
+    rows[valid] = bank.weight.detach()[offs[valid] + flat[valid]]
+    return rows, offs, valid
+
+
+class _CpuExchangeRowsFn(torch.autograd.Function):
+    """forward: owner rows -> all_to_all -> rows at the sender's slots;
+    backward: slot gradients -> reverse all_to_all -> owner SGD (lr / W)."""
+
+    @staticmethod
+    def forward(ctx, trigger, bank: ShardedEmbeddingBank, recv):
+        rows, offs, valid = _cpu_owner_rows(bank, recv)
+        ctx.bank, ctx.recv, ctx.offs, ctx.valid = bank, recv, offs, valid
+        return bank.comm.exchange(rows.float())
+
+    @staticmethod
+    def backward(ctx, g):
+        bank = ctx.bank
+        g_recv = bank.comm.exchange(g.contiguous())
+        flat = ctx.recv.reshape(-1).long()
+        idx = (ctx.offs + flat)[ctx.valid]
+        cols = bank.dim + (1 if bank.has_w else 0)
+        upd = g_recv[ctx.valid][:, :cols].to(bank.weight.dtype)
+        with torch.no_grad():
+            w = bank.weight
+            acc = torch.zeros(w.shape[0], cols, dtype=torch.float32)
+            acc.index_add_(0, idx, upd.float())  # fixed (slot) order
+            touched = torch.zeros(w.shape[0], dtype=torch.bool)
+            touched[idx] = True
+            lr = bank.current_lr() / bank.world
+            w[touched, :cols] = (w[touched, :cols].float() - lr * acc[touched]).to(w.dtype)
+        return None, None, None
+
+
+def cpu_sharded_interact(bank: ShardedEmbeddingBank, ids, dense, dense_w, bias, use_fm2: bool,
+                         first_order: bool, x0_cols: int, x0_dtype):
+    from pytorchrec_amd import cpu_path
+    send, pos = cpu_bucketize(bank, ids)
+    recv = bank.comm.exchange(send)
+    trig = torch.zeros(0, requires_grad=True) if torch.is_grad_enabled() else None
+    rows = _CpuExchangeRowsFn.apply(trig, bank, recv)
+    g = [rows.index_select(0, pos[f].long()) for f in range(bank.n_tables)]
+    return cpu_path.interact_rows(g, bank.dim, dense, dense_w, bias, use_fm2, first_order,
+                                  x0_cols, x0_dtype)
+
+
+def sharded_interact(bank: ShardedEmbeddingBank, ids, dense, dense_w, bias, fm2: bool,
+                     first_order: bool, x0_cols: int, x0_dtype):
+    if not bank.weight.is_cuda:
+        return cpu_sharded_interact(bank, ids, dense, dense_w, bias, fm2, first_order, x0_cols,
+                                    x0_dtype)
+    trigger = _trigger(bank)
+    return _ShardedInteractFn.apply(dense_w, bias, trigger, bank, ids, dense, fm2, first_order,
+                                    int(x0_cols), x0_dtype)
+
+
+__all__ = ["ShardComm", "ShardedEmbeddingBank", "sharded_tables", "make_bank", "default_cap",
+           "sharded_interact", "shard_bucketize", "shard_gather", "shard_lookup_grad",
+           "owner_plan", "owner_apply", "remote_desc", "shard_interact", "cpu_bucketize"]

@@ -1,0 +1,153 @@
+"""Row-sharded tables + data-parallel dense tower over world_size 2 (gloo, CPU).
+
+The N>1 path of SURVEY.md §8e, run as two processes on the CPU with the same
+exchange protocol (bucketize -> all_to_all ids -> owner gather -> all_to_all rows;
+backward: slot gradients -> reverse all_to_all -> owner SGD / W; dense grads
+all-reduced and averaged).  Checked against ONE process training the unsharded
+model on the concatenation of both ranks' batches: same loss, same dense
+parameters, and every shard equal to its rows of the single-process tables.
+"""
+import os
+import socket
+import tempfile
+
+import numpy as np
+import pytest
+import torch
+
+from conftest import ROOT
+
+F_ROWS = [50, 7, 129, 1]   # includes a single-row table (empty on rank 1)
+DIM, N_DENSE, B, LAYERS, LR = 8, 3, 32, (16, 8), 0.05
+
+
+def _free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def _columns():
+    from pytorchrec_amd.feature_column import CategoricalColumnWithIdentity, NumericColumn
+    sparse = [CategoricalColumnWithIdentity(n, f"c_c_C{i}") for i, n in enumerate(F_ROWS)]
+    dense = [NumericColumn(f"c_n_I{i}") for i in range(N_DENSE)]
+    label = CategoricalColumnWithIdentity(2, "label")
+    return sparse, dense, label
+
+
+def _batch(seed, n):
+    g = torch.Generator().manual_seed(seed)
+    data = {f"c_c_C{i}": torch.randint(0, r, (n,), generator=g, dtype=torch.int32)
+            for i, r in enumerate(F_ROWS)}
+    for i in range(N_DENSE):
+        data[f"c_n_I{i}"] = torch.rand(n, generator=g)
+    data["label"] = (torch.rand(n, generator=g) < 0.3).to(torch.int32)
+    return data
+
+
+def _reference_model():
+    from pytorchrec_amd.model import DeepFM
+    sparse, dense, label = _columns()
+    torch.manual_seed(0)
+    return DeepFM(sparse, dense, label, emb_size=DIM, layers=LAYERS, random_seed=7)
+
+
+def _train(model, batches):
+    from pytorchrec_amd.loss import BCEWithLogitsLoss
+    opt = torch.optim.SGD(model.get_parameters(), lr=LR)
+    model.compile(opt, BCEWithLogitsLoss(), [], torch.device("cpu"))
+    return [float(model.train_step(b)["loss"].detach()) for b in batches]
+
+
+def _worker(rank, world, port, out_dir, steps):
+    import torch.distributed as dist
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from pytorchrec_amd.model import DeepFM
+        from pytorchrec_amd.sharding import ShardComm, sharded_tables
+        comm = ShardComm()
+        ref = _reference_model()  # same init on every rank: the global tables to shard
+        sparse, dense, label = _columns()
+        with sharded_tables(comm, cap=B):
+            model = DeepFM(sparse, dense, label, emb_size=DIM, layers=LAYERS, random_seed=7)
+        tables = [ref.embeddings.weight[o:o + n] for o, n in
+                  zip(ref.embeddings.row_offset, ref.embeddings.category_nums)]
+        model.embeddings.load_global_(tables)
+        dense_sd = {k: v for k, v in ref.state_dict().items() if not k.startswith("embeddings")}
+        model.load_state_dict(dense_sd, strict=False)
+        model.distribute(comm)
+        batches = []
+        for s in range(steps):
+            full = _batch(100 + s, B * world)
+            batches.append({k: v[rank * B:(rank + 1) * B] for k, v in full.items()})
+        losses = _train(model, batches)
+        out = {"losses": np.array(losses)}
+        for k, v in model.state_dict().items():
+            out[k.replace(".", "__")] = v.detach().numpy()
+        np.savez(os.path.join(out_dir, f"rank{rank}.npz"), **out)
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("steps", [2])
+def test_two_rank_sharded_deepfm_matches_single_process(steps):
+    import torch.multiprocessing as mp
+    world = 2
+    with tempfile.TemporaryDirectory() as d:
+        mp.spawn(_worker, args=(world, _free_port(), d, steps), nprocs=world, join=True)
+        res = [dict(np.load(os.path.join(d, f"rank{r}.npz"))) for r in range(world)]
+    ref = _reference_model()
+    ref_losses = _train(ref, [_batch(100 + s, B * world) for s in range(steps)])
+    # the global loss is the mean of the ranks' (equal-size) batch means
+    got = (res[0]["losses"] + res[1]["losses"]) / 2
+    np.testing.assert_allclose(got, ref_losses, rtol=1e-5, atol=1e-6)
+    sd = ref.state_dict()
+    for k, v in sd.items():
+        if k.startswith("embeddings"):
+            continue
+        for r in range(world):
+            np.testing.assert_allclose(res[r][k.replace(".", "__")], v.numpy(), rtol=1e-5,
+                                       atol=1e-6, err_msg=k)
+    bank = ref.embeddings
+    cols = bank.dim + 1
+    for r in range(world):
+        w = res[r]["embeddings__weight"]
+        o_local = 0
+        for f, (o, n) in enumerate(zip(bank.row_offset, bank.category_nums)):
+            rows = bank.weight.detach()[o:o + n][r::world, :cols].numpy()
+            np.testing.assert_allclose(w[o_local:o_local + rows.shape[0], :cols], rows,
+                                       rtol=1e-5, atol=1e-6, err_msg=f"rank {r} table {f}")
+            o_local += rows.shape[0]
+
+
+def test_cpu_bucketize_slots_are_stable_and_complete():
+    from pytorchrec_amd.sharding import ShardComm, ShardedEmbeddingBank, cpu_bucketize
+    comm = ShardComm(world=3, rank=1)
+    bank = ShardedEmbeddingBank([10, 31], 4, comm, cap=8)
+    ids = [torch.tensor([0, 3, 6, 1, 9, 4, 2], dtype=torch.int32),
+           torch.tensor([30, 2, 2, 5, 29, 0, 11], dtype=torch.int32)]
+    send, pos = cpu_bucketize(bank, ids)
+    assert send.shape == (3, 2, 8) and pos.shape == (2, 7)
+    flat = send.reshape(-1)
+    for f, t in enumerate(ids):
+        for b, i in enumerate(t.tolist()):
+            p = int(pos[f, b])
+            owner, rem = divmod(p, 2 * 8)
+            assert owner == i % 3 and rem // 8 == f
+            assert int(flat[p]) == i // 3
+    # stable: owner 0 of table 0 gets ids 0, 3, 6, 9 in sample order
+    assert send[0, 0, :4].tolist() == [0, 1, 2, 3] and send[0, 0, 4:].tolist() == [-1] * 4
+    with pytest.raises(IndexError):
+        cpu_bucketize(bank, [torch.tensor([10], dtype=torch.int32), torch.tensor([0], dtype=torch.int32)])
+    small = ShardedEmbeddingBank([10, 31], 4, comm, cap=1)
+    with pytest.raises(RuntimeError, match="overflow"):
+        cpu_bucketize(small, [torch.tensor([0, 3], dtype=torch.int32), torch.tensor([1, 2], dtype=torch.int32)])
+
+
+def test_shard_row_split():
+    from pytorchrec_amd.sharding import ShardComm, ShardedEmbeddingBank
+    rows = [10, 7, 1]
+    got = [ShardedEmbeddingBank(rows, 4, ShardComm(world=3, rank=r)).category_nums for r in range(3)]
+    assert got == [[4, 3, 1], [3, 2, 0], [3, 2, 0]]
+    assert [sum(g[f] for g in got) for f in range(3)] == rows

@@ -49,6 +49,10 @@ def parse():
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--cpu-seconds", type=float, default=12.0)
     p.add_argument("--no-roofline", action="store_true")
+    p.add_argument("--shard", action="store_true",
+                   help="row-sharded tables + DP even at N=1 (always on for N>1)")
+    p.add_argument("--force-collectives", action="store_true",
+                   help="issue the all-to-alls / all-reduce even at N=1 (RCCL capture check)")
     return p.parse_args()
 
 
@@ -56,15 +60,23 @@ def parse():
 # workload
 # ----------------------------------------------------------------------------
 
-def build_deepfm(args, device):
+def build_deepfm(args, device, comm=None):
+    """C2 DeepFM; with ``comm`` the tables are row-sharded over its ranks (each rank
+    allocates only its shard) and the dense tower is data-parallel."""
+    import contextlib
     from pytorchrec_amd.feature_column import CategoricalColumnWithIdentity, NumericColumn
     from pytorchrec_amd.model import DeepFM
+    from pytorchrec_amd.sharding import sharded_tables
     sparse = [CategoricalColumnWithIdentity(args.rows_per_table, f"c_c_C{f + 1}")
               for f in range(CRITEO_FIELDS)]
     dense = [NumericColumn(f"c_n_I{j + 1}") for j in range(CRITEO_DENSE)]
     label = CategoricalColumnWithIdentity(2, "label")
-    model = DeepFM(sparse, dense, label, emb_size=16, layers=(400, 400, 400), dropout=0.0,
-                   emb_dtype=torch.bfloat16, device=device, random_seed=2020)
+    ctx = sharded_tables(comm, max_batch=args.batch) if comm is not None else contextlib.nullcontext()
+    with ctx:
+        model = DeepFM(sparse, dense, label, emb_size=16, layers=(400, 400, 400), dropout=0.0,
+                       emb_dtype=torch.bfloat16, device=device, random_seed=2020)
+    if comm is not None:
+        model.distribute(comm)
     return model, sparse, dense, label
 
 
@@ -130,16 +142,24 @@ def time_launches(fn, reps=100):
 
 def kernel_rooflines(model, data, args):
     """Average duration of each HBM-bound embedding kernel, launched exactly as the
-    train step launches it, and its algorithmic bytes."""
+    train step launches it, and its algorithmic bytes.  Measured on
+    an unsharded C2 bank of the same shapes (at N>1 the model's tables are shards)."""
     from pytorchrec_amd import _mrec, embedding as E
-    bank = model.embeddings
+    dev = torch.device("cuda", torch.cuda.current_device())
+    bank = E.EmbeddingBank([args.rows_per_table] * CRITEO_FIELDS, 16, with_first_order=True,
+                           dtype=torch.bfloat16, device=dev)
+    E.init_bank_(bank, generator=torch.Generator(device=dev).manual_seed(5))
+    bank.use_fused_sgd(args.lr)
+    bank.check_ids = False
+    dense_weight = torch.randn(CRITEO_DENSE, device=dev) * 0.01
+    global_bias = torch.zeros(1, device=dev)
     B, F, D = args.batch, bank.n_tables, bank.dim
     ids = model._ids(data)
     dense = model._dense(data)
     out = {}
     with torch.no_grad():
         def fwd():
-            E._InteractFn.forward(_Ctx(), bank.weight, model.dense_weight, model.global_bias, None,
+            E._InteractFn.forward(_Ctx(), bank.weight, dense_weight, global_bias, None,
                                   bank, ids, dense, True, True, model.x0_cols, torch.bfloat16)
         # bytes/sample: ids F*4 + useful row bytes F*(D+1)*2 + dense 13*4 + x0 write
         # x0_cols*2 + logit 4 + fm_sum D*4
@@ -155,9 +175,9 @@ def kernel_rooflines(model, data, args):
         t = time_launches(plan)
         out["mrec_emb_bwd_plan"] = (t, (F * 4 + F * 12) * B)
 
-        x0, logit = E._InteractFn.forward(_Ctx(), bank.weight, model.dense_weight,
-                                          model.global_bias, None, bank, ids, dense, True, True,
-                                          model.x0_cols, torch.bfloat16)
+        x0, logit = E._InteractFn.forward(_Ctx(), bank.weight, dense_weight, global_bias, None,
+                                          bank, ids, dense, True, True, model.x0_cols,
+                                          torch.bfloat16)
         fm_sum = torch.zeros(B, D, device=x0.device)
         dx0 = torch.zeros_like(x0)
         dl = torch.zeros(B, device=x0.device)
@@ -229,16 +249,25 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    if world > 1:
+    sharded = world > 1 or args.shard
+    if world > 1 or args.force_collectives:
         import torch.distributed as dist
         torch.cuda.set_device(local)
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        os.environ.setdefault("MASTER_PORT", "29561")
+        os.environ.setdefault("RANK", "0")
+        os.environ.setdefault("WORLD_SIZE", "1")
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
     device = torch.device("cuda", local)
     torch.cuda.set_device(device)
 
     if args.model != "deepfm":
         raise SystemExit("only --model deepfm is wired into bench.py this round")
-    model, sparse, dense_cols, label_col = build_deepfm(args, device)
+    comm = None
+    if sharded:
+        from pytorchrec_amd.sharding import ShardComm
+        comm = ShardComm(force_collectives=args.force_collectives)
+    model, sparse, dense_cols, label_col = build_deepfm(args, device, comm)
     from pytorchrec_amd.loss import BCEWithLogitsLoss
     model.compile(torch.optim.SGD(model.get_parameters(), lr=args.lr), BCEWithLogitsLoss(), [],
                   device)
@@ -265,12 +294,22 @@ def main():
                 step()
         torch.cuda.current_stream().wait_stream(s)
         graph = torch.cuda.CUDAGraph()
-        with torch.cuda.graph(graph):
-            step()
+        try:
+            with torch.cuda.graph(graph):
+                step()
+        except Exception as e:  # e.g. a collective the runtime cannot capture
+            print(f"bench: HIP graph capture failed ({type(e).__name__}: {e}); running eagerly",
+                  file=sys.stderr, flush=True)
+            args.no_graph = True
+            torch.cuda.synchronize()
+            graph = None
 
         def run(i):
             static.copy_(bufs[i % 4])
-            graph.replay()
+            if graph is None:
+                step()
+            else:
+                graph.replay()
 
     for i in range(args.warmup):
         run(i)
@@ -286,6 +325,10 @@ def main():
         run(i)
     barrier()
     elapsed = time.perf_counter() - t0
+    from pytorchrec_amd.sharding import ShardedEmbeddingBank
+    for b in model.embedding_banks():
+        if isinstance(b, ShardedEmbeddingBank):
+            b.check_flags()  # an exchange overflow would make the run invalid: raise
     if world > 1:
         t = torch.tensor([elapsed], device=device, dtype=torch.float64)
         torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX)
@@ -310,7 +353,7 @@ def main():
                                "with packed first-order weight, 13 dense, MLP 400-400-400, BCE, "
                                "SGD lr %g (fused row-sparse update)" % (args.rows_per_table, args.lr),
                    "global_batch": args.batch * world, "batch_per_gpu": args.batch,
-                   "parallelism": f"dp{world}" if world > 1 else "single",
+                   "parallelism": (f"dp{world}+rowshard{world}" if sharded else "single"),
                    "hip_graph": not args.no_graph},
     }
     if rank == 0 and not args.no_roofline:
@@ -334,7 +377,7 @@ def main():
         result["cpu_baseline"] = cpu_baseline(args)
     if rank == 0:
         print(json.dumps(result), flush=True)
-    if world > 1:
+    if torch.distributed.is_initialized():
         torch.distributed.destroy_process_group()
 
 

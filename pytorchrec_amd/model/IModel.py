@@ -182,7 +182,8 @@ class IModel(Module, IWithArguments, ABC):
         loss = self.compiled_loss(prediction, target)
         self.compiled_optimizers.zero_grad()
         loss.backward()
-        if getattr(self, "dp_comm", None) is not None and self.dp_comm.world > 1:
+        comm = getattr(self, "dp_comm", None)
+        if comm is not None and (comm.world > 1 or comm.force):
             self._allreduce_dense_grads()
         self.compiled_optimizers.step(closure=None)
         return {"loss": loss}

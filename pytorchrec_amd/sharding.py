@@ -49,17 +49,20 @@ class ShardComm:
     """Equal-split all-to-all and mean all-reduce on a ``torch.distributed`` group
     (RCCL for GPU tensors, gloo for CPU tensors).  ``world == 1`` needs no group."""
 
-    def __init__(self, group=None, world: Optional[int] = None, rank: Optional[int] = None):
+    def __init__(self, group=None, world: Optional[int] = None, rank: Optional[int] = None,
+                 force_collectives: bool = False):
         self.group = group
         if world is None:
             world = dist.get_world_size(group) if dist.is_initialized() else 1
         if rank is None:
             rank = dist.get_rank(group) if dist.is_initialized() else 0
         self.world, self.rank = int(world), int(rank)
+        # issue the collectives even at world 1 (exercises RCCL + graph capture on one GPU)
+        self.force = bool(force_collectives) and dist.is_initialized()
 
     def exchange(self, send: torch.Tensor) -> torch.Tensor:
         """``out[s]`` = part ``rank`` of rank s's ``send`` (dim 0 split in W equal parts)."""
-        if self.world == 1:
+        if self.world == 1 and not self.force:
             return send
         send = send.contiguous()
         out = torch.empty_like(send)
@@ -67,7 +70,7 @@ class ShardComm:
         return out
 
     def allreduce_mean_(self, flat: torch.Tensor) -> torch.Tensor:
-        if self.world > 1:
+        if self.world > 1 or self.force:
             dist.all_reduce(flat, group=self.group)
             flat.div_(self.world)
         return flat

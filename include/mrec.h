@@ -293,12 +293,12 @@ size_t mrec_gemm_workspace_size(int64_t M, int64_t N, int64_t K, int32_t split_k
 /*
  * C[M, N] = epi( sum_k A(m, k) B(k, n) ), A and B bf16 with 16-byte aligned rows
  * (fp32 weights go through mrec_weight_prep), fp32 accumulation on
- * v_mfma_f32_16x16x32_bf16.  Each 256-thread workgroup computes a 64x64 tile over
- * a K slab of <= 448: both operand slabs are brought into LDS by
- * global_load_lds_dwordx4 (LDS-DMA, swizzled images, no register staging), COL
- * operands are read back with ds_read_b64_tr_b16; K is split over
- * max(split_k, ceil(K/448)) workgroups, partials reduced in fixed order
- * (deterministic) through `workspace` (mrec_gemm_workspace_size bytes).
+ * v_mfma_f32_16x16x32_bf16.  Each 256-thread workgroup computes a 64x64 tile over a
+ * K slice; operands are brought into LDS by global_load_lds_dwordx4 (LDS-DMA,
+ * swizzled images, no register staging) through a 3-deep ring of 64-wide k
+ * groups, COL operands are read back with ds_read_b64_tr_b16; K is split over
+ * split_k workgroups, partials reduced in fixed order (deterministic) through
+ * `workspace` (mrec_gemm_workspace_size bytes).
  * Layout ROW: element (i, k) at ptr[i*ld + k]; COL: at ptr[k*ld + i] (for B, i is
  * the output column n; nn.Linear's [out, in] weight is B in ROW layout).
  * b_ones_col == N appends a column of ones to B, so epi->ones_out[m] = sum_k A(m, k):

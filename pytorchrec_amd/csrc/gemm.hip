@@ -3,12 +3,11 @@
 //   C[m, n] = epi( sum_k A(m, k) * B(k, n) ),  A, B bf16, fp32 accumulation
 //
 // Operands are ROW (k contiguous) or COL (m / n contiguous).  One 256-thread
-// workgroup computes a 64x64 output tile over a K slab of <= 448 (4 waves in 2x2,
-// each wave 2x2 v_mfma_f32_16x16x32_bf16 tiles).  The slab is moved into LDS with
-// global_load_lds_dwordx4 (LDS-DMA: no VGPR staging, no per-element VALU), in
-// 64-wide k groups that are all put in flight at once; the MFMA loop consumes group
-// g as soon as its DMA has landed (s_waitcnt vmcnt + barrier), so the copy of the
-// later groups overlaps the math on the earlier ones.
+// workgroup computes a 64x64 output tile over a K slice (4 waves in 2x2, each wave
+// 2x2 v_mfma_f32_16x16x32_bf16 tiles).  Operands move into LDS with
+// global_load_lds_dwordx4 (LDS-DMA: no VGPR staging, no per-element VALU) in
+// 64-wide k groups through a 3-deep ring (48 KiB, three workgroups per CU): group
+// g+2 is in flight while the MFMAs consume group g (s_waitcnt vmcnt + barrier).
 //
 // LDS images (per operand, per k group of 64: 64 rows x 64 k = 8 KiB):
 //   ROW: [row][8 slots of 16 B], chunk c (8 k) of row r in slot c ^ (r & 7) — the
@@ -34,7 +33,7 @@ namespace mrec {
 constexpr int BM = 64, BN = 64;
 constexpr int GEMM_THREADS = 256;
 constexpr int KG = 64;                 // k per staging group
-constexpr int SLAB_KMAX = 448;         // k per workgroup: 2 x 7 groups x 8 KiB = 112 KiB LDS
+constexpr int NBUF = 3;                // k-group ring depth: 3 x 16 KiB = 48 KiB LDS, 3 workgroups / CU
 constexpr int GROUP_ELEMS = 64 * KG;   // one operand's group image (bf16 elements)
 constexpr int TLD = BN + 4;            // fp32 row stride of the C tile staged in LDS
 
@@ -82,19 +81,6 @@ template <int N>
 __device__ __forceinline__ void wait_vmcnt() {
   __builtin_amdgcn_s_waitcnt((N & 15) | ((N >> 4) << 14) | (7 << 4) | (15 << 8));
 }
-__device__ __forceinline__ void wait_vmcnt_dyn(int n) {
-  switch (n) {
-    case 0: wait_vmcnt<0>(); break;
-    case 4: wait_vmcnt<4>(); break;
-    case 8: wait_vmcnt<8>(); break;
-    case 12: wait_vmcnt<12>(); break;
-    case 16: wait_vmcnt<16>(); break;
-    case 20: wait_vmcnt<20>(); break;
-    case 24: wait_vmcnt<24>(); break;
-    default: wait_vmcnt<0>(); break;
-  }
-}
-
 // Per-lane DMA source walker for one operand.  Every wave issues 2 instructions per
 // k group (pieces t = wave and wave + 4 of the group's 8), each moving 1 KiB.
 template <bool COL>
@@ -135,20 +121,6 @@ struct DmaSrc {
     }
   }
 };
-
-// write 1.0 into tile column `col` of the B image for k < kvalid (the ones column)
-template <bool COL>
-__device__ __forceinline__ void ones_column(uint16_t *img, int col, int klen, int kvalid) {
-  for (int k = threadIdx.x; k < klen; k += GEMM_THREADS) {
-    const uint16_t v = k < kvalid ? uint16_t(0x3f80) : uint16_t(0);
-    if constexpr (!COL) {
-      const int c = k >> 3;
-      img[(c >> 3) * GROUP_ELEMS + col * KG + (((c & 7) ^ (col & 7)) << 3) + (k & 7)] = v;
-    } else {
-      img[(k >> 3) * 512 + (col >> 4) * 128 + (k & 7) * 16 + (col & 15)] = v;
-    }
-  }
-}
 
 // scalar epilogue of one element (split-K reduce and unaligned outputs)
 __device__ __forceinline__ void epilogue_elem(const GemmArgs &g, int64_t m, int64_t n, float acc) {
@@ -269,29 +241,21 @@ __global__ __launch_bounds__(GEMM_THREADS) void gemm_dma_kernel(GemmArgs g) {
   const int64_t ke = min(g.K, kb + g.k_per_split);
   const int64_t krel = ke > kb ? ke - kb : 0;
   const int nkg = static_cast<int>((krel + KG - 1) / KG);
-  uint16_t *As = smem;
-  uint16_t *Bs = smem + nkg * GROUP_ELEMS;
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int wm = wave >> 1, wn = wave & 1;
   const int64_t m0 = static_cast<int64_t>(blockIdx.y) * BM;
   const int64_t n0 = static_cast<int64_t>(blockIdx.x) * BN;
-
-  {
-    const DmaSrc<A_COL> da(g.A, g.lda, g.M, m0, kb, wave, lane);
-    const DmaSrc<B_COL> db(g.B, g.ldb, g.b_cols, n0, kb, wave, lane);
-    for (int kg = 0; kg < nkg; ++kg) {
-      da.issue(kg, krel, As + kg * GROUP_ELEMS, wave);
-      db.issue(kg, krel, Bs + kg * GROUP_ELEMS, wave);
-    }
+  // ring of NBUF k-group buffers, each [A group image | B group image]
+  auto a_buf = [&](int kg) { return smem + (kg % NBUF) * 2 * GROUP_ELEMS; };
+  auto b_buf = [&](int kg) { return smem + (kg % NBUF) * 2 * GROUP_ELEMS + GROUP_ELEMS; };
+  const DmaSrc<A_COL> da(g.A, g.lda, g.M, m0, kb, wave, lane);
+  const DmaSrc<B_COL> db(g.B, g.ldb, g.b_cols, n0, kb, wave, lane);
+  for (int kg = 0; kg < NBUF - 1 && kg < nkg; ++kg) {
+    da.issue(kg, krel, a_buf(kg), wave);
+    db.issue(kg, krel, b_buf(kg), wave);
   }
   const bool ones_here = g.b_ones_col >= n0 && g.b_ones_col < n0 + BN;  // uniform
-  if (ones_here) {
-    wait_vmcnt<0>();
-    __syncthreads();
-    ones_column<B_COL>(Bs, static_cast<int>(g.b_ones_col - n0), nkg * KG, static_cast<int>(krel));
-    __syncthreads();
-  }
 
   // per-lane fragment offsets within a group image, for the group's two k steps
   const int g4 = lane >> 4, l15 = lane & 15;
@@ -315,12 +279,34 @@ __global__ __launch_bounds__(GEMM_THREADS) void gemm_dma_kernel(GemmArgs g) {
     for (int j = 0; j < 2; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
   for (int kg = 0; kg < nkg; ++kg) {
-    // this wave's DMAs of groups <= kg have landed; the barrier makes that true for
-    // every wave.  A bare s_barrier (with a compiler memory clobber): __syncthreads'
-    // release fence would wait for vmcnt(0), i.e. for the whole slab.
-    if (!ones_here) wait_vmcnt_dyn(4 * (nkg - 1 - kg));
+    // group kg has landed for this wave when at most the one group issued after it
+    // (4 DMAs per wave) is still in flight; the barrier makes that true for every
+    // wave and also retires every wave's reads of the buffer about to be refilled.
+    // A bare s_barrier (with a compiler memory clobber): __syncthreads' release
+    // fence would wait for vmcnt(0), i.e. drain the prefetch too.
+    if (kg + 1 < nkg)
+      wait_vmcnt<4>();
+    else
+      wait_vmcnt<0>();
     asm volatile("s_barrier" ::: "memory");
-    const uint16_t *ag = As + kg * GROUP_ELEMS, *bg = Bs + kg * GROUP_ELEMS;
+    if (kg + NBUF - 1 < nkg) {
+      da.issue(kg + NBUF - 1, krel, a_buf(kg + NBUF - 1), wave);
+      db.issue(kg + NBUF - 1, krel, b_buf(kg + NBUF - 1), wave);
+    }
+    if (ones_here) {  // the bias-gradient ones column of this group (rare, uniform)
+      uint16_t *bimg = b_buf(kg);
+      const int col = static_cast<int>(g.b_ones_col - n0);
+      if (tid < KG) {
+        const int k = tid;
+        const uint16_t v = kg * KG + k < krel ? uint16_t(0x3f80) : uint16_t(0);
+        if constexpr (!B_COL)
+          bimg[col * KG + ((((k >> 3) & 7) ^ (col & 7)) << 3) + (k & 7)] = v;
+        else
+          bimg[(k >> 3) * 512 + (col >> 4) * 128 + (k & 7) * 16 + (col & 15)] = v;
+      }
+      __syncthreads();
+    }
+    const uint16_t *ag = a_buf(kg), *bg = b_buf(kg);
 #pragma unroll
     for (int s = 0; s < 2; ++s) {
       bf16x8 a[2], b[2];
@@ -439,31 +425,21 @@ static bool aligned16(const void *p, int64_t ld, int es) {
   return p && (reinterpret_cast<uintptr_t>(p) & 15) == 0 && (ld * es) % 16 == 0;
 }
 
-// K slab per workgroup (multiple of 64, <= SLAB_KMAX) and the resulting split count
+// K slab per workgroup (multiple of 64) and the resulting split count
 static void plan_split(int64_t K, int32_t split_req, int64_t *kps, int32_t *splits) {
-  int64_t s = split_req < 1 ? 1 : split_req;
+  const int64_t s = split_req < 1 ? 1 : split_req;
   int64_t k = ((K + s - 1) / s + KG - 1) / KG * KG;
-  if (k > SLAB_KMAX) {
-    s = (K + SLAB_KMAX - 1) / SLAB_KMAX;
-    k = ((K + s - 1) / s + KG - 1) / KG * KG;
-  }
   if (k < KG) k = KG;
   *kps = k;
   *splits = static_cast<int32_t>(K > 0 ? (K + k - 1) / k : 1);
 }
 
+constexpr size_t kGemmLds = std::max<size_t>(NBUF * 2 * GROUP_ELEMS * sizeof(uint16_t),
+                                             BM * TLD * sizeof(float));
+
 template <bool AC, bool BC>
 static void launch_dma(const GemmArgs &g, dim3 grid, hipStream_t s) {
-  static bool attr = false;
-  const size_t lds = std::max<size_t>(2 * 64 * static_cast<size_t>(g.k_per_split) * sizeof(uint16_t),
-                                      BM * TLD * sizeof(float));
-  if (!attr) {
-    (void)hipFuncSetAttribute(reinterpret_cast<const void *>(gemm_dma_kernel<AC, BC>),
-                              hipFuncAttributeMaxDynamicSharedMemorySize,
-                              2 * 64 * SLAB_KMAX * static_cast<int>(sizeof(uint16_t)));
-    attr = true;
-  }
-  gemm_dma_kernel<AC, BC><<<grid, GEMM_THREADS, lds, s>>>(g);
+  gemm_dma_kernel<AC, BC><<<grid, GEMM_THREADS, kGemmLds, s>>>(g);
 }
 
 }  // namespace mrec

@@ -45,11 +45,11 @@ def _op(t: torch.Tensor, layout: int) -> _mrec.Operand:
 
 
 def _split_for(M: int, N: int, K: int) -> int:
-    """K slabs per output tile: at least ceil(K / 448) (the library enforces it),
-    more while a small-output long-K GEMM (weight gradients) leaves CUs idle."""
+    """K slices per output tile: more while a small-output long-K GEMM (weight
+    gradients) would leave most of the 256 CUs (3 workgroups each) idle."""
     tiles = ((M + 63) // 64) * ((N + 63) // 64)
-    s = max(1, -(-K // 448))
-    while tiles * s < 256 and K // (s + 1) >= 128 and s < 64:
+    s = 1
+    while tiles * s < 384 and K // (s + 1) >= 256 and s < 64:
         s += 1
     return s
 

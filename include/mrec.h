@@ -32,7 +32,7 @@
 extern "C" {
 #endif
 
-#define MREC_ABI_VERSION 3
+#define MREC_ABI_VERSION 5
 #define MREC_MAX_TABLES 64      /* tables per table bank / per call */
 #define MREC_BWD_MAX_BATCH 8192  /* lookups per table per plan/apply call */
 
@@ -286,6 +286,19 @@ typedef struct {
   const void *mask;
   int64_t ld_mask;
   float *ones_out;
+  /* Fused SGD (update != 0; then bias/act/mul/add/aux/mask must be unset and C
+   * fp32): C is a master weight updated in place, C[m, n] -= lr * v, and
+   * ones_out[m] -= lr * (row sum), instead of being overwritten; the new C is
+   * re-emitted as bf16 images for the next forward, img_row[m * ld_img_row + n]
+   * and img_tr[n * ld_img_tr + m] (either may be NULL).  A Linear's weight-gradient
+   * GEMM then IS its torch.optim.SGD step (no momentum / weight decay;
+   * IModel.py:116-125) — no gradient tensor, no optimizer or conversion kernels. */
+  int32_t update;
+  float lr;
+  void *img_row;
+  int64_t ld_img_row;
+  void *img_tr;
+  int64_t ld_img_tr;
 } mrec_epilogue;
 
 size_t mrec_gemm_workspace_size(int64_t M, int64_t N, int64_t K, int32_t split_k);
@@ -351,15 +364,42 @@ mrec_status mrec_bce_bwd(const float *z, const float *y, int64_t batch, const fl
                          mrec_stream stream);
 
 /*
+ * Fused CTR head + BCE-with-logits (forward AND the loss gradient, one pass over h;
+ * the train step of a Linear(H, 1) output layer on a ReLU MLP, the mean BCE loss):
+ *   z[b]  = base[b] + bias + h[b] . w                   (prediction logit)
+ *   dz[b] = (sigmoid(z[b]) - y[b]) / batch               (d mean-loss / d z)
+ *   dh[b, :] = dz[b] * w * (relu_mask ? h[b, :] > 0 : 1)  (bf16, pad columns 0)
+ *   *loss = mean_b (max(z,0) - z y + log1p(exp(-|z|)))
+ * and per-workgroup partials of dW = sum_b dz[b] h[b, :] and db = sum_b dz[b] in
+ * part[mrec_ctr_head_parts(batch)][ldp >= H + 1].  The loss is reduced in the same
+ * launch through loss_part[parts] and a ticket (*ticket must be 0 on entry and is
+ * left 0).  H <= 1024, h / dh rows 16-byte aligned.
+ * mrec_ctr_head_finish sums the partials in fixed order and, scaled by the
+ * upstream gradient *g (NULL = 1), applies SGD (update: w -= lr g dW, bias -= lr g db)
+ * or writes dw_out / db_out.  Replaces Linear(H,1) + BCEWithLogitsLoss forward and
+ * backward (NCF.py:51,74 head; losses.py:8-12 lacks BCE).
+ */
+int64_t mrec_ctr_head_parts(int64_t batch);
+mrec_status mrec_ctr_head_fwd(const void *h, int64_t ldh, int64_t batch, int32_t H, const float *w,
+                              const float *bias, const float *base, const float *y,
+                              int32_t relu_mask, float *z, float *dz, void *dh, int64_t lddh,
+                              float *part, int64_t ldp, float *loss_part, uint32_t *ticket,
+                              float *loss, mrec_stream stream);
+mrec_status mrec_ctr_head_finish(const float *part, int64_t ldp, int64_t batch, int32_t H,
+                                 const float *g, int32_t update, float lr, float *w, float *bias,
+                                 float *dw_out, float *db_out, mrec_stream stream);
+
+/*
  * out[c] = sum_b s[b] X[b, c] for c < C, and *total = sum_b s[b] (if total != NULL):
  * the gradients of a small Linear / bias fed by per-sample scalars (dense
- * first-order weights, global bias, Linear(H, 1)).  Deterministic two-pass
- * reduction through `workspace` (mrec_colsum_workspace_size(C) bytes).
+ * first-order weights, global bias, Linear(H, 1)).  One launch, one workgroup per
+ * 8 columns, fixed-order tree reduction (deterministic).  With update != 0 the sums
+ * are applied as SGD instead: out[c] -= lr * sum, *total -= lr * sum (fused
+ * optimizer step of those parameters).
  */
-size_t mrec_colsum_workspace_size(int64_t C);
 mrec_status mrec_colsum(const float *s, const void *X, mrec_dtype x_dtype, int64_t ldx,
-                        int64_t batch, int64_t C, float *out, float *total, void *workspace,
-                        size_t ws_bytes, mrec_stream stream);
+                        int64_t batch, int64_t C, float *out, float *total, int32_t update,
+                        float lr, mrec_stream stream);
 
 #ifdef __cplusplus
 }

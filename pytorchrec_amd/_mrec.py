@@ -20,7 +20,7 @@ import torch  # noqa: F401  (must precede the dlopen, see module docstring)
 LIB_DIR = os.path.join(os.path.dirname(os.path.abspath(__file__)), "lib")
 LIB_PATH = os.path.join(LIB_DIR, "libmrec.so")
 
-ABI_VERSION = 3
+ABI_VERSION = 5
 MAX_TABLES = 64
 BWD_MAX_BATCH = 8192
 
@@ -79,7 +79,10 @@ class Epilogue(ctypes.Structure):
                 ("add", ctypes.c_void_p), ("ld_add", ctypes.c_int64),
                 ("aux", ctypes.c_void_p), ("ld_aux", ctypes.c_int64),
                 ("mask", ctypes.c_void_p), ("ld_mask", ctypes.c_int64),
-                ("ones_out", ctypes.c_void_p)]
+                ("ones_out", ctypes.c_void_p),
+                ("update", ctypes.c_int32), ("lr", ctypes.c_float),
+                ("img_row", ctypes.c_void_p), ("ld_img_row", ctypes.c_int64),
+                ("img_tr", ctypes.c_void_p), ("ld_img_tr", ctypes.c_int64)]
 
 
 LAYOUT_ROW, LAYOUT_COL = 0, 1
@@ -129,9 +132,13 @@ SIGNATURES = {
     "mrec_head_bwd": (ctypes.c_int, [_vp, _vp, _i64, _i32, _vp, _i64, _vp, _i64, _vp]),
     "mrec_bce_fwd": (ctypes.c_int, [_vp, _vp, _i64, _vp, _vp]),
     "mrec_bce_bwd": (ctypes.c_int, [_vp, _vp, _i64, _vp, _vp, _vp]),
-    "mrec_colsum_workspace_size": (ctypes.c_size_t, [_i64]),
-    "mrec_colsum": (ctypes.c_int, [_vp, _vp, ctypes.c_int, _i64, _i64, _i64, _vp, _vp, _vp,
-                                   ctypes.c_size_t, _vp]),
+    "mrec_ctr_head_parts": (ctypes.c_int64, [_i64]),
+    "mrec_ctr_head_fwd": (ctypes.c_int, [_vp, _i64, _i64, _i32, _vp, _vp, _vp, _vp, _i32, _vp, _vp,
+                                         _vp, _i64, _vp, _i64, _vp, _vp, _vp, _vp]),
+    "mrec_ctr_head_finish": (ctypes.c_int, [_vp, _i64, _i64, _i32, _vp, _i32, _f32, _vp, _vp, _vp,
+                                            _vp, _vp]),
+    "mrec_colsum": (ctypes.c_int, [_vp, _vp, ctypes.c_int, _i64, _i64, _i64, _vp, _vp, _i32,
+                                   _f32, _vp]),
 }
 
 _lib = None

@@ -70,6 +70,12 @@ struct GemmArgs {
   int64_t k_per_split;
   float *ws;
   int64_t ldws;    // row stride of a split-K partial slab (round8(ncols))
+  int update;      // fused SGD: C -= lr * v (fp32 master), images re-emitted
+  float lr;
+  uint16_t *img_row;
+  int64_t ld_img_row;
+  uint16_t *img_tr;
+  int64_t ld_img_tr;
 };
 
 __device__ __forceinline__ float bf(uint16_t h) { return __uint_as_float(uint32_t(h) << 16); }
@@ -124,6 +130,20 @@ struct DmaSrc {
 
 // scalar epilogue of one element (split-K reduce and unaligned outputs)
 __device__ __forceinline__ void epilogue_elem(const GemmArgs &g, int64_t m, int64_t n, float acc) {
+  if (g.update) {  // fused SGD step of a master weight (+ its bias through the ones column)
+    if (n == g.b_ones_col) {
+      if (g.ones_out) g.ones_out[m] = fmaf(-g.lr, acc, g.ones_out[m]);
+      return;
+    }
+    if (n >= g.N) return;
+    float *c = static_cast<float *>(g.C) + m * g.ldc + n;
+    const float w = fmaf(-g.lr, acc, *c);
+    *c = w;
+    const uint16_t h = f32_to_bf16_rne(w);
+    if (g.img_row) g.img_row[m * g.ld_img_row + n] = h;
+    if (g.img_tr) g.img_tr[n * g.ld_img_tr + m] = h;
+    return;
+  }
   if (n == g.b_ones_col) {
     if (g.ones_out) g.ones_out[m] = acc;
     if (n < g.pad_to) {
@@ -170,6 +190,12 @@ __device__ __forceinline__ void unpack8(const uint4 r, float (&f)[8]) {
 // 16-B epilogue of columns [n, n + 8) of row m (n % 8 == 0, n < max(N + ones, pad_to))
 __device__ __forceinline__ void epilogue_chunk(const GemmArgs &g, int64_t m, int64_t n,
                                                float (&v)[8]) {
+  if (g.update) {
+#pragma unroll
+    for (int j = 0; j < 8; ++j)
+      if (n + j < g.N || n + j == g.b_ones_col) epilogue_elem(g, m, n + j, v[j]);
+    return;
+  }
   if (g.b_ones_col >= n && g.b_ones_col < n + 8 && g.ones_out) {
     float o = 0.f;
 #pragma unroll
@@ -505,11 +531,22 @@ mrec_status mrec_gemm(int64_t M, int64_t N, int64_t K, const mrec_operand *A,
     g.mask = static_cast<const uint16_t *>(epi->mask);
     g.ld_mask = epi->ld_mask;
     g.ones_out = epi->ones_out;
+    g.update = epi->update ? 1 : 0;
+    g.lr = epi->lr;
+    g.img_row = static_cast<uint16_t *>(epi->img_row);
+    g.ld_img_row = epi->ld_img_row;
+    g.img_tr = static_cast<uint16_t *>(epi->img_tr);
+    g.ld_img_tr = epi->ld_img_tr;
+    MREC_CHECK_ARG(!g.update || (c_dtype == MREC_F32 && !g.bias && !g.act && !g.mul && !g.add &&
+                                 !g.aux && !g.mask),
+                   "update epilogue: C must be fp32 and bias/act/mul/add/aux/mask unset");
+    MREC_CHECK_ARG(!g.img_row || g.ld_img_row >= N, "ld_img_row < N");
+    MREC_CHECK_ARG(!g.img_tr || g.ld_img_tr >= M, "ld_img_tr < M");
   }
   g.C = C;
   g.ldc = ldc;
   g.c_f32 = c_dtype == MREC_F32;
-  g.pad_to = std::min<int64_t>(ldc, (N + 7) / 8 * 8);
+  g.pad_to = g.update ? N : std::min<int64_t>(ldc, (N + 7) / 8 * 8);
   g.ldws = (ncols + 7) / 8 * 8;
   g.vec = aligned16(C, ldc, g.c_f32 ? 4 : 2) && (!g.mul || aligned16(g.mul, g.ld_mul, 2)) &&
           (!g.add || aligned16(g.add, g.ld_add, 2)) && (!g.aux || aligned16(g.aux, g.ld_aux, 2)) &&

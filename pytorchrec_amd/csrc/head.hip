@@ -104,54 +104,233 @@ __global__ __launch_bounds__(256) void bce_bwd_kernel(const float *__restrict__ 
   dz[i] = scale * (sig - y[i]);
 }
 
-// column sums: partial[r][c] = sum_{b in chunk r} s[b] * X[b, c]; chunk r of rows
-constexpr int CS_COLS = 64, CS_ROWLANES = 4, CS_CHUNKS = 32;
+// column sums: one 1024-thread workgroup per 8 columns (the last one, when asked,
+// sums s itself); rows strided over the threads (4 independent loads in flight per
+// thread at B = 4096), then a fixed-order tree (wave butterfly, then the 16 wave
+// partials summed in order): bitwise reproducible.
+constexpr int CS_T = 1024;
+constexpr int CS_W = CS_T / 64;
 
-__global__ __launch_bounds__(256) void colsum_partial_kernel(const float *__restrict__ s,
-                                                             const void *__restrict__ X, int x_bf16,
-                                                             int64_t ldx, int64_t B, int64_t C,
-                                                             float *__restrict__ part,
-                                                             int with_total) {
-  __shared__ float red[CS_ROWLANES][CS_COLS + 1];
-  const int cl = threadIdx.x % CS_COLS, rl = threadIdx.x / CS_COLS;
-  const int64_t c = static_cast<int64_t>(blockIdx.x) * CS_COLS + cl;
-  const int64_t rows_per = (B + CS_CHUNKS - 1) / CS_CHUNKS;
-  const int64_t b0 = static_cast<int64_t>(blockIdx.y) * rows_per;
-  const int64_t b1 = min(B, b0 + rows_per);
-  const int64_t Ct = C + (with_total ? 1 : 0);  // column C = sum of s (the bias gradient)
-  float acc = 0.f;
-  if (c < Ct) {
-    for (int64_t b = b0 + rl; b < b1; b += CS_ROWLANES) {
-      float x = 1.f;
-      if (c < C)
-        x = x_bf16 ? bf16_to_f32(static_cast<const uint16_t *>(X)[b * ldx + c])
-                   : static_cast<const float *>(X)[b * ldx + c];
-      acc = fmaf(s[b], x, acc);
+__global__ __launch_bounds__(CS_T) void colsum_kernel(const float *__restrict__ s,
+                                                      const void *__restrict__ X, int x_bf16,
+                                                      int vec, int64_t ldx, int64_t B, int64_t C,
+                                                      float *__restrict__ out,
+                                                      float *__restrict__ total, int update,
+                                                      float lr) {
+  __shared__ float red[CS_W][9];
+  const int64_t c0 = static_cast<int64_t>(blockIdx.x) * 8;
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const bool tot_block = c0 >= C;
+  float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+#pragma unroll 4
+  for (int64_t b = tid; b < B; b += CS_T) {
+    const float sb = s[b];
+    if (tot_block) {
+      acc[0] += sb;
+      continue;
     }
-  }
-  red[rl][cl] = acc;
-  __syncthreads();
-  if (rl == 0 && c < Ct) {
-    float t = 0.f;
+    float x[8];
+    if (vec) {
+      Vec<uint16_t>::to_f32(*reinterpret_cast<const uint4 *>(static_cast<const uint16_t *>(X) +
+                                                             b * ldx + c0), x);
+    } else {
 #pragma unroll
-    for (int k = 0; k < CS_ROWLANES; ++k) t += red[k][cl];
-    part[static_cast<int64_t>(blockIdx.y) * Ct + c] = t;
+      for (int j = 0; j < 8; ++j) {
+        const int64_t c = c0 + j;
+        x[j] = c >= C ? 0.f
+                      : (x_bf16 ? bf16_to_f32(static_cast<const uint16_t *>(X)[b * ldx + c])
+                                : static_cast<const float *>(X)[b * ldx + c]);
+      }
+    }
+#pragma unroll
+    for (int j = 0; j < 8; ++j) acc[j] = fmaf(sb, x[j], acc[j]);
+  }
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) acc[j] += __shfl_xor(acc[j], off);
+  }
+  if (lane == 0) {
+#pragma unroll
+    for (int j = 0; j < 8; ++j) red[w][j] = acc[j];
+  }
+  __syncthreads();
+  if (tid < 8) {
+    float v = 0.f;
+#pragma unroll
+    for (int k = 0; k < CS_W; ++k) v += red[k][tid];
+    if (tot_block) {
+      if (tid == 0) total[0] = update ? fmaf(-lr, v, total[0]) : v;
+    } else if (c0 + tid < C) {
+      out[c0 + tid] = update ? fmaf(-lr, v, out[c0 + tid]) : v;
+    }
   }
 }
 
-__global__ __launch_bounds__(256) void colsum_final_kernel(const float *__restrict__ part,
-                                                           int64_t C, int with_total,
-                                                           float *__restrict__ out,
-                                                           float *__restrict__ total) {
-  const int64_t Ct = C + (with_total ? 1 : 0);
-  const int64_t c = static_cast<int64_t>(blockIdx.x) * 256 + threadIdx.x;
-  if (c >= Ct) return;
-  float t = 0.f;
-  for (int r = 0; r < CS_CHUNKS; ++r) t += part[r * Ct + c];
-  if (c < C)
-    out[c] = t;
-  else
-    total[0] = t;
+// ---------------------------------------------------------------------------
+// fused CTR head + BCE-with-logits, forward and backward in one pass over h
+// ---------------------------------------------------------------------------
+constexpr int HEAD_RPW = 4;                     // rows per wave
+constexpr int HEAD_RPB = 4 * HEAD_RPW;          // rows per 256-thread workgroup
+constexpr int HEAD_MAXH = 1024;                 // h width handled (2 chunks of 8 per lane)
+
+__global__ __launch_bounds__(256) void ctr_head_kernel(
+    const uint16_t *__restrict__ h, int64_t ldh, int64_t B, int H, const float *__restrict__ w,
+    const float *__restrict__ bias, const float *__restrict__ base, const float *__restrict__ y,
+    int relu, float *__restrict__ z, float *__restrict__ dz, uint16_t *__restrict__ dh,
+    int64_t lddh, float *__restrict__ part, int64_t ldp, float *__restrict__ loss_part,
+    unsigned *__restrict__ ticket, float *__restrict__ loss) {
+  __shared__ float red[4][HEAD_MAXH + 4];
+  __shared__ float sred[4][2];
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const int64_t r0 = (static_cast<int64_t>(blockIdx.x) * 4 + wv) * HEAD_RPW;
+  const float invB = 1.f / static_cast<float>(B);
+  const float b0 = bias ? bias[0] : 0.f;
+  constexpr int NC = HEAD_MAXH / 512;  // chunks of 8 per lane
+  float wr[NC][8], acc[NC][8];
+#pragma unroll
+  for (int q = 0; q < NC; ++q) {
+    const int c = (q * 64 + lane) * 8;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      wr[q][j] = c + j < H ? w[c + j] : 0.f;
+      acc[q][j] = 0.f;
+    }
+  }
+  float dzs = 0.f, ls = 0.f;
+  for (int rr = 0; rr < HEAD_RPW; ++rr) {
+    const int64_t r = r0 + rr;
+    if (r >= B) break;  // uniform per wave
+    float hv[NC][8];
+    float dot = 0.f;
+#pragma unroll
+    for (int q = 0; q < NC; ++q) {
+      const int c = (q * 64 + lane) * 8;
+      if (c < H) {
+        Vec<uint16_t>::to_f32(*reinterpret_cast<const uint4 *>(h + r * ldh + c), hv[q]);
+      } else {
+#pragma unroll
+        for (int j = 0; j < 8; ++j) hv[q][j] = 0.f;
+      }
+#pragma unroll
+      for (int j = 0; j < 8; ++j) dot = fmaf(hv[q][j], wr[q][j], dot);
+    }
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) dot += __shfl_xor(dot, off);
+    const float zz = dot + b0 + (base ? base[r] : 0.f);
+    const float yy = y[r];
+    const float d = (1.f / (1.f + __expf(-zz)) - yy) * invB;
+    if (lane == 0) {
+      z[r] = zz;
+      dz[r] = d;
+      dzs += d;
+      ls += fmaxf(zz, 0.f) - zz * yy + log1pf(__expf(-fabsf(zz)));
+    }
+#pragma unroll
+    for (int q = 0; q < NC; ++q) {
+      const int c = (q * 64 + lane) * 8;
+      if (c >= lddh) continue;
+      float g[8];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        g[j] = d * wr[q][j];
+        if (relu && !(hv[q][j] > 0.f)) g[j] = 0.f;
+        acc[q][j] = fmaf(d, hv[q][j], acc[q][j]);
+      }
+      *reinterpret_cast<uint4 *>(dh + r * lddh + c) =
+          make_uint4(pack_bf16x2(g[0], g[1]), pack_bf16x2(g[2], g[3]), pack_bf16x2(g[4], g[5]),
+                     pack_bf16x2(g[6], g[7]));
+    }
+  }
+  // workgroup partial of dW (4 waves summed in order), db and the loss
+#pragma unroll
+  for (int q = 0; q < NC; ++q) {
+    const int c = (q * 64 + lane) * 8;
+#pragma unroll
+    for (int j = 0; j < 8; ++j)
+      if (c + j < H) red[wv][c + j] = acc[q][j];
+  }
+  if (lane == 0) {
+    sred[wv][0] = dzs;
+    sred[wv][1] = ls;
+  }
+  __syncthreads();
+  float *prow = part + static_cast<int64_t>(blockIdx.x) * ldp;
+  for (int c = threadIdx.x; c < H; c += 256)
+    prow[c] = (red[0][c] + red[1][c]) + (red[2][c] + red[3][c]);
+  __shared__ unsigned s_last;
+  if (threadIdx.x == 0) {
+    prow[H] = (sred[0][0] + sred[1][0]) + (sred[2][0] + sred[3][0]);
+    // the loss: per-workgroup partial as a write-through granule, a per-call ticket,
+    // the last arriver sums the partials in a fixed order (deterministic).
+    // cdna_hip_programming.md §6 G16 (granule stores + relaxed agent ticket).
+    const float lp = (sred[0][1] + sred[1][1]) + (sred[2][1] + sred[3][1]);
+    __hip_atomic_store(loss_part + blockIdx.x, lp, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    const unsigned old = __hip_atomic_fetch_add(ticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    s_last = old == gridDim.x - 1 ? 1u : 0u;
+    if (s_last) {
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __hip_atomic_store(ticket, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+  }
+  __syncthreads();
+  if (!s_last) return;
+  float t = 0.f;  // thread k sums partials k, k + 256, ...: every load in flight at once
+  for (unsigned k = threadIdx.x; k < gridDim.x; k += 256)
+    t += __hip_atomic_load(loss_part + k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) t += __shfl_xor(t, off);
+  if (lane == 0) sred[wv][1] = t;
+  __syncthreads();
+  if (threadIdx.x == 0) loss[0] = ((sred[0][1] + sred[1][1]) + (sred[2][1] + sred[3][1])) * invB;
+}
+
+// sum the per-workgroup partials (fixed order) -> dW [H] and db; then either SGD on
+// (w, bias) with lr * g, or write g * dW / g * db
+__global__ __launch_bounds__(256) void ctr_head_finish_kernel(
+    const float *__restrict__ part, int64_t ldp, int nparts, int H, const float *__restrict__ gp,
+    int update, float lr, float *__restrict__ w, float *__restrict__ bias,
+    float *__restrict__ dw_out, float *__restrict__ db_out) {
+  __shared__ float red[4][9];
+  const int c0 = blockIdx.x * 8;
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+  for (int k = threadIdx.x; k < nparts; k += 256) {
+#pragma unroll
+    for (int j = 0; j < 8; ++j)
+      if (c0 + j <= H) acc[j] += part[static_cast<int64_t>(k) * ldp + c0 + j];
+  }
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) acc[j] += __shfl_xor(acc[j], off);
+  }
+  if (lane == 0) {
+#pragma unroll
+    for (int j = 0; j < 8; ++j) red[wv][j] = acc[j];
+  }
+  __syncthreads();
+  if (threadIdx.x < 8) {
+    const int c = c0 + threadIdx.x;
+    if (c > H) return;
+    const float g = gp ? gp[0] : 1.f;
+    const float v = ((red[0][threadIdx.x] + red[1][threadIdx.x]) +
+                     (red[2][threadIdx.x] + red[3][threadIdx.x])) * g;
+    if (c < H) {
+      if (update)
+        w[c] = fmaf(-lr, v, w[c]);
+      else if (dw_out)
+        dw_out[c] = v;
+    } else {
+      if (update) {
+        if (bias) bias[0] = fmaf(-lr, v, bias[0]);
+      } else if (db_out) {
+        db_out[0] = v;
+      }
+    }
+  }
 }
 
 }  // namespace mrec
@@ -209,29 +388,53 @@ mrec_status mrec_bce_bwd(const float *z, const float *y, int64_t batch, const fl
   return launch_status("mrec_bce_bwd");
 }
 
-size_t mrec_colsum_workspace_size(int64_t C) {
-  return static_cast<size_t>(CS_CHUNKS) * static_cast<size_t>(C + 1) * 4;
-}
-
 mrec_status mrec_colsum(const float *s, const void *X, mrec_dtype x_dtype, int64_t ldx,
-                        int64_t batch, int64_t C, float *out, float *total, void *workspace,
-                        size_t ws_bytes, mrec_stream stream) {
+                        int64_t batch, int64_t C, float *out, float *total, int32_t update,
+                        float lr, mrec_stream stream) {
   MREC_CHECK_ARG(s != nullptr, "s is NULL");
   MREC_CHECK_ARG(C == 0 || (X && out), "X/out NULL");
   MREC_CHECK_ARG(x_dtype == MREC_F32 || x_dtype == MREC_BF16, "X must be f32 or bf16");
   MREC_CHECK_ARG(batch >= 0 && C >= 0 && (C == 0 || ldx >= C), "bad shape");
-  MREC_CHECK_ARG(workspace && ws_bytes >= mrec_colsum_workspace_size(C), "workspace too small");
   if (C == 0 && !total) return MREC_OK;
-  const int wt = total ? 1 : 0;
-  hipStream_t st = static_cast<hipStream_t>(stream);
-  float *part = static_cast<float *>(workspace);
-  const dim3 g1(static_cast<unsigned>((C + wt + CS_COLS - 1) / CS_COLS), CS_CHUNKS);
-  colsum_partial_kernel<<<g1, 256, 0, st>>>(s, X, x_dtype == MREC_BF16, ldx, batch, C, part, wt);
-  mrec_status r = launch_status("mrec_colsum(partial)");
-  if (r != MREC_OK) return r;
-  colsum_final_kernel<<<dim3(static_cast<unsigned>((C + wt + 255) / 256)), 256, 0, st>>>(
-      part, C, wt, out, total);
-  return launch_status("mrec_colsum(final)");
+  const int vec = x_dtype == MREC_BF16 && (reinterpret_cast<uintptr_t>(X) & 15) == 0 &&
+                  ldx % 8 == 0;
+  const unsigned blocks = static_cast<unsigned>((C + 7) / 8 + (total ? 1 : 0));
+  colsum_kernel<<<dim3(blocks), CS_T, 0, static_cast<hipStream_t>(stream)>>>(
+      s, X, x_dtype == MREC_BF16, vec, ldx, batch, C, out, total, update, lr);
+  return launch_status("mrec_colsum");
+}
+
+int64_t mrec_ctr_head_parts(int64_t batch) { return (batch + HEAD_RPB - 1) / HEAD_RPB; }
+
+mrec_status mrec_ctr_head_fwd(const void *h, int64_t ldh, int64_t batch, int32_t H, const float *w,
+                              const float *bias, const float *base, const float *y,
+                              int32_t relu_mask, float *z, float *dz, void *dh, int64_t lddh,
+                              float *part, int64_t ldp, float *loss_part, uint32_t *ticket,
+                              float *loss, mrec_stream stream) {
+  MREC_CHECK_ARG(h && w && y && z && dz && dh && part && loss_part && ticket && loss,
+                 "NULL pointer");
+  MREC_CHECK_ARG(batch >= 1 && H >= 1 && H <= HEAD_MAXH && ldh >= H && lddh >= H, "bad shape");
+  MREC_CHECK_ARG((reinterpret_cast<uintptr_t>(h) & 15) == 0 && ldh % 8 == 0 &&
+                     (reinterpret_cast<uintptr_t>(dh) & 15) == 0 && lddh % 8 == 0,
+                 "h / dh rows must be 16-byte aligned");
+  MREC_CHECK_ARG(ldp >= H + 1, "ldp < H + 1");
+  const int64_t nb = mrec_ctr_head_parts(batch);
+  ctr_head_kernel<<<dim3(static_cast<unsigned>(nb)), 256, 0, static_cast<hipStream_t>(stream)>>>(
+      static_cast<const uint16_t *>(h), ldh, batch, H, w, bias, base, y, relu_mask, z, dz,
+      static_cast<uint16_t *>(dh), lddh, part, ldp, loss_part, ticket, loss);
+  return launch_status("mrec_ctr_head_fwd");
+}
+
+mrec_status mrec_ctr_head_finish(const float *part, int64_t ldp, int64_t batch, int32_t H,
+                                 const float *g, int32_t update, float lr, float *w, float *bias,
+                                 float *dw_out, float *db_out, mrec_stream stream) {
+  MREC_CHECK_ARG(part != nullptr && H >= 1 && batch >= 1, "bad arguments");
+  MREC_CHECK_ARG(!update || w, "update needs w");
+  const int nparts = static_cast<int>(mrec_ctr_head_parts(batch));
+  ctr_head_finish_kernel<<<dim3(static_cast<unsigned>((H + 1 + 7) / 8)), 256, 0,
+                           static_cast<hipStream_t>(stream)>>>(part, ldp, nparts, H, g, update, lr,
+                                                               w, bias, dw_out, db_out);
+  return launch_status("mrec_ctr_head_finish");
 }
 
 }  // extern "C"

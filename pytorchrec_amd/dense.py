@@ -73,7 +73,8 @@ def _is_relu_out(x: torch.Tensor) -> bool:
 
 
 def gemm(A, a_layout, B, b_layout, M, N, K, *, ones_out=None, b_cols=None, bias=None, act=0,
-         mul=None, add=None, aux=None, mask=None, out=None, out_dtype=_BF16, split_k=None):
+         mul=None, add=None, aux=None, mask=None, out=None, out_dtype=_BF16, split_k=None,
+         sgd_lr=None, img_row=None, img_tr=None):
     """C[M, N] = epi(A[M, K] @ B[K, N]) on libmrec (see include/mrec.h mrec_gemm).
     ``ones_out`` (fp32 [M]) receives sum_k A(m, k) through an appended ones column;
     ``mask`` ([M, N] bf16) zeroes outputs where mask <= 0 (ReLU')."""
@@ -88,7 +89,10 @@ def gemm(A, a_layout, B, b_layout, M, N, K, *, ones_out=None, b_cols=None, bias=
                          _mrec.ptr(add), add.stride(0) if add is not None else 0,
                          _mrec.ptr(aux), aux.stride(0) if aux is not None else 0,
                          _mrec.ptr(mask), mask.stride(0) if mask is not None else 0,
-                         _mrec.ptr(ones_out))
+                         _mrec.ptr(ones_out), int(sgd_lr is not None),
+                         float(sgd_lr) if sgd_lr is not None else 0.0,
+                         _mrec.ptr(img_row), img_row.stride(0) if img_row is not None else 0,
+                         _mrec.ptr(img_tr), img_tr.stride(0) if img_tr is not None else 0)
     a_op, b_op = _op(A, a_layout), _op(B, b_layout)
     _mrec.call("mrec_gemm", M, N, K, ctypes.byref(a_op), ctypes.byref(b_op),
                N if ones_out is not None else -1, N if b_cols is None else b_cols,
@@ -107,6 +111,37 @@ def weight_prep(W: torch.Tensor, row: bool = True, tr: bool = True):
                wr.stride(0) if wr is not None else 0, _mrec.ptr(wt),
                wt.stride(0) if wt is not None else 0, _mrec.stream_handle())
     return wr, wt
+
+
+def weight_images(weight: torch.Tensor):
+    """(row, transposed) bf16 images of a Parameter, cached on it and rebuilt only
+    when torch modified the weight (version counter).  A fused SGD step rewrites the
+    images itself, in the same kernel that updates the fp32 weight."""
+    c = getattr(weight, "_mrec_img", None)
+    if (c is not None and c[0] == weight._version and c[1].device == weight.device
+            and c[1].shape[0] == weight.shape[0]):
+        return c[1], c[2]
+    wr, wt = weight_prep(weight)
+    weight._mrec_img = (weight._version, wr, wt)
+    return wr, wt
+
+
+def sgd_lr(*params) -> Optional[float]:
+    """The learning rate when every given parameter (None entries ignored) is
+    trained by plain SGD fused into its backward (IModel.compile marks them), with
+    one common lr; else None (the gradient is returned to the optimizer)."""
+    lr = None
+    for p in params:
+        if p is None:
+            continue
+        g = getattr(p, "_mrec_sgd_group", None)
+        if g is None:
+            return None
+        if lr is None:
+            lr = float(g["lr"])
+        elif float(g["lr"]) != lr:
+            return None
+    return lr
 
 
 def _bf16_rows(t: torch.Tensor) -> torch.Tensor:
@@ -129,26 +164,28 @@ def _weight_f32(w: torch.Tensor) -> torch.Tensor:
 
 class _LinearFn(torch.autograd.Function):
     """y = act(x[:, :K] W^T + b) with W [N, K] fp32 (nn.Linear layout).
-    x_relu: x is a ReLU output, so dx is masked by x in the dx GEMM's epilogue."""
+    x_relu: x is a ReLU output, so dx is masked by x in the dx GEMM's epilogue.
+    With fused SGD (sgd_lr) the weight-gradient GEMM applies W -= lr dW, b -= lr db
+    and rewrites the bf16 images; no gradient is returned."""
 
     @staticmethod
     def forward(ctx, x, weight, bias, relu: bool, out_dtype, x_relu: bool):
         x = _bf16_rows(x)
         M, K_x = x.shape
         N, K = weight.shape
-        need_dx = ctx.needs_input_grad[0]
-        wr, wt = weight_prep(weight, row=True, tr=need_dx)
+        wr, wt = weight_images(weight)
         b = bias.detach().float().contiguous() if bias is not None else None
         y = gemm(x, _mrec.LAYOUT_ROW, wr[:, :K], _mrec.LAYOUT_ROW, M, N, K, bias=b,
                  act=_mrec.ACT_RELU if relu else _mrec.ACT_NONE, out_dtype=out_dtype)
-        ctx.save_for_backward(x, wt, y if relu else None)
+        ctx.save_for_backward(x, y if relu else None)
         ctx.relu, ctx.has_bias, ctx.NK, ctx.x_relu = relu, bias is not None, (N, K), x_relu
         ctx.y_ptr = y.data_ptr()
+        ctx.weight, ctx.bias, ctx.wr, ctx.wt = weight, bias, wr, wt
         return y
 
     @staticmethod
     def backward(ctx, dy):
-        x, wt, y = ctx.saved_tensors
+        x, y = ctx.saved_tensors
         M, K_x = x.shape
         N, K = ctx.NK
         if ctx.relu and not _premasked(dy, ctx.y_ptr):
@@ -157,16 +194,23 @@ class _LinearFn(torch.autograd.Function):
         dx = dW = db = None
         if ctx.needs_input_grad[0]:
             # dx[m, k] = sum_n dZ[m, n] W[n, k]; B(k'=n, col=k) = W^T[k*ld + n] -> ROW
-            dx = gemm(dy, _mrec.LAYOUT_ROW, wt, _mrec.LAYOUT_ROW, M, K_x, N, b_cols=K,
+            dx = gemm(dy, _mrec.LAYOUT_ROW, ctx.wt, _mrec.LAYOUT_ROW, M, K_x, N, b_cols=K,
                       mask=x if ctx.x_relu else None, out_dtype=_BF16)
             if ctx.x_relu:
                 _stamp(dx, x)
         if ctx.needs_input_grad[1] or ctx.needs_input_grad[2]:
             # dW[n, k] = sum_m dZ[m, n] x[m, k]: A(i=n, red=m) = dy[m*ld + n] -> COL,
             # B(red=m, col=k) = x[m*ld + k] -> COL; ones column -> db
-            dW = torch.empty(N, K, dtype=torch.float32, device=dy.device)
-            db = torch.empty(N, dtype=torch.float32, device=dy.device) if ctx.has_bias else None
-            gemm(dy, _mrec.LAYOUT_COL, x, _mrec.LAYOUT_COL, N, K, M, ones_out=db, out=dW)
+            lr = sgd_lr(ctx.weight, ctx.bias)
+            if lr is not None:  # runs after the dx GEMM has read the old images
+                gemm(dy, _mrec.LAYOUT_COL, x, _mrec.LAYOUT_COL, N, K, M,
+                     ones_out=ctx.bias.detach() if ctx.has_bias else None,
+                     out=ctx.weight.detach(), out_dtype=torch.float32, sgd_lr=lr,
+                     img_row=ctx.wr, img_tr=ctx.wt)
+            else:
+                dW = torch.empty(N, K, dtype=torch.float32, device=dy.device)
+                db = torch.empty(N, dtype=torch.float32, device=dy.device) if ctx.has_bias else None
+                gemm(dy, _mrec.LAYOUT_COL, x, _mrec.LAYOUT_COL, N, K, M, ones_out=db, out=dW)
         return dx, dW, db, None, None, None
 
 
@@ -195,18 +239,20 @@ class _CrossFn(torch.autograd.Function):
         x0, xl = _bf16_rows(x0), _bf16_rows(xl)
         M = xl.shape[0]
         d = weight.shape[0]
-        wr, wt = weight_prep(weight)
+        wr, wt = weight_images(weight)
         b = bias.detach().float().contiguous() if bias is not None else None
         z = _alloc(M, d, _BF16, xl.device)
         out = gemm(xl, _mrec.LAYOUT_ROW, wr[:, :d], _mrec.LAYOUT_ROW, M, d, d, bias=b, mul=x0,
                    add=xl, aux=z)
-        ctx.save_for_backward(x0, xl, wt, z)
+        ctx.save_for_backward(x0, xl, z)
         ctx.has_bias = bias is not None
+        ctx.weight, ctx.bias, ctx.wr, ctx.wt = weight, bias, wr, wt
         return out
 
     @staticmethod
     def backward(ctx, g):
-        x0, xl, wt, z = ctx.saved_tensors
+        x0, xl, z = ctx.saved_tensors
+        wt = ctx.wt
         g = _bf16_rows(g)
         M = g.shape[0]
         d = z.shape[1]
@@ -217,9 +263,16 @@ class _CrossFn(torch.autograd.Function):
             dz.as_strided((M, dz.stride(0) - d), (dz.stride(0), 1), d).zero_()
         dxl = gemm(dz, _mrec.LAYOUT_ROW, wt, _mrec.LAYOUT_ROW, M, xl.shape[1], d, b_cols=d,
                    add=_pad_cols(g, xl.shape[1]))
-        dW = torch.empty(d, d, dtype=torch.float32, device=g.device)
-        db = torch.empty(d, dtype=torch.float32, device=g.device) if ctx.has_bias else None
-        gemm(dz, _mrec.LAYOUT_COL, xl, _mrec.LAYOUT_COL, d, d, M, ones_out=db, out=dW)
+        dW = db = None
+        lr = sgd_lr(ctx.weight, ctx.bias)
+        if lr is not None:
+            gemm(dz, _mrec.LAYOUT_COL, xl, _mrec.LAYOUT_COL, d, d, M,
+                 ones_out=ctx.bias.detach() if ctx.has_bias else None, out=ctx.weight.detach(),
+                 out_dtype=torch.float32, sgd_lr=lr, img_row=ctx.wr, img_tr=ctx.wt)
+        else:
+            dW = torch.empty(d, d, dtype=torch.float32, device=g.device)
+            db = torch.empty(d, dtype=torch.float32, device=g.device) if ctx.has_bias else None
+            gemm(dz, _mrec.LAYOUT_COL, xl, _mrec.LAYOUT_COL, d, d, M, ones_out=db, out=dW)
         dx0 = (g.float() * z.float()).to(_BF16)
         if x0.shape[1] > d:
             dx0 = F.pad(dx0, (0, x0.shape[1] - d))
@@ -260,22 +313,27 @@ def din_attention(q: torch.Tensor, k: torch.Tensor, valid: torch.Tensor, att_mlp
     return (a.unsqueeze(-1) * k.float()).sum(1)
 
 
-def colsum(s: torch.Tensor, X: Optional[torch.Tensor], want_total: bool = True):
-    """(sum_b s[b] X[b, :], sum_b s[b]) with libmrec's deterministic column sum."""
+def colsum(s: torch.Tensor, X: Optional[torch.Tensor], want_total: bool = True, *,
+           out: Optional[torch.Tensor] = None, total: Optional[torch.Tensor] = None,
+           sgd_lr: Optional[float] = None):
+    """(sum_b s[b] X[b, :], sum_b s[b]) with libmrec's deterministic column sum.
+    With ``sgd_lr`` the sums are applied in place as SGD to ``out`` / ``total``
+    (parameters) instead: p -= lr * sum."""
     s = s.contiguous().float()
     C = 0 if X is None else X.shape[1]
     dev = s.device
-    out = torch.empty(C, dtype=torch.float32, device=dev)
-    tot = torch.empty(1, dtype=torch.float32, device=dev) if want_total else None
-    wsb = _mrec.lib().mrec_colsum_workspace_size(C)
-    ws = torch.empty(wsb, dtype=torch.uint8, device=dev)
+    if out is None and C:
+        out = torch.empty(C, dtype=torch.float32, device=dev)
+    if total is None and want_total:
+        total = torch.empty(1, dtype=torch.float32, device=dev)
     if X is not None and X.stride(1) != 1:
         X = X.contiguous()
     _mrec.call("mrec_colsum", s.data_ptr(), _mrec.ptr(X),
                _mrec.dtype_code(X.dtype) if X is not None else _mrec.F32,
-               X.stride(0) if X is not None else 0, s.shape[0], C, out.data_ptr(), _mrec.ptr(tot),
-               ws.data_ptr(), wsb, _mrec.stream_handle())
-    return out, tot
+               X.stride(0) if X is not None else 0, s.shape[0], C, _mrec.ptr(out),
+               _mrec.ptr(total) if want_total else None, int(sgd_lr is not None),
+               float(sgd_lr or 0.0), _mrec.stream_handle())
+    return out, (total if want_total else None)
 
 
 class _HeadFn(torch.autograd.Function):
@@ -293,6 +351,7 @@ class _HeadFn(torch.autograd.Function):
                    _mrec.ptr(base_c), z.data_ptr(), _mrec.stream_handle())
         ctx.save_for_backward(h, w)
         ctx.has_bias, ctx.has_base, ctx.h_relu = bias is not None, base is not None, h_relu
+        ctx.weight, ctx.bias = weight, bias
         return z
 
     @staticmethod
@@ -308,8 +367,15 @@ class _HeadFn(torch.autograd.Function):
                        dh.stride(0), _mrec.stream_handle())
             if ctx.h_relu:
                 _stamp(dh, h)
-        dW, db = colsum(dz, h, want_total=ctx.has_bias)
-        return dh, dW.reshape(1, H), db, (dz if ctx.has_base else None), None
+        lr = sgd_lr(ctx.weight, ctx.bias)
+        if lr is not None and ctx.weight.is_contiguous():
+            colsum(dz, h, want_total=ctx.has_bias, out=ctx.weight.detach().view(-1),
+                   total=ctx.bias.detach() if ctx.has_bias else None, sgd_lr=lr)
+            dW = db = None
+        else:
+            dW, db = colsum(dz, h, want_total=ctx.has_bias)
+            dW = dW.reshape(1, H)
+        return dh, dW, db, (dz if ctx.has_base else None), None
 
 
 def head(h: torch.Tensor, weight: torch.Tensor, bias: Optional[torch.Tensor],
@@ -320,3 +386,100 @@ def head(h: torch.Tensor, weight: torch.Tensor, bias: Optional[torch.Tensor],
         z = F.linear(h.float(), weight.float(), None if bias is None else bias.float()).reshape(-1)
         return z if base is None else z + base.float()
     return _HeadFn.apply(h, weight, bias, base, _is_relu_out(h))
+
+
+# ----------------------------------------------------------------------------
+# fused CTR head + BCE loss (the train step's last layer and its loss)
+# ----------------------------------------------------------------------------
+
+_TICKETS = {}
+_ONES = {}
+
+
+def _ticket(dev) -> torch.Tensor:
+    t = _TICKETS.get(dev)
+    if t is None:
+        t = torch.zeros(1, dtype=torch.int32, device=dev)  # zero once; kernels leave it zero
+        _TICKETS[dev] = t
+    return t
+
+
+def grad_one(dev) -> torch.Tensor:
+    """Persistent scalar 1.0 used as the loss gradient (no fill kernel per step, and
+    lets the fused head skip scaling its stashed gradients)."""
+    t = _ONES.get(dev)
+    if t is None:
+        t = torch.ones((), dtype=torch.float32, device=dev)
+        _ONES[dev] = t
+    return t
+
+
+class _CTRHeadBCEFn(torch.autograd.Function):
+    """loss = BCEWithLogits(base + h W^T + b, y) (mean) for a Linear(H, 1) head.
+    The forward kernel also produces dh, dz and the dW / db partials; the backward
+    only reduces the partials (fused SGD of W, b when compiled with plain SGD)."""
+
+    @staticmethod
+    def forward(ctx, h, weight, bias, base, y, h_relu: bool):
+        h = _bf16_rows(h)
+        B, H = h.shape
+        dev = h.device
+        w = _weight_f32(weight).reshape(-1)
+        b = bias.detach().float() if bias is not None else None
+        base_c = base.detach().float().contiguous() if base is not None else None
+        y = y.detach().float().contiguous()
+        z = torch.empty(B, dtype=torch.float32, device=dev)
+        dz = torch.empty(B, dtype=torch.float32, device=dev)
+        dh = _alloc(B, H, _BF16, dev)
+        nparts = int(_mrec.lib().mrec_ctr_head_parts(B))
+        ldp = _r8(H + 1)
+        part = torch.empty(nparts, ldp, dtype=torch.float32, device=dev)
+        loss_part = torch.empty(nparts, dtype=torch.float32, device=dev)
+        loss = torch.empty(1, dtype=torch.float32, device=dev)
+        _mrec.call("mrec_ctr_head_fwd", h.data_ptr(), h.stride(0), B, H, w.data_ptr(),
+                   _mrec.ptr(b), _mrec.ptr(base_c), y.data_ptr(), int(bool(h_relu)),
+                   z.data_ptr(), dz.data_ptr(), dh.data_ptr(), dh.stride(0), part.data_ptr(), ldp,
+                   loss_part.data_ptr(), _ticket(dev).data_ptr(), loss.data_ptr(),
+                   _mrec.stream_handle())
+        if h_relu:
+            _stamp(dh, h)
+        ctx.save_for_backward(part, dz, dh)
+        ctx.weight, ctx.bias, ctx.H, ctx.B, ctx.has_base = weight, bias, H, B, base is not None
+        ctx.mark_non_differentiable(z)
+        ctx.set_materialize_grads(False)  # no zero-filled gradient for z
+        return loss.reshape(()), z
+
+    @staticmethod
+    def backward(ctx, gloss, gz=None):
+        part, dz, dh = ctx.saved_tensors
+        dev = part.device
+        g = gloss.detach().float().reshape(1).contiguous()
+        one = g.data_ptr() == grad_one(dev).data_ptr()
+        lr = sgd_lr(ctx.weight, ctx.bias)
+        dW = db = None
+        if lr is not None and ctx.weight.is_contiguous():
+            _mrec.call("mrec_ctr_head_finish", part.data_ptr(), part.stride(0), ctx.B, ctx.H,
+                       None if one else g.data_ptr(), 1, lr, ctx.weight.detach().data_ptr(),
+                       _mrec.ptr(ctx.bias.detach() if ctx.bias is not None else None), None,
+                       None, _mrec.stream_handle())
+        else:
+            dW = torch.empty(1, ctx.H, dtype=torch.float32, device=dev)
+            db = torch.empty(1, dtype=torch.float32, device=dev) if ctx.bias is not None else None
+            _mrec.call("mrec_ctr_head_finish", part.data_ptr(), part.stride(0), ctx.B, ctx.H,
+                       g.data_ptr(), 0, 0.0, None, None, dW.data_ptr(), _mrec.ptr(db),
+                       _mrec.stream_handle())
+        if not one:
+            dh = (dh.float() * g).to(_BF16)
+            dz = dz * g
+        return dh, dW, db, (dz if ctx.has_base else None), None, None
+
+
+def ctr_head_bce(h: torch.Tensor, weight: torch.Tensor, bias: Optional[torch.Tensor],
+                 base: Optional[torch.Tensor], y: torch.Tensor):
+    """(loss, z): mean BCE-with-logits of z = base + h W^T + b against y — the CTR
+    models' output layer and loss in one kernel (GPU, training) — else the plain
+    ``head`` + torch loss."""
+    if h.is_cuda and torch.is_grad_enabled() and h.shape[1] <= 1024:
+        return _CTRHeadBCEFn.apply(h, weight, bias, base, y, _is_relu_out(h))
+    z = head(h, weight, bias, base)
+    return F.binary_cross_entropy_with_logits(z.float(), y.float()), z

@@ -363,6 +363,7 @@ class _InteractFn(torch.autograd.Function):
         ctx.save_for_backward(x0, fm_sum, dense)
         ctx.has_dense_w = dense_w is not None
         ctx.has_bias = bias is not None
+        ctx.dense_w, ctx.bias = dense_w, bias
         if x0 is None:
             return logit
         return x0, logit
@@ -385,14 +386,25 @@ class _InteractFn(torch.autograd.Function):
         if bank.update == "sgd" or bank.weight.requires_grad:
             grad = _backward_into_bank(bank, ctx.ids, ctx.B, ctx.plan_ws, dx=dx0, dfm=dfm,
                                        fm_sum=fm_sum, x0=x0 if dfm is not None else None, dw=dw)
-        g_dense_w = g_bias = None
-        if dlogit is not None and (ctx.has_dense_w or ctx.has_bias):
-            from pytorchrec_amd.dense import colsum
-            X = dense if (ctx.has_dense_w and dense is not None) else None
-            gw, gb = colsum(dlogit, X, want_total=ctx.has_bias)
-            g_dense_w = gw if X is not None else None
-            g_bias = gb
+        g_dense_w, g_bias = _dense_first_order_grads(ctx, dlogit, dense)
         return grad, g_dense_w, g_bias, None, None, None, None, None, None, None, None
+
+
+def _dense_first_order_grads(ctx, dlogit, dense):
+    """Gradients of the dense first-order weight and the global bias (column sums of
+    dlogit), or — when both train by fused SGD — their in-place update."""
+    if dlogit is None or not (ctx.has_dense_w or ctx.has_bias):
+        return None, None
+    from pytorchrec_amd.dense import colsum, sgd_lr
+    X = dense if (ctx.has_dense_w and dense is not None) else None
+    lr = sgd_lr(ctx.dense_w if X is not None else None, ctx.bias)
+    if lr is not None:
+        colsum(dlogit, X, want_total=ctx.has_bias,
+               out=ctx.dense_w.detach() if X is not None else None,
+               total=ctx.bias.detach() if ctx.has_bias else None, sgd_lr=lr)
+        return None, None
+    gw, gb = colsum(dlogit, X, want_total=ctx.has_bias)
+    return (gw if X is not None else None), gb
 
 
 def interact(bank: EmbeddingBank, ids: Sequence[torch.Tensor], dense: Optional[torch.Tensor] = None,

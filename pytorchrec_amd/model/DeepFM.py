@@ -155,10 +155,20 @@ class DeepFM(_CTRBase):
             self.mlp.to(dev)
             self.prediction.to(dev)
 
-    def forward(self, data: Dict[str, Tensor]):
+    def _deep(self, data: Dict[str, Tensor]):
         x0, logit = interact(self.embeddings, self._ids(data), self._dense(data),
                              self.dense_weight, self.global_bias, fm2=True, first_order=True,
                              x0_cols=self.x0_cols, x0_dtype=self._x0_dtype())
-        h = self.mlp(x0)
+        return self.mlp(x0), logit
+
+    def forward(self, data: Dict[str, Tensor]):
+        h, logit = self._deep(data)
         prediction = dense_ops.head(h, self.prediction.weight, self.prediction.bias, base=logit)
         return prediction, self._target(data)
+
+    def fused_bce_loss(self, data: Dict[str, Tensor]):
+        """Training loss (BCE with logits, mean) with the output layer fused into it."""
+        h, logit = self._deep(data)
+        loss, _ = dense_ops.ctr_head_bce(h, self.prediction.weight, self.prediction.bias, logit,
+                                         self._target(data))
+        return loss

@@ -114,6 +114,7 @@ class IModel(Module, IWithArguments, ABC):
         self.compiled_device = device
         self.to(device)
         self._configure_embedding_update(optimizer)
+        self._configure_dense_update(optimizer)
         self._is_compiled = True
 
     def embedding_banks(self):
@@ -144,6 +145,26 @@ class IModel(Module, IWithArguments, ABC):
             elif group is not None or bank.update != "sgd":
                 bank.use_dense_grad()
 
+    def _configure_dense_update(self, optimizer: Optimizer):
+        """Plain SGD on one process: every dense parameter is updated inside its own
+        backward kernel (weight-gradient GEMM / column-sum epilogue), which also
+        refreshes the bf16 weight images — no gradient tensors, no optimizer or
+        conversion kernels.  Identical to torch.optim.SGD(lr) for these groups.
+        Data-parallel training keeps the gradients (they must be all-reduced first)."""
+        comm = getattr(self, "dp_comm", None)
+        dp = comm is not None and (comm.world > 1 or comm.force)
+        for p in self.parameters():
+            if hasattr(p, "_mrec_sgd_group"):
+                del p._mrec_sgd_group
+        if dp or not isinstance(optimizer, torch.optim.SGD):
+            return
+        for g in optimizer.param_groups:
+            if (g.get("momentum", 0) == 0 and g.get("weight_decay", 0) == 0
+                    and not g.get("nesterov", False) and not g.get("maximize", False)
+                    and g.get("dampening", 0) == 0):
+                for p in g["params"]:
+                    p._mrec_sgd_group = g
+
     # -- data parallel (one process per GPU; SURVEY.md §8e) ------------------------
     def distribute(self, comm):
         """Make this replica data-parallel over ``comm`` (a sharding.ShardComm):
@@ -154,6 +175,8 @@ class IModel(Module, IWithArguments, ABC):
         with torch.no_grad():
             for p in self._dp_params():
                 comm.broadcast_(p.data)
+        if self._is_compiled:
+            self._configure_dense_update(self.compiled_optimizers)
         return self
 
     def _dp_params(self):
@@ -178,15 +201,33 @@ class IModel(Module, IWithArguments, ABC):
     def train_step(self, data: Dict):
         self.train()
         data = tensor_to_device(data, self.compiled_device)
-        prediction, target = self(data)
-        loss = self.compiled_loss(prediction, target)
-        self.compiled_optimizers.zero_grad()
-        loss.backward()
+        fused = self._fused_loss_fn()
+        if fused is not None:
+            # output layer + loss (+ their gradients) in one kernel; same math as
+            # self(data) followed by compiled_loss (BCEWithLogits, mean)
+            loss = fused(data)
+            self.compiled_optimizers.zero_grad()
+            from pytorchrec_amd.dense import grad_one
+            loss.backward(grad_one(loss.device))
+        else:
+            prediction, target = self(data)
+            loss = self.compiled_loss(prediction, target)
+            self.compiled_optimizers.zero_grad()
+            loss.backward()
         comm = getattr(self, "dp_comm", None)
         if comm is not None and (comm.world > 1 or comm.force):
             self._allreduce_dense_grads()
         self.compiled_optimizers.step(closure=None)
         return {"loss": loss}
+
+    def _fused_loss_fn(self):
+        """A model may provide ``fused_bce_loss(data)`` (the CTR models do); it is
+        used when the compiled loss is BCEWithLogitsLoss."""
+        from pytorchrec_amd.loss import BCEWithLogitsLoss
+        fn = getattr(self, "fused_bce_loss", None)
+        if fn is None or not isinstance(self.compiled_loss, BCEWithLogitsLoss):
+            return None
+        return fn
 
     def test_step(self, data):
         self.eval()

@@ -37,7 +37,8 @@ import torch
 import torch.distributed as dist
 
 from pytorchrec_amd import _mrec
-from pytorchrec_amd.embedding import EmbeddingBank, _AsyncPlanBase, _side_stream, _trigger
+from pytorchrec_amd.embedding import (EmbeddingBank, _AsyncPlanBase, _dense_first_order_grads,
+                                      _side_stream, _trigger)
 
 
 # ----------------------------------------------------------------------------
@@ -312,6 +313,7 @@ class _ShardedInteractFn(torch.autograd.Function):
         ctx.bank, ctx.B, ctx.plan = bank, B, plan
         ctx.fm2, ctx.first_order = fm2, first_order
         ctx.has_dense_w, ctx.has_bias = dense_w is not None, bias is not None
+        ctx.dense_w, ctx.bias = dense_w, bias
         ctx.save_for_backward(x0, fm_sum, dense, pos)
         if x0 is None:
             return logit
@@ -336,13 +338,7 @@ class _ShardedInteractFn(torch.autograd.Function):
                                        x0=x0 if dfm is not None else None, dw=dw)
             g_recv = bank.comm.exchange(g_send)
             owner_apply(bank, ctx.plan.get(), g_recv, bank.current_lr() / bank.world)
-        g_dense_w = g_bias = None
-        if dlogit is not None and (ctx.has_dense_w or ctx.has_bias):
-            from pytorchrec_amd.dense import colsum
-            X = dense if (ctx.has_dense_w and dense is not None) else None
-            gw, gb = colsum(dlogit, X, want_total=ctx.has_bias)
-            g_dense_w = gw if X is not None else None
-            g_bias = gb
+        g_dense_w, g_bias = _dense_first_order_grads(ctx, dlogit, dense)
         return g_dense_w, g_bias, None, None, None, None, None, None, None, None
 
 

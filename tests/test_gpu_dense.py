@@ -243,3 +243,100 @@ def test_deepfm_train_step_matches_oracle_model(gpu):
         dw_got = m.embeddings.first_order(f).detach().double().cpu() - before_w[f]
         dw_want = r.w1[f].weight.detach()[:, 0] - before_w[f]
         assert float((dw_got - dw_want).abs().max()) <= 0.02 * (float(dw_want.abs().max()) + 1e-12)
+
+
+def test_fused_sgd_linear_matches_torch_sgd(gpu):
+    """Plain SGD fused into the weight-gradient GEMM (IModel.compile marks the
+    parameters): W -= lr dW, b -= lr db and refreshed bf16 images, against
+    torch.optim.SGD applied to the gradients of the unfused path."""
+    from pytorchrec_amd import dense as D
+    from pytorchrec_amd.model.layer import MLP
+    torch.manual_seed(0)
+    a = MLP(96, [64, 48], "relu", 0.0).to(gpu)
+    b = MLP(96, [64, 48], "relu", 0.0).to(gpu)
+    b.load_state_dict(a.state_dict())
+    lr = 0.1
+    group = {"lr": lr}
+    for p in b.parameters():
+        p._mrec_sgd_group = group
+    x = torch.randn(300, 96, device=gpu).to(torch.bfloat16)
+    dout = torch.randn(300, 48, device=gpu).to(torch.bfloat16)
+    for _ in range(2):
+        a(x).backward(dout)
+        with torch.no_grad():
+            for p in a.parameters():
+                p -= lr * p.grad
+                p.grad = None
+        b(x).backward(dout)
+    for (k, pa), pb in zip(a.state_dict().items(), b.state_dict().values()):
+        assert pb.grad is None if hasattr(pb, "grad") else True
+        np.testing.assert_allclose(pb.cpu().numpy(), pa.cpu().numpy(), rtol=1e-5, atol=1e-6,
+                                   err_msg=k)
+    for m in b.modules():
+        if isinstance(m, torch.nn.Linear):
+            wr, wt = D.weight_images(m.weight)
+            wr2, wt2 = D.weight_prep(m.weight)
+            assert torch.equal(wr, wr2) and torch.equal(wt, wt2)
+
+
+def test_colsum_and_fused_update(gpu):
+    from pytorchrec_amd import dense as D
+    g = torch.Generator().manual_seed(2)
+    B, H = 4096, 400
+    s = torch.randn(B, generator=g).to(gpu)
+    X = D._alloc(B, H, torch.bfloat16, gpu)
+    X.copy_(torch.randn(B, H, generator=g).to(torch.bfloat16))
+    out, tot = D.colsum(s, X)
+    want = (s.double()[:, None] * X.double()).sum(0)
+    np.testing.assert_allclose(out.cpu().numpy(), want.cpu().numpy(), rtol=1e-4, atol=1e-3)
+    np.testing.assert_allclose(tot.item(), s.double().sum().item(), rtol=1e-5, atol=1e-4)
+    out2, tot2 = D.colsum(s, X)
+    assert torch.equal(out, out2) and torch.equal(tot, tot2)  # deterministic
+    dense = torch.rand(B, 13, generator=g).to(gpu)  # fp32, unaligned rows
+    o3, _ = D.colsum(s, dense, want_total=False)
+    np.testing.assert_allclose(o3.cpu().numpy(), (s.double()[:, None] * dense.double()).sum(0).cpu().numpy(),
+                               rtol=1e-4, atol=1e-3)
+    w = torch.randn(13, device=gpu)
+    b = torch.randn(1, device=gpu)
+    w0, b0 = w.clone(), b.clone()
+    D.colsum(s, dense, want_total=True, out=w, total=b, sgd_lr=0.5)
+    torch.testing.assert_close(w, w0 - 0.5 * o3, rtol=1e-5, atol=1e-5)
+    torch.testing.assert_close(b, b0 - 0.5 * tot, rtol=1e-5, atol=1e-5)
+
+
+@pytest.mark.parametrize("gscale", [1.0, 0.37])
+def test_ctr_head_bce_fused_matches_torch(gpu, gscale):
+    """Fused Linear(H,1) + BCEWithLogits (mean): loss, logits and every gradient
+    against torch fp64 on the same bf16 h (ReLU-masked dh)."""
+    from pytorchrec_amd import dense as D
+    g = torch.Generator().manual_seed(11)
+    B, H = 1000, 400
+    hraw = torch.relu(torch.randn(B, H, generator=g)).to(torch.bfloat16)
+    h = D._alloc(B, H, torch.bfloat16, gpu)
+    h.copy_(hraw)
+    setattr(h, D._RELU_OUT, True)
+    W = (torch.randn(1, H, generator=g) * 0.05).to(gpu).requires_grad_()
+    b = torch.randn(1, generator=g).to(gpu).requires_grad_()
+    base = torch.randn(B, generator=g).to(gpu).requires_grad_()
+    y = (torch.rand(B, generator=g) < 0.3).float().to(gpu)
+    hh = h.detach().clone().requires_grad_()
+    setattr(hh, D._RELU_OUT, True)
+    loss, z = D.ctr_head_bce(hh, W, b, base, y)
+    gl = D.grad_one(gpu) if gscale == 1.0 else torch.tensor(gscale, device=gpu)
+    loss.backward(gl)
+    Wr = W.detach().double().requires_grad_()
+    br = b.detach().double().requires_grad_()
+    baser = base.detach().double().requires_grad_()
+    hr = hraw.double().to(gpu).requires_grad_()
+    zr = baser + hr @ Wr.T.reshape(-1) + br
+    lr_ = torch.nn.functional.binary_cross_entropy_with_logits(zr, y.double())
+    (lr_ * gscale).backward()
+    torch.testing.assert_close(z.double(), zr.detach(), rtol=1e-5, atol=1e-5)
+    torch.testing.assert_close(loss.double(), lr_.detach(), rtol=1e-5, atol=1e-6)
+    torch.testing.assert_close(W.grad.double(), Wr.grad, rtol=1e-4, atol=1e-6)
+    torch.testing.assert_close(b.grad.double(), br.grad, rtol=1e-4, atol=1e-7)
+    torch.testing.assert_close(base.grad.double(), baser.grad, rtol=1e-5, atol=1e-9)
+    want_dh = hr.grad * (hr.detach() > 0)
+    # one bf16 rounding of dh; a second one when a non-unit loss gradient rescales it
+    tol = 2 ** -8 if gscale == 1.0 else 2 ** -7
+    torch.testing.assert_close(hh.grad.double(), want_dh, rtol=tol, atol=1e-7)

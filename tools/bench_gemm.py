@@ -74,6 +74,9 @@ def main():
         "dx": lambda: dyb @ wb,
         "dw": lambda: dyb.t() @ xb,
     }
+    for sk in (1, 2, 4, 8):
+        cases[f"dw/s{sk}"] = (lambda sk=sk: D.gemm(dy, _mrec.LAYOUT_COL, x, _mrec.LAYOUT_COL, N, K, M,
+                                                   ones_out=db, out=dW, split_k=sk))
     for name, fn in cases.items():
         if a.only and name != a.only:
             continue

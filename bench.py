@@ -3,16 +3,17 @@
 
     python bench.py [--gpus N] [--steps K] [--warmup W] [--model deepfm|dcnv2|din]
 
-One step = one full training step (interact fwd -> MLP fwd -> BCE -> MLP bwd ->
-embedding sorted-segment backward with the SGD update fused -> SGD on the dense
-params) over one synthetic Criteo-shaped batch that is already
-resident in HBM.  The step is captured once in a HIP graph and replayed; before
-each replay the next of 4 pre-generated batches is copied into the graph's input
-buffer (one D2D copy, inside the timed region).
+One step = one full training step (interact fwd -> MLP fwd -> head + BCE ->
+MLP bwd -> embedding sorted-segment backward, with SGD fused into every
+parameter's backward kernel) over one synthetic Criteo-shaped batch (SURVEY.md
+§8(d)) that is already resident in HBM.  The step is captured as a HIP graph per
+pre-generated batch (4 batches, used in place) and the graphs are replayed in turn.
 
-For N > 1 the driver launches one process per GPU (torch.distributed.run); each
-rank trains on its own 4096 samples (weak scaling) and the MAX elapsed time over
-ranks is reported.  Rank 0 prints ONE JSON line.
+For N > 1 the driver launches one process per GPU (torch.distributed.run); the
+tables are row-sharded over the ranks and the dense tower is data-parallel
+(RCCL all-to-all / all-reduce inside the captured step); each rank trains on its
+own 4096 samples (weak scaling) and the MAX elapsed time over ranks is reported.
+Rank 0 prints ONE JSON line.
 """
 from __future__ import annotations
 
@@ -276,40 +277,39 @@ def main():
     assert model.embeddings.update == "sgd", "SGD must fuse into the embedding backward"
 
     bufs = [make_batch_buffer(args, sparse, 1000 * rank + s, device) for s in range(4)]
-    static = bufs[0].clone()
-    data = batch_views(static, args, sparse, dense_cols, label_col)
+    datas = [batch_views(b, args, sparse, dense_cols, label_col) for b in bufs]
 
-    def step():
-        return model.train_step(data)["loss"]
+    def step(d):
+        return model.train_step(d)["loss"]
 
-    if args.no_graph:
-        def run(i):
-            static.copy_(bufs[i % 4])
-            step()
-    else:
+    graphs = None
+    if not args.no_graph:
+        # one graph per resident batch (inputs used in place: no staging copy)
         s = torch.cuda.Stream()
         s.wait_stream(torch.cuda.current_stream())
         with torch.cuda.stream(s):
-            for _ in range(3):
-                step()
+            for k in range(3):
+                step(datas[k % 4])
         torch.cuda.current_stream().wait_stream(s)
-        graph = torch.cuda.CUDAGraph()
         try:
-            with torch.cuda.graph(graph):
-                step()
+            graphs = []
+            for d in datas:
+                g = torch.cuda.CUDAGraph()
+                with torch.cuda.graph(g):
+                    step(d)
+                graphs.append(g)
         except Exception as e:  # e.g. a collective the runtime cannot capture
             print(f"bench: HIP graph capture failed ({type(e).__name__}: {e}); running eagerly",
                   file=sys.stderr, flush=True)
             args.no_graph = True
             torch.cuda.synchronize()
-            graph = None
+            graphs = None
 
-        def run(i):
-            static.copy_(bufs[i % 4])
-            if graph is None:
-                step()
-            else:
-                graph.replay()
+    def run(i):
+        if graphs is None:
+            step(datas[i % 4])
+        else:
+            graphs[i % 4].replay()
 
     for i in range(args.warmup):
         run(i)
@@ -357,7 +357,7 @@ def main():
                    "hip_graph": not args.no_graph},
     }
     if rank == 0 and not args.no_roofline:
-        ks = kernel_rooflines(model, data, args)
+        ks = kernel_rooflines(model, datas[0], args)
         # achieved = sum of algorithmic bytes of the HBM-bound
         # embedding-path kernels / sum of their measured launch durations
         t = sum(v[0] for v in ks.values())

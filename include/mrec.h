@@ -366,28 +366,33 @@ mrec_status mrec_bce_bwd(const float *z, const float *y, int64_t batch, const fl
 /*
  * Fused CTR head + BCE-with-logits (forward AND the loss gradient, one pass over h;
  * the train step of a Linear(H, 1) output layer on a ReLU MLP, the mean BCE loss):
- *   z[b]  = base[b] + bias + h[b] . w                   (prediction logit)
- *   dz[b] = (sigmoid(z[b]) - y[b]) / batch               (d mean-loss / d z)
- *   dh[b, :] = dz[b] * w * (relu_mask ? h[b, :] > 0 : 1)  (bf16, pad columns 0)
+ *   z[b]  = base[b] + bias + h[b] . w + xs[b, :ns] . ws + b2   (prediction logit;
+ *           xs / ws / b2: an optional side linear term such as DeepFM's dense
+ *           first-order weight and global bias, ns <= 64)
+ *   dz[b] = (sigmoid(z[b]) - y[b]) / batch                       (d mean-loss / d z)
+ *   dh[b, :] = dz[b] * w * (relu_mask ? h[b, :] > 0 : 1)          (bf16, pad columns 0)
  *   *loss = mean_b (max(z,0) - z y + log1p(exp(-|z|)))
- * and per-workgroup partials of dW = sum_b dz[b] h[b, :] and db = sum_b dz[b] in
- * part[mrec_ctr_head_parts(batch)][ldp >= H + 1].  The loss is reduced in the same
- * launch through loss_part[parts] and a ticket (*ticket must be 0 on entry and is
- * left 0).  H <= 1024, h / dh rows 16-byte aligned.
+ * and per-workgroup partials [dW (H) | sum dz | dws (ns)] in
+ * part[mrec_ctr_head_parts(batch)][ldp >= H + 1 + ns].  The loss is reduced in the
+ * same launch through loss_part[parts] and a ticket (*ticket must be 0 on entry and
+ * is left 0).  H <= 1024, h / dh rows 16-byte aligned.
  * mrec_ctr_head_finish sums the partials in fixed order and, scaled by the
- * upstream gradient *g (NULL = 1), applies SGD (update: w -= lr g dW, bias -= lr g db)
- * or writes dw_out / db_out.  Replaces Linear(H,1) + BCEWithLogitsLoss forward and
- * backward (NCF.py:51,74 head; losses.py:8-12 lacks BCE).
+ * upstream gradient *g (NULL = 1), applies SGD (update: w -= lr g dW, ws -= lr g dws,
+ * bias and b2 -= lr g sum dz) or writes dw_out / db_out / dws_out / db2_out.
+ * Replaces Linear(H,1) + BCEWithLogitsLoss forward and backward (NCF.py:51,74 head;
+ * losses.py:8-12 lacks BCE).
  */
 int64_t mrec_ctr_head_parts(int64_t batch);
 mrec_status mrec_ctr_head_fwd(const void *h, int64_t ldh, int64_t batch, int32_t H, const float *w,
                               const float *bias, const float *base, const float *y,
-                              int32_t relu_mask, float *z, float *dz, void *dh, int64_t lddh,
-                              float *part, int64_t ldp, float *loss_part, uint32_t *ticket,
-                              float *loss, mrec_stream stream);
+                              const float *xs, int64_t ldxs, int32_t ns, const float *ws,
+                              const float *b2, int32_t relu_mask, float *z, float *dz, void *dh,
+                              int64_t lddh, float *part, int64_t ldp, float *loss_part,
+                              uint32_t *ticket, float *loss, mrec_stream stream);
 mrec_status mrec_ctr_head_finish(const float *part, int64_t ldp, int64_t batch, int32_t H,
-                                 const float *g, int32_t update, float lr, float *w, float *bias,
-                                 float *dw_out, float *db_out, mrec_stream stream);
+                                 int32_t ns, const float *g, int32_t update, float lr, float *w,
+                                 float *bias, float *ws, float *b2, float *dw_out, float *db_out,
+                                 float *dws_out, float *db2_out, mrec_stream stream);
 
 /*
  * out[c] = sum_b s[b] X[b, c] for c < C, and *total = sum_b s[b] (if total != NULL):

@@ -133,10 +133,11 @@ SIGNATURES = {
     "mrec_bce_fwd": (ctypes.c_int, [_vp, _vp, _i64, _vp, _vp]),
     "mrec_bce_bwd": (ctypes.c_int, [_vp, _vp, _i64, _vp, _vp, _vp]),
     "mrec_ctr_head_parts": (ctypes.c_int64, [_i64]),
-    "mrec_ctr_head_fwd": (ctypes.c_int, [_vp, _i64, _i64, _i32, _vp, _vp, _vp, _vp, _i32, _vp, _vp,
-                                         _vp, _i64, _vp, _i64, _vp, _vp, _vp, _vp]),
-    "mrec_ctr_head_finish": (ctypes.c_int, [_vp, _i64, _i64, _i32, _vp, _i32, _f32, _vp, _vp, _vp,
-                                            _vp, _vp]),
+    "mrec_ctr_head_fwd": (ctypes.c_int, [_vp, _i64, _i64, _i32, _vp, _vp, _vp, _vp, _vp, _i64,
+                                         _i32, _vp, _vp, _i32, _vp, _vp, _vp, _i64, _vp, _i64,
+                                         _vp, _vp, _vp, _vp]),
+    "mrec_ctr_head_finish": (ctypes.c_int, [_vp, _i64, _i64, _i32, _i32, _vp, _i32, _f32, _vp, _vp,
+                                            _vp, _vp, _vp, _vp, _vp, _vp, _vp]),
     "mrec_colsum": (ctypes.c_int, [_vp, _vp, ctypes.c_int, _i64, _i64, _i64, _vp, _vp, _i32,
                                    _f32, _vp]),
 }

@@ -177,15 +177,18 @@ constexpr int HEAD_MAXH = 1024;                 // h width handled (2 chunks of 
 __global__ __launch_bounds__(256) void ctr_head_kernel(
     const uint16_t *__restrict__ h, int64_t ldh, int64_t B, int H, const float *__restrict__ w,
     const float *__restrict__ bias, const float *__restrict__ base, const float *__restrict__ y,
-    int relu, float *__restrict__ z, float *__restrict__ dz, uint16_t *__restrict__ dh,
-    int64_t lddh, float *__restrict__ part, int64_t ldp, float *__restrict__ loss_part,
-    unsigned *__restrict__ ticket, float *__restrict__ loss) {
-  __shared__ float red[4][HEAD_MAXH + 4];
+    const float *__restrict__ xs, int64_t ldxs, int ns, const float *__restrict__ ws,
+    const float *__restrict__ b2, int relu, float *__restrict__ z, float *__restrict__ dz,
+    uint16_t *__restrict__ dh, int64_t lddh, float *__restrict__ part, int64_t ldp,
+    float *__restrict__ loss_part, unsigned *__restrict__ ticket, float *__restrict__ loss) {
+  __shared__ float red[4][HEAD_MAXH + 1 + 64];
   __shared__ float sred[4][2];
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
   const int64_t r0 = (static_cast<int64_t>(blockIdx.x) * 4 + wv) * HEAD_RPW;
   const float invB = 1.f / static_cast<float>(B);
-  const float b0 = bias ? bias[0] : 0.f;
+  const float b0 = (bias ? bias[0] : 0.f) + (b2 ? b2[0] : 0.f);
+  const float wsl = lane < ns ? ws[lane] : 0.f;  // side linear: lane j holds ws[j] (ns <= 64)
+  float sacc = 0.f;
   constexpr int NC = HEAD_MAXH / 512;  // chunks of 8 per lane
   float wr[NC][8], acc[NC][8];
 #pragma unroll
@@ -215,11 +218,14 @@ __global__ __launch_bounds__(256) void ctr_head_kernel(
 #pragma unroll
       for (int j = 0; j < 8; ++j) dot = fmaf(hv[q][j], wr[q][j], dot);
     }
+    const float xsv = lane < ns ? xs[r * ldxs + lane] : 0.f;
+    dot = fmaf(xsv, wsl, dot);
 #pragma unroll
     for (int off = 32; off > 0; off >>= 1) dot += __shfl_xor(dot, off);
     const float zz = dot + b0 + (base ? base[r] : 0.f);
     const float yy = y[r];
     const float d = (1.f / (1.f + __expf(-zz)) - yy) * invB;
+    sacc = fmaf(d, xsv, sacc);
     if (lane == 0) {
       z[r] = zz;
       dz[r] = d;
@@ -250,14 +256,15 @@ __global__ __launch_bounds__(256) void ctr_head_kernel(
     for (int j = 0; j < 8; ++j)
       if (c + j < H) red[wv][c + j] = acc[q][j];
   }
+  if (lane < ns) red[wv][H + 1 + lane] = sacc;
   if (lane == 0) {
     sred[wv][0] = dzs;
     sred[wv][1] = ls;
   }
   __syncthreads();
   float *prow = part + static_cast<int64_t>(blockIdx.x) * ldp;
-  for (int c = threadIdx.x; c < H; c += 256)
-    prow[c] = (red[0][c] + red[1][c]) + (red[2][c] + red[3][c]);
+  for (int c = threadIdx.x; c < H + 1 + ns; c += 256)
+    if (c != H) prow[c] = (red[0][c] + red[1][c]) + (red[2][c] + red[3][c]);
   __shared__ unsigned s_last;
   if (threadIdx.x == 0) {
     prow[H] = (sred[0][0] + sred[1][0]) + (sred[2][0] + sred[3][0]);
@@ -290,9 +297,11 @@ __global__ __launch_bounds__(256) void ctr_head_kernel(
 // sum the per-workgroup partials (fixed order) -> dW [H] and db; then either SGD on
 // (w, bias) with lr * g, or write g * dW / g * db
 __global__ __launch_bounds__(256) void ctr_head_finish_kernel(
-    const float *__restrict__ part, int64_t ldp, int nparts, int H, const float *__restrict__ gp,
-    int update, float lr, float *__restrict__ w, float *__restrict__ bias,
-    float *__restrict__ dw_out, float *__restrict__ db_out) {
+    const float *__restrict__ part, int64_t ldp, int nparts, int H, int ns,
+    const float *__restrict__ gp, int update, float lr, float *__restrict__ w,
+    float *__restrict__ bias, float *__restrict__ ws, float *__restrict__ b2,
+    float *__restrict__ dw_out, float *__restrict__ db_out, float *__restrict__ dws_out,
+    float *__restrict__ db2_out) {
   __shared__ float red[4][9];
   const int c0 = blockIdx.x * 8;
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
@@ -300,7 +309,7 @@ __global__ __launch_bounds__(256) void ctr_head_finish_kernel(
   for (int k = threadIdx.x; k < nparts; k += 256) {
 #pragma unroll
     for (int j = 0; j < 8; ++j)
-      if (c0 + j <= H) acc[j] += part[static_cast<int64_t>(k) * ldp + c0 + j];
+      if (c0 + j <= H + ns) acc[j] += part[static_cast<int64_t>(k) * ldp + c0 + j];
   }
 #pragma unroll
   for (int j = 0; j < 8; ++j) {
@@ -314,7 +323,7 @@ __global__ __launch_bounds__(256) void ctr_head_finish_kernel(
   __syncthreads();
   if (threadIdx.x < 8) {
     const int c = c0 + threadIdx.x;
-    if (c > H) return;
+    if (c > H + ns) return;
     const float g = gp ? gp[0] : 1.f;
     const float v = ((red[0][threadIdx.x] + red[1][threadIdx.x]) +
                      (red[2][threadIdx.x] + red[3][threadIdx.x])) * g;
@@ -323,12 +332,20 @@ __global__ __launch_bounds__(256) void ctr_head_finish_kernel(
         w[c] = fmaf(-lr, v, w[c]);
       else if (dw_out)
         dw_out[c] = v;
-    } else {
+    } else if (c == H) {  // both biases have gradient sum(dz)
       if (update) {
         if (bias) bias[0] = fmaf(-lr, v, bias[0]);
-      } else if (db_out) {
-        db_out[0] = v;
+        if (b2) b2[0] = fmaf(-lr, v, b2[0]);
+      } else {
+        if (db_out) db_out[0] = v;
+        if (db2_out) db2_out[0] = v;
       }
+    } else {
+      const int j = c - H - 1;
+      if (update)
+        ws[j] = fmaf(-lr, v, ws[j]);
+      else if (dws_out)
+        dws_out[j] = v;
     }
   }
 }
@@ -408,32 +425,37 @@ int64_t mrec_ctr_head_parts(int64_t batch) { return (batch + HEAD_RPB - 1) / HEA
 
 mrec_status mrec_ctr_head_fwd(const void *h, int64_t ldh, int64_t batch, int32_t H, const float *w,
                               const float *bias, const float *base, const float *y,
-                              int32_t relu_mask, float *z, float *dz, void *dh, int64_t lddh,
-                              float *part, int64_t ldp, float *loss_part, uint32_t *ticket,
-                              float *loss, mrec_stream stream) {
+                              const float *xs, int64_t ldxs, int32_t ns, const float *ws,
+                              const float *b2, int32_t relu_mask, float *z, float *dz, void *dh,
+                              int64_t lddh, float *part, int64_t ldp, float *loss_part,
+                              uint32_t *ticket, float *loss, mrec_stream stream) {
   MREC_CHECK_ARG(h && w && y && z && dz && dh && part && loss_part && ticket && loss,
                  "NULL pointer");
   MREC_CHECK_ARG(batch >= 1 && H >= 1 && H <= HEAD_MAXH && ldh >= H && lddh >= H, "bad shape");
   MREC_CHECK_ARG((reinterpret_cast<uintptr_t>(h) & 15) == 0 && ldh % 8 == 0 &&
                      (reinterpret_cast<uintptr_t>(dh) & 15) == 0 && lddh % 8 == 0,
                  "h / dh rows must be 16-byte aligned");
-  MREC_CHECK_ARG(ldp >= H + 1, "ldp < H + 1");
+  MREC_CHECK_ARG(ns >= 0 && ns <= 64 && (ns == 0 || (xs && ws && ldxs >= ns)),
+                 "side linear: 0 <= ns <= 64 with xs / ws");
+  MREC_CHECK_ARG(ldp >= H + 1 + ns, "ldp < H + 1 + ns");
   const int64_t nb = mrec_ctr_head_parts(batch);
   ctr_head_kernel<<<dim3(static_cast<unsigned>(nb)), 256, 0, static_cast<hipStream_t>(stream)>>>(
-      static_cast<const uint16_t *>(h), ldh, batch, H, w, bias, base, y, relu_mask, z, dz,
-      static_cast<uint16_t *>(dh), lddh, part, ldp, loss_part, ticket, loss);
+      static_cast<const uint16_t *>(h), ldh, batch, H, w, bias, base, y, xs, ldxs, ns, ws, b2,
+      relu_mask, z, dz, static_cast<uint16_t *>(dh), lddh, part, ldp, loss_part, ticket, loss);
   return launch_status("mrec_ctr_head_fwd");
 }
 
 mrec_status mrec_ctr_head_finish(const float *part, int64_t ldp, int64_t batch, int32_t H,
-                                 const float *g, int32_t update, float lr, float *w, float *bias,
-                                 float *dw_out, float *db_out, mrec_stream stream) {
-  MREC_CHECK_ARG(part != nullptr && H >= 1 && batch >= 1, "bad arguments");
-  MREC_CHECK_ARG(!update || w, "update needs w");
+                                 int32_t ns, const float *g, int32_t update, float lr, float *w,
+                                 float *bias, float *ws, float *b2, float *dw_out, float *db_out,
+                                 float *dws_out, float *db2_out, mrec_stream stream) {
+  MREC_CHECK_ARG(part != nullptr && H >= 1 && batch >= 1 && ns >= 0 && ns <= 64, "bad arguments");
+  MREC_CHECK_ARG(!update || (w && (ns == 0 || ws)), "update needs w (and ws)");
   const int nparts = static_cast<int>(mrec_ctr_head_parts(batch));
-  ctr_head_finish_kernel<<<dim3(static_cast<unsigned>((H + 1 + 7) / 8)), 256, 0,
-                           static_cast<hipStream_t>(stream)>>>(part, ldp, nparts, H, g, update, lr,
-                                                               w, bias, dw_out, db_out);
+  ctr_head_finish_kernel<<<dim3(static_cast<unsigned>((H + 1 + ns + 7) / 8)), 256, 0,
+                           static_cast<hipStream_t>(stream)>>>(part, ldp, nparts, H, ns, g, update,
+                                                               lr, w, bias, ws, b2, dw_out, db_out,
+                                                               dws_out, db2_out);
   return launch_status("mrec_ctr_head_finish");
 }
 

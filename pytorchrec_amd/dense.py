@@ -415,12 +415,14 @@ def grad_one(dev) -> torch.Tensor:
 
 
 class _CTRHeadBCEFn(torch.autograd.Function):
-    """loss = BCEWithLogits(base + h W^T + b, y) (mean) for a Linear(H, 1) head.
-    The forward kernel also produces dh, dz and the dW / db partials; the backward
-    only reduces the partials (fused SGD of W, b when compiled with plain SGD)."""
+    """loss = BCEWithLogits(base + h W^T + b [+ xs ws + b2], y) (mean) for a
+    Linear(H, 1) head (+ an optional side linear term: DeepFM's dense first-order
+    weight and global bias).  The forward kernel also produces dh, dz and the
+    parameter-gradient partials; the backward only reduces the partials (fused SGD
+    of W, b, ws, b2 when compiled with plain SGD)."""
 
     @staticmethod
-    def forward(ctx, h, weight, bias, base, y, h_relu: bool):
+    def forward(ctx, h, weight, bias, base, ws, b2, y, xs, h_relu: bool):
         h = _bf16_rows(h)
         B, H = h.shape
         dev = h.device
@@ -428,23 +430,33 @@ class _CTRHeadBCEFn(torch.autograd.Function):
         b = bias.detach().float() if bias is not None else None
         base_c = base.detach().float().contiguous() if base is not None else None
         y = y.detach().float().contiguous()
+        ns = 0
+        if xs is not None:
+            xs = xs.detach().float()
+            if xs.stride(1) != 1:
+                xs = xs.contiguous()
+            ns = xs.shape[1]
+        wsd = ws.detach().float().contiguous() if ws is not None else None
+        b2d = b2.detach().float() if b2 is not None else None
         z = torch.empty(B, dtype=torch.float32, device=dev)
         dz = torch.empty(B, dtype=torch.float32, device=dev)
         dh = _alloc(B, H, _BF16, dev)
         nparts = int(_mrec.lib().mrec_ctr_head_parts(B))
-        ldp = _r8(H + 1)
+        ldp = _r8(H + 1 + ns)
         part = torch.empty(nparts, ldp, dtype=torch.float32, device=dev)
         loss_part = torch.empty(nparts, dtype=torch.float32, device=dev)
         loss = torch.empty(1, dtype=torch.float32, device=dev)
         _mrec.call("mrec_ctr_head_fwd", h.data_ptr(), h.stride(0), B, H, w.data_ptr(),
-                   _mrec.ptr(b), _mrec.ptr(base_c), y.data_ptr(), int(bool(h_relu)),
-                   z.data_ptr(), dz.data_ptr(), dh.data_ptr(), dh.stride(0), part.data_ptr(), ldp,
-                   loss_part.data_ptr(), _ticket(dev).data_ptr(), loss.data_ptr(),
-                   _mrec.stream_handle())
+                   _mrec.ptr(b), _mrec.ptr(base_c), y.data_ptr(), _mrec.ptr(xs),
+                   xs.stride(0) if xs is not None else 0, ns, _mrec.ptr(wsd), _mrec.ptr(b2d),
+                   int(bool(h_relu)), z.data_ptr(), dz.data_ptr(), dh.data_ptr(), dh.stride(0),
+                   part.data_ptr(), ldp, loss_part.data_ptr(), _ticket(dev).data_ptr(),
+                   loss.data_ptr(), _mrec.stream_handle())
         if h_relu:
             _stamp(dh, h)
         ctx.save_for_backward(part, dz, dh)
-        ctx.weight, ctx.bias, ctx.H, ctx.B, ctx.has_base = weight, bias, H, B, base is not None
+        ctx.weight, ctx.bias, ctx.ws, ctx.b2 = weight, bias, ws, b2
+        ctx.H, ctx.B, ctx.ns, ctx.has_base = H, B, ns, base is not None
         ctx.mark_non_differentiable(z)
         ctx.set_materialize_grads(False)  # no zero-filled gradient for z
         return loss.reshape(()), z
@@ -455,31 +467,42 @@ class _CTRHeadBCEFn(torch.autograd.Function):
         dev = part.device
         g = gloss.detach().float().reshape(1).contiguous()
         one = g.data_ptr() == grad_one(dev).data_ptr()
-        lr = sgd_lr(ctx.weight, ctx.bias)
-        dW = db = None
+        lr = sgd_lr(ctx.weight, ctx.bias, ctx.ws, ctx.b2)
+        dW = db = dws = db2 = None
+        det = (lambda t: None if t is None else t.detach())
         if lr is not None and ctx.weight.is_contiguous():
             _mrec.call("mrec_ctr_head_finish", part.data_ptr(), part.stride(0), ctx.B, ctx.H,
-                       None if one else g.data_ptr(), 1, lr, ctx.weight.detach().data_ptr(),
-                       _mrec.ptr(ctx.bias.detach() if ctx.bias is not None else None), None,
-                       None, _mrec.stream_handle())
-        else:
-            dW = torch.empty(1, ctx.H, dtype=torch.float32, device=dev)
-            db = torch.empty(1, dtype=torch.float32, device=dev) if ctx.bias is not None else None
-            _mrec.call("mrec_ctr_head_finish", part.data_ptr(), part.stride(0), ctx.B, ctx.H,
-                       g.data_ptr(), 0, 0.0, None, None, dW.data_ptr(), _mrec.ptr(db),
+                       ctx.ns, None if one else g.data_ptr(), 1, lr,
+                       ctx.weight.detach().data_ptr(), _mrec.ptr(det(ctx.bias)),
+                       _mrec.ptr(det(ctx.ws)), _mrec.ptr(det(ctx.b2)), None, None, None, None,
                        _mrec.stream_handle())
+        else:
+            f32 = dict(dtype=torch.float32, device=dev)
+            dW = torch.empty(1, ctx.H, **f32)
+            db = torch.empty(1, **f32) if ctx.bias is not None else None
+            dws = torch.empty(ctx.ns, **f32) if ctx.ws is not None else None
+            db2 = torch.empty(1, **f32) if ctx.b2 is not None else None
+            _mrec.call("mrec_ctr_head_finish", part.data_ptr(), part.stride(0), ctx.B, ctx.H,
+                       ctx.ns, g.data_ptr(), 0, 0.0, None, None, None, None, dW.data_ptr(),
+                       _mrec.ptr(db), _mrec.ptr(dws), _mrec.ptr(db2), _mrec.stream_handle())
         if not one:
             dh = (dh.float() * g).to(_BF16)
             dz = dz * g
-        return dh, dW, db, (dz if ctx.has_base else None), None, None
+        return dh, dW, db, (dz if ctx.has_base else None), dws, db2, None, None, None
 
 
 def ctr_head_bce(h: torch.Tensor, weight: torch.Tensor, bias: Optional[torch.Tensor],
-                 base: Optional[torch.Tensor], y: torch.Tensor):
-    """(loss, z): mean BCE-with-logits of z = base + h W^T + b against y — the CTR
-    models' output layer and loss in one kernel (GPU, training) — else the plain
-    ``head`` + torch loss."""
-    if h.is_cuda and torch.is_grad_enabled() and h.shape[1] <= 1024:
-        return _CTRHeadBCEFn.apply(h, weight, bias, base, y, _is_relu_out(h))
+                 base: Optional[torch.Tensor], y: torch.Tensor, xs: Optional[torch.Tensor] = None,
+                 ws: Optional[torch.Tensor] = None, b2: Optional[torch.Tensor] = None):
+    """(loss, z): mean BCE-with-logits of z = base + h W^T + b (+ xs ws + b2) against
+    y — the CTR models' output layer and loss in one kernel (GPU, training) — else
+    the plain ``head`` + torch loss."""
+    ns = 0 if xs is None else xs.shape[1]
+    if h.is_cuda and torch.is_grad_enabled() and h.shape[1] <= 1024 and ns <= 64:
+        return _CTRHeadBCEFn.apply(h, weight, bias, base, ws, b2, y, xs, _is_relu_out(h))
     z = head(h, weight, bias, base)
+    if xs is not None:
+        z = z + xs.float() @ ws.float()
+    if b2 is not None:
+        z = z + b2.float()
     return F.binary_cross_entropy_with_logits(z.float(), y.float()), z

@@ -155,20 +155,24 @@ class DeepFM(_CTRBase):
             self.mlp.to(dev)
             self.prediction.to(dev)
 
-    def _deep(self, data: Dict[str, Tensor]):
-        x0, logit = interact(self.embeddings, self._ids(data), self._dense(data),
-                             self.dense_weight, self.global_bias, fm2=True, first_order=True,
-                             x0_cols=self.x0_cols, x0_dtype=self._x0_dtype())
+    def _deep(self, data: Dict[str, Tensor], dense, with_linear: bool):
+        lin = (self.dense_weight, self.global_bias) if with_linear else (None, None)
+        x0, logit = interact(self.embeddings, self._ids(data), dense, *lin, fm2=True,
+                             first_order=True, x0_cols=self.x0_cols, x0_dtype=self._x0_dtype())
         return self.mlp(x0), logit
 
     def forward(self, data: Dict[str, Tensor]):
-        h, logit = self._deep(data)
+        h, logit = self._deep(data, self._dense(data), True)
         prediction = dense_ops.head(h, self.prediction.weight, self.prediction.bias, base=logit)
         return prediction, self._target(data)
 
     def fused_bce_loss(self, data: Dict[str, Tensor]):
-        """Training loss (BCE with logits, mean) with the output layer fused into it."""
-        h, logit = self._deep(data)
+        """Training loss (BCE with logits, mean): the output layer, the dense
+        first-order term + global bias and the loss in one kernel (same sum as
+        ``forward`` + the loss, in a different fp32 order)."""
+        dense = self._dense(data)
+        h, logit = self._deep(data, dense, False)
         loss, _ = dense_ops.ctr_head_bce(h, self.prediction.weight, self.prediction.bias, logit,
-                                         self._target(data))
+                                         self._target(data), xs=dense, ws=self.dense_weight,
+                                         b2=self.global_bias)
         return loss

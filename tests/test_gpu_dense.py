@@ -319,16 +319,21 @@ def test_ctr_head_bce_fused_matches_torch(gpu, gscale):
     b = torch.randn(1, generator=g).to(gpu).requires_grad_()
     base = torch.randn(B, generator=g).to(gpu).requires_grad_()
     y = (torch.rand(B, generator=g) < 0.3).float().to(gpu)
+    xs = torch.rand(B, 13, generator=g).to(gpu)          # side linear (dense first order)
+    ws = (torch.randn(13, generator=g) * 0.1).to(gpu).requires_grad_()
+    b2 = torch.randn(1, generator=g).to(gpu).requires_grad_()
     hh = h.detach().clone().requires_grad_()
     setattr(hh, D._RELU_OUT, True)
-    loss, z = D.ctr_head_bce(hh, W, b, base, y)
+    loss, z = D.ctr_head_bce(hh, W, b, base, y, xs=xs, ws=ws, b2=b2)
     gl = D.grad_one(gpu) if gscale == 1.0 else torch.tensor(gscale, device=gpu)
     loss.backward(gl)
     Wr = W.detach().double().requires_grad_()
     br = b.detach().double().requires_grad_()
     baser = base.detach().double().requires_grad_()
     hr = hraw.double().to(gpu).requires_grad_()
-    zr = baser + hr @ Wr.T.reshape(-1) + br
+    wsr = ws.detach().double().requires_grad_()
+    b2r = b2.detach().double().requires_grad_()
+    zr = baser + hr @ Wr.T.reshape(-1) + br + xs.double() @ wsr + b2r
     lr_ = torch.nn.functional.binary_cross_entropy_with_logits(zr, y.double())
     (lr_ * gscale).backward()
     torch.testing.assert_close(z.double(), zr.detach(), rtol=1e-5, atol=1e-5)
@@ -336,6 +341,8 @@ def test_ctr_head_bce_fused_matches_torch(gpu, gscale):
     torch.testing.assert_close(W.grad.double(), Wr.grad, rtol=1e-4, atol=1e-6)
     torch.testing.assert_close(b.grad.double(), br.grad, rtol=1e-4, atol=1e-7)
     torch.testing.assert_close(base.grad.double(), baser.grad, rtol=1e-5, atol=1e-9)
+    torch.testing.assert_close(ws.grad.double(), wsr.grad, rtol=1e-4, atol=1e-7)
+    torch.testing.assert_close(b2.grad.double(), b2r.grad, rtol=1e-4, atol=1e-7)
     want_dh = hr.grad * (hr.detach() > 0)
     # one bf16 rounding of dh; a second one when a non-unit loss gradient rescales it
     tol = 2 ** -8 if gscale == 1.0 else 2 ** -7

@@ -18,7 +18,7 @@ import threading
 import torch  # noqa: F401  (must precede the dlopen, see module docstring)
 
 LIB_DIR = os.path.join(os.path.dirname(os.path.abspath(__file__)), "lib")
-LIB_PATH = os.path.join(LIB_DIR, "libmrec.so")
+LIB_PATH = os.environ.get("MREC_LIB_PATH") or os.path.join(LIB_DIR, "libmrec.so")
 
 ABI_VERSION = 5
 MAX_TABLES = 64

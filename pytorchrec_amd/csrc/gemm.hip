@@ -33,7 +33,10 @@ namespace mrec {
 constexpr int BM = 64, BN = 64;
 constexpr int GEMM_THREADS = 256;
 constexpr int KG = 64;                 // k per staging group
-constexpr int NBUF = 3;                // k-group ring depth: 3 x 16 KiB = 48 KiB LDS, 3 workgroups / CU
+#ifndef MREC_GEMM_NBUF
+#define MREC_GEMM_NBUF 3
+#endif
+constexpr int NBUF = MREC_GEMM_NBUF;   // k-group ring depth, 16 KiB per group: 3 -> 48 KiB, 3 WG/CU (4: +3%, 5: +5%, 6: +50% measured)
 constexpr int GROUP_ELEMS = 64 * KG;   // one operand's group image (bf16 elements)
 constexpr int TLD = BN + 4;            // fp32 row stride of the C tile staged in LDS
 
@@ -70,6 +73,9 @@ struct GemmArgs {
   int64_t k_per_split;
   float *ws;
   int64_t ldws;    // row stride of a split-K partial slab (round8(ncols))
+  int ntn;         // output tiles along N
+  int ntiles;      // output tiles (M x N)
+  int xchunk;      // tiles per XCD slot: ceil(ntiles / 8)
   int update;      // fused SGD: C -= lr * v (fp32 master), images re-emitted
   float lr;
   uint16_t *img_row;
@@ -270,8 +276,14 @@ __global__ __launch_bounds__(GEMM_THREADS) void gemm_dma_kernel(GemmArgs g) {
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int wm = wave >> 1, wn = wave & 1;
-  const int64_t m0 = static_cast<int64_t>(blockIdx.y) * BM;
-  const int64_t n0 = static_cast<int64_t>(blockIdx.x) * BN;
+  // XCD-aware tile order: workgroup b runs on XCD b % 8 (dispatch round-robin; a
+  // speed heuristic only), so XCD x gets the contiguous m-major tile range
+  // [x * xchunk, (x + 1) * xchunk) and the N-tiles sharing an A row panel meet in
+  // one XCD's L2 instead of being fetched by all eight.
+  const int tile = (blockIdx.x & 7) * g.xchunk + (blockIdx.x >> 3);
+  if (tile >= g.ntiles) return;  // uniform: padding workgroups of the last XCD slots
+  const int64_t m0 = static_cast<int64_t>(tile / g.ntn) * BM;
+  const int64_t n0 = static_cast<int64_t>(tile % g.ntn) * BN;
   // ring of NBUF k-group buffers, each [A group image | B group image]
   auto a_buf = [&](int kg) { return smem + (kg % NBUF) * 2 * GROUP_ELEMS; };
   auto b_buf = [&](int kg) { return smem + (kg % NBUF) * 2 * GROUP_ELEMS + GROUP_ELEMS; };
@@ -310,10 +322,15 @@ __global__ __launch_bounds__(GEMM_THREADS) void gemm_dma_kernel(GemmArgs g) {
     // wave and also retires every wave's reads of the buffer about to be refilled.
     // A bare s_barrier (with a compiler memory clobber): __syncthreads' release
     // fence would wait for vmcnt(0), i.e. drain the prefetch too.
-    if (kg + 1 < nkg)
-      wait_vmcnt<4>();
-    else
-      wait_vmcnt<0>();
+    switch (min(nkg - 1 - kg, NBUF - 2)) {  // groups allowed in flight after group kg
+      case 0: wait_vmcnt<0>(); break;
+      case 1: wait_vmcnt<4>(); break;
+      case 2: wait_vmcnt<8>(); break;
+      case 3: wait_vmcnt<12>(); break;
+      case 4: wait_vmcnt<16>(); break;
+      case 5: wait_vmcnt<20>(); break;
+      default: wait_vmcnt<24>(); break;
+    }
     asm volatile("s_barrier" ::: "memory");
     if (kg + NBUF - 1 < nkg) {
       da.issue(kg + NBUF - 1, krel, a_buf(kg + NBUF - 1), wave);
@@ -465,6 +482,13 @@ constexpr size_t kGemmLds = std::max<size_t>(NBUF * 2 * GROUP_ELEMS * sizeof(uin
 
 template <bool AC, bool BC>
 static void launch_dma(const GemmArgs &g, dim3 grid, hipStream_t s) {
+  static const bool attr = [] {  // > 64 KiB of dynamic LDS must be opted into, once
+    (void)hipFuncSetAttribute(reinterpret_cast<const void *>(gemm_dma_kernel<AC, BC>),
+                              hipFuncAttributeMaxDynamicSharedMemorySize,
+                              static_cast<int>(kGemmLds));
+    return true;
+  }();
+  (void)attr;
   gemm_dma_kernel<AC, BC><<<grid, GEMM_THREADS, kGemmLds, s>>>(g);
 }
 
@@ -555,8 +579,10 @@ mrec_status mrec_gemm(int64_t M, int64_t N, int64_t K, const mrec_operand *A,
   g.split_k = splits;
   g.k_per_split = kps;
   hipStream_t s = static_cast<hipStream_t>(stream);
-  const dim3 grid(static_cast<unsigned>((ncols + BN - 1) / BN),
-                  static_cast<unsigned>((M + BM - 1) / BM), static_cast<unsigned>(splits));
+  g.ntn = static_cast<int>((ncols + BN - 1) / BN);
+  g.ntiles = g.ntn * static_cast<int>((M + BM - 1) / BM);
+  g.xchunk = (g.ntiles + 7) / 8;
+  const dim3 grid(static_cast<unsigned>(8 * g.xchunk), 1u, static_cast<unsigned>(splits));
   if (!a_col && !b_col)
     launch_dma<false, false>(g, grid, s);
   else if (!a_col && b_col)

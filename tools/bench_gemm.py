@@ -74,6 +74,14 @@ def main():
         "dx": lambda: dyb @ wb,
         "dw": lambda: dyb.t() @ xb,
     }
+    tiny = torch.zeros(1, device=dev)
+    cases["empty-kernel"] = lambda: tiny.add_(1.0)
+    for kk in (64, 128, 256):
+        xk = D._alloc(M, kk, torch.bfloat16, dev)
+        xk.normal_()
+        wk, _ = D.weight_prep(torch.randn(N, kk, device=dev) * 0.05)
+        cases[f"fwd/K{kk}"] = (lambda xk=xk, wk=wk, kk=kk: D.gemm(xk, _mrec.LAYOUT_ROW, wk[:, :kk],
+                                                                 _mrec.LAYOUT_ROW, M, N, kk))
     for sk in (1, 2, 4, 8):
         cases[f"dw/s{sk}"] = (lambda sk=sk: D.gemm(dy, _mrec.LAYOUT_COL, x, _mrec.LAYOUT_COL, N, K, M,
                                                    ones_out=db, out=dW, split_k=sk))

@@ -32,7 +32,7 @@
 extern "C" {
 #endif
 
-#define MREC_ABI_VERSION 5
+#define MREC_ABI_VERSION 6
 #define MREC_MAX_TABLES 64      /* tables per table bank / per call */
 #define MREC_BWD_MAX_BATCH 8192  /* lookups per table per plan/apply call */
 
@@ -325,6 +325,36 @@ mrec_status mrec_gemm(int64_t M, int64_t N, int64_t K, const mrec_operand *A,
                       const mrec_operand *B, int64_t b_ones_col, int64_t b_cols,
                       const mrec_epilogue *epi, void *C, mrec_dtype c_dtype, int64_t ldc,
                       int32_t split_k, void *workspace, size_t ws_bytes, mrec_stream stream);
+
+/* phases of a GEMM inside mrec_gemm_multi */
+#define MREC_GEMM_FULL 0    /* product + epilogue (split_k must resolve to 1) */
+#define MREC_GEMM_PARTIAL 1 /* split-K: fp32 partial slabs into workspace only */
+#define MREC_GEMM_REDUCE 2  /* split-K: fixed-order slab reduction + epilogue only */
+
+typedef struct {
+  int64_t M, N, K;
+  const mrec_operand *A;
+  const mrec_operand *B;
+  int64_t b_ones_col;
+  int64_t b_cols;
+  const mrec_epilogue *epi;
+  void *C;
+  mrec_dtype c_dtype;
+  int64_t ldc;
+  int32_t split_k;
+  void *workspace;
+  size_t ws_bytes;
+  int32_t phase; /* MREC_GEMM_* */
+} mrec_gemm_call;
+
+/*
+ * Up to 4 independent GEMM phases in ONE launch (same arguments and results as
+ * mrec_gemm; a split-K GEMM is run as PARTIAL in one call and REDUCE in a later one,
+ * same arguments and workspace).  The calls must not depend on each other.  Used
+ * for a backward layer: its dx GEMM, its dW partial slabs and the previous layer's
+ * dW reduction (+ fused SGD) overlap instead of paying three launch boundaries.
+ */
+mrec_status mrec_gemm_multi(int32_t n, const mrec_gemm_call *calls, mrec_stream stream);
 
 /*
  * fp32 [N, K] weight (row stride ldw) -> bf16 images for the GEMMs: `row`

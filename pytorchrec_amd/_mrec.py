@@ -20,7 +20,7 @@ import torch  # noqa: F401  (must precede the dlopen, see module docstring)
 LIB_DIR = os.path.join(os.path.dirname(os.path.abspath(__file__)), "lib")
 LIB_PATH = os.environ.get("MREC_LIB_PATH") or os.path.join(LIB_DIR, "libmrec.so")
 
-ABI_VERSION = 5
+ABI_VERSION = 6
 MAX_TABLES = 64
 BWD_MAX_BATCH = 8192
 
@@ -85,6 +85,18 @@ class Epilogue(ctypes.Structure):
                 ("img_tr", ctypes.c_void_p), ("ld_img_tr", ctypes.c_int64)]
 
 
+class GemmCall(ctypes.Structure):
+    _fields_ = [("M", ctypes.c_int64), ("N", ctypes.c_int64), ("K", ctypes.c_int64),
+                ("A", ctypes.POINTER(Operand)), ("B", ctypes.POINTER(Operand)),
+                ("b_ones_col", ctypes.c_int64), ("b_cols", ctypes.c_int64),
+                ("epi", ctypes.POINTER(Epilogue)), ("C", ctypes.c_void_p), ("c_dtype", ctypes.c_int),
+                ("ldc", ctypes.c_int64), ("split_k", ctypes.c_int32),
+                ("workspace", ctypes.c_void_p), ("ws_bytes", ctypes.c_size_t),
+                ("phase", ctypes.c_int32)]
+
+
+GEMM_FULL, GEMM_PARTIAL, GEMM_REDUCE = 0, 1, 2
+
 LAYOUT_ROW, LAYOUT_COL = 0, 1
 ACT_NONE, ACT_RELU = 0, 1
 
@@ -127,6 +139,7 @@ SIGNATURES = {
     "mrec_gemm_workspace_size": (ctypes.c_size_t, [_i64, _i64, _i64, _i32]),
     "mrec_gemm": (ctypes.c_int, [_i64, _i64, _i64, _op_p, _op_p, _i64, _i64, _epi_p,
                                  _vp, ctypes.c_int, _i64, _i32, _vp, ctypes.c_size_t, _vp]),
+    "mrec_gemm_multi": (ctypes.c_int, [_i32, ctypes.POINTER(GemmCall), _vp]),
     "mrec_weight_prep": (ctypes.c_int, [_vp, _i64, _i64, _i64, _vp, _i64, _vp, _i64, _vp]),
     "mrec_head_fwd": (ctypes.c_int, [_vp, _i64, _i64, _i32, _vp, _vp, _vp, _vp, _vp]),
     "mrec_head_bwd": (ctypes.c_int, [_vp, _vp, _i64, _i32, _vp, _i64, _vp, _i64, _vp]),

@@ -266,10 +266,10 @@ __device__ __forceinline__ void epilogue_chunk(const GemmArgs &g, int64_t m, int
 // ---------------------------------------------------------------------------
 // the kernel
 // ---------------------------------------------------------------------------
+// one output tile (workgroup `bx` of the tile grid, K slice `bz`)
 template <bool A_COL, bool B_COL>
-__global__ __launch_bounds__(GEMM_THREADS) void gemm_dma_kernel(GemmArgs g) {
-  extern __shared__ __attribute__((aligned(16))) uint16_t smem[];
-  const int64_t kb = static_cast<int64_t>(blockIdx.z) * g.k_per_split;
+__device__ __forceinline__ void gemm_tile(const GemmArgs &g, int bx, int bz, uint16_t *smem) {
+  const int64_t kb = static_cast<int64_t>(bz) * g.k_per_split;
   const int64_t ke = min(g.K, kb + g.k_per_split);
   const int64_t krel = ke > kb ? ke - kb : 0;
   const int nkg = static_cast<int>((krel + KG - 1) / KG);
@@ -280,7 +280,7 @@ __global__ __launch_bounds__(GEMM_THREADS) void gemm_dma_kernel(GemmArgs g) {
   // speed heuristic only), so XCD x gets the contiguous m-major tile range
   // [x * xchunk, (x + 1) * xchunk) and the N-tiles sharing an A row panel meet in
   // one XCD's L2 instead of being fetched by all eight.
-  const int tile = (blockIdx.x & 7) * g.xchunk + (blockIdx.x >> 3);
+  const int tile = (bx & 7) * g.xchunk + (bx >> 3);
   if (tile >= g.ntiles) return;  // uniform: padding workgroups of the last XCD slots
   const int64_t m0 = static_cast<int64_t>(tile / g.ntn) * BM;
   const int64_t n0 = static_cast<int64_t>(tile % g.ntn) * BN;
@@ -406,7 +406,7 @@ __global__ __launch_bounds__(GEMM_THREADS) void gemm_dma_kernel(GemmArgs g) {
     v[4] = x1.x; v[5] = x1.y; v[6] = x1.z; v[7] = x1.w;
     if (g.split_k > 1) {
       if (n < ncols) {
-        float *w = g.ws + (static_cast<int64_t>(blockIdx.z) * g.M + m) * g.ldws + n;
+        float *w = g.ws + (static_cast<int64_t>(bz) * g.M + m) * g.ldws + n;
         *reinterpret_cast<float4 *>(w) = x0;
         *reinterpret_cast<float4 *>(w + 4) = x1;
       }
@@ -416,14 +416,19 @@ __global__ __launch_bounds__(GEMM_THREADS) void gemm_dma_kernel(GemmArgs g) {
   }
 }
 
+template <bool A_COL, bool B_COL>
+__global__ __launch_bounds__(GEMM_THREADS) void gemm_dma_kernel(GemmArgs g) {
+  extern __shared__ __attribute__((aligned(16))) uint16_t smem[];
+  gemm_tile<A_COL, B_COL>(g, blockIdx.x, blockIdx.z, smem);
+}
+
 // fixed-order reduction of the split-K partial slabs + epilogue (4 columns / thread)
-__global__ __launch_bounds__(256) void splitk_reduce_kernel(GemmArgs g) {
+__device__ __forceinline__ void splitk_reduce_body(const GemmArgs &g, int64_t bid, int64_t nblk) {
   const int64_t ncols = g.b_ones_col >= 0 ? g.b_ones_col + 1 : g.N;
   const int64_t q = g.ldws / 4;
   const int64_t total = g.M * q;
   const int64_t slab = g.M * g.ldws;
-  for (int64_t i = static_cast<int64_t>(blockIdx.x) * 256 + threadIdx.x; i < total;
-       i += static_cast<int64_t>(gridDim.x) * 256) {
+  for (int64_t i = bid * 256 + threadIdx.x; i < total; i += nblk * 256) {
     const int64_t m = i / q, n = (i - m * q) * 4;
     if (n >= ncols && n >= g.pad_to) continue;
     float4 s = *reinterpret_cast<const float4 *>(g.ws + m * g.ldws + n);
@@ -435,6 +440,46 @@ __global__ __launch_bounds__(256) void splitk_reduce_kernel(GemmArgs g) {
 #pragma unroll
     for (int j = 0; j < 4; ++j)
       if (n + j < ncols || n + j < g.pad_to) epilogue_elem(g, m, n + j, e[j]);
+  }
+}
+
+__global__ __launch_bounds__(256) void splitk_reduce_kernel(GemmArgs g) {
+  splitk_reduce_body(g, blockIdx.x, gridDim.x);
+}
+
+// ---------------------------------------------------------------------------
+// several independent problems in ONE launch (a backward layer's dx GEMM, its dW
+// partial slabs and the previous layer's deferred dW reduction + fused SGD): the
+// workgroups of problem p are [start[p], start[p+1]), starts multiples of 8 so the
+// XCD-aware tile order holds inside each problem.  Latency-bound neighbours
+// overlap instead of paying a launch boundary each.
+// ---------------------------------------------------------------------------
+constexpr int MULTI_MAX = 4;
+enum : int { JOB_GEMM_RR = 0, JOB_GEMM_RC = 1, JOB_GEMM_CR = 2, JOB_GEMM_CC = 3, JOB_REDUCE = 4 };
+
+struct MultiArgs {
+  int n;
+  int kind[MULTI_MAX];
+  int tile_blocks[MULTI_MAX];  // workgroups per K slice (GEMM jobs)
+  int nblk[MULTI_MAX];         // workgroups with work (the rest pad to a multiple of 8)
+  int start[MULTI_MAX + 1];
+  GemmArgs g[MULTI_MAX];
+};
+
+__global__ __launch_bounds__(GEMM_THREADS) void gemm_multi_kernel(MultiArgs ma) {
+  extern __shared__ __attribute__((aligned(16))) uint16_t smem[];
+  const int b = blockIdx.x;
+  int p = 0;
+  while (p + 1 < ma.n && b >= ma.start[p + 1]) ++p;  // uniform
+  const int local = b - ma.start[p];
+  if (local >= ma.nblk[p]) return;
+  const GemmArgs &g = ma.g[p];
+  switch (ma.kind[p]) {
+    case JOB_GEMM_RR: gemm_tile<false, false>(g, local % ma.tile_blocks[p], local / ma.tile_blocks[p], smem); break;
+    case JOB_GEMM_RC: gemm_tile<false, true>(g, local % ma.tile_blocks[p], local / ma.tile_blocks[p], smem); break;
+    case JOB_GEMM_CR: gemm_tile<true, false>(g, local % ma.tile_blocks[p], local / ma.tile_blocks[p], smem); break;
+    case JOB_GEMM_CC: gemm_tile<true, true>(g, local % ma.tile_blocks[p], local / ma.tile_blocks[p], smem); break;
+    default: splitk_reduce_body(g, local, ma.nblk[p]); break;
   }
 }
 
@@ -507,10 +552,16 @@ size_t mrec_gemm_workspace_size(int64_t M, int64_t N, int64_t K, int32_t split_k
          static_cast<size_t>((N + 1 + 7) / 8 * 8) * 4;
 }
 
-mrec_status mrec_gemm(int64_t M, int64_t N, int64_t K, const mrec_operand *A,
-                      const mrec_operand *B, int64_t b_ones_col, int64_t b_cols,
-                      const mrec_epilogue *epi, void *C, mrec_dtype c_dtype, int64_t ldc,
-                      int32_t split_k, void *workspace, size_t ws_bytes, mrec_stream stream) {
+}  // extern "C"
+
+namespace mrec {
+
+// validate one GEMM call and fill its kernel arguments; *ncols_out = 0 means "no work"
+static mrec_status build_gemm(int64_t M, int64_t N, int64_t K, const mrec_operand *A,
+                              const mrec_operand *B, int64_t b_ones_col, int64_t b_cols,
+                              const mrec_epilogue *epi, void *C, mrec_dtype c_dtype, int64_t ldc,
+                              int32_t split_k, void *workspace, size_t ws_bytes, GemmArgs *out,
+                              int *kind, int64_t *ncols_out) {
   MREC_CHECK_ARG(M >= 0 && N >= 0 && K >= 0, "negative size");
   MREC_CHECK_ARG(A && A->ptr && B && B->ptr && C, "NULL operand");
   MREC_CHECK_ARG(A->dtype == MREC_BF16 && B->dtype == MREC_BF16,
@@ -531,7 +582,7 @@ mrec_status mrec_gemm(int64_t M, int64_t N, int64_t K, const mrec_operand *A,
   }
   MREC_CHECK_ARG(splits == 1 || workspace, "split-K needs a workspace");
   const int64_t ncols = b_ones_col >= 0 ? N + 1 : N;
-  if (M == 0 || ncols == 0) return MREC_OK;
+  *ncols_out = (M == 0) ? 0 : ncols;
   GemmArgs g = {};
   g.M = M;
   g.N = N;
@@ -540,7 +591,7 @@ mrec_status mrec_gemm(int64_t M, int64_t N, int64_t K, const mrec_operand *A,
   g.lda = A->ld;
   g.B = static_cast<const uint16_t *>(B->ptr);
   g.ldb = B->ld;
-  const bool a_col = A->layout == MREC_LAYOUT_COL, b_col = B->layout == MREC_LAYOUT_COL;
+  *kind = (A->layout == MREC_LAYOUT_COL ? 2 : 0) | (B->layout == MREC_LAYOUT_COL ? 1 : 0);
   g.b_ones_col = b_ones_col;
   g.b_cols = b_cols;
   if (epi) {
@@ -578,25 +629,95 @@ mrec_status mrec_gemm(int64_t M, int64_t N, int64_t K, const mrec_operand *A,
   g.ws = static_cast<float *>(workspace);
   g.split_k = splits;
   g.k_per_split = kps;
-  hipStream_t s = static_cast<hipStream_t>(stream);
   g.ntn = static_cast<int>((ncols + BN - 1) / BN);
   g.ntiles = g.ntn * static_cast<int>((M + BM - 1) / BM);
   g.xchunk = (g.ntiles + 7) / 8;
-  const dim3 grid(static_cast<unsigned>(8 * g.xchunk), 1u, static_cast<unsigned>(splits));
-  if (!a_col && !b_col)
-    launch_dma<false, false>(g, grid, s);
-  else if (!a_col && b_col)
-    launch_dma<false, true>(g, grid, s);
-  else if (a_col && !b_col)
-    launch_dma<true, false>(g, grid, s);
-  else
-    launch_dma<true, true>(g, grid, s);
-  mrec_status st = launch_status("mrec_gemm");
-  if (st != MREC_OK || splits == 1) return st;
-  const int64_t total = M * (g.ldws / 4);
-  const unsigned rb = static_cast<unsigned>(std::min<int64_t>((total + 255) / 256, 2048));
-  splitk_reduce_kernel<<<rb, 256, 0, s>>>(g);
+  *out = g;
+  return MREC_OK;
+}
+
+static int64_t reduce_blocks(const GemmArgs &g) {
+  const int64_t total = g.M * (g.ldws / 4);
+  return std::min<int64_t>((total + 255) / 256, 2048);
+}
+
+}  // namespace mrec
+
+extern "C" {
+
+mrec_status mrec_gemm(int64_t M, int64_t N, int64_t K, const mrec_operand *A,
+                      const mrec_operand *B, int64_t b_ones_col, int64_t b_cols,
+                      const mrec_epilogue *epi, void *C, mrec_dtype c_dtype, int64_t ldc,
+                      int32_t split_k, void *workspace, size_t ws_bytes, mrec_stream stream) {
+  GemmArgs g;
+  int kind;
+  int64_t ncols;
+  mrec_status st = build_gemm(M, N, K, A, B, b_ones_col, b_cols, epi, C, c_dtype, ldc, split_k,
+                              workspace, ws_bytes, &g, &kind, &ncols);
+  if (st != MREC_OK || ncols == 0) return st;
+  hipStream_t s = static_cast<hipStream_t>(stream);
+  const dim3 grid(static_cast<unsigned>(8 * g.xchunk), 1u, static_cast<unsigned>(g.split_k));
+  switch (kind) {
+    case 0: launch_dma<false, false>(g, grid, s); break;
+    case 1: launch_dma<false, true>(g, grid, s); break;
+    case 2: launch_dma<true, false>(g, grid, s); break;
+    default: launch_dma<true, true>(g, grid, s); break;
+  }
+  st = launch_status("mrec_gemm");
+  if (st != MREC_OK || g.split_k == 1) return st;
+  splitk_reduce_kernel<<<dim3(static_cast<unsigned>(reduce_blocks(g))), 256, 0, s>>>(g);
   return launch_status("mrec_gemm(split-k reduce)");
+}
+
+mrec_status mrec_gemm_multi(int32_t n, const mrec_gemm_call *calls, mrec_stream stream) {
+  MREC_CHECK_ARG(n >= 0 && n <= MULTI_MAX && (n == 0 || calls), "n out of [0, 4]");
+  MultiArgs ma = {};
+  int blocks = 0;
+  for (int i = 0; i < n; ++i) {
+    const mrec_gemm_call &c = calls[i];
+    GemmArgs g;
+    int kind;
+    int64_t ncols;
+    mrec_status st = build_gemm(c.M, c.N, c.K, c.A, c.B, c.b_ones_col, c.b_cols, c.epi, c.C,
+                                c.c_dtype, c.ldc, c.split_k, c.workspace, c.ws_bytes, &g, &kind,
+                                &ncols);
+    if (st != MREC_OK) return st;
+    MREC_CHECK_ARG(c.phase == MREC_GEMM_FULL || c.phase == MREC_GEMM_PARTIAL ||
+                       c.phase == MREC_GEMM_REDUCE, "bad phase");
+    MREC_CHECK_ARG(c.phase != MREC_GEMM_FULL || g.split_k == 1,
+                   "a split-K GEMM in mrec_gemm_multi must be PARTIAL (then REDUCE later)");
+    MREC_CHECK_ARG(c.phase == MREC_GEMM_FULL || g.split_k > 1, "PARTIAL / REDUCE need split-K");
+    const int j = ma.n;
+    int64_t nb = 0;
+    if (ncols > 0) {
+      if (c.phase == MREC_GEMM_REDUCE) {
+        ma.kind[j] = JOB_REDUCE;
+        nb = reduce_blocks(g);
+      } else {
+        ma.kind[j] = kind;
+        ma.tile_blocks[j] = 8 * g.xchunk;
+        nb = static_cast<int64_t>(8) * g.xchunk * g.split_k;
+      }
+    }
+    if (nb == 0) continue;
+    ma.nblk[j] = static_cast<int>(nb);
+    ma.g[j] = g;
+    ma.start[j] = blocks;
+    blocks += static_cast<int>((nb + 7) / 8 * 8);
+    ma.n = j + 1;
+  }
+  if (ma.n == 0) return MREC_OK;
+  ma.start[ma.n] = blocks;
+  static const bool attr = [] {
+    (void)hipFuncSetAttribute(reinterpret_cast<const void *>(gemm_multi_kernel),
+                              hipFuncAttributeMaxDynamicSharedMemorySize,
+                              static_cast<int>(kGemmLds));
+    return true;
+  }();
+  (void)attr;
+  gemm_multi_kernel<<<dim3(static_cast<unsigned>(blocks)), GEMM_THREADS, kGemmLds,
+                      static_cast<hipStream_t>(stream)>>>(ma);
+  return launch_status("mrec_gemm_multi");
 }
 
 mrec_status mrec_weight_prep(const float *W, int64_t N, int64_t K, int64_t ldw, void *row,

@@ -101,6 +101,89 @@ def gemm(A, a_layout, B, b_layout, M, N, K, *, ones_out=None, b_cols=None, bias=
     return out
 
 
+class _Call:
+    """One GEMM of an mrec_gemm_multi launch (the ctypes structs + every tensor they
+    point at, kept alive until the launch that runs it)."""
+
+    def __init__(self, A, a_layout, B, b_layout, M, N, K, phase, *, ones_out=None, b_cols=None,
+                 mask=None, out=None, out_dtype=_BF16, split_k=1, sgd_lr=None, img_row=None,
+                 img_tr=None, ws=None):
+        dev = A.device
+        if out is None:
+            out = _alloc(M, N, out_dtype, dev)
+        ws_bytes = _mrec.lib().mrec_gemm_workspace_size(M, N, K, split_k)
+        if ws_bytes and ws is None:
+            ws = torch.empty(ws_bytes, dtype=torch.uint8, device=dev)
+        self.out, self.ws = out, ws
+        self.keep = [A, B, ones_out, mask, img_row, img_tr, out, ws]
+        self.epi = _mrec.Epilogue(None, 0, None, 0, None, 0, None, 0,
+                                  _mrec.ptr(mask), mask.stride(0) if mask is not None else 0,
+                                  _mrec.ptr(ones_out), int(sgd_lr is not None),
+                                  float(sgd_lr) if sgd_lr is not None else 0.0,
+                                  _mrec.ptr(img_row), img_row.stride(0) if img_row is not None else 0,
+                                  _mrec.ptr(img_tr), img_tr.stride(0) if img_tr is not None else 0)
+        self.a, self.b = _op(A, a_layout), _op(B, b_layout)
+        self.args = (M, N, K, N if ones_out is not None else -1, N if b_cols is None else b_cols,
+                     out.data_ptr(), _mrec.dtype_code(out.dtype), out.stride(0), split_k,
+                     _mrec.ptr(ws), ws_bytes)
+        self.phase = phase
+        self.writes = {p for p in (out.data_ptr(), _mrec.ptr(ones_out), _mrec.ptr(img_row),
+                                   _mrec.ptr(img_tr)) if p}
+        self.reads = {A.data_ptr(), B.data_ptr()}
+
+    def with_phase(self, phase):
+        c = object.__new__(_Call)
+        c.__dict__.update(self.__dict__)
+        c.phase = phase
+        return c
+
+    def struct(self) -> _mrec.GemmCall:
+        M, N, K, ones, bcols, C, cdt, ldc, sk, ws, wsb = self.args
+        return _mrec.GemmCall(M, N, K, ctypes.pointer(self.a), ctypes.pointer(self.b), ones, bcols,
+                              ctypes.pointer(self.epi), C, cdt, ldc, sk, ws, wsb, self.phase)
+
+
+_PENDING = []  # deferred split-K reductions (fused SGD of a layer's W, b and images)
+
+
+def launch_multi(calls):
+    """Run ``calls`` plus the pending deferred reductions in as few launches as
+    possible (<= 4 problems each; a pending job that writes what a call reads is
+    flushed first)."""
+    global _PENDING
+    pend = _PENDING
+    reads = set().union(*[c.reads for c in calls]) if calls else set()
+    if any(p.writes & reads for p in pend):
+        _run(pend)
+        pend = []
+    jobs = list(calls) + pend
+    _PENDING = []
+    for i in range(0, len(jobs), 4):
+        _run(jobs[i:i + 4])
+
+
+def _run(jobs):
+    if not jobs:
+        return
+    arr = (_mrec.GemmCall * len(jobs))(*[j.struct() for j in jobs])
+    _mrec.call("mrec_gemm_multi", len(jobs), arr, _mrec.stream_handle())
+
+
+def flush_pending():
+    """Apply every deferred reduction now (queued as an autograd end-of-backward
+    callback whenever one is deferred, so a backward pass never ends with work
+    pending)."""
+    global _PENDING
+    pend, _PENDING = _PENDING, []
+    for i in range(0, len(pend), 4):
+        _run(pend[i:i + 4])
+
+
+def _defer(call: "_Call"):
+    _PENDING.append(call.with_phase(_mrec.GEMM_REDUCE))
+    torch.autograd.Variable._execution_engine.queue_callback(flush_pending)
+
+
 def weight_prep(W: torch.Tensor, row: bool = True, tr: bool = True):
     """bf16 images of an fp32 [N, K] weight: row [N, r8(K)] and W^T [K, r8(N)]."""
     W = _weight_f32(W)
@@ -173,6 +256,7 @@ class _LinearFn(torch.autograd.Function):
         x = _bf16_rows(x)
         M, K_x = x.shape
         N, K = weight.shape
+        flush_pending()
         wr, wt = weight_images(weight)
         b = bias.detach().float().contiguous() if bias is not None else None
         y = gemm(x, _mrec.LAYOUT_ROW, wr[:, :K], _mrec.LAYOUT_ROW, M, N, K, bias=b,
@@ -192,25 +276,45 @@ class _LinearFn(torch.autograd.Function):
             dy = torch.where(y > 0, dy.to(y.dtype), torch.zeros((), dtype=y.dtype, device=y.device))
         dy = _bf16_rows(dy)
         dx = dW = db = None
+        need_w = ctx.needs_input_grad[1] or ctx.needs_input_grad[2]
+        lr = sgd_lr(ctx.weight, ctx.bias) if need_w else None
+        if lr is not None:
+            # one launch: dx GEMM + dW partial slabs (+ earlier layers' deferred dW
+            # reductions); this layer's reduction + SGD runs in the next launch
+            calls = []
+            if ctx.needs_input_grad[0]:
+                cdx = _Call(dy, _mrec.LAYOUT_ROW, ctx.wt, _mrec.LAYOUT_ROW, M, K_x, N,
+                            _mrec.GEMM_FULL, b_cols=K, mask=x if ctx.x_relu else None)
+                calls.append(cdx)
+                dx = cdx.out
+            sk = _split_for(N, K + 1, M)
+            cdw = _Call(dy, _mrec.LAYOUT_COL, x, _mrec.LAYOUT_COL, N, K, M,
+                        _mrec.GEMM_PARTIAL if sk > 1 else _mrec.GEMM_FULL,
+                        ones_out=ctx.bias.detach() if ctx.has_bias else None,
+                        out=ctx.weight.detach(), out_dtype=torch.float32, split_k=sk, sgd_lr=lr,
+                        img_row=ctx.wr, img_tr=ctx.wt)
+            if sk > 1:
+                launch_multi(calls + [cdw])
+                _defer(cdw)
+            else:  # the dW epilogue rewrites wt, which the dx GEMM reads: two launches
+                launch_multi(calls)
+                launch_multi([cdw])
+            if ctx.x_relu and dx is not None:
+                _stamp(dx, x)
+            return dx, None, None, None, None, None
         if ctx.needs_input_grad[0]:
             # dx[m, k] = sum_n dZ[m, n] W[n, k]; B(k'=n, col=k) = W^T[k*ld + n] -> ROW
+            flush_pending()
             dx = gemm(dy, _mrec.LAYOUT_ROW, ctx.wt, _mrec.LAYOUT_ROW, M, K_x, N, b_cols=K,
                       mask=x if ctx.x_relu else None, out_dtype=_BF16)
             if ctx.x_relu:
                 _stamp(dx, x)
-        if ctx.needs_input_grad[1] or ctx.needs_input_grad[2]:
+        if need_w:
             # dW[n, k] = sum_m dZ[m, n] x[m, k]: A(i=n, red=m) = dy[m*ld + n] -> COL,
             # B(red=m, col=k) = x[m*ld + k] -> COL; ones column -> db
-            lr = sgd_lr(ctx.weight, ctx.bias)
-            if lr is not None:  # runs after the dx GEMM has read the old images
-                gemm(dy, _mrec.LAYOUT_COL, x, _mrec.LAYOUT_COL, N, K, M,
-                     ones_out=ctx.bias.detach() if ctx.has_bias else None,
-                     out=ctx.weight.detach(), out_dtype=torch.float32, sgd_lr=lr,
-                     img_row=ctx.wr, img_tr=ctx.wt)
-            else:
-                dW = torch.empty(N, K, dtype=torch.float32, device=dy.device)
-                db = torch.empty(N, dtype=torch.float32, device=dy.device) if ctx.has_bias else None
-                gemm(dy, _mrec.LAYOUT_COL, x, _mrec.LAYOUT_COL, N, K, M, ones_out=db, out=dW)
+            dW = torch.empty(N, K, dtype=torch.float32, device=dy.device)
+            db = torch.empty(N, dtype=torch.float32, device=dy.device) if ctx.has_bias else None
+            gemm(dy, _mrec.LAYOUT_COL, x, _mrec.LAYOUT_COL, N, K, M, ones_out=db, out=dW)
         return dx, dW, db, None, None, None
 
 

@@ -174,6 +174,7 @@ constexpr int HEAD_RPW = 4;                     // rows per wave
 constexpr int HEAD_RPB = 4 * HEAD_RPW;          // rows per 256-thread workgroup
 constexpr int HEAD_MAXH = 1024;                 // h width handled (2 chunks of 8 per lane)
 
+template <int NC>  // chunks of 8 columns per lane: H <= 512 * NC
 __global__ __launch_bounds__(256) void ctr_head_kernel(
     const uint16_t *__restrict__ h, int64_t ldh, int64_t B, int H, const float *__restrict__ w,
     const float *__restrict__ bias, const float *__restrict__ base, const float *__restrict__ y,
@@ -189,7 +190,6 @@ __global__ __launch_bounds__(256) void ctr_head_kernel(
   const float b0 = (bias ? bias[0] : 0.f) + (b2 ? b2[0] : 0.f);
   const float wsl = lane < ns ? ws[lane] : 0.f;  // side linear: lane j holds ws[j] (ns <= 64)
   float sacc = 0.f;
-  constexpr int NC = HEAD_MAXH / 512;  // chunks of 8 per lane
   float wr[NC][8], acc[NC][8];
 #pragma unroll
   for (int q = 0; q < NC; ++q) {
@@ -201,6 +201,24 @@ __global__ __launch_bounds__(256) void ctr_head_kernel(
     }
   }
   float dzs = 0.f, ls = 0.f;
+  // every load of the wave's rows in flight before any math
+  uint4 hraw[HEAD_RPW][NC];
+  float xsr[HEAD_RPW], baser[HEAD_RPW], yr[HEAD_RPW];
+#pragma unroll
+  for (int rr = 0; rr < HEAD_RPW; ++rr) {
+    const int64_t r = r0 + rr;
+    const bool ok = r < B;
+#pragma unroll
+    for (int q = 0; q < NC; ++q) {
+      const int c = (q * 64 + lane) * 8;
+      hraw[rr][q] = (ok && c < H) ? *reinterpret_cast<const uint4 *>(h + r * ldh + c)
+                                  : make_uint4(0u, 0u, 0u, 0u);
+    }
+    xsr[rr] = (ok && lane < ns) ? xs[r * ldxs + lane] : 0.f;
+    baser[rr] = (ok && base) ? base[r] : 0.f;
+    yr[rr] = ok ? y[r] : 0.f;
+  }
+#pragma unroll
   for (int rr = 0; rr < HEAD_RPW; ++rr) {
     const int64_t r = r0 + rr;
     if (r >= B) break;  // uniform per wave
@@ -208,22 +226,16 @@ __global__ __launch_bounds__(256) void ctr_head_kernel(
     float dot = 0.f;
 #pragma unroll
     for (int q = 0; q < NC; ++q) {
-      const int c = (q * 64 + lane) * 8;
-      if (c < H) {
-        Vec<uint16_t>::to_f32(*reinterpret_cast<const uint4 *>(h + r * ldh + c), hv[q]);
-      } else {
-#pragma unroll
-        for (int j = 0; j < 8; ++j) hv[q][j] = 0.f;
-      }
+      Vec<uint16_t>::to_f32(hraw[rr][q], hv[q]);
 #pragma unroll
       for (int j = 0; j < 8; ++j) dot = fmaf(hv[q][j], wr[q][j], dot);
     }
-    const float xsv = lane < ns ? xs[r * ldxs + lane] : 0.f;
+    const float xsv = xsr[rr];
     dot = fmaf(xsv, wsl, dot);
 #pragma unroll
     for (int off = 32; off > 0; off >>= 1) dot += __shfl_xor(dot, off);
-    const float zz = dot + b0 + (base ? base[r] : 0.f);
-    const float yy = y[r];
+    const float zz = dot + b0 + baser[rr];
+    const float yy = yr[rr];
     const float d = (1.f / (1.f + __expf(-zz)) - yy) * invB;
     sacc = fmaf(d, xsv, sacc);
     if (lane == 0) {
@@ -439,9 +451,16 @@ mrec_status mrec_ctr_head_fwd(const void *h, int64_t ldh, int64_t batch, int32_t
                  "side linear: 0 <= ns <= 64 with xs / ws");
   MREC_CHECK_ARG(ldp >= H + 1 + ns, "ldp < H + 1 + ns");
   const int64_t nb = mrec_ctr_head_parts(batch);
-  ctr_head_kernel<<<dim3(static_cast<unsigned>(nb)), 256, 0, static_cast<hipStream_t>(stream)>>>(
-      static_cast<const uint16_t *>(h), ldh, batch, H, w, bias, base, y, xs, ldxs, ns, ws, b2,
-      relu_mask, z, dz, static_cast<uint16_t *>(dh), lddh, part, ldp, loss_part, ticket, loss);
+  const dim3 grid(static_cast<unsigned>(nb));
+  hipStream_t st = static_cast<hipStream_t>(stream);
+  if (H <= 512)
+    ctr_head_kernel<1><<<grid, 256, 0, st>>>(
+        static_cast<const uint16_t *>(h), ldh, batch, H, w, bias, base, y, xs, ldxs, ns, ws, b2,
+        relu_mask, z, dz, static_cast<uint16_t *>(dh), lddh, part, ldp, loss_part, ticket, loss);
+  else
+    ctr_head_kernel<2><<<grid, 256, 0, st>>>(
+        static_cast<const uint16_t *>(h), ldh, batch, H, w, bias, base, y, xs, ldxs, ns, ws, b2,
+        relu_mask, z, dz, static_cast<uint16_t *>(dh), lddh, part, ldp, loss_part, ticket, loss);
   return launch_status("mrec_ctr_head_fwd");
 }
 

@@ -81,6 +81,61 @@ def build_deepfm(args, device, comm=None):
     return model, sparse, dense, label
 
 
+def build_dcnv2(args, device, comm=None):
+    """C3 DCN-v2: the C2 inputs (no first-order), 3 full-rank cross layers over
+    x0 (26*16 + 13 = 429 wide) stacked with the deep MLP 400-400."""
+    from pytorchrec_amd.feature_column import CategoricalColumnWithIdentity, NumericColumn
+    from pytorchrec_amd.model import DCNv2
+    if comm is not None:
+        raise SystemExit("bench.py: --model dcnv2 is single-GPU (config C3)")
+    sparse = [CategoricalColumnWithIdentity(args.rows_per_table, f"c_c_C{f + 1}")
+              for f in range(CRITEO_FIELDS)]
+    dense = [NumericColumn(f"c_n_I{j + 1}") for j in range(CRITEO_DENSE)]
+    label = CategoricalColumnWithIdentity(2, "label")
+    model = DCNv2(sparse, dense, label, emb_size=16, cross_layers=3, layers=(400, 400),
+                  emb_dtype=torch.bfloat16, device=device, random_seed=2020)
+    return model, sparse, dense, label
+
+
+DIN_ITEMS, DIN_CATES, DIN_L = 63001 + 1, 801 + 1, 50
+
+
+def build_din(args, device, comm=None):
+    """C4 DIN, Amazon-Electronics-shaped: item 63,001 (+PAD) and category 801
+    (+PAD) tables, D=16, history L=50, attention MLP 80-40-1, top MLP 200-80-1."""
+    from pytorchrec_amd.feature_column import CategoricalColumnWithIdentity
+    from pytorchrec_amd.model import DIN
+    if comm is not None:
+        raise SystemExit("bench.py: --model din is single-GPU (config C4)")
+    iid = CategoricalColumnWithIdentity(DIN_ITEMS, "iid")
+    cid = CategoricalColumnWithIdentity(DIN_CATES, "cid")
+    his = CategoricalColumnWithIdentity(DIN_ITEMS, "pos_his")
+    hcat = CategoricalColumnWithIdentity(DIN_CATES, "pos_his_cate")
+    label = CategoricalColumnWithIdentity(2, "label")
+    model = DIN(iid, cid, his, hcat, label, emb_size=16, att_layers=(80, 40), layers=(200, 80),
+                emb_dtype=torch.bfloat16, device=device, random_seed=2020)
+    return model, None, None, label
+
+
+def din_batch(args, seed, device):
+    """Uniform ids (seeds 0..3), history lengths U{1..50}, tail-padded with 0
+    (interaction_history_list.py:17-29), labels Bernoulli(0.25)."""
+    B = args.batch
+    g = torch.Generator().manual_seed(seed)
+    iid = torch.randint(1, DIN_ITEMS, (B,), generator=g, dtype=torch.int32)
+    cid = torch.randint(1, DIN_CATES, (B,), generator=g, dtype=torch.int32)
+    his = torch.randint(1, DIN_ITEMS, (B, DIN_L), generator=g, dtype=torch.int32)
+    hcat = torch.randint(1, DIN_CATES, (B, DIN_L), generator=g, dtype=torch.int32)
+    lens = torch.randint(1, DIN_L + 1, (B, 1), generator=g)
+    pad = torch.arange(DIN_L)[None, :] >= lens
+    his[pad] = 0
+    hcat[pad] = 0
+    label = (torch.rand(B, generator=g) < 0.25).float()
+    return {"iid": iid.to(device), "cid": cid.to(device), "pos_his": his.to(device),
+            "pos_his_cate": hcat.to(device), "pos_his_len": lens.reshape(-1).to(device),
+            "label": label.to(device)}
+
+
 def make_batch_buffer(args, sparse, seed, device):
     """One contiguous byte buffer per batch: ids [F, B] int32 | dense [B, 13] f32 |
     label [B] f32; returns (buffer, views-builder)."""
@@ -262,13 +317,12 @@ def main():
     device = torch.device("cuda", local)
     torch.cuda.set_device(device)
 
-    if args.model != "deepfm":
-        raise SystemExit("only --model deepfm is wired into bench.py this round")
     comm = None
     if sharded:
         from pytorchrec_amd.sharding import ShardComm
         comm = ShardComm(force_collectives=args.force_collectives)
-    model, sparse, dense_cols, label_col = build_deepfm(args, device, comm)
+    builder = {"deepfm": build_deepfm, "dcnv2": build_dcnv2, "din": build_din}[args.model]
+    model, sparse, dense_cols, label_col = builder(args, device, comm)
     from pytorchrec_amd.loss import BCEWithLogitsLoss
     model.compile(torch.optim.SGD(model.get_parameters(), lr=args.lr), BCEWithLogitsLoss(), [],
                   device)
@@ -276,8 +330,11 @@ def main():
         bank.check_ids = False  # no host sync inside the captured step
     assert model.embeddings.update == "sgd", "SGD must fuse into the embedding backward"
 
-    bufs = [make_batch_buffer(args, sparse, 1000 * rank + s, device) for s in range(4)]
-    datas = [batch_views(b, args, sparse, dense_cols, label_col) for b in bufs]
+    if args.model == "din":
+        datas = [din_batch(args, 1000 * rank + s, device) for s in range(4)]
+    else:
+        bufs = [make_batch_buffer(args, sparse, 1000 * rank + s, device) for s in range(4)]
+        datas = [batch_views(b, args, sparse, dense_cols, label_col) for b in bufs]
 
     def step(d):
         return model.train_step(d)["loss"]
@@ -335,8 +392,27 @@ def main():
         elapsed = float(t)
 
     samples = args.batch * world * args.steps
+    workloads = {
+        "deepfm": "DeepFM Criteo-shaped (C2): 26 sparse x %d rows, D=16 bf16 tables with packed "
+                  "first-order weight, 13 dense, MLP 400-400-400, BCE, SGD lr %g (fused "
+                  "row-sparse update)" % (args.rows_per_table, args.lr),
+        "dcnv2": "DCN-v2 Criteo-shaped (C3): 26 sparse x %d rows, D=16 bf16, 13 dense, 3 cross "
+                 "layers 429x429, deep MLP 400-400, BCE, SGD lr %g" % (args.rows_per_table, args.lr),
+        "din": "DIN Amazon-Electronics-shaped (C4): items 63,001(+PAD) / categories 801(+PAD), "
+               "D=16 bf16, history L=50 (lengths U{1..50}), attention MLP 80-40-1, top MLP "
+               "200-80-1, BCE, SGD lr %g" % args.lr,
+    }
+    metrics = {
+        "deepfm": "samples/sec DeepFM Criteo-shaped batch 4096 at 1/2/4/8 MI355X; % HBM roofline",
+        "dcnv2": "samples/sec DCN-v2 Criteo-shaped batch 4096, 3 cross layers, 1 MI355X",
+        "din": "samples/sec DIN Amazon-Electronics-shaped batch 4096, L=50, 1 MI355X",
+    }
+    data_desc = ("synthetic (Amazon-Electronics-shaped: uniform ids seeds 0..3, U{1..50} history "
+                 "lengths, Bernoulli(0.25) labels)" if args.model == "din" else
+                 "synthetic (Criteo-shaped: uniform ids seed 0, U[0,1) dense, Bernoulli(0.25) "
+                 "labels)" + (f", zipf {args.zipf}" if args.zipf else ""))
     result = {
-        "metric": "samples/sec DeepFM Criteo-shaped batch 4096 per GPU (train step)",
+        "metric": metrics[args.model],
         "value": round(samples / elapsed, 1),
         "unit": "samples/s",
         "n_gpus": world,
@@ -347,16 +423,13 @@ def main():
         "scaling": "weak",
         "vs_baseline": None,
         "dtype": "bf16",
-        "data": "synthetic (Criteo-shaped: uniform ids seed 0, U[0,1) dense, Bernoulli(0.25) labels)"
-                + (f", zipf {args.zipf}" if args.zipf else ""),
-        "config": {"workload": "DeepFM Criteo-shaped (C2): 26 sparse x %d rows, D=16 bf16 tables "
-                               "with packed first-order weight, 13 dense, MLP 400-400-400, BCE, "
-                               "SGD lr %g (fused row-sparse update)" % (args.rows_per_table, args.lr),
+        "data": data_desc,
+        "config": {"workload": workloads[args.model],
                    "global_batch": args.batch * world, "batch_per_gpu": args.batch,
                    "parallelism": (f"dp{world}+rowshard{world}" if sharded else "single"),
                    "hip_graph": not args.no_graph},
     }
-    if rank == 0 and not args.no_roofline:
+    if rank == 0 and not args.no_roofline and args.model == "deepfm":
         ks = kernel_rooflines(model, datas[0], args)
         # achieved = sum of algorithmic bytes of the HBM-bound
         # embedding-path kernels / sum of their measured launch durations
@@ -373,7 +446,7 @@ def main():
         result["roofline_kernels"] = {k: {"avg_us": round(v[0] * 1e6, 3), "bytes": v[1],
                                           "GB/s": round(v[1] / v[0] / 1e9, 1)}
                                       for k, v in ks.items()}
-    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+    if rank == 0 and world == 1 and not args.no_cpu_baseline and args.model == "deepfm":
         result["cpu_baseline"] = cpu_baseline(args)
     if rank == 0:
         print(json.dumps(result), flush=True)

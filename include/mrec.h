@@ -32,7 +32,7 @@
 extern "C" {
 #endif
 
-#define MREC_ABI_VERSION 6
+#define MREC_ABI_VERSION 7
 #define MREC_MAX_TABLES 64      /* tables per table bank / per call */
 #define MREC_BWD_MAX_BATCH 8192  /* lookups per table per plan/apply call */
 
@@ -392,6 +392,40 @@ mrec_status mrec_bce_fwd(const float *z, const float *y, int64_t batch, float *l
                          mrec_stream stream);
 mrec_status mrec_bce_bwd(const float *z, const float *y, int64_t batch, const float *g, float *dz,
                          mrec_stream stream);
+
+/* ------------------------------------------------------------------------- */
+/* DIN target attention (config C4; absent from the reference: SURVEY.md A11) */
+/* ------------------------------------------------------------------------- */
+/*
+ * feat[b*L + j, :] = [q_b | k_bj | q_b - k_bj | q_b * k_bj]   (bf16, 4E columns)
+ * — the attention-unit input; q [B, E], k [B*L, E] bf16 (the gathered target and
+ * history rows), 16-B aligned rows, E % 8 == 0, E <= 64, L <= 64.
+ */
+mrec_status mrec_din_feat_fwd(const void *q, int64_t ldq, const void *k, int64_t ldk,
+                              int64_t batch, int32_t L, int32_t E, void *feat, int64_t ldf,
+                              mrec_stream stream);
+/*
+ * Masked softmax pooling, one wave per sample: a_bj = softmax_j(s_bj) over valid j
+ * (his[b, j] > 0 or j == 0: get_valid_his_index, torchrec/model/utils.py:5-10;
+ * invalid -> -inf as scaled_dot_product_attention, SASRec.py:26-29);
+ * top[b, :] = [q_b | sum_j a_bj k_bj | 0-pad] (bf16, the top MLP's input).
+ * s[(b*L + j) * ld_s] fp32 scores; a [B, L] fp32 saved for the backward.
+ */
+mrec_status mrec_din_pool_fwd(const float *s, int64_t ld_s, const int32_t *his, int64_t ld_his,
+                              const void *q, int64_t ldq, const void *k, int64_t ldk,
+                              int64_t batch, int32_t L, int32_t E, float *a, void *top,
+                              int64_t ldt, mrec_stream stream);
+/* pooling backward from dtop[:, E:2E] = du: ds_bj = a_bj (du.k_bj - sum_i a_bi du.k_bi),
+ * dk_bj = a_bj du (fp32, written) */
+mrec_status mrec_din_pool_bwd(const void *dtop, int64_t lddt, const float *a, const void *k,
+                              int64_t ldk, int64_t batch, int32_t L, int32_t E, float *ds,
+                              float *dk, int64_t lddk, mrec_stream stream);
+/* attention-unit input backward: dk_bj += df_k - df_(q-k) + df_(q*k) q_b;
+ * dq_b = dtop[b, :E] + sum_j (df_q + df_(q-k) + df_(q*k) k_bj)  (position order) */
+mrec_status mrec_din_feat_bwd(const void *dfeat, int64_t lddf, const void *dtop, int64_t lddt,
+                              const void *q, int64_t ldq, const void *k, int64_t ldk,
+                              int64_t batch, int32_t L, int32_t E, float *dk, int64_t lddk,
+                              float *dq, int64_t lddq, mrec_stream stream);
 
 /*
  * Fused CTR head + BCE-with-logits (forward AND the loss gradient, one pass over h;

@@ -20,7 +20,7 @@ import torch  # noqa: F401  (must precede the dlopen, see module docstring)
 LIB_DIR = os.path.join(os.path.dirname(os.path.abspath(__file__)), "lib")
 LIB_PATH = os.environ.get("MREC_LIB_PATH") or os.path.join(LIB_DIR, "libmrec.so")
 
-ABI_VERSION = 6
+ABI_VERSION = 7
 MAX_TABLES = 64
 BWD_MAX_BATCH = 8192
 
@@ -145,6 +145,13 @@ SIGNATURES = {
     "mrec_head_bwd": (ctypes.c_int, [_vp, _vp, _i64, _i32, _vp, _i64, _vp, _i64, _vp]),
     "mrec_bce_fwd": (ctypes.c_int, [_vp, _vp, _i64, _vp, _vp]),
     "mrec_bce_bwd": (ctypes.c_int, [_vp, _vp, _i64, _vp, _vp, _vp]),
+    "mrec_din_feat_fwd": (ctypes.c_int, [_vp, _i64, _vp, _i64, _i64, _i32, _i32, _vp, _i64, _vp]),
+    "mrec_din_pool_fwd": (ctypes.c_int, [_vp, _i64, _vp, _i64, _vp, _i64, _vp, _i64, _i64, _i32,
+                                         _i32, _vp, _vp, _i64, _vp]),
+    "mrec_din_pool_bwd": (ctypes.c_int, [_vp, _i64, _vp, _vp, _i64, _i64, _i32, _i32, _vp, _vp,
+                                         _i64, _vp]),
+    "mrec_din_feat_bwd": (ctypes.c_int, [_vp, _i64, _vp, _i64, _vp, _i64, _vp, _i64, _i64, _i32,
+                                         _i32, _vp, _i64, _vp, _i64, _vp]),
     "mrec_ctr_head_parts": (ctypes.c_int64, [_i64]),
     "mrec_ctr_head_fwd": (ctypes.c_int, [_vp, _i64, _i64, _i32, _vp, _vp, _vp, _vp, _vp, _i64,
                                          _i32, _vp, _vp, _i32, _vp, _vp, _vp, _i64, _vp, _i64,

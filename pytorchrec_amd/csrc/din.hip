@@ -1,0 +1,250 @@
+// DIN target-attention pooling (config C4).
+//
+//   feat[b*L+j] = [q_b | k_bj | q_b - k_bj | q_b * k_bj]          (attention-unit input)
+//   s_bj = att_out(att_mlp(feat[b*L+j]))                          (MFMA GEMMs, mrec_gemm)
+//   a_bj = softmax_j over valid j (his_bj > 0 or j == 0), invalid -> 0
+//   x_top[b] = [q_b | u_b],  u_b = sum_j a_bj k_bj                 (input of the top MLP)
+//
+// The reference has no DIN; its idioms are the masked softmax of
+// scaled_dot_product_attention (SASRec.py:14-31, invalid keys -> -inf) and the
+// history validity of get_valid_his_index (torchrec/model/utils.py:5-10).
+// One wave per sample for the pooling (lane j = history position j, L <= 64):
+// masked max / sum by wave shuffles, the weighted sum over positions through a
+// per-wave LDS transpose summed in position order (deterministic).
+#include "common.h"
+
+namespace mrec {
+
+constexpr int DIN_MAXL = 64;
+constexpr int DIN_MAXE = 64;
+
+__device__ __forceinline__ bool din_valid(const int32_t *his, int64_t ldh, int64_t b, int j) {
+  return j == 0 || his[b * ldh + j] > 0;
+}
+
+// one thread per (row b*L+j, 8-element chunk of E)
+__global__ __launch_bounds__(256) void din_feat_fwd_kernel(const uint16_t *__restrict__ q,
+                                                           int64_t ldq,
+                                                           const uint16_t *__restrict__ k,
+                                                           int64_t ldk, int64_t rows, int L, int E,
+                                                           uint16_t *__restrict__ feat,
+                                                           int64_t ldf) {
+  const int ch = E / 8;
+  const int64_t t = static_cast<int64_t>(blockIdx.x) * 256 + threadIdx.x;
+  if (t >= rows * ch) return;
+  const int64_t r = t / ch;
+  const int c = static_cast<int>(t % ch) * 8;
+  const int64_t b = r / L;
+  float qv[8], kv[8];
+  Vec<uint16_t>::to_f32(*reinterpret_cast<const uint4 *>(q + b * ldq + c), qv);
+  Vec<uint16_t>::to_f32(*reinterpret_cast<const uint4 *>(k + r * ldk + c), kv);
+  uint16_t *o = feat + r * ldf + c;
+  *reinterpret_cast<uint4 *>(o) = *reinterpret_cast<const uint4 *>(q + b * ldq + c);
+  *reinterpret_cast<uint4 *>(o + E) = *reinterpret_cast<const uint4 *>(k + r * ldk + c);
+  float d[8], p[8];
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    d[i] = qv[i] - kv[i];
+    p[i] = qv[i] * kv[i];
+  }
+  *reinterpret_cast<uint4 *>(o + 2 * E) =
+      make_uint4(pack_bf16x2(d[0], d[1]), pack_bf16x2(d[2], d[3]), pack_bf16x2(d[4], d[5]),
+                 pack_bf16x2(d[6], d[7]));
+  *reinterpret_cast<uint4 *>(o + 3 * E) =
+      make_uint4(pack_bf16x2(p[0], p[1]), pack_bf16x2(p[2], p[3]), pack_bf16x2(p[4], p[5]),
+                 pack_bf16x2(p[6], p[7]));
+}
+
+// 4 samples per 256-thread workgroup, one wave each
+__global__ __launch_bounds__(256) void din_pool_fwd_kernel(
+    const float *__restrict__ s, int64_t lds, const int32_t *__restrict__ his, int64_t ldh,
+    const uint16_t *__restrict__ q, int64_t ldq, const uint16_t *__restrict__ k, int64_t ldk,
+    int64_t B, int L, int E, float *__restrict__ a_out, uint16_t *__restrict__ top, int64_t ldt) {
+  __shared__ float tr[4][DIN_MAXL][DIN_MAXE + 1];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int64_t b = static_cast<int64_t>(blockIdx.x) * 4 + w;
+  if (b >= B) return;  // uniform per wave; no block-wide barrier below
+  const bool on = lane < L;
+  const bool val = on && din_valid(his, ldh, b, lane);
+  const float sj = val ? s[(b * L + lane) * lds] : -INFINITY;
+  float m = sj;
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) m = fmaxf(m, __shfl_xor(m, off));
+  const float e = val ? __expf(sj - m) : 0.f;
+  float sum = e;
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) sum += __shfl_xor(sum, off);
+  const float a = e / sum;
+  if (on) a_out[b * L + lane] = a;
+  if (on) {
+    const uint16_t *kr = k + (b * L + lane) * ldk;
+    for (int c = 0; c < E; c += 8) {
+      float kv[8];
+      Vec<uint16_t>::to_f32(*reinterpret_cast<const uint4 *>(kr + c), kv);
+#pragma unroll
+      for (int i = 0; i < 8; ++i) tr[w][lane][c + i] = a * kv[i];
+    }
+  }
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // this wave's LDS writes, then its reads
+  if (lane < E) {
+    float u = 0.f;
+    for (int j = 0; j < L; ++j) u += tr[w][j][lane];  // position order
+    top[b * ldt + E + lane] = f32_to_bf16_rne(u);
+    top[b * ldt + lane] = q[b * ldq + lane];
+  }
+  for (int c = 2 * E + lane; c < ldt; c += 64) top[b * ldt + c] = 0;  // zero pad columns
+}
+
+// pooling backward: du = dtop[:, E:2E]; g_j = du . k_j;
+//   ds_j = a_j (g_j - sum_i a_i g_i);  dk_j = a_j du  (fp32, written, not added)
+__global__ __launch_bounds__(256) void din_pool_bwd_kernel(
+    const uint16_t *__restrict__ dtop, int64_t lddt, const float *__restrict__ a_in,
+    const uint16_t *__restrict__ k, int64_t ldk, int64_t B, int L, int E, float *__restrict__ ds,
+    float *__restrict__ dk, int64_t lddk) {
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int64_t b = static_cast<int64_t>(blockIdx.x) * 4 + w;
+  if (b >= B) return;
+  const bool on = lane < L;
+  const float a = on ? a_in[b * L + lane] : 0.f;
+  float g = 0.f;
+  if (on) {
+    const uint16_t *kr = k + (b * L + lane) * ldk;
+    const uint16_t *du = dtop + b * lddt + E;
+    float *dkr = dk + (b * L + lane) * lddk;
+    for (int c = 0; c < E; c += 8) {
+      float kv[8], dv[8];
+      Vec<uint16_t>::to_f32(*reinterpret_cast<const uint4 *>(kr + c), kv);
+      Vec<uint16_t>::to_f32(*reinterpret_cast<const uint4 *>(du + c), dv);
+#pragma unroll
+      for (int i = 0; i < 8; ++i) {
+        g = fmaf(dv[i], kv[i], g);
+        dkr[c + i] = a * dv[i];
+      }
+    }
+  }
+  float ag = a * g;
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) ag += __shfl_xor(ag, off);
+  if (on) ds[b * L + lane] = a * (g - ag);
+}
+
+// attention-unit input backward (+ the pooling's dk, + the direct q gradient):
+//   dk_j += df_k - df_(q-k) + df_(q*k) * q
+//   dq    = dtop[:, :E] + sum_j (df_q + df_(q-k) + df_(q*k) * k_j)      (position order)
+__global__ __launch_bounds__(256) void din_feat_bwd_kernel(
+    const uint16_t *__restrict__ df, int64_t lddf, const uint16_t *__restrict__ dtop,
+    int64_t lddt, const uint16_t *__restrict__ q, int64_t ldq, const uint16_t *__restrict__ k,
+    int64_t ldk, int64_t B, int L, int E, float *__restrict__ dk, int64_t lddk,
+    float *__restrict__ dq, int64_t lddq) {
+  __shared__ float tr[4][DIN_MAXL][DIN_MAXE + 1];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int64_t b = static_cast<int64_t>(blockIdx.x) * 4 + w;
+  if (b >= B) return;
+  if (lane < L) {
+    const int64_t r = b * L + lane;
+    const uint16_t *d = df + r * lddf;
+    const uint16_t *kr = k + r * ldk;
+    const uint16_t *qr = q + b * ldq;
+    float *dkr = dk + r * lddk;
+    for (int c = 0; c < E; c += 8) {
+      float f0[8], f1[8], f2[8], f3[8], kv[8], qv[8];
+      Vec<uint16_t>::to_f32(*reinterpret_cast<const uint4 *>(d + c), f0);
+      Vec<uint16_t>::to_f32(*reinterpret_cast<const uint4 *>(d + E + c), f1);
+      Vec<uint16_t>::to_f32(*reinterpret_cast<const uint4 *>(d + 2 * E + c), f2);
+      Vec<uint16_t>::to_f32(*reinterpret_cast<const uint4 *>(d + 3 * E + c), f3);
+      Vec<uint16_t>::to_f32(*reinterpret_cast<const uint4 *>(kr + c), kv);
+      Vec<uint16_t>::to_f32(*reinterpret_cast<const uint4 *>(qr + c), qv);
+#pragma unroll
+      for (int i = 0; i < 8; ++i) {
+        dkr[c + i] += f1[i] - f2[i] + f3[i] * qv[i];
+        tr[w][lane][c + i] = f0[i] + f2[i] + f3[i] * kv[i];
+      }
+    }
+  }
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // this wave's LDS writes, then its reads
+  if (lane < E) {
+    float v = bf16_to_f32(dtop[b * lddt + lane]);
+    for (int j = 0; j < L; ++j) v += tr[w][j][lane];
+    dq[b * lddq + lane] = v;
+  }
+}
+
+static bool a16(const void *p, int64_t ld) {
+  return (reinterpret_cast<uintptr_t>(p) & 15) == 0 && ld % 8 == 0;
+}
+
+}  // namespace mrec
+
+using namespace mrec;
+
+extern "C" {
+
+mrec_status mrec_din_feat_fwd(const void *q, int64_t ldq, const void *k, int64_t ldk,
+                              int64_t batch, int32_t L, int32_t E, void *feat, int64_t ldf,
+                              mrec_stream stream) {
+  MREC_CHECK_ARG(q && k && feat, "NULL pointer");
+  MREC_CHECK_ARG(batch >= 0 && L >= 1 && L <= DIN_MAXL && E >= 8 && E <= DIN_MAXE && E % 8 == 0,
+                 "need 1 <= L <= 64, 8 <= E <= 64, E % 8 == 0");
+  MREC_CHECK_ARG(a16(q, ldq) && a16(k, ldk) && a16(feat, ldf) && ldf >= 4 * E,
+                 "rows must be 16-byte aligned, ldf >= 4E");
+  const int64_t rows = batch * L;
+  if (rows == 0) return MREC_OK;
+  const int64_t threads = rows * (E / 8);
+  din_feat_fwd_kernel<<<dim3(static_cast<unsigned>((threads + 255) / 256)), 256, 0,
+                        static_cast<hipStream_t>(stream)>>>(
+      static_cast<const uint16_t *>(q), ldq, static_cast<const uint16_t *>(k), ldk, rows, L, E,
+      static_cast<uint16_t *>(feat), ldf);
+  return launch_status("mrec_din_feat_fwd");
+}
+
+mrec_status mrec_din_pool_fwd(const float *s, int64_t ld_s, const int32_t *his, int64_t ld_his,
+                              const void *q,
+                              int64_t ldq, const void *k, int64_t ldk, int64_t batch, int32_t L,
+                              int32_t E, float *a, void *top, int64_t ldt, mrec_stream stream) {
+  MREC_CHECK_ARG(s && his && q && k && a && top, "NULL pointer");
+  MREC_CHECK_ARG(batch >= 0 && L >= 1 && L <= DIN_MAXL && E >= 8 && E <= DIN_MAXE && E % 8 == 0,
+                 "need 1 <= L <= 64, 8 <= E <= 64, E % 8 == 0");
+  MREC_CHECK_ARG(a16(k, ldk) && ldt >= 2 * E && ld_his >= L && ld_s >= 1, "bad strides");
+  if (batch == 0) return MREC_OK;
+  din_pool_fwd_kernel<<<dim3(static_cast<unsigned>((batch + 3) / 4)), 256, 0,
+                        static_cast<hipStream_t>(stream)>>>(
+      s, ld_s, his, ld_his, static_cast<const uint16_t *>(q), ldq, static_cast<const uint16_t *>(k), ldk,
+      batch, L, E, a, static_cast<uint16_t *>(top), ldt);
+  return launch_status("mrec_din_pool_fwd");
+}
+
+mrec_status mrec_din_pool_bwd(const void *dtop, int64_t lddt, const float *a, const void *k,
+                              int64_t ldk, int64_t batch, int32_t L, int32_t E, float *ds,
+                              float *dk, int64_t lddk, mrec_stream stream) {
+  MREC_CHECK_ARG(dtop && a && k && ds && dk, "NULL pointer");
+  MREC_CHECK_ARG(batch >= 0 && L >= 1 && L <= DIN_MAXL && E >= 8 && E <= DIN_MAXE && E % 8 == 0,
+                 "need 1 <= L <= 64, 8 <= E <= 64, E % 8 == 0");
+  MREC_CHECK_ARG(a16(dtop, lddt) && a16(k, ldk) && lddt >= 2 * E && lddk >= E, "bad strides");
+  if (batch == 0) return MREC_OK;
+  din_pool_bwd_kernel<<<dim3(static_cast<unsigned>((batch + 3) / 4)), 256, 0,
+                        static_cast<hipStream_t>(stream)>>>(
+      static_cast<const uint16_t *>(dtop), lddt, a, static_cast<const uint16_t *>(k), ldk, batch,
+      L, E, ds, dk, lddk);
+  return launch_status("mrec_din_pool_bwd");
+}
+
+mrec_status mrec_din_feat_bwd(const void *dfeat, int64_t lddf, const void *dtop, int64_t lddt,
+                              const void *q, int64_t ldq, const void *k, int64_t ldk,
+                              int64_t batch, int32_t L, int32_t E, float *dk, int64_t lddk,
+                              float *dq, int64_t lddq, mrec_stream stream) {
+  MREC_CHECK_ARG(dfeat && dtop && q && k && dk && dq, "NULL pointer");
+  MREC_CHECK_ARG(batch >= 0 && L >= 1 && L <= DIN_MAXL && E >= 8 && E <= DIN_MAXE && E % 8 == 0,
+                 "need 1 <= L <= 64, 8 <= E <= 64, E % 8 == 0");
+  MREC_CHECK_ARG(a16(dfeat, lddf) && a16(q, ldq) && a16(k, ldk) && lddf >= 4 * E && lddk >= E &&
+                     lddq >= E,
+                 "bad strides");
+  if (batch == 0) return MREC_OK;
+  din_feat_bwd_kernel<<<dim3(static_cast<unsigned>((batch + 3) / 4)), 256, 0,
+                        static_cast<hipStream_t>(stream)>>>(
+      static_cast<const uint16_t *>(dfeat), lddf, static_cast<const uint16_t *>(dtop), lddt,
+      static_cast<const uint16_t *>(q), ldq, static_cast<const uint16_t *>(k), ldk, batch, L, E, dk,
+      lddk, dq, lddq);
+  return launch_status("mrec_din_feat_bwd");
+}
+
+}  // extern "C"

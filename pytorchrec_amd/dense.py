@@ -233,7 +233,11 @@ def _bf16_rows(t: torch.Tensor) -> torch.Tensor:
     if (t.dtype == _BF16 and t.stride(-1) == 1 and t.stride(0) % 8 == 0
             and t.data_ptr() % 16 == 0):
         return t
-    out = _alloc(t.shape[0], t.shape[1], _BF16, t.device)
+    M, N = t.shape
+    if N % 8:  # the pad columns are read by 16-B staging: they must be zero
+        out = torch.zeros(M, _r8(N), dtype=_BF16, device=t.device)[:, :N]
+    else:
+        out = _alloc(M, N, _BF16, t.device)
     out.copy_(t)
     return out
 
@@ -404,8 +408,9 @@ def cross(x0: torch.Tensor, xl: torch.Tensor, weight: torch.Tensor,
 
 def din_attention(q: torch.Tensor, k: torch.Tensor, valid: torch.Tensor, att_mlp,
                   att_out: torch.nn.Linear):
-    """DIN target attention: s_j = att_out(att_mlp([q, k_j, q-k_j, q*k_j]));
-    a = softmax over valid j (invalid -> -inf, SASRec.py:26-29); u = sum_j a_j k_j.
+    """DIN target attention (torch ops; the CPU path and the reference restatement):
+    s_j = att_out(att_mlp([q, k_j, q-k_j, q*k_j])); a = softmax over valid j
+    (invalid -> -inf, SASRec.py:26-29); u = sum_j a_j k_j.
     q [B, E], k [B, L, E], valid [B, L] bool -> u [B, E] (fp32)."""
     B, L, E = k.shape
     qb = q.unsqueeze(1).expand(B, L, E).to(k.dtype)
@@ -415,6 +420,83 @@ def din_attention(q: torch.Tensor, k: torch.Tensor, valid: torch.Tensor, att_mlp
     s = s.masked_fill(~valid, float("-inf"))
     a = torch.softmax(s, dim=-1)
     return (a.unsqueeze(-1) * k.float()).sum(1)
+
+
+class _DinState:
+    """Carries the pooling backward's dk / dq pieces to the feature backward (the
+    pooling backward always runs first: its ds feeds the attention MLP backward)."""
+
+
+class _DinFeatFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, q, k, st: _DinState, L: int):
+        B, E = q.shape
+        feat = _alloc(B * L, 4 * E, _BF16, q.device)
+        _mrec.call("mrec_din_feat_fwd", q.data_ptr(), q.stride(0), k.data_ptr(), k.stride(0), B, L,
+                   E, feat.data_ptr(), feat.stride(0), _mrec.stream_handle())
+        ctx.save_for_backward(q, k)
+        ctx.st, ctx.L = st, L
+        return feat
+
+    @staticmethod
+    def backward(ctx, dfeat):
+        q, k = ctx.saved_tensors
+        st = ctx.st
+        B, E = q.shape
+        dfeat = _bf16_rows(dfeat)
+        dq = torch.empty(B, E, dtype=torch.float32, device=q.device)
+        _mrec.call("mrec_din_feat_bwd", dfeat.data_ptr(), dfeat.stride(0), st.dtop.data_ptr(),
+                   st.dtop.stride(0), q.data_ptr(), q.stride(0), k.data_ptr(), k.stride(0), B,
+                   ctx.L, E, st.dk.data_ptr(), st.dk.stride(0), dq.data_ptr(), dq.stride(0),
+                   _mrec.stream_handle())
+        dk = st.dk
+        del st.dk, st.dtop
+        return dq, dk, None, None
+
+
+class _DinPoolFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, s, q, k, his, st: _DinState, L: int):
+        B, E = q.shape
+        a = torch.empty(B, L, dtype=torch.float32, device=q.device)
+        top = _alloc(B, 2 * E, _BF16, q.device)
+        his = his.to(torch.int32)
+        _mrec.call("mrec_din_pool_fwd", s.data_ptr(), s.stride(0), his.data_ptr(), his.stride(0),
+                   q.data_ptr(), q.stride(0), k.data_ptr(), k.stride(0), B, L, E, a.data_ptr(),
+                   top.data_ptr(), top.stride(0), _mrec.stream_handle())
+        ctx.save_for_backward(a, k)
+        ctx.st, ctx.L, ctx.E, ctx.s_shape = st, L, E, s.shape
+        return top
+
+    @staticmethod
+    def backward(ctx, dtop):
+        a, k = ctx.saved_tensors
+        st = ctx.st
+        B, L, E = a.shape[0], ctx.L, ctx.E
+        dtop = _bf16_rows(dtop)
+        ds = torch.empty(B * L, 1, dtype=torch.float32, device=a.device)
+        dk = torch.empty(B * L, E, dtype=torch.float32, device=a.device)
+        _mrec.call("mrec_din_pool_bwd", dtop.data_ptr(), dtop.stride(0), a.data_ptr(), k.data_ptr(),
+                   k.stride(0), B, L, E, ds.data_ptr(), dk.data_ptr(), dk.stride(0),
+                   _mrec.stream_handle())
+        st.dk, st.dtop = dk, dtop
+        return ds, None, None, None, None, None
+
+
+def din_attention_top(q: torch.Tensor, k: torch.Tensor, his: torch.Tensor, att_mlp,
+                      att_out: torch.nn.Linear) -> torch.Tensor:
+    """The DIN top-MLP input [q | u] (bf16 [B, 2E]) on libmrec kernels: attention-unit
+    input builder, MFMA attention MLP + Linear(h, 1), masked-softmax pooling; the
+    backward is the pooling / builder kernels.  q [B, E], k [B*L, E] (bf16, the
+    gathered target and history rows), his [B, L] ids (validity)."""
+    B, E = q.shape
+    L = his.shape[1]
+    q, k = _bf16_rows(q), _bf16_rows(k)
+    st = _DinState()
+    feat = _DinFeatFn.apply(q, k, st, L)
+    h = att_mlp(feat)
+    s = linear(h, att_out.weight, att_out.bias, out_dtype=torch.float32)
+    return _DinPoolFn.apply(s, q, k, his, st, L)
 
 
 def colsum(s: torch.Tensor, X: Optional[torch.Tensor], want_total: bool = True, *,

@@ -68,12 +68,21 @@ class DCNv2(_CTRBase):
             for m in (self.cross, self.mlp, self.prediction):
                 m.to(dev)
 
-    def forward(self, data: Dict[str, Tensor]):
+    def _deep(self, data: Dict[str, Tensor]):
         x0, _ = interact(self.embeddings, self._ids(data), self._dense(data), None, None,
                          fm2=False, first_order=False, x0_cols=self.x0_cols,
                          x0_dtype=self._x0_dtype())
         x = x0
         for layer in self.cross:
             x = dense_ops.cross(x0, x, layer.weight, layer.bias)
-        h = self.mlp(x)
+        return self.mlp(x)
+
+    def forward(self, data: Dict[str, Tensor]):
+        h = self._deep(data)
         return dense_ops.head(h, self.prediction.weight, self.prediction.bias), self._target(data)
+
+    def fused_bce_loss(self, data: Dict[str, Tensor]):
+        """Training loss (BCE with logits, mean) with the output layer fused into it."""
+        loss, _ = dense_ops.ctr_head_bce(self._deep(data), self.prediction.weight,
+                                         self.prediction.bias, None, self._target(data))
+        return loss

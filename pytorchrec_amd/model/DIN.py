@@ -77,23 +77,39 @@ class DIN(IModel):
             for m in (self.att_mlp, self.att_out, self.mlp, self.prediction):
                 m.to(dev)
 
-    def forward(self, data: Dict[str, Tensor]):
+    def _top(self, data: Dict[str, Tensor]):
         bank = self.embeddings
         on_gpu = bank.weight.is_cuda
         act_dtype = torch.bfloat16 if on_gpu else torch.float32
-        q = gather(bank, [self.iid_column.get_feature_ids(data),
-                          self.cid_column.get_feature_ids(data)], out_dtype=act_dtype)
+        iid = self.iid_column.get_feature_ids(data)
+        cid = self.cid_column.get_feature_ids(data)
         his = self.his_column.get_feature_ids(data)
         hcat = self.his_cate_column.get_feature_ids(data)
         B, L = his.shape
-        k = gather(bank, [his.reshape(-1), hcat.reshape(-1)], out_dtype=act_dtype)
-        k = k.reshape(B, L, -1)
+        # target and history rows in ONE lookup per table (one sorted-segment
+        # backward, one SGD update per row, as a single nn.Embedding call would do)
+        rows = gather(bank, [torch.cat([iid.reshape(-1), his.reshape(-1).to(iid.dtype)]),
+                             torch.cat([cid.reshape(-1), hcat.reshape(-1).to(cid.dtype)])],
+                      out_dtype=act_dtype)
+        q, k = rows[:B], rows[B:]
+        if on_gpu:
+            return dense_ops.din_attention_top(q, k, his, self.att_mlp, self.att_out)
         valid = his > 0
         valid[:, 0] = True
-        u = dense_ops.din_attention(q, k, valid, self.att_mlp, self.att_out)
-        h = self.mlp(torch.cat([q.float(), u], dim=-1).to(act_dtype))
+        u = dense_ops.din_attention(q, k.reshape(B, L, -1), valid, self.att_mlp, self.att_out)
+        return torch.cat([q.float(), u], dim=-1)
+
+    def forward(self, data: Dict[str, Tensor]):
+        h = self.mlp(self._top(data))
         logit = dense_ops.head(h, self.prediction.weight, self.prediction.bias)
         target = None
         if self.label_column is not None and self.label_column.feature_name in data:
             target = data[self.label_column.feature_name].float()
         return logit.reshape(-1).float(), target
+
+    def fused_bce_loss(self, data: Dict[str, Tensor]):
+        """Training loss (BCE with logits, mean) with the output layer fused into it."""
+        h = self.mlp(self._top(data))
+        y = data[self.label_column.feature_name].float()
+        loss, _ = dense_ops.ctr_head_bce(h, self.prediction.weight, self.prediction.bias, None, y)
+        return loss

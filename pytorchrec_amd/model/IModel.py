@@ -261,7 +261,7 @@ class IModel(Module, IWithArguments, ABC):
             logs = {}
             for data in self._loader(dataset, batch_size, shuffle, workers, drop_last):
                 logs = self.train_step(data)
-            epoch_logs = {k: float(v) for k, v in logs.items()}
+            epoch_logs = {k: float(v.detach() if torch.is_tensor(v) else v) for k, v in logs.items()}
             if dev_dataset is not None and (epoch + 1) % dev_freq == 0:
                 epoch_logs.update(self.evaluate(dev_dataset, dev_batch_size or batch_size,
                                                 verbose=verbose, workers=workers))

@@ -1,12 +1,15 @@
 // Embedding backward: deterministic sorted-segment scatter-add with a fused
 // row-sparse update.
 //
-// plan  : one 1024-thread workgroup per table sorts its ids with a stable LDS
-//         radix sort (<= 8192 keys, 4-bit digits), then emits the
-//         permutation, the unique rows and their segment starts.  Depends only on
-//         the ids, so it can overlap the MLP forward on a side stream.
+// plan  : one 1024-thread workgroup per table groups the lookups by row.
+//         Batches <= 4096: an LDS hash table and packed atomics (three barriers)
+//         give every row a segment, unordered.  Batches <= 8192: a stable LDS
+//         radix sort.  Outputs: the lookups grouped by row (perm), the segment
+//         starts / lengths and the rows.  Depends only on the ids, so it can
+//         overlap the MLP forward on a side stream.
 // apply : one LPR-lane worker per unique row sums the per-lookup gradients of
-//         its segment in fp32, ascending sample order (bitwise reproducible), and
+//         its segment in fp32, ascending sample order (bitwise reproducible and
+//         independent of the plan's layout), and
 //         updates the row once (SGD, or accumulates a dense grad).  Segments
 //         longer than SHORT_SEG (hot Zipf rows) are summed by the whole workgroup
 //         with a fixed-order LDS tree so one hot row cannot serialise a worker.
@@ -19,17 +22,25 @@ constexpr int kMaxPlanKeys = 8192;
 constexpr int kShortSeg = 16;
 
 struct TableWs {  // per-table workspace view
-  int32_t *hdr;   // [4] = {n_unique, n_valid, 0, 0}
-  int32_t *perm;  // [Bp]   sample index of sorted position i
+  int32_t *hdr;   // [4] = {n_unique segments, n_valid lookups, 0, layout}
+  int32_t *perm;  // [Bp]   sample index of position i
   int32_t *seg;   // [Bp+1] segment starts
   int32_t *uniq;  // [Bp]   local row id of segment u
+  int32_t *segn;  // [Bp]   segment lengths (hash layout only)
 };
+// layout 0 (sorted plan): segments in ascending row order, each segment's
+//   lookups in ascending sample order, segment u ends at seg[u + 1].
+// layout 1 (hash plan): segments in arbitrary order, segn[u] lookups each, the
+//   lookups of a segment in arbitrary order -- apply restores ascending sample
+//   order itself, so the arithmetic is identical to layout 0.
+constexpr int kLayoutSorted = 0;
+constexpr int kLayoutHash = 1;
 
 __host__ __device__ inline int64_t pad4(int64_t x) { return (x + 3) & ~int64_t(3); }
 
 __host__ __device__ inline int64_t table_ws_bytes(int64_t batch) {
   const int64_t bp = pad4(batch);
-  int64_t bytes = 4 * (4 + bp + (bp + 4) + bp);
+  int64_t bytes = 4 * (4 + bp + (bp + 4) + bp + bp);
   return (bytes + 255) & ~int64_t(255);
 }
 
@@ -41,6 +52,7 @@ __host__ __device__ inline TableWs table_ws(const void *ws, int f, int64_t batch
   t.perm = t.hdr + 4;
   t.seg = t.perm + bp;
   t.uniq = t.seg + bp + 4;
+  t.segn = t.uniq + bp;
   return t;
 }
 
@@ -103,35 +115,29 @@ __device__ void block_exclusive_scan(uint32_t *a, int n, uint32_t *wtot, uint32_
   __syncthreads();
 }
 
-__global__ __launch_bounds__(kPlanThreads) void plan_kernel(BankArgs bank, IdsArgs ids, int64_t B,
-                                                            int rounds, void *ws,
-                                                            int32_t *__restrict__ oob,
-                                                            uint64_t *__restrict__ d_step) {
-  __shared__ uint32_t keyA[kMaxPlanKeys], keyB[kMaxPlanKeys];
-  __shared__ uint16_t payA[kMaxPlanKeys], payB[kMaxPlanKeys];
-  __shared__ uint32_t hist[kDigits * kMaxGroups];
-  __shared__ uint32_t wtot[kPlanThreads / 64];
-  __shared__ uint32_t s_total;
-  __shared__ int32_t s_nvalid;
-  const int f = blockIdx.x;
+#ifdef MREC_PLAN_PROF
+__device__ uint64_t g_plan_prof[16];
+#define PLAN_STAMP(k)                                              \
+  do {                                                             \
+    __syncthreads();                                               \
+    if (threadIdx.x == 0 && blockIdx.x == 0) g_plan_prof[k] = wall_clock64(); \
+  } while (0)
+#else
+#define PLAN_STAMP(k) \
+  do {                \
+  } while (0)
+#endif
+
+// Stable LSD radix sort of N = rounds * 1024 LDS keys (payload = element index),
+// then segment detection; writes perm / seg / uniq / hdr[0..1] of table t.
+// Keys >= rows are invalid and sort last.  Must be called by all 1024 threads.
+__device__ void sort_and_segment(uint32_t *keyA, uint32_t *keyB, uint16_t *payA, uint16_t *payB,
+                                 int rounds, uint32_t rows, uint32_t *hist, uint32_t *wtot,
+                                 const TableWs &t, uint32_t *s_total, int32_t *s_nvalid) {
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
-  const uint32_t rows = static_cast<uint32_t>(bank.rows[f]);
   const int N = rounds * kPlanThreads;
   const int G = rounds * (kPlanThreads / 64);
-  for (int i = tid; i < N; i += kPlanThreads) {
-    uint32_t key = rows;  // invalid / padding
-    if (i < B) {
-      const int64_t id = load_id(ids, f, i);
-      if (id >= 0 && id < static_cast<int64_t>(rows)) {
-        key = static_cast<uint32_t>(id);
-      } else if (oob && !(ids.pad_negative && id < 0)) {
-        *oob = 1;
-      }
-    }
-    keyA[i] = key;
-    payA[i] = static_cast<uint16_t>(i);
-  }
-  if (tid == 0) s_nvalid = 0;
+  if (tid == 0) *s_nvalid = 0;
   const int bits = 32 - __clz(rows);  // covers every key value 0..rows
   const int passes = (bits + kRadixBits - 1) / kRadixBits;
   uint32_t *kin = keyA, *kout = keyB;
@@ -161,6 +167,7 @@ __global__ __launch_bounds__(kPlanThreads) void plan_kernel(BankArgs bank, IdsAr
     __syncthreads();
     uint32_t *tk = kin; kin = kout; kout = tk;
     uint16_t *tp = pin; pin = pout; pout = tp;
+    if (p < 4) PLAN_STAMP(5 + p);
   }
   // segments: head flags over the sorted valid prefix, block scan of per-thread counts
   const int chunk = (N + kPlanThreads - 1) / kPlanThreads;
@@ -173,9 +180,9 @@ __global__ __launch_bounds__(kPlanThreads) void plan_kernel(BankArgs bank, IdsAr
   }
   hist[tid] = cnt;
   __syncthreads();
-  block_exclusive_scan(hist, kPlanThreads, wtot, &s_total);
+  block_exclusive_scan(hist, kPlanThreads, wtot, s_total);
+  PLAN_STAMP(9);
   uint32_t u = hist[tid];
-  TableWs t = table_ws(ws, f, B);
   for (int i = lo; i < hi; ++i) {
     const uint32_t k = kin[i];
     if (k >= rows) break;
@@ -185,16 +192,177 @@ __global__ __launch_bounds__(kPlanThreads) void plan_kernel(BankArgs bank, IdsAr
       t.uniq[u] = static_cast<int32_t>(k);
       ++u;
     }
-    if (i + 1 == N || kin[i + 1] >= rows) s_nvalid = i + 1;  // the one last valid element
+    if (i + 1 == N || kin[i + 1] >= rows) *s_nvalid = i + 1;  // the one last valid element
   }
   __syncthreads();
   if (tid == 0) {
-    const int nu = static_cast<int>(s_total);
+    const int nu = static_cast<int>(*s_total);
     t.hdr[0] = nu;
-    t.hdr[1] = s_nvalid;
-    t.seg[nu] = s_nvalid;
+    t.hdr[1] = *s_nvalid;
+    t.seg[nu] = *s_nvalid;
+  }
+}
+
+__global__ __launch_bounds__(kPlanThreads) void plan_kernel(BankArgs bank, IdsArgs ids, int64_t B,
+                                                            int rounds, void *ws,
+                                                            int32_t *__restrict__ oob,
+                                                            uint64_t *__restrict__ d_step) {
+  __shared__ uint32_t keyA[kMaxPlanKeys], keyB[kMaxPlanKeys];
+  __shared__ uint16_t payA[kMaxPlanKeys], payB[kMaxPlanKeys];
+  __shared__ uint32_t hist[kDigits * kMaxGroups];
+  __shared__ uint32_t wtot[kPlanThreads / 64];
+  __shared__ uint32_t s_total;
+  __shared__ int32_t s_nvalid;
+  const int f = blockIdx.x;
+  const int tid = threadIdx.x;
+  const uint32_t rows = static_cast<uint32_t>(bank.rows[f]);
+  const int N = rounds * kPlanThreads;
+  for (int i = tid; i < N; i += kPlanThreads) {
+    uint32_t key = rows;  // invalid / padding
+    if (i < B) {
+      const int64_t id = load_id(ids, f, i);
+      if (id >= 0 && id < static_cast<int64_t>(rows)) {
+        key = static_cast<uint32_t>(id);
+      } else if (oob && !(ids.pad_negative && id < 0)) {
+        *oob = 1;
+      }
+    }
+    keyA[i] = key;
+    payA[i] = static_cast<uint16_t>(i);
+  }
+  const TableWs t = table_ws(ws, f, B);
+  sort_and_segment(keyA, keyB, payA, payB, rounds, rows, hist, wtot, t, &s_total, &s_nvalid);
+  if (tid == 0) {
+    t.hdr[2] = 0;
+    t.hdr[3] = kLayoutSorted;
     if (d_step && f == 0) *d_step += 1;
   }
+}
+
+// ---------------------------------------------------------------------------
+// hash plan (batch <= 4096).  A workgroup barrier costs ~135 ns at 1024 threads
+// (tools/micro/barrier.hip) and every 4-bit radix pass needs six, so the sorted
+// plan spends most of its time in barriers.  The hash plan needs three:
+//   1. insert: each valid id goes into an LDS hash table (linear probing),
+//      counting its lookups (low 16 bits of the slot word);
+//   2. claim: every lookup takes a ticket on its slot (high 16 bits); ticket 0
+//      allocates the row's segment -- a wave-aggregated packed atomic hands out
+//      {segment index, start} -- and publishes the start in the slot;
+//   3. place: lookup i goes to perm[start + ticket].
+// Segment order and the order inside a segment follow the atomics, so the
+// workspace layout is not deterministic; apply sorts every segment's lookups
+// back into ascending sample order, so the updates are.
+// ---------------------------------------------------------------------------
+constexpr int kHashMaxKeys = 4096;
+constexpr int kHashSlots = 8192;  // load factor <= 1/2
+constexpr uint32_t kEmpty = 0xffffffffu;
+constexpr int kHashRounds = kHashMaxKeys / kPlanThreads;  // 4
+
+__global__ __launch_bounds__(kPlanThreads) void plan_hash_kernel(BankArgs bank, IdsArgs ids,
+                                                                 int64_t B, void *ws,
+                                                                 int32_t *__restrict__ oob,
+                                                                 uint64_t *__restrict__ d_step) {
+  __shared__ uint32_t hkey[kHashSlots];  // row id; after the claim: segment start
+  __shared__ uint32_t hcnt[kHashSlots];  // (tickets << 16) | lookups
+  __shared__ uint32_t s_tot;             // (segments << 16) | lookups placed
+  const int f = blockIdx.x;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const uint32_t rows = static_cast<uint32_t>(bank.rows[f]);
+  const bool direct = rows <= static_cast<uint32_t>(kHashSlots);
+  const TableWs t = table_ws(ws, f, B);
+  PLAN_STAMP(0);
+  // ids of this thread's lookups, loads issued before anything waits on them
+  int64_t id[kHashRounds];
+#pragma unroll
+  for (int r = 0; r < kHashRounds; ++r) {
+    const int i = r * kPlanThreads + tid;
+    id[r] = i < B ? load_id(ids, f, i) : -1;
+  }
+  for (int i = tid; i < kHashSlots; i += kPlanThreads) {
+    hkey[i] = kEmpty;
+    hcnt[i] = 0u;
+  }
+  if (tid == 0) s_tot = 0u;
+  __syncthreads();
+  PLAN_STAMP(1);
+  // 1. insert
+  uint32_t slot[kHashRounds];
+#pragma unroll
+  for (int r = 0; r < kHashRounds; ++r) {
+    const int i = r * kPlanThreads + tid;
+    slot[r] = kEmpty;
+    if (i < B) {
+      if (id[r] >= 0 && id[r] < static_cast<int64_t>(rows)) {
+        const uint32_t key = static_cast<uint32_t>(id[r]);
+        uint32_t h = key;  // tables of <= kHashSlots rows index the slots directly
+        if (!direct) {
+          h = (key * 2654435761u) >> 19;  // 13 bits
+          for (;;) {
+            const uint32_t old = atomicCAS(&hkey[h], kEmpty, key);
+            if (old == kEmpty || old == key) break;
+            h = (h + 1) & (kHashSlots - 1);
+          }
+        }
+        atomicAdd(&hcnt[h], 1u);
+        slot[r] = h;
+      } else if (oob && !(ids.pad_negative && id[r] < 0)) {
+        *oob = 1;
+      }
+    }
+  }
+  __syncthreads();
+  PLAN_STAMP(2);
+  // 2. claim
+  const uint64_t lt = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
+  uint32_t ticket[kHashRounds];
+#pragma unroll
+  for (int r = 0; r < kHashRounds; ++r) {
+    if (r * kPlanThreads >= B) break;  // uniform
+    uint32_t cnt = 0;
+    ticket[r] = 0;
+    if (slot[r] != kEmpty) {
+      const uint32_t old = atomicAdd(&hcnt[slot[r]], 1u << 16);
+      ticket[r] = old >> 16;
+      cnt = old & 0xffffu;
+    }
+    const bool claim = slot[r] != kEmpty && ticket[r] == 0;
+    const uint64_t mc = __ballot(claim);
+    if (mc == 0) continue;  // uniform
+    uint32_t incl = claim ? cnt : 0u;  // inclusive scan of the claimed lengths
+#pragma unroll
+    for (int off = 1; off < 64; off <<= 1) {
+      const uint32_t v = __shfl_up(incl, off);
+      if (lane >= off) incl += v;
+    }
+    const int last = 63 - __clzll(mc);
+    uint32_t base = 0;
+    if (lane == last) base = atomicAdd(&s_tot, (static_cast<uint32_t>(__popcll(mc)) << 16) | incl);
+    base = __shfl(base, last);
+    if (claim) {
+      const uint32_t u = (base >> 16) + __popcll(mc & lt);
+      const uint32_t start = (base & 0xffffu) + incl - cnt;
+      t.uniq[u] = static_cast<int32_t>(direct ? slot[r] : hkey[slot[r]]);
+      t.seg[u] = static_cast<int32_t>(start);
+      t.segn[u] = static_cast<int32_t>(cnt);
+      hkey[slot[r]] = start;  // only the claimer reads this slot's key
+    }
+  }
+  __syncthreads();
+  PLAN_STAMP(3);
+  // 3. place
+#pragma unroll
+  for (int r = 0; r < kHashRounds; ++r) {
+    const int i = r * kPlanThreads + tid;
+    if (i < B && slot[r] != kEmpty) t.perm[hkey[slot[r]] + ticket[r]] = i;
+  }
+  if (tid == 0) {
+    t.hdr[0] = static_cast<int32_t>(s_tot >> 16);
+    t.hdr[1] = static_cast<int32_t>(s_tot & 0xffffu);
+    t.hdr[2] = 0;
+    t.hdr[3] = kLayoutHash;
+    if (d_step && f == 0) *d_step += 1;
+  }
+  PLAN_STAMP(4);
 }
 
 // ---------------------------------------------------------------------------
@@ -344,6 +512,31 @@ __device__ __forceinline__ void apply_row(const BankArgs &bank, const ApplyArgs 
   *reinterpret_cast<uint4 *>(p) = out;
 }
 
+__device__ __forceinline__ void cswap(int &a, int &b) {
+  const int lo = min(a, b), hi = max(a, b);
+  a = lo;
+  b = hi;
+}
+
+// ascending bitonic network on r[0, N) (compile-time indices: stays in VGPRs)
+template <int N>
+__device__ __forceinline__ void bitonic_sort(int *r) {
+#pragma unroll
+  for (int k = 2; k <= N; k <<= 1)
+#pragma unroll
+    for (int j = k >> 1; j > 0; j >>= 1)
+#pragma unroll
+      for (int i = 0; i < N; ++i) {
+        const int l = i ^ j;
+        if (l > i) {
+          if ((i & k) == 0)
+            cswap(r[i], r[l]);
+          else
+            cswap(r[l], r[i]);
+        }
+      }
+}
+
 template <typename T, int LPR>
 __global__ __launch_bounds__(256) void apply_kernel(BankArgs bank, int64_t B, const void *ws,
                                                     ApplyArgs a) {
@@ -353,9 +546,13 @@ __global__ __launch_bounds__(256) void apply_kernel(BankArgs bank, int64_t B, co
   __shared__ int32_t long_list[WPB];
   __shared__ int32_t n_long;
   __shared__ float red[WPB][LPR * EPL + 1];
+  __shared__ uint32_t bits[kHashMaxKeys / 32];
+  __shared__ uint16_t srt[kHashMaxKeys];
+  __shared__ uint32_t wsum0;
   const int f = blockIdx.y;
   const TableWs t = table_ws(ws, f, B);
   const int nu = t.hdr[0];
+  const bool hashed = t.hdr[3] == kLayoutHash;
   const int ublk = blockIdx.x * WPB;
   if (ublk >= nu) return;  // uniform per block
   const int worker = threadIdx.x / LPR;
@@ -370,11 +567,11 @@ __global__ __launch_bounds__(256) void apply_kernel(BankArgs bank, int64_t B, co
 
   const int u = ublk + worker;
   bool mine = u < nu;
-  int start = 0, end = 0;
+  int start = 0, n = 0;
   if (mine) {
     start = t.seg[u];
-    end = t.seg[u + 1];
-    if (end - start > kShortSeg) {
+    n = hashed ? t.segn[u] : t.seg[u + 1] - start;
+    if (n > kShortSeg) {
       if (l == 0) long_list[atomicAdd(&n_long, 1)] = u;
       mine = false;
     }
@@ -383,29 +580,83 @@ __global__ __launch_bounds__(256) void apply_kernel(BankArgs bank, int64_t B, co
     float acc[EPL];
 #pragma unroll
     for (int j = 0; j < EPL; ++j) acc[j] = 0.f;
-    for (int i = start; i < end; i += 4) {
-      int bb[4];
+    if (hashed) {
+      // unordered segment of <= 16 lookups: sort the sample indices in registers,
+      // then sum in ascending order exactly like the sorted layout
+      int r[kShortSeg];
 #pragma unroll
-      for (int k = 0; k < 4; ++k) bb[k] = (i + k < end) ? t.perm[i + k] : -1;
+      for (int j = 0; j < kShortSeg; ++j) r[j] = j < n ? t.perm[start + j] : INT_MAX;
+      if (n <= 2)
+        bitonic_sort<2>(r);
+      else if (n <= 4)
+        bitonic_sort<4>(r);
+      else if (n <= 8)
+        bitonic_sort<8>(r);
+      else
+        bitonic_sort<16>(r);
 #pragma unroll
-      for (int k = 0; k < 4; ++k)
-        if (bb[k] >= 0) add_lookup_grad<EPL>(a, bb[k], f, D, e0, v_lane, w_lane, acc);
+      for (int j = 0; j < kShortSeg; ++j)
+        if (j < n) add_lookup_grad<EPL>(a, r[j], f, D, e0, v_lane, w_lane, acc);
+    } else {
+      const int end = start + n;
+      for (int i = start; i < end; i += 4) {
+        int bb[4];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) bb[k] = (i + k < end) ? t.perm[i + k] : -1;
+#pragma unroll
+        for (int k = 0; k < 4; ++k)
+          if (bb[k] >= 0) add_lookup_grad<EPL>(a, bb[k], f, D, e0, v_lane, w_lane, acc);
+      }
     }
     apply_row<T>(bank, a, f, t.uniq[u], e0, v_lane, acc);
   }
   __syncthreads();
   const int nl = n_long;
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   for (int k = 0; k < nl; ++k) {
     // each hot segment is summed independently, so the (atomic) list order
     // does not change any result
     const int uu = long_list[k];
-    const int s0 = t.seg[uu], s1 = t.seg[uu + 1];
+    const int s0 = t.seg[uu];
+    const int sn = hashed ? t.segn[uu] : t.seg[uu + 1] - s0;
+    if (hashed) {
+      // ascending sample order through an LDS bitmap of the batch (B <= 4096;
+      // a sample looks a table up once, so the bits are the segment)
+      for (int i = tid; i < kHashMaxKeys / 32; i += 256) bits[i] = 0u;
+      __syncthreads();
+      for (int i = tid; i < sn; i += 256) {
+        const int b = t.perm[s0 + i];
+        atomicOr(&bits[b >> 5], 1u << (b & 31));
+      }
+      __syncthreads();
+      const uint32_t word = tid < kHashMaxKeys / 32 ? bits[tid] : 0u;
+      const uint32_t c = __popc(word);
+      uint32_t incl = c;
+#pragma unroll
+      for (int off = 1; off < 64; off <<= 1) {
+        const uint32_t v = __shfl_up(incl, off);
+        if (lane >= off) incl += v;
+      }
+      if (tid == 63) wsum0 = incl;
+      __syncthreads();
+      if (tid < kHashMaxKeys / 32) {
+        uint32_t pos = incl - c + (wid == 1 ? wsum0 : 0u);
+        uint32_t w = word;
+        while (w) {
+          const int bit = __ffs(w) - 1;
+          srt[pos++] = static_cast<uint16_t>(tid * 32 + bit);
+          w &= w - 1;
+        }
+      }
+      __syncthreads();
+    }
     float acc[EPL];
 #pragma unroll
     for (int j = 0; j < EPL; ++j) acc[j] = 0.f;
     if (live)
-      for (int i = s0 + worker; i < s1; i += WPB)
-        add_lookup_grad<EPL>(a, t.perm[i], f, D, e0, v_lane, w_lane, acc);
+      for (int i = worker; i < sn; i += WPB)
+        add_lookup_grad<EPL>(a, hashed ? static_cast<int>(srt[i]) : t.perm[s0 + i], f, D, e0,
+                             v_lane, w_lane, acc);
 #pragma unroll
     for (int j = 0; j < EPL; ++j) red[worker][e0 + j] = acc[j];
     __syncthreads();
@@ -431,6 +682,10 @@ using namespace mrec;
 
 extern "C" {
 
+#ifdef MREC_PLAN_PROF
+void mrec_plan_prof_read(uint64_t *out16) { hipMemcpyFromSymbol(out16, HIP_SYMBOL(g_plan_prof), 128); }
+#endif
+
 size_t mrec_emb_bwd_workspace_size(int32_t n_tables, int64_t batch) {
   if (n_tables <= 0 || batch < 0) return 0;
   return static_cast<size_t>(n_tables) * static_cast<size_t>(table_ws_bytes(batch));
@@ -454,6 +709,11 @@ mrec_status mrec_emb_bwd_plan(const mrec_table_bank *bank, const mrec_ids *ids, 
   for (int f = 0; f < ba.n_tables; ++f)
     MREC_CHECK_ARG(ba.rows[f] < (int64_t(1) << 31), "rows per table must be < 2^31");
   const int rounds = static_cast<int>((batch + kPlanThreads - 1) / kPlanThreads);
+  if (batch >= 1 && batch <= kHashMaxKeys) {
+    plan_hash_kernel<<<dim3(ba.n_tables), kPlanThreads, 0, static_cast<hipStream_t>(stream)>>>(
+        ba, ia, batch, workspace, d_oob_flag, d_step);
+    return launch_status("mrec_emb_bwd_plan");
+  }
   plan_kernel<<<dim3(ba.n_tables), kPlanThreads, 0, static_cast<hipStream_t>(stream)>>>(
       ba, ia, batch, rounds < 1 ? 1 : rounds, workspace, d_oob_flag, d_step);
   return launch_status("mrec_emb_bwd_plan");

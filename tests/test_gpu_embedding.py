@@ -280,6 +280,42 @@ def test_plan_handles_all_duplicates_and_single_row(gpu):
     assert np.all(g[0] == B) and np.all(g[1:] == 0)
 
 
+@pytest.mark.parametrize("B", [1, 777, 4096, 4097, 8192])
+def test_dense_grad_bit_exact_ascending_order(gpu, B):
+    """Both plans (hash plan for B <= 4096: singles + sorted duplicates; full
+    sort above) sum a row's lookups in fp32, ascending sample order: for rows
+    hit <= kShortSeg (16) times bitwise equal to a sequential fp32 np.add.at.
+    Hot rows use the fixed-order workgroup tree: fp32-reordering tolerance, and
+    bitwise reproducible run to run.  Large table (hash path), mid table, and a
+    small table (full-sort branch of the hash kernel); Zipf ids so singles,
+    short and hot segments all occur."""
+    from pytorchrec_amd.embedding import gather
+    rng = np.random.default_rng(100 + B)
+    nums = [200000, 4096, 50]
+    D, F = 8, 3
+    bank = _bank(nums, D, False, torch.float32, update="dense")
+    _fill(bank, [np.zeros((n, D), np.float32) for n in nums])
+    ids_np = np.stack([np.minimum(rng.zipf(1.1, B) - 1, n - 1) if f != 1 else rng.integers(0, n, B)
+                       for f, n in enumerate(nums)], 1)
+    ids = [torch.from_numpy(ids_np[:, f]).to(gpu) for f in range(F)]
+    out = gather(bank, ids, out_dtype=torch.float32)
+    dy = rng.standard_normal((B, F * D)).astype(np.float32)
+    out.backward(torch.from_numpy(dy).to(gpu))
+    got = bank.weight.grad[:, :D].detach().cpu().numpy().copy()
+    bank.weight.grad = None
+    gather(bank, ids, out_dtype=torch.float32).backward(torch.from_numpy(dy).to(gpu))
+    assert np.array_equal(got.view(np.uint32), bank.weight.grad[:, :D].cpu().numpy().view(np.uint32))
+    for f in range(F):
+        o, n = bank.row_offset[f], nums[f]
+        want = np.zeros((n, D), np.float32)
+        np.add.at(want, ids_np[:, f], dy[:, f * D:(f + 1) * D])  # sequential fp32, index order
+        cnt = np.bincount(ids_np[:, f], minlength=n)
+        short = cnt <= 16
+        assert np.array_equal(got[o:o + n][short].view(np.uint32), want[short].view(np.uint32)), f
+        mag = ref.dense_grad(n, ids_np[:, f], np.abs(dy[:, f * D:(f + 1) * D]))
+        assert np.all(np.abs(got[o:o + n] - want) <= 1e-6 * mag + 1e-30), f
+
+
 def test_backward_large_batch_is_chunked(gpu):
     """B > MREC_BWD_MAX_BATCH runs as sequential plan/apply chunks."""
     from pytorchrec_amd.embedding import gather

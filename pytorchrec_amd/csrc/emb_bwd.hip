@@ -17,22 +17,31 @@
 
 namespace mrec {
 
+#ifndef MREC_APPLY_EXP
+#define MREC_APPLY_EXP 0  // microbenchmark variants (tools/bench_apply.py); 0 = product
+#endif
+
 constexpr int kPlanThreads = 1024;
 constexpr int kMaxPlanKeys = 8192;
 constexpr int kShortSeg = 16;
 
 struct TableWs {  // per-table workspace view
-  int32_t *hdr;   // [4] = {n_unique segments, n_valid lookups, 0, layout}
+  int32_t *hdr;   // [4] = {n segments, n lookups in segments, 0, layout}
+  int4 *desc;     // [Bp/2+4] hash layout: segment u = {row, n, b0 | start, b1}
   int32_t *perm;  // [Bp]   sample index of position i
-  int32_t *seg;   // [Bp+1] segment starts
-  int32_t *uniq;  // [Bp]   local row id of segment u
-  int32_t *segn;  // [Bp]   segment lengths (hash layout only)
+  int32_t *seg;   // [Bp+1] sorted layout: segment starts
+  int32_t *uniq;  // [Bp]   sorted layout: local row id of segment u
+  int32_t *lut;   // [Bp]   hash layout: row of lookup b if no other lookup hits it, else -1
 };
 // layout 0 (sorted plan): segments in ascending row order, each segment's
-//   lookups in ascending sample order, segment u ends at seg[u + 1].
-// layout 1 (hash plan): segments in arbitrary order, segn[u] lookups each, the
-//   lookups of a segment in arbitrary order -- apply restores ascending sample
-//   order itself, so the arithmetic is identical to layout 0.
+//   lookups in ascending sample order in perm, segment u = [seg[u], seg[u + 1]).
+// layout 1 (hash plan): only rows hit more than once get a segment (<= B/2 of
+//   them), in arbitrary order; a row hit once is listed in lut[b] of its lookup
+//   and updated sample-major by apply.  Segment u is desc[u] = {row, n, b0, b1}
+//   when n == 2 (both lookups in the descriptor) and {row, n, start, -} with the
+//   lookups in perm[start, start + n) otherwise.  The order of a segment's
+//   lookups is arbitrary -- apply restores ascending sample order itself, so
+//   the arithmetic is identical to layout 0.
 constexpr int kLayoutSorted = 0;
 constexpr int kLayoutHash = 1;
 
@@ -40,7 +49,7 @@ __host__ __device__ inline int64_t pad4(int64_t x) { return (x + 3) & ~int64_t(3
 
 __host__ __device__ inline int64_t table_ws_bytes(int64_t batch) {
   const int64_t bp = pad4(batch);
-  int64_t bytes = 4 * (4 + bp + (bp + 4) + bp + bp);
+  int64_t bytes = 16 + 16 * (bp / 2 + 4) + 4 * (bp + (bp + 4) + bp + bp);
   return (bytes + 255) & ~int64_t(255);
 }
 
@@ -49,10 +58,11 @@ __host__ __device__ inline TableWs table_ws(const void *ws, int f, int64_t batch
   const int64_t bp = pad4(batch);
   TableWs t;
   t.hdr = reinterpret_cast<int32_t *>(base);
-  t.perm = t.hdr + 4;
+  t.desc = reinterpret_cast<int4 *>(base + 16);
+  t.perm = reinterpret_cast<int32_t *>(t.desc + bp / 2 + 4);
   t.seg = t.perm + bp;
   t.uniq = t.seg + bp + 4;
-  t.segn = t.uniq + bp;
+  t.lut = t.uniq + bp;
   return t;
 }
 
@@ -245,10 +255,11 @@ __global__ __launch_bounds__(kPlanThreads) void plan_kernel(BankArgs bank, IdsAr
 // plan spends most of its time in barriers.  The hash plan needs three:
 //   1. insert: each valid id goes into an LDS hash table (linear probing),
 //      counting its lookups (low 16 bits of the slot word);
-//   2. claim: every lookup takes a ticket on its slot (high 16 bits); ticket 0
-//      allocates the row's segment -- a wave-aggregated packed atomic hands out
+//   2. claim: a row hit once is written to lut[i] of its lookup; otherwise every
+//      lookup takes a ticket on its slot (high 16 bits) and ticket 0 allocates
+//      the row's segment -- a wave-aggregated packed atomic hands out
 //      {segment index, start} -- and publishes the start in the slot;
-//   3. place: lookup i goes to perm[start + ticket].
+//   3. place: lookup i of a repeated row goes to perm[start + ticket].
 // Segment order and the order inside a segment follow the atomics, so the
 // workspace layout is not deterministic; apply sorts every segment's lookups
 // back into ascending sample order, so the updates are.
@@ -314,18 +325,28 @@ __global__ __launch_bounds__(kPlanThreads) void plan_hash_kernel(BankArgs bank, 
   PLAN_STAMP(2);
   // 2. claim
   const uint64_t lt = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
-  uint32_t ticket[kHashRounds];
+  uint32_t ticket[kHashRounds], count[kHashRounds];
+#pragma unroll
+  for (int r = 0; r < kHashRounds; ++r) {
+    ticket[r] = 0;
+    count[r] = 0;
+  }
 #pragma unroll
   for (int r = 0; r < kHashRounds; ++r) {
     if (r * kPlanThreads >= B) break;  // uniform
     uint32_t cnt = 0;
-    ticket[r] = 0;
     if (slot[r] != kEmpty) {
       const uint32_t old = atomicAdd(&hcnt[slot[r]], 1u << 16);
       ticket[r] = old >> 16;
       cnt = old & 0xffffu;
+      count[r] = cnt;
     }
-    const bool claim = slot[r] != kEmpty && ticket[r] == 0;
+    {
+      const int i = r * kPlanThreads + tid;
+      if (i < B)
+        t.lut[i] = cnt == 1 ? static_cast<int32_t>(direct ? slot[r] : hkey[slot[r]]) : -1;
+    }
+    const bool claim = cnt > 1 && ticket[r] == 0;
     const uint64_t mc = __ballot(claim);
     if (mc == 0) continue;  // uniform
     uint32_t incl = claim ? cnt : 0u;  // inclusive scan of the claimed lengths
@@ -341,10 +362,11 @@ __global__ __launch_bounds__(kPlanThreads) void plan_hash_kernel(BankArgs bank, 
     if (claim) {
       const uint32_t u = (base >> 16) + __popcll(mc & lt);
       const uint32_t start = (base & 0xffffu) + incl - cnt;
-      t.uniq[u] = static_cast<int32_t>(direct ? slot[r] : hkey[slot[r]]);
-      t.seg[u] = static_cast<int32_t>(start);
-      t.segn[u] = static_cast<int32_t>(cnt);
-      hkey[slot[r]] = start;  // only the claimer reads this slot's key
+      int32_t *d = reinterpret_cast<int32_t *>(t.desc + u);
+      d[0] = static_cast<int32_t>(direct ? slot[r] : hkey[slot[r]]);
+      d[1] = static_cast<int32_t>(cnt);
+      if (cnt > 2) d[2] = static_cast<int32_t>(start);
+      hkey[slot[r]] = (u << 16) | start;  // only the claimer reads this slot's key
     }
   }
   __syncthreads();
@@ -353,7 +375,13 @@ __global__ __launch_bounds__(kPlanThreads) void plan_hash_kernel(BankArgs bank, 
 #pragma unroll
   for (int r = 0; r < kHashRounds; ++r) {
     const int i = r * kPlanThreads + tid;
-    if (i < B && slot[r] != kEmpty) t.perm[hkey[slot[r]] + ticket[r]] = i;
+    if (i < B && count[r] > 1) {
+      const uint32_t us = hkey[slot[r]];
+      if (count[r] == 2)
+        reinterpret_cast<int32_t *>(t.desc + (us >> 16))[2 + ticket[r]] = i;
+      else
+        t.perm[(us & 0xffffu) + ticket[r]] = i;
+    }
   }
   if (tid == 0) {
     t.hdr[0] = static_cast<int32_t>(s_tot >> 16);
@@ -416,30 +444,25 @@ __device__ __forceinline__ void load_bf16xN(const uint16_t *p, float *v) {
   }
 }
 
-// gradient of lookup (b, f) for this lane's EPL elements, added into acc
+// gradient of lookup (b, f) for this lane's EPL elements (w lane: g[0])
 template <int EPL>
-__device__ __forceinline__ void add_lookup_grad(const ApplyArgs &a, int64_t b, int f, int D,
-                                                int e0, bool v_lane, bool w_lane, float *acc) {
+__device__ __forceinline__ void lookup_grad(const ApplyArgs &a, int64_t b, int f, int D, int e0,
+                                            bool v_lane, bool w_lane, float *g) {
+#pragma unroll
+  for (int j = 0; j < EPL; ++j) g[j] = 0.f;
   if (a.g_occ) {
     const int64_t idx = a.chunk ? (b / a.chunk) * a.chunk_stride + f * a.chunk + b % a.chunk : b;
-    const float *g = a.g_occ + idx * a.g_ld;
-    if (v_lane) {
-      float t[EPL];
-      load_f32xN<EPL>(g + e0, t);
-#pragma unroll
-      for (int j = 0; j < EPL; ++j) acc[j] += t[j];
-    } else if (w_lane) {
-      acc[0] += g[D];
-    }
+    const float *go = a.g_occ + idx * a.g_ld;
+    if (v_lane)
+      load_f32xN<EPL>(go + e0, g);
+    else if (w_lane)
+      g[0] = go[D];
     return;
   }
   if (v_lane) {
-    // per-lookup gradient first, then one add into the segment sum: the same
-    // arithmetic as mrec_shard_lookup_grad, so sharded and unsharded updates agree
+    // the same arithmetic as mrec_shard_lookup_grad, so sharded and unsharded
+    // updates agree
     const int64_t col = static_cast<int64_t>(f) * D + e0;
-    float g[EPL];
-#pragma unroll
-    for (int j = 0; j < EPL; ++j) g[j] = 0.f;
     if (a.dx) {
       if (a.dx_bf16)
         load_bf16xN<EPL>(static_cast<const uint16_t *>(a.dx) + b * a.dx_ld + col, g);
@@ -457,23 +480,39 @@ __device__ __forceinline__ void add_lookup_grad(const ApplyArgs &a, int64_t b, i
 #pragma unroll
       for (int j = 0; j < EPL; ++j) g[j] = fmaf(c, s[j] - v[j], g[j]);
     }
-#pragma unroll
-    for (int j = 0; j < EPL; ++j) acc[j] += g[j];
   } else if (w_lane && a.dw) {
-    acc[0] += a.dw[b];
+    g[0] = a.dw[b];
   }
 }
 
+// per-lookup gradient first, then one add into the segment sum
+template <int EPL>
+__device__ __forceinline__ void add_lookup_grad(const ApplyArgs &a, int64_t b, int f, int D,
+                                                int e0, bool v_lane, bool w_lane, float *acc) {
+  float g[EPL];
+  lookup_grad<EPL>(a, b, f, D, e0, v_lane, w_lane, g);
+#pragma unroll
+  for (int j = 0; j < EPL; ++j) acc[j] += g[j];
+}
+
 template <typename T>
-__device__ __forceinline__ void apply_row(const BankArgs &bank, const ApplyArgs &a, int f,
-                                          int64_t row, int e0, bool v_lane, const float *acc) {
-  constexpr int EPL = Vec<T>::EPL;
+__device__ __forceinline__ T *row_ptr(const BankArgs &bank, const ApplyArgs &a, int f,
+                                      int64_t row, int e0) {
   const int64_t grow = bank.row_offset[f] + row;
   const int64_t off = grow * static_cast<int64_t>(bank.row_stride) + e0;
-  T *p = reinterpret_cast<T *>(a.mode == MREC_BWD_DENSE_GRAD ? static_cast<char *>(a.grad)
+  return reinterpret_cast<T *>(a.mode == MREC_BWD_DENSE_GRAD ? static_cast<char *>(a.grad)
                                                               : bank.data) +
          off;
-  const uint4 raw = *reinterpret_cast<const uint4 *>(p);
+}
+
+// new value of this lane's 16 bytes of the row from its old contents `raw`
+template <typename T>
+__device__ __forceinline__ void apply_row_raw(const BankArgs &bank, const ApplyArgs &a, int f,
+                                              int64_t row, int e0, bool v_lane, const float *acc,
+                                              const uint4 raw) {
+  constexpr int EPL = Vec<T>::EPL;
+  const int64_t grow = bank.row_offset[f] + row;
+  T *p = row_ptr<T>(bank, a, f, row, e0);
   float old[EPL];
   Vec<T>::to_f32(raw, old);
   const int live = v_lane ? EPL : 1;  // w lane: only element D is live
@@ -512,6 +551,13 @@ __device__ __forceinline__ void apply_row(const BankArgs &bank, const ApplyArgs 
   *reinterpret_cast<uint4 *>(p) = out;
 }
 
+template <typename T>
+__device__ __forceinline__ void apply_row(const BankArgs &bank, const ApplyArgs &a, int f,
+                                          int64_t row, int e0, bool v_lane, const float *acc) {
+  const uint4 raw = *reinterpret_cast<const uint4 *>(row_ptr<T>(bank, a, f, row, e0));
+  apply_row_raw<T>(bank, a, f, row, e0, v_lane, acc, raw);
+}
+
 __device__ __forceinline__ void cswap(int &a, int &b) {
   const int lo = min(a, b), hi = max(a, b);
   a = lo;
@@ -537,9 +583,15 @@ __device__ __forceinline__ void bitonic_sort(int *r) {
       }
 }
 
+// Grid (1-D): F * seg_blocks segment blocks (table f = blk / seg_blocks), then,
+// for the hash layout, ceil(B * F / WPB) sample-major blocks for the rows hit
+// once: worker q handles lookup (b, f) = (q / F, q % F), so a wave reads
+// consecutive slices of the dx / x0 rows (coalesced) and updates rows no other
+// lookup touches.
 template <typename T, int LPR>
-__global__ __launch_bounds__(256) void apply_kernel(BankArgs bank, int64_t B, const void *ws,
-                                                    ApplyArgs a) {
+__global__ __launch_bounds__(256, 6) void apply_kernel(BankArgs bank, int64_t B, const void *ws,
+                                                       ApplyArgs a, int seg_blocks,
+                                                       int hash_layout) {
   if (a.d_step) a.seed += *a.d_step * 0x9e3779b97f4a7c15ull;
   constexpr int EPL = Vec<T>::EPL;
   constexpr int WPB = 256 / LPR;
@@ -549,66 +601,111 @@ __global__ __launch_bounds__(256) void apply_kernel(BankArgs bank, int64_t B, co
   __shared__ uint32_t bits[kHashMaxKeys / 32];
   __shared__ uint16_t srt[kHashMaxKeys];
   __shared__ uint32_t wsum0;
-  const int f = blockIdx.y;
-  const TableWs t = table_ws(ws, f, B);
-  const int nu = t.hdr[0];
-  const bool hashed = t.hdr[3] == kLayoutHash;
-  const int ublk = blockIdx.x * WPB;
-  if (ublk >= nu) return;  // uniform per block
   const int worker = threadIdx.x / LPR;
   const int l = threadIdx.x % LPR;
   const int e0 = l * EPL;
   const int D = bank.dim;
+  const int F = bank.n_tables;
   const bool v_lane = e0 + EPL <= D;
   const bool w_lane = bank.has_w && e0 == D;
   const bool live = v_lane || w_lane;
+#if MREC_APPLY_EXP == 6
+  // sample-major blocks first
+  const int n_sm = gridDim.x - F * seg_blocks;
+  const int blk = blockIdx.x < n_sm ? blockIdx.x + F * seg_blocks : blockIdx.x - n_sm;
+#else
+  const int blk = blockIdx.x;
+#endif
+#if MREC_APPLY_EXP == 1
+  return;
+#endif
+#if MREC_APPLY_EXP == 2
+  if (blk < F * seg_blocks) return;
+#endif
+#if MREC_APPLY_EXP == 3
+  if (blk >= F * seg_blocks) return;
+#endif
+  if (blk >= F * seg_blocks) {
+    // rows hit once (hash layout): one lookup per worker, sample-major
+    const int q = (blk - F * seg_blocks) * WPB + worker;
+    if (q >= B * F || !live) return;
+    const int b = q / F, f = q - b * F;
+    const int row = table_ws(ws, f, B).lut[b];
+    float g[EPL];
+#if MREC_APPLY_EXP == 5
+#pragma unroll
+    for (int j = 0; j < EPL; ++j) g[j] = 1e-9f * b;
+#else
+    lookup_grad<EPL>(a, b, f, D, e0, v_lane, w_lane, g);
+#endif
+#if MREC_APPLY_EXP == 4
+    if (g[0] == 12345.f) *(float *)a.grad = g[1];
+    return;
+#endif
+    if (row >= 0) {
+      float acc[EPL];
+#pragma unroll
+      for (int j = 0; j < EPL; ++j) acc[j] = 0.f + g[j];
+      apply_row<T>(bank, a, f, row, e0, v_lane, acc);
+    }
+    return;
+  }
+  const int f = blk / seg_blocks;
+  const TableWs t = table_ws(ws, f, B);
+  const int ublk = (blk - f * seg_blocks) * WPB;
+  const int u = ublk + worker;
+  // the segment descriptor is loaded together with the header (one latency)
+  int4 d = make_int4(0, 0, 0, 0);
+  if (hash_layout) {
+    if (u <= B / 2) d = t.desc[u];
+  } else if (u < B) {
+    d.x = t.uniq[u];
+    d.z = t.seg[u];
+    d.y = t.seg[u + 1] - d.z;
+  }
+  const int nu = t.hdr[0];
+  if (ublk >= nu) return;  // uniform per block
   if (threadIdx.x == 0) n_long = 0;
   __syncthreads();
 
-  const int u = ublk + worker;
+  const int row = d.x, n = d.y;
   bool mine = u < nu;
-  int start = 0, n = 0;
-  if (mine) {
-    start = t.seg[u];
-    n = hashed ? t.segn[u] : t.seg[u + 1] - start;
-    if (n > kShortSeg) {
-      if (l == 0) long_list[atomicAdd(&n_long, 1)] = u;
-      mine = false;
-    }
+  if (mine && n > kShortSeg) {
+    if (l == 0) long_list[atomicAdd(&n_long, 1)] = u;
+    mine = false;
   }
   if (mine && live) {
+    // the row's old contents are fetched first, in parallel with the gradients
+    const uint4 raw = *reinterpret_cast<const uint4 *>(row_ptr<T>(bank, a, f, row, e0));
     float acc[EPL];
 #pragma unroll
     for (int j = 0; j < EPL; ++j) acc[j] = 0.f;
-    if (hashed) {
-      // unordered segment of <= 16 lookups: sort the sample indices in registers,
-      // then sum in ascending order exactly like the sorted layout
+    if (hash_layout && n == 2) {
+      // the common repeated row: both lookups in the descriptor, loaded together
+      float g0[EPL], g1[EPL];
+      lookup_grad<EPL>(a, min(d.z, d.w), f, D, e0, v_lane, w_lane, g0);
+      lookup_grad<EPL>(a, max(d.z, d.w), f, D, e0, v_lane, w_lane, g1);
+#pragma unroll
+      for (int j = 0; j < EPL; ++j) acc[j] = (acc[j] + g0[j]) + g1[j];
+    } else {
+      // sample indices of the segment (<= 16) in registers, ascending: the sorted
+      // layout has them in order, the hash layout is sorted here by a network
       int r[kShortSeg];
 #pragma unroll
-      for (int j = 0; j < kShortSeg; ++j) r[j] = j < n ? t.perm[start + j] : INT_MAX;
-      if (n <= 2)
-        bitonic_sort<2>(r);
-      else if (n <= 4)
-        bitonic_sort<4>(r);
-      else if (n <= 8)
-        bitonic_sort<8>(r);
-      else
-        bitonic_sort<16>(r);
+      for (int j = 0; j < kShortSeg; ++j) r[j] = j < n ? t.perm[d.z + j] : INT_MAX;
+      if (hash_layout) {
+        if (n <= 4)
+          bitonic_sort<4>(r);
+        else if (n <= 8)
+          bitonic_sort<8>(r);
+        else
+          bitonic_sort<16>(r);
+      }
 #pragma unroll
       for (int j = 0; j < kShortSeg; ++j)
         if (j < n) add_lookup_grad<EPL>(a, r[j], f, D, e0, v_lane, w_lane, acc);
-    } else {
-      const int end = start + n;
-      for (int i = start; i < end; i += 4) {
-        int bb[4];
-#pragma unroll
-        for (int k = 0; k < 4; ++k) bb[k] = (i + k < end) ? t.perm[i + k] : -1;
-#pragma unroll
-        for (int k = 0; k < 4; ++k)
-          if (bb[k] >= 0) add_lookup_grad<EPL>(a, bb[k], f, D, e0, v_lane, w_lane, acc);
-      }
     }
-    apply_row<T>(bank, a, f, t.uniq[u], e0, v_lane, acc);
+    apply_row_raw<T>(bank, a, f, row, e0, v_lane, acc, raw);
   }
   __syncthreads();
   const int nl = n_long;
@@ -617,9 +714,18 @@ __global__ __launch_bounds__(256) void apply_kernel(BankArgs bank, int64_t B, co
     // each hot segment is summed independently, so the (atomic) list order
     // does not change any result
     const int uu = long_list[k];
-    const int s0 = t.seg[uu];
-    const int sn = hashed ? t.segn[uu] : t.seg[uu + 1] - s0;
-    if (hashed) {
+    int s0, sn, lrow;
+    if (hash_layout) {
+      const int4 dd = t.desc[uu];
+      lrow = dd.x;
+      sn = dd.y;
+      s0 = dd.z;
+    } else {
+      lrow = t.uniq[uu];
+      s0 = t.seg[uu];
+      sn = t.seg[uu + 1] - s0;
+    }
+    if (hash_layout) {
       // ascending sample order through an LDS bitmap of the batch (B <= 4096;
       // a sample looks a table up once, so the bits are the segment)
       for (int i = tid; i < kHashMaxKeys / 32; i += 256) bits[i] = 0u;
@@ -655,8 +761,8 @@ __global__ __launch_bounds__(256) void apply_kernel(BankArgs bank, int64_t B, co
     for (int j = 0; j < EPL; ++j) acc[j] = 0.f;
     if (live)
       for (int i = worker; i < sn; i += WPB)
-        add_lookup_grad<EPL>(a, hashed ? static_cast<int>(srt[i]) : t.perm[s0 + i], f, D, e0,
-                             v_lane, w_lane, acc);
+        add_lookup_grad<EPL>(a, hash_layout ? static_cast<int>(srt[i]) : t.perm[s0 + i], f, D,
+                             e0, v_lane, w_lane, acc);
 #pragma unroll
     for (int j = 0; j < EPL; ++j) red[worker][e0 + j] = acc[j];
     __syncthreads();
@@ -670,7 +776,7 @@ __global__ __launch_bounds__(256) void apply_kernel(BankArgs bank, int64_t B, co
     if (worker == 0 && live) {
 #pragma unroll
       for (int j = 0; j < EPL; ++j) acc[j] = red[0][e0 + j];
-      apply_row<T>(bank, a, f, t.uniq[uu], e0, v_lane, acc);
+      apply_row<T>(bank, a, f, lrow, e0, v_lane, acc);
     }
     __syncthreads();
   }
@@ -798,8 +904,13 @@ mrec_status mrec_emb_bwd_apply_given(const mrec_table_bank *bank, int64_t batch,
   a.chunk_stride = chunk_stride;
   hipStream_t s = static_cast<hipStream_t>(stream);
   const int wpb = 256 / lpr;
-  const dim3 grid(static_cast<unsigned>((batch + wpb - 1) / wpb), static_cast<unsigned>(F));
-#define MREC_AK(T, L) apply_kernel<T, L><<<grid, 256, 0, s>>>(ba, batch, workspace, a)
+  // hash layout (batch <= kHashMaxKeys, see mrec_emb_bwd_plan): segments only for
+  // rows hit twice or more (<= batch / 2 of them), plus the sample-major blocks
+  const bool hash = batch <= kHashMaxKeys;
+  const int seg_blocks = static_cast<int>(((hash ? batch / 2 : batch) + wpb - 1) / wpb);
+  const int64_t sm_blocks = hash ? (batch * F + wpb - 1) / wpb : 0;
+  const dim3 grid(static_cast<unsigned>(static_cast<int64_t>(seg_blocks) * F + sm_blocks));
+#define MREC_AK(T, L) apply_kernel<T, L><<<grid, 256, 0, s>>>(ba, batch, workspace, a, seg_blocks, hash ? 1 : 0)
   if (bank->dtype == MREC_BF16) {
     switch (lpr) {
       case 1: MREC_AK(uint16_t, 1); break;

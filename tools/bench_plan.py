@@ -34,11 +34,19 @@ def main():
         _plan()
     torch.cuda.synchronize()
     n = 200
-    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-    e0.record()
-    for _ in range(n):
-        _plan()
-    e1.record()
+    # graph-captured back-to-back launches: device time, no host launch overhead
+    s = torch.cuda.Stream()
+    s.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(s):
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g, stream=s):
+            for _ in range(n):
+                _plan()
+        g.replay()
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record(s)
+        g.replay()
+        e1.record(s)
     torch.cuda.synchronize()
     print(f"plan B={B} rows={rows} zipf={zipf}: {e0.elapsed_time(e1) * 1e3 / n:.2f} us/launch")
     lib = _mrec.lib()

@@ -1,0 +1,6 @@
+set -o pipefail
+cd $GRAFT_REPO_ROOT
+timeout -k 10 60 python tools/bench_apply.py || exit 1
+for e in; do
+  MREC_LIB_PATH=$GRAFT_REPO_ROOT/pytorchrec_amd/lib/variants/libmrec_exp$e.so timeout -k 10 60 python tools/bench_apply.py || exit 1
+done

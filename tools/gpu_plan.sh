@@ -6,5 +6,5 @@ tail -1 gpurun_out/emb_tests.log
 for a in "4096 38462" "4096 3" "4096 50" "4096 1000000" "4096 38462 zipf" "4096 1000000 zipf" "8192 38462"; do
   timeout -k 10 60 python tools/bench_plan.py $a || exit 1
 done
-MREC_LIB_PATH=$GRAFT_REPO_ROOT/pytorchrec_amd/lib/variants/libmrec_planprof.so timeout -k 10 60 python tools/bench_plan.py 4096 38462 || exit 1
+
 bash tools/gpu_round.sh

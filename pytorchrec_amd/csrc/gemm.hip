@@ -266,9 +266,24 @@ __device__ __forceinline__ void epilogue_chunk(const GemmArgs &g, int64_t m, int
 // ---------------------------------------------------------------------------
 // the kernel
 // ---------------------------------------------------------------------------
+#ifdef MREC_GEMM_PROF
+// per-workgroup wall-clock stamps (100 MHz) of the last launch: start, first
+// k group landed, main loop done, epilogue stores retired (tools/bench_gemm.py --prof)
+__device__ uint64_t g_gemm_prof[4096][4];
+#define GEMM_STAMP(k)                                                          \
+  do {                                                                         \
+    if (threadIdx.x == 0 && bz == 0 && bx < 4096) g_gemm_prof[bx][k] = wall_clock64(); \
+  } while (0)
+#else
+#define GEMM_STAMP(k) \
+  do {                \
+  } while (0)
+#endif
+
 // one output tile (workgroup `bx` of the tile grid, K slice `bz`)
 template <bool A_COL, bool B_COL>
 __device__ __forceinline__ void gemm_tile(const GemmArgs &g, int bx, int bz, uint16_t *smem) {
+  GEMM_STAMP(0);
   const int64_t kb = static_cast<int64_t>(bz) * g.k_per_split;
   const int64_t ke = min(g.K, kb + g.k_per_split);
   const int64_t krel = ke > kb ? ke - kb : 0;
@@ -332,6 +347,7 @@ __device__ __forceinline__ void gemm_tile(const GemmArgs &g, int bx, int bz, uin
       default: wait_vmcnt<24>(); break;
     }
     asm volatile("s_barrier" ::: "memory");
+    if (kg == 0) GEMM_STAMP(1);
     if (kg + NBUF - 1 < nkg) {
       da.issue(kg + NBUF - 1, krel, a_buf(kg + NBUF - 1), wave);
       db.issue(kg + NBUF - 1, krel, b_buf(kg + NBUF - 1), wave);
@@ -382,6 +398,7 @@ __device__ __forceinline__ void gemm_tile(const GemmArgs &g, int bx, int bz, uin
 
   // ---- epilogue: C tile -> LDS (fp32) -> 8-column chunks ----
   __syncthreads();
+  GEMM_STAMP(2);
   float *T = reinterpret_cast<float *>(smem);
 #pragma unroll
   for (int i = 0; i < 2; ++i)
@@ -414,6 +431,10 @@ __device__ __forceinline__ void gemm_tile(const GemmArgs &g, int bx, int bz, uin
       epilogue_chunk(g, m, n, v);
     }
   }
+#ifdef MREC_GEMM_PROF
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  GEMM_STAMP(3);
+#endif
 }
 
 template <bool A_COL, bool B_COL>
@@ -668,6 +689,12 @@ mrec_status mrec_gemm(int64_t M, int64_t N, int64_t K, const mrec_operand *A,
   splitk_reduce_kernel<<<dim3(static_cast<unsigned>(reduce_blocks(g))), 256, 0, s>>>(g);
   return launch_status("mrec_gemm(split-k reduce)");
 }
+
+#ifdef MREC_GEMM_PROF
+void mrec_gemm_prof_read(uint64_t *out, int n) {
+  (void)hipMemcpyFromSymbol(out, HIP_SYMBOL(g_gemm_prof), sizeof(uint64_t) * 4 * n);
+}
+#endif
 
 mrec_status mrec_gemm_multi(int32_t n, const mrec_gemm_call *calls, mrec_stream stream) {
   MREC_CHECK_ARG(n >= 0 && n <= MULTI_MAX && (n == 0 || calls), "n out of [0, 4]");

@@ -38,10 +38,32 @@ def timed(fn, reps):
     return e0.elapsed_time(e1) * 1e3 / (reps // 10 * 10)
 
 
+def prof_report(fn):
+    import ctypes
+    import numpy as np
+    n = 4096
+    buf = (ctypes.c_uint64 * (4 * n))()
+    _mrec.lib().mrec_gemm_prof_read(buf, n)
+    t = np.frombuffer(buf, dtype=np.uint64).reshape(n, 4).astype(np.int64)
+    t = t[(t[:, 0] > 0) & (t[:, 3] >= t[:, 0])]
+    recent = t[:, 0] >= t[:, 0].max() - 100000  # the last launch only (1 ms window)
+    t = t[recent]
+    t0 = t[:, 0].min()
+    ns = lambda x: x * 10  # noqa: E731
+    q = lambda x: np.percentile(ns(x), [0, 50, 100]).round(0).tolist()  # noqa: E731
+    print(f"    {len(t)} workgroups; span {ns(t[:, 3].max() - t0)} ns")
+    print(f"    start offset  min/med/max {q(t[:, 0] - t0)}")
+    print(f"    first group   {q(t[:, 1] - t[:, 0])}")
+    print(f"    main loop     {q(t[:, 2] - t[:, 1])}")
+    print(f"    epilogue      {q(t[:, 3] - t[:, 2])}")
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--reps", type=int, default=200)
     ap.add_argument("--only", default="")
+    ap.add_argument("--prof", action="store_true",
+                    help="print per-workgroup phase times (library built with -DMREC_GEMM_PROF)")
     a = ap.parse_args()
     dev = torch.device("cuda:0")
     M, N, K = 4096, 400, 429
@@ -94,6 +116,10 @@ def main():
             tr = timed(ref[name], a.reps)
             line += f"   | torch/hipBLASLt {tr:8.2f} us"
         print(line, flush=True)
+        if a.prof and hasattr(_mrec.lib(), "mrec_gemm_prof_read"):
+            fn()
+            torch.cuda.synchronize()
+            prof_report(fn)
 
 
 if __name__ == "__main__":

@@ -47,6 +47,9 @@ def parse():
     p.add_argument("--zipf", type=float, default=0.0, help="Zipf alpha for ids (0 = uniform)")
     p.add_argument("--lr", type=float, default=1e-2)
     p.add_argument("--no-graph", action="store_true")
+    p.add_argument("--graph-steps", type=int, default=4,
+                   help="consecutive train steps (one per resident batch) captured in one HIP "
+                        "graph: one graph launch per G steps instead of per step")
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--cpu-seconds", type=float, default=12.0)
     p.add_argument("--no-roofline", action="store_true")
@@ -216,7 +219,8 @@ def kernel_rooflines(model, data, args):
     with torch.no_grad():
         def fwd():
             E._InteractFn.forward(_Ctx(), bank.weight, dense_weight, global_bias, None,
-                                  bank, ids, dense, True, True, model.x0_cols, torch.bfloat16)
+                                  bank, ids, dense, True, True, model.x0_cols, torch.bfloat16,
+                                  False)
         # bytes/sample: ids F*4 + useful row bytes F*(D+1)*2 + dense 13*4 + x0 write
         # x0_cols*2 + logit 4 + fm_sum D*4
         fwd_bytes = F * 4 + F * (D + 1) * 2 + CRITEO_DENSE * 4 + model.x0_cols * 2 + 4 + D * 4
@@ -233,7 +237,7 @@ def kernel_rooflines(model, data, args):
 
         x0, logit = E._InteractFn.forward(_Ctx(), bank.weight, dense_weight, global_bias, None,
                                           bank, ids, dense, True, True, model.x0_cols,
-                                          torch.bfloat16)
+                                          torch.bfloat16, False)
         fm_sum = torch.zeros(B, D, device=x0.device)
         dx0 = torch.zeros_like(x0)
         dl = torch.zeros(B, device=x0.device)
@@ -355,6 +359,13 @@ def main():
                 with torch.cuda.graph(g):
                     step(d)
                 graphs.append(g)
+            multi = None
+            G = max(1, min(args.graph_steps, 4))
+            if G > 1:
+                multi = torch.cuda.CUDAGraph()
+                with torch.cuda.graph(multi):
+                    for k in range(G):
+                        step(datas[k])
         except Exception as e:  # e.g. a collective the runtime cannot capture
             print(f"bench: HIP graph capture failed ({type(e).__name__}: {e}); running eagerly",
                   file=sys.stderr, flush=True)
@@ -368,8 +379,21 @@ def main():
         else:
             graphs[i % 4].replay()
 
-    for i in range(args.warmup):
-        run(i)
+    def run_steps(n):
+        """n train steps, batch i % 4 at step i: G-step graphs while n allows, then
+        single-step graphs (the G-step graph starts at batch 0: n is split so)."""
+        i = 0
+        if graphs is not None and multi is not None:
+            while n - i >= G:
+                multi.replay()
+                i += G
+        while i < n:
+            run(i)
+            i += 1
+
+    if graphs is None:
+        multi, G = None, 1
+    run_steps(args.warmup)
 
     def barrier():
         if world > 1:
@@ -378,8 +402,7 @@ def main():
 
     barrier()
     t0 = time.perf_counter()
-    for i in range(args.steps):
-        run(i)
+    run_steps(args.steps)
     barrier()
     elapsed = time.perf_counter() - t0
     from pytorchrec_amd.sharding import ShardedEmbeddingBank
@@ -427,7 +450,8 @@ def main():
         "config": {"workload": workloads[args.model],
                    "global_batch": args.batch * world, "batch_per_gpu": args.batch,
                    "parallelism": (f"dp{world}+rowshard{world}" if sharded else "single"),
-                   "hip_graph": not args.no_graph},
+                   "hip_graph": not args.no_graph,
+                   "steps_per_graph": G if graphs is not None else 0},
     }
     if rank == 0 and not args.no_roofline and args.model == "deepfm":
         ks = kernel_rooflines(model, datas[0], args)

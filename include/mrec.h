@@ -32,9 +32,10 @@
 extern "C" {
 #endif
 
-#define MREC_ABI_VERSION 7
+#define MREC_ABI_VERSION 8
 #define MREC_MAX_TABLES 64      /* tables per table bank / per call */
 #define MREC_BWD_MAX_BATCH 8192  /* lookups per table per plan/apply call */
+#define MREC_BWD_HASH_MAX_BATCH 4096  /* batches up to this use the hash plan */
 
 typedef enum {
   MREC_OK = 0,
@@ -157,11 +158,12 @@ typedef enum {
 size_t mrec_emb_bwd_workspace_size(int32_t n_tables, int64_t batch);
 
 /*
- * Deterministic sorted-segment plan: per table, the lookups are sorted by
- * (id, sample) in LDS and segmented by unique row.  Depends only on the ids, so
- * it can run on a side stream as soon as the batch is resident.  If d_step
- * (device uint64, may be NULL) is given the plan increments it once, so a graph
- * replayed step after step still draws fresh stochastic-rounding bits.
+ * Plan of the embedding backward: per table the lookups are grouped by row (an
+ * LDS hash table for batch <= MREC_BWD_HASH_MAX_BATCH, a stable LDS radix sort
+ * up to MREC_BWD_MAX_BATCH).  Depends only on the ids, so it can run as soon as
+ * the batch is resident (or inside a GEMM launch: mrec_gemm_multi_plan).  If
+ * d_step (device uint64, may be NULL) is given the plan increments it once, so a
+ * graph replayed step after step still draws fresh stochastic-rounding bits.
  */
 mrec_status mrec_emb_bwd_plan(const mrec_table_bank *bank, const mrec_ids *ids, int64_t batch,
                               void *workspace, size_t ws_bytes, int32_t *d_oob_flag,
@@ -355,6 +357,27 @@ typedef struct {
  * dW reduction (+ fused SGD) overlap instead of paying three launch boundaries.
  */
 mrec_status mrec_gemm_multi(int32_t n, const mrec_gemm_call *calls, mrec_stream stream);
+
+/* an embedding-backward hash plan (arguments of mrec_emb_bwd_plan) */
+typedef struct {
+  const mrec_table_bank *bank;
+  const mrec_ids *ids;
+  int64_t batch; /* 1 .. MREC_BWD_HASH_MAX_BATCH */
+  void *workspace;
+  size_t ws_bytes;
+  int32_t *d_oob_flag;
+  uint64_t *d_step;
+} mrec_plan_job;
+
+/*
+ * mrec_gemm_multi plus the embedding-backward plan of `plan` (may be NULL) run by
+ * extra workgroups of the same launch, one per table: a HIP graph runs the
+ * step's kernels one after another, so a plan launched on its own sits on the
+ * critical path; beside a latency-bound backward GEMM it is hidden.  Same
+ * workspace contents as mrec_emb_bwd_plan.
+ */
+mrec_status mrec_gemm_multi_plan(int32_t n, const mrec_gemm_call *calls, const mrec_plan_job *plan,
+                                 mrec_stream stream);
 
 /*
  * fp32 [N, K] weight (row stride ldw) -> bf16 images for the GEMMs: `row`

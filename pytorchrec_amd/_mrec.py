@@ -20,9 +20,10 @@ import torch  # noqa: F401  (must precede the dlopen, see module docstring)
 LIB_DIR = os.path.join(os.path.dirname(os.path.abspath(__file__)), "lib")
 LIB_PATH = os.environ.get("MREC_LIB_PATH") or os.path.join(LIB_DIR, "libmrec.so")
 
-ABI_VERSION = 7
+ABI_VERSION = 8
 MAX_TABLES = 64
 BWD_MAX_BATCH = 8192
+BWD_HASH_MAX_BATCH = 4096  # batches up to this use the hash plan (fusable into a GEMM launch)
 
 # mrec_status
 OK, EINVAL, EOOB, EHIP, ERCCL, ENOSPC = range(6)
@@ -97,6 +98,13 @@ class GemmCall(ctypes.Structure):
 
 GEMM_FULL, GEMM_PARTIAL, GEMM_REDUCE = 0, 1, 2
 
+
+class PlanJob(ctypes.Structure):
+    _fields_ = [("bank", ctypes.POINTER(TableBank)), ("ids", ctypes.POINTER(Ids)),
+                ("batch", ctypes.c_int64), ("workspace", ctypes.c_void_p),
+                ("ws_bytes", ctypes.c_size_t), ("d_oob_flag", ctypes.c_void_p),
+                ("d_step", ctypes.c_void_p)]
+
 LAYOUT_ROW, LAYOUT_COL = 0, 1
 ACT_NONE, ACT_RELU = 0, 1
 
@@ -140,6 +148,8 @@ SIGNATURES = {
     "mrec_gemm": (ctypes.c_int, [_i64, _i64, _i64, _op_p, _op_p, _i64, _i64, _epi_p,
                                  _vp, ctypes.c_int, _i64, _i32, _vp, ctypes.c_size_t, _vp]),
     "mrec_gemm_multi": (ctypes.c_int, [_i32, ctypes.POINTER(GemmCall), _vp]),
+    "mrec_gemm_multi_plan": (ctypes.c_int, [_i32, ctypes.POINTER(GemmCall),
+                                            ctypes.POINTER(PlanJob), _vp]),
     "mrec_weight_prep": (ctypes.c_int, [_vp, _i64, _i64, _i64, _vp, _i64, _vp, _i64, _vp]),
     "mrec_head_fwd": (ctypes.c_int, [_vp, _i64, _i64, _i32, _vp, _vp, _vp, _vp, _vp]),
     "mrec_head_bwd": (ctypes.c_int, [_vp, _vp, _i64, _i32, _vp, _i64, _vp, _i64, _vp]),

@@ -27,6 +27,7 @@
 #include <algorithm>
 
 #include "common.h"
+#include "emb_plan.h"
 
 namespace mrec {
 
@@ -476,20 +477,41 @@ __global__ __launch_bounds__(256) void splitk_reduce_kernel(GemmArgs g) {
 // overlap instead of paying a launch boundary each.
 // ---------------------------------------------------------------------------
 constexpr int MULTI_MAX = 4;
+constexpr size_t kGemmLdsMin = NBUF * 2 * GROUP_ELEMS * sizeof(uint16_t);  // <= kGemmLds
 enum : int { JOB_GEMM_RR = 0, JOB_GEMM_RC = 1, JOB_GEMM_CR = 2, JOB_GEMM_CC = 3, JOB_REDUCE = 4 };
+
+struct PlanJob {  // an embedding-backward hash plan run by the first workgroups
+  BankArgs bank;
+  IdsArgs ids;
+  int64_t B;
+  void *ws;
+  int32_t *oob;
+  uint64_t *d_step;
+};
 
 struct MultiArgs {
   int n;
+  int plan_blocks;  // leading workgroups that run `plan` (one per table, padded to 8)
   int kind[MULTI_MAX];
   int tile_blocks[MULTI_MAX];  // workgroups per K slice (GEMM jobs)
   int nblk[MULTI_MAX];         // workgroups with work (the rest pad to a multiple of 8)
   int start[MULTI_MAX + 1];
   GemmArgs g[MULTI_MAX];
+  PlanJob plan;
 };
+
+static_assert((2 * kHashSlotsSmall + 1) * 4 <= kGemmLdsMin, "plan table exceeds the GEMM LDS");
 
 __global__ __launch_bounds__(GEMM_THREADS) void gemm_multi_kernel(MultiArgs ma) {
   extern __shared__ __attribute__((aligned(16))) uint16_t smem[];
-  const int b = blockIdx.x;
+  if (static_cast<int>(blockIdx.x) < ma.plan_blocks) {  // uniform
+    if (static_cast<int>(blockIdx.x) < ma.plan.bank.n_tables)
+      plan_hash_body<GEMM_THREADS, kHashSlotsSmall>(ma.plan.bank, ma.plan.ids, ma.plan.B,
+                                                     ma.plan.ws, ma.plan.oob, ma.plan.d_step,
+                                                     blockIdx.x, reinterpret_cast<uint32_t *>(smem));
+    return;
+  }
+  const int b = blockIdx.x - ma.plan_blocks;
   int p = 0;
   while (p + 1 < ma.n && b >= ma.start[p + 1]) ++p;  // uniform
   const int local = b - ma.start[p];
@@ -697,8 +719,33 @@ void mrec_gemm_prof_read(uint64_t *out, int n) {
 #endif
 
 mrec_status mrec_gemm_multi(int32_t n, const mrec_gemm_call *calls, mrec_stream stream) {
+  return mrec_gemm_multi_plan(n, calls, nullptr, stream);
+}
+
+mrec_status mrec_gemm_multi_plan(int32_t n, const mrec_gemm_call *calls, const mrec_plan_job *plan,
+                                 mrec_stream stream) {
   MREC_CHECK_ARG(n >= 0 && n <= MULTI_MAX && (n == 0 || calls), "n out of [0, 4]");
   MultiArgs ma = {};
+  if (plan) {
+    int eb, lpr;
+    mrec_status st = make_bank_args(plan->bank, &ma.plan.bank, &eb, &lpr);
+    if (st != MREC_OK) return st;
+    if ((st = make_ids_args(plan->ids, ma.plan.bank.n_tables, &ma.plan.ids)) != MREC_OK) return st;
+    MREC_CHECK_ARG(plan->batch >= 1 && plan->batch <= kHashMaxKeys,
+                   "plan batch must be in [1, MREC_BWD_HASH_MAX_BATCH]");
+    MREC_CHECK_ARG(plan->workspace != nullptr, "plan workspace is NULL");
+    if (plan->ws_bytes < mrec_emb_bwd_workspace_size(ma.plan.bank.n_tables, plan->batch)) {
+      set_error("mrec_gemm_multi_plan: plan workspace too small");
+      return MREC_ENOSPC;
+    }
+    for (int f = 0; f < ma.plan.bank.n_tables; ++f)
+      MREC_CHECK_ARG(ma.plan.bank.rows[f] < (int64_t(1) << 31), "rows per table must be < 2^31");
+    ma.plan.B = plan->batch;
+    ma.plan.ws = plan->workspace;
+    ma.plan.oob = plan->d_oob_flag;
+    ma.plan.d_step = plan->d_step;
+    ma.plan_blocks = (ma.plan.bank.n_tables + 7) / 8 * 8;
+  }
   int blocks = 0;
   for (int i = 0; i < n; ++i) {
     const mrec_gemm_call &c = calls[i];
@@ -733,7 +780,7 @@ mrec_status mrec_gemm_multi(int32_t n, const mrec_gemm_call *calls, mrec_stream 
     blocks += static_cast<int>((nb + 7) / 8 * 8);
     ma.n = j + 1;
   }
-  if (ma.n == 0) return MREC_OK;
+  if (ma.n == 0 && ma.plan_blocks == 0) return MREC_OK;
   ma.start[ma.n] = blocks;
   static const bool attr = [] {
     (void)hipFuncSetAttribute(reinterpret_cast<const void *>(gemm_multi_kernel),
@@ -742,8 +789,8 @@ mrec_status mrec_gemm_multi(int32_t n, const mrec_gemm_call *calls, mrec_stream 
     return true;
   }();
   (void)attr;
-  gemm_multi_kernel<<<dim3(static_cast<unsigned>(blocks)), GEMM_THREADS, kGemmLds,
-                      static_cast<hipStream_t>(stream)>>>(ma);
+  gemm_multi_kernel<<<dim3(static_cast<unsigned>(ma.plan_blocks + blocks)), GEMM_THREADS,
+                      kGemmLds, static_cast<hipStream_t>(stream)>>>(ma);
   return launch_status("mrec_gemm_multi");
 }
 

@@ -27,6 +27,8 @@ Update modes (``EmbeddingBank.update``):
 """
 from __future__ import annotations
 
+import ctypes
+import os
 from typing import List, Optional, Sequence
 
 import torch
@@ -208,6 +210,54 @@ class _AsyncPlan(_AsyncPlanBase):
         super().__init__(bank.weight.device, lambda: _plan(bank, ids, 0, batch, None), ids)
 
 
+class _FusedPlan:
+    """Hash plan (batch <= BWD_HASH_MAX_BATCH) run by spare workgroups of the next
+    backward GEMM launch (``dense.defer_plan``), on the same stream; ``get`` launches
+    it on its own if no GEMM launch took it (no MLP, or not fused-SGD)."""
+
+    def __init__(self, bank: EmbeddingBank, ids, batch: int):
+        from pytorchrec_amd import dense as dense_ops
+        n = bank.n_tables
+        self.ws_bytes = _mrec.lib().mrec_emb_bwd_workspace_size(n, batch)
+        self.ws = torch.empty(self.ws_bytes, dtype=torch.uint8, device=bank.weight.device)
+        self.bank, self.ids, self.batch = bank, ids, batch
+        self.idd = _ids_desc(ids)
+        self.launched = False
+        dense_ops.defer_plan(self)
+
+    def job(self) -> _mrec.PlanJob:
+        desc = self.bank.desc()
+        desc.ref()  # refresh the data pointer
+        self._job = _mrec.PlanJob(ctypes.pointer(desc.struct), ctypes.pointer(self.idd.struct),
+                                  self.batch, self.ws.data_ptr(), self.ws_bytes, None,
+                                  self.bank.step_counter().data_ptr())
+        return self._job
+
+    def get(self):
+        if not self.launched:
+            _mrec.call("mrec_emb_bwd_plan", self.bank.desc().ref(), self.idd.ref(), self.batch,
+                       self.ws.data_ptr(), self.ws_bytes, None,
+                       self.bank.step_counter().data_ptr(), _mrec.stream_handle())
+            self.launched = True
+        return self.ws, self.ws_bytes
+
+
+# The plan inside a backward GEMM launch (256-thread workgroups sharing CUs with
+# the GEMM) measured slower than the standalone 1024-thread plan kernel (C2:
+# 36-48 us launch vs 19 + 10 us), so it is opt-in (MREC_FUSE_PLAN=1).
+FUSE_PLAN = os.environ.get("MREC_FUSE_PLAN", "0") == "1"
+
+
+def _make_plan(bank: EmbeddingBank, ids, batch: int):
+    if FUSE_PLAN and 1 <= batch <= _mrec.BWD_HASH_MAX_BATCH:
+        return _FusedPlan(bank, ids, batch)
+    if torch.cuda.is_current_stream_capturing():
+        # a HIP graph runs its kernels one after another anyway, and the side
+        # stream's fork/join cost 11 us per step (C2): plan in the backward
+        return None
+    return _AsyncPlan(bank, ids, batch)
+
+
 def _apply(bank: EmbeddingBank, ws, ws_bytes, count, dx=None, dfm=None, fm_sum=None, x0=None,
            dw=None, grad=None):
     """Run the fused backward for lookups [0, count) described by ``ws``; the
@@ -240,7 +290,7 @@ def _backward_into_bank(bank: EmbeddingBank, ids, batch, plan_ws, dx=None, dfm=N
     if bank.update == "dense":
         grad = torch.zeros_like(bank.weight)
     if plan_ws is not None:
-        ws, wsb = plan_ws.get() if isinstance(plan_ws, _AsyncPlan) else plan_ws
+        ws, wsb = plan_ws.get() if isinstance(plan_ws, (_AsyncPlan, _FusedPlan)) else plan_ws
         _apply(bank, ws, wsb, batch, dx, dfm, fm_sum, x0, dw, grad)
         return grad
     for s, c in _chunks(batch):
@@ -264,7 +314,7 @@ def _needs_backward(bank: EmbeddingBank) -> bool:
 class _GatherFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, weight, trigger, bank: EmbeddingBank, ids: List[torch.Tensor], out_dtype,
-                want_w: bool):
+                want_w: bool, need_bwd: bool):
         B = ids[0].shape[0]
         F, D = bank.n_tables, bank.dim
         dev = weight.device
@@ -276,8 +326,8 @@ class _GatherFn(torch.autograd.Function):
                        out.data_ptr(), _mrec.dtype_code(out_dtype), out.stride(0),
                        _mrec.ptr(w_out), _mrec.ptr(flag), _mrec.stream_handle())
         plan_ws = None
-        if _needs_backward(bank) and 0 < B <= _mrec.BWD_MAX_BATCH:
-            plan_ws = _AsyncPlan(bank, ids, B)
+        if need_bwd and 0 < B <= _mrec.BWD_MAX_BATCH:
+            plan_ws = _make_plan(bank, ids, B)
         _raise_if_oob(flag)
         ctx.bank, ctx.ids, ctx.B, ctx.plan_ws = bank, ids, B, plan_ws
         if want_w:
@@ -295,7 +345,7 @@ class _GatherFn(torch.autograd.Function):
                                           "per call; use interact() for multi-field models")
             dw = dw_out.reshape(-1).contiguous().float()
         grad = _backward_into_bank(bank, ctx.ids, ctx.B, ctx.plan_ws, dx=dx, dw=dw)
-        return grad, None, None, None, None, None
+        return grad, None, None, None, None, None, None
 
 
 def gather(bank: EmbeddingBank, ids: Sequence[torch.Tensor], out_dtype=None, with_w=False):
@@ -310,7 +360,10 @@ def gather(bank: EmbeddingBank, ids: Sequence[torch.Tensor], out_dtype=None, wit
     if not bank.weight.is_cuda:
         return cpu_path.gather(bank, ids, out_dtype, with_w)
     trigger = _trigger(bank)
-    return _GatherFn.apply(bank.weight, trigger, bank, ids, out_dtype, with_w)
+    # (grad mode is off inside Function.forward: decide here whether a backward
+    # will run, so the plan can be queued ahead of it)
+    return _GatherFn.apply(bank.weight, trigger, bank, ids, out_dtype, with_w,
+                           _needs_backward(bank))
 
 
 _TRIGGERS = {}
@@ -336,7 +389,7 @@ def _trigger(bank: EmbeddingBank):
 class _InteractFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, weight, dense_w, bias, trigger, bank: EmbeddingBank, ids, dense, fm2: bool,
-                first_order: bool, x0_cols: int, x0_dtype):
+                first_order: bool, x0_cols: int, x0_dtype, need_bwd: bool):
         B = ids[0].shape[0]
         dev = weight.device
         n_dense = 0 if dense is None else dense.shape[1]
@@ -355,8 +408,8 @@ class _InteractFn(torch.autograd.Function):
                        int(x0_cols), logit.data_ptr(), _mrec.ptr(fm_sum), _mrec.ptr(flag),
                        _mrec.stream_handle())
         plan_ws = None
-        if _needs_backward(bank) and 0 < B <= _mrec.BWD_MAX_BATCH:
-            plan_ws = _AsyncPlan(bank, ids, B)
+        if need_bwd and 0 < B <= _mrec.BWD_MAX_BATCH:
+            plan_ws = _make_plan(bank, ids, B)
         _raise_if_oob(flag)
         ctx.bank, ctx.ids, ctx.B, ctx.plan_ws = bank, ids, B, plan_ws
         ctx.fm2, ctx.first_order = fm2, first_order
@@ -387,7 +440,7 @@ class _InteractFn(torch.autograd.Function):
             grad = _backward_into_bank(bank, ctx.ids, ctx.B, ctx.plan_ws, dx=dx0, dfm=dfm,
                                        fm_sum=fm_sum, x0=x0 if dfm is not None else None, dw=dw)
         g_dense_w, g_bias = _dense_first_order_grads(ctx, dlogit, dense)
-        return grad, g_dense_w, g_bias, None, None, None, None, None, None, None, None
+        return grad, g_dense_w, g_bias, None, None, None, None, None, None, None, None, None
 
 
 def _dense_first_order_grads(ctx, dlogit, dense):
@@ -432,7 +485,7 @@ def interact(bank: EmbeddingBank, ids: Sequence[torch.Tensor], dense: Optional[t
                                  x0_dtype)
     trigger = _trigger(bank)
     return _InteractFn.apply(bank.weight, dense_w, bias, trigger, bank, ids, dense, fm2,
-                             first_order, int(x0_cols), x0_dtype)
+                             first_order, int(x0_cols), x0_dtype, _needs_backward(bank))
 
 
 def fm2_dense(v: torch.Tensor) -> torch.Tensor:

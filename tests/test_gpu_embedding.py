@@ -343,3 +343,40 @@ def test_fm2_dense_kernel(gpu):
     dy = rng.standard_normal(300).astype(np.float32)
     y.backward(torch.from_numpy(dy).to(gpu))
     np.testing.assert_allclose(vt.grad.detach().cpu().numpy(), ref.fm2_bwd(v, dy), rtol=1e-5, atol=1e-5)
+
+
+@pytest.mark.parametrize("rows", [7, 5000, 200000])
+def test_plan_inside_gemm_launch_matches_standalone(gpu, rows):
+    """mrec_gemm_multi_plan's plan (256-thread workgroups, 6016-slot table) drives
+    the same updates as the standalone 1024-thread plan kernel: bitwise."""
+    import ctypes
+    from pytorchrec_amd import _mrec
+    rng = np.random.default_rng(rows)
+    B, F, D = 4096, 3, 16
+    ids_np = np.stack([np.minimum(rng.zipf(1.2, B) - 1, rows - 1), rng.integers(0, rows, B),
+                       rng.integers(0, max(1, rows // 3), B)], 1).astype(np.int64)
+    ids = [torch.from_numpy(np.ascontiguousarray(ids_np[:, f])).to(gpu) for f in range(F)]
+    dy = torch.from_numpy(rng.standard_normal((B, F * D)).astype(np.float32)).to(gpu)
+    results = []
+    for fused in (False, True):
+        bank = _bank([rows] * F, D, False, torch.float32, update="dense")
+        _fill(bank, [np.zeros((rows, D), np.float32)] * F)
+        idd = _mrec.IdsDesc(ids)
+        wsb = _mrec.lib().mrec_emb_bwd_workspace_size(F, B)
+        ws = torch.zeros(wsb, dtype=torch.uint8, device=gpu)
+        if fused:
+            job = _mrec.PlanJob(ctypes.pointer(bank.desc().struct), ctypes.pointer(idd.struct), B,
+                                ws.data_ptr(), wsb, None, None)
+            bank.desc().ref()
+            _mrec.call("mrec_gemm_multi_plan", 0, None, ctypes.byref(job), _mrec.stream_handle())
+        else:
+            _mrec.call("mrec_emb_bwd_plan", bank.desc().ref(), idd.ref(), B, ws.data_ptr(), wsb,
+                       None, None, _mrec.stream_handle())
+        grad = torch.zeros_like(bank.weight)
+        _mrec.call("mrec_emb_bwd_apply", bank.desc().ref(), B, ws.data_ptr(), wsb, dy.data_ptr(),
+                   _mrec.F32, dy.stride(0), None, None, None, _mrec.F32, 0, None,
+                   _mrec.BWD_DENSE_GRAD, 0.0, 0, None, grad.data_ptr(), _mrec.stream_handle())
+        results.append(grad[:, :D].cpu().numpy())
+    assert np.array_equal(results[0].view(np.uint32), results[1].view(np.uint32))
+    want = ref.dense_grad(rows, ids_np[:, 0], dy[:, :D].cpu().numpy())
+    np.testing.assert_allclose(results[1][:rows], want, rtol=1e-5, atol=1e-5)

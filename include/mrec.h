@@ -187,6 +187,25 @@ mrec_status mrec_emb_bwd_apply(const mrec_table_bank *bank, int64_t batch, const
                                mrec_bwd_mode mode, float lr, uint64_t seed,
                                const uint64_t *d_step, void *grad, mrec_stream stream);
 
+struct mrec_gemm_call_s; /* mrec_gemm_call, defined with the GEMM entry points below */
+
+/*
+ * mrec_emb_bwd_apply plus up to 2 deferred split-K weight-gradient reductions
+ * (mrec_gemm_call with phase MREC_GEMM_REDUCE, e.g. the first MLP layer's dW +
+ * fused SGD) run by extra workgroups of the same launch.  They must not touch
+ * what the apply reads or writes.  A HIP graph runs the step's kernels one after
+ * another, so a reduction launched on its own costs a full kernel on the
+ * critical path.
+ */
+mrec_status mrec_emb_bwd_apply_ex(const mrec_table_bank *bank, int64_t batch,
+                                  const void *workspace, size_t ws_bytes, const void *dx,
+                                  mrec_dtype dx_dtype, int64_t dx_ld, const float *dfm,
+                                  const float *fm_sum, const void *x0, mrec_dtype x0_dtype,
+                                  int64_t x0_ld, const float *dw, mrec_bwd_mode mode, float lr,
+                                  uint64_t seed, const uint64_t *d_step, void *grad,
+                                  int32_t n_reduce, const struct mrec_gemm_call_s *reduce,
+                                  mrec_stream stream);
+
 /*
  * mrec_emb_bwd_apply with the per-lookup gradient rows given directly instead of
  * derived from dx / dfm / dw (those must be NULL when g_occ is set): lookup b of
@@ -333,7 +352,7 @@ mrec_status mrec_gemm(int64_t M, int64_t N, int64_t K, const mrec_operand *A,
 #define MREC_GEMM_PARTIAL 1 /* split-K: fp32 partial slabs into workspace only */
 #define MREC_GEMM_REDUCE 2  /* split-K: fixed-order slab reduction + epilogue only */
 
-typedef struct {
+typedef struct mrec_gemm_call_s {
   int64_t M, N, K;
   const mrec_operand *A;
   const mrec_operand *B;

@@ -134,6 +134,10 @@ SIGNATURES = {
     "mrec_emb_bwd_apply": (ctypes.c_int, [_bank_p, _i64, _vp, ctypes.c_size_t, _vp, ctypes.c_int,
                                           _i64, _vp, _vp, _vp, ctypes.c_int, _i64, _vp,
                                           ctypes.c_int, _f32, ctypes.c_uint64, _vp, _vp, _vp]),
+    "mrec_emb_bwd_apply_ex": (ctypes.c_int, [_bank_p, _i64, _vp, ctypes.c_size_t, _vp, ctypes.c_int,
+                                             _i64, _vp, _vp, _vp, ctypes.c_int, _i64, _vp,
+                                             ctypes.c_int, _f32, ctypes.c_uint64, _vp, _vp, _i32,
+                                             ctypes.POINTER(GemmCall), _vp]),
     "mrec_emb_bwd_apply_given": (ctypes.c_int, [_bank_p, _i64, _vp, ctypes.c_size_t, _vp,
                                                 ctypes.c_int, _i64, _vp, _vp, _vp, ctypes.c_int,
                                                 _i64, _vp, _vp, _i64, _i64, _i64, ctypes.c_int,

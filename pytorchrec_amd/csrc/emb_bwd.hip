@@ -15,6 +15,7 @@
 //         with a fixed-order LDS tree so one hot row cannot serialise a worker.
 #include "common.h"
 #include "emb_plan.h"
+#include "gemm_common.h"
 
 namespace mrec {
 
@@ -398,6 +399,17 @@ __device__ __forceinline__ void bitonic_sort(int *r) {
       }
 }
 
+// deferred split-K weight-gradient reductions (+ fused SGD) run by trailing
+// workgroups of the apply launch: independent of the embedding update, and a
+// launch of their own would cost a kernel boundary on the step's serial path
+constexpr int kMaxCoReduce = 2;
+struct CoReduce {
+  int n;
+  int nblk[kMaxCoReduce];
+  int start[kMaxCoReduce + 1];  // workgroup offsets after the apply blocks
+  GemmArgs g[kMaxCoReduce];
+};
+
 // Grid (1-D): F * seg_blocks segment blocks (table f = blk / seg_blocks), then,
 // for the hash layout, ceil(B * F / WPB) sample-major blocks for the rows hit
 // once: worker q handles lookup (b, f) = (q / F, q % F), so a wave reads
@@ -406,7 +418,16 @@ __device__ __forceinline__ void bitonic_sort(int *r) {
 template <typename T, int LPR>
 __global__ __launch_bounds__(256, 6) void apply_kernel(BankArgs bank, int64_t B, const void *ws,
                                                        ApplyArgs a, int seg_blocks,
-                                                       int hash_layout) {
+                                                       int hash_layout, int apply_blocks,
+                                                       CoReduce co) {
+  if (static_cast<int>(blockIdx.x) >= apply_blocks) {  // uniform: a co-launched reduction
+    const int b = blockIdx.x - apply_blocks;
+    int p = 0;
+    while (p + 1 < co.n && b >= co.start[p + 1]) ++p;
+    const int local = b - co.start[p];
+    if (local < co.nblk[p]) splitk_reduce_body(co.g[p], local, co.nblk[p]);
+    return;
+  }
   if (a.d_step) a.seed += *a.d_step * 0x9e3779b97f4a7c15ull;
   constexpr int EPL = Vec<T>::EPL;
   constexpr int WPB = 256 / LPR;
@@ -640,15 +661,41 @@ mrec_status mrec_emb_bwd_plan(const mrec_table_bank *bank, const mrec_ids *ids, 
   return launch_status("mrec_emb_bwd_plan");
 }
 
+}  // extern "C"
+
+static mrec_status apply_impl(const mrec_table_bank *bank, int64_t batch, const void *workspace,
+                              size_t ws_bytes, const void *dx, mrec_dtype dx_dtype, int64_t dx_ld,
+                              const float *dfm, const float *fm_sum, const void *x0,
+                              mrec_dtype x0_dtype, int64_t x0_ld, const float *dw,
+                              const float *g_occ, int64_t g_ld, int64_t chunk,
+                              int64_t chunk_stride, mrec_bwd_mode mode, float lr, uint64_t seed,
+                              const uint64_t *d_step, void *grad, int32_t n_reduce,
+                              const mrec_gemm_call *reduce, mrec_stream stream);
+
+extern "C" {
+
 mrec_status mrec_emb_bwd_apply(const mrec_table_bank *bank, int64_t batch, const void *workspace,
                                size_t ws_bytes, const void *dx, mrec_dtype dx_dtype, int64_t dx_ld,
                                const float *dfm, const float *fm_sum, const void *x0,
                                mrec_dtype x0_dtype, int64_t x0_ld, const float *dw,
                                mrec_bwd_mode mode, float lr, uint64_t seed,
                                const uint64_t *d_step, void *grad, mrec_stream stream) {
-  return mrec_emb_bwd_apply_given(bank, batch, workspace, ws_bytes, dx, dx_dtype, dx_ld, dfm,
-                                  fm_sum, x0, x0_dtype, x0_ld, dw, nullptr, 0, 0, 0, mode, lr,
-                                  seed, d_step, grad, stream);
+  return apply_impl(bank, batch, workspace, ws_bytes, dx, dx_dtype, dx_ld, dfm, fm_sum, x0,
+                    x0_dtype, x0_ld, dw, nullptr, 0, 0, 0, mode, lr, seed, d_step, grad, 0,
+                    nullptr, stream);
+}
+
+mrec_status mrec_emb_bwd_apply_ex(const mrec_table_bank *bank, int64_t batch,
+                                  const void *workspace, size_t ws_bytes, const void *dx,
+                                  mrec_dtype dx_dtype, int64_t dx_ld, const float *dfm,
+                                  const float *fm_sum, const void *x0, mrec_dtype x0_dtype,
+                                  int64_t x0_ld, const float *dw, mrec_bwd_mode mode, float lr,
+                                  uint64_t seed, const uint64_t *d_step, void *grad,
+                                  int32_t n_reduce, const mrec_gemm_call *reduce,
+                                  mrec_stream stream) {
+  return apply_impl(bank, batch, workspace, ws_bytes, dx, dx_dtype, dx_ld, dfm, fm_sum, x0,
+                    x0_dtype, x0_ld, dw, nullptr, 0, 0, 0, mode, lr, seed, d_step, grad, n_reduce,
+                    reduce, stream);
 }
 
 mrec_status mrec_emb_bwd_apply_given(const mrec_table_bank *bank, int64_t batch,
@@ -659,6 +706,21 @@ mrec_status mrec_emb_bwd_apply_given(const mrec_table_bank *bank, int64_t batch,
                                      int64_t g_ld, int64_t chunk, int64_t chunk_stride,
                                      mrec_bwd_mode mode, float lr, uint64_t seed,
                                      const uint64_t *d_step, void *grad, mrec_stream stream) {
+  return apply_impl(bank, batch, workspace, ws_bytes, dx, dx_dtype, dx_ld, dfm, fm_sum, x0,
+                    x0_dtype, x0_ld, dw, g_occ, g_ld, chunk, chunk_stride, mode, lr, seed, d_step,
+                    grad, 0, nullptr, stream);
+}
+
+}  // extern "C"
+
+static mrec_status apply_impl(const mrec_table_bank *bank, int64_t batch, const void *workspace,
+                              size_t ws_bytes, const void *dx, mrec_dtype dx_dtype, int64_t dx_ld,
+                              const float *dfm, const float *fm_sum, const void *x0,
+                              mrec_dtype x0_dtype, int64_t x0_ld, const float *dw,
+                              const float *g_occ, int64_t g_ld, int64_t chunk,
+                              int64_t chunk_stride, mrec_bwd_mode mode, float lr, uint64_t seed,
+                              const uint64_t *d_step, void *grad, int32_t n_reduce,
+                              const mrec_gemm_call *reduce, mrec_stream stream) {
   BankArgs ba;
   int eb, lpr;
   mrec_status st = make_bank_args(bank, &ba, &eb, &lpr);
@@ -697,7 +759,6 @@ mrec_status mrec_emb_bwd_apply_given(const mrec_table_bank *bank, int64_t batch,
                    "g_occ rows must be 16B aligned, g_ld >= dim + has_w, g_ld % 4 == 0");
     MREC_CHECK_ARG(chunk >= 0 && (chunk == 0 || chunk_stride >= F * chunk), "bad chunk");
   }
-  if (batch == 0) return MREC_OK;
   ApplyArgs a;
   a.dx = dx;
   a.dx_ld = dx_ld;
@@ -724,8 +785,27 @@ mrec_status mrec_emb_bwd_apply_given(const mrec_table_bank *bank, int64_t batch,
   const bool hash = batch <= kHashMaxKeys;
   const int seg_blocks = static_cast<int>(((hash ? batch / 2 : batch) + wpb - 1) / wpb);
   const int64_t sm_blocks = hash ? (batch * F + wpb - 1) / wpb : 0;
-  const dim3 grid(static_cast<unsigned>(static_cast<int64_t>(seg_blocks) * F + sm_blocks));
-#define MREC_AK(T, L) apply_kernel<T, L><<<grid, 256, 0, s>>>(ba, batch, workspace, a, seg_blocks, hash ? 1 : 0)
+  const int apply_blocks = static_cast<int>(static_cast<int64_t>(seg_blocks) * F + sm_blocks);
+  CoReduce co = {};
+  int co_blocks = 0;
+  MREC_CHECK_ARG(n_reduce >= 0 && n_reduce <= kMaxCoReduce && (n_reduce == 0 || reduce),
+                 "n_reduce out of [0, 2]");
+  for (int i = 0; i < n_reduce; ++i) {
+    int64_t nb = 0;
+    mrec_status st = build_reduce_job(reduce[i], &co.g[co.n], &nb);
+    if (st != MREC_OK) return st;
+    if (nb == 0) continue;
+    co.nblk[co.n] = static_cast<int>(nb);
+    co.start[co.n] = co_blocks;
+    co_blocks += static_cast<int>(nb);
+    ++co.n;
+  }
+  co.start[co.n] = co_blocks;
+  if (apply_blocks + co_blocks == 0) return MREC_OK;  // (batch 0 still runs the reductions)
+  const dim3 grid(static_cast<unsigned>(apply_blocks + co_blocks));
+#define MREC_AK(T, L) \
+  apply_kernel<T, L><<<grid, 256, 0, s>>>(ba, batch, workspace, a, seg_blocks, hash ? 1 : 0, \
+                                          apply_blocks, co)
   if (bank->dtype == MREC_BF16) {
     switch (lpr) {
       case 1: MREC_AK(uint16_t, 1); break;
@@ -746,5 +826,3 @@ mrec_status mrec_emb_bwd_apply_given(const mrec_table_bank *bank, int64_t batch,
 #undef MREC_AK
   return launch_status("mrec_emb_bwd_apply");
 }
-
-}  // extern "C"

@@ -28,6 +28,7 @@
 
 #include "common.h"
 #include "emb_plan.h"
+#include "gemm_common.h"
 
 namespace mrec {
 
@@ -45,47 +46,6 @@ typedef short bf16x8 __attribute__((ext_vector_type(8)));
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 typedef short v4s __attribute__((ext_vector_type(4)));
 typedef __attribute__((address_space(3))) v4s lds_v4s;
-
-struct GemmArgs {
-  int64_t M, N, K;
-  const uint16_t *A;
-  int64_t lda;
-  const uint16_t *B;
-  int64_t ldb;
-  int64_t b_ones_col;
-  int64_t b_cols;
-  const float *bias;
-  int act;
-  const uint16_t *mul;
-  int64_t ld_mul;
-  const uint16_t *add;
-  int64_t ld_add;
-  uint16_t *aux;
-  int64_t ld_aux;
-  const uint16_t *mask;
-  int64_t ld_mask;
-  void *C;
-  int64_t ldc;
-  int c_f32;
-  int vec;         // C / aux / mul / add / mask rows 16-B aligned: 16-B epilogue stores
-  int64_t pad_to;  // columns [N, pad_to) of C are written as 0
-  float *ones_out;
-  int split_k;
-  int64_t k_per_split;
-  float *ws;
-  int64_t ldws;    // row stride of a split-K partial slab (round8(ncols))
-  int ntn;         // output tiles along N
-  int ntiles;      // output tiles (M x N)
-  int xchunk;      // tiles per XCD slot: ceil(ntiles / 8)
-  int update;      // fused SGD: C -= lr * v (fp32 master), images re-emitted
-  float lr;
-  uint16_t *img_row;
-  int64_t ld_img_row;
-  uint16_t *img_tr;
-  int64_t ld_img_tr;
-};
-
-__device__ __forceinline__ float bf(uint16_t h) { return __uint_as_float(uint32_t(h) << 16); }
 
 __device__ __attribute__((aligned(64))) uint4 g_zero_page[64];
 
@@ -134,56 +94,6 @@ struct DmaSrc {
     }
   }
 };
-
-// scalar epilogue of one element (split-K reduce and unaligned outputs)
-__device__ __forceinline__ void epilogue_elem(const GemmArgs &g, int64_t m, int64_t n, float acc) {
-  if (g.update) {  // fused SGD step of a master weight (+ its bias through the ones column)
-    if (n == g.b_ones_col) {
-      if (g.ones_out) g.ones_out[m] = fmaf(-g.lr, acc, g.ones_out[m]);
-      return;
-    }
-    if (n >= g.N) return;
-    float *c = static_cast<float *>(g.C) + m * g.ldc + n;
-    const float w = fmaf(-g.lr, acc, *c);
-    *c = w;
-    const uint16_t h = f32_to_bf16_rne(w);
-    if (g.img_row) g.img_row[m * g.ld_img_row + n] = h;
-    if (g.img_tr) g.img_tr[n * g.ld_img_tr + m] = h;
-    return;
-  }
-  if (n == g.b_ones_col) {
-    if (g.ones_out) g.ones_out[m] = acc;
-    if (n < g.pad_to) {
-      if (g.c_f32)
-        static_cast<float *>(g.C)[m * g.ldc + n] = 0.f;
-      else
-        static_cast<uint16_t *>(g.C)[m * g.ldc + n] = 0;
-    }
-    return;
-  }
-  if (n >= g.N) {
-    if (n < g.pad_to) {
-      if (g.c_f32)
-        static_cast<float *>(g.C)[m * g.ldc + n] = 0.f;
-      else
-        static_cast<uint16_t *>(g.C)[m * g.ldc + n] = 0;
-    }
-    return;
-  }
-  float v = acc + (g.bias ? g.bias[n] : 0.f);
-  if (g.aux) g.aux[m * g.ld_aux + n] = f32_to_bf16_rne(v);
-  if (g.act == 1) v = fmaxf(v, 0.f);
-  if (g.mul) v *= bf(g.mul[m * g.ld_mul + n]);
-  if (g.add) v += bf(g.add[m * g.ld_add + n]);
-  if (g.mask) {
-    const uint16_t mv = g.mask[m * g.ld_mask + n];
-    if (mv == 0 || (mv & 0x8000u)) v = 0.f;
-  }
-  if (g.c_f32)
-    static_cast<float *>(g.C)[m * g.ldc + n] = v;
-  else
-    static_cast<uint16_t *>(g.C)[m * g.ldc + n] = f32_to_bf16_rne(v);
-}
 
 __device__ __forceinline__ void unpack8(const uint4 r, float (&f)[8]) {
   const uint32_t w[4] = {r.x, r.y, r.z, r.w};
@@ -444,27 +354,6 @@ __global__ __launch_bounds__(GEMM_THREADS) void gemm_dma_kernel(GemmArgs g) {
   gemm_tile<A_COL, B_COL>(g, blockIdx.x, blockIdx.z, smem);
 }
 
-// fixed-order reduction of the split-K partial slabs + epilogue (4 columns / thread)
-__device__ __forceinline__ void splitk_reduce_body(const GemmArgs &g, int64_t bid, int64_t nblk) {
-  const int64_t ncols = g.b_ones_col >= 0 ? g.b_ones_col + 1 : g.N;
-  const int64_t q = g.ldws / 4;
-  const int64_t total = g.M * q;
-  const int64_t slab = g.M * g.ldws;
-  for (int64_t i = bid * 256 + threadIdx.x; i < total; i += nblk * 256) {
-    const int64_t m = i / q, n = (i - m * q) * 4;
-    if (n >= ncols && n >= g.pad_to) continue;
-    float4 s = *reinterpret_cast<const float4 *>(g.ws + m * g.ldws + n);
-    for (int z = 1; z < g.split_k; ++z) {
-      const float4 t = *reinterpret_cast<const float4 *>(g.ws + z * slab + m * g.ldws + n);
-      s.x += t.x; s.y += t.y; s.z += t.z; s.w += t.w;
-    }
-    const float e[4] = {s.x, s.y, s.z, s.w};
-#pragma unroll
-    for (int j = 0; j < 4; ++j)
-      if (n + j < ncols || n + j < g.pad_to) epilogue_elem(g, m, n + j, e[j]);
-  }
-}
-
 __global__ __launch_bounds__(256) void splitk_reduce_kernel(GemmArgs g) {
   splitk_reduce_body(g, blockIdx.x, gridDim.x);
 }
@@ -679,9 +568,22 @@ static mrec_status build_gemm(int64_t M, int64_t N, int64_t K, const mrec_operan
   return MREC_OK;
 }
 
-static int64_t reduce_blocks(const GemmArgs &g) {
+int64_t reduce_blocks(const GemmArgs &g) {
   const int64_t total = g.M * (g.ldws / 4);
   return std::min<int64_t>((total + 255) / 256, 2048);
+}
+
+mrec_status build_reduce_job(const mrec_gemm_call &c, GemmArgs *g, int64_t *nblk) {
+  int kind;
+  int64_t ncols;
+  mrec_status st = build_gemm(c.M, c.N, c.K, c.A, c.B, c.b_ones_col, c.b_cols, c.epi, c.C,
+                              c.c_dtype, c.ldc, c.split_k, c.workspace, c.ws_bytes, g, &kind,
+                              &ncols);
+  if (st != MREC_OK) return st;
+  MREC_CHECK_ARG(c.phase == MREC_GEMM_REDUCE && g->split_k > 1,
+                 "a co-launched GEMM job must be a split-K REDUCE");
+  *nblk = ncols > 0 ? reduce_blocks(*g) : 0;
+  return MREC_OK;
 }
 
 }  // namespace mrec

@@ -218,6 +218,14 @@ def flush_pending():
         _run(pend[i:i + 4])
 
 
+def take_pending(n: int):
+    """Remove and return up to ``n`` deferred reductions, for a launch that runs
+    them beside its own work (``mrec_emb_bwd_apply_ex``)."""
+    global _PENDING
+    jobs, _PENDING = _PENDING[:n], _PENDING[n:]
+    return jobs
+
+
 def _defer(call: "_Call"):
     _PENDING.append(call.with_phase(_mrec.GEMM_REDUCE))
     torch.autograd.Variable._execution_engine.queue_callback(flush_pending)

@@ -270,12 +270,17 @@ def _apply(bank: EmbeddingBank, ws, ws_bytes, count, dx=None, dfm=None, fm_sum=N
         mode, lr = _mrec.BWD_DENSE_GRAD, 0.0
     dx_dt = _mrec.dtype_code(dx.dtype) if dx is not None else _mrec.F32
     x0_dt = _mrec.dtype_code(x0.dtype) if x0 is not None else _mrec.F32
-    _mrec.call("mrec_emb_bwd_apply", bank.desc().ref(), count, ws.data_ptr(), ws_bytes,
+    # deferred MLP weight-gradient reductions (+ fused SGD) ride along this launch
+    from pytorchrec_amd import dense as dense_ops
+    jobs = dense_ops.take_pending(2)
+    arr = (_mrec.GemmCall * len(jobs))(*[j.struct() for j in jobs]) if jobs else None
+    _mrec.call("mrec_emb_bwd_apply_ex", bank.desc().ref(), count, ws.data_ptr(), ws_bytes,
                _mrec.ptr(dx), dx_dt, dx.stride(0) if dx is not None else 0,
                _mrec.ptr(dfm), _mrec.ptr(fm_sum), _mrec.ptr(x0), x0_dt,
                x0.stride(0) if x0 is not None else 0, _mrec.ptr(dw), mode, float(lr),
-               bank.next_seed(), bank.step_counter().data_ptr(), _mrec.ptr(grad),
-               _mrec.stream_handle())
+               bank.next_seed(), bank.step_counter().data_ptr(), _mrec.ptr(grad), len(jobs),
+               arr, _mrec.stream_handle())
+    del jobs
 
 
 def _chunks(batch: int):

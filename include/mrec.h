@@ -161,7 +161,7 @@ size_t mrec_emb_bwd_workspace_size(int32_t n_tables, int64_t batch);
  * Plan of the embedding backward: per table the lookups are grouped by row (an
  * LDS hash table for batch <= MREC_BWD_HASH_MAX_BATCH, a stable LDS radix sort
  * up to MREC_BWD_MAX_BATCH).  Depends only on the ids, so it can run as soon as
- * the batch is resident (or inside a GEMM launch: mrec_gemm_multi_plan).  If
+ * the batch is resident (or inside a GEMM launch: mrec_gemm_multi_ex).  If
  * d_step (device uint64, may be NULL) is given the plan increments it once, so a
  * graph replayed step after step still draws fresh stochastic-rounding bits.
  */
@@ -388,15 +388,29 @@ typedef struct {
   uint64_t *d_step;
 } mrec_plan_job;
 
+/* the CTR head's parameter finish (arguments of mrec_ctr_head_finish) */
+typedef struct {
+  const float *part;
+  int64_t ldp;
+  int64_t batch;
+  int32_t H, ns;
+  const float *g;
+  int32_t update;
+  float lr;
+  float *w, *bias, *ws, *b2;
+  float *dw_out, *db_out, *dws_out, *db2_out;
+} mrec_head_finish_job;
+
 /*
- * mrec_gemm_multi plus the embedding-backward plan of `plan` (may be NULL) run by
- * extra workgroups of the same launch, one per table: a HIP graph runs the
- * step's kernels one after another, so a plan launched on its own sits on the
- * critical path; beside a latency-bound backward GEMM it is hidden.  Same
- * workspace contents as mrec_emb_bwd_plan.
+ * mrec_gemm_multi plus, in extra workgroups of the same launch, the embedding-
+ * backward plan of `plan` and/or the CTR head finish of `finish` (either may be
+ * NULL).  A HIP graph runs the step's kernels one after another, so a small
+ * kernel of its own sits on the critical path; beside latency-bound backward
+ * GEMMs it is hidden.  Same results as mrec_emb_bwd_plan / mrec_ctr_head_finish.
+ * The jobs must be independent of the GEMM calls.
  */
-mrec_status mrec_gemm_multi_plan(int32_t n, const mrec_gemm_call *calls, const mrec_plan_job *plan,
-                                 mrec_stream stream);
+mrec_status mrec_gemm_multi_ex(int32_t n, const mrec_gemm_call *calls, const mrec_plan_job *plan,
+                               const mrec_head_finish_job *finish, mrec_stream stream);
 
 /*
  * fp32 [N, K] weight (row stride ldw) -> bf16 images for the GEMMs: `row`

@@ -105,6 +105,15 @@ class PlanJob(ctypes.Structure):
                 ("ws_bytes", ctypes.c_size_t), ("d_oob_flag", ctypes.c_void_p),
                 ("d_step", ctypes.c_void_p)]
 
+
+class HeadFinishJob(ctypes.Structure):
+    _fields_ = [("part", ctypes.c_void_p), ("ldp", ctypes.c_int64), ("batch", ctypes.c_int64),
+                ("H", ctypes.c_int32), ("ns", ctypes.c_int32), ("g", ctypes.c_void_p),
+                ("update", ctypes.c_int32), ("lr", ctypes.c_float), ("w", ctypes.c_void_p),
+                ("bias", ctypes.c_void_p), ("ws", ctypes.c_void_p), ("b2", ctypes.c_void_p),
+                ("dw_out", ctypes.c_void_p), ("db_out", ctypes.c_void_p),
+                ("dws_out", ctypes.c_void_p), ("db2_out", ctypes.c_void_p)]
+
 LAYOUT_ROW, LAYOUT_COL = 0, 1
 ACT_NONE, ACT_RELU = 0, 1
 
@@ -152,8 +161,8 @@ SIGNATURES = {
     "mrec_gemm": (ctypes.c_int, [_i64, _i64, _i64, _op_p, _op_p, _i64, _i64, _epi_p,
                                  _vp, ctypes.c_int, _i64, _i32, _vp, ctypes.c_size_t, _vp]),
     "mrec_gemm_multi": (ctypes.c_int, [_i32, ctypes.POINTER(GemmCall), _vp]),
-    "mrec_gemm_multi_plan": (ctypes.c_int, [_i32, ctypes.POINTER(GemmCall),
-                                            ctypes.POINTER(PlanJob), _vp]),
+    "mrec_gemm_multi_ex": (ctypes.c_int, [_i32, ctypes.POINTER(GemmCall), ctypes.POINTER(PlanJob),
+                                          ctypes.POINTER(HeadFinishJob), _vp]),
     "mrec_weight_prep": (ctypes.c_int, [_vp, _i64, _i64, _i64, _vp, _i64, _vp, _i64, _vp]),
     "mrec_head_fwd": (ctypes.c_int, [_vp, _i64, _i64, _i32, _vp, _vp, _vp, _vp, _vp]),
     "mrec_head_bwd": (ctypes.c_int, [_vp, _vp, _i64, _i32, _vp, _i64, _vp, _i64, _vp]),

@@ -29,6 +29,7 @@
 #include "common.h"
 #include "emb_plan.h"
 #include "gemm_common.h"
+#include "head_common.h"
 
 namespace mrec {
 
@@ -381,6 +382,8 @@ struct PlanJob {  // an embedding-backward hash plan run by the first workgroups
 struct MultiArgs {
   int n;
   int plan_blocks;  // leading workgroups that run `plan` (one per table, padded to 8)
+  int fin_blocks;   // then the CTR head finish (padded to 8)
+  HeadFinishArgs fin;
   int kind[MULTI_MAX];
   int tile_blocks[MULTI_MAX];  // workgroups per K slice (GEMM jobs)
   int nblk[MULTI_MAX];         // workgroups with work (the rest pad to a multiple of 8)
@@ -400,7 +403,13 @@ __global__ __launch_bounds__(GEMM_THREADS) void gemm_multi_kernel(MultiArgs ma) 
                                                      blockIdx.x, reinterpret_cast<uint32_t *>(smem));
     return;
   }
-  const int b = blockIdx.x - ma.plan_blocks;
+  if (static_cast<int>(blockIdx.x) < ma.plan_blocks + ma.fin_blocks) {  // uniform
+    const int fb = blockIdx.x - ma.plan_blocks;
+    if (fb < head_finish_blocks(ma.fin.H, ma.fin.ns))
+      ctr_head_finish_body(ma.fin, fb, reinterpret_cast<float (*)[9]>(smem));
+    return;
+  }
+  const int b = blockIdx.x - ma.plan_blocks - ma.fin_blocks;
   int p = 0;
   while (p + 1 < ma.n && b >= ma.start[p + 1]) ++p;  // uniform
   const int local = b - ma.start[p];
@@ -621,13 +630,22 @@ void mrec_gemm_prof_read(uint64_t *out, int n) {
 #endif
 
 mrec_status mrec_gemm_multi(int32_t n, const mrec_gemm_call *calls, mrec_stream stream) {
-  return mrec_gemm_multi_plan(n, calls, nullptr, stream);
+  return mrec_gemm_multi_ex(n, calls, nullptr, nullptr, stream);
 }
 
-mrec_status mrec_gemm_multi_plan(int32_t n, const mrec_gemm_call *calls, const mrec_plan_job *plan,
-                                 mrec_stream stream) {
+mrec_status mrec_gemm_multi_ex(int32_t n, const mrec_gemm_call *calls, const mrec_plan_job *plan,
+                               const mrec_head_finish_job *finish, mrec_stream stream) {
   MREC_CHECK_ARG(n >= 0 && n <= MULTI_MAX && (n == 0 || calls), "n out of [0, 4]");
   MultiArgs ma = {};
+  if (finish) {
+    const mrec_head_finish_job &f = *finish;
+    mrec_status st = build_head_finish(f.part, f.ldp, f.batch, f.H, f.ns, f.g, f.update, f.lr,
+                                       f.w, f.bias, f.ws, f.b2, f.dw_out, f.db_out, f.dws_out,
+                                       f.db2_out, &ma.fin);
+    if (st != MREC_OK) return st;
+    ma.fin_blocks = (f.H + 1 + f.ns + 7) / 8;
+    ma.fin_blocks = (ma.fin_blocks + 7) / 8 * 8;
+  }
   if (plan) {
     int eb, lpr;
     mrec_status st = make_bank_args(plan->bank, &ma.plan.bank, &eb, &lpr);
@@ -637,7 +655,7 @@ mrec_status mrec_gemm_multi_plan(int32_t n, const mrec_gemm_call *calls, const m
                    "plan batch must be in [1, MREC_BWD_HASH_MAX_BATCH]");
     MREC_CHECK_ARG(plan->workspace != nullptr, "plan workspace is NULL");
     if (plan->ws_bytes < mrec_emb_bwd_workspace_size(ma.plan.bank.n_tables, plan->batch)) {
-      set_error("mrec_gemm_multi_plan: plan workspace too small");
+      set_error("mrec_gemm_multi_ex: plan workspace too small");
       return MREC_ENOSPC;
     }
     for (int f = 0; f < ma.plan.bank.n_tables; ++f)
@@ -682,7 +700,7 @@ mrec_status mrec_gemm_multi_plan(int32_t n, const mrec_gemm_call *calls, const m
     blocks += static_cast<int>((nb + 7) / 8 * 8);
     ma.n = j + 1;
   }
-  if (ma.n == 0 && ma.plan_blocks == 0) return MREC_OK;
+  if (ma.n == 0 && ma.plan_blocks == 0 && ma.fin_blocks == 0) return MREC_OK;
   ma.start[ma.n] = blocks;
   static const bool attr = [] {
     (void)hipFuncSetAttribute(reinterpret_cast<const void *>(gemm_multi_kernel),
@@ -691,7 +709,7 @@ mrec_status mrec_gemm_multi_plan(int32_t n, const mrec_gemm_call *calls, const m
     return true;
   }();
   (void)attr;
-  gemm_multi_kernel<<<dim3(static_cast<unsigned>(ma.plan_blocks + blocks)), GEMM_THREADS,
+  gemm_multi_kernel<<<dim3(static_cast<unsigned>(ma.plan_blocks + ma.fin_blocks + blocks)), GEMM_THREADS,
                       kGemmLds, static_cast<hipStream_t>(stream)>>>(ma);
   return launch_status("mrec_gemm_multi");
 }

@@ -7,6 +7,7 @@
 #include <algorithm>
 
 #include "common.h"
+#include "head_common.h"
 
 namespace mrec {
 
@@ -308,58 +309,21 @@ __global__ __launch_bounds__(256) void ctr_head_kernel(
 
 // sum the per-workgroup partials (fixed order) -> dW [H] and db; then either SGD on
 // (w, bias) with lr * g, or write g * dW / g * db
-__global__ __launch_bounds__(256) void ctr_head_finish_kernel(
-    const float *__restrict__ part, int64_t ldp, int nparts, int H, int ns,
-    const float *__restrict__ gp, int update, float lr, float *__restrict__ w,
-    float *__restrict__ bias, float *__restrict__ ws, float *__restrict__ b2,
-    float *__restrict__ dw_out, float *__restrict__ db_out, float *__restrict__ dws_out,
-    float *__restrict__ db2_out) {
+__global__ __launch_bounds__(256) void ctr_head_finish_kernel(HeadFinishArgs a) {
   __shared__ float red[4][9];
-  const int c0 = blockIdx.x * 8;
-  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-  float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
-  for (int k = threadIdx.x; k < nparts; k += 256) {
-#pragma unroll
-    for (int j = 0; j < 8; ++j)
-      if (c0 + j <= H + ns) acc[j] += part[static_cast<int64_t>(k) * ldp + c0 + j];
-  }
-#pragma unroll
-  for (int j = 0; j < 8; ++j) {
-#pragma unroll
-    for (int off = 32; off > 0; off >>= 1) acc[j] += __shfl_xor(acc[j], off);
-  }
-  if (lane == 0) {
-#pragma unroll
-    for (int j = 0; j < 8; ++j) red[wv][j] = acc[j];
-  }
-  __syncthreads();
-  if (threadIdx.x < 8) {
-    const int c = c0 + threadIdx.x;
-    if (c > H + ns) return;
-    const float g = gp ? gp[0] : 1.f;
-    const float v = ((red[0][threadIdx.x] + red[1][threadIdx.x]) +
-                     (red[2][threadIdx.x] + red[3][threadIdx.x])) * g;
-    if (c < H) {
-      if (update)
-        w[c] = fmaf(-lr, v, w[c]);
-      else if (dw_out)
-        dw_out[c] = v;
-    } else if (c == H) {  // both biases have gradient sum(dz)
-      if (update) {
-        if (bias) bias[0] = fmaf(-lr, v, bias[0]);
-        if (b2) b2[0] = fmaf(-lr, v, b2[0]);
-      } else {
-        if (db_out) db_out[0] = v;
-        if (db2_out) db2_out[0] = v;
-      }
-    } else {
-      const int j = c - H - 1;
-      if (update)
-        ws[j] = fmaf(-lr, v, ws[j]);
-      else if (dws_out)
-        dws_out[j] = v;
-    }
-  }
+  ctr_head_finish_body(a, blockIdx.x, red);
+}
+
+mrec_status build_head_finish(const float *part, int64_t ldp, int64_t batch, int32_t H,
+                              int32_t ns, const float *g, int32_t update, float lr, float *w,
+                              float *bias, float *ws, float *b2, float *dw_out, float *db_out,
+                              float *dws_out, float *db2_out, HeadFinishArgs *out) {
+  MREC_CHECK_ARG(part != nullptr && H >= 1 && batch >= 1 && ns >= 0 && ns <= 64, "bad arguments");
+  MREC_CHECK_ARG(!update || (w && (ns == 0 || ws)), "update needs w (and ws)");
+  MREC_CHECK_ARG(ldp >= H + 1 + ns, "ldp < H + 1 + ns");
+  *out = HeadFinishArgs{part, ldp, static_cast<int>(mrec_ctr_head_parts(batch)), H, ns, g,
+                        update, lr, w, bias, ws, b2, dw_out, db_out, dws_out, db2_out};
+  return MREC_OK;
 }
 
 }  // namespace mrec
@@ -468,13 +432,12 @@ mrec_status mrec_ctr_head_finish(const float *part, int64_t ldp, int64_t batch, 
                                  int32_t ns, const float *g, int32_t update, float lr, float *w,
                                  float *bias, float *ws, float *b2, float *dw_out, float *db_out,
                                  float *dws_out, float *db2_out, mrec_stream stream) {
-  MREC_CHECK_ARG(part != nullptr && H >= 1 && batch >= 1 && ns >= 0 && ns <= 64, "bad arguments");
-  MREC_CHECK_ARG(!update || (w && (ns == 0 || ws)), "update needs w (and ws)");
-  const int nparts = static_cast<int>(mrec_ctr_head_parts(batch));
+  HeadFinishArgs a;
+  mrec_status st = build_head_finish(part, ldp, batch, H, ns, g, update, lr, w, bias, ws, b2,
+                                     dw_out, db_out, dws_out, db2_out, &a);
+  if (st != MREC_OK) return st;
   ctr_head_finish_kernel<<<dim3(static_cast<unsigned>((H + 1 + ns + 7) / 8)), 256, 0,
-                           static_cast<hipStream_t>(stream)>>>(part, ldp, nparts, H, ns, g, update,
-                                                               lr, w, bias, ws, b2, dw_out, db_out,
-                                                               dws_out, db2_out);
+                           static_cast<hipStream_t>(stream)>>>(a);
   return launch_status("mrec_ctr_head_finish");
 }
 

@@ -195,17 +195,51 @@ def launch_multi(calls):
         _run(jobs[i:i + 4])
 
 
+class _HeadFinish:
+    """A deferred mrec_ctr_head_finish in SGD-update mode (the head's W, b and side
+    linear ws, b2): run by spare workgroups of the next GEMM launch, or on its own
+    at the end of the backward."""
+
+    def __init__(self, part, B, H, ns, g, lr, w, bias, ws, b2):
+        self.keep = [part, g, w, bias, ws, b2]
+        self.struct = _mrec.HeadFinishJob(part.data_ptr(), part.stride(0), B, H, ns, _mrec.ptr(g),
+                                          1, float(lr), w.data_ptr(), _mrec.ptr(bias),
+                                          _mrec.ptr(ws), _mrec.ptr(b2), None, None, None, None)
+
+    def run(self):
+        j = self.struct
+        _mrec.call("mrec_ctr_head_finish", j.part, j.ldp, j.batch, j.H, j.ns, j.g, 1, j.lr, j.w,
+                   j.bias, j.ws, j.b2, None, None, None, None, _mrec.stream_handle())
+
+
+_FINISH = []
+
+
+def defer_head_finish(fin: _HeadFinish):
+    _flush_finish()
+    _FINISH.append(fin)
+    torch.autograd.Variable._execution_engine.queue_callback(flush_pending)
+
+
+def _flush_finish():
+    while _FINISH:
+        _FINISH.pop(0).run()
+
+
 def _run(jobs):
     if not jobs:
         return
     arr = (_mrec.GemmCall * len(jobs))(*[j.struct() for j in jobs])
     plan = _take_plan()
-    if plan is None:
+    fin = _FINISH.pop(0) if _FINISH else None
+    if plan is None and fin is None:
         _mrec.call("mrec_gemm_multi", len(jobs), arr, _mrec.stream_handle())
         return
-    job = plan.job()
-    _mrec.call("mrec_gemm_multi_plan", len(jobs), arr, ctypes.byref(job), _mrec.stream_handle())
-    plan.launched = True
+    pj = plan.job() if plan is not None else None
+    _mrec.call("mrec_gemm_multi_ex", len(jobs), arr, ctypes.byref(pj) if pj is not None else None,
+               ctypes.byref(fin.struct) if fin is not None else None, _mrec.stream_handle())
+    if plan is not None:
+        plan.launched = True
 
 
 def flush_pending():
@@ -216,6 +250,7 @@ def flush_pending():
     pend, _PENDING = _PENDING, []
     for i in range(0, len(pend), 4):
         _run(pend[i:i + 4])
+    _flush_finish()
 
 
 def take_pending(n: int):
@@ -704,11 +739,10 @@ class _CTRHeadBCEFn(torch.autograd.Function):
         dW = db = dws = db2 = None
         det = (lambda t: None if t is None else t.detach())
         if lr is not None and ctx.weight.is_contiguous():
-            _mrec.call("mrec_ctr_head_finish", part.data_ptr(), part.stride(0), ctx.B, ctx.H,
-                       ctx.ns, None if one else g.data_ptr(), 1, lr,
-                       ctx.weight.detach().data_ptr(), _mrec.ptr(det(ctx.bias)),
-                       _mrec.ptr(det(ctx.ws)), _mrec.ptr(det(ctx.b2)), None, None, None, None,
-                       _mrec.stream_handle())
+            # independent of the backward GEMMs: rides along the next one
+            defer_head_finish(_HeadFinish(part, ctx.B, ctx.H, ctx.ns, None if one else g, lr,
+                                          ctx.weight.detach(), det(ctx.bias), det(ctx.ws),
+                                          det(ctx.b2)))
         else:
             f32 = dict(dtype=torch.float32, device=dev)
             dW = torch.empty(1, ctx.H, **f32)

@@ -347,7 +347,7 @@ def test_fm2_dense_kernel(gpu):
 
 @pytest.mark.parametrize("rows", [7, 5000, 200000])
 def test_plan_inside_gemm_launch_matches_standalone(gpu, rows):
-    """mrec_gemm_multi_plan's plan (256-thread workgroups, 6016-slot table) drives
+    """mrec_gemm_multi_ex's plan (256-thread workgroups, 6016-slot table) drives
     the same updates as the standalone 1024-thread plan kernel: bitwise."""
     import ctypes
     from pytorchrec_amd import _mrec
@@ -368,7 +368,8 @@ def test_plan_inside_gemm_launch_matches_standalone(gpu, rows):
             job = _mrec.PlanJob(ctypes.pointer(bank.desc().struct), ctypes.pointer(idd.struct), B,
                                 ws.data_ptr(), wsb, None, None)
             bank.desc().ref()
-            _mrec.call("mrec_gemm_multi_plan", 0, None, ctypes.byref(job), _mrec.stream_handle())
+            _mrec.call("mrec_gemm_multi_ex", 0, None, ctypes.byref(job), None,
+                       _mrec.stream_handle())
         else:
             _mrec.call("mrec_emb_bwd_plan", bank.desc().ref(), idd.ref(), B, ws.data_ptr(), wsb,
                        None, None, _mrec.stream_handle())

@@ -217,23 +217,22 @@ def kernel_rooflines(model, data, args):
     dense = model._dense(data)
     out = {}
     with torch.no_grad():
+        # the step's forward launch: interaction + the backward's hash plan in one
+        # kernel (mrec_interact_fwd_ex)
         def fwd():
             E._InteractFn.forward(_Ctx(), bank.weight, dense_weight, global_bias, None,
                                   bank, ids, dense, True, True, model.x0_cols, torch.bfloat16,
-                                  False)
+                                  True)
         # bytes/sample: ids F*4 + useful row bytes F*(D+1)*2 + dense 13*4 + x0 write
-        # x0_cols*2 + logit 4 + fm_sum D*4
+        # x0_cols*2 + logit 4 + fm_sum D*4; plan: ids F*4 again + per lookup one
+        # 12-B workspace entry (row table / descriptor / permutation)
         fwd_bytes = F * 4 + F * (D + 1) * 2 + CRITEO_DENSE * 4 + model.x0_cols * 2 + 4 + D * 4
+        plan_bytes = F * 4 + F * 12
         t = time_launches(fwd)
-        out["mrec_interact_fwd"] = (t, fwd_bytes * B)
+        out["mrec_interact_fwd_ex"] = (t, (fwd_bytes + plan_bytes) * B)
 
         ws, wsb = E._plan(bank, ids, 0, B, None)
         torch.cuda.synchronize()
-
-        def plan():
-            E._plan(bank, ids, 0, B, None)
-        t = time_launches(plan)
-        out["mrec_emb_bwd_plan"] = (t, (F * 4 + F * 12) * B)
 
         x0, logit = E._InteractFn.forward(_Ctx(), bank.weight, dense_weight, global_bias, None,
                                           bank, ids, dense, True, True, model.x0_cols,

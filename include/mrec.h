@@ -169,6 +169,30 @@ mrec_status mrec_emb_bwd_plan(const mrec_table_bank *bank, const mrec_ids *ids, 
                               void *workspace, size_t ws_bytes, int32_t *d_oob_flag,
                               uint64_t *d_step, mrec_stream stream);
 
+/* an embedding-backward hash plan (arguments of mrec_emb_bwd_plan) */
+typedef struct {
+  const mrec_table_bank *bank;
+  const mrec_ids *ids;
+  int64_t batch; /* 1 .. MREC_BWD_HASH_MAX_BATCH */
+  void *workspace;
+  size_t ws_bytes;
+  int32_t *d_oob_flag;
+  uint64_t *d_step;
+} mrec_plan_job;
+
+/*
+ * mrec_interact_fwd plus the embedding-backward hash plan of `plan` (may be NULL;
+ * batch <= MREC_BWD_HASH_MAX_BATCH) in leading workgroups of the same launch: the
+ * plan depends only on the ids, and beside the latency-bound interaction it costs
+ * no kernel boundary.  Same outputs as the two calls made separately.
+ */
+mrec_status mrec_interact_fwd_ex(const mrec_table_bank *bank, const mrec_ids *ids, int64_t batch,
+                                 const float *dense, int32_t n_dense, int64_t dense_ld,
+                                 const float *dense_w, const float *bias, int32_t flags, void *x0,
+                                 mrec_dtype x0_dtype, int64_t x0_ld, int32_t x0_cols, float *logit,
+                                 float *fm_sum, int32_t *d_oob_flag, const mrec_plan_job *plan,
+                                 mrec_stream stream);
+
 /*
  * Gradient sources of lookup (b, f) (each may be NULL = 0):
  *   g_v[d] = dx[b, f*dim + d]                                (dx: F32/BF16, row stride dx_ld)
@@ -377,16 +401,6 @@ typedef struct mrec_gemm_call_s {
  */
 mrec_status mrec_gemm_multi(int32_t n, const mrec_gemm_call *calls, mrec_stream stream);
 
-/* an embedding-backward hash plan (arguments of mrec_emb_bwd_plan) */
-typedef struct {
-  const mrec_table_bank *bank;
-  const mrec_ids *ids;
-  int64_t batch; /* 1 .. MREC_BWD_HASH_MAX_BATCH */
-  void *workspace;
-  size_t ws_bytes;
-  int32_t *d_oob_flag;
-  uint64_t *d_step;
-} mrec_plan_job;
 
 /* the CTR head's parameter finish (arguments of mrec_ctr_head_finish) */
 typedef struct {

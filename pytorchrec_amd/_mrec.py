@@ -135,6 +135,9 @@ SIGNATURES = {
                                            _vp, _vp]),
     "mrec_interact_fwd": (ctypes.c_int, [_bank_p, _ids_p, _i64, _vp, _i32, _i64, _vp, _vp, _i32,
                                          _vp, ctypes.c_int, _i64, _i32, _vp, _vp, _vp, _vp]),
+    "mrec_interact_fwd_ex": (ctypes.c_int, [_bank_p, _ids_p, _i64, _vp, _i32, _i64, _vp, _vp, _i32,
+                                            _vp, ctypes.c_int, _i64, _i32, _vp, _vp, _vp,
+                                            ctypes.POINTER(PlanJob), _vp]),
     "mrec_fm2_fwd": (ctypes.c_int, [_vp, _i64, _i32, _i32, _vp, _vp]),
     "mrec_fm2_bwd": (ctypes.c_int, [_vp, _vp, _i64, _i32, _i32, _vp, _vp]),
     "mrec_emb_bwd_workspace_size": (ctypes.c_size_t, [_i32, _i64]),

@@ -618,6 +618,27 @@ __global__ __launch_bounds__(256, 6) void apply_kernel(BankArgs bank, int64_t B,
   }
 }
 
+mrec_status build_plan_job(const mrec_plan_job *plan, PlanJob *out) {
+  int eb, lpr;
+  mrec_status st = make_bank_args(plan->bank, &out->bank, &eb, &lpr);
+  if (st != MREC_OK) return st;
+  if ((st = make_ids_args(plan->ids, out->bank.n_tables, &out->ids)) != MREC_OK) return st;
+  MREC_CHECK_ARG(plan->batch >= 1 && plan->batch <= kHashMaxKeys,
+                 "plan batch must be in [1, MREC_BWD_HASH_MAX_BATCH]");
+  MREC_CHECK_ARG(plan->workspace != nullptr, "plan workspace is NULL");
+  if (plan->ws_bytes < static_cast<size_t>(out->bank.n_tables) * table_ws_bytes(plan->batch)) {
+    set_error("plan workspace too small");
+    return MREC_ENOSPC;
+  }
+  for (int f = 0; f < out->bank.n_tables; ++f)
+    MREC_CHECK_ARG(out->bank.rows[f] < (int64_t(1) << 31), "rows per table must be < 2^31");
+  out->B = plan->batch;
+  out->ws = plan->workspace;
+  out->oob = plan->d_oob_flag;
+  out->d_step = plan->d_step;
+  return MREC_OK;
+}
+
 }  // namespace mrec
 
 using namespace mrec;

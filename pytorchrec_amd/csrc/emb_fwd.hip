@@ -5,6 +5,7 @@
 // of LPR = row_bytes/16 consecutive lanes with one 16-byte load each, so one
 // wave-instruction reads 64/LPR whole rows, each as one contiguous request.
 #include "common.h"
+#include "emb_plan.h"
 
 namespace mrec {
 
@@ -61,18 +62,40 @@ __global__ __launch_bounds__(256) void gather_kernel(BankArgs bank, IdsArgs ids,
 // ---------------------------------------------------------------------------
 // fused interaction: one wave per sample
 // ---------------------------------------------------------------------------
+struct InteractArgs {
+  const float *dense;
+  int n_dense;
+  int64_t dense_ld;
+  const float *dense_w;
+  const float *bias;
+  int flags;
+  void *x0v;
+  int64_t x0_ld;
+  int x0_cols;
+  float *logit;
+  float *fm_sum;
+  int32_t *oob;
+};
+
+// sample b, by the wave whose lane this is
 template <typename T, int LPR, bool X0_BF16>
-__global__ __launch_bounds__(256) void interact_kernel(
-    BankArgs bank, IdsArgs ids, int64_t B, const float *__restrict__ dense, int n_dense,
-    int64_t dense_ld, const float *__restrict__ dense_w, const float *__restrict__ bias, int flags,
-    void *__restrict__ x0v, int64_t x0_ld, int x0_cols, float *__restrict__ logit,
-    float *__restrict__ fm_sum, int32_t *__restrict__ oob) {
+__device__ __forceinline__ void interact_sample(const BankArgs &bank, const IdsArgs &ids,
+                                                const InteractArgs &ia, int64_t b, int lane) {
   constexpr int EPL = Vec<T>::EPL;
   constexpr int WPW = 64 / LPR;                             // rows per wave-instruction
   constexpr int MAXIT = (MREC_MAX_TABLES + WPW - 1) / WPW;  // field iterations
-  const int lane = threadIdx.x & 63;
-  const int64_t b = static_cast<int64_t>(blockIdx.x) * 4 + (threadIdx.x >> 6);
-  if (b >= B) return;
+  const float *__restrict__ dense = ia.dense;
+  const int n_dense = ia.n_dense;
+  const int64_t dense_ld = ia.dense_ld;
+  const float *__restrict__ dense_w = ia.dense_w;
+  const float *__restrict__ bias = ia.bias;
+  const int flags = ia.flags;
+  void *__restrict__ x0v = ia.x0v;
+  const int64_t x0_ld = ia.x0_ld;
+  const int x0_cols = ia.x0_cols;
+  float *__restrict__ logit = ia.logit;
+  float *__restrict__ fm_sum = ia.fm_sum;
+  int32_t *__restrict__ oob = ia.oob;
   const int worker = lane / LPR;
   const int l = lane % LPR;
   const int e0 = l * EPL;
@@ -189,6 +212,33 @@ __global__ __launch_bounds__(256) void interact_kernel(
   }
 }
 
+template <typename T, int LPR, bool X0_BF16>
+__global__ __launch_bounds__(256) void interact_kernel(BankArgs bank, IdsArgs ids, int64_t B,
+                                                       InteractArgs ia) {
+  const int64_t b = static_cast<int64_t>(blockIdx.x) * 4 + (threadIdx.x >> 6);
+  if (b >= B) return;
+  interact_sample<T, LPR, X0_BF16>(bank, ids, ia, b, threadIdx.x & 63);
+}
+
+// the interaction (16 samples per 1024-thread workgroup) with the embedding-
+// backward hash plan in the leading workgroups: a HIP graph runs the step's
+// kernels one after another, so the plan would otherwise cost a kernel of its own
+template <typename T, int LPR, bool X0_BF16>
+__global__ __launch_bounds__(1024) void interact_plan_kernel(BankArgs bank, IdsArgs ids, int64_t B,
+                                                             InteractArgs ia, PlanJob plan,
+                                                             int plan_blocks) {
+  __shared__ uint32_t smem[2 * kHashSlots + 1];
+  if (static_cast<int>(blockIdx.x) < plan_blocks) {  // uniform
+    if (static_cast<int>(blockIdx.x) < plan.bank.n_tables)
+      plan_hash_body<1024, kHashSlots>(plan.bank, plan.ids, plan.B, plan.ws, plan.oob,
+                                       plan.d_step, blockIdx.x, smem);
+    return;
+  }
+  const int64_t b = static_cast<int64_t>(blockIdx.x - plan_blocks) * 16 + (threadIdx.x >> 6);
+  if (b >= B) return;
+  interact_sample<T, LPR, X0_BF16>(bank, ids, ia, b, threadIdx.x & 63);
+}
+
 // ---------------------------------------------------------------------------
 // standalone FM2 on [B, F, D] fp32: one wave per sample, lanes over d
 // ---------------------------------------------------------------------------
@@ -249,15 +299,18 @@ static void launch_gather(int lpr, const BankArgs &ba, const IdsArgs &ia, int64_
 }
 
 template <typename T, bool XB>
-static void launch_interact(int lpr, const BankArgs &ba, const IdsArgs &ia, int64_t B,
-                            const float *dense, int n_dense, int64_t dense_ld, const float *dense_w,
-                            const float *bias, int flags, void *x0, int64_t x0_ld, int x0_cols,
-                            float *logit, float *fm_sum, int32_t *oob, hipStream_t s) {
+static void launch_interact(int lpr, const BankArgs &ba, const IdsArgs &ids, int64_t B,
+                            const InteractArgs &ia, const PlanJob *plan, hipStream_t s) {
+  const int pb = plan ? plan->bank.n_tables : 0;
   const dim3 grid(static_cast<unsigned>((B + 3) / 4));
+  const dim3 grid_p(static_cast<unsigned>(pb + (B + 15) / 16));
 #define MREC_IK(L)                                                                          \
-  interact_kernel<T, L, XB><<<grid, 256, 0, s>>>(ba, ia, B, dense, n_dense, dense_ld, dense_w, \
-                                                 bias, flags, x0, x0_ld, x0_cols, logit,       \
-                                                 fm_sum, oob)
+  do {                                                                                      \
+    if (plan)                                                                               \
+      interact_plan_kernel<T, L, XB><<<grid_p, 1024, 0, s>>>(ba, ids, B, ia, *plan, pb);    \
+    else                                                                                    \
+      interact_kernel<T, L, XB><<<grid, 256, 0, s>>>(ba, ids, B, ia);                       \
+  } while (0)
   switch (lpr) {
     case 1: MREC_IK(1); break;
     case 2: MREC_IK(2); break;
@@ -313,6 +366,16 @@ mrec_status mrec_interact_fwd(const mrec_table_bank *bank, const mrec_ids *ids, 
                               const float *dense_w, const float *bias, int32_t flags, void *x0,
                               mrec_dtype x0_dtype, int64_t x0_ld, int32_t x0_cols, float *logit,
                               float *fm_sum, int32_t *d_oob_flag, mrec_stream stream) {
+  return mrec_interact_fwd_ex(bank, ids, batch, dense, n_dense, dense_ld, dense_w, bias, flags, x0,
+                              x0_dtype, x0_ld, x0_cols, logit, fm_sum, d_oob_flag, nullptr, stream);
+}
+
+mrec_status mrec_interact_fwd_ex(const mrec_table_bank *bank, const mrec_ids *ids, int64_t batch,
+                                 const float *dense, int32_t n_dense, int64_t dense_ld,
+                                 const float *dense_w, const float *bias, int32_t flags, void *x0,
+                                 mrec_dtype x0_dtype, int64_t x0_ld, int32_t x0_cols, float *logit,
+                                 float *fm_sum, int32_t *d_oob_flag, const mrec_plan_job *plan,
+                                 mrec_stream stream) {
   BankArgs ba;
   IdsArgs ia;
   int eb, lpr;
@@ -336,23 +399,26 @@ mrec_status mrec_interact_fwd(const mrec_table_bank *bank, const mrec_ids *ids, 
   }
   MREC_CHECK_ARG(fm_sum == nullptr || (reinterpret_cast<uintptr_t>(fm_sum) & 15) == 0,
                  "fm_sum not 16B aligned");
+  PlanJob pj;
+  if (plan) {
+    if ((st = build_plan_job(plan, &pj)) != MREC_OK) return st;
+  }
   if (batch == 0) return MREC_OK;
   hipStream_t s = static_cast<hipStream_t>(stream);
   const bool xb16 = x0 && x0_dtype == MREC_BF16;
+  const InteractArgs args{dense, n_dense, dense_ld, dense_w, bias,   flags,
+                          x0,    x0_ld,   x0_cols,  logit,   fm_sum, d_oob_flag};
+  const PlanJob *pp = plan ? &pj : nullptr;
   if (bank->dtype == MREC_BF16) {
     if (xb16)
-      launch_interact<uint16_t, true>(lpr, ba, ia, batch, dense, n_dense, dense_ld, dense_w, bias,
-                                      flags, x0, x0_ld, x0_cols, logit, fm_sum, d_oob_flag, s);
+      launch_interact<uint16_t, true>(lpr, ba, ia, batch, args, pp, s);
     else
-      launch_interact<uint16_t, false>(lpr, ba, ia, batch, dense, n_dense, dense_ld, dense_w, bias,
-                                       flags, x0, x0_ld, x0_cols, logit, fm_sum, d_oob_flag, s);
+      launch_interact<uint16_t, false>(lpr, ba, ia, batch, args, pp, s);
   } else {
     if (xb16)
-      launch_interact<float, true>(lpr, ba, ia, batch, dense, n_dense, dense_ld, dense_w, bias,
-                                   flags, x0, x0_ld, x0_cols, logit, fm_sum, d_oob_flag, s);
+      launch_interact<float, true>(lpr, ba, ia, batch, args, pp, s);
     else
-      launch_interact<float, false>(lpr, ba, ia, batch, dense, n_dense, dense_ld, dense_w, bias,
-                                    flags, x0, x0_ld, x0_cols, logit, fm_sum, d_oob_flag, s);
+      launch_interact<float, false>(lpr, ba, ia, batch, args, pp, s);
   }
   return launch_status("mrec_interact_fwd");
 }

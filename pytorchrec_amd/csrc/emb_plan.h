@@ -207,4 +207,16 @@ __device__ __forceinline__ void plan_hash_body(const BankArgs &bank, const IdsAr
   PLAN_STAMP(4);
 }
 
+struct PlanJob {  // an embedding-backward hash plan run by spare workgroups of another launch
+  BankArgs bank;
+  IdsArgs ids;
+  int64_t B;
+  void *ws;
+  int32_t *oob;
+  uint64_t *d_step;
+};
+
+// host: validate a mrec_plan_job and fill its kernel arguments (emb_bwd.hip)
+mrec_status build_plan_job(const mrec_plan_job *plan, PlanJob *out);
+
 }  // namespace mrec

@@ -370,15 +370,6 @@ constexpr int MULTI_MAX = 4;
 constexpr size_t kGemmLdsMin = NBUF * 2 * GROUP_ELEMS * sizeof(uint16_t);  // <= kGemmLds
 enum : int { JOB_GEMM_RR = 0, JOB_GEMM_RC = 1, JOB_GEMM_CR = 2, JOB_GEMM_CC = 3, JOB_REDUCE = 4 };
 
-struct PlanJob {  // an embedding-backward hash plan run by the first workgroups
-  BankArgs bank;
-  IdsArgs ids;
-  int64_t B;
-  void *ws;
-  int32_t *oob;
-  uint64_t *d_step;
-};
-
 struct MultiArgs {
   int n;
   int plan_blocks;  // leading workgroups that run `plan` (one per table, padded to 8)
@@ -647,23 +638,8 @@ mrec_status mrec_gemm_multi_ex(int32_t n, const mrec_gemm_call *calls, const mre
     ma.fin_blocks = (ma.fin_blocks + 7) / 8 * 8;
   }
   if (plan) {
-    int eb, lpr;
-    mrec_status st = make_bank_args(plan->bank, &ma.plan.bank, &eb, &lpr);
+    mrec_status st = build_plan_job(plan, &ma.plan);
     if (st != MREC_OK) return st;
-    if ((st = make_ids_args(plan->ids, ma.plan.bank.n_tables, &ma.plan.ids)) != MREC_OK) return st;
-    MREC_CHECK_ARG(plan->batch >= 1 && plan->batch <= kHashMaxKeys,
-                   "plan batch must be in [1, MREC_BWD_HASH_MAX_BATCH]");
-    MREC_CHECK_ARG(plan->workspace != nullptr, "plan workspace is NULL");
-    if (plan->ws_bytes < mrec_emb_bwd_workspace_size(ma.plan.bank.n_tables, plan->batch)) {
-      set_error("mrec_gemm_multi_ex: plan workspace too small");
-      return MREC_ENOSPC;
-    }
-    for (int f = 0; f < ma.plan.bank.n_tables; ++f)
-      MREC_CHECK_ARG(ma.plan.bank.rows[f] < (int64_t(1) << 31), "rows per table must be < 2^31");
-    ma.plan.B = plan->batch;
-    ma.plan.ws = plan->workspace;
-    ma.plan.oob = plan->d_oob_flag;
-    ma.plan.d_step = plan->d_step;
     ma.plan_blocks = (ma.plan.bank.n_tables + 7) / 8 * 8;
   }
   int blocks = 0;

@@ -405,15 +405,25 @@ class _InteractFn(torch.autograd.Function):
         logit = torch.empty(B, dtype=torch.float32, device=dev)
         fm_sum = torch.empty(B, bank.dim, dtype=torch.float32, device=dev) if fm2 else None
         flag = _oob_flag(bank, dev)
+        plan_ws, job = None, None
+        idd = _ids_desc(ids)
+        if need_bwd and 0 < B <= _mrec.BWD_HASH_MAX_BATCH:
+            # the backward's hash plan runs in leading workgroups of this launch
+            wsb = _mrec.lib().mrec_emb_bwd_workspace_size(bank.n_tables, B)
+            ws = torch.empty(wsb, dtype=torch.uint8, device=dev)
+            desc = bank.desc()
+            desc.ref()
+            job = _mrec.PlanJob(ctypes.pointer(desc.struct), ctypes.pointer(idd.struct), B,
+                                ws.data_ptr(), wsb, None, bank.step_counter().data_ptr())
+            plan_ws = (ws, wsb)
         if B:
-            _mrec.call("mrec_interact_fwd", bank.desc().ref(), _ids_desc(ids).ref(), B,
+            _mrec.call("mrec_interact_fwd_ex", bank.desc().ref(), idd.ref(), B,
                        _mrec.ptr(dense), n_dense, dense.stride(0) if dense is not None else 0,
                        _mrec.ptr(dense_w), _mrec.ptr(bias), flags, _mrec.ptr(x0),
                        _mrec.dtype_code(x0_dtype), x0.stride(0) if x0 is not None else 0,
                        int(x0_cols), logit.data_ptr(), _mrec.ptr(fm_sum), _mrec.ptr(flag),
-                       _mrec.stream_handle())
-        plan_ws = None
-        if need_bwd and 0 < B <= _mrec.BWD_MAX_BATCH:
+                       ctypes.byref(job) if job is not None else None, _mrec.stream_handle())
+        if need_bwd and plan_ws is None and 0 < B <= _mrec.BWD_MAX_BATCH:
             plan_ws = _make_plan(bank, ids, B)
         _raise_if_oob(flag)
         ctx.bank, ctx.ids, ctx.B, ctx.plan_ws = bank, ids, B, plan_ws

@@ -19,9 +19,11 @@ import json
 import os
 import sys
 
-KERNELS = {"interact_kernel": "mrec_interact_fwd", "plan_kernel": "mrec_emb_bwd_plan",
+# substring of the kernel name -> key (first match wins)
+KERNELS = {"interact_plan_kernel": "mrec_interact_fwd_ex", "interact_kernel": "mrec_interact_fwd",
+           "plan_hash_kernel": "mrec_emb_bwd_plan", "plan_kernel": "mrec_emb_bwd_plan",
            "apply_kernel": "mrec_emb_bwd_apply", "gemm_dma_kernel": "mrec_gemm",
-           "gather_kernel": "mrec_emb_gather_fwd"}
+           "gemm_multi_kernel": "mrec_gemm_multi", "gather_kernel": "mrec_emb_gather_fwd"}
 
 
 def per_kernel(d, counter):
@@ -34,6 +36,7 @@ def per_kernel(d, counter):
         for k, v in KERNELS.items():
             if k in name:
                 agg[v].append(float(r["Counter_Value"]))
+                break
     return {k: sum(v) / len(v) for k, v in agg.items()}, {k: len(v) for k, v in agg.items()}
 
 

@@ -205,11 +205,15 @@ def kernel_rooflines(model, data, args):
     an unsharded C2 bank of the same shapes (at N>1 the model's tables are shards)."""
     from pytorchrec_amd import _mrec, embedding as E
     dev = torch.device("cuda", torch.cuda.current_device())
-    bank = E.EmbeddingBank([args.rows_per_table] * CRITEO_FIELDS, 16, with_first_order=True,
-                           dtype=torch.bfloat16, device=dev)
-    E.init_bank_(bank, generator=torch.Generator(device=dev).manual_seed(5))
-    bank.use_fused_sgd(args.lr)
-    bank.check_ids = False
+    if type(model.embeddings) is E.EmbeddingBank:
+        bank = model.embeddings  # unsharded: time the model's own bank (no second copy of
+        # a 100M-row C5 bank); the timed updates run after the timed region
+    else:
+        bank = E.EmbeddingBank([args.rows_per_table] * CRITEO_FIELDS, 16, with_first_order=True,
+                               dtype=torch.bfloat16, device=dev)
+        E.init_bank_(bank, generator=torch.Generator(device=dev).manual_seed(5))
+        bank.use_fused_sgd(args.lr)
+        bank.check_ids = False
     dense_weight = torch.randn(CRITEO_DENSE, device=dev) * 0.01
     global_bias = torch.zeros(1, device=dev)
     B, F, D = args.batch, bank.n_tables, bank.dim

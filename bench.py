@@ -55,6 +55,9 @@ def parse():
     p.add_argument("--no-roofline", action="store_true")
     p.add_argument("--shard", action="store_true",
                    help="row-sharded tables + DP even at N=1 (always on for N>1)")
+    p.add_argument("--shard-cap", type=int, default=None,
+                   help="exchange slots per (owner, table); default: sharding.default_cap "
+                        "(uniform ids), min(batch, 8192 / W) with --zipf")
     p.add_argument("--force-collectives", action="store_true",
                    help="issue the all-to-alls / all-reduce even at N=1 (RCCL capture check)")
     return p.parse_args()
@@ -75,7 +78,11 @@ def build_deepfm(args, device, comm=None):
               for f in range(CRITEO_FIELDS)]
     dense = [NumericColumn(f"c_n_I{j + 1}") for j in range(CRITEO_DENSE)]
     label = CategoricalColumnWithIdentity(2, "label")
-    ctx = sharded_tables(comm, max_batch=args.batch) if comm is not None else contextlib.nullcontext()
+    cap = args.shard_cap
+    if cap is None and args.zipf > 0 and comm is not None:
+        cap = min(args.batch, 8192 // comm.world)  # skewed ids: no tight capacity
+    ctx = (sharded_tables(comm, cap=cap, max_batch=args.batch) if comm is not None
+           else contextlib.nullcontext())
     with ctx:
         model = DeepFM(sparse, dense, label, emb_size=16, layers=(400, 400, 400), dropout=0.0,
                        emb_dtype=torch.bfloat16, device=device, random_seed=2020)
@@ -359,14 +366,14 @@ def main():
             graphs = []
             for d in datas:
                 g = torch.cuda.CUDAGraph()
-                with torch.cuda.graph(g):
+                with torch.cuda.graph(g, capture_error_mode="thread_local"):
                     step(d)
                 graphs.append(g)
             multi = None
             G = max(1, min(args.graph_steps, 4))
             if G > 1:
                 multi = torch.cuda.CUDAGraph()
-                with torch.cuda.graph(multi):
+                with torch.cuda.graph(multi, capture_error_mode="thread_local"):
                     for k in range(G):
                         step(datas[k])
         except Exception as e:  # e.g. a collective the runtime cannot capture
@@ -477,8 +484,22 @@ def main():
         result["cpu_baseline"] = cpu_baseline(args)
     if rank == 0:
         print(json.dumps(result), flush=True)
+    # teardown: captured graphs hold RCCL kernels of the communicator, so they are
+    # released (and the device drained) before the process group goes away
+    del run, run_steps
+    graphs = multi = g = None
+    import gc
+    gc.collect()
+    torch.cuda.synchronize()
     if torch.distributed.is_initialized():
-        torch.distributed.destroy_process_group()
+        # destroy_process_group() hangs on this image once RCCL kernels were
+        # captured in a HIP graph (measured at world 1: > 120 s); every rank has
+        # finished its device work and rank 0 has printed, so leave without it
+        torch.distributed.barrier()
+        torch.cuda.synchronize()
+        sys.stdout.flush()
+        sys.stderr.flush()
+        os._exit(0)
 
 
 if __name__ == "__main__":

@@ -32,7 +32,7 @@
 extern "C" {
 #endif
 
-#define MREC_ABI_VERSION 8
+#define MREC_ABI_VERSION 9
 #define MREC_MAX_TABLES 64      /* tables per table bank / per call */
 #define MREC_BWD_MAX_BATCH 8192  /* lookups per table per plan/apply call */
 #define MREC_BWD_HASH_MAX_BATCH 4096  /* batches up to this use the hash plan */
@@ -236,7 +236,8 @@ mrec_status mrec_emb_bwd_apply_ex(const mrec_table_bank *bank, int64_t batch,
  * table f contributes g_occ[idx * g_ld + 0 .. dim(+1)), idx = b when chunk == 0,
  * else (b / chunk) * chunk_stride + f * chunk + b % chunk — the receive buffer of
  * mrec_shard_lookup_grad rows after the reverse all-to-all (fp32, g_ld % 4 == 0).
- * The owner side of a row-sharded table (SURVEY.md §8e backward).
+ * The owner side of a row-sharded table (SURVEY.md §8e backward).  Like
+ * mrec_emb_bwd_apply_ex, up to 2 deferred weight-gradient reductions may ride along.
  */
 mrec_status mrec_emb_bwd_apply_given(const mrec_table_bank *bank, int64_t batch,
                                      const void *workspace, size_t ws_bytes, const void *dx,
@@ -245,7 +246,8 @@ mrec_status mrec_emb_bwd_apply_given(const mrec_table_bank *bank, int64_t batch,
                                      int64_t x0_ld, const float *dw, const float *g_occ,
                                      int64_t g_ld, int64_t chunk, int64_t chunk_stride,
                                      mrec_bwd_mode mode, float lr, uint64_t seed,
-                                     const uint64_t *d_step, void *grad, mrec_stream stream);
+                                     const uint64_t *d_step, void *grad, int32_t n_reduce,
+                                     const struct mrec_gemm_call_s *reduce, mrec_stream stream);
 
 /* ------------------------------------------------------------------------- */
 /* Row-sharded tables (one process per GPU, W = world size)                   */
@@ -434,6 +436,28 @@ mrec_status mrec_gemm_multi_ex(int32_t n, const mrec_gemm_call *calls, const mre
  */
 mrec_status mrec_weight_prep(const float *W, int64_t N, int64_t K, int64_t ldw, void *row,
                              int64_t ldr, void *tr, int64_t ldt, mrec_stream stream);
+
+/*
+ * Data-parallel dense update: for each job, w -= lr * g over an fp32 [N, K]
+ * parameter (row strides ldw / ldg; a vector is N = 1), then the weight's bf16
+ * images are re-emitted from the new w like mrec_weight_prep (`img_row` [N, ld_row]
+ * and/or `img_tr` = W^T [K, ld_tr], pad columns zero; either may be NULL).  Up to
+ * 16 jobs, ONE launch.  Replaces torch.optim.SGD.step() on the all-reduced
+ * gradients (optimizers.py:7-11, reached from IModel.train_step, IModel.py:122-124)
+ * plus a weight_prep per layer; lr already carries the 1/world of the gradient mean.
+ */
+typedef struct {
+  float *w;
+  const float *g;
+  int64_t N, K, ldw, ldg;
+  float lr;
+  void *img_row;
+  int64_t ld_row;
+  void *img_tr;
+  int64_t ld_tr;
+} mrec_sgd_job;
+
+mrec_status mrec_sgd_multi(int32_t n, const mrec_sgd_job *jobs, mrec_stream stream);
 
 /* ------------------------------------------------------------------------- */
 /* CTR head and loss                                                          */

@@ -20,7 +20,7 @@ import torch  # noqa: F401  (must precede the dlopen, see module docstring)
 LIB_DIR = os.path.join(os.path.dirname(os.path.abspath(__file__)), "lib")
 LIB_PATH = os.environ.get("MREC_LIB_PATH") or os.path.join(LIB_DIR, "libmrec.so")
 
-ABI_VERSION = 8
+ABI_VERSION = 9
 MAX_TABLES = 64
 BWD_MAX_BATCH = 8192
 BWD_HASH_MAX_BATCH = 4096  # batches up to this use the hash plan (fusable into a GEMM launch)
@@ -114,6 +114,13 @@ class HeadFinishJob(ctypes.Structure):
                 ("dw_out", ctypes.c_void_p), ("db_out", ctypes.c_void_p),
                 ("dws_out", ctypes.c_void_p), ("db2_out", ctypes.c_void_p)]
 
+class SgdJob(ctypes.Structure):
+    _fields_ = [("w", ctypes.c_void_p), ("g", ctypes.c_void_p), ("N", ctypes.c_int64),
+                ("K", ctypes.c_int64), ("ldw", ctypes.c_int64), ("ldg", ctypes.c_int64),
+                ("lr", ctypes.c_float), ("img_row", ctypes.c_void_p), ("ld_row", ctypes.c_int64),
+                ("img_tr", ctypes.c_void_p), ("ld_tr", ctypes.c_int64)]
+
+
 LAYOUT_ROW, LAYOUT_COL = 0, 1
 ACT_NONE, ACT_RELU = 0, 1
 
@@ -153,7 +160,8 @@ SIGNATURES = {
     "mrec_emb_bwd_apply_given": (ctypes.c_int, [_bank_p, _i64, _vp, ctypes.c_size_t, _vp,
                                                 ctypes.c_int, _i64, _vp, _vp, _vp, ctypes.c_int,
                                                 _i64, _vp, _vp, _i64, _i64, _i64, ctypes.c_int,
-                                                _f32, ctypes.c_uint64, _vp, _vp, _vp]),
+                                                _f32, ctypes.c_uint64, _vp, _vp, _i32,
+                                                ctypes.POINTER(GemmCall), _vp]),
     "mrec_shard_bucketize": (ctypes.c_int, [_ids_p, _i32, ctypes.POINTER(ctypes.c_int64), _i64,
                                             _i32, _i32, _vp, _vp, _vp, _vp, _vp]),
     "mrec_shard_gather": (ctypes.c_int, [_bank_p, _vp, _i32, _i32, _vp, _vp]),
@@ -167,6 +175,7 @@ SIGNATURES = {
     "mrec_gemm_multi_ex": (ctypes.c_int, [_i32, ctypes.POINTER(GemmCall), ctypes.POINTER(PlanJob),
                                           ctypes.POINTER(HeadFinishJob), _vp]),
     "mrec_weight_prep": (ctypes.c_int, [_vp, _i64, _i64, _i64, _vp, _i64, _vp, _i64, _vp]),
+    "mrec_sgd_multi": (ctypes.c_int, [_i32, ctypes.POINTER(SgdJob), _vp]),
     "mrec_head_fwd": (ctypes.c_int, [_vp, _i64, _i64, _i32, _vp, _vp, _vp, _vp, _vp]),
     "mrec_head_bwd": (ctypes.c_int, [_vp, _vp, _i64, _i32, _vp, _i64, _vp, _i64, _vp]),
     "mrec_bce_fwd": (ctypes.c_int, [_vp, _vp, _i64, _vp, _vp]),

@@ -434,9 +434,9 @@ __global__ __launch_bounds__(256, 6) void apply_kernel(BankArgs bank, int64_t B,
   __shared__ int32_t long_list[WPB];
   __shared__ int32_t n_long;
   __shared__ float red[WPB][LPR * EPL + 1];
-  __shared__ uint32_t bits[kHashMaxKeys / 32];
-  __shared__ uint16_t srt[kHashMaxKeys];
-  __shared__ uint32_t wsum0;
+  __shared__ uint32_t bits[kHashMaxEntries / 32];
+  __shared__ uint16_t srt[kHashMaxEntries];
+  __shared__ uint32_t wsum[4];
   const int worker = threadIdx.x / LPR;
   const int l = threadIdx.x % LPR;
   const int e0 = l * EPL;
@@ -562,16 +562,18 @@ __global__ __launch_bounds__(256, 6) void apply_kernel(BankArgs bank, int64_t B,
       sn = t.seg[uu + 1] - s0;
     }
     if (hash_layout) {
-      // ascending sample order through an LDS bitmap of the batch (B <= 4096;
-      // a sample looks a table up once, so the bits are the segment)
-      for (int i = tid; i < kHashMaxKeys / 32; i += 256) bits[i] = 0u;
+      // ascending sample order through an LDS bitmap of the batch (B <= 8192
+      // entries; a sample / exchange slot looks a table up once, so the bits are
+      // the segment)
+      const int nwords = static_cast<int>((B + 31) / 32);  // <= 256: one per thread
+      if (tid < nwords) bits[tid] = 0u;
       __syncthreads();
       for (int i = tid; i < sn; i += 256) {
         const int b = t.perm[s0 + i];
         atomicOr(&bits[b >> 5], 1u << (b & 31));
       }
       __syncthreads();
-      const uint32_t word = tid < kHashMaxKeys / 32 ? bits[tid] : 0u;
+      const uint32_t word = tid < nwords ? bits[tid] : 0u;
       const uint32_t c = __popc(word);
       uint32_t incl = c;
 #pragma unroll
@@ -579,10 +581,11 @@ __global__ __launch_bounds__(256, 6) void apply_kernel(BankArgs bank, int64_t B,
         const uint32_t v = __shfl_up(incl, off);
         if (lane >= off) incl += v;
       }
-      if (tid == 63) wsum0 = incl;
+      if (lane == 63) wsum[wid] = incl;
       __syncthreads();
-      if (tid < kHashMaxKeys / 32) {
-        uint32_t pos = incl - c + (wid == 1 ? wsum0 : 0u);
+      if (tid < nwords) {
+        uint32_t pos = incl - c;
+        for (int k2 = 0; k2 < wid; ++k2) pos += wsum[k2];
         uint32_t w = word;
         while (w) {
           const int bit = __ffs(w) - 1;
@@ -623,8 +626,9 @@ mrec_status build_plan_job(const mrec_plan_job *plan, PlanJob *out) {
   mrec_status st = make_bank_args(plan->bank, &out->bank, &eb, &lpr);
   if (st != MREC_OK) return st;
   if ((st = make_ids_args(plan->ids, out->bank.n_tables, &out->ids)) != MREC_OK) return st;
-  MREC_CHECK_ARG(plan->batch >= 1 && plan->batch <= kHashMaxKeys,
-                 "plan batch must be in [1, MREC_BWD_HASH_MAX_BATCH]");
+  MREC_CHECK_ARG(plan->batch >= 1 && hash_layout(plan->batch, out->ids.pad_negative != 0),
+                 "plan batch must be in [1, MREC_BWD_HASH_MAX_BATCH] (padded exchange views: "
+                 "[1, MREC_BWD_MAX_BATCH])");
   MREC_CHECK_ARG(plan->workspace != nullptr, "plan workspace is NULL");
   if (plan->ws_bytes < static_cast<size_t>(out->bank.n_tables) * table_ws_bytes(plan->batch)) {
     set_error("plan workspace too small");
@@ -672,7 +676,7 @@ mrec_status mrec_emb_bwd_plan(const mrec_table_bank *bank, const mrec_ids *ids, 
   for (int f = 0; f < ba.n_tables; ++f)
     MREC_CHECK_ARG(ba.rows[f] < (int64_t(1) << 31), "rows per table must be < 2^31");
   const int rounds = static_cast<int>((batch + kPlanThreads - 1) / kPlanThreads);
-  if (batch >= 1 && batch <= kHashMaxKeys) {
+  if (batch >= 1 && hash_layout(batch, ia.pad_negative != 0)) {
     plan_hash_kernel<<<dim3(ba.n_tables), kPlanThreads, 0, static_cast<hipStream_t>(stream)>>>(
         ba, ia, batch, workspace, d_oob_flag, d_step);
     return launch_status("mrec_emb_bwd_plan");
@@ -726,10 +730,11 @@ mrec_status mrec_emb_bwd_apply_given(const mrec_table_bank *bank, int64_t batch,
                                      int64_t x0_ld, const float *dw, const float *g_occ,
                                      int64_t g_ld, int64_t chunk, int64_t chunk_stride,
                                      mrec_bwd_mode mode, float lr, uint64_t seed,
-                                     const uint64_t *d_step, void *grad, mrec_stream stream) {
+                                     const uint64_t *d_step, void *grad, int32_t n_reduce,
+                                     const mrec_gemm_call *reduce, mrec_stream stream) {
   return apply_impl(bank, batch, workspace, ws_bytes, dx, dx_dtype, dx_ld, dfm, fm_sum, x0,
                     x0_dtype, x0_ld, dw, g_occ, g_ld, chunk, chunk_stride, mode, lr, seed, d_step,
-                    grad, 0, nullptr, stream);
+                    grad, n_reduce, reduce, stream);
 }
 
 }  // extern "C"
@@ -803,7 +808,7 @@ static mrec_status apply_impl(const mrec_table_bank *bank, int64_t batch, const 
   const int wpb = 256 / lpr;
   // hash layout (batch <= kHashMaxKeys, see mrec_emb_bwd_plan): segments only for
   // rows hit twice or more (<= batch / 2 of them), plus the sample-major blocks
-  const bool hash = batch <= kHashMaxKeys;
+  const bool hash = hash_layout(batch, g_occ != nullptr);  // given grads: an exchange view
   const int seg_blocks = static_cast<int>(((hash ? batch / 2 : batch) + wpb - 1) / wpb);
   const int64_t sm_blocks = hash ? (batch * F + wpb - 1) / wpb : 0;
   const int apply_blocks = static_cast<int>(static_cast<int64_t>(seg_blocks) * F + sm_blocks);

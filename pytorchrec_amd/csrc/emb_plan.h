@@ -77,17 +77,24 @@ __device__ uint64_t g_plan_prof[16];
 // workspace layout is not deterministic; apply sorts every segment's lookups
 // back into ascending sample order, so the updates are.
 // ---------------------------------------------------------------------------
-constexpr int kHashMaxKeys = 4096;
+constexpr int kHashMaxKeys = 4096;     // dense batches up to this use the hash plan
+constexpr int kHashMaxEntries = 8192;  // padded exchange views (ids.pad_negative) up to this:
+                                       // their valid ids are ~1/2 of the entries (cap = 2x share)
 constexpr int kHashSlots = 8192;  // load factor <= 1/2 (standalone 1024-thread kernel)
 constexpr int kHashSlotsSmall = 6016;  // 47 KiB: the plan inside a GEMM launch (<= 48 KiB LDS)
 constexpr uint32_t kEmpty = 0xffffffffu;
 
-template <int THREADS, int SLOTS>
+// hash layout for `batch` entries (the same rule in plan and apply)
+__host__ __device__ inline bool hash_layout(int64_t batch, bool padded) {
+  return batch <= kHashMaxKeys || (padded && batch <= kHashMaxEntries);
+}
+
+template <int THREADS, int SLOTS, int MAXB = kHashMaxEntries>
 __device__ __forceinline__ void plan_hash_body(const BankArgs &bank, const IdsArgs &ids, int64_t B,
                                                void *ws, int32_t *__restrict__ oob,
                                                uint64_t *__restrict__ d_step, int f,
                                                uint32_t *smem) {
-  constexpr int kRounds = kHashMaxKeys / THREADS;
+  constexpr int kRounds = MAXB / THREADS;
   uint32_t *hkey = smem;          // [SLOTS] row id; after the claim: (segment << 16) | start
   uint32_t *hcnt = smem + SLOTS;  // [SLOTS] (tickets << 16) | lookups
   uint32_t &s_tot = smem[2 * SLOTS];  // (segments << 16) | lookups placed

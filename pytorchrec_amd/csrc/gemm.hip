@@ -389,7 +389,7 @@ __global__ __launch_bounds__(GEMM_THREADS) void gemm_multi_kernel(MultiArgs ma) 
   extern __shared__ __attribute__((aligned(16))) uint16_t smem[];
   if (static_cast<int>(blockIdx.x) < ma.plan_blocks) {  // uniform
     if (static_cast<int>(blockIdx.x) < ma.plan.bank.n_tables)
-      plan_hash_body<GEMM_THREADS, kHashSlotsSmall>(ma.plan.bank, ma.plan.ids, ma.plan.B,
+      plan_hash_body<GEMM_THREADS, kHashSlotsSmall, kHashMaxKeys>(ma.plan.bank, ma.plan.ids, ma.plan.B,
                                                      ma.plan.ws, ma.plan.oob, ma.plan.d_step,
                                                      blockIdx.x, reinterpret_cast<uint32_t *>(smem));
     return;
@@ -640,6 +640,7 @@ mrec_status mrec_gemm_multi_ex(int32_t n, const mrec_gemm_call *calls, const mre
   if (plan) {
     mrec_status st = build_plan_job(plan, &ma.plan);
     if (st != MREC_OK) return st;
+    MREC_CHECK_ARG(ma.plan.B <= kHashMaxKeys, "a plan inside a GEMM launch takes <= 4096 ids");
     ma.plan_blocks = (ma.plan.bank.n_tables + 7) / 8 * 8;
   }
   int blocks = 0;

@@ -6,8 +6,9 @@
 // gather      (owner,  fwd) : rows of the received local ids -> send buffer;
 // lookup_grad (sender, bwd) : per-lookup gradient rows written to the slot the row
 //                             came from, ready for the reverse all-to-all.
-// The owner's update reuses mrec_emb_bwd_plan (chunked, padding-aware ids) and
-// mrec_emb_bwd_apply_given.  All three kernels are HBM/latency bound byte moves.
+// The owner's update reuses the hash plan over the padded exchange view (run inside
+// the interaction launch, mrec_interact_fwd_ex) and mrec_emb_bwd_apply_given.  All
+// three kernels are HBM/latency bound byte moves.
 #include <algorithm>
 
 #include "common.h"
@@ -82,15 +83,31 @@ __global__ __launch_bounds__(kBT) void bucketize_kernel(IdsArgs ids, RowsArg row
   const int nh = (W + 1) * G;
   const int nbits = 32 - __clz(static_cast<uint32_t>(W));  // values 0..W
   const uint64_t lt = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
+  // every round's id is loaded before the first is used (one memory latency, not
+  // one per round); ids < rows < 2^31, so owner / local row use 32-bit division
+  constexpr int kPre = 8;
+  int64_t pre[kPre];
+#pragma unroll
+  for (int r = 0; r < kPre; ++r) {
+    const int64_t i = static_cast<int64_t>(r) * kBT + tid;
+    pre[r] = (r < rounds && i < B) ? load_id(ids, f, i) : -1;
+  }
+  auto id_of = [&](int r, int64_t i) -> int64_t {
+    if (i >= B) return -1;
+    if (r < kPre) {
+#pragma unroll
+      for (int k = 0; k < kPre; ++k)
+        if (k == r) return pre[k];
+    }
+    return load_id(ids, f, i);
+  };
   for (int i = tid; i < nh; i += kBT) hist[i] = 0u;
   __syncthreads();
   for (int r = 0; r < rounds; ++r) {
     const int64_t i = static_cast<int64_t>(r) * kBT + tid;
     uint32_t d = static_cast<uint32_t>(W);
-    if (i < B) {
-      const int64_t id = load_id(ids, f, i);
-      if (id >= 0 && id < rows_f) d = static_cast<uint32_t>(id % W);
-    }
+    const int64_t id = id_of(r, i);
+    if (id >= 0 && id < rows_f) d = static_cast<uint32_t>(id) % static_cast<uint32_t>(W);
     const uint64_t m = same_value_lanes(d, nbits);
     if ((m & lt) == 0) hist[d * G + r * kBWaves + wid] = __popcll(m);
   }
@@ -99,11 +116,8 @@ __global__ __launch_bounds__(kBT) void bucketize_kernel(IdsArgs ids, RowsArg row
   for (int r = 0; r < rounds; ++r) {
     const int64_t i = static_cast<int64_t>(r) * kBT + tid;
     uint32_t d = static_cast<uint32_t>(W);
-    int64_t id = -1;
-    if (i < B) {
-      id = load_id(ids, f, i);
-      if (id >= 0 && id < rows_f) d = static_cast<uint32_t>(id % W);
-    }
+    const int64_t id = id_of(r, i);
+    if (id >= 0 && id < rows_f) d = static_cast<uint32_t>(id) % static_cast<uint32_t>(W);
     const uint64_t m = same_value_lanes(d, nbits);
     if (i >= B) continue;
     if (d == static_cast<uint32_t>(W)) {
@@ -118,7 +132,7 @@ __global__ __launch_bounds__(kBT) void bucketize_kernel(IdsArgs ids, RowsArg row
       continue;
     }
     const int64_t s = (static_cast<int64_t>(d) * F + f) * cap + slot;
-    send_ids[s] = static_cast<int32_t>(id / W);
+    send_ids[s] = static_cast<int32_t>(static_cast<uint32_t>(id) / static_cast<uint32_t>(W));
     pos[f * B + i] = static_cast<int32_t>(s);
   }
   // padding slots of every owner part
@@ -166,33 +180,58 @@ __device__ __forceinline__ float ld_elem(const void *p, int bf16, int64_t i) {
   return bf16 ? bf16_to_f32(static_cast<const uint16_t *>(p)[i]) : static_cast<const float *>(p)[i];
 }
 
-// one thread per (table, sample, 4-float chunk of the gradient row)
-__global__ __launch_bounds__(256) void lookup_grad_kernel(LookupGradArgs a) {
-  const int64_t t = static_cast<int64_t>(blockIdx.x) * 256 + threadIdx.x;
-  const int64_t fb = t / a.chunks;
-  const int c = static_cast<int>(t % a.chunks);
-  if (fb >= static_cast<int64_t>(a.F) * a.B) return;
-  const int f = static_cast<int>(fb / a.B);
-  const int64_t b = fb % a.B;
-  const int32_t p = a.pos[fb];
-  if (p < 0) return;
-  float g[4];
-#pragma unroll
-  for (int j = 0; j < 4; ++j) {
-    const int e = c * 4 + j;
-    float v = 0.f;
-    if (e < a.D) {
-      const int64_t col = static_cast<int64_t>(f) * a.D + e;
-      if (a.dx) v += ld_elem(a.dx, a.dx_bf16, b * a.dx_ld + col);
-      if (a.dfm)
-        v = fmaf(a.dfm[b], a.fm_sum[b * a.D + e] - ld_elem(a.x0, a.x0_bf16, b * a.x0_ld + col), v);
-    } else if (e == a.D && a.has_w && a.dw) {
-      v = a.dw[b];
-    }
-    g[j] = v;
+// 4 consecutive elements (4-aligned, 8/16-B aligned rows) as floats
+__device__ __forceinline__ void ld4(const void *p, int bf16, int64_t i, float *v) {
+  if (bf16) {
+    const uint2 r = *reinterpret_cast<const uint2 *>(static_cast<const uint16_t *>(p) + i);
+    v[0] = __uint_as_float(r.x << 16);
+    v[1] = __uint_as_float(r.x & 0xffff0000u);
+    v[2] = __uint_as_float(r.y << 16);
+    v[3] = __uint_as_float(r.y & 0xffff0000u);
+  } else {
+    const float4 r = *reinterpret_cast<const float4 *>(static_cast<const float *>(p) + i);
+    v[0] = r.x;
+    v[1] = r.y;
+    v[2] = r.z;
+    v[3] = r.w;
   }
-  *reinterpret_cast<float4 *>(a.g + static_cast<int64_t>(p) * a.g_ld + c * 4) =
-      make_float4(g[0], g[1], g[2], g[3]);
+}
+
+// one wave per sample; lane -> (table f, 4-float chunk c) items, so the sample's
+// dx / x0 row segments are read contiguously and every 16-B gradient chunk lands
+// in the row of the slot its lookup's row came from
+__global__ __launch_bounds__(256) void lookup_grad_kernel(LookupGradArgs a) {
+  const int64_t b = static_cast<int64_t>(blockIdx.x) * 4 + (threadIdx.x >> 6);
+  const int lane = threadIdx.x & 63;
+  if (b >= a.B) return;
+  const float dfm = a.dfm ? a.dfm[b] : 0.f;
+  const float dw = (a.dw && a.has_w) ? a.dw[b] : 0.f;
+  const int items = a.F * a.chunks;
+  for (int it = lane; it < items; it += 64) {
+    const int f = it / a.chunks;
+    const int c = it - f * a.chunks;
+    const int32_t p = a.pos[static_cast<int64_t>(f) * a.B + b];
+    if (p < 0) continue;
+    float g[4] = {0.f, 0.f, 0.f, 0.f};
+    const int e0 = c * 4;
+    if (e0 < a.D) {  // D % 4 == 0: the chunk is all embedding elements
+      const int64_t col = static_cast<int64_t>(f) * a.D + e0;
+      if (a.dx) ld4(a.dx, a.dx_bf16, b * a.dx_ld + col, g);
+      if (a.dfm) {
+        float x[4];
+        ld4(a.x0, a.x0_bf16, b * a.x0_ld + col, x);
+        const float4 s = *reinterpret_cast<const float4 *>(a.fm_sum + b * a.D + e0);
+        g[0] = fmaf(dfm, s.x - x[0], g[0]);
+        g[1] = fmaf(dfm, s.y - x[1], g[1]);
+        g[2] = fmaf(dfm, s.z - x[2], g[2]);
+        g[3] = fmaf(dfm, s.w - x[3], g[3]);
+      }
+    } else if (e0 == a.D) {
+      g[0] = dw;
+    }
+    *reinterpret_cast<float4 *>(a.g + static_cast<int64_t>(p) * a.g_ld + e0) =
+        make_float4(g[0], g[1], g[2], g[3]);
+  }
 }
 
 }  // namespace mrec
@@ -215,7 +254,10 @@ mrec_status mrec_shard_bucketize(const mrec_ids *ids, int32_t n_tables, const in
   MREC_CHECK_ARG((world + 1) * std::max<int64_t>(groups, 1) <= kBHist,
                  "(world + 1) * ceil(batch / 64) must be <= 2048");
   RowsArg ra;
-  for (int f = 0; f < MREC_MAX_TABLES; ++f) ra.v[f] = f < n_tables ? rows[f] : 0;
+  for (int f = 0; f < MREC_MAX_TABLES; ++f) {
+    ra.v[f] = f < n_tables ? rows[f] : 0;
+    MREC_CHECK_ARG(ra.v[f] >= 0 && ra.v[f] < (int64_t(1) << 31), "rows per table must be < 2^31");
+  }
   bucketize_kernel<<<dim3(n_tables), kBT, 0, static_cast<hipStream_t>(stream)>>>(
       ia, ra, batch, world, cap, n_tables, send_ids, pos, d_overflow, d_oob_flag);
   return launch_status("mrec_shard_bucketize");
@@ -251,8 +293,12 @@ mrec_status mrec_shard_lookup_grad(int64_t batch, int32_t n_tables, int32_t dim,
                                    const void *x0, mrec_dtype x0_dtype, int64_t x0_ld,
                                    const float *dw, float *g_out, int64_t g_ld,
                                    mrec_stream stream) {
-  MREC_CHECK_ARG(batch >= 0 && n_tables >= 1 && dim >= 1, "bad shape");
+  MREC_CHECK_ARG(batch >= 0 && n_tables >= 1 && dim >= 1 && dim % 4 == 0, "bad shape");
   MREC_CHECK_ARG(pos && g_out, "NULL pointer");
+  MREC_CHECK_ARG(!dx || (reinterpret_cast<uintptr_t>(dx) & 15) == 0, "dx not 16B aligned");
+  MREC_CHECK_ARG(!dfm || ((reinterpret_cast<uintptr_t>(x0) & 15) == 0 &&
+                          (reinterpret_cast<uintptr_t>(fm_sum) & 15) == 0),
+                 "x0 / fm_sum not 16B aligned");
   MREC_CHECK_ARG(g_ld % 4 == 0 && g_ld >= dim + (has_w ? 1 : 0) &&
                      (reinterpret_cast<uintptr_t>(g_out) & 15) == 0,
                  "g_out rows must be 16B aligned with g_ld % 4 == 0 and >= dim + has_w");
@@ -279,8 +325,7 @@ mrec_status mrec_shard_lookup_grad(int64_t batch, int32_t n_tables, int32_t dim,
   a.D = dim;
   a.has_w = has_w ? 1 : 0;
   a.chunks = (dim + a.has_w + 3) / 4;
-  const int64_t threads = static_cast<int64_t>(n_tables) * batch * a.chunks;
-  lookup_grad_kernel<<<dim3(static_cast<unsigned>((threads + 255) / 256)), 256, 0,
+  lookup_grad_kernel<<<dim3(static_cast<unsigned>((batch + 3) / 4)), 256, 0,
                        static_cast<hipStream_t>(stream)>>>(a);
   return launch_status("mrec_shard_lookup_grad");
 }

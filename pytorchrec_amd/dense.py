@@ -200,16 +200,23 @@ class _HeadFinish:
     linear ws, b2): run by spare workgroups of the next GEMM launch, or on its own
     at the end of the backward."""
 
-    def __init__(self, part, B, H, ns, g, lr, w, bias, ws, b2):
-        self.keep = [part, g, w, bias, ws, b2]
-        self.struct = _mrec.HeadFinishJob(part.data_ptr(), part.stride(0), B, H, ns, _mrec.ptr(g),
-                                          1, float(lr), w.data_ptr(), _mrec.ptr(bias),
-                                          _mrec.ptr(ws), _mrec.ptr(b2), None, None, None, None)
+    def __init__(self, part, B, H, ns, g, lr, w, bias, ws, b2, grads=None):
+        self.keep = [part, g, w, bias, ws, b2, grads]
+        if grads is None:  # SGD update in place
+            self.struct = _mrec.HeadFinishJob(part.data_ptr(), part.stride(0), B, H, ns,
+                                              _mrec.ptr(g), 1, float(lr), w.data_ptr(),
+                                              _mrec.ptr(bias), _mrec.ptr(ws), _mrec.ptr(b2),
+                                              None, None, None, None)
+        else:  # gradients into the data-parallel flat buffer views
+            self.struct = _mrec.HeadFinishJob(part.data_ptr(), part.stride(0), B, H, ns,
+                                              _mrec.ptr(g), 0, 0.0, None, None, None, None,
+                                              *[_mrec.ptr(t) for t in grads])
 
     def run(self):
         j = self.struct
-        _mrec.call("mrec_ctr_head_finish", j.part, j.ldp, j.batch, j.H, j.ns, j.g, 1, j.lr, j.w,
-                   j.bias, j.ws, j.b2, None, None, None, None, _mrec.stream_handle())
+        _mrec.call("mrec_ctr_head_finish", j.part, j.ldp, j.batch, j.H, j.ns, j.g, j.update, j.lr,
+                   j.w, j.bias, j.ws, j.b2, j.dw_out, j.db_out, j.dws_out, j.db2_out,
+                   _mrec.stream_handle())
 
 
 _FINISH = []
@@ -309,6 +316,23 @@ def sgd_lr(*params) -> Optional[float]:
     return lr
 
 
+def dp_grads(*params):
+    """Data-parallel flat-gradient views of ``params`` (None entries ignored), or
+    None unless every given parameter has one (``IModel.distribute`` assigns them:
+    the backward kernels write the gradients there, IModel all-reduces the flat
+    buffer once and applies SGD with one mrec_sgd_multi launch)."""
+    out = []
+    for p in params:
+        if p is None:
+            out.append(None)
+            continue
+        g = getattr(p, "_mrec_dp_grad", None)
+        if g is None:
+            return None
+        out.append(g)
+    return out
+
+
 def _bf16_rows(t: torch.Tensor) -> torch.Tensor:
     """bf16 [M, N] with 16-byte aligned rows (what mrec_gemm requires); copies into
     an r8-padded buffer only when the input is not already laid out that way."""
@@ -364,9 +388,12 @@ class _LinearFn(torch.autograd.Function):
         dx = dW = db = None
         need_w = ctx.needs_input_grad[1] or ctx.needs_input_grad[2]
         lr = sgd_lr(ctx.weight, ctx.bias) if need_w else None
-        if lr is not None:
+        dpg = dp_grads(ctx.weight, ctx.bias) if need_w and lr is None else None
+        if lr is not None or dpg is not None:
             # one launch: dx GEMM + dW partial slabs (+ earlier layers' deferred dW
-            # reductions); this layer's reduction + SGD runs in the next launch
+            # reductions); this layer's reduction + SGD runs in the next launch.
+            # Data-parallel: the reduction writes dW / db into the flat gradient
+            # buffer that IModel all-reduces (then one mrec_sgd_multi updates)
             calls = []
             if ctx.needs_input_grad[0]:
                 cdx = _Call(dy, _mrec.LAYOUT_ROW, ctx.wt, _mrec.LAYOUT_ROW, M, K_x, N,
@@ -374,14 +401,21 @@ class _LinearFn(torch.autograd.Function):
                 calls.append(cdx)
                 dx = cdx.out
             sk = _DW_SPLIT or _split_beside(N, K + 1, M)
-            cdw = _Call(dy, _mrec.LAYOUT_COL, x, _mrec.LAYOUT_COL, N, K, M,
-                        _mrec.GEMM_PARTIAL if sk > 1 else _mrec.GEMM_FULL,
-                        ones_out=ctx.bias.detach() if ctx.has_bias else None,
-                        out=ctx.weight.detach(), out_dtype=torch.float32, split_k=sk, sgd_lr=lr,
-                        img_row=ctx.wr, img_tr=ctx.wt)
+            if dpg is not None:
+                cdw = _Call(dy, _mrec.LAYOUT_COL, x, _mrec.LAYOUT_COL, N, K, M,
+                            _mrec.GEMM_PARTIAL if sk > 1 else _mrec.GEMM_FULL,
+                            ones_out=dpg[1], out=dpg[0], out_dtype=torch.float32, split_k=sk)
+            else:
+                cdw = _Call(dy, _mrec.LAYOUT_COL, x, _mrec.LAYOUT_COL, N, K, M,
+                            _mrec.GEMM_PARTIAL if sk > 1 else _mrec.GEMM_FULL,
+                            ones_out=ctx.bias.detach() if ctx.has_bias else None,
+                            out=ctx.weight.detach(), out_dtype=torch.float32, split_k=sk,
+                            sgd_lr=lr, img_row=ctx.wr, img_tr=ctx.wt)
             if sk > 1:
                 launch_multi(calls + [cdw])
                 _defer(cdw)
+            elif dpg is not None:  # plain dW output: independent of the dx GEMM
+                launch_multi(calls + [cdw])
             else:  # the dW epilogue rewrites wt, which the dx GEMM reads: two launches
                 launch_multi(calls)
                 launch_multi([cdw])
@@ -738,11 +772,15 @@ class _CTRHeadBCEFn(torch.autograd.Function):
         lr = sgd_lr(ctx.weight, ctx.bias, ctx.ws, ctx.b2)
         dW = db = dws = db2 = None
         det = (lambda t: None if t is None else t.detach())
+        dpg = dp_grads(ctx.weight, ctx.bias, ctx.ws, ctx.b2) if lr is None else None
         if lr is not None and ctx.weight.is_contiguous():
             # independent of the backward GEMMs: rides along the next one
             defer_head_finish(_HeadFinish(part, ctx.B, ctx.H, ctx.ns, None if one else g, lr,
                                           ctx.weight.detach(), det(ctx.bias), det(ctx.ws),
                                           det(ctx.b2)))
+        elif dpg is not None:
+            defer_head_finish(_HeadFinish(part, ctx.B, ctx.H, ctx.ns, None if one else g, None,
+                                          None, None, None, None, grads=dpg))
         else:
             f32 = dict(dtype=torch.float32, device=dev)
             dW = torch.empty(1, ctx.H, **f32)

@@ -154,16 +154,62 @@ class IModel(Module, IWithArguments, ABC):
         comm = getattr(self, "dp_comm", None)
         dp = comm is not None and (comm.world > 1 or comm.force)
         for p in self.parameters():
-            if hasattr(p, "_mrec_sgd_group"):
-                del p._mrec_sgd_group
-        if dp or not isinstance(optimizer, torch.optim.SGD):
+            for a in ("_mrec_sgd_group", "_mrec_dp_group", "_mrec_dp_grad"):
+                if hasattr(p, a):
+                    delattr(p, a)
+        self._dp_flat = None
+        if not isinstance(optimizer, torch.optim.SGD):
             return
+        plain = []
         for g in optimizer.param_groups:
             if (g.get("momentum", 0) == 0 and g.get("weight_decay", 0) == 0
                     and not g.get("nesterov", False) and not g.get("maximize", False)
                     and g.get("dampening", 0) == 0):
-                for p in g["params"]:
-                    p._mrec_sgd_group = g
+                plain += [(p, g) for p in g["params"]]
+        if not dp:
+            for p, g in plain:
+                p._mrec_sgd_group = g
+            return
+        # data parallel on the GPU: the backward kernels write the dense gradients
+        # into ONE flat fp32 buffer (a view per parameter, 16-B aligned rows), the
+        # step all-reduces it once and applies SGD to every parameter (and its bf16
+        # GEMM images) in one mrec_sgd_multi launch
+        dp_ids = {id(p) for p in self._dp_params()}
+        plain = [(p, g) for p, g in plain
+                 if id(p) in dp_ids and p.is_cuda and p.dim() <= 2 and p.is_contiguous()]
+        if not plain or len(plain) > 16:
+            return
+        layout, off = [], 0
+        for p, g in plain:
+            n, k = (1, p.numel()) if p.dim() < 2 else p.shape
+            ld = (k + 7) // 8 * 8
+            layout.append((p, g, n, k, ld, off))
+            off += n * ld
+        flat = torch.zeros(max(off, 1), dtype=torch.float32, device=plain[0][0].device)
+        for p, g, n, k, ld, o in layout:
+            view = flat[o:o + n * ld].view(n, ld)[:, :k]
+            p._mrec_dp_grad = view if p.dim() == 2 else view.reshape(-1)
+            p._mrec_dp_group = g
+        self._dp_flat = (flat, layout)
+
+    def _dp_flat_step(self):
+        """All-reduce the flat gradient buffer (sum) and apply SGD with lr / world to
+        every parameter that owns a view of it, plus its cached bf16 images."""
+        from pytorchrec_amd import _mrec
+        flat, layout = self._dp_flat
+        comm = self.dp_comm
+        comm.allreduce_sum_(flat)
+        jobs = []
+        for p, g, n, k, ld, o in layout:
+            img = getattr(p, "_mrec_img", None) if p.dim() == 2 else None
+            wr, wt = (img[1], img[2]) if img is not None and img[0] == p._version else (None, None)
+            jobs.append(_mrec.SgdJob(p.data_ptr(), flat.data_ptr() + 4 * o, n, k,
+                                     p.stride(0) if p.dim() == 2 else k, ld,
+                                     float(g["lr"]) / comm.world,
+                                     _mrec.ptr(wr), wr.stride(0) if wr is not None else 0,
+                                     _mrec.ptr(wt), wt.stride(0) if wt is not None else 0))
+        arr = (_mrec.SgdJob * len(jobs))(*jobs)
+        _mrec.call("mrec_sgd_multi", len(jobs), arr, _mrec.stream_handle())
 
     # -- data parallel (one process per GPU; SURVEY.md §8e) ------------------------
     def distribute(self, comm):
@@ -216,7 +262,9 @@ class IModel(Module, IWithArguments, ABC):
             loss.backward()
         comm = getattr(self, "dp_comm", None)
         if comm is not None and (comm.world > 1 or comm.force):
-            self._allreduce_dense_grads()
+            if getattr(self, "_dp_flat", None) is not None:
+                self._dp_flat_step()
+            self._allreduce_dense_grads()  # parameters outside the flat buffer
         self.compiled_optimizers.step(closure=None)
         return {"loss": loss}
 

@@ -12,7 +12,8 @@ The dense tower stays data-parallel.  One training step of a sharded bank:
   ---- backward ----
   sender  per-lookup gradient rows into the same slots       mrec_shard_lookup_grad
           all_to_all gradients to the owners                 (equal split)
-  owner   sorted-segment plan over the received ids          mrec_emb_bwd_plan (chunked view)
+  owner   hash plan over the received ids (padded view),     run by leading workgroups
+          of the interaction launch                          (mrec_interact_fwd_ex)
           fixed-order segment sums + fused SGD               mrec_emb_bwd_apply_given
 
 Every exchange buffer is ``[W][n_tables][cap]`` slots, so all collectives are
@@ -31,14 +32,14 @@ from __future__ import annotations
 
 import contextlib
 import ctypes
+import math
 from typing import List, Optional, Sequence
 
 import torch
 import torch.distributed as dist
 
 from pytorchrec_amd import _mrec
-from pytorchrec_amd.embedding import (EmbeddingBank, _AsyncPlanBase, _dense_first_order_grads,
-                                      _side_stream, _trigger)
+from pytorchrec_amd.embedding import EmbeddingBank, _dense_first_order_grads, _trigger
 
 
 # ----------------------------------------------------------------------------
@@ -70,6 +71,11 @@ class ShardComm:
         dist.all_to_all_single(out, send, group=self.group)
         return out
 
+    def allreduce_sum_(self, flat: torch.Tensor) -> torch.Tensor:
+        if self.world > 1 or self.force:
+            dist.all_reduce(flat, group=self.group)
+        return flat
+
     def allreduce_mean_(self, flat: torch.Tensor) -> torch.Tensor:
         if self.world > 1 or self.force:
             dist.all_reduce(flat, group=self.group)
@@ -82,12 +88,25 @@ class ShardComm:
         return t
 
 
-def default_cap(batch: int, world: int) -> int:
-    """Slots per (owner, table): every id fits at W <= 2; at larger W twice the
-    uniform share (hot Zipf owners reach ~1.6x at W = 8), bounded so the owner's
-    per-table plan stays within MREC_BWD_MAX_BATCH keys."""
-    cap = min(int(batch), _mrec.BWD_MAX_BATCH // int(world))
-    return max(1, cap)
+def default_cap(batch: int, world: int, rows: Optional[Sequence[int]] = None,
+                sigmas: float = 8.0) -> int:
+    """Slots per (owner, table), sized for ids spread uniformly over each table: the
+    count of a table's ids owned by one rank is Binomial(batch, p) with p the
+    largest owner share of the table's rows (ceil(n / W) / n, 1/W for big tables),
+    so mean + 8 sd (rounded up to 8) overflows with probability < 1e-14 per (owner,
+    table) — at W = 8, B = 4096 that is 688 slots for a mean of 512, where a 2x
+    share would move 1.5x the bytes over xGMI in each of the three all-to-alls.
+    Skewed ids (Zipf) need a larger ``cap`` (an overflow is raised, never dropped).
+    Bounded so the owner's per-table plan stays within MREC_BWD_MAX_BATCH entries."""
+    batch, world = int(batch), int(world)
+    if world <= 1:
+        cap = batch
+    else:
+        shares = [-(-int(n) // world) / int(n) for n in (rows or []) if int(n) > 0]
+        p = max(shares + [1.0 / world])
+        sd = math.sqrt(batch * p * (1.0 - p))
+        cap = (int(math.ceil(batch * p + sigmas * sd)) + 7) // 8 * 8
+    return max(1, min(batch, cap, _mrec.BWD_MAX_BATCH // world))
 
 
 # ----------------------------------------------------------------------------
@@ -112,7 +131,8 @@ class ShardedEmbeddingBank(EmbeddingBank):
         self.global_rows = [int(n) for n in category_nums]
         self.comm = comm
         self.world, self.rank = W, r
-        self.cap = int(cap) if cap is not None else default_cap(max_batch, W)
+        self.cap = (int(cap) if cap is not None
+                    else default_cap(max_batch, W, self.global_rows))
         if W * self.cap > _mrec.BWD_MAX_BATCH:
             raise ValueError(f"world * cap = {W * self.cap} exceeds MREC_BWD_MAX_BATCH")
         self._flags = None  # device int32 [2] = {overflow, oob}, sticky until checked
@@ -222,10 +242,29 @@ def remote_desc(bank: ShardedEmbeddingBank, rows_recv: torch.Tensor) -> _mrec.Ba
     return _mrec.BankDesc(rows_recv, [0] * F, [n] * F, bank.dim, bank.has_w)
 
 
+def owner_plan_job(bank: ShardedEmbeddingBank, recv_ids: torch.Tensor):
+    """The owner's backward plan as a job for the interaction launch (hash layout
+    over the padded exchange view, <= MREC_BWD_MAX_BATCH entries) ->
+    (job, (ws, ws_bytes), keep-alive)."""
+    F, W, cap = bank.n_tables, bank.world, bank.cap
+    n = W * cap
+    wsb = _mrec.lib().mrec_emb_bwd_workspace_size(F, n)
+    ws = torch.empty(wsb, dtype=torch.uint8, device=bank.weight.device)
+    desc = bank.desc()
+    desc.ref()
+    idd = _mrec.IdsDesc.exchange_view(recv_ids, F, cap)
+    fl = bank.flags()
+    job = _mrec.PlanJob(ctypes.pointer(desc.struct), ctypes.pointer(idd.struct), n, ws.data_ptr(),
+                        wsb, fl.data_ptr() + 4, bank.step_counter().data_ptr())
+    return job, (ws, wsb), (desc, idd, recv_ids)
+
+
 def shard_interact(bank: ShardedEmbeddingBank, rows_recv: torch.Tensor, pos: torch.Tensor,
-                   dense, dense_w, bias, fm2: bool, first_order: bool, x0_cols: int, x0_dtype):
+                   dense, dense_w, bias, fm2: bool, first_order: bool, x0_cols: int, x0_dtype,
+                   plan_job=None):
     """Sender: mrec_interact_fwd over the received rows (ids = slots) ->
-    (x0 or None, logit, fm_sum or None)."""
+    (x0 or None, logit, fm_sum or None).  ``plan_job`` (owner_plan_job) runs the
+    owner's backward plan in leading workgroups of the same launch."""
     B = pos.shape[1]
     dev = bank.weight.device
     rdesc = remote_desc(bank, rows_recv)
@@ -236,12 +275,13 @@ def shard_interact(bank: ShardedEmbeddingBank, rows_recv: torch.Tensor, pos: tor
     fm_sum = torch.empty(B, bank.dim, dtype=torch.float32, device=dev) if fm2 else None
     fl = bank.flags()
     if B:
-        _mrec.call("mrec_interact_fwd", rdesc.ref(),
+        _mrec.call("mrec_interact_fwd_ex", rdesc.ref(),
                    _mrec.IdsDesc([pos[f] for f in range(bank.n_tables)]).ref(), B,
                    _mrec.ptr(dense), n_dense, dense.stride(0) if dense is not None else 0,
                    _mrec.ptr(dense_w), _mrec.ptr(bias), flags, _mrec.ptr(x0),
                    _mrec.dtype_code(x0_dtype), x0.stride(0) if x0 is not None else 0,
                    int(x0_cols), logit.data_ptr(), _mrec.ptr(fm_sum), fl.data_ptr() + 4,
+                   ctypes.byref(plan_job) if plan_job is not None else None,
                    _mrec.stream_handle())
     return x0, logit, fm_sum
 
@@ -257,11 +297,6 @@ def owner_plan(bank: ShardedEmbeddingBank, recv_ids: torch.Tensor):
     _mrec.call("mrec_emb_bwd_plan", bank.desc().ref(), desc.ref(), n, ws.data_ptr(), wsb,
                fl.data_ptr() + 4, bank.step_counter().data_ptr(), _mrec.stream_handle())
     return ws, wsb
-
-
-class _AsyncOwnerPlan(_AsyncPlanBase):
-    def __init__(self, bank: ShardedEmbeddingBank, recv_ids: torch.Tensor):
-        super().__init__(bank.weight.device, lambda: owner_plan(bank, recv_ids), [recv_ids])
 
 
 def shard_lookup_grad(bank: ShardedEmbeddingBank, pos: torch.Tensor, batch: int, dx=None,
@@ -284,10 +319,15 @@ def owner_apply(bank: ShardedEmbeddingBank, plan, g_recv: torch.Tensor, lr: floa
     F, W, cap = bank.n_tables, bank.world, bank.cap
     mode = _mrec.BWD_SGD_SR if (bank.stochastic_rounding and
                                 bank.weight.dtype == torch.bfloat16) else _mrec.BWD_SGD
+    # deferred MLP weight-gradient reductions ride along this launch
+    from pytorchrec_amd import dense as dense_ops
+    jobs = dense_ops.take_pending(2)
+    arr = (_mrec.GemmCall * len(jobs))(*[j.struct() for j in jobs]) if jobs else None
     _mrec.call("mrec_emb_bwd_apply_given", bank.desc().ref(), W * cap, ws.data_ptr(), wsb,
                None, _mrec.F32, 0, None, None, None, _mrec.F32, 0, None, g_recv.data_ptr(),
                g_recv.shape[1], cap, F * cap, mode, float(lr), bank.next_seed(),
-               bank.step_counter().data_ptr(), None, _mrec.stream_handle())
+               bank.step_counter().data_ptr(), None, len(jobs), arr, _mrec.stream_handle())
+    del jobs
 
 
 # ----------------------------------------------------------------------------
@@ -304,10 +344,12 @@ class _ShardedInteractFn(torch.autograd.Function):
         comm = bank.comm
         send_ids, pos = shard_bucketize(bank, ids)
         recv_ids = comm.exchange(send_ids)
-        plan = _AsyncOwnerPlan(bank, recv_ids) if trigger is not None else None
         rows_recv = comm.exchange(shard_gather(bank, recv_ids))
+        job, plan, keep = (owner_plan_job(bank, recv_ids) if trigger is not None
+                           else (None, None, None))
         x0, logit, fm_sum = shard_interact(bank, rows_recv, pos, dense, dense_w, bias, fm2,
-                                           first_order, x0_cols, x0_dtype)
+                                           first_order, x0_cols, x0_dtype, plan_job=job)
+        del keep
         if bank.check_ids:
             bank.check_flags()
         ctx.bank, ctx.B, ctx.plan = bank, B, plan
@@ -337,7 +379,7 @@ class _ShardedInteractFn(torch.autograd.Function):
             g_send = shard_lookup_grad(bank, pos, ctx.B, dx=dx0, dfm=dfm, fm_sum=fm_sum,
                                        x0=x0 if dfm is not None else None, dw=dw)
             g_recv = bank.comm.exchange(g_send)
-            owner_apply(bank, ctx.plan.get(), g_recv, bank.current_lr() / bank.world)
+            owner_apply(bank, ctx.plan, g_recv, bank.current_lr() / bank.world)
         g_dense_w, g_bias = _dense_first_order_grads(ctx, dlogit, dense)
         return g_dense_w, g_bias, None, None, None, None, None, None, None, None
 
@@ -434,4 +476,5 @@ def sharded_interact(bank: ShardedEmbeddingBank, ids, dense, dense_w, bias, fm2:
 
 __all__ = ["ShardComm", "ShardedEmbeddingBank", "sharded_tables", "make_bank", "default_cap",
            "sharded_interact", "shard_bucketize", "shard_gather", "shard_lookup_grad",
-           "owner_plan", "owner_apply", "remote_desc", "shard_interact", "cpu_bucketize"]
+           "owner_plan", "owner_plan_job", "owner_apply", "remote_desc", "shard_interact",
+           "cpu_bucketize"]

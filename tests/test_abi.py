@@ -83,6 +83,12 @@ def test_invalid_arguments_return_einval(lib):
                                  None, None, None)
     assert st == _mrec.EINVAL
     assert lib.mrec_last_error()
+    # data-parallel SGD: too many jobs, NULL gradient
+    jobs = (_mrec.SgdJob * 17)()
+    assert lib.mrec_sgd_multi(17, jobs, None) == _mrec.EINVAL
+    jobs[0] = _mrec.SgdJob(64, None, 4, 4, 4, 8, 0.1, None, 0, None, 0)
+    assert lib.mrec_sgd_multi(1, jobs, None) == _mrec.EINVAL
+    assert b"NULL" in lib.mrec_last_error()
 
 
 def test_product_path_has_no_cpu_fallback_for_gpu_tensors():

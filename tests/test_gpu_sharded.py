@@ -46,16 +46,23 @@ def _exchange(sends, W):
     return [torch.cat([p[r] for p in parts], 0).reshape(sends[r].shape) for r in range(W)]
 
 
-@pytest.mark.parametrize("W,zipf", [(2, False), (4, False), (4, True), (3, True)])
-def test_sharded_forward_backward_bit_exact(gpu, W, zipf):
+@pytest.mark.parametrize("W,zipf,B,fused", [(2, False, 512, False), (4, False, 512, True),
+                                            (4, True, 512, False), (3, True, 512, True),
+                                            (2, False, 4096, True), (2, True, 4096, False),
+                                            (8, False, 1024, True)])
+def test_sharded_forward_backward_bit_exact(gpu, W, zipf, B, fused):
+    """fused: the owner's plan runs inside the sender's interaction launch
+    (owner_plan_job); else the standalone plan.  W * cap > 4096 entries takes the
+    padded-view hash plan.  Skewed ids get cap = B (the default cap is sized for
+    uniform ids)."""
     from pytorchrec_amd import embedding as E
     from pytorchrec_amd import sharding as S
-    B = 512
     glob = _global_bank(gpu)
     banks = []
     for r in range(W):
         b = S.ShardedEmbeddingBank(ROWS, D, S.ShardComm(world=W, rank=r), with_first_order=True,
-                                   dtype=torch.bfloat16, max_batch=B, device=gpu)
+                                   dtype=torch.bfloat16, max_batch=B, device=gpu,
+                                   cap=B if zipf else None)
         b.load_global_(_tables(glob))
         b.stochastic_rounding = False
         banks.append(b)
@@ -71,8 +78,13 @@ def test_sharded_forward_backward_bit_exact(gpu, W, zipf):
         assert torch.equal(sends[r].cpu(), ref_send) and torch.equal(poss[r].cpu(), ref_pos)
     recvs = _exchange(list(sends), W)
     rows = _exchange([S.shard_gather(banks[r], recvs[r]) for r in range(W)], W)
-    outs = [S.shard_interact(banks[r], rows[r], poss[r], dense[r], dense_w, bias, True, True,
-                             x0_cols, torch.bfloat16) for r in range(W)]
+    plans, outs = [], []
+    for r in range(W):
+        job, plan, keep = (S.owner_plan_job(banks[r], recvs[r]) if fused else (None, None, None))
+        outs.append(S.shard_interact(banks[r], rows[r], poss[r], dense[r], dense_w, bias, True,
+                                     True, x0_cols, torch.bfloat16, plan_job=job))
+        plans.append(plan if fused else S.owner_plan(banks[r], recvs[r]))
+        del keep
     for r in range(W):
         banks[r].check_flags()
     with torch.no_grad():
@@ -89,7 +101,7 @@ def test_sharded_forward_backward_bit_exact(gpu, W, zipf):
                               x0=outs[r][0], dw=dl[r]) for r in range(W)]
     grecv = _exchange(gs, W)
     for r in range(W):
-        S.owner_apply(banks[r], S.owner_plan(banks[r], recvs[r]), grecv[r], lr)
+        S.owner_apply(banks[r], plans[r], grecv[r], lr)
         banks[r].check_flags()
     # reference: one bank, concatenated batch (rank 0's samples first)
     glob.use_fused_sgd(lr)
@@ -155,3 +167,74 @@ def test_world1_sharded_deepfm_step_equals_unsharded(gpu):
     assert la == lb
     for (k, va), vb in zip(a.state_dict().items(), b.state_dict().values()):
         assert torch.equal(va, vb), k
+
+
+@pytest.fixture
+def rccl_world1(gpu):
+    """A real one-rank RCCL process group (collectives forced at world 1)."""
+    import os
+    import torch.distributed as dist
+    os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+    os.environ["MASTER_PORT"] = os.environ.get("MREC_TEST_PORT", "29613")
+    dist.init_process_group("nccl", rank=0, world_size=1, device_id=gpu)
+    try:
+        yield
+    finally:
+        dist.destroy_process_group()
+
+
+def test_world1_rccl_dp_sharded_deepfm_step_equals_unsharded(gpu, rccl_world1):
+    """Row-sharded tables + data-parallel dense tower with every collective issued
+    (all_to_all x3, one flat all_reduce + mrec_sgd_multi) == the single-process
+    fused step, bit for bit (the sum over one rank is exact)."""
+    from pytorchrec_amd.loss import BCEWithLogitsLoss
+    from pytorchrec_amd.sharding import ShardComm
+    a, b = _deepfm(gpu, False), _deepfm(gpu, True)
+    b.load_state_dict(a.state_dict())
+    b.embeddings.comm = ShardComm(force_collectives=True)
+    b.distribute(ShardComm(force_collectives=True))
+    data = {f"c_c_C{i}": t for i, t in enumerate(_ids(gpu, 256, 7))}
+    g = torch.Generator().manual_seed(8)
+    for i in range(13):
+        data[f"c_n_I{i}"] = torch.rand(256, generator=g).to(gpu)
+    data["label"] = (torch.rand(256, generator=g) < 0.25).to(torch.int32).to(gpu)
+    for m in (a, b):
+        m.compile(torch.optim.SGD(m.get_parameters(), lr=0.05), BCEWithLogitsLoss(), [], gpu)
+    assert b._dp_flat is not None and len(b._dp_flat[1]) == 8  # 2 MLP + head (W, b), w_dense, bias
+    la = [float(a.train_step(data)["loss"].detach()) for _ in range(3)]
+    lb = [float(b.train_step(data)["loss"].detach()) for _ in range(3)]
+    assert la == lb
+    for (k, va), vb in zip(a.state_dict().items(), b.state_dict().values()):
+        assert torch.equal(va, vb), k
+
+
+def test_sgd_multi_matches_torch_and_weight_prep(gpu):
+    """mrec_sgd_multi: w -= lr g for several shapes in one launch, images equal
+    to mrec_weight_prep of the updated weight (pad columns zero)."""
+    from pytorchrec_amd import _mrec
+    from pytorchrec_amd.dense import weight_prep
+    shapes = [(400, 429), (1, 400), (13,), (1,), (37, 5)]
+    ws, jobs, keep = [], [], []
+    for sh in shapes:
+        w = torch.randn(*sh, device=gpu)
+        n, k = (1, w.numel()) if w.dim() < 2 else w.shape
+        ld = (k + 7) // 8 * 8
+        gbuf = torch.randn(n, ld, device=gpu)
+        want = (w.reshape(n, k).double() - 0.25 * gbuf[:, :k].double()).float()
+        img = None
+        if w.dim() == 2:
+            img = (torch.full((n, (k + 7) // 8 * 8), 7, dtype=torch.bfloat16, device=gpu),
+                   torch.full((k, (n + 7) // 8 * 8), 7, dtype=torch.bfloat16, device=gpu))
+        jobs.append(_mrec.SgdJob(w.data_ptr(), gbuf.data_ptr(), n, k, k, ld, 0.25,
+                                 _mrec.ptr(img[0]) if img else None, img[0].stride(0) if img else 0,
+                                 _mrec.ptr(img[1]) if img else None, img[1].stride(0) if img else 0))
+        ws.append((w, img, want))
+        keep.append(gbuf)
+    arr = (_mrec.SgdJob * len(jobs))(*jobs)
+    _mrec.call("mrec_sgd_multi", len(jobs), arr, _mrec.stream_handle())
+    for w, img, want in ws:
+        n, k = want.shape
+        torch.testing.assert_close(w.reshape(n, k), want, rtol=0, atol=1e-6)
+        if img is not None:
+            wr, wt = weight_prep(w)
+            assert torch.equal(img[0], wr) and torch.equal(img[1], wt)

@@ -486,12 +486,15 @@ def main():
         print(json.dumps(result), flush=True)
     # teardown: captured graphs hold RCCL kernels of the communicator, so they are
     # released (and the device drained) before the process group goes away
+    captured = graphs is not None
     del run, run_steps
     graphs = multi = g = None
     import gc
     gc.collect()
     torch.cuda.synchronize()
-    if torch.distributed.is_initialized():
+    if torch.distributed.is_initialized() and not captured:
+        torch.distributed.destroy_process_group()
+    elif torch.distributed.is_initialized():
         # destroy_process_group() hangs on this image once RCCL kernels were
         # captured in a HIP graph (measured at world 1: > 120 s); every rank has
         # finished its device work and rank 0 has printed, so leave without it

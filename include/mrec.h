@@ -211,6 +211,33 @@ mrec_status mrec_emb_bwd_apply(const mrec_table_bank *bank, int64_t batch, const
                                mrec_bwd_mode mode, float lr, uint64_t seed,
                                const uint64_t *d_step, void *grad, mrec_stream stream);
 
+/*
+ * Large-batch embedding backward (more than MREC_BWD_MAX_BATCH lookups per table,
+ * e.g. DIN's B x L history lookups; banks of <= 2^24 rows in total): a device-wide
+ * counting sort by row (plan) and ONE update per row with the sum of all its
+ * lookups (apply) — what aten::embedding_dense_backward + the optimizer step do
+ * for nn.Embedding (reached from FunkSVD.py:39-41 style
+ * tables), instead of one SGD step per 8192-lookup chunk.  Rows hit <= 16 times
+ * are summed in ascending sample order (as mrec_emb_bwd_apply); hotter rows are
+ * summed in 64-bit fixed point scaled to the row's largest gradient (exact,
+ * order-independent, bitwise reproducible).  Same arguments and modes as
+ * mrec_emb_bwd_plan / mrec_emb_bwd_apply; `batch` = lookups per table.
+ * The first mrec_emb_bwd_large_zero_bytes() bytes of the workspace must be zero
+ * before its first use (torch.zeros); every apply leaves them zero again.
+ */
+size_t mrec_emb_bwd_large_workspace_size(const mrec_table_bank *bank, int64_t batch);
+size_t mrec_emb_bwd_large_zero_bytes(const mrec_table_bank *bank, int64_t batch);
+mrec_status mrec_emb_bwd_large_plan(const mrec_table_bank *bank, const mrec_ids *ids, int64_t batch,
+                                    void *workspace, size_t ws_bytes, int32_t *d_oob_flag,
+                                    mrec_stream stream);
+mrec_status mrec_emb_bwd_large_apply(const mrec_table_bank *bank, int64_t batch,
+                                     const void *workspace, size_t ws_bytes, const void *dx,
+                                     mrec_dtype dx_dtype, int64_t dx_ld, const float *dfm,
+                                     const float *fm_sum, const void *x0, mrec_dtype x0_dtype,
+                                     int64_t x0_ld, const float *dw, mrec_bwd_mode mode, float lr,
+                                     uint64_t seed, const uint64_t *d_step, void *grad,
+                                     mrec_stream stream);
+
 struct mrec_gemm_call_s; /* mrec_gemm_call, defined with the GEMM entry points below */
 
 /*

@@ -1,0 +1,197 @@
+// Embedding-backward apply helpers: the per-lookup gradient, the row update
+// (SGD with RNE / stochastic rounding, or dense-gradient accumulation) and the
+// register sort network.  Shared by the batched apply (emb_bwd.hip) and the
+// large-batch path (emb_bwd_large.hip).
+#pragma once
+#include "common.h"
+
+namespace mrec {
+
+struct ApplyArgs {
+  const void *dx;
+  int64_t dx_ld;
+  int dx_bf16;
+  const float *dfm;
+  const float *fm_sum;
+  const void *x0;
+  int64_t x0_ld;
+  int x0_bf16;
+  const float *dw;
+  int mode;
+  float lr;
+  uint64_t seed;
+  const uint64_t *d_step;
+  void *grad;
+  // per-lookup gradient rows given directly (owner side of a sharded table):
+  // lookup b of table f -> g_occ[idx * g_ld + e], idx = chunked(b) + f * chunk
+  const float *g_occ;
+  int64_t g_ld;
+  int64_t chunk;
+  int64_t chunk_stride;
+};
+
+template <int EPL>
+__device__ __forceinline__ void load_f32xN(const float *p, float *v) {
+#pragma unroll
+  for (int j = 0; j < EPL; j += 4) {
+    const float4 x = *reinterpret_cast<const float4 *>(p + j);
+    v[j] = x.x;
+    v[j + 1] = x.y;
+    v[j + 2] = x.z;
+    v[j + 3] = x.w;
+  }
+}
+
+template <int EPL>
+__device__ __forceinline__ void load_bf16xN(const uint16_t *p, float *v) {
+  if constexpr (EPL == 8) {
+    Vec<uint16_t>::to_f32(*reinterpret_cast<const uint4 *>(p), v);
+  } else {
+    const uint2 r = *reinterpret_cast<const uint2 *>(p);
+    v[0] = __uint_as_float(r.x << 16);
+    v[1] = __uint_as_float(r.x & 0xffff0000u);
+    v[2] = __uint_as_float(r.y << 16);
+    v[3] = __uint_as_float(r.y & 0xffff0000u);
+  }
+}
+
+// gradient of lookup (b, f) for this lane's EPL elements (w lane: g[0])
+template <int EPL>
+__device__ __forceinline__ void lookup_grad(const ApplyArgs &a, int64_t b, int f, int D, int e0,
+                                            bool v_lane, bool w_lane, float *g) {
+#pragma unroll
+  for (int j = 0; j < EPL; ++j) g[j] = 0.f;
+  if (a.g_occ) {
+    const int64_t idx = a.chunk ? (b / a.chunk) * a.chunk_stride + f * a.chunk + b % a.chunk : b;
+    const float *go = a.g_occ + idx * a.g_ld;
+    if (v_lane)
+      load_f32xN<EPL>(go + e0, g);
+    else if (w_lane)
+      g[0] = go[D];
+    return;
+  }
+  if (v_lane) {
+    // the same arithmetic as mrec_shard_lookup_grad, so sharded and unsharded
+    // updates agree
+    const int64_t col = static_cast<int64_t>(f) * D + e0;
+    if (a.dx) {
+      if (a.dx_bf16)
+        load_bf16xN<EPL>(static_cast<const uint16_t *>(a.dx) + b * a.dx_ld + col, g);
+      else
+        load_f32xN<EPL>(static_cast<const float *>(a.dx) + b * a.dx_ld + col, g);
+    }
+    if (a.dfm) {
+      const float c = a.dfm[b];
+      float s[EPL], v[EPL];
+      load_f32xN<EPL>(a.fm_sum + b * D + e0, s);
+      if (a.x0_bf16)
+        load_bf16xN<EPL>(static_cast<const uint16_t *>(a.x0) + b * a.x0_ld + col, v);
+      else
+        load_f32xN<EPL>(static_cast<const float *>(a.x0) + b * a.x0_ld + col, v);
+#pragma unroll
+      for (int j = 0; j < EPL; ++j) g[j] = fmaf(c, s[j] - v[j], g[j]);
+    }
+  } else if (w_lane && a.dw) {
+    g[0] = a.dw[b];
+  }
+}
+
+// per-lookup gradient first, then one add into the segment sum
+template <int EPL>
+__device__ __forceinline__ void add_lookup_grad(const ApplyArgs &a, int64_t b, int f, int D,
+                                                int e0, bool v_lane, bool w_lane, float *acc) {
+  float g[EPL];
+  lookup_grad<EPL>(a, b, f, D, e0, v_lane, w_lane, g);
+#pragma unroll
+  for (int j = 0; j < EPL; ++j) acc[j] += g[j];
+}
+
+template <typename T>
+__device__ __forceinline__ T *row_ptr(const BankArgs &bank, const ApplyArgs &a, int f,
+                                      int64_t row, int e0) {
+  const int64_t grow = bank.row_offset[f] + row;
+  const int64_t off = grow * static_cast<int64_t>(bank.row_stride) + e0;
+  return reinterpret_cast<T *>(a.mode == MREC_BWD_DENSE_GRAD ? static_cast<char *>(a.grad)
+                                                              : bank.data) +
+         off;
+}
+
+// new value of this lane's 16 bytes of the row from its old contents `raw`
+template <typename T>
+__device__ __forceinline__ void apply_row_raw(const BankArgs &bank, const ApplyArgs &a, int f,
+                                              int64_t row, int e0, bool v_lane, const float *acc,
+                                              const uint4 raw) {
+  constexpr int EPL = Vec<T>::EPL;
+  const int64_t grow = bank.row_offset[f] + row;
+  T *p = row_ptr<T>(bank, a, f, row, e0);
+  float old[EPL];
+  Vec<T>::to_f32(raw, old);
+  const int live = v_lane ? EPL : 1;  // w lane: only element D is live
+  float nv[EPL];
+#pragma unroll
+  for (int j = 0; j < EPL; ++j)
+    nv[j] = (a.mode == MREC_BWD_DENSE_GRAD) ? old[j] + acc[j] : fmaf(-a.lr, acc[j], old[j]);
+  uint4 out;
+  if constexpr (sizeof(T) == 4) {
+    const uint32_t o[4] = {raw.x, raw.y, raw.z, raw.w};
+    uint32_t w[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) w[j] = j < live ? __float_as_uint(nv[j]) : o[j];
+    out = make_uint4(w[0], w[1], w[2], w[3]);
+  } else {
+    const uint32_t o[4] = {raw.x, raw.y, raw.z, raw.w};
+    uint32_t w[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      uint16_t h[2];
+#pragma unroll
+      for (int q = 0; q < 2; ++q) {
+        const int j = 2 * k + q;
+        if (j < live) {
+          h[q] = (a.mode == MREC_BWD_SGD_SR)
+                     ? f32_to_bf16_sr(nv[j], hash3(a.seed, grow, static_cast<uint32_t>(e0 + j)))
+                     : f32_to_bf16_rne(nv[j]);
+        } else {
+          h[q] = static_cast<uint16_t>(q ? (o[k] >> 16) : (o[k] & 0xffffu));
+        }
+      }
+      w[k] = static_cast<uint32_t>(h[0]) | (static_cast<uint32_t>(h[1]) << 16);
+    }
+    out = make_uint4(w[0], w[1], w[2], w[3]);
+  }
+  *reinterpret_cast<uint4 *>(p) = out;
+}
+
+template <typename T>
+__device__ __forceinline__ void apply_row(const BankArgs &bank, const ApplyArgs &a, int f,
+                                          int64_t row, int e0, bool v_lane, const float *acc) {
+  const uint4 raw = *reinterpret_cast<const uint4 *>(row_ptr<T>(bank, a, f, row, e0));
+  apply_row_raw<T>(bank, a, f, row, e0, v_lane, acc, raw);
+}
+
+__device__ __forceinline__ void cswap(int &a, int &b) {
+  const int lo = min(a, b), hi = max(a, b);
+  a = lo;
+  b = hi;
+}
+
+// ascending bitonic network on r[0, N) (compile-time indices: stays in VGPRs)
+template <int N>
+__device__ __forceinline__ void bitonic_sort(int *r) {
+#pragma unroll
+  for (int k = 2; k <= N; k <<= 1)
+#pragma unroll
+    for (int j = k >> 1; j > 0; j >>= 1)
+#pragma unroll
+      for (int i = 0; i < N; ++i) {
+        const int l = i ^ j;
+        if (l > i) {
+          if ((i & k) == 0)
+            cswap(r[i], r[l]);
+          else
+            cswap(r[l], r[i]);
+        }
+      }
+}
+
+}  // namespace mrec

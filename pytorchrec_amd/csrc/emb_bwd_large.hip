@@ -1,0 +1,645 @@
+// Embedding backward for batches beyond one plan workgroup (> MREC_BWD_MAX_BATCH
+// lookups per table, e.g. DIN's B x L history lookups): a device-wide counting
+// sort by row, then one update per row.  Replaces the autograd of nn.Embedding
+// (aten::embedding_dense_backward) at these sizes, with the
+// same guarantees as the batched path: every row is updated ONCE with the sum of
+// all its lookups' gradients, and results are bitwise reproducible.
+//
+// plan  (5 launches): memset counts -> count (atomic per-row histogram) ->
+//       blocksum -> scan (segment starts, ascending unique-row list, long-segment
+//       work list) -> place (lookup indices into their row's segment; the order
+//       inside a segment follows the atomics, so it is NOT used for arithmetic).
+// apply (3 launches): a segment of <= 16 lookups is sorted by a register network
+//       and summed in ascending sample order (identical arithmetic to the batched
+//       path).  A longer (hot) segment is split into chunks summed in parallel in
+//       FIXED POINT: each gradient element is scaled by 2^S (S from the segment's
+//       max |g| and length, so the sum cannot overflow int64) and the int64
+//       partials are added with atomics — integer addition is associative, so the
+//       result does not depend on the order, and it is exact up to the one
+//       rounding of each term to 2^-S (relative 2^-45 of the largest term).
+#include <algorithm>
+
+#include "common.h"
+#include "emb_apply.h"
+
+namespace mrec {
+
+constexpr int kLgRowsPerBlock = 4096;  // scan block: 256 threads x 16 rows
+constexpr int kLgChunk = 2048;         // lookups per long-segment work item
+constexpr int kLgShort = 16;           // segments up to this: register sort
+constexpr int64_t kLgMaxRows = int64_t(1) << 24;
+constexpr int kLgApplyBlocks = 2048;   // grid-stride launches (device-side counts)
+
+// workspace layout (all offsets 256-B aligned)
+struct LgWs {
+  int32_t *hdr;     // [8]: 0 unique rows, 1 long segments, 2 chunks
+  int32_t *cnt;     // [R]
+  int32_t *start;   // [R]
+  int32_t *blk;     // [2 * nblk]: per scan block (lookups, nonzero rows)
+  int32_t *uniq;    // [U] global row (ascending)
+  int32_t *ustart;  // [U]
+  int32_t *ulen;    // [U]
+  int32_t *ulong;   // [U] long-segment index or -1
+  int32_t *perm;    // [N] lookup index b (table implied by the row)
+  int32_t *longs;   // [U] unique index of long segment L
+  int2 *chunks;     // [C] (L, chunk)
+  uint32_t *segmax; // [U] max |g| bits of long segment L (zero on entry, left zero)
+  long long *acc;   // [U * stride] fixed-point sums (zero on entry, left zero)
+};
+
+__host__ __device__ inline int64_t lg_align(int64_t x) { return (x + 255) & ~int64_t(255); }
+
+__host__ __device__ inline int64_t lg_ws_bytes(int64_t R, int64_t N, int stride, LgWs *w,
+                                               char *base) {
+  const int64_t nblk = (R + kLgRowsPerBlock - 1) / kLgRowsPerBlock;
+  const int64_t U = R < N ? R : N;
+  const int64_t C = N / kLgChunk + U + 1;
+  int64_t o = 0;
+  auto take = [&](int64_t bytes) {
+    const int64_t at = o;
+    o = lg_align(o + bytes);
+    return at;
+  };
+  const int64_t o_hdr = take(32), o_segmax = take(4 * U), o_acc = take(8 * U * stride);
+  const int64_t o_cnt = take(4 * R), o_start = take(4 * R), o_blk = take(8 * nblk);
+  const int64_t o_uniq = take(4 * U), o_ustart = take(4 * U), o_ulen = take(4 * U);
+  const int64_t o_ulong = take(4 * U), o_perm = take(4 * N), o_longs = take(4 * U);
+  const int64_t o_chunks = take(8 * C);
+  if (w) {
+    w->hdr = reinterpret_cast<int32_t *>(base + o_hdr);
+    w->segmax = reinterpret_cast<uint32_t *>(base + o_segmax);
+    w->acc = reinterpret_cast<long long *>(base + o_acc);
+    w->cnt = reinterpret_cast<int32_t *>(base + o_cnt);
+    w->start = reinterpret_cast<int32_t *>(base + o_start);
+    w->blk = reinterpret_cast<int32_t *>(base + o_blk);
+    w->uniq = reinterpret_cast<int32_t *>(base + o_uniq);
+    w->ustart = reinterpret_cast<int32_t *>(base + o_ustart);
+    w->ulen = reinterpret_cast<int32_t *>(base + o_ulen);
+    w->ulong = reinterpret_cast<int32_t *>(base + o_ulong);
+    w->perm = reinterpret_cast<int32_t *>(base + o_perm);
+    w->longs = reinterpret_cast<int32_t *>(base + o_longs);
+    w->chunks = reinterpret_cast<int2 *>(base + o_chunks);
+  }
+  return o;
+}
+
+// bytes that must be zero before the first call (every apply leaves them zero)
+__host__ inline int64_t lg_zero_bytes(int64_t R, int64_t N, int stride) {
+  const int64_t U = R < N ? R : N;
+  return lg_align(32) + lg_align(4 * U) + lg_align(8 * U * stride);
+}
+
+__device__ __forceinline__ int table_of_row(const BankArgs &bank, int64_t grow) {
+  int f = 0;
+  while (f + 1 < bank.n_tables && bank.row_offset[f + 1] <= grow) ++f;
+  return f;
+}
+
+// ---- plan -------------------------------------------------------------------
+// A wave's 64 lanes hold 64 consecutive lookups.  Equal rows in consecutive lanes
+// (a DIN history's PAD tail, Zipf repeats) form a run that takes ONE atomic for
+// the whole run: a hot row would otherwise serialise ~10^5 atomics on one L2
+// address (measured 1.5 ms per call at C4).
+struct Run {
+  int32_t r;     // global row, -1 = invalid / padding
+  int head;      // lane of the first lookup of this lane's run
+  int len;       // run length (valid at the head)
+};
+
+__device__ __forceinline__ Run lane_run(int32_t r) {
+  const int lane = threadIdx.x & 63;
+  const int32_t prev = __shfl_up(r, 1);
+  const bool change = lane == 0 || prev != r;
+  const uint64_t changes = __ballot(change);
+  const uint64_t upto = lane == 63 ? ~0ull : ((2ull << lane) - 1);
+  Run out;
+  out.r = r;
+  out.head = 63 - __clzll(changes & upto);
+  const uint64_t after = lane == 63 ? 0ull : (changes & ~upto);
+  out.len = (after ? __ffsll(static_cast<unsigned long long>(after)) - 1 : 64) - lane;
+  return out;
+}
+
+__device__ __forceinline__ int32_t lookup_row(const BankArgs &bank, const IdsArgs &ids, int64_t n,
+                                              int64_t i, int64_t total, int64_t *b_out,
+                                              int32_t *__restrict__ oob) {
+  if (i >= total) return -1;
+  const int f = static_cast<int>(i / n);
+  const int64_t b = i - f * n;
+  *b_out = b;
+  const int64_t id = load_id(ids, f, b);
+  if (id >= 0 && id < bank.rows[f]) return static_cast<int32_t>(bank.row_offset[f] + id);
+  if (oob && !(ids.pad_negative && id < 0)) *oob = 1;
+  return -1;
+}
+
+// Runs are further combined per workgroup in an LDS hash (a row's runs from
+// different samples, e.g. one PAD run per history): a workgroup covers
+// kLgIter * 256 consecutive lookups and pays ONE global atomic per distinct row
+// it holds in LDS; a run whose row finds no LDS slot within kLgProbe probes goes
+// to global memory directly.
+constexpr int kLgIter = 8;
+constexpr int kLgSlots = 2048;
+constexpr int kLgProbe = 8;
+constexpr uint32_t kLgEmpty = 0xffffffffu;
+
+__device__ __forceinline__ int lg_slot(uint32_t *key, int32_t r) {
+  uint32_t h = (static_cast<uint32_t>(r) * 2654435761u) >> 21;  // 11 bits
+  for (int p = 0; p < kLgProbe; ++p) {
+    const uint32_t old = atomicCAS(&key[h], kLgEmpty, static_cast<uint32_t>(r));
+    if (old == kLgEmpty || old == static_cast<uint32_t>(r)) return static_cast<int>(h);
+    h = (h + 1) & (kLgSlots - 1);
+  }
+  return -1;
+}
+
+__global__ __launch_bounds__(256) void lg_count_kernel(BankArgs bank, IdsArgs ids, int64_t n,
+                                                       LgWs w, int32_t *__restrict__ oob) {
+  __shared__ uint32_t key[kLgSlots];
+  __shared__ int32_t val[kLgSlots];
+  if (blockIdx.x == 0 && threadIdx.x < 8) w.hdr[threadIdx.x] = 0;
+  for (int i = threadIdx.x; i < kLgSlots; i += 256) {
+    key[i] = kLgEmpty;
+    val[i] = 0;
+  }
+  __syncthreads();
+  const int64_t total = n * bank.n_tables;
+  const int64_t base = static_cast<int64_t>(blockIdx.x) * 256 * kLgIter;
+  for (int it = 0; it < kLgIter; ++it) {
+    int64_t b;
+    const Run u = lane_run(lookup_row(bank, ids, n, base + it * 256 + threadIdx.x, total, &b,
+                                      oob));
+    if (u.r >= 0 && u.head == (threadIdx.x & 63)) {
+      const int h = lg_slot(key, u.r);
+      if (h >= 0)
+        atomicAdd(&val[h], u.len);
+      else
+        atomicAdd(&w.cnt[u.r], u.len);
+    }
+  }
+  __syncthreads();
+  for (int i = threadIdx.x; i < kLgSlots; i += 256)
+    if (key[i] != kLgEmpty) atomicAdd(&w.cnt[key[i]], val[i]);
+}
+
+// block reduce of two int32 values (256 threads), result valid in thread 0
+__device__ __forceinline__ int2 block_sum2(int a, int b, int2 *red) {
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) {
+    a += __shfl_xor(a, off);
+    b += __shfl_xor(b, off);
+  }
+  if (lane == 0) red[wid] = make_int2(a, b);
+  __syncthreads();
+  int2 s = make_int2(0, 0);
+  if (threadIdx.x == 0)
+    for (int k = 0; k < 4; ++k) {
+      s.x += red[k].x;
+      s.y += red[k].y;
+    }
+  return s;
+}
+
+__global__ __launch_bounds__(256) void lg_blocksum_kernel(int64_t R, LgWs w) {
+  __shared__ int2 red[4];
+  const int64_t r0 = static_cast<int64_t>(blockIdx.x) * kLgRowsPerBlock + threadIdx.x * 16;
+  int s = 0, nz = 0;
+  for (int j = 0; j < 16; ++j) {
+    const int c = r0 + j < R ? w.cnt[r0 + j] : 0;
+    s += c;
+    nz += c > 0;
+  }
+  const int2 t = block_sum2(s, nz, red);
+  if (threadIdx.x == 0) {
+    w.blk[2 * blockIdx.x] = t.x;
+    w.blk[2 * blockIdx.x + 1] = t.y;
+  }
+}
+
+__global__ __launch_bounds__(256) void lg_scan_kernel(int64_t R, int nblk, LgWs w) {
+  __shared__ int2 red[4];
+  __shared__ int2 wex[4];
+  __shared__ int2 base;
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  // prefix of the earlier blocks
+  int ps = 0, pn = 0;
+  for (int k = tid; k < static_cast<int>(blockIdx.x); k += 256) {
+    ps += w.blk[2 * k];
+    pn += w.blk[2 * k + 1];
+  }
+  const int2 p = block_sum2(ps, pn, red);
+  if (tid == 0) base = p;
+  __syncthreads();
+  const int64_t r0 = static_cast<int64_t>(blockIdx.x) * kLgRowsPerBlock + tid * 16;
+  int c[16];
+  int s = 0, nz = 0;
+#pragma unroll
+  for (int j = 0; j < 16; ++j) {
+    c[j] = r0 + j < R ? w.cnt[r0 + j] : 0;
+    s += c[j];
+    nz += c[j] > 0;
+  }
+  // exclusive scan over threads of (s, nz)
+  int is = s, in = nz;
+#pragma unroll
+  for (int off = 1; off < 64; off <<= 1) {
+    const int ts = __shfl_up(is, off), tn = __shfl_up(in, off);
+    if (lane >= off) {
+      is += ts;
+      in += tn;
+    }
+  }
+  if (lane == 63) wex[wid] = make_int2(is, in);
+  __syncthreads();
+  int es = base.x + is - s, en = base.y + in - nz;
+  for (int k = 0; k < wid; ++k) {
+    es += wex[k].x;
+    en += wex[k].y;
+  }
+  // long segments and their chunks: one reservation per wave (a per-row atomic on
+  // the two list counters serialised ~10^3 atomics on one address at C4)
+  int nl = 0, nc = 0;
+#pragma unroll
+  for (int j = 0; j < 16; ++j)
+    if (c[j] > kLgShort) {
+      ++nl;
+      nc += (c[j] + kLgChunk - 1) / kLgChunk;
+    }
+  int il = nl, ic = nc;
+#pragma unroll
+  for (int off = 1; off < 64; off <<= 1) {
+    const int tl = __shfl_up(il, off), tc = __shfl_up(ic, off);
+    if (lane >= off) {
+      il += tl;
+      ic += tc;
+    }
+  }
+  int bl = 0, bc = 0;
+  if (lane == 63 && il > 0) {
+    bl = atomicAdd(&w.hdr[1], il);
+    bc = atomicAdd(&w.hdr[2], ic);
+  }
+  int L = __shfl(bl, 63) + il - nl;
+  int cb = __shfl(bc, 63) + ic - nc;
+#pragma unroll
+  for (int j = 0; j < 16; ++j) {
+    const int64_t r = r0 + j;
+    if (r >= R) break;
+    w.start[r] = es;
+    if (c[j] > 0) {
+      w.uniq[en] = static_cast<int32_t>(r);
+      w.ustart[en] = es;
+      w.ulen[en] = c[j];
+      int32_t myL = -1;
+      if (c[j] > kLgShort) {
+        myL = L++;
+        w.longs[myL] = en;
+        const int nch = (c[j] + kLgChunk - 1) / kLgChunk;
+        for (int k = 0; k < nch; ++k) w.chunks[cb + k] = make_int2(myL, k);
+        cb += nch;
+      }
+      w.ulong[en] = myL;
+      ++en;
+    }
+    es += c[j];
+  }
+  if (blockIdx.x == static_cast<unsigned>(nblk - 1) && tid == 255) w.hdr[0] = en;
+}
+
+// the same workgroup ranges as lg_count_kernel: runs take consecutive positions
+// inside their row's LDS slot, the slot reserves its rows' positions with ONE
+// global atomic, then every lookup is written to its position
+__global__ __launch_bounds__(256) void lg_place_kernel(BankArgs bank, IdsArgs ids, int64_t n,
+                                                       LgWs w) {
+  __shared__ uint32_t key[kLgSlots];
+  __shared__ int32_t val[kLgSlots];
+  const int lane = threadIdx.x & 63;
+  for (int i = threadIdx.x; i < kLgSlots; i += 256) {
+    key[i] = kLgEmpty;
+    val[i] = 0;
+  }
+  __syncthreads();
+  const int64_t total = n * bank.n_tables;
+  const int64_t base = static_cast<int64_t>(blockIdx.x) * 256 * kLgIter;
+  int32_t row[kLgIter], bb[kLgIter], slot[kLgIter], off[kLgIter];
+#pragma unroll
+  for (int it = 0; it < kLgIter; ++it) {
+    int64_t b = 0;
+    const Run u = lane_run(lookup_row(bank, ids, n, base + it * 256 + threadIdx.x, total, &b,
+                                      nullptr));
+    int h = -1, k = 0;
+    if (u.r >= 0 && u.head == lane) {
+      h = lg_slot(key, u.r);
+      if (h >= 0)
+        k = atomicAdd(&val[h], u.len);  // offset inside the slot's block of positions
+      else
+        k = atomicSub(&w.cnt[u.r], u.len) - u.len;  // a global block of its own
+    }
+    h = __shfl(h, u.head);
+    k = __shfl(k, u.head);
+    row[it] = u.r;
+    bb[it] = static_cast<int32_t>(b);
+    slot[it] = h;
+    off[it] = k + (lane - u.head);
+  }
+  __syncthreads();
+  // one global reservation per slot: val becomes the slot's first position
+  for (int i = threadIdx.x; i < kLgSlots; i += 256)
+    if (key[i] != kLgEmpty) val[i] = atomicSub(&w.cnt[key[i]], val[i]) - val[i];
+  __syncthreads();
+#pragma unroll
+  for (int it = 0; it < kLgIter; ++it) {
+    if (row[it] < 0) continue;
+    const int pos = (slot[it] >= 0 ? val[slot[it]] : 0) + off[it];
+    w.perm[w.start[row[it]] + pos] = bb[it];
+  }
+}
+
+// ---- apply -------------------------------------------------------------------
+// pass 1 over the long segments' chunks: max |g| per segment (bits of a
+// non-negative float order like the float)
+template <typename T, int LPR>
+__global__ __launch_bounds__(256) void lg_longmax_kernel(BankArgs bank, int64_t n, LgWs w,
+                                                         ApplyArgs a) {
+  constexpr int EPL = Vec<T>::EPL;
+  constexpr int WPB = 256 / LPR;
+  const int worker = threadIdx.x / LPR, l = threadIdx.x % LPR, e0 = l * EPL;
+  const int D = bank.dim;
+  const bool v_lane = e0 + EPL <= D, w_lane = bank.has_w && e0 == D;
+  const int nchunks = w.hdr[2];
+  for (int j = blockIdx.x; j < nchunks; j += gridDim.x) {
+    const int2 ch = w.chunks[j];
+    const int u = w.longs[ch.x];
+    const int f = table_of_row(bank, w.uniq[u]);
+    const int s0 = w.ustart[u] + ch.y * kLgChunk;
+    const int s1 = min(w.ustart[u] + w.ulen[u], s0 + kLgChunk);
+    float m = 0.f;
+    if (v_lane || w_lane)
+      for (int i = s0 + worker; i < s1; i += WPB) {
+        float g[EPL];
+        lookup_grad<EPL>(a, w.perm[i], f, D, e0, v_lane, w_lane, g);
+#pragma unroll
+        for (int q = 0; q < EPL; ++q) m = fmaxf(m, fabsf(g[q]));
+      }
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) m = fmaxf(m, __shfl_xor(m, off));
+    if ((threadIdx.x & 63) == 0 && m > 0.f) atomicMax(&w.segmax[ch.x], __float_as_uint(m));
+  }
+}
+
+// fixed-point scale of long segment L: sum of len terms of |x| <= max stays < 2^62
+__device__ __forceinline__ int lg_scale(float mx, int len) {
+  if (!(mx > 0.f)) return 0;
+  int e;
+  frexpf(mx, &e);  // mx < 2^e
+  int lb = 0;
+  while ((1 << lb) < len) ++lb;  // len <= 2^lb
+  return 61 - e - lb;            // |sum| < 2^(e + lb + S) = 2^61
+}
+
+// pass 2: fixed-point chunk sums added into the segment's int64 accumulator
+template <typename T, int LPR>
+__global__ __launch_bounds__(256) void lg_longacc_kernel(BankArgs bank, int64_t n, LgWs w,
+                                                         ApplyArgs a, int stride) {
+  constexpr int EPL = Vec<T>::EPL;
+  constexpr int WPB = 256 / LPR;
+  __shared__ long long red[WPB][LPR * EPL];
+  const int worker = threadIdx.x / LPR, l = threadIdx.x % LPR, e0 = l * EPL;
+  const int D = bank.dim;
+  const bool v_lane = e0 + EPL <= D, w_lane = bank.has_w && e0 == D;
+  const int nchunks = w.hdr[2];
+  for (int j = blockIdx.x; j < nchunks; j += gridDim.x) {
+    const int2 ch = w.chunks[j];
+    const int u = w.longs[ch.x];
+    const int f = table_of_row(bank, w.uniq[u]);
+    const int s0 = w.ustart[u] + ch.y * kLgChunk;
+    const int s1 = min(w.ustart[u] + w.ulen[u], s0 + kLgChunk);
+    const int S = lg_scale(__uint_as_float(w.segmax[ch.x]), w.ulen[u]);
+    long long acc[EPL];
+#pragma unroll
+    for (int q = 0; q < EPL; ++q) acc[q] = 0;
+    if (v_lane || w_lane)
+      for (int i = s0 + worker; i < s1; i += WPB) {
+        float g[EPL];
+        lookup_grad<EPL>(a, w.perm[i], f, D, e0, v_lane, w_lane, g);
+#pragma unroll
+        for (int q = 0; q < EPL; ++q) acc[q] += llrint(ldexp(static_cast<double>(g[q]), S));
+      }
+#pragma unroll
+    for (int q = 0; q < EPL; ++q) red[worker][e0 + q] = acc[q];
+    __syncthreads();
+    for (int sft = WPB / 2; sft > 0; sft >>= 1) {
+      if (worker < sft) {
+#pragma unroll
+        for (int q = 0; q < EPL; ++q) red[worker][e0 + q] += red[worker + sft][e0 + q];
+      }
+      __syncthreads();
+    }
+    if (worker == 0 && (v_lane || w_lane)) {
+      long long *dst = w.acc + static_cast<int64_t>(ch.x) * stride + e0;
+#pragma unroll
+      for (int q = 0; q < EPL; ++q)
+        atomicAdd(reinterpret_cast<unsigned long long *>(dst + q),
+                  static_cast<unsigned long long>(red[0][e0 + q]));
+    }
+    __syncthreads();
+  }
+}
+
+// one update per unique row
+template <typename T, int LPR>
+__global__ __launch_bounds__(256) void lg_apply_kernel(BankArgs bank, int64_t n, LgWs w,
+                                                       ApplyArgs a, int stride) {
+  constexpr int EPL = Vec<T>::EPL;
+  constexpr int WPB = 256 / LPR;
+  if (a.d_step) a.seed += *a.d_step * 0x9e3779b97f4a7c15ull;
+  const int worker = threadIdx.x / LPR, l = threadIdx.x % LPR, e0 = l * EPL;
+  const int D = bank.dim;
+  const bool v_lane = e0 + EPL <= D, w_lane = bank.has_w && e0 == D;
+  if (!(v_lane || w_lane)) return;
+  const int nu = w.hdr[0];
+  for (int u = blockIdx.x * WPB + worker; u < nu; u += gridDim.x * WPB) {
+    const int64_t grow = w.uniq[u];
+    const int f = table_of_row(bank, grow);
+    const int64_t row = grow - bank.row_offset[f];
+    const int len = w.ulen[u];
+    float acc[EPL];
+#pragma unroll
+    for (int q = 0; q < EPL; ++q) acc[q] = 0.f;
+    const int L = w.ulong[u];
+    if (L < 0) {
+      int r[kLgShort];
+#pragma unroll
+      for (int j = 0; j < kLgShort; ++j) r[j] = j < len ? w.perm[w.ustart[u] + j] : INT_MAX;
+      if (len <= 4)
+        bitonic_sort<4>(r);
+      else if (len <= 8)
+        bitonic_sort<8>(r);
+      else
+        bitonic_sort<16>(r);
+#pragma unroll
+      for (int j = 0; j < kLgShort; ++j)
+        if (j < len) add_lookup_grad<EPL>(a, r[j], f, D, e0, v_lane, w_lane, acc);
+    } else {
+      const int S = lg_scale(__uint_as_float(w.segmax[L]), len);
+      long long *src = w.acc + static_cast<int64_t>(L) * stride + e0;
+#pragma unroll
+      for (int q = 0; q < EPL; ++q) {
+        acc[q] = static_cast<float>(ldexp(static_cast<double>(src[q]), -S));
+        src[q] = 0;  // left zero for the next call
+      }
+      if (l == 0) w.segmax[L] = 0u;
+    }
+    apply_row<T>(bank, a, f, row, e0, v_lane, acc);
+  }
+}
+
+}  // namespace mrec
+
+using namespace mrec;
+
+extern "C" {
+
+size_t mrec_emb_bwd_large_workspace_size(const mrec_table_bank *bank, int64_t batch) {
+  if (!bank || batch < 0 || bank->n_tables < 1) return 0;
+  int64_t R = 0;
+  for (int f = 0; f < bank->n_tables; ++f) R += bank->rows[f];
+  return static_cast<size_t>(lg_ws_bytes(R, batch * bank->n_tables, bank->row_stride, nullptr,
+                                         nullptr));
+}
+
+size_t mrec_emb_bwd_large_zero_bytes(const mrec_table_bank *bank, int64_t batch) {
+  if (!bank || batch < 0 || bank->n_tables < 1) return 0;
+  int64_t R = 0;
+  for (int f = 0; f < bank->n_tables; ++f) R += bank->rows[f];
+  return static_cast<size_t>(lg_zero_bytes(R, batch * bank->n_tables, bank->row_stride));
+}
+
+static mrec_status lg_setup(const mrec_table_bank *bank, int64_t batch, void *ws, size_t ws_bytes,
+                            BankArgs *ba, int *lpr, int64_t *R, LgWs *w) {
+  int eb;
+  mrec_status st = make_bank_args(bank, ba, &eb, lpr);
+  if (st != MREC_OK) return st;
+  MREC_CHECK_ARG(batch >= 0 && batch < (int64_t(1) << 31) / ba->n_tables,
+                 "batch * n_tables must be < 2^31");
+  MREC_CHECK_ARG(ws != nullptr, "workspace is NULL");
+  *R = 0;
+  for (int f = 0; f < ba->n_tables; ++f) *R += ba->rows[f];
+  MREC_CHECK_ARG(*R <= kLgMaxRows, "total rows must be <= 2^24 for the large-batch path");
+  const int64_t need = lg_ws_bytes(*R, batch * ba->n_tables, ba->row_stride, w,
+                                   static_cast<char *>(ws));
+  if (ws_bytes < static_cast<size_t>(need)) {
+    set_error("large-batch workspace too small");
+    return MREC_ENOSPC;
+  }
+  return MREC_OK;
+}
+
+mrec_status mrec_emb_bwd_large_plan(const mrec_table_bank *bank, const mrec_ids *ids, int64_t batch,
+                                    void *workspace, size_t ws_bytes, int32_t *d_oob_flag,
+                                    mrec_stream stream) {
+  BankArgs ba;
+  IdsArgs ia;
+  int lpr;
+  int64_t R;
+  LgWs w;
+  mrec_status st = lg_setup(bank, batch, workspace, ws_bytes, &ba, &lpr, &R, &w);
+  if (st != MREC_OK) return st;
+  if ((st = make_ids_args(ids, ba.n_tables, &ia)) != MREC_OK) return st;
+  hipStream_t s = static_cast<hipStream_t>(stream);
+  if (batch == 0) return MREC_OK;  // (apply returns early for batch 0 as well)
+  if (hipMemsetAsync(w.cnt, 0, static_cast<size_t>(R) * 4, s) != hipSuccess)
+    return launch_status("mrec_emb_bwd_large_plan (memset)");
+  const int64_t total = batch * ba.n_tables;
+  const int nblk = static_cast<int>((R + kLgRowsPerBlock - 1) / kLgRowsPerBlock);
+  const unsigned gl = static_cast<unsigned>((total + 256 * kLgIter - 1) / (256 * kLgIter));
+  lg_count_kernel<<<dim3(gl), 256, 0, s>>>(ba, ia, batch, w, d_oob_flag);
+  lg_blocksum_kernel<<<dim3(nblk), 256, 0, s>>>(R, w);
+  lg_scan_kernel<<<dim3(nblk), 256, 0, s>>>(R, nblk, w);
+  lg_place_kernel<<<dim3(gl), 256, 0, s>>>(ba, ia, batch, w);
+  return launch_status("mrec_emb_bwd_large_plan");
+}
+
+mrec_status mrec_emb_bwd_large_apply(const mrec_table_bank *bank, int64_t batch,
+                                     const void *workspace, size_t ws_bytes, const void *dx,
+                                     mrec_dtype dx_dtype, int64_t dx_ld, const float *dfm,
+                                     const float *fm_sum, const void *x0, mrec_dtype x0_dtype,
+                                     int64_t x0_ld, const float *dw, mrec_bwd_mode mode, float lr,
+                                     uint64_t seed, const uint64_t *d_step, void *grad,
+                                     mrec_stream stream) {
+  BankArgs ba;
+  int lpr;
+  int64_t R;
+  LgWs w;
+  mrec_status st = lg_setup(bank, batch, const_cast<void *>(workspace), ws_bytes, &ba, &lpr, &R,
+                            &w);
+  if (st != MREC_OK) return st;
+  MREC_CHECK_ARG(mode == MREC_BWD_DENSE_GRAD || mode == MREC_BWD_SGD || mode == MREC_BWD_SGD_SR,
+                 "bad mode");
+  MREC_CHECK_ARG(mode != MREC_BWD_DENSE_GRAD || grad != nullptr, "DENSE_GRAD needs grad");
+  const int F = ba.n_tables, D = ba.dim;
+  if (dx) {
+    MREC_CHECK_ARG(dx_dtype == MREC_F32 || dx_dtype == MREC_BF16, "dx dtype must be F32/BF16");
+    const int xb = dx_dtype == MREC_F32 ? 4 : 2;
+    MREC_CHECK_ARG(dx_ld >= static_cast<int64_t>(F) * D, "dx_ld < F*dim");
+    MREC_CHECK_ARG((reinterpret_cast<uintptr_t>(dx) & 15) == 0 && (dx_ld * xb) % 16 == 0,
+                   "dx must be 16B aligned with 16B-multiple rows");
+  }
+  if (dfm) {
+    MREC_CHECK_ARG(fm_sum != nullptr && x0 != nullptr, "dfm needs fm_sum and x0");
+    MREC_CHECK_ARG(x0_dtype == MREC_F32 || x0_dtype == MREC_BF16, "x0 dtype must be F32/BF16");
+    const int xb = x0_dtype == MREC_F32 ? 4 : 2;
+    MREC_CHECK_ARG(x0_ld >= static_cast<int64_t>(F) * D, "x0_ld < F*dim");
+    MREC_CHECK_ARG((reinterpret_cast<uintptr_t>(x0) & 15) == 0 && (x0_ld * xb) % 16 == 0 &&
+                       (reinterpret_cast<uintptr_t>(fm_sum) & 15) == 0,
+                   "x0/fm_sum must be 16B aligned with 16B-multiple rows");
+  }
+  MREC_CHECK_ARG(dw == nullptr || ba.has_w, "dw given but bank has no w column");
+  ApplyArgs a = {};
+  a.dx = dx;
+  a.dx_ld = dx_ld;
+  a.dx_bf16 = dx_dtype == MREC_BF16;
+  a.dfm = dfm;
+  a.fm_sum = fm_sum;
+  a.x0 = x0;
+  a.x0_ld = x0_ld;
+  a.x0_bf16 = x0_dtype == MREC_BF16;
+  a.dw = dw;
+  a.mode = mode;
+  a.lr = lr;
+  a.seed = seed;
+  a.d_step = d_step;
+  a.grad = grad;
+  if (batch == 0) return MREC_OK;
+  hipStream_t s = static_cast<hipStream_t>(stream);
+  const int stride = ba.row_stride;
+  const dim3 g(kLgApplyBlocks);
+#define MREC_LG(T, L)                                                         \
+  do {                                                                        \
+    lg_longmax_kernel<T, L><<<g, 256, 0, s>>>(ba, batch, w, a);               \
+    lg_longacc_kernel<T, L><<<g, 256, 0, s>>>(ba, batch, w, a, stride);       \
+    lg_apply_kernel<T, L><<<g, 256, 0, s>>>(ba, batch, w, a, stride);         \
+  } while (0)
+  if (bank->dtype == MREC_BF16) {
+    switch (lpr) {
+      case 1: MREC_LG(uint16_t, 1); break;
+      case 2: MREC_LG(uint16_t, 2); break;
+      case 4: MREC_LG(uint16_t, 4); break;
+      case 8: MREC_LG(uint16_t, 8); break;
+      default: MREC_LG(uint16_t, 16); break;
+    }
+  } else {
+    switch (lpr) {
+      case 1: MREC_LG(float, 1); break;
+      case 2: MREC_LG(float, 2); break;
+      case 4: MREC_LG(float, 4); break;
+      case 8: MREC_LG(float, 8); break;
+      default: MREC_LG(float, 16); break;
+    }
+  }
+#undef MREC_LG
+  return launch_status("mrec_emb_bwd_large_apply");
+}
+
+}  // extern "C"

@@ -288,6 +288,44 @@ def _chunks(batch: int):
     return [(s, min(step, batch - s)) for s in range(0, batch, step)] or [(0, 0)]
 
 
+LARGE_MAX_ROWS = 1 << 24  # banks up to this many rows take the large-batch path
+# MREC_LARGE_BATCH=0: chunked plan/apply pairs instead (one SGD step per chunk)
+LARGE_BATCH = os.environ.get("MREC_LARGE_BATCH", "1") == "1"
+
+
+def _large_ws(bank: EmbeddingBank, batch: int) -> torch.Tensor:
+    """The large-batch workspace, kept on the bank per batch size: zeroed once at
+    allocation, every mrec_emb_bwd_large_apply leaves its zero region zero."""
+    cache = getattr(bank, "_large_ws_cache", None)
+    if cache is None or cache[0] != batch or cache[1].device != bank.weight.device:
+        nbytes = _mrec.lib().mrec_emb_bwd_large_workspace_size(bank.desc().ref(), batch)
+        cache = (batch, torch.zeros(nbytes, dtype=torch.uint8, device=bank.weight.device))
+        bank._large_ws_cache = cache
+    return cache[1]
+
+
+def _backward_large(bank: EmbeddingBank, ids, batch, grad, dx=None, dfm=None, fm_sum=None,
+                    x0=None, dw=None):
+    """One device-wide plan + ONE update per row for batches beyond a plan
+    workgroup (DIN's B x L history lookups): emb_bwd_large.hip."""
+    ws = _large_ws(bank, batch)
+    _mrec.call("mrec_emb_bwd_large_plan", bank.desc().ref(), _ids_desc(ids).ref(), batch,
+               ws.data_ptr(), ws.numel(), None, _mrec.stream_handle())
+    if bank.update == "sgd":
+        mode = _mrec.BWD_SGD_SR if (bank.stochastic_rounding and
+                                    bank.weight.dtype == torch.bfloat16) else _mrec.BWD_SGD
+        lr = bank.current_lr()
+    else:
+        mode, lr = _mrec.BWD_DENSE_GRAD, 0.0
+    _mrec.call("mrec_emb_bwd_large_apply", bank.desc().ref(), batch, ws.data_ptr(), ws.numel(),
+               _mrec.ptr(dx), _mrec.dtype_code(dx.dtype) if dx is not None else _mrec.F32,
+               dx.stride(0) if dx is not None else 0, _mrec.ptr(dfm), _mrec.ptr(fm_sum),
+               _mrec.ptr(x0), _mrec.dtype_code(x0.dtype) if x0 is not None else _mrec.F32,
+               x0.stride(0) if x0 is not None else 0, _mrec.ptr(dw), mode, float(lr),
+               bank.next_seed(), bank.step_counter().data_ptr(), _mrec.ptr(grad),
+               _mrec.stream_handle())
+
+
 def _backward_into_bank(bank: EmbeddingBank, ids, batch, plan_ws, dx=None, dfm=None,
                         fm_sum=None, x0=None, dw=None):
     """Shared backward: returns the dense grad (dense mode) or None (fused SGD)."""
@@ -297,6 +335,9 @@ def _backward_into_bank(bank: EmbeddingBank, ids, batch, plan_ws, dx=None, dfm=N
     if plan_ws is not None:
         ws, wsb = plan_ws.get() if isinstance(plan_ws, (_AsyncPlan, _FusedPlan)) else plan_ws
         _apply(bank, ws, wsb, batch, dx, dfm, fm_sum, x0, dw, grad)
+        return grad
+    if batch > _mrec.BWD_MAX_BATCH and bank.total_rows <= LARGE_MAX_ROWS and LARGE_BATCH:
+        _backward_large(bank, ids, batch, grad, dx, dfm, fm_sum, x0, dw)
         return grad
     for s, c in _chunks(batch):
         if c == 0:

@@ -316,20 +316,85 @@ def test_dense_grad_bit_exact_ascending_order(gpu, B):
         assert np.all(np.abs(got[o:o + n] - want) <= 1e-6 * mag + 1e-30), f
 
 
-def test_backward_large_batch_is_chunked(gpu):
-    """B > MREC_BWD_MAX_BATCH runs as sequential plan/apply chunks."""
+def _large_case(rng, nums, B):
+    """ids with every segment kind: rows hit once, 2..16 times (register sort),
+    17..2048 (one fixed-point chunk), and one row per table hit > 2048 times
+    (several chunks), plus a DIN-like PAD row 0."""
+    cols = []
+    for n in nums:
+        x = rng.integers(0, n, B)
+        x[rng.random(B) < 0.3] = 0                      # hot PAD row: ~0.3 B lookups
+        if n > 64:
+            x[rng.random(B) < 0.05] = rng.integers(1, 40, 1)[0]  # a second hot row
+        cols.append(x)
+    return np.stack(cols, 1)
+
+
+@pytest.mark.parametrize("B,nums", [(20000, [63002, 802]), (9000, [5, 70001, 1])])
+def test_backward_large_batch_dense_grad(gpu, B, nums):
+    """B > MREC_BWD_MAX_BATCH: device-wide plan + ONE accumulation per row
+    (emb_bwd_large.hip).  Rows hit <= 16 times: bitwise equal to sequential fp32
+    np.add.at (ascending sample order); hotter rows (fixed-point sums): within fp32
+    rounding of the fp64 oracle; bitwise reproducible run to run."""
     from pytorchrec_amd.embedding import gather
-    rng = np.random.default_rng(13)
-    B = 40000
-    bank = _bank([700], 8, False, torch.float32, update="dense")
-    _fill(bank, [rng.standard_normal((700, 8)).astype(np.float32)])
-    ids_np = rng.integers(0, 700, B)
-    out = gather(bank, [torch.from_numpy(ids_np).to(gpu)])
-    dy = rng.standard_normal((B, 8)).astype(np.float32)
+    rng = np.random.default_rng(B)
+    D, F = 16, len(nums)
+    bank = _bank(nums, D, False, torch.float32, update="dense")
+    _fill(bank, [np.zeros((n, D), np.float32) for n in nums])
+    ids_np = _large_case(rng, nums, B)
+    ids = [torch.from_numpy(ids_np[:, f].astype(np.int32)).to(gpu) for f in range(F)]
+    dy = (rng.standard_normal((B, F * D)) * 1e-3).astype(np.float32)
+    gather(bank, ids, out_dtype=torch.float32).backward(torch.from_numpy(dy).to(gpu))
+    got = bank.weight.grad[:, :D].detach().cpu().numpy().copy()
+    bank.weight.grad = None
+    gather(bank, ids, out_dtype=torch.float32).backward(torch.from_numpy(dy).to(gpu))
+    assert np.array_equal(got.view(np.uint32), bank.weight.grad[:, :D].cpu().numpy().view(np.uint32))
+    for f in range(F):
+        o, n = bank.row_offset[f], nums[f]
+        seq = np.zeros((n, D), np.float32)
+        np.add.at(seq, ids_np[:, f], dy[:, f * D:(f + 1) * D])
+        cnt = np.bincount(ids_np[:, f], minlength=n)
+        short = cnt <= 16
+        assert np.array_equal(got[o:o + n][short].view(np.uint32), seq[short].view(np.uint32)), f
+        want = ref.dense_grad(n, ids_np[:, f], dy[:, f * D:(f + 1) * D].astype(np.float64))
+        mag = ref.dense_grad(n, ids_np[:, f], np.abs(dy[:, f * D:(f + 1) * D]).astype(np.float64))
+        # hot rows (fixed point): one fp32 rounding of the exact sum (+ 2^-45 of the
+        # largest term per lookup)
+        hot = ~short
+        assert hot.any()
+        err = np.abs(got[o:o + n][hot] - want[hot])
+        assert np.all(err <= 2 ** -24 * np.abs(want[hot]) + 1e-12 * mag[hot] + 1e-30), f
+
+
+def test_backward_large_batch_sgd_one_update_per_row(gpu):
+    """Fused SGD at B > MREC_BWD_MAX_BATCH updates every touched row exactly once:
+    new = RNE_bf16(old - lr * sum g), equal to the fp64 oracle's sum rounded once
+    (within 1 bf16 ulp, where the fp32 sum may straddle a rounding boundary);
+    untouched rows keep their bits."""
+    from pytorchrec_amd.embedding import gather
+    rng = np.random.default_rng(3)
+    nums, D, B, lr = [63002, 802], 16, 30000, 0.5
+    bank = _bank(nums, D, False, torch.bfloat16, update="sgd")
+    bank.use_fused_sgd(lr)
+    bank.stochastic_rounding = False
+    tabs = [ref.f32_to_bf16_bits(rng.standard_normal((n, D)).astype(np.float32) * 0.1)
+            for n in nums]
+    _fill(bank, tabs)
+    before = _as_f32(_bits(bank.weight[:, :D]))
+    ids_np = _large_case(rng, nums, B)
+    ids = [torch.from_numpy(ids_np[:, f].astype(np.int32)).to(gpu) for f in range(2)]
+    dy = (rng.standard_normal((B, 2 * D)) * 1e-2).astype(np.float32)
+    out = gather(bank, ids, out_dtype=torch.float32)
     out.backward(torch.from_numpy(dy).to(gpu))
-    want = ref.dense_grad(700, ids_np, dy)
-    np.testing.assert_allclose(bank.weight.grad[:, :8].detach().cpu().numpy(), want, rtol=1e-5,
-                               atol=1e-5 * np.abs(want).max())
+    after = _as_f32(_bits(bank.weight[:, :D]))
+    for f in range(2):
+        o, n = bank.row_offset[f], nums[f]
+        g = ref.dense_grad(n, ids_np[:, f], dy[:, f * D:(f + 1) * D].astype(np.float64))
+        want = before[o:o + n].astype(np.float64) - lr * g
+        touched = np.bincount(ids_np[:, f], minlength=n) > 0
+        assert np.array_equal(after[o:o + n][~touched], before[o:o + n][~touched])
+        err = np.abs(after[o:o + n][touched] - want[touched])
+        assert np.all(err <= ref.bf16_ulp(want[touched]) * 1.01), f
 
 
 def test_fm2_dense_kernel(gpu):

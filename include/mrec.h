@@ -465,6 +465,19 @@ mrec_status mrec_weight_prep(const float *W, int64_t N, int64_t K, int64_t ldw, 
                              int64_t ldr, void *tr, int64_t ldt, mrec_stream stream);
 
 /*
+ * DCN-v2 cross-network backward, elementwise stage of layer l (bf16 [M, d] rows,
+ * SURVEY.md §8(a) A10): dz = g*x0; acc = (acc_init ? 0 : acc) + g*z (fp32); if
+ * addend != NULL, addend = bf16(acc + g) (layer 0: its dx_l GEMM adds it and
+ * yields dx0).  All rows hold round8(d) columns, 16-byte aligned; pad columns of
+ * dz / acc / addend are zeroed.
+ */
+mrec_status mrec_dcn_cross_bwd_prep(int64_t M, int64_t d, const void *g, int64_t ldg,
+                                    const void *x0, int64_t ldx0, const void *z, int64_t ldz,
+                                    void *dz, int64_t lddz, float *acc, int64_t ldacc,
+                                    int32_t acc_init, void *addend, int64_t ldadd,
+                                    mrec_stream stream);
+
+/*
  * Data-parallel dense update: for each job, w -= lr * g over an fp32 [N, K]
  * parameter (row strides ldw / ldg; a vector is N = 1), then the weight's bf16
  * images are re-emitted from the new w like mrec_weight_prep (`img_row` [N, ld_row]

@@ -176,6 +176,8 @@ SIGNATURES = {
                                           ctypes.POINTER(HeadFinishJob), _vp]),
     "mrec_weight_prep": (ctypes.c_int, [_vp, _i64, _i64, _i64, _vp, _i64, _vp, _i64, _vp]),
     "mrec_sgd_multi": (ctypes.c_int, [_i32, ctypes.POINTER(SgdJob), _vp]),
+    "mrec_dcn_cross_bwd_prep": (ctypes.c_int, [_i64, _i64, _vp, _i64, _vp, _i64, _vp, _i64, _vp,
+                                               _i64, _vp, _i64, _i32, _vp, _i64, _vp]),
     "mrec_emb_bwd_large_workspace_size": (ctypes.c_size_t, [_bank_p, _i64]),
     "mrec_emb_bwd_large_zero_bytes": (ctypes.c_size_t, [_bank_p, _i64]),
     "mrec_emb_bwd_large_plan": (ctypes.c_int, [_bank_p, _ids_p, _i64, _vp, ctypes.c_size_t, _vp,

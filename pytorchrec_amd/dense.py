@@ -21,7 +21,7 @@ from __future__ import annotations
 
 import ctypes
 import os
-from typing import Optional
+from typing import Optional, Sequence
 
 import torch
 import torch.nn.functional as F
@@ -123,7 +123,7 @@ class _Call:
 
     def __init__(self, A, a_layout, B, b_layout, M, N, K, phase, *, ones_out=None, b_cols=None,
                  mask=None, out=None, out_dtype=_BF16, split_k=1, sgd_lr=None, img_row=None,
-                 img_tr=None, ws=None):
+                 img_tr=None, ws=None, add=None):
         dev = A.device
         if out is None:
             out = _alloc(M, N, out_dtype, dev)
@@ -131,8 +131,9 @@ class _Call:
         if ws_bytes and ws is None:
             ws = torch.empty(ws_bytes, dtype=torch.uint8, device=dev)
         self.out, self.ws = out, ws
-        self.keep = [A, B, ones_out, mask, img_row, img_tr, out, ws]
-        self.epi = _mrec.Epilogue(None, 0, None, 0, None, 0, None, 0,
+        self.keep = [A, B, ones_out, mask, img_row, img_tr, out, ws, add]
+        self.epi = _mrec.Epilogue(None, 0, None, 0,
+                                  _mrec.ptr(add), add.stride(0) if add is not None else 0, None, 0,
                                   _mrec.ptr(mask), mask.stride(0) if mask is not None else 0,
                                   _mrec.ptr(ones_out), int(sgd_lr is not None),
                                   float(sgd_lr) if sgd_lr is not None else 0.0,
@@ -145,7 +146,7 @@ class _Call:
         self.phase = phase
         self.writes = {p for p in (out.data_ptr(), _mrec.ptr(ones_out), _mrec.ptr(img_row),
                                    _mrec.ptr(img_tr)) if p}
-        self.reads = {A.data_ptr(), B.data_ptr()}
+        self.reads = {A.data_ptr(), B.data_ptr()} | ({add.data_ptr()} if add is not None else set())
 
     def with_phase(self, phase):
         c = object.__new__(_Call)
@@ -501,6 +502,103 @@ class _CrossFn(torch.autograd.Function):
         if x0.shape[1] > d:
             dx0 = F.pad(dx0, (0, x0.shape[1] - d))
         return dx0, dxl, dW, db
+
+
+class _CrossNetFn(torch.autograd.Function):
+    """The whole DCN-v2 cross network x_{l+1} = x0 * (x_l W_l^T + b_l) + x_l,
+    l = 0..L-1, as one autograd node: forward = one fused GEMM per layer; backward
+    per layer = ONE elementwise kernel (mrec_dcn_cross_bwd_prep: dz = g*x0 and the
+    fp32 sum over layers of g*z, i.e. x0's multiplier gradient) + the dx_l GEMM
+    (layer 0 adds that sum, so its output is dx0) + the dW GEMM (fused SGD when
+    compiled with plain SGD, data-parallel gradient views, else returned)."""
+
+    @staticmethod
+    def forward(ctx, x0, n, *params):
+        weights, biases = params[:n], params[n:]
+        x0 = _bf16_rows(x0)
+        xl = x0
+        saved = []
+        for W, b in zip(weights, biases):
+            M = xl.shape[0]
+            d = W.shape[0]
+            wr, wt = weight_images(W)
+            bb = b.detach().float().contiguous() if b is not None else None
+            z = _alloc(M, d, _BF16, xl.device)
+            out = gemm(xl, _mrec.LAYOUT_ROW, wr[:, :d], _mrec.LAYOUT_ROW, M, d, d, bias=bb,
+                       mul=x0, add=xl, aux=z)
+            saved.append((xl, z, wr, wt))
+            xl = out
+        ctx.x0, ctx.saved, ctx.weights, ctx.biases = x0, saved, weights, biases
+        return xl
+
+    @staticmethod
+    def backward(ctx, g):
+        x0, saved = ctx.x0, ctx.saved
+        L = len(saved)
+        g = _bf16_rows(g)
+        M = g.shape[0]
+        d = saved[0][1].shape[1]
+        acc = torch.empty(M, _r8(d), dtype=torch.float32, device=g.device)
+        dWs, dbs = [None] * L, [None] * L
+        for l in reversed(range(L)):
+            xl, z, wr, wt = saved[l]
+            W, b = ctx.weights[l], ctx.biases[l]
+            dz = _alloc(M, d, _BF16, g.device)
+            addend = _alloc(M, xl.shape[1], _BF16, g.device) if l == 0 else None
+            _mrec.call("mrec_dcn_cross_bwd_prep", M, d, g.data_ptr(), g.stride(0),
+                       x0.data_ptr(), x0.stride(0), z.data_ptr(), z.stride(0), dz.data_ptr(),
+                       dz.stride(0), acc.data_ptr(), acc.stride(0), int(l == L - 1),
+                       _mrec.ptr(addend), addend.stride(0) if addend is not None else 0,
+                       _mrec.stream_handle())
+            # dx_l = dz W (+ g: x_l feeds the residual; layer 0: + sum_l g_l*z_l too)
+            add = addend if l == 0 else _pad_cols(g, xl.shape[1])
+            lr = sgd_lr(W, b)
+            dpg = dp_grads(W, b) if lr is None else None
+            if lr is not None or dpg is not None:
+                # one launch: dx GEMM + dW split-K slabs (+ the previous layer's deferred
+                # dW reduction); this layer's reduction rides in the next launch
+                cdx = _Call(dz, _mrec.LAYOUT_ROW, wt, _mrec.LAYOUT_ROW, M, xl.shape[1], d,
+                            _mrec.GEMM_FULL, b_cols=d, add=add)
+                sk = _DW_SPLIT or _split_beside(d, d + 1, M)
+                ph = _mrec.GEMM_PARTIAL if sk > 1 else _mrec.GEMM_FULL
+                if dpg is not None:
+                    cdw = _Call(dz, _mrec.LAYOUT_COL, xl, _mrec.LAYOUT_COL, d, d, M, ph,
+                                ones_out=dpg[1], out=dpg[0], out_dtype=torch.float32, split_k=sk)
+                else:
+                    cdw = _Call(dz, _mrec.LAYOUT_COL, xl, _mrec.LAYOUT_COL, d, d, M, ph,
+                                ones_out=b.detach() if b is not None else None, out=W.detach(),
+                                out_dtype=torch.float32, split_k=sk, sgd_lr=lr, img_row=wr,
+                                img_tr=wt)
+                if sk > 1:
+                    launch_multi([cdx, cdw])
+                    _defer(cdw)
+                elif dpg is not None:
+                    launch_multi([cdx, cdw])
+                else:  # the dW epilogue rewrites wt, which the dx GEMM reads
+                    launch_multi([cdx])
+                    launch_multi([cdw])
+                g = cdx.out
+                continue
+            flush_pending()
+            gx = gemm(dz, _mrec.LAYOUT_ROW, wt, _mrec.LAYOUT_ROW, M, xl.shape[1], d, b_cols=d,
+                      add=add)
+            dWs[l] = torch.empty(d, d, dtype=torch.float32, device=g.device)
+            dbs[l] = torch.empty(d, dtype=torch.float32, device=g.device) if b is not None else None
+            gemm(dz, _mrec.LAYOUT_COL, xl, _mrec.LAYOUT_COL, d, d, M, ones_out=dbs[l], out=dWs[l])
+            g = gx
+        ctx.saved = None
+        return (g, None, *dWs, *dbs)
+
+
+def cross_net(x0: torch.Tensor, weights: Sequence[torch.Tensor],
+              biases: Sequence[Optional[torch.Tensor]]) -> torch.Tensor:
+    """A stack of DCN-v2 cross layers over x0 (one autograd node on the GPU)."""
+    if not x0.is_cuda or any(b is None for b in biases):
+        x = x0
+        for W, b in zip(weights, biases):
+            x = cross(x0, x, W, b)
+        return x
+    return _CrossNetFn.apply(x0, len(weights), *weights, *biases)
 
 
 def _pad_cols(t: torch.Tensor, n: int) -> torch.Tensor:

@@ -72,9 +72,7 @@ class DCNv2(_CTRBase):
         x0, _ = interact(self.embeddings, self._ids(data), self._dense(data), None, None,
                          fm2=False, first_order=False, x0_cols=self.x0_cols,
                          x0_dtype=self._x0_dtype())
-        x = x0
-        for layer in self.cross:
-            x = dense_ops.cross(x0, x, layer.weight, layer.bias)
+        x = dense_ops.cross_net(x0, [c.weight for c in self.cross], [c.bias for c in self.cross])
         return self.mlp(x)
 
     def forward(self, data: Dict[str, Tensor]):

@@ -163,7 +163,10 @@ def test_mlp_matches_reference_golden_g6(gpu):
         np.testing.assert_allclose(g_, want, rtol=3e-2, atol=3e-2 * np.abs(want).max())
 
 
-def test_dcn_cross_forward_backward(gpu):
+@pytest.mark.parametrize("net", [False, True])
+def test_dcn_cross_forward_backward(gpu, net):
+    """net=False: layer by layer (dense.cross); net=True: the whole cross network as
+    one autograd node (dense.cross_net, mrec_dcn_cross_bwd_prep)."""
     from pytorchrec_amd import dense as D
     rng = np.random.default_rng(21)
     M, d = 256, 45
@@ -173,9 +176,12 @@ def test_dcn_cross_forward_backward(gpu):
     Wg = [w.to(gpu).requires_grad_() for w in W]
     bg = [v.to(gpu).requires_grad_() for v in b]
     x0g = x0.to(gpu).requires_grad_()
-    x = x0g
-    for i in range(3):
-        x = D.cross(x0g, x, Wg[i], bg[i])
+    if net:
+        x = D.cross_net(x0g, Wg, bg)
+    else:
+        x = x0g
+        for i in range(3):
+            x = D.cross(x0g, x, Wg[i], bg[i])
     dout = rng.standard_normal((M, d)).astype(np.float32)
     x.backward(torch.from_numpy(dout).to(gpu).to(x.dtype))
     layers = [(w.numpy(), v.numpy()) for w, v in zip(W, b)]
@@ -347,3 +353,41 @@ def test_ctr_head_bce_fused_matches_torch(gpu, gscale):
     # one bf16 rounding of dh; a second one when a non-unit loss gradient rescales it
     tol = 2 ** -8 if gscale == 1.0 else 2 ** -7
     torch.testing.assert_close(hh.grad.double(), want_dh, rtol=tol, atol=1e-7)
+
+
+def test_dcnv2_fused_step_matches_unfused(gpu):
+    """DCN-v2 train step with every dense update fused into the backward kernels
+    (cross network as one autograd node + multi-GEMM launches) == the same step
+    with gradients returned to torch.optim.SGD (up to fp32 fma-vs-mul-add)."""
+    from pytorchrec_amd.feature_column import CategoricalColumnWithIdentity, NumericColumn
+    from pytorchrec_amd.loss import BCEWithLogitsLoss
+    from pytorchrec_amd.model import DCNv2
+    nums = [50, 80, 3, 200]
+    sparse = [CategoricalColumnWithIdentity(n, f"c{f}") for f, n in enumerate(nums)]
+    dense = [NumericColumn(f"d{j}") for j in range(5)]
+    lab = CategoricalColumnWithIdentity(2, "label")
+    ms = [DCNv2(sparse, dense, lab, emb_size=16, cross_layers=3, layers=(64, 32), device=gpu,
+                random_seed=3) for _ in range(2)]
+    with torch.no_grad():
+        for p in ms[0].parameters():
+            if p.dim() == 2 and p.shape[0] == p.shape[1]:
+                p.mul_(20.0)  # cross weights large enough to matter
+    ms[1].load_state_dict(ms[0].state_dict())
+    for m in ms:
+        m.compile(torch.optim.SGD(m.get_parameters(), lr=0.05), BCEWithLogitsLoss(), [], gpu)
+    for p in ms[1].parameters():  # force the unfused path on model 1
+        if hasattr(p, "_mrec_sgd_group"):
+            del p._mrec_sgd_group
+    g = torch.Generator().manual_seed(9)
+    B = 512
+    data = {c.feature_name: torch.randint(0, c.category_num, (B,), generator=g).to(gpu)
+            for c in sparse}
+    data.update({c.feature_name: torch.rand(B, generator=g).to(gpu) for c in dense})
+    data["label"] = (torch.rand(B, generator=g) < 0.3).to(torch.int32).to(gpu)
+    for _ in range(2):
+        la = float(ms[0].train_step(data)["loss"].detach())
+        lb = float(ms[1].train_step(data)["loss"].detach())
+        assert abs(la - lb) <= 1e-5 * abs(lb), (la, lb)
+    for (k, va), vb in zip(ms[0].state_dict().items(), ms[1].state_dict().values()):
+        if "cross" in k or "mlp" in k or "prediction" in k:
+            torch.testing.assert_close(va.float(), vb.float(), rtol=1e-4, atol=1e-6, msg=k)

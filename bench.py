@@ -53,6 +53,8 @@ def parse():
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--cpu-seconds", type=float, default=12.0)
     p.add_argument("--no-roofline", action="store_true")
+    p.add_argument("--no-h2d", action="store_true",
+                   help="skip the PCIe-inclusive (host-fed columnar loader) measurement")
     p.add_argument("--shard", action="store_true",
                    help="row-sharded tables + DP even at N=1 (always on for N>1)")
     p.add_argument("--shard-cap", type=int, default=None,
@@ -284,6 +286,52 @@ class _Ctx:
 
 
 # ----------------------------------------------------------------------------
+# PCIe-inclusive rate: the same step fed from host memory by the columnar loader
+# ----------------------------------------------------------------------------
+
+def pcie_inclusive(step, args, sparse, dense_cols, label_col, device):
+    """Train steps whose batches start in HOST memory: ``ColumnarLoader`` packs the
+    epoch into pinned memory (outside the timed region, as a real epoch would be
+    prepared ahead), then each batch crosses PCIe as one DMA on a side stream,
+    ``depth - 1`` batches ahead, overlapped with the steps (one HIP graph per
+    loader slot).  Reported beside ``value``, never as it."""
+    from pytorchrec_amd.loader import ColumnarDataset, ColumnarLoader
+    B = args.batch
+    n_batches = max(args.steps, 12)
+    N = B * n_batches
+    g = torch.Generator().manual_seed(7)
+    cols = {c.feature_name: torch.randint(0, c.category_num, (N,), generator=g,
+                                          dtype=torch.int32) for c in sparse}
+    for c in dense_cols:
+        cols[c.feature_name] = torch.rand(N, generator=g)
+    cols[label_col.feature_name] = (torch.rand(N, generator=g) < 0.25).float()
+    ds = ColumnarDataset(cols, dense_group=[c.feature_name for c in dense_cols])
+    ld = ColumnarLoader(ds, B, device, depth=3)
+    for s, _ in ld.iter_slots():  # eager epoch: warms the model and fills every slot
+        step(ld.slot_views(s))
+    torch.cuda.synchronize()
+    graphs = []
+    for k in range(ld.depth):
+        gr = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(gr, capture_error_mode="thread_local"):
+            step(ld.slot_views(k))
+        graphs.append(gr)
+    ld.prepare_epoch()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    n = 0
+    for s, _ in ld.iter_slots():
+        graphs[s].replay()
+        n += 1
+    torch.cuda.synchronize()
+    el = time.perf_counter() - t0
+    return {"value": round(n * B / el, 1), "unit": "samples/s", "steps": n,
+            "ms_per_step": round(el / n * 1e3, 4), "h2d_bytes_per_step": ld.layout.slot_bytes,
+            "feed": "ColumnarLoader (pytorchrec_amd/loader.py), depth 3: one packed pinned "
+                    "H2D copy per batch on a side stream, one HIP graph per slot"}
+
+
+# ----------------------------------------------------------------------------
 # CPU baseline (oracle restatement of the reference path; rank 0, N = 1 only)
 # ----------------------------------------------------------------------------
 
@@ -480,6 +528,10 @@ def main():
         result["roofline_kernels"] = {k: {"avg_us": round(v[0] * 1e6, 3), "bytes": v[1],
                                           "GB/s": round(v[1] / v[0] / 1e9, 1)}
                                       for k, v in ks.items()}
+    if (world == 1 and not sharded and not args.no_h2d and not args.no_graph
+            and args.model == "deepfm"):
+        result["pcie_inclusive"] = pcie_inclusive(step, args, sparse, dense_cols, label_col,
+                                                  device)
     if rank == 0 and world == 1 and not args.no_cpu_baseline and args.model == "deepfm":
         result["cpu_baseline"] = cpu_baseline(args)
     if rank == 0:

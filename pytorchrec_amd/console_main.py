@@ -61,6 +61,9 @@ def parse(argv=None):
     p.add_argument("--l2", type=float, default=0.0)
     p.add_argument("--loss", default="bce", choices=["bce"])
     p.add_argument("--num_workers", type=int, default=0)
+    p.add_argument("--loader", default="columnar", choices=["columnar", "dataloader"],
+                   help="columnar: packed pinned batches (pytorchrec_amd/loader.py); "
+                        "dataloader: the reference's per-sample DataLoader path")
     p.add_argument("--dev_freq", type=int, default=1)
     p.add_argument("--emb_size", type=int, default=16)
     p.add_argument("--train_rows", type=int, default=1_000_209, help="ML-1M has 1,000,209 ratings")
@@ -91,13 +94,15 @@ def main(argv=None) -> dict:
            else torch.optim.Adam(params, lr=a.lr, weight_decay=a.l2))
     metrics = [get_metric(m) for m in a.metrics.split(",") if m.strip()]
     model.compile(opt, get_loss(a.loss)(), metrics, device)
-    train = _Rows(synthetic_ml1m(a.train_rows, a.random_seed))
-    dev = _Rows(synthetic_ml1m(a.dev_rows, a.random_seed + 1))
+    from pytorchrec_amd.loader import ColumnarDataset
+    wrap = ColumnarDataset if a.loader == "columnar" else _Rows
+    train = wrap(synthetic_ml1m(a.train_rows, a.random_seed))
+    dev = wrap(synthetic_ml1m(a.dev_rows, a.random_seed + 1))
     t0 = time.perf_counter()
     history = model.fit(train, a.batch_size, a.epoch, dev_dataset=dev, verbose=1,
                         workers=a.num_workers, dev_freq=a.dev_freq)
     secs = time.perf_counter() - t0
-    out = {"model": a.model_name, "device": str(device), "epochs": a.epoch,
+    out = {"model": a.model_name, "device": str(device), "epochs": a.epoch, "loader": a.loader,
            "train_rows": a.train_rows, "samples_per_s": round(a.epoch * a.train_rows / secs, 1),
            "history": history}
     print(json.dumps(out), flush=True)

@@ -290,6 +290,19 @@ class IModel(Module, IWithArguments, ABC):
         return prediction
 
     def _loader(self, dataset, batch_size, shuffle=False, workers=0, drop_last=False):
+        """A ``ColumnarDataset`` is fed by the pipelined columnar loader (one packed
+        H2D copy per batch, overlapped with the steps; pytorchrec_amd/loader.py);
+        any other dataset by the reference's per-sample DataLoader."""
+        from pytorchrec_amd.loader import ColumnarDataset, ColumnarLoader
+        if isinstance(dataset, ColumnarDataset):
+            key = (id(dataset), int(batch_size), bool(shuffle), bool(drop_last))
+            cache = self.__dict__.setdefault("_columnar_loaders", {})
+            ld = cache.get(key)
+            if ld is None or ld.device != self.compiled_device:
+                ld = ColumnarLoader(dataset, batch_size, self.compiled_device, shuffle=shuffle,
+                                    drop_last=drop_last)
+                cache[key] = ld
+            return ld
         from torch.utils.data import DataLoader
         return DataLoader(dataset=dataset, batch_size=batch_size, shuffle=shuffle,
                           num_workers=workers, drop_last=drop_last)

@@ -29,3 +29,16 @@ def test_metrics_match_definitions():
     want_ll = -np.mean(y * np.log(p) + (1 - y) * np.log(1 - p))
     assert abs(LogLoss()(z, y) - want_ll) < 1e-9
     assert AUC()(z, np.ones_like(z)) != AUC()(z, np.ones_like(z))  # nan: one class only
+
+
+def test_cli_columnar_and_dataloader_paths_agree():
+    """Both feeds run the CLI end to end (exact equality of the two feeds is
+    checked in tests/test_loader.py with shuffling off; here fit shuffles, and
+    the two feeds draw their permutations from different generators)."""
+    outs = [console_main.main(["--model_name", "fm", "--gpu", "-1", "--epoch", "1",
+                               "--batch_size", "1024", "--train_rows", "6000", "--dev_rows",
+                               "2000", "--lr", "0.1", "--loader", ld])
+            for ld in ("columnar", "dataloader")]
+    assert [o["loader"] for o in outs] == ["columnar", "dataloader"]
+    for o in outs:
+        assert np.isfinite(o["history"][0]["loss"]) and 0.0 <= o["history"][0]["auc"] <= 1.0

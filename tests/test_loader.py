@@ -142,7 +142,13 @@ def test_gpu_pipelined_batches_bit_exact_and_training_matches_resident(gpu):
     n, batch = 1000, 128
     cols = _columns(n, seed=1)
     ds = _dataset(n, seed=1)
-    ld = ColumnarLoader(ds, batch, device=gpu, shuffle=True, seed=11, depth=2)
+    for side in (False, True):
+        _check_pipelined(ColumnarLoader(ds, batch, device=gpu, shuffle=True, seed=11, depth=2,
+                                        side_stream=side), cols, n, batch)
+    _check_training(cols, n, batch, gpu)
+
+
+def _check_pipelined(ld, cols, n, batch):
     order = torch.randperm(n, generator=torch.Generator().manual_seed(11))
     seen = []
     for j, b in enumerate(ld):
@@ -156,6 +162,9 @@ def test_gpu_pipelined_batches_bit_exact_and_training_matches_resident(gpu):
         assert torch.equal(b["c_c_C0"].cpu(), want["c_c_C0"]), j
     assert len(seen) == len(ld) == 8
 
+
+def _check_training(cols, n, batch, gpu):
+    from pytorchrec_amd.loss import BCEWithLogitsLoss
     # DeepFM trained through the loader == trained on the same batches made resident
     cols.pop("pos_his")
     cds = ColumnarDataset(cols, dense_group=[f"c_n_I{j}" for j in range(N_DENSE)])

@@ -292,7 +292,7 @@ class _Ctx:
 def pcie_inclusive(step, args, sparse, dense_cols, label_col, device):
     """Train steps whose batches start in HOST memory: ``ColumnarLoader`` packs the
     epoch into pinned memory (outside the timed region, as a real epoch would be
-    prepared ahead), then each batch crosses PCIe as one DMA enqueued
+    prepared ahead), then each batch crosses PCIe as one copy kernel enqueued
     ``depth - 1`` batches ahead on the step's stream (one HIP graph per loader
     slot).  Reported beside ``value``, never as it."""
     from pytorchrec_amd.loader import ColumnarDataset, ColumnarLoader
@@ -328,8 +328,8 @@ def pcie_inclusive(step, args, sparse, dense_cols, label_col, device):
     return {"value": round(n * B / el, 1), "unit": "samples/s", "steps": n,
             "ms_per_step": round(el / n * 1e3, 4), "h2d_bytes_per_step": ld.layout.slot_bytes,
             "feed": "ColumnarLoader (pytorchrec_amd/loader.py), depth 3: one packed pinned "
-                    "H2D copy per batch, enqueued ahead on the step stream, one HIP graph "
-                    "per slot"}
+                    "record per batch copied by mrec_batch_stage (kernel reading the host "
+                    "record over PCIe), enqueued ahead on the step stream, one HIP graph per slot"}
 
 
 # ----------------------------------------------------------------------------

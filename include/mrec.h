@@ -32,7 +32,7 @@
 extern "C" {
 #endif
 
-#define MREC_ABI_VERSION 9
+#define MREC_ABI_VERSION 10
 #define MREC_MAX_TABLES 64      /* tables per table bank / per call */
 #define MREC_BWD_MAX_BATCH 8192  /* lookups per table per plan/apply call */
 #define MREC_BWD_HASH_MAX_BATCH 4096  /* batches up to this use the hash plan */
@@ -498,6 +498,19 @@ typedef struct {
 } mrec_sgd_job;
 
 mrec_status mrec_sgd_multi(int32_t n, const mrec_sgd_job *jobs, mrec_stream stream);
+
+/* ------------------------------------------------------------------------- */
+/* Batch feed                                                                 */
+/* ------------------------------------------------------------------------- */
+
+/* Copy one packed batch record (pytorchrec_amd/loader.py PackedLayout) from
+ * PINNED, device-visible host memory into its device slot with a kernel on
+ * `stream` (the compute queue reads the host pages over PCIe; no DMA engine, so
+ * a graph launched behind it does not wait on the host).  16-B aligned, bytes a
+ * multiple of 16.  Replaces the per-tensor blocking `.to(device)` of
+ * IModel.train_step (torchrec/model/IModel.py:119) fed by
+ * SimpleDataReader.__getitem__ (torchrec/data/SimpleDataReader.py:323-331). */
+mrec_status mrec_batch_stage(void *dst, const void *host_src, int64_t bytes, mrec_stream stream);
 
 /* ------------------------------------------------------------------------- */
 /* CTR head and loss                                                          */

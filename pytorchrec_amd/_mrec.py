@@ -20,7 +20,7 @@ import torch  # noqa: F401  (must precede the dlopen, see module docstring)
 LIB_DIR = os.path.join(os.path.dirname(os.path.abspath(__file__)), "lib")
 LIB_PATH = os.environ.get("MREC_LIB_PATH") or os.path.join(LIB_DIR, "libmrec.so")
 
-ABI_VERSION = 9
+ABI_VERSION = 10
 MAX_TABLES = 64
 BWD_MAX_BATCH = 8192
 BWD_HASH_MAX_BATCH = 4096  # batches up to this use the hash plan (fusable into a GEMM launch)
@@ -176,6 +176,7 @@ SIGNATURES = {
                                           ctypes.POINTER(HeadFinishJob), _vp]),
     "mrec_weight_prep": (ctypes.c_int, [_vp, _i64, _i64, _i64, _vp, _i64, _vp, _i64, _vp]),
     "mrec_sgd_multi": (ctypes.c_int, [_i32, ctypes.POINTER(SgdJob), _vp]),
+    "mrec_batch_stage": (ctypes.c_int, [_vp, _vp, _i64, _vp]),
     "mrec_dcn_cross_bwd_prep": (ctypes.c_int, [_i64, _i64, _vp, _i64, _vp, _i64, _vp, _i64, _vp,
                                                _i64, _vp, _i64, _i32, _vp, _i64, _vp]),
     "mrec_emb_bwd_large_workspace_size": (ctypes.c_size_t, [_bank_p, _i64]),

@@ -11,14 +11,15 @@ a 127 µs GPU step does.
 Here, once per epoch, the (shuffled) dataset is packed batch-major into ONE
 pinned host buffer: batch j is a contiguous ``slot_bytes`` record holding every
 column of its samples (``PackedLayout``: one 256-B aligned segment per column,
-ids first).  A batch then crosses PCIe as ONE DMA (655 KB at Criteo shape,
-21 µs) into one of ``depth`` device slots, enqueued ``depth - 1`` batches ahead
-on the consumer's stream, so stream order alone keeps a slot from being refilled
-before its step ran and the host loop never blocks.  (A side copy stream ordered
-by events would overlap the DMA with compute, but on this ROCm a graph launch
-behind a cross-stream event wait blocks the host: measured 0.22-0.32 ms/step
-against 0.163 ms same-stream and 0.131 ms with resident batches,
-``tools/h2d_probe.py``; ``side_stream=True`` keeps that mode.)  The
+ids first).  A batch then crosses PCIe as ONE copy (655 KB at Criteo shape)
+into one of ``depth`` device slots, enqueued ``depth - 1`` batches ahead on the
+consumer's stream, so stream order alone keeps a slot from being refilled before
+its step ran.  The copy is a libmrec kernel reading the pinned record over PCIe
+(``mrec_batch_stage``, ``copy="kernel"``): with ``hipMemcpyAsync`` (a DMA
+engine, ``copy="dma"``) or a side copy stream ordered by events
+(``copy="side"``) a HIP graph launched behind the copy waits on the host
+(measured 0.19-0.43 ms/step against 0.13 with resident batches,
+``tools/h2d_probe.py``).  The
 yielded batch dict holds views into the slot: the keys and per-sample meaning
 are the reference's (``const.py:78-98``), plus ``"__dense__"`` = the dense
 feature columns pre-stacked ``[n, k]`` in the order ``dense_group`` names them
@@ -40,6 +41,8 @@ from typing import Dict, Iterator, List, Mapping, Optional, Sequence, Tuple
 import numpy as np
 import torch
 from torch import Tensor
+
+from pytorchrec_amd import _mrec
 
 _ALIGN = 256
 
@@ -157,12 +160,13 @@ class ColumnarLoader:
 
     Mirrors the ``DataLoader`` arguments ``IModel.fit`` passes (batch_size,
     shuffle, drop_last; IModel.py:183-190).  ``depth`` device slots (>= 2) bound
-        how far the copies run ahead.  ``side_stream=True`` issues the copies on a
-    side stream ordered by events (overlaps compute; see the module doc)."""
+        how far the copies run ahead; ``copy`` selects the H2D mechanism (module doc).
+    A GPU batch of a ``copy="kernel"`` loader needs libmrec (raises
+    ``MrecUnavailable`` without it: there is no silent fallback)."""
 
     def __init__(self, dataset: ColumnarDataset, batch_size: int, device=None,
                  shuffle: bool = False, drop_last: bool = False, seed: int = 0, depth: int = 3,
-                 side_stream: bool = False):
+                 copy: str = "kernel"):
         if not isinstance(dataset, ColumnarDataset):
             raise TypeError("ColumnarLoader needs a ColumnarDataset")
         if int(batch_size) < 1:
@@ -176,7 +180,10 @@ class ColumnarLoader:
         self.drop_last = bool(drop_last)
         self.seed = int(seed)
         self.depth = int(depth)
-        self.side_stream = bool(side_stream)
+        if copy not in ("kernel", "dma", "side"):
+            raise ValueError(f"copy must be 'kernel', 'dma' or 'side', got {copy!r}")
+        self.copy = copy
+        self.side_stream = copy == "side"
         self.epoch = 0
         self.layout = PackedLayout(dataset, self.batch_size)
         self._host: Optional[Tensor] = None
@@ -248,7 +255,11 @@ class ColumnarLoader:
         for i, n in enumerate(sizes):
             while issued < min(len(sizes), i + self.depth):
                 s = issued % self.depth
-                if not self.side_stream:  # stream order alone protects the slot
+                if self.copy == "kernel":  # stream order alone protects the slot
+                    _mrec.call("mrec_batch_stage", self._slots[s].data_ptr(),
+                               host[issued].data_ptr(), self.layout.slot_bytes,
+                               _mrec.stream_handle(self.device))
+                elif self.copy == "dma":
                     self._slots[s].copy_(host[issued], non_blocking=True)
                 else:
                     with torch.cuda.stream(cs):

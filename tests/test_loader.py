@@ -89,6 +89,11 @@ def test_dataset_getitem_is_the_reference_sample_dict():
         ColumnarDataset({"a": np.zeros(3, np.int64)}, dense_group=["a"])
 
 
+def test_copy_mode_is_validated():
+    with pytest.raises(ValueError):
+        ColumnarLoader(_dataset(4), 2, copy="memcpy")
+
+
 def test_int64_ids_beyond_int32_stay_int64():
     ds = ColumnarDataset({"c_c_big": np.array([0, 1 << 40, 3], np.int64)})
     b = next(iter(ColumnarLoader(ds, 4)))
@@ -138,14 +143,19 @@ def test_fit_through_columnar_loader_equals_fit_through_dataloader():
 
 @pytest.mark.gpu
 def test_gpu_pipelined_batches_bit_exact_and_training_matches_resident(gpu):
-    from pytorchrec_amd.loss import BCEWithLogitsLoss
     n, batch = 1000, 128
     cols = _columns(n, seed=1)
     ds = _dataset(n, seed=1)
-    for side in (False, True):
+    for copy in ("kernel", "dma", "side"):
         _check_pipelined(ColumnarLoader(ds, batch, device=gpu, shuffle=True, seed=11, depth=2,
-                                        side_stream=side), cols, n, batch)
+                                        copy=copy), cols, n, batch)
     _check_training(cols, n, batch, gpu)
+    # the stage kernel refuses pageable host memory instead of faulting on it
+    from pytorchrec_amd import _mrec
+    d = torch.empty(64, dtype=torch.uint8, device=gpu)
+    with pytest.raises(Exception, match="pinned"):
+        _mrec.call("mrec_batch_stage", d.data_ptr(), torch.zeros(64, dtype=torch.uint8).data_ptr(),
+                   64, _mrec.stream_handle(gpu))
 
 
 def _check_pipelined(ld, cols, n, batch):

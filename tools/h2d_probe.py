@@ -24,9 +24,9 @@ def main():
     cols[label_col.feature_name] = (torch.rand(B * nb, generator=g) < 0.25).float()
     ds = ColumnarDataset(cols, dense_group=[c.feature_name for c in dense_cols])
     out = {}
-    for depth, side in ((3, True), (4, True), (3, False), (4, True)):
-        ld = ColumnarLoader(ds, B, dev, depth=depth, side_stream=side)
-        depth = f"{depth}{'s' if side else 'q'}"
+    for depth, mode in ((3, "kernel"), (3, "dma"), (3, "side"), (4, "kernel")):
+        ld = ColumnarLoader(ds, B, dev, depth=depth, copy=mode)
+        depth = f"{depth}_{mode}"
         nd = ld.depth
         for s, _ in ld.iter_slots():
             step(ld.slot_views(s))

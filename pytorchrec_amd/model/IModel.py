@@ -84,6 +84,35 @@ class IModel(Module, IWithArguments, ABC):
     def save_weights(self, filepath: str):
         torch.save(self.state_dict(), filepath, pickle_protocol=pickle.HIGHEST_PROTOCOL)
 
+    # -- row-sharded checkpoints -------------------------
+    def global_state_dict(self) -> Dict:
+        """``state_dict()`` with every row-sharded bank replaced by the full bank in
+        the unsharded layout, so the keys and shapes are exactly those of the same
+        model built without sharding (and of the reference's per-field tables via
+        ``EmbeddingBank.table``).  Collective over the shard group."""
+        from pytorchrec_amd.sharding import ShardedEmbeddingBank
+        sd = self.state_dict()
+        for name, m in self.named_modules():
+            if isinstance(m, ShardedEmbeddingBank):
+                sd[(name + "." if name else "") + "weight"] = m.gather_global()
+        return sd
+
+    def load_global_state_dict(self, state_dict: Dict, strict: bool = True):
+        """Load a checkpoint in the unsharded layout (``global_state_dict`` or a
+        single-GPU ``state_dict``); each row-sharded bank keeps its own rows."""
+        from pytorchrec_amd.sharding import ShardedEmbeddingBank
+        sd = dict(state_dict)
+        for name, m in self.named_modules():
+            if isinstance(m, ShardedEmbeddingBank):
+                m.load_global_bank_(sd.pop((name + "." if name else "") + "weight"))
+        missing = [k for k in self.load_state_dict(sd, strict=False).missing_keys
+                   if not any(isinstance(m, ShardedEmbeddingBank) and
+                              k == (n + "." if n else "") + "weight"
+                              for n, m in self.named_modules())]
+        if strict and missing:
+            raise RuntimeError(f"missing keys in state_dict: {missing}")
+        return self
+
     def save_best_weights(self):
         self.best_state_dict = copy.deepcopy(tensor_to_device(self.state_dict(), torch.device("cpu")))
 

@@ -170,8 +170,48 @@ class ShardedEmbeddingBank(EmbeddingBank):
             src = t[self.rank::self.world]
             o = self.row_offset[f]
             cols = self.dim + (1 if self.has_w else 0)
-            self.weight[o:o + n, :cols].copy_(src[:, :cols].to(self.weight.dtype))
+            self.weight[o:o + n, :cols].copy_(src[:, :cols].to(device=self.weight.device,
+                                                                   dtype=self.weight.dtype))
         return self
+
+    @torch.no_grad()
+    def gather_global(self) -> torch.Tensor:
+        """The full bank in the UNSHARDED layout (``EmbeddingBank(global_rows)``:
+        tables concatenated, same row pitch), assembled on every rank: per table one
+        all_gather of the shards padded to ceil(rows / W) rows, then global row i =
+        row i // W of rank i % W.  Collective: every rank must call it."""
+        W = self.world
+        full = torch.empty(sum(self.global_rows), self.row_stride, dtype=self.weight.dtype,
+                           device=self.weight.device)
+        g_off = 0
+        for f, n in enumerate(self.global_rows):
+            per = -(-n // W)
+            local = self.weight[self.row_offset[f]:self.row_offset[f] + self.category_nums[f]]
+            if W == 1:
+                full[g_off:g_off + n] = local
+            else:
+                pad = torch.zeros(per, self.row_stride, dtype=self.weight.dtype,
+                                  device=self.weight.device)
+                pad[:local.shape[0]] = local
+                parts = [torch.empty_like(pad) for _ in range(W)]
+                dist.all_gather(parts, pad, group=self.comm.group)
+                # [W, per, stride] -> [per, W, stride]: row j of rank r is global j*W + r
+                inter = torch.stack(parts, 1).reshape(per * W, self.row_stride)
+                full[g_off:g_off + n] = inter[:n]
+            g_off += n
+        return full
+
+    @torch.no_grad()
+    def load_global_bank_(self, full: torch.Tensor):
+        """Inverse of ``gather_global``: take this rank's rows of a full bank in the
+        unsharded layout (e.g. a single-GPU checkpoint's ``embeddings.weight``)."""
+        if tuple(full.shape) != (sum(self.global_rows), self.row_stride):
+            raise ValueError(f"full bank shape {tuple(full.shape)} != "
+                             f"({sum(self.global_rows)}, {self.row_stride})")
+        offs = [0]
+        for n in self.global_rows:
+            offs.append(offs[-1] + n)
+        return self.load_global_([full[offs[f]:offs[f + 1]] for f in range(len(self.global_rows))])
 
     def local_rows_of(self, f: int) -> torch.Tensor:
         """Global ids of this shard's rows of table f."""

@@ -85,6 +85,19 @@ def _worker(rank, world, port, out_dir, steps):
         out = {"losses": np.array(losses)}
         for k, v in model.state_dict().items():
             out[k.replace(".", "__")] = v.detach().numpy()
+        # sharded checkpoint: full bank in the unsharded layout on every rank, and a
+        # fresh sharded replica restored from it holds exactly this rank's rows
+        gsd = model.global_state_dict()
+        out["global_bank"] = gsd["embeddings.weight"].detach().numpy()
+        with sharded_tables(comm, cap=B):
+            fresh = DeepFM(sparse, dense, label, emb_size=DIM, layers=LAYERS, random_seed=99)
+        fresh.load_global_state_dict(gsd)
+        cols = model.embeddings.dim + 1
+        same = torch.equal(fresh.embeddings.weight[:, :cols], model.embeddings.weight[:, :cols])
+        for k, v in model.state_dict().items():
+            if not k.startswith("embeddings"):
+                same = same and torch.equal(fresh.state_dict()[k], v)
+        out["reload_ok"] = np.array(bool(same))
         np.savez(os.path.join(out_dir, f"rank{rank}.npz"), **out)
     finally:
         dist.destroy_process_group()
@@ -111,6 +124,11 @@ def test_two_rank_sharded_deepfm_matches_single_process(steps):
                                        atol=1e-6, err_msg=k)
     bank = ref.embeddings
     cols = bank.dim + 1
+    for r in range(world):
+        assert bool(res[r]["reload_ok"]), f"rank {r}: load_global_state_dict did not restore"
+        assert res[r]["global_bank"].shape == tuple(bank.weight.shape)
+        np.testing.assert_allclose(res[r]["global_bank"][:, :cols],
+                                   bank.weight.detach()[:, :cols].numpy(), rtol=1e-5, atol=1e-6)
     for r in range(world):
         w = res[r]["embeddings__weight"]
         o_local = 0

@@ -70,11 +70,33 @@ class RefDeepFM(nn.Module):
         return logit
 
 
+class _RoundBF16(torch.autograd.Function):
+    """Identity that rounds its value (forward) and its gradient (backward) to bf16."""
+
+    @staticmethod
+    def forward(ctx, x):
+        return x.to(torch.bfloat16).to(x.dtype)
+
+    @staticmethod
+    def backward(ctx, g):
+        return g.to(torch.bfloat16).to(g.dtype)
+
+
+def _rb(x):
+    return _RoundBF16.apply(x)
+
+
 class RefDCNv2(nn.Module):
-    """Stacked DCN-v2 the reference way (cross layers = nn.Linear(d, d))."""
+    """Stacked DCN-v2 the reference way (cross layers = nn.Linear(d, d)).
+
+    ``bf16_points=True`` is NOT the reference: the same model with every tensor the
+    MI355X path stores in bf16 rounded there (x0, the cross outputs, MLP
+    activations, the weights as GEMM operands, and the gradients at the same
+    points; fp32 accumulation).  Its distance to the fp64 model is what bf16
+    storage alone costs — the parity tests use it to size their tolerance."""
 
     def __init__(self, category_nums: List[int], n_dense: int, emb_size=16, n_cross=3,
-                 layers=(400, 400), dtype=torch.float32, seed=2020):
+                 layers=(400, 400), dtype=torch.float32, seed=2020, bf16_points=False):
         super().__init__()
         torch.manual_seed(seed)
         self.emb = nn.ModuleList([nn.Embedding(n, emb_size) for n in category_nums])
@@ -82,16 +104,27 @@ class RefDCNv2(nn.Module):
         self.cross = nn.ModuleList([nn.Linear(d, d) for _ in range(n_cross)])
         self.mlp = _mlp([d, *layers])
         self.out = nn.Linear(layers[-1], 1)
+        self.bf16_points = bf16_points
         self.apply(_reset)
         self.to(dtype)
 
     def forward(self, ids, dense):
         v = torch.cat([e(ids[:, f]) for f, e in enumerate(self.emb)], 1)
         x0 = torch.cat([v, dense], 1) if dense is not None else v
+        if not self.bf16_points:
+            x = x0
+            for c in self.cross:
+                x = x0 * c(x) + x
+            return self.out(self.mlp(x)).squeeze(-1)
+        lin = (lambda x, m: x @ _rb(m.weight).T + m.bias)
+        x0 = _rb(x0)
         x = x0
         for c in self.cross:
-            x = x0 * c(x) + x
-        return self.out(self.mlp(x)).squeeze(-1)
+            x = _rb(x0 * lin(x, c) + x)
+        for m in self.mlp:
+            if isinstance(m, nn.Linear):
+                x = _rb(torch.relu(lin(x, m)))
+        return (x @ self.out.weight.T + self.out.bias).squeeze(-1)
 
 
 def sgd_train_step(model: nn.Module, opt: torch.optim.Optimizer, ids, dense, label):

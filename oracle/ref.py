@@ -321,12 +321,33 @@ def din_attention_pool(q, k, valid, att_layers, att_out):
     acts = mlp_fwd(feat, att_layers)
     Wo, bo = att_out
     s = linear(acts[-1], Wo, bo).reshape(B, L)
+    u, a = din_softmax_pool(s, valid, k)
+    return u, a, s
+
+
+def din_softmax_pool(s, valid, k):
+    """The pooling half of ``din_attention_pool`` given the scores: masked softmax
+    over the valid history positions (invalid -> -inf, then the row max is
+    subtracted; SASRec.py:26-29) and u = sum_j a_j k_j.
+    s [B,L], valid [B,L], k [B,L,E] -> (u [B,E], a [B,L])."""
+    s = np.asarray(s, np.float64)
+    k = np.asarray(k, np.float64)
     sm = np.where(np.asarray(valid).astype(bool), s, -np.inf)
     sm = sm - sm.max(-1, keepdims=True)
     e = np.exp(sm)
     a = e / e.sum(-1, keepdims=True)
-    u = (a[..., None] * k).sum(1)
-    return u, a, s
+    return (a[..., None] * k).sum(1), a
+
+
+def din_softmax_pool_bwd(a, k, du):
+    """Backward of ``din_softmax_pool``: with g_j = du . k_j,
+    ds_j = a_j (g_j - sum_i a_i g_i) and dk_j = a_j du.  -> (ds [B,L], dk [B,L,E])."""
+    a = np.asarray(a, np.float64)
+    k = np.asarray(k, np.float64)
+    du = np.asarray(du, np.float64)
+    g = (k * du[:, None, :]).sum(-1)
+    ds = a * (g - (a * g).sum(-1, keepdims=True))
+    return ds, a[..., None] * du[:, None, :]
 
 
 # ----------------------------------------------------------------------------

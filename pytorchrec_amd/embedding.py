@@ -441,6 +441,12 @@ class _InteractFn(torch.autograd.Function):
         n_dense = 0 if dense is None else dense.shape[1]
         flags = (_mrec.INTERACT_FM2 if fm2 else 0) | (_mrec.INTERACT_FIRST_ORDER if first_order else 0)
         x0 = None
+        ret_x0 = bool(x0_cols)
+        if fm2 and need_bwd and not x0_cols:
+            # the FM gradient of lookup (b, f) is dfm_b * (fm_sum_b - v_bf): keep the
+            # gathered rows for the backward (an exact copy in the bank's dtype)
+            x0_cols = (bank.n_tables * bank.dim + n_dense + 7) // 8 * 8
+            x0_dtype = weight.dtype
         if x0_cols:
             x0 = torch.empty(B, x0_cols, dtype=x0_dtype, device=dev)
         logit = torch.empty(B, dtype=torch.float32, device=dev)
@@ -473,13 +479,14 @@ class _InteractFn(torch.autograd.Function):
         ctx.has_dense_w = dense_w is not None
         ctx.has_bias = bias is not None
         ctx.dense_w, ctx.bias = dense_w, bias
-        if x0 is None:
+        ctx.ret_x0 = ret_x0
+        if not ret_x0:
             return logit
         return x0, logit
 
     @staticmethod
     def backward(ctx, *grads):
-        if len(grads) == 2:
+        if ctx.ret_x0:
             dx0, dlogit = grads
         else:
             dx0, dlogit = None, grads[0]

@@ -192,6 +192,8 @@ class ColumnarLoader:
         self._copy_stream = None
         self._copied: List = []
         self._released: List = []
+        self._reading = None  # event after the latest enqueued read of the host buffer
+        self._iterating = False
 
     def __len__(self) -> int:
         n, b = self.dataset.n, self.batch_size
@@ -208,12 +210,19 @@ class ColumnarLoader:
         return torch.randperm(self.dataset.n, generator=g)
 
     def prepare_epoch(self) -> List[int]:
-        """Pack the next epoch into the host buffer (once; the next iteration uses it)."""
+        """Pack the next epoch into the host buffer (once; the next iteration uses it).
+        Not while an epoch is being iterated: its remaining batches are staged from
+        this same buffer (RuntimeError).  Before packing it waits for the device
+        copies already enqueued from the buffer (the last batches of the previous
+        epoch may still be queued behind the steps)."""
+        if self._iterating:
+            raise RuntimeError("ColumnarLoader.prepare_epoch() while an epoch is being "
+                               "iterated: finish (or close) that iteration first")
         if self._packed is None:
             sizes = self._sizes()
             nb = max(len(sizes), 1)
-            if self._copy_stream is not None:
-                self._copy_stream.synchronize()  # the last epoch's copies read the buffer
+            if self._reading is not None:
+                self._reading.synchronize()  # enqueued copies of the last epoch read the buffer
             if self._host is None or self._host.shape[0] < nb:
                 self._host = torch.empty(nb, self.layout.slot_bytes, dtype=torch.uint8,
                                          pin_memory=self.device.type == "cuda")
@@ -251,28 +260,37 @@ class ColumnarLoader:
         self._ensure_slots()
         sizes = self._take_epoch()
         cs, host = self._copy_stream, self._host
-        issued = 0
-        for i, n in enumerate(sizes):
-            while issued < min(len(sizes), i + self.depth):
-                s = issued % self.depth
-                if self.copy == "kernel":  # stream order alone protects the slot
-                    _mrec.call("mrec_batch_stage", self._slots[s].data_ptr(),
-                               host[issued].data_ptr(), self.layout.slot_bytes,
-                               _mrec.stream_handle(self.device))
-                elif self.copy == "dma":
-                    self._slots[s].copy_(host[issued], non_blocking=True)
-                else:
-                    with torch.cuda.stream(cs):
-                        cs.wait_event(self._released[s])  # the consumer's last use of slot s
+        if self._reading is None:
+            self._reading = torch.cuda.Event()
+        self._iterating = True
+        try:
+            issued = 0
+            for i, n in enumerate(sizes):
+                while issued < min(len(sizes), i + self.depth):
+                    s = issued % self.depth
+                    if self.copy == "kernel":  # stream order alone protects the slot
+                        _mrec.call("mrec_batch_stage", self._slots[s].data_ptr(),
+                                   host[issued].data_ptr(), self.layout.slot_bytes,
+                                   _mrec.stream_handle(self.device))
+                        self._reading.record(torch.cuda.current_stream(self.device))
+                    elif self.copy == "dma":
                         self._slots[s].copy_(host[issued], non_blocking=True)
-                        self._copied[s].record(cs)
-                issued += 1
-            s = i % self.depth
-            if self.side_stream:
-                torch.cuda.current_stream(self.device).wait_event(self._copied[s])
-            yield s, n
-            if self.side_stream:
-                self._released[s].record(torch.cuda.current_stream(self.device))
+                        self._reading.record(torch.cuda.current_stream(self.device))
+                    else:
+                        with torch.cuda.stream(cs):
+                            cs.wait_event(self._released[s])  # the consumer's last use of slot s
+                            self._slots[s].copy_(host[issued], non_blocking=True)
+                            self._copied[s].record(cs)
+                            self._reading.record(cs)
+                    issued += 1
+                s = i % self.depth
+                if self.side_stream:
+                    torch.cuda.current_stream(self.device).wait_event(self._copied[s])
+                yield s, n
+                if self.side_stream:
+                    self._released[s].record(torch.cuda.current_stream(self.device))
+        finally:
+            self._iterating = False
 
     def __iter__(self) -> Iterator[Dict[str, Tensor]]:
         if self.device.type == "cuda":
@@ -280,5 +298,9 @@ class ColumnarLoader:
                 yield self.layout.views(self._slots[s], n)
         else:
             sizes = self._take_epoch()
-            for j, n in enumerate(sizes):
-                yield self.layout.views(self._host[j], n)
+            self._iterating = True  # the batches are views of the host buffer
+            try:
+                for j, n in enumerate(sizes):
+                    yield self.layout.views(self._host[j], n)
+            finally:
+                self._iterating = False

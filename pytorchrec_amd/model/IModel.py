@@ -26,7 +26,6 @@ MI355X additions (documented deviations):
 from __future__ import annotations
 
 import copy
-import pickle
 from abc import ABC, abstractmethod
 from typing import Dict, List, Optional
 
@@ -82,7 +81,11 @@ class IModel(Module, IWithArguments, ABC):
         self.to(device)
 
     def save_weights(self, filepath: str):
-        torch.save(self.state_dict(), filepath, pickle_protocol=pickle.HIGHEST_PROTOCOL)
+        # the reference pickles with HIGHEST_PROTOCOL (IModel.py:79-81); torch >= 2.6
+        # loads with weights_only=True, whose unpickler rejects protocol >= 4 frames,
+        # so the default protocol keeps the file loadable safely (here and by the
+        # reference's own torch.load on a current torch)
+        torch.save(self.state_dict(), filepath)
 
     # -- row-sharded checkpoints -------------------------
     def global_state_dict(self) -> Dict:
@@ -102,15 +105,22 @@ class IModel(Module, IWithArguments, ABC):
         single-GPU ``state_dict``); each row-sharded bank keeps its own rows."""
         from pytorchrec_amd.sharding import ShardedEmbeddingBank
         sd = dict(state_dict)
+        bank_keys, missing = set(), []
         for name, m in self.named_modules():
             if isinstance(m, ShardedEmbeddingBank):
-                m.load_global_bank_(sd.pop((name + "." if name else "") + "weight"))
-        missing = [k for k in self.load_state_dict(sd, strict=False).missing_keys
-                   if not any(isinstance(m, ShardedEmbeddingBank) and
-                              k == (n + "." if n else "") + "weight"
-                              for n, m in self.named_modules())]
-        if strict and missing:
-            raise RuntimeError(f"missing keys in state_dict: {missing}")
+                key = (name + "." if name else "") + "weight"
+                bank_keys.add(key)
+                w = sd.pop(key, None)
+                if w is None:
+                    missing.append(key)
+                else:
+                    m.load_global_bank_(w)
+        res = self.load_state_dict(sd, strict=False)
+        missing += [k for k in res.missing_keys if k not in bank_keys]
+        unexpected = list(res.unexpected_keys)
+        if strict and (missing or unexpected):
+            raise RuntimeError(f"Error(s) in loading state_dict for {type(self).__name__}: "
+                               f"missing keys {missing}, unexpected keys {unexpected}")
         return self
 
     def save_best_weights(self):
@@ -157,10 +167,19 @@ class IModel(Module, IWithArguments, ABC):
             if isinstance(bank, ShardedEmbeddingBank):
                 g0 = optimizer.param_groups[0]
                 if not (isinstance(optimizer, torch.optim.SGD) and g0.get("momentum", 0) == 0
-                        and not g0.get("nesterov", False) and not g0.get("maximize", False)):
+                        and not g0.get("nesterov", False) and not g0.get("maximize", False)
+                        and g0.get("weight_decay", 0) == 0 and g0.get("dampening", 0) == 0):
                     raise NotImplementedError("row-sharded tables train with the fused SGD "
-                                              "update only (torch.optim.SGD, no momentum)")
+                                              "update only (torch.optim.SGD: no momentum, "
+                                              "weight_decay, dampening or nesterov)")
                 bank.use_fused_sgd(g0["lr"], g0)
+                continue
+            if self._dp_active():
+                # a replicated (unsharded) bank under data parallelism: its dense
+                # gradient goes through the same all-reduce as the dense tower, so
+                # the replicas cannot drift apart (a fused per-rank update would
+                # apply each rank's own batch only)
+                bank.use_dense_grad()
                 continue
             group = None
             for g in optimizer.param_groups:
@@ -204,8 +223,10 @@ class IModel(Module, IWithArguments, ABC):
         # step all-reduces it once and applies SGD to every parameter (and its bf16
         # GEMM images) in one mrec_sgd_multi launch
         dp_ids = {id(p) for p in self._dp_params()}
+        banks = {id(b.weight) for b in self.embedding_banks()}  # dense-grad replicated tables
         plain = [(p, g) for p, g in plain
-                 if id(p) in dp_ids and p.is_cuda and p.dim() <= 2 and p.is_contiguous()]
+                 if id(p) in dp_ids and id(p) not in banks and p.is_cuda and p.dim() <= 2
+                 and p.is_contiguous()]
         if not plain or len(plain) > 16:
             return
         layout, off = [], 0
@@ -245,14 +266,21 @@ class IModel(Module, IWithArguments, ABC):
         """Make this replica data-parallel over ``comm`` (a sharding.ShardComm):
         rank 0's dense parameters are broadcast now, and every train_step averages
         the dense gradients over the ranks (one flat all-reduce) before the
-        optimizer step.  Row-sharded tables exchange rows themselves."""
+        optimizer step.  Row-sharded tables exchange rows themselves; unsharded
+        tables are replicated and train through the dense-gradient all-reduce."""
         self.dp_comm = comm
+        if self._is_compiled:
+            self._configure_embedding_update(self.compiled_optimizers)
         with torch.no_grad():
             for p in self._dp_params():
                 comm.broadcast_(p.data)
         if self._is_compiled:
             self._configure_dense_update(self.compiled_optimizers)
         return self
+
+    def _dp_active(self) -> bool:
+        comm = getattr(self, "dp_comm", None)
+        return comm is not None and (comm.world > 1 or comm.force)
 
     def _dp_params(self):
         from pytorchrec_amd.sharding import ShardedEmbeddingBank

@@ -1,4 +1,4 @@
-"""Generate the golden vectors G1-G8 (+G10) by running the reference itself.
+"""Generate the golden vectors G1-G8 (+G10, G11) by running the reference itself.
 
 Run IN THE BUILD CONTAINER ONLY (the reference never travels to the GPU box):
 
@@ -209,6 +209,22 @@ def main():
           nop=num.get_feature_data(bc, NormalizationMode.NOP).numpy(),
           max_min=num.get_feature_data(bc, NormalizationMode.MAX_MIN).numpy(),
           z_score=num.get_feature_data(bc, NormalizationMode.Z_SCORE).numpy())
+
+    # ---- G11: FunkSVD sampled (ranking) branch, iid [B, N] ----------------------
+    # (FunkSVD.py:56-65: prediction [B, N] = u_b . i_{b,n}, target [B, N] with
+    # column 0 = 1); own generator so G1-G10 stay byte-identical
+    g11 = torch.Generator().manual_seed(1111)
+    n_cand = 5
+    b11 = {"uid": torch.randint(0, rows_u, (24,), generator=g11).int(),
+           "iid": torch.randint(0, rows_i, (24, n_cand), generator=g11).int()}
+    b11["iid"][3, :] = 0  # repeated candidates / row 0 are ordinary rows
+    b11["iid"][4, 1:] = b11["iid"][4, 0]
+    funk.eval()
+    with torch.no_grad():
+        pred11, tgt11 = funk(b11)
+    _save("g11_funksvd_sampled.npz", u_table=funk.u_embeddings.weight.detach().numpy(),
+          i_table=funk.i_embeddings.weight.detach().numpy(), uid=b11["uid"].numpy(),
+          iid=b11["iid"].numpy(), prediction=pred11.numpy(), target=tgt11.numpy())
 
 
 if __name__ == "__main__":

@@ -141,6 +141,20 @@ def test_fit_through_columnar_loader_equals_fit_through_dataloader():
         torch.testing.assert_close(hist[1][k], hist[3][k], rtol=1e-6, atol=1e-7, msg=k)
 
 
+def test_prepare_epoch_refused_while_iterating():
+    """The host buffer holds the epoch being iterated: repacking it mid-epoch would
+    duplicate / drop samples, so it raises; a finished or closed
+    iteration releases it."""
+    ld = ColumnarLoader(_dataset(100), 32, shuffle=True)
+    it = iter(ld)
+    next(it)
+    with pytest.raises(RuntimeError, match="being iterated"):
+        ld.prepare_epoch()
+    it.close()
+    ld.prepare_epoch()
+    assert len(list(ld)) == 4
+
+
 @pytest.mark.gpu
 def test_gpu_pipelined_batches_bit_exact_and_training_matches_resident(gpu):
     n, batch = 1000, 128
@@ -149,6 +163,8 @@ def test_gpu_pipelined_batches_bit_exact_and_training_matches_resident(gpu):
     for copy in ("kernel", "dma", "side"):
         _check_pipelined(ColumnarLoader(ds, batch, device=gpu, shuffle=True, seed=11, depth=2,
                                         copy=copy), cols, n, batch)
+    for copy in ("kernel", "dma"):
+        _check_back_to_back_epochs(ds, cols, n, batch, gpu, copy)
     _check_training(cols, n, batch, gpu)
     # the stage kernel refuses pageable host memory instead of faulting on it
     from pytorchrec_amd import _mrec
@@ -171,6 +187,24 @@ def _check_pipelined(ld, cols, n, batch):
         torch.cuda._sleep(2_000_000)
         assert torch.equal(b["c_c_C0"].cpu(), want["c_c_C0"]), j
     assert len(seen) == len(ld) == 8
+
+
+def _check_back_to_back_epochs(ds, cols, n, batch, gpu, copy):
+    """Two shuffled epochs with no host sync between them behind a slow consumer:
+    packing epoch 2 must wait for epoch 1's last enqueued copies, which still read
+    the host buffer."""
+    ld = ColumnarLoader(ds, batch, device=gpu, shuffle=True, seed=21, depth=3, copy=copy)
+    got = []
+    for _ in range(2):
+        for b in ld:
+            torch.cuda._sleep(3_000_000)
+            got.append(b["c_c_C1"].clone())
+    torch.cuda.synchronize()
+    for e in range(2):
+        order = torch.randperm(n, generator=torch.Generator().manual_seed(21 + e))
+        for j in range(len(ld)):
+            want = _expected(cols, order[j * batch:(j + 1) * batch])["c_c_C1"]
+            assert torch.equal(got[e * len(ld) + j].cpu(), want), (copy, e, j)
 
 
 def _check_training(cols, n, batch, gpu):

@@ -139,6 +139,67 @@ def test_two_rank_sharded_deepfm_matches_single_process(steps):
             o_local += rows.shape[0]
 
 
+def _worker_replicated(rank, world, port, out_dir, steps):
+    """Unsharded (replicated) tables under distribute(), compiled BEFORE distribute:
+    the bank must leave the per-rank fused update and train through the all-reduce
+    (ADVICE r01); a sharded bank with weight_decay must be refused."""
+    import torch.distributed as dist
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from pytorchrec_amd.loss import BCEWithLogitsLoss
+        from pytorchrec_amd.model import DeepFM
+        from pytorchrec_amd.sharding import ShardComm, sharded_tables
+        comm = ShardComm()
+        model = _reference_model()
+        if rank == 1:  # a different local init: distribute() must broadcast rank 0's
+            with torch.no_grad():
+                model.embeddings.weight.mul_(3.0)
+        opt = torch.optim.SGD(model.get_parameters(), lr=LR)
+        model.compile(opt, BCEWithLogitsLoss(), [], torch.device("cpu"))
+        assert model.embeddings.update == "sgd"
+        model.distribute(comm)
+        assert model.embeddings.update == "dense"
+        losses = []
+        for s in range(steps):
+            full = _batch(100 + s, B * world)
+            losses.append(float(model.train_step(
+                {k: v[rank * B:(rank + 1) * B] for k, v in full.items()})["loss"].detach()))
+        out = {"losses": np.array(losses)}
+        for k, v in model.state_dict().items():
+            out[k.replace(".", "__")] = v.detach().numpy()
+        sparse, dense, label = _columns()
+        with sharded_tables(comm, cap=B):
+            sh = DeepFM(sparse, dense, label, emb_size=DIM, layers=LAYERS, random_seed=7)
+        refused = False
+        try:
+            sh.compile(torch.optim.SGD(sh.get_parameters(), lr=LR, weight_decay=1e-4),
+                       BCEWithLogitsLoss(), [], torch.device("cpu"))
+        except NotImplementedError:
+            refused = True
+        out["wd_refused"] = np.array(refused)
+        np.savez(os.path.join(out_dir, f"rank{rank}.npz"), **out)
+    finally:
+        dist.destroy_process_group()
+
+
+def test_two_rank_replicated_tables_stay_identical():
+    import torch.multiprocessing as mp
+    world, steps = 2, 2
+    with tempfile.TemporaryDirectory() as d:
+        mp.spawn(_worker_replicated, args=(world, _free_port(), d, steps), nprocs=world, join=True)
+        res = [dict(np.load(os.path.join(d, f"rank{r}.npz"))) for r in range(world)]
+    ref = _reference_model()
+    ref_losses = _train(ref, [_batch(100 + s, B * world) for s in range(steps)])
+    np.testing.assert_allclose((res[0]["losses"] + res[1]["losses"]) / 2, ref_losses, rtol=1e-5,
+                               atol=1e-6)
+    for k, v in ref.state_dict().items():
+        key = k.replace(".", "__")
+        assert np.array_equal(res[0][key], res[1][key]), f"replicas diverged: {k}"
+        np.testing.assert_allclose(res[0][key], v.numpy(), rtol=1e-5, atol=1e-6, err_msg=k)
+    assert bool(res[0]["wd_refused"]) and bool(res[1]["wd_refused"])
+
+
 def test_cpu_bucketize_slots_are_stable_and_complete():
     from pytorchrec_amd.sharding import ShardComm, ShardedEmbeddingBank, cpu_bucketize
     comm = ShardComm(world=3, rank=1)

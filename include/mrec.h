@@ -32,7 +32,7 @@
 extern "C" {
 #endif
 
-#define MREC_ABI_VERSION 10
+#define MREC_ABI_VERSION 11
 #define MREC_MAX_TABLES 64      /* tables per table bank / per call */
 #define MREC_BWD_MAX_BATCH 8192  /* lookups per table per plan/apply call */
 #define MREC_BWD_HASH_MAX_BATCH 4096  /* batches up to this use the hash plan */
@@ -342,6 +342,9 @@ typedef struct {
 #define MREC_ACT_NONE 0
 #define MREC_ACT_RELU 1
 
+#define MREC_IMG_ROW_TR 0 /* bf16 weight images: row-major [N, ld] and W^T [K, ld] */
+#define MREC_IMG_TOWER 1  /* MFMA-fragment images of the fused tower (mrec_tower_*) */
+
 /* v = acc + bias[n]; aux[m,n] = v; v = act(v); v *= mul[m,n]; v += add[m,n];
  * v = (mask[m,n] > 0) ? v : 0; C = v.  Every pointer may be NULL (term skipped);
  * mul/add/aux/mask are bf16 [M, ld].  `mask` applies the ReLU' of the layer that
@@ -373,6 +376,9 @@ typedef struct {
   int64_t ld_img_row;
   void *img_tr;
   int64_t ld_img_tr;
+  /* MREC_IMG_ROW_TR: img_row / img_tr as above; MREC_IMG_TOWER: they are the
+   * fwd / bwd MFMA-fragment images of mrec_tower_fwd_bwd (ld_* ignored). */
+  int32_t img_kind;
 } mrec_epilogue;
 
 size_t mrec_gemm_workspace_size(int64_t M, int64_t N, int64_t K, int32_t split_k);
@@ -495,9 +501,75 @@ typedef struct {
   int64_t ld_row;
   void *img_tr;
   int64_t ld_tr;
+  int32_t img_kind; /* MREC_IMG_ROW_TR or MREC_IMG_TOWER (see mrec_epilogue) */
 } mrec_sgd_job;
 
 mrec_status mrec_sgd_multi(int32_t n, const mrec_sgd_job *jobs, mrec_stream stream);
+
+/*
+ * Fused MLP tower + CTR head + BCE loss, forward AND the input-gradient half of
+ * the backward, in ONE launch (the reference's MLP =
+ * Linear -> ReLU per layer (MLP.py:8-23, Dense.py:4-24), then Linear(N_L, 1) and
+ * the loss of IModel.train_step (IModel.py:116-125)).  Every row of the batch is
+ * independent until the weight gradients, so one 512-thread workgroup owns 16 rows
+ * for the whole chain: activations stay in LDS, the bf16 weights stream from L2
+ * in MFMA-fragment order (v_mfma_f32_16x16x32_bf16, fp32 accumulation), and
+ *   h_l = relu(h_{l-1} W_l^T + b_l), l = 1..L (h_0 = x0);
+ *   z = h_L . head_w + head_b + base + xs . ws + b2;  loss = mean BCE(z, y);
+ *   dz = (sigmoid(z) - y) / batch;  dh_L = dz head_w * [h_L > 0];
+ *   dh_{l-1} = (dh_l W_l) * [h_{l-1} > 0];  dx0 = dh_1 W_1.
+ * Outputs (bf16 [batch, ld], pad columns zero): h_out[l] for l < L (NULL: not
+ * stored), dh_out[l] for every l (the weight-gradient GEMMs' operands), dx0
+ * (NULL: not stored); fp32 z, dz [batch]; the head-parameter partials (one row of
+ * [dW_head (N_L) | sum dz | dws (ns)] per 16 rows, the layout
+ * mrec_ctr_head_finish reduces; ceil(batch/16) rows); the loss (ticket / last
+ * workgroup, deterministic, like mrec_ctr_head_fwd).
+ * Weights: w_fwd[l] / w_bwd[l] are the layer's tower images (mrec_tower_weight_prep;
+ * the fused SGD epilogues keep them current with img_kind = MREC_IMG_TOWER).
+ * Limits: 1 <= L <= 4, every width in [1, 512], ns <= 64.
+ */
+typedef struct {
+  int64_t batch;
+  int32_t n_layers;
+  int32_t width[5];          /* width[0] = x0 columns (K0), width[l] = N_l */
+  const void *x0;            /* bf16 [batch, ld_x0], ld_x0 >= round8(K0), pad columns zero */
+  int64_t ld_x0;
+  const void *w_fwd[4];      /* bf16 tower images of W_l [N_l, N_{l-1}] */
+  const void *w_bwd[4];
+  const float *bias[4];      /* [N_l] (NULL: no bias) */
+  const float *head_w;       /* [N_L] */
+  const float *head_b;       /* [1] or NULL */
+  const float *base;         /* [batch] per-sample logit added to z (FM part) or NULL */
+  const float *xs;           /* side linear: xs [batch, ld_xs] fp32 . ws [ns] (+ b2) */
+  int64_t ld_xs;
+  int32_t ns;
+  const float *ws;
+  const float *b2;
+  const float *y;            /* labels [batch] */
+  void *h_out[4];
+  int64_t ld_h[4];
+  void *dh_out[4];
+  int64_t ld_dh[4];
+  void *dx0;
+  int64_t ld_dx0;
+  float *z;                  /* may be NULL */
+  float *dz;
+  float *part;
+  int64_t ldp;               /* >= N_L + 1 + ns */
+  float *loss_part;          /* [ceil(batch/16)] scratch */
+  uint32_t *ticket;          /* device word, zero before the first call; left zero */
+  float *loss;               /* [1] */
+} mrec_tower_args;
+
+mrec_status mrec_tower_fwd_bwd(const mrec_tower_args *a, mrec_stream stream);
+
+/* elements of the fwd (bwd = 0) or bwd (bwd = 1) tower image of an [N, K] weight */
+int64_t mrec_tower_image_elems(int64_t N, int64_t K, int32_t bwd);
+
+/* fp32 W [N, K] (row stride ldw) -> its tower images (either may be NULL).  Only
+ * real elements are written: allocate the images zeroed once. */
+mrec_status mrec_tower_weight_prep(const float *W, int64_t N, int64_t K, int64_t ldw,
+                                   void *img_fwd, void *img_bwd, mrec_stream stream);
 
 /* ------------------------------------------------------------------------- */
 /* Batch feed                                                                 */

@@ -20,7 +20,7 @@ import torch  # noqa: F401  (must precede the dlopen, see module docstring)
 LIB_DIR = os.path.join(os.path.dirname(os.path.abspath(__file__)), "lib")
 LIB_PATH = os.environ.get("MREC_LIB_PATH") or os.path.join(LIB_DIR, "libmrec.so")
 
-ABI_VERSION = 10
+ABI_VERSION = 11
 MAX_TABLES = 64
 BWD_MAX_BATCH = 8192
 BWD_HASH_MAX_BATCH = 4096  # batches up to this use the hash plan (fusable into a GEMM launch)
@@ -83,7 +83,11 @@ class Epilogue(ctypes.Structure):
                 ("ones_out", ctypes.c_void_p),
                 ("update", ctypes.c_int32), ("lr", ctypes.c_float),
                 ("img_row", ctypes.c_void_p), ("ld_img_row", ctypes.c_int64),
-                ("img_tr", ctypes.c_void_p), ("ld_img_tr", ctypes.c_int64)]
+                ("img_tr", ctypes.c_void_p), ("ld_img_tr", ctypes.c_int64),
+                ("img_kind", ctypes.c_int32)]
+
+
+IMG_ROW_TR, IMG_TOWER = 0, 1
 
 
 class GemmCall(ctypes.Structure):
@@ -118,7 +122,28 @@ class SgdJob(ctypes.Structure):
     _fields_ = [("w", ctypes.c_void_p), ("g", ctypes.c_void_p), ("N", ctypes.c_int64),
                 ("K", ctypes.c_int64), ("ldw", ctypes.c_int64), ("ldg", ctypes.c_int64),
                 ("lr", ctypes.c_float), ("img_row", ctypes.c_void_p), ("ld_row", ctypes.c_int64),
-                ("img_tr", ctypes.c_void_p), ("ld_tr", ctypes.c_int64)]
+                ("img_tr", ctypes.c_void_p), ("ld_tr", ctypes.c_int64),
+                ("img_kind", ctypes.c_int32)]
+
+
+class TowerArgs(ctypes.Structure):
+    """mrec_tower_args (include/mrec.h)."""
+    _fields_ = [("batch", ctypes.c_int64), ("n_layers", ctypes.c_int32),
+                ("width", ctypes.c_int32 * 5),
+                ("x0", ctypes.c_void_p), ("ld_x0", ctypes.c_int64),
+                ("w_fwd", ctypes.c_void_p * 4), ("w_bwd", ctypes.c_void_p * 4),
+                ("bias", ctypes.c_void_p * 4),
+                ("head_w", ctypes.c_void_p), ("head_b", ctypes.c_void_p),
+                ("base", ctypes.c_void_p), ("xs", ctypes.c_void_p), ("ld_xs", ctypes.c_int64),
+                ("ns", ctypes.c_int32), ("ws", ctypes.c_void_p), ("b2", ctypes.c_void_p),
+                ("y", ctypes.c_void_p),
+                ("h_out", ctypes.c_void_p * 4), ("ld_h", ctypes.c_int64 * 4),
+                ("dh_out", ctypes.c_void_p * 4), ("ld_dh", ctypes.c_int64 * 4),
+                ("dx0", ctypes.c_void_p), ("ld_dx0", ctypes.c_int64),
+                ("z", ctypes.c_void_p), ("dz", ctypes.c_void_p),
+                ("part", ctypes.c_void_p), ("ldp", ctypes.c_int64),
+                ("loss_part", ctypes.c_void_p), ("ticket", ctypes.c_void_p),
+                ("loss", ctypes.c_void_p)]
 
 
 LAYOUT_ROW, LAYOUT_COL = 0, 1
@@ -206,6 +231,9 @@ SIGNATURES = {
                                             _vp, _vp, _vp, _vp, _vp, _vp, _vp]),
     "mrec_colsum": (ctypes.c_int, [_vp, _vp, ctypes.c_int, _i64, _i64, _i64, _vp, _vp, _i32,
                                    _f32, _vp]),
+    "mrec_tower_fwd_bwd": (ctypes.c_int, [ctypes.POINTER(TowerArgs), _vp]),
+    "mrec_tower_image_elems": (ctypes.c_int64, [_i64, _i64, _i32]),
+    "mrec_tower_weight_prep": (ctypes.c_int, [_vp, _i64, _i64, _i64, _vp, _vp, _vp]),
 }
 
 _lib = None

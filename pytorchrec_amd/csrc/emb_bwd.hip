@@ -216,7 +216,7 @@ __global__ __launch_bounds__(kPlanThreads) void plan_hash_kernel(BankArgs bank, 
 // deferred split-K weight-gradient reductions (+ fused SGD) run by trailing
 // workgroups of the apply launch: independent of the embedding update, and a
 // launch of their own would cost a kernel boundary on the step's serial path
-constexpr int kMaxCoReduce = 2;
+constexpr int kMaxCoReduce = 4;
 struct CoReduce {
   int n;
   int nblk[kMaxCoReduce];
@@ -629,7 +629,7 @@ static mrec_status apply_impl(const mrec_table_bank *bank, int64_t batch, const 
   CoReduce co = {};
   int co_blocks = 0;
   MREC_CHECK_ARG(n_reduce >= 0 && n_reduce <= kMaxCoReduce && (n_reduce == 0 || reduce),
-                 "n_reduce out of [0, 2]");
+                 "n_reduce out of [0, 4]");
   for (int i = 0; i < n_reduce; ++i) {
     int64_t nb = 0;
     mrec_status st = build_reduce_job(reduce[i], &co.g[co.n], &nb);

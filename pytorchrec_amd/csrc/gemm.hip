@@ -544,18 +544,24 @@ static mrec_status build_gemm(int64_t M, int64_t N, int64_t K, const mrec_operan
     g.ld_img_row = epi->ld_img_row;
     g.img_tr = static_cast<uint16_t *>(epi->img_tr);
     g.ld_img_tr = epi->ld_img_tr;
+    g.img_kind = epi->img_kind;
+    MREC_CHECK_ARG(g.img_kind == kImgRowTr || g.img_kind == kImgTower, "bad img_kind");
     MREC_CHECK_ARG(!g.update || (c_dtype == MREC_F32 && !g.bias && !g.act && !g.mul && !g.add &&
                                  !g.aux && !g.mask),
                    "update epilogue: C must be fp32 and bias/act/mul/add/aux/mask unset");
-    MREC_CHECK_ARG(!g.img_row || g.ld_img_row >= N, "ld_img_row < N");
-    MREC_CHECK_ARG(!g.img_tr || g.ld_img_tr >= M, "ld_img_tr < M");
+    MREC_CHECK_ARG(g.img_kind == kImgTower || !g.img_row || g.ld_img_row >= N, "ld_img_row < N");
+    MREC_CHECK_ARG(g.img_kind == kImgTower || !g.img_tr || g.ld_img_tr >= M, "ld_img_tr < M");
   }
   g.C = C;
   g.ldc = ldc;
   g.c_f32 = c_dtype == MREC_F32;
   g.pad_to = g.update ? N : std::min<int64_t>(ldc, (N + 7) / 8 * 8);
   g.ldws = (ncols + 7) / 8 * 8;
-  g.vec = aligned16(C, ldc, g.c_f32 ? 4 : 2) && (!g.mul || aligned16(g.mul, g.ld_mul, 2)) &&
+  // 16-B epilogue stores write whole 8-column chunks: only when C's rows hold
+  // round8(N) columns (an [M, N] fp32 C with N = 4 mod 8 is 16-B aligned per row
+  // but an 8-wide chunk at the row end would spill into the next row)
+  g.vec = aligned16(C, ldc, g.c_f32 ? 4 : 2) && ldc >= (N + 7) / 8 * 8 &&
+          (!g.mul || aligned16(g.mul, g.ld_mul, 2)) &&
           (!g.add || aligned16(g.add, g.ld_add, 2)) && (!g.aux || aligned16(g.aux, g.ld_aux, 2)) &&
           (!g.mask || aligned16(g.mask, g.ld_mask, 2));
   g.ws = static_cast<float *>(workspace);

@@ -3,6 +3,7 @@
 // their own work (emb_bwd.hip: mrec_emb_bwd_apply_ex).
 #pragma once
 #include "common.h"
+#include "tower_common.h"
 
 namespace mrec {
 
@@ -43,6 +44,7 @@ struct GemmArgs {
   int64_t ld_img_row;
   uint16_t *img_tr;
   int64_t ld_img_tr;
+  int img_kind;    // kImgRowTr / kImgTower (tower_common.h)
 };
 
 __device__ __forceinline__ float bf(uint16_t h) { return __uint_as_float(uint32_t(h) << 16); }
@@ -59,6 +61,11 @@ __device__ __forceinline__ void epilogue_elem(const GemmArgs &g, int64_t m, int6
     const float w = fmaf(-g.lr, acc, *c);
     *c = w;
     const uint16_t h = f32_to_bf16_rne(w);
+    if (g.img_kind == kImgTower) {  // W [M, N]: the fused tower's fragment images
+      if (g.img_row) g.img_row[tower_idx_fwd(m, n, g.N)] = h;
+      if (g.img_tr) g.img_tr[tower_idx_bwd(m, n, g.M)] = h;
+      return;
+    }
     if (g.img_row) g.img_row[m * g.ld_img_row + n] = h;
     if (g.img_tr) g.img_tr[n * g.ld_img_tr + m] = h;
     return;

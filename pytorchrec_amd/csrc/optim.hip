@@ -7,6 +7,7 @@
 // process the SGD of these parameters is fused into their backward kernels
 // instead; data parallelism must sum the gradients over ranks first.
 #include "common.h"
+#include "tower_common.h"
 
 namespace mrec {
 
@@ -20,6 +21,7 @@ struct SgdJobArgs {
   uint16_t *img_tr;
   int64_t N, K, ldw, ldg, ld_row, ld_tr;
   float lr;
+  int img_kind;  // kImgRowTr / kImgTower
   int tiles_k;  // 32-column tiles along K
   int first;    // first workgroup of this job
 };
@@ -49,9 +51,17 @@ __global__ __launch_bounds__(256) void sgd_multi_kernel(SgdArgs a) {
       *p = v;
     }
     tile[r][tx] = v;
+    if (J.img_kind == kImgTower) {  // the fused tower's fragment images (real elements)
+      if (n < J.N && k < J.K) {
+        const uint16_t h = f32_to_bf16_rne(v);
+        if (J.img_row) J.img_row[tower_idx_fwd(n, k, J.K)] = h;
+        if (J.img_tr) J.img_tr[tower_idx_bwd(n, k, J.N)] = h;
+      }
+      continue;
+    }
     if (J.img_row && n < J.N && k < J.ld_row) J.img_row[n * J.ld_row + k] = f32_to_bf16_rne(v);
   }
-  if (J.img_tr) {  // uniform per workgroup
+  if (J.img_tr && J.img_kind != kImgTower) {  // uniform per workgroup
     __syncthreads();
     for (int r = ty; r < kTile; r += 8) {
       const int64_t k = k0 + r, n = n0 + tx;
@@ -75,8 +85,10 @@ mrec_status mrec_sgd_multi(int32_t n, const mrec_sgd_job *jobs, mrec_stream stre
     const mrec_sgd_job &s = jobs[i];
     MREC_CHECK_ARG(s.w != nullptr && s.g != nullptr, "w or g is NULL");
     MREC_CHECK_ARG(s.N >= 0 && s.K >= 0 && s.ldw >= s.K && s.ldg >= s.K, "bad shape / ld");
-    MREC_CHECK_ARG(s.img_row == nullptr || s.ld_row >= s.K, "ld_row < K");
-    MREC_CHECK_ARG(s.img_tr == nullptr || s.ld_tr >= s.N, "ld_tr < N");
+    MREC_CHECK_ARG(s.img_kind == kImgRowTr || s.img_kind == kImgTower, "bad img_kind");
+    const bool packed = s.img_kind == kImgTower;
+    MREC_CHECK_ARG(packed || s.img_row == nullptr || s.ld_row >= s.K, "ld_row < K");
+    MREC_CHECK_ARG(packed || s.img_tr == nullptr || s.ld_tr >= s.N, "ld_tr < N");
     SgdJobArgs &J = a.job[a.n];
     J.w = s.w;
     J.g = s.g;
@@ -89,9 +101,11 @@ mrec_status mrec_sgd_multi(int32_t n, const mrec_sgd_job *jobs, mrec_stream stre
     J.ld_row = s.ld_row;
     J.ld_tr = s.ld_tr;
     J.lr = s.lr;
-    // the images' pad columns (up to ld) are written as zero by the edge tiles
-    const int64_t kc = std::max<int64_t>(s.K, s.img_row ? s.ld_row : 0);
-    const int64_t nc = std::max<int64_t>(s.N, s.img_tr ? s.ld_tr : 0);
+    J.img_kind = s.img_kind;
+    // the row-major images' pad columns (up to ld) are written as zero by the edge
+    // tiles; tower images keep their (zero) pad entries untouched
+    const int64_t kc = packed ? s.K : std::max<int64_t>(s.K, s.img_row ? s.ld_row : 0);
+    const int64_t nc = packed ? s.N : std::max<int64_t>(s.N, s.img_tr ? s.ld_tr : 0);
     if (s.N == 0 || s.K == 0) continue;
     J.tiles_k = static_cast<int>((kc + kTile - 1) / kTile);
     const int64_t tiles = ((nc + kTile - 1) / kTile) * J.tiles_k;

@@ -1,0 +1,677 @@
+// Fused MLP tower + CTR head + BCE: forward and the input-gradient backward of the
+// whole dense tower in ONE launch (include/mrec.h mrec_tower_fwd_bwd).
+//
+// Why one launch: at B = 4096 each 400-wide layer is ~1.4 GFLOP, i.e. well under a
+// microsecond of MFMA work, but as its own GEMM launch it costs ~9 us (dispatch,
+// the first k group's latency, the epilogue drain) and the activations make an
+// HBM round trip.  Every row is independent until the weight gradients, so one
+// workgroup owns 16 rows for the whole chain (fwd layers -> head + loss -> dx
+// chain) and nothing but the weights crosses workgroups.
+//
+// Layout (one 512-thread workgroup = 8 waves, 16 rows):
+//   * LDS holds the 16-row activation blocks: x0, h_1..h_L (kept for the ReLU
+//     masks of the backward) and two gradient blocks (ping-pong), row-major bf16
+//     with a row stride = 32 (mod 256) bytes, which makes the fragment reads
+//     (ds_read_b128, lane l: row l % 16, 16 B at k 8 (l / 16)) bank-conflict free;
+//   * the product is computed transposed, y^T = W x^T: the weight is MFMA operand
+//     A and streams from L2 in fragment order (tower_common.h: one 1 KiB
+//     global_load_dwordx4 per 16x32 block), the activation block is operand B,
+//     read from LDS once per k step and shared by the wave's (<= 4) output tiles;
+//   * lane l of the 16x16 accumulator holds y[row l % 16][4 (l / 16) .. + 4]:
+//     the epilogue writes 8 contiguous bytes (ds_write_b64) per tile;
+//   * PF k steps of weight fragments are in flight per wave (8 waves x 4 tiles x
+//     PF x 1 KiB = 128 KiB per CU): the layer is bound by the CU's L2 read rate.
+// Outputs (h_l, dh_l, dx0) leave LDS as coalesced 16-B row stores behind each
+// layer, overlapped with the next layer's weight stream.
+#include <algorithm>
+#include <cstdlib>
+
+#include "common.h"
+#include "tower_common.h"
+
+namespace mrec {
+
+constexpr int TW_ROWS = 16;
+constexpr int TW_THREADS = 512;
+constexpr int TW_WAVES = TW_THREADS / 64;
+constexpr int TW_MAXL = 4;
+constexpr int TW_MAXW = 512;
+constexpr int TW_PF_DEFAULT = 4;         // k steps of weight fragments in flight per wave
+constexpr int TW_TPW = 4;                // output tiles per wave (<= 32 tiles = 512 wide)
+constexpr int TW_MAXNS = 64;             // side-linear width
+
+typedef short bf16x8 __attribute__((ext_vector_type(8)));
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+
+struct TowerArgs {
+  int64_t B;
+  int L;
+  int width[TW_MAXL + 1];
+  const uint16_t *x0;
+  int64_t ld_x0;
+  const uint16_t *wf[TW_MAXL];
+  const uint16_t *wb[TW_MAXL];
+  int wf_bytes[TW_MAXL], wb_bytes[TW_MAXL];
+  const float *bias[TW_MAXL];
+  const float *head_w;
+  const float *head_b;
+  const float *base;
+  const float *xs;
+  int64_t ld_xs;
+  int ns;
+  const float *ws;
+  const float *b2;
+  const float *y;
+  uint16_t *h_out[TW_MAXL];
+  int64_t ld_h[TW_MAXL];
+  uint16_t *dh_out[TW_MAXL];
+  int64_t ld_dh[TW_MAXL];
+  uint16_t *dx0;
+  int64_t ld_dx0;
+  float *z;
+  float *dz;
+  float *part;
+  int64_t ldp;
+  float *loss_part;
+  unsigned *ticket;
+  float *loss;
+  float invB;
+  // LDS plan (bytes): buffer offsets and row strides
+  int off_x, s_x;
+  int off_h[TW_MAXL], s_h[TW_MAXL];
+  int off_g[2], s_g;
+  int off_f;   // 2 x 16 floats: dz and loss per row
+  int off_p;   // staged parameters (floats): biases, head_w, ws, b0, y, base, xs
+  int p_bias[TW_MAXL], p_hw, p_ws, p_b0, p_y, p_base, p_xs, p_z, p_part;
+  int lds_bytes;
+  int rotate;  // per-workgroup k-step rotation (MREC_TOWER_ROT=0 disables)
+  unsigned long long *stamps;  // diagnostics: [grid][16] wall-clock stamps (NULL: off)
+  int store_mode;  // tower_store (MREC_TOWER_STORE)
+};
+
+__host__ __device__ __forceinline__ int tw_ceil(int a, int b) { return (a + b - 1) / b; }
+// readable columns of a block: whole k steps of 32
+__host__ __device__ __forceinline__ int tw_cols(int w) { return tw_ceil(w, 32) * 32; }
+// row stride: the readable columns rounded up to 32 (mod 256) bytes
+__host__ __device__ __forceinline__ int tw_stride(int w) {
+  return tw_ceil(tw_cols(w) * 2 - 32, 256) * 256 + 32;
+}
+
+__device__ __forceinline__ bool bf16_pos(uint32_t h) { return h != 0u && !(h & 0x8000u); }
+
+typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
+
+// The MFMA main loop of one layer for a wave with NT real output tiles and G
+// groups of PF k steps (both compile-time: the loop is straight-line code, so the
+// compiler's vmcnt accounting keeps (PF - 1) * NT weight fragments in flight
+// instead of draining at a loop header).  Weight fragments come in by buffer
+// loads: voffset = the lane's slot of the tile, soffset = the k step
+// (wave-uniform); a step past `ksteps` uses soffset = the image size, which the
+// descriptor's range check turns into zeros (their MFMAs add nothing).  One
+// sched_barrier per step keeps the refill loads right behind the step's MFMAs.
+// Every workgroup streams the same weight image; starting each at its own k step
+// (rot = blockIdx % ksteps, the steps taken cyclically) spreads the CUs of an XCD
+// over the image's lines instead of having them all request the same L2 lines at
+// once.  (A different fp32 summation order per workgroup; deterministic.)
+__device__ __forceinline__ int tw_rot(int s, int rot, int ksteps) {
+  if (s >= ksteps) return 0;  // padded step: the range check zeroes its weights (any finite B)
+  const int r = s + rot;
+  return r >= ksteps ? r - ksteps : r;
+}
+
+template <int NT, int G, int TW_PF>
+__device__ __forceinline__ void tower_mfma_g(f32x4 (&acc)[TW_TPW], __amdgpu_buffer_rsrc_t rsrc,
+                                             const int (&voff)[TW_TPW], int img_bytes,
+                                             const char *brow, int ksteps, int rot) {
+  bf16x8 wfr[TW_PF][NT];
+#pragma unroll
+  for (int p = 0; p < TW_PF; ++p) {
+    const int so = p < ksteps ? tw_rot(p, rot, ksteps) * 1024 : img_bytes;
+#pragma unroll
+    for (int i = 0; i < NT; ++i)
+      wfr[p][i] = __builtin_bit_cast(bf16x8, __builtin_amdgcn_raw_buffer_load_b128(rsrc, voff[i], so, 0));
+  }
+#pragma unroll
+  for (int s = 0; s < G * TW_PF; ++s) {
+    const int p = s % TW_PF;
+    const bf16x8 b = *reinterpret_cast<const bf16x8 *>(brow + tw_rot(s, rot, ksteps) * 64);
+#pragma unroll
+    for (int i = 0; i < NT; ++i)
+      acc[i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wfr[p][i], b, acc[i], 0, 0, 0);
+    const int sn = s + TW_PF;
+    if (sn < G * TW_PF) {  // compile-time
+      const int so = sn < ksteps ? tw_rot(sn, rot, ksteps) * 1024 : img_bytes;
+#pragma unroll
+      for (int i = 0; i < NT; ++i)
+        wfr[p][i] = __builtin_bit_cast(bf16x8, __builtin_amdgcn_raw_buffer_load_b128(rsrc, voff[i], so, 0));
+    }
+    __builtin_amdgcn_sched_barrier(0);
+  }
+}
+
+// dispatch on the number of PF-step groups (ksteps <= 16: widths <= 512)
+template <int NT, int TW_PF, int G = 1>
+__device__ __forceinline__ void tower_mfma(f32x4 (&acc)[TW_TPW], __amdgpu_buffer_rsrc_t rsrc,
+                                           const int (&voff)[TW_TPW], int img_bytes,
+                                           const char *brow, int ksteps, int rot) {
+  if constexpr (G * TW_PF >= 16) {
+    tower_mfma_g<NT, G, TW_PF>(acc, rsrc, voff, img_bytes, brow, ksteps, rot);
+  } else {
+    if (ksteps <= G * TW_PF)
+      tower_mfma_g<NT, G, TW_PF>(acc, rsrc, voff, img_bytes, brow, ksteps, rot);
+    else
+      tower_mfma<NT, TW_PF, G + 1>(acc, rsrc, voff, img_bytes, brow, ksteps, rot);
+  }
+}
+
+// One layer on the MFMA pipe: out[m][c] for the wave's output tiles c in
+// [16 t, 16 t + 16), t = wave + 8 i, from `in` (LDS block, k steps of 32) and the
+// A-operand image (tiles x ksteps blocks of 1 KiB).  Epilogue per element:
+//   FWD: relu(acc + bias[c]) (c < width_out, else 0);
+//   BWD: acc, times [mask[m][c] > 0] when mask != NULL.
+// Tiles in [ntiles, 2 ceil(width_out / 32)) are written as zeros (the next
+// layer reads whole k steps of 32).
+template <bool BWD, int TW_PF>
+__device__ __forceinline__ void tower_layer(const uint16_t *__restrict__ img, int img_bytes,
+                                            int ksteps, int width_out, const char *in, int s_in, char *out,
+                                            int s_out, const float *__restrict__ bias,
+                                            const char *mask, int s_mask, int rotate) {
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int g = lane >> 4, r16 = lane & 15;
+  const int ntiles = tw_ceil(width_out, 16);
+  const int ztiles = 2 * tw_ceil(width_out, 32);
+  int nreal = 0;
+#pragma unroll
+  for (int i = 0; i < TW_TPW; ++i) nreal += (wave + TW_WAVES * i < ntiles) ? 1 : 0;
+
+  int voff[TW_TPW];  // byte offset of this lane's 16 B in step 0 of each tile
+#pragma unroll
+  for (int i = 0; i < TW_TPW; ++i) voff[i] = ((wave + TW_WAVES * i) * ksteps * 512 + lane * 8) * 2;
+  const __amdgpu_buffer_rsrc_t rsrc =
+      __builtin_amdgcn_make_buffer_rsrc(const_cast<uint16_t *>(img), 0, img_bytes, 0x00020000);
+
+  f32x4 acc[TW_TPW];
+#pragma unroll
+  for (int i = 0; i < TW_TPW; ++i) acc[i] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  const char *brow = in + r16 * s_in + g * 16;
+  const int rot = rotate ? static_cast<int>(blockIdx.x % static_cast<unsigned>(ksteps)) : 0;
+  switch (nreal) {  // uniform per wave
+    case 4: tower_mfma<4, TW_PF>(acc, rsrc, voff, img_bytes, brow, ksteps, rot); break;
+    case 3: tower_mfma<3, TW_PF>(acc, rsrc, voff, img_bytes, brow, ksteps, rot); break;
+    case 2: tower_mfma<2, TW_PF>(acc, rsrc, voff, img_bytes, brow, ksteps, rot); break;
+    case 1: tower_mfma<1, TW_PF>(acc, rsrc, voff, img_bytes, brow, ksteps, rot); break;
+    default: break;
+  }
+
+  // epilogue: lane holds rows c = 16 t + 4 g + r (r = 0..3) of column m = r16
+#pragma unroll
+  for (int i = 0; i < TW_TPW; ++i) {
+    const int t = wave + TW_WAVES * i;
+    if (t >= ztiles) break;  // uniform
+    const int c0 = 16 * t + 4 * g;
+    float v[4] = {0.f, 0.f, 0.f, 0.f};
+    if (t < ntiles) {
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int c = c0 + r;
+        float x = acc[i][r];
+        if constexpr (!BWD) {
+          x = c < width_out ? fmaxf(x + (bias ? bias[c] : 0.f), 0.f) : 0.f;
+        }
+        v[r] = x;
+      }
+      if (BWD && mask) {
+        const uint2 mk = *reinterpret_cast<const uint2 *>(mask + r16 * s_mask + c0 * 2);
+        if (!bf16_pos(mk.x & 0xffffu)) v[0] = 0.f;
+        if (!bf16_pos(mk.x >> 16)) v[1] = 0.f;
+        if (!bf16_pos(mk.y & 0xffffu)) v[2] = 0.f;
+        if (!bf16_pos(mk.y >> 16)) v[3] = 0.f;
+      }
+    }
+    *reinterpret_cast<uint2 *>(out + r16 * s_out + c0 * 2) =
+        make_uint2(pack_bf16x2(v[0], v[1]), pack_bf16x2(v[2], v[3]));
+  }
+}
+
+// rows [0, 16) of an LDS block -> global bf16 [B, ld], columns [0, round8(width)).
+// store_mode 1 (default): sc1 write-through stores, which do not keep the line in
+// the XCD's L2 (MI355X_MICROARCH.md, store flavours), so the ~2.5 MB of
+// activation / gradient rows an XCD writes per launch do not evict the weight
+// images every workgroup re-reads; 0: plain stores; 2: no stores (timing only).
+__device__ __forceinline__ void tower_store(const char *blk, int s_blk, int width, uint16_t *dst,
+                                            int64_t ld, int64_t row0, int64_t B, int store_mode) {
+  if (!dst || store_mode == 2) return;
+  const int chunks = tw_ceil(width, 8);
+  const int rows = static_cast<int>(min<int64_t>(TW_ROWS, B - row0));
+  const __amdgpu_buffer_rsrc_t rsrc = __builtin_amdgcn_make_buffer_rsrc(
+      dst + row0 * ld, 0, static_cast<int>(rows * ld * 2), 0x00020000);
+  for (int i = threadIdx.x; i < TW_ROWS * chunks; i += TW_THREADS) {
+    const int r = i / chunks, c = i - r * chunks;
+    if (r < rows) {
+      const u32x4 v = *reinterpret_cast<const u32x4 *>(blk + r * s_blk + c * 16);
+      const int off = static_cast<int>((r * ld + c * 8) * 2);
+      if (store_mode == 1)
+        __builtin_amdgcn_raw_buffer_store_b128(v, rsrc, off, 0, 16);
+      else
+        __builtin_amdgcn_raw_buffer_store_b128(v, rsrc, off, 0, 0);
+    }
+  }
+}
+
+// diagnostics: stamps go to LDS (a global store before a barrier would be waited
+// for by it) and leave at the end of the workgroup
+#define TW_STAMP(k)                                                                  \
+  do {                                                                               \
+    if (a.stamps && tid == 0) s_stamp[(k)] = wall_clock64();                         \
+  } while (0)
+
+template <int TW_PF>
+__global__ __launch_bounds__(TW_THREADS) void tower_kernel(TowerArgs a) {
+  extern __shared__ __attribute__((aligned(16))) char lds[];
+  const int tid = threadIdx.x, lane = tid & 63;
+  __shared__ unsigned long long s_stamp[16];
+  TW_STAMP(0);
+  const int64_t row0 = static_cast<int64_t>(blockIdx.x) * TW_ROWS;
+  const int L = a.L;
+
+  // ---- prologue: x0 rows into registers, zero LDS, stage the small parameters,
+  // then x0 into its block (the loads' latency overlaps the fills) ------------
+  const int xchunks = tw_ceil(a.width[0], 8);
+  uint4 xr[2];
+#pragma unroll
+  for (int q = 0; q < 2; ++q) {
+    const int i = tid + q * TW_THREADS;
+    const int r = i / xchunks, c = i - r * xchunks;
+    xr[q] = (i < TW_ROWS * xchunks && row0 + r < a.B)
+                ? *reinterpret_cast<const uint4 *>(a.x0 + (row0 + r) * a.ld_x0 + c * 8)
+                : make_uint4(0u, 0u, 0u, 0u);
+  }
+  for (int i = tid * 16; i < a.off_p; i += TW_THREADS * 16)
+    *reinterpret_cast<uint4 *>(lds + i) = make_uint4(0u, 0u, 0u, 0u);
+  float *prm = reinterpret_cast<float *>(lds + a.off_p);
+  {
+    const int H = a.width[L];
+    for (int l = 0; l < L; ++l)
+      for (int c = tid; c < a.width[l + 1]; c += TW_THREADS)
+        prm[a.p_bias[l] + c] = a.bias[l] ? a.bias[l][c] : 0.f;
+    for (int c = tid; c < H; c += TW_THREADS) prm[a.p_hw + c] = a.head_w[c];
+    for (int c = tid; c < a.ns; c += TW_THREADS) prm[a.p_ws + c] = a.ws[c];
+    if (tid == 0) prm[a.p_b0] = (a.head_b ? a.head_b[0] : 0.f) + (a.b2 ? a.b2[0] : 0.f);
+    if (tid < TW_ROWS) {
+      const bool ok = row0 + tid < a.B;
+      prm[a.p_y + tid] = ok ? a.y[row0 + tid] : 0.f;
+      prm[a.p_base + tid] = (ok && a.base) ? a.base[row0 + tid] : 0.f;
+    }
+    for (int i = tid; i < TW_ROWS * a.ns; i += TW_THREADS) {
+      const int r = i / a.ns, j = i - r * a.ns;
+      prm[a.p_xs + i] = row0 + r < a.B ? a.xs[(row0 + r) * a.ld_xs + j] : 0.f;
+    }
+  }
+  __syncthreads();
+#pragma unroll
+  for (int q = 0; q < 2; ++q) {
+    const int i = tid + q * TW_THREADS;
+    const int r = i / xchunks, c = i - r * xchunks;
+    if (i < TW_ROWS * xchunks)
+      *reinterpret_cast<uint4 *>(lds + a.off_x + r * a.s_x + c * 16) = xr[q];
+  }
+  __syncthreads();
+  TW_STAMP(1);
+
+  // ---- forward: h_l = relu(h_{l-1} W_l^T + b_l) --------------------------------
+  for (int l = 0; l < L; ++l) {
+    const char *in = lds + (l == 0 ? a.off_x : a.off_h[l - 1]);
+    const int s_in = l == 0 ? a.s_x : a.s_h[l - 1];
+    tower_layer<false, TW_PF>(a.wf[l], a.wf_bytes[l], tw_ceil(a.width[l], 32), a.width[l + 1], in, s_in,
+                       lds + a.off_h[l], a.s_h[l], prm + a.p_bias[l], nullptr, 0, a.rotate);
+    __syncthreads();
+    TW_STAMP(2 + l);
+    if (l + 1 < L) tower_store(lds + a.off_h[l], a.s_h[l], a.width[l + 1], a.h_out[l], a.ld_h[l],
+                               row0, a.B, a.store_mode);
+  }
+
+  // ---- head + BCE: thread (m = tid / 32, c = tid % 32), parameters from LDS ----
+  // (results go to LDS first: a barrier behind global stores would wait for them)
+  const int H = a.width[L];
+  const char *hL = lds + a.off_h[L - 1];
+  const int s_hL = a.s_h[L - 1];
+  float *f_dz = reinterpret_cast<float *>(lds + a.off_f);
+  float *f_loss = f_dz + TW_ROWS;
+  float *f_z = prm + a.p_z;
+  float *f_part = prm + a.p_part;
+  const float *hw = prm + a.p_hw;
+  {
+    const int m = tid >> 5, c = tid & 31;
+    const bool ok = row0 + m < a.B;
+    float dot = 0.f;
+    for (int j = c; j * 8 < H; j += 32) {
+      const uint4 hv = *reinterpret_cast<const uint4 *>(hL + m * s_hL + j * 16);
+      float hf[8];
+      Vec<uint16_t>::to_f32(hv, hf);
+#pragma unroll
+      for (int q = 0; q < 8; ++q) {
+        const int n = j * 8 + q;
+        dot = fmaf(hf[q], n < H ? hw[n] : 0.f, dot);
+      }
+    }
+    for (int j = c; j < a.ns; j += 32) dot = fmaf(prm[a.p_xs + m * a.ns + j], prm[a.p_ws + j], dot);
+#pragma unroll
+    for (int off = 16; off > 0; off >>= 1) dot += __shfl_xor(dot, off);
+    if (c == 0) {
+      float d = 0.f, lo = 0.f, zz = 0.f;
+      if (ok) {
+        zz = dot + prm[a.p_b0] + prm[a.p_base + m];
+        const float yy = prm[a.p_y + m];
+        d = (1.f / (1.f + __expf(-zz)) - yy) * a.invB;
+        lo = fmaxf(zz, 0.f) - zz * yy + log1pf(__expf(-fabsf(zz)));
+      }
+      f_dz[m] = d;
+      f_loss[m] = lo;
+      f_z[m] = zz;
+    }
+  }
+  __syncthreads();
+  // dh_L = dz * head_w * [h_L > 0] -> gradient block 0
+  {
+    char *g0 = lds + a.off_g[0];
+    const int m = tid >> 5, c = tid & 31;
+    const float d = f_dz[m];
+    for (int j = c; j * 8 < H; j += 32) {
+      const uint4 hv = *reinterpret_cast<const uint4 *>(hL + m * s_hL + j * 16);
+      const uint32_t hwd[4] = {hv.x, hv.y, hv.z, hv.w};
+      float gv[8];
+#pragma unroll
+      for (int q = 0; q < 8; ++q) {
+        const int n = j * 8 + q;
+        const uint32_t hb = (q & 1) ? (hwd[q >> 1] >> 16) : (hwd[q >> 1] & 0xffffu);
+        gv[q] = (n < H && bf16_pos(hb)) ? d * hw[n] : 0.f;
+      }
+      *reinterpret_cast<uint4 *>(g0 + m * a.s_g + j * 16) =
+          make_uint4(pack_bf16x2(gv[0], gv[1]), pack_bf16x2(gv[2], gv[3]),
+                     pack_bf16x2(gv[4], gv[5]), pack_bf16x2(gv[6], gv[7]));
+    }
+  }
+  // head-parameter partials: [sum_m dz_m h_L[m] | sum dz | sum_m dz_m xs[m]]
+  for (int c = tid; c < H + 1 + a.ns; c += TW_THREADS) {
+    float sacc = 0.f;
+    if (c < H) {
+      for (int m = 0; m < TW_ROWS; ++m)
+        sacc = fmaf(f_dz[m], bf16_to_f32(*reinterpret_cast<const uint16_t *>(hL + m * s_hL + c * 2)), sacc);
+    } else if (c == H) {
+      for (int m = 0; m < TW_ROWS; ++m) sacc += f_dz[m];
+    } else {
+      const int j = c - H - 1;
+      for (int m = 0; m < TW_ROWS; ++m) sacc = fmaf(f_dz[m], prm[a.p_xs + m * a.ns + j], sacc);
+    }
+    f_part[c] = sacc;
+  }
+  __syncthreads();
+  TW_STAMP(6);
+  // now the global stores, behind the backward's first weight stream
+  {
+    float *prow = a.part + static_cast<int64_t>(blockIdx.x) * a.ldp;
+    for (int c = tid; c < H + 1 + a.ns; c += TW_THREADS) prow[c] = f_part[c];
+    if (tid < TW_ROWS && row0 + tid < a.B) {
+      a.dz[row0 + tid] = f_dz[tid];
+      if (a.z) a.z[row0 + tid] = f_z[tid];
+    }
+  }
+  tower_store(lds + a.off_g[0], a.s_g, H, a.dh_out[L - 1], a.ld_dh[L - 1], row0, a.B, a.store_mode);
+
+  // ---- backward: dh_{l-1} = (dh_l W_l) * [h_{l-1} > 0], dx0 = dh_1 W_1 ----------
+  __shared__ unsigned s_last;
+  int cur = 0;
+  for (int l = L - 1; l >= 0; --l) {
+    const char *gin = lds + a.off_g[cur];
+    char *gout = lds + a.off_g[cur ^ 1];
+    const char *mask = l > 0 ? lds + a.off_h[l - 1] : nullptr;
+    const int s_mask = l > 0 ? a.s_h[l - 1] : 0;
+    tower_layer<true, TW_PF>(a.wb[l], a.wb_bytes[l], tw_ceil(a.width[l + 1], 32), a.width[l], gin, a.s_g, gout, a.s_g,
+                      nullptr, mask, s_mask, a.rotate);
+    __syncthreads();
+    TW_STAMP(7 + (L - 1 - l));
+    if (l > 0) {
+      tower_store(gout, a.s_g, a.width[l], a.dh_out[l - 1], a.ld_dh[l - 1], row0, a.B, a.store_mode);
+    } else {
+      // the loss: this workgroup's partial as a write-through granule + a relaxed
+      // agent ticket (cdna_hip_programming.md §6 G16), before the dx0 stores so the
+      // wait drains little; the last arriver sums the partials below
+      if (tid == 0) {
+        float lp = 0.f;
+        for (int m = 0; m < TW_ROWS; ++m) lp += f_loss[m];
+        __hip_atomic_store(a.loss_part + blockIdx.x, lp, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        const unsigned old = __hip_atomic_fetch_add(a.ticket, 1u, __ATOMIC_RELAXED,
+                                                    __HIP_MEMORY_SCOPE_AGENT);
+        s_last = old == gridDim.x - 1 ? 1u : 0u;
+      }
+      tower_store(gout, a.s_g, a.width[0], a.dx0, a.ld_dx0, row0, a.B, a.store_mode);
+    }
+    cur ^= 1;
+  }
+
+  // ---- the last ticket holder sums the loss partials (fixed order) ------------------
+  TW_STAMP(11);
+  __syncthreads();
+  if (tid == 0 && s_last) {
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __hip_atomic_store(a.ticket, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+  __syncthreads();
+  TW_STAMP(12);
+  if (a.stamps && tid < 13) a.stamps[blockIdx.x * 16 + tid] = s_stamp[tid];
+  if (!s_last) return;
+  float t = 0.f;
+  for (unsigned k = tid; k < gridDim.x; k += TW_THREADS)
+    t += __hip_atomic_load(a.loss_part + k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) t += __shfl_xor(t, off);
+  float *wsum = f_loss;  // 8 waves (the per-row losses are no longer needed)
+  __syncthreads();
+  if (lane == 0) wsum[tid >> 6] = t;
+  __syncthreads();
+  if (tid == 0) {
+    float s = 0.f;
+    for (int w = 0; w < TW_WAVES; ++w) s += wsum[w];
+    a.loss[0] = s * a.invB;
+  }
+}
+
+// ---------------------------------------------------------------------------
+// image prep: fp32 W [N, K] -> tower fwd / bwd images (real elements only)
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void tower_prep_kernel(const float *__restrict__ W, int64_t N,
+                                                         int64_t K, int64_t ldw,
+                                                         uint16_t *__restrict__ pf,
+                                                         uint16_t *__restrict__ pb) {
+  const int64_t i = static_cast<int64_t>(blockIdx.x) * 256 + threadIdx.x;
+  if (i >= N * K) return;
+  const int64_t n = i / K, k = i - n * K;
+  const uint16_t h = f32_to_bf16_rne(W[n * ldw + k]);
+  if (pf) pf[tower_idx_fwd(n, k, K)] = h;
+  if (pb) pb[tower_idx_bwd(n, k, N)] = h;
+}
+
+static unsigned long long *g_tower_stamps = nullptr;  // mrec_tower_debug_stamps
+
+static bool al16(const void *p, int64_t ld) {
+  return p && (reinterpret_cast<uintptr_t>(p) & 15) == 0 && ld % 8 == 0;
+}
+
+}  // namespace mrec
+
+using namespace mrec;
+
+extern "C" {
+
+// diagnostics (not in mrec.h): route per-workgroup phase stamps ([grid][16] uint64,
+// 100 MHz wall clock) of the next tower launches to `buf` (NULL: off)
+void mrec_tower_debug_stamps(void *buf) { g_tower_stamps = static_cast<unsigned long long *>(buf); }
+
+int64_t mrec_tower_image_elems(int64_t N, int64_t K, int32_t bwd) {
+  return bwd ? tower_img_elems_bwd(N, K) : tower_img_elems_fwd(N, K);
+}
+
+mrec_status mrec_tower_weight_prep(const float *W, int64_t N, int64_t K, int64_t ldw,
+                                   void *img_fwd, void *img_bwd, mrec_stream stream) {
+  MREC_CHECK_ARG(W && (img_fwd || img_bwd), "NULL pointer");
+  MREC_CHECK_ARG(N >= 0 && K >= 0 && ldw >= K, "bad shape");
+  if (N == 0 || K == 0) return MREC_OK;
+  const int64_t n = N * K;
+  tower_prep_kernel<<<dim3(static_cast<unsigned>((n + 255) / 256)), 256, 0,
+                      static_cast<hipStream_t>(stream)>>>(W, N, K, ldw,
+                                                          static_cast<uint16_t *>(img_fwd),
+                                                          static_cast<uint16_t *>(img_bwd));
+  return launch_status("mrec_tower_weight_prep");
+}
+
+mrec_status mrec_tower_fwd_bwd(const mrec_tower_args *p, mrec_stream stream) {
+  MREC_CHECK_ARG(p != nullptr, "NULL args");
+  const mrec_tower_args &s = *p;
+  MREC_CHECK_ARG(s.batch >= 0, "negative batch");
+  MREC_CHECK_ARG(s.n_layers >= 1 && s.n_layers <= TW_MAXL, "n_layers must be in [1, 4]");
+  const int L = s.n_layers;
+  for (int l = 0; l <= L; ++l)
+    MREC_CHECK_ARG(s.width[l] >= 1 && s.width[l] <= TW_MAXW, "every width must be in [1, 512]");
+  MREC_CHECK_ARG(al16(s.x0, s.ld_x0) && s.ld_x0 >= (s.width[0] + 7) / 8 * 8,
+                 "x0 rows must be 16-B aligned with ld_x0 >= round8(width[0])");
+  for (int l = 0; l < L; ++l) {
+    MREC_CHECK_ARG(s.w_fwd[l] && s.w_bwd[l], "NULL weight image");
+    const int w = s.width[l + 1];
+    MREC_CHECK_ARG(al16(s.dh_out[l], s.ld_dh[l]) && s.ld_dh[l] >= (w + 7) / 8 * 8,
+                   "dh_out rows must be 16-B aligned with ld >= round8(width)");
+    if (l + 1 < L && s.h_out[l])
+      MREC_CHECK_ARG(al16(s.h_out[l], s.ld_h[l]) && s.ld_h[l] >= (w + 7) / 8 * 8,
+                     "h_out rows must be 16-B aligned with ld >= round8(width)");
+  }
+  MREC_CHECK_ARG(!s.dx0 || (al16(s.dx0, s.ld_dx0) && s.ld_dx0 >= (s.width[0] + 7) / 8 * 8),
+                 "dx0 rows must be 16-B aligned with ld >= round8(width[0])");
+  MREC_CHECK_ARG(s.head_w && s.y && s.dz && s.part && s.loss_part && s.ticket && s.loss,
+                 "NULL head / loss pointer");
+  MREC_CHECK_ARG(s.ns >= 0 && s.ns <= TW_MAXNS && (s.ns == 0 || (s.xs && s.ws)),
+                 "side linear: ns in [0, 64] with xs and ws");
+  MREC_CHECK_ARG(s.ldp >= s.width[L] + 1 + s.ns, "ldp < N_L + 1 + ns");
+  if (s.batch == 0) return MREC_OK;
+
+  TowerArgs a{};
+  a.B = s.batch;
+  a.L = L;
+  for (int l = 0; l <= L; ++l) a.width[l] = s.width[l];
+  a.x0 = static_cast<const uint16_t *>(s.x0);
+  a.ld_x0 = s.ld_x0;
+  int wmax = s.width[0];
+  for (int l = 0; l < L; ++l) {
+    a.wf[l] = static_cast<const uint16_t *>(s.w_fwd[l]);
+    a.wb[l] = static_cast<const uint16_t *>(s.w_bwd[l]);
+    a.wf_bytes[l] = static_cast<int>(tower_img_elems_fwd(s.width[l + 1], s.width[l]) * 2);
+    a.wb_bytes[l] = static_cast<int>(tower_img_elems_bwd(s.width[l + 1], s.width[l]) * 2);
+    a.bias[l] = s.bias[l];
+    a.h_out[l] = static_cast<uint16_t *>(s.h_out[l]);
+    a.ld_h[l] = s.ld_h[l];
+    a.dh_out[l] = static_cast<uint16_t *>(s.dh_out[l]);
+    a.ld_dh[l] = s.ld_dh[l];
+    wmax = std::max(wmax, s.width[l + 1]);
+  }
+  a.head_w = s.head_w;
+  a.head_b = s.head_b;
+  a.base = s.base;
+  a.xs = s.xs;
+  a.ld_xs = s.ld_xs;
+  a.ns = s.ns;
+  a.ws = s.ws;
+  a.b2 = s.b2;
+  a.y = s.y;
+  a.dx0 = static_cast<uint16_t *>(s.dx0);
+  a.ld_dx0 = s.ld_dx0;
+  a.z = s.z;
+  a.dz = s.dz;
+  a.part = s.part;
+  a.ldp = s.ldp;
+  a.loss_part = s.loss_part;
+  a.ticket = s.ticket;
+  a.loss = s.loss;
+  a.invB = 1.f / static_cast<float>(s.batch);
+  static const int rot_env = [] {
+    const char *e = getenv("MREC_TOWER_ROT");
+    return (e && e[0] == '0') ? 0 : 1;
+  }();
+  a.rotate = rot_env;
+  a.stamps = g_tower_stamps;
+  static const int store_env = [] {
+    const char *e = getenv("MREC_TOWER_STORE");
+    return e ? atoi(e) : 1;
+  }();
+  a.store_mode = store_env;
+  int off = 0;
+  a.off_x = off;
+  a.s_x = tw_stride(s.width[0]);
+  off += TW_ROWS * a.s_x;
+  for (int l = 0; l < L; ++l) {
+    a.off_h[l] = off;
+    a.s_h[l] = tw_stride(s.width[l + 1]);
+    off += TW_ROWS * a.s_h[l];
+  }
+  a.s_g = tw_stride(wmax);
+  a.off_g[0] = off;
+  off += TW_ROWS * a.s_g;
+  a.off_g[1] = off;
+  off += TW_ROWS * a.s_g;
+  a.off_f = off;
+  off += 2 * TW_ROWS * 4;
+  off = (off + 15) / 16 * 16;
+  a.off_p = off;  // everything before off_p is zero-filled by the kernel
+  int np = 0;
+  for (int l = 0; l < L; ++l) {
+    a.p_bias[l] = np;
+    np += s.width[l + 1];
+  }
+  a.p_hw = np;
+  np += s.width[L];
+  a.p_ws = np;
+  np += s.ns;
+  a.p_b0 = np;
+  np += 1;
+  a.p_y = np;
+  np += TW_ROWS;
+  a.p_base = np;
+  np += TW_ROWS;
+  a.p_xs = np;
+  np += TW_ROWS * s.ns;
+  a.p_z = np;
+  np += TW_ROWS;
+  a.p_part = np;
+  np += s.width[L] + 1 + s.ns;
+  off += np * 4;
+  a.lds_bytes = (off + 15) / 16 * 16;
+  constexpr int kMaxDyn = 160 * 1024 - 256;  // the kernel's static LDS (s_last) is on top
+  MREC_CHECK_ARG(a.lds_bytes <= kMaxDyn, "activation blocks exceed the 160 KiB LDS");
+  static int attr_set = [] {
+    for (const void *k : {reinterpret_cast<const void *>(tower_kernel<4>),
+                          reinterpret_cast<const void *>(tower_kernel<6>),
+                          reinterpret_cast<const void *>(tower_kernel<8>)})
+      (void)hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, kMaxDyn);
+    (void)hipGetLastError();  // a refused attribute must not read as a failed launch
+    return 1;
+  }();
+  (void)attr_set;
+  static const int pf_env = [] {  // MREC_TOWER_PF: weight k steps in flight per wave
+    const char *e = getenv("MREC_TOWER_PF");
+    const int v = e ? atoi(e) : TW_PF_DEFAULT;
+    return (v == 6 || v == 8) ? v : 4;
+  }();
+  const int64_t grid = (s.batch + TW_ROWS - 1) / TW_ROWS;
+  const dim3 gd(static_cast<unsigned>(grid));
+  hipStream_t st = static_cast<hipStream_t>(stream);
+  if (pf_env == 8)
+    tower_kernel<8><<<gd, TW_THREADS, a.lds_bytes, st>>>(a);
+  else if (pf_env == 6)
+    tower_kernel<6><<<gd, TW_THREADS, a.lds_bytes, st>>>(a);
+  else
+    tower_kernel<4><<<gd, TW_THREADS, a.lds_bytes, st>>>(a);
+  return launch_status("mrec_tower_fwd_bwd");
+}
+
+}  // extern "C"

@@ -90,7 +90,7 @@ def _is_relu_out(x: torch.Tensor) -> bool:
 
 def gemm(A, a_layout, B, b_layout, M, N, K, *, ones_out=None, b_cols=None, bias=None, act=0,
          mul=None, add=None, aux=None, mask=None, out=None, out_dtype=_BF16, split_k=None,
-         sgd_lr=None, img_row=None, img_tr=None):
+         sgd_lr=None, img_row=None, img_tr=None, img_kind=0):
     """C[M, N] = epi(A[M, K] @ B[K, N]) on libmrec (see include/mrec.h mrec_gemm).
     ``ones_out`` (fp32 [M]) receives sum_k A(m, k) through an appended ones column;
     ``mask`` ([M, N] bf16) zeroes outputs where mask <= 0 (ReLU')."""
@@ -108,7 +108,8 @@ def gemm(A, a_layout, B, b_layout, M, N, K, *, ones_out=None, b_cols=None, bias=
                          _mrec.ptr(ones_out), int(sgd_lr is not None),
                          float(sgd_lr) if sgd_lr is not None else 0.0,
                          _mrec.ptr(img_row), img_row.stride(0) if img_row is not None else 0,
-                         _mrec.ptr(img_tr), img_tr.stride(0) if img_tr is not None else 0)
+                         _mrec.ptr(img_tr), img_tr.stride(0) if img_tr is not None else 0,
+                         img_kind)
     a_op, b_op = _op(A, a_layout), _op(B, b_layout)
     _mrec.call("mrec_gemm", M, N, K, ctypes.byref(a_op), ctypes.byref(b_op),
                N if ones_out is not None else -1, N if b_cols is None else b_cols,
@@ -123,7 +124,7 @@ class _Call:
 
     def __init__(self, A, a_layout, B, b_layout, M, N, K, phase, *, ones_out=None, b_cols=None,
                  mask=None, out=None, out_dtype=_BF16, split_k=1, sgd_lr=None, img_row=None,
-                 img_tr=None, ws=None, add=None):
+                 img_tr=None, ws=None, add=None, img_kind=0):
         dev = A.device
         if out is None:
             out = _alloc(M, N, out_dtype, dev)
@@ -138,7 +139,8 @@ class _Call:
                                   _mrec.ptr(ones_out), int(sgd_lr is not None),
                                   float(sgd_lr) if sgd_lr is not None else 0.0,
                                   _mrec.ptr(img_row), img_row.stride(0) if img_row is not None else 0,
-                                  _mrec.ptr(img_tr), img_tr.stride(0) if img_tr is not None else 0)
+                                  _mrec.ptr(img_tr), img_tr.stride(0) if img_tr is not None else 0,
+                                  img_kind)
         self.a, self.b = _op(A, a_layout), _op(B, b_layout)
         self.args = (M, N, K, N if ones_out is not None else -1, N if b_cols is None else b_cols,
                      out.data_ptr(), _mrec.dtype_code(out.dtype), out.stride(0), split_k,
@@ -286,17 +288,66 @@ def weight_prep(W: torch.Tensor, row: bool = True, tr: bool = True):
     return wr, wt
 
 
+# bf16 images of an fp32 master weight, cached on the Parameter per kind:
+#   "rowtr": row-major W and W^T (operands of mrec_gemm);
+#   "tower": the MFMA-fragment images of the fused tower (mrec_tower_fwd_bwd).
+# An entry is valid while (weight._version, weight._mrec_gen) is unchanged: torch
+# modifying the weight bumps the version; a kernel updating it in place (fused
+# SGD) re-emits the images it was handed and ``images_updated`` bumps the
+# generation and re-stamps that kind, so only the other kind goes stale.
+_IMG_ATTR = {"rowtr": "_mrec_img", "tower": "_mrec_timg"}
+
+
+def _img_state(weight):
+    return weight._version, getattr(weight, "_mrec_gen", 0)
+
+
+def cached_images(weight: torch.Tensor, kind: str):
+    """The valid cached ``kind`` images of ``weight`` (a pair) or None."""
+    c = getattr(weight, _IMG_ATTR[kind], None)
+    if (c is not None and (c[0], c[1]) == _img_state(weight) and c[2].device == weight.device):
+        return c[2], c[3]
+    return None
+
+
+def images_updated(weight: torch.Tensor, kind: str):
+    """An in-place update of ``weight`` (fused SGD) has been enqueued that also
+    rewrites its ``kind`` images: they stay valid, every other kind is stale."""
+    gen = getattr(weight, "_mrec_gen", 0) + 1
+    weight._mrec_gen = gen
+    attr = _IMG_ATTR[kind]
+    c = getattr(weight, attr, None)
+    if c is not None:
+        setattr(weight, attr, (weight._version, gen) + tuple(c[2:]))
+
+
 def weight_images(weight: torch.Tensor):
     """(row, transposed) bf16 images of a Parameter, cached on it and rebuilt only
-    when torch modified the weight (version counter).  A fused SGD step rewrites the
-    images itself, in the same kernel that updates the fp32 weight."""
-    c = getattr(weight, "_mrec_img", None)
-    if (c is not None and c[0] == weight._version and c[1].device == weight.device
-            and c[1].shape[0] == weight.shape[0]):
-        return c[1], c[2]
+    when the weight changed since (see ``_IMG_ATTR``)."""
+    c = cached_images(weight, "rowtr")
+    if c is not None and c[0].shape[0] == weight.shape[0]:
+        return c
     wr, wt = weight_prep(weight)
-    weight._mrec_img = (weight._version, wr, wt)
+    weight._mrec_img = _img_state(weight) + (wr, wt)
     return wr, wt
+
+
+def tower_images(weight: torch.Tensor):
+    """(fwd, bwd) MFMA-fragment images of a Linear weight [N, K] for the fused
+    tower (csrc/tower_common.h), cached like ``weight_images``.  Zero-initialised:
+    the prep writes only real elements, the pad entries stay zero."""
+    c = cached_images(weight, "tower")
+    if c is not None:
+        return c
+    W = _weight_f32(weight)
+    N, K = W.shape
+    lib = _mrec.lib()
+    pf = torch.zeros(int(lib.mrec_tower_image_elems(N, K, 0)), dtype=_BF16, device=W.device)
+    pb = torch.zeros(int(lib.mrec_tower_image_elems(N, K, 1)), dtype=_BF16, device=W.device)
+    _mrec.call("mrec_tower_weight_prep", W.data_ptr(), N, K, W.stride(0), pf.data_ptr(),
+               pb.data_ptr(), _mrec.stream_handle())
+    weight._mrec_timg = _img_state(weight) + (pf, pb)
+    return pf, pb
 
 
 def sgd_lr(*params) -> Optional[float]:
@@ -412,6 +463,7 @@ class _LinearFn(torch.autograd.Function):
                             ones_out=ctx.bias.detach() if ctx.has_bias else None,
                             out=ctx.weight.detach(), out_dtype=torch.float32, split_k=sk,
                             sgd_lr=lr, img_row=ctx.wr, img_tr=ctx.wt)
+                images_updated(ctx.weight, "rowtr")
             if sk > 1:
                 launch_multi(calls + [cdw])
                 _defer(cdw)
@@ -494,6 +546,7 @@ class _CrossFn(torch.autograd.Function):
             gemm(dz, _mrec.LAYOUT_COL, xl, _mrec.LAYOUT_COL, d, d, M,
                  ones_out=ctx.bias.detach() if ctx.has_bias else None, out=ctx.weight.detach(),
                  out_dtype=torch.float32, sgd_lr=lr, img_row=ctx.wr, img_tr=ctx.wt)
+            images_updated(ctx.weight, "rowtr")
         else:
             dW = torch.empty(d, d, dtype=torch.float32, device=g.device)
             db = torch.empty(d, dtype=torch.float32, device=g.device) if ctx.has_bias else None
@@ -569,6 +622,7 @@ class _CrossNetFn(torch.autograd.Function):
                                 ones_out=b.detach() if b is not None else None, out=W.detach(),
                                 out_dtype=torch.float32, split_k=sk, sgd_lr=lr, img_row=wr,
                                 img_tr=wt)
+                    images_updated(W, "rowtr")
                 if sk > 1:
                     launch_multi([cdx, cdw])
                     _defer(cdw)
@@ -909,3 +963,209 @@ def ctr_head_bce(h: torch.Tensor, weight: torch.Tensor, bias: Optional[torch.Ten
     if b2 is not None:
         z = z + b2.float()
     return F.binary_cross_entropy_with_logits(z.float(), y.float()), z
+
+
+# ----------------------------------------------------------------------------
+# fused MLP tower + CTR head + BCE (mrec_tower_fwd_bwd)
+# ----------------------------------------------------------------------------
+
+TOWER = os.environ.get("MREC_TOWER", "1") == "1"
+TOWER_MAXL, TOWER_MAXW = 4, 512
+
+
+def _mlp_linears(mlp) -> list:
+    return [m.linear for m in mlp.mlp] if hasattr(mlp, "mlp") else list(mlp)
+
+
+def tower_supported(x0: torch.Tensor, mlp, head: torch.nn.Linear, xs=None) -> bool:
+    """The fused tower covers the reference MLP (Linear -> ReLU per layer,
+    Dense.py:4-24) with dropout 0 (or eval) + Linear(N_L, 1) + BCE on the GPU."""
+    if not (TOWER and x0.is_cuda and torch.is_grad_enabled() and x0.dtype == _BF16):
+        return False
+    dense_layers = list(mlp.mlp) if hasattr(mlp, "mlp") else None
+    if not dense_layers or len(dense_layers) > TOWER_MAXL:
+        return False
+    if any(d.dropout.p > 0 and d.training for d in dense_layers):
+        return False
+    lins = [d.linear for d in dense_layers]
+    widths = [lins[0].in_features] + [l.out_features for l in lins]
+    if any(w > TOWER_MAXW for w in widths) or head.out_features != 1:
+        return False
+    if any(l.weight.dtype != torch.float32 or not l.weight.is_contiguous() for l in lins):
+        return False
+    if xs is not None and xs.shape[1] > 64:
+        return False
+    return (x0.shape[1] >= widths[0] and x0.stride(1) == 1 and x0.stride(0) % 8 == 0
+            and x0.data_ptr() % 16 == 0)
+
+
+def _split_tower(tiles_total: int, K: int) -> int:
+    """K slices of the tower's weight-gradient GEMMs, which share one launch: about
+    two residency waves of 256-thread workgroups, slices of >= 256 rows."""
+    s = 1
+    while tiles_total * (s + 1) <= 640 and K // (s + 1) >= 256 and s < 64:
+        s += 1
+    return s
+
+
+class _TowerBCEFn(torch.autograd.Function):
+    """loss = BCEWithLogits(MLP(x0) . w + b + base [+ xs . ws + b2], y) (mean).
+    Forward = ONE mrec_tower_fwd_bwd launch, which also produces every input /
+    pre-activation gradient (dx0, dz, dh_l); backward = the weight-gradient GEMMs
+    (one mrec_gemm_multi launch with the head finish; fused SGD when compiled with
+    plain SGD, the split-K reductions ride in the next launch)."""
+
+    @staticmethod
+    def forward(ctx, x0, base, xs, y, n_layers, *params):
+        L = n_layers
+        Ws, bs = params[:L], params[L:2 * L]
+        head_w, head_b, ws, b2 = params[2 * L:2 * L + 4]
+        B = x0.shape[0]
+        dev = x0.device
+        widths = [Ws[0].shape[1]] + [W.shape[0] for W in Ws]
+        imgs = [tower_images(W) for W in Ws]
+        hs = [_alloc(B, widths[l + 1], _BF16, dev) for l in range(L - 1)]
+        dhs = [_alloc(B, widths[l + 1], _BF16, dev) for l in range(L)]
+        dx0 = None
+        if ctx.needs_input_grad[0]:  # x0's shape (it may carry zero pad columns past K0)
+            Kx = x0.shape[1]
+            dx0 = (_alloc(B, Kx, _BF16, dev) if _r8(Kx) == _r8(widths[0]) else
+                   torch.zeros(B, _r8(Kx), dtype=_BF16, device=dev)[:, :Kx])
+        dz = torch.empty(B, dtype=torch.float32, device=dev)
+        ns = 0 if xs is None else xs.shape[1]
+        if xs is not None:
+            xs = xs.detach().float()
+            if xs.stride(1) != 1:
+                xs = xs.contiguous()
+        H = widths[L]
+        nparts = int(_mrec.lib().mrec_ctr_head_parts(B))
+        ldp = _r8(H + 1 + ns)
+        part = torch.empty(nparts, ldp, dtype=torch.float32, device=dev)
+        loss_part = torch.empty(nparts, dtype=torch.float32, device=dev)
+        loss = torch.empty(1, dtype=torch.float32, device=dev)
+        f32 = lambda t: None if t is None else t.detach().float().contiguous()  # noqa: E731
+        hw, hb, wsd, b2d = f32(head_w).reshape(-1), f32(head_b), f32(ws), f32(b2)
+        bsd = [f32(b) for b in bs]
+        base_c = f32(base)
+        yc = y.detach().float().contiguous()
+        a = _mrec.TowerArgs()
+        a.batch, a.n_layers = B, L
+        for l in range(L + 1):
+            a.width[l] = widths[l]
+        a.x0, a.ld_x0 = x0.data_ptr(), x0.stride(0)
+        for l in range(L):
+            a.w_fwd[l], a.w_bwd[l] = imgs[l][0].data_ptr(), imgs[l][1].data_ptr()
+            a.bias[l] = _mrec.ptr(bsd[l])
+            a.dh_out[l], a.ld_dh[l] = dhs[l].data_ptr(), dhs[l].stride(0)
+            if l < L - 1:
+                a.h_out[l], a.ld_h[l] = hs[l].data_ptr(), hs[l].stride(0)
+        a.head_w, a.head_b, a.base = hw.data_ptr(), _mrec.ptr(hb), _mrec.ptr(base_c)
+        a.xs, a.ld_xs, a.ns = _mrec.ptr(xs), xs.stride(0) if xs is not None else 0, ns
+        a.ws, a.b2, a.y = _mrec.ptr(wsd), _mrec.ptr(b2d), yc.data_ptr()
+        a.dx0, a.ld_dx0 = _mrec.ptr(dx0), dx0.stride(0) if dx0 is not None else 0
+        a.z, a.dz = None, dz.data_ptr()
+        a.part, a.ldp = part.data_ptr(), ldp
+        a.loss_part, a.ticket, a.loss = loss_part.data_ptr(), _ticket(dev).data_ptr(), loss.data_ptr()
+        _mrec.call("mrec_tower_fwd_bwd", ctypes.byref(a), _mrec.stream_handle())
+        ctx.save_for_backward(x0, dz, part, dx0, *hs, *dhs)
+        ctx.L, ctx.B, ctx.H, ctx.ns, ctx.widths = L, B, H, ns, widths
+        ctx.Ws, ctx.bs, ctx.imgs = Ws, bs, imgs
+        ctx.head = (head_w, head_b, ws, b2)
+        ctx.has_base = base is not None
+        ctx.mark_non_differentiable(dz)
+        return loss.reshape(())
+
+    @staticmethod
+    def backward(ctx, gloss):
+        L, B = ctx.L, ctx.B
+        saved = ctx.saved_tensors
+        x0, dz, part, dx0 = saved[:4]
+        hs, dhs = list(saved[4:4 + L - 1]), list(saved[4 + L - 1:])
+        dev = part.device
+        g = gloss.detach().float().reshape(1).contiguous()
+        one = g.data_ptr() == grad_one(dev).data_ptr()
+        if not one:  # a scaled loss: every stashed gradient scales with it
+            dz = dz * g
+            dx0 = (dx0.float() * g).to(_BF16) if dx0 is not None else None
+            dhs = [_bf16_rows((d.float() * g).to(_BF16)) for d in dhs]
+        widths, Ws, bs = ctx.widths, ctx.Ws, ctx.bs
+        head_w, head_b, ws, b2 = ctx.head
+        xin = [x0[:, :widths[0]]] + hs
+        # --- weight gradients of the L layers: one launch ---
+        lr = sgd_lr(*Ws, *bs)
+        dpg = dp_grads(*Ws, *bs) if lr is None else None
+        need_w = any(ctx.needs_input_grad[5:5 + 2 * L])
+        dWs, dbs = [None] * L, [None] * L
+        calls = []
+        if need_w:
+            tiles = sum(((widths[l + 1] + 63) // 64) * ((widths[l] + 1 + 63) // 64) for l in range(L))
+            sk = _split_tower(tiles, B)
+            ph = _mrec.GEMM_PARTIAL if sk > 1 else _mrec.GEMM_FULL
+            for l in range(L):
+                N, K = widths[l + 1], widths[l]
+                bias_l = bs[l]
+                if lr is not None:
+                    c = _Call(dhs[l], _mrec.LAYOUT_COL, xin[l], _mrec.LAYOUT_COL, N, K, B, ph,
+                              ones_out=bias_l.detach() if bias_l is not None else None,
+                              out=Ws[l].detach(), out_dtype=torch.float32, split_k=sk, sgd_lr=lr,
+                              img_row=ctx.imgs[l][0], img_tr=ctx.imgs[l][1],
+                              img_kind=_mrec.IMG_TOWER)
+                    images_updated(Ws[l], "tower")
+                elif dpg is not None:
+                    c = _Call(dhs[l], _mrec.LAYOUT_COL, xin[l], _mrec.LAYOUT_COL, N, K, B, ph,
+                              ones_out=dpg[L + l], out=dpg[l], out_dtype=torch.float32,
+                              split_k=sk)
+                else:
+                    dWs[l] = torch.empty(N, K, dtype=torch.float32, device=dev)
+                    dbs[l] = (torch.empty(N, dtype=torch.float32, device=dev)
+                              if bias_l is not None else None)
+                    c = _Call(dhs[l], _mrec.LAYOUT_COL, xin[l], _mrec.LAYOUT_COL, N, K, B, ph,
+                              ones_out=dbs[l], out=dWs[l], out_dtype=torch.float32, split_k=sk)
+                calls.append(c)
+        # --- the head's parameters (w, b, ws, b2): fixed-order partial sums ---
+        hlr = sgd_lr(head_w, head_b, ws, b2)
+        det = (lambda t: None if t is None else t.detach())
+        hdp = dp_grads(head_w, head_b, ws, b2) if hlr is None else None
+        dW_h = db_h = dws = db2 = None
+        if hlr is not None and head_w.is_contiguous():
+            defer_head_finish(_HeadFinish(part, B, ctx.H, ctx.ns, None if one else g, hlr,
+                                          head_w.detach(), det(head_b), det(ws), det(b2)))
+        elif hdp is not None:
+            defer_head_finish(_HeadFinish(part, B, ctx.H, ctx.ns, None if one else g, None,
+                                          None, None, None, None, grads=hdp))
+        else:
+            f32 = dict(dtype=torch.float32, device=dev)
+            dW_h = torch.empty(1, ctx.H, **f32)
+            db_h = torch.empty(1, **f32) if head_b is not None else None
+            dws = torch.empty(ctx.ns, **f32) if ws is not None else None
+            db2 = torch.empty(1, **f32) if b2 is not None else None
+            _mrec.call("mrec_ctr_head_finish", part.data_ptr(), part.stride(0), B, ctx.H, ctx.ns,
+                       g.data_ptr(), 0, 0.0, None, None, None, None, dW_h.data_ptr(),
+                       _mrec.ptr(db_h), _mrec.ptr(dws), _mrec.ptr(db2), _mrec.stream_handle())
+        if calls:
+            launch_multi(calls)
+            if calls[0].args[8] > 1:  # split-K partial slabs: now the reductions
+                if lr is None and dpg is None:
+                    # returned gradients: autograd may copy them on return, so they must
+                    # be complete before this backward returns
+                    _run([c.with_phase(_mrec.GEMM_REDUCE) for c in calls])
+                else:  # in-place SGD / flat DP buffer: ride in the next launches
+                    for c in calls:
+                        _defer(c)
+        else:
+            _flush_finish()
+        return (dx0, dz if ctx.has_base else None, None, None, None, *dWs, *dbs,
+                dW_h, db_h, dws, db2)
+
+
+def tower_bce(x0: torch.Tensor, mlp, head: torch.nn.Linear, base: Optional[torch.Tensor],
+              y: torch.Tensor, xs: Optional[torch.Tensor] = None, ws: Optional[torch.Tensor] = None,
+              b2: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """Training loss of a CTR model's deep part: mean BCE-with-logits of
+    MLP(x0) . head.weight + head.bias + base (+ xs . ws + b2) — the reference MLP
+    (MLP.py:8-23) and Linear(N_L, 1) — as one fused tower launch (caller checks
+    ``tower_supported``)."""
+    lins = _mlp_linears(mlp)
+    params = ([l.weight for l in lins] + [l.bias for l in lins] +
+              [head.weight, head.bias, ws, b2])
+    return _TowerBCEFn.apply(x0, base, xs, y, len(lins), *params)

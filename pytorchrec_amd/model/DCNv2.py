@@ -68,19 +68,25 @@ class DCNv2(_CTRBase):
             for m in (self.cross, self.mlp, self.prediction):
                 m.to(dev)
 
-    def _deep(self, data: Dict[str, Tensor]):
+    def _cross(self, data: Dict[str, Tensor]):
         x0, _ = interact(self.embeddings, self._ids(data), self._dense(data), None, None,
                          fm2=False, first_order=False, x0_cols=self.x0_cols,
                          x0_dtype=self._x0_dtype())
-        x = dense_ops.cross_net(x0, [c.weight for c in self.cross], [c.bias for c in self.cross])
-        return self.mlp(x)
+        return dense_ops.cross_net(x0, [c.weight for c in self.cross], [c.bias for c in self.cross])
+
+    def _deep(self, data: Dict[str, Tensor]):
+        return self.mlp(self._cross(data))
 
     def forward(self, data: Dict[str, Tensor]):
         h = self._deep(data)
         return dense_ops.head(h, self.prediction.weight, self.prediction.bias), self._target(data)
 
     def fused_bce_loss(self, data: Dict[str, Tensor]):
-        """Training loss (BCE with logits, mean) with the output layer fused into it."""
-        loss, _ = dense_ops.ctr_head_bce(self._deep(data), self.prediction.weight,
+        """Training loss (BCE with logits, mean): the deep MLP, the output layer and the
+        loss as one fused tower launch (or the output layer fused into the loss)."""
+        x = self._cross(data)
+        if dense_ops.tower_supported(x, self.mlp, self.prediction):
+            return dense_ops.tower_bce(x, self.mlp, self.prediction, None, self._target(data))
+        loss, _ = dense_ops.ctr_head_bce(self.mlp(x), self.prediction.weight,
                                          self.prediction.bias, None, self._target(data))
         return loss

@@ -109,7 +109,10 @@ class DIN(IModel):
 
     def fused_bce_loss(self, data: Dict[str, Tensor]):
         """Training loss (BCE with logits, mean) with the output layer fused into it."""
-        h = self.mlp(self._top(data))
+        top = self._top(data)
         y = data[self.label_column.feature_name].float()
+        if dense_ops.tower_supported(top, self.mlp, self.prediction):
+            return dense_ops.tower_bce(top, self.mlp, self.prediction, None, y)
+        h = self.mlp(top)
         loss, _ = dense_ops.ctr_head_bce(h, self.prediction.weight, self.prediction.bias, None, y)
         return loss

@@ -171,8 +171,13 @@ class DeepFM(_CTRBase):
         first-order term + global bias and the loss in one kernel (same sum as
         ``forward`` + the loss, in a different fp32 order)."""
         dense = self._dense(data)
-        h, logit = self._deep(data, dense, False)
-        loss, _ = dense_ops.ctr_head_bce(h, self.prediction.weight, self.prediction.bias, logit,
-                                         self._target(data), xs=dense, ws=self.dense_weight,
+        x0, logit = interact(self.embeddings, self._ids(data), dense, None, None, fm2=True,
+                             first_order=True, x0_cols=self.x0_cols, x0_dtype=self._x0_dtype())
+        if dense_ops.tower_supported(x0, self.mlp, self.prediction, dense):
+            # MLP + output layer + loss and the MLP's input gradients: one launch
+            return dense_ops.tower_bce(x0, self.mlp, self.prediction, logit, self._target(data),
+                                       xs=dense, ws=self.dense_weight, b2=self.global_bias)
+        loss, _ = dense_ops.ctr_head_bce(self.mlp(x0), self.prediction.weight, self.prediction.bias,
+                                         logit, self._target(data), xs=dense, ws=self.dense_weight,
                                          b2=self.global_bias)
         return loss

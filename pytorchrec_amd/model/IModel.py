@@ -249,15 +249,25 @@ class IModel(Module, IWithArguments, ABC):
         flat, layout = self._dp_flat
         comm = self.dp_comm
         comm.allreduce_sum_(flat)
+        from pytorchrec_amd.dense import cached_images, images_updated
         jobs = []
         for p, g, n, k, ld, o in layout:
-            img = getattr(p, "_mrec_img", None) if p.dim() == 2 else None
-            wr, wt = (img[1], img[2]) if img is not None and img[0] == p._version else (None, None)
+            kind, imgs = None, None
+            if p.dim() == 2:  # re-emit the images the kernels use (tower first)
+                for kind in ("tower", "rowtr"):
+                    imgs = cached_images(p, kind)
+                    if imgs is not None:
+                        break
+            wr, wt = imgs if imgs is not None else (None, None)
+            packed = kind == "tower" and imgs is not None
             jobs.append(_mrec.SgdJob(p.data_ptr(), flat.data_ptr() + 4 * o, n, k,
                                      p.stride(0) if p.dim() == 2 else k, ld,
                                      float(g["lr"]) / comm.world,
-                                     _mrec.ptr(wr), wr.stride(0) if wr is not None else 0,
-                                     _mrec.ptr(wt), wt.stride(0) if wt is not None else 0))
+                                     _mrec.ptr(wr), 0 if packed or wr is None else wr.stride(0),
+                                     _mrec.ptr(wt), 0 if packed or wt is None else wt.stride(0),
+                                     _mrec.IMG_TOWER if packed else _mrec.IMG_ROW_TR))
+            if imgs is not None:
+                images_updated(p, kind)
         arr = (_mrec.SgdJob * len(jobs))(*jobs)
         _mrec.call("mrec_sgd_multi", len(jobs), arr, _mrec.stream_handle())
 

@@ -361,7 +361,7 @@ def owner_apply(bank: ShardedEmbeddingBank, plan, g_recv: torch.Tensor, lr: floa
                                 bank.weight.dtype == torch.bfloat16) else _mrec.BWD_SGD
     # deferred MLP weight-gradient reductions ride along this launch
     from pytorchrec_amd import dense as dense_ops
-    jobs = dense_ops.take_pending(2)
+    jobs = dense_ops.take_pending(4)
     arr = (_mrec.GemmCall * len(jobs))(*[j.struct() for j in jobs]) if jobs else None
     _mrec.call("mrec_emb_bwd_apply_given", bank.desc().ref(), W * cap, ws.data_ptr(), wsb,
                None, _mrec.F32, 0, None, None, None, _mrec.F32, 0, None, g_recv.data_ptr(),

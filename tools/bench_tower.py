@@ -1,0 +1,101 @@
+"""Time one mrec_tower_fwd_bwd launch at a tower shape (default: C2, B=4096,
+429 -> 400 -> 400 -> 400 -> 1): 100 launches captured in a HIP graph, HIP events on
+the launch stream.  Prints us per launch and the weight-stream rate per CU."""
+import argparse
+import ctypes
+import json
+import sys
+
+import torch
+
+sys.path.insert(0, ".")
+from pytorchrec_amd import _mrec, dense as D  # noqa: E402
+
+p = argparse.ArgumentParser()
+p.add_argument("--batch", type=int, default=4096)
+p.add_argument("--widths", default="429,400,400,400")
+p.add_argument("--reps", type=int, default=100)
+args = p.parse_args()
+widths = [int(x) for x in args.widths.split(",")]
+B, L = args.batch, len(widths) - 1
+dev = torch.device("cuda")
+g = torch.Generator().manual_seed(0)
+Ws = [(torch.randn(widths[l + 1], widths[l], generator=g) / widths[l] ** 0.5).to(dev) for l in range(L)]
+bs = [(torch.randn(widths[l + 1], generator=g) * 0.1).to(dev) for l in range(L)]
+hw = (torch.randn(widths[-1], generator=g) / widths[-1] ** 0.5).to(dev)
+x0 = torch.zeros(B, D._r8(widths[0]), dtype=torch.bfloat16, device=dev)
+x0[:, :widths[0]] = torch.randn(B, widths[0], generator=g).to(torch.bfloat16).to(dev)
+y = (torch.rand(B, generator=g) < 0.3).float().to(dev)
+imgs = [D.tower_images(W) for W in Ws]
+hs = [D._alloc(B, widths[l + 1], torch.bfloat16, dev) for l in range(L - 1)]
+dhs = [D._alloc(B, widths[l + 1], torch.bfloat16, dev) for l in range(L)]
+dx0 = D._alloc(B, widths[0], torch.bfloat16, dev)
+dz = torch.empty(B, device=dev)
+H = widths[-1]
+npart = int(_mrec.lib().mrec_ctr_head_parts(B))
+part = torch.empty(npart, D._r8(H + 1), device=dev)
+lp = torch.empty(npart, device=dev)
+loss = torch.empty(1, device=dev)
+a = _mrec.TowerArgs()
+a.batch, a.n_layers = B, L
+for l in range(L + 1):
+    a.width[l] = widths[l]
+a.x0, a.ld_x0 = x0.data_ptr(), x0.stride(0)
+for l in range(L):
+    a.w_fwd[l], a.w_bwd[l] = imgs[l][0].data_ptr(), imgs[l][1].data_ptr()
+    a.bias[l] = bs[l].data_ptr()
+    a.dh_out[l], a.ld_dh[l] = dhs[l].data_ptr(), dhs[l].stride(0)
+    if l < L - 1:
+        a.h_out[l], a.ld_h[l] = hs[l].data_ptr(), hs[l].stride(0)
+a.head_w, a.y = hw.data_ptr(), y.data_ptr()
+a.dx0, a.ld_dx0 = dx0.data_ptr(), dx0.stride(0)
+a.dz, a.part, a.ldp = dz.data_ptr(), part.data_ptr(), part.stride(0)
+a.loss_part, a.ticket, a.loss = lp.data_ptr(), D._ticket(dev).data_ptr(), loss.data_ptr()
+
+
+def launch():
+    _mrec.call("mrec_tower_fwd_bwd", ctypes.byref(a), _mrec.stream_handle())
+
+
+s = torch.cuda.Stream()
+s.wait_stream(torch.cuda.current_stream())
+with torch.cuda.stream(s):
+    launch()
+    gr = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(gr, stream=s):
+        for _ in range(args.reps):
+            launch()
+    gr.replay()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record(s)
+    gr.replay()
+    e1.record(s)
+e1.synchronize()
+us = e0.elapsed_time(e1) / args.reps * 1e3
+wbytes = sum(int(im[0].numel() + im[1].numel()) * 2 for im in imgs)
+flops = 2 * B * sum(widths[l] * widths[l + 1] for l in range(L)) * 2
+print(json.dumps({"widths": widths, "batch": B, "us": round(us, 2),
+                  "weight_stream_GBps_per_CU": round(wbytes / (us * 1e-6) / 1e9, 1),
+                  "TFLOPs": round(flops / (us * 1e-6) / 1e12, 1)}))
+
+# ---- phase stamps of one launch (diagnostic build hook) ------------------------
+grid = (B + 15) // 16
+st = torch.zeros(grid, 16, dtype=torch.int64, device=dev)
+fn = _mrec.lib().mrec_tower_debug_stamps
+fn.argtypes, fn.restype = [ctypes.c_void_p], None
+for _ in range(3):
+    launch()
+fn(st.data_ptr())
+launch()
+fn(None)
+torch.cuda.synchronize()
+t = st.cpu().double() * 10.0 / 1e3  # 100 MHz ticks -> us
+t0 = t[:, 0].min()
+names = {0: "start", 1: "x0 loaded", 2: "fwd1", 3: "fwd2", 4: "fwd3", 5: "fwd4", 6: "head",
+         7: "bwd_L", 8: "bwd_L-1", 9: "bwd_L-2", 10: "bwd_L-3", 11: "bwd done", 12: "ticket"}
+used = [k for k in range(13) if bool((st[:, k] != 0).all())]
+rows = []
+for k in used:
+    col = t[:, k] - t0
+    rows.append(f"{names.get(k, k):>10}: min {float(col.min()):7.2f} med {float(col.median()):7.2f} max {float(col.max()):7.2f} us")
+print("\n".join(rows))

@@ -1,7 +1,8 @@
-# all GPU tests, one process, then smoke
+# GPU tests in one process (MREC_TESTS: pytest selection args, default the whole
+# -m gpu suite), stopping at the first failure
 set -o pipefail
 R=$GRAFT_REPO_ROOT
 cd $R
 mkdir -p gpurun_out
-timeout -k 10 900 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread ${MREC_TESTS:-} > gpurun_out/gpu_tests.log 2>&1 || { echo TESTS_FAIL; tail -60 gpurun_out/gpu_tests.log; exit 1; }
+timeout -k 10 900 python -u -m pytest ${MREC_TESTS:-tests} -m gpu -x -v --timeout 300 --timeout-method thread > gpurun_out/gpu_tests.log 2>&1 || { echo TESTS_FAIL; tail -60 gpurun_out/gpu_tests.log; exit 1; }
 tail -3 gpurun_out/gpu_tests.log

@@ -208,75 +208,149 @@ def time_launches(fn, reps=100):
     return e0.elapsed_time(e1) / reps * 1e-3  # seconds per launch
 
 
+def alg_bytes_per_sample(F, D, n_dense, first_order):
+    """SURVEY.md §8(d) algorithmic bytes per sample, bf16 weights, int32 ids:
+    fwd = ids F*4 + useful row bytes F*(D+w)*2 + dense n_dense*4 + label 4;
+    bwd = ids F*4 + row-sparse read-modify-write 2*F*(D+w)*2.
+    C2 DeepFM: 1,044 + 1,872 = 2,916; C3 DCN-v2 (no w): 992 + 1,768 = 2,760."""
+    row = (D + (1 if first_order else 0)) * 2
+    return F * 4 + F * row + n_dense * 4 + 4, F * 4 + 2 * F * row
+
+
 def kernel_rooflines(model, data, args):
     """Average duration of each HBM-bound embedding kernel, launched exactly as the
-    train step launches it, and its algorithmic bytes.  Measured on
-    an unsharded C2 bank of the same shapes (at N>1 the model's tables are shards)."""
+    train step launches it, with its algorithmic bytes (what
+    ``roofline.achieved`` uses) and its as-implemented bytes.
+    Measured on an unsharded bank of the model's shapes (at N>1 the model's tables
+    are shards).  Returns {kernel: (seconds, algorithmic bytes, as-implemented bytes)}."""
     from pytorchrec_amd import _mrec, embedding as E
     dev = torch.device("cuda", torch.cuda.current_device())
+    first_order = bool(model.embeddings.has_w)
     if type(model.embeddings) is E.EmbeddingBank:
         bank = model.embeddings  # unsharded: time the model's own bank (no second copy of
         # a 100M-row C5 bank); the timed updates run after the timed region
     else:
-        bank = E.EmbeddingBank([args.rows_per_table] * CRITEO_FIELDS, 16, with_first_order=True,
-                               dtype=torch.bfloat16, device=dev)
+        bank = E.EmbeddingBank([args.rows_per_table] * CRITEO_FIELDS, 16,
+                               with_first_order=first_order, dtype=torch.bfloat16, device=dev)
         E.init_bank_(bank, generator=torch.Generator(device=dev).manual_seed(5))
         bank.use_fused_sgd(args.lr)
         bank.check_ids = False
-    dense_weight = torch.randn(CRITEO_DENSE, device=dev) * 0.01
-    global_bias = torch.zeros(1, device=dev)
+    fm = first_order  # DeepFM: FM2 + first order; DCN-v2: plain gather into x0
+    dense_weight = torch.randn(CRITEO_DENSE, device=dev) * 0.01 if fm else None
+    global_bias = torch.zeros(1, device=dev) if fm else None
     B, F, D = args.batch, bank.n_tables, bank.dim
     ids = model._ids(data)
     dense = model._dense(data)
+    alg_fwd, alg_bwd = alg_bytes_per_sample(F, D, CRITEO_DENSE, first_order)
+    w = 1 if first_order else 0
     out = {}
     with torch.no_grad():
         # the step's forward launch: interaction + the backward's hash plan in one
         # kernel (mrec_interact_fwd_ex)
         def fwd():
             E._InteractFn.forward(_Ctx(), bank.weight, dense_weight, global_bias, None,
-                                  bank, ids, dense, True, True, model.x0_cols, torch.bfloat16,
+                                  bank, ids, dense, fm, fm, model.x0_cols, torch.bfloat16,
                                   True)
-        # bytes/sample: ids F*4 + useful row bytes F*(D+1)*2 + dense 13*4 + x0 write
-        # x0_cols*2 + logit 4 + fm_sum D*4; plan: ids F*4 again + per lookup one
-        # 12-B workspace entry (row table / descriptor / permutation)
-        fwd_bytes = F * 4 + F * (D + 1) * 2 + CRITEO_DENSE * 4 + model.x0_cols * 2 + 4 + D * 4
-        plan_bytes = F * 4 + F * 12
+        # as implemented, bytes/sample: ids F*4 + useful row bytes F*(D+w)*2 + dense
+        # 13*4 + x0 write x0_cols*2 + logit 4 + fm_sum D*4; plan: ids F*4 again + per
+        # lookup one 12-B workspace entry (row table / descriptor / permutation)
+        impl_fwd = (F * 4 + F * (D + w) * 2 + CRITEO_DENSE * 4 + model.x0_cols * 2 + 4
+                    + (D * 4 if fm else 0) + F * 4 + F * 12)
         t = time_launches(fwd)
-        out["mrec_interact_fwd_ex"] = (t, (fwd_bytes + plan_bytes) * B)
+        out["mrec_interact_fwd_ex"] = (t, alg_fwd * B, impl_fwd * B)
 
         ws, wsb = E._plan(bank, ids, 0, B, None)
         torch.cuda.synchronize()
 
         x0, logit = E._InteractFn.forward(_Ctx(), bank.weight, dense_weight, global_bias, None,
-                                          bank, ids, dense, True, True, model.x0_cols,
+                                          bank, ids, dense, fm, fm, model.x0_cols,
                                           torch.bfloat16, False)
-        fm_sum = torch.zeros(B, D, device=x0.device)
+        fm_sum = torch.zeros(B, D, device=x0.device) if fm else None
         dx0 = torch.zeros_like(x0)
-        dl = torch.zeros(B, device=x0.device)
+        dl = torch.zeros(B, device=x0.device) if fm else None
 
         def apply():
-            E._apply(bank, ws, wsb, B, dx=dx0, dfm=dl, fm_sum=fm_sum, x0=x0, dw=dl)
+            E._apply(bank, ws, wsb, B, dx=dx0, dfm=dl, fm_sum=fm_sum, x0=x0 if fm else None, dw=dl)
         t = time_launches(apply)
-        # per lookup: perm 4 + dx D*2 + v re-read D*2 + row read+write 2*(D+1)*2;
-        # per sample: fm_sum D*4 + dlogit 4
-        apply_bytes = F * (4 + D * 2 + D * 2 + 2 * (D + 1) * 2) + D * 4 + 4
-        out["mrec_emb_bwd_apply"] = (t, apply_bytes * B)
+        # as implemented, per lookup: perm/row table 4 + dx D*2 (+ v re-read D*2 for
+        # the FM term) + row read+write 2*(D+w)*2; per sample: fm_sum D*4 + dlogit 4
+        impl_bwd = (F * (4 + D * 2 + (D * 2 if fm else 0) + 2 * (D + w) * 2)
+                    + ((D * 4 + 4) if fm else 0))
+        out["mrec_emb_bwd_apply"] = (t, alg_bwd * B, impl_bwd * B)
     return out
 
 
-PMC_FILE = os.path.join(os.path.dirname(os.path.abspath(__file__)), "profiles", "pmc_traffic.json")
+PROFILES = os.path.join(os.path.dirname(os.path.abspath(__file__)), "profiles")
+PMC_FILE = os.path.join(PROFILES, "pmc_traffic.json")
+CEIL_FILE = os.path.join(PROFILES, "ceilings.json")
 
 
-def pmc_traffic(kernels):
-    """HBM bytes per launch summed over ``kernels`` from the committed PMC pass
+def pmc_traffic(kernels, args):
+    """HBM bytes per launch summed over ``kernels`` from the committed PMC passes
     (tools/gpu_pmc.sh: rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE in separate runs of
-    this bench; FETCH_SIZE doubled per the gfx950 correction), or None."""
+    this bench, corrected by the calibration tools/pmc_traffic.py applies), with the
+    run they came from.  rocprof cannot count the run it is printed by, so the
+    stamp names the profiled run; the traffic is only reported when that run had
+    this workload (same model, batch, rows per table).  Returns (bytes | None, stamp)."""
     try:
         with open(PMC_FILE) as fh:
-            pmc = json.load(fh)["kernels"]
-        return int(sum(pmc[k]["hbm_bytes_per_launch"] for k in kernels))
-    except (OSError, KeyError, ValueError):
+            pmc = json.load(fh)
+        run = pmc.get("run", {})
+        want = {"model": args.model, "batch": args.batch, "rows_per_table": args.rows_per_table}
+        if any(run.get(k) != v for k, v in want.items()):
+            return None, {"file": "profiles/pmc_traffic.json", "mismatch": run}
+        per = pmc["kernels"][args.model]
+        return int(sum(per[k]["hbm_bytes_per_launch"] for k in kernels)), {
+            "file": "profiles/pmc_traffic.json", "run": run,
+            "correction": pmc.get("correction")}
+    except (OSError, KeyError, ValueError, TypeError):
+        return None, None
+
+
+def attainable():
+    """The measured ceiling the embedding path is compared with beside the spec peak:
+    random 64-B row gathers from the C2-sized (64 MB, Infinity-Cache resident) table,
+    bandwidth form, from the committed step-0 microbenchmark (tools/micro/ceilings.hip,
+    profiles/ceilings.json)."""
+    try:
+        with open(CEIL_FILE) as fh:
+            c = json.load(fh)
+        g = [x for x in c["gather"] if x["row_bytes"] == 64 and x["table_bytes"] == 64 << 20][0]
+        return {"GB/s": g["row_GB/s"], "what": "random 64-B row gather, 64 MB table, 16 M lookups",
+                "stream_copy_GB/s": c["stream_copy"]["GB/s"], "file": "profiles/ceilings.json"}
+    except (OSError, KeyError, ValueError, IndexError):
         return None
+
+
+MFMA_PEAK_TFLOPS = 2500.0  # dense bf16 (MI355X_MICROARCH.md)
+
+
+def end_to_end(args, per_gpu_samples_s):
+    """End-to-end samples/s per GPU against min(HBM, MFMA) samples/s roofline,
+    SURVEY.md §8(d): HBM = 8 TB/s / algorithmic train-step bytes per sample, MFMA =
+    2.5 PFLOP/s / train FLOP per sample (fwd + 2x for the backward)."""
+    if args.model == "din":
+        # fwd 51*2*4 + 51*2*16*2 + 8 ids/rows/len; bwd 408 + 2*3264
+        nbytes = 3680 + 6936
+        # attention unit [B*L, 64] -> 80 -> 40 -> 1 and top [B, 64] -> 200 -> 80 -> 1
+        fwd = DIN_L * 2 * (64 * 80 + 80 * 40 + 40) + 2 * (64 * 200 + 200 * 80 + 80)
+    else:
+        fo = args.model == "deepfm"
+        f, b = alg_bytes_per_sample(CRITEO_FIELDS, 16, CRITEO_DENSE, fo)
+        nbytes = f + b
+        d0 = CRITEO_FIELDS * 16 + CRITEO_DENSE
+        if fo:
+            fwd = 2 * (d0 * 400 + 400 * 400 + 400 * 400 + 400)
+        else:  # 3 cross layers d0 x d0 + deep 400-400 + head over [x_3 | h_2]
+            fwd = 2 * (3 * d0 * d0 + d0 * 400 + 400 * 400 + (d0 + 400))
+    flops = 3 * fwd
+    hbm = HBM_PEAK_GBS * 1e9 / nbytes
+    mfma = MFMA_PEAK_TFLOPS * 1e12 / flops
+    return {"samples_per_s_per_gpu": round(per_gpu_samples_s, 1),
+            "alg_bytes_per_sample": nbytes, "train_flop_per_sample": flops,
+            "hbm_roofline_samples_per_s": round(hbm, 1),
+            "mfma_roofline_samples_per_s": round(mfma, 1),
+            "frac_of_min_roofline": round(per_gpu_samples_s / min(hbm, mfma), 4)}
 
 
 class _Ctx:
@@ -512,23 +586,35 @@ def main():
                    "hip_graph": not args.no_graph,
                    "steps_per_graph": G if graphs is not None else 0},
     }
-    if rank == 0 and not args.no_roofline and args.model == "deepfm":
+    if rank == 0 and not args.no_roofline and args.model in ("deepfm", "dcnv2"):
         ks = kernel_rooflines(model, datas[0], args)
-        # achieved = sum of algorithmic bytes of the HBM-bound
+        # achieved = sum of the algorithmic bytes of the HBM-bound
         # embedding-path kernels / sum of their measured launch durations
         t = sum(v[0] for v in ks.values())
         nbytes = sum(v[1] for v in ks.values())
+        impl = sum(v[2] for v in ks.values())
         ach = nbytes / t / 1e9
-        traffic = pmc_traffic(list(ks))
+        traffic, tsrc = pmc_traffic(list(ks), args)
         result["roofline"] = {"bound": "hbm",
                               "kernel": "embedding path: " + " + ".join(ks),
                               "achieved": round(ach, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                               "frac": round(ach / HBM_PEAK_GBS, 4),
                               "traffic": traffic,
-                              "avg_us": round(t * 1e6, 3), "bytes_per_launch": nbytes}
+                              "avg_us": round(t * 1e6, 3), "bytes_per_launch": nbytes,
+                              "bytes_rule": "SURVEY.md §8(d) algorithmic bytes per sample x batch",
+                              "as_implemented_bytes_per_launch": impl,
+                              "as_implemented_GB/s": round(impl / t / 1e9, 1),
+                              "traffic_source": tsrc}
+        att = attainable()
+        if att:
+            result["roofline"]["attainable"] = att
+            result["roofline"]["frac_of_attainable"] = round(ach / att["GB/s"], 4)
         result["roofline_kernels"] = {k: {"avg_us": round(v[0] * 1e6, 3), "bytes": v[1],
-                                          "GB/s": round(v[1] / v[0] / 1e9, 1)}
+                                          "GB/s": round(v[1] / v[0] / 1e9, 1),
+                                          "as_implemented_bytes": v[2]}
                                       for k, v in ks.items()}
+    if rank == 0:
+        result["end_to_end"] = end_to_end(args, result["value"] / world)
     if (world == 1 and not sharded and not args.no_h2d and not args.no_graph
             and args.model == "deepfm"):
         result["pcie_inclusive"] = pcie_inclusive(step, args, sparse, dense_cols, label_col,

@@ -32,7 +32,7 @@
 extern "C" {
 #endif
 
-#define MREC_ABI_VERSION 11
+#define MREC_ABI_VERSION 12
 #define MREC_MAX_TABLES 64      /* tables per table bank / per call */
 #define MREC_BWD_MAX_BATCH 8192  /* lookups per table per plan/apply call */
 #define MREC_BWD_HASH_MAX_BATCH 4096  /* batches up to this use the hash plan */
@@ -451,12 +451,14 @@ typedef struct {
 } mrec_head_finish_job;
 
 /*
- * mrec_gemm_multi plus, in extra workgroups of the same launch, the embedding-
- * backward plan of `plan` and/or the CTR head finish of `finish` (either may be
- * NULL).  A HIP graph runs the step's kernels one after another, so a small
- * kernel of its own sits on the critical path; beside latency-bound backward
- * GEMMs it is hidden.  Same results as mrec_emb_bwd_plan / mrec_ctr_head_finish.
- * The jobs must be independent of the GEMM calls.
+ * mrec_gemm_multi plus, in extra workgroups of the same launch, the CTR head
+ * finish of `finish` (may be NULL).  A HIP graph runs the step's kernels one
+ * after another, so a small kernel of its own sits on the critical path; beside
+ * latency-bound backward GEMMs it is hidden.  Same results as
+ * mrec_ctr_head_finish.  The job must be independent of the GEMM calls.
+ * `plan` must be NULL (ABI 12): the embedding-backward plan rides in the
+ * interaction launch (mrec_interact_fwd_ex) -- inside a GEMM launch its
+ * registers held the GEMM at half occupancy -- and a plan job here is EINVAL.
  */
 mrec_status mrec_gemm_multi_ex(int32_t n, const mrec_gemm_call *calls, const mrec_plan_job *plan,
                                const mrec_head_finish_job *finish, mrec_stream stream);

@@ -20,7 +20,7 @@ import torch  # noqa: F401  (must precede the dlopen, see module docstring)
 LIB_DIR = os.path.join(os.path.dirname(os.path.abspath(__file__)), "lib")
 LIB_PATH = os.environ.get("MREC_LIB_PATH") or os.path.join(LIB_DIR, "libmrec.so")
 
-ABI_VERSION = 11
+ABI_VERSION = 12
 MAX_TABLES = 64
 BWD_MAX_BATCH = 8192
 BWD_HASH_MAX_BATCH = 4096  # batches up to this use the hash plan (fusable into a GEMM launch)
@@ -261,7 +261,8 @@ def lib():
             fn.restype = res
             fn.argtypes = args
         v = handle.mrec_abi_version()
-        if v != ABI_VERSION:
+        # (MREC_ABI_ANY=1: an older diagnostic build for an A/B timing, tools/gpu_ab.sh)
+        if v != ABI_VERSION and os.environ.get("MREC_ABI_ANY") != "1":
             raise MrecUnavailable(f"libmrec ABI {v} != expected {ABI_VERSION}; rebuild it")
         _lib = handle
         return _lib

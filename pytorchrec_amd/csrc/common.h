@@ -36,6 +36,7 @@ struct BankArgs {
   int32_t dim;
   int32_t row_stride;  // elements
   int32_t has_w;
+  int32_t lpr;  // lanes per row: row bytes / 16
 };
 
 struct IdsArgs {

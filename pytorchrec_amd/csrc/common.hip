@@ -49,6 +49,7 @@ mrec_status make_bank_args(const mrec_table_bank *bank, BankArgs *out, int *elem
   out->has_w = bank->has_w ? 1 : 0;
   *elem_bytes = eb;
   *lanes_per_row = static_cast<int>(row_bytes / 16);
+  out->lpr = *lanes_per_row;
   return MREC_OK;
 }
 

@@ -96,6 +96,53 @@ __device__ __forceinline__ void lookup_grad(const ApplyArgs &a, int64_t b, int f
   }
 }
 
+// gradient of lookup (b, f) with the row's current values v (this lane's EPL
+// elements, bank dtype widened) for the FM term: the hash-layout apply reads the
+// row it updates anyway, so the gathered rows are not re-read from x0
+template <int EPL>
+__device__ __forceinline__ void lookup_grad_v(const ApplyArgs &a, int64_t b, int f, int D, int e0,
+                                              bool v_lane, bool w_lane, const float *v, float *g) {
+#pragma unroll
+  for (int j = 0; j < EPL; ++j) g[j] = 0.f;
+  if (a.g_occ) {
+    const int64_t idx = a.chunk ? (b / a.chunk) * a.chunk_stride + f * a.chunk + b % a.chunk : b;
+    const float *go = a.g_occ + idx * a.g_ld;
+    if (v_lane)
+      load_f32xN<EPL>(go + e0, g);
+    else if (w_lane)
+      g[0] = go[D];
+    return;
+  }
+  if (v_lane) {
+    const int64_t col = static_cast<int64_t>(f) * D + e0;
+    if (a.dx) {
+      if (a.dx_bf16)
+        load_bf16xN<EPL>(static_cast<const uint16_t *>(a.dx) + b * a.dx_ld + col, g);
+      else
+        load_f32xN<EPL>(static_cast<const float *>(a.dx) + b * a.dx_ld + col, g);
+    }
+    if (a.dfm) {
+      const float c = a.dfm[b];
+      float s[EPL];
+      load_f32xN<EPL>(a.fm_sum + b * D + e0, s);
+#pragma unroll
+      for (int j = 0; j < EPL; ++j) g[j] = fmaf(c, s[j] - v[j], g[j]);
+    }
+  } else if (w_lane && a.dw) {
+    g[0] = a.dw[b];
+  }
+}
+
+template <int EPL>
+__device__ __forceinline__ void add_lookup_grad_v(const ApplyArgs &a, int64_t b, int f, int D,
+                                                  int e0, bool v_lane, bool w_lane, const float *v,
+                                                  float *acc) {
+  float g[EPL];
+  lookup_grad_v<EPL>(a, b, f, D, e0, v_lane, w_lane, v, g);
+#pragma unroll
+  for (int j = 0; j < EPL; ++j) acc[j] += g[j];
+}
+
 // per-lookup gradient first, then one add into the segment sum
 template <int EPL>
 __device__ __forceinline__ void add_lookup_grad(const ApplyArgs &a, int64_t b, int f, int D,
@@ -106,31 +153,40 @@ __device__ __forceinline__ void add_lookup_grad(const ApplyArgs &a, int64_t b, i
   for (int j = 0; j < EPL; ++j) acc[j] += g[j];
 }
 
-template <typename T>
-__device__ __forceinline__ T *row_ptr(const BankArgs &bank, const ApplyArgs &a, int f,
-                                      int64_t row, int e0) {
-  const int64_t grow = bank.row_offset[f] + row;
+// element e0 of global row `grow` (table offset already added): the bank, or the
+// dense gradient buffer in DENSE_GRAD mode
+// (MODE >= 0: the update mode fixed at compile time, else a.mode)
+template <typename T, int MODE = -1>
+__device__ __forceinline__ T *row_ptr_g(const BankArgs &bank, const ApplyArgs &a, int64_t grow,
+                                        int e0) {
+  const int mode = MODE >= 0 ? MODE : a.mode;
   const int64_t off = grow * static_cast<int64_t>(bank.row_stride) + e0;
-  return reinterpret_cast<T *>(a.mode == MREC_BWD_DENSE_GRAD ? static_cast<char *>(a.grad)
-                                                              : bank.data) +
+  return reinterpret_cast<T *>(mode == MREC_BWD_DENSE_GRAD ? static_cast<char *>(a.grad)
+                                                            : bank.data) +
          off;
 }
 
-// new value of this lane's 16 bytes of the row from its old contents `raw`
 template <typename T>
-__device__ __forceinline__ void apply_row_raw(const BankArgs &bank, const ApplyArgs &a, int f,
-                                              int64_t row, int e0, bool v_lane, const float *acc,
-                                              const uint4 raw) {
+__device__ __forceinline__ T *row_ptr(const BankArgs &bank, const ApplyArgs &a, int f,
+                                      int64_t row, int e0) {
+  return row_ptr_g<T>(bank, a, bank.row_offset[f] + row, e0);
+}
+
+// new value of this lane's 16 bytes of global row `grow` from its old contents `raw`
+template <typename T, int MODE = -1>
+__device__ __forceinline__ void apply_row_raw_g(const BankArgs &bank, const ApplyArgs &a,
+                                                int64_t grow, int e0, bool v_lane,
+                                                const float *acc, const uint4 raw) {
   constexpr int EPL = Vec<T>::EPL;
-  const int64_t grow = bank.row_offset[f] + row;
-  T *p = row_ptr<T>(bank, a, f, row, e0);
+  const int mode = MODE >= 0 ? MODE : a.mode;
+  T *p = row_ptr_g<T, MODE>(bank, a, grow, e0);
   float old[EPL];
   Vec<T>::to_f32(raw, old);
   const int live = v_lane ? EPL : 1;  // w lane: only element D is live
   float nv[EPL];
 #pragma unroll
   for (int j = 0; j < EPL; ++j)
-    nv[j] = (a.mode == MREC_BWD_DENSE_GRAD) ? old[j] + acc[j] : fmaf(-a.lr, acc[j], old[j]);
+    nv[j] = (mode == MREC_BWD_DENSE_GRAD) ? old[j] + acc[j] : fmaf(-a.lr, acc[j], old[j]);
   uint4 out;
   if constexpr (sizeof(T) == 4) {
     const uint32_t o[4] = {raw.x, raw.y, raw.z, raw.w};
@@ -148,7 +204,7 @@ __device__ __forceinline__ void apply_row_raw(const BankArgs &bank, const ApplyA
       for (int q = 0; q < 2; ++q) {
         const int j = 2 * k + q;
         if (j < live) {
-          h[q] = (a.mode == MREC_BWD_SGD_SR)
+          h[q] = (mode == MREC_BWD_SGD_SR)
                      ? f32_to_bf16_sr(nv[j], hash3(a.seed, grow, static_cast<uint32_t>(e0 + j)))
                      : f32_to_bf16_rne(nv[j]);
         } else {
@@ -160,6 +216,13 @@ __device__ __forceinline__ void apply_row_raw(const BankArgs &bank, const ApplyA
     out = make_uint4(w[0], w[1], w[2], w[3]);
   }
   *reinterpret_cast<uint4 *>(p) = out;
+}
+
+template <typename T>
+__device__ __forceinline__ void apply_row_raw(const BankArgs &bank, const ApplyArgs &a, int f,
+                                              int64_t row, int e0, bool v_lane, const float *acc,
+                                              const uint4 raw) {
+  apply_row_raw_g<T>(bank, a, bank.row_offset[f] + row, e0, v_lane, acc, raw);
 }
 
 template <typename T>

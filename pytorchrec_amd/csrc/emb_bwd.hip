@@ -25,7 +25,6 @@ namespace mrec {
 #endif
 
 constexpr int kMaxPlanKeys = 8192;
-constexpr int kShortSeg = 16;
 
 // ---------------------------------------------------------------------------
 // plan: stable LSD radix sort of the table's ids in LDS
@@ -206,8 +205,9 @@ __global__ __launch_bounds__(kPlanThreads) void plan_hash_kernel(BankArgs bank, 
                                                                  int64_t B, void *ws,
                                                                  int32_t *__restrict__ oob,
                                                                  uint64_t *__restrict__ d_step) {
-  __shared__ uint32_t smem[2 * kHashSlots + 1];
-  plan_hash_body<kPlanThreads, kHashSlots>(bank, ids, B, ws, oob, d_step, blockIdx.x, smem);
+  __shared__ uint32_t smem[2 * kHashSlots + 2];
+  plan_hash_body<kPlanThreads, kHashSlots>(bank, ids, B, ws, oob, d_step, blockIdx.x / kPlanBuckets,
+                                           blockIdx.x % kPlanBuckets, smem);
 }
 
 // ---------------------------------------------------------------------------
@@ -224,33 +224,205 @@ struct CoReduce {
   GemmArgs g[kMaxCoReduce];
 };
 
-// Grid (1-D): F * seg_blocks segment blocks (table f = blk / seg_blocks), then,
-// for the hash layout, ceil(B * F / WPB) sample-major blocks for the rows hit
-// once: worker q handles lookup (b, f) = (q / F, q % F), so a wave reads
-// consecutive slices of the dx / x0 rows (coalesced) and updates rows no other
-// lookup touches.
+__device__ __forceinline__ bool co_reduce(const CoReduce &co, int b) {
+  int p = 0;
+  while (p + 1 < co.n && b >= co.start[p + 1]) ++p;
+  const int local = b - co.start[p];
+  if (local < co.nblk[p]) splitk_reduce_body(co.g[p], local, co.nblk[p]);
+  return true;
+}
+
+// One hot segment (> kShortSeg lookups) summed by the whole workgroup, in a
+// fixed order independent of how the plan listed it: the samples go into an LDS
+// bitmap of the batch (<= kHashMaxEntries), worker w sums the w-th, (w + WPB)-th
+// ... smallest samples (rank -> sample by a binary search over per-word popcount
+// prefixes), then a fixed shuffle tree inside each wave and the 4 wave partials
+// in order.  ~2.6 KiB of LDS, so the apply launch keeps full occupancy.
 template <typename T, int LPR>
-__global__ __launch_bounds__(256, 6) void apply_kernel(BankArgs bank, int64_t B, const void *ws,
-                                                       ApplyArgs a, int seg_blocks,
-                                                       int hash_layout, int apply_blocks,
-                                                       CoReduce co) {
-  if (static_cast<int>(blockIdx.x) >= apply_blocks) {  // uniform: a co-launched reduction
-    const int b = blockIdx.x - apply_blocks;
-    int p = 0;
-    while (p + 1 < co.n && b >= co.start[p + 1]) ++p;
-    const int local = b - co.start[p];
-    if (local < co.nblk[p]) splitk_reduce_body(co.g[p], local, co.nblk[p]);
+struct HotSeg {
+  static constexpr int EPL = Vec<T>::EPL;
+  static constexpr int WPB = 256 / LPR;
+  uint32_t bits[kHashMaxEntries / 32];
+  uint32_t pre[kHashMaxEntries / 32];
+  float red[4][LPR * EPL];
+  uint32_t wsum[4];
+
+  // samples: perm[0, sn); v: the row's values for the FM term (nullptr: take v
+  // from x0, the sorted layout's rule)
+  template <bool ROW_V, int MODE = -1>
+  __device__ __forceinline__ void run(const BankArgs &bank, const ApplyArgs &a, int f, int64_t row,
+                                      const int32_t *perm, int sn, int64_t B, const float *v,
+                                      int worker, int e0, bool v_lane, bool w_lane, bool live) {
+    const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+    const int D = bank.dim;
+    const int nwords = static_cast<int>((B + 31) / 32);  // <= 256: one per thread
+    if (tid < nwords) bits[tid] = 0u;
+    __syncthreads();
+    for (int i = tid; i < sn; i += 256) {
+      const int b = perm[i];
+      atomicOr(&bits[b >> 5], 1u << (b & 31));
+    }
+    __syncthreads();
+    const uint32_t c = tid < nwords ? __popc(bits[tid]) : 0u;
+    uint32_t incl = c;
+#pragma unroll
+    for (int off = 1; off < 64; off <<= 1) {
+      const uint32_t x = __shfl_up(incl, off);
+      if (lane >= off) incl += x;
+    }
+    if (lane == 63) wsum[wid] = incl;
+    __syncthreads();
+    if (tid < nwords) {
+      uint32_t p = incl - c;
+      for (int k2 = 0; k2 < wid; ++k2) p += wsum[k2];
+      pre[tid] = p;
+    }
+    __syncthreads();
+    float acc[EPL];
+#pragma unroll
+    for (int j = 0; j < EPL; ++j) acc[j] = 0.f;
+    if (live) {
+#pragma unroll 1
+      for (int i = worker; i < sn; i += WPB) {
+        int lo = 0, hi = nwords - 1;  // last word with pre <= i
+        while (lo < hi) {
+          const int mid = (lo + hi + 1) >> 1;
+          if (static_cast<int>(pre[mid]) <= i) lo = mid; else hi = mid - 1;
+        }
+        uint32_t w = bits[lo];
+        for (int k = i - static_cast<int>(pre[lo]); k > 0; --k) w &= w - 1;
+        const int b = lo * 32 + __ffs(w) - 1;
+        float g[EPL];
+        if constexpr (ROW_V)
+          lookup_grad_v<EPL>(a, b, f, D, e0, v_lane, w_lane, v, g);
+        else
+          lookup_grad<EPL>(a, b, f, D, e0, v_lane, w_lane, g);
+#pragma unroll
+        for (int j = 0; j < EPL; ++j) acc[j] += g[j];
+      }
+    }
+#pragma unroll
+    for (int off = LPR; off < 64; off <<= 1)
+#pragma unroll
+      for (int j = 0; j < EPL; ++j) acc[j] += __shfl_xor(acc[j], off);
+    if (lane < LPR)
+#pragma unroll
+      for (int j = 0; j < EPL; ++j) red[wid][e0 + j] = acc[j];
+    __syncthreads();
+    if (tid < LPR && live) {
+#pragma unroll
+      for (int j = 0; j < EPL; ++j) acc[j] = ((red[0][e0 + j] + red[1][e0 + j]) + red[2][e0 + j]) + red[3][e0 + j];
+      const int64_t grow = bank.row_offset[f] + row;
+      const uint4 raw = *reinterpret_cast<const uint4 *>(row_ptr_g<T, MODE>(bank, a, grow, e0));
+      apply_row_raw_g<T, MODE>(bank, a, grow, e0, v_lane, acc, raw);
+    }
+    __syncthreads();
+  }
+};
+
+// ---------------------------------------------------------------------------
+// apply, hash layout (emb_plan.h).  Grid (1-D):
+//   * F * kPlanBuckets segment blocks, first (dispatched first): block (f, r)
+//     updates the repeated rows of its bucket, one LPR-lane worker per segment of
+//     <= short_seg lookups (the lookups' sample indices are ranked inside the
+//     worker by shuffles, their gradients loaded kSegBatch at a time and summed in
+//     ascending sample order -- the order of a sequential scatter-add), then the
+//     bucket's hot segments with the whole workgroup (HotSeg);
+//   * ceil(B * F / WPB) sample-major blocks for the rows hit once: worker q takes
+//     lookup (b, f) = (q / F, q % F), so a wave reads one 64-B stretch of lut and
+//     consecutive slices of the dx rows (coalesced);
+//   * the co-launched split-K reductions.
+// The FM term of a lookup's gradient, dfm_b (fm_sum_b - v), takes v from the row
+// it updates (the forward gathered the same bits): the gathered rows are not
+// re-read from x0.  Row offsets come from the plan's copy in the workspace.
+// ---------------------------------------------------------------------------
+#ifndef MREC_APPLY_WAVES
+#define MREC_APPLY_WAVES 6  // waves per SIMD: every sample-major block of C2 resident at once
+#endif
+constexpr int kSegBatch = 1;  // gradient loads in flight per segment step
+
+template <typename T, int LPR, int MODE>
+__device__ __forceinline__ void apply_segment(const BankArgs &bank, const ApplyArgs &a,
+                                              const BucketWs &t, int f, int64_t toff_f,
+                                              const int4 d, int l, int e0, bool v_lane,
+                                              bool w_lane, bool live) {
+  constexpr int EPL = Vec<T>::EPL;
+  constexpr int PER = (kShortSeg + LPR - 1) / LPR;  // samples held per lane
+  const int D = bank.dim;
+  const int n = d.y;
+  const int64_t grow = toff_f + d.x;
+  uint4 raw = make_uint4(0u, 0u, 0u, 0u);
+  if (live) raw = *reinterpret_cast<const uint4 *>(row_ptr_g<T, MODE>(bank, a, grow, e0));
+  float v[EPL];
+#pragma unroll
+  for (int j = 0; j < EPL; ++j) v[j] = 0.f;
+  if (a.dfm && v_lane) {
+    const uint4 vr = MODE == MREC_BWD_DENSE_GRAD
+                         ? *reinterpret_cast<const uint4 *>(reinterpret_cast<const T *>(bank.data) +
+                                                            grow * static_cast<int64_t>(bank.row_stride) + e0)
+                         : raw;
+    Vec<T>::to_f32(vr, v);
+  }
+  float acc[EPL];
+#pragma unroll
+  for (int j = 0; j < EPL; ++j) acc[j] = 0.f;
+  if (n == 2) {  // both lookups in the descriptor: ascending b, loads in flight together
+    if (live) {
+      float g0[EPL], g1[EPL];
+      lookup_grad_v<EPL>(a, min(d.z, d.w), f, D, e0, v_lane, w_lane, v, g0);
+      lookup_grad_v<EPL>(a, max(d.z, d.w), f, D, e0, v_lane, w_lane, v, g1);
+#pragma unroll
+      for (int j = 0; j < EPL; ++j) acc[j] = (acc[j] + g0[j]) + g1[j];
+    }
+  } else {
+    // the worker's lanes hold the n (<= short_seg) samples, PER each; step k takes
+    // the k-th smallest (the samples of a segment are distinct) by an in-worker min
+    int p[PER];
+#pragma unroll
+    for (int i = 0; i < PER; ++i) p[i] = l + i * LPR < n ? t.perm[d.z + l + i * LPR] : INT_MAX;
+    int last = -1;
+#pragma unroll 1
+    for (int k0 = 0; k0 < n; k0 += kSegBatch) {
+      int sb[kSegBatch];
+#pragma unroll
+      for (int k = 0; k < kSegBatch; ++k) {
+        int m = INT_MAX;
+#pragma unroll
+        for (int i = 0; i < PER; ++i) m = (p[i] > last && p[i] < m) ? p[i] : m;
+#pragma unroll
+        for (int off = 1; off < LPR; off <<= 1) m = min(m, __shfl_xor(m, off));
+        sb[k] = m;
+        if (m != INT_MAX) last = m;
+      }
+      float g[kSegBatch][EPL];
+#pragma unroll
+      for (int k = 0; k < kSegBatch; ++k) {
+#pragma unroll
+        for (int j = 0; j < EPL; ++j) g[k][j] = 0.f;
+        if (live && sb[k] != INT_MAX) lookup_grad_v<EPL>(a, sb[k], f, D, e0, v_lane, w_lane, v, g[k]);
+      }
+#pragma unroll
+      for (int k = 0; k < kSegBatch; ++k)
+        if (sb[k] != INT_MAX)
+#pragma unroll
+          for (int j = 0; j < EPL; ++j) acc[j] += g[k][j];
+    }
+  }
+  if (live) apply_row_raw_g<T, MODE>(bank, a, grow, e0, v_lane, acc, raw);
+}
+
+template <typename T, int LPR, int MODE>
+__global__ __launch_bounds__(256, MREC_APPLY_WAVES) void apply_hash_kernel(BankArgs bank, int64_t B,
+                                                                           const void *ws, ApplyArgs a,
+                                                                           int seg_blocks, int sm_blocks,
+                                                                           CoReduce co) {
+  if (static_cast<int>(blockIdx.x) >= seg_blocks + sm_blocks) {  // uniform
+    co_reduce(co, blockIdx.x - seg_blocks - sm_blocks);
     return;
   }
   if (a.d_step) a.seed += *a.d_step * 0x9e3779b97f4a7c15ull;
   constexpr int EPL = Vec<T>::EPL;
   constexpr int WPB = 256 / LPR;
-  __shared__ int32_t long_list[WPB];
-  __shared__ int32_t n_long;
-  __shared__ float red[WPB][LPR * EPL + 1];
-  __shared__ uint32_t bits[kHashMaxEntries / 32];
-  __shared__ uint16_t srt[kHashMaxEntries];
-  __shared__ uint32_t wsum[4];
   const int worker = threadIdx.x / LPR;
   const int l = threadIdx.x % LPR;
   const int e0 = l * EPL;
@@ -259,66 +431,123 @@ __global__ __launch_bounds__(256, 6) void apply_kernel(BankArgs bank, int64_t B,
   const bool v_lane = e0 + EPL <= D;
   const bool w_lane = bank.has_w && e0 == D;
   const bool live = v_lane || w_lane;
-#if MREC_APPLY_EXP == 6
-  // sample-major blocks first
-  const int n_sm = gridDim.x - F * seg_blocks;
-  const int blk = blockIdx.x < n_sm ? blockIdx.x + F * seg_blocks : blockIdx.x - n_sm;
-#else
   const int blk = blockIdx.x;
-#endif
-#if MREC_APPLY_EXP == 1
-  return;
-#endif
-#if MREC_APPLY_EXP == 2
-  if (blk < F * seg_blocks) return;
-#endif
-#if MREC_APPLY_EXP == 3
-  if (blk >= F * seg_blocks) return;
-#endif
-  if (blk >= F * seg_blocks) {
-    // rows hit once (hash layout): one lookup per worker, sample-major
-    const int q = (blk - F * seg_blocks) * WPB + worker;
-    if (q >= B * F || !live) return;
-    const int b = q / F, f = q - b * F;
-    const int row = table_ws(ws, f, B).lut[b];
-    float g[EPL];
-#if MREC_APPLY_EXP == 5
-#pragma unroll
-    for (int j = 0; j < EPL; ++j) g[j] = 1e-9f * b;
-#else
-    lookup_grad<EPL>(a, b, f, D, e0, v_lane, w_lane, g);
-#endif
-#if MREC_APPLY_EXP == 4
-    if (g[0] == 12345.f) *(float *)a.grad = g[1];
+  const int64_t *__restrict__ toff = table_offsets(ws, F, B);
+
+  if (blk < seg_blocks) {  // uniform: the repeated rows of one (table, bucket)
+#if MREC_APPLY_EXP == 8
     return;
 #endif
-    if (row >= 0) {
-      float acc[EPL];
+    const int f = blk / kPlanBuckets, r = blk - f * kPlanBuckets;
+    const BucketWs t = bucket_ws(ws, f, r, B);
+    const int nseg = t.hdr[0];
+    const int nl = t.hdr[2];
+    const int64_t toff_f = bank.row_offset[f];
+    const int sshort = short_seg(LPR);
+    for (int s0 = 0; s0 < nseg; s0 += WPB) {  // uniform
+      const int s = s0 + worker;
+      if (s < nseg) {
+        const int4 d = t.desc[s];
+        if (d.y <= sshort)
+          apply_segment<T, LPR, MODE>(bank, a, t, f, toff_f, d, l, e0, v_lane, w_lane, live);
+      }
+    }
+    if (nl == 0) return;  // uniform
+#if MREC_APPLY_EXP == 10
+    return;
+#endif
+    __syncthreads();
+    __shared__ HotSeg<T, LPR> hot;
+    for (int k = 0; k < nl; ++k) {
+      const int4 d = t.desc[t.longl[k]];
+      float v[EPL];
 #pragma unroll
-      for (int j = 0; j < EPL; ++j) acc[j] = 0.f + g[j];
-      apply_row<T>(bank, a, f, row, e0, v_lane, acc);
+      for (int j = 0; j < EPL; ++j) v[j] = 0.f;
+      if (a.dfm && v_lane) {
+        const uint4 vr = *reinterpret_cast<const uint4 *>(
+            reinterpret_cast<const T *>(bank.data) +
+            (toff_f + d.x) * static_cast<int64_t>(bank.row_stride) + e0);
+        Vec<T>::to_f32(vr, v);
+      }
+      hot.template run<true, MODE>(bank, a, f, d.x, t.perm + d.z, d.y, B, v, worker, e0, v_lane,
+                                   w_lane, live);
     }
     return;
   }
+
+  // a row hit once: one lookup, one update
+  const int64_t q = static_cast<int64_t>(blk - seg_blocks) * WPB + worker;
+  if (q >= B * F || !live) return;
+  const int code = lookup_table(ws, F, B)[q];
+  if (code < 0) return;
+  const int64_t b = q / F;
+  const int f = static_cast<int>(q - b * F);
+  const int64_t grow = toff[f] + code;
+  const uint4 raw = *reinterpret_cast<const uint4 *>(row_ptr_g<T, MODE>(bank, a, grow, e0));
+  float v[EPL];
+  if (a.dfm && v_lane) {
+    const uint4 vr = MODE == MREC_BWD_DENSE_GRAD
+                         ? *reinterpret_cast<const uint4 *>(reinterpret_cast<const T *>(bank.data) +
+                                                            grow * static_cast<int64_t>(bank.row_stride) + e0)
+                         : raw;
+    Vec<T>::to_f32(vr, v);
+  }
+  float acc[EPL];
+#pragma unroll
+  for (int j = 0; j < EPL; ++j) acc[j] = 0.f;
+  add_lookup_grad_v<EPL>(a, b, f, D, e0, v_lane, w_lane, v, acc);
+#if MREC_APPLY_EXP == 9
+  if (acc[0] == 12345.f) *(float *)a.grad = acc[1];
+  return;
+#endif
+  apply_row_raw_g<T, MODE>(bank, a, grow, e0, v_lane, acc, raw);
+}
+
+// ---------------------------------------------------------------------------
+// apply, sorted layout (batches up to MREC_BWD_MAX_BATCH): one LPR-lane worker
+// per segment (= unique row) sums its lookups in ascending sample order;
+// segments longer than kShortSeg are summed by the whole workgroup.  Grid:
+// F * seg_blocks segment blocks (table f = blk / seg_blocks), then the
+// co-launched reductions.
+// ---------------------------------------------------------------------------
+template <typename T, int LPR>
+__global__ __launch_bounds__(256, 6) void apply_kernel(BankArgs bank, int64_t B, const void *ws,
+                                                       ApplyArgs a, int seg_blocks,
+                                                       int apply_blocks, CoReduce co) {
+  if (static_cast<int>(blockIdx.x) >= apply_blocks) {  // uniform: a co-launched reduction
+    co_reduce(co, blockIdx.x - apply_blocks);
+    return;
+  }
+  if (a.d_step) a.seed += *a.d_step * 0x9e3779b97f4a7c15ull;
+  constexpr int EPL = Vec<T>::EPL;
+  constexpr int WPB = 256 / LPR;
+  __shared__ int32_t long_list[WPB];
+  __shared__ int32_t n_long;
+  __shared__ HotSeg<T, LPR> hot;
+  const int worker = threadIdx.x / LPR;
+  const int l = threadIdx.x % LPR;
+  const int e0 = l * EPL;
+  const int D = bank.dim;
+  const bool v_lane = e0 + EPL <= D;
+  const bool w_lane = bank.has_w && e0 == D;
+  const bool live = v_lane || w_lane;
+  const int blk = blockIdx.x;
   const int f = blk / seg_blocks;
   const TableWs t = table_ws(ws, f, B);
   const int ublk = (blk - f * seg_blocks) * WPB;
   const int u = ublk + worker;
-  // the segment descriptor is loaded together with the header (one latency)
-  int4 d = make_int4(0, 0, 0, 0);
-  if (hash_layout) {
-    if (u <= B / 2) d = t.desc[u];
-  } else if (u < B) {
-    d.x = t.uniq[u];
-    d.z = t.seg[u];
-    d.y = t.seg[u + 1] - d.z;
+  // the segment is loaded together with the header (one latency)
+  int row = 0, s0 = 0, n = 0;
+  if (u < B) {
+    row = t.uniq[u];
+    s0 = t.seg[u];
+    n = t.seg[u + 1] - s0;
   }
   const int nu = t.hdr[0];
   if (ublk >= nu) return;  // uniform per block
   if (threadIdx.x == 0) n_long = 0;
   __syncthreads();
 
-  const int row = d.x, n = d.y;
   bool mine = u < nu;
   if (mine && n > kShortSeg) {
     if (l == 0) long_list[atomicAdd(&n_long, 1)] = u;
@@ -330,108 +559,21 @@ __global__ __launch_bounds__(256, 6) void apply_kernel(BankArgs bank, int64_t B,
     float acc[EPL];
 #pragma unroll
     for (int j = 0; j < EPL; ++j) acc[j] = 0.f;
-    if (hash_layout && n == 2) {
-      // the common repeated row: both lookups in the descriptor, loaded together
-      float g0[EPL], g1[EPL];
-      lookup_grad<EPL>(a, min(d.z, d.w), f, D, e0, v_lane, w_lane, g0);
-      lookup_grad<EPL>(a, max(d.z, d.w), f, D, e0, v_lane, w_lane, g1);
-#pragma unroll
-      for (int j = 0; j < EPL; ++j) acc[j] = (acc[j] + g0[j]) + g1[j];
-    } else {
-      // sample indices of the segment (<= 16) in registers, ascending: the sorted
-      // layout has them in order, the hash layout is sorted here by a network
-      int r[kShortSeg];
-#pragma unroll
-      for (int j = 0; j < kShortSeg; ++j) r[j] = j < n ? t.perm[d.z + j] : INT_MAX;
-      if (hash_layout) {
-        if (n <= 4)
-          bitonic_sort<4>(r);
-        else if (n <= 8)
-          bitonic_sort<8>(r);
-        else
-          bitonic_sort<16>(r);
-      }
-#pragma unroll
-      for (int j = 0; j < kShortSeg; ++j)
-        if (j < n) add_lookup_grad<EPL>(a, r[j], f, D, e0, v_lane, w_lane, acc);
-    }
+    for (int j = 0; j < n; ++j) add_lookup_grad<EPL>(a, t.perm[s0 + j], f, D, e0, v_lane, w_lane, acc);
     apply_row_raw<T>(bank, a, f, row, e0, v_lane, acc, raw);
   }
   __syncthreads();
   const int nl = n_long;
-  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   for (int k = 0; k < nl; ++k) {
-    // each hot segment is summed independently, so the (atomic) list order
-    // does not change any result
+    // each hot segment is summed independently, so the (atomic) list order does
+    // not change any result; the sorted layout's perm is already ascending, the
+    // bitmap pass keeps it so
     const int uu = long_list[k];
-    int s0, sn, lrow;
-    if (hash_layout) {
-      const int4 dd = t.desc[uu];
-      lrow = dd.x;
-      sn = dd.y;
-      s0 = dd.z;
-    } else {
-      lrow = t.uniq[uu];
-      s0 = t.seg[uu];
-      sn = t.seg[uu + 1] - s0;
-    }
-    if (hash_layout) {
-      // ascending sample order through an LDS bitmap of the batch (B <= 8192
-      // entries; a sample / exchange slot looks a table up once, so the bits are
-      // the segment)
-      const int nwords = static_cast<int>((B + 31) / 32);  // <= 256: one per thread
-      if (tid < nwords) bits[tid] = 0u;
-      __syncthreads();
-      for (int i = tid; i < sn; i += 256) {
-        const int b = t.perm[s0 + i];
-        atomicOr(&bits[b >> 5], 1u << (b & 31));
-      }
-      __syncthreads();
-      const uint32_t word = tid < nwords ? bits[tid] : 0u;
-      const uint32_t c = __popc(word);
-      uint32_t incl = c;
-#pragma unroll
-      for (int off = 1; off < 64; off <<= 1) {
-        const uint32_t v = __shfl_up(incl, off);
-        if (lane >= off) incl += v;
-      }
-      if (lane == 63) wsum[wid] = incl;
-      __syncthreads();
-      if (tid < nwords) {
-        uint32_t pos = incl - c;
-        for (int k2 = 0; k2 < wid; ++k2) pos += wsum[k2];
-        uint32_t w = word;
-        while (w) {
-          const int bit = __ffs(w) - 1;
-          srt[pos++] = static_cast<uint16_t>(tid * 32 + bit);
-          w &= w - 1;
-        }
-      }
-      __syncthreads();
-    }
-    float acc[EPL];
-#pragma unroll
-    for (int j = 0; j < EPL; ++j) acc[j] = 0.f;
-    if (live)
-      for (int i = worker; i < sn; i += WPB)
-        add_lookup_grad<EPL>(a, hash_layout ? static_cast<int>(srt[i]) : t.perm[s0 + i], f, D,
-                             e0, v_lane, w_lane, acc);
-#pragma unroll
-    for (int j = 0; j < EPL; ++j) red[worker][e0 + j] = acc[j];
-    __syncthreads();
-    for (int sft = WPB / 2; sft > 0; sft >>= 1) {
-      if (worker < sft) {
-#pragma unroll
-        for (int j = 0; j < EPL; ++j) red[worker][e0 + j] += red[worker + sft][e0 + j];
-      }
-      __syncthreads();
-    }
-    if (worker == 0 && live) {
-#pragma unroll
-      for (int j = 0; j < EPL; ++j) acc[j] = red[0][e0 + j];
-      apply_row<T>(bank, a, f, lrow, e0, v_lane, acc);
-    }
-    __syncthreads();
+    const int lrow = t.uniq[uu];
+    const int ls0 = t.seg[uu];
+    const int sn = t.seg[uu + 1] - ls0;
+    hot.template run<false>(bank, a, f, lrow, t.perm + ls0, sn, B, nullptr, worker, e0, v_lane,
+                            w_lane, live);
   }
 }
 
@@ -444,7 +586,7 @@ mrec_status build_plan_job(const mrec_plan_job *plan, PlanJob *out) {
                  "plan batch must be in [1, MREC_BWD_HASH_MAX_BATCH] (padded exchange views: "
                  "[1, MREC_BWD_MAX_BATCH])");
   MREC_CHECK_ARG(plan->workspace != nullptr, "plan workspace is NULL");
-  if (plan->ws_bytes < static_cast<size_t>(out->bank.n_tables) * table_ws_bytes(plan->batch)) {
+  if (plan->ws_bytes < static_cast<size_t>(hash_ws_bytes(out->bank.n_tables, plan->batch))) {
     set_error("plan workspace too small");
     return MREC_ENOSPC;
   }
@@ -469,7 +611,11 @@ void mrec_plan_prof_read(uint64_t *out16) { hipMemcpyFromSymbol(out16, HIP_SYMBO
 
 size_t mrec_emb_bwd_workspace_size(int32_t n_tables, int64_t batch) {
   if (n_tables <= 0 || batch < 0) return 0;
-  return static_cast<size_t>(n_tables) * static_cast<size_t>(table_ws_bytes(batch));
+  // the larger of the two layouts (which one a call takes depends on whether its
+  // ids are a padded exchange view, not known here)
+  const int64_t sorted = int64_t(n_tables) * table_ws_bytes(batch);
+  const int64_t hashed = hash_ws_bytes(n_tables, batch);
+  return static_cast<size_t>(sorted > hashed ? sorted : hashed);
 }
 
 mrec_status mrec_emb_bwd_plan(const mrec_table_bank *bank, const mrec_ids *ids, int64_t batch,
@@ -491,7 +637,8 @@ mrec_status mrec_emb_bwd_plan(const mrec_table_bank *bank, const mrec_ids *ids, 
     MREC_CHECK_ARG(ba.rows[f] < (int64_t(1) << 31), "rows per table must be < 2^31");
   const int rounds = static_cast<int>((batch + kPlanThreads - 1) / kPlanThreads);
   if (batch >= 1 && hash_layout(batch, ia.pad_negative != 0)) {
-    plan_hash_kernel<<<dim3(ba.n_tables), kPlanThreads, 0, static_cast<hipStream_t>(stream)>>>(
+    plan_hash_kernel<<<dim3(ba.n_tables * kPlanBuckets), kPlanThreads, 0,
+                       static_cast<hipStream_t>(stream)>>>(
         ba, ia, batch, workspace, d_oob_flag, d_step);
     return launch_status("mrec_emb_bwd_plan");
   }
@@ -620,12 +767,15 @@ static mrec_status apply_impl(const mrec_table_bank *bank, int64_t batch, const 
   a.chunk_stride = chunk_stride;
   hipStream_t s = static_cast<hipStream_t>(stream);
   const int wpb = 256 / lpr;
-  // hash layout (batch <= kHashMaxKeys, see mrec_emb_bwd_plan): segments only for
-  // rows hit twice or more (<= batch / 2 of them), plus the sample-major blocks
+  // hash layout (batch <= kHashMaxKeys or an exchange view, see mrec_emb_bwd_plan):
+  // sample-major blocks + one hot-segment block per (table, bucket); sorted
+  // layout: one block per WPB segments of each table
   const bool hash = hash_layout(batch, g_occ != nullptr);  // given grads: an exchange view
-  const int seg_blocks = static_cast<int>(((hash ? batch / 2 : batch) + wpb - 1) / wpb);
+  const int seg_blocks = hash ? (batch > 0 ? F * kPlanBuckets : 0)
+                              : static_cast<int>((batch + wpb - 1) / wpb);
   const int64_t sm_blocks = hash ? (batch * F + wpb - 1) / wpb : 0;
-  const int apply_blocks = static_cast<int>(static_cast<int64_t>(seg_blocks) * F + sm_blocks);
+  const int apply_blocks =
+      static_cast<int>(hash ? seg_blocks + sm_blocks : static_cast<int64_t>(seg_blocks) * F);
   CoReduce co = {};
   int co_blocks = 0;
   MREC_CHECK_ARG(n_reduce >= 0 && n_reduce <= kMaxCoReduce && (n_reduce == 0 || reduce),
@@ -643,9 +793,18 @@ static mrec_status apply_impl(const mrec_table_bank *bank, int64_t batch, const 
   co.start[co.n] = co_blocks;
   if (apply_blocks + co_blocks == 0) return MREC_OK;  // (batch 0 still runs the reductions)
   const dim3 grid(static_cast<unsigned>(apply_blocks + co_blocks));
-#define MREC_AK(T, L) \
-  apply_kernel<T, L><<<grid, 256, 0, s>>>(ba, batch, workspace, a, seg_blocks, hash ? 1 : 0, \
-                                          apply_blocks, co)
+#define MREC_AKM(T, L, M) \
+  apply_hash_kernel<T, L, M><<<grid, 256, 0, s>>>(ba, batch, workspace, a, seg_blocks, static_cast<int>(sm_blocks), co)
+#define MREC_AK(T, L)                                                                            \
+  do {                                                                                           \
+    if (hash) {                                                                                  \
+      if (mode == MREC_BWD_SGD) MREC_AKM(T, L, MREC_BWD_SGD);                                    \
+      else if (mode == MREC_BWD_SGD_SR) MREC_AKM(T, L, MREC_BWD_SGD_SR);                         \
+      else MREC_AKM(T, L, MREC_BWD_DENSE_GRAD);                                                  \
+    } else                                                                                       \
+      apply_kernel<T, L><<<grid, 256, 0, s>>>(ba, batch, workspace, a, seg_blocks, apply_blocks, \
+                                              co);                                               \
+  } while (0)
   if (bank->dtype == MREC_BF16) {
     switch (lpr) {
       case 1: MREC_AK(uint16_t, 1); break;
@@ -664,5 +823,6 @@ static mrec_status apply_impl(const mrec_table_bank *bank, int64_t batch, const 
     }
   }
 #undef MREC_AK
+#undef MREC_AKM
   return launch_status("mrec_emb_bwd_apply");
 }

@@ -227,11 +227,10 @@ template <typename T, int LPR, bool X0_BF16>
 __global__ __launch_bounds__(1024) void interact_plan_kernel(BankArgs bank, IdsArgs ids, int64_t B,
                                                              InteractArgs ia, PlanJob plan,
                                                              int plan_blocks) {
-  __shared__ uint32_t smem[2 * kHashSlots + 1];
-  if (static_cast<int>(blockIdx.x) < plan_blocks) {  // uniform
-    if (static_cast<int>(blockIdx.x) < plan.bank.n_tables)
-      plan_hash_body<1024, kHashSlots>(plan.bank, plan.ids, plan.B, plan.ws, plan.oob,
-                                       plan.d_step, blockIdx.x, smem);
+  __shared__ uint32_t smem[2 * kHashSlots + 2];
+  if (static_cast<int>(blockIdx.x) < plan_blocks) {  // uniform: (table, bucket) plans
+    plan_hash_body<1024, kHashSlots>(plan.bank, plan.ids, plan.B, plan.ws, plan.oob, plan.d_step,
+                                     blockIdx.x / kPlanBuckets, blockIdx.x % kPlanBuckets, smem);
     return;
   }
   const int64_t b = static_cast<int64_t>(blockIdx.x - plan_blocks) * 16 + (threadIdx.x >> 6);
@@ -301,7 +300,7 @@ static void launch_gather(int lpr, const BankArgs &ba, const IdsArgs &ia, int64_
 template <typename T, bool XB>
 static void launch_interact(int lpr, const BankArgs &ba, const IdsArgs &ids, int64_t B,
                             const InteractArgs &ia, const PlanJob *plan, hipStream_t s) {
-  const int pb = plan ? plan->bank.n_tables : 0;
+  const int pb = plan ? plan->bank.n_tables * kPlanBuckets : 0;
   const dim3 grid(static_cast<unsigned>((B + 3) / 4));
   const dim3 grid_p(static_cast<unsigned>(pb + (B + 15) / 16));
 #define MREC_IK(L)                                                                          \

@@ -8,23 +8,18 @@ namespace mrec {
 
 constexpr int kPlanThreads = 1024;
 
-struct TableWs {  // per-table workspace view
+struct TableWs {  // per-table workspace view of the sorted layout
   int32_t *hdr;   // [4] = {n segments, n lookups in segments, 0, layout}
-  int4 *desc;     // [Bp/2+4] hash layout: segment u = {row, n, b0 | start, b1}
   int32_t *perm;  // [Bp]   sample index of position i
-  int32_t *seg;   // [Bp+1] sorted layout: segment starts
-  int32_t *uniq;  // [Bp]   sorted layout: local row id of segment u
-  int32_t *lut;   // [Bp]   hash layout: row of lookup b if no other lookup hits it, else -1
+  int32_t *seg;   // [Bp+1] segment starts
+  int32_t *uniq;  // [Bp]   local row id of segment u
 };
-// layout 0 (sorted plan): segments in ascending row order, each segment's
-//   lookups in ascending sample order in perm, segment u = [seg[u], seg[u + 1]).
-// layout 1 (hash plan): only rows hit more than once get a segment (<= B/2 of
-//   them), in arbitrary order; a row hit once is listed in lut[b] of its lookup
-//   and updated sample-major by apply.  Segment u is desc[u] = {row, n, b0, b1}
-//   when n == 2 (both lookups in the descriptor) and {row, n, start, -} with the
-//   lookups in perm[start, start + n) otherwise.  The order of a segment's
-//   lookups is arbitrary -- apply restores ascending sample order itself, so
-//   the arithmetic is identical to layout 0.
+// layout 0 (sorted plan, batches up to MREC_BWD_MAX_BATCH): segments in
+//   ascending row order, each segment's lookups in ascending sample order in
+//   perm, segment u = [seg[u], seg[u + 1]).
+// layout 1 (hash plan, batch <= MREC_BWD_HASH_MAX_BATCH or a padded exchange view):
+//   per (table, bucket) descriptors of the rows hit more than once, and the
+//   sample-major lookup table lut[b][f] (below, BucketWs / lookup_table).
 constexpr int kLayoutSorted = 0;
 constexpr int kLayoutHash = 1;
 
@@ -32,7 +27,7 @@ __host__ __device__ inline int64_t pad4(int64_t x) { return (x + 3) & ~int64_t(3
 
 __host__ __device__ inline int64_t table_ws_bytes(int64_t batch) {
   const int64_t bp = pad4(batch);
-  int64_t bytes = 16 + 16 * (bp / 2 + 4) + 4 * (bp + (bp + 4) + bp + bp);
+  int64_t bytes = 16 + 4 * (bp + (bp + 4) + bp);
   return (bytes + 255) & ~int64_t(255);
 }
 
@@ -41,11 +36,9 @@ __host__ __device__ inline TableWs table_ws(const void *ws, int f, int64_t batch
   const int64_t bp = pad4(batch);
   TableWs t;
   t.hdr = reinterpret_cast<int32_t *>(base);
-  t.desc = reinterpret_cast<int4 *>(base + 16);
-  t.perm = reinterpret_cast<int32_t *>(t.desc + bp / 2 + 4);
+  t.perm = reinterpret_cast<int32_t *>(base + 16);
   t.seg = t.perm + bp;
   t.uniq = t.seg + bp + 4;
-  t.lut = t.uniq + bp;
   return t;
 }
 
@@ -63,82 +56,164 @@ __device__ uint64_t g_plan_prof[16];
 #endif
 
 // ---------------------------------------------------------------------------
-// hash plan (batch <= 4096).  A workgroup barrier costs ~135 ns at 1024 threads
-// (tools/micro/barrier.hip) and every 4-bit radix pass needs six, so the sorted
-// plan spends most of its time in barriers.  The hash plan needs three:
-//   1. insert: each valid id goes into an LDS hash table (linear probing),
-//      counting its lookups (low 16 bits of the slot word);
-//   2. claim: a row hit once is written to lut[i] of its lookup; otherwise every
-//      lookup takes a ticket on its slot (high 16 bits) and ticket 0 allocates
-//      the row's segment -- a wave-aggregated packed atomic hands out
-//      {segment index, start} -- and publishes the start in the slot;
-//   3. place: lookup i of a repeated row goes to perm[start + ticket].
-// Segment order and the order inside a segment follow the atomics, so the
-// workspace layout is not deterministic; apply sorts every segment's lookups
-// back into ascending sample order, so the updates are.
+// hash plan (batch <= 4096; padded exchange views <= 8192 entries).
+//
+// Work split: table f's rows are cut into kPlanBuckets buckets by a hash of the
+// row id, and one workgroup plans each (table, bucket): it loads all of the
+// table's ids (L2 hits after the first), keeps the ones of its bucket and groups
+// them in an LDS hash table.  Buckets partition the rows, so no row's lookups
+// are split over workgroups and no cross-workgroup merge is needed; a table's
+// plan runs on 4 CUs instead of 1 (C2: 104 workgroups beside the interaction).
+// A workgroup barrier costs ~135 ns at 1024 threads (tools/micro/barrier.hip);
+// the body needs three:
+//   1. insert: each id of the bucket goes into the hash table (linear probing;
+//      tables of <= SLOTS rows index the slots directly), counting its lookups;
+//   2. claim: every lookup takes a ticket on its slot; a row hit once writes its
+//      row into the sample-major lookup table lut[b][f], the lookups of a
+//      repeated row write -1 there and ticket 0 allocates the row's segment
+//      (wave-aggregated packed LDS atomic: {segment, perm start}) and publishes
+//      the start in the slot;
+//   3. place: lookup i of a repeated row goes into the segment descriptor (two
+//      lookups) or to perm[start + ticket].
+// Segments longer than short_seg (hot rows) are also listed in the bucket's long
+// list, which apply sums with a whole workgroup.  The order of a segment's
+// lookups follows the atomics; apply sorts them back into ascending sample
+// order, so the arithmetic does not depend on the schedule.
 // ---------------------------------------------------------------------------
 constexpr int kHashMaxKeys = 4096;     // dense batches up to this use the hash plan
 constexpr int kHashMaxEntries = 8192;  // padded exchange views (ids.pad_negative) up to this:
                                        // their valid ids are ~1/2 of the entries (cap = 2x share)
-constexpr int kHashSlots = 8192;  // load factor <= 1/2 (standalone 1024-thread kernel)
-constexpr int kHashSlotsSmall = 6016;  // 47 KiB: the plan inside a GEMM launch (<= 48 KiB LDS)
+constexpr int kHashSlots = 8192;       // per workgroup: any bucket fits at load factor <= 1/2
+constexpr int kPlanBuckets = 4;        // workgroups per table
+constexpr int kShortSeg = 16;          // longer segments: the bucket's long list
 constexpr uint32_t kEmpty = 0xffffffffu;
+
+// segments up to this many lookups are summed by one wave of the apply (one
+// lookup per LPR-lane worker), longer ones by a whole workgroup
+__host__ __device__ inline int short_seg(int lpr) {
+  return 64 / lpr < kShortSeg ? 64 / lpr : kShortSeg;
+}
 
 // hash layout for `batch` entries (the same rule in plan and apply)
 __host__ __device__ inline bool hash_layout(int64_t batch, bool padded) {
   return batch <= kHashMaxKeys || (padded && batch <= kHashMaxEntries);
 }
 
+__host__ __device__ inline uint32_t plan_bucket(uint32_t key) {
+  return (key * 0x85ebca77u) >> (32 - 2);  // top 2 bits: kPlanBuckets = 4
+}
+static_assert(kPlanBuckets == 4, "plan_bucket takes the top 2 bits");
+
+// hash-layout workspace: F x kPlanBuckets bucket regions, then lut[B][F]
+struct BucketWs {
+  int32_t *hdr;    // [4] = {segments, perm entries, long segments, layout}
+  int4 *desc;      // [seg_cap] segment u = {row, n, b0 | perm start, b1}
+  int32_t *perm;   // [B] lookups of segments with n > 2
+  int32_t *longl;  // [B / kShortSeg + 4] segment ids of the long segments
+};
+
+__host__ __device__ inline int64_t seg_cap(int64_t batch) { return batch / 2 + 4; }
+
+__host__ __device__ inline int64_t bucket_ws_bytes(int64_t batch) {
+  const int64_t bp = pad4(batch);
+  const int64_t bytes = 16 + 16 * seg_cap(batch) + 4 * bp + 4 * (bp / kShortSeg + 4);
+  return (bytes + 255) & ~int64_t(255);
+}
+
+__host__ __device__ inline int64_t hash_ws_bytes(int n_tables, int64_t batch) {
+  const int64_t lut = (4 * pad4(batch) * n_tables + 255) & ~int64_t(255);
+  const int64_t offs = (8 * int64_t(n_tables) + 255) & ~int64_t(255);
+  return int64_t(n_tables) * kPlanBuckets * bucket_ws_bytes(batch) + lut + offs;
+}
+
+__host__ __device__ inline BucketWs bucket_ws(const void *ws, int f, int r, int64_t batch) {
+  char *base = static_cast<char *>(const_cast<void *>(ws)) +
+               (int64_t(f) * kPlanBuckets + r) * bucket_ws_bytes(batch);
+  BucketWs t;
+  t.hdr = reinterpret_cast<int32_t *>(base);
+  t.desc = reinterpret_cast<int4 *>(base + 16);
+  t.perm = reinterpret_cast<int32_t *>(t.desc + seg_cap(batch));
+  t.longl = t.perm + pad4(batch);
+  return t;
+}
+
+// lut[b * F + f]: row (>= 0) of a row hit once, -1 otherwise (a repeated row's
+// lookup, an invalid id)
+__host__ __device__ inline int32_t *lookup_table(const void *ws, int n_tables, int64_t batch) {
+  return reinterpret_cast<int32_t *>(static_cast<char *>(const_cast<void *>(ws)) +
+                                     int64_t(n_tables) * kPlanBuckets * bucket_ws_bytes(batch));
+}
+
+// the bank's table row offsets, copied by the plan: the apply indexes them per
+// lane from memory (a per-lane index into the kernel-argument array would be
+// lowered to a select chain over all of it in scalar registers)
+__host__ __device__ inline int64_t *table_offsets(const void *ws, int n_tables, int64_t batch) {
+  return reinterpret_cast<int64_t *>(
+      reinterpret_cast<char *>(lookup_table(ws, n_tables, batch)) +
+      ((4 * pad4(batch) * n_tables + 255) & ~int64_t(255)));
+}
+
+// smem: 2 * SLOTS + 2 words.  Called by all THREADS threads of the workgroup that
+// plans (table f, bucket r).
 template <int THREADS, int SLOTS, int MAXB = kHashMaxEntries>
 __device__ __forceinline__ void plan_hash_body(const BankArgs &bank, const IdsArgs &ids, int64_t B,
                                                void *ws, int32_t *__restrict__ oob,
-                                               uint64_t *__restrict__ d_step, int f,
+                                               uint64_t *__restrict__ d_step, int f, int r,
                                                uint32_t *smem) {
   constexpr int kRounds = MAXB / THREADS;
   uint32_t *hkey = smem;          // [SLOTS] row id; after the claim: (segment << 16) | start
   uint32_t *hcnt = smem + SLOTS;  // [SLOTS] (tickets << 16) | lookups
-  uint32_t &s_tot = smem[2 * SLOTS];  // (segments << 16) | lookups placed
+  uint32_t &s_tot = smem[2 * SLOTS];       // (segments << 16) | perm entries
+  uint32_t &s_long = smem[2 * SLOTS + 1];  // long segments
   const int tid = threadIdx.x, lane = tid & 63;
+  const int F = bank.n_tables;
   const uint32_t rows = static_cast<uint32_t>(bank.rows[f]);
   const bool direct = rows <= static_cast<uint32_t>(SLOTS);
-  const TableWs t = table_ws(ws, f, B);
+  const BucketWs t = bucket_ws(ws, f, r, B);
+  int32_t *__restrict__ lut = lookup_table(ws, F, B);
   PLAN_STAMP(0);
   // ids of this thread's lookups, loads issued before anything waits on them
   int64_t id[kRounds];
 #pragma unroll
-  for (int r = 0; r < kRounds; ++r) {
-    const int i = r * THREADS + tid;
-    id[r] = i < B ? load_id(ids, f, i) : -1;
+  for (int k = 0; k < kRounds; ++k) {
+    const int i = k * THREADS + tid;
+    id[k] = i < B ? load_id(ids, f, i) : -1;
   }
   for (int i = tid; i < SLOTS; i += THREADS) {
     hkey[i] = kEmpty;
     hcnt[i] = 0u;
   }
-  if (tid == 0) s_tot = 0u;
+  if (tid == 0) {
+    s_tot = 0u;
+    s_long = 0u;
+  }
   __syncthreads();
   PLAN_STAMP(1);
-  // 1. insert
+  // 1. insert (this bucket's valid ids); invalid ids are bucket 0's
   uint32_t slot[kRounds];
 #pragma unroll
-  for (int r = 0; r < kRounds; ++r) {
-    const int i = r * THREADS + tid;
-    slot[r] = kEmpty;
+  for (int k = 0; k < kRounds; ++k) {
+    const int i = k * THREADS + tid;
+    slot[k] = kEmpty;
     if (i < B) {
-      if (id[r] >= 0 && id[r] < static_cast<int64_t>(rows)) {
-        const uint32_t key = static_cast<uint32_t>(id[r]);
-        uint32_t h = key;  // tables of <= SLOTS rows index the slots directly
-        if (!direct) {
-          h = static_cast<uint32_t>((static_cast<uint64_t>(key * 2654435761u) * SLOTS) >> 32);
-          for (;;) {
-            const uint32_t old = atomicCAS(&hkey[h], kEmpty, key);
-            if (old == kEmpty || old == key) break;
-            h = h + 1 == SLOTS ? 0u : h + 1;
+      if (id[k] >= 0 && id[k] < static_cast<int64_t>(rows)) {
+        const uint32_t key = static_cast<uint32_t>(id[k]);
+        if (plan_bucket(key) == static_cast<uint32_t>(r)) {
+          uint32_t h = key;
+          if (!direct) {
+            h = static_cast<uint32_t>((static_cast<uint64_t>(key * 2654435761u) * SLOTS) >> 32);
+            for (;;) {
+              const uint32_t old = atomicCAS(&hkey[h], kEmpty, key);
+              if (old == kEmpty || old == key) break;
+              h = h + 1 == SLOTS ? 0u : h + 1;
+            }
           }
+          atomicAdd(&hcnt[h], 1u);
+          slot[k] = h;
         }
-        atomicAdd(&hcnt[h], 1u);
-        slot[r] = h;
-      } else if (oob && !(ids.pad_negative && id[r] < 0)) {
-        *oob = 1;
+      } else if (r == 0) {
+        lut[static_cast<int64_t>(i) * F + f] = -1;
+        if (oob && !(ids.pad_negative && id[k] < 0)) *oob = 1;
       }
     }
   }
@@ -148,29 +223,29 @@ __device__ __forceinline__ void plan_hash_body(const BankArgs &bank, const IdsAr
   const uint64_t lt = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
   uint32_t ticket[kRounds], count[kRounds];
 #pragma unroll
-  for (int r = 0; r < kRounds; ++r) {
-    ticket[r] = 0;
-    count[r] = 0;
+  for (int k = 0; k < kRounds; ++k) {
+    ticket[k] = 0;
+    count[k] = 0;
   }
 #pragma unroll
-  for (int r = 0; r < kRounds; ++r) {
-    if (r * THREADS >= B) break;  // uniform
+  for (int k = 0; k < kRounds; ++k) {
+    if (k * THREADS >= B) break;  // uniform
+    const int i = k * THREADS + tid;
     uint32_t cnt = 0;
-    if (slot[r] != kEmpty) {
-      const uint32_t old = atomicAdd(&hcnt[slot[r]], 1u << 16);
-      ticket[r] = old >> 16;
+    if (slot[k] != kEmpty) {
+      const uint32_t old = atomicAdd(&hcnt[slot[k]], 1u << 16);
+      ticket[k] = old >> 16;
       cnt = old & 0xffffu;
-      count[r] = cnt;
+      count[k] = cnt;
+      const uint32_t row = direct ? slot[k] : hkey[slot[k]];
+      if (cnt == 1) lut[static_cast<int64_t>(i) * F + f] = static_cast<int32_t>(row);
+      else if (ticket[k] != 0) lut[static_cast<int64_t>(i) * F + f] = -1;
     }
-    {
-      const int i = r * THREADS + tid;
-      if (i < B)
-        t.lut[i] = cnt == 1 ? static_cast<int32_t>(direct ? slot[r] : hkey[slot[r]]) : -1;
-    }
-    const bool claim = cnt > 1 && ticket[r] == 0;
+    const bool claim = cnt > 1 && ticket[k] == 0;
     const uint64_t mc = __ballot(claim);
     if (mc == 0) continue;  // uniform
-    uint32_t incl = claim ? cnt : 0u;  // inclusive scan of the claimed lengths
+    const uint32_t need = (claim && cnt > 2) ? cnt : 0u;  // perm entries
+    uint32_t incl = need;  // inclusive scan of the perm entries claimed
 #pragma unroll
     for (int off = 1; off < 64; off <<= 1) {
       const uint32_t v = __shfl_up(incl, off);
@@ -182,34 +257,39 @@ __device__ __forceinline__ void plan_hash_body(const BankArgs &bank, const IdsAr
     base = __shfl(base, last);
     if (claim) {
       const uint32_t u = (base >> 16) + __popcll(mc & lt);
-      const uint32_t start = (base & 0xffffu) + incl - cnt;
+      const uint32_t start = (base & 0xffffu) + incl - need;
+      const uint32_t row = direct ? slot[k] : hkey[slot[k]];
       int32_t *d = reinterpret_cast<int32_t *>(t.desc + u);
-      d[0] = static_cast<int32_t>(direct ? slot[r] : hkey[slot[r]]);
+      d[0] = static_cast<int32_t>(row);
       d[1] = static_cast<int32_t>(cnt);
       if (cnt > 2) d[2] = static_cast<int32_t>(start);
-      hkey[slot[r]] = (u << 16) | start;  // only the claimer reads this slot's key
+      hkey[slot[k]] = (u << 16) | start;  // only the claimer reads this slot's key
+      lut[static_cast<int64_t>(i) * F + f] = -1;
+      if (cnt > static_cast<uint32_t>(short_seg(bank.lpr)))
+        t.longl[atomicAdd(&s_long, 1u)] = static_cast<int32_t>(u);
     }
   }
   __syncthreads();
   PLAN_STAMP(3);
   // 3. place
 #pragma unroll
-  for (int r = 0; r < kRounds; ++r) {
-    const int i = r * THREADS + tid;
-    if (i < B && count[r] > 1) {
-      const uint32_t us = hkey[slot[r]];
-      if (count[r] == 2)
-        reinterpret_cast<int32_t *>(t.desc + (us >> 16))[2 + ticket[r]] = i;
+  for (int k = 0; k < kRounds; ++k) {
+    const int i = k * THREADS + tid;
+    if (i < B && count[k] > 1) {
+      const uint32_t us = hkey[slot[k]];
+      if (count[k] == 2)
+        reinterpret_cast<int32_t *>(t.desc + (us >> 16))[2 + ticket[k]] = i;
       else
-        t.perm[(us & 0xffffu) + ticket[r]] = i;
+        t.perm[(us & 0xffffu) + ticket[k]] = i;
     }
   }
   if (tid == 0) {
     t.hdr[0] = static_cast<int32_t>(s_tot >> 16);
     t.hdr[1] = static_cast<int32_t>(s_tot & 0xffffu);
-    t.hdr[2] = 0;
+    t.hdr[2] = static_cast<int32_t>(s_long);
     t.hdr[3] = kLayoutHash;
-    if (d_step && f == 0) *d_step += 1;
+    if (r == 0) table_offsets(ws, F, B)[f] = bank.row_offset[f];
+    if (d_step && f == 0 && r == 0) *d_step += 1;
   }
   PLAN_STAMP(4);
 }

@@ -27,7 +27,6 @@
 #include <algorithm>
 
 #include "common.h"
-#include "emb_plan.h"
 #include "gemm_common.h"
 #include "head_common.h"
 
@@ -372,7 +371,7 @@ enum : int { JOB_GEMM_RR = 0, JOB_GEMM_RC = 1, JOB_GEMM_CR = 2, JOB_GEMM_CC = 3,
 
 struct MultiArgs {
   int n;
-  int plan_blocks;  // leading workgroups that run `plan` (one per table, padded to 8)
+  int plan_blocks;  // 0 (the embedding-backward plan rides in the interaction launch)
   int fin_blocks;   // then the CTR head finish (padded to 8)
   HeadFinishArgs fin;
   int kind[MULTI_MAX];
@@ -380,20 +379,10 @@ struct MultiArgs {
   int nblk[MULTI_MAX];         // workgroups with work (the rest pad to a multiple of 8)
   int start[MULTI_MAX + 1];
   GemmArgs g[MULTI_MAX];
-  PlanJob plan;
 };
-
-static_assert((2 * kHashSlotsSmall + 1) * 4 <= kGemmLdsMin, "plan table exceeds the GEMM LDS");
 
 __global__ __launch_bounds__(GEMM_THREADS) void gemm_multi_kernel(MultiArgs ma) {
   extern __shared__ __attribute__((aligned(16))) uint16_t smem[];
-  if (static_cast<int>(blockIdx.x) < ma.plan_blocks) {  // uniform
-    if (static_cast<int>(blockIdx.x) < ma.plan.bank.n_tables)
-      plan_hash_body<GEMM_THREADS, kHashSlotsSmall, kHashMaxKeys>(ma.plan.bank, ma.plan.ids, ma.plan.B,
-                                                     ma.plan.ws, ma.plan.oob, ma.plan.d_step,
-                                                     blockIdx.x, reinterpret_cast<uint32_t *>(smem));
-    return;
-  }
   if (static_cast<int>(blockIdx.x) < ma.plan_blocks + ma.fin_blocks) {  // uniform
     const int fb = blockIdx.x - ma.plan_blocks;
     if (fb < head_finish_blocks(ma.fin.H, ma.fin.ns))
@@ -643,12 +632,10 @@ mrec_status mrec_gemm_multi_ex(int32_t n, const mrec_gemm_call *calls, const mre
     ma.fin_blocks = (f.H + 1 + f.ns + 7) / 8;
     ma.fin_blocks = (ma.fin_blocks + 7) / 8 * 8;
   }
-  if (plan) {
-    mrec_status st = build_plan_job(plan, &ma.plan);
-    if (st != MREC_OK) return st;
-    MREC_CHECK_ARG(ma.plan.B <= kHashMaxKeys, "a plan inside a GEMM launch takes <= 4096 ids");
-    ma.plan_blocks = (ma.plan.bank.n_tables + 7) / 8 * 8;
-  }
+  // the embedding-backward plan runs in the interaction launch (mrec_interact_fwd_ex):
+  // inside a GEMM launch it held the GEMM at half occupancy (the plan body's registers)
+  MREC_CHECK_ARG(plan == nullptr, "a plan job inside a GEMM launch is no longer supported: "
+                                  "pass it to mrec_interact_fwd_ex");
   int blocks = 0;
   for (int i = 0; i < n; ++i) {
     const mrec_gemm_call &c = calls[i];

@@ -163,23 +163,6 @@ class _Call:
 
 
 _PENDING = []  # deferred split-K reductions (fused SGD of a layer's W, b and images)
-_PLAN = []  # at most one embedding-backward plan waiting to ride along a GEMM launch
-
-
-def defer_plan(plan):
-    """Queue an embedding-backward hash plan (``embedding._FusedPlan``) to run in
-    the workgroups of the next mrec_gemm_multi launch (a HIP graph serialises
-    kernels, so a plan kernel of its own would sit on the critical path).  The
-    plan launches itself standalone if its consumer needs it first."""
-    _PLAN[:] = [plan]
-
-
-def _take_plan():
-    while _PLAN:
-        p = _PLAN.pop()
-        if not p.launched:
-            return p
-    return None
 
 
 def launch_multi(calls):
@@ -240,16 +223,12 @@ def _run(jobs):
     if not jobs:
         return
     arr = (_mrec.GemmCall * len(jobs))(*[j.struct() for j in jobs])
-    plan = _take_plan()
     fin = _FINISH.pop(0) if _FINISH else None
-    if plan is None and fin is None:
+    if fin is None:
         _mrec.call("mrec_gemm_multi", len(jobs), arr, _mrec.stream_handle())
         return
-    pj = plan.job() if plan is not None else None
-    _mrec.call("mrec_gemm_multi_ex", len(jobs), arr, ctypes.byref(pj) if pj is not None else None,
-               ctypes.byref(fin.struct) if fin is not None else None, _mrec.stream_handle())
-    if plan is not None:
-        plan.launched = True
+    _mrec.call("mrec_gemm_multi_ex", len(jobs), arr, None, ctypes.byref(fin.struct),
+               _mrec.stream_handle())
 
 
 def flush_pending():

@@ -210,47 +210,7 @@ class _AsyncPlan(_AsyncPlanBase):
         super().__init__(bank.weight.device, lambda: _plan(bank, ids, 0, batch, None), ids)
 
 
-class _FusedPlan:
-    """Hash plan (batch <= BWD_HASH_MAX_BATCH) run by spare workgroups of the next
-    backward GEMM launch (``dense.defer_plan``), on the same stream; ``get`` launches
-    it on its own if no GEMM launch took it (no MLP, or not fused-SGD)."""
-
-    def __init__(self, bank: EmbeddingBank, ids, batch: int):
-        from pytorchrec_amd import dense as dense_ops
-        n = bank.n_tables
-        self.ws_bytes = _mrec.lib().mrec_emb_bwd_workspace_size(n, batch)
-        self.ws = torch.empty(self.ws_bytes, dtype=torch.uint8, device=bank.weight.device)
-        self.bank, self.ids, self.batch = bank, ids, batch
-        self.idd = _ids_desc(ids)
-        self.launched = False
-        dense_ops.defer_plan(self)
-
-    def job(self) -> _mrec.PlanJob:
-        desc = self.bank.desc()
-        desc.ref()  # refresh the data pointer
-        self._job = _mrec.PlanJob(ctypes.pointer(desc.struct), ctypes.pointer(self.idd.struct),
-                                  self.batch, self.ws.data_ptr(), self.ws_bytes, None,
-                                  self.bank.step_counter().data_ptr())
-        return self._job
-
-    def get(self):
-        if not self.launched:
-            _mrec.call("mrec_emb_bwd_plan", self.bank.desc().ref(), self.idd.ref(), self.batch,
-                       self.ws.data_ptr(), self.ws_bytes, None,
-                       self.bank.step_counter().data_ptr(), _mrec.stream_handle())
-            self.launched = True
-        return self.ws, self.ws_bytes
-
-
-# The plan inside a backward GEMM launch (256-thread workgroups sharing CUs with
-# the GEMM) measured slower than the standalone 1024-thread plan kernel (C2:
-# 36-48 us launch vs 19 + 10 us), so it is opt-in (MREC_FUSE_PLAN=1).
-FUSE_PLAN = os.environ.get("MREC_FUSE_PLAN", "0") == "1"
-
-
 def _make_plan(bank: EmbeddingBank, ids, batch: int):
-    if FUSE_PLAN and 1 <= batch <= _mrec.BWD_HASH_MAX_BATCH:
-        return _FusedPlan(bank, ids, batch)
     if torch.cuda.is_current_stream_capturing():
         # a HIP graph runs its kernels one after another anyway, and the side
         # stream's fork/join cost 11 us per step (C2): plan in the backward
@@ -333,7 +293,7 @@ def _backward_into_bank(bank: EmbeddingBank, ids, batch, plan_ws, dx=None, dfm=N
     if bank.update == "dense":
         grad = torch.zeros_like(bank.weight)
     if plan_ws is not None:
-        ws, wsb = plan_ws.get() if isinstance(plan_ws, (_AsyncPlan, _FusedPlan)) else plan_ws
+        ws, wsb = plan_ws.get() if isinstance(plan_ws, _AsyncPlan) else plan_ws
         _apply(bank, ws, wsb, batch, dx, dfm, fm_sum, x0, dw, grad)
         return grad
     if batch > _mrec.BWD_MAX_BATCH and bank.total_rows <= LARGE_MAX_ROWS and LARGE_BATCH:

@@ -411,9 +411,12 @@ def test_fm2_dense_kernel(gpu):
 
 
 @pytest.mark.parametrize("rows", [7, 5000, 200000])
-def test_plan_inside_gemm_launch_matches_standalone(gpu, rows):
-    """mrec_gemm_multi_ex's plan (256-thread workgroups, 6016-slot table) drives
-    the same updates as the standalone 1024-thread plan kernel: bitwise."""
+def test_plan_inside_interaction_launch_matches_standalone(gpu, rows):
+    """The (table, bucket) hash plan run by leading workgroups of the interaction
+    launch (mrec_interact_fwd_ex) drives the same updates as the standalone plan
+    kernel: bitwise, on hot Zipf rows, uniform rows and a table of 7 rows (every
+    row repeated: direct-indexed slots); and a plan job inside a GEMM launch is
+    refused (ABI 12)."""
     import ctypes
     from pytorchrec_amd import _mrec
     rng = np.random.default_rng(rows)
@@ -433,8 +436,13 @@ def test_plan_inside_gemm_launch_matches_standalone(gpu, rows):
             job = _mrec.PlanJob(ctypes.pointer(bank.desc().struct), ctypes.pointer(idd.struct), B,
                                 ws.data_ptr(), wsb, None, None)
             bank.desc().ref()
-            _mrec.call("mrec_gemm_multi_ex", 0, None, ctypes.byref(job), None,
-                       _mrec.stream_handle())
+            logit = torch.empty(B, device=gpu)
+            _mrec.call("mrec_interact_fwd_ex", bank.desc().ref(), idd.ref(), B, None, 0, 0, None,
+                       None, 0, None, _mrec.F32, 0, 0, logit.data_ptr(), None, None,
+                       ctypes.byref(job), _mrec.stream_handle())
+            with pytest.raises(_mrec.MrecError):
+                _mrec.call("mrec_gemm_multi_ex", 0, None, ctypes.byref(job), None,
+                           _mrec.stream_handle())
         else:
             _mrec.call("mrec_emb_bwd_plan", bank.desc().ref(), idd.ref(), B, ws.data_ptr(), wsb,
                        None, None, _mrec.stream_handle())

@@ -32,7 +32,7 @@
 extern "C" {
 #endif
 
-#define MREC_ABI_VERSION 12
+#define MREC_ABI_VERSION 13
 #define MREC_MAX_TABLES 64      /* tables per table bank / per call */
 #define MREC_BWD_MAX_BATCH 8192  /* lookups per table per plan/apply call */
 #define MREC_BWD_HASH_MAX_BATCH 4096  /* batches up to this use the hash plan */
@@ -60,6 +60,8 @@ typedef void *mrec_stream; /* hipStream_t */
  * Replaces F x torch.nn.Embedding(rows_f, dim) (+ Embedding(rows_f, 1) biases)
  * built in IModel._init_weights (FunkSVD.py:39-41, SVDPP.py:36-42).
  */
+struct mrec_optim_s; /* mrec_optim: the fused row-sparse optimizer state, below */
+
 typedef struct {
   void *data;                 /* device */
   const int64_t *row_offset;  /* HOST [n_tables] */
@@ -69,6 +71,9 @@ typedef struct {
   int32_t row_stride; /* elements */
   int32_t has_w;
   mrec_dtype dtype; /* MREC_F32 or MREC_BF16 */
+  /* HOST, may be NULL: optimizer state of the fused updates MREC_BWD_ADAGRAD /
+   * _ROWWISE_ADAGRAD / _ADAM (the state belongs to the table like its rows) */
+  const struct mrec_optim_s *optim;
 } mrec_table_bank;
 
 /*
@@ -149,8 +154,61 @@ typedef enum {
   MREC_BWD_DENSE_GRAD = 0, /* grad[row] += sum g  (grad laid out like the bank, dtype of bank;
                               caller zero-fills; == aten::embedding_dense_backward) */
   MREC_BWD_SGD = 1,        /* bank[row] -= lr * sum g, round-to-nearest-even */
-  MREC_BWD_SGD_SR = 2      /* bank[row] -= lr * sum g, stochastic rounding (bf16 banks) */
+  MREC_BWD_SGD_SR = 2,     /* bank[row] -= lr * sum g, stochastic rounding (bf16 banks) */
+  /* fused optimizers (bank->optim required; fp32 math on the row, one rounding of
+   * the result into a bf16 bank).  g = the row's summed gradient this step. */
+  MREC_BWD_ADAGRAD = 3,    /* torch.optim.Adagrad (lr_decay 0, initial accumulator 0, no
+                              weight decay): s += g^2, w -= lr g / (sqrt(s) + eps);
+                              rows not looked up are unchanged, exactly as in the dense
+                              optimizer */
+  MREC_BWD_ROWWISE_ADAGRAD = 4, /* one accumulator per row for the vector (s += mean_d g_d^2)
+                              and one for the first-order weight: w_d -= lr g_d /
+                              (sqrt(s) + eps) */
+  MREC_BWD_ADAM = 5        /* dense-compatible Adam / AdamW (reference optim/AdamW.py:21-61,
+                              torch.optim.Adam): a row brought from step row_step[row] to t
+                              runs the zero-gradient steps it missed (momentum decay, L2
+                              decay, decoupled decay) in order, then step t with g; rows
+                              not looked up catch up at their next lookup or at
+                              mrec_emb_optim_flush, after which the table and state equal
+                              dense Adam's */
 } mrec_bwd_mode;
+
+#define MREC_OPT_DECOUPLED_WD 1       /* AdamW: w -= lr * wd * w after the step (reference
+                                         AdamW.py:58-59), eps added to sqrt(v) before the
+                                         bias correction of the step size (AdamW.py:50-56);
+                                         else torch.optim.Adam: L2 decay g += wd * w, eps
+                                         after sqrt(v / (1 - beta2^t)) */
+#define MREC_OPT_NO_BIAS_CORRECTION 2 /* AdamW(correct_bias=False) */
+
+typedef struct mrec_optim_s {
+  int32_t kind;        /* the optimizer's mrec_bwd_mode (ADAGRAD / ROWWISE_ADAGRAD / ADAM) */
+  float lr;            /* ADAM: lr of the zero-gradient catch-up steps run when a stale row is
+                          READ (forward gathers); the apply's own lr argument steps the rows it
+                          updates.  Exact while lr is constant: flush before changing it */
+  double beta1, beta2; /* double: the bias corrections 1 - beta^t are formed in double, as the
+                          dense optimizers do on the host */
+  float eps, weight_decay;
+  float grad_scale;   /* the optimizer sees grad_scale * g (a row-sharded owner: 1 / world) */
+  int32_t flags;      /* MREC_OPT_* */
+  float *state0;      /* ADAGRAD: sum of g^2 [total_rows, state_ld]; ROWWISE_ADAGRAD: [total_rows, 2]
+                         (vector, first-order weight); ADAM: exp_avg [total_rows, state_ld] */
+  float *state1;      /* ADAM: exp_avg_sq [total_rows, state_ld] */
+  int32_t *row_step;  /* ADAM: the step each row is current to [total_rows] (zero at start) */
+  const int64_t *d_t; /* ADAM: device step counter t, advanced by the caller before each step's
+                         apply (stream-ordered, so it stays correct under graph replay) */
+  int64_t state_ld;   /* floats per state row: mrec_emb_optim_state_ld */
+} mrec_optim;
+
+/* floats per optimizer-state row for a bank of `dim` (+ first-order weight) */
+int64_t mrec_emb_optim_state_ld(int32_t dim, int32_t has_w);
+
+/*
+ * MREC_BWD_ADAM: bring every row not updated at the current step t (*d_t) up to t
+ * by zero-gradient steps, so the table and state equal dense Adam's (call before
+ * evaluation, checkpointing or a change of lr).  Other modes: no-op.
+ */
+mrec_status mrec_emb_optim_flush(const mrec_table_bank *bank, mrec_bwd_mode mode, float lr,
+                                 mrec_stream stream);
 
 /*
  * Bytes of workspace mrec_emb_bwd needs for `batch` lookups per table.

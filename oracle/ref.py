@@ -362,3 +362,54 @@ def bce_with_logits(z, y):
     loss = np.mean(np.maximum(z, 0) - z * y + np.log1p(np.exp(-np.abs(z))))
     dz = (1.0 / (1.0 + np.exp(-z)) - y) / z.shape[0]
     return loss, dz
+
+
+# ----------------------------------------------------------------------------
+# Optimizers on a dense table: the reference steps every
+# row of every nn.Embedding each step (IModel.py:116-125 -> optimizer.step()).
+# ----------------------------------------------------------------------------
+
+
+def adamw_step(p, g, m, v, t, lr, betas=(0.9, 0.999), eps=1e-6, weight_decay=0.0,
+               correct_bias=True):
+    """One step of the reference AdamW (torchrec/optim/AdamW.py:46-59) on dense
+    arrays, in place on p, m, v (float64): m = b1 m + (1-b1) g; v = b2 v + (1-b2) g^2;
+    p -= lr sqrt(1-b2^t)/(1-b1^t) m / (sqrt(v) + eps); then p -= lr wd p."""
+    b1, b2 = betas
+    m *= b1
+    m += (1.0 - b1) * g
+    v *= b2
+    v += (1.0 - b2) * g * g
+    step = lr
+    if correct_bias:
+        step = lr * np.sqrt(1.0 - b2 ** t) / (1.0 - b1 ** t)
+    p -= step * m / (np.sqrt(v) + eps)
+    if weight_decay > 0.0:
+        p -= lr * weight_decay * p
+
+
+def adam_step(p, g, m, v, t, lr, betas=(0.9, 0.999), eps=1e-8, weight_decay=0.0):
+    """One step of ``torch.optim.Adam`` (the reference's "adam", optimizers.py:9):
+    g += wd p (L2); m, v as AdamW; p -= lr/(1-b1^t) m / (sqrt(v)/sqrt(1-b2^t) + eps)."""
+    b1, b2 = betas
+    g = g + weight_decay * p if weight_decay else g
+    m *= b1
+    m += (1.0 - b1) * g
+    v *= b2
+    v += (1.0 - b2) * g * g
+    p -= (lr / (1.0 - b1 ** t)) * m / (np.sqrt(v) / np.sqrt(1.0 - b2 ** t) + eps)
+
+
+def adagrad_step(p, g, s, lr, eps=1e-10):
+    """``torch.optim.Adagrad`` (lr_decay 0, weight_decay 0, initial accumulator 0):
+    s += g^2; p -= lr g / (sqrt(s) + eps)."""
+    s += g * g
+    p -= lr * g / (np.sqrt(s) + eps)
+
+
+def rowwise_adagrad_step(p, g, s, lr, eps=1e-10):
+    """Row-wise Adagrad (pytorchrec_amd.optim.RowWiseAdagrad; no reference
+    counterpart): s[r] += mean_d g[r, d]^2; p[r] -= lr g[r] / (sqrt(s[r]) + eps).
+    p, g [rows, D]; s [rows]."""
+    s += (g * g).mean(axis=1)
+    p -= lr * g / (np.sqrt(s)[:, None] + eps)

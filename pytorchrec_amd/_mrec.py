@@ -20,7 +20,7 @@ import torch  # noqa: F401  (must precede the dlopen, see module docstring)
 LIB_DIR = os.path.join(os.path.dirname(os.path.abspath(__file__)), "lib")
 LIB_PATH = os.environ.get("MREC_LIB_PATH") or os.path.join(LIB_DIR, "libmrec.so")
 
-ABI_VERSION = 12
+ABI_VERSION = 13
 MAX_TABLES = 64
 BWD_MAX_BATCH = 8192
 BWD_HASH_MAX_BATCH = 4096  # batches up to this use the hash plan (fusable into a GEMM launch)
@@ -34,6 +34,8 @@ INTERACT_FM2 = 1
 INTERACT_FIRST_ORDER = 2
 # bwd modes
 BWD_DENSE_GRAD, BWD_SGD, BWD_SGD_SR = 0, 1, 2
+BWD_ADAGRAD, BWD_ROWWISE_ADAGRAD, BWD_ADAM = 3, 4, 5  # fused optimizers (bank.optim)
+OPT_DECOUPLED_WD, OPT_NO_BIAS_CORRECTION = 1, 2
 
 _STATUS_NAMES = {OK: "MREC_OK", EINVAL: "MREC_EINVAL", EOOB: "MREC_EOOB", EHIP: "MREC_EHIP",
                  ERCCL: "MREC_ERCCL", ENOSPC: "MREC_ENOSPC"}
@@ -57,7 +59,20 @@ class TableBank(ctypes.Structure):
                 ("dim", ctypes.c_int32),
                 ("row_stride", ctypes.c_int32),
                 ("has_w", ctypes.c_int32),
-                ("dtype", ctypes.c_int)]
+                ("dtype", ctypes.c_int),
+                ("optim", ctypes.c_void_p)]
+
+
+class Optim(ctypes.Structure):
+    """mrec_optim: fused row-sparse optimizer state (include/mrec.h)."""
+    _fields_ = [("kind", ctypes.c_int32), ("lr", ctypes.c_float),
+                ("beta1", ctypes.c_double), ("beta2", ctypes.c_double),
+                ("eps", ctypes.c_float), ("weight_decay", ctypes.c_float),
+                ("grad_scale", ctypes.c_float),
+                ("flags", ctypes.c_int32),
+                ("state0", ctypes.c_void_p), ("state1", ctypes.c_void_p),
+                ("row_step", ctypes.c_void_p), ("d_t", ctypes.c_void_p),
+                ("state_ld", ctypes.c_int64)]
 
 
 class Ids(ctypes.Structure):
@@ -162,6 +177,9 @@ _epi_p = ctypes.POINTER(Epilogue)
 # name -> (restype, argtypes); the set the header declares (checked by tests)
 SIGNATURES = {
     "mrec_abi_version": (ctypes.c_int, []),
+    "mrec_emb_optim_state_ld": (ctypes.c_int64, [ctypes.c_int32, ctypes.c_int32]),
+    "mrec_emb_optim_flush": (ctypes.c_int, [_bank_p, ctypes.c_int, ctypes.c_float,
+                                            ctypes.c_void_p]),
     "mrec_last_error": (ctypes.c_char_p, []),
     "mrec_emb_gather_fwd": (ctypes.c_int, [_bank_p, _ids_p, _i64, _vp, ctypes.c_int, _i64, _vp,
                                            _vp, _vp]),
@@ -317,7 +335,13 @@ class BankDesc:
         self._rows = (ctypes.c_int64 * n)(*[int(x) for x in rows])
         self.weight = weight
         self.struct = TableBank(weight.data_ptr(), self._off, self._rows, n, int(dim),
-                                int(weight.shape[1]), int(bool(has_w)), dtype_code(weight.dtype))
+                                int(weight.shape[1]), int(bool(has_w)), dtype_code(weight.dtype),
+                                None)
+        self.optim = None  # Optim struct kept alive with its state tensors (set_optim)
+
+    def set_optim(self, optim: "Optim | None"):
+        self.optim = optim
+        self.struct.optim = ctypes.cast(ctypes.pointer(optim), ctypes.c_void_p) if optim else None
 
     def ref(self):
         self.struct.data = self.weight.data_ptr()

@@ -28,6 +28,18 @@ mrec_status launch_status(const char *what);  // hipGetLastError -> status
 // ---------------------------------------------------------------------------
 // kernel argument blocks (passed by value; <= 4 KiB kernarg segment)
 // ---------------------------------------------------------------------------
+// fused optimizer of the update (mrec_optim); kind = the apply's mode
+struct OptArgs {
+  int kind;  // the optimizer's mrec_bwd_mode (0: none)
+  double beta1, beta2;
+  float eps, wd, gscale, lr;
+  int flags;
+  float *s0, *s1;
+  int32_t *row_step;
+  const int64_t *d_t;
+  int64_t ld;
+};
+
 struct BankArgs {
   char *data;
   int64_t row_offset[MREC_MAX_TABLES];
@@ -37,6 +49,7 @@ struct BankArgs {
   int32_t row_stride;  // elements
   int32_t has_w;
   int32_t lpr;  // lanes per row: row bytes / 16
+  OptArgs adam;  // a fused Adam's state (kind MREC_BWD_ADAM) for reads of current rows
 };
 
 struct IdsArgs {
@@ -51,6 +64,8 @@ struct IdsArgs {
 mrec_status make_bank_args(const mrec_table_bank *bank, BankArgs *out, int *elem_bytes,
                            int *lanes_per_row);
 mrec_status make_ids_args(const mrec_ids *ids, int n_tables, IdsArgs *out);
+// the fused optimizer of a mode >= MREC_BWD_ADAGRAD from bank->optim (checked)
+mrec_status make_opt_args(const mrec_table_bank *bank, int mode, OptArgs *out);
 
 // ---------------------------------------------------------------------------
 // device helpers
@@ -121,6 +136,106 @@ struct Vec<float> {
 __device__ __forceinline__ uint32_t pack_bf16x2(float lo, float hi) {
   return static_cast<uint32_t>(f32_to_bf16_rne(lo)) |
          (static_cast<uint32_t>(f32_to_bf16_rne(hi)) << 16);
+}
+
+// Per-step scalars of Adam / AdamW at step s (b1p = beta1^s, b2p = beta2^s, in
+// double like the host-side scalars of the dense optimizers).
+struct AdamStep {
+  float b1, omb1, b2, omb2;  // beta1, 1 - beta1, beta2, 1 - beta2 (rounded from double)
+  float step;                // lr / bc1 (Adam) or lr sqrt(bc2) / bc1 (AdamW)
+  float rbc2;                // 1 / sqrt(bc2) (Adam)
+};
+__device__ __forceinline__ AdamStep adam_scalars(const OptArgs &o, float lr, double b1p,
+                                                 double b2p) {
+  AdamStep a;
+  a.b1 = static_cast<float>(o.beta1);
+  a.omb1 = static_cast<float>(1.0 - o.beta1);
+  a.b2 = static_cast<float>(o.beta2);
+  a.omb2 = static_cast<float>(1.0 - o.beta2);
+  const bool bc = !(o.flags & MREC_OPT_NO_BIAS_CORRECTION);
+  const double bc1 = bc ? 1.0 - b1p : 1.0;
+  const double bc2 = bc ? 1.0 - b2p : 1.0;
+  if (o.flags & MREC_OPT_DECOUPLED_WD) {
+    a.step = static_cast<float>(bc ? lr * sqrt(bc2) / bc1 : lr);
+    a.rbc2 = 1.f;
+  } else {
+    a.step = static_cast<float>(lr / bc1);
+    a.rbc2 = static_cast<float>(1.0 / sqrt(bc2));
+  }
+  return a;
+}
+
+// One Adam / AdamW step of one element, in the operation order of the reference
+// (optim/AdamW.py:46-59) / torch.optim.Adam.
+__device__ __forceinline__ void adam_elem(const OptArgs &o, const AdamStep &s, float lr, float g,
+                                          float &p, float &m, float &v) {
+  const bool decoupled = o.flags & MREC_OPT_DECOUPLED_WD;
+  if (!decoupled && o.wd != 0.f) g = fmaf(o.wd, p, g);
+  m = fmaf(s.b1, m, s.omb1 * g);
+  v = fmaf(s.b2, v, s.omb2 * g * g);
+  if (decoupled) {
+    p = p - s.step * (m / (sqrtf(v) + o.eps));
+    if (o.wd > 0.f) p = p - (lr * o.wd) * p;
+  } else {
+    const float denom = sqrtf(v) * s.rbc2 + o.eps;
+    p = p - s.step * (m / denom);
+  }
+}
+
+
+// A row of a bank trained by the fused (lazy, dense-compatible) Adam is stored as of
+// its last update, row_step[grow]; dense Adam would have moved it on every step
+// since (momentum).  Readers that need its value as of step `t_now` (the forward
+// gathers: t_now = completed steps; the apply's FM term: t_now = t - 1) run the
+// missed zero-gradient steps on this lane's 16 bytes in registers, without writing
+// (the update of the row does the same steps and writes).  Bank dtype in and out.
+template <typename T>
+__device__ __forceinline__ uint4 adam_current(const BankArgs &bank, int64_t grow, int e0, int n,
+                                              uint4 raw, int64_t t_now) {
+  constexpr int EPL = Vec<T>::EPL;
+  const OptArgs &o = bank.adam;
+  if (o.kind != MREC_BWD_ADAM || n == 0) return raw;
+  const int64_t t0 = o.row_step[grow];
+  if (t0 >= t_now) return raw;
+  float p[EPL], m[EPL], v[EPL];
+  Vec<T>::to_f32(raw, p);
+  const float *mp = o.s0 + grow * o.ld + e0;
+  const float *vp = o.s1 + grow * o.ld + e0;
+#pragma unroll
+  for (int j = 0; j < EPL; ++j) {
+    m[j] = j < n ? mp[j] : 0.f;
+    v[j] = j < n ? vp[j] : 0.f;
+  }
+  double b1p = pow(o.beta1, static_cast<double>(t0 + 1));
+  double b2p = pow(o.beta2, static_cast<double>(t0 + 1));
+  for (int64_t st = t0 + 1; st <= t_now; ++st) {
+    const AdamStep sc = adam_scalars(o, o.lr, b1p, b2p);
+#pragma unroll
+    for (int j = 0; j < EPL; ++j)
+      if (j < n) adam_elem(o, sc, o.lr, 0.f, p[j], m[j], v[j]);
+    b1p *= o.beta1;
+    b2p *= o.beta2;
+  }
+  const uint32_t w[4] = {raw.x, raw.y, raw.z, raw.w};
+  uint32_t r[4];
+  if constexpr (sizeof(T) == 4) {
+#pragma unroll
+    for (int j = 0; j < 4; ++j) r[j] = j < n ? __float_as_uint(p[j]) : w[j];
+  } else {
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const uint32_t lo = 2 * k < n ? f32_to_bf16_rne(p[2 * k]) : (w[k] & 0xffffu);
+      const uint32_t hi = 2 * k + 1 < n ? f32_to_bf16_rne(p[2 * k + 1]) : (w[k] >> 16);
+      r[k] = lo | (hi << 16);
+    }
+  }
+  return make_uint4(r[0], r[1], r[2], r[3]);
+}
+
+// elements of a lane's 16 bytes that are live (vector or first-order weight)
+__device__ __forceinline__ int live_elems(const BankArgs &bank, int e0, int epl) {
+  if (e0 + epl <= bank.dim) return epl;
+  return (bank.has_w && e0 == bank.dim) ? 1 : 0;
 }
 
 }  // namespace mrec

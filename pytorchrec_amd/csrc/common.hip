@@ -50,6 +50,46 @@ mrec_status make_bank_args(const mrec_table_bank *bank, BankArgs *out, int *elem
   *elem_bytes = eb;
   *lanes_per_row = static_cast<int>(row_bytes / 16);
   out->lpr = *lanes_per_row;
+  // a fused Adam bank: readers catch stale rows up (adam_current)
+  out->adam = OptArgs{};
+  if (bank->optim && bank->optim->kind == MREC_BWD_ADAM) {
+    const mrec_status st = make_opt_args(bank, MREC_BWD_ADAM, &out->adam);
+    if (st != MREC_OK) return st;
+  }
+  return MREC_OK;
+}
+
+// host: the fused optimizer of a mode >= MREC_BWD_ADAGRAD from bank->optim
+mrec_status make_opt_args(const mrec_table_bank *bank, int mode, OptArgs *out) {
+  *out = OptArgs{};
+  if (mode <= MREC_BWD_SGD_SR) return MREC_OK;
+  const mrec_optim *o = bank->optim;
+  MREC_CHECK_ARG(o != nullptr, "fused optimizer mode without bank->optim");
+  MREC_CHECK_ARG(o->state0 != nullptr, "optimizer state0 is NULL");
+  const int64_t need = mrec_emb_optim_state_ld(bank->dim, bank->has_w);
+  MREC_CHECK_ARG(mode == MREC_BWD_ROWWISE_ADAGRAD || (o->state_ld >= need && o->state_ld % 4 == 0),
+                 "optimizer state_ld < mrec_emb_optim_state_ld or not a multiple of 4");
+  MREC_CHECK_ARG((reinterpret_cast<uintptr_t>(o->state0) & 15) == 0, "optimizer state not 16B aligned");
+  if (mode == MREC_BWD_ADAM) {
+    MREC_CHECK_ARG(o->state1 && o->row_step && o->d_t, "ADAM needs state1, row_step and d_t");
+    MREC_CHECK_ARG((reinterpret_cast<uintptr_t>(o->state1) & 15) == 0, "optimizer state not 16B aligned");
+    MREC_CHECK_ARG(o->beta1 >= 0.f && o->beta1 < 1.f && o->beta2 >= 0.f && o->beta2 < 1.f,
+                   "betas must be in [0, 1)");
+  }
+  MREC_CHECK_ARG(o->eps >= 0.f, "eps < 0");
+  out->kind = mode;
+  out->lr = o->lr;
+  out->eps = o->eps;
+  out->beta1 = o->beta1;
+  out->beta2 = o->beta2;
+  out->wd = o->weight_decay;
+  out->gscale = o->grad_scale;
+  out->flags = o->flags;
+  out->s0 = o->state0;
+  out->s1 = o->state1;
+  out->row_step = o->row_step;
+  out->d_t = o->d_t;
+  out->ld = o->state_ld;
   return MREC_OK;
 }
 

@@ -28,6 +28,7 @@ struct ApplyArgs {
   int64_t g_ld;
   int64_t chunk;
   int64_t chunk_stride;
+  OptArgs opt;
 };
 
 template <int EPL>
@@ -230,6 +231,115 @@ __device__ __forceinline__ void apply_row(const BankArgs &bank, const ApplyArgs 
                                           int64_t row, int e0, bool v_lane, const float *acc) {
   const uint4 raw = *reinterpret_cast<const uint4 *>(row_ptr<T>(bank, a, f, row, e0));
   apply_row_raw<T>(bank, a, f, row, e0, v_lane, acc, raw);
+}
+
+// Fused-optimizer update of this lane's 16 bytes of global row `grow` with the
+// row's summed gradient `acc` (modes ADAGRAD / ROWWISE_ADAGRAD / ADAM).  Called by
+// ALL LPR lanes of the row's worker (row-wise Adagrad sums g^2 across them);
+// lanes without a live element (`live` false) only take part in that sum.
+template <typename T, int LPR>
+__device__ __forceinline__ void opt_row_update(const BankArgs &bank, const ApplyArgs &a,
+                                               int64_t grow, int e0, bool v_lane, bool w_lane,
+                                               bool live, const float *acc, const uint4 raw) {
+  constexpr int EPL = Vec<T>::EPL;
+  const OptArgs &o = a.opt;
+  const int n = v_lane ? EPL : (w_lane ? 1 : 0);
+  float g[EPL];
+#pragma unroll
+  for (int j = 0; j < EPL; ++j) g[j] = acc[j] * o.gscale;
+  acc = g;
+  float sq = 0.f;
+  if (a.mode == MREC_BWD_ROWWISE_ADAGRAD) {
+    if (v_lane)
+#pragma unroll
+      for (int j = 0; j < EPL; ++j) sq = fmaf(acc[j], acc[j], sq);
+#pragma unroll
+    for (int off = 1; off < LPR; off <<= 1) sq += __shfl_xor(sq, off);
+  }
+  if (!live) return;
+  float p[EPL];
+  Vec<T>::to_f32(raw, p);
+  if (a.mode == MREC_BWD_ROWWISE_ADAGRAD) {
+    float *st = o.s0 + grow * 2 + (v_lane ? 0 : 1);
+    const float G = *st + (v_lane ? sq / static_cast<float>(bank.dim) : acc[0] * acc[0]);
+    if (e0 == 0 || w_lane) *st = G;
+    const float den = sqrtf(G) + o.eps;
+#pragma unroll
+    for (int j = 0; j < EPL; ++j)
+      if (j < n) p[j] = p[j] - a.lr * (acc[j] / den);
+  } else if (a.mode == MREC_BWD_ADAGRAD) {
+    float *st = o.s0 + grow * o.ld + e0;
+#pragma unroll
+    for (int j = 0; j < EPL; ++j) {
+      if (j < n) {
+        const float sum = fmaf(acc[j], acc[j], st[j]);
+        st[j] = sum;
+        p[j] = p[j] - a.lr * (acc[j] / (sqrtf(sum) + o.eps));
+      }
+    }
+  } else {  // MREC_BWD_ADAM
+    const int64_t t = *o.d_t;
+    const int64_t t0 = o.row_step[grow];
+    float *mp = o.s0 + grow * o.ld + e0;
+    float *vp = o.s1 + grow * o.ld + e0;
+    float m[EPL], v[EPL];
+#pragma unroll
+    for (int j = 0; j < EPL; ++j) {
+      m[j] = j < n ? mp[j] : 0.f;
+      v[j] = j < n ? vp[j] : 0.f;
+    }
+    double b1p = pow(o.beta1, static_cast<double>(t0 + 1));
+    double b2p = pow(o.beta2, static_cast<double>(t0 + 1));
+    for (int64_t st = t0 + 1; st < t; ++st) {  // the zero-gradient steps this row missed
+      const AdamStep sc = adam_scalars(o, a.lr, b1p, b2p);
+#pragma unroll
+      for (int j = 0; j < EPL; ++j)
+        if (j < n) adam_elem(o, sc, a.lr, 0.f, p[j], m[j], v[j]);
+      b1p *= o.beta1;
+      b2p *= o.beta2;
+    }
+    const AdamStep sc = adam_scalars(o, a.lr, b1p, b2p);
+#pragma unroll
+    for (int j = 0; j < EPL; ++j)
+      if (j < n) adam_elem(o, sc, a.lr, acc[j], p[j], m[j], v[j]);
+#pragma unroll
+    for (int j = 0; j < EPL; ++j) {
+      if (j < n) {
+        mp[j] = m[j];
+        vp[j] = v[j];
+      }
+    }
+    if (e0 == 0) o.row_step[grow] = static_cast<int32_t>(t);
+  }
+  // pack: live elements rounded once (RNE), the rest keep their bits
+  T *dst = reinterpret_cast<T *>(bank.data) + grow * static_cast<int64_t>(bank.row_stride) + e0;
+  const uint32_t w[4] = {raw.x, raw.y, raw.z, raw.w};
+  uint32_t o4[4];
+  if constexpr (sizeof(T) == 4) {
+#pragma unroll
+    for (int j = 0; j < 4; ++j) o4[j] = j < n ? __float_as_uint(p[j]) : w[j];
+  } else {
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const uint32_t lo = 2 * k < n ? f32_to_bf16_rne(p[2 * k]) : (w[k] & 0xffffu);
+      const uint32_t hi = 2 * k + 1 < n ? f32_to_bf16_rne(p[2 * k + 1]) : (w[k] >> 16);
+      o4[k] = lo | (hi << 16);
+    }
+  }
+  *reinterpret_cast<uint4 *>(dst) = make_uint4(o4[0], o4[1], o4[2], o4[3]);
+}
+
+// The row update of every apply path: fixed modes by template (MODE >= 0), else
+// the runtime mode; all LPR lanes of the worker call it.
+template <typename T, int LPR, int MODE>
+__device__ __forceinline__ void row_update(const BankArgs &bank, const ApplyArgs &a, int64_t grow,
+                                           int e0, bool v_lane, bool w_lane, bool live,
+                                           const float *acc, const uint4 raw) {
+  if (MODE >= 0 || a.mode <= MREC_BWD_SGD_SR) {
+    if (live) apply_row_raw_g<T, MODE>(bank, a, grow, e0, v_lane, acc, raw);
+  } else {
+    opt_row_update<T, LPR>(bank, a, grow, e0, v_lane, w_lane, live, acc, raw);
+  }
 }
 
 __device__ __forceinline__ void cswap(int &a, int &b) {

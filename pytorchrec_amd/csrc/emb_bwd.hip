@@ -13,6 +13,8 @@
 //         updates the row once (SGD, or accumulates a dense grad).  Segments
 //         longer than SHORT_SEG (hot Zipf rows) are summed by the whole workgroup
 //         with a fixed-order LDS tree so one hot row cannot serialise a worker.
+#include <algorithm>
+
 #include "common.h"
 #include "emb_apply.h"
 #include "emb_plan.h"
@@ -309,12 +311,13 @@ struct HotSeg {
 #pragma unroll
       for (int j = 0; j < EPL; ++j) red[wid][e0 + j] = acc[j];
     __syncthreads();
-    if (tid < LPR && live) {
+    if (tid < LPR) {  // worker 0, all its lanes (the row update may reduce across them)
 #pragma unroll
       for (int j = 0; j < EPL; ++j) acc[j] = ((red[0][e0 + j] + red[1][e0 + j]) + red[2][e0 + j]) + red[3][e0 + j];
       const int64_t grow = bank.row_offset[f] + row;
-      const uint4 raw = *reinterpret_cast<const uint4 *>(row_ptr_g<T, MODE>(bank, a, grow, e0));
-      apply_row_raw_g<T, MODE>(bank, a, grow, e0, v_lane, acc, raw);
+      uint4 raw = make_uint4(0u, 0u, 0u, 0u);
+      if (live) raw = *reinterpret_cast<const uint4 *>(row_ptr_g<T, MODE>(bank, a, grow, e0));
+      row_update<T, LPR, MODE>(bank, a, grow, e0, v_lane, w_lane, live, acc, raw);
     }
     __syncthreads();
   }
@@ -357,10 +360,12 @@ __device__ __forceinline__ void apply_segment(const BankArgs &bank, const ApplyA
 #pragma unroll
   for (int j = 0; j < EPL; ++j) v[j] = 0.f;
   if (a.dfm && v_lane) {
-    const uint4 vr = MODE == MREC_BWD_DENSE_GRAD
-                         ? *reinterpret_cast<const uint4 *>(reinterpret_cast<const T *>(bank.data) +
-                                                            grow * static_cast<int64_t>(bank.row_stride) + e0)
-                         : raw;
+    uint4 vr = MODE == MREC_BWD_DENSE_GRAD
+                   ? *reinterpret_cast<const uint4 *>(reinterpret_cast<const T *>(bank.data) +
+                                                      grow * static_cast<int64_t>(bank.row_stride) + e0)
+                   : raw;
+    if (MODE < 0 && bank.adam.kind)  // the row as the forward read it: as of step t - 1
+      vr = adam_current<T>(bank, grow, e0, EPL, vr, *bank.adam.d_t - 1);
     Vec<T>::to_f32(vr, v);
   }
   float acc[EPL];
@@ -408,7 +413,7 @@ __device__ __forceinline__ void apply_segment(const BankArgs &bank, const ApplyA
           for (int j = 0; j < EPL; ++j) acc[j] += g[k][j];
     }
   }
-  if (live) apply_row_raw_g<T, MODE>(bank, a, grow, e0, v_lane, acc, raw);
+  row_update<T, LPR, MODE>(bank, a, grow, e0, v_lane, w_lane, live, acc, raw);
 }
 
 template <typename T, int LPR, int MODE>
@@ -416,10 +421,23 @@ __global__ __launch_bounds__(256, MREC_APPLY_WAVES) void apply_hash_kernel(BankA
                                                                            const void *ws, ApplyArgs a,
                                                                            int seg_blocks, int sm_blocks,
                                                                            CoReduce co) {
-  if (static_cast<int>(blockIdx.x) >= seg_blocks + sm_blocks) {  // uniform
+  // the co-launched reductions take the leading workgroups: independent of the
+  // embedding update, they start first instead of trailing it
+#if MREC_APPLY_EXP == 13  // (diagnostic: reductions trailing the apply blocks)
+  const int co_blocks = 0;
+  if (static_cast<int>(blockIdx.x) >= seg_blocks + sm_blocks) {
     co_reduce(co, blockIdx.x - seg_blocks - sm_blocks);
     return;
   }
+#else
+  const int co_blocks = co.start[co.n];
+  if (static_cast<int>(blockIdx.x) < co_blocks) {  // uniform
+#if MREC_APPLY_EXP != 12
+    co_reduce(co, blockIdx.x);
+#endif
+    return;
+  }
+#endif
   if (a.d_step) a.seed += *a.d_step * 0x9e3779b97f4a7c15ull;
   constexpr int EPL = Vec<T>::EPL;
   constexpr int WPB = 256 / LPR;
@@ -431,7 +449,7 @@ __global__ __launch_bounds__(256, MREC_APPLY_WAVES) void apply_hash_kernel(BankA
   const bool v_lane = e0 + EPL <= D;
   const bool w_lane = bank.has_w && e0 == D;
   const bool live = v_lane || w_lane;
-  const int blk = blockIdx.x;
+  const int blk = blockIdx.x - co_blocks;
   const int64_t *__restrict__ toff = table_offsets(ws, F, B);
 
   if (blk < seg_blocks) {  // uniform: the repeated rows of one (table, bucket)
@@ -464,9 +482,11 @@ __global__ __launch_bounds__(256, MREC_APPLY_WAVES) void apply_hash_kernel(BankA
 #pragma unroll
       for (int j = 0; j < EPL; ++j) v[j] = 0.f;
       if (a.dfm && v_lane) {
-        const uint4 vr = *reinterpret_cast<const uint4 *>(
+        uint4 vr = *reinterpret_cast<const uint4 *>(
             reinterpret_cast<const T *>(bank.data) +
             (toff_f + d.x) * static_cast<int64_t>(bank.row_stride) + e0);
+        if (MODE < 0 && bank.adam.kind)  // the row as the forward read it
+          vr = adam_current<T>(bank, toff_f + d.x, e0, EPL, vr, *bank.adam.d_t - 1);
         Vec<T>::to_f32(vr, v);
       }
       hot.template run<true, MODE>(bank, a, f, d.x, t.perm + d.z, d.y, B, v, worker, e0, v_lane,
@@ -477,30 +497,35 @@ __global__ __launch_bounds__(256, MREC_APPLY_WAVES) void apply_hash_kernel(BankA
 
   // a row hit once: one lookup, one update
   const int64_t q = static_cast<int64_t>(blk - seg_blocks) * WPB + worker;
-  if (q >= B * F || !live) return;
+  if (q >= B * F) return;  // whole workers
+  const bool rowwise = MODE < 0 && a.mode == MREC_BWD_ROWWISE_ADAGRAD;
+  if (!live && !rowwise) return;
   const int code = lookup_table(ws, F, B)[q];
-  if (code < 0) return;
+  if (code < 0) return;  // whole workers
   const int64_t b = q / F;
   const int f = static_cast<int>(q - b * F);
   const int64_t grow = toff[f] + code;
-  const uint4 raw = *reinterpret_cast<const uint4 *>(row_ptr_g<T, MODE>(bank, a, grow, e0));
+  uint4 raw = make_uint4(0u, 0u, 0u, 0u);
+  if (live) raw = *reinterpret_cast<const uint4 *>(row_ptr_g<T, MODE>(bank, a, grow, e0));
   float v[EPL];
   if (a.dfm && v_lane) {
-    const uint4 vr = MODE == MREC_BWD_DENSE_GRAD
-                         ? *reinterpret_cast<const uint4 *>(reinterpret_cast<const T *>(bank.data) +
-                                                            grow * static_cast<int64_t>(bank.row_stride) + e0)
-                         : raw;
+    uint4 vr = MODE == MREC_BWD_DENSE_GRAD
+                   ? *reinterpret_cast<const uint4 *>(reinterpret_cast<const T *>(bank.data) +
+                                                      grow * static_cast<int64_t>(bank.row_stride) + e0)
+                   : raw;
+    if (MODE < 0 && bank.adam.kind)  // the row as the forward read it: as of step t - 1
+      vr = adam_current<T>(bank, grow, e0, EPL, vr, *bank.adam.d_t - 1);
     Vec<T>::to_f32(vr, v);
   }
   float acc[EPL];
 #pragma unroll
   for (int j = 0; j < EPL; ++j) acc[j] = 0.f;
-  add_lookup_grad_v<EPL>(a, b, f, D, e0, v_lane, w_lane, v, acc);
+  if (live) add_lookup_grad_v<EPL>(a, b, f, D, e0, v_lane, w_lane, v, acc);
 #if MREC_APPLY_EXP == 9
   if (acc[0] == 12345.f) *(float *)a.grad = acc[1];
   return;
 #endif
-  apply_row_raw_g<T, MODE>(bank, a, grow, e0, v_lane, acc, raw);
+  row_update<T, LPR, MODE>(bank, a, grow, e0, v_lane, w_lane, live, acc, raw);
 }
 
 // ---------------------------------------------------------------------------
@@ -553,14 +578,16 @@ __global__ __launch_bounds__(256, 6) void apply_kernel(BankArgs bank, int64_t B,
     if (l == 0) long_list[atomicAdd(&n_long, 1)] = u;
     mine = false;
   }
-  if (mine && live) {
+  if (mine) {  // all the worker's lanes (the row update may reduce across them)
     // the row's old contents are fetched first, in parallel with the gradients
-    const uint4 raw = *reinterpret_cast<const uint4 *>(row_ptr<T>(bank, a, f, row, e0));
+    uint4 raw = make_uint4(0u, 0u, 0u, 0u);
+    if (live) raw = *reinterpret_cast<const uint4 *>(row_ptr<T>(bank, a, f, row, e0));
     float acc[EPL];
 #pragma unroll
     for (int j = 0; j < EPL; ++j) acc[j] = 0.f;
-    for (int j = 0; j < n; ++j) add_lookup_grad<EPL>(a, t.perm[s0 + j], f, D, e0, v_lane, w_lane, acc);
-    apply_row_raw<T>(bank, a, f, row, e0, v_lane, acc, raw);
+    if (live)
+      for (int j = 0; j < n; ++j) add_lookup_grad<EPL>(a, t.perm[s0 + j], f, D, e0, v_lane, w_lane, acc);
+    row_update<T, LPR, -1>(bank, a, bank.row_offset[f] + row, e0, v_lane, w_lane, live, acc, raw);
   }
   __syncthreads();
   const int nl = n_long;
@@ -574,6 +601,30 @@ __global__ __launch_bounds__(256, 6) void apply_kernel(BankArgs bank, int64_t B,
     const int sn = t.seg[uu + 1] - ls0;
     hot.template run<false>(bank, a, f, lrow, t.perm + ls0, sn, B, nullptr, worker, e0, v_lane,
                             w_lane, live);
+  }
+}
+
+// MREC_BWD_ADAM: every row behind the current step t runs its missed zero-gradient
+// steps (opt_row_update with g = 0 brings it to t); one LPR-lane worker per row
+template <typename T, int LPR>
+__global__ __launch_bounds__(256) void optim_flush_kernel(BankArgs bank, int64_t total_rows,
+                                                          ApplyArgs a) {
+  constexpr int EPL = Vec<T>::EPL;
+  constexpr int WPB = 256 / LPR;
+  const int worker = threadIdx.x / LPR, l = threadIdx.x % LPR, e0 = l * EPL;
+  const int D = bank.dim;
+  const bool v_lane = e0 + EPL <= D, w_lane = bank.has_w && e0 == D;
+  const bool live = v_lane || w_lane;
+  const int64_t t = *a.opt.d_t;
+  float acc[EPL];
+#pragma unroll
+  for (int j = 0; j < EPL; ++j) acc[j] = 0.f;
+  for (int64_t r = static_cast<int64_t>(blockIdx.x) * WPB + worker; r < total_rows;
+       r += static_cast<int64_t>(gridDim.x) * WPB) {
+    if (a.opt.row_step[r] >= t) continue;  // whole workers
+    uint4 raw = make_uint4(0u, 0u, 0u, 0u);
+    if (live) raw = *reinterpret_cast<const uint4 *>(row_ptr_g<T>(bank, a, r, e0));
+    opt_row_update<T, LPR>(bank, a, r, e0, v_lane, w_lane, live, acc, raw);
   }
 }
 
@@ -608,6 +659,50 @@ extern "C" {
 #ifdef MREC_PLAN_PROF
 void mrec_plan_prof_read(uint64_t *out16) { hipMemcpyFromSymbol(out16, HIP_SYMBOL(g_plan_prof), 128); }
 #endif
+
+int64_t mrec_emb_optim_state_ld(int32_t dim, int32_t has_w) {
+  return (static_cast<int64_t>(dim) + (has_w ? 1 : 0) + 3) / 4 * 4;
+}
+
+mrec_status mrec_emb_optim_flush(const mrec_table_bank *bank, mrec_bwd_mode mode, float lr,
+                                 mrec_stream stream) {
+  BankArgs ba;
+  int eb, lpr;
+  mrec_status st = make_bank_args(bank, &ba, &eb, &lpr);
+  if (st != MREC_OK) return st;
+  if (mode != MREC_BWD_ADAM) return MREC_OK;
+  ApplyArgs a{};
+  a.mode = mode;
+  a.lr = lr;
+  if ((st = make_opt_args(bank, mode, &a.opt)) != MREC_OK) return st;
+  int64_t total = 0;
+  for (int f = 0; f < ba.n_tables; ++f) total = std::max(total, ba.row_offset[f] + ba.rows[f]);
+  if (total == 0) return MREC_OK;
+  const int wpb = 256 / lpr;
+  const int64_t want = (total + wpb - 1) / wpb;
+  const dim3 grid(static_cast<unsigned>(std::min<int64_t>(want, 8192)));
+  hipStream_t s = static_cast<hipStream_t>(stream);
+#define MREC_FK(T, L) optim_flush_kernel<T, L><<<grid, 256, 0, s>>>(ba, total, a)
+  if (bank->dtype == MREC_BF16) {
+    switch (lpr) {
+      case 1: MREC_FK(uint16_t, 1); break;
+      case 2: MREC_FK(uint16_t, 2); break;
+      case 4: MREC_FK(uint16_t, 4); break;
+      case 8: MREC_FK(uint16_t, 8); break;
+      default: MREC_FK(uint16_t, 16); break;
+    }
+  } else {
+    switch (lpr) {
+      case 1: MREC_FK(float, 1); break;
+      case 2: MREC_FK(float, 2); break;
+      case 4: MREC_FK(float, 4); break;
+      case 8: MREC_FK(float, 8); break;
+      default: MREC_FK(float, 16); break;
+    }
+  }
+#undef MREC_FK
+  return launch_status("mrec_emb_optim_flush");
+}
 
 size_t mrec_emb_bwd_workspace_size(int32_t n_tables, int64_t batch) {
   if (n_tables <= 0 || batch < 0) return 0;
@@ -718,9 +813,10 @@ static mrec_status apply_impl(const mrec_table_bank *bank, int64_t batch, const 
     set_error("mrec_emb_bwd_apply: workspace too small");
     return MREC_ENOSPC;
   }
-  MREC_CHECK_ARG(mode == MREC_BWD_DENSE_GRAD || mode == MREC_BWD_SGD || mode == MREC_BWD_SGD_SR,
-                 "bad mode");
+  MREC_CHECK_ARG(mode >= MREC_BWD_DENSE_GRAD && mode <= MREC_BWD_ADAM, "bad mode");
   MREC_CHECK_ARG(mode != MREC_BWD_DENSE_GRAD || grad != nullptr, "DENSE_GRAD needs grad");
+  OptArgs opt{};
+  if ((st = make_opt_args(bank, mode, &opt)) != MREC_OK) return st;
   const int F = ba.n_tables, D = ba.dim;
   if (dx) {
     MREC_CHECK_ARG(dx_dtype == MREC_F32 || dx_dtype == MREC_BF16, "dx dtype must be F32/BF16");
@@ -765,6 +861,7 @@ static mrec_status apply_impl(const mrec_table_bank *bank, int64_t batch, const 
   a.g_ld = g_ld;
   a.chunk = chunk;
   a.chunk_stride = chunk_stride;
+  a.opt = opt;
   hipStream_t s = static_cast<hipStream_t>(stream);
   const int wpb = 256 / lpr;
   // hash layout (batch <= kHashMaxKeys or an exchange view, see mrec_emb_bwd_plan):
@@ -800,7 +897,8 @@ static mrec_status apply_impl(const mrec_table_bank *bank, int64_t batch, const 
     if (hash) {                                                                                  \
       if (mode == MREC_BWD_SGD) MREC_AKM(T, L, MREC_BWD_SGD);                                    \
       else if (mode == MREC_BWD_SGD_SR) MREC_AKM(T, L, MREC_BWD_SGD_SR);                         \
-      else MREC_AKM(T, L, MREC_BWD_DENSE_GRAD);                                                  \
+      else if (mode == MREC_BWD_DENSE_GRAD) MREC_AKM(T, L, MREC_BWD_DENSE_GRAD);                 \
+      else MREC_AKM(T, L, -1); /* fused optimizers */                                            \
     } else                                                                                       \
       apply_kernel<T, L><<<grid, 256, 0, s>>>(ba, batch, workspace, a, seg_blocks, apply_blocks, \
                                               co);                                               \

@@ -457,7 +457,10 @@ __global__ __launch_bounds__(256) void lg_apply_kernel(BankArgs bank, int64_t n,
   const int worker = threadIdx.x / LPR, l = threadIdx.x % LPR, e0 = l * EPL;
   const int D = bank.dim;
   const bool v_lane = e0 + EPL <= D, w_lane = bank.has_w && e0 == D;
-  if (!(v_lane || w_lane)) return;
+  const bool live = v_lane || w_lane;
+  // (lanes without a live element stay: a fused row-wise optimizer reduces
+  // across the worker's lanes)
+  if (!live && a.mode != MREC_BWD_ROWWISE_ADAGRAD) return;
   const int nu = w.hdr[0];
   for (int u = blockIdx.x * WPB + worker; u < nu; u += gridDim.x * WPB) {
     const int64_t grow = w.uniq[u];
@@ -468,7 +471,8 @@ __global__ __launch_bounds__(256) void lg_apply_kernel(BankArgs bank, int64_t n,
 #pragma unroll
     for (int q = 0; q < EPL; ++q) acc[q] = 0.f;
     const int L = w.ulong[u];
-    if (L < 0) {
+    if (!live) {
+    } else if (L < 0) {
       int r[kLgShort];
 #pragma unroll
       for (int j = 0; j < kLgShort; ++j) r[j] = j < len ? w.perm[w.ustart[u] + j] : INT_MAX;
@@ -491,7 +495,10 @@ __global__ __launch_bounds__(256) void lg_apply_kernel(BankArgs bank, int64_t n,
       }
       if (l == 0) w.segmax[L] = 0u;
     }
-    apply_row<T>(bank, a, f, row, e0, v_lane, acc);
+    uint4 raw = make_uint4(0u, 0u, 0u, 0u);
+    if (live) raw = *reinterpret_cast<const uint4 *>(row_ptr_g<T>(bank, a, grow, e0));
+    row_update<T, LPR, -1>(bank, a, grow, e0, v_lane, w_lane, live, acc, raw);
+    (void)row;
   }
 }
 
@@ -575,8 +582,12 @@ mrec_status mrec_emb_bwd_large_apply(const mrec_table_bank *bank, int64_t batch,
   mrec_status st = lg_setup(bank, batch, const_cast<void *>(workspace), ws_bytes, &ba, &lpr, &R,
                             &w);
   if (st != MREC_OK) return st;
-  MREC_CHECK_ARG(mode == MREC_BWD_DENSE_GRAD || mode == MREC_BWD_SGD || mode == MREC_BWD_SGD_SR,
-                 "bad mode");
+  MREC_CHECK_ARG(mode >= MREC_BWD_DENSE_GRAD && mode <= MREC_BWD_ADAM, "bad mode");
+  OptArgs opt{};
+  {
+    const mrec_status so = make_opt_args(bank, mode, &opt);
+    if (so != MREC_OK) return so;
+  }
   MREC_CHECK_ARG(mode != MREC_BWD_DENSE_GRAD || grad != nullptr, "DENSE_GRAD needs grad");
   const int F = ba.n_tables, D = ba.dim;
   if (dx) {
@@ -610,6 +621,7 @@ mrec_status mrec_emb_bwd_large_apply(const mrec_table_bank *bank, int64_t batch,
   a.lr = lr;
   a.seed = seed;
   a.d_step = d_step;
+  a.opt = opt;
   a.grad = grad;
   if (batch == 0) return MREC_OK;
   hipStream_t s = static_cast<hipStream_t>(stream);

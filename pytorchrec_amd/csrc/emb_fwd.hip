@@ -32,6 +32,9 @@ __global__ __launch_bounds__(256) void gather_kernel(BankArgs bank, IdsArgs ids,
     const T *row = reinterpret_cast<const T *>(bank.data) +
                    (bank.row_offset[f] + id) * static_cast<int64_t>(bank.row_stride);
     raw = *reinterpret_cast<const uint4 *>(row + l * EPL);
+    if (bank.adam.kind)  // a lazily updated Adam bank: the row as of the last step
+      raw = adam_current<T>(bank, bank.row_offset[f] + id, l * EPL, live_elems(bank, l * EPL, EPL),
+                            raw, *bank.adam.d_t);
   } else if (l == 0 && oob) {
     *oob = 1;
   }
@@ -116,6 +119,9 @@ __device__ __forceinline__ void interact_sample(const BankArgs &bank, const IdsA
         const T *row = reinterpret_cast<const T *>(bank.data) +
                        (bank.row_offset[f] + id) * static_cast<int64_t>(bank.row_stride);
         raw[it] = *reinterpret_cast<const uint4 *>(row + e0);
+        if (bank.adam.kind)  // a lazily updated Adam bank: the row as of the last step
+          raw[it] = adam_current<T>(bank, bank.row_offset[f] + id, e0, live_elems(bank, e0, EPL),
+                                    raw[it], *bank.adam.d_t);
       } else if (l == 0 && oob) {
         *oob = 1;
       }

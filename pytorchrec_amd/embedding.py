@@ -23,7 +23,14 @@ Update modes (``EmbeddingBank.update``):
   "sgd"       the backward applies row-sparse SGD in place (identical to dense
               SGD without momentum / weight decay), the gradient never exists;
               ``IModel.compile`` switches to it when the compiled optimizer is
-              plain SGD (SURVEY.md §7 hard part 5).
+              plain SGD (SURVEY.md §7 hard part 5);
+  "adagrad" / "rowwise_adagrad" / "adam"
+              the same with a fused optimizer whose state lives beside the bank
+              (include/mrec.h MREC_BWD_ADAGRAD / _ROWWISE_ADAGRAD / _ADAM):
+              torch.optim.Adagrad, row-wise Adagrad (``optim.RowWiseAdagrad``),
+              and dense-compatible Adam / the reference AdamW (rows catch up on the
+              zero-gradient steps they missed; ``flush_optimizer`` brings every row
+              to the current step).
 """
 from __future__ import annotations
 
@@ -62,7 +69,7 @@ class EmbeddingBank(torch.nn.Module):
         if len(category_nums) < 1:
             raise ValueError("need at least one table")
         if update not in ("dense", "sgd"):
-            raise ValueError(f"update must be 'dense' or 'sgd', got {update!r}")
+            raise ValueError(f"update must be 'dense' or 'sgd', got {update!r}")  # (others: use_fused_optimizer)
         es = torch.tensor([], dtype=dtype).element_size()
         if dim <= 0 or (dim * es) % 16:
             raise ValueError(f"dim*{es}B must be a positive multiple of 16 bytes (dim={dim})")
@@ -86,6 +93,8 @@ class EmbeddingBank(torch.nn.Module):
         self.check_ids = True  # raise IndexError on out-of-range ids (syncs once per call)
         self._seed = 0x5eed
         self._desc = None
+        self._optim = None  # _mrec.Optim of a fused optimizer (use_fused_optimizer)
+        self.optim_state = None
         self._step = None  # device uint64 counter (SR bits stay fresh under graph replay)
 
     @property
@@ -98,10 +107,86 @@ class EmbeddingBank(torch.nn.Module):
         self.sgd_lr = float(lr)
         self.sgd_group = group
         self.weight.requires_grad_(False)
+        self._set_optim(None)
 
     def use_dense_grad(self):
         self.update = "dense"
         self.weight.requires_grad_(True)
+        self._set_optim(None)
+
+    FUSED_OPTIMIZERS = ("adagrad", "rowwise_adagrad", "adam")
+
+    def use_fused_optimizer(self, kind: str, group, *, eps: float, betas=(0.9, 0.999),
+                            weight_decay: float = 0.0, decoupled: bool = False,
+                            bias_correction: bool = True, grad_scale: float = 1.0):
+        """Row-sparse fused optimizer: the state tensors are allocated here (zeros,
+        as the dense optimizers start), ``group`` supplies the lr each step."""
+        if kind not in self.FUSED_OPTIMIZERS:
+            raise ValueError(f"fused optimizer must be one of {self.FUSED_OPTIMIZERS}")
+        dev = self.weight.device
+        f32 = dict(dtype=torch.float32, device=dev)
+        ld = int(_mrec.lib().mrec_emb_optim_state_ld(self.dim, int(self.has_w)))
+        st = {}
+        if kind == "adagrad":
+            st["s0"] = torch.zeros(self.total_rows, ld, **f32)
+        elif kind == "rowwise_adagrad":
+            st["s0"] = torch.zeros(self.total_rows, 2, **f32)
+        else:
+            st["s0"] = torch.zeros(self.total_rows, ld, **f32)
+            st["s1"] = torch.zeros(self.total_rows, ld, **f32)
+            st["row_step"] = torch.zeros(self.total_rows, dtype=torch.int32, device=dev)
+            st["t"] = torch.zeros(1, dtype=torch.int64, device=dev)
+        flags = ((_mrec.OPT_DECOUPLED_WD if decoupled else 0)
+                 | (0 if bias_correction else _mrec.OPT_NO_BIAS_CORRECTION))
+        self.optim_state = st
+        kind_code = {"adagrad": _mrec.BWD_ADAGRAD, "rowwise_adagrad": _mrec.BWD_ROWWISE_ADAGRAD,
+                     "adam": _mrec.BWD_ADAM}[kind]
+        self._optim = _mrec.Optim(kind_code, float(group["lr"]), float(betas[0]), float(betas[1]),
+                                  float(eps),
+                                  float(weight_decay), float(grad_scale), flags,
+                                  st["s0"].data_ptr(), _mrec.ptr(st.get("s1")),
+                                  _mrec.ptr(st.get("row_step")), _mrec.ptr(st.get("t")), ld)
+        self.update = kind
+        self.sgd_lr = None
+        self.sgd_group = group
+        self.weight.requires_grad_(False)
+        self._set_optim(self._optim)
+
+    def _set_optim(self, optim):
+        self._optim = optim
+        if optim is None:
+            self.optim_state = None
+        if self._desc is not None:
+            self._desc.set_optim(optim)
+
+    @property
+    def fused(self) -> bool:
+        """The update happens inside the backward (no table gradient exists)."""
+        return self.update != "dense"
+
+    def apply_mode(self):
+        """(mrec_bwd_mode, lr) of this step's fused update; for Adam the device step
+        counter advances first (stream-ordered: right under graph replay too)."""
+        if self.update == "sgd":
+            mode = (_mrec.BWD_SGD_SR if (self.stochastic_rounding and
+                                         self.weight.dtype == torch.bfloat16) else _mrec.BWD_SGD)
+            return mode, self.current_lr()
+        if self.update == "dense":
+            return _mrec.BWD_DENSE_GRAD, 0.0
+        if self.update == "adam":
+            self.optim_state["t"].add_(1)
+            self._optim.lr = float(self.current_lr())  # catch-up lr of stale-row reads
+        mode = {"adagrad": _mrec.BWD_ADAGRAD, "rowwise_adagrad": _mrec.BWD_ROWWISE_ADAGRAD,
+                "adam": _mrec.BWD_ADAM}[self.update]
+        return mode, self.current_lr()
+
+    def flush_optimizer(self):
+        """Dense-compatible Adam: bring the rows not looked up at the current step
+        up to it (their missed zero-gradient steps), so the table equals dense
+        Adam's.  Other update modes: nothing to do."""
+        if self.update == "adam" and self.weight.is_cuda:
+            _mrec.call("mrec_emb_optim_flush", self.desc().ref(), _mrec.BWD_ADAM,
+                       float(self.current_lr()), _mrec.stream_handle())
 
     def current_lr(self) -> float:
         if self.sgd_group is not None:
@@ -134,6 +219,7 @@ class EmbeddingBank(torch.nn.Module):
         if self._desc is None or self._desc.weight is not self.weight:
             self._desc = _mrec.BankDesc(self.weight, self.row_offset, self.category_nums,
                                         self.dim, self.has_w)
+            self._desc.set_optim(self._optim)
         return self._desc
 
     def extra_repr(self) -> str:
@@ -222,12 +308,7 @@ def _apply(bank: EmbeddingBank, ws, ws_bytes, count, dx=None, dfm=None, fm_sum=N
            dw=None, grad=None):
     """Run the fused backward for lookups [0, count) described by ``ws``; the
     per-sample tensors must already be sliced to the same chunk."""
-    if bank.update == "sgd":
-        mode = _mrec.BWD_SGD_SR if (bank.stochastic_rounding and
-                                    bank.weight.dtype == torch.bfloat16) else _mrec.BWD_SGD
-        lr = bank.current_lr()
-    else:
-        mode, lr = _mrec.BWD_DENSE_GRAD, 0.0
+    mode, lr = bank.apply_mode()
     dx_dt = _mrec.dtype_code(dx.dtype) if dx is not None else _mrec.F32
     x0_dt = _mrec.dtype_code(x0.dtype) if x0 is not None else _mrec.F32
     # deferred MLP weight-gradient reductions (+ fused SGD) ride along this launch
@@ -271,12 +352,7 @@ def _backward_large(bank: EmbeddingBank, ids, batch, grad, dx=None, dfm=None, fm
     ws = _large_ws(bank, batch)
     _mrec.call("mrec_emb_bwd_large_plan", bank.desc().ref(), _ids_desc(ids).ref(), batch,
                ws.data_ptr(), ws.numel(), None, _mrec.stream_handle())
-    if bank.update == "sgd":
-        mode = _mrec.BWD_SGD_SR if (bank.stochastic_rounding and
-                                    bank.weight.dtype == torch.bfloat16) else _mrec.BWD_SGD
-        lr = bank.current_lr()
-    else:
-        mode, lr = _mrec.BWD_DENSE_GRAD, 0.0
+    mode, lr = bank.apply_mode()
     _mrec.call("mrec_emb_bwd_large_apply", bank.desc().ref(), batch, ws.data_ptr(), ws.numel(),
                _mrec.ptr(dx), _mrec.dtype_code(dx.dtype) if dx is not None else _mrec.F32,
                dx.stride(0) if dx is not None else 0, _mrec.ptr(dfm), _mrec.ptr(fm_sum),
@@ -299,6 +375,10 @@ def _backward_into_bank(bank: EmbeddingBank, ids, batch, plan_ws, dx=None, dfm=N
     if batch > _mrec.BWD_MAX_BATCH and bank.total_rows <= LARGE_MAX_ROWS and LARGE_BATCH:
         _backward_large(bank, ids, batch, grad, dx, dfm, fm_sum, x0, dw)
         return grad
+    if bank.update == "adam" and batch > _mrec.BWD_MAX_BATCH:
+        raise NotImplementedError("fused Adam takes one apply per step: batches above "
+                                  f"{_mrec.BWD_MAX_BATCH} lookups per table need the large-batch "
+                                  "path (MREC_LARGE_BATCH=1, banks up to 2^24 rows)")
     for s, c in _chunks(batch):
         if c == 0:
             continue
@@ -309,7 +389,7 @@ def _backward_into_bank(bank: EmbeddingBank, ids, batch, plan_ws, dx=None, dfm=N
 
 
 def _needs_backward(bank: EmbeddingBank) -> bool:
-    return torch.is_grad_enabled() and (bank.update == "sgd" or bank.weight.requires_grad)
+    return torch.is_grad_enabled() and (bank.fused or bank.weight.requires_grad)
 
 
 # ----------------------------------------------------------------------------
@@ -378,7 +458,7 @@ _TRIGGERS = {}
 def _trigger(bank: EmbeddingBank):
     """A 0-element leaf that requires grad, so autograd calls our backward even when
     the bank itself is updated in place (fused SGD, weight.requires_grad False)."""
-    if bank.update != "sgd" or not torch.is_grad_enabled():
+    if not bank.fused or not torch.is_grad_enabled():
         return None
     t = _TRIGGERS.get(bank.weight.device)
     if t is None:
@@ -459,7 +539,7 @@ class _InteractFn(torch.autograd.Function):
         if dx0 is not None:
             dx0 = dx0.contiguous()
         grad = None
-        if bank.update == "sgd" or bank.weight.requires_grad:
+        if bank.fused or bank.weight.requires_grad:
             grad = _backward_into_bank(bank, ctx.ids, ctx.B, ctx.plan_ws, dx=dx0, dfm=dfm,
                                        fm_sum=fm_sum, x0=x0 if dfm is not None else None, dw=dw)
         g_dense_w, g_bias = _dense_first_order_grads(ctx, dlogit, dense)

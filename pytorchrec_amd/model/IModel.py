@@ -156,23 +156,51 @@ class IModel(Module, IWithArguments, ABC):
         self._configure_dense_update(optimizer)
         self._is_compiled = True
 
+    def flush_embedding_optimizers(self):
+        """Dense-compatible fused Adam: bring every table row to the current step
+        (EmbeddingBank.flush_optimizer) before the tables are read as a whole --
+        evaluation, prediction, checkpoints."""
+        for bank in self.embedding_banks():
+            bank.flush_optimizer()
+
+    def state_dict(self, *args, **kwargs):
+        self.flush_embedding_optimizers()
+        return super().state_dict(*args, **kwargs)
+
     def embedding_banks(self):
         from pytorchrec_amd.embedding import EmbeddingBank
         return [m for m in self.modules() if isinstance(m, EmbeddingBank)]
 
     def _configure_embedding_update(self, optimizer: Optimizer):
-        """Fuse the table update into the backward when that is exactly dense SGD."""
+        """Fuse the table update into the backward when it is exactly the compiled
+        optimizer's: plain SGD, Adagrad, row-wise Adagrad, Adam / the reference
+        AdamW (pytorchrec_amd.optim.fused_spec; Adam dense-compatible through
+        catch-up steps and ``flush_optimizer``)."""
+        from pytorchrec_amd.optim import fused_spec
         from pytorchrec_amd.sharding import ShardedEmbeddingBank
+
+        def plain_sgd(g, sharded=False):
+            return (isinstance(optimizer, torch.optim.SGD) and g.get("momentum", 0) == 0
+                    and not g.get("nesterov", False) and not g.get("maximize", False)
+                    and g.get("weight_decay", 0) == 0
+                    and (not sharded or g.get("dampening", 0) == 0))
+
         for bank in self.embedding_banks():
             if isinstance(bank, ShardedEmbeddingBank):
                 g0 = optimizer.param_groups[0]
-                if not (isinstance(optimizer, torch.optim.SGD) and g0.get("momentum", 0) == 0
-                        and not g0.get("nesterov", False) and not g0.get("maximize", False)
-                        and g0.get("weight_decay", 0) == 0 and g0.get("dampening", 0) == 0):
-                    raise NotImplementedError("row-sharded tables train with the fused SGD "
-                                              "update only (torch.optim.SGD: no momentum, "
-                                              "weight_decay, dampening or nesterov)")
-                bank.use_fused_sgd(g0["lr"], g0)
+                sgd = plain_sgd(g0, sharded=True)
+                spec = None if sgd else fused_spec(optimizer, g0)
+                if not sgd and spec is None:
+                    raise NotImplementedError(
+                        "row-sharded tables train with a fused update: torch.optim.SGD (no "
+                        "momentum, weight_decay, dampening or nesterov), Adagrad (no lr_decay / "
+                        "weight_decay), optim.RowWiseAdagrad, torch.optim.Adam (no amsgrad) "
+                        "or optim.AdamW")
+                if spec is None:
+                    bank.use_fused_sgd(g0["lr"], g0)
+                else:
+                    kind = spec.pop("kind")
+                    bank.use_fused_optimizer(kind, g0, grad_scale=1.0 / bank.world, **spec)
                 continue
             if self._dp_active():
                 # a replicated (unsharded) bank under data parallelism: its dense
@@ -185,11 +213,13 @@ class IModel(Module, IWithArguments, ABC):
             for g in optimizer.param_groups:
                 if any(p is bank.weight for p in g["params"]):
                     group = g
-            plain_sgd = (isinstance(optimizer, torch.optim.SGD) and group is not None
-                         and group.get("momentum", 0) == 0 and group.get("weight_decay", 0) == 0
-                         and not group.get("nesterov", False) and not group.get("maximize", False))
-            if plain_sgd:
+            spec = (fused_spec(optimizer, group) if group is not None and bank.weight.is_cuda
+                    else None)
+            if group is not None and plain_sgd(group):
                 bank.use_fused_sgd(group["lr"], group)
+            elif spec is not None:
+                kind = spec.pop("kind")
+                bank.use_fused_optimizer(kind, group, **spec)
             elif group is not None or bank.update != "sgd":
                 bank.use_dense_grad()
 
@@ -404,6 +434,7 @@ class IModel(Module, IWithArguments, ABC):
     @torch.no_grad()
     def evaluate(self, dataset, batch_size: int, verbose: int = 1, callbacks=None, workers: int = 0):
         self._assert_compile_was_called()
+        self.flush_embedding_optimizers()
         preds, targets = [], []
         for data in self._loader(dataset, batch_size, workers=workers):
             p, t = self.test_step(data)
@@ -416,6 +447,7 @@ class IModel(Module, IWithArguments, ABC):
 
     @torch.no_grad()
     def predict(self, dataset, batch_size: int, verbose: int = 0, callbacks=None, workers: int = 0):
+        self.flush_embedding_optimizers()
         preds = [self.predict_step(d).detach().float().cpu().numpy()
                  for d in self._loader(dataset, batch_size, workers=workers)]
         return np.concatenate(preds) if preds else np.zeros(0)

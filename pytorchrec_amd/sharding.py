@@ -353,12 +353,22 @@ def shard_lookup_grad(bank: ShardedEmbeddingBank, pos: torch.Tensor, batch: int,
     return g
 
 
-def owner_apply(bank: ShardedEmbeddingBank, plan, g_recv: torch.Tensor, lr: float):
-    """Owner: fixed-order segment sums of the received gradient rows + SGD(lr)."""
+def owner_apply(bank: ShardedEmbeddingBank, plan, g_recv: torch.Tensor,
+                lr: Optional[float] = None):
+    """Owner: fixed-order segment sums of the received gradient rows + the fused
+    update.  The rows arrive summed over the W ranks' batches; each rank's loss is
+    its own batch mean, so SGD steps with lr / W and a fused optimizer sees the
+    sum scaled by 1 / W (its grad_scale): the data-parallel mean gradient.  An
+    explicit ``lr`` runs plain SGD with exactly that step (kernel tests)."""
     ws, wsb = plan
     F, W, cap = bank.n_tables, bank.world, bank.cap
-    mode = _mrec.BWD_SGD_SR if (bank.stochastic_rounding and
-                                bank.weight.dtype == torch.bfloat16) else _mrec.BWD_SGD
+    if lr is not None:
+        mode = (_mrec.BWD_SGD_SR if (bank.stochastic_rounding and
+                                     bank.weight.dtype == torch.bfloat16) else _mrec.BWD_SGD)
+    else:
+        mode, lr = bank.apply_mode()
+        if mode in (_mrec.BWD_SGD, _mrec.BWD_SGD_SR):
+            lr = lr / W
     # deferred MLP weight-gradient reductions ride along this launch
     from pytorchrec_amd import dense as dense_ops
     jobs = dense_ops.take_pending(4)
@@ -419,7 +429,7 @@ class _ShardedInteractFn(torch.autograd.Function):
             g_send = shard_lookup_grad(bank, pos, ctx.B, dx=dx0, dfm=dfm, fm_sum=fm_sum,
                                        x0=x0 if dfm is not None else None, dw=dw)
             g_recv = bank.comm.exchange(g_send)
-            owner_apply(bank, ctx.plan, g_recv, bank.current_lr() / bank.world)
+            owner_apply(bank, ctx.plan, g_recv)
         g_dense_w, g_bias = _dense_first_order_grads(ctx, dlogit, dense)
         return g_dense_w, g_bias, None, None, None, None, None, None, None, None
 

@@ -1,4 +1,4 @@
-"""Generate the golden vectors G1-G8 (+G10, G11) by running the reference itself.
+"""Generate the golden vectors G1-G8 (+G10-G12) by running the reference itself.
 
 Run IN THE BUILD CONTAINER ONLY (the reference never travels to the GPU box):
 
@@ -227,5 +227,51 @@ def main():
           iid=b11["iid"].numpy(), prediction=pred11.numpy(), target=tgt11.numpy())
 
 
+def g12():
+    """G12: the reference optimizers' dense steps over an embedding-shaped table
+    whose rows get no gradient on some steps (rows still move under Adam's
+    momentum): torchrec.optim.AdamW (AdamW.py:21-61; with and without
+    correct_bias, weight decay) and get_optimizer("adam") (optimizers.py:9,
+    torch.optim.Adam, L2 weight decay).  Pins oracle/ref.py adamw_step / adam_step
+    and the fused row-sparse Adam (tests/test_gpu_optim.py)."""
+    if "torchrec" not in sys.modules:
+        try:
+            import torchrec  # noqa: F401
+        except ImportError:
+            raise SystemExit("run with PYTHONPATH=/root/reference")
+    from torchrec.optim.AdamW import AdamW
+    from torchrec.optim.optimizers import get_optimizer
+    torch.set_num_threads(1)
+    g = torch.Generator().manual_seed(1212)
+    rows, D, steps = 12, 5, 4
+    w0 = torch.randn(rows, D, generator=g) * 0.1
+    grads = torch.randn(steps, rows, D, generator=g) * 0.5
+    mask = torch.rand(steps, rows, generator=g) < 0.5  # rows looked up at each step
+    grads = grads * mask[..., None]
+    out = {"w0": w0.numpy(), "grads": grads.numpy(), "mask": mask.numpy()}
+    configs = {"adamw": lambda p: AdamW([p], lr=0.05, betas=(0.9, 0.999), eps=1e-6,
+                                        weight_decay=0.1, correct_bias=True),
+               "adamw_nobc": lambda p: AdamW([p], lr=0.05, eps=1e-6, correct_bias=False),
+               "adam": lambda p: get_optimizer("adam")([p], lr=0.05, betas=(0.8, 0.99),
+                                                       eps=1e-8, weight_decay=0.05)}
+    import warnings
+    for name, make in configs.items():
+        p = torch.nn.Parameter(w0.clone())
+        opt = make(p)
+        traj = []
+        for s in range(steps):
+            p.grad = grads[s].clone()
+            with warnings.catch_warnings():
+                warnings.simplefilter("ignore")  # the reference's deprecated add_(alpha, t)
+                opt.step()
+            traj.append(p.detach().clone().numpy())
+        out[name] = np.stack(traj)
+    _save("g12_optimizers.npz", **out)
+
+
 if __name__ == "__main__":
-    main()
+    if sys.argv[1:] == ["g12"]:
+        g12()
+    else:
+        main()
+        g12()

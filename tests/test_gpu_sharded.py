@@ -169,6 +169,40 @@ def test_world1_sharded_deepfm_step_equals_unsharded(gpu):
         assert torch.equal(va, vb), k
 
 
+@pytest.mark.parametrize("opt", ["adagrad", "rowwise_adagrad", "adam", "adamw"])
+def test_world1_sharded_fused_optimizers_equal_unsharded(gpu, opt):
+    """Row-sharded tables train with the fused optimizers too (owner apply with the
+    gradient scale 1/W): at W = 1 the sharded model equals the unsharded one over
+    batches that leave rows out for a step (the lazy Adam's catch-up on reads and
+    updates on both paths)."""
+    from pytorchrec_amd.loss import BCEWithLogitsLoss
+    from pytorchrec_amd.optim import AdamW, RowWiseAdagrad
+    a, b = _deepfm(gpu, False), _deepfm(gpu, True)
+    b.load_state_dict(a.state_dict())
+    batches = []
+    for s in range(3):
+        data = {f"c_c_C{i}": t for i, t in enumerate(_ids(gpu, 256, 20 + s))}
+        g = torch.Generator().manual_seed(30 + s)
+        for i in range(13):
+            data[f"c_n_I{i}"] = torch.rand(256, generator=g).to(gpu)
+        data["label"] = (torch.rand(256, generator=g) < 0.25).to(torch.int32).to(gpu)
+        batches.append(data)
+    make = {"adagrad": lambda p: torch.optim.Adagrad(p, lr=0.05),
+            "rowwise_adagrad": lambda p: RowWiseAdagrad(p, lr=0.05),
+            "adam": lambda p: torch.optim.Adam(p, lr=0.01, weight_decay=0.01),
+            "adamw": lambda p: AdamW(p, lr=0.01, weight_decay=0.01)}[opt]
+    for m in (a, b):
+        m.compile(make(m.get_parameters()), BCEWithLogitsLoss(), [], gpu)
+    kind = "adam" if opt == "adamw" else opt
+    assert a.embeddings.update == kind and b.embeddings.update == kind
+    la = [float(a.train_step(d)["loss"].detach()) for d in batches]
+    lb = [float(b.train_step(d)["loss"].detach()) for d in batches]
+    np.testing.assert_allclose(la, lb, rtol=1e-6)
+    sa, sb = a.state_dict(), b.state_dict()
+    for k in sa:
+        torch.testing.assert_close(sa[k].float(), sb[k].float(), rtol=1e-5, atol=1e-6)
+
+
 @pytest.fixture
 def rccl_world1(gpu):
     """A real one-rank RCCL process group (collectives forced at world 1)."""

@@ -439,6 +439,11 @@ def cpu_baseline(args):
 
 def main():
     args = parse()
+    # stdout carries exactly one JSON line: anything a native library prints there
+    # (RCCL's version banner at communicator init) goes to stderr instead
+    sys.stdout.flush()
+    json_out = os.fdopen(os.dup(1), "w")
+    os.dup2(2, 1)
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
@@ -622,27 +627,34 @@ def main():
     if rank == 0 and world == 1 and not args.no_cpu_baseline and args.model == "deepfm":
         result["cpu_baseline"] = cpu_baseline(args)
     if rank == 0:
-        print(json.dumps(result), flush=True)
-    # teardown: captured graphs hold RCCL kernels of the communicator, so they are
-    # released (and the device drained) before the process group goes away
-    captured = graphs is not None
+        print(json.dumps(result), file=json_out, flush=True)
+    # teardown: a HIP graph that captured RCCL work keeps a reference on the
+    # communicator, and ncclCommDestroy waits for every such graph to be destroyed
+    # (measured, tools/destroy_probe.py: destroy_process_group hangs while the graph
+    # lives, returns in 0.4 s once it is released).  So every captured graph is
+    # reset -- also any the gc still finds -- before the process group goes away.
     del run, run_steps
     graphs = multi = g = None
+    n = release_graphs()
+    if n:
+        print(f"bench: reset {n} HIP graph(s) still reachable at teardown", file=sys.stderr,
+              flush=True)
+    if torch.distributed.is_initialized():
+        torch.distributed.destroy_process_group()
+
+
+def release_graphs() -> int:
+    """Reset every torch CUDAGraph the garbage collector can still reach (their
+    captured RCCL plans hold the communicator), then drain the device."""
     import gc
     gc.collect()
+    live = [o for o in gc.get_objects() if isinstance(o, torch.cuda.CUDAGraph)]
+    for gr in live:
+        gr.reset()
+    n = len(live)
+    del live
     torch.cuda.synchronize()
-    if torch.distributed.is_initialized() and not captured:
-        torch.distributed.destroy_process_group()
-    elif torch.distributed.is_initialized():
-        # destroy_process_group() hangs on this image once RCCL kernels were
-        # captured in a HIP graph (measured at world 1: > 120 s); every rank has
-        # finished its device work and rank 0 has printed, so leave without it
-        torch.distributed.barrier()
-        torch.cuda.synchronize()
-        sys.stdout.flush()
-        sys.stderr.flush()
-        os._exit(0)
-
+    return n
 
 if __name__ == "__main__":
     main()

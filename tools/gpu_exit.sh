@@ -1,9 +1,13 @@
-# does the sharded + RCCL bench exit cleanly, directly and under torch.distributed.run?
+# bench.py with every collective issued at world 1 (RCCL captured in HIP graphs)
+# must exit through destroy_process_group: timed, under its own limit
 set -o pipefail
-R=$GRAFT_REPO_ROOT
-cd $R
-mkdir -p gpurun_out/dp
-timeout -k 10 120 python -u bench.py --steps 20 --warmup 4 --no-cpu-baseline --no-roofline --shard --force-collectives > gpurun_out/dp/bench.json 2> gpurun_out/dp/bench.err; echo "rc=$?"
-grep metric gpurun_out/dp/bench.json | cut -c1-200
-timeout -k 10 120 python -u -m torch.distributed.run --nnodes=1 --nproc-per-node 1 --master-addr 127.0.0.1 --master-port 29577 bench.py --steps 20 --warmup 4 --no-cpu-baseline --no-roofline --force-collectives > gpurun_out/dp/bench_tr.json 2> gpurun_out/dp/bench_tr.err; echo "rc=$?"
-grep metric gpurun_out/dp/bench_tr.json | cut -c1-200
+cd $GRAFT_REPO_ROOT
+mkdir -p gpurun_out/exit
+t0=$(date +%s.%N)
+timeout -k 10 180 python -u bench.py --force-collectives --steps 20 --warmup 5 --no-cpu-baseline --no-h2d > gpurun_out/exit/bench_force.json 2> gpurun_out/exit/bench_force.err
+rc=$?
+t1=$(date +%s.%N)
+echo "force-collectives bench rc=$rc wall=$(python -c "print(round($t1-$t0,1))")s"
+grep -v amdgpu.ids gpurun_out/exit/bench_force.err | tail -5
+cut -c1-300 gpurun_out/exit/bench_force.json
+exit $rc

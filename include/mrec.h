@@ -32,7 +32,7 @@
 extern "C" {
 #endif
 
-#define MREC_ABI_VERSION 13
+#define MREC_ABI_VERSION 14
 #define MREC_MAX_TABLES 64      /* tables per table bank / per call */
 #define MREC_BWD_MAX_BATCH 8192  /* lookups per table per plan/apply call */
 #define MREC_BWD_HASH_MAX_BATCH 4096  /* batches up to this use the hash plan */
@@ -333,6 +333,44 @@ mrec_status mrec_emb_bwd_apply_given(const mrec_table_bank *bank, int64_t batch,
                                      mrec_bwd_mode mode, float lr, uint64_t seed,
                                      const uint64_t *d_step, void *grad, int32_t n_reduce,
                                      const struct mrec_gemm_call_s *reduce, mrec_stream stream);
+
+/* ------------------------------------------------------------------------- */
+/* Communicator (RCCL over xGMI) for the row-sharded exchange                  */
+/* ------------------------------------------------------------------------- */
+/*
+ * SURVEY.md §8(b) B2 comm entry points: with these and the mrec_shard_* kernels a
+ * binding that is not torch (cgo, JNI, a C++ trainer) runs the sharded step.  The
+ * reference has no communication at all (torchrec/task/Task.py:187-190 trains on
+ * one device).  RCCL is opened at run time (MREC_RCCL_LIB, else the librccl
+ * already in the process, else librccl.so): MREC_ERCCL when absent.
+ *
+ * Rank 0 calls mrec_comm_unique_id and hands the 128 bytes to every rank by any
+ * host channel; each rank (one process per GPU, its HIP device current) calls
+ * mrec_comm_init.  Exchanges are equal-split all-to-alls: part p of `send` (W
+ * parts of the given size) goes to rank p, part p of `recv` comes from rank p --
+ * the layout of mrec_shard_bucketize / mrec_shard_gather / mrec_shard_lookup_grad
+ * buffers.  Stream-ordered on the caller's stream, capturable in a HIP graph; a
+ * graph that captured them must be destroyed before mrec_comm_destroy (RCCL waits
+ * for it).
+ */
+#define MREC_COMM_ID_BYTES 128
+typedef struct mrec_comm_s mrec_comm;
+mrec_status mrec_comm_unique_id(void *id_out /* MREC_COMM_ID_BYTES */);
+mrec_status mrec_comm_init(const void *unique_id, int32_t rank, int32_t world, mrec_comm **out);
+mrec_status mrec_comm_destroy(mrec_comm *comm);
+int32_t mrec_comm_world(const mrec_comm *comm);
+int32_t mrec_comm_rank(const mrec_comm *comm);
+/* ids of the lookups for each owner: W x per_peer int32 (mrec_shard_bucketize send_ids) */
+mrec_status mrec_a2a_ids(mrec_comm *comm, const int32_t *send_ids, int32_t *recv_ids,
+                         int64_t per_peer, mrec_stream stream);
+/* gathered rows back to the requesters: W x bytes_per_peer (multiple of 16) */
+mrec_status mrec_a2a_rows_fwd(mrec_comm *comm, const void *send_rows, void *recv_rows,
+                              int64_t bytes_per_peer, mrec_stream stream);
+/* per-lookup gradient rows to the owners: W x floats_per_peer fp32 */
+mrec_status mrec_a2a_rows_bwd(mrec_comm *comm, const float *send_grads, float *recv_grads,
+                              int64_t floats_per_peer, mrec_stream stream);
+/* the data-parallel dense gradient buffer, summed over the ranks in place */
+mrec_status mrec_allreduce_sum_f32(mrec_comm *comm, float *buf, int64_t n, mrec_stream stream);
 
 /* ------------------------------------------------------------------------- */
 /* Row-sharded tables (one process per GPU, W = world size)                   */

@@ -20,7 +20,7 @@ import torch  # noqa: F401  (must precede the dlopen, see module docstring)
 LIB_DIR = os.path.join(os.path.dirname(os.path.abspath(__file__)), "lib")
 LIB_PATH = os.environ.get("MREC_LIB_PATH") or os.path.join(LIB_DIR, "libmrec.so")
 
-ABI_VERSION = 13
+ABI_VERSION = 14
 MAX_TABLES = 64
 BWD_MAX_BATCH = 8192
 BWD_HASH_MAX_BATCH = 4096  # batches up to this use the hash plan (fusable into a GEMM launch)
@@ -178,6 +178,20 @@ _epi_p = ctypes.POINTER(Epilogue)
 SIGNATURES = {
     "mrec_abi_version": (ctypes.c_int, []),
     "mrec_emb_optim_state_ld": (ctypes.c_int64, [ctypes.c_int32, ctypes.c_int32]),
+    "mrec_comm_unique_id": (ctypes.c_int, [ctypes.c_void_p]),
+    "mrec_comm_init": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int32, ctypes.c_int32,
+                                      ctypes.POINTER(ctypes.c_void_p)]),
+    "mrec_comm_destroy": (ctypes.c_int, [ctypes.c_void_p]),
+    "mrec_comm_world": (ctypes.c_int32, [ctypes.c_void_p]),
+    "mrec_comm_rank": (ctypes.c_int32, [ctypes.c_void_p]),
+    "mrec_a2a_ids": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
+                                    ctypes.c_int64, ctypes.c_void_p]),
+    "mrec_a2a_rows_fwd": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
+                                         ctypes.c_int64, ctypes.c_void_p]),
+    "mrec_a2a_rows_bwd": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
+                                         ctypes.c_int64, ctypes.c_void_p]),
+    "mrec_allreduce_sum_f32": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int64,
+                                              ctypes.c_void_p]),
     "mrec_emb_optim_flush": (ctypes.c_int, [_bank_p, ctypes.c_int, ctypes.c_float,
                                             ctypes.c_void_p]),
     "mrec_last_error": (ctypes.c_char_p, []),

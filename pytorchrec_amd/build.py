@@ -65,7 +65,7 @@ def build_lib(force: bool = False, verbose: bool = True) -> str:
         if verbose and out.strip():
             sys.stderr.write(out.decode())
     tmp = LIB + ".tmp"
-    link = [HIPCC, f"--offload-arch={ARCH}", "-shared", "-fPIC", *objs, "-o", tmp]
+    link = [HIPCC, f"--offload-arch={ARCH}", "-shared", "-fPIC", *objs, "-ldl", "-o", tmp]
     r = subprocess.run(link, stdout=subprocess.PIPE, stderr=subprocess.STDOUT)
     if r.returncode != 0:
         raise RuntimeError(f"link failed: {r.stdout.decode()}")

@@ -88,6 +88,73 @@ class ShardComm:
         return t
 
 
+class MrecComm:
+    """The ShardComm interface over libmrec's own RCCL communicator (include/mrec.h
+    mrec_comm_* / mrec_a2a_* / mrec_allreduce_sum_f32): the exchange a non-torch
+    binding would drive, usable from Python for the same sharded step.  The
+    128-byte RCCL unique id goes from rank 0 to the others over ``id_channel``
+    (a torch.distributed group of any backend, gloo included); world 1 needs none.
+    ``close()`` (after every HIP graph that captured its collectives is released)
+    destroys the communicator."""
+
+    def __init__(self, world: int = 1, rank: int = 0, id_channel=None):
+        lib = _mrec.lib()
+        uid = (ctypes.c_char * 128)()
+        if rank == 0:
+            _mrec.call("mrec_comm_unique_id", ctypes.cast(uid, ctypes.c_void_p))
+        if world > 1:
+            if not dist.is_initialized():
+                raise RuntimeError("MrecComm at world > 1 needs torch.distributed for the id")
+            box = [bytes(uid)]
+            dist.broadcast_object_list(box, src=0, group=id_channel)
+            ctypes.memmove(uid, box[0], 128)
+        h = ctypes.c_void_p()
+        _mrec.call("mrec_comm_init", ctypes.cast(uid, ctypes.c_void_p), int(rank), int(world),
+                   ctypes.byref(h))
+        self._h = h
+        self.world, self.rank = int(lib.mrec_comm_world(h)), int(lib.mrec_comm_rank(h))
+        self.force = True  # the collectives run even at world 1
+        self.group = None
+
+    def exchange(self, send: torch.Tensor) -> torch.Tensor:
+        """``out[s]`` = part ``rank`` of rank s's ``send`` (dim 0 in W equal parts)."""
+        send = send.contiguous()
+        out = torch.empty_like(send)
+        per = send.numel() // self.world
+        st = _mrec.stream_handle()
+        if send.dtype == torch.int32:
+            _mrec.call("mrec_a2a_ids", self._h, send.data_ptr(), out.data_ptr(), per, st)
+        elif send.dtype == torch.float32:
+            _mrec.call("mrec_a2a_rows_bwd", self._h, send.data_ptr(), out.data_ptr(), per, st)
+        else:
+            _mrec.call("mrec_a2a_rows_fwd", self._h, send.data_ptr(), out.data_ptr(),
+                       per * send.element_size(), st)
+        return out
+
+    def allreduce_sum_(self, flat: torch.Tensor) -> torch.Tensor:
+        if flat.dtype != torch.float32 or not flat.is_contiguous():
+            raise ValueError("mrec_allreduce_sum_f32 takes a contiguous fp32 buffer")
+        _mrec.call("mrec_allreduce_sum_f32", self._h, flat.data_ptr(), flat.numel(),
+                   _mrec.stream_handle())
+        return flat
+
+    def allreduce_mean_(self, flat: torch.Tensor) -> torch.Tensor:
+        self.allreduce_sum_(flat)
+        if self.world > 1:
+            flat.div_(self.world)
+        return flat
+
+    def broadcast_(self, t: torch.Tensor, src: int = 0) -> torch.Tensor:
+        if self.world > 1:
+            dist.broadcast(t, src)
+        return t
+
+    def close(self):
+        if self._h:
+            _mrec.call("mrec_comm_destroy", self._h)
+            self._h = None
+
+
 def default_cap(batch: int, world: int, rows: Optional[Sequence[int]] = None,
                 sigmas: float = 8.0) -> int:
     """Slots per (owner, table), sized for ids spread uniformly over each table: the

@@ -242,6 +242,60 @@ def test_world1_rccl_dp_sharded_deepfm_step_equals_unsharded(gpu, rccl_world1):
         assert torch.equal(va, vb), k
 
 
+def test_world1_mrec_comm_sharded_step_equals_unsharded(gpu):
+    """The C-ABI communicator (mrec_comm_init / mrec_a2a_* / mrec_allreduce_sum_f32,
+    RCCL opened by libmrec, no torch.distributed at all) drives the row-sharded +
+    data-parallel step at world 1 with every exchange issued: bit-identical to the
+    single-process step; the step captured in a HIP graph replays, and once the
+    graph is released mrec_comm_destroy returns."""
+    import gc
+    from pytorchrec_amd.loss import BCEWithLogitsLoss
+    from pytorchrec_amd.sharding import MrecComm
+    comm = MrecComm(world=1, rank=0)
+    a, b = _deepfm(gpu, False), _deepfm(gpu, True)
+    b.load_state_dict(a.state_dict())
+    b.embeddings.comm = comm
+    b.distribute(comm)
+    data = {f"c_c_C{i}": t for i, t in enumerate(_ids(gpu, 256, 9))}
+    g = torch.Generator().manual_seed(10)
+    for i in range(13):
+        data[f"c_n_I{i}"] = torch.rand(256, generator=g).to(gpu)
+    data["label"] = (torch.rand(256, generator=g) < 0.25).to(torch.int32).to(gpu)
+    for m in (a, b):
+        m.compile(torch.optim.SGD(m.get_parameters(), lr=0.05), BCEWithLogitsLoss(), [], gpu)
+        for bank in m.embedding_banks():
+            # RNE updates: a replayed graph reuses its captured host seed, an eager step
+            # draws a new one, so stochastic rounding would differ between the two
+            bank.stochastic_rounding = False
+    la = [float(a.train_step(data)["loss"].detach()) for _ in range(3)]
+    lb = [float(b.train_step(data)["loss"].detach()) for _ in range(3)]
+    assert la == lb
+    for (k, va), vb in zip(a.state_dict().items(), b.state_dict().values()):
+        assert torch.equal(va, vb), k
+    for bank in b.embedding_banks():
+        bank.check_ids = False
+    s = torch.cuda.Stream()
+    s.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(s):
+        b.train_step(data)
+    torch.cuda.current_stream().wait_stream(s)
+    graph = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(graph):
+        b.train_step(data)
+    for _ in range(2):
+        graph.replay()
+    a.train_step(data)
+    a.train_step(data)
+    a.train_step(data)
+    torch.cuda.synchronize()
+    for (k, va), vb in zip(a.state_dict().items(), b.state_dict().values()):
+        assert torch.equal(va, vb), k
+    del graph
+    gc.collect()
+    torch.cuda.synchronize()
+    comm.close()
+
+
 def test_sgd_multi_matches_torch_and_weight_prep(gpu):
     """mrec_sgd_multi: w -= lr g for several shapes in one launch, images equal
     to mrec_weight_prep of the updated weight (pad columns zero)."""

@@ -40,7 +40,7 @@ def main():
         if p.wait() != 0:
             raise SystemExit("compile failed")
     lib = os.path.join(out_dir, f"libmrec_{name}.so")
-    subprocess.check_call([B.HIPCC, f"--offload-arch={B.ARCH}", "-shared", "-fPIC", *objs, "-o", lib])
+    subprocess.check_call([B.HIPCC, f"--offload-arch={B.ARCH}", "-shared", "-fPIC", *objs, "-ldl", "-o", lib])
     print(lib)
 
 

@@ -295,10 +295,12 @@ def pmc_traffic(kernels, args):
     try:
         with open(PMC_FILE) as fh:
             pmc = json.load(fh)
-        run = pmc.get("run", {})
         want = {"model": args.model, "batch": args.batch, "rows_per_table": args.rows_per_table}
-        if any(run.get(k) != v for k, v in want.items()):
-            return None, {"file": "profiles/pmc_traffic.json", "mismatch": run}
+        runs = [r for r in pmc.get("runs", [pmc.get("run", {})])
+                if all(r.get(k) == v for k, v in want.items())]
+        if not runs:
+            return None, {"file": "profiles/pmc_traffic.json", "no_run_for": want}
+        run = runs[0]
         per = pmc["kernels"][args.model]
         return int(sum(per[k]["hbm_bytes_per_launch"] for k in kernels)), {
             "file": "profiles/pmc_traffic.json", "run": run,
@@ -410,9 +412,37 @@ def pcie_inclusive(step, args, sparse, dense_cols, label_col, device):
 # CPU baseline (oracle restatement of the reference path; rank 0, N = 1 only)
 # ----------------------------------------------------------------------------
 
+def host_cpu() -> dict:
+    """The host's CPU (lscpu) and the share of it this process may use: the GPU box
+    runs one job per GPU and gives it OMP_NUM_THREADS (16) of the host's cores."""
+    info = {}
+    try:
+        import subprocess
+        out = subprocess.run(["lscpu"], capture_output=True, text=True, timeout=10).stdout
+        for line in out.splitlines():
+            k, _, v = line.partition(":")
+            info[k.strip()] = v.strip()
+    except (OSError, ValueError):
+        pass
+    def num(k):
+        try:
+            return int(info.get(k, ""))
+        except ValueError:
+            return None
+    sockets, cps, tpc = num("Socket(s)"), num("Core(s) per socket"), num("Thread(s) per core")
+    phys = sockets * cps if sockets and cps else None
+    affinity = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else os.cpu_count()
+    share = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or affinity
+    return {"model": info.get("Model name"), "sockets": sockets, "cores_per_socket": cps,
+            "threads_per_core": tpc, "physical_cores": phys, "affinity_cpus": affinity,
+            "job_cpu_share": share,
+            "threads_used": max(1, min(share, affinity, phys or affinity))}
+
+
 def cpu_baseline(args):
     from oracle.models import RefDeepFM, criteo_batch, sgd_train_step
-    threads = min(16, os.cpu_count() or 1)
+    cpu = host_cpu()
+    threads = cpu["threads_used"]
     torch.set_num_threads(threads)
     nums = [args.rows_per_table] * CRITEO_FIELDS
     m = RefDeepFM(nums, CRITEO_DENSE, 16, (400, 400, 400))
@@ -427,11 +457,13 @@ def cpu_baseline(args):
         ts.append(time.perf_counter() - t)
     med = statistics.median(ts)
     return {"value": round(args.batch / med, 1), "unit": "samples/s", "cores": threads,
-            "kind": "port",
+            "kind": "port", "host_cpu": cpu,
             "sample": (f"{len(ts)} timed steps (median, after 3 warm-up) of the fp32 torch-CPU "
                        f"restatement of the reference path (26 nn.Embedding + 26 Embedding(rows,1), "
                        f"MLP 429-400-400-400-1, BCE, dense-grad SGD) at B={args.batch}, "
-                       f"{args.rows_per_table} rows/table; {threads} threads"),
+                       f"{args.rows_per_table} rows/table; {threads} threads = the job's CPU "
+                       f"share (OMP_NUM_THREADS) of {cpu['physical_cores']} physical cores "
+                       f"({cpu['sockets']} x {cpu['model']})"),
             "ms_per_step": round(med * 1e3, 3)}
 
 

@@ -12,7 +12,9 @@ namespace mrec {
 // ---------------------------------------------------------------------------
 // plain gather: worker per (b, f) lookup
 // ---------------------------------------------------------------------------
-template <typename T, typename O, int LPR>
+// ADAM: the bank trains with the lazy fused Adam (stale rows are caught up on
+// read); a template flag so the common instantiation carries none of that code
+template <typename T, typename O, int LPR, bool ADAM = false>
 __global__ __launch_bounds__(256) void gather_kernel(BankArgs bank, IdsArgs ids, int64_t B,
                                                      O *__restrict__ out, int64_t out_ld,
                                                      float *__restrict__ w_out,
@@ -32,7 +34,7 @@ __global__ __launch_bounds__(256) void gather_kernel(BankArgs bank, IdsArgs ids,
     const T *row = reinterpret_cast<const T *>(bank.data) +
                    (bank.row_offset[f] + id) * static_cast<int64_t>(bank.row_stride);
     raw = *reinterpret_cast<const uint4 *>(row + l * EPL);
-    if (bank.adam.kind)  // a lazily updated Adam bank: the row as of the last step
+    if constexpr (ADAM)  // a lazily updated Adam bank: the row as of the last step
       raw = adam_current<T>(bank, bank.row_offset[f] + id, l * EPL, live_elems(bank, l * EPL, EPL),
                             raw, *bank.adam.d_t);
   } else if (l == 0 && oob) {
@@ -81,7 +83,7 @@ struct InteractArgs {
 };
 
 // sample b, by the wave whose lane this is
-template <typename T, int LPR, bool X0_BF16>
+template <typename T, int LPR, bool X0_BF16, bool ADAM>
 __device__ __forceinline__ void interact_sample(const BankArgs &bank, const IdsArgs &ids,
                                                 const InteractArgs &ia, int64_t b, int lane) {
   constexpr int EPL = Vec<T>::EPL;
@@ -119,7 +121,7 @@ __device__ __forceinline__ void interact_sample(const BankArgs &bank, const IdsA
         const T *row = reinterpret_cast<const T *>(bank.data) +
                        (bank.row_offset[f] + id) * static_cast<int64_t>(bank.row_stride);
         raw[it] = *reinterpret_cast<const uint4 *>(row + e0);
-        if (bank.adam.kind)  // a lazily updated Adam bank: the row as of the last step
+        if constexpr (ADAM)  // a lazily updated Adam bank: the row as of the last step
           raw[it] = adam_current<T>(bank, bank.row_offset[f] + id, e0, live_elems(bank, e0, EPL),
                                     raw[it], *bank.adam.d_t);
       } else if (l == 0 && oob) {
@@ -218,18 +220,18 @@ __device__ __forceinline__ void interact_sample(const BankArgs &bank, const IdsA
   }
 }
 
-template <typename T, int LPR, bool X0_BF16>
+template <typename T, int LPR, bool X0_BF16, bool ADAM>
 __global__ __launch_bounds__(256) void interact_kernel(BankArgs bank, IdsArgs ids, int64_t B,
                                                        InteractArgs ia) {
   const int64_t b = static_cast<int64_t>(blockIdx.x) * 4 + (threadIdx.x >> 6);
   if (b >= B) return;
-  interact_sample<T, LPR, X0_BF16>(bank, ids, ia, b, threadIdx.x & 63);
+  interact_sample<T, LPR, X0_BF16, ADAM>(bank, ids, ia, b, threadIdx.x & 63);
 }
 
 // the interaction (16 samples per 1024-thread workgroup) with the embedding-
 // backward hash plan in the leading workgroups: a HIP graph runs the step's
 // kernels one after another, so the plan would otherwise cost a kernel of its own
-template <typename T, int LPR, bool X0_BF16>
+template <typename T, int LPR, bool X0_BF16, bool ADAM>
 __global__ __launch_bounds__(1024) void interact_plan_kernel(BankArgs bank, IdsArgs ids, int64_t B,
                                                              InteractArgs ia, PlanJob plan,
                                                              int plan_blocks) {
@@ -241,7 +243,7 @@ __global__ __launch_bounds__(1024) void interact_plan_kernel(BankArgs bank, IdsA
   }
   const int64_t b = static_cast<int64_t>(blockIdx.x - plan_blocks) * 16 + (threadIdx.x >> 6);
   if (b >= B) return;
-  interact_sample<T, LPR, X0_BF16>(bank, ids, ia, b, threadIdx.x & 63);
+  interact_sample<T, LPR, X0_BF16, ADAM>(bank, ids, ia, b, threadIdx.x & 63);
 }
 
 // ---------------------------------------------------------------------------
@@ -294,13 +296,20 @@ static void launch_gather(int lpr, const BankArgs &ba, const IdsArgs &ia, int64_
   const int wpb = 256 / lpr;
   const dim3 grid(static_cast<unsigned>((work + wpb - 1) / wpb));
   O *o = static_cast<O *>(out);
-  switch (lpr) {
-    case 1: gather_kernel<T, O, 1><<<grid, 256, 0, s>>>(ba, ia, B, o, out_ld, w_out, oob); break;
-    case 2: gather_kernel<T, O, 2><<<grid, 256, 0, s>>>(ba, ia, B, o, out_ld, w_out, oob); break;
-    case 4: gather_kernel<T, O, 4><<<grid, 256, 0, s>>>(ba, ia, B, o, out_ld, w_out, oob); break;
-    case 8: gather_kernel<T, O, 8><<<grid, 256, 0, s>>>(ba, ia, B, o, out_ld, w_out, oob); break;
-    default: gather_kernel<T, O, 16><<<grid, 256, 0, s>>>(ba, ia, B, o, out_ld, w_out, oob); break;
+#define MREC_GK(A)                                                                                \
+  switch (lpr) {                                                                                  \
+    case 1: gather_kernel<T, O, 1, A><<<grid, 256, 0, s>>>(ba, ia, B, o, out_ld, w_out, oob); break; \
+    case 2: gather_kernel<T, O, 2, A><<<grid, 256, 0, s>>>(ba, ia, B, o, out_ld, w_out, oob); break; \
+    case 4: gather_kernel<T, O, 4, A><<<grid, 256, 0, s>>>(ba, ia, B, o, out_ld, w_out, oob); break; \
+    case 8: gather_kernel<T, O, 8, A><<<grid, 256, 0, s>>>(ba, ia, B, o, out_ld, w_out, oob); break; \
+    default: gather_kernel<T, O, 16, A><<<grid, 256, 0, s>>>(ba, ia, B, o, out_ld, w_out, oob); break; \
   }
+  if (ba.adam.kind) {
+    MREC_GK(true)
+  } else {
+    MREC_GK(false)
+  }
+#undef MREC_GK
 }
 
 template <typename T, bool XB>
@@ -309,12 +318,19 @@ static void launch_interact(int lpr, const BankArgs &ba, const IdsArgs &ids, int
   const int pb = plan ? plan->bank.n_tables * kPlanBuckets : 0;
   const dim3 grid(static_cast<unsigned>((B + 3) / 4));
   const dim3 grid_p(static_cast<unsigned>(pb + (B + 15) / 16));
-#define MREC_IK(L)                                                                          \
+#define MREC_IKA(L, A)                                                                      \
   do {                                                                                      \
     if (plan)                                                                               \
-      interact_plan_kernel<T, L, XB><<<grid_p, 1024, 0, s>>>(ba, ids, B, ia, *plan, pb);    \
+      interact_plan_kernel<T, L, XB, A><<<grid_p, 1024, 0, s>>>(ba, ids, B, ia, *plan, pb); \
     else                                                                                    \
-      interact_kernel<T, L, XB><<<grid, 256, 0, s>>>(ba, ids, B, ia);                       \
+      interact_kernel<T, L, XB, A><<<grid, 256, 0, s>>>(ba, ids, B, ia);                    \
+  } while (0)
+#define MREC_IK(L)              \
+  do {                          \
+    if (ba.adam.kind)           \
+      MREC_IKA(L, true);        \
+    else                        \
+      MREC_IKA(L, false);       \
   } while (0)
   switch (lpr) {
     case 1: MREC_IK(1); break;
@@ -324,6 +340,7 @@ static void launch_interact(int lpr, const BankArgs &ba, const IdsArgs &ids, int
     default: MREC_IK(16); break;
   }
 #undef MREC_IK
+#undef MREC_IKA
 }
 
 }  // namespace mrec

@@ -143,7 +143,7 @@ __global__ __launch_bounds__(kBT) void bucketize_kernel(IdsArgs ids, RowsArg row
   }
 }
 
-template <int LPR, typename T = uint16_t>
+template <int LPR, typename T = uint16_t, bool ADAM = false>
 __global__ __launch_bounds__(256) void shard_gather_kernel(BankArgs bank, const int32_t *__restrict__ recv,
                                                            int64_t n, int cap,
                                                            uint4 *__restrict__ out) {
@@ -156,7 +156,7 @@ __global__ __launch_bounds__(256) void shard_gather_kernel(BankArgs bank, const 
   uint4 v = make_uint4(0u, 0u, 0u, 0u);
   if (id >= 0 && id < bank.rows[f]) {
     v = reinterpret_cast<const uint4 *>(bank.data)[(bank.row_offset[f] + id) * LPR + l];
-    if (bank.adam.kind) {  // a lazily updated Adam bank: the row as of the last step
+    if constexpr (ADAM) {  // a lazily updated Adam bank: the row as of the last step
       constexpr int EPL = Vec<T>::EPL;
       v = adam_current<T>(bank, bank.row_offset[f] + id, l * EPL, live_elems(bank, l * EPL, EPL), v,
                           *bank.adam.d_t);
@@ -283,18 +283,20 @@ mrec_status mrec_shard_gather(const mrec_table_bank *local, const int32_t *recv_
   const dim3 grid(static_cast<unsigned>((threads + 255) / 256));
   hipStream_t s = static_cast<hipStream_t>(stream);
   uint4 *out = static_cast<uint4 *>(rows_out);
-#define MREC_SGK(T)                                                                           \
-  switch (lpr) {                                                                              \
-    case 1: shard_gather_kernel<1, T><<<grid, 256, 0, s>>>(ba, recv_ids, n, cap, out); break;  \
-    case 2: shard_gather_kernel<2, T><<<grid, 256, 0, s>>>(ba, recv_ids, n, cap, out); break;  \
-    case 4: shard_gather_kernel<4, T><<<grid, 256, 0, s>>>(ba, recv_ids, n, cap, out); break;  \
-    case 8: shard_gather_kernel<8, T><<<grid, 256, 0, s>>>(ba, recv_ids, n, cap, out); break;  \
-    default: shard_gather_kernel<16, T><<<grid, 256, 0, s>>>(ba, recv_ids, n, cap, out); break; \
+#define MREC_SGK(T, A)                                                                           \
+  switch (lpr) {                                                                                 \
+    case 1: shard_gather_kernel<1, T, A><<<grid, 256, 0, s>>>(ba, recv_ids, n, cap, out); break;  \
+    case 2: shard_gather_kernel<2, T, A><<<grid, 256, 0, s>>>(ba, recv_ids, n, cap, out); break;  \
+    case 4: shard_gather_kernel<4, T, A><<<grid, 256, 0, s>>>(ba, recv_ids, n, cap, out); break;  \
+    case 8: shard_gather_kernel<8, T, A><<<grid, 256, 0, s>>>(ba, recv_ids, n, cap, out); break;  \
+    default: shard_gather_kernel<16, T, A><<<grid, 256, 0, s>>>(ba, recv_ids, n, cap, out); break; \
   }
-  if (local->dtype == MREC_BF16) {
-    MREC_SGK(uint16_t)
+  if (!ba.adam.kind) {
+    MREC_SGK(uint16_t, false)  // (T only matters to the Adam catch-up)
+  } else if (local->dtype == MREC_BF16) {
+    MREC_SGK(uint16_t, true)
   } else {
-    MREC_SGK(float)
+    MREC_SGK(float, true)
   }
 #undef MREC_SGK
   return launch_status("mrec_shard_gather");

@@ -1,5 +1,8 @@
 """Pin the CPU oracle (oracle/ref.py) against golden vectors produced by the
 reference itself (tests/golden/make_golden.py).  CPU only."""
+import os
+import sys
+
 import numpy as np
 import pytest
 
@@ -175,3 +178,65 @@ def test_bf16_rne_matches_torch():
     x[:4] = [0.0, -0.0, np.inf, -np.inf]
     t = torch.from_numpy(x).to(torch.bfloat16).view(torch.int16).numpy().view(np.uint16)
     assert np.array_equal(ref.f32_to_bf16_bits(x), t)
+
+
+# ---- G9: the build's own restatement (oracle/restate.py), fp64 and fp32 ----------
+
+def _g9():
+    sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden"))
+    import make_g9
+    return make_g9
+
+
+def test_g9_restatement_pinned_fp64_fp32():
+    """Recompute every G9 output in both widths: fp64 must reproduce the fixture to
+    rounding, fp32 to fp32 reassociation (BLAS blocking may differ by machine)."""
+    m, g = _g9(), golden("g9_restatement.npz")
+    a = {k: g[k] for k in g.files}
+    for name, dt, rtol in (("f64", np.float64, 1e-12), ("f32", np.float32, 2e-5)):
+        got = m.small_outputs(a, dt)
+        for k, v in got.items():
+            want = g[f"{k}_{name}"]
+            np.testing.assert_allclose(np.asarray(v, np.float64), want, rtol=rtol,
+                                       atol=rtol * np.abs(want).max(), err_msg=f"{k}_{name}")
+    # fp32 vs fp64: what the reference's own fp32 arithmetic costs on this path
+    for k in ("fm", "deepfm", "dcnv2", "din_u"):
+        w = g[f"{k}_f64"]
+        assert np.max(np.abs(g[f"{k}_f32"] - w)) <= 1e-5 * np.abs(w).max(), k
+
+
+def test_g9_restatement_agrees_with_cited_pieces():
+    """restate.py's fp64 path == the composition of ref.py's cited functions."""
+    g = golden("g9_restatement.npz")
+    tabs, ids = list(g["tables"]), g["ids"]
+    v = np.stack([ref.gather(t, ids[:, f]) for f, t in enumerate(tabs)], 1)
+    wg = np.stack([g["wtabs"][f][ids[:, f]] for f in range(len(tabs))], 1)
+    fm = ref.fm2(v) + ref.first_order(wg, g["dense"], g["dense_w"], float(g["bias"]))
+    np.testing.assert_allclose(fm, g["fm_f64"], rtol=1e-12, atol=1e-14)
+    mlp = [(g["mlp_W0"], g["mlp_b0"]), (g["mlp_W1"], g["mlp_b1"])]
+    x0 = np.concatenate([v.reshape(v.shape[0], -1), g["dense"]], 1)
+    deep = ref.linear(ref.mlp_fwd(x0, mlp)[-1], g["out_W"], g["out_b"])[:, 0]
+    np.testing.assert_allclose(fm + deep, g["deepfm_f64"], rtol=1e-12, atol=1e-14)
+    xs, _ = ref.dcn_cross_fwd(x0, [(g[f"cross_W{i}"], g[f"cross_b{i}"]) for i in range(3)])
+    dcn = ref.linear(ref.mlp_fwd(xs[-1], mlp)[-1], g["out_W"], g["out_b"])[:, 0]
+    np.testing.assert_allclose(dcn, g["dcnv2_f64"], rtol=1e-12, atol=1e-14)
+    u, _, s = ref.din_attention_pool(g["din_q"], g["din_k"], g["din_valid"],
+                                     [(g["din_att_W0"], g["din_att_b0"])],
+                                     (g["din_out_W"], g["din_out_b"]))
+    np.testing.assert_allclose(u, g["din_u_f64"], rtol=1e-12, atol=1e-14)
+    np.testing.assert_allclose(s, g["din_s_f64"], rtol=1e-12, atol=1e-14)
+    z, dz = ref.bce_with_logits(g["deepfm_f64"], g["label"])
+    np.testing.assert_allclose(z, float(g["deepfm_loss_f64"]), rtol=1e-12)
+
+
+def test_g9_full_size_c2_hash_and_checksum():
+    """The B = 4096 C2 case: seeded inputs hash exactly; the fp64 FM logits'
+    checksum (sum, sum |z|, first 32) is reproduced."""
+    m, g = _g9(), golden("g9_restatement.npz")
+    tables, wtabs, ids, dense, dense_w = m.c2_inputs()
+    assert m.c2_hash(tables, wtabs, ids, dense, dense_w) == str(g["c2_sha256"])
+    from oracle import restate
+    z, _ = restate.fm_logits(list(tables), list(wtabs), ids, dense, dense_w, 0.0, np.float64)
+    sums, head = m.c2_checksum(z)
+    np.testing.assert_allclose(sums, g["c2_fm_sums"], rtol=1e-10)
+    np.testing.assert_allclose(head, g["c2_fm_head"], rtol=1e-12)

@@ -32,7 +32,7 @@
 extern "C" {
 #endif
 
-#define MREC_ABI_VERSION 14
+#define MREC_ABI_VERSION 15
 #define MREC_MAX_TABLES 64      /* tables per table bank / per call */
 #define MREC_BWD_MAX_BATCH 8192  /* lookups per table per plan/apply call */
 #define MREC_BWD_HASH_MAX_BATCH 4096  /* batches up to this use the hash plan */
@@ -533,6 +533,7 @@ typedef struct mrec_gemm_call_s {
 mrec_status mrec_gemm_multi(int32_t n, const mrec_gemm_call *calls, mrec_stream stream);
 
 
+
 /* the CTR head's parameter finish (arguments of mrec_ctr_head_finish) */
 typedef struct {
   const float *part;
@@ -657,9 +658,52 @@ typedef struct {
   float *loss_part;          /* [ceil(batch/16)] scratch */
   uint32_t *ticket;          /* device word, zero before the first call; left zero */
   float *loss;               /* [1] */
+  /* ABI 15: kfrag != 0 -> h_out[l] / dh_out[l] are k-fragment images of [batch,
+   * N_l] (mrec_kfrag_elems; ld_h / ld_dh ignored) and x0_img (may be NULL) receives
+   * the k-fragment image of x0 [batch, N_0]: the operands of mrec_tower_dw */
+  int32_t kfrag;
+  void *x0_img;
 } mrec_tower_args;
 
 mrec_status mrec_tower_fwd_bwd(const mrec_tower_args *a, mrec_stream stream);
+
+/*
+ * Weight gradients of the fused tower (ABI 15): for every layer l,
+ *   partial slab z of dW_l [n_out, n_in + 1] = sum over K slice z of the batch of
+ *   dY_l[b]^T [X_l[b] | 1]        (column n_in: the bias gradient)
+ * written to ws[l] + z * n_out * ldws[l] (fp32) -- exactly the split-K PARTIAL slabs
+ * of mrec_gemm(n_out, n_in, batch, dY_l COL, X_l COL, b_ones_col = n_in, ...,
+ * split_k = splits), so a later mrec_gemm_multi REDUCE job of that call (same
+ * workspace) finishes it (fixed-order sum + epilogue / fused SGD).  `splits` must
+ * be an effective count for the batch (B = 4096: 2, 4, 5, 8, 16 ...).
+ * dy_img / x_img are k-fragment images (mrec_kfrag_elems / mrec_kfrag_pack; the
+ * tower writes them, mrec_tower_args.kfrag).  `finish` (may be NULL): the CTR head
+ * finish in extra workgroups of the same launch (as mrec_gemm_multi_ex).
+ * Replaces the weight-gradient half of autograd through nn.Linear in the
+ * reference MLP (MLP.py:8-23, Dense.py:12-24) for the tower path.
+ */
+typedef struct {
+  int32_t n_layers;          /* 1..4 */
+  int64_t batch;
+  int32_t n_out[4], n_in[4];
+  const void *dy_img[4];     /* bf16 k-fragment image of dY_l [batch, n_out] */
+  const void *x_img[4];      /* bf16 k-fragment image of X_l [batch, n_in] */
+  float *ws[4];              /* splits x n_out x ldws fp32 */
+  int64_t ldws[4];           /* >= n_in + 1 (mrec_gemm's slab stride: round8(n_in + 1)) */
+  int32_t splits;
+} mrec_tower_dw_args;
+
+mrec_status mrec_tower_dw(const mrec_tower_dw_args *args, const mrec_head_finish_job *finish,
+                          mrec_stream stream);
+
+/* elements of the k-fragment image of a [rows, cols] matrix: one 1 KiB block per 16
+ * columns x 32 rows, block (c / 16) * ceil(rows / 32) + r / 32, lane
+ * c % 16 + 16 ((r % 32) / 8), element r % 8 (the MFMA operand order) */
+int64_t mrec_kfrag_elems(int64_t rows, int64_t cols);
+
+/* row-major bf16 [rows, cols] (row stride ld) -> its k-fragment image (pads zero) */
+mrec_status mrec_kfrag_pack(const void *x, int64_t rows, int64_t cols, int64_t ld, void *img,
+                            mrec_stream stream);
 
 /* elements of the fwd (bwd = 0) or bwd (bwd = 1) tower image of an [N, K] weight */
 int64_t mrec_tower_image_elems(int64_t N, int64_t K, int32_t bwd);

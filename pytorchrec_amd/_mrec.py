@@ -20,7 +20,7 @@ import torch  # noqa: F401  (must precede the dlopen, see module docstring)
 LIB_DIR = os.path.join(os.path.dirname(os.path.abspath(__file__)), "lib")
 LIB_PATH = os.environ.get("MREC_LIB_PATH") or os.path.join(LIB_DIR, "libmrec.so")
 
-ABI_VERSION = 14
+ABI_VERSION = 15
 MAX_TABLES = 64
 BWD_MAX_BATCH = 8192
 BWD_HASH_MAX_BATCH = 4096  # batches up to this use the hash plan (fusable into a GEMM launch)
@@ -158,7 +158,16 @@ class TowerArgs(ctypes.Structure):
                 ("z", ctypes.c_void_p), ("dz", ctypes.c_void_p),
                 ("part", ctypes.c_void_p), ("ldp", ctypes.c_int64),
                 ("loss_part", ctypes.c_void_p), ("ticket", ctypes.c_void_p),
-                ("loss", ctypes.c_void_p)]
+                ("loss", ctypes.c_void_p), ("kfrag", ctypes.c_int32), ("x0_img", ctypes.c_void_p)]
+
+
+class TowerDwArgs(ctypes.Structure):
+    """mrec_tower_dw_args (include/mrec.h)."""
+    _fields_ = [("n_layers", ctypes.c_int32), ("batch", ctypes.c_int64),
+                ("n_out", ctypes.c_int32 * 4), ("n_in", ctypes.c_int32 * 4),
+                ("dy_img", ctypes.c_void_p * 4), ("x_img", ctypes.c_void_p * 4),
+                ("ws", ctypes.c_void_p * 4), ("ldws", ctypes.c_int64 * 4),
+                ("splits", ctypes.c_int32)]
 
 
 LAYOUT_ROW, LAYOUT_COL = 0, 1
@@ -229,6 +238,9 @@ SIGNATURES = {
     "mrec_gemm": (ctypes.c_int, [_i64, _i64, _i64, _op_p, _op_p, _i64, _i64, _epi_p,
                                  _vp, ctypes.c_int, _i64, _i32, _vp, ctypes.c_size_t, _vp]),
     "mrec_gemm_multi": (ctypes.c_int, [_i32, ctypes.POINTER(GemmCall), _vp]),
+    "mrec_tower_dw": (ctypes.c_int, [ctypes.POINTER(TowerDwArgs), ctypes.POINTER(HeadFinishJob), _vp]),
+    "mrec_kfrag_elems": (_i64, [_i64, _i64]),
+    "mrec_kfrag_pack": (ctypes.c_int, [_vp, _i64, _i64, _i64, _vp, _vp]),
     "mrec_gemm_multi_ex": (ctypes.c_int, [_i32, ctypes.POINTER(GemmCall), ctypes.POINTER(PlanJob),
                                           ctypes.POINTER(HeadFinishJob), _vp]),
     "mrec_weight_prep": (ctypes.c_int, [_vp, _i64, _i64, _i64, _vp, _i64, _vp, _i64, _vp]),

@@ -19,12 +19,35 @@ struct HeadFinishArgs {
 
 __device__ __forceinline__ int head_finish_blocks(int H, int ns) { return (H + 1 + ns + 7) / 8; }
 
-// workgroup `bid` (256 threads) finishes columns [8 bid, 8 bid + 8) of [w | bias | ws]
+// workgroup `bid` (T = 256 or 64 threads) finishes columns [8 bid, 8 bid + 8) of
+// [w | bias | ws]; the same fixed summation order for either T (the 4 waves' lanes
+// of the 256-thread form are the 64-thread form's 4 strides)
+template <int T = 256>
 __device__ __forceinline__ void ctr_head_finish_body(const HeadFinishArgs &a, int bid,
                                                      float (*red)[9]) {
   const int H = a.H, ns = a.ns;
   const int c0 = bid * 8;
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  if constexpr (T == 64) {
+    for (int w = 0; w < 4; ++w) {  // the 4 "waves" of the 256-thread order, one after another
+      float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+      for (int k = w * 64 + lane; k < a.nparts; k += 256) {
+#pragma unroll
+        for (int j = 0; j < 8; ++j)
+          if (c0 + j <= H + ns) acc[j] += a.part[static_cast<int64_t>(k) * a.ldp + c0 + j];
+      }
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+#pragma unroll
+        for (int off = 32; off > 0; off >>= 1) acc[j] += __shfl_xor(acc[j], off);
+      }
+      if (lane == 0) {
+#pragma unroll
+        for (int j = 0; j < 8; ++j) red[w][j] = acc[j];
+      }
+    }
+    __syncthreads();
+  } else {
   float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
   for (int k = threadIdx.x; k < a.nparts; k += 256) {
 #pragma unroll
@@ -41,6 +64,7 @@ __device__ __forceinline__ void ctr_head_finish_body(const HeadFinishArgs &a, in
     for (int j = 0; j < 8; ++j) red[wv][j] = acc[j];
   }
   __syncthreads();
+  }
   if (threadIdx.x < 8) {
     const int c = c0 + threadIdx.x;
     if (c > H + ns) return;

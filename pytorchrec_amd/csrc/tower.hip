@@ -87,6 +87,9 @@ struct TowerArgs {
   int rotate;  // per-workgroup k-step rotation (MREC_TOWER_ROT=0 disables)
   unsigned long long *stamps;  // diagnostics: [grid][16] wall-clock stamps (NULL: off)
   int store_mode;  // tower_store (MREC_TOWER_STORE)
+  int kfrag;       // h_out / dh_out / x0_img are k-fragment images (tower_common.h)
+  int nsteps;      // their k steps: ceil(B / 32)
+  uint16_t *x0_img;
 };
 
 __host__ __device__ __forceinline__ int tw_ceil(int a, int b) { return (a + b - 1) / b; }
@@ -260,6 +263,50 @@ __device__ __forceinline__ void tower_store(const char *blk, int s_blk, int widt
   }
 }
 
+// rows [0, 16) of an LDS block -> the k-fragment image `img` of [B, width]
+// (tower_common.h kfrag_idx): per 16-column tile the workgroup's half of the
+// 32-row step is 32 lanes x 16 B = one contiguous 512-B piece.  Rows >= B are
+// written as zeros; the last workgroup also zeroes the other half of its step when
+// no workgroup owns it, so the image never holds stale rows (the weight-gradient
+// kernel multiplies whole steps).
+__device__ __forceinline__ void tower_store_kfrag(const char *blk, int s_blk, int width, uint16_t *img,
+                                                  int nsteps, int64_t row0, int64_t B, int store_mode) {
+  if (!img || store_mode == 2) return;
+  const int ctiles = tw_ceil(width, 16);
+  const int st = static_cast<int>(row0 >> 5), h = static_cast<int>((row0 >> 4) & 1);
+  const int per = (h == 0 && row0 + TW_ROWS >= B) ? 64 : 32;
+  const int bytes = static_cast<int>(kfrag_elems(B, width) * 2);
+  const __amdgpu_buffer_rsrc_t rsrc = __builtin_amdgcn_make_buffer_rsrc(img, 0, bytes, 0x00020000);
+  for (int idx = threadIdx.x; idx < ctiles * per; idx += TW_THREADS) {
+    const int t = idx / per, j = idx - t * per;
+    const int gl = j >> 4, c = t * 16 + (j & 15);
+    uint32_t w[4] = {0u, 0u, 0u, 0u};
+    if (gl < 2 && c < width) {
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        const int r = 8 * gl + e;
+        const uint32_t v = row0 + r < B ? *reinterpret_cast<const uint16_t *>(blk + r * s_blk + c * 2) : 0u;
+        w[e >> 1] |= v << (16 * (e & 1));
+      }
+    }
+    const int off = ((t * nsteps + st) * 64 + (c & 15) + 16 * (2 * h + gl)) * 16;
+    const u32x4 v = u32x4{w[0], w[1], w[2], w[3]};
+    if (store_mode == 1)
+      __builtin_amdgcn_raw_buffer_store_b128(v, rsrc, off, 0, 16);
+    else
+      __builtin_amdgcn_raw_buffer_store_b128(v, rsrc, off, 0, 0);
+  }
+}
+
+// an activation / gradient block leaves in the launch's layout
+__device__ __forceinline__ void tower_out(const TowerArgs &a, const char *blk, int s_blk, int width,
+                                          uint16_t *dst, int64_t ld, int64_t row0) {
+  if (a.kfrag)
+    tower_store_kfrag(blk, s_blk, width, dst, a.nsteps, row0, a.B, a.store_mode);
+  else
+    tower_store(blk, s_blk, width, dst, ld, row0, a.B, a.store_mode);
+}
+
 // diagnostics: stamps go to LDS (a global store before a barrier would be waited
 // for by it) and leave at the end of the workgroup
 #define TW_STAMP(k)                                                                  \
@@ -319,6 +366,8 @@ __global__ __launch_bounds__(TW_THREADS) void tower_kernel(TowerArgs a) {
   }
   __syncthreads();
   TW_STAMP(1);
+  if (a.kfrag) tower_store_kfrag(lds + a.off_x, a.s_x, a.width[0], a.x0_img, a.nsteps, row0, a.B,
+                                 a.store_mode);
 
   // ---- forward: h_l = relu(h_{l-1} W_l^T + b_l) --------------------------------
   for (int l = 0; l < L; ++l) {
@@ -328,8 +377,7 @@ __global__ __launch_bounds__(TW_THREADS) void tower_kernel(TowerArgs a) {
                        lds + a.off_h[l], a.s_h[l], prm + a.p_bias[l], nullptr, 0, a.rotate);
     __syncthreads();
     TW_STAMP(2 + l);
-    if (l + 1 < L) tower_store(lds + a.off_h[l], a.s_h[l], a.width[l + 1], a.h_out[l], a.ld_h[l],
-                               row0, a.B, a.store_mode);
+    if (l + 1 < L) tower_out(a, lds + a.off_h[l], a.s_h[l], a.width[l + 1], a.h_out[l], a.ld_h[l], row0);
   }
 
   // ---- head + BCE: thread (m = tid / 32, c = tid % 32), parameters from LDS ----
@@ -418,7 +466,7 @@ __global__ __launch_bounds__(TW_THREADS) void tower_kernel(TowerArgs a) {
       if (a.z) a.z[row0 + tid] = f_z[tid];
     }
   }
-  tower_store(lds + a.off_g[0], a.s_g, H, a.dh_out[L - 1], a.ld_dh[L - 1], row0, a.B, a.store_mode);
+  tower_out(a, lds + a.off_g[0], a.s_g, H, a.dh_out[L - 1], a.ld_dh[L - 1], row0);
 
   // ---- backward: dh_{l-1} = (dh_l W_l) * [h_{l-1} > 0], dx0 = dh_1 W_1 ----------
   __shared__ unsigned s_last;
@@ -433,7 +481,7 @@ __global__ __launch_bounds__(TW_THREADS) void tower_kernel(TowerArgs a) {
     __syncthreads();
     TW_STAMP(7 + (L - 1 - l));
     if (l > 0) {
-      tower_store(gout, a.s_g, a.width[l], a.dh_out[l - 1], a.ld_dh[l - 1], row0, a.B, a.store_mode);
+      tower_out(a, gout, a.s_g, a.width[l], a.dh_out[l - 1], a.ld_dh[l - 1], row0);
     } else {
       // the loss: this workgroup's partial as a write-through granule + a relaxed
       // agent ticket (cdna_hip_programming.md §6 G16), before the dx0 stores so the
@@ -538,15 +586,25 @@ mrec_status mrec_tower_fwd_bwd(const mrec_tower_args *p, mrec_stream stream) {
     MREC_CHECK_ARG(s.width[l] >= 1 && s.width[l] <= TW_MAXW, "every width must be in [1, 512]");
   MREC_CHECK_ARG(al16(s.x0, s.ld_x0) && s.ld_x0 >= (s.width[0] + 7) / 8 * 8,
                  "x0 rows must be 16-B aligned with ld_x0 >= round8(width[0])");
+  const bool kf = s.kfrag != 0;
+  auto al = [](const void *q) { return q && (reinterpret_cast<uintptr_t>(q) & 15) == 0; };
   for (int l = 0; l < L; ++l) {
     MREC_CHECK_ARG(s.w_fwd[l] && s.w_bwd[l], "NULL weight image");
     const int w = s.width[l + 1];
+    if (kf) {
+      MREC_CHECK_ARG(al(s.dh_out[l]) && (l + 1 >= L || !s.h_out[l] || al(s.h_out[l])),
+                     "k-fragment images must be 16-B aligned");
+      continue;
+    }
     MREC_CHECK_ARG(al16(s.dh_out[l], s.ld_dh[l]) && s.ld_dh[l] >= (w + 7) / 8 * 8,
                    "dh_out rows must be 16-B aligned with ld >= round8(width)");
     if (l + 1 < L && s.h_out[l])
       MREC_CHECK_ARG(al16(s.h_out[l], s.ld_h[l]) && s.ld_h[l] >= (w + 7) / 8 * 8,
                      "h_out rows must be 16-B aligned with ld >= round8(width)");
   }
+  MREC_CHECK_ARG(!kf || !s.x0_img || al(s.x0_img), "x0_img must be 16-B aligned");
+  MREC_CHECK_ARG(!kf || kfrag_elems(s.batch, TW_MAXW) * 2 < (int64_t(1) << 31),
+                 "batch too large for k-fragment images");
   MREC_CHECK_ARG(!s.dx0 || (al16(s.dx0, s.ld_dx0) && s.ld_dx0 >= (s.width[0] + 7) / 8 * 8),
                  "dx0 rows must be 16-B aligned with ld >= round8(width[0])");
   MREC_CHECK_ARG(s.head_w && s.y && s.dz && s.part && s.loss_part && s.ticket && s.loss,
@@ -605,6 +663,9 @@ mrec_status mrec_tower_fwd_bwd(const mrec_tower_args *p, mrec_stream stream) {
     return e ? atoi(e) : 1;
   }();
   a.store_mode = store_env;
+  a.kfrag = kf ? 1 : 0;
+  a.nsteps = static_cast<int>((s.batch + 31) / 32);
+  a.x0_img = kf ? static_cast<uint16_t *>(s.x0_img) : nullptr;
   int off = 0;
   a.off_x = off;
   a.s_x = tw_stride(s.width[0]);

@@ -46,4 +46,17 @@ __host__ __device__ __forceinline__ int64_t tower_idx_bwd(int64_t n, int64_t k, 
   return (blk * 64 + lane) * 8 + (n & 7);
 }
 
+// k-fragment image of an activation / gradient matrix X [B, C] (batch-major), the
+// operand layout of the tower's weight-gradient kernel (tower_dw.hip): one 1 KiB
+// block per 16 columns x 32 batch rows (tile t = c / 16, k step s = b / 32, block
+// t * ceil(B/32) + s), lane l of the block = column 16 t + l % 16, rows
+// 32 s + 8 (l / 16) .. + 8 -- v_mfma_f32_16x16x32_bf16 operand order for A (dY^T)
+// and B (X) alike.  Rows past B and columns past C are zero.
+__host__ __device__ __forceinline__ int64_t kfrag_elems(int64_t rows, int64_t cols) {
+  return ((cols + 15) / 16) * ((rows + 31) / 32) * 512;
+}
+__host__ __device__ __forceinline__ int64_t kfrag_idx(int64_t b, int64_t c, int64_t nsteps) {
+  return (((c >> 4) * nsteps + (b >> 5)) * 64 + (c & 15) + 16 * ((b & 31) >> 3)) * 8 + (b & 7);
+}
+
 }  // namespace mrec

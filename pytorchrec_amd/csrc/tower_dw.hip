@@ -1,0 +1,406 @@
+// Weight gradients of the fused MLP tower, dW_l = dY_l^T X_l (+ the bias gradient
+// sum_b dY_l[b] in column n_in), over the batch, as split-K partial slabs
+// (include/mrec.h mrec_tower_dw).
+//
+// Why not the generic GEMM (gemm.hip): its COL x COL path stages both operands in
+// LDS through a barrier-coupled 3-deep ring and ran the tower's three dW at
+// 24 us (~60 TFLOP/s, bench_gemm dw3), with every k group of a workgroup waiting on
+// its slowest wave.  Here the operands are stored by the tower itself in the
+// k-fragment layout (tower_common.h, kfrag_idx): one 1 KiB block per 16 columns x
+// 32 batch rows, in v_mfma_f32_16x16x32_bf16 operand order for BOTH operands (lane
+// l: column l % 16, rows 8 (l / 16) .. + 8).  Every wave streams its own fragments
+// straight into VGPRs (one fully coalesced 1 KiB buffer load per fragment, PF k
+// steps in flight, no LDS, no barrier) -- the fused tower's weight-stream pattern,
+// which runs at the CU's L2 read rate.
+//
+// Geometry: a 256-thread workgroup owns a 128 x 128 output block (4 waves in 2 x 2,
+// each 64 x 64 = 4 x 4 MFMA tiles; waves of a row / column load the same A / B
+// blocks back to back, the second usually from L1) for one K slice; the bias
+// column's fragments are synthesised (ones).  Steps past the slice load from an
+// out-of-range offset (zeros) so the pipeline never branches.
+#include <algorithm>
+#include <cstdlib>
+
+#include "common.h"
+#include "head_common.h"
+#include "tower_common.h"
+
+namespace mrec {
+
+#ifndef MREC_TDW_EXP
+#define MREC_TDW_EXP 0
+#endif
+constexpr int DW_THREADS = 256;
+constexpr int DW_PF = 4;       // k steps of fragments in flight per wave
+constexpr int DW_MAXL = 4;
+constexpr int DW_BLK = 128;    // output block edge (8 MFMA tiles)
+constexpr int DW_OOB = 1 << 30;  // a voffset past every image: the load returns zeros
+
+typedef short bf16x8 __attribute__((ext_vector_type(8)));
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+
+struct DwLayer {
+  const uint16_t *dy;  // k-fragment image of dY [B, n_out]
+  const uint16_t *x;   // k-fragment image of X [B, n_in]
+  float *ws;           // partial slabs [splits][n_out][ldws]
+  int64_t ldws;
+  int n_out, n_in;
+  int dy_bytes, x_bytes;
+  int nbn, nbk;        // output blocks along n_out / (n_in + 1)
+  int start;           // first workgroup of this layer (after the finish blocks)
+};
+
+struct DwArgs {
+  int L;
+  int nsteps;          // k steps of 32 batch rows
+  int splits;
+  int steps_per_split;
+  DwLayer lay[DW_MAXL];
+  int fin_blocks;
+  HeadFinishArgs fin;
+};
+
+// One wave per workgroup, one 64 x 64 output tile (4 x 4 MFMA tiles) per wave.
+template <int PF>
+__global__ __launch_bounds__(64) void tower_dw_kernel(DwArgs a) {
+  __shared__ __attribute__((aligned(16))) float tile[64 * 68];  // epilogue transpose
+  if (static_cast<int>(blockIdx.x) < a.fin_blocks) {  // uniform
+    if (static_cast<int>(blockIdx.x) < head_finish_blocks(a.fin.H, a.fin.ns))
+      ctr_head_finish_body<64>(a.fin, blockIdx.x, reinterpret_cast<float (*)[9]>(tile));
+    return;
+  }
+  const int b = blockIdx.x - a.fin_blocks;
+  int l = 0;
+  while (l + 1 < a.L && b >= a.lay[l + 1].start) ++l;  // uniform
+  const DwLayer &y = a.lay[l];
+  const int local = b - y.start;
+  const int z = local % a.splits, blk = local / a.splits;
+  if (blk >= y.nbn * y.nbk) return;
+  const int bn = blk / y.nbk, bk = blk - bn * y.nbk;
+  const int lane = threadIdx.x & 63;
+  const int nt0 = bn * 4;  // the wave's first n_out tile
+  const int kt0 = bk * 4;  // its first n_in (+ bias) tile
+  const int s_beg = z * a.steps_per_split;
+  const int s_n = max(0, min(a.nsteps, s_beg + a.steps_per_split) - s_beg);
+
+  const __amdgpu_buffer_rsrc_t ra =
+      __builtin_amdgcn_make_buffer_rsrc(const_cast<uint16_t *>(y.dy), 0, y.dy_bytes, 0x00020000);
+  const __amdgpu_buffer_rsrc_t rb =
+      __builtin_amdgcn_make_buffer_rsrc(const_cast<uint16_t *>(y.x), 0, y.x_bytes, 0x00020000);
+  // byte offset of this lane's 16 B in step s_beg of each tile (tiles past the
+  // image read zeros through the range check)
+  int va[4], vb[4];
+  const int atiles = (y.n_out + 15) / 16, btiles = (y.n_in + 15) / 16;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    va[i] = nt0 + i < atiles ? ((nt0 + i) * a.nsteps + s_beg) * 1024 + lane * 16 : DW_OOB;
+    vb[i] = kt0 + i < btiles ? ((kt0 + i) * a.nsteps + s_beg) * 1024 + lane * 16 : DW_OOB;
+  }
+  // the bias column n_in: its tile gets ones in that column (its other columns
+  // hold X's zero padding, or nothing past the image)
+  const int ones_tile = y.n_in / 16;
+  const bool ones_lane = (lane & 15) == (y.n_in & 15);
+  const bf16x8 ones = bf16x8{0x3f80, 0x3f80, 0x3f80, 0x3f80, 0x3f80, 0x3f80, 0x3f80, 0x3f80};
+  bool ones_j[4];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) ones_j[j] = kt0 + j == ones_tile && ones_lane;
+
+  f32x4 acc[4][4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  bf16x8 fa[PF][4], fb[PF][4];
+  auto load = [&](int p, int s) {  // step s of the slice (past it: zeros)
+    const int so = s < s_n ? s * 1024 : DW_OOB;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      fa[p][i] = __builtin_bit_cast(bf16x8, __builtin_amdgcn_raw_buffer_load_b128(ra, va[i] + so, 0, 0));
+      fb[p][i] = __builtin_bit_cast(bf16x8, __builtin_amdgcn_raw_buffer_load_b128(rb, vb[i] + so, 0, 0));
+    }
+  };
+#pragma unroll
+  for (int p = 0; p < PF; ++p) {
+    load(p, p);
+    __builtin_amdgcn_sched_barrier(0);  // issue order = consumption order (waitcnt)
+  }
+#if MREC_TDW_EXP == 4  // diagnostics: no main loop
+  const int total = 0;
+#else
+  const int total = (s_n + PF - 1) / PF * PF;
+#endif
+  for (int base = 0; base < total; base += PF) {
+#pragma unroll
+    for (int p = 0; p < PF; ++p) {
+      bf16x8 bj[4];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) bj[j] = ones_j[j] ? ones : fb[p][j];
+#if MREC_TDW_EXP == 1  // diagnostics: loads only
+#pragma unroll
+      for (int i = 0; i < 4; ++i) acc[i][0][0] += __builtin_bit_cast(float, int(fa[p][i][0] ^ bj[i][1]));
+#else
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[p][i], bj[j], acc[i][j], 0, 0, 0);
+#endif
+#if MREC_TDW_EXP != 2  // 2: MFMAs on the prologue's fragments only
+      load(p, base + p + PF);
+#endif
+      __builtin_amdgcn_sched_barrier(0);
+    }
+  }
+
+  // partial slab z: lane holds rows 16 i + 4 (lane / 16) + r of column 16 j +
+  // lane % 16 of the tile; through LDS so that the slab rows leave as 16-B stores
+  // (16 lanes = one 256-B row segment)
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) tile[(i * 16 + 4 * (lane >> 4) + r) * 68 + j * 16 + (lane & 15)] = acc[i][j][r];
+  __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): one wave, no barrier needed
+  __builtin_amdgcn_wave_barrier();
+  float *slab = y.ws + static_cast<int64_t>(z) * y.n_out * y.ldws;
+  const int m0 = nt0 * 16, n = kt0 * 16 + (lane & 15) * 4;
+#pragma unroll 4
+  for (int it = 0; it < 16; ++it) {
+    const int row = it * 4 + (lane >> 4);
+    const int m = m0 + row;
+    if (m < y.n_out && n < y.ldws) {
+      const float4 v = *reinterpret_cast<const float4 *>(tile + row * 68 + (lane & 15) * 4);
+#if MREC_TDW_EXP == 3  // diagnostics: no slab stores (kept alive)
+      if (v.x == 1.2345e-30f)
+#endif
+      *reinterpret_cast<float4 *>(slab + static_cast<int64_t>(m) * y.ldws + n) = v;
+    }
+  }
+}
+
+// The same block with the fragments shared through LDS: the 16 distinct 1 KiB
+// fragments of a k step (8 of dY^T, 8 of X) are loaded once per workgroup -- 4 per
+// wave, PF steps ahead in VGPRs -- stored to a 2-slot LDS ring, and every wave
+// reads the 8 it multiplies (ds_read_b128, lane-linear: conflict free).  Without
+// it each wave fetched its own 8 fragments from L2 (twice the workgroup's bytes:
+// the second wave's loads of a shared fragment did not hit in L1), and the CU's
+// L2 read rate bounded the kernel.  One barrier per k step.
+template <int PF>
+__global__ __launch_bounds__(DW_THREADS, 1) void tower_dw_lds_kernel(DwArgs a) {
+  __shared__ float red[4][9];
+  __shared__ __attribute__((aligned(16))) bf16x8 ring[2][16][64];
+  if (static_cast<int>(blockIdx.x) < a.fin_blocks) {  // uniform
+    if (static_cast<int>(blockIdx.x) < head_finish_blocks(a.fin.H, a.fin.ns))
+      ctr_head_finish_body(a.fin, blockIdx.x, red);
+    return;
+  }
+  const int b = blockIdx.x - a.fin_blocks;
+  int l = 0;
+  while (l + 1 < a.L && b >= a.lay[l + 1].start) ++l;  // uniform
+  const DwLayer &y = a.lay[l];
+  const int local = b - y.start;
+  const int z = local % a.splits, blk = local / a.splits;
+  if (blk >= y.nbn * y.nbk) return;
+  const int bn = blk / y.nbk, bk = blk - bn * y.nbk;
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int wm = wave >> 1, wn = wave & 1;
+  const int s_beg = z * a.steps_per_split;
+  const int s_n = max(0, min(a.nsteps, s_beg + a.steps_per_split) - s_beg);
+
+  const __amdgpu_buffer_rsrc_t ra =
+      __builtin_amdgcn_make_buffer_rsrc(const_cast<uint16_t *>(y.dy), 0, y.dy_bytes, 0x00020000);
+  const __amdgpu_buffer_rsrc_t rb =
+      __builtin_amdgcn_make_buffer_rsrc(const_cast<uint16_t *>(y.x), 0, y.x_bytes, 0x00020000);
+  // this wave loads fragments f = 4 wave + q of the workgroup's 16 (0-7: dY^T tiles
+  // 8 bn + f, 8-15: X tiles 8 bk + f - 8); waves 0-1 load A, 2-3 load B
+  const bool loads_a = wave < 2;
+  const int atiles = (y.n_out + 15) / 16, btiles = (y.n_in + 15) / 16;
+  int vo[4];
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    const int f = wave * 4 + q;
+    const int t = loads_a ? bn * 8 + f : bk * 8 + f - 8;
+    const int nt = loads_a ? atiles : btiles;
+    vo[q] = t < nt ? (t * a.nsteps + s_beg) * 1024 + lane * 16 : DW_OOB;
+  }
+  const int ones_tile = y.n_in / 16;
+  const bool ones_lane = (lane & 15) == (y.n_in & 15);
+  const bf16x8 ones = bf16x8{0x3f80, 0x3f80, 0x3f80, 0x3f80, 0x3f80, 0x3f80, 0x3f80, 0x3f80};
+  bool ones_j[4];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) ones_j[j] = bk * 8 + wn * 4 + j == ones_tile && ones_lane;
+
+  f32x4 acc[4][4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  bf16x8 fr[PF][4];
+  auto load = [&](int p, int s) {
+    const int so = s < s_n ? s * 1024 : DW_OOB;
+#pragma unroll
+    for (int q = 0; q < 4; ++q)
+      fr[p][q] = __builtin_bit_cast(
+          bf16x8, loads_a ? __builtin_amdgcn_raw_buffer_load_b128(ra, vo[q] + so, 0, 0)
+                          : __builtin_amdgcn_raw_buffer_load_b128(rb, vo[q] + so, 0, 0));
+  };
+#pragma unroll
+  for (int p = 0; p < PF; ++p) {
+    load(p, p);
+    __builtin_amdgcn_sched_barrier(0);
+  }
+  const int total = (s_n + PF - 1) / PF * PF;
+  for (int base = 0; base < total; base += PF) {
+#pragma unroll
+    for (int p = 0; p < PF; ++p) {
+      const int slot = p & 1;  // PF even: step base + p uses slot (base + p) & 1
+#pragma unroll
+      for (int q = 0; q < 4; ++q) ring[slot][wave * 4 + q][lane] = fr[p][q];
+      __syncthreads();  // slot written by all; the reads of its previous use retired
+      load(p, base + p + PF);
+      bf16x8 fa[4], fb[4];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) fa[i] = ring[slot][wm * 4 + i][lane];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const bf16x8 t = ring[slot][8 + wn * 4 + j][lane];
+        fb[j] = ones_j[j] ? ones : t;
+      }
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[i], fb[j], acc[i][j], 0, 0, 0);
+      __builtin_amdgcn_sched_barrier(0);
+    }
+  }
+
+  const int ncols = y.n_in + 1;
+  float *slab = y.ws + static_cast<int64_t>(z) * y.n_out * y.ldws;
+  const int nt0 = bn * 8 + wm * 4, kt0 = bk * 8 + wn * 4;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int n = (kt0 + j) * 16 + (lane & 15);
+      if (n >= ncols) continue;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int m = (nt0 + i) * 16 + 4 * (lane >> 4) + r;
+        if (m < y.n_out) slab[static_cast<int64_t>(m) * y.ldws + n] = acc[i][j][r];
+      }
+    }
+  }
+}
+
+// row-major bf16 [rows, cols] (row stride ld) -> k-fragment image (pad rows /
+// columns zero); one thread per 16-B lane slot of the image
+__global__ __launch_bounds__(256) void kfrag_pack_kernel(const uint16_t *__restrict__ x, int64_t rows,
+                                                         int64_t cols, int64_t ld,
+                                                         uint16_t *__restrict__ img, int64_t slots) {
+  const int64_t i = static_cast<int64_t>(blockIdx.x) * 256 + threadIdx.x;
+  if (i >= slots) return;
+  const int64_t nsteps = (rows + 31) / 32;
+  const int64_t blk = i / 64, lane = i % 64;
+  const int64_t t = blk / nsteps, s = blk - t * nsteps;
+  const int64_t c = t * 16 + (lane & 15);
+  const int64_t r0 = s * 32 + 8 * (lane >> 4);
+  uint16_t v[8];
+#pragma unroll
+  for (int e = 0; e < 8; ++e) v[e] = (c < cols && r0 + e < rows) ? x[(r0 + e) * ld + c] : uint16_t(0);
+  *reinterpret_cast<uint4 *>(img + i * 8) =
+      make_uint4(v[0] | (uint32_t(v[1]) << 16), v[2] | (uint32_t(v[3]) << 16),
+                 v[4] | (uint32_t(v[5]) << 16), v[6] | (uint32_t(v[7]) << 16));
+}
+
+}  // namespace mrec
+
+using namespace mrec;
+
+extern "C" {
+
+int64_t mrec_kfrag_elems(int64_t rows, int64_t cols) { return kfrag_elems(rows, cols); }
+
+mrec_status mrec_kfrag_pack(const void *x, int64_t rows, int64_t cols, int64_t ld, void *img,
+                            mrec_stream stream) {
+  MREC_CHECK_ARG(x && img, "NULL pointer");
+  MREC_CHECK_ARG(rows >= 0 && cols >= 0 && ld >= cols, "bad shape");
+  const int64_t slots = kfrag_elems(rows, cols) / 8;
+  if (slots == 0) return MREC_OK;
+  kfrag_pack_kernel<<<dim3(static_cast<unsigned>((slots + 255) / 256)), 256, 0,
+                      static_cast<hipStream_t>(stream)>>>(static_cast<const uint16_t *>(x), rows, cols,
+                                                          ld, static_cast<uint16_t *>(img), slots);
+  return launch_status("mrec_kfrag_pack");
+}
+
+mrec_status mrec_tower_dw(const mrec_tower_dw_args *p, const mrec_head_finish_job *finish,
+                          mrec_stream stream) {
+  MREC_CHECK_ARG(p != nullptr, "NULL args");
+  const mrec_tower_dw_args &s = *p;
+  MREC_CHECK_ARG(s.n_layers >= 1 && s.n_layers <= DW_MAXL, "n_layers must be in [1, 4]");
+  MREC_CHECK_ARG(s.batch >= 0, "negative batch");
+  MREC_CHECK_ARG(s.splits >= 1 && s.splits <= 64, "splits out of [1, 64]");
+  {  // the split count the REDUCE jobs use (mrec_gemm_workspace_size(.., K = batch, splits))
+    const int64_t k = ((s.batch + s.splits - 1) / s.splits + 63) / 64 * 64;
+    const int64_t eff = s.batch > 0 ? (s.batch + std::max<int64_t>(k, 64) - 1) / std::max<int64_t>(k, 64) : 1;
+    MREC_CHECK_ARG(eff == s.splits, "splits must be an effective split-K count for this batch "
+                                    "(ceil(B / round64(ceil(B / splits))) == splits)");
+  }
+  static const int lds_env = [] {  // MREC_TDW_LDS=1: the LDS-shared 128 x 128 kernel (A/B)
+    const char *e = getenv("MREC_TDW_LDS");
+    return (e && e[0] == '1') ? 1 : 0;
+  }();
+  DwArgs a{};
+  a.L = s.n_layers;
+  a.nsteps = static_cast<int>((s.batch + 31) / 32);
+  a.splits = s.splits;
+  a.steps_per_split = (a.nsteps + s.splits - 1) / s.splits;
+  if (finish) {
+    const mrec_head_finish_job &f = *finish;
+    mrec_status st = build_head_finish(f.part, f.ldp, f.batch, f.H, f.ns, f.g, f.update, f.lr,
+                                       f.w, f.bias, f.ws, f.b2, f.dw_out, f.db_out, f.dws_out,
+                                       f.db2_out, &a.fin);
+    if (st != MREC_OK) return st;
+    a.fin_blocks = (f.H + 1 + f.ns + 7) / 8;
+  }
+  int blocks = 0;
+  for (int l = 0; l < a.L; ++l) {
+    const int no = s.n_out[l], ni = s.n_in[l];
+    MREC_CHECK_ARG(no >= 1 && ni >= 1, "n_out / n_in must be >= 1");
+    MREC_CHECK_ARG(s.dy_img[l] && s.x_img[l] && s.ws[l], "NULL image / workspace");
+    MREC_CHECK_ARG(s.ldws[l] >= ni + 1, "ldws < n_in + 1");
+    MREC_CHECK_ARG(kfrag_elems(s.batch, no) * 2 < DW_OOB && kfrag_elems(s.batch, ni) * 2 < DW_OOB,
+                   "k-fragment image exceeds 1 GiB");
+    DwLayer &y = a.lay[l];
+    y.dy = static_cast<const uint16_t *>(s.dy_img[l]);
+    y.x = static_cast<const uint16_t *>(s.x_img[l]);
+    y.ws = s.ws[l];
+    y.ldws = s.ldws[l];
+    y.n_out = no;
+    y.n_in = ni;
+    y.dy_bytes = static_cast<int>(kfrag_elems(s.batch, no) * 2);
+    y.x_bytes = static_cast<int>(kfrag_elems(s.batch, ni) * 2);
+    MREC_CHECK_ARG(s.ldws[l] % 4 == 0 && reinterpret_cast<uintptr_t>(s.ws[l]) % 16 == 0,
+                   "ws rows must be 16-B aligned (ldws % 4 == 0)");
+    const int edge = lds_env ? DW_BLK : 64;  // workgroup block edge of the chosen kernel
+    y.nbn = (no + edge - 1) / edge;
+    y.nbk = (ni + 1 + edge - 1) / edge;
+    y.start = blocks;
+    blocks += y.nbn * y.nbk * s.splits;
+  }
+  const int grid = a.fin_blocks + blocks;
+  if (grid == 0) return MREC_OK;
+  if (lds_env)
+    tower_dw_lds_kernel<DW_PF><<<dim3(static_cast<unsigned>(grid)), DW_THREADS, 0,
+                                 static_cast<hipStream_t>(stream)>>>(a);
+  else
+    tower_dw_kernel<DW_PF><<<dim3(static_cast<unsigned>(grid)), 64, 0,
+                             static_cast<hipStream_t>(stream)>>>(a);
+  return launch_status("mrec_tower_dw");
+}
+
+}  // extern "C"

@@ -978,11 +978,32 @@ def tower_supported(x0: torch.Tensor, mlp, head: torch.nn.Linear, xs=None) -> bo
             and x0.data_ptr() % 16 == 0)
 
 
-def _split_tower(tiles_total: int, K: int) -> int:
-    """K slices of the tower's weight-gradient GEMMs, which share one launch: about
-    two residency waves of 256-thread workgroups, slices of >= 256 rows."""
+def _eff_split(K: int, s: int) -> int:
+    """mrec_gemm's split-K count for K and a requested s (plan_split in gemm.hip)."""
+    k = max(((K + s - 1) // s + 63) // 64 * 64, 64)
+    return (K + k - 1) // k if K > 0 else 1
+
+
+def _tdw_splits(B: int) -> int:
+    """K slices of mrec_tower_dw (0: not used).  4 at B = 4096: about 2.3 one-wave
+    workgroups per CU over the 147 64 x 64 tiles of the C2 tower, partial slabs of
+    8.3 MB (8 slices ran no faster and double the slabs the reduction reads)."""
+    if os.environ.get("MREC_TOWER_DW", "1") == "0" or B < 256:
+        return 0
+    for s in (4, 2):
+        if _eff_split(B, s) == s:
+            return s
+    return 0
+
+
+def _split_tower(widths, K: int) -> int:
+    """K slices of the tower's weight-gradient GEMMs (generic mrec_gemm_multi path,
+    dW_l [N_l, K_l + 1] over the batch), which share one launch: about two residency
+    waves of 256-thread workgroups (3 per CU), slices of >= 256 rows."""
+    tiles = sum(((widths[l + 1] + 63) // 64) * ((widths[l] + 1 + 63) // 64)
+                for l in range(len(widths) - 1))
     s = 1
-    while tiles_total * (s + 1) <= 640 and K // (s + 1) >= 256 and s < 64:
+    while tiles * (s + 1) <= 640 and K // (s + 1) >= 256 and s < 64:
         s += 1
     return s
 
@@ -1003,8 +1024,19 @@ class _TowerBCEFn(torch.autograd.Function):
         dev = x0.device
         widths = [Ws[0].shape[1]] + [W.shape[0] for W in Ws]
         imgs = [tower_images(W) for W in Ws]
-        hs = [_alloc(B, widths[l + 1], _BF16, dev) for l in range(L - 1)]
-        dhs = [_alloc(B, widths[l + 1], _BF16, dev) for l in range(L)]
+        # the weight gradients' operands: k-fragment images for mrec_tower_dw (the
+        # tower writes them, x0's too), else row-major for the generic GEMM
+        tdw = _tdw_splits(B) if any(ctx.needs_input_grad[5:5 + 2 * L]) else 0
+        if tdw:
+            kf = lambda n: torch.empty(int(_mrec.lib().mrec_kfrag_elems(B, n)), dtype=_BF16,  # noqa: E731
+                                       device=dev)
+            hs = [kf(widths[l + 1]) for l in range(L - 1)]
+            dhs = [kf(widths[l + 1]) for l in range(L)]
+            x0_img = kf(widths[0])
+        else:
+            hs = [_alloc(B, widths[l + 1], _BF16, dev) for l in range(L - 1)]
+            dhs = [_alloc(B, widths[l + 1], _BF16, dev) for l in range(L)]
+            x0_img = None
         dx0 = None
         if ctx.needs_input_grad[0]:  # x0's shape (it may carry zero pad columns past K0)
             Kx = x0.shape[1]
@@ -1038,6 +1070,7 @@ class _TowerBCEFn(torch.autograd.Function):
             a.dh_out[l], a.ld_dh[l] = dhs[l].data_ptr(), dhs[l].stride(0)
             if l < L - 1:
                 a.h_out[l], a.ld_h[l] = hs[l].data_ptr(), hs[l].stride(0)
+        a.kfrag, a.x0_img = int(bool(tdw)), _mrec.ptr(x0_img)
         a.head_w, a.head_b, a.base = hw.data_ptr(), _mrec.ptr(hb), _mrec.ptr(base_c)
         a.xs, a.ld_xs, a.ns = _mrec.ptr(xs), xs.stride(0) if xs is not None else 0, ns
         a.ws, a.b2, a.y = _mrec.ptr(wsd), _mrec.ptr(b2d), yc.data_ptr()
@@ -1046,8 +1079,9 @@ class _TowerBCEFn(torch.autograd.Function):
         a.part, a.ldp = part.data_ptr(), ldp
         a.loss_part, a.ticket, a.loss = loss_part.data_ptr(), _ticket(dev).data_ptr(), loss.data_ptr()
         _mrec.call("mrec_tower_fwd_bwd", ctypes.byref(a), _mrec.stream_handle())
-        ctx.save_for_backward(x0, dz, part, dx0, *hs, *dhs)
+        ctx.save_for_backward(x0 if x0_img is None else x0_img, dz, part, dx0, *hs, *dhs)
         ctx.L, ctx.B, ctx.H, ctx.ns, ctx.widths = L, B, H, ns, widths
+        ctx.tdw = tdw
         ctx.Ws, ctx.bs, ctx.imgs = Ws, bs, imgs
         ctx.head = (head_w, head_b, ws, b2)
         ctx.has_base = base is not None
@@ -1063,13 +1097,15 @@ class _TowerBCEFn(torch.autograd.Function):
         dev = part.device
         g = gloss.detach().float().reshape(1).contiguous()
         one = g.data_ptr() == grad_one(dev).data_ptr()
+        tdw = ctx.tdw
         if not one:  # a scaled loss: every stashed gradient scales with it
             dz = dz * g
             dx0 = (dx0.float() * g).to(_BF16) if dx0 is not None else None
-            dhs = [_bf16_rows((d.float() * g).to(_BF16)) for d in dhs]
+            dhs = [(d.float() * g).to(_BF16) if tdw else _bf16_rows((d.float() * g).to(_BF16))
+                   for d in dhs]
         widths, Ws, bs = ctx.widths, ctx.Ws, ctx.bs
         head_w, head_b, ws, b2 = ctx.head
-        xin = [x0[:, :widths[0]]] + hs
+        xin = ([x0] if tdw else [x0[:, :widths[0]]]) + hs
         # --- weight gradients of the L layers: one launch ---
         lr = sgd_lr(*Ws, *bs)
         dpg = dp_grads(*Ws, *bs) if lr is None else None
@@ -1077,28 +1113,30 @@ class _TowerBCEFn(torch.autograd.Function):
         dWs, dbs = [None] * L, [None] * L
         calls = []
         if need_w:
-            tiles = sum(((widths[l + 1] + 63) // 64) * ((widths[l] + 1 + 63) // 64) for l in range(L))
-            sk = _split_tower(tiles, B)
+            sk = tdw or _split_tower(widths, B)
             ph = _mrec.GEMM_PARTIAL if sk > 1 else _mrec.GEMM_FULL
+            # with mrec_tower_dw the calls below only carry the REDUCE phase's
+            # arguments (its operands are never read: k-fragment images as stand-ins)
+            opnd = (lambda t: t.view(-1, 8)) if tdw else (lambda t: t)  # noqa: E731
             for l in range(L):
                 N, K = widths[l + 1], widths[l]
                 bias_l = bs[l]
                 if lr is not None:
-                    c = _Call(dhs[l], _mrec.LAYOUT_COL, xin[l], _mrec.LAYOUT_COL, N, K, B, ph,
+                    c = _Call(opnd(dhs[l]), _mrec.LAYOUT_COL, opnd(xin[l]), _mrec.LAYOUT_COL, N, K, B, ph,
                               ones_out=bias_l.detach() if bias_l is not None else None,
                               out=Ws[l].detach(), out_dtype=torch.float32, split_k=sk, sgd_lr=lr,
                               img_row=ctx.imgs[l][0], img_tr=ctx.imgs[l][1],
                               img_kind=_mrec.IMG_TOWER)
                     images_updated(Ws[l], "tower")
                 elif dpg is not None:
-                    c = _Call(dhs[l], _mrec.LAYOUT_COL, xin[l], _mrec.LAYOUT_COL, N, K, B, ph,
+                    c = _Call(opnd(dhs[l]), _mrec.LAYOUT_COL, opnd(xin[l]), _mrec.LAYOUT_COL, N, K, B, ph,
                               ones_out=dpg[L + l], out=dpg[l], out_dtype=torch.float32,
                               split_k=sk)
                 else:
                     dWs[l] = torch.empty(N, K, dtype=torch.float32, device=dev)
                     dbs[l] = (torch.empty(N, dtype=torch.float32, device=dev)
                               if bias_l is not None else None)
-                    c = _Call(dhs[l], _mrec.LAYOUT_COL, xin[l], _mrec.LAYOUT_COL, N, K, B, ph,
+                    c = _Call(opnd(dhs[l]), _mrec.LAYOUT_COL, opnd(xin[l]), _mrec.LAYOUT_COL, N, K, B, ph,
                               ones_out=dbs[l], out=dWs[l], out_dtype=torch.float32, split_k=sk)
                 calls.append(c)
         # --- the head's parameters (w, b, ws, b2): fixed-order partial sums ---
@@ -1121,7 +1159,14 @@ class _TowerBCEFn(torch.autograd.Function):
             _mrec.call("mrec_ctr_head_finish", part.data_ptr(), part.stride(0), B, ctx.H, ctx.ns,
                        g.data_ptr(), 0, 0.0, None, None, None, None, dW_h.data_ptr(),
                        _mrec.ptr(db_h), _mrec.ptr(dws), _mrec.ptr(db2), _mrec.stream_handle())
-        if calls:
+        if calls and tdw:
+            _tower_dw(calls, dhs, xin, widths, B, tdw)
+            if lr is None and dpg is None:
+                _run([c.with_phase(_mrec.GEMM_REDUCE) for c in calls])
+            else:
+                for c in calls:
+                    _defer(c)
+        elif calls:
             launch_multi(calls)
             if calls[0].args[8] > 1:  # split-K partial slabs: now the reductions
                 if lr is None and dpg is None:
@@ -1135,6 +1180,31 @@ class _TowerBCEFn(torch.autograd.Function):
             _flush_finish()
         return (dx0, dz if ctx.has_base else None, None, None, None, *dWs, *dbs,
                 dW_h, db_h, dws, db2)
+
+
+def _tower_dw(calls, dhs, xin, widths, B: int, splits: int):
+    """The tower's weight-gradient partial slabs by mrec_tower_dw from the
+    k-fragment images (+ the deferred CTR head finish in the same launch); the
+    split-K REDUCE of each call (fused SGD / flat DP buffer / returned gradient)
+    follows as usual.  Pending reductions that write what this reads run first."""
+    global _PENDING
+    reads = {t.data_ptr() for t in list(dhs) + list(xin)}
+    if any(p.writes & reads for p in _PENDING):
+        _run(_PENDING)
+        _PENDING = []
+    a = _mrec.TowerDwArgs()
+    a.n_layers, a.batch, a.splits = len(calls), B, splits
+    for l, c in enumerate(calls):
+        a.n_out[l], a.n_in[l] = widths[l + 1], widths[l]
+        a.dy_img[l], a.x_img[l] = dhs[l].data_ptr(), xin[l].data_ptr()
+        a.ws[l], a.ldws[l] = c.ws.data_ptr(), (widths[l] + 1 + 7) // 8 * 8
+    fin = _FINISH.pop(0) if _FINISH else None
+    _mrec.call("mrec_tower_dw", ctypes.byref(a), ctypes.byref(fin.struct) if fin else None,
+               _mrec.stream_handle())
+    pend = _PENDING
+    _PENDING = []
+    for i in range(0, len(pend), 4):
+        _run(pend[i:i + 4])
 
 
 def tower_bce(x0: torch.Tensor, mlp, head: torch.nn.Linear, base: Optional[torch.Tensor],

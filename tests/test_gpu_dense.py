@@ -70,6 +70,65 @@ def test_gemm_weight_grad_col_col_ones_column(gpu, split_k):
     assert ok, worst
 
 
+def _kfrag_np(x):
+    """numpy restatement of the k-fragment image (tower_common.h kfrag_idx)."""
+    rows, cols = x.shape
+    ns, nt = (rows + 31) // 32, (cols + 15) // 16
+    img = np.zeros(nt * ns * 512, dtype=x.dtype)
+    b, c = np.meshgrid(np.arange(rows), np.arange(cols), indexing="ij")
+    idx = (((c >> 4) * ns + (b >> 5)) * 64 + (c & 15) + 16 * ((b & 31) >> 3)) * 8 + (b & 7)
+    img[idx.reshape(-1)] = x.reshape(-1)
+    return img
+
+
+@pytest.mark.parametrize("case", ["tower", "ragged"])
+def test_tower_dw_kfrag_partials_reduce_to_weight_grads(gpu, case):
+    """mrec_tower_dw on k-fragment images (mrec_kfrag_pack, checked bitwise against
+    the numpy layout) writes split-K slabs that the generic REDUCE job sums into
+    dW = dY^T X and db = sum_b dY, as mrec_gemm would."""
+    import ctypes
+    from pytorchrec_amd import dense as D, _mrec
+    lib = _mrec.lib()
+    if case == "tower":
+        B, shapes, splits = 4096, [(400, 429), (400, 400), (400, 400)], 5
+    else:
+        B, shapes, splits = 333, [(77, 50), (200, 129)], 2
+    g = torch.Generator().manual_seed(23)
+    a = _mrec.TowerDwArgs()
+    a.n_layers, a.batch, a.splits = len(shapes), B, splits
+    keep, checks = [], []
+    for l, (no, ni) in enumerate(shapes):
+        dy = D._bf16_rows(torch.randn(B, no, generator=g).to(torch.bfloat16).to(gpu))
+        x = D._bf16_rows(torch.randn(B, ni, generator=g).to(torch.bfloat16).to(gpu))
+        imgs = []
+        for t, n in ((dy, no), (x, ni)):
+            im = torch.empty(int(lib.mrec_kfrag_elems(B, n)), dtype=torch.bfloat16, device=gpu)
+            _mrec.call("mrec_kfrag_pack", t.data_ptr(), B, n, t.stride(0), im.data_ptr(),
+                       _mrec.stream_handle())
+            imgs.append(im)
+        if l == 0:
+            want = _kfrag_np(dy[:, :no].cpu().view(torch.int16).numpy())
+            assert np.array_equal(imgs[0].cpu().view(torch.int16).numpy(), want)
+        db = torch.empty(no, dtype=torch.float32, device=gpu)
+        call = D._Call(dy, _mrec.LAYOUT_COL, x, _mrec.LAYOUT_COL, no, ni, B, _mrec.GEMM_REDUCE,
+                       ones_out=db, out_dtype=torch.float32, split_k=splits)
+        a.n_out[l], a.n_in[l] = no, ni
+        a.dy_img[l], a.x_img[l] = imgs[0].data_ptr(), imgs[1].data_ptr()
+        a.ws[l], a.ldws[l] = call.ws.data_ptr(), (ni + 1 + 7) // 8 * 8
+        keep += [dy, x, imgs, call]
+        dz = _bf(dy)
+        checks.append((call, db, dz.T @ _bf(x), dz.sum(0), dz.abs().T @ _bf(x).abs(), dz.abs().sum(0)))
+    _mrec.call("mrec_tower_dw", ctypes.byref(a), None, _mrec.stream_handle())
+    D._run([c[0] for c in checks])
+    torch.cuda.synchronize()
+    for c, db, ww, wb, mw, mb in checks:
+        ni = ww.shape[1]
+        ok, worst = _close(c.out[:, :ni], ww, mw, out_bf16=False)
+        assert ok, worst
+        ok, worst = _close(db, wb, mb, out_bf16=False)
+        assert ok, worst
+
+
 @pytest.mark.parametrize("masked", [False, True])
 def test_gemm_input_grad_row_col_with_zero_pad(gpu, masked):
     """dx = dZ W with W fp32 [N, K] read as a COL operand (== W^T read as ROW);

@@ -107,8 +107,42 @@ def main():
     for sk in (1, 2, 4, 8):
         cases[f"dw/s{sk}"] = (lambda sk=sk: D.gemm(dy, _mrec.LAYOUT_COL, x, _mrec.LAYOUT_COL, N, K, M,
                                                    ones_out=db, out=dW, split_k=sk))
+    # the tower's three weight-gradient GEMMs as ONE mrec_gemm_multi launch (PARTIAL
+    # phase, as in the training step; split from dense._split_tower)
+    widths = [429, 400, 400, 400]
+    sk3 = D._split_tower(widths, M)
+    xs3 = [x] + [D._alloc(M, 400, torch.bfloat16, dev).normal_() for _ in range(2)]
+    dys3 = [D._alloc(M, 400, torch.bfloat16, dev).normal_() for _ in range(3)]
+    calls3 = [D._Call(dys3[l], _mrec.LAYOUT_COL, xs3[l][:, :widths[l]], _mrec.LAYOUT_COL, 400,
+                      widths[l], M, _mrec.GEMM_PARTIAL if sk3 > 1 else _mrec.GEMM_FULL,
+                      ones_out=torch.empty(400, device=dev), out_dtype=torch.float32, split_k=sk3)
+              for l in range(3)]
+    print(f"dw3: split_k {sk3}")
+    cases["dw3"] = lambda: D._run(calls3)
+    # the same three weight gradients by mrec_tower_dw on k-fragment images
+    import ctypes
+    lib = _mrec.lib()
+    for ksplit in (4, 5, 8):
+        ta = _mrec.TowerDwArgs()
+        ta.n_layers, ta.batch, ta.splits = 3, M, ksplit
+        keep = []
+        for l in range(3):
+            ims = []
+            for t, n in ((dys3[l], 400), (xs3[l], widths[l])):
+                im = torch.zeros(int(lib.mrec_kfrag_elems(M, n)), dtype=torch.bfloat16, device=dev)
+                _mrec.call("mrec_kfrag_pack", t.data_ptr(), M, n, t.stride(0), im.data_ptr(),
+                           _mrec.stream_handle())
+                ims.append(im)
+            wsb = int(lib.mrec_gemm_workspace_size(400, widths[l], M, ksplit))
+            ws = torch.empty(wsb // 4, dtype=torch.float32, device=dev)
+            keep += ims + [ws]
+            ta.n_out[l], ta.n_in[l] = 400, widths[l]
+            ta.dy_img[l], ta.x_img[l] = ims[0].data_ptr(), ims[1].data_ptr()
+            ta.ws[l], ta.ldws[l] = ws.data_ptr(), (widths[l] + 1 + 7) // 8 * 8
+        cases[f"tdw/s{ksplit}"] = (lambda ta=ta, keep=keep: _mrec.call(
+            "mrec_tower_dw", ctypes.byref(ta), None, _mrec.stream_handle()))
     for name, fn in cases.items():
-        if a.only and name != a.only:
+        if a.only and not name.startswith(a.only):
             continue
         t = timed(fn, a.reps)
         line = f"{name:5s} mrec {t:8.2f} us  {flop / t / 1e6:8.1f} TFLOP/s"

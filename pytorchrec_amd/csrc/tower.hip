@@ -274,27 +274,50 @@ __device__ __forceinline__ void tower_store_kfrag(const char *blk, int s_blk, in
   if (!img || store_mode == 2) return;
   const int ctiles = tw_ceil(width, 16);
   const int st = static_cast<int>(row0 >> 5), h = static_cast<int>((row0 >> 4) & 1);
-  const int per = (h == 0 && row0 + TW_ROWS >= B) ? 64 : 32;
   const int bytes = static_cast<int>(kfrag_elems(B, width) * 2);
   const __amdgpu_buffer_rsrc_t rsrc = __builtin_amdgcn_make_buffer_rsrc(img, 0, bytes, 0x00020000);
-  for (int idx = threadIdx.x; idx < ctiles * per; idx += TW_THREADS) {
-    const int t = idx / per, j = idx - t * per;
-    const int gl = j >> 4, c = t * 16 + (j & 15);
-    uint32_t w[4] = {0u, 0u, 0u, 0u};
-    if (gl < 2 && c < width) {
-#pragma unroll
-      for (int e = 0; e < 8; ++e) {
-        const int r = 8 * gl + e;
-        const uint32_t v = row0 + r < B ? *reinterpret_cast<const uint16_t *>(blk + r * s_blk + c * 2) : 0u;
-        w[e >> 1] |= v << (16 * (e & 1));
-      }
-    }
-    const int off = ((t * nsteps + st) * 64 + (c & 15) + 16 * (2 * h + gl)) * 16;
-    const u32x4 v = u32x4{w[0], w[1], w[2], w[3]};
+  auto put = [&](u32x4 v, int off) {  // store_mode 1: write-through (see tower_store)
     if (store_mode == 1)
       __builtin_amdgcn_raw_buffer_store_b128(v, rsrc, off, 0, 16);
     else
       __builtin_amdgcn_raw_buffer_store_b128(v, rsrc, off, 0, 0);
+  };
+  // 16 lanes per (tile t, 8-row group gl): two ds_read_b64_tr_b16 give lane i the 8
+  // rows of column 16 t + i (lane i addresses row 8 gl + i / 4 (+ 4), columns
+  // 16 t + 4 (i % 4) .. + 4; rows 32 B apart mod 256: conflict free).  Every lane
+  // of a wave runs the reads (EXEC all ones), idle ones on tile 0.
+  const int n = ctiles * 32;
+  const int i16 = threadIdx.x & 15;
+  for (int base = 0; base < n; base += TW_THREADS) {
+    const int idx = base + static_cast<int>(threadIdx.x);
+    const bool on = idx < n;
+    const int t = on ? idx >> 5 : 0, gl = (idx >> 4) & 1;
+    const char *q = blk + (8 * gl + (i16 >> 2)) * s_blk + (t * 16 + 4 * (i16 & 3)) * 2;
+    typedef short v4s_t __attribute__((ext_vector_type(4)));
+    typedef __attribute__((address_space(3))) v4s_t lds_v4s_t;
+    const v4s_t lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4s_t *)(q));
+    const v4s_t hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4s_t *)(q + 4 * s_blk));
+    if (!on) continue;
+    uint32_t w[4] = {static_cast<uint16_t>(lo[0]) | (uint32_t(static_cast<uint16_t>(lo[1])) << 16),
+                     static_cast<uint16_t>(lo[2]) | (uint32_t(static_cast<uint16_t>(lo[3])) << 16),
+                     static_cast<uint16_t>(hi[0]) | (uint32_t(static_cast<uint16_t>(hi[1])) << 16),
+                     static_cast<uint16_t>(hi[2]) | (uint32_t(static_cast<uint16_t>(hi[3])) << 16)};
+    const int64_t rlim = B - row0 - 8 * gl;  // rows of this group inside the batch
+    if (rlim < 8) {
+#pragma unroll
+      for (int e = 0; e < 8; ++e)
+        if (e >= rlim) w[e >> 1] &= (e & 1) ? 0x0000ffffu : 0xffff0000u;
+    }
+    const int off = ((t * nsteps + st) * 64 + i16 + 16 * (2 * h + gl)) * 16;
+    put(u32x4{w[0], w[1], w[2], w[3]}, off);
+  }
+  // the last workgroup zeroes the step's other half when no workgroup owns it
+  if (h == 0 && row0 + TW_ROWS >= B) {
+    for (int idx = threadIdx.x; idx < n; idx += TW_THREADS) {
+      const int t = idx >> 5, j = idx & 31;
+      const int off = ((t * nsteps + st) * 64 + 32 + j) * 16;
+      put(u32x4{0u, 0u, 0u, 0u}, off);
+    }
   }
 }
 

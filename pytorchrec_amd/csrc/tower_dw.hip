@@ -13,11 +13,15 @@
 // steps in flight, no LDS, no barrier) -- the fused tower's weight-stream pattern,
 // which runs at the CU's L2 read rate.
 //
-// Geometry: a 256-thread workgroup owns a 128 x 128 output block (4 waves in 2 x 2,
-// each 64 x 64 = 4 x 4 MFMA tiles; waves of a row / column load the same A / B
-// blocks back to back, the second usually from L1) for one K slice; the bias
+// Geometry: one wave per workgroup owns a 64 x 64 output tile (4 x 4 MFMA tiles)
+// for one K slice (C2: 147 tiles x 4 slices = 588 waves, ~2.3 per CU); the bias
 // column's fragments are synthesised (ones).  Steps past the slice load from an
-// out-of-range offset (zeros) so the pipeline never branches.
+// out-of-range offset (zeros) so the pipeline never branches.  Measured (bench_gemm
+// tdw, C2 tower): 15.7 us, of which ~6 us is launch + first-fragment latency +
+// slab stores (a loop-free build) and the loop streams ~150 MB of fragments at
+// ~65 GB/s per CU (the L2 read rate); a 256-thread variant sharing each step's 16
+// fragments through LDS (half the bytes) ran 17.6-20.4 us: its per-step barrier
+// serialised the waves.  Slices: 4 (8 ran equal, with twice the partial slabs).
 #include <algorithm>
 #include <cstdlib>
 
@@ -30,10 +34,9 @@ namespace mrec {
 #ifndef MREC_TDW_EXP
 #define MREC_TDW_EXP 0
 #endif
-constexpr int DW_THREADS = 256;
 constexpr int DW_PF = 4;       // k steps of fragments in flight per wave
 constexpr int DW_MAXL = 4;
-constexpr int DW_BLK = 128;    // output block edge (8 MFMA tiles)
+constexpr int DW_TILE = 64;    // output tile edge of one wave (4 MFMA tiles)
 constexpr int DW_OOB = 1 << 30;  // a voffset past every image: the load returns zeros
 
 typedef short bf16x8 __attribute__((ext_vector_type(8)));
@@ -180,123 +183,6 @@ __global__ __launch_bounds__(64) void tower_dw_kernel(DwArgs a) {
   }
 }
 
-// The same block with the fragments shared through LDS: the 16 distinct 1 KiB
-// fragments of a k step (8 of dY^T, 8 of X) are loaded once per workgroup -- 4 per
-// wave, PF steps ahead in VGPRs -- stored to a 2-slot LDS ring, and every wave
-// reads the 8 it multiplies (ds_read_b128, lane-linear: conflict free).  Without
-// it each wave fetched its own 8 fragments from L2 (twice the workgroup's bytes:
-// the second wave's loads of a shared fragment did not hit in L1), and the CU's
-// L2 read rate bounded the kernel.  One barrier per k step.
-template <int PF>
-__global__ __launch_bounds__(DW_THREADS, 1) void tower_dw_lds_kernel(DwArgs a) {
-  __shared__ float red[4][9];
-  __shared__ __attribute__((aligned(16))) bf16x8 ring[2][16][64];
-  if (static_cast<int>(blockIdx.x) < a.fin_blocks) {  // uniform
-    if (static_cast<int>(blockIdx.x) < head_finish_blocks(a.fin.H, a.fin.ns))
-      ctr_head_finish_body(a.fin, blockIdx.x, red);
-    return;
-  }
-  const int b = blockIdx.x - a.fin_blocks;
-  int l = 0;
-  while (l + 1 < a.L && b >= a.lay[l + 1].start) ++l;  // uniform
-  const DwLayer &y = a.lay[l];
-  const int local = b - y.start;
-  const int z = local % a.splits, blk = local / a.splits;
-  if (blk >= y.nbn * y.nbk) return;
-  const int bn = blk / y.nbk, bk = blk - bn * y.nbk;
-  const int lane = threadIdx.x & 63;
-  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const int wm = wave >> 1, wn = wave & 1;
-  const int s_beg = z * a.steps_per_split;
-  const int s_n = max(0, min(a.nsteps, s_beg + a.steps_per_split) - s_beg);
-
-  const __amdgpu_buffer_rsrc_t ra =
-      __builtin_amdgcn_make_buffer_rsrc(const_cast<uint16_t *>(y.dy), 0, y.dy_bytes, 0x00020000);
-  const __amdgpu_buffer_rsrc_t rb =
-      __builtin_amdgcn_make_buffer_rsrc(const_cast<uint16_t *>(y.x), 0, y.x_bytes, 0x00020000);
-  // this wave loads fragments f = 4 wave + q of the workgroup's 16 (0-7: dY^T tiles
-  // 8 bn + f, 8-15: X tiles 8 bk + f - 8); waves 0-1 load A, 2-3 load B
-  const bool loads_a = wave < 2;
-  const int atiles = (y.n_out + 15) / 16, btiles = (y.n_in + 15) / 16;
-  int vo[4];
-#pragma unroll
-  for (int q = 0; q < 4; ++q) {
-    const int f = wave * 4 + q;
-    const int t = loads_a ? bn * 8 + f : bk * 8 + f - 8;
-    const int nt = loads_a ? atiles : btiles;
-    vo[q] = t < nt ? (t * a.nsteps + s_beg) * 1024 + lane * 16 : DW_OOB;
-  }
-  const int ones_tile = y.n_in / 16;
-  const bool ones_lane = (lane & 15) == (y.n_in & 15);
-  const bf16x8 ones = bf16x8{0x3f80, 0x3f80, 0x3f80, 0x3f80, 0x3f80, 0x3f80, 0x3f80, 0x3f80};
-  bool ones_j[4];
-#pragma unroll
-  for (int j = 0; j < 4; ++j) ones_j[j] = bk * 8 + wn * 4 + j == ones_tile && ones_lane;
-
-  f32x4 acc[4][4];
-#pragma unroll
-  for (int i = 0; i < 4; ++i)
-#pragma unroll
-    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-
-  bf16x8 fr[PF][4];
-  auto load = [&](int p, int s) {
-    const int so = s < s_n ? s * 1024 : DW_OOB;
-#pragma unroll
-    for (int q = 0; q < 4; ++q)
-      fr[p][q] = __builtin_bit_cast(
-          bf16x8, loads_a ? __builtin_amdgcn_raw_buffer_load_b128(ra, vo[q] + so, 0, 0)
-                          : __builtin_amdgcn_raw_buffer_load_b128(rb, vo[q] + so, 0, 0));
-  };
-#pragma unroll
-  for (int p = 0; p < PF; ++p) {
-    load(p, p);
-    __builtin_amdgcn_sched_barrier(0);
-  }
-  const int total = (s_n + PF - 1) / PF * PF;
-  for (int base = 0; base < total; base += PF) {
-#pragma unroll
-    for (int p = 0; p < PF; ++p) {
-      const int slot = p & 1;  // PF even: step base + p uses slot (base + p) & 1
-#pragma unroll
-      for (int q = 0; q < 4; ++q) ring[slot][wave * 4 + q][lane] = fr[p][q];
-      __syncthreads();  // slot written by all; the reads of its previous use retired
-      load(p, base + p + PF);
-      bf16x8 fa[4], fb[4];
-#pragma unroll
-      for (int i = 0; i < 4; ++i) fa[i] = ring[slot][wm * 4 + i][lane];
-#pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        const bf16x8 t = ring[slot][8 + wn * 4 + j][lane];
-        fb[j] = ones_j[j] ? ones : t;
-      }
-#pragma unroll
-      for (int i = 0; i < 4; ++i)
-#pragma unroll
-        for (int j = 0; j < 4; ++j)
-          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[i], fb[j], acc[i][j], 0, 0, 0);
-      __builtin_amdgcn_sched_barrier(0);
-    }
-  }
-
-  const int ncols = y.n_in + 1;
-  float *slab = y.ws + static_cast<int64_t>(z) * y.n_out * y.ldws;
-  const int nt0 = bn * 8 + wm * 4, kt0 = bk * 8 + wn * 4;
-#pragma unroll
-  for (int i = 0; i < 4; ++i) {
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      const int n = (kt0 + j) * 16 + (lane & 15);
-      if (n >= ncols) continue;
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int m = (nt0 + i) * 16 + 4 * (lane >> 4) + r;
-        if (m < y.n_out) slab[static_cast<int64_t>(m) * y.ldws + n] = acc[i][j][r];
-      }
-    }
-  }
-}
-
 // row-major bf16 [rows, cols] (row stride ld) -> k-fragment image (pad rows /
 // columns zero); one thread per 16-B lane slot of the image
 __global__ __launch_bounds__(256) void kfrag_pack_kernel(const uint16_t *__restrict__ x, int64_t rows,
@@ -350,10 +236,6 @@ mrec_status mrec_tower_dw(const mrec_tower_dw_args *p, const mrec_head_finish_jo
     MREC_CHECK_ARG(eff == s.splits, "splits must be an effective split-K count for this batch "
                                     "(ceil(B / round64(ceil(B / splits))) == splits)");
   }
-  static const int lds_env = [] {  // MREC_TDW_LDS=1: the LDS-shared 128 x 128 kernel (A/B)
-    const char *e = getenv("MREC_TDW_LDS");
-    return (e && e[0] == '1') ? 1 : 0;
-  }();
   DwArgs a{};
   a.L = s.n_layers;
   a.nsteps = static_cast<int>((s.batch + 31) / 32);
@@ -386,20 +268,15 @@ mrec_status mrec_tower_dw(const mrec_tower_dw_args *p, const mrec_head_finish_jo
     y.x_bytes = static_cast<int>(kfrag_elems(s.batch, ni) * 2);
     MREC_CHECK_ARG(s.ldws[l] % 4 == 0 && reinterpret_cast<uintptr_t>(s.ws[l]) % 16 == 0,
                    "ws rows must be 16-B aligned (ldws % 4 == 0)");
-    const int edge = lds_env ? DW_BLK : 64;  // workgroup block edge of the chosen kernel
-    y.nbn = (no + edge - 1) / edge;
-    y.nbk = (ni + 1 + edge - 1) / edge;
+    y.nbn = (no + DW_TILE - 1) / DW_TILE;
+    y.nbk = (ni + 1 + DW_TILE - 1) / DW_TILE;
     y.start = blocks;
     blocks += y.nbn * y.nbk * s.splits;
   }
   const int grid = a.fin_blocks + blocks;
   if (grid == 0) return MREC_OK;
-  if (lds_env)
-    tower_dw_lds_kernel<DW_PF><<<dim3(static_cast<unsigned>(grid)), DW_THREADS, 0,
-                                 static_cast<hipStream_t>(stream)>>>(a);
-  else
-    tower_dw_kernel<DW_PF><<<dim3(static_cast<unsigned>(grid)), 64, 0,
-                             static_cast<hipStream_t>(stream)>>>(a);
+  tower_dw_kernel<DW_PF><<<dim3(static_cast<unsigned>(grid)), 64, 0,
+                           static_cast<hipStream_t>(stream)>>>(a);
   return launch_status("mrec_tower_dw");
 }
 

@@ -1,0 +1,11 @@
+# tower-path parity tests, the standalone tower timing, the C2 bench and its rocprof stats
+set -o pipefail
+mkdir -p gpurun_out/tw
+timeout -k 10 300 python -u -m pytest tests/test_gpu_dense.py tests/test_gpu_tower.py tests/test_gpu_pins.py -x -q --timeout 120 --timeout-method thread > gpurun_out/tw/tests.txt 2>&1 || { tail -40 gpurun_out/tw/tests.txt; exit 1; }
+tail -2 gpurun_out/tw/tests.txt
+timeout -k 10 120 python -u tools/bench_tower.py > gpurun_out/tw/tower.txt 2>&1 || { tail -20 gpurun_out/tw/tower.txt; exit 1; }
+grep -v amdgpu.ids gpurun_out/tw/tower.txt | head -3
+for i in 1 2; do
+timeout -k 10 200 python -u bench.py --steps 200 --warmup 20 --no-cpu-baseline > gpurun_out/tw/bench$i.json 2> gpurun_out/tw/bench$i.err || { tail -30 gpurun_out/tw/bench$i.err; exit 1; }
+python -c "import json;d=json.load(open('gpurun_out/tw/bench$i.json'));print(d['ms_per_step'], d['value'])"
+done

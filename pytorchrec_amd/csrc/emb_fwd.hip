@@ -82,6 +82,23 @@ struct InteractArgs {
   int32_t *oob;
 };
 
+#ifdef MREC_INTERACT_PROF
+// diagnostics: per-sample wall-clock stamps (100 MHz) of the last launch: start,
+// ids landed, rows landed, x0 / sums issued, logit issued (mrec_interact_prof_read)
+__device__ uint64_t g_interact_prof[8192][5];
+#define IA_STAMP(k, dep)                                                        \
+  do {                                                                          \
+    if (lane == 0 && b < 8192) {                                                \
+      asm volatile("" ::"v"(dep));                                              \
+      g_interact_prof[b][k] = __builtin_amdgcn_s_memrealtime();                 \
+    }                                                                           \
+  } while (0)
+#else
+#define IA_STAMP(k, dep) \
+  do {                   \
+  } while (0)
+#endif
+
 // sample b, by the wave whose lane this is
 template <typename T, int LPR, bool X0_BF16, bool ADAM>
 __device__ __forceinline__ void interact_sample(const BankArgs &bank, const IdsArgs &ids,
@@ -110,6 +127,13 @@ __device__ __forceinline__ void interact_sample(const BankArgs &bank, const IdsA
   const bool w_lane = bank.has_w && e0 == D;
 
   // phase 1: issue every row load of this sample before consuming any
+  IA_STAMP(0, 0);
+#ifdef MREC_INTERACT_PROF
+  {
+    const int64_t id0 = load_id(ids, worker < F ? worker : 0, b);
+    IA_STAMP(1, static_cast<int>(id0));
+  }
+#endif
   uint4 raw[MAXIT];
 #pragma unroll
   for (int it = 0; it < MAXIT; ++it) {
@@ -130,6 +154,7 @@ __device__ __forceinline__ void interact_sample(const BankArgs &bank, const IdsA
     }
   }
 
+  IA_STAMP(2, raw[0].x ^ raw[MAXIT - 1].x);
   // phase 2: per-lane sums over this lane's fields + deep-input write
   float s[EPL], q[EPL];
 #pragma unroll
@@ -196,6 +221,7 @@ __device__ __forceinline__ void interact_sample(const BankArgs &bank, const IdsA
       *reinterpret_cast<float4 *>(dst + j) = make_float4(s[j], s[j + 1], s[j + 2], s[j + 3]);
   }
 
+  IA_STAMP(3, __float_as_int(fm));
   // dense features: first-order dot + copy into x0, zero the pad columns
   float ds = 0.f;
   if (dense_w)
@@ -218,6 +244,7 @@ __device__ __forceinline__ void interact_sample(const BankArgs &bank, const IdsA
     if (flags & MREC_INTERACT_FIRST_ORDER) y += wsum;
     logit[b] = y;
   }
+  IA_STAMP(4, __float_as_int(ds));
 }
 
 template <typename T, int LPR, bool X0_BF16, bool ADAM>
@@ -466,3 +493,9 @@ mrec_status mrec_fm2_bwd(const float *v, const float *dy, int64_t batch, int32_t
 }
 
 }  // extern "C"
+
+#ifdef MREC_INTERACT_PROF
+extern "C" void mrec_interact_prof_read(uint64_t *out, int n) {
+  (void)hipMemcpyFromSymbol(out, HIP_SYMBOL(mrec::g_interact_prof), sizeof(uint64_t) * 5 * n);
+}
+#endif

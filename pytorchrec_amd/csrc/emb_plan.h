@@ -63,7 +63,9 @@ __device__ uint64_t g_plan_prof[16];
 // table's ids (L2 hits after the first), keeps the ones of its bucket and groups
 // them in an LDS hash table.  Buckets partition the rows, so no row's lookups
 // are split over workgroups and no cross-workgroup merge is needed; a table's
-// plan runs on 4 CUs instead of 1 (C2: 104 workgroups beside the interaction).
+// plan runs on 8 CUs instead of 1 (C2: 208 workgroups beside the interaction; 8
+// buckets over 4: interaction + apply 21.2 -> 19.4 us, step 0.0937 -> 0.0917 ms,
+// same-box A/B -- the apply's segment blocks are per (table, bucket) too).
 // A workgroup barrier costs ~135 ns at 1024 threads (tools/micro/barrier.hip);
 // the body needs three:
 //   1. insert: each id of the bucket goes into the hash table (linear probing;
@@ -84,7 +86,10 @@ constexpr int kHashMaxKeys = 4096;     // dense batches up to this use the hash 
 constexpr int kHashMaxEntries = 8192;  // padded exchange views (ids.pad_negative) up to this:
                                        // their valid ids are ~1/2 of the entries (cap = 2x share)
 constexpr int kHashSlots = 8192;       // per workgroup: any bucket fits at load factor <= 1/2
-constexpr int kPlanBuckets = 4;        // workgroups per table
+#ifndef MREC_PLAN_BUCKETS_LOG2
+#define MREC_PLAN_BUCKETS_LOG2 3
+#endif
+constexpr int kPlanBuckets = 1 << MREC_PLAN_BUCKETS_LOG2;  // workgroups per table
 constexpr int kShortSeg = 16;          // longer segments: the bucket's long list
 constexpr uint32_t kEmpty = 0xffffffffu;
 
@@ -100,9 +105,8 @@ __host__ __device__ inline bool hash_layout(int64_t batch, bool padded) {
 }
 
 __host__ __device__ inline uint32_t plan_bucket(uint32_t key) {
-  return (key * 0x85ebca77u) >> (32 - 2);  // top 2 bits: kPlanBuckets = 4
+  return (key * 0x85ebca77u) >> (32 - MREC_PLAN_BUCKETS_LOG2);  // the top bits
 }
-static_assert(kPlanBuckets == 4, "plan_bucket takes the top 2 bits");
 
 // hash-layout workspace: F x kPlanBuckets bucket regions, then lut[B][F]
 struct BucketWs {

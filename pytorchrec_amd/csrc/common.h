@@ -70,6 +70,38 @@ mrec_status make_opt_args(const mrec_table_bank *bank, int mode, OptArgs *out);
 // ---------------------------------------------------------------------------
 // device helpers
 // ---------------------------------------------------------------------------
+// ---------------------------------------------------------------------------
+// cross-lane sums without the LDS crossbar: DPP row rotations inside a 16-lane row
+// and the gfx950 permlane swaps across rows / halves (ds_bpermute, which
+// __shfl_xor lowers to, costs an LDS transfer per value: the interaction's 68
+// per wave took ~3 us of an 8 us launch, tools/bench_interact.py)
+// ---------------------------------------------------------------------------
+template <int CTRL>
+__device__ __forceinline__ float dpp_f32(float v) {
+  return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), CTRL, 0xf, 0xf, false));
+}
+__device__ __forceinline__ float swap16_sum(float v) {  // + the paired row (rows 0<->1, 2<->3)
+  const auto r = __builtin_amdgcn_permlane16_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+  return __uint_as_float(r[0]) + __uint_as_float(r[1]);
+}
+__device__ __forceinline__ float swap32_sum(float v) {  // + the other half of the wave
+  const auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+  return __uint_as_float(r[0]) + __uint_as_float(r[1]);
+}
+// sum over the 16 lanes of the wave with this lane's index mod 4 (every lane gets it)
+__device__ __forceinline__ float sum_mod4_lanes(float v) {
+  v += dpp_f32<0x124>(v);  // row_ror:4
+  v += dpp_f32<0x128>(v);  // row_ror:8
+  return swap32_sum(swap16_sum(v));
+}
+// sum over this lane's quad (lanes 4q .. 4q + 3)
+__device__ __forceinline__ float sum_quad(float v) {
+  v += dpp_f32<0xb1>(v);  // quad_perm [1, 0, 3, 2]
+  return v + dpp_f32<0x4e>(v);  // quad_perm [2, 3, 0, 1]
+}
+// sum over all 64 lanes
+__device__ __forceinline__ float sum_wave(float v) { return sum_mod4_lanes(sum_quad(v)); }
+
 __device__ __forceinline__ float bf16_to_f32(uint16_t h) {
   return __uint_as_float(static_cast<uint32_t>(h) << 16);
 }

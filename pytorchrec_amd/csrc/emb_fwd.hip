@@ -194,25 +194,42 @@ __device__ __forceinline__ void interact_sample(const BankArgs &bank, const IdsA
     }
   }
 
-  // reduce over workers (lanes with equal l)
+  // reduce over workers (lanes with equal l): sum_d S_d^2 - sum_{f,d} v_fd^2, so
+  // each lane folds its squares first and the workers reduce EPL + 2 values
+  float qt = 0.f;
 #pragma unroll
-  for (int off = LPR; off < 64; off <<= 1) {
-#pragma unroll
-    for (int j = 0; j < EPL; ++j) {
-      s[j] += __shfl_xor(s[j], off);
-      q[j] += __shfl_xor(q[j], off);
-    }
-    wsum += __shfl_xor(wsum, off);
-  }
+  for (int j = 0; j < EPL; ++j) qt += q[j];
   float fm = 0.f;
-  if (v_lane) {
+  if constexpr (LPR == 4) {  // DPP rows + permlane swaps (common.h), no LDS traffic
 #pragma unroll
-    for (int j = 0; j < EPL; ++j) fm += s[j] * s[j] - q[j];
-  }
+    for (int j = 0; j < EPL; ++j) s[j] = sum_mod4_lanes(s[j]);
+    qt = sum_mod4_lanes(qt);
+    wsum = sum_mod4_lanes(wsum);
+    if (v_lane) {
 #pragma unroll
-  for (int off = 1; off < LPR; off <<= 1) {
-    fm += __shfl_xor(fm, off);
-    wsum += __shfl_xor(wsum, off);
+      for (int j = 0; j < EPL; ++j) fm = fmaf(s[j], s[j], fm);
+      fm -= qt;
+    }
+    fm = sum_quad(fm);
+    wsum = sum_quad(wsum);
+  } else {
+#pragma unroll
+    for (int off = LPR; off < 64; off <<= 1) {
+#pragma unroll
+      for (int j = 0; j < EPL; ++j) s[j] += __shfl_xor(s[j], off);
+      qt += __shfl_xor(qt, off);
+      wsum += __shfl_xor(wsum, off);
+    }
+    if (v_lane) {
+#pragma unroll
+      for (int j = 0; j < EPL; ++j) fm = fmaf(s[j], s[j], fm);
+      fm -= qt;
+    }
+#pragma unroll
+    for (int off = 1; off < LPR; off <<= 1) {
+      fm += __shfl_xor(fm, off);
+      wsum += __shfl_xor(wsum, off);
+    }
   }
   if (fm_sum && worker == 0 && v_lane) {
     float *dst = fm_sum + b * D + e0;
@@ -226,8 +243,7 @@ __device__ __forceinline__ void interact_sample(const BankArgs &bank, const IdsA
   float ds = 0.f;
   if (dense_w)
     for (int j = lane; j < n_dense; j += 64) ds = fmaf(dense[b * dense_ld + j], dense_w[j], ds);
-#pragma unroll
-  for (int off = 1; off < 64; off <<= 1) ds += __shfl_xor(ds, off);
+  ds = sum_wave(ds);
   if (x0v) {
     const int base = F * D;
     for (int c = base + lane; c < x0_cols; c += 64) {

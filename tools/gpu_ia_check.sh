@@ -1,0 +1,10 @@
+set -o pipefail
+mkdir -p gpurun_out/ia
+timeout -k 10 300 python -u -m pytest tests/test_gpu_embedding.py tests/test_gpu_g9.py tests/test_gpu_sharded.py tests/test_gpu_optim.py -x -q --timeout 120 --timeout-method thread > gpurun_out/ia/tests.txt 2>&1 || { tail -30 gpurun_out/ia/tests.txt; exit 1; }
+tail -1 gpurun_out/ia/tests.txt
+timeout -k 10 120 python -u tools/bench_interact.py > gpurun_out/ia/base.txt 2>&1 || { tail -20 gpurun_out/ia/base.txt; exit 1; }
+grep interact gpurun_out/ia/base.txt
+for i in 1 2; do
+timeout -k 10 200 python -u bench.py --steps 200 --warmup 20 --no-cpu-baseline > gpurun_out/ia/bench$i.json 2> gpurun_out/ia/bench$i.err || { tail -30 gpurun_out/ia/bench$i.err; exit 1; }
+python -c "import json;d=json.load(open('gpurun_out/ia/bench$i.json'));print(d['ms_per_step'], d['value'], d['roofline']['avg_us'], d['roofline']['frac'])"
+done

@@ -444,6 +444,7 @@ __global__ __launch_bounds__(TW_THREADS) void tower_kernel(TowerArgs a) {
     }
   }
   __syncthreads();
+  TW_STAMP(5);
   // dh_L = dz * head_w * [h_L > 0] -> gradient block 0
   {
     char *g0 = lds + a.off_g[0];
@@ -464,6 +465,7 @@ __global__ __launch_bounds__(TW_THREADS) void tower_kernel(TowerArgs a) {
                      pack_bf16x2(gv[4], gv[5]), pack_bf16x2(gv[6], gv[7]));
     }
   }
+  TW_STAMP(13);
   // head-parameter partials: [sum_m dz_m h_L[m] | sum dz | sum_m dz_m xs[m]]
   for (int c = tid; c < H + 1 + a.ns; c += TW_THREADS) {
     float sacc = 0.f;
@@ -478,6 +480,7 @@ __global__ __launch_bounds__(TW_THREADS) void tower_kernel(TowerArgs a) {
     }
     f_part[c] = sacc;
   }
+  TW_STAMP(14);
   __syncthreads();
   TW_STAMP(6);
   // now the global stores, behind the backward's first weight stream
@@ -533,7 +536,7 @@ __global__ __launch_bounds__(TW_THREADS) void tower_kernel(TowerArgs a) {
   }
   __syncthreads();
   TW_STAMP(12);
-  if (a.stamps && tid < 13) a.stamps[blockIdx.x * 16 + tid] = s_stamp[tid];
+  if (a.stamps && tid < 16) a.stamps[blockIdx.x * 16 + tid] = s_stamp[tid];
   if (!s_last) return;
   float t = 0.f;
   for (unsigned k = tid; k < gridDim.x; k += TW_THREADS)

@@ -15,6 +15,7 @@ p = argparse.ArgumentParser()
 p.add_argument("--batch", type=int, default=4096)
 p.add_argument("--widths", default="429,400,400,400")
 p.add_argument("--reps", type=int, default=100)
+p.add_argument("--rowmajor", action="store_true", help="row-major operand outputs (kfrag off)")
 args = p.parse_args()
 widths = [int(x) for x in args.widths.split(",")]
 B, L = args.batch, len(widths) - 1
@@ -27,8 +28,16 @@ x0 = torch.zeros(B, D._r8(widths[0]), dtype=torch.bfloat16, device=dev)
 x0[:, :widths[0]] = torch.randn(B, widths[0], generator=g).to(torch.bfloat16).to(dev)
 y = (torch.rand(B, generator=g) < 0.3).float().to(dev)
 imgs = [D.tower_images(W) for W in Ws]
-hs = [D._alloc(B, widths[l + 1], torch.bfloat16, dev) for l in range(L - 1)]
-dhs = [D._alloc(B, widths[l + 1], torch.bfloat16, dev) for l in range(L)]
+kfrag = "--rowmajor" not in sys.argv  # the training step's layout: k-fragment images
+if kfrag:
+    kf = lambda n: torch.empty(int(_mrec.lib().mrec_kfrag_elems(B, n)), dtype=torch.bfloat16,  # noqa: E731
+                               device=dev)
+    hs = [kf(widths[l + 1]) for l in range(L - 1)]
+    dhs = [kf(widths[l + 1]) for l in range(L)]
+    x0_img = kf(widths[0])
+else:
+    hs = [D._alloc(B, widths[l + 1], torch.bfloat16, dev) for l in range(L - 1)]
+    dhs = [D._alloc(B, widths[l + 1], torch.bfloat16, dev) for l in range(L)]
 dx0 = D._alloc(B, widths[0], torch.bfloat16, dev)
 dz = torch.empty(B, device=dev)
 H = widths[-1]
@@ -51,6 +60,8 @@ a.head_w, a.y = hw.data_ptr(), y.data_ptr()
 a.dx0, a.ld_dx0 = dx0.data_ptr(), dx0.stride(0)
 a.dz, a.part, a.ldp = dz.data_ptr(), part.data_ptr(), part.stride(0)
 a.loss_part, a.ticket, a.loss = lp.data_ptr(), D._ticket(dev).data_ptr(), loss.data_ptr()
+if kfrag:
+    a.kfrag, a.x0_img = 1, x0_img.data_ptr()
 
 
 def launch():
@@ -91,9 +102,10 @@ fn(None)
 torch.cuda.synchronize()
 t = st.cpu().double() * 10.0 / 1e3  # 100 MHz ticks -> us
 t0 = t[:, 0].min()
-names = {0: "start", 1: "x0 loaded", 2: "fwd1", 3: "fwd2", 4: "fwd3", 5: "fwd4", 6: "head",
+names = {0: "start", 1: "x0 loaded", 2: "fwd1", 3: "fwd2", 4: "fwd3", 5: "head dot",
+         13: "dh_L (w0)", 14: "parts (w0)", 6: "head",
          7: "bwd_L", 8: "bwd_L-1", 9: "bwd_L-2", 10: "bwd_L-3", 11: "bwd done", 12: "ticket"}
-used = [k for k in range(13) if bool((st[:, k] != 0).all())]
+used = [k for k in (0, 1, 2, 3, 4, 5, 13, 14, 6, 7, 8, 9, 10, 11, 12) if bool((st[:, k] != 0).all())]
 rows = []
 for k in used:
     col = t[:, k] - t0

@@ -207,7 +207,7 @@ __global__ __launch_bounds__(kPlanThreads) void plan_hash_kernel(BankArgs bank, 
                                                                  int64_t B, void *ws,
                                                                  int32_t *__restrict__ oob,
                                                                  uint64_t *__restrict__ d_step) {
-  __shared__ uint32_t smem[2 * kHashSlots + 2];
+  __shared__ __attribute__((aligned(16))) uint32_t smem[2 * kHashSlots + 2];
   plan_hash_body<kPlanThreads, kHashSlots>(bank, ids, B, ws, oob, d_step, blockIdx.x / kPlanBuckets,
                                            blockIdx.x % kPlanBuckets, smem);
 }

@@ -278,7 +278,7 @@ template <typename T, int LPR, bool X0_BF16, bool ADAM>
 __global__ __launch_bounds__(1024) void interact_plan_kernel(BankArgs bank, IdsArgs ids, int64_t B,
                                                              InteractArgs ia, PlanJob plan,
                                                              int plan_blocks) {
-  __shared__ uint32_t smem[2 * kHashSlots + 2];
+  __shared__ __attribute__((aligned(16))) uint32_t smem[2 * kHashSlots + 2];
   if (static_cast<int>(blockIdx.x) < plan_blocks) {  // uniform: (table, bucket) plans
     plan_hash_body<1024, kHashSlots>(plan.bank, plan.ids, plan.B, plan.ws, plan.oob, plan.d_step,
                                      blockIdx.x / kPlanBuckets, blockIdx.x % kPlanBuckets, smem);

@@ -183,9 +183,10 @@ __device__ __forceinline__ void plan_hash_body(const BankArgs &bank, const IdsAr
     const int i = k * THREADS + tid;
     id[k] = i < B ? load_id(ids, f, i) : -1;
   }
-  for (int i = tid; i < SLOTS; i += THREADS) {
-    hkey[i] = kEmpty;
-    hcnt[i] = 0u;
+  static_assert(SLOTS % (4 * THREADS) == 0, "16-B LDS init");
+  for (int i = 4 * tid; i < SLOTS; i += 4 * THREADS) {
+    *reinterpret_cast<uint4 *>(hkey + i) = make_uint4(kEmpty, kEmpty, kEmpty, kEmpty);
+    *reinterpret_cast<uint4 *>(hcnt + i) = make_uint4(0u, 0u, 0u, 0u);
   }
   if (tid == 0) {
     s_tot = 0u;
@@ -250,10 +251,12 @@ __device__ __forceinline__ void plan_hash_body(const BankArgs &bank, const IdsAr
     if (mc == 0) continue;  // uniform
     const uint32_t need = (claim && cnt > 2) ? cnt : 0u;  // perm entries
     uint32_t incl = need;  // inclusive scan of the perm entries claimed
-#pragma unroll
-    for (int off = 1; off < 64; off <<= 1) {
-      const uint32_t v = __shfl_up(incl, off);
-      if (lane >= off) incl += v;
+    if (__ballot(need != 0u) != 0ull) {  // uniform: only rows hit >= 3 times take perm
+#pragma unroll                              // entries (most claims are pairs: no scan)
+      for (int off = 1; off < 64; off <<= 1) {
+        const uint32_t v = __shfl_up(incl, off);
+        if (lane >= off) incl += v;
+      }
     }
     const int last = 63 - __clzll(mc);
     uint32_t base = 0;

@@ -104,15 +104,71 @@ __device__ __forceinline__ void epilogue_elem(const GemmArgs &g, int64_t m, int6
     static_cast<uint16_t *>(g.C)[m * g.ldc + n] = f32_to_bf16_rne(v);
 }
 
+// the fused-SGD update of a 4 x 4 block (rows m0..m0+3, columns n..n+3 < N, m0 % 4
+// == n % 4 == 0) of a weight with tower images: the fp32 master rows as float4,
+// each image as four 8-byte stores -- tower_idx_fwd keeps 4 consecutive k (= n)
+// of a row together, tower_idx_bwd 4 consecutive n (= m) of a column (instead of
+// 32 scattered 2-byte stores)
+__device__ __forceinline__ void update_block4_tower(const GemmArgs &g, int64_t m0, int64_t n,
+                                                    const float4 (&v)[4]) {
+  float w[4][4];
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    float *c = static_cast<float *>(g.C) + (m0 + r) * g.ldc + n;
+    const float4 old = *reinterpret_cast<const float4 *>(c);
+    w[r][0] = fmaf(-g.lr, v[r].x, old.x);
+    w[r][1] = fmaf(-g.lr, v[r].y, old.y);
+    w[r][2] = fmaf(-g.lr, v[r].z, old.z);
+    w[r][3] = fmaf(-g.lr, v[r].w, old.w);
+    *reinterpret_cast<float4 *>(c) = make_float4(w[r][0], w[r][1], w[r][2], w[r][3]);
+    if (g.img_row)
+      *reinterpret_cast<uint2 *>(g.img_row + tower_idx_fwd(m0 + r, n, g.N)) =
+          make_uint2(pack_bf16x2(w[r][0], w[r][1]), pack_bf16x2(w[r][2], w[r][3]));
+  }
+  if (g.img_tr) {
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+      *reinterpret_cast<uint2 *>(g.img_tr + tower_idx_bwd(m0, n + j, g.M)) =
+          make_uint2(pack_bf16x2(w[0][j], w[1][j]), pack_bf16x2(w[2][j], w[3][j]));
+  }
+}
+
 // fixed-order reduction of the split-K partial slabs + epilogue (4 columns / thread)
 __device__ __forceinline__ void splitk_reduce_body(const GemmArgs &g, int64_t bid, int64_t nblk) {
   const int64_t ncols = g.b_ones_col >= 0 ? g.b_ones_col + 1 : g.N;
   const int64_t q = g.ldws / 4;
-  const int64_t total = g.M * q;
   const int64_t slab = g.M * g.ldws;
+  // fused SGD into tower images: 4 x 4 blocks over rows [0, M4), columns < N in
+  // whole fours, the same fixed summation order per element
+#ifdef MREC_NO_BLK4  // diagnostics: the per-element path only
+  const bool blk4 = false;
+#else
+  const bool blk4 = g.update && g.img_kind == kImgTower && (g.ldc % 4) == 0 &&
+                    (reinterpret_cast<uintptr_t>(g.C) & 15) == 0;
+#endif
+  const int64_t M4 = blk4 ? g.M / 4 * 4 : 0;
+  const int64_t N4 = blk4 ? g.N / 4 : 0;  // whole column fours inside W
+  if (blk4) {
+    const int64_t tot4 = (M4 / 4) * N4;
+    for (int64_t i = bid * 256 + threadIdx.x; i < tot4; i += nblk * 256) {
+      const int64_t m0 = (i / N4) * 4, n = (i % N4) * 4;
+      float4 v[4];
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        v[r] = *reinterpret_cast<const float4 *>(g.ws + (m0 + r) * g.ldws + n);
+        for (int z = 1; z < g.split_k; ++z) {
+          const float4 t = *reinterpret_cast<const float4 *>(g.ws + z * slab + (m0 + r) * g.ldws + n);
+          v[r].x += t.x; v[r].y += t.y; v[r].z += t.z; v[r].w += t.w;
+        }
+      }
+      update_block4_tower(g, m0, n, v);
+    }
+  }
+  const int64_t total = g.M * q;
   for (int64_t i = bid * 256 + threadIdx.x; i < total; i += nblk * 256) {
     const int64_t m = i / q, n = (i - m * q) * 4;
     if (n >= ncols && n >= g.pad_to) continue;
+    if (m < M4 && n + 4 <= N4 * 4) continue;  // done above in a 4 x 4 block
     float4 s = *reinterpret_cast<const float4 *>(g.ws + m * g.ldws + n);
     for (int z = 1; z < g.split_k; ++z) {
       const float4 t = *reinterpret_cast<const float4 *>(g.ws + z * slab + m * g.ldws + n);

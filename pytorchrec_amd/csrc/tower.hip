@@ -358,26 +358,44 @@ __global__ __launch_bounds__(TW_THREADS) void tower_kernel(TowerArgs a) {
                 ? *reinterpret_cast<const uint4 *>(a.x0 + (row0 + r) * a.ld_x0 + c * 8)
                 : make_uint4(0u, 0u, 0u, 0u);
   }
+  // the small parameters: every global load of this thread is issued before any
+  // is consumed (one memory round trip; as store-after-load loops they were ~7
+  // dependent trips, 4.8 us in the training step with x0 and the labels fresh
+  // from the previous launch: tools/step_tower_stamps.py)
+  const int H = a.width[L];
+  float pb[TW_MAXL], phw, pws, pyb[2], pxs[2];
+#pragma unroll
+  for (int l = 0; l < TW_MAXL; ++l)  // widths <= 512 = TW_THREADS: one column per thread
+    pb[l] = (l < L && tid < a.width[l + 1] && a.bias[l]) ? a.bias[l][tid] : 0.f;
+  phw = tid < H ? a.head_w[tid] : 0.f;
+  pws = tid < a.ns ? a.ws[tid] : 0.f;
+  const bool yrow = tid < TW_ROWS && row0 + tid < a.B;
+  pyb[0] = yrow ? a.y[row0 + tid] : 0.f;
+  pyb[1] = (yrow && a.base) ? a.base[row0 + tid] : 0.f;
+#pragma unroll
+  for (int q = 0; q < 2; ++q) {  // TW_ROWS * ns <= 16 * 64 = 2 per thread
+    const int i = tid + q * TW_THREADS;
+    const int r = a.ns ? i / a.ns : 0, j = i - r * a.ns;
+    pxs[q] = (i < TW_ROWS * a.ns && row0 + r < a.B) ? a.xs[(row0 + r) * a.ld_xs + j] : 0.f;
+  }
+  const float pb0 = tid == 0 ? (a.head_b ? a.head_b[0] : 0.f) + (a.b2 ? a.b2[0] : 0.f) : 0.f;
   for (int i = tid * 16; i < a.off_p; i += TW_THREADS * 16)
     *reinterpret_cast<uint4 *>(lds + i) = make_uint4(0u, 0u, 0u, 0u);
   float *prm = reinterpret_cast<float *>(lds + a.off_p);
-  {
-    const int H = a.width[L];
-    for (int l = 0; l < L; ++l)
-      for (int c = tid; c < a.width[l + 1]; c += TW_THREADS)
-        prm[a.p_bias[l] + c] = a.bias[l] ? a.bias[l][c] : 0.f;
-    for (int c = tid; c < H; c += TW_THREADS) prm[a.p_hw + c] = a.head_w[c];
-    for (int c = tid; c < a.ns; c += TW_THREADS) prm[a.p_ws + c] = a.ws[c];
-    if (tid == 0) prm[a.p_b0] = (a.head_b ? a.head_b[0] : 0.f) + (a.b2 ? a.b2[0] : 0.f);
-    if (tid < TW_ROWS) {
-      const bool ok = row0 + tid < a.B;
-      prm[a.p_y + tid] = ok ? a.y[row0 + tid] : 0.f;
-      prm[a.p_base + tid] = (ok && a.base) ? a.base[row0 + tid] : 0.f;
-    }
-    for (int i = tid; i < TW_ROWS * a.ns; i += TW_THREADS) {
-      const int r = i / a.ns, j = i - r * a.ns;
-      prm[a.p_xs + i] = row0 + r < a.B ? a.xs[(row0 + r) * a.ld_xs + j] : 0.f;
-    }
+#pragma unroll
+  for (int l = 0; l < TW_MAXL; ++l)
+    if (l < L && tid < a.width[l + 1]) prm[a.p_bias[l] + tid] = pb[l];
+  if (tid < H) prm[a.p_hw + tid] = phw;
+  if (tid < a.ns) prm[a.p_ws + tid] = pws;
+  if (tid == 0) prm[a.p_b0] = pb0;
+  if (tid < TW_ROWS) {
+    prm[a.p_y + tid] = pyb[0];
+    prm[a.p_base + tid] = pyb[1];
+  }
+#pragma unroll
+  for (int q = 0; q < 2; ++q) {
+    const int i = tid + q * TW_THREADS;
+    if (i < TW_ROWS * a.ns) prm[a.p_xs + i] = pxs[q];
   }
   __syncthreads();
 #pragma unroll
@@ -405,7 +423,6 @@ __global__ __launch_bounds__(TW_THREADS) void tower_kernel(TowerArgs a) {
 
   // ---- head + BCE: thread (m = tid / 32, c = tid % 32), parameters from LDS ----
   // (results go to LDS first: a barrier behind global stores would wait for them)
-  const int H = a.width[L];
   const char *hL = lds + a.off_h[L - 1];
   const int s_hL = a.s_h[L - 1];
   float *f_dz = reinterpret_cast<float *>(lds + a.off_f);

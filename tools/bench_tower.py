@@ -16,6 +16,8 @@ p.add_argument("--batch", type=int, default=4096)
 p.add_argument("--widths", default="429,400,400,400")
 p.add_argument("--reps", type=int, default=100)
 p.add_argument("--rowmajor", action="store_true", help="row-major operand outputs (kfrag off)")
+p.add_argument("--cold", action="store_true", help="128 MB fill before every launch (timed with it)")
+p.add_argument("--reemit", action="store_true", help="re-emit the weight images before every launch")
 args = p.parse_args()
 widths = [int(x) for x in args.widths.split(",")]
 B, L = args.batch, len(widths) - 1
@@ -64,7 +66,17 @@ if kfrag:
     a.kfrag, a.x0_img = 1, x0_img.data_ptr()
 
 
+flush = torch.empty(128 << 20, dtype=torch.uint8, device=dev) if "--cold" in sys.argv else None
+reemit = "--reemit" in sys.argv
+
+
 def launch():
+    if flush is not None:  # evict L2 and most of the Infinity Cache before each launch
+        flush.fill_(1)
+    if reemit:  # the step's SGD rewrites the weight images before the next tower
+        for W, im in zip(Ws, imgs):
+            _mrec.call("mrec_tower_weight_prep", W.data_ptr(), W.shape[0], W.shape[1], W.stride(0),
+                       im[0].data_ptr(), im[1].data_ptr(), _mrec.stream_handle())
     _mrec.call("mrec_tower_fwd_bwd", ctypes.byref(a), _mrec.stream_handle())
 
 

@@ -1,0 +1,50 @@
+"""Per-workgroup phase stamps of the fused tower INSIDE the C2 training step
+(bench.py's model and batches, eager steps), to compare with the standalone
+tools/bench_tower.py timeline."""
+import ctypes
+import os
+import sys
+
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+sys.argv = sys.argv[:1]
+import bench  # noqa: E402
+from pytorchrec_amd import _mrec  # noqa: E402
+from pytorchrec_amd.loss import BCEWithLogitsLoss  # noqa: E402
+
+
+def main():
+    args = bench.parse()
+    dev = torch.device("cuda", 0)
+    model, sparse, dense_cols, label_col = bench.build_deepfm(args, dev)
+    model.compile(torch.optim.SGD(model.get_parameters(), lr=args.lr), BCEWithLogitsLoss(), [], dev)
+    for bank in model.embedding_banks():
+        bank.check_ids = False
+    bufs = [bench.make_batch_buffer(args, sparse, s, dev) for s in range(2)]
+    datas = [bench.batch_views(b, args, sparse, dense_cols, label_col) for b in bufs]
+    for k in range(5):
+        model.train_step(datas[k % 2])
+    torch.cuda.synchronize()
+    grid = (args.batch + 15) // 16
+    st = torch.zeros(grid, 16, dtype=torch.int64, device=dev)
+    fn = _mrec.lib().mrec_tower_debug_stamps
+    fn.argtypes, fn.restype = [ctypes.c_void_p], None
+    fn(st.data_ptr())
+    model.train_step(datas[1])
+    fn(None)
+    torch.cuda.synchronize()
+    t = st.cpu().double() * 10.0 / 1e3
+    t0 = t[:, 0].min()
+    names = {0: "start", 1: "x0 loaded", 2: "fwd1", 3: "fwd2", 4: "fwd3", 5: "head dot",
+             13: "dh_L (w0)", 14: "parts (w0)", 6: "head", 7: "bwd_L", 8: "bwd_L-1",
+             9: "bwd_L-2", 11: "bwd done", 12: "ticket"}
+    for k, n in names.items():
+        if bool((st[:, k] != 0).all()):
+            c = t[:, k] - t0
+            print(f"{n:>10}: min {float(c.min()):7.2f} med {float(c.median()):7.2f} "
+                  f"max {float(c.max()):7.2f} us")
+
+
+if __name__ == "__main__":
+    main()

@@ -500,10 +500,34 @@ __global__ __launch_bounds__(256, MREC_APPLY_WAVES) void apply_hash_kernel(BankA
   if (q >= B * F) return;  // whole workers
   const bool rowwise = MODE < 0 && a.mode == MREC_BWD_ROWWISE_ADAGRAD;
   if (!live && !rowwise) return;
-  const int code = lookup_table(ws, F, B)[q];
-  if (code < 0) return;  // whole workers
   const int64_t b = q / F;
   const int f = static_cast<int>(q - b * F);
+  const int code = lookup_table(ws, F, B)[q];
+  // this lookup's gradient inputs depend on (b, f) only: issued beside the lut load,
+  // not behind the branch on its verdict (one memory round trip less per row)
+  float gdx[EPL], fs[EPL];
+  float dfm_c = 0.f;
+#pragma unroll
+  for (int j = 0; j < EPL; ++j) gdx[j] = fs[j] = 0.f;
+  const bool pre = live && !a.g_occ;
+  if (pre) {
+    if (v_lane) {
+      const int64_t col = static_cast<int64_t>(f) * D + e0;
+      if (a.dx) {
+        if (a.dx_bf16)
+          load_bf16xN<EPL>(static_cast<const uint16_t *>(a.dx) + b * a.dx_ld + col, gdx);
+        else
+          load_f32xN<EPL>(static_cast<const float *>(a.dx) + b * a.dx_ld + col, gdx);
+      }
+      if (a.dfm) {
+        dfm_c = a.dfm[b];
+        load_f32xN<EPL>(a.fm_sum + b * D + e0, fs);
+      }
+    } else if (w_lane && a.dw) {
+      gdx[0] = a.dw[b];
+    }
+  }
+  if (code < 0) return;  // whole workers
   const int64_t grow = toff[f] + code;
   uint4 raw = make_uint4(0u, 0u, 0u, 0u);
   if (live) raw = *reinterpret_cast<const uint4 *>(row_ptr_g<T, MODE>(bank, a, grow, e0));
@@ -520,7 +544,16 @@ __global__ __launch_bounds__(256, MREC_APPLY_WAVES) void apply_hash_kernel(BankA
   float acc[EPL];
 #pragma unroll
   for (int j = 0; j < EPL; ++j) acc[j] = 0.f;
-  if (live) add_lookup_grad_v<EPL>(a, b, f, D, e0, v_lane, w_lane, v, acc);
+  if (pre) {  // = add_lookup_grad_v on the pre-loaded inputs (same operations)
+    if (v_lane && a.dfm) {
+#pragma unroll
+      for (int j = 0; j < EPL; ++j) gdx[j] = fmaf(dfm_c, fs[j] - v[j], gdx[j]);
+    }
+#pragma unroll
+    for (int j = 0; j < EPL; ++j) acc[j] += gdx[j];
+  } else if (live) {
+    add_lookup_grad_v<EPL>(a, b, f, D, e0, v_lane, w_lane, v, acc);
+  }
 #if MREC_APPLY_EXP == 9
   if (acc[0] == 12345.f) *(float *)a.grad = acc[1];
   return;

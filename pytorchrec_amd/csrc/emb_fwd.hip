@@ -126,6 +126,14 @@ __device__ __forceinline__ void interact_sample(const BankArgs &bank, const IdsA
   const bool v_lane = e0 + EPL <= D;
   const bool w_lane = bank.has_w && e0 == D;
 
+  // the dense features and their first-order weights depend on b only: loaded
+  // first, so their latency hides under the id -> row chain (n_dense <= 64)
+  const bool dense64 = n_dense <= 64;
+  float dv = 0.f, dwv = 0.f;
+  if (dense64 && lane < n_dense) {
+    dv = dense[b * dense_ld + lane];
+    if (dense_w) dwv = dense_w[lane];
+  }
   // phase 1: issue every row load of this sample before consuming any
   IA_STAMP(0, 0);
 #ifdef MREC_INTERACT_PROF
@@ -241,13 +249,16 @@ __device__ __forceinline__ void interact_sample(const BankArgs &bank, const IdsA
   IA_STAMP(3, __float_as_int(fm));
   // dense features: first-order dot + copy into x0, zero the pad columns
   float ds = 0.f;
-  if (dense_w)
+  if (dense64)
+    ds = dv * dwv;
+  else if (dense_w)
     for (int j = lane; j < n_dense; j += 64) ds = fmaf(dense[b * dense_ld + j], dense_w[j], ds);
   ds = sum_wave(ds);
   if (x0v) {
     const int base = F * D;
     for (int c = base + lane; c < x0_cols; c += 64) {
-      const float x = (c - base < n_dense) ? dense[b * dense_ld + (c - base)] : 0.f;
+      const int j = c - base;
+      const float x = j < n_dense ? (dense64 && j == lane ? dv : dense[b * dense_ld + j]) : 0.f;
       if constexpr (X0_BF16)
         static_cast<uint16_t *>(x0v)[b * x0_ld + c] = f32_to_bf16_rne(x);
       else

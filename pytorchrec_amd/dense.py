@@ -990,7 +990,8 @@ def _tdw_splits(B: int) -> int:
     8.3 MB (8 slices ran no faster and double the slabs the reduction reads)."""
     if os.environ.get("MREC_TOWER_DW", "1") == "0" or B < 256:
         return 0
-    for s in (4, 2):
+    want = int(os.environ.get("MREC_TDW_SPLITS", "4"))  # A/B knob
+    for s in (want, 4, 2):
         if _eff_split(B, s) == s:
             return s
     return 0

@@ -140,25 +140,45 @@ __global__ __launch_bounds__(256) void din_feat_bwd_kernel(
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const int64_t b = static_cast<int64_t>(blockIdx.x) * 4 + w;
   if (b >= B) return;
-  if (lane < L) {
-    const int64_t r = b * L + lane;
+  // lane task t = (history position j, 8-column chunk c): consecutive lanes take
+  // consecutive chunks of a row, so the df / k reads and the dk read-modify-write
+  // are 16-B accesses along rows (one lane per whole row made every dk access a
+  // scalar 4-B one, 67 us per C4 step)
+  const int nc = E / 8;
+  const bool vec = (reinterpret_cast<uintptr_t>(dk) & 15) == 0 && (lddk & 3) == 0;
+  for (int t = lane; t < L * nc; t += 64) {
+    const int j = t / nc, c = (t - j * nc) * 8;
+    const int64_t r = b * L + j;
     const uint16_t *d = df + r * lddf;
-    const uint16_t *kr = k + r * ldk;
-    const uint16_t *qr = q + b * ldq;
-    float *dkr = dk + r * lddk;
-    for (int c = 0; c < E; c += 8) {
-      float f0[8], f1[8], f2[8], f3[8], kv[8], qv[8];
-      Vec<uint16_t>::to_f32(*reinterpret_cast<const uint4 *>(d + c), f0);
-      Vec<uint16_t>::to_f32(*reinterpret_cast<const uint4 *>(d + E + c), f1);
-      Vec<uint16_t>::to_f32(*reinterpret_cast<const uint4 *>(d + 2 * E + c), f2);
-      Vec<uint16_t>::to_f32(*reinterpret_cast<const uint4 *>(d + 3 * E + c), f3);
-      Vec<uint16_t>::to_f32(*reinterpret_cast<const uint4 *>(kr + c), kv);
-      Vec<uint16_t>::to_f32(*reinterpret_cast<const uint4 *>(qr + c), qv);
+    float f0[8], f1[8], f2[8], f3[8], kv[8], qv[8];
+    Vec<uint16_t>::to_f32(*reinterpret_cast<const uint4 *>(d + c), f0);
+    Vec<uint16_t>::to_f32(*reinterpret_cast<const uint4 *>(d + E + c), f1);
+    Vec<uint16_t>::to_f32(*reinterpret_cast<const uint4 *>(d + 2 * E + c), f2);
+    Vec<uint16_t>::to_f32(*reinterpret_cast<const uint4 *>(d + 3 * E + c), f3);
+    Vec<uint16_t>::to_f32(*reinterpret_cast<const uint4 *>(k + r * ldk + c), kv);
+    Vec<uint16_t>::to_f32(*reinterpret_cast<const uint4 *>(q + b * ldq + c), qv);
+    float *dkr = dk + r * lddk + c;
+    float o[8];
+    if (vec) {
+      const float4 a0 = *reinterpret_cast<const float4 *>(dkr);
+      const float4 a1 = *reinterpret_cast<const float4 *>(dkr + 4);
+      o[0] = a0.x; o[1] = a0.y; o[2] = a0.z; o[3] = a0.w;
+      o[4] = a1.x; o[5] = a1.y; o[6] = a1.z; o[7] = a1.w;
+    } else {
 #pragma unroll
-      for (int i = 0; i < 8; ++i) {
-        dkr[c + i] += f1[i] - f2[i] + f3[i] * qv[i];
-        tr[w][lane][c + i] = f0[i] + f2[i] + f3[i] * kv[i];
-      }
+      for (int i = 0; i < 8; ++i) o[i] = dkr[i];
+    }
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      o[i] += f1[i] - f2[i] + f3[i] * qv[i];
+      tr[w][j][c + i] = f0[i] + f2[i] + f3[i] * kv[i];
+    }
+    if (vec) {
+      *reinterpret_cast<float4 *>(dkr) = make_float4(o[0], o[1], o[2], o[3]);
+      *reinterpret_cast<float4 *>(dkr + 4) = make_float4(o[4], o[5], o[6], o[7]);
+    } else {
+#pragma unroll
+      for (int i = 0; i < 8; ++i) dkr[i] = o[i];
     }
   }
   asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // this wave's LDS writes, then its reads

@@ -787,6 +787,13 @@ mrec_status mrec_din_feat_bwd(const void *dfeat, int64_t lddf, const void *dtop,
                               const void *q, int64_t ldq, const void *k, int64_t ldk,
                               int64_t batch, int32_t L, int32_t E, float *dk, int64_t lddk,
                               float *dq, int64_t lddq, mrec_stream stream);
+/* the same, with dq and the final dk written as ONE bf16 gradient of the gathered
+ * rows [target rows b < batch | history rows batch + b L + j] (row stride ld_rows;
+ * dk read, not written): the gather's input gradient in the bank's dtype (ABI 15) */
+mrec_status mrec_din_feat_bwd_rows(const void *dfeat, int64_t lddf, const void *dtop, int64_t lddt,
+                                   const void *q, int64_t ldq, const void *k, int64_t ldk,
+                                   int64_t batch, int32_t L, int32_t E, const float *dk,
+                                   int64_t lddk, void *d_rows, int64_t ld_rows, mrec_stream stream);
 
 /*
  * Fused CTR head + BCE-with-logits (forward AND the loss gradient, one pass over h;

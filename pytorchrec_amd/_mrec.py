@@ -267,6 +267,8 @@ SIGNATURES = {
                                          _i64, _vp]),
     "mrec_din_feat_bwd": (ctypes.c_int, [_vp, _i64, _vp, _i64, _vp, _i64, _vp, _i64, _i64, _i32,
                                          _i32, _vp, _i64, _vp, _i64, _vp]),
+    "mrec_din_feat_bwd_rows": (ctypes.c_int, [_vp, _i64, _vp, _i64, _vp, _i64, _vp, _i64, _i64, _i32,
+                                              _i32, _vp, _i64, _vp, _i64, _vp]),
     "mrec_ctr_head_parts": (ctypes.c_int64, [_i64]),
     "mrec_ctr_head_fwd": (ctypes.c_int, [_vp, _i64, _i64, _i32, _vp, _vp, _vp, _vp, _vp, _i64,
                                          _i32, _vp, _vp, _i32, _vp, _vp, _vp, _i64, _vp, _i64,

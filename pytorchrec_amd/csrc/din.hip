@@ -131,11 +131,16 @@ __global__ __launch_bounds__(256) void din_pool_bwd_kernel(
 // attention-unit input backward (+ the pooling's dk, + the direct q gradient):
 //   dk_j += df_k - df_(q-k) + df_(q*k) * q
 //   dq    = dtop[:, :E] + sum_j (df_q + df_(q-k) + df_(q*k) * k_j)      (position order)
+// ROWS: the final dq / dk go to one bf16 gradient of the gathered rows
+// [target rows (B) | history rows (B L)] (row stride ld_rows) instead of fp32 dq
+// and dk in place -- the gather's input gradient as autograd wants it (bf16),
+// without slice-backward zero fills, copies and an add of the two pieces
+template <bool ROWS>
 __global__ __launch_bounds__(256) void din_feat_bwd_kernel(
     const uint16_t *__restrict__ df, int64_t lddf, const uint16_t *__restrict__ dtop,
     int64_t lddt, const uint16_t *__restrict__ q, int64_t ldq, const uint16_t *__restrict__ k,
     int64_t ldk, int64_t B, int L, int E, float *__restrict__ dk, int64_t lddk,
-    float *__restrict__ dq, int64_t lddq) {
+    float *__restrict__ dq, int64_t lddq, uint16_t *__restrict__ drows, int64_t ld_rows) {
   __shared__ float tr[4][DIN_MAXL][DIN_MAXE + 1];
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const int64_t b = static_cast<int64_t>(blockIdx.x) * 4 + w;
@@ -173,7 +178,11 @@ __global__ __launch_bounds__(256) void din_feat_bwd_kernel(
       o[i] += f1[i] - f2[i] + f3[i] * qv[i];
       tr[w][j][c + i] = f0[i] + f2[i] + f3[i] * kv[i];
     }
-    if (vec) {
+    if constexpr (ROWS) {
+      *reinterpret_cast<uint4 *>(drows + (B + r) * ld_rows + c) =
+          make_uint4(pack_bf16x2(o[0], o[1]), pack_bf16x2(o[2], o[3]), pack_bf16x2(o[4], o[5]),
+                     pack_bf16x2(o[6], o[7]));
+    } else if (vec) {
       *reinterpret_cast<float4 *>(dkr) = make_float4(o[0], o[1], o[2], o[3]);
       *reinterpret_cast<float4 *>(dkr + 4) = make_float4(o[4], o[5], o[6], o[7]);
     } else {
@@ -185,7 +194,10 @@ __global__ __launch_bounds__(256) void din_feat_bwd_kernel(
   if (lane < E) {
     float v = bf16_to_f32(dtop[b * lddt + lane]);
     for (int j = 0; j < L; ++j) v += tr[w][j][lane];
-    dq[b * lddq + lane] = v;
+    if constexpr (ROWS)
+      drows[b * ld_rows + lane] = f32_to_bf16_rne(v);
+    else
+      dq[b * lddq + lane] = v;
   }
 }
 
@@ -259,12 +271,31 @@ mrec_status mrec_din_feat_bwd(const void *dfeat, int64_t lddf, const void *dtop,
                      lddq >= E,
                  "bad strides");
   if (batch == 0) return MREC_OK;
-  din_feat_bwd_kernel<<<dim3(static_cast<unsigned>((batch + 3) / 4)), 256, 0,
-                        static_cast<hipStream_t>(stream)>>>(
+  din_feat_bwd_kernel<false><<<dim3(static_cast<unsigned>((batch + 3) / 4)), 256, 0,
+                               static_cast<hipStream_t>(stream)>>>(
       static_cast<const uint16_t *>(dfeat), lddf, static_cast<const uint16_t *>(dtop), lddt,
       static_cast<const uint16_t *>(q), ldq, static_cast<const uint16_t *>(k), ldk, batch, L, E, dk,
-      lddk, dq, lddq);
+      lddk, dq, lddq, nullptr, 0);
   return launch_status("mrec_din_feat_bwd");
+}
+
+mrec_status mrec_din_feat_bwd_rows(const void *dfeat, int64_t lddf, const void *dtop, int64_t lddt,
+                                   const void *q, int64_t ldq, const void *k, int64_t ldk,
+                                   int64_t batch, int32_t L, int32_t E, const float *dk,
+                                   int64_t lddk, void *d_rows, int64_t ld_rows, mrec_stream stream) {
+  MREC_CHECK_ARG(dfeat && dtop && q && k && dk && d_rows, "NULL pointer");
+  MREC_CHECK_ARG(batch >= 0 && L >= 1 && L <= DIN_MAXL && E >= 8 && E <= DIN_MAXE && E % 8 == 0,
+                 "need 1 <= L <= 64, 8 <= E <= 64, E % 8 == 0");
+  MREC_CHECK_ARG(a16(dfeat, lddf) && a16(q, ldq) && a16(k, ldk) && a16(d_rows, ld_rows) &&
+                     lddf >= 4 * E && lddk >= E && ld_rows >= E,
+                 "bad strides");
+  if (batch == 0) return MREC_OK;
+  din_feat_bwd_kernel<true><<<dim3(static_cast<unsigned>((batch + 3) / 4)), 256, 0,
+                              static_cast<hipStream_t>(stream)>>>(
+      static_cast<const uint16_t *>(dfeat), lddf, static_cast<const uint16_t *>(dtop), lddt,
+      static_cast<const uint16_t *>(q), ldq, static_cast<const uint16_t *>(k), ldk, batch, L, E,
+      const_cast<float *>(dk), lddk, nullptr, 0, static_cast<uint16_t *>(d_rows), ld_rows);
+  return launch_status("mrec_din_feat_bwd_rows");
 }
 
 }  // extern "C"

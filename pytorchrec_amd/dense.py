@@ -730,6 +730,52 @@ class _DinPoolFn(torch.autograd.Function):
         return ds, None, None, None, None, None
 
 
+class _DinRowsFeatFn(torch.autograd.Function):
+    """_DinFeatFn over the gathered rows [q (B) | k (B L)] as ONE input: the backward
+    returns the rows' bf16 gradient from one kernel (mrec_din_feat_bwd_rows), so
+    autograd adds no slice-backward zero fills, copies or dtype casts."""
+
+    @staticmethod
+    def forward(ctx, rows, B: int, st: _DinState, L: int):
+        q, k = rows[:B], rows[B:]
+        E = rows.shape[1]
+        feat = _alloc(B * L, 4 * E, _BF16, rows.device)
+        _mrec.call("mrec_din_feat_fwd", q.data_ptr(), q.stride(0), k.data_ptr(), k.stride(0), B, L,
+                   E, feat.data_ptr(), feat.stride(0), _mrec.stream_handle())
+        ctx.save_for_backward(rows)
+        ctx.st, ctx.L, ctx.B = st, L, B
+        return feat
+
+    @staticmethod
+    def backward(ctx, dfeat):
+        rows, = ctx.saved_tensors
+        st, B, L = ctx.st, ctx.B, ctx.L
+        q, k = rows[:B], rows[B:]
+        E = rows.shape[1]
+        dfeat = _bf16_rows(dfeat)
+        d_rows = torch.empty_like(rows)
+        _mrec.call("mrec_din_feat_bwd_rows", dfeat.data_ptr(), dfeat.stride(0), st.dtop.data_ptr(),
+                   st.dtop.stride(0), q.data_ptr(), q.stride(0), k.data_ptr(), k.stride(0), B, L, E,
+                   st.dk.data_ptr(), st.dk.stride(0), d_rows.data_ptr(), d_rows.stride(0),
+                   _mrec.stream_handle())
+        del st.dk, st.dtop
+        return d_rows, None, None, None
+
+
+def din_attention_top_rows(rows: torch.Tensor, B: int, his: torch.Tensor, att_mlp,
+                           att_out: torch.nn.Linear) -> torch.Tensor:
+    """din_attention_top over the gather output rows [q (B) | k (B L)] (bf16, 16-B
+    aligned rows): the rows' gradient comes back as one bf16 tensor."""
+    L = his.shape[1]
+    rows = _bf16_rows(rows)
+    st = _DinState()
+    feat = _DinRowsFeatFn.apply(rows, B, st, L)
+    h = att_mlp(feat)
+    s = linear(h, att_out.weight, att_out.bias, out_dtype=torch.float32)
+    r = rows.detach()
+    return _DinPoolFn.apply(s, r[:B], r[B:], his, st, L)
+
+
 def din_attention_top(q: torch.Tensor, k: torch.Tensor, his: torch.Tensor, att_mlp,
                       att_out: torch.nn.Linear) -> torch.Tensor:
     """The DIN top-MLP input [q | u] (bf16 [B, 2E]) on libmrec kernels: attention-unit

@@ -91,9 +91,9 @@ class DIN(IModel):
         rows = gather(bank, [torch.cat([iid.reshape(-1), his.reshape(-1).to(iid.dtype)]),
                              torch.cat([cid.reshape(-1), hcat.reshape(-1).to(cid.dtype)])],
                       out_dtype=act_dtype)
-        q, k = rows[:B], rows[B:]
         if on_gpu:
-            return dense_ops.din_attention_top(q, k, his, self.att_mlp, self.att_out)
+            return dense_ops.din_attention_top_rows(rows, B, his, self.att_mlp, self.att_out)
+        q, k = rows[:B], rows[B:]
         valid = his > 0
         valid[:, 0] = True
         u = dense_ops.din_attention(q, k.reshape(B, L, -1), valid, self.att_mlp, self.att_out)

@@ -72,6 +72,28 @@ def test_din_forward_matches_oracle_and_torch(gpu):
     np.testing.assert_allclose(got[:, E:].numpy(), u, rtol=3e-2, atol=3e-2 * np.abs(u).max())
 
 
+def test_din_rows_path_equals_split_path_bitwise(gpu):
+    """din_attention_top_rows (the model's path: one bf16 gradient of the gathered
+    rows from mrec_din_feat_bwd_rows) == din_attention_top on the q / k slices with
+    autograd casting dq / dk to bf16: same output bits, same gradient bits."""
+    from pytorchrec_amd import dense as D
+    att, out, q, k, his = _block(gpu, seed=5)
+    B, E = q.shape
+    rows = torch.cat([q, k]).detach().clone().requires_grad_()
+    top_r = D.din_attention_top_rows(rows, B, his, att, out)
+    g = torch.Generator().manual_seed(4)
+    dtop = torch.randn(B, 2 * E, generator=g).to(gpu).to(top_r.dtype)
+    top_r.backward(dtop)
+    qg = q.detach().clone().requires_grad_()
+    kg = k.detach().clone().requires_grad_()
+    top_s = D.din_attention_top(qg, kg, his, att, out)
+    top_s.backward(dtop)
+    assert torch.equal(top_r, top_s)
+    assert rows.grad.dtype == torch.bfloat16
+    assert torch.equal(rows.grad[:B], qg.grad.to(torch.bfloat16))
+    assert torch.equal(rows.grad[B:], kg.grad.to(torch.bfloat16))
+
+
 def test_din_backward_matches_torch(gpu):
     from pytorchrec_amd import dense as D
     att, out, q, k, his = _block(gpu, seed=3)

@@ -165,10 +165,16 @@ __global__ __launch_bounds__(256) void lg_count_kernel(BankArgs bank, IdsArgs id
   __syncthreads();
   const int64_t total = n * bank.n_tables;
   const int64_t base = static_cast<int64_t>(blockIdx.x) * 256 * kLgIter;
+  // every id load of this thread first (one memory round trip, not kLgIter)
+  int32_t rr[kLgIter];
+#pragma unroll
   for (int it = 0; it < kLgIter; ++it) {
     int64_t b;
-    const Run u = lane_run(lookup_row(bank, ids, n, base + it * 256 + threadIdx.x, total, &b,
-                                      oob));
+    rr[it] = lookup_row(bank, ids, n, base + it * 256 + threadIdx.x, total, &b, oob);
+  }
+#pragma unroll
+  for (int it = 0; it < kLgIter; ++it) {
+    const Run u = lane_run(rr[it]);
     if (u.r >= 0 && u.head == (threadIdx.x & 63)) {
       const int h = lg_slot(key, u.r);
       if (h >= 0)
@@ -324,10 +330,14 @@ __global__ __launch_bounds__(256) void lg_place_kernel(BankArgs bank, IdsArgs id
   const int64_t base = static_cast<int64_t>(blockIdx.x) * 256 * kLgIter;
   int32_t row[kLgIter], bb[kLgIter], slot[kLgIter], off[kLgIter];
 #pragma unroll
-  for (int it = 0; it < kLgIter; ++it) {
+  for (int it = 0; it < kLgIter; ++it) {  // every id load first (one memory round trip)
     int64_t b = 0;
-    const Run u = lane_run(lookup_row(bank, ids, n, base + it * 256 + threadIdx.x, total, &b,
-                                      nullptr));
+    row[it] = lookup_row(bank, ids, n, base + it * 256 + threadIdx.x, total, &b, nullptr);
+    bb[it] = static_cast<int32_t>(b);
+  }
+#pragma unroll
+  for (int it = 0; it < kLgIter; ++it) {
+    const Run u = lane_run(row[it]);
     int h = -1, k = 0;
     if (u.r >= 0 && u.head == lane) {
       h = lg_slot(key, u.r);
@@ -338,8 +348,6 @@ __global__ __launch_bounds__(256) void lg_place_kernel(BankArgs bank, IdsArgs id
     }
     h = __shfl(h, u.head);
     k = __shfl(k, u.head);
-    row[it] = u.r;
-    bb[it] = static_cast<int32_t>(b);
     slot[it] = h;
     off[it] = k + (lane - u.head);
   }

@@ -385,7 +385,7 @@ __global__ __launch_bounds__(TW_THREADS) void tower_kernel(TowerArgs a) {
 #pragma unroll
   for (int l = 0; l < TW_MAXL; ++l)
     if (l < L && tid < a.width[l + 1]) prm[a.p_bias[l] + tid] = pb[l];
-  if (tid < H) prm[a.p_hw + tid] = phw;
+  if (tid < (H + 7) / 8 * 8) prm[a.p_hw + tid] = phw;  // zero past H: whole chunks
   if (tid < a.ns) prm[a.p_ws + tid] = pws;
   if (tid == 0) prm[a.p_b0] = pb0;
   if (tid < TW_ROWS) {
@@ -434,15 +434,15 @@ __global__ __launch_bounds__(TW_THREADS) void tower_kernel(TowerArgs a) {
     const int m = tid >> 5, c = tid & 31;
     const bool ok = row0 + m < a.B;
     float dot = 0.f;
-    for (int j = c; j * 8 < H; j += 32) {
+    for (int j = c; j * 8 < H; j += 32) {  // hw is zero past H (whole chunks in LDS)
       const uint4 hv = *reinterpret_cast<const uint4 *>(hL + m * s_hL + j * 16);
+      const float4 w0 = *reinterpret_cast<const float4 *>(hw + j * 8);
+      const float4 w1 = *reinterpret_cast<const float4 *>(hw + j * 8 + 4);
+      const float wv[8] = {w0.x, w0.y, w0.z, w0.w, w1.x, w1.y, w1.z, w1.w};
       float hf[8];
       Vec<uint16_t>::to_f32(hv, hf);
 #pragma unroll
-      for (int q = 0; q < 8; ++q) {
-        const int n = j * 8 + q;
-        dot = fmaf(hf[q], n < H ? hw[n] : 0.f, dot);
-      }
+      for (int q = 0; q < 8; ++q) dot = fmaf(hf[q], wv[q], dot);
     }
     for (int j = c; j < a.ns; j += 32) dot = fmaf(prm[a.p_xs + m * a.ns + j], prm[a.p_ws + j], dot);
 #pragma unroll
@@ -470,12 +470,14 @@ __global__ __launch_bounds__(TW_THREADS) void tower_kernel(TowerArgs a) {
     for (int j = c; j * 8 < H; j += 32) {
       const uint4 hv = *reinterpret_cast<const uint4 *>(hL + m * s_hL + j * 16);
       const uint32_t hwd[4] = {hv.x, hv.y, hv.z, hv.w};
+      const float4 w0 = *reinterpret_cast<const float4 *>(hw + j * 8);
+      const float4 w1 = *reinterpret_cast<const float4 *>(hw + j * 8 + 4);
+      const float wv[8] = {w0.x, w0.y, w0.z, w0.w, w1.x, w1.y, w1.z, w1.w};
       float gv[8];
 #pragma unroll
       for (int q = 0; q < 8; ++q) {
-        const int n = j * 8 + q;
         const uint32_t hb = (q & 1) ? (hwd[q >> 1] >> 16) : (hwd[q >> 1] & 0xffffu);
-        gv[q] = (n < H && bf16_pos(hb)) ? d * hw[n] : 0.f;
+        gv[q] = bf16_pos(hb) ? d * wv[q] : 0.f;  // pad columns: h = 0 and hw = 0
       }
       *reinterpret_cast<uint4 *>(g0 + m * a.s_g + j * 16) =
           make_uint4(pack_bf16x2(gv[0], gv[1]), pack_bf16x2(gv[2], gv[3]),
@@ -487,8 +489,15 @@ __global__ __launch_bounds__(TW_THREADS) void tower_kernel(TowerArgs a) {
   for (int c = tid; c < H + 1 + a.ns; c += TW_THREADS) {
     float sacc = 0.f;
     if (c < H) {
+      float dzv[TW_ROWS];
+#pragma unroll
+      for (int m4 = 0; m4 < TW_ROWS; m4 += 4) {
+        const float4 t = *reinterpret_cast<const float4 *>(f_dz + m4);
+        dzv[m4] = t.x; dzv[m4 + 1] = t.y; dzv[m4 + 2] = t.z; dzv[m4 + 3] = t.w;
+      }
+#pragma unroll
       for (int m = 0; m < TW_ROWS; ++m)
-        sacc = fmaf(f_dz[m], bf16_to_f32(*reinterpret_cast<const uint16_t *>(hL + m * s_hL + c * 2)), sacc);
+        sacc = fmaf(dzv[m], bf16_to_f32(*reinterpret_cast<const uint16_t *>(hL + m * s_hL + c * 2)), sacc);
     } else if (c == H) {
       for (int m = 0; m < TW_ROWS; ++m) sacc += f_dz[m];
     } else {
@@ -730,12 +739,12 @@ mrec_status mrec_tower_fwd_bwd(const mrec_tower_args *p, mrec_stream stream) {
   int np = 0;
   for (int l = 0; l < L; ++l) {
     a.p_bias[l] = np;
-    np += s.width[l + 1];
+    np += (s.width[l + 1] + 3) / 4 * 4;  // segments 16-B aligned (float4 reads)
   }
   a.p_hw = np;
-  np += s.width[L];
+  np += (s.width[L] + 7) / 8 * 8;  // whole 8-column chunks, pad zero (the LDS fill)
   a.p_ws = np;
-  np += s.ns;
+  np += (s.ns + 3) / 4 * 4;
   a.p_b0 = np;
   np += 1;
   a.p_y = np;

@@ -407,8 +407,6 @@ __global__ __launch_bounds__(TW_THREADS) void tower_kernel(TowerArgs a) {
   }
   __syncthreads();
   TW_STAMP(1);
-  if (a.kfrag) tower_store_kfrag(lds + a.off_x, a.s_x, a.width[0], a.x0_img, a.nsteps, row0, a.B,
-                                 a.store_mode);
 
   // ---- forward: h_l = relu(h_{l-1} W_l^T + b_l) --------------------------------
   for (int l = 0; l < L; ++l) {
@@ -418,6 +416,11 @@ __global__ __launch_bounds__(TW_THREADS) void tower_kernel(TowerArgs a) {
                        lds + a.off_h[l], a.s_h[l], prm + a.p_bias[l], nullptr, 0, a.rotate);
     __syncthreads();
     TW_STAMP(2 + l);
+    // x0's k-fragment image leaves behind layer 1 (x0's block stays in LDS): issued
+    // before it, its stores delayed the first weight fragments by ~1 us
+    if (l == 0 && a.kfrag)
+      tower_store_kfrag(lds + a.off_x, a.s_x, a.width[0], a.x0_img, a.nsteps, row0, a.B,
+                        a.store_mode);
     if (l + 1 < L) tower_out(a, lds + a.off_h[l], a.s_h[l], a.width[l + 1], a.h_out[l], a.ld_h[l], row0);
   }
 
@@ -445,8 +448,11 @@ __global__ __launch_bounds__(TW_THREADS) void tower_kernel(TowerArgs a) {
       for (int q = 0; q < 8; ++q) dot = fmaf(hf[q], wv[q], dot);
     }
     for (int j = c; j < a.ns; j += 32) dot = fmaf(prm[a.p_xs + m * a.ns + j], prm[a.p_ws + j], dot);
-#pragma unroll
-    for (int off = 16; off > 0; off >>= 1) dot += __shfl_xor(dot, off);
+    // sum over the 32 lanes of row m (two 16-lane rows): DPP + one permlane swap
+    dot = sum_quad(dot);
+    dot += dpp_f32<0x124>(dot);  // row_ror:4
+    dot += dpp_f32<0x128>(dot);  // row_ror:8
+    dot = swap16_sum(dot);
     if (c == 0) {
       float d = 0.f, lo = 0.f, zz = 0.f;
       if (ok) {

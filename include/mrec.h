@@ -32,7 +32,7 @@
 extern "C" {
 #endif
 
-#define MREC_ABI_VERSION 15
+#define MREC_ABI_VERSION 16
 #define MREC_MAX_TABLES 64      /* tables per table bank / per call */
 #define MREC_BWD_MAX_BATCH 8192  /* lookups per table per plan/apply call */
 #define MREC_BWD_HASH_MAX_BATCH 4096  /* batches up to this use the hash plan */
@@ -663,7 +663,16 @@ typedef struct {
    * the k-fragment image of x0 [batch, N_0]: the operands of mrec_tower_dw */
   int32_t kfrag;
   void *x0_img;
+  /* ABI 16: what runs after the forward (MREC_TOWER_*).  BCE: the loss above.
+   * FORWARD: z only (h_L . head_w + head_b + base + xs . ws + b2, z required), then
+   * the launch ends (no y, dz, part, loss, stores; the attention unit's scores).
+   * GIVEN_DZ: dz = dz_in (no loss; y, loss_part, ticket, loss, dz may be NULL); the
+   * backward as for BCE (dh_out, dx0, head partials, images). */
+  int32_t mode;
+  const float *dz_in;        /* [batch] for MREC_TOWER_GIVEN_DZ */
 } mrec_tower_args;
+
+enum { MREC_TOWER_BCE = 0, MREC_TOWER_FORWARD = 1, MREC_TOWER_GIVEN_DZ = 2 };
 
 mrec_status mrec_tower_fwd_bwd(const mrec_tower_args *a, mrec_stream stream);
 

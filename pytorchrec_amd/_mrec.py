@@ -20,7 +20,7 @@ import torch  # noqa: F401  (must precede the dlopen, see module docstring)
 LIB_DIR = os.path.join(os.path.dirname(os.path.abspath(__file__)), "lib")
 LIB_PATH = os.environ.get("MREC_LIB_PATH") or os.path.join(LIB_DIR, "libmrec.so")
 
-ABI_VERSION = 15
+ABI_VERSION = 16
 MAX_TABLES = 64
 BWD_MAX_BATCH = 8192
 BWD_HASH_MAX_BATCH = 4096  # batches up to this use the hash plan (fusable into a GEMM launch)
@@ -141,6 +141,9 @@ class SgdJob(ctypes.Structure):
                 ("img_kind", ctypes.c_int32)]
 
 
+TOWER_BCE, TOWER_FORWARD, TOWER_GIVEN_DZ = 0, 1, 2  # mrec_tower_args.mode
+
+
 class TowerArgs(ctypes.Structure):
     """mrec_tower_args (include/mrec.h)."""
     _fields_ = [("batch", ctypes.c_int64), ("n_layers", ctypes.c_int32),
@@ -158,7 +161,8 @@ class TowerArgs(ctypes.Structure):
                 ("z", ctypes.c_void_p), ("dz", ctypes.c_void_p),
                 ("part", ctypes.c_void_p), ("ldp", ctypes.c_int64),
                 ("loss_part", ctypes.c_void_p), ("ticket", ctypes.c_void_p),
-                ("loss", ctypes.c_void_p), ("kfrag", ctypes.c_int32), ("x0_img", ctypes.c_void_p)]
+                ("loss", ctypes.c_void_p), ("kfrag", ctypes.c_int32), ("x0_img", ctypes.c_void_p),
+                ("mode", ctypes.c_int32), ("dz_in", ctypes.c_void_p)]
 
 
 class TowerDwArgs(ctypes.Structure):

@@ -90,6 +90,8 @@ struct TowerArgs {
   int kfrag;       // h_out / dh_out / x0_img are k-fragment images (tower_common.h)
   int nsteps;      // their k steps: ceil(B / 32)
   uint16_t *x0_img;
+  int mode;        // MREC_TOWER_BCE / _FORWARD / _GIVEN_DZ
+  const float *dz_in;
 };
 
 __host__ __device__ __forceinline__ int tw_ceil(int a, int b) { return (a + b - 1) / b; }
@@ -370,7 +372,8 @@ __global__ __launch_bounds__(TW_THREADS) void tower_kernel(TowerArgs a) {
   phw = tid < H ? a.head_w[tid] : 0.f;
   pws = tid < a.ns ? a.ws[tid] : 0.f;
   const bool yrow = tid < TW_ROWS && row0 + tid < a.B;
-  pyb[0] = yrow ? a.y[row0 + tid] : 0.f;
+  const float *ysrc = a.mode == MREC_TOWER_GIVEN_DZ ? a.dz_in : a.y;  // p_y: labels or given dz
+  pyb[0] = (yrow && ysrc) ? ysrc[row0 + tid] : 0.f;
   pyb[1] = (yrow && a.base) ? a.base[row0 + tid] : 0.f;
 #pragma unroll
   for (int q = 0; q < 2; ++q) {  // TW_ROWS * ns <= 16 * 64 = 2 per thread
@@ -455,7 +458,9 @@ __global__ __launch_bounds__(TW_THREADS) void tower_kernel(TowerArgs a) {
     dot = swap16_sum(dot);
     if (c == 0) {
       float d = 0.f, lo = 0.f, zz = 0.f;
-      if (ok) {
+      if (ok && a.mode == MREC_TOWER_GIVEN_DZ) {
+        d = prm[a.p_y + m];
+      } else if (ok) {
         zz = dot + prm[a.p_b0] + prm[a.p_base + m];
         const float yy = prm[a.p_y + m];
         d = (1.f / (1.f + __expf(-zz)) - yy) * a.invB;
@@ -468,6 +473,10 @@ __global__ __launch_bounds__(TW_THREADS) void tower_kernel(TowerArgs a) {
   }
   __syncthreads();
   TW_STAMP(5);
+  if (a.mode == MREC_TOWER_FORWARD) {  // the scores only
+    if (tid < TW_ROWS && row0 + tid < a.B) a.z[row0 + tid] = f_z[tid];
+    return;
+  }
   // dh_L = dz * head_w * [h_L > 0] -> gradient block 0
   {
     char *g0 = lds + a.off_g[0];
@@ -520,8 +529,8 @@ __global__ __launch_bounds__(TW_THREADS) void tower_kernel(TowerArgs a) {
     float *prow = a.part + static_cast<int64_t>(blockIdx.x) * a.ldp;
     for (int c = tid; c < H + 1 + a.ns; c += TW_THREADS) prow[c] = f_part[c];
     if (tid < TW_ROWS && row0 + tid < a.B) {
-      a.dz[row0 + tid] = f_dz[tid];
-      if (a.z) a.z[row0 + tid] = f_z[tid];
+      if (a.dz) a.dz[row0 + tid] = f_dz[tid];
+      if (a.z && a.mode == MREC_TOWER_BCE) a.z[row0 + tid] = f_z[tid];
     }
   }
   tower_out(a, lds + a.off_g[0], a.s_g, H, a.dh_out[L - 1], a.ld_dh[L - 1], row0);
@@ -544,7 +553,8 @@ __global__ __launch_bounds__(TW_THREADS) void tower_kernel(TowerArgs a) {
       // the loss: this workgroup's partial as a write-through granule + a relaxed
       // agent ticket (cdna_hip_programming.md §6 G16), before the dx0 stores so the
       // wait drains little; the last arriver sums the partials below
-      if (tid == 0) {
+      if (tid == 0 && a.mode != MREC_TOWER_BCE) s_last = 0u;
+      if (tid == 0 && a.mode == MREC_TOWER_BCE) {
         float lp = 0.f;
         for (int m = 0; m < TW_ROWS; ++m) lp += f_loss[m];
         __hip_atomic_store(a.loss_part + blockIdx.x, lp, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -646,9 +656,11 @@ mrec_status mrec_tower_fwd_bwd(const mrec_tower_args *p, mrec_stream stream) {
                  "x0 rows must be 16-B aligned with ld_x0 >= round8(width[0])");
   const bool kf = s.kfrag != 0;
   auto al = [](const void *q) { return q && (reinterpret_cast<uintptr_t>(q) & 15) == 0; };
+  const bool fwd_only = s.mode == MREC_TOWER_FORWARD;  // nothing but z is written
   for (int l = 0; l < L; ++l) {
     MREC_CHECK_ARG(s.w_fwd[l] && s.w_bwd[l], "NULL weight image");
     const int w = s.width[l + 1];
+    if (fwd_only) continue;
     if (kf) {
       MREC_CHECK_ARG(al(s.dh_out[l]) && (l + 1 >= L || !s.h_out[l] || al(s.h_out[l])),
                      "k-fragment images must be 16-B aligned");
@@ -663,10 +675,17 @@ mrec_status mrec_tower_fwd_bwd(const mrec_tower_args *p, mrec_stream stream) {
   MREC_CHECK_ARG(!kf || !s.x0_img || al(s.x0_img), "x0_img must be 16-B aligned");
   MREC_CHECK_ARG(!kf || kfrag_elems(s.batch, TW_MAXW) * 2 < (int64_t(1) << 31),
                  "batch too large for k-fragment images");
-  MREC_CHECK_ARG(!s.dx0 || (al16(s.dx0, s.ld_dx0) && s.ld_dx0 >= (s.width[0] + 7) / 8 * 8),
+  MREC_CHECK_ARG(fwd_only || !s.dx0 || (al16(s.dx0, s.ld_dx0) && s.ld_dx0 >= (s.width[0] + 7) / 8 * 8),
                  "dx0 rows must be 16-B aligned with ld >= round8(width[0])");
-  MREC_CHECK_ARG(s.head_w && s.y && s.dz && s.part && s.loss_part && s.ticket && s.loss,
-                 "NULL head / loss pointer");
+  MREC_CHECK_ARG(s.mode >= MREC_TOWER_BCE && s.mode <= MREC_TOWER_GIVEN_DZ, "bad mode");
+  MREC_CHECK_ARG(s.head_w, "NULL head_w");
+  if (s.mode == MREC_TOWER_BCE)
+    MREC_CHECK_ARG(s.y && s.dz && s.part && s.loss_part && s.ticket && s.loss,
+                   "NULL head / loss pointer");
+  else if (s.mode == MREC_TOWER_FORWARD)
+    MREC_CHECK_ARG(s.z, "MREC_TOWER_FORWARD needs z");
+  else
+    MREC_CHECK_ARG(s.dz_in && s.part, "MREC_TOWER_GIVEN_DZ needs dz_in and part");
   MREC_CHECK_ARG(s.ns >= 0 && s.ns <= TW_MAXNS && (s.ns == 0 || (s.xs && s.ws)),
                  "side linear: ns in [0, 64] with xs and ws");
   MREC_CHECK_ARG(s.ldp >= s.width[L] + 1 + s.ns, "ldp < N_L + 1 + ns");
@@ -724,6 +743,12 @@ mrec_status mrec_tower_fwd_bwd(const mrec_tower_args *p, mrec_stream stream) {
   a.kfrag = kf ? 1 : 0;
   a.nsteps = static_cast<int>((s.batch + 31) / 32);
   a.x0_img = kf ? static_cast<uint16_t *>(s.x0_img) : nullptr;
+  a.mode = s.mode;
+  a.dz_in = s.dz_in;
+  if (a.mode == MREC_TOWER_FORWARD) {  // nothing leaves but z
+    a.x0_img = nullptr;
+    for (int l = 0; l < L; ++l) a.h_out[l] = nullptr;
+  }
   int off = 0;
   a.off_x = off;
   a.s_x = tw_stride(s.width[0]);

@@ -762,6 +762,22 @@ class _DinRowsFeatFn(torch.autograd.Function):
         return d_rows, None, None, None
 
 
+# opt-in (MREC_DIN_TOWER=1): measured at C4 the score tower is slower than the
+# GEMMs (fwd 279, bwd 527, weight gradients 213 us vs ~360 us for the GEMM path in
+# all): 12,800 16-row workgroups at 2 per CU run 25 residency rounds of the tower's
+# latency chain, and the k-fragment images of 204,800 rows go through HBM
+DIN_TOWER = os.environ.get("MREC_DIN_TOWER", "0") == "1"
+
+
+def _din_scores(feat: torch.Tensor, att_mlp, att_out: torch.nn.Linear) -> torch.Tensor:
+    """Attention-unit scores [B L, 1] fp32: the attention MLP's GEMMs + Linear(h, 1),
+    or the score tower (one launch each way) with MREC_DIN_TOWER=1."""
+    if DIN_TOWER and tower_supported(feat, att_mlp, att_out):
+        return score_tower(feat, att_mlp, att_out).reshape(-1, 1)
+    h = att_mlp(feat)
+    return linear(h, att_out.weight, att_out.bias, out_dtype=torch.float32)
+
+
 def din_attention_top_rows(rows: torch.Tensor, B: int, his: torch.Tensor, att_mlp,
                            att_out: torch.nn.Linear) -> torch.Tensor:
     """din_attention_top over the gather output rows [q (B) | k (B L)] (bf16, 16-B
@@ -770,8 +786,7 @@ def din_attention_top_rows(rows: torch.Tensor, B: int, his: torch.Tensor, att_ml
     rows = _bf16_rows(rows)
     st = _DinState()
     feat = _DinRowsFeatFn.apply(rows, B, st, L)
-    h = att_mlp(feat)
-    s = linear(h, att_out.weight, att_out.bias, out_dtype=torch.float32)
+    s = _din_scores(feat, att_mlp, att_out)
     r = rows.detach()
     return _DinPoolFn.apply(s, r[:B], r[B:], his, st, L)
 
@@ -787,8 +802,7 @@ def din_attention_top(q: torch.Tensor, k: torch.Tensor, his: torch.Tensor, att_m
     q, k = _bf16_rows(q), _bf16_rows(k)
     st = _DinState()
     feat = _DinFeatFn.apply(q, k, st, L)
-    h = att_mlp(feat)
-    s = linear(h, att_out.weight, att_out.bias, out_dtype=torch.float32)
+    s = _din_scores(feat, att_mlp, att_out)
     return _DinPoolFn.apply(s, q, k, his, st, L)
 
 
@@ -1030,15 +1044,23 @@ def _eff_split(K: int, s: int) -> int:
     return (K + k - 1) // k if K > 0 else 1
 
 
-def _tdw_splits(B: int) -> int:
-    """K slices of mrec_tower_dw (0: not used).  4 at B = 4096: about 2.3 one-wave
-    workgroups per CU over the 147 64 x 64 tiles of the C2 tower, partial slabs of
-    8.3 MB (8 slices ran no faster and double the slabs the reduction reads)."""
+def _tdw_tiles(widths) -> int:
+    """64 x 64 output tiles of the tower's dW_l = dY_l^T [X_l | 1]."""
+    return sum(((widths[l + 1] + 63) // 64) * ((widths[l] + 1 + 63) // 64)
+               for l in range(len(widths) - 1))
+
+
+def _tdw_splits(B: int, widths=None) -> int:
+    """K slices of mrec_tower_dw (0: not used): about 640 one-wave workgroups (2.5
+    per CU) over the tiles, slices of >= 256 rows, at most 64.  4 for the C2 tower
+    (147 tiles; 8 slices ran no faster and double the slabs the reduction reads), 64
+    for DIN's attention unit (8 tiles over 204,800 rows)."""
     if os.environ.get("MREC_TOWER_DW", "1") == "0" or B < 256:
         return 0
-    want = int(os.environ.get("MREC_TDW_SPLITS", "4"))  # A/B knob
-    for s in (want, 4, 2):
-        if _eff_split(B, s) == s:
+    env = os.environ.get("MREC_TDW_SPLITS")  # A/B knob
+    want = int(env) if env else (4 if widths is None else max(1, min(64, 640 // _tdw_tiles(widths))))
+    for s in range(want, 1, -1):
+        if B // s >= 256 and _eff_split(B, s) == s:
             return s
     return 0
 
@@ -1073,7 +1095,7 @@ class _TowerBCEFn(torch.autograd.Function):
         imgs = [tower_images(W) for W in Ws]
         # the weight gradients' operands: k-fragment images for mrec_tower_dw (the
         # tower writes them, x0's too), else row-major for the generic GEMM
-        tdw = _tdw_splits(B) if any(ctx.needs_input_grad[5:5 + 2 * L]) else 0
+        tdw = _tdw_splits(B, widths) if any(ctx.needs_input_grad[5:5 + 2 * L]) else 0
         if tdw:
             kf = lambda n: torch.empty(int(_mrec.lib().mrec_kfrag_elems(B, n)), dtype=_BF16,  # noqa: E731
                                        device=dev)
@@ -1150,83 +1172,97 @@ class _TowerBCEFn(torch.autograd.Function):
             dx0 = (dx0.float() * g).to(_BF16) if dx0 is not None else None
             dhs = [(d.float() * g).to(_BF16) if tdw else _bf16_rows((d.float() * g).to(_BF16))
                    for d in dhs]
-        widths, Ws, bs = ctx.widths, ctx.Ws, ctx.bs
-        head_w, head_b, ws, b2 = ctx.head
-        xin = ([x0] if tdw else [x0[:, :widths[0]]]) + hs
-        # --- weight gradients of the L layers: one launch ---
-        lr = sgd_lr(*Ws, *bs)
-        dpg = dp_grads(*Ws, *bs) if lr is None else None
-        need_w = any(ctx.needs_input_grad[5:5 + 2 * L])
-        dWs, dbs = [None] * L, [None] * L
-        calls = []
-        if need_w:
-            sk = tdw or _split_tower(widths, B)
-            ph = _mrec.GEMM_PARTIAL if sk > 1 else _mrec.GEMM_FULL
-            # with mrec_tower_dw the calls below only carry the REDUCE phase's
-            # arguments (its operands are never read: k-fragment images as stand-ins)
-            opnd = (lambda t: t.view(-1, 8)) if tdw else (lambda t: t)  # noqa: E731
-            for l in range(L):
-                N, K = widths[l + 1], widths[l]
-                bias_l = bs[l]
-                if lr is not None:
-                    c = _Call(opnd(dhs[l]), _mrec.LAYOUT_COL, opnd(xin[l]), _mrec.LAYOUT_COL, N, K, B, ph,
-                              ones_out=bias_l.detach() if bias_l is not None else None,
-                              out=Ws[l].detach(), out_dtype=torch.float32, split_k=sk, sgd_lr=lr,
-                              img_row=ctx.imgs[l][0], img_tr=ctx.imgs[l][1],
-                              img_kind=_mrec.IMG_TOWER)
-                    images_updated(Ws[l], "tower")
-                elif dpg is not None:
-                    c = _Call(opnd(dhs[l]), _mrec.LAYOUT_COL, opnd(xin[l]), _mrec.LAYOUT_COL, N, K, B, ph,
-                              ones_out=dpg[L + l], out=dpg[l], out_dtype=torch.float32,
-                              split_k=sk)
-                else:
-                    dWs[l] = torch.empty(N, K, dtype=torch.float32, device=dev)
-                    dbs[l] = (torch.empty(N, dtype=torch.float32, device=dev)
-                              if bias_l is not None else None)
-                    c = _Call(opnd(dhs[l]), _mrec.LAYOUT_COL, opnd(xin[l]), _mrec.LAYOUT_COL, N, K, B, ph,
-                              ones_out=dbs[l], out=dWs[l], out_dtype=torch.float32, split_k=sk)
-                calls.append(c)
-        # --- the head's parameters (w, b, ws, b2): fixed-order partial sums ---
-        hlr = sgd_lr(head_w, head_b, ws, b2)
-        det = (lambda t: None if t is None else t.detach())
-        hdp = dp_grads(head_w, head_b, ws, b2) if hlr is None else None
-        dW_h = db_h = dws = db2 = None
-        if hlr is not None and head_w.is_contiguous():
-            defer_head_finish(_HeadFinish(part, B, ctx.H, ctx.ns, None if one else g, hlr,
-                                          head_w.detach(), det(head_b), det(ws), det(b2)))
-        elif hdp is not None:
-            defer_head_finish(_HeadFinish(part, B, ctx.H, ctx.ns, None if one else g, None,
-                                          None, None, None, None, grads=hdp))
-        else:
-            f32 = dict(dtype=torch.float32, device=dev)
-            dW_h = torch.empty(1, ctx.H, **f32)
-            db_h = torch.empty(1, **f32) if head_b is not None else None
-            dws = torch.empty(ctx.ns, **f32) if ws is not None else None
-            db2 = torch.empty(1, **f32) if b2 is not None else None
-            _mrec.call("mrec_ctr_head_finish", part.data_ptr(), part.stride(0), B, ctx.H, ctx.ns,
-                       g.data_ptr(), 0, 0.0, None, None, None, None, dW_h.data_ptr(),
-                       _mrec.ptr(db_h), _mrec.ptr(dws), _mrec.ptr(db2), _mrec.stream_handle())
-        if calls and tdw:
-            _tower_dw(calls, dhs, xin, widths, B, tdw)
-            if lr is None and dpg is None:
-                _run([c.with_phase(_mrec.GEMM_REDUCE) for c in calls])
-            else:
-                for c in calls:
-                    _defer(c)
-        elif calls:
-            launch_multi(calls)
-            if calls[0].args[8] > 1:  # split-K partial slabs: now the reductions
-                if lr is None and dpg is None:
-                    # returned gradients: autograd may copy them on return, so they must
-                    # be complete before this backward returns
-                    _run([c.with_phase(_mrec.GEMM_REDUCE) for c in calls])
-                else:  # in-place SGD / flat DP buffer: ride in the next launches
-                    for c in calls:
-                        _defer(c)
-        else:
-            _flush_finish()
+        grads = _tower_param_grads(ctx.widths, ctx.Ws, ctx.bs, ctx.imgs, ctx.head, B, ctx.H, ctx.ns,
+                                   x0, hs, dhs, part, g, one, tdw,
+                                   any(ctx.needs_input_grad[5:5 + 2 * L]))
+        dWs, dbs, (dW_h, db_h, dws, db2) = grads
         return (dx0, dz if ctx.has_base else None, None, None, None, *dWs, *dbs,
                 dW_h, db_h, dws, db2)
+
+
+def _tower_param_grads(widths, Ws, bs, imgs, head, B: int, H: int, ns: int, x0, hs, dhs, part, g,
+                       one: bool, tdw: int, need_w: bool):
+    """The weight-gradient tail of a fused tower (BCE and given-dz modes): the L
+    layers' dW = dh^T [h | 1] (mrec_tower_dw from the k-fragment images, else the
+    generic split-K GEMMs) + the head parameters from the tower's partials; fused
+    SGD / flat DP buffer / returned gradients as the parameters ask.  ->
+    (dWs, dbs, (dW_h, db_h, dws, db2)), None where not returned."""
+    head_w, head_b, ws, b2 = head
+    L = len(Ws)
+    dev = part.device
+    xin = ([x0] if tdw else [x0[:, :widths[0]]]) + hs
+    # --- weight gradients of the L layers: one launch ---
+    lr = sgd_lr(*Ws, *bs)
+    dpg = dp_grads(*Ws, *bs) if lr is None else None
+    dWs, dbs = [None] * L, [None] * L
+    calls = []
+    if need_w:
+        sk = tdw or _split_tower(widths, B)
+        ph = _mrec.GEMM_PARTIAL if sk > 1 else _mrec.GEMM_FULL
+        # with mrec_tower_dw the calls below only carry the REDUCE phase's
+        # arguments (its operands are never read: k-fragment images as stand-ins)
+        opnd = (lambda t: t.view(-1, 8)) if tdw else (lambda t: t)  # noqa: E731
+        for l in range(L):
+            N, K = widths[l + 1], widths[l]
+            bias_l = bs[l]
+            if lr is not None:
+                c = _Call(opnd(dhs[l]), _mrec.LAYOUT_COL, opnd(xin[l]), _mrec.LAYOUT_COL, N, K, B, ph,
+                          ones_out=bias_l.detach() if bias_l is not None else None,
+                          out=Ws[l].detach(), out_dtype=torch.float32, split_k=sk, sgd_lr=lr,
+                          img_row=imgs[l][0], img_tr=imgs[l][1],
+                          img_kind=_mrec.IMG_TOWER)
+                images_updated(Ws[l], "tower")
+            elif dpg is not None:
+                c = _Call(opnd(dhs[l]), _mrec.LAYOUT_COL, opnd(xin[l]), _mrec.LAYOUT_COL, N, K, B, ph,
+                          ones_out=dpg[L + l], out=dpg[l], out_dtype=torch.float32,
+                          split_k=sk)
+            else:
+                dWs[l] = torch.empty(N, K, dtype=torch.float32, device=dev)
+                dbs[l] = (torch.empty(N, dtype=torch.float32, device=dev)
+                          if bias_l is not None else None)
+                c = _Call(opnd(dhs[l]), _mrec.LAYOUT_COL, opnd(xin[l]), _mrec.LAYOUT_COL, N, K, B, ph,
+                          ones_out=dbs[l], out=dWs[l], out_dtype=torch.float32, split_k=sk)
+            calls.append(c)
+    # --- the head's parameters (w, b, ws, b2): fixed-order partial sums ---
+    hlr = sgd_lr(head_w, head_b, ws, b2)
+    det = (lambda t: None if t is None else t.detach())
+    hdp = dp_grads(head_w, head_b, ws, b2) if hlr is None else None
+    dW_h = db_h = dws = db2 = None
+    if hlr is not None and head_w.is_contiguous():
+        defer_head_finish(_HeadFinish(part, B, H, ns, None if one else g, hlr,
+                                      head_w.detach(), det(head_b), det(ws), det(b2)))
+    elif hdp is not None:
+        defer_head_finish(_HeadFinish(part, B, H, ns, None if one else g, None,
+                                      None, None, None, None, grads=hdp))
+    else:
+        f32 = dict(dtype=torch.float32, device=dev)
+        dW_h = torch.empty(1, H, **f32)
+        db_h = torch.empty(1, **f32) if head_b is not None else None
+        dws = torch.empty(ns, **f32) if ws is not None else None
+        db2 = torch.empty(1, **f32) if b2 is not None else None
+        _mrec.call("mrec_ctr_head_finish", part.data_ptr(), part.stride(0), B, H, ns,
+                   g.data_ptr(), 0, 0.0, None, None, None, None, dW_h.data_ptr(),
+                   _mrec.ptr(db_h), _mrec.ptr(dws), _mrec.ptr(db2), _mrec.stream_handle())
+    if calls and tdw:
+        _tower_dw(calls, dhs, xin, widths, B, tdw)
+        if lr is None and dpg is None:
+            _run([c.with_phase(_mrec.GEMM_REDUCE) for c in calls])
+        else:
+            for c in calls:
+                _defer(c)
+    elif calls:
+        launch_multi(calls)
+        if calls[0].args[8] > 1:  # split-K partial slabs: now the reductions
+            if lr is None and dpg is None:
+                # returned gradients: autograd may copy them on return, so they must
+                # be complete before this backward returns
+                _run([c.with_phase(_mrec.GEMM_REDUCE) for c in calls])
+            else:  # in-place SGD / flat DP buffer: ride in the next launches
+                for c in calls:
+                    _defer(c)
+    else:
+        _flush_finish()
+    return dWs, dbs, (dW_h, db_h, dws, db2)
 
 
 def _tower_dw(calls, dhs, xin, widths, B: int, splits: int):
@@ -1265,3 +1301,99 @@ def tower_bce(x0: torch.Tensor, mlp, head: torch.nn.Linear, base: Optional[torch
     params = ([l.weight for l in lins] + [l.bias for l in lins] +
               [head.weight, head.bias, ws, b2])
     return _TowerBCEFn.apply(x0, base, xs, y, len(lins), *params)
+
+
+class _ScoreTowerFn(torch.autograd.Function):
+    """s = MLP(x0) . w + b per row (fp32 [B]): DIN's attention unit (att_mlp +
+    att_out over the [q, k, q-k, q*k] rows) on the fused tower.  Forward = one
+    MREC_TOWER_FORWARD launch (the scores only, nothing else leaves LDS); backward =
+    one MREC_TOWER_GIVEN_DZ launch with dz = ds (the forward recomputed in LDS:
+    dx0 and every pre-activation gradient, the k-fragment images) + mrec_tower_dw +
+    the head finish, as the BCE tower's backward."""
+
+    @staticmethod
+    def _args(x0, widths, imgs, bsd, hw, hb):
+        a = _mrec.TowerArgs()
+        L = len(widths) - 1
+        a.batch, a.n_layers = x0.shape[0], L
+        for l in range(L + 1):
+            a.width[l] = widths[l]
+        a.x0, a.ld_x0 = x0.data_ptr(), x0.stride(0)
+        for l in range(L):
+            a.w_fwd[l], a.w_bwd[l] = imgs[l][0].data_ptr(), imgs[l][1].data_ptr()
+            a.bias[l] = _mrec.ptr(bsd[l])
+        a.head_w, a.head_b = hw.data_ptr(), _mrec.ptr(hb)
+        return a
+
+    @staticmethod
+    def forward(ctx, x0, n_layers, *params):
+        L = n_layers
+        Ws, bs = params[:L], params[L:2 * L]
+        head_w, head_b = params[2 * L:2 * L + 2]
+        B = x0.shape[0]
+        widths = [Ws[0].shape[1]] + [W.shape[0] for W in Ws]
+        imgs = [tower_images(W) for W in Ws]
+        f32 = lambda t: None if t is None else t.detach().float().contiguous()  # noqa: E731
+        bsd, hw, hb = [f32(b) for b in bs], f32(head_w).reshape(-1), f32(head_b)
+        z = torch.empty(B, dtype=torch.float32, device=x0.device)
+        a = _ScoreTowerFn._args(x0, widths, imgs, bsd, hw, hb)
+        a.mode, a.z, a.ldp = _mrec.TOWER_FORWARD, z.data_ptr(), _r8(widths[L] + 1)
+        _mrec.call("mrec_tower_fwd_bwd", ctypes.byref(a), _mrec.stream_handle())
+        ctx.save_for_backward(x0)
+        ctx.L, ctx.widths, ctx.Ws, ctx.bs, ctx.imgs = L, widths, Ws, bs, imgs
+        ctx.head = (head_w, head_b, None, None)
+        ctx.keep = (bsd, hw, hb)
+        return z
+
+    @staticmethod
+    def backward(ctx, ds):
+        x0, = ctx.saved_tensors
+        L, widths = ctx.L, ctx.widths
+        B = x0.shape[0]
+        dev = x0.device
+        ds = ds.detach().float().reshape(B).contiguous()
+        need_w = any(ctx.needs_input_grad[2:2 + 2 * L])
+        tdw = _tdw_splits(B, widths) if need_w else 0
+        if tdw:
+            kf = lambda n: torch.empty(int(_mrec.lib().mrec_kfrag_elems(B, n)), dtype=_BF16,  # noqa: E731
+                                       device=dev)
+            hs = [kf(widths[l + 1]) for l in range(L - 1)]
+            dhs = [kf(widths[l + 1]) for l in range(L)]
+            x0_img = kf(widths[0])
+        else:
+            hs = [_alloc(B, widths[l + 1], _BF16, dev) for l in range(L - 1)]
+            dhs = [_alloc(B, widths[l + 1], _BF16, dev) for l in range(L)]
+            x0_img = None
+        dx0 = None
+        if ctx.needs_input_grad[0]:
+            Kx = x0.shape[1]
+            dx0 = (_alloc(B, Kx, _BF16, dev) if _r8(Kx) == _r8(widths[0]) else
+                   torch.zeros(B, _r8(Kx), dtype=_BF16, device=dev)[:, :Kx])
+        H = widths[L]
+        ldp = _r8(H + 1)
+        part = torch.empty(int(_mrec.lib().mrec_ctr_head_parts(B)), ldp, dtype=torch.float32,
+                           device=dev)
+        bsd, hw, hb = ctx.keep
+        a = _ScoreTowerFn._args(x0, widths, ctx.imgs, bsd, hw, hb)
+        for l in range(L):
+            a.dh_out[l], a.ld_dh[l] = dhs[l].data_ptr(), dhs[l].stride(0)
+            if l < L - 1:
+                a.h_out[l], a.ld_h[l] = hs[l].data_ptr(), hs[l].stride(0)
+        a.kfrag, a.x0_img = int(bool(tdw)), _mrec.ptr(x0_img)
+        a.dx0, a.ld_dx0 = _mrec.ptr(dx0), dx0.stride(0) if dx0 is not None else 0
+        a.part, a.ldp = part.data_ptr(), ldp
+        a.mode, a.dz_in = _mrec.TOWER_GIVEN_DZ, ds.data_ptr()
+        _mrec.call("mrec_tower_fwd_bwd", ctypes.byref(a), _mrec.stream_handle())
+        g = grad_one(dev)
+        dWs, dbs, (dW_h, db_h, _, _) = _tower_param_grads(
+            widths, ctx.Ws, ctx.bs, ctx.imgs, ctx.head, B, H, 0, x0_img if tdw else x0, hs, dhs,
+            part, g, True, tdw, need_w)
+        return (dx0, None, *dWs, *dbs, dW_h, db_h)
+
+
+def score_tower(x0: torch.Tensor, mlp, head: torch.nn.Linear) -> torch.Tensor:
+    """MLP(x0) . head.weight + head.bias per row (fp32 [B]) on the fused tower
+    (caller checks ``tower_supported``): DIN's attention-unit scores."""
+    lins = _mlp_linears(mlp)
+    params = [l.weight for l in lins] + [l.bias for l in lins] + [head.weight, head.bias]
+    return _ScoreTowerFn.apply(x0, len(lins), *params)

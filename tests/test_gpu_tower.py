@@ -191,3 +191,70 @@ def test_train_steps_tower_on_vs_off(gpu, model):
         d = (sa[k] - sb[k]).abs().max().item()
         scale = sb[k].abs().max().item() + 1e-12
         assert d <= 2e-2 * scale, (k, d / scale)
+
+
+@pytest.mark.parametrize("widths,B", [((128, 80, 40), 3200), ((45, 70, 33), 1000),
+                                      ((128, 80, 40), 24000)])
+def test_score_tower_matches_layered_path_and_fp64(gpu, widths, B):
+    """The score tower (DIN's attention unit: MREC_TOWER_FORWARD scores, then a
+    MREC_TOWER_GIVEN_DZ backward that recomputes the forward in LDS) against the
+    layered path (one GEMM per layer + Linear(h, 1): the same bf16 rounding points)
+    with the bar of the BCE tower's test, and against the fp64 oracle on the same
+    bf16 weights / inputs (l2 within 8e-2).  The 24,000-row case runs
+    mrec_tower_dw with many K slices."""
+    from pytorchrec_amd import dense as D
+    mlp, head = _mlp(widths, gpu, seed=B + 7)
+    x0 = _x0(B, widths[0], gpu, seed=B + 8)
+    g = torch.Generator().manual_seed(B + 9)
+    ds = (torch.randn(B, 1, generator=g) * 1e-3).to(gpu)
+    lins = [d.linear for d in mlp.mlp]
+    params = list(mlp.parameters()) + list(head.parameters())
+
+    xg = x0.detach().requires_grad_()
+    assert D.tower_supported(xg, mlp, head)
+    s = D.score_tower(xg, mlp, head).reshape(-1, 1)
+    s.backward(ds)
+    got = {"s": s.detach(), "dx0": xg.grad}
+    for i, l in enumerate(lins):
+        got[f"dW{i}"], got[f"db{i}"] = l.weight.grad.clone(), l.bias.grad.clone()
+    got["dW_head"], got["db_head"] = head.weight.grad.clone(), head.bias.grad.clone()
+
+    for p in params:
+        p.grad = None
+    xl = x0.detach().requires_grad_()
+    sl = D.linear(mlp(xl), head.weight, head.bias, out_dtype=torch.float32)
+    sl.backward(ds)
+    want = {"s": sl.detach(), "dx0": xl.grad}
+    for i, l in enumerate(lins):
+        want[f"dW{i}"], want[f"db{i}"] = l.weight.grad, l.bias.grad
+    want["dW_head"], want["db_head"] = head.weight.grad, head.bias.grad
+    # the layered head rounds dh_L = ds w at a different point (its Linear(h, 1)
+    # backward), so sums with heavy cancellation (the bias gradients) differ by
+    # ~2^-9 of their magnitude: a 4e-3 mean bar here, the tight bar elsewhere
+    for name in want:
+        a, b = got[name].double().cpu(), want[name].double().cpu().reshape(got[name].shape)
+        mag = float(b.abs().max()) + 1e-30
+        err = (a - b).abs()
+        assert float(err.mean()) <= 4e-3 * mag, (name, float(err.mean()) / mag)
+        assert float((err > 2e-2 * mag).double().mean()) <= 1e-3, name
+
+    layers = [(ref.bf16_round(l.weight.detach().cpu().numpy()), l.bias.detach().cpu().numpy())
+              for l in lins]
+    acts = ref.mlp_fwd(x0.detach().float().cpu().numpy(), layers)
+    hw = head.weight.detach().cpu().numpy().reshape(-1)
+    z = acts[-1] @ hw + float(head.bias)
+    dz = ds.cpu().numpy().reshape(-1).astype(np.float64)
+    dx_ref, lgr = ref.mlp_bwd(acts, layers, dz[:, None] * hw[None, :])
+
+    def close(a, w, name):
+        a = a.detach().double().cpu().numpy().reshape(w.shape)
+        l2 = np.linalg.norm(a - w) / (np.linalg.norm(w) + 1e-30)
+        assert l2 <= 8e-2, (name, l2)
+
+    close(got["s"], z, "s")
+    close(got["dx0"], dx_ref, "dx0")
+    for l, (wW, wb) in enumerate(lgr):
+        close(got[f"dW{l}"], wW, f"dW{l}")
+        close(got[f"db{l}"], wb, f"db{l}")
+    close(got["dW_head"].reshape(-1), acts[-1].T @ dz, "dW_head")
+    close(got["db_head"], np.array([dz.sum()]), "db_head")

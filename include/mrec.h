@@ -32,7 +32,7 @@
 extern "C" {
 #endif
 
-#define MREC_ABI_VERSION 16
+#define MREC_ABI_VERSION 17
 #define MREC_MAX_TABLES 64      /* tables per table bank / per call */
 #define MREC_BWD_MAX_BATCH 8192  /* lookups per table per plan/apply call */
 #define MREC_BWD_HASH_MAX_BATCH 4096  /* batches up to this use the hash plan */
@@ -803,6 +803,47 @@ mrec_status mrec_din_feat_bwd_rows(const void *dfeat, int64_t lddf, const void *
                                    const void *q, int64_t ldq, const void *k, int64_t ldk,
                                    int64_t batch, int32_t L, int32_t E, const float *dk,
                                    int64_t lddk, void *d_rows, int64_t ld_rows, mrec_stream stream);
+
+/*
+ * Fused DIN attention unit (ABI 17): one launch each way replaces
+ * mrec_din_feat_fwd + the attention MLP's GEMMs + Linear(H2, 1) + mrec_din_pool_fwd
+ * (forward) and mrec_din_pool_bwd + the GEMMs' backward + mrec_din_feat_bwd_rows
+ * (backward).  Per sample, in LDS only: X = [q | k_j | q - k_j | q * k_j] (bf16),
+ * s_j = w3 . relu(W2 relu(W1 x_j + b1) + b2) + b3 (bf16 MFMA operands, fp32
+ * accumulation), the masked softmax / pooling of mrec_din_pool_fwd, and in the
+ * backward the MLP recomputed, dX kept fp32 into the rows' gradient.
+ *   rows    gathered bf16 rows [q (batch) | k (batch L)] (row stride ld_rows, 16-B
+ *           aligned), his [batch, L] ids (validity: his > 0 or j == 0);
+ *   w1 [H1, 4E] (ldw1), b1 [H1], w2 [H2, H1] (ldw2), b2 [H2], w3 [H2], b3 [1]:
+ *           fp32 masters (nn.Linear layout; converted to bf16 in the kernel);
+ *   fwd:    a [batch, L] softmax weights (saved for the backward), top [batch, ldt]
+ *           = [q | u | 0-pad] bf16;
+ *   bwd:    d_rows (same layout as rows) = the rows' bf16 gradient, part
+ *           [parts][mrec_din_att_param_count] fp32 weight-gradient partials
+ *           (parts = mrec_din_att_parts(batch));
+ *   wgrad:  fixed-order sum of the partials into grads (flat [dW1 | dW2 | db1 | db2 |
+ *           dw3 | db3]) or, with grads == NULL, SGD in place: p -= lr * grad.
+ * Compiled shapes (mrec_din_att_supported): (E, H1, H2) with E in {16, 32} and
+ * the tile counts of (32, 80, 40) (config C4) or (16, <= 32, <= 16); L <= 64.
+ */
+int32_t mrec_din_att_supported(int32_t E, int32_t H1, int32_t H2);
+int64_t mrec_din_att_parts(int64_t batch);
+int64_t mrec_din_att_param_count(int32_t E, int32_t H1, int32_t H2);
+mrec_status mrec_din_att_fwd(const void *rows, int64_t ld_rows, const int32_t *his, int64_t ld_his,
+                             int64_t batch, int32_t L, int32_t E, const float *w1, int64_t ldw1,
+                             const float *b1, int32_t H1, const float *w2, int64_t ldw2,
+                             const float *b2, int32_t H2, const float *w3, const float *b3,
+                             float *a, void *top, int64_t ldt, mrec_stream stream);
+mrec_status mrec_din_att_bwd(const void *rows, int64_t ld_rows, int64_t batch, int32_t L,
+                             int32_t E, const float *w1, int64_t ldw1, const float *b1, int32_t H1,
+                             const float *w2, int64_t ldw2, const float *b2, int32_t H2,
+                             const float *w3, const float *b3, const float *a, const void *dtop,
+                             int64_t lddt, void *d_rows, int64_t ld_drows, float *part,
+                             int64_t parts, mrec_stream stream);
+mrec_status mrec_din_att_wgrad(const float *part, int64_t parts, int32_t E, int32_t H1, int32_t H2,
+                               float *grads, float lr, float *w1, int64_t ldw1, float *b1,
+                               float *w2, int64_t ldw2, float *b2, float *w3, float *b3,
+                               mrec_stream stream);
 
 /*
  * Fused CTR head + BCE-with-logits (forward AND the loss gradient, one pass over h;

@@ -1,0 +1,892 @@
+// DIN attention unit fused per sample (config C4).
+//
+// One workgroup (4 waves) per sample b at a time, persistent over samples.  The
+// attention-unit input X = [q | k_j | q - k_j | q * k_j] (64 padded history rows x
+// 4E), the MLP activations and every gradient live in LDS only; the MLP weights
+// are staged once per workgroup as bf16 in both operand orders.  What the layered
+// path (mrec_din_feat_fwd + three mrec_gemm layers + mrec_din_pool_*) moved
+// through HBM per step at C4 -- the [B L, 128] input, the [B L, 80] / [B L, 40]
+// activations and their gradients, ~0.4 GB -- never leaves the CU.
+//
+//   forward   s_j = w3 . relu(W2 relu(W1 x_j + b1) + b2) + b3
+//             a   = softmax_j over valid j (his[b, j] > 0 or j == 0), invalid -> 0
+//             top[b] = [q | sum_j a_j k_j | 0-pad]          (same math as din.hip)
+//   backward  (given dtop and the saved a) ds_j = a_j (du.k_j - sum_i a_i du.k_i),
+//             the MLP recomputed and back-propagated with bf16 MFMA operands
+//             (fp32 accumulation, as the layered GEMMs), dX in fp32 straight into
+//             dk_j = a_j du + df_k - df_(q-k) + df_(q*k) q and
+//             dq   = dtop_q + sum_j (df_q + df_(q-k) + df_(q*k) k_j), written as
+//             ONE bf16 gradient of the gathered rows; weight gradients accumulated
+//             in MFMA registers across the workgroup's samples, one partial per
+//             workgroup, summed in fixed order by din_att_wgrad_kernel.
+//
+// All GEMMs are v_mfma_f32_16x16x32_bf16 with both operands read as 16-B LDS
+// vectors: lane l holds A[m = l % 16][k = 8 (l / 16) .. + 8] and the B^T row
+// B[k .. + 8][n = l % 16]; so every operand buffer is stored "row = output index,
+// contiguous along k" and the reductions over history rows read transposed copies
+// ([feature][row]) written beside the row-major ones.
+#include "common.h"
+
+namespace mrec {
+
+typedef short da_bf16x8 __attribute__((ext_vector_type(8)));
+typedef float da_f32x4 __attribute__((ext_vector_type(4)));
+
+constexpr int DA_ROWS = 64;              // history positions per sample, padded
+constexpr int DA_THREADS = 256;          // 4 waves; wave w owns rows 16w .. 16w + 15
+constexpr int DA_LDT = DA_ROWS + 8;      // row stride of the [feature][row] buffers
+
+struct DinAttArgs {
+  const uint16_t *rows;  // gathered rows [q (batch) | k (batch L)] bf16
+  int64_t ld_rows;
+  const int32_t *his;
+  int64_t ld_his;
+  const float *w1, *b1, *w2, *b2, *w3, *b3;  // fp32 masters, nn.Linear layout
+  int64_t ldw1, ldw2;
+  int64_t batch;
+  int L, H1, H2;
+  float *a;  // [batch, L] softmax weights (written by fwd, read by bwd)
+  uint16_t *top;
+  int64_t ldt;
+  const uint16_t *dtop;
+  int64_t lddt;
+  uint16_t *drows;
+  int64_t ld_drows;
+  float *part;  // [gridDim.x][P] weight-gradient partials
+  int64_t P;
+};
+
+__device__ __forceinline__ da_bf16x8 da_frag(const uint16_t *base, int ld, int r0, int k0,
+                                             int lane) {
+  return *reinterpret_cast<const da_bf16x8 *>(base + (r0 + (lane & 15)) * ld + k0 +
+                                              8 * (lane >> 4));
+}
+
+__device__ __forceinline__ da_f32x4 da_mfma(da_bf16x8 a, da_bf16x8 b, da_f32x4 c) {
+  return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
+}
+
+// sum over the 16 lanes of a row group (lanes 16 g .. 16 g + 15)
+// (DPP row rotations, no LDS crossbar; lanes may differ in the last bit, callers
+// use one lane's value)
+__device__ __forceinline__ float da_sum16(float v) {
+  v += dpp_f32<0x128>(v);  // row_ror:8
+  v += dpp_f32<0x124>(v);  // row_ror:4
+  v += dpp_f32<0x122>(v);  // row_ror:2
+  return v + dpp_f32<0x121>(v);  // row_ror:1
+}
+
+template <int E, int H1T, int H1K, int H2T, int H2K>
+struct DaShape {
+  static constexpr int E4 = 4 * E;
+  static constexpr int KT1 = E4 / 32;  // k steps of layer 1
+  static constexpr int NTX = E4 / 16;  // column tiles of X
+  static constexpr int LDX = E4 + 8;
+  static constexpr int H1N = 16 * H1T;  // layer-1 outputs, tile padded
+  static constexpr int H1P = 32 * H1K;  // ... k-step padded
+  static constexpr int LDH = H1P + 8;
+  static constexpr int H2N = 16 * H2T;
+  static constexpr int H2P = 32 * H2K;
+  static constexpr int LDW2T = H2P + 8;
+  static_assert(E % 16 == 0 && E4 % 32 == 0, "E must be a multiple of 16");
+  static_assert(H1N <= H1P && H2N <= H2P, "k-step padding covers the tiles");
+  static_assert(H2P <= H1P, "dZ2 aliases H1 with H1's row stride");
+  static_assert(H1P <= E4, "dZ1 aliases X");
+  // bf16 element offsets of the LDS buffers (16-B aligned: every size % 8 == 0)
+  static constexpr int oX = 0;                       // X [64][LDX]   (bwd: dZ1 [64][LDH])
+  static constexpr int oH1 = oX + DA_ROWS * LDX;     // H1 [64][LDH]  (bwd: dZ2 [64][LDH])
+  static constexpr int oW1 = oH1 + DA_ROWS * LDH;    // W1 [H1N][LDX]
+  static constexpr int oW2 = oW1 + H1N * LDX;        // W2 [H2N][LDH]
+  static constexpr int fwd_end = oW2 + H2N * LDH;
+  static constexpr int oXT = fwd_end;                // X^T [E4][LDT]
+  static constexpr int oH1T = oXT + E4 * DA_LDT;     // H1^T [H1N][LDT]
+  static constexpr int oZ1T = oH1T + H1N * DA_LDT;   // dZ1^T [H1N][LDT]
+  static constexpr int oZ2T = oZ1T + H1N * DA_LDT;   // dZ2^T [H2N][LDT]
+  static constexpr int oW1T = oZ2T + H2N * DA_LDT;   // W1^T [E4][LDH]
+  static constexpr int oW2T = oW1T + E4 * LDH;       // W2^T [H1N][LDW2T]
+  static constexpr int bwd_end = oW2T + H1N * LDW2T;
+  // fp32 tail: b1 [H1N], b2 [H2N], w3 [H2N], q [E], du [E], g [64], dq parts [4][E]
+  static constexpr int nf32 = H1N + 2 * H2N + 2 * E + DA_ROWS + 4 * E;
+  static constexpr size_t fwd_bytes = fwd_end * 2 + (H1N + 2 * H2N + 2 * DA_ROWS + DA_THREADS) * 4;
+  static constexpr size_t bwd_bytes = bwd_end * 2 + nf32 * 4;
+};
+
+__device__ __forceinline__ void da_zero_lds(char *lds, size_t bytes) {
+  for (size_t o = threadIdx.x * 16; o < bytes; o += DA_THREADS * 16)
+    *reinterpret_cast<uint4 *>(lds + o) = make_uint4(0, 0, 0, 0);
+}
+
+// Weights once per workgroup: every float4 load of a thread is issued before any
+// is converted (a load -> store loop of ~55 dependent L2 round trips per thread
+// cost ~40 us per launch).  Needs ldw1, ldw2, H1 multiples of 4, 16-B aligned w1 / w2.
+template <class S, bool BWD>
+__device__ void da_stage_weights(const DinAttArgs &p, uint16_t *sm, float *sb1, float *sb2,
+                                 float *sw3) {
+  const int tid = threadIdx.x;
+  constexpr int Q1 = S::H1N * S::E4 / 4, N1 = (Q1 + DA_THREADS - 1) / DA_THREADS;
+  constexpr int Q2 = S::H2N * S::H1N / 4, N2 = (Q2 + DA_THREADS - 1) / DA_THREADS;
+  float4 v1[N1], v2[N2];
+#pragma unroll
+  for (int it = 0; it < N1; ++it) {
+    const int i = (tid + it * DA_THREADS) * 4, n = i / S::E4, k = i - n * S::E4;
+    v1[it] = (i < S::H1N * S::E4 && n < p.H1)
+                 ? *reinterpret_cast<const float4 *>(p.w1 + n * p.ldw1 + k)
+                 : make_float4(0.f, 0.f, 0.f, 0.f);
+  }
+#pragma unroll
+  for (int it = 0; it < N2; ++it) {
+    const int i = (tid + it * DA_THREADS) * 4, n = i / S::H1N, k = i - n * S::H1N;
+    v2[it] = (i < S::H2N * S::H1N && n < p.H2 && k < p.H1)
+                 ? *reinterpret_cast<const float4 *>(p.w2 + n * p.ldw2 + k)
+                 : make_float4(0.f, 0.f, 0.f, 0.f);
+  }
+  for (int i = tid; i < S::H1N; i += DA_THREADS) sb1[i] = i < p.H1 ? p.b1[i] : 0.f;
+  for (int i = tid; i < S::H2N; i += DA_THREADS) {
+    sb2[i] = i < p.H2 ? p.b2[i] : 0.f;
+    sw3[i] = i < p.H2 ? p.w3[i] : 0.f;
+  }
+#pragma unroll
+  for (int it = 0; it < N1; ++it) {
+    const int i = (tid + it * DA_THREADS) * 4, n = i / S::E4, k = i - n * S::E4;
+    if (i >= S::H1N * S::E4) continue;
+    const uint16_t h[4] = {f32_to_bf16_rne(v1[it].x), f32_to_bf16_rne(v1[it].y),
+                           f32_to_bf16_rne(v1[it].z), f32_to_bf16_rne(v1[it].w)};
+    *reinterpret_cast<uint2 *>(sm + S::oW1 + n * S::LDX + k) =
+        make_uint2(h[0] | (static_cast<uint32_t>(h[1]) << 16),
+                   h[2] | (static_cast<uint32_t>(h[3]) << 16));
+    if constexpr (BWD) {
+#pragma unroll
+      for (int c = 0; c < 4; ++c) sm[S::oW1T + (k + c) * S::LDH + n] = h[c];
+    }
+  }
+#pragma unroll
+  for (int it = 0; it < N2; ++it) {
+    const int i = (tid + it * DA_THREADS) * 4, n = i / S::H1N, k = i - n * S::H1N;
+    if (i >= S::H2N * S::H1N) continue;
+    const uint16_t h[4] = {f32_to_bf16_rne(v2[it].x), f32_to_bf16_rne(v2[it].y),
+                           f32_to_bf16_rne(v2[it].z), f32_to_bf16_rne(v2[it].w)};
+    *reinterpret_cast<uint2 *>(sm + S::oW2 + n * S::LDH + k) =
+        make_uint2(h[0] | (static_cast<uint32_t>(h[1]) << 16),
+                   h[2] | (static_cast<uint32_t>(h[3]) << 16));
+    if constexpr (BWD) {
+#pragma unroll
+      for (int c = 0; c < 4; ++c) sm[S::oW2T + (k + c) * S::LDW2T + n] = h[c];
+    }
+  }
+}
+
+// row chunk task of the X builders: thread t -> history row j, 8 columns at c
+template <int E>
+struct DaTask {
+  static constexpr int CH = E / 8;  // 16-B chunks per q / k row
+  int j, c;
+  bool on;
+  __device__ DaTask(int t) : j(t / CH), c((t % CH) * 8), on(t < DA_ROWS * CH) {}
+};
+
+// global inputs of one sample for thread t, loaded one sample ahead (their
+// latency overlaps the previous sample's LDS / MFMA phases)
+struct DaRaw {
+  uint4 q, k, du;  // q / k chunk (bf16 x 8), du chunk (bwd)
+  float a;         // bwd: a[b, lane]
+  int valid;       // fwd: history position `lane` valid
+};
+
+template <int E, bool BWD>
+__device__ __forceinline__ DaRaw da_load(const DinAttArgs &p, int64_t b, const DaTask<E> &t,
+                                         int lane) {
+  DaRaw r;
+  r.q = r.k = r.du = make_uint4(0, 0, 0, 0);
+  r.a = 0.f;
+  r.valid = 0;
+  if (t.on) {
+    r.q = *reinterpret_cast<const uint4 *>(p.rows + b * p.ld_rows + t.c);
+    if (t.j < p.L)
+      r.k = *reinterpret_cast<const uint4 *>(p.rows + (p.batch + b * p.L + t.j) * p.ld_rows + t.c);
+    if constexpr (BWD)
+      r.du = *reinterpret_cast<const uint4 *>(p.dtop + b * p.lddt + E + t.c);
+  }
+  if constexpr (BWD) {
+    if (lane < p.L) r.a = p.a[b * p.L + lane];
+  } else {
+    r.valid = lane < p.L && (lane == 0 || p.his[b * p.ld_his + lane] > 0);
+  }
+  return r;
+}
+
+// X row j of sample b: [q | k | q - k | q * k] as bf16 (the rounding of
+// din_feat_fwd_kernel); rows j >= L are zero.  Returns k (fp32) and q (fp32).
+template <class S, int E, bool TR>
+__device__ __forceinline__ void da_build_x(const DinAttArgs &p, const DaRaw &raw,
+                                           const DaTask<E> &t, uint16_t *sm, float (&qv)[8],
+                                           float (&kv)[8]) {
+  const uint4 qraw = raw.q, kraw = raw.k;
+  const bool real = t.j < p.L;
+  Vec<uint16_t>::to_f32(qraw, qv);
+  Vec<uint16_t>::to_f32(kraw, kv);
+  float d[8], m[8];
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    d[i] = qv[i] - kv[i];
+    m[i] = qv[i] * kv[i];
+  }
+  uint4 dq = make_uint4(pack_bf16x2(d[0], d[1]), pack_bf16x2(d[2], d[3]), pack_bf16x2(d[4], d[5]),
+                        pack_bf16x2(d[6], d[7]));
+  uint4 mq = make_uint4(pack_bf16x2(m[0], m[1]), pack_bf16x2(m[2], m[3]), pack_bf16x2(m[4], m[5]),
+                        pack_bf16x2(m[6], m[7]));
+  uint4 qq = qraw;
+  if (!real) qq = dq = mq = make_uint4(0, 0, 0, 0);
+  uint16_t *x = sm + S::oX + t.j * S::LDX + t.c;
+  *reinterpret_cast<uint4 *>(x) = qq;
+  *reinterpret_cast<uint4 *>(x + E) = kraw;
+  *reinterpret_cast<uint4 *>(x + 2 * E) = dq;
+  *reinterpret_cast<uint4 *>(x + 3 * E) = mq;
+  if constexpr (TR) {
+    uint16_t *xt = sm + S::oXT + t.c * DA_LDT + t.j;
+    const uint4 parts[4] = {qq, kraw, dq, mq};
+#pragma unroll
+    for (int g = 0; g < 4; ++g) {
+      const uint32_t u[4] = {parts[g].x, parts[g].y, parts[g].z, parts[g].w};
+#pragma unroll
+      for (int i = 0; i < 8; ++i)
+        xt[(g * E + i) * DA_LDT] = static_cast<uint16_t>(u[i >> 1] >> (16 * (i & 1)));
+    }
+  }
+}
+
+// layer 1 of this wave's rows: acc[n] = X[rows] W1^T (n-th 16-column tile)
+template <class S, int H1T>
+__device__ __forceinline__ void da_layer1(const uint16_t *sm, int w, int lane,
+                                          da_f32x4 (&acc)[H1T]) {
+#pragma unroll
+  for (int n = 0; n < H1T; ++n) acc[n] = da_f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int s = 0; s < S::KT1; ++s) {
+    const da_bf16x8 a = da_frag(sm + S::oX, S::LDX, 16 * w, 32 * s, lane);
+#pragma unroll
+    for (int n = 0; n < H1T; ++n)
+      acc[n] = da_mfma(a, da_frag(sm + S::oW1, S::LDX, 16 * n, 32 * s, lane), acc[n]);
+  }
+}
+
+// layer 2 of this wave's rows: acc[n] = H1[rows] W2^T
+template <class S, int H1K, int H2T>
+__device__ __forceinline__ void da_layer2(const uint16_t *sm, int w, int lane,
+                                          da_f32x4 (&acc)[H2T]) {
+#pragma unroll
+  for (int n = 0; n < H2T; ++n) acc[n] = da_f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int s = 0; s < H1K; ++s) {
+    const da_bf16x8 a = da_frag(sm + S::oH1, S::LDH, 16 * w, 32 * s, lane);
+#pragma unroll
+    for (int n = 0; n < H2T; ++n)
+      acc[n] = da_mfma(a, da_frag(sm + S::oW2, S::LDH, 16 * n, 32 * s, lane), acc[n]);
+  }
+}
+
+// ---------------------------------------------------------------------------
+// forward: scores, masked softmax, pooling -> top, a
+// ---------------------------------------------------------------------------
+template <int E, int H1T, int H1K, int H2T, int H2K>
+__global__ __launch_bounds__(DA_THREADS) void din_att_fwd_kernel(DinAttArgs p) {
+  using S = DaShape<E, H1T, H1K, H2T, H2K>;
+  extern __shared__ __attribute__((aligned(16))) char da_lds[];
+  uint16_t *sm = reinterpret_cast<uint16_t *>(da_lds);
+  float *sb1 = reinterpret_cast<float *>(da_lds + S::fwd_end * 2);
+  float *sb2 = sb1 + S::H1N;
+  float *sw3 = sb2 + S::H2N;
+  float *ss = sw3 + S::H2N;  // scores [64]
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  da_zero_lds(da_lds, S::fwd_end * 2);
+  __syncthreads();
+  da_stage_weights<S, false>(p, sm, sb1, sb2, sw3);
+  const float b3 = p.b3[0];
+  const DaTask<E> task(tid);
+  float *sa = ss + DA_ROWS;  // softmax weights [64]
+  float *su = sa + DA_ROWS;  // pooled-sum parts [DA_THREADS / E][E]
+  DaRaw cur = {};
+  if (blockIdx.x < p.batch) cur = da_load<E, false>(p, blockIdx.x, task, lane);
+  for (int64_t b = blockIdx.x; b < p.batch; b += gridDim.x) {
+    DaRaw nxt = {};
+    if (b + gridDim.x < p.batch) nxt = da_load<E, false>(p, b + gridDim.x, task, lane);
+    if (task.on) {
+      float qv[8], kv[8];
+      da_build_x<S, E, false>(p, cur, task, sm, qv, kv);
+    }
+    __syncthreads();
+    {
+      da_f32x4 acc[H1T];
+      da_layer1<S, H1T>(sm, w, lane, acc);
+#pragma unroll
+      for (int n = 0; n < H1T; ++n) {
+        const int col = 16 * n + (lane & 15);
+        const float bias = sb1[col];
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const int r = 16 * w + 4 * (lane >> 4) + i;
+          sm[S::oH1 + r * S::LDH + col] = f32_to_bf16_rne(fmaxf(acc[n][i] + bias, 0.f));
+        }
+      }
+    }
+    __syncthreads();
+    {
+      da_f32x4 acc[H2T];
+      da_layer2<S, H1K, H2T>(sm, w, lane, acc);
+      float part[4] = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int n = 0; n < H2T; ++n) {
+        const int col = 16 * n + (lane & 15);
+        const float bias = sb2[col], wv = sw3[col];
+#pragma unroll
+        for (int i = 0; i < 4; ++i) part[i] = fmaf(fmaxf(acc[n][i] + bias, 0.f), wv, part[i]);
+      }
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const float v = da_sum16(part[i]);
+        if ((lane & 15) == 0) ss[16 * w + 4 * (lane >> 4) + i] = v + b3;
+      }
+    }
+    __syncthreads();
+    // masked softmax over history positions (lane j), as din_pool_fwd_kernel, in
+    // every wave (no extra barrier); wave 0 stores a
+    {
+      const float sj = cur.valid ? ss[lane] : -INFINITY;
+      float m = sj;
+#pragma unroll
+      for (int off = 32; off > 0; off >>= 1) m = fmaxf(m, __shfl_xor(m, off));
+      const float e = cur.valid ? __expf(sj - m) : 0.f;
+      const float a = e / sum_wave(e);
+      if (w == 0) {
+        sa[lane] = a;
+        if (lane < p.L) p.a[b * p.L + lane] = a;
+      }
+    }
+    __syncthreads();
+    // u[e] = sum_j a_j k_j[e]: thread (part g, column e) sums positions j = g mod G,
+    // the G parts are then added in part order (fixed order, deterministic)
+    constexpr int G = DA_THREADS / E;
+    {
+      const int e = tid % E, g = tid / E;
+      float u = 0.f;
+      for (int j = g; j < p.L; j += G)
+        u = fmaf(sa[j], bf16_to_f32(sm[S::oX + j * S::LDX + E + e]), u);
+      su[g * E + e] = u;
+    }
+    __syncthreads();
+    if (tid < E) {
+      float u = 0.f;
+#pragma unroll
+      for (int g = 0; g < G; ++g) u += su[g * E + tid];
+      uint16_t *tp = p.top + b * p.ldt;
+      tp[tid] = sm[S::oX + tid];  // q (row 0's q block)
+      tp[E + tid] = f32_to_bf16_rne(u);
+    }
+    for (int c = 2 * E + tid; c < p.ldt; c += DA_THREADS) p.top[b * p.ldt + c] = 0;
+    cur = nxt;
+    // the next sample's X build overwrites X (read above by the pooled sum): the
+    // barrier at the top of the next iteration's layer 1 comes after the build, so
+    // one here
+    __syncthreads();
+  }
+}
+
+// ---------------------------------------------------------------------------
+// backward: pooling backward, MLP recomputed + back-propagated, dX -> d rows,
+// weight-gradient partials per workgroup
+// ---------------------------------------------------------------------------
+template <int E, int H1T, int H1K, int H2T, int H2K>
+__global__ __launch_bounds__(DA_THREADS) void din_att_bwd_kernel(DinAttArgs p) {
+  using S = DaShape<E, H1T, H1K, H2T, H2K>;
+  constexpr int NTX = S::NTX;
+  constexpr int NW1 = (H1T * NTX + 3) / 4;  // dW1 tiles per wave
+  constexpr int NW2 = (H2T * H1T + 3) / 4;  // dW2 tiles per wave
+  extern __shared__ __attribute__((aligned(16))) char da_lds[];
+  uint16_t *sm = reinterpret_cast<uint16_t *>(da_lds);
+  float *sb1 = reinterpret_cast<float *>(da_lds + S::bwd_end * 2);
+  float *sb2 = sb1 + S::H1N;
+  float *sw3 = sb2 + S::H2N;
+  float *sq = sw3 + S::H2N;  // q [E] fp32
+  float *sdu = sq + E;       // du = dtop[b, E:2E] [E]
+  float *sg = sdu + E;       // g_j = du . k_j [64]
+  float *sdq = sg + DA_ROWS;  // per-wave dq parts [4][E]
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  da_zero_lds(da_lds, S::bwd_end * 2);
+  __syncthreads();
+  da_stage_weights<S, true>(p, sm, sb1, sb2, sw3);
+  const DaTask<E> task(tid);
+
+  da_f32x4 gw1[NW1], gw2[NW2];
+#pragma unroll
+  for (int i = 0; i < NW1; ++i) gw1[i] = da_f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int i = 0; i < NW2; ++i) gw2[i] = da_f32x4{0.f, 0.f, 0.f, 0.f};
+  float gb1[H1T], gb2[H2T], gw3[H2T];  // per-lane column partials (column 16 n + lane % 16)
+#pragma unroll
+  for (int n = 0; n < H1T; ++n) gb1[n] = 0.f;
+#pragma unroll
+  for (int n = 0; n < H2T; ++n) gb2[n] = gw3[n] = 0.f;
+  float gb3 = 0.f;
+
+  DaRaw cur = {};
+  if (blockIdx.x < p.batch) cur = da_load<E, true>(p, blockIdx.x, task, lane);
+  for (int64_t b = blockIdx.x; b < p.batch; b += gridDim.x) {
+    DaRaw nxt = {};
+    if (b + gridDim.x < p.batch) nxt = da_load<E, true>(p, b + gridDim.x, task, lane);
+    // ---- phase 0: X / X^T, q, du, g_j = du . k_j ----
+    if (task.on) {
+      float qv[8], kv[8], dv[8];
+      da_build_x<S, E, true>(p, cur, task, sm, qv, kv);
+      Vec<uint16_t>::to_f32(cur.du, dv);
+      float g = 0.f;
+#pragma unroll
+      for (int i = 0; i < 8; ++i) g = fmaf(dv[i], kv[i], g);
+#pragma unroll
+      for (int off = 1; off < DaTask<E>::CH; off <<= 1) g += __shfl_xor(g, off);
+      if (task.c == 0) sg[task.j] = g;
+      if (task.j == 0) {
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+          sq[task.c + i] = qv[i];
+          sdu[task.c + i] = dv[i];
+        }
+      }
+    }
+    const float aj = cur.a;  // lane = history row
+    __syncthreads();
+    // ---- phase 1: ds (every wave, lane = row), layer 1 -> H1, H1^T ----
+    const float gj = sg[lane];
+    const float ag = sum_wave(aj * gj);
+    const float dsj = aj * (gj - ag);
+    if (w == 0) gb3 += sum_wave(dsj);  // lane 0's value is written
+    {
+      da_f32x4 acc[H1T];
+      da_layer1<S, H1T>(sm, w, lane, acc);
+#pragma unroll
+      for (int n = 0; n < H1T; ++n) {
+        const int col = 16 * n + (lane & 15);
+        const float bias = sb1[col];
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const int r = 16 * w + 4 * (lane >> 4) + i;
+          const uint16_t h = f32_to_bf16_rne(fmaxf(acc[n][i] + bias, 0.f));
+          sm[S::oH1 + r * S::LDH + col] = h;
+          sm[S::oH1T + col * DA_LDT + r] = h;
+        }
+      }
+    }
+    __syncthreads();
+    // ---- phase 2: layer 2, dZ2 = ds w3 relu'(z2) -> dZ2 (over this wave's H1 rows), dZ2^T ----
+    {
+      da_f32x4 acc[H2T];
+      da_layer2<S, H1K, H2T>(sm, w, lane, acc);
+#pragma unroll
+      for (int n = 0; n < H2T; ++n) {
+        const int col = 16 * n + (lane & 15);
+        const float bias = sb2[col], wv = sw3[col];
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const int r = 16 * w + 4 * (lane >> 4) + i;
+          const float dsr = __shfl(dsj, r);
+          const float h2 = fmaxf(acc[n][i] + bias, 0.f);
+          const float dz = h2 > 0.f ? dsr * wv : 0.f;
+          gw3[n] = fmaf(dsr, h2, gw3[n]);
+          gb2[n] += dz;
+          const uint16_t hz = f32_to_bf16_rne(dz);
+          sm[S::oH1 + r * S::LDH + col] = hz;  // dZ2 over H1 (this wave's rows, read above)
+          sm[S::oZ2T + col * DA_LDT + r] = hz;
+        }
+      }
+    }
+    __syncthreads();
+    // ---- phase 3: dH1 = dZ2 W2, dZ1 = dH1 relu'(H1) -> dZ1 (over X), dZ1^T; dW2 ----
+    {
+      da_f32x4 acc[H1T];
+#pragma unroll
+      for (int n = 0; n < H1T; ++n) acc[n] = da_f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int s = 0; s < H2K; ++s) {
+        const da_bf16x8 a = da_frag(sm + S::oH1, S::LDH, 16 * w, 32 * s, lane);
+#pragma unroll
+        for (int n = 0; n < H1T; ++n)
+          acc[n] = da_mfma(a, da_frag(sm + S::oW2T, S::LDW2T, 16 * n, 32 * s, lane), acc[n]);
+      }
+#pragma unroll
+      for (int n = 0; n < H1T; ++n) {
+        const int col = 16 * n + (lane & 15);
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const int r = 16 * w + 4 * (lane >> 4) + i;
+          const uint16_t h = sm[S::oH1T + col * DA_LDT + r];
+          const float dz = (h != 0 && !(h & 0x8000u)) ? acc[n][i] : 0.f;
+          gb1[n] += dz;
+          const uint16_t hz = f32_to_bf16_rne(dz);
+          sm[S::oX + r * S::LDH + col] = hz;  // dZ1 over X (dead since phase 1)
+          sm[S::oZ1T + col * DA_LDT + r] = hz;
+        }
+      }
+#pragma unroll
+      for (int i = 0; i < NW2; ++i) {
+        const int t = w + 4 * i;
+        if (t < H2T * H1T) {
+          const int m = t / H1T, n = t - m * H1T;
+#pragma unroll
+          for (int s = 0; s < 2; ++s)
+            gw2[i] = da_mfma(da_frag(sm + S::oZ2T, DA_LDT, 16 * m, 32 * s, lane),
+                             da_frag(sm + S::oH1T, DA_LDT, 16 * n, 32 * s, lane), gw2[i]);
+        }
+      }
+    }
+    __syncthreads();
+    // ---- phase 4: dX = dZ1 W1 -> d rows (dk per row, dq parts); dW1 ----
+    {
+      da_f32x4 acc[NTX];
+#pragma unroll
+      for (int n = 0; n < NTX; ++n) acc[n] = da_f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int s = 0; s < H1K; ++s) {
+        const da_bf16x8 a = da_frag(sm + S::oX, S::LDH, 16 * w, 32 * s, lane);
+#pragma unroll
+        for (int n = 0; n < NTX; ++n)
+          acc[n] = da_mfma(a, da_frag(sm + S::oW1T, S::LDH, 16 * n, 32 * s, lane), acc[n]);
+      }
+      constexpr int EC = E / 16;  // column tiles per block of X
+#pragma unroll
+      for (int c16 = 0; c16 < EC; ++c16) {
+        const int e = 16 * c16 + (lane & 15);
+        const float qe = sq[e], due = sdu[e];
+        float dqp = 0.f;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const int r = 16 * w + 4 * (lane >> 4) + i;
+          const float dfq = acc[c16][i], dfk = acc[EC + c16][i];
+          const float dfd = acc[2 * EC + c16][i], dfm = acc[3 * EC + c16][i];
+          const float ke = bf16_to_f32(sm[S::oXT + (E + e) * DA_LDT + r]);
+          const float ar = __shfl(aj, r);
+          const float dk = fmaf(ar, due, dfk - dfd + dfm * qe);
+          if (r < p.L)
+            p.drows[(p.batch + b * p.L + r) * p.ld_drows + e] = f32_to_bf16_rne(dk);
+          dqp += dfq + dfd + dfm * ke;
+        }
+        dqp = swap32_sum(swap16_sum(dqp));  // the 4 row groups of column e
+        if (lane < 16) sdq[w * E + e] = dqp;
+      }
+#pragma unroll
+      for (int i = 0; i < NW1; ++i) {
+        const int t = w + 4 * i;
+        if (t < H1T * NTX) {
+          const int m = t / NTX, n = t - m * NTX;
+#pragma unroll
+          for (int s = 0; s < 2; ++s)
+            gw1[i] = da_mfma(da_frag(sm + S::oZ1T, DA_LDT, 16 * m, 32 * s, lane),
+                             da_frag(sm + S::oXT, DA_LDT, 16 * n, 32 * s, lane), gw1[i]);
+        }
+      }
+    }
+    __syncthreads();
+    if (tid < E) {
+      const float v = bf16_to_f32(p.dtop[b * p.lddt + tid]) + sdq[tid] + sdq[E + tid] +
+                      sdq[2 * E + tid] + sdq[3 * E + tid];
+      p.drows[b * p.ld_drows + tid] = f32_to_bf16_rne(v);
+    }
+    cur = nxt;
+  }
+
+  // ---- weight-gradient partials of this workgroup ----
+  float *part = p.part + static_cast<int64_t>(blockIdx.x) * p.P;
+  const int E4 = S::E4, H1 = p.H1, H2 = p.H2;
+  float *pw2 = part + H1 * E4, *pb1 = pw2 + H2 * H1, *pb2 = pb1 + H1, *pw3 = pb2 + H2,
+        *pb3 = pw3 + H2;
+#pragma unroll
+  for (int i = 0; i < NW1; ++i) {
+    const int t = w + 4 * i;
+    if (t < H1T * NTX) {
+      const int m = t / NTX, n = t - m * NTX;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int h = 16 * m + 4 * (lane >> 4) + j;
+        if (h < H1) part[h * E4 + 16 * n + (lane & 15)] = gw1[i][j];
+      }
+    }
+  }
+#pragma unroll
+  for (int i = 0; i < NW2; ++i) {
+    const int t = w + 4 * i;
+    if (t < H2T * H1T) {
+      const int m = t / H1T, n = t - m * H1T;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int h2 = 16 * m + 4 * (lane >> 4) + j, h1 = 16 * n + (lane & 15);
+        if (h2 < H2 && h1 < H1) pw2[h2 * H1 + h1] = gw2[i][j];
+      }
+    }
+  }
+  // column partials: lanes l, l + 16, l + 32, l + 48 hold the same column; then the waves
+  __syncthreads();
+  float *red = reinterpret_cast<float *>(da_lds);  // [4][H1N + 2 H2N] (LDS now dead)
+  constexpr int RW = S::H1N + 2 * S::H2N;
+#pragma unroll
+  for (int n = 0; n < H1T; ++n) {
+    float v = gb1[n];
+    v += __shfl_xor(v, 16);
+    v += __shfl_xor(v, 32);
+    if (lane < 16) red[w * RW + 16 * n + lane] = v;
+  }
+#pragma unroll
+  for (int n = 0; n < H2T; ++n) {
+    float v = gb2[n], u = gw3[n];
+    v += __shfl_xor(v, 16);
+    v += __shfl_xor(v, 32);
+    u += __shfl_xor(u, 16);
+    u += __shfl_xor(u, 32);
+    if (lane < 16) {
+      red[w * RW + S::H1N + 16 * n + lane] = v;
+      red[w * RW + S::H1N + S::H2N + 16 * n + lane] = u;
+    }
+  }
+  __syncthreads();
+  for (int c = tid; c < RW; c += DA_THREADS) {
+    const float v = red[c] + red[RW + c] + red[2 * RW + c] + red[3 * RW + c];
+    if (c < S::H1N) {
+      if (c < H1) pb1[c] = v;
+    } else if (c < S::H1N + S::H2N) {
+      if (c - S::H1N < H2) pb2[c - S::H1N] = v;
+    } else if (c - S::H1N - S::H2N < H2) {
+      pw3[c - S::H1N - S::H2N] = v;
+    }
+  }
+  if (tid == 0) pb3[0] = gb3;
+}
+
+// fixed-order sum of the workgroup partials; grads (flat, P) or SGD in place.
+// Block: 64 columns x 4 slices of the partials (each slice summed in order with 4
+// loads in flight), the 4 slice sums added in slice order.
+__global__ __launch_bounds__(256) void din_att_wgrad_kernel(
+    const float *__restrict__ part, int parts, int64_t P, int E4, int H1, int H2, float *grads,
+    float lr, float *w1, int64_t ldw1, float *b1, float *w2, int64_t ldw2, float *b2, float *w3,
+    float *b3) {
+  __shared__ float red[4][64];
+  const int cl = threadIdx.x & 63, sl = threadIdx.x >> 6;
+  const int64_t i = static_cast<int64_t>(blockIdx.x) * 64 + cl;
+  const int per = (parts + 3) / 4, g0 = sl * per, g1 = min(parts, g0 + per);
+  float v = 0.f;
+  if (i < P) {
+    int g = g0;
+    for (; g + 4 <= g1; g += 4) {
+      const float x0 = part[(g + 0) * P + i], x1 = part[(g + 1) * P + i];
+      const float x2 = part[(g + 2) * P + i], x3 = part[(g + 3) * P + i];
+      v += x0;
+      v += x1;
+      v += x2;
+      v += x3;
+    }
+    for (; g < g1; ++g) v += part[g * P + i];
+  }
+  red[sl][cl] = v;
+  __syncthreads();
+  if (sl != 0 || i >= P) return;
+  v = red[0][cl] + red[1][cl] + red[2][cl] + red[3][cl];
+  if (grads) {
+    grads[i] = v;
+    return;
+  }
+  int64_t o = i;
+  if (o < H1 * E4) {
+    float &x = w1[(o / E4) * ldw1 + o % E4];
+    x -= lr * v;
+    return;
+  }
+  o -= H1 * E4;
+  if (o < H2 * H1) {
+    float &x = w2[(o / H1) * ldw2 + o % H1];
+    x -= lr * v;
+    return;
+  }
+  o -= H2 * H1;
+  if (o < H1) { b1[o] -= lr * v; return; }
+  o -= H1;
+  if (o < H2) { b2[o] -= lr * v; return; }
+  o -= H2;
+  if (o < H2) { w3[o] -= lr * v; return; }
+  b3[0] -= lr * v;
+}
+
+}  // namespace mrec
+
+using namespace mrec;
+
+namespace {
+
+// the compiled attention-unit shapes: (E, H1, H2) -> kernels
+#define MREC_DA_SHAPES(X) \
+  X(32, 5, 3, 3, 2)       \
+  X(16, 2, 1, 1, 1)
+
+template <int E, int H1T, int H1K, int H2T, int H2K>
+bool da_match(int e, int h1, int h2) {
+  return e == E && (h1 + 15) / 16 == H1T && (h1 + 31) / 32 == H1K && (h2 + 15) / 16 == H2T &&
+         (h2 + 31) / 32 == H2K;
+}
+
+int da_cus() {
+  static const int n = [] {
+    int dev = 0, v = 0;
+    if (hipGetDevice(&dev) != hipSuccess ||
+        hipDeviceGetAttribute(&v, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
+        v <= 0)
+      v = 256;
+    (void)hipGetLastError();
+    return v;
+  }();
+  return n;
+}
+
+template <int E, int H1T, int H1K, int H2T, int H2K>
+void da_set_attrs() {
+  using S = DaShape<E, H1T, H1K, H2T, H2K>;
+  (void)hipFuncSetAttribute(reinterpret_cast<const void *>(din_att_fwd_kernel<E, H1T, H1K, H2T, H2K>),
+                            hipFuncAttributeMaxDynamicSharedMemorySize,
+                            static_cast<int>(S::fwd_bytes));
+  (void)hipFuncSetAttribute(reinterpret_cast<const void *>(din_att_bwd_kernel<E, H1T, H1K, H2T, H2K>),
+                            hipFuncAttributeMaxDynamicSharedMemorySize,
+                            static_cast<int>(S::bwd_bytes));
+  (void)hipGetLastError();
+}
+
+bool da_supported(int E, int H1, int H2) {
+  if (H1 % 4 != 0) return false;
+#define X(e, a, b, c, d) if (da_match<e, a, b, c, d>(E, H1, H2)) return true;
+  MREC_DA_SHAPES(X)
+#undef X
+  return false;
+}
+
+}  // namespace
+
+extern "C" {
+
+int32_t mrec_din_att_supported(int32_t E, int32_t H1, int32_t H2) {
+  return da_supported(E, H1, H2) ? 1 : 0;
+}
+
+int64_t mrec_din_att_parts(int64_t batch) {
+  const int64_t g = da_cus();
+  return batch < g ? (batch > 0 ? batch : 1) : g;
+}
+
+int64_t mrec_din_att_param_count(int32_t E, int32_t H1, int32_t H2) {
+  return static_cast<int64_t>(H1) * 4 * E + static_cast<int64_t>(H2) * H1 + H1 + 2 * H2 + 1;
+}
+
+static mrec_status da_check(const void *rows, int64_t ld_rows, int64_t batch, int32_t L, int32_t E,
+                            const float *w1, int64_t ldw1, const float *b1, int32_t H1,
+                            const float *w2, int64_t ldw2, const float *b2, int32_t H2,
+                            const float *w3, const float *b3) {
+  MREC_CHECK_ARG(rows && w1 && b1 && w2 && b2 && w3 && b3, "NULL pointer");
+  MREC_CHECK_ARG(batch >= 0 && L >= 1 && L <= DA_ROWS, "need 1 <= L <= 64");
+  MREC_CHECK_ARG(da_supported(E, H1, H2), "attention-unit shape (E, H1, H2) not compiled");
+  MREC_CHECK_ARG((reinterpret_cast<uintptr_t>(rows) & 15) == 0 && ld_rows % 8 == 0 &&
+                     ld_rows >= E,
+                 "rows must be 16-byte aligned bf16 rows of >= E elements");
+  MREC_CHECK_ARG(ldw1 >= 4 * E && ldw2 >= H1 && ldw1 % 4 == 0 && ldw2 % 4 == 0 && H1 % 4 == 0 &&
+                     (reinterpret_cast<uintptr_t>(w1) & 15) == 0 &&
+                     (reinterpret_cast<uintptr_t>(w2) & 15) == 0,
+                 "w1 / w2 16-byte aligned, ldw1, ldw2 and H1 multiples of 4");
+  return MREC_OK;
+}
+
+mrec_status mrec_din_att_fwd(const void *rows, int64_t ld_rows, const int32_t *his, int64_t ld_his,
+                             int64_t batch, int32_t L, int32_t E, const float *w1, int64_t ldw1,
+                             const float *b1, int32_t H1, const float *w2, int64_t ldw2,
+                             const float *b2, int32_t H2, const float *w3, const float *b3,
+                             float *a, void *top, int64_t ldt, mrec_stream stream) {
+  const mrec_status st = da_check(rows, ld_rows, batch, L, E, w1, ldw1, b1, H1, w2, ldw2, b2, H2,
+                                  w3, b3);
+  if (st != MREC_OK) return st;
+  MREC_CHECK_ARG(his && a && top, "NULL pointer");
+  MREC_CHECK_ARG(ld_his >= L && ldt >= 2 * E, "bad strides");
+  if (batch == 0) return MREC_OK;
+  DinAttArgs p{};
+  p.rows = static_cast<const uint16_t *>(rows);
+  p.ld_rows = ld_rows;
+  p.his = his;
+  p.ld_his = ld_his;
+  p.w1 = w1, p.b1 = b1, p.w2 = w2, p.b2 = b2, p.w3 = w3, p.b3 = b3;
+  p.ldw1 = ldw1, p.ldw2 = ldw2;
+  p.batch = batch, p.L = L, p.H1 = H1, p.H2 = H2;
+  p.a = a;
+  p.top = static_cast<uint16_t *>(top);
+  p.ldt = ldt;
+  const int64_t grid = std::min<int64_t>(batch, 2 * static_cast<int64_t>(da_cus()));
+  hipStream_t s = static_cast<hipStream_t>(stream);
+#define X(e, h1t, h1k, h2t, h2k)                                                              \
+  if (da_match<e, h1t, h1k, h2t, h2k>(E, H1, H2)) {                                         \
+    static const int once = (da_set_attrs<e, h1t, h1k, h2t, h2k>(), 1);                     \
+    (void)once;                                                                             \
+    din_att_fwd_kernel<e, h1t, h1k, h2t, h2k>                                               \
+        <<<dim3(static_cast<unsigned>(grid)), DA_THREADS,                                   \
+           DaShape<e, h1t, h1k, h2t, h2k>::fwd_bytes, s>>>(p);                              \
+    return launch_status("mrec_din_att_fwd");                                               \
+  }
+  MREC_DA_SHAPES(X)
+#undef X
+  return MREC_EINVAL;
+}
+
+mrec_status mrec_din_att_bwd(const void *rows, int64_t ld_rows, int64_t batch, int32_t L,
+                             int32_t E, const float *w1, int64_t ldw1, const float *b1, int32_t H1,
+                             const float *w2, int64_t ldw2, const float *b2, int32_t H2,
+                             const float *w3, const float *b3, const float *a, const void *dtop,
+                             int64_t lddt, void *d_rows, int64_t ld_drows, float *part,
+                             int64_t parts, mrec_stream stream) {
+  const mrec_status st = da_check(rows, ld_rows, batch, L, E, w1, ldw1, b1, H1, w2, ldw2, b2, H2,
+                                  w3, b3);
+  if (st != MREC_OK) return st;
+  MREC_CHECK_ARG(a && dtop && d_rows && part, "NULL pointer");
+  MREC_CHECK_ARG((reinterpret_cast<uintptr_t>(dtop) & 15) == 0 && lddt % 8 == 0 && lddt >= 2 * E,
+                 "dtop must be 16-byte aligned bf16 rows of >= 2E elements");
+  MREC_CHECK_ARG(ld_drows >= E, "bad d_rows stride");
+  MREC_CHECK_ARG(parts == mrec_din_att_parts(batch), "parts must be mrec_din_att_parts(batch)");
+  if (batch == 0) return MREC_OK;
+  DinAttArgs p{};
+  p.rows = static_cast<const uint16_t *>(rows);
+  p.ld_rows = ld_rows;
+  p.w1 = w1, p.b1 = b1, p.w2 = w2, p.b2 = b2, p.w3 = w3, p.b3 = b3;
+  p.ldw1 = ldw1, p.ldw2 = ldw2;
+  p.batch = batch, p.L = L, p.H1 = H1, p.H2 = H2;
+  p.a = const_cast<float *>(a);
+  p.dtop = static_cast<const uint16_t *>(dtop);
+  p.lddt = lddt;
+  p.drows = static_cast<uint16_t *>(d_rows);
+  p.ld_drows = ld_drows;
+  p.part = part;
+  p.P = mrec_din_att_param_count(E, H1, H2);
+  hipStream_t s = static_cast<hipStream_t>(stream);
+#define X(e, h1t, h1k, h2t, h2k)                                                              \
+  if (da_match<e, h1t, h1k, h2t, h2k>(E, H1, H2)) {                                         \
+    static const int once = (da_set_attrs<e, h1t, h1k, h2t, h2k>(), 1);                     \
+    (void)once;                                                                             \
+    din_att_bwd_kernel<e, h1t, h1k, h2t, h2k>                                               \
+        <<<dim3(static_cast<unsigned>(parts)), DA_THREADS,                                  \
+           DaShape<e, h1t, h1k, h2t, h2k>::bwd_bytes, s>>>(p);                              \
+    return launch_status("mrec_din_att_bwd");                                               \
+  }
+  MREC_DA_SHAPES(X)
+#undef X
+  return MREC_EINVAL;
+}
+
+mrec_status mrec_din_att_wgrad(const float *part, int64_t parts, int32_t E, int32_t H1, int32_t H2,
+                               float *grads, float lr, float *w1, int64_t ldw1, float *b1,
+                               float *w2, int64_t ldw2, float *b2, float *w3, float *b3,
+                               mrec_stream stream) {
+  MREC_CHECK_ARG(part && parts >= 1, "NULL pointer / no partials");
+  MREC_CHECK_ARG(grads || (w1 && b1 && w2 && b2 && w3 && b3), "need grads or the parameters");
+  const int64_t P = mrec_din_att_param_count(E, H1, H2);
+  din_att_wgrad_kernel<<<dim3(static_cast<unsigned>((P + 63) / 64)), 256, 0,
+                         static_cast<hipStream_t>(stream)>>>(
+      part, static_cast<int>(parts), P, 4 * E, H1, H2, grads, lr, w1, ldw1, b1, w2, ldw2, b2, w3,
+      b3);
+  return launch_status("mrec_din_att_wgrad");
+}
+
+}  // extern "C"

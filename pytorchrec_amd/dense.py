@@ -778,12 +778,120 @@ def _din_scores(feat: torch.Tensor, att_mlp, att_out: torch.nn.Linear) -> torch.
     return linear(h, att_out.weight, att_out.bias, out_dtype=torch.float32)
 
 
+# the fused attention unit (mrec_din_att_*, din_att.hip) is the default for the
+# compiled shapes; MREC_DIN_FUSED=0 selects the layered kernels (A/B, parity tests)
+DIN_FUSED = os.environ.get("MREC_DIN_FUSED", "1") == "1"
+
+
+def _din_att_linears(att_mlp, att_out):
+    lins = [m for m in att_mlp.modules() if isinstance(m, torch.nn.Linear)]
+    return lins + [att_out]
+
+
+def din_att_supported(E: int, att_mlp, att_out: torch.nn.Linear) -> bool:
+    """True when the fused attention unit covers this block: two ReLU Dense layers
+    + Linear(H2, 1), all with bias, no active dropout, a compiled (E, H1, H2)."""
+    lins = _din_att_linears(att_mlp, att_out)
+    if len(lins) != 3 or any(m.bias is None for m in lins) or lins[2].out_features != 1:
+        return False
+    if att_mlp.training and any(isinstance(m, torch.nn.Dropout) and m.p > 0
+                                for m in att_mlp.modules()):
+        return False
+    H1, H2 = lins[0].out_features, lins[1].out_features
+    if (lins[0].in_features != 4 * E or lins[1].in_features != H1
+            or lins[2].in_features != H2):
+        return False
+    return bool(_mrec.lib().mrec_din_att_supported(E, H1, H2))
+
+
+def _weights_changed(*params):
+    """An in-place kernel update of these fp32 masters that re-emitted no image:
+    every cached bf16 image kind goes stale."""
+    for p in params:
+        p._mrec_gen = getattr(p, "_mrec_gen", 0) + 1
+
+
+class _DinAttFn(torch.autograd.Function):
+    """The whole DIN attention unit over the gathered rows [q (B) | k (B L)]: one
+    forward launch (features, MLP, scores, masked softmax, pooling -> top) and one
+    backward launch (the rows' bf16 gradient + weight-gradient partials) plus the
+    partials' fixed-order sum, which applies the fused SGD when the optimizer is
+    plain SGD (sgd_lr) or hands the gradients to it."""
+
+    @staticmethod
+    def forward(ctx, rows, his, B: int, L: int, w1, b1, w2, b2, w3, b3):
+        E = rows.shape[1]
+        H1, H2 = w1.shape[0], w2.shape[0]
+        ws = [_weight_f32(w1), b1.detach().float().contiguous(), _weight_f32(w2),
+              b2.detach().float().contiguous(), w3.detach().float().reshape(-1).contiguous(),
+              b3.detach().float().contiguous()]
+        his = his.to(torch.int32)
+        if his.stride(1) != 1:
+            his = his.contiguous()
+        a = torch.empty(B, L, dtype=torch.float32, device=rows.device)
+        top = _alloc(B, 2 * E, _BF16, rows.device)
+        _mrec.call("mrec_din_att_fwd", rows.data_ptr(), rows.stride(0), his.data_ptr(),
+                   his.stride(0), B, L, E, ws[0].data_ptr(), ws[0].stride(0), ws[1].data_ptr(),
+                   H1, ws[2].data_ptr(), ws[2].stride(0), ws[3].data_ptr(), H2, ws[4].data_ptr(),
+                   ws[5].data_ptr(), a.data_ptr(), top.data_ptr(), top.stride(0),
+                   _mrec.stream_handle())
+        ctx.save_for_backward(rows, a)
+        ctx.ws, ctx.params, ctx.B, ctx.L = ws, (w1, b1, w2, b2, w3, b3), B, L
+        return top
+
+    @staticmethod
+    def backward(ctx, dtop):
+        rows, a = ctx.saved_tensors
+        ws, params, B, L = ctx.ws, ctx.params, ctx.B, ctx.L
+        E = rows.shape[1]
+        H1, H2 = params[0].shape[0], params[2].shape[0]
+        dtop = _bf16_rows(dtop)
+        d_rows = _alloc(rows.shape[0], E, _BF16, rows.device)
+        lib = _mrec.lib()
+        parts = int(lib.mrec_din_att_parts(B))
+        P = int(lib.mrec_din_att_param_count(E, H1, H2))
+        part = torch.empty(parts, P, dtype=torch.float32, device=rows.device)
+        st = _mrec.stream_handle()
+        _mrec.call("mrec_din_att_bwd", rows.data_ptr(), rows.stride(0), B, L, E,
+                   ws[0].data_ptr(), ws[0].stride(0), ws[1].data_ptr(), H1, ws[2].data_ptr(),
+                   ws[2].stride(0), ws[3].data_ptr(), H2, ws[4].data_ptr(), ws[5].data_ptr(),
+                   a.data_ptr(), dtop.data_ptr(), dtop.stride(0), d_rows.data_ptr(),
+                   d_rows.stride(0), part.data_ptr(), parts, st)
+        ctx.ws = None
+        w1, b1, w2, b2, w3, b3 = params
+        lr = sgd_lr(*params)
+        inplace = (lr is not None and all(p.dtype == torch.float32 and p.is_contiguous()
+                                          for p in params))
+        if inplace:
+            _mrec.call("mrec_din_att_wgrad", part.data_ptr(), parts, E, H1, H2, None, lr,
+                       w1.data_ptr(), w1.stride(0), b1.data_ptr(), w2.data_ptr(), w2.stride(0),
+                       b2.data_ptr(), w3.data_ptr(), b3.data_ptr(), st)
+            _weights_changed(*params)
+            return d_rows, None, None, None, None, None, None, None, None, None
+        g = torch.empty(P, dtype=torch.float32, device=rows.device)
+        _mrec.call("mrec_din_att_wgrad", part.data_ptr(), parts, E, H1, H2, g.data_ptr(), 0.0,
+                   None, 0, None, None, 0, None, None, None, st)
+        gw1, gw2, gb1, gb2, gw3, gb3 = torch.split(g, [H1 * 4 * E, H2 * H1, H1, H2, H2, 1])
+        grads = [t.view_as(p) for t, p in zip((gw1, gb1, gw2, gb2, gw3, gb3), params)]
+        dpg = dp_grads(*params)
+        if dpg is not None:  # data parallel: into the flat buffer IModel all-reduces
+            for dst, src in zip(dpg, grads):
+                dst.copy_(src.view_as(dst))
+            return d_rows, None, None, None, None, None, None, None, None, None
+        return (d_rows, None, None, None, *grads)
+
+
 def din_attention_top_rows(rows: torch.Tensor, B: int, his: torch.Tensor, att_mlp,
                            att_out: torch.nn.Linear) -> torch.Tensor:
     """din_attention_top over the gather output rows [q (B) | k (B L)] (bf16, 16-B
-    aligned rows): the rows' gradient comes back as one bf16 tensor."""
+    aligned rows): the rows' gradient comes back as one bf16 tensor.  The fused
+    attention unit (one launch each way) when it covers the block."""
     L = his.shape[1]
     rows = _bf16_rows(rows)
+    if DIN_FUSED and din_att_supported(rows.shape[1], att_mlp, att_out):
+        w1, w2, w3 = (m.weight for m in _din_att_linears(att_mlp, att_out))
+        b1, b2, b3 = (m.bias for m in _din_att_linears(att_mlp, att_out))
+        return _DinAttFn.apply(rows, his, B, L, w1, b1, w2, b2, w3, b3)
     st = _DinState()
     feat = _DinRowsFeatFn.apply(rows, B, st, L)
     s = _din_scores(feat, att_mlp, att_out)

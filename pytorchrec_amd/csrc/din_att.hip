@@ -1,6 +1,6 @@
 // DIN attention unit fused per sample (config C4).
 //
-// One workgroup (4 waves) per sample b at a time, persistent over samples.  The
+// One workgroup (8 waves) per sample b at a time, persistent over samples.  The
 // attention-unit input X = [q | k_j | q - k_j | q * k_j] (64 padded history rows x
 // 4E), the MLP activations and every gradient live in LDS only; the MLP weights
 // are staged once per workgroup as bf16 in both operand orders.  What the layered
@@ -33,7 +33,8 @@ typedef short da_bf16x8 __attribute__((ext_vector_type(8)));
 typedef float da_f32x4 __attribute__((ext_vector_type(4)));
 
 constexpr int DA_ROWS = 64;              // history positions per sample, padded
-constexpr int DA_THREADS = 256;          // 4 waves; wave w owns rows 16w .. 16w + 15
+constexpr int DA_CG = 2;                 // column groups: 8 waves = 4 row tiles x 2
+constexpr int DA_THREADS = 64 * 4 * DA_CG;
 constexpr int DA_LDT = DA_ROWS + 8;      // row stride of the [feature][row] buffers
 
 struct DinAttArgs {
@@ -107,7 +108,8 @@ struct DaShape {
   static constexpr int bwd_end = oW2T + H1N * LDW2T;
   // fp32 tail: b1 [H1N], b2 [H2N], w3 [H2N], q [E], du [E], g [64], dq parts [4][E]
   static constexpr int nf32 = H1N + 2 * H2N + 2 * E + DA_ROWS + 4 * E;
-  static constexpr size_t fwd_bytes = fwd_end * 2 + (H1N + 2 * H2N + 2 * DA_ROWS + DA_THREADS) * 4;
+  static constexpr size_t fwd_bytes =
+      fwd_end * 2 + (H1N + 2 * H2N + (DA_CG + 1) * DA_ROWS + DA_THREADS) * 4;
   static constexpr size_t bwd_bytes = bwd_end * 2 + nf32 * 4;
 };
 
@@ -254,33 +256,41 @@ __device__ __forceinline__ void da_build_x(const DinAttArgs &p, const DaRaw &raw
   }
 }
 
-// layer 1 of this wave's rows: acc[n] = X[rows] W1^T (n-th 16-column tile)
+// Wave w = (row tile rt = w % 4: rows 16 rt .. + 15, column group cg = w / 4):
+// a GEMM's 16-column output tiles n = cg, cg + DA_CG, ... of the wave's rows.
+// layer 1: acc[jn] = X[rows] W1^T (tile n = cg + DA_CG jn)
 template <class S, int H1T>
-__device__ __forceinline__ void da_layer1(const uint16_t *sm, int w, int lane,
-                                          da_f32x4 (&acc)[H1T]) {
+__device__ __forceinline__ void da_layer1(const uint16_t *sm, int rt, int cg, int lane,
+                                          da_f32x4 (&acc)[(H1T + DA_CG - 1) / DA_CG]) {
+  constexpr int J = (H1T + DA_CG - 1) / DA_CG;
 #pragma unroll
-  for (int n = 0; n < H1T; ++n) acc[n] = da_f32x4{0.f, 0.f, 0.f, 0.f};
+  for (int jn = 0; jn < J; ++jn) acc[jn] = da_f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
   for (int s = 0; s < S::KT1; ++s) {
-    const da_bf16x8 a = da_frag(sm + S::oX, S::LDX, 16 * w, 32 * s, lane);
+    const da_bf16x8 a = da_frag(sm + S::oX, S::LDX, 16 * rt, 32 * s, lane);
 #pragma unroll
-    for (int n = 0; n < H1T; ++n)
-      acc[n] = da_mfma(a, da_frag(sm + S::oW1, S::LDX, 16 * n, 32 * s, lane), acc[n]);
+    for (int jn = 0; jn < J; ++jn) {
+      const int n = cg + DA_CG * jn;
+      if (n < H1T) acc[jn] = da_mfma(a, da_frag(sm + S::oW1, S::LDX, 16 * n, 32 * s, lane), acc[jn]);
+    }
   }
 }
 
-// layer 2 of this wave's rows: acc[n] = H1[rows] W2^T
+// layer 2: acc[jn] = H1[rows] W2^T
 template <class S, int H1K, int H2T>
-__device__ __forceinline__ void da_layer2(const uint16_t *sm, int w, int lane,
-                                          da_f32x4 (&acc)[H2T]) {
+__device__ __forceinline__ void da_layer2(const uint16_t *sm, int rt, int cg, int lane,
+                                          da_f32x4 (&acc)[(H2T + DA_CG - 1) / DA_CG]) {
+  constexpr int J = (H2T + DA_CG - 1) / DA_CG;
 #pragma unroll
-  for (int n = 0; n < H2T; ++n) acc[n] = da_f32x4{0.f, 0.f, 0.f, 0.f};
+  for (int jn = 0; jn < J; ++jn) acc[jn] = da_f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
   for (int s = 0; s < H1K; ++s) {
-    const da_bf16x8 a = da_frag(sm + S::oH1, S::LDH, 16 * w, 32 * s, lane);
+    const da_bf16x8 a = da_frag(sm + S::oH1, S::LDH, 16 * rt, 32 * s, lane);
 #pragma unroll
-    for (int n = 0; n < H2T; ++n)
-      acc[n] = da_mfma(a, da_frag(sm + S::oW2, S::LDH, 16 * n, 32 * s, lane), acc[n]);
+    for (int jn = 0; jn < J; ++jn) {
+      const int n = cg + DA_CG * jn;
+      if (n < H2T) acc[jn] = da_mfma(a, da_frag(sm + S::oW2, S::LDH, 16 * n, 32 * s, lane), acc[jn]);
+    }
   }
 }
 
@@ -290,20 +300,21 @@ __device__ __forceinline__ void da_layer2(const uint16_t *sm, int w, int lane,
 template <int E, int H1T, int H1K, int H2T, int H2K>
 __global__ __launch_bounds__(DA_THREADS) void din_att_fwd_kernel(DinAttArgs p) {
   using S = DaShape<E, H1T, H1K, H2T, H2K>;
+  constexpr int J1 = (H1T + DA_CG - 1) / DA_CG, J2 = (H2T + DA_CG - 1) / DA_CG;
   extern __shared__ __attribute__((aligned(16))) char da_lds[];
   uint16_t *sm = reinterpret_cast<uint16_t *>(da_lds);
   float *sb1 = reinterpret_cast<float *>(da_lds + S::fwd_end * 2);
   float *sb2 = sb1 + S::H1N;
   float *sw3 = sb2 + S::H2N;
-  float *ss = sw3 + S::H2N;  // scores [64]
-  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  float *ss = sw3 + S::H2N;        // score parts [DA_CG][64]
+  float *sa = ss + DA_CG * DA_ROWS;  // softmax weights [64]
+  float *su = sa + DA_ROWS;        // pooled-sum parts [DA_THREADS / E][E]
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, rt = w & 3, cg = w >> 2;
   da_zero_lds(da_lds, S::fwd_end * 2);
   __syncthreads();
   da_stage_weights<S, false>(p, sm, sb1, sb2, sw3);
   const float b3 = p.b3[0];
   const DaTask<E> task(tid);
-  float *sa = ss + DA_ROWS;  // softmax weights [64]
-  float *su = sa + DA_ROWS;  // pooled-sum parts [DA_THREADS / E][E]
   DaRaw cur = {};
   if (blockIdx.x < p.batch) cur = da_load<E, false>(p, blockIdx.x, task, lane);
   for (int64_t b = blockIdx.x; b < p.batch; b += gridDim.x) {
@@ -315,42 +326,49 @@ __global__ __launch_bounds__(DA_THREADS) void din_att_fwd_kernel(DinAttArgs p) {
     }
     __syncthreads();
     {
-      da_f32x4 acc[H1T];
-      da_layer1<S, H1T>(sm, w, lane, acc);
+      da_f32x4 acc[J1];
+      da_layer1<S, H1T>(sm, rt, cg, lane, acc);
 #pragma unroll
-      for (int n = 0; n < H1T; ++n) {
+      for (int jn = 0; jn < J1; ++jn) {
+        const int n = cg + DA_CG * jn;
+        if (n >= H1T) continue;
         const int col = 16 * n + (lane & 15);
         const float bias = sb1[col];
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
-          const int r = 16 * w + 4 * (lane >> 4) + i;
-          sm[S::oH1 + r * S::LDH + col] = f32_to_bf16_rne(fmaxf(acc[n][i] + bias, 0.f));
+          const int r = 16 * rt + 4 * (lane >> 4) + i;
+          sm[S::oH1 + r * S::LDH + col] = f32_to_bf16_rne(fmaxf(acc[jn][i] + bias, 0.f));
         }
       }
     }
     __syncthreads();
     {
-      da_f32x4 acc[H2T];
-      da_layer2<S, H1K, H2T>(sm, w, lane, acc);
+      da_f32x4 acc[J2];
+      da_layer2<S, H1K, H2T>(sm, rt, cg, lane, acc);
       float part[4] = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-      for (int n = 0; n < H2T; ++n) {
+      for (int jn = 0; jn < J2; ++jn) {
+        const int n = cg + DA_CG * jn;
+        if (n >= H2T) continue;
         const int col = 16 * n + (lane & 15);
         const float bias = sb2[col], wv = sw3[col];
 #pragma unroll
-        for (int i = 0; i < 4; ++i) part[i] = fmaf(fmaxf(acc[n][i] + bias, 0.f), wv, part[i]);
+        for (int i = 0; i < 4; ++i) part[i] = fmaf(fmaxf(acc[jn][i] + bias, 0.f), wv, part[i]);
       }
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
         const float v = da_sum16(part[i]);
-        if ((lane & 15) == 0) ss[16 * w + 4 * (lane >> 4) + i] = v + b3;
+        if ((lane & 15) == 0) ss[cg * DA_ROWS + 16 * rt + 4 * (lane >> 4) + i] = v;
       }
     }
     __syncthreads();
     // masked softmax over history positions (lane j), as din_pool_fwd_kernel, in
     // every wave (no extra barrier); wave 0 stores a
     {
-      const float sj = cur.valid ? ss[lane] : -INFINITY;
+      float sc = b3;
+#pragma unroll
+      for (int g = 0; g < DA_CG; ++g) sc += ss[g * DA_ROWS + lane];
+      const float sj = cur.valid ? sc : -INFINITY;
       float m = sj;
 #pragma unroll
       for (int off = 32; off > 0; off >>= 1) m = fmaxf(m, __shfl_xor(m, off));
@@ -383,10 +401,7 @@ __global__ __launch_bounds__(DA_THREADS) void din_att_fwd_kernel(DinAttArgs p) {
     }
     for (int c = 2 * E + tid; c < p.ldt; c += DA_THREADS) p.top[b * p.ldt + c] = 0;
     cur = nxt;
-    // the next sample's X build overwrites X (read above by the pooled sum): the
-    // barrier at the top of the next iteration's layer 1 comes after the build, so
-    // one here
-    __syncthreads();
+    __syncthreads();  // the next sample's X build overwrites X, read by the pooled sum
   }
 }
 
@@ -398,8 +413,12 @@ template <int E, int H1T, int H1K, int H2T, int H2K>
 __global__ __launch_bounds__(DA_THREADS) void din_att_bwd_kernel(DinAttArgs p) {
   using S = DaShape<E, H1T, H1K, H2T, H2K>;
   constexpr int NTX = S::NTX;
-  constexpr int NW1 = (H1T * NTX + 3) / 4;  // dW1 tiles per wave
-  constexpr int NW2 = (H2T * H1T + 3) / 4;  // dW2 tiles per wave
+  constexpr int EC = E / 16;  // column tiles per block of X
+  constexpr int J1 = (H1T + DA_CG - 1) / DA_CG, J2 = (H2T + DA_CG - 1) / DA_CG;
+  constexpr int JX = (EC + DA_CG - 1) / DA_CG;
+  constexpr int NWV = DA_THREADS / 64;
+  constexpr int NW1 = (H1T * NTX + NWV - 1) / NWV;  // dW1 tiles per wave
+  constexpr int NW2 = (H2T * H1T + NWV - 1) / NWV;  // dW2 tiles per wave
   extern __shared__ __attribute__((aligned(16))) char da_lds[];
   uint16_t *sm = reinterpret_cast<uint16_t *>(da_lds);
   float *sb1 = reinterpret_cast<float *>(da_lds + S::bwd_end * 2);
@@ -408,8 +427,8 @@ __global__ __launch_bounds__(DA_THREADS) void din_att_bwd_kernel(DinAttArgs p) {
   float *sq = sw3 + S::H2N;  // q [E] fp32
   float *sdu = sq + E;       // du = dtop[b, E:2E] [E]
   float *sg = sdu + E;       // g_j = du . k_j [64]
-  float *sdq = sg + DA_ROWS;  // per-wave dq parts [4][E]
-  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  float *sdq = sg + DA_ROWS;  // per-row-tile dq parts [4][E]
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, rt = w & 3, cg = w >> 2;
   da_zero_lds(da_lds, S::bwd_end * 2);
   __syncthreads();
   da_stage_weights<S, true>(p, sm, sb1, sb2, sw3);
@@ -420,11 +439,11 @@ __global__ __launch_bounds__(DA_THREADS) void din_att_bwd_kernel(DinAttArgs p) {
   for (int i = 0; i < NW1; ++i) gw1[i] = da_f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
   for (int i = 0; i < NW2; ++i) gw2[i] = da_f32x4{0.f, 0.f, 0.f, 0.f};
-  float gb1[H1T], gb2[H2T], gw3[H2T];  // per-lane column partials (column 16 n + lane % 16)
+  float gb1[J1], gb2[J2], gw3[J2];  // per-lane column partials (column 16 n + lane % 16)
 #pragma unroll
-  for (int n = 0; n < H1T; ++n) gb1[n] = 0.f;
+  for (int n = 0; n < J1; ++n) gb1[n] = 0.f;
 #pragma unroll
-  for (int n = 0; n < H2T; ++n) gb2[n] = gw3[n] = 0.f;
+  for (int n = 0; n < J2; ++n) gb2[n] = gw3[n] = 0.f;
   float gb3 = 0.f;
 
   DaRaw cur = {};
@@ -459,40 +478,45 @@ __global__ __launch_bounds__(DA_THREADS) void din_att_bwd_kernel(DinAttArgs p) {
     const float dsj = aj * (gj - ag);
     if (w == 0) gb3 += sum_wave(dsj);  // lane 0's value is written
     {
-      da_f32x4 acc[H1T];
-      da_layer1<S, H1T>(sm, w, lane, acc);
+      da_f32x4 acc[J1];
+      da_layer1<S, H1T>(sm, rt, cg, lane, acc);
 #pragma unroll
-      for (int n = 0; n < H1T; ++n) {
+      for (int jn = 0; jn < J1; ++jn) {
+        const int n = cg + DA_CG * jn;
+        if (n >= H1T) continue;
         const int col = 16 * n + (lane & 15);
         const float bias = sb1[col];
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
-          const int r = 16 * w + 4 * (lane >> 4) + i;
-          const uint16_t h = f32_to_bf16_rne(fmaxf(acc[n][i] + bias, 0.f));
+          const int r = 16 * rt + 4 * (lane >> 4) + i;
+          const uint16_t h = f32_to_bf16_rne(fmaxf(acc[jn][i] + bias, 0.f));
           sm[S::oH1 + r * S::LDH + col] = h;
           sm[S::oH1T + col * DA_LDT + r] = h;
         }
       }
     }
     __syncthreads();
-    // ---- phase 2: layer 2, dZ2 = ds w3 relu'(z2) -> dZ2 (over this wave's H1 rows), dZ2^T ----
+    // ---- phase 2: layer 2, dZ2 = ds w3 relu'(z2) -> dZ2 (over H1), dZ2^T ----
     {
-      da_f32x4 acc[H2T];
-      da_layer2<S, H1K, H2T>(sm, w, lane, acc);
+      da_f32x4 acc[J2];
+      da_layer2<S, H1K, H2T>(sm, rt, cg, lane, acc);
+      __syncthreads();  // both column groups' reads of these H1 rows precede the dZ2 stores
 #pragma unroll
-      for (int n = 0; n < H2T; ++n) {
+      for (int jn = 0; jn < J2; ++jn) {
+        const int n = cg + DA_CG * jn;
+        if (n >= H2T) continue;
         const int col = 16 * n + (lane & 15);
         const float bias = sb2[col], wv = sw3[col];
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
-          const int r = 16 * w + 4 * (lane >> 4) + i;
+          const int r = 16 * rt + 4 * (lane >> 4) + i;
           const float dsr = __shfl(dsj, r);
-          const float h2 = fmaxf(acc[n][i] + bias, 0.f);
+          const float h2 = fmaxf(acc[jn][i] + bias, 0.f);
           const float dz = h2 > 0.f ? dsr * wv : 0.f;
-          gw3[n] = fmaf(dsr, h2, gw3[n]);
-          gb2[n] += dz;
+          gw3[jn] = fmaf(dsr, h2, gw3[jn]);
+          gb2[jn] += dz;
           const uint16_t hz = f32_to_bf16_rne(dz);
-          sm[S::oH1 + r * S::LDH + col] = hz;  // dZ2 over H1 (this wave's rows, read above)
+          sm[S::oH1 + r * S::LDH + col] = hz;
           sm[S::oZ2T + col * DA_LDT + r] = hz;
         }
       }
@@ -500,25 +524,30 @@ __global__ __launch_bounds__(DA_THREADS) void din_att_bwd_kernel(DinAttArgs p) {
     __syncthreads();
     // ---- phase 3: dH1 = dZ2 W2, dZ1 = dH1 relu'(H1) -> dZ1 (over X), dZ1^T; dW2 ----
     {
-      da_f32x4 acc[H1T];
+      da_f32x4 acc[J1];
 #pragma unroll
-      for (int n = 0; n < H1T; ++n) acc[n] = da_f32x4{0.f, 0.f, 0.f, 0.f};
+      for (int jn = 0; jn < J1; ++jn) acc[jn] = da_f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
       for (int s = 0; s < H2K; ++s) {
-        const da_bf16x8 a = da_frag(sm + S::oH1, S::LDH, 16 * w, 32 * s, lane);
+        const da_bf16x8 a = da_frag(sm + S::oH1, S::LDH, 16 * rt, 32 * s, lane);
 #pragma unroll
-        for (int n = 0; n < H1T; ++n)
-          acc[n] = da_mfma(a, da_frag(sm + S::oW2T, S::LDW2T, 16 * n, 32 * s, lane), acc[n]);
+        for (int jn = 0; jn < J1; ++jn) {
+          const int n = cg + DA_CG * jn;
+          if (n < H1T)
+            acc[jn] = da_mfma(a, da_frag(sm + S::oW2T, S::LDW2T, 16 * n, 32 * s, lane), acc[jn]);
+        }
       }
 #pragma unroll
-      for (int n = 0; n < H1T; ++n) {
+      for (int jn = 0; jn < J1; ++jn) {
+        const int n = cg + DA_CG * jn;
+        if (n >= H1T) continue;
         const int col = 16 * n + (lane & 15);
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
-          const int r = 16 * w + 4 * (lane >> 4) + i;
+          const int r = 16 * rt + 4 * (lane >> 4) + i;
           const uint16_t h = sm[S::oH1T + col * DA_LDT + r];
-          const float dz = (h != 0 && !(h & 0x8000u)) ? acc[n][i] : 0.f;
-          gb1[n] += dz;
+          const float dz = (h != 0 && !(h & 0x8000u)) ? acc[jn][i] : 0.f;
+          gb1[jn] += dz;
           const uint16_t hz = f32_to_bf16_rne(dz);
           sm[S::oX + r * S::LDH + col] = hz;  // dZ1 over X (dead since phase 1)
           sm[S::oZ1T + col * DA_LDT + r] = hz;
@@ -526,7 +555,7 @@ __global__ __launch_bounds__(DA_THREADS) void din_att_bwd_kernel(DinAttArgs p) {
       }
 #pragma unroll
       for (int i = 0; i < NW2; ++i) {
-        const int t = w + 4 * i;
+        const int t = w + NWV * i;
         if (t < H2T * H1T) {
           const int m = t / H1T, n = t - m * H1T;
 #pragma unroll
@@ -539,27 +568,38 @@ __global__ __launch_bounds__(DA_THREADS) void din_att_bwd_kernel(DinAttArgs p) {
     __syncthreads();
     // ---- phase 4: dX = dZ1 W1 -> d rows (dk per row, dq parts); dW1 ----
     {
-      da_f32x4 acc[NTX];
+      // the wave's X column tiles: blocks q / k / q-k / q*k of column tiles c16 = cg + DA_CG jx
+      da_f32x4 acc[JX][4];
 #pragma unroll
-      for (int n = 0; n < NTX; ++n) acc[n] = da_f32x4{0.f, 0.f, 0.f, 0.f};
+      for (int jx = 0; jx < JX; ++jx)
+#pragma unroll
+        for (int blk = 0; blk < 4; ++blk) acc[jx][blk] = da_f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
       for (int s = 0; s < H1K; ++s) {
-        const da_bf16x8 a = da_frag(sm + S::oX, S::LDH, 16 * w, 32 * s, lane);
+        const da_bf16x8 a = da_frag(sm + S::oX, S::LDH, 16 * rt, 32 * s, lane);
 #pragma unroll
-        for (int n = 0; n < NTX; ++n)
-          acc[n] = da_mfma(a, da_frag(sm + S::oW1T, S::LDH, 16 * n, 32 * s, lane), acc[n]);
+        for (int jx = 0; jx < JX; ++jx) {
+          const int c16 = cg + DA_CG * jx;
+          if (c16 >= EC) continue;
+#pragma unroll
+          for (int blk = 0; blk < 4; ++blk)
+            acc[jx][blk] = da_mfma(
+                a, da_frag(sm + S::oW1T, S::LDH, 16 * (blk * EC + c16), 32 * s, lane),
+                acc[jx][blk]);
+        }
       }
-      constexpr int EC = E / 16;  // column tiles per block of X
 #pragma unroll
-      for (int c16 = 0; c16 < EC; ++c16) {
+      for (int jx = 0; jx < JX; ++jx) {
+        const int c16 = cg + DA_CG * jx;
+        if (c16 >= EC) continue;
         const int e = 16 * c16 + (lane & 15);
         const float qe = sq[e], due = sdu[e];
         float dqp = 0.f;
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
-          const int r = 16 * w + 4 * (lane >> 4) + i;
-          const float dfq = acc[c16][i], dfk = acc[EC + c16][i];
-          const float dfd = acc[2 * EC + c16][i], dfm = acc[3 * EC + c16][i];
+          const int r = 16 * rt + 4 * (lane >> 4) + i;
+          const float dfq = acc[jx][0][i], dfk = acc[jx][1][i];
+          const float dfd = acc[jx][2][i], dfm = acc[jx][3][i];
           const float ke = bf16_to_f32(sm[S::oXT + (E + e) * DA_LDT + r]);
           const float ar = __shfl(aj, r);
           const float dk = fmaf(ar, due, dfk - dfd + dfm * qe);
@@ -568,11 +608,11 @@ __global__ __launch_bounds__(DA_THREADS) void din_att_bwd_kernel(DinAttArgs p) {
           dqp += dfq + dfd + dfm * ke;
         }
         dqp = swap32_sum(swap16_sum(dqp));  // the 4 row groups of column e
-        if (lane < 16) sdq[w * E + e] = dqp;
+        if (lane < 16) sdq[rt * E + e] = dqp;
       }
 #pragma unroll
       for (int i = 0; i < NW1; ++i) {
-        const int t = w + 4 * i;
+        const int t = w + NWV * i;
         if (t < H1T * NTX) {
           const int m = t / NTX, n = t - m * NTX;
 #pragma unroll
@@ -598,7 +638,7 @@ __global__ __launch_bounds__(DA_THREADS) void din_att_bwd_kernel(DinAttArgs p) {
         *pb3 = pw3 + H2;
 #pragma unroll
   for (int i = 0; i < NW1; ++i) {
-    const int t = w + 4 * i;
+    const int t = w + NWV * i;
     if (t < H1T * NTX) {
       const int m = t / NTX, n = t - m * NTX;
 #pragma unroll
@@ -610,7 +650,7 @@ __global__ __launch_bounds__(DA_THREADS) void din_att_bwd_kernel(DinAttArgs p) {
   }
 #pragma unroll
   for (int i = 0; i < NW2; ++i) {
-    const int t = w + 4 * i;
+    const int t = w + NWV * i;
     if (t < H2T * H1T) {
       const int m = t / H1T, n = t - m * H1T;
 #pragma unroll
@@ -620,27 +660,24 @@ __global__ __launch_bounds__(DA_THREADS) void din_att_bwd_kernel(DinAttArgs p) {
       }
     }
   }
-  // column partials: lanes l, l + 16, l + 32, l + 48 hold the same column; then the waves
+  // column partials: lanes l, l + 16, l + 32, l + 48 hold the same column; then the
+  // 4 row tiles (each column belongs to one column group)
   __syncthreads();
   float *red = reinterpret_cast<float *>(da_lds);  // [4][H1N + 2 H2N] (LDS now dead)
   constexpr int RW = S::H1N + 2 * S::H2N;
 #pragma unroll
-  for (int n = 0; n < H1T; ++n) {
-    float v = gb1[n];
-    v += __shfl_xor(v, 16);
-    v += __shfl_xor(v, 32);
-    if (lane < 16) red[w * RW + 16 * n + lane] = v;
+  for (int jn = 0; jn < J1; ++jn) {
+    const int n = cg + DA_CG * jn;
+    const float v = swap32_sum(swap16_sum(gb1[jn]));
+    if (n < H1T && lane < 16) red[rt * RW + 16 * n + lane] = v;
   }
 #pragma unroll
-  for (int n = 0; n < H2T; ++n) {
-    float v = gb2[n], u = gw3[n];
-    v += __shfl_xor(v, 16);
-    v += __shfl_xor(v, 32);
-    u += __shfl_xor(u, 16);
-    u += __shfl_xor(u, 32);
-    if (lane < 16) {
-      red[w * RW + S::H1N + 16 * n + lane] = v;
-      red[w * RW + S::H1N + S::H2N + 16 * n + lane] = u;
+  for (int jn = 0; jn < J2; ++jn) {
+    const int n = cg + DA_CG * jn;
+    const float v = swap32_sum(swap16_sum(gb2[jn])), u = swap32_sum(swap16_sum(gw3[jn]));
+    if (n < H2T && lane < 16) {
+      red[rt * RW + S::H1N + 16 * n + lane] = v;
+      red[rt * RW + S::H1N + S::H2N + 16 * n + lane] = u;
     }
   }
   __syncthreads();

@@ -280,6 +280,66 @@ def kernel_rooflines(model, data, args):
     return out
 
 
+def din_rooflines(model, data, args):
+    """The fused DIN attention-unit kernels (mrec_din_att_fwd / _bwd, din_att.hip),
+    each launched as the train step launches it on the step's own gathered rows,
+    timed with HIP events over back-to-back graph replays.  Algorithmic FLOP per
+    sample (SURVEY.md §8(d) style, history positions L = 50, unit 4E=128 -> 80 -> 40
+    -> 1): forward F = 2 L (128*80 + 80*40 + 40); the backward launch recomputes the
+    forward and back-propagates (dX and dW: 2F) = 3F.  HBM bytes per sample: fwd
+    reads q + L k rows (E=32 bf16) + L history ids, writes a (L fp32) + top (2E
+    bf16); bwd reads the rows, a, dtop and writes the rows' gradient.
+    Returns {kernel: (seconds, flop per launch, bytes per launch)}."""
+    from pytorchrec_amd import _mrec, dense as D
+    lins = D._din_att_linears(model.att_mlp, model.att_out)
+    B, L, E = args.batch, DIN_L, 2 * model.emb_size
+    assert D.din_att_supported(E, model.att_mlp, model.att_out)
+    dev = model.embeddings.weight.device
+    from pytorchrec_amd.embedding import gather
+    iid = model.iid_column.get_feature_ids(data)
+    cid = model.cid_column.get_feature_ids(data)
+    his = model.his_column.get_feature_ids(data)
+    hcat = model.his_cate_column.get_feature_ids(data)
+    with torch.no_grad():
+        rows = D._bf16_rows(gather(model.embeddings,
+                                   [torch.cat([iid.reshape(-1), his.reshape(-1).to(iid.dtype)]),
+                                    torch.cat([cid.reshape(-1),
+                                               hcat.reshape(-1).to(cid.dtype)])],
+                                   out_dtype=torch.bfloat16))
+    his32 = his.to(torch.int32).contiguous()
+    w1, w2, w3 = (D._weight_f32(m.weight) for m in lins)
+    b1, b2, b3 = (m.bias.detach().float().contiguous() for m in lins)
+    w3 = w3.reshape(-1)
+    H1, H2 = w1.shape[0], w2.shape[0]
+    a = torch.empty(B, L, dtype=torch.float32, device=dev)
+    top = D._alloc(B, 2 * E, torch.bfloat16, dev)
+    dtop = torch.randn(B, 2 * E, device=dev).to(torch.bfloat16)
+    d_rows = D._alloc(rows.shape[0], E, torch.bfloat16, dev)
+    lib = _mrec.lib()
+    parts = int(lib.mrec_din_att_parts(B))
+    part = torch.empty(parts, int(lib.mrec_din_att_param_count(E, H1, H2)),
+                       dtype=torch.float32, device=dev)
+    wargs = (w1.data_ptr(), w1.stride(0), b1.data_ptr(), H1, w2.data_ptr(), w2.stride(0),
+             b2.data_ptr(), H2, w3.data_ptr(), b3.data_ptr())
+
+    def fwd():
+        _mrec.call("mrec_din_att_fwd", rows.data_ptr(), rows.stride(0), his32.data_ptr(),
+                   his32.stride(0), B, L, E, *wargs, a.data_ptr(), top.data_ptr(),
+                   top.stride(0), _mrec.stream_handle())
+
+    def bwd():
+        _mrec.call("mrec_din_att_bwd", rows.data_ptr(), rows.stride(0), B, L, E, *wargs,
+                   a.data_ptr(), dtop.data_ptr(), dtop.stride(0), d_rows.data_ptr(),
+                   d_rows.stride(0), part.data_ptr(), parts, _mrec.stream_handle())
+    F = 2 * L * (4 * E * H1 + H1 * H2 + H2)
+    row_b = (1 + L) * E * 2
+    out = {"mrec_din_att_fwd": (time_launches(fwd, 20), F * B,
+                                (row_b + L * 4 + L * 4 + 2 * E * 2) * B),
+           "mrec_din_att_bwd": (time_launches(bwd, 20), 3 * F * B,
+                                (2 * row_b + L * 4 + 2 * E * 2) * B)}
+    return out
+
+
 PROFILES = os.path.join(os.path.dirname(os.path.abspath(__file__)), "profiles")
 PMC_FILE = os.path.join(PROFILES, "pmc_traffic.json")
 CEIL_FILE = os.path.join(PROFILES, "ceilings.json")
@@ -334,8 +394,8 @@ def end_to_end(args, per_gpu_samples_s):
     if args.model == "din":
         # fwd 51*2*4 + 51*2*16*2 + 8 ids/rows/len; bwd 408 + 2*3264
         nbytes = 3680 + 6936
-        # attention unit [B*L, 64] -> 80 -> 40 -> 1 and top [B, 64] -> 200 -> 80 -> 1
-        fwd = DIN_L * 2 * (64 * 80 + 80 * 40 + 40) + 2 * (64 * 200 + 200 * 80 + 80)
+        # attention unit [B*L, 4E = 128] -> 80 -> 40 -> 1 and top [B, 2E = 64] -> 200 -> 80 -> 1
+        fwd = DIN_L * 2 * (128 * 80 + 80 * 40 + 40) + 2 * (64 * 200 + 200 * 80 + 80)
     else:
         fo = args.model == "deepfm"
         f, b = alg_bytes_per_sample(CRITEO_FIELDS, 16, CRITEO_DENSE, fo)
@@ -649,6 +709,25 @@ def main():
         result["roofline_kernels"] = {k: {"avg_us": round(v[0] * 1e6, 3), "bytes": v[1],
                                           "GB/s": round(v[1] / v[0] / 1e9, 1),
                                           "as_implemented_bytes": v[2]}
+                                      for k, v in ks.items()}
+    if rank == 0 and not args.no_roofline and args.model == "din":
+        ks = din_rooflines(model, datas[0], args)
+        name = max(ks, key=lambda k: ks[k][0])  # the dominant kernel
+        t, fl, nb = ks[name]
+        ach = fl / t / 1e12
+        result["roofline"] = {"bound": "mfma", "kernel": name,
+                              "achieved": round(ach, 2), "peak": MFMA_PEAK_TFLOPS,
+                              "unit": "TFLOP/s", "frac": round(ach / MFMA_PEAK_TFLOPS, 4),
+                              "traffic": None, "avg_us": round(t * 1e6, 3),
+                              "flop_per_launch": fl,
+                              "flop_rule": "attention unit 2 L (128*80 + 80*40 + 40) per "
+                                           "sample forward, x3 for the backward launch "
+                                           "(forward recomputed)",
+                              "hbm_GB/s": round(nb / t / 1e9, 1),
+                              "hbm_frac": round(nb / t / 1e9 / HBM_PEAK_GBS, 4)}
+        result["roofline_kernels"] = {k: {"avg_us": round(v[0] * 1e6, 3), "flop": v[1],
+                                          "TFLOP/s": round(v[1] / v[0] / 1e12, 2),
+                                          "bytes": v[2], "GB/s": round(v[2] / v[0] / 1e9, 1)}
                                       for k, v in ks.items()}
     if rank == 0:
         result["end_to_end"] = end_to_end(args, result["value"] / world)

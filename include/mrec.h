@@ -805,6 +805,19 @@ mrec_status mrec_din_feat_bwd_rows(const void *dfeat, int64_t lddf, const void *
                                    int64_t lddk, void *d_rows, int64_t ld_rows, mrec_stream stream);
 
 /*
+ * DIN lookup ids (ABI 17): out_item / out_cate [batch + batch L] int32 =
+ * [target ids | history ids with invalid positions (his <= 0 and j > 0) as -1].
+ * With mrec_ids.pad_negative set, the gather returns a zero row for -1 and the
+ * embedding backward skips it: a masked history position has an exactly zero
+ * gradient (softmax weight 0), so its PAD-row lookups need no update.
+ * iid / cid [batch], his / hcat [batch, ld >= L], all of ids_dtype (I32 / I64).
+ */
+mrec_status mrec_din_lookup_ids(const void *iid, const void *cid, const void *his, int64_t ld_his,
+                                const void *hcat, int64_t ld_hcat, int32_t ids_dtype,
+                                int64_t batch, int32_t L, int32_t *out_item, int32_t *out_cate,
+                                mrec_stream stream);
+
+/*
  * Fused DIN attention unit (ABI 17): one launch each way replaces
  * mrec_din_feat_fwd + the attention MLP's GEMMs + Linear(H2, 1) + mrec_din_pool_fwd
  * (forward) and mrec_din_pool_bwd + the GEMMs' backward + mrec_din_feat_bwd_rows

@@ -273,6 +273,8 @@ SIGNATURES = {
                                          _i32, _vp, _i64, _vp, _i64, _vp]),
     "mrec_din_feat_bwd_rows": (ctypes.c_int, [_vp, _i64, _vp, _i64, _vp, _i64, _vp, _i64, _i64, _i32,
                                               _i32, _vp, _i64, _vp, _i64, _vp]),
+    "mrec_din_lookup_ids": (ctypes.c_int, [_vp, _vp, _vp, _i64, _vp, _i64, _i32, _i64, _i32, _vp,
+                                           _vp, _vp]),
     "mrec_din_att_supported": (ctypes.c_int32, [_i32, _i32, _i32]),
     "mrec_din_att_parts": (ctypes.c_int64, [_i64]),
     "mrec_din_att_param_count": (ctypes.c_int64, [_i32, _i32, _i32]),

@@ -201,6 +201,31 @@ __global__ __launch_bounds__(256) void din_feat_bwd_kernel(
   }
 }
 
+// DIN lookup ids, one thread per (sample, slot 0..L): out[b] = target id, out[B + b L
+// + j] = history id if position j is valid (his > 0 or j == 0), else -1 (a padded
+// slot: zero row forward, skipped by the backward), for the item and category tables
+template <typename I>
+__global__ __launch_bounds__(256) void din_ids_kernel(const I *__restrict__ iid,
+                                                      const I *__restrict__ cid,
+                                                      const I *__restrict__ his, int64_t ldh,
+                                                      const I *__restrict__ hcat, int64_t ldc,
+                                                      int64_t B, int L, int32_t *__restrict__ out_i,
+                                                      int32_t *__restrict__ out_c) {
+  const int64_t t = static_cast<int64_t>(blockIdx.x) * 256 + threadIdx.x;
+  if (t >= B * (L + 1)) return;
+  const int64_t b = t / (L + 1);
+  const int j = static_cast<int>(t - b * (L + 1));
+  if (j == L) {
+    out_i[b] = static_cast<int32_t>(iid[b]);
+    out_c[b] = static_cast<int32_t>(cid[b]);
+    return;
+  }
+  const I h = his[b * ldh + j];
+  const bool valid = j == 0 || h > 0;
+  out_i[B + b * L + j] = valid ? static_cast<int32_t>(h) : -1;
+  out_c[B + b * L + j] = valid ? static_cast<int32_t>(hcat[b * ldc + j]) : -1;
+}
+
 static bool a16(const void *p, int64_t ld) {
   return (reinterpret_cast<uintptr_t>(p) & 15) == 0 && ld % 8 == 0;
 }
@@ -210,6 +235,30 @@ static bool a16(const void *p, int64_t ld) {
 using namespace mrec;
 
 extern "C" {
+
+mrec_status mrec_din_lookup_ids(const void *iid, const void *cid, const void *his, int64_t ld_his,
+                                const void *hcat, int64_t ld_hcat, int32_t ids_dtype,
+                                int64_t batch, int32_t L, int32_t *out_item, int32_t *out_cate,
+                                mrec_stream stream) {
+  MREC_CHECK_ARG(iid && cid && his && hcat && out_item && out_cate, "NULL pointer");
+  MREC_CHECK_ARG(batch >= 0 && L >= 1 && ld_his >= L && ld_hcat >= L, "bad shape / strides");
+  MREC_CHECK_ARG(ids_dtype == MREC_I32 || ids_dtype == MREC_I64, "ids must be int32 or int64");
+  if (batch == 0) return MREC_OK;
+  const int64_t n = batch * (L + 1);
+  const dim3 g(static_cast<unsigned>((n + 255) / 256));
+  hipStream_t s = static_cast<hipStream_t>(stream);
+  if (ids_dtype == MREC_I32)
+    din_ids_kernel<int32_t><<<g, 256, 0, s>>>(
+        static_cast<const int32_t *>(iid), static_cast<const int32_t *>(cid),
+        static_cast<const int32_t *>(his), ld_his, static_cast<const int32_t *>(hcat), ld_hcat,
+        batch, L, out_item, out_cate);
+  else
+    din_ids_kernel<int64_t><<<g, 256, 0, s>>>(
+        static_cast<const int64_t *>(iid), static_cast<const int64_t *>(cid),
+        static_cast<const int64_t *>(his), ld_his, static_cast<const int64_t *>(hcat), ld_hcat,
+        batch, L, out_item, out_cate);
+  return launch_status("mrec_din_lookup_ids");
+}
 
 mrec_status mrec_din_feat_fwd(const void *q, int64_t ldq, const void *k, int64_t ldk,
                               int64_t batch, int32_t L, int32_t E, void *feat, int64_t ldf,

@@ -37,8 +37,8 @@ __global__ __launch_bounds__(256) void gather_kernel(BankArgs bank, IdsArgs ids,
     if constexpr (ADAM)  // a lazily updated Adam bank: the row as of the last step
       raw = adam_current<T>(bank, bank.row_offset[f] + id, l * EPL, live_elems(bank, l * EPL, EPL),
                             raw, *bank.adam.d_t);
-  } else if (l == 0 && oob) {
-    *oob = 1;
+  } else if (l == 0 && oob && !(ids.pad_negative && id < 0)) {
+    *oob = 1;  // (a negative id of a padded view is a zero row, skipped by the backward)
   }
   const int D = bank.dim;
   const int e0 = l * EPL;

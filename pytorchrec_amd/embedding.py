@@ -242,10 +242,17 @@ def _raise_if_oob(flag: Optional[torch.Tensor]):
         raise IndexError("index out of range in self")
 
 
+class PaddedIds(list):
+    """Per-field id tensors whose negative ids are padding slots (mrec_ids.pad_negative):
+    the gather returns a zero row for them and the backward skips them."""
+    pad_negative = True
+
+
 def _ids_desc(ids: Sequence[torch.Tensor], start: int = 0, count: Optional[int] = None):
+    pn = getattr(ids, "pad_negative", False)
     if start == 0 and count is None:
-        return _mrec.IdsDesc(ids)
-    return _mrec.IdsDesc([t[start:start + count] for t in ids])
+        return _mrec.IdsDesc(ids, pad_negative=pn)
+    return _mrec.IdsDesc([t[start:start + count] for t in ids], pad_negative=pn)
 
 
 def _plan(bank: EmbeddingBank, ids, start: int, count: int, flag):
@@ -434,12 +441,14 @@ class _GatherFn(torch.autograd.Function):
         return grad, None, None, None, None, None, None
 
 
-def gather(bank: EmbeddingBank, ids: Sequence[torch.Tensor], out_dtype=None, with_w=False):
+def gather(bank: EmbeddingBank, ids: Sequence[torch.Tensor], out_dtype=None, with_w=False,
+           pad_negative: bool = False):
     """out[b, f*D:(f+1)*D] = table_f[ids[f][b]] — F ``nn.Embedding`` lookups.
 
-    Returns [B, F*D] (and [B, F] first-order weights if ``with_w``).
+    Returns [B, F*D] (and [B, F] first-order weights if ``with_w``).  With
+    ``pad_negative`` a negative id is a padding slot: a zero row, no gradient.
     """
-    ids = list(ids)
+    ids = PaddedIds(ids) if pad_negative else list(ids)
     if len(ids) != bank.n_tables:
         raise ValueError(f"expected {bank.n_tables} id tensors, got {len(ids)}")
     out_dtype = out_dtype or bank.weight.dtype

@@ -317,3 +317,36 @@ def test_din_fused_rejects_bad_arguments(gpu):
                    w.data_ptr(), 128, w.data_ptr(), 80, w.data_ptr(), 80, w.data_ptr(), 40,
                    w.data_ptr(), w.data_ptr(), w.data_ptr(), x.data_ptr(), 64,
                    _mrec.stream_handle())
+
+
+def test_din_padded_history_lookups_equal_plain_ids(gpu, monkeypatch):
+    """Masked history positions as padding slots (-1: zero row, skipped by the
+    embedding backward) train exactly like the plain ids: their gradient is exactly
+    zero (softmax weight 0).  Two SGD steps at B=512 (large-batch backward): every
+    parameter and every table row bitwise equal, except the PAD row 0, which still
+    gets the forced-valid position-0 lookups and whose hot-row fixed-point sum is
+    scaled by its lookup count (1e-6 relative)."""
+    import bench
+    from pytorchrec_amd.loss import BCEWithLogitsLoss
+    from pytorchrec_amd.model import DIN
+
+    class A:
+        batch, lr = 512, 0.05
+    res = {}
+    for skip in (True, False):
+        monkeypatch.setattr(DIN, "pad_skip", skip)
+        model, _, _, _ = bench.build_din(A, gpu)
+        model.compile(torch.optim.SGD(model.get_parameters(), lr=A.lr), BCEWithLogitsLoss(), [],
+                      gpu)
+        losses = [float(model.train_step(bench.din_batch(A, s, gpu))["loss"].detach())
+                  for s in range(2)]
+        res[skip] = (losses, model)
+    (l1, m1), (l0, m0) = res[True], res[False]
+    assert l1 == l0
+    for (n, a), (_, b) in zip(m1.named_parameters(), m0.named_parameters()):
+        if "embeddings" not in n:
+            assert torch.equal(a, b), n
+    for f in range(m0.embeddings.n_tables):  # row 0 of each table is PAD
+        a, b = m1.embeddings.table(f).detach(), m0.embeddings.table(f).detach()
+        assert torch.equal(a[1:], b[1:]), f
+        torch.testing.assert_close(a[0].float(), b[0].float(), rtol=1e-2, atol=1e-6)

@@ -256,15 +256,17 @@ __device__ __forceinline__ void da_build_x(const DinAttArgs &p, const DaRaw &raw
   }
 }
 
-// Wave w = (row tile rt = w % 4: rows 16 rt .. + 15, column group cg = w / 4):
+// Wave w = (row tile rt = w / 2: rows 16 rt .. + 15, column group cg = w % 2; the
+// waves of one SIMD, w and w + 4, hold different row tiles):
 // a GEMM's 16-column output tiles n = cg, cg + DA_CG, ... of the wave's rows.
 // layer 1: acc[jn] = X[rows] W1^T (tile n = cg + DA_CG jn)
 template <class S, int H1T>
-__device__ __forceinline__ void da_layer1(const uint16_t *sm, int rt, int cg, int lane,
+__device__ __forceinline__ void da_layer1(const uint16_t *sm, int rt, int cg, int lane, bool on,
                                           da_f32x4 (&acc)[(H1T + DA_CG - 1) / DA_CG]) {
   constexpr int J = (H1T + DA_CG - 1) / DA_CG;
 #pragma unroll
   for (int jn = 0; jn < J; ++jn) acc[jn] = da_f32x4{0.f, 0.f, 0.f, 0.f};
+  if (!on) return;
 #pragma unroll
   for (int s = 0; s < S::KT1; ++s) {
     const da_bf16x8 a = da_frag(sm + S::oX, S::LDX, 16 * rt, 32 * s, lane);
@@ -278,11 +280,12 @@ __device__ __forceinline__ void da_layer1(const uint16_t *sm, int rt, int cg, in
 
 // layer 2: acc[jn] = H1[rows] W2^T
 template <class S, int H1K, int H2T>
-__device__ __forceinline__ void da_layer2(const uint16_t *sm, int rt, int cg, int lane,
+__device__ __forceinline__ void da_layer2(const uint16_t *sm, int rt, int cg, int lane, bool on,
                                           da_f32x4 (&acc)[(H2T + DA_CG - 1) / DA_CG]) {
   constexpr int J = (H2T + DA_CG - 1) / DA_CG;
 #pragma unroll
   for (int jn = 0; jn < J; ++jn) acc[jn] = da_f32x4{0.f, 0.f, 0.f, 0.f};
+  if (!on) return;
 #pragma unroll
   for (int s = 0; s < H1K; ++s) {
     const da_bf16x8 a = da_frag(sm + S::oH1, S::LDH, 16 * rt, 32 * s, lane);
@@ -309,7 +312,7 @@ __global__ __launch_bounds__(DA_THREADS) void din_att_fwd_kernel(DinAttArgs p) {
   float *ss = sw3 + S::H2N;        // score parts [DA_CG][64]
   float *sa = ss + DA_CG * DA_ROWS;  // softmax weights [64]
   float *su = sa + DA_ROWS;        // pooled-sum parts [DA_THREADS / E][E]
-  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, rt = w & 3, cg = w >> 2;
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, rt = w >> 1, cg = w & 1;
   da_zero_lds(da_lds, S::fwd_end * 2);
   __syncthreads();
   da_stage_weights<S, false>(p, sm, sb1, sb2, sw3);
@@ -324,10 +327,14 @@ __global__ __launch_bounds__(DA_THREADS) void din_att_fwd_kernel(DinAttArgs p) {
       float qv[8], kv[8];
       da_build_x<S, E, false>(p, cur, task, sm, qv, kv);
     }
+    // rows past the last valid history position only feed masked scores: their
+    // row tiles skip the MLP (wave-uniform: every wave holds all 64 validity bits)
+    const uint64_t vm = __ballot(cur.valid);
+    const bool act = 16 * rt < (vm ? 64 - __clzll(vm) : 0);
     __syncthreads();
     {
       da_f32x4 acc[J1];
-      da_layer1<S, H1T>(sm, rt, cg, lane, acc);
+      da_layer1<S, H1T>(sm, rt, cg, lane, act, acc);
 #pragma unroll
       for (int jn = 0; jn < J1; ++jn) {
         const int n = cg + DA_CG * jn;
@@ -344,7 +351,7 @@ __global__ __launch_bounds__(DA_THREADS) void din_att_fwd_kernel(DinAttArgs p) {
     __syncthreads();
     {
       da_f32x4 acc[J2];
-      da_layer2<S, H1K, H2T>(sm, rt, cg, lane, acc);
+      da_layer2<S, H1K, H2T>(sm, rt, cg, lane, act, acc);
       float part[4] = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
       for (int jn = 0; jn < J2; ++jn) {
@@ -428,7 +435,7 @@ __global__ __launch_bounds__(DA_THREADS) void din_att_bwd_kernel(DinAttArgs p) {
   float *sdu = sq + E;       // du = dtop[b, E:2E] [E]
   float *sg = sdu + E;       // g_j = du . k_j [64]
   float *sdq = sg + DA_ROWS;  // per-row-tile dq parts [4][E]
-  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, rt = w & 3, cg = w >> 2;
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, rt = w >> 1, cg = w & 1;
   da_zero_lds(da_lds, S::bwd_end * 2);
   __syncthreads();
   da_stage_weights<S, true>(p, sm, sb1, sb2, sw3);
@@ -471,6 +478,13 @@ __global__ __launch_bounds__(DA_THREADS) void din_att_bwd_kernel(DinAttArgs p) {
       }
     }
     const float aj = cur.a;  // lane = history row
+    // rows past the last one with a_j != 0 have ds = 0, dX = 0 and add nothing to the
+    // weight gradients: their row tiles skip every MFMA (accumulators stay 0, so the
+    // epilogues store the same zeros), and the dW k steps past them are skipped
+    const uint64_t am = __ballot(aj != 0.f);
+    const int nv = am ? 64 - __clzll(am) : 0;
+    const bool act = 16 * rt < nv;
+    const int kk = nv > 32 ? 2 : 1;
     __syncthreads();
     // ---- phase 1: ds (every wave, lane = row), layer 1 -> H1, H1^T ----
     const float gj = sg[lane];
@@ -479,7 +493,7 @@ __global__ __launch_bounds__(DA_THREADS) void din_att_bwd_kernel(DinAttArgs p) {
     if (w == 0) gb3 += sum_wave(dsj);  // lane 0's value is written
     {
       da_f32x4 acc[J1];
-      da_layer1<S, H1T>(sm, rt, cg, lane, acc);
+      da_layer1<S, H1T>(sm, rt, cg, lane, act, acc);
 #pragma unroll
       for (int jn = 0; jn < J1; ++jn) {
         const int n = cg + DA_CG * jn;
@@ -499,7 +513,7 @@ __global__ __launch_bounds__(DA_THREADS) void din_att_bwd_kernel(DinAttArgs p) {
     // ---- phase 2: layer 2, dZ2 = ds w3 relu'(z2) -> dZ2 (over H1), dZ2^T ----
     {
       da_f32x4 acc[J2];
-      da_layer2<S, H1K, H2T>(sm, rt, cg, lane, acc);
+      da_layer2<S, H1K, H2T>(sm, rt, cg, lane, act, acc);
       __syncthreads();  // both column groups' reads of these H1 rows precede the dZ2 stores
 #pragma unroll
       for (int jn = 0; jn < J2; ++jn) {
@@ -529,6 +543,7 @@ __global__ __launch_bounds__(DA_THREADS) void din_att_bwd_kernel(DinAttArgs p) {
       for (int jn = 0; jn < J1; ++jn) acc[jn] = da_f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
       for (int s = 0; s < H2K; ++s) {
+        if (!act) break;
         const da_bf16x8 a = da_frag(sm + S::oH1, S::LDH, 16 * rt, 32 * s, lane);
 #pragma unroll
         for (int jn = 0; jn < J1; ++jn) {
@@ -560,6 +575,7 @@ __global__ __launch_bounds__(DA_THREADS) void din_att_bwd_kernel(DinAttArgs p) {
           const int m = t / H1T, n = t - m * H1T;
 #pragma unroll
           for (int s = 0; s < 2; ++s)
+            if (s < kk)
             gw2[i] = da_mfma(da_frag(sm + S::oZ2T, DA_LDT, 16 * m, 32 * s, lane),
                              da_frag(sm + S::oH1T, DA_LDT, 16 * n, 32 * s, lane), gw2[i]);
         }
@@ -576,6 +592,7 @@ __global__ __launch_bounds__(DA_THREADS) void din_att_bwd_kernel(DinAttArgs p) {
         for (int blk = 0; blk < 4; ++blk) acc[jx][blk] = da_f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
       for (int s = 0; s < H1K; ++s) {
+        if (!act) break;
         const da_bf16x8 a = da_frag(sm + S::oX, S::LDH, 16 * rt, 32 * s, lane);
 #pragma unroll
         for (int jx = 0; jx < JX; ++jx) {
@@ -617,6 +634,7 @@ __global__ __launch_bounds__(DA_THREADS) void din_att_bwd_kernel(DinAttArgs p) {
           const int m = t / NTX, n = t - m * NTX;
 #pragma unroll
           for (int s = 0; s < 2; ++s)
+            if (s < kk)
             gw1[i] = da_mfma(da_frag(sm + S::oZ1T, DA_LDT, 16 * m, 32 * s, lane),
                              da_frag(sm + S::oXT, DA_LDT, 16 * n, 32 * s, lane), gw1[i]);
         }

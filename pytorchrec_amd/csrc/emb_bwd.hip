@@ -230,7 +230,7 @@ __device__ __forceinline__ bool co_reduce(const CoReduce &co, int b) {
   int p = 0;
   while (p + 1 < co.n && b >= co.start[p + 1]) ++p;
   const int local = b - co.start[p];
-  if (local < co.nblk[p]) splitk_reduce_body(co.g[p], local, co.nblk[p]);
+  if (local < co.nblk[p]) splitk_reduce_body<false>(co.g[p], local, co.nblk[p]);
   return true;
 }
 

@@ -133,19 +133,24 @@ __device__ __forceinline__ void update_block4_tower(const GemmArgs &g, int64_t m
   }
 }
 
-// slab 0 + slab 1 + ... + slab sk-1 of 4 columns, in slab order; the loads of 8
-// slabs are issued before their adds (one memory round trip per 8 slabs instead of
-// one per slab: the DIN top tower's 16-slice reduce took 28 us as a dependent chain)
+// slab 0 + slab 1 + ... + slab sk-1 of 4 columns, in slab order.  DEEP: the loads
+// of 8 slabs are issued before their adds (one memory round trip per 8 slabs
+// instead of one per slab: the DIN top tower's 16-slice reduce took 28 us as a
+// dependent chain); the embedding apply's co-launched reduce (4 slices) keeps the
+// plain loop, whose registers do not weigh on the apply
+template <bool DEEP>
 __device__ __forceinline__ float4 splitk_sum4(const float *p, int64_t slab, int sk) {
   float4 s = *reinterpret_cast<const float4 *>(p);
   int z = 1;
-  for (; z + 8 <= sk; z += 8) {
-    float4 t[8];
+  if constexpr (DEEP) {
+    for (; z + 8 <= sk; z += 8) {
+      float4 t[8];
 #pragma unroll
-    for (int u = 0; u < 8; ++u) t[u] = *reinterpret_cast<const float4 *>(p + (z + u) * slab);
+      for (int u = 0; u < 8; ++u) t[u] = *reinterpret_cast<const float4 *>(p + (z + u) * slab);
 #pragma unroll
-    for (int u = 0; u < 8; ++u) {
-      s.x += t[u].x; s.y += t[u].y; s.z += t[u].z; s.w += t[u].w;
+      for (int u = 0; u < 8; ++u) {
+        s.x += t[u].x; s.y += t[u].y; s.z += t[u].z; s.w += t[u].w;
+      }
     }
   }
   for (; z < sk; ++z) {
@@ -156,6 +161,7 @@ __device__ __forceinline__ float4 splitk_sum4(const float *p, int64_t slab, int 
 }
 
 // fixed-order reduction of the split-K partial slabs + epilogue (4 columns / thread)
+template <bool DEEP = true>
 __device__ __forceinline__ void splitk_reduce_body(const GemmArgs &g, int64_t bid, int64_t nblk) {
   const int64_t ncols = g.b_ones_col >= 0 ? g.b_ones_col + 1 : g.N;
   const int64_t q = g.ldws / 4;
@@ -177,7 +183,7 @@ __device__ __forceinline__ void splitk_reduce_body(const GemmArgs &g, int64_t bi
       float4 v[4];
 #pragma unroll
       for (int r = 0; r < 4; ++r)
-        v[r] = splitk_sum4(g.ws + (m0 + r) * g.ldws + n, slab, g.split_k);
+        v[r] = splitk_sum4<DEEP>(g.ws + (m0 + r) * g.ldws + n, slab, g.split_k);
       update_block4_tower(g, m0, n, v);
     }
   }
@@ -186,7 +192,7 @@ __device__ __forceinline__ void splitk_reduce_body(const GemmArgs &g, int64_t bi
     const int64_t m = i / q, n = (i - m * q) * 4;
     if (n >= ncols && n >= g.pad_to) continue;
     if (m < M4 && n + 4 <= N4 * 4) continue;  // done above in a 4 x 4 block
-    const float4 s = splitk_sum4(g.ws + m * g.ldws + n, slab, g.split_k);
+    const float4 s = splitk_sum4<DEEP>(g.ws + m * g.ldws + n, slab, g.split_k);
     const float e[4] = {s.x, s.y, s.z, s.w};
 #pragma unroll
     for (int j = 0; j < 4; ++j)

@@ -319,27 +319,35 @@ def test_din_fused_rejects_bad_arguments(gpu):
                    _mrec.stream_handle())
 
 
-def test_din_padded_history_lookups_equal_plain_ids(gpu, monkeypatch):
+@pytest.mark.parametrize("batch,ids64", [(512, False), (64, True)])
+def test_din_padded_history_lookups_equal_plain_ids(gpu, monkeypatch, batch, ids64):
     """Masked history positions as padding slots (-1: zero row, skipped by the
     embedding backward) train exactly like the plain ids: their gradient is exactly
     zero (softmax weight 0).  Two SGD steps at B=512 (large-batch backward): every
     parameter and every table row bitwise equal, except the PAD row 0, which still
     gets the forced-valid position-0 lookups and whose hot-row fixed-point sum is
-    scaled by its lookup count (1e-6 relative)."""
+    scaled by its lookup count (1e-6 relative).  B=512: the large-batch backward
+    (26 K lookups per table); B=64 with int64 ids: the hash-plan backward."""
     import bench
     from pytorchrec_amd.loss import BCEWithLogitsLoss
     from pytorchrec_amd.model import DIN
 
     class A:
-        batch, lr = 512, 0.05
+        lr = 0.05
+    A.batch = batch
+
+    def data(s):
+        d = bench.din_batch(A, s, gpu)
+        if ids64:
+            d = {k: (v.long() if v.dtype == torch.int32 else v) for k, v in d.items()}
+        return d
     res = {}
     for skip in (True, False):
         monkeypatch.setattr(DIN, "pad_skip", skip)
         model, _, _, _ = bench.build_din(A, gpu)
         model.compile(torch.optim.SGD(model.get_parameters(), lr=A.lr), BCEWithLogitsLoss(), [],
                       gpu)
-        losses = [float(model.train_step(bench.din_batch(A, s, gpu))["loss"].detach())
-                  for s in range(2)]
+        losses = [float(model.train_step(data(s))["loss"].detach()) for s in range(2)]
         res[skip] = (losses, model)
     (l1, m1), (l0, m0) = res[True], res[False]
     assert l1 == l0

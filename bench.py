@@ -9,11 +9,13 @@ parameter's backward kernel) over one synthetic Criteo-shaped batch (SURVEY.md
 §8(d)) that is already resident in HBM.  The step is captured as a HIP graph per
 pre-generated batch (4 batches, used in place) and the graphs are replayed in turn.
 
-For N > 1 the driver launches one process per GPU (torch.distributed.run); the
-tables are row-sharded over the ranks and the dense tower is data-parallel
-(RCCL all-to-all / all-reduce inside the captured step); each rank trains on its
-own 4096 samples (weak scaling) and the MAX elapsed time over ranks is reported.
-Rank 0 prints ONE JSON line.
+For N > 1 one process runs per GPU: either torch.distributed.run starts them
+(WORLD_SIZE set, must equal --gpus) or ``bench.py --gpus N`` starts them itself
+(``launch``: subprocess children, rank 0's line relayed).  N > 1 defaults to the C5
+workload (100M-row tables); the tables are row-sharded over the ranks and the
+dense tower is data-parallel (RCCL all-to-all / all-reduce inside the captured
+step); each rank trains on its own 4096 samples (weak scaling) and the MAX
+elapsed time over ranks is reported.  Rank 0 prints ONE JSON line.
 """
 from __future__ import annotations
 
@@ -33,6 +35,7 @@ import torch  # noqa: E402
 CRITEO_FIELDS = 26
 CRITEO_DENSE = 13
 CRITEO_ROWS = 38462  # ceil(1,000,000 / 26), SURVEY.md §8(d) C2
+C5_ROWS = 100_000_000  # rows per table, SURVEY.md §8(d) C5 (row-sharded over the ranks)
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md chip table (spec)
 
 
@@ -43,7 +46,9 @@ def parse():
     p.add_argument("--warmup", type=int, default=10)
     p.add_argument("--model", default="deepfm", choices=["deepfm", "dcnv2", "din"])
     p.add_argument("--batch", type=int, default=4096)
-    p.add_argument("--rows-per-table", type=int, default=CRITEO_ROWS)
+    p.add_argument("--rows-per-table", type=int, default=None,
+                   help="rows of each of the 26 tables (default: 38,462 at N=1 = C2; "
+                        "100,000,000 at N>1 = C5)")
     p.add_argument("--zipf", type=float, default=0.0, help="Zipf alpha for ids (0 = uniform)")
     p.add_argument("--lr", type=float, default=1e-2)
     p.add_argument("--no-graph", action="store_true")
@@ -62,7 +67,67 @@ def parse():
                         "(uniform ids), min(batch, 8192 / W) with --zipf")
     p.add_argument("--force-collectives", action="store_true",
                    help="issue the all-to-alls / all-reduce even at N=1 (RCCL capture check)")
-    return p.parse_args()
+    p.add_argument("--stub-step", action="store_true",
+                   help="launcher check without a GPU: each rank's step is one gloo all-reduce")
+    args = p.parse_args()
+    if args.rows_per_table is None:
+        # N = 1: C2 (~1M rows); N > 1: C5, 100M-row tables row-sharded over the ranks
+        args.rows_per_table = C5_ROWS if args.gpus > 1 else CRITEO_ROWS
+    return args
+
+
+# ----------------------------------------------------------------------------
+# launcher: `bench.py --gpus N` without torch.distributed.run
+# ----------------------------------------------------------------------------
+
+def launch(args) -> int:
+    """One child process per GPU (RANK / LOCAL_RANK / WORLD_SIZE / MASTER_* set, a
+    free 127.0.0.1 port), started with subprocess from this parent, which never
+    touches the GPU (no exec).  Rank 0's JSON line is relayed on stdout; if any rank
+    fails the others are stopped (by PID) and the parent exits non-zero."""
+    import socket
+    import subprocess
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as sk:
+        sk.bind(("127.0.0.1", 0))
+        port = sk.getsockname()[1]
+    procs = []
+    for r in range(args.gpus):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(args.gpus),
+                   LOCAL_WORLD_SIZE=str(args.gpus), MASTER_ADDR="127.0.0.1",
+                   MASTER_PORT=str(port))
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + sys.argv[1:],
+                                      env=env, stdout=subprocess.PIPE if r == 0 else
+                                      subprocess.DEVNULL))
+    rc = 0
+    try:
+        while True:
+            alive = False
+            for r, pr in enumerate(procs):
+                code = pr.poll()
+                if code is None:
+                    alive = True
+                elif code != 0 and rc == 0:
+                    rc = code
+                    print(f"bench: rank {r} exited with {code}; stopping the other ranks",
+                          file=sys.stderr, flush=True)
+                    for q in procs:
+                        if q.poll() is None:
+                            q.terminate()
+            if not alive:
+                break
+            time.sleep(0.05)
+    finally:
+        for q in procs:
+            if q.poll() is None:
+                q.kill()
+    out0 = procs[0].stdout.read() if procs[0].stdout is not None else b""
+    lines = [ln for ln in out0.decode(errors="replace").splitlines() if ln.startswith("{")]
+    if rc == 0 and lines:
+        print(lines[-1], flush=True)
+    elif rc == 0:
+        print("bench: rank 0 printed no JSON line", file=sys.stderr, flush=True)
+        rc = 1
+    return rc
 
 
 # ----------------------------------------------------------------------------
@@ -230,7 +295,10 @@ def kernel_rooflines(model, data, args):
         bank = model.embeddings  # unsharded: time the model's own bank (no second copy of
         # a 100M-row C5 bank); the timed updates run after the timed region
     else:
-        bank = E.EmbeddingBank([args.rows_per_table] * CRITEO_FIELDS, 16,
+        # sharded model: a bank of one shard's rows (the per-GPU footprint; a second
+        # full C5 bank would not fit beside the shard)
+        world = max(1, int(os.environ.get("WORLD_SIZE", "1")))
+        bank = E.EmbeddingBank([max(1, args.rows_per_table // world)] * CRITEO_FIELDS, 16,
                                with_first_order=first_order, dtype=torch.bfloat16, device=dev)
         E.init_bank_(bank, generator=torch.Generator(device=dev).manual_seed(5))
         bank.use_fused_sgd(args.lr)
@@ -529,16 +597,65 @@ def cpu_baseline(args):
 
 # ----------------------------------------------------------------------------
 
+def stub_main(args, json_out, world, rank):
+    """--stub-step: the launcher and the max-over-ranks timing without a GPU (CPU
+    tests): each step is one gloo all-reduce of a small tensor."""
+    import torch.distributed as dist
+    if os.environ.get("BENCH_STUB_FAIL_RANK") == str(rank):  # launcher test: a rank dies
+        raise SystemExit(3)
+    if world > 1:
+        dist.init_process_group("gloo")
+    t = torch.ones(1024)
+
+    def step():
+        if world > 1:
+            dist.all_reduce(t)
+    for _ in range(args.warmup):
+        step()
+    if world > 1:
+        dist.barrier()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+    if world > 1:
+        dist.barrier()
+    el = torch.tensor([time.perf_counter() - t0], dtype=torch.float64)
+    if world > 1:
+        dist.all_reduce(el, op=dist.ReduceOp.MAX)
+    el = float(el)
+    if rank == 0:
+        print(json.dumps({"metric": "launcher stub (gloo all-reduce per step, no GPU)",
+                          "value": round(args.batch * world * args.steps / max(el, 1e-9), 1),
+                          "unit": "samples/s", "n_gpus": world, "steps": args.steps,
+                          "warmup": args.warmup, "ms_per_step": round(el / args.steps * 1e3, 4),
+                          "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
+                          "dtype": "f32", "data": "synthetic",
+                          "config": {"workload": "stub", "global_batch": args.batch * world,
+                                     "rows_per_table": args.rows_per_table,
+                                     "parallelism": f"gloo{world}"}}),
+              file=json_out, flush=True)
+    if dist.is_initialized():
+        dist.destroy_process_group()
+
+
 def main():
     args = parse()
+    env_world = os.environ.get("WORLD_SIZE")
+    if args.gpus > 1 and env_world is None:
+        sys.exit(launch(args))
+    world = int(env_world or "1")
+    if world != args.gpus:
+        raise SystemExit(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={world}: launch one "
+                         f"process per GPU (bench.py --gpus N starts them itself)")
     # stdout carries exactly one JSON line: anything a native library prints there
     # (RCCL's version banner at communicator init) goes to stderr instead
     sys.stdout.flush()
     json_out = os.fdopen(os.dup(1), "w")
     os.dup2(2, 1)
-    world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    if args.stub_step:
+        return stub_main(args, json_out, world, rank)
     sharded = world > 1 or args.shard
     if world > 1 or args.force_collectives:
         import torch.distributed as dist
@@ -646,9 +763,12 @@ def main():
 
     samples = args.batch * world * args.steps
     workloads = {
-        "deepfm": "DeepFM Criteo-shaped (C2): 26 sparse x %d rows, D=16 bf16 tables with packed "
+        "deepfm": "DeepFM Criteo-shaped (%s): 26 sparse x %d rows, D=16 bf16 tables with packed "
                   "first-order weight, 13 dense, MLP 400-400-400, BCE, SGD lr %g (fused "
-                  "row-sparse update)" % (args.rows_per_table, args.lr),
+                  "row-sparse update)%s" % (
+                      "C5" if args.rows_per_table >= C5_ROWS else "C2", args.rows_per_table,
+                      args.lr, ", tables row-sharded (id mod %d) over the ranks, RCCL "
+                      "all-to-all" % world if sharded else ""),
         "dcnv2": "DCN-v2 Criteo-shaped (C3): 26 sparse x %d rows, D=16 bf16, 13 dense, 3 cross "
                  "layers 429x429, deep MLP 400-400, BCE, SGD lr %g" % (args.rows_per_table, args.lr),
         "din": "DIN Amazon-Electronics-shaped (C4): items 63,001(+PAD) / categories 801(+PAD), "

@@ -806,7 +806,11 @@ mrec_status mrec_din_feat_bwd_rows(const void *dfeat, int64_t lddf, const void *
 
 /*
  * DIN lookup ids (ABI 17): out_item / out_cate [batch + batch L] int32 =
- * [target ids | history ids with invalid positions (his <= 0 and j > 0) as -1].
+ * [target ids | history ids with PAD positions (his == 0 and j > 0) as -1].
+ * Any other id that is negative or >= 2^31 (a target, position 0, a negative his,
+ * the category of a non-PAD position) is written as INT32_MAX so that the gather's
+ * range check reports it (tables must have < 2^31 - 1 rows), as nn.Embedding raises
+ * IndexError on it (the reference, torchrec/model/*.py).
  * With mrec_ids.pad_negative set, the gather returns a zero row for -1 and the
  * embedding backward skips it: a masked history position has an exactly zero
  * gradient (softmax weight 0), so its PAD-row lookups need no update.

@@ -37,10 +37,18 @@ def _mlp(units: Sequence[int]) -> nn.Sequential:
 
 
 class RefDeepFM(nn.Module):
-    """DeepFM the reference way.  ``deep=False`` gives FM (config C1)."""
+    """DeepFM the reference way.  ``deep=False`` gives FM (config C1).
+
+    ``bf16_points=True`` is NOT the reference: the same model with every tensor the
+    MI355X tower stores in bf16 rounded there (x0 = [v | dense], the MLP weights as
+    MFMA operands, each hidden activation, and the gradients at the same points:
+    dh_l, dx0; fp32 accumulation; the FM / first-order terms and the output layer's
+    weights stay fp32).  The C2 parity test sizes its bar by this model's distance
+    to the fp64 one."""
 
     def __init__(self, category_nums: List[int], n_dense: int, emb_size: int = 16,
-                 layers=(400, 400, 400), deep: bool = True, dtype=torch.float32, seed: int = 2020):
+                 layers=(400, 400, 400), deep: bool = True, dtype=torch.float32, seed: int = 2020,
+                 bf16_points: bool = False):
         super().__init__()
         torch.manual_seed(seed)
         self.F, self.D, self.n_dense = len(category_nums), emb_size, n_dense
@@ -49,6 +57,7 @@ class RefDeepFM(nn.Module):
         self.dense_w = nn.Linear(n_dense, 1, bias=False) if n_dense else None
         self.global_bias = nn.Parameter(torch.zeros(1))
         self.deep = deep
+        self.bf16_points = bf16_points
         if deep:
             self.mlp = _mlp([self.F * emb_size + n_dense, *layers])
             self.out = nn.Linear(layers[-1], 1)
@@ -66,7 +75,13 @@ class RefDeepFM(nn.Module):
             logit = logit + self.dense_w(dense).squeeze(-1)
         if self.deep:
             x0 = torch.cat([v.reshape(v.shape[0], -1)] + ([dense] if self.n_dense else []), 1)
-            logit = logit + self.out(self.mlp(x0)).squeeze(-1)
+            if not self.bf16_points:
+                return logit + self.out(self.mlp(x0)).squeeze(-1)
+            x = _rb(x0)
+            for m in self.mlp:
+                if isinstance(m, nn.Linear):
+                    x = _rb(torch.relu(x @ _rbv(m.weight).T + m.bias))
+            logit = logit + (x @ self.out.weight.T + self.out.bias).squeeze(-1)
         return logit
 
 
@@ -84,6 +99,23 @@ class _RoundBF16(torch.autograd.Function):
 
 def _rb(x):
     return _RoundBF16.apply(x)
+
+
+class _RoundBF16Value(torch.autograd.Function):
+    """Rounds the value to bf16, passes the gradient through unrounded (a weight
+    read as a bf16 MFMA operand whose gradient is accumulated and kept in fp32)."""
+
+    @staticmethod
+    def forward(ctx, x):
+        return x.to(torch.bfloat16).to(x.dtype)
+
+    @staticmethod
+    def backward(ctx, g):
+        return g
+
+
+def _rbv(x):
+    return _RoundBF16Value.apply(x)
 
 
 class RefDCNv2(nn.Module):

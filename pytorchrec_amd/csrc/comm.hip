@@ -18,6 +18,8 @@
 #include <cstring>
 #include <string>
 
+#include <mutex>
+
 #include "common.h"
 
 namespace {
@@ -45,13 +47,12 @@ struct Rccl {
 };
 
 Rccl g_rccl;
-bool g_tried = false;
 std::string g_open_error;
+std::once_flag g_rccl_once;
 
-bool load_rccl() {
-  if (g_rccl.h) return true;
-  if (g_tried) return false;
-  g_tried = true;
+// opens RCCL once per process (std::call_once: concurrent first callers, e.g. one
+// host thread per device, all wait for the one load and see its result and error)
+void open_rccl() {
   const char *env = getenv("MREC_RCCL_LIB");
   const char *names[] = {env, "librccl.so", "librccl.so.1", "/opt/rocm/lib/librccl.so.1"};
   void *h = nullptr;
@@ -62,7 +63,7 @@ bool load_rccl() {
   if (!h) {
     const char *e = dlerror();
     g_open_error = std::string("cannot open RCCL (librccl.so): ") + (e ? e : "?");
-    return false;
+    return;
   }
   Rccl r;
   r.h = h;
@@ -83,10 +84,14 @@ bool load_rccl() {
   r.error_string = reinterpret_cast<decltype(r.error_string)>(sym("ncclGetErrorString"));
   if (!ok) {
     g_open_error = "RCCL library lacks a required symbol";
-    return false;
+    return;
   }
   g_rccl = r;
-  return true;
+}
+
+bool load_rccl() {
+  std::call_once(g_rccl_once, open_rccl);
+  return g_rccl.h != nullptr;
 }
 
 mrec_status rccl_status(rccl_result r, const char *what) {

@@ -203,7 +203,19 @@ __global__ __launch_bounds__(256) void din_feat_bwd_kernel(
 
 // DIN lookup ids, one thread per (sample, slot 0..L): out[b] = target id, out[B + b L
 // + j] = history id if position j is valid (his > 0 or j == 0), else -1 (a padded
-// slot: zero row forward, skipped by the backward), for the item and category tables
+// slot: zero row forward, skipped by the backward), for the item and category tables.
+// Only a PAD history position (his == 0, j > 0) becomes a padding slot.  Every other
+// id that is negative or does not fit int32 -- the targets, position 0, a negative
+// his anywhere, the category of a non-PAD position, a negative category anywhere --
+// becomes INT32_MAX, a row no table has (the host checks category_num < 2^31 - 1),
+// so the gather's range check raises IndexError for it as nn.Embedding does over
+// the whole [B, L] tensors: never a silent zero row or a wrapped row.  (Not
+// detected: a category id >= its table's rows at a PAD position.)
+template <typename I>
+__device__ __forceinline__ int32_t din_narrow_id(I v) {
+  return (v < 0 || v >= static_cast<I>(INT32_MAX)) ? INT32_MAX : static_cast<int32_t>(v);
+}
+
 template <typename I>
 __global__ __launch_bounds__(256) void din_ids_kernel(const I *__restrict__ iid,
                                                       const I *__restrict__ cid,
@@ -216,14 +228,15 @@ __global__ __launch_bounds__(256) void din_ids_kernel(const I *__restrict__ iid,
   const int64_t b = t / (L + 1);
   const int j = static_cast<int>(t - b * (L + 1));
   if (j == L) {
-    out_i[b] = static_cast<int32_t>(iid[b]);
-    out_c[b] = static_cast<int32_t>(cid[b]);
+    out_i[b] = din_narrow_id(iid[b]);
+    out_c[b] = din_narrow_id(cid[b]);
     return;
   }
   const I h = his[b * ldh + j];
-  const bool valid = j == 0 || h > 0;
-  out_i[B + b * L + j] = valid ? static_cast<int32_t>(h) : -1;
-  out_c[B + b * L + j] = valid ? static_cast<int32_t>(hcat[b * ldc + j]) : -1;
+  const I c = hcat[b * ldc + j];
+  const bool pad = j > 0 && h == 0;  // masked (h < 0 is an error wherever it sits)
+  out_i[B + b * L + j] = pad ? -1 : din_narrow_id(h);
+  out_c[B + b * L + j] = (pad && c >= 0) ? -1 : din_narrow_id(c);
 }
 
 static bool a16(const void *p, int64_t ld) {

@@ -174,8 +174,15 @@ class EmbeddingBank(torch.nn.Module):
         if self.update == "dense":
             return _mrec.BWD_DENSE_GRAD, 0.0
         if self.update == "adam":
+            new_lr = ctypes.c_float(self.current_lr()).value
+            if new_lr != self._optim.lr and self.weight.is_cuda:
+                # the lr changed (a scheduler, a manual decay): rows not looked up since
+                # the last step owe their missed zero-gradient steps at the OLD lr, as
+                # dense Adam took them; bring every row to the current step first
+                _mrec.call("mrec_emb_optim_flush", self.desc().ref(), _mrec.BWD_ADAM,
+                           float(self._optim.lr), _mrec.stream_handle())
             self.optim_state["t"].add_(1)
-            self._optim.lr = float(self.current_lr())  # catch-up lr of stale-row reads
+            self._optim.lr = new_lr  # catch-up lr of stale-row reads from now on
         mode = {"adagrad": _mrec.BWD_ADAGRAD, "rowwise_adagrad": _mrec.BWD_ROWWISE_ADAGRAD,
                 "adam": _mrec.BWD_ADAM}[self.update]
         return mode, self.current_lr()

@@ -28,10 +28,14 @@ from pytorchrec_amd.model.layer.MLP import MLP
 from pytorchrec_amd.utils.argument import ArgumentDescription
 
 
-def din_lookup_ids(iid: Tensor, cid: Tensor, his: Tensor, hcat: Tensor):
+def din_lookup_ids(iid: Tensor, cid: Tensor, his: Tensor, hcat: Tensor, rows=None):
     """[target ids | history ids, invalid positions -1] for the item and category
-    tables (int32, one kernel: mrec_din_lookup_ids)."""
+    tables (int32, one kernel: mrec_din_lookup_ids).  A looked-up id that is negative
+    or past int32 becomes INT32_MAX, which the gather's range check reports as
+    IndexError (``rows``: the two tables' row counts, all below INT32_MAX)."""
     from pytorchrec_amd import _mrec
+    if rows is not None and max(rows) >= 2 ** 31 - 1:
+        raise ValueError("DIN padded lookups need tables of fewer than 2^31 - 1 rows")
     B, L = his.shape
     dt = his.dtype
     iid, cid = iid.reshape(-1).to(dt).contiguous(), cid.reshape(-1).to(dt).contiguous()
@@ -116,7 +120,7 @@ class DIN(IModel):
             # masked history positions (softmax weight 0: an exactly zero gradient)
             # become padding slots (-1): zero rows forward, skipped by the backward, so
             # the PAD row is not a ~B L / 2-lookup hot row of every step's update
-            ids_i, ids_c = din_lookup_ids(iid, cid, his, hcat)
+            ids_i, ids_c = din_lookup_ids(iid, cid, his, hcat, bank.category_nums)
             rows = gather(bank, [ids_i, ids_c], out_dtype=act_dtype, pad_negative=True)
             return dense_ops.din_attention_top_rows(rows, B, his, self.att_mlp, self.att_out)
         rows = gather(bank, [torch.cat([iid.reshape(-1), his.reshape(-1).to(iid.dtype)]),

@@ -143,6 +143,11 @@ def fused_spec(optimizer: Optimizer, group: dict) -> Optional[dict]:
     if type(optimizer) is Adam:
         if group.get("amsgrad", False):
             return None
+        if group.get("decoupled_weight_decay", False) and group.get("weight_decay", 0.0) != 0:
+            # torch >= 2.6 Adam(decoupled_weight_decay=True) decays p by lr*wd BEFORE the
+            # moment update; the fused kernel's decoupled order is the reference AdamW's
+            # (decay after the step, AdamW.py:53-59): keep the dense gradient instead
+            return None
         return dict(kind="adam", eps=group["eps"], betas=group["betas"],
                     weight_decay=group.get("weight_decay", 0.0), decoupled=False)
     return None

@@ -194,12 +194,18 @@ def _errs(got, want, mag=None):
 
 
 @pytest.mark.parametrize("B,L,E,H1,H2,full", [(64, 50, 32, 80, 40, False),
+                                              (4096, 50, 32, 80, 40, False),
+                                              (300, 50, 32, 80, 40, False),
                                               (48, 64, 32, 80, 40, True),
                                               (37, 1, 32, 80, 40, True),
                                               (40, 37, 16, 24, 12, False)])
 def test_din_fused_unit_matches_fp64_reference(gpu, monkeypatch, B, L, E, H1, H2, full):
     """Fused forward (top) and backward (rows' gradient, all six weight gradients)
-    against the fp64 restatement, with the layered GPU path (same bf16 operand
+    against the fp64 restatement, on every sample.  B = 4096 is C4's batch: each
+    persistent workgroup then runs ~16 samples, prefetching the next one's rows and
+    accumulating dW1 / dW2 across its samples in MFMA registers (the weight
+    gradients below sum all 4096 samples); B = 300 is not a multiple of the CU
+    count (uneven samples per workgroup).  Also with the layered GPU path (same bf16 operand
     roundings: X, H1, dZ) measured on the same inputs as the yardstick.
     Bar per quantity: max error <= max(tol, 1.5 x the layered path's max error)
     (tol 3e-2 forward, 5e-2 gradients, relative to the magnitude: a ReLU whose bf16
@@ -358,3 +364,38 @@ def test_din_padded_history_lookups_equal_plain_ids(gpu, monkeypatch, batch, ids
         a, b = m1.embeddings.table(f).detach(), m0.embeddings.table(f).detach()
         assert torch.equal(a[1:], b[1:]), f
         torch.testing.assert_close(a[0].float(), b[0].float(), rtol=1e-2, atol=1e-6)
+
+
+@pytest.mark.parametrize("what", ["neg_iid", "neg_his0", "big_hcat", "neg_cid", "big_his64"])
+def test_din_padded_lookups_still_raise_on_bad_ids(gpu, monkeypatch, what):
+    """With padding slots on (DIN.pad_skip), only an INVALID history position is a
+    padding slot.  A looked-up id out of range -- a negative target id, a negative
+    id at position 0 (always valid), an out-of-range category at a valid position,
+    an int64 history id >= 2^31 -- raises IndexError like nn.Embedding, never a
+    silent zero row or a wrapped row."""
+    import bench
+    from pytorchrec_amd.model import DIN
+
+    class A:
+        batch, lr = 64, 0.05
+    monkeypatch.setattr(DIN, "pad_skip", True)
+    model, _, _, _ = bench.build_din(A, gpu)
+    data = bench.din_batch(A, 0, gpu)
+    if what == "big_his64":
+        data = {k: (v.long() if v.dtype == torch.int32 else v) for k, v in data.items()}
+    valid_pos = 0  # position 0 is always valid
+    if what == "neg_iid":
+        data["iid"][5] = -3
+    elif what == "neg_cid":
+        data["cid"][7] = -1
+    elif what == "neg_his0":
+        data["pos_his"][9, valid_pos] = -2
+    elif what == "big_hcat":
+        data["pos_his_cate"][11, valid_pos] = bench.DIN_CATES + 5
+    else:
+        data["pos_his"][3, valid_pos] = 2 ** 31 + 4  # would wrap to row 4 as int32
+    with pytest.raises(IndexError):
+        model(data)
+        torch.cuda.synchronize()
+    # the unmodified batch runs
+    model(bench.din_batch(A, 0, gpu))

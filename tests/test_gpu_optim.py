@@ -90,7 +90,7 @@ def _oracle_step(kind, spec, P, G, S, t, lr):
                            spec["weight_decay"], spec.get("bias_correction", True))
 
 
-def _run(name, dtype, rows, B, steps, has_w, F, D=16, lr=0.05, seed=0):
+def _run(name, dtype, rows, B, steps, has_w, F, D=16, lr=0.05, seed=0, lr_sched=None):
     from pytorchrec_amd.embedding import gather
     spec, kind = SPECS[name]
     spec = dict(spec)
@@ -111,6 +111,8 @@ def _run(name, dtype, rows, B, steps, has_w, F, D=16, lr=0.05, seed=0):
         S = [(np.zeros((rows, n)), np.zeros((rows, n))) for _ in range(F)]
     sched = [_ids_schedule(rng, rows, B, steps) for _ in range(F)]
     for s in range(steps):
+        if lr_sched is not None:  # an LR scheduler changing the group's lr between steps
+            lr = group["lr"] = lr_sched[s]
         ids = [torch.from_numpy(sched[f][s].astype(np.int32)).cuda() for f in range(F)]
         dy = (rng.standard_normal((B, F * D)) * 0.5).astype(np.float32)
         dyt = torch.from_numpy(dy).cuda()
@@ -136,6 +138,17 @@ def _run(name, dtype, rows, B, steps, has_w, F, D=16, lr=0.05, seed=0):
 def test_fused_optimizer_fp32_matches_dense(gpu, name):
     got, want = _run(name, torch.float32, rows=61, B=96, steps=6, has_w=False, F=3)
     for f in range(3):
+        np.testing.assert_allclose(got[f], want[f], rtol=1e-5, atol=1e-6)
+
+
+@pytest.mark.parametrize("name", ["adam", "adamw_ref", "adagrad"])
+def test_fused_optimizer_lr_change_matches_dense(gpu, name):
+    """The group's lr changes between steps (a scheduler): rows not looked up since
+    the change took their missed zero-gradient Adam steps at the OLD lr in dense
+    Adam, so the fused bank flushes them before installing the new lr."""
+    got, want = _run(name, torch.float32, rows=61, B=96, steps=6, has_w=False, F=2, seed=9,
+                     lr_sched=[0.05, 0.05, 0.02, 0.02, 0.1, 0.005])
+    for f in range(2):
         np.testing.assert_allclose(got[f], want[f], rtol=1e-5, atol=1e-6)
 
 

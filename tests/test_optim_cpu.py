@@ -77,3 +77,7 @@ def test_optimizer_registry_and_fused_spec():
     assert b["kind"] == "adam" and not b["decoupled"] and b["weight_decay"] == 0.2
     assert spec(torch.optim.Adam(p, amsgrad=True)) is None
     assert spec(torch.optim.AdamW(p)) is None  # torch's AdamW orders its decay differently
+    # torch Adam(decoupled_weight_decay=True) decays before the moment update: dense grad
+    assert spec(torch.optim.Adam(p, weight_decay=0.1, decoupled_weight_decay=True)) is None
+    c = spec(torch.optim.Adam(p, decoupled_weight_decay=True))  # no decay: plain Adam
+    assert c["kind"] == "adam" and c["weight_decay"] == 0.0

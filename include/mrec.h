@@ -32,7 +32,7 @@
 extern "C" {
 #endif
 
-#define MREC_ABI_VERSION 17
+#define MREC_ABI_VERSION 18
 #define MREC_MAX_TABLES 64      /* tables per table bank / per call */
 #define MREC_BWD_MAX_BATCH 8192  /* lookups per table per plan/apply call */
 #define MREC_BWD_HASH_MAX_BATCH 4096  /* batches up to this use the hash plan */
@@ -670,7 +670,20 @@ typedef struct {
    * backward as for BCE (dh_out, dx0, head partials, images). */
   int32_t mode;
   const float *dz_in;        /* [batch] for MREC_TOWER_GIVEN_DZ */
+  /* ABI 18: workspace of the cluster kernel (mrec_tower_cluster_ws_bytes(batch)
+   * bytes, 256-B aligned, ZEROED before its first use, left as found).  With it, and
+   * when 4 workgroups per 64 rows fit the device's CUs at once (batch <= 4096 on
+   * MI355X), every 64-row block is computed by 4 workgroups that each own a quarter
+   * of every layer's output columns and swap their slices through the workspace
+   * (pytorchrec_amd/csrc/tower_cl.hip): a quarter of the weight traffic per
+   * workgroup.  NULL: one workgroup per 16 rows.  Word 0 of the workspace becomes
+   * non-zero if a workgroup ever waited ~seconds for its cluster (results invalid). */
+  void *cl_ws;
+  int64_t cl_ws_bytes;
 } mrec_tower_args;
+
+/* bytes of mrec_tower_args.cl_ws for a batch */
+int64_t mrec_tower_cluster_ws_bytes(int64_t batch);
 
 enum { MREC_TOWER_BCE = 0, MREC_TOWER_FORWARD = 1, MREC_TOWER_GIVEN_DZ = 2 };
 
@@ -810,7 +823,7 @@ mrec_status mrec_din_feat_bwd_rows(const void *dfeat, int64_t lddf, const void *
  * Any other id that is negative or >= 2^31 (a target, position 0, a negative his,
  * the category of a non-PAD position) is written as INT32_MAX so that the gather's
  * range check reports it (tables must have < 2^31 - 1 rows), as nn.Embedding raises
- * IndexError on it (the reference, torchrec/model/*.py).
+ * IndexError on it (the reference models under torchrec/model/).
  * With mrec_ids.pad_negative set, the gather returns a zero row for -1 and the
  * embedding backward skips it: a masked history position has an exactly zero
  * gradient (softmax weight 0), so its PAD-row lookups need no update.

@@ -20,7 +20,7 @@ import torch  # noqa: F401  (must precede the dlopen, see module docstring)
 LIB_DIR = os.path.join(os.path.dirname(os.path.abspath(__file__)), "lib")
 LIB_PATH = os.environ.get("MREC_LIB_PATH") or os.path.join(LIB_DIR, "libmrec.so")
 
-ABI_VERSION = 17
+ABI_VERSION = 18
 MAX_TABLES = 64
 BWD_MAX_BATCH = 8192
 BWD_HASH_MAX_BATCH = 4096  # batches up to this use the hash plan (fusable into a GEMM launch)
@@ -162,7 +162,8 @@ class TowerArgs(ctypes.Structure):
                 ("part", ctypes.c_void_p), ("ldp", ctypes.c_int64),
                 ("loss_part", ctypes.c_void_p), ("ticket", ctypes.c_void_p),
                 ("loss", ctypes.c_void_p), ("kfrag", ctypes.c_int32), ("x0_img", ctypes.c_void_p),
-                ("mode", ctypes.c_int32), ("dz_in", ctypes.c_void_p)]
+                ("mode", ctypes.c_int32), ("dz_in", ctypes.c_void_p),
+                ("cl_ws", ctypes.c_void_p), ("cl_ws_bytes", ctypes.c_int64)]
 
 
 class TowerDwArgs(ctypes.Structure):
@@ -295,6 +296,7 @@ SIGNATURES = {
     "mrec_colsum": (ctypes.c_int, [_vp, _vp, ctypes.c_int, _i64, _i64, _i64, _vp, _vp, _i32,
                                    _f32, _vp]),
     "mrec_tower_fwd_bwd": (ctypes.c_int, [ctypes.POINTER(TowerArgs), _vp]),
+    "mrec_tower_cluster_ws_bytes": (_i64, [_i64]),
     "mrec_tower_image_elems": (ctypes.c_int64, [_i64, _i64, _i32]),
     "mrec_tower_weight_prep": (ctypes.c_int, [_vp, _i64, _i64, _i64, _vp, _vp, _vp]),
 }

@@ -94,15 +94,6 @@ struct TowerArgs {
   const float *dz_in;
 };
 
-__host__ __device__ __forceinline__ int tw_ceil(int a, int b) { return (a + b - 1) / b; }
-// readable columns of a block: whole k steps of 32
-__host__ __device__ __forceinline__ int tw_cols(int w) { return tw_ceil(w, 32) * 32; }
-// row stride: the readable columns rounded up to 32 (mod 256) bytes
-__host__ __device__ __forceinline__ int tw_stride(int w) {
-  return tw_ceil(tw_cols(w) * 2 - 32, 256) * 256 + 32;
-}
-
-__device__ __forceinline__ bool bf16_pos(uint32_t h) { return h != 0u && !(h & 0x8000u); }
 
 typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
 
@@ -613,6 +604,11 @@ __global__ __launch_bounds__(256) void tower_prep_kernel(const float *__restrict
 
 static unsigned long long *g_tower_stamps = nullptr;  // mrec_tower_debug_stamps
 
+unsigned long long *tower_debug_stamps() { return g_tower_stamps; }
+
+// tower_cl.hip: the cluster kernel (false: not applicable, run the 16-row kernel)
+bool tower_cluster_launch(const mrec_tower_args &s, hipStream_t st, mrec_status *status);
+
 static bool al16(const void *p, int64_t ld) {
   return p && (reinterpret_cast<uintptr_t>(p) & 15) == 0 && ld % 8 == 0;
 }
@@ -806,9 +802,13 @@ mrec_status mrec_tower_fwd_bwd(const mrec_tower_args *p, mrec_stream stream) {
     const int v = e ? atoi(e) : TW_PF_DEFAULT;
     return (v == 6 || v == 8) ? v : 4;
   }();
+  hipStream_t st = static_cast<hipStream_t>(stream);
+  {
+    mrec_status cs = MREC_OK;  // 64-row clusters of 4 workgroups when they fit (tower_cl.hip)
+    if (tower_cluster_launch(s, st, &cs)) return cs;
+  }
   const int64_t grid = (s.batch + TW_ROWS - 1) / TW_ROWS;
   const dim3 gd(static_cast<unsigned>(grid));
-  hipStream_t st = static_cast<hipStream_t>(stream);
   if (pf_env == 8)
     tower_kernel<8><<<gd, TW_THREADS, a.lds_bytes, st>>>(a);
   else if (pf_env == 6)

@@ -59,4 +59,16 @@ __host__ __device__ __forceinline__ int64_t kfrag_idx(int64_t b, int64_t c, int6
   return (((c >> 4) * nsteps + (b >> 5)) * 64 + (c & 15) + 16 * ((b & 31) >> 3)) * 8 + (b & 7);
 }
 
+__host__ __device__ __forceinline__ int tw_ceil(int a, int b) { return (a + b - 1) / b; }
+// readable columns of an LDS activation block: whole k steps of 32
+__host__ __device__ __forceinline__ int tw_cols(int w) { return tw_ceil(w, 32) * 32; }
+// LDS row stride: the readable columns rounded up to 32 (mod 256) bytes, which makes
+// the MFMA operand reads (ds_read_b128, lane l: row l % 16, 16 B at k 8 (l / 16))
+// bank-conflict free
+__host__ __device__ __forceinline__ int tw_stride(int w) {
+  return tw_ceil(tw_cols(w) * 2 - 32, 256) * 256 + 32;
+}
+
+__device__ __forceinline__ bool bf16_pos(uint32_t h) { return h != 0u && !(h & 0x8000u); }
+
 }  // namespace mrec

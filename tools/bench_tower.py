@@ -18,6 +18,7 @@ p.add_argument("--reps", type=int, default=100)
 p.add_argument("--rowmajor", action="store_true", help="row-major operand outputs (kfrag off)")
 p.add_argument("--cold", action="store_true", help="128 MB fill before every launch (timed with it)")
 p.add_argument("--reemit", action="store_true", help="re-emit the weight images before every launch")
+p.add_argument("--no-cluster", action="store_true", help="the 16-row kernel (no cluster workspace)")
 args = p.parse_args()
 widths = [int(x) for x in args.widths.split(",")]
 B, L = args.batch, len(widths) - 1
@@ -64,6 +65,10 @@ a.dz, a.part, a.ldp = dz.data_ptr(), part.data_ptr(), part.stride(0)
 a.loss_part, a.ticket, a.loss = lp.data_ptr(), D._ticket(dev).data_ptr(), loss.data_ptr()
 if kfrag:
     a.kfrag, a.x0_img = 1, x0_img.data_ptr()
+cluster = not args.no_cluster
+if cluster:
+    cws = D.tower_cluster_ws(dev, B)
+    a.cl_ws, a.cl_ws_bytes = cws.data_ptr(), cws.numel()
 
 
 flush = torch.empty(128 << 20, dtype=torch.uint8, device=dev) if "--cold" in sys.argv else None
@@ -97,13 +102,14 @@ e1.synchronize()
 us = e0.elapsed_time(e1) / args.reps * 1e3
 wbytes = sum(int(im[0].numel() + im[1].numel()) * 2 for im in imgs)
 flops = 2 * B * sum(widths[l] * widths[l + 1] for l in range(L)) * 2
-print(json.dumps({"widths": widths, "batch": B, "us": round(us, 2),
+print(json.dumps({"widths": widths, "batch": B, "cluster": cluster, "us": round(us, 2),
                   "weight_stream_GBps_per_CU": round(wbytes / (us * 1e-6) / 1e9, 1),
                   "TFLOPs": round(flops / (us * 1e-6) / 1e12, 1)}))
 
 # ---- phase stamps of one launch (diagnostic build hook) ------------------------
-grid = (B + 15) // 16
-st = torch.zeros(grid, 16, dtype=torch.int64, device=dev)
+NS = 32 if cluster else 16
+grid = ((B + 63) // 64) * 4 if cluster else (B + 15) // 16
+st = torch.zeros(grid, NS, dtype=torch.int64, device=dev)
 fn = _mrec.lib().mrec_tower_debug_stamps
 fn.argtypes, fn.restype = [ctypes.c_void_p], None
 for _ in range(3):
@@ -114,12 +120,24 @@ fn(None)
 torch.cuda.synchronize()
 t = st.cpu().double() * 10.0 / 1e3  # 100 MHz ticks -> us
 t0 = t[:, 0].min()
-names = {0: "start", 1: "x0 loaded", 2: "fwd1", 3: "fwd2", 4: "fwd3", 5: "head dot",
-         13: "dh_L (w0)", 14: "parts (w0)", 6: "head",
-         7: "bwd_L", 8: "bwd_L-1", 9: "bwd_L-2", 10: "bwd_L-3", 11: "bwd done", 12: "ticket"}
-used = [k for k in (0, 1, 2, 3, 4, 5, 13, 14, 6, 7, 8, 9, 10, 11, 12) if bool((st[:, k] != 0).all())]
+if cluster:
+    names = {0: "start", 1: "x0 loaded"}
+    for l in range(L):
+        names.update({2 + 3 * l: f"fwd{l} peers in", 3 + 3 * l: f"fwd{l} done",
+                      4 + 3 * l: f"fwd{l} published"})
+    names.update({14: "z published", 15: "z peers in", 16: "dh_L published", 29: "end"})
+    for j, l in enumerate(range(L - 1, -1, -1)):
+        sb = 17 + 3 * j
+        names.update({sb: f"bwd{l} peers in", sb + 1: f"bwd{l} done", sb + 2: f"bwd{l} published"})
+    order = sorted(names)
+else:
+    names = {0: "start", 1: "x0 loaded", 2: "fwd1", 3: "fwd2", 4: "fwd3", 5: "head dot",
+             13: "dh_L (w0)", 14: "parts (w0)", 6: "head",
+             7: "bwd_L", 8: "bwd_L-1", 9: "bwd_L-2", 10: "bwd_L-3", 11: "bwd done", 12: "ticket"}
+    order = (0, 1, 2, 3, 4, 5, 13, 14, 6, 7, 8, 9, 10, 11, 12)
+used = [k for k in order if k in names and bool((st[:, k] != 0).all())]
 rows = []
 for k in used:
     col = t[:, k] - t0
-    rows.append(f"{names.get(k, k):>10}: min {float(col.min()):7.2f} med {float(col.median()):7.2f} max {float(col.max()):7.2f} us")
+    rows.append(f"{k:3d} {names.get(k, k):>18}: min {float(col.min()):7.2f} med {float(col.median()):7.2f} max {float(col.max()):7.2f} us")
 print("\n".join(rows))

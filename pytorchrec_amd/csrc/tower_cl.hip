@@ -151,16 +151,17 @@ __device__ __forceinline__ void cl_gather_peers(const ClArgs &a, const uint16_t 
   const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
       const_cast<uint16_t *>(xb + row0 * CL_LDX), 0, rows * CL_LDX * 2, 0x00020000);
   constexpr int MAXQ = (CL_ROWS * 2 * 32) / CL_THREADS;  // <= 64 chunks per row
+  // every load is issued unconditionally (an invalid one at an offset past the
+  // descriptor's range reads zeros) and consumed after the last: as branches, each
+  // load was followed by its own wait, one round trip per chunk
   u32x4 v[MAXQ];
 #pragma unroll
   for (int q = 0; q < MAXQ; ++q) {
     const int i = threadIdx.x + q * CL_THREADS;
-    v[q] = u32x4{0u, 0u, 0u, 0u};
-    if (i < CL_ROWS * nch) {
-      const int r = i / nch, k = i - r * nch;
-      const int ch = k < 2 * t0 ? k : k + 2 * (t1 - t0);
-      if (r < rows) v[q] = __builtin_amdgcn_raw_buffer_load_b128(rs, (r * CL_LDX + ch * 8) * 2, 0, kSc1);
-    }
+    const int r = i / nch, k = i - r * nch;
+    const int ch = k < 2 * t0 ? k : k + 2 * (t1 - t0);
+    const int off = (i < CL_ROWS * nch && r < rows) ? (r * CL_LDX + ch * 8) * 2 : 0x40000000;
+    v[q] = __builtin_amdgcn_raw_buffer_load_b128(rs, off, 0, kSc1);
   }
   const int s_in = a.s_in;
 #pragma unroll
@@ -441,14 +442,18 @@ __global__ __launch_bounds__(CL_THREADS) void tower_cl_kernel(ClArgs a) {
   {
     const int xch = tw_ceil(a.width[0], 8);
     constexpr int XQ = (CL_ROWS * 64) / CL_THREADS;  // <= 64 chunks per row (512 columns)
-    uint4 xr[XQ];
+    const int xrows = static_cast<int>(min<int64_t>(CL_ROWS, a.B - row0));
+    const __amdgpu_buffer_rsrc_t xrs = __builtin_amdgcn_make_buffer_rsrc(
+        const_cast<uint16_t *>(a.x0 + row0 * a.ld_x0), 0, static_cast<int>(xrows * a.ld_x0 * 2),
+        0x00020000);
+    u32x4 xr[XQ];  // unconditional loads (out-of-range offsets read zeros), one wait
 #pragma unroll
     for (int q = 0; q < XQ; ++q) {
       const int i = tid + q * CL_THREADS;
       const int r = i / xch, k = i - r * xch;
-      xr[q] = (i < CL_ROWS * xch && row0 + r < a.B)
-                  ? *reinterpret_cast<const uint4 *>(a.x0 + (row0 + r) * a.ld_x0 + k * 8)
-                  : make_uint4(0u, 0u, 0u, 0u);
+      const int off = (i < CL_ROWS * xch && r < xrows) ? static_cast<int>((r * a.ld_x0 + k * 8) * 2)
+                                                       : 0x40000000;
+      xr[q] = __builtin_amdgcn_raw_buffer_load_b128(xrs, off, 0, 0);
     }
     float pb[CL_MAXL];
 #pragma unroll
@@ -487,7 +492,7 @@ __global__ __launch_bounds__(CL_THREADS) void tower_cl_kernel(ClArgs a) {
     for (int q = 0; q < XQ; ++q) {
       const int i = tid + q * CL_THREADS;
       const int r = i / xch, k = i - r * xch;
-      if (i < CL_ROWS * xch) *reinterpret_cast<uint4 *>(in + r * a.s_in + k * 16) = xr[q];
+      if (i < CL_ROWS * xch) *reinterpret_cast<u32x4 *>(in + r * a.s_in + k * 16) = xr[q];
     }
     __syncthreads();
   }

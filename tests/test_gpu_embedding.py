@@ -245,6 +245,55 @@ def test_fused_sgd_f32_matches_oracle(gpu, zipf):
     assert bias.grad is not None and abs(float(bias.grad) - dlogit.sum()) < 1e-3
 
 
+@pytest.mark.parametrize("sr", [False, True])
+def test_fused_sgd_c2_zipf_b4096(gpu, sr):
+    """The bench's batch on the C2 bank (26 x 38,462 bf16 rows with the packed
+    first-order column) with Zipf(1.05) ids (SURVEY.md §8(d) variant): hot rows take
+    hundreds of lookups per step (the apply's segment / hot-row paths).  Fused SGD
+    through the interaction backward (dx from the tower, FM2 and first-order
+    gradients, duplicates summed: IModel.py:116-125 -> embedding_dense_backward)
+    against ref.sgd_rows in fp64: every touched value within 1 bf16 ulp (RNE: the
+    one rounding of w - lr g; SR: either neighbour), untouched rows bit-identical."""
+    from pytorchrec_amd.embedding import interact
+    rng = np.random.default_rng(105)
+    F, R, D, B, lr = 26, 38462, 16, 4096, 0.5
+    nums = [R] * F
+    bank = _bank(nums, D, True, torch.bfloat16, update="sgd")
+    bank.use_fused_sgd(lr=lr)
+    bank.stochastic_rounding = sr
+    bank.check_ids = False
+    tabs = _rand_tables(rng, nums, D, torch.bfloat16)
+    wts = [ref.bf16_bits_to_f32(ref.f32_to_bf16_bits((rng.standard_normal(R) * 0.3).astype(np.float32)))
+           for _ in range(F)]
+    _fill(bank, tabs, wts)
+    before = bank.weight.detach().clone()
+    ids_np = np.stack([np.minimum(rng.zipf(1.05, B) - 1, R - 1) for _ in range(F)], 1)
+    assert np.bincount(ids_np[:, 0]).max() > 100  # hot rows present
+    ids = [torch.from_numpy(ids_np[:, f].astype(np.int32)).to(gpu) for f in range(F)]
+    x0, logit = interact(bank, ids, fm2=True, first_order=True, x0_cols=F * D,
+                         x0_dtype=torch.bfloat16)
+    dx0 = ref.bf16_round((rng.standard_normal((B, F * D)) * 0.01).astype(np.float32))
+    dlogit = (rng.standard_normal(B) * 0.01).astype(np.float32)
+    torch.autograd.backward([x0, logit], [torch.from_numpy(dx0.astype(np.float32)).to(gpu).to(
+        torch.bfloat16), torch.from_numpy(dlogit).to(gpu)])
+    v = np.stack([_as_f32(tabs[f])[ids_np[:, f]] for f in range(F)], 1).astype(np.float64)
+    gv = dx0.reshape(B, F, D) + ref.fm2_bwd(v, dlogit)
+    after = _bits(bank.weight)
+    for f in range(F):
+        o = bank.row_offset[f]
+        want = ref.sgd_rows(_as_f32(tabs[f]), ids_np[:, f], gv[:, f], lr)
+        want_w = ref.sgd_rows(wts[f][:, None].astype(np.float64), ids_np[:, f], dlogit[:, None],
+                              lr)[:, 0]
+        got = ref.bf16_bits_to_f32(after[o:o + R, :D + 1]).astype(np.float64)
+        touched = np.unique(ids_np[:, f])
+        assert np.all(np.abs(got[touched, :D] - want[touched]) <=
+                      ref.bf16_ulp(want[touched]) * 1.0001), f
+        assert np.all(np.abs(got[touched, D] - want_w[touched]) <=
+                      ref.bf16_ulp(want_w[touched]) * 1.0001), f
+        untouched = np.setdiff1d(np.arange(R), touched)
+        assert torch.equal(bank.weight[o + untouched].cpu(), before[o + untouched].cpu()), f
+
+
 def test_fused_sgd_bf16_stochastic_rounding_within_one_ulp(gpu):
     from pytorchrec_amd.embedding import gather
     rng = np.random.default_rng(11)

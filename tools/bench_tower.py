@@ -67,6 +67,7 @@ if kfrag:
     a.kfrag, a.x0_img = 1, x0_img.data_ptr()
 cluster = not args.no_cluster
 if cluster:
+    D.TOWER_CLUSTER = True
     cws = D.tower_cluster_ws(dev, B)
     a.cl_ws, a.cl_ws_bytes = cws.data_ptr(), cws.numel()
 

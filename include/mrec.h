@@ -32,7 +32,7 @@
 extern "C" {
 #endif
 
-#define MREC_ABI_VERSION 18
+#define MREC_ABI_VERSION 19
 #define MREC_MAX_TABLES 64      /* tables per table bank / per call */
 #define MREC_BWD_MAX_BATCH 8192  /* lookups per table per plan/apply call */
 #define MREC_BWD_HASH_MAX_BATCH 4096  /* batches up to this use the hash plan */
@@ -418,6 +418,49 @@ mrec_status mrec_shard_lookup_grad(int64_t batch, int32_t n_tables, int32_t dim,
                                    const void *x0, mrec_dtype x0_dtype, int64_t x0_ld,
                                    const float *dw, float *g_out, int64_t g_ld,
                                    mrec_stream stream);
+
+/*
+ * Compact exchange (ABI 19).  What crosses xGMI per step is one record per
+ * DISTINCT (owner, table, id) each way instead of one 64-B slot row forward and
+ * one fp32 slot row back per lookup:
+ *   sender  mrec_shard_bucketize_dedup -> all-to-all ids (W parts of
+ *           n_tables*cap + n_tables int32: slots, then the per-table counts)
+ *   owner   mrec_shard_gather_wire     -> all-to-all rows (W parts of cap_rows
+ *           records of mrec_shard_wire_bytes each: bf16 dim 16 + w = 36 B)
+ *   sender  mrec_shard_wire_unpack     -> rows in the slot layout of
+ *           mrec_shard_gather (the interaction reads them by pos, unchanged)
+ *   backward: the sender sums the gradients of the lookups of each slot (a
+ *           DENSE_GRAD apply over the slot rows, fixed ascending order), packs them
+ *           (mrec_shard_wire_pack, table dtype) -> all-to-all -> the owner unpacks
+ *           them to fp32 slots (mrec_shard_wire_unpack, to_f32) for
+ *           mrec_emb_bwd_apply_given.
+ * A part's records: table f's entries at [prefix(f), prefix(f) + count(f)) with
+ * prefix(f) = sum of the counts of tables < f, so cap_rows bounds the owner's
+ * total over all tables (far tighter than n_tables * cap); more sets *d_overflow
+ * (the caller raises; nothing is silently dropped from a valid step).
+ */
+mrec_status mrec_shard_bucketize_dedup(const mrec_ids *ids, int32_t n_tables, const int64_t *rows,
+                                       int64_t batch, int32_t world, int32_t cap,
+                                       int32_t *send_ids, int32_t *pos, int32_t *d_overflow,
+                                       int32_t *d_oob_flag, mrec_stream stream);
+/* bytes of one wire record: round4((dim + has_w) * element bytes) */
+int32_t mrec_shard_wire_bytes(int32_t dim, int32_t has_w, mrec_dtype dtype);
+/* owner: rows of the received ids (header = recv_ids) -> wire (no lazy-Adam banks) */
+mrec_status mrec_shard_gather_wire(const mrec_table_bank *local, const int32_t *recv_ids,
+                                   int32_t world, int32_t cap, int32_t cap_rows, void *wire,
+                                   int32_t *d_overflow, mrec_stream stream);
+/* wire records -> slot rows [(p * n_tables + f) * cap + j] (pitch slot_bytes; to_f32:
+ * bf16 records widened to fp32); zero (may be NULL): zero_bytes of the same rows of a
+ * second buffer are cleared (the sender's gradient sums) */
+mrec_status mrec_shard_wire_unpack(const void *wire, int32_t rec_bytes, const int32_t *hdr_ids,
+                                   int32_t world, int32_t n_tables, int32_t cap, int32_t cap_rows,
+                                   void *slots, int64_t slot_bytes, int32_t to_f32, void *zero,
+                                   int64_t zero_bytes, int32_t *d_overflow, mrec_stream stream);
+/* slot rows -> wire records (the first rec_bytes of each row) */
+mrec_status mrec_shard_wire_pack(const void *slots, int64_t slot_bytes, int32_t rec_bytes,
+                                 const int32_t *hdr_ids, int32_t world, int32_t n_tables,
+                                 int32_t cap, int32_t cap_rows, void *wire, int32_t *d_overflow,
+                                 mrec_stream stream);
 
 /* ------------------------------------------------------------------------- */
 /* Dense towers: MFMA bf16 GEMM with fused epilogues                          */

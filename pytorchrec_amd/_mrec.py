@@ -20,7 +20,7 @@ import torch  # noqa: F401  (must precede the dlopen, see module docstring)
 LIB_DIR = os.path.join(os.path.dirname(os.path.abspath(__file__)), "lib")
 LIB_PATH = os.environ.get("MREC_LIB_PATH") or os.path.join(LIB_DIR, "libmrec.so")
 
-ABI_VERSION = 18
+ABI_VERSION = 19
 MAX_TABLES = 64
 BWD_MAX_BATCH = 8192
 BWD_HASH_MAX_BATCH = 4096  # batches up to this use the hash plan (fusable into a GEMM launch)
@@ -295,6 +295,14 @@ SIGNATURES = {
                                             _vp, _vp, _vp, _vp, _vp, _vp, _vp]),
     "mrec_colsum": (ctypes.c_int, [_vp, _vp, ctypes.c_int, _i64, _i64, _i64, _vp, _vp, _i32,
                                    _f32, _vp]),
+    "mrec_shard_bucketize_dedup": (ctypes.c_int, [_ids_p, _i32, ctypes.POINTER(ctypes.c_int64),
+                                                  _i64, _i32, _i32, _vp, _vp, _vp, _vp, _vp]),
+    "mrec_shard_wire_bytes": (_i32, [_i32, _i32, _i32]),
+    "mrec_shard_gather_wire": (ctypes.c_int, [_bank_p, _vp, _i32, _i32, _i32, _vp, _vp, _vp]),
+    "mrec_shard_wire_unpack": (ctypes.c_int, [_vp, _i32, _vp, _i32, _i32, _i32, _i32, _vp, _i64,
+                                              _i32, _vp, _i64, _vp, _vp]),
+    "mrec_shard_wire_pack": (ctypes.c_int, [_vp, _i64, _i32, _vp, _i32, _i32, _i32, _i32, _vp, _vp,
+                                            _vp]),
     "mrec_tower_fwd_bwd": (ctypes.c_int, [ctypes.POINTER(TowerArgs), _vp]),
     "mrec_tower_cluster_ws_bytes": (_i64, [_i64]),
     "mrec_tower_image_elems": (ctypes.c_int64, [_i64, _i64, _i32]),
@@ -425,12 +433,14 @@ class IdsDesc:
                           int(bool(pad_negative)))
 
     @classmethod
-    def exchange_view(cls, buf: torch.Tensor, n_tables: int, cap: int):
-        """Owner-side view of a receive buffer [W][n_tables][cap] (int32, -1 = pad):
-        table f's W*cap entries at buf[f*cap + (i // cap) * n_tables*cap + i % cap]."""
+    def exchange_view(cls, buf: torch.Tensor, n_tables: int, cap: int, part: int = 0):
+        """Owner-side view of a receive buffer of W parts [n_tables][cap] (int32, -1 =
+        pad; ``part`` = int32 per part when the parts carry more, e.g. the compact
+        exchange's counts header): table f's W*cap entries at
+        buf[f*cap + (i // cap) * part + i % cap]."""
         flat = buf.reshape(-1)
         d = cls([flat[f * cap:] for f in range(n_tables)], chunk=cap,
-                chunk_stride=n_tables * cap, pad_negative=True)
+                chunk_stride=part or n_tables * cap, pad_negative=True)
         return d
 
     def ref(self):

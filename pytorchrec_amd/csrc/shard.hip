@@ -1,4 +1,6 @@
 // Row-sharded embedding tables: the id -> owner exchange around the hot path.
+// (The compact exchange of ABI 19 -- bucketize_dedup, gather_wire, wire_move -- is
+// described at its kernels below.)
 //
 // bucketize   (sender, fwd) : stable counting sort of each table's ids by owner
 //                             rank (id % W) into fixed-capacity send slots, and the
@@ -140,6 +142,241 @@ __global__ __launch_bounds__(kBT) void bucketize_kernel(IdsArgs ids, RowsArg row
     const uint32_t cnt = min(static_cast<uint32_t>(cap), hist[(d + 1) * G] - hist[d * G]);
     int32_t *part = send_ids + (static_cast<int64_t>(d) * F + f) * cap;
     for (int s = static_cast<int>(cnt) + tid; s < cap; s += kBT) part[s] = -1;
+  }
+}
+
+// ---------------------------------------------------------------------------
+// Compact (deduplicated) exchange, ABI 19.
+//
+// bucketize_dedup: as bucketize, but only the FIRST lookup of each distinct id
+// (ascending sample order) takes a slot -- the distinct ids of a table are found in
+// an LDS hash table (linear probing; the smallest sample index of each id kept by
+// an LDS atomic min) -- and every later lookup of that id gets the same pos.  Each
+// owner part of send_ids is [n_tables][cap] slots followed by the n_tables counts
+// (the header every wire kernel reads).
+// ---------------------------------------------------------------------------
+
+constexpr uint32_t kEmpty = 0xffffffffu;
+
+__device__ __forceinline__ uint32_t id_hash(uint32_t x, uint32_t mask) {
+  return (x * 2654435761u) & mask;
+}
+
+__global__ __launch_bounds__(kBT) void bucketize_dedup_kernel(IdsArgs ids, RowsArg rows, int64_t B,
+                                                              int W, int cap, int F, int hs,
+                                                              int32_t *__restrict__ send_ids,
+                                                              int32_t *__restrict__ pos,
+                                                              int32_t *__restrict__ overflow,
+                                                              int32_t *__restrict__ oob) {
+  __shared__ uint32_t hist[kBHist];
+  __shared__ uint32_t wtot[kBWaves];
+  extern __shared__ uint32_t hash_lds[];  // keys [hs] | (first << 16 | slot) [hs]
+  uint32_t *keys = hash_lds;
+  uint32_t *fs = hash_lds + hs;
+  const uint32_t hmask = static_cast<uint32_t>(hs - 1);
+  const int f = blockIdx.x;
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int64_t rows_f = rows.v[f];
+  const int rounds = static_cast<int>((B + kBT - 1) / kBT);  // <= 8 (B <= 8192)
+  const int G = rounds * kBWaves;
+  const int nh = (W + 1) * G;
+  const int nbits = 32 - __clz(static_cast<uint32_t>(W));
+  const uint64_t lt = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
+  const int64_t P = static_cast<int64_t>(F) * cap + F;  // int32 per owner part
+  constexpr int kR = 8;
+  int64_t idv[kR];
+#pragma unroll
+  for (int r = 0; r < kR; ++r) {
+    const int64_t i = static_cast<int64_t>(r) * kBT + tid;
+    idv[r] = (r < rounds && i < B) ? load_id(ids, f, i) : -2;
+  }
+  for (int i = tid; i < nh; i += kBT) hist[i] = 0u;
+  for (int i = tid; i < hs; i += kBT) {
+    keys[i] = kEmpty;
+    fs[i] = kEmpty;
+  }
+  __syncthreads();
+  // 1. distinct ids: insert, keep the first sample index of each
+  uint32_t hpos[kR];
+#pragma unroll
+  for (int r = 0; r < kR; ++r) {
+    hpos[r] = kEmpty;
+    const int64_t id = idv[r];
+    if (id >= 0 && id < rows_f) {
+      const uint32_t key = static_cast<uint32_t>(id);
+      uint32_t h = id_hash(key, hmask);
+      while (true) {
+        const uint32_t prev = atomicCAS(&keys[h], kEmpty, key);
+        if (prev == kEmpty || prev == key) break;
+        h = (h + 1) & hmask;
+      }
+      hpos[r] = h;
+      atomicMin(&fs[h], (static_cast<uint32_t>(r * kBT + tid) << 16) | 0xffffu);
+    }
+  }
+  __syncthreads();
+  // 2. stable per-owner ranks of the first lookups (owner W = no slot)
+  uint32_t dv[kR];
+#pragma unroll
+  for (int r = 0; r < kR; ++r) {
+    if (r >= rounds) continue;
+    uint32_t d = static_cast<uint32_t>(W);
+    const uint32_t i = static_cast<uint32_t>(r * kBT + tid);
+    if (hpos[r] != kEmpty && (fs[hpos[r]] >> 16) == i)
+      d = static_cast<uint32_t>(idv[r]) % static_cast<uint32_t>(W);
+    dv[r] = d;
+    const uint64_t m = same_value_lanes(d, nbits);
+    if ((m & lt) == 0) hist[d * G + r * kBWaves + wid] = __popcll(m);
+  }
+  __syncthreads();
+  scan_2048(hist, nh, wtot);
+#pragma unroll
+  for (int r = 0; r < kR; ++r) {
+    if (r >= rounds) continue;
+    const uint32_t d = dv[r];
+    const uint64_t m = same_value_lanes(d, nbits);
+    if (d == static_cast<uint32_t>(W)) continue;
+    uint32_t slot = hist[d * G + r * kBWaves + wid] + __popcll(m & lt) - hist[d * G];
+    if (slot >= static_cast<uint32_t>(cap)) {
+      if (overflow) *overflow = 1;
+      slot = 0xffffu;
+    } else {
+      send_ids[d * P + static_cast<int64_t>(f) * cap + slot] =
+          static_cast<int32_t>(static_cast<uint32_t>(idv[r]) / static_cast<uint32_t>(W));
+    }
+    fs[hpos[r]] = (static_cast<uint32_t>(r * kBT + tid) << 16) | slot;
+  }
+  __syncthreads();
+  // 3. every lookup: the slot of its id
+#pragma unroll
+  for (int r = 0; r < kR; ++r) {
+    const int64_t i = static_cast<int64_t>(r) * kBT + tid;
+    if (r >= rounds || i >= B) continue;
+    const int64_t id = idv[r];
+    if (hpos[r] == kEmpty) {
+      if (oob && id != -2) *oob = 1;
+      pos[f * B + i] = -1;
+      continue;
+    }
+    const uint32_t slot = fs[hpos[r]] & 0xffffu;
+    const uint32_t d = static_cast<uint32_t>(id) % static_cast<uint32_t>(W);
+    pos[f * B + i] = slot == 0xffffu ? -1 : static_cast<int32_t>((static_cast<int64_t>(d) * F + f) * cap + slot);
+  }
+  // 4. counts header and padding slots of every owner part
+  for (int d = 0; d < W; ++d) {
+    const uint32_t cnt = min(static_cast<uint32_t>(cap), hist[(d + 1) * G] - hist[d * G]);
+    int32_t *part = send_ids + d * P + static_cast<int64_t>(f) * cap;
+    for (int s = static_cast<int>(cnt) + tid; s < cap; s += kBT) part[s] = -1;
+    if (tid == 0) send_ids[d * P + static_cast<int64_t>(F) * cap + f] = static_cast<int32_t>(cnt);
+  }
+}
+
+// ---------------------------------------------------------------------------
+// wire records: round4((dim + has_w) * elem bytes) bytes per distinct row (bf16,
+// dim 16 + w: 36 B, against 64 B per slot), part p of a wire buffer holds cap_rows
+// records; table f's entries of part p start at prefix_p(f) = sum_{g<f} count_p(g)
+// (the counts of the header of `hdr`, W parts of n_tables*cap + n_tables int32).
+// One 256-thread workgroup per (part, table), one thread per record, dword copies.
+// ---------------------------------------------------------------------------
+
+struct WireArgs {
+  const int32_t *hdr;  // W parts of F*cap + F (counts at F*cap + f)
+  int W, F, cap, cap_rows;
+  int rec_dw;          // dwords per record
+  int32_t *overflow;
+};
+
+// prefix of table f in part p, and its count; flags (and clips to) cap_rows
+__device__ __forceinline__ void wire_span(const WireArgs &w, int p, int f, int *base, int *cnt) {
+  const int32_t *h = w.hdr + static_cast<int64_t>(p) * (static_cast<int64_t>(w.F) * w.cap + w.F) +
+                     static_cast<int64_t>(w.F) * w.cap;
+  int pre = 0;
+  for (int g = 0; g < f; ++g) pre += h[g];
+  int c = h[f];
+  if (pre + c > w.cap_rows) {
+    if (w.overflow && threadIdx.x == 0) *w.overflow = 1;
+    c = max(0, w.cap_rows - pre);
+  }
+  *base = p * w.cap_rows + pre;
+  *cnt = c;
+}
+
+// owner: local bank rows of part p's received ids -> wire records
+__global__ __launch_bounds__(256) void gather_wire_kernel(BankArgs bank, WireArgs w,
+                                                          const int32_t *__restrict__ recv,
+                                                          uint32_t *__restrict__ wire) {
+  const int p = blockIdx.x / w.F, f = blockIdx.x % w.F;
+  int base, cnt;
+  wire_span(w, p, f, &base, &cnt);
+  const int32_t *ids = recv + static_cast<int64_t>(p) * (static_cast<int64_t>(w.F) * w.cap + w.F) +
+                       static_cast<int64_t>(f) * w.cap;
+  for (int j = threadIdx.x; j < cnt; j += 256) {
+    const int64_t id = ids[j];
+    uint32_t *dst = wire + static_cast<int64_t>(base + j) * w.rec_dw;
+    if (id < 0 || id >= bank.rows[f]) {
+      for (int k = 0; k < w.rec_dw; ++k) dst[k] = 0u;
+      continue;
+    }
+    const uint32_t *src = reinterpret_cast<const uint32_t *>(bank.data) +
+                          (bank.row_offset[f] + id) * (bank.lpr * 4);
+    uint32_t v[18];
+#pragma unroll
+    for (int k = 0; k < 18; ++k)
+      if (k < w.rec_dw) v[k] = src[k];
+#pragma unroll
+    for (int k = 0; k < 18; ++k)
+      if (k < w.rec_dw) dst[k] = v[k];
+  }
+}
+
+// wire records <-> slot rows [(p * F + f) * cap + j] of `slots` (row pitch slot_dw
+// dwords).  unpack: the record into the slot row (dwords past the record zeroed;
+// with to_f32 the bf16 record is widened to fp32: dwords of fp32 = 2 x record
+// elements), and optionally zero `zero_dw` dwords of the same row of `zero`;
+// pack: the slot row's first rec_dw dwords into the record.
+template <bool UNPACK, bool TO_F32>
+__global__ __launch_bounds__(256) void wire_move_kernel(WireArgs w, uint32_t *__restrict__ wire,
+                                                        uint32_t *__restrict__ slots, int slot_dw,
+                                                        uint32_t *__restrict__ zero, int zero_dw) {
+  const int p = blockIdx.x / w.F, f = blockIdx.x % w.F;
+  int base, cnt;
+  wire_span(w, p, f, &base, &cnt);
+  for (int j = threadIdx.x; j < cnt; j += 256) {
+    uint32_t *rec = wire + static_cast<int64_t>(base + j) * w.rec_dw;
+    const int64_t srow = (static_cast<int64_t>(p) * w.F + f) * w.cap + j;
+    uint32_t *row = slots + srow * slot_dw;
+    if constexpr (UNPACK) {
+      uint32_t v[18];
+#pragma unroll
+      for (int k = 0; k < 18; ++k)
+        if (k < w.rec_dw) v[k] = rec[k];
+      if constexpr (TO_F32) {  // bf16 pairs -> two fp32
+#pragma unroll
+        for (int k = 0; k < 18; ++k)
+          if (k < w.rec_dw && 2 * k + 1 < slot_dw) {
+            row[2 * k] = v[k] << 16;
+            row[2 * k + 1] = v[k] & 0xffff0000u;
+          }
+        for (int k = 2 * w.rec_dw; k < slot_dw; ++k) row[k] = 0u;
+      } else {
+#pragma unroll
+        for (int k = 0; k < 18; ++k)
+          if (k < w.rec_dw) row[k] = v[k];
+        for (int k = w.rec_dw; k < slot_dw; ++k) row[k] = 0u;
+      }
+      if (zero) {
+        uint32_t *z = zero + srow * zero_dw;
+        for (int k = 0; k < zero_dw; ++k) z[k] = 0u;
+      }
+    } else {
+      uint32_t v[18];
+#pragma unroll
+      for (int k = 0; k < 18; ++k)
+        if (k < w.rec_dw) v[k] = row[k];
+#pragma unroll
+      for (int k = 0; k < 18; ++k)
+        if (k < w.rec_dw) rec[k] = v[k];
+    }
   }
 }
 
@@ -343,6 +580,131 @@ mrec_status mrec_shard_lookup_grad(int64_t batch, int32_t n_tables, int32_t dim,
   lookup_grad_kernel<<<dim3(static_cast<unsigned>((batch + 3) / 4)), 256, 0,
                        static_cast<hipStream_t>(stream)>>>(a);
   return launch_status("mrec_shard_lookup_grad");
+}
+
+
+// ---- compact exchange (ABI 19) ----------------------------------------------
+
+mrec_status mrec_shard_bucketize_dedup(const mrec_ids *ids, int32_t n_tables, const int64_t *rows,
+                                       int64_t batch, int32_t world, int32_t cap,
+                                       int32_t *send_ids, int32_t *pos, int32_t *d_overflow,
+                                       int32_t *d_oob_flag, mrec_stream stream) {
+  MREC_CHECK_ARG(n_tables >= 1 && n_tables <= MREC_MAX_TABLES, "n_tables out of range");
+  MREC_CHECK_ARG(rows != nullptr && send_ids && pos, "NULL pointer");
+  MREC_CHECK_ARG(world >= 1 && cap >= 1 && cap < 65535 && batch >= 0 && batch <= 8192,
+                 "bad world / cap / batch (batch <= 8192, cap < 65535)");
+  IdsArgs ia;
+  mrec_status st = make_ids_args(ids, n_tables, &ia);
+  if (st != MREC_OK) return st;
+  const int64_t groups = (batch + kBT - 1) / kBT * kBWaves;
+  MREC_CHECK_ARG((world + 1) * std::max<int64_t>(groups, 1) <= kBHist,
+                 "(world + 1) * ceil(batch / 64) must be <= 2048");
+  RowsArg ra;
+  for (int f = 0; f < MREC_MAX_TABLES; ++f) {
+    ra.v[f] = f < n_tables ? rows[f] : 0;
+    MREC_CHECK_ARG(ra.v[f] >= 0 && ra.v[f] < (int64_t(1) << 31), "rows per table must be < 2^31");
+  }
+  int hs = 1024;
+  while (hs < 2 * batch) hs *= 2;  // load factor <= 1/2
+  const size_t lds = static_cast<size_t>(hs) * 8;
+  static int attr = [] {
+    (void)hipFuncSetAttribute(reinterpret_cast<const void *>(bucketize_dedup_kernel),
+                              hipFuncAttributeMaxDynamicSharedMemorySize, 16384 * 8);
+    (void)hipGetLastError();
+    return 1;
+  }();
+  (void)attr;
+  bucketize_dedup_kernel<<<dim3(n_tables), kBT, lds, static_cast<hipStream_t>(stream)>>>(
+      ia, ra, batch, world, cap, n_tables, hs, send_ids, pos, d_overflow, d_oob_flag);
+  return launch_status("mrec_shard_bucketize_dedup");
+}
+
+int32_t mrec_shard_wire_bytes(int32_t dim, int32_t has_w, mrec_dtype dtype) {
+  const int es = dtype == MREC_BF16 ? 2 : 4;
+  return ((dim + (has_w ? 1 : 0)) * es + 3) / 4 * 4;
+}
+
+static mrec_status wire_args(const int32_t *hdr, int32_t world, int32_t n_tables, int32_t cap,
+                             int32_t cap_rows, int32_t rec_bytes, int32_t *d_overflow,
+                             WireArgs *w) {
+  MREC_CHECK_ARG(hdr != nullptr, "NULL header ids");
+  MREC_CHECK_ARG(world >= 1 && n_tables >= 1 && n_tables <= MREC_MAX_TABLES && cap >= 1 &&
+                     cap_rows >= 1, "bad world / tables / cap");
+  MREC_CHECK_ARG(rec_bytes % 4 == 0 && rec_bytes >= 4 && rec_bytes <= 72,
+                 "record bytes must be a multiple of 4 in [4, 72]");
+  w->hdr = hdr;
+  w->W = world;
+  w->F = n_tables;
+  w->cap = cap;
+  w->cap_rows = cap_rows;
+  w->rec_dw = rec_bytes / 4;
+  w->overflow = d_overflow;
+  return MREC_OK;
+}
+
+mrec_status mrec_shard_gather_wire(const mrec_table_bank *local, const int32_t *recv_ids,
+                                   int32_t world, int32_t cap, int32_t cap_rows, void *wire,
+                                   int32_t *d_overflow, mrec_stream stream) {
+  BankArgs ba;
+  int eb, lpr;
+  mrec_status st = make_bank_args(local, &ba, &eb, &lpr);
+  if (st != MREC_OK) return st;
+  MREC_CHECK_ARG(!ba.adam.kind, "the wire gather does not catch up lazy Adam rows: "
+                                "use mrec_shard_gather");
+  MREC_CHECK_ARG(recv_ids && wire, "NULL pointer");
+  MREC_CHECK_ARG((reinterpret_cast<uintptr_t>(wire) & 3) == 0, "wire not 4-B aligned");
+  const int rec = mrec_shard_wire_bytes(ba.dim, ba.has_w, local->dtype);
+  MREC_CHECK_ARG(rec <= ba.row_stride * eb, "record wider than the bank row");
+  WireArgs w;
+  st = wire_args(recv_ids, world, ba.n_tables, cap, cap_rows, rec, d_overflow, &w);
+  if (st != MREC_OK) return st;
+  gather_wire_kernel<<<dim3(world * ba.n_tables), 256, 0, static_cast<hipStream_t>(stream)>>>(
+      ba, w, recv_ids, static_cast<uint32_t *>(wire));
+  return launch_status("mrec_shard_gather_wire");
+}
+
+mrec_status mrec_shard_wire_unpack(const void *wire, int32_t rec_bytes, const int32_t *hdr_ids,
+                                   int32_t world, int32_t n_tables, int32_t cap, int32_t cap_rows,
+                                   void *slots, int64_t slot_bytes, int32_t to_f32, void *zero,
+                                   int64_t zero_bytes, int32_t *d_overflow, mrec_stream stream) {
+  WireArgs w;
+  mrec_status st = wire_args(hdr_ids, world, n_tables, cap, cap_rows, rec_bytes, d_overflow, &w);
+  if (st != MREC_OK) return st;
+  MREC_CHECK_ARG(wire && slots, "NULL pointer");
+  MREC_CHECK_ARG(slot_bytes % 4 == 0 && zero_bytes % 4 == 0 && zero_bytes >= 0,
+                 "row pitches must be multiples of 4 bytes");
+  MREC_CHECK_ARG(slot_bytes >= (to_f32 ? 2 : 1) * rec_bytes, "slot rows narrower than the record");
+  MREC_CHECK_ARG(!zero || zero_bytes > 0, "zero rows need their pitch");
+  const dim3 g(static_cast<unsigned>(world * n_tables));
+  hipStream_t s = static_cast<hipStream_t>(stream);
+  uint32_t *wp = static_cast<uint32_t *>(const_cast<void *>(wire));
+  if (to_f32)
+    wire_move_kernel<true, true><<<g, 256, 0, s>>>(w, wp, static_cast<uint32_t *>(slots),
+                                                   static_cast<int>(slot_bytes / 4),
+                                                   static_cast<uint32_t *>(zero),
+                                                   static_cast<int>(zero_bytes / 4));
+  else
+    wire_move_kernel<true, false><<<g, 256, 0, s>>>(w, wp, static_cast<uint32_t *>(slots),
+                                                    static_cast<int>(slot_bytes / 4),
+                                                    static_cast<uint32_t *>(zero),
+                                                    static_cast<int>(zero_bytes / 4));
+  return launch_status("mrec_shard_wire_unpack");
+}
+
+mrec_status mrec_shard_wire_pack(const void *slots, int64_t slot_bytes, int32_t rec_bytes,
+                                 const int32_t *hdr_ids, int32_t world, int32_t n_tables,
+                                 int32_t cap, int32_t cap_rows, void *wire, int32_t *d_overflow,
+                                 mrec_stream stream) {
+  WireArgs w;
+  mrec_status st = wire_args(hdr_ids, world, n_tables, cap, cap_rows, rec_bytes, d_overflow, &w);
+  if (st != MREC_OK) return st;
+  MREC_CHECK_ARG(wire && slots, "NULL pointer");
+  MREC_CHECK_ARG(slot_bytes % 4 == 0 && slot_bytes >= rec_bytes, "bad slot pitch");
+  wire_move_kernel<false, false><<<dim3(static_cast<unsigned>(world * n_tables)), 256, 0,
+                                   static_cast<hipStream_t>(stream)>>>(
+      w, static_cast<uint32_t *>(wire), static_cast<uint32_t *>(const_cast<void *>(slots)),
+      static_cast<int>(slot_bytes / 4), nullptr, 0);
+  return launch_status("mrec_shard_wire_pack");
 }
 
 }  // extern "C"

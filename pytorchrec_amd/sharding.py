@@ -2,26 +2,40 @@
 
 One process per GPU.  Table f is split cyclically: global id ``i`` lives on rank
 ``i % W`` as local row ``i // W`` (cyclic, so Zipf-hot rows spread over owners).
-The dense tower stays data-parallel.  One training step of a sharded bank:
+The dense tower stays data-parallel.  One training step of a sharded bank (the
+compact exchange, include/mrec.h ABI 19):
 
-  sender  bucketize ids by owner into fixed-capacity slots   mrec_shard_bucketize
-          all_to_all ids                                     (equal split, RCCL)
-  owner   gather the requested rows                          mrec_shard_gather
-          all_to_all rows back                               (equal split)
-  sender  interaction on the received rows                   mrec_interact_fwd
+  sender  distinct ids per (owner, table) into fixed-capacity    mrec_shard_bucketize_dedup
+          slots, every lookup's slot (pos), per-table counts
+          all_to_all ids                                         (equal split, RCCL)
+  owner   rows of the received ids -> one 36-B record per        mrec_shard_gather_wire
+          distinct row, packed per owner over all tables
+          all_to_all records back                                (equal split)
+  sender  records -> slot rows (+ zero the gradient sums)        mrec_shard_wire_unpack
+          interaction on the slot rows, with the sender's        mrec_interact_fwd_ex
+          backward plan over pos in the same launch
   ---- backward ----
-  sender  per-lookup gradient rows into the same slots       mrec_shard_lookup_grad
-          all_to_all gradients to the owners                 (equal split)
-  owner   hash plan over the received ids (padded view),     run by leading workgroups
-          of the interaction launch                          (mrec_interact_fwd_ex)
-          fixed-order segment sums + fused SGD               mrec_emb_bwd_apply_given
+  sender  gradient sum of each slot's lookups (fixed ascending   mrec_emb_bwd_apply_ex
+          order, DENSE_GRAD into the slot rows)                  (DENSE_GRAD)
+          -> one record per distinct row, table dtype            mrec_shard_wire_pack
+          all_to_all records to the owners                       (equal split)
+  owner   records -> fp32 slots; plan over the received ids;     mrec_shard_wire_unpack,
+          fixed-order sums over the senders + fused SGD          mrec_emb_bwd_apply_given
 
-Every exchange buffer is ``[W][n_tables][cap]`` slots, so all collectives are
-equal-split: no host sync, capturable in a HIP graph.  A slot overflow (more than
-``cap`` ids of one table for one owner in a rank's batch) is flagged on the
+so the bytes on xGMI per rank and direction are ~cap_rows x 36 B per peer (one
+record per distinct id; bf16, D = 16 + w) instead of n_tables x cap x 64 B rows
+and 80-B fp32 gradients.  Banks under a fused lazy Adam (whose reads must catch
+rows up) keep the slot exchange of ABI 14 (one 64-B row / fp32 gradient per
+lookup).
+
+Every exchange buffer has W equal parts, so all collectives are equal-split: no
+host sync, capturable in a HIP graph.  An overflow (more distinct ids of one table
+for one owner than ``cap``, or of all tables than ``cap_rows``) is flagged on the
 device and raised, never dropped silently.  The loss is the mean over each rank's
 batch, so the global objective is the mean of the ranks' losses: dense gradients
 are all-reduced and averaged, and owners scale the summed row gradients by 1/W.
+A row's gradient is summed per rank first (ascending sample order), then over the
+ranks in rank order -- the data-parallel reduction order.
 
 The reference has no sharding (it keeps one dense ``nn.Embedding`` per field,
 FunkSVD.py:39-41); the per-field semantics (gather, duplicate-summing backward,
@@ -176,6 +190,27 @@ def default_cap(batch: int, world: int, rows: Optional[Sequence[int]] = None,
     return max(1, min(batch, cap, _mrec.BWD_MAX_BATCH // world))
 
 
+def default_cap_rows(batch: int, world: int, rows: Sequence[int], cap: int,
+                     sigmas: float = 8.0) -> int:
+    """Records per owner part of the compact exchange (all tables together): the
+    number of one rank's lookups owned by one rank is a sum over the tables of
+    Binomial(batch, p_f), so mean + 8 sd of the SUM (rounded up to 8) -- at W = 8,
+    B = 4096, 26 large tables: 14,176 records for a mean of 13,312, where 26
+    per-table capacities of 688 would be 17,888 -- bounded by n_tables * cap."""
+    batch, world = int(batch), int(world)
+    n_tab = max(1, len(rows))
+    if world <= 1:
+        return max(1, n_tab * min(batch, cap))
+    mean = var = 0.0
+    for n in rows:
+        n = int(n)
+        p = (-(-n // world) / n) if n > 0 else 0.0
+        mean += batch * p
+        var += batch * p * (1.0 - p)
+    c = (int(math.ceil(mean + sigmas * math.sqrt(var))) + 7) // 8 * 8
+    return max(1, min(c, n_tab * cap))
+
+
 # ----------------------------------------------------------------------------
 # the sharded bank
 # ----------------------------------------------------------------------------
@@ -204,6 +239,27 @@ class ShardedEmbeddingBank(EmbeddingBank):
             raise ValueError(f"world * cap = {W * self.cap} exceeds MREC_BWD_MAX_BATCH")
         self._flags = None  # device int32 [2] = {overflow, oob}, sticky until checked
         self._global_rows_arr = (ctypes.c_int64 * len(self.global_rows))(*self.global_rows)
+        # the compact exchange (one record per distinct id, ABI 19) at world > 1
+        # ("always": at world 1 too); False: one slot row per lookup (ABI 14) -- always
+        # for a fused lazy Adam bank.  At world 1 nothing crosses xGMI and the slot
+        # path keeps the step bit-identical to the unsharded bank (the compact path
+        # rounds each rank's gradient sum of a bf16 row to bf16 on the wire).
+        self.compact = True
+        self.cap_rows = default_cap_rows(max_batch, W, self.global_rows, self.cap)
+
+    @property
+    def part(self) -> int:
+        """int32 per owner part of the compact ids message: slots, then counts."""
+        return self.n_tables * self.cap + self.n_tables
+
+    def wire_bytes(self) -> int:
+        dt = _mrec.dtype_code(self.weight.dtype)
+        return int(_mrec.lib().mrec_shard_wire_bytes(self.dim, int(self.has_w), dt))
+
+    def use_compact(self, batch: int) -> bool:
+        on = self.compact == "always" or (bool(self.compact) and self.world > 1)
+        return (on and self.update != "adam" and batch <= _mrec.BWD_MAX_BATCH
+                and self.cap < 65535)
 
     @property
     def g_ld(self) -> int:
@@ -285,7 +341,8 @@ class ShardedEmbeddingBank(EmbeddingBank):
         return torch.arange(self.rank, self.global_rows[f], self.world)
 
     def extra_repr(self) -> str:
-        return super().extra_repr() + f", world={self.world}, rank={self.rank}, cap={self.cap}"
+        return (super().extra_repr() + f", world={self.world}, rank={self.rank}, cap={self.cap}, "
+                f"cap_rows={self.cap_rows}, compact={self.compact}")
 
 
 _ACTIVE: List[tuple] = []
@@ -341,6 +398,107 @@ def shard_gather(bank: ShardedEmbeddingBank, recv_ids: torch.Tensor) -> torch.Te
     return out
 
 
+def shard_bucketize_dedup(bank: ShardedEmbeddingBank, ids: Sequence[torch.Tensor]):
+    """-> (send_ids [W, F*cap + F] int32: distinct ids per (owner, table) + counts,
+    pos [F, B] int32: the slot of every lookup)."""
+    F, W, cap = bank.n_tables, bank.world, bank.cap
+    B = ids[0].shape[0]
+    dev = bank.weight.device
+    send = torch.empty(W, bank.part, dtype=torch.int32, device=dev)
+    pos = torch.empty(F, B, dtype=torch.int32, device=dev)
+    fl = bank.flags()
+    _mrec.call("mrec_shard_bucketize_dedup", _mrec.IdsDesc(ids).ref(), F, bank._global_rows_arr,
+               B, W, cap, send.data_ptr(), pos.data_ptr(), fl.data_ptr(), fl.data_ptr() + 4,
+               _mrec.stream_handle())
+    return send, pos
+
+
+def shard_gather_wire(bank: ShardedEmbeddingBank, recv_ids: torch.Tensor) -> torch.Tensor:
+    """Owner: one record per received distinct id -> [W, cap_rows * record] bytes."""
+    W, rb = bank.world, bank.wire_bytes()
+    wire = torch.empty(W, bank.cap_rows * rb, dtype=torch.uint8, device=bank.weight.device)
+    fl = bank.flags()
+    _mrec.call("mrec_shard_gather_wire", bank.desc().ref(), recv_ids.data_ptr(), W, bank.cap,
+               bank.cap_rows, wire.data_ptr(), fl.data_ptr(), _mrec.stream_handle())
+    return wire
+
+
+def shard_wire_unpack(bank: ShardedEmbeddingBank, wire: torch.Tensor, hdr: torch.Tensor,
+                      slots: torch.Tensor, to_f32: bool = False,
+                      zero: Optional[torch.Tensor] = None):
+    """Records -> slot rows [W*F*cap, ...] (``hdr``: the ids message whose counts
+    describe ``wire``); ``zero``: the same rows of a second buffer are cleared."""
+    fl = bank.flags()
+    _mrec.call("mrec_shard_wire_unpack", wire.data_ptr(), bank.wire_bytes(), hdr.data_ptr(),
+               bank.world, bank.n_tables, bank.cap, bank.cap_rows, slots.data_ptr(),
+               slots.stride(0) * slots.element_size(), int(to_f32), _mrec.ptr(zero),
+               zero.stride(0) * zero.element_size() if zero is not None else 0, fl.data_ptr(),
+               _mrec.stream_handle())
+    return slots
+
+
+def shard_wire_pack(bank: ShardedEmbeddingBank, slots: torch.Tensor, hdr: torch.Tensor):
+    """Slot rows (the table dtype) -> records [W, cap_rows * record] bytes."""
+    W, rb = bank.world, bank.wire_bytes()
+    wire = torch.empty(W, bank.cap_rows * rb, dtype=torch.uint8, device=bank.weight.device)
+    fl = bank.flags()
+    _mrec.call("mrec_shard_wire_pack", slots.data_ptr(), slots.stride(0) * slots.element_size(),
+               rb, hdr.data_ptr(), W, bank.n_tables, bank.cap, bank.cap_rows, wire.data_ptr(),
+               fl.data_ptr(), _mrec.stream_handle())
+    return wire
+
+
+def sender_plan_job(bank: ShardedEmbeddingBank, rows_recv: torch.Tensor, pos: torch.Tensor):
+    """The sender's backward plan over its lookups' slots (the slot rows seen as a
+    bank, ids = pos) as a job for the interaction launch -> (job, (ws, bytes), keep)."""
+    F = bank.n_tables
+    B = pos.shape[1]
+    wsb = _mrec.lib().mrec_emb_bwd_workspace_size(F, B)
+    ws = torch.empty(wsb, dtype=torch.uint8, device=bank.weight.device)
+    rdesc = remote_desc(bank, rows_recv)
+    rdesc.ref()
+    idd = _mrec.IdsDesc([pos[f] for f in range(F)])
+    fl = bank.flags()
+    job = _mrec.PlanJob(ctypes.pointer(rdesc.struct), ctypes.pointer(idd.struct), B, ws.data_ptr(),
+                        wsb, fl.data_ptr() + 4, None)
+    return job, (ws, wsb), (rdesc, idd, pos, rows_recv)
+
+
+def sender_plan(bank: ShardedEmbeddingBank, rows_recv: torch.Tensor, pos: torch.Tensor):
+    """sender_plan_job as its own launch (batches above MREC_BWD_HASH_MAX_BATCH)."""
+    F = bank.n_tables
+    B = pos.shape[1]
+    wsb = _mrec.lib().mrec_emb_bwd_workspace_size(F, B)
+    ws = torch.empty(wsb, dtype=torch.uint8, device=bank.weight.device)
+    fl = bank.flags()
+    _mrec.call("mrec_emb_bwd_plan", remote_desc(bank, rows_recv).ref(),
+               _mrec.IdsDesc([pos[f] for f in range(F)]).ref(), B, ws.data_ptr(), wsb,
+               fl.data_ptr() + 4, None, _mrec.stream_handle())
+    return ws, wsb
+
+
+def sender_grad_sums(bank: ShardedEmbeddingBank, rows_recv: torch.Tensor, pos: torch.Tensor,
+                     plan, gsum: torch.Tensor, dx=None, dfm=None, fm_sum=None, x0=None, dw=None):
+    """Sender: per slot, the sum of its lookups' gradient rows (fp32, ascending
+    sample order; stored in the table dtype = the wire format) into ``gsum``
+    (slot rows, zeroed by the unpack).  The deferred MLP weight-gradient
+    reductions ride along this launch."""
+    ws, wsb = plan
+    B = pos.shape[1]
+    from pytorchrec_amd import dense as dense_ops
+    jobs = dense_ops.take_pending(4)
+    arr = (_mrec.GemmCall * len(jobs))(*[j.struct() for j in jobs]) if jobs else None
+    rdesc = remote_desc(bank, rows_recv)
+    _mrec.call("mrec_emb_bwd_apply_ex", rdesc.ref(), B, ws.data_ptr(), wsb,
+               _mrec.ptr(dx), _mrec.dtype_code(dx.dtype) if dx is not None else _mrec.F32,
+               dx.stride(0) if dx is not None else 0, _mrec.ptr(dfm), _mrec.ptr(fm_sum),
+               _mrec.ptr(x0), _mrec.dtype_code(x0.dtype) if x0 is not None else _mrec.F32,
+               x0.stride(0) if x0 is not None else 0, _mrec.ptr(dw), _mrec.BWD_DENSE_GRAD, 0.0,
+               0, None, gsum.data_ptr(), len(jobs), arr, _mrec.stream_handle())
+    del jobs
+    return gsum
+
+
 def remote_desc(bank: ShardedEmbeddingBank, rows_recv: torch.Tensor) -> _mrec.BankDesc:
     """The received rows seen as a bank: F tables over the same buffer, each table's
     'id' being the slot index (pos)."""
@@ -349,9 +507,10 @@ def remote_desc(bank: ShardedEmbeddingBank, rows_recv: torch.Tensor) -> _mrec.Ba
     return _mrec.BankDesc(rows_recv, [0] * F, [n] * F, bank.dim, bank.has_w)
 
 
-def owner_plan_job(bank: ShardedEmbeddingBank, recv_ids: torch.Tensor):
+def owner_plan_job(bank: ShardedEmbeddingBank, recv_ids: torch.Tensor, part: int = 0):
     """The owner's backward plan as a job for the interaction launch (hash layout
-    over the padded exchange view, <= MREC_BWD_MAX_BATCH entries) ->
+    over the padded exchange view, <= MREC_BWD_MAX_BATCH entries; ``part``: int32
+    per owner part of the ids message, 0 = n_tables * cap) ->
     (job, (ws, ws_bytes), keep-alive)."""
     F, W, cap = bank.n_tables, bank.world, bank.cap
     n = W * cap
@@ -359,7 +518,7 @@ def owner_plan_job(bank: ShardedEmbeddingBank, recv_ids: torch.Tensor):
     ws = torch.empty(wsb, dtype=torch.uint8, device=bank.weight.device)
     desc = bank.desc()
     desc.ref()
-    idd = _mrec.IdsDesc.exchange_view(recv_ids, F, cap)
+    idd = _mrec.IdsDesc.exchange_view(recv_ids, F, cap, part)
     fl = bank.flags()
     job = _mrec.PlanJob(ctypes.pointer(desc.struct), ctypes.pointer(idd.struct), n, ws.data_ptr(),
                         wsb, fl.data_ptr() + 4, bank.step_counter().data_ptr())
@@ -393,13 +552,14 @@ def shard_interact(bank: ShardedEmbeddingBank, rows_recv: torch.Tensor, pos: tor
     return x0, logit, fm_sum
 
 
-def owner_plan(bank: ShardedEmbeddingBank, recv_ids: torch.Tensor):
-    """Sorted-segment plan of the owner's received ids (padding skipped)."""
+def owner_plan(bank: ShardedEmbeddingBank, recv_ids: torch.Tensor, part: int = 0):
+    """Sorted-segment plan of the owner's received ids (padding skipped; ``part``
+    as in owner_plan_job)."""
     F, W, cap = bank.n_tables, bank.world, bank.cap
     n = W * cap
     wsb = _mrec.lib().mrec_emb_bwd_workspace_size(F, n)
     ws = torch.empty(wsb, dtype=torch.uint8, device=bank.weight.device)
-    desc = _mrec.IdsDesc.exchange_view(recv_ids, F, cap)
+    desc = _mrec.IdsDesc.exchange_view(recv_ids, F, cap, part)
     fl = bank.flags()
     _mrec.call("mrec_emb_bwd_plan", bank.desc().ref(), desc.ref(), n, ws.data_ptr(), wsb,
                fl.data_ptr() + 4, bank.step_counter().data_ptr(), _mrec.stream_handle())
@@ -421,7 +581,7 @@ def shard_lookup_grad(bank: ShardedEmbeddingBank, pos: torch.Tensor, batch: int,
 
 
 def owner_apply(bank: ShardedEmbeddingBank, plan, g_recv: torch.Tensor,
-                lr: Optional[float] = None):
+                lr: Optional[float] = None, grad: Optional[torch.Tensor] = None):
     """Owner: fixed-order segment sums of the received gradient rows + the fused
     update.  The rows arrive summed over the W ranks' batches; each rank's loss is
     its own batch mean, so SGD steps with lr / W and a fused optimizer sees the
@@ -429,7 +589,9 @@ def owner_apply(bank: ShardedEmbeddingBank, plan, g_recv: torch.Tensor,
     explicit ``lr`` runs plain SGD with exactly that step (kernel tests)."""
     ws, wsb = plan
     F, W, cap = bank.n_tables, bank.world, bank.cap
-    if lr is not None:
+    if grad is not None:  # the summed gradient into a dense buffer (kernel tests)
+        mode, lr = _mrec.BWD_DENSE_GRAD, 0.0
+    elif lr is not None:
         mode = (_mrec.BWD_SGD_SR if (bank.stochastic_rounding and
                                      bank.weight.dtype == torch.bfloat16) else _mrec.BWD_SGD)
     else:
@@ -443,7 +605,8 @@ def owner_apply(bank: ShardedEmbeddingBank, plan, g_recv: torch.Tensor,
     _mrec.call("mrec_emb_bwd_apply_given", bank.desc().ref(), W * cap, ws.data_ptr(), wsb,
                None, _mrec.F32, 0, None, None, None, _mrec.F32, 0, None, g_recv.data_ptr(),
                g_recv.shape[1], cap, F * cap, mode, float(lr), bank.next_seed(),
-               bank.step_counter().data_ptr(), None, len(jobs), arr, _mrec.stream_handle())
+               bank.step_counter().data_ptr(), _mrec.ptr(grad), len(jobs), arr,
+               _mrec.stream_handle())
     del jobs
 
 
@@ -452,7 +615,75 @@ def owner_apply(bank: ShardedEmbeddingBank, plan, g_recv: torch.Tensor,
 # ----------------------------------------------------------------------------
 
 
+class _CompactInteractFn(torch.autograd.Function):
+    """The compact exchange (module docstring): distinct ids out, one record per
+    distinct row back, one summed gradient per distinct row to the owners."""
+
+    @staticmethod
+    def forward(ctx, dense_w, bias, trigger, bank: ShardedEmbeddingBank, ids, dense, fm2: bool,
+                first_order: bool, x0_cols: int, x0_dtype):
+        B = ids[0].shape[0]
+        dev = bank.weight.device
+        comm = bank.comm
+        send, pos = shard_bucketize_dedup(bank, ids)
+        recv = comm.exchange(send)
+        wire = comm.exchange(shard_gather_wire(bank, recv))
+        n = bank.world * bank.n_tables * bank.cap
+        rows_recv = torch.empty(n, bank.row_stride, dtype=bank.weight.dtype, device=dev)
+        train = trigger is not None
+        gsum = torch.empty_like(rows_recv) if train else None
+        shard_wire_unpack(bank, wire, send, rows_recv, zero=gsum)
+        fuse = train and B <= _mrec.BWD_HASH_MAX_BATCH
+        job, splan, keep = (sender_plan_job(bank, rows_recv, pos) if fuse
+                            else (None, None, None))
+        x0, logit, fm_sum = shard_interact(bank, rows_recv, pos, dense, dense_w, bias, fm2,
+                                           first_order, x0_cols, x0_dtype, plan_job=job)
+        del keep
+        if train and not fuse:
+            splan = sender_plan(bank, rows_recv, pos)
+        oplan = owner_plan(bank, recv, bank.part) if train else None
+        if bank.check_ids:
+            bank.check_flags()
+        ctx.bank, ctx.B = bank, B
+        ctx.splan, ctx.oplan = splan, oplan
+        ctx.fm2, ctx.first_order = fm2, first_order
+        ctx.has_dense_w, ctx.has_bias = dense_w is not None, bias is not None
+        ctx.dense_w, ctx.bias = dense_w, bias
+        ctx.save_for_backward(x0, fm_sum, dense, pos, send, recv, rows_recv, gsum)
+        if x0 is None:
+            return logit
+        return x0, logit
+
+    @staticmethod
+    def backward(ctx, *grads):
+        if len(grads) == 2:
+            dx0, dlogit = grads
+        else:
+            dx0, dlogit = None, grads[0]
+        x0, fm_sum, dense, pos, send, recv, rows_recv, gsum = ctx.saved_tensors
+        bank = ctx.bank
+        if dlogit is not None:
+            dlogit = dlogit.contiguous().float()
+        dfm = dlogit if (ctx.fm2 and dlogit is not None) else None
+        dw = dlogit if (ctx.first_order and dlogit is not None) else None
+        if dx0 is not None:
+            dx0 = dx0.contiguous()
+        if ctx.splan is not None:
+            sender_grad_sums(bank, rows_recv, pos, ctx.splan, gsum, dx=dx0, dfm=dfm,
+                             fm_sum=fm_sum, x0=x0 if dfm is not None else None, dw=dw)
+            wire_g = bank.comm.exchange(shard_wire_pack(bank, gsum, send))
+            g_recv = torch.empty(bank.world * bank.n_tables * bank.cap, bank.g_ld,
+                                 dtype=torch.float32, device=gsum.device)
+            shard_wire_unpack(bank, wire_g, recv, g_recv, to_f32=gsum.dtype != torch.float32)
+            owner_apply(bank, ctx.oplan, g_recv)
+        g_dense_w, g_bias = _dense_first_order_grads(ctx, dlogit, dense)
+        return g_dense_w, g_bias, None, None, None, None, None, None, None, None
+
+
 class _ShardedInteractFn(torch.autograd.Function):
+    """The slot exchange of ABI 14 (one row / fp32 gradient per lookup): banks under
+    a fused lazy Adam, and ``ShardedEmbeddingBank.compact = False``."""
+
     @staticmethod
     def forward(ctx, dense_w, bias, trigger, bank: ShardedEmbeddingBank, ids, dense, fm2: bool,
                 first_order: bool, x0_cols: int, x0_dtype):
@@ -529,8 +760,45 @@ def cpu_bucketize(bank: ShardedEmbeddingBank, ids: Sequence[torch.Tensor]):
     return send, pos
 
 
+def cpu_bucketize_dedup(bank: ShardedEmbeddingBank, ids: Sequence[torch.Tensor]):
+    """CPU restatement of mrec_shard_bucketize_dedup: per (owner, table) the
+    distinct ids in the order of their first lookup, every lookup's slot, the
+    counts header -> (send [W, F*cap + F] int32, pos [F, B] int32)."""
+    F, W, cap = bank.n_tables, bank.world, bank.cap
+    B = ids[0].shape[0]
+    send = torch.full((W, bank.part), -1, dtype=torch.int32)
+    pos = torch.empty(F, B, dtype=torch.int32)
+    ar = torch.arange(B)
+    for f, t in enumerate(ids):
+        t = t.long()
+        if t.numel() and (int(t.min()) < 0 or int(t.max()) >= bank.global_rows[f]):
+            raise IndexError("index out of range in self")
+        owner = t % W
+        uniq, inv = torch.unique(t, return_inverse=True)
+        first = torch.full((uniq.numel(),), B, dtype=torch.long)
+        first.scatter_reduce_(0, inv, ar, reduce="amin")
+        rep = first[inv] == ar
+        slot_u = torch.empty(uniq.numel(), dtype=torch.long)
+        for o in range(W):
+            r = torch.nonzero(rep & (owner == o)).reshape(-1)  # ascending sample order
+            if r.numel() > cap:
+                raise RuntimeError(f"row-sharded exchange overflow: more than cap={cap} ids of "
+                                   "one table for one owner in a batch; raise cap")
+            slot_u[inv[r]] = torch.arange(r.numel())
+            send[o, f * cap:f * cap + r.numel()] = (t[r] // W).to(torch.int32)
+            send[o, F * cap + f] = r.numel()
+        pos[f] = ((owner * F + f) * cap + slot_u[inv]).to(torch.int32)
+    for o in range(W):
+        if int(send[o, F * cap:].sum()) > bank.cap_rows:
+            raise RuntimeError(f"row-sharded exchange overflow: more than cap_rows="
+                               f"{bank.cap_rows} distinct ids for one owner in a batch")
+    return send, pos
+
+
 def _cpu_owner_rows(bank: ShardedEmbeddingBank, recv: torch.Tensor) -> torch.Tensor:
     F, cap = bank.n_tables, bank.cap
+    if recv.shape[-1] == bank.part:  # the compact ids message: slots, then the counts
+        recv = recv[:, :F * cap]
     flat = recv.reshape(-1).long()
     f_of = (torch.arange(flat.numel()) // cap) % F
     offs = torch.tensor(bank.row_offset, dtype=torch.long)[f_of]
@@ -554,7 +822,10 @@ class _CpuExchangeRowsFn(torch.autograd.Function):
     def backward(ctx, g):
         bank = ctx.bank
         g_recv = bank.comm.exchange(g.contiguous())
-        flat = ctx.recv.reshape(-1).long()
+        recv = ctx.recv
+        if recv.shape[-1] == bank.part:
+            recv = recv[:, :bank.n_tables * bank.cap]
+        flat = recv.reshape(-1).long()
         idx = (ctx.offs + flat)[ctx.valid]
         cols = bank.dim + (1 if bank.has_w else 0)
         upd = g_recv[ctx.valid][:, :cols].to(bank.weight.dtype)
@@ -572,7 +843,9 @@ class _CpuExchangeRowsFn(torch.autograd.Function):
 def cpu_sharded_interact(bank: ShardedEmbeddingBank, ids, dense, dense_w, bias, use_fm2: bool,
                          first_order: bool, x0_cols: int, x0_dtype):
     from pytorchrec_amd import cpu_path
-    send, pos = cpu_bucketize(bank, ids)
+    B = ids[0].shape[0]
+    send, pos = (cpu_bucketize_dedup(bank, ids) if bank.use_compact(B)
+                 else cpu_bucketize(bank, ids))
     recv = bank.comm.exchange(send)
     trig = torch.zeros(0, requires_grad=True) if torch.is_grad_enabled() else None
     rows = _CpuExchangeRowsFn.apply(trig, bank, recv)
@@ -587,11 +860,14 @@ def sharded_interact(bank: ShardedEmbeddingBank, ids, dense, dense_w, bias, fm2:
         return cpu_sharded_interact(bank, ids, dense, dense_w, bias, fm2, first_order, x0_cols,
                                     x0_dtype)
     trigger = _trigger(bank)
-    return _ShardedInteractFn.apply(dense_w, bias, trigger, bank, ids, dense, fm2, first_order,
-                                    int(x0_cols), x0_dtype)
+    fn = _CompactInteractFn if bank.use_compact(ids[0].shape[0]) else _ShardedInteractFn
+    return fn.apply(dense_w, bias, trigger, bank, ids, dense, fm2, first_order, int(x0_cols),
+                    x0_dtype)
 
 
 __all__ = ["ShardComm", "ShardedEmbeddingBank", "sharded_tables", "make_bank", "default_cap",
-           "sharded_interact", "shard_bucketize", "shard_gather", "shard_lookup_grad",
-           "owner_plan", "owner_plan_job", "owner_apply", "remote_desc", "shard_interact",
-           "cpu_bucketize"]
+           "default_cap_rows", "sharded_interact", "shard_bucketize", "shard_gather",
+           "shard_lookup_grad", "shard_bucketize_dedup", "shard_gather_wire", "shard_wire_unpack",
+           "shard_wire_pack", "sender_plan_job", "sender_grad_sums", "owner_plan",
+           "owner_plan_job", "owner_apply", "remote_desc", "shard_interact", "cpu_bucketize",
+           "cpu_bucketize_dedup"]

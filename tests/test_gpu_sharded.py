@@ -326,3 +326,124 @@ def test_sgd_multi_matches_torch_and_weight_prep(gpu):
         if img is not None:
             wr, wt = weight_prep(w)
             assert torch.equal(img[0], wr) and torch.equal(img[1], wt)
+
+
+# ---------------------------------------------------------------------------
+# compact exchange (ABI 19): distinct ids, 36-B records, summed gradients
+# ---------------------------------------------------------------------------
+
+@pytest.mark.parametrize("W,zipf,B", [(2, False, 512), (4, True, 512), (8, False, 1024),
+                                      (3, True, 4096), (8, True, 4096), (2, False, 8192)])
+def test_compact_exchange_simulated_bit_exact(gpu, W, zipf, B):
+    """W ranks simulated in one process (all-to-alls by slicing), every stage checked:
+      * bucketize_dedup == its CPU restatement (cpu_bucketize_dedup): the distinct
+        ids per (owner, table) in first-lookup order, every lookup's slot, counts;
+      * the records unpacked at the sender hold exactly the looked-up rows (bit
+        copy) and the interaction over them == the unsharded bank's (bit-exact);
+      * the sender's per-slot gradient sums == rank r's own dense gradient of the
+        unsharded bank (same kernels: fixed ascending order, rounded once to the
+        table dtype -- the wire format);
+      * the owner's sum over the senders (DENSE_GRAD) == the fp32 sum of the ranks'
+        bf16 gradients in rank order, rounded once (bit-exact);
+      * with fused SGD the owners' rows are within 1 bf16 ulp of that sum applied.
+    Per-rank bytes on the wire are checked against the slot exchange."""
+    from pytorchrec_amd import embedding as E
+    from pytorchrec_amd import sharding as S
+    glob = _global_bank(gpu)
+    banks = []
+    for r in range(W):
+        b = S.ShardedEmbeddingBank(ROWS, D, S.ShardComm(world=W, rank=r), with_first_order=True,
+                                   dtype=torch.bfloat16, max_batch=B, device=gpu,
+                                   cap=min(B, 8192 // W) if zipf else None)
+        b.load_global_(_tables(glob))
+        b.stochastic_rounding = False
+        assert b.use_compact(B)
+        banks.append(b)
+    ids = [_ids(gpu, B, 40 + r, zipf) for r in range(W)]
+    dense = [torch.rand(B, 13, device=gpu) for _ in range(W)]
+    dense_w = torch.randn(13, device=gpu)
+    bias = torch.randn(1, device=gpu)
+    x0_cols = 112
+    F = len(ROWS)
+    sends, poss = zip(*[S.shard_bucketize_dedup(banks[r], ids[r]) for r in range(W)])
+    for r in range(W):
+        ref_send, ref_pos = S.cpu_bucketize_dedup(banks[r], [t.cpu() for t in ids[r]])
+        assert torch.equal(sends[r].cpu(), ref_send) and torch.equal(poss[r].cpu(), ref_pos), r
+    recvs = _exchange(list(sends), W)
+    wires = _exchange([S.shard_gather_wire(banks[r], recvs[r]) for r in range(W)], W)
+    n = W * F * banks[0].cap
+    rows, gsums, outs, plans, oplans = [], [], [], [], []
+    for r in range(W):
+        rr = torch.empty(n, banks[r].row_stride, dtype=torch.bfloat16, device=gpu)
+        gs = torch.empty_like(rr)
+        S.shard_wire_unpack(banks[r], wires[r], sends[r], rr, zero=gs)
+        rows.append(rr)
+        gsums.append(gs)
+        fuse = B <= 4096
+        job, sp, keep = S.sender_plan_job(banks[r], rr, poss[r]) if fuse else (None, None, None)
+        outs.append(S.shard_interact(banks[r], rr, poss[r], dense[r], dense_w, bias, True, True,
+                                     x0_cols, torch.bfloat16, plan_job=job))
+        del keep
+        plans.append(sp if fuse else S.sender_plan(banks[r], rr, poss[r]))
+        oplans.append(S.owner_plan(banks[r], recvs[r], banks[r].part))
+    for r in range(W):
+        banks[r].check_flags()
+        gw = glob.weight
+        for f in range(F):
+            p = poss[r][f].long()
+            want = gw[glob.row_offset[f] + ids[r][f].long(), :D + 1]
+            assert torch.equal(rows[r][p, :D + 1], want), (r, f)
+        with torch.no_grad():
+            x0, logit = E.interact(glob, ids[r], dense[r], dense_w, bias, True, True, x0_cols,
+                                   torch.bfloat16)
+        assert torch.equal(outs[r][0], x0) and torch.equal(outs[r][1], logit), r
+    # ---- backward
+    dx0 = [torch.randn(B, x0_cols, device=gpu).to(torch.bfloat16) for _ in range(W)]
+    dl = [torch.randn(B, device=gpu) for _ in range(W)]
+    rank_grads = []
+    for r in range(W):
+        S.sender_grad_sums(banks[r], rows[r], poss[r], plans[r], gsums[r], dx=dx0[r], dfm=dl[r],
+                           fm_sum=outs[r][2], x0=outs[r][0], dw=dl[r])
+        # reference: rank r's dense gradient of the unsharded bank (bf16, same kernels)
+        ref = E.EmbeddingBank(ROWS, D, with_first_order=True, dtype=torch.bfloat16,
+                              update="dense", device=gpu)
+        with torch.no_grad():
+            ref.weight.copy_(glob.weight)
+        gref = E._backward_into_bank(ref, ids[r], B, None, dx=dx0[r], dfm=dl[r],
+                                     fm_sum=outs[r][2], x0=outs[r][0], dw=dl[r])
+        rank_grads.append(gref)
+        for f in range(F):
+            p = poss[r][f].long()
+            want = gref[glob.row_offset[f] + ids[r][f].long(), :D + 1]
+            assert torch.equal(gsums[r][p, :D + 1], want), (r, f)
+    wire_g = _exchange([S.shard_wire_pack(banks[r], gsums[r], sends[r]) for r in range(W)], W)
+    tot = torch.zeros_like(rank_grads[0], dtype=torch.float32)
+    for g in rank_grads:  # the owners' order: source rank 0, 1, ...
+        tot += g.float()
+    for r in range(W):
+        g_recv = torch.empty(n, banks[r].g_ld, dtype=torch.float32, device=gpu)
+        S.shard_wire_unpack(banks[r], wire_g[r], recvs[r], g_recv, to_f32=True)
+        own = torch.zeros_like(banks[r].weight)
+        S.owner_apply(banks[r], oplans[r], g_recv, grad=own)
+        banks[r].check_flags()
+        for f, (o, cnt) in enumerate(zip(banks[r].row_offset, banks[r].category_nums)):
+            want = tot[glob.row_offset[f]:glob.row_offset[f] + ROWS[f]][r::W, :D + 1]
+            assert torch.equal(own[o:o + cnt, :D + 1], want.to(torch.bfloat16)), (r, f)
+        # fused SGD from the same sums: within one bf16 ulp of w - lr * sum
+        lr = 0.5
+        before = banks[r].weight.detach().clone()
+        S.owner_apply(banks[r], oplans[r], g_recv, lr)
+        for f, (o, cnt) in enumerate(zip(banks[r].row_offset, banks[r].category_nums)):
+            g = tot[glob.row_offset[f]:glob.row_offset[f] + ROWS[f]][r::W, :D + 1].double()
+            w0 = before[o:o + cnt, :D + 1].double()
+            want = w0 - lr * g
+            got = banks[r].weight[o:o + cnt, :D + 1].double()
+            ulp = torch.from_numpy(np.spacing(np.abs(want.cpu().numpy()).astype(np.float32))
+                                   .astype(np.float64)).to(gpu) * 2 ** 16  # bf16 ulp
+            assert bool(((got - want).abs() <= ulp * 1.0001 + 1e-30).all()), (r, f)
+    # bytes on the wire per rank and direction vs the slot exchange
+    rb = banks[0].wire_bytes()
+    compact = W * banks[0].cap_rows * rb
+    slot = W * F * banks[0].cap * banks[0].row_stride * 2
+    assert compact < slot
+

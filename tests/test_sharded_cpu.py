@@ -230,3 +230,46 @@ def test_shard_row_split():
     got = [ShardedEmbeddingBank(rows, 4, ShardComm(world=3, rank=r)).category_nums for r in range(3)]
     assert got == [[4, 3, 1], [3, 2, 0], [3, 2, 0]]
     assert [sum(g[f] for g in got) for f in range(3)] == rows
+
+
+def test_compact_exchange_wire_bytes_c5_w8():
+    """Sizing at the C5 shape (W = 8, B = 4096, 26 tables of 100M rows, bf16 D = 16 +
+    w): <= 4 MB per rank and direction in the compact exchange, on CPU (no device)."""
+    from pytorchrec_amd import sharding as S
+    W, B, F, R = 8, 4096, 26, 100_000_000
+    cap = S.default_cap(B, W, [R] * F)
+    cap_rows = S.default_cap_rows(B, W, [R] * F, cap)
+    rec = 36  # mrec_shard_wire_bytes(16, 1, bf16)
+    remote = (W - 1) * cap_rows * rec  # the part for this rank stays local
+    assert cap_rows * W * rec <= 4.1e6 and remote <= 4e6, (cap_rows, remote)
+
+
+def test_cpu_bucketize_dedup_layout():
+    """The compact ids message on the CPU: per (owner, table) the distinct ids in
+    first-lookup order (as local ids), -1 padding, the counts header, and every
+    lookup's pos pointing at its id's slot."""
+    from pytorchrec_amd.sharding import ShardComm, ShardedEmbeddingBank, cpu_bucketize_dedup
+    W, B = 3, 40
+    rows = [17, 5, 1000]
+    bank = ShardedEmbeddingBank(rows, 8, ShardComm(world=W, rank=0), cap=B, max_batch=B)
+    g = torch.Generator().manual_seed(0)
+    ids = [torch.randint(0, n, (B,), generator=g, dtype=torch.int32) for n in rows]
+    send, pos = cpu_bucketize_dedup(bank, ids)
+    F, cap = len(rows), bank.cap
+    for f, t in enumerate(ids):
+        for o in range(W):
+            seen = []
+            for b in range(B):
+                i = int(t[b])
+                if i % W == o and i not in seen:
+                    seen.append(i)
+            cnt = int(send[o, F * cap + f])
+            assert cnt == len(seen)
+            assert send[o, f * cap:f * cap + cnt].tolist() == [i // W for i in seen]
+            assert bool((send[o, f * cap + cnt:(f + 1) * cap] == -1).all())
+        for b in range(B):
+            i = int(t[b])
+            p = int(pos[f, b])
+            o, rest = divmod(p, F * cap)
+            assert o == i % W and rest // cap == f
+            assert int(send[o, f * cap + rest % cap]) == i // W

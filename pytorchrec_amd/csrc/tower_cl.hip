@@ -51,7 +51,6 @@ constexpr int CL_WAVES = CL_THREADS / 64;
 constexpr int CL_MAXL = 4;
 constexpr int CL_MAXT = 8;        // tiles per slice (width <= 512 -> 32 tiles / 4)
 constexpr int CL_LDX = 512;       // exchange buffer row stride (elements)
-constexpr int CL_PF = 6;          // k steps of weight fragments in flight per wave
 constexpr unsigned CL_SPIN_MAX = 1u << 22;
 
 typedef short bf16x8 __attribute__((ext_vector_type(8)));
@@ -93,10 +92,16 @@ struct ClArgs {
   int store_mode;
   int rotate;
   unsigned long long *stamps;  // diagnostics: [grid][32] wall-clock stamps (NULL: off)
+  int force_sc1;  // MREC_TOWER_CL_SC1=1: the placement-independent hand-off everywhere
+  int diag;  // timing experiments only (MREC_TOWER_CL_DIAG): 1 no polls, 2 no weight loads,
+             // 4 no peer gathers -- wrong results
   // cluster workspace
   unsigned *err;
-  unsigned *sync;  // one counter per cluster, 128 B apart
-  float *zx;       // [nclus][4][64] partial logits
+  unsigned *epoch;   // launch counter: hand-off flags are epoch * 64 + hand-offs done
+  unsigned *gticket; // workgroups finished (the last one advances the epoch)
+  unsigned *flags;   // [nclus][4] hand-off flags (one 16-B granule per cluster)
+  unsigned *xcc;     // [nclus][4] (epoch + 1) << 4 | XCD of each member
+  float *zx;         // [nclus][4][64] partial logits
   uint16_t *xb[2]; // exchange buffers [B][CL_LDX] bf16 (ping-pong by hand-off parity)
   int nclus;
   // LDS plan (bytes)
@@ -119,18 +124,47 @@ __device__ __forceinline__ int cl_rot(int s, int rot, int ksteps) {
 // hand-off
 // ---------------------------------------------------------------------------
 
-// one lane adds this workgroup's arrival after every wave drained its stores
-__device__ __forceinline__ void cl_signal(unsigned *ctr) {
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();
-  if (threadIdx.x == 0) __hip_atomic_fetch_add(ctr, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+// Hand-off state of a workgroup.  Members of a cluster that all sit on one XCD
+// ("local": checked at run time from HW_REG_XCC_ID, placement only decides speed)
+// hand off through that XCD's L2: plain stores (the lines stay in L2), plain flag
+// stores, sc1 loads (L1 bypassed, served by the shared L2).  Otherwise sc1 stores of
+// data and flags (written through to memory) and sc1 loads: the placement-independent
+// form of MI355X_MICROARCH.md's hand-off table (row 1).
+struct ClSync {
+  unsigned *flags;  // the cluster's 4 flags (16-B aligned)
+  unsigned base;    // epoch * 64
+  int c;
+  int local;
+};
+
+__device__ __forceinline__ unsigned cl_xcc_id() {
+  return static_cast<unsigned>(__builtin_amdgcn_s_getreg((3 << 11) | 20)) & 15u;  // HW_REG_XCC_ID
 }
 
-// wait until all 4 workgroups of the cluster signalled hand-off h (counter >= 4 (h+1))
-__device__ __forceinline__ void cl_wait(const ClArgs &a, unsigned *ctr, unsigned target) {
+// producer: after every wave drained its stores, one lane publishes hand-off h
+__device__ __forceinline__ void cl_signal(const ClSync &sy, unsigned h) {
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
   if (threadIdx.x == 0) {
+    const unsigned v = sy.base + h + 1;
+    if (sy.local)
+      *reinterpret_cast<volatile unsigned *>(sy.flags + sy.c) = v;
+    else
+      __hip_atomic_store(sy.flags + sy.c, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+}
+
+// consumer: one lane polls the cluster's 4 flags (one 16-B sc1 load) until every
+// member published hand-off h; the others wait at the barrier
+__device__ __forceinline__ void cl_wait(const ClArgs &a, const ClSync &sy, unsigned h) {
+  if (threadIdx.x == 0) {
+    const unsigned target = sy.base + h + 1;
+    const __amdgpu_buffer_rsrc_t rs =
+        __builtin_amdgcn_make_buffer_rsrc(sy.flags, 0, 16, 0x00020000);
     unsigned n = 0;
-    while (__hip_atomic_load(ctr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < target) {
+    while (true) {
+      const u32x4 f = __builtin_amdgcn_raw_buffer_load_b128(rs, 0, 0, kSc1);
+      if (min(min(f[0], f[1]), min(f[2], f[3])) >= target) break;
       __builtin_amdgcn_s_sleep(1);
       if (++n == CL_SPIN_MAX) {
         __hip_atomic_store(a.err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -185,7 +219,7 @@ __device__ __forceinline__ void cl_gather_peers(const ClArgs &a, const uint16_t 
 // own slice OWN (nt tiles) -> IN columns [16 t0, 16 (t0 + nt)) and, when xb, the
 // exchange buffer (sc1 stores, rows < B)
 __device__ __forceinline__ void cl_publish(const ClArgs &a, const char *own, char *in, uint16_t *xb,
-                                           int t0, int nt, int64_t row0) {
+                                           int t0, int nt, int64_t row0, int local) {
   const int nch = 2 * nt;
   const int rows = static_cast<int>(min<int64_t>(CL_ROWS, a.B - row0));
   const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
@@ -195,8 +229,12 @@ __device__ __forceinline__ void cl_publish(const ClArgs &a, const char *own, cha
     const int r = i / nch, k = i - r * nch;
     const u32x4 v = *reinterpret_cast<const u32x4 *>(own + r * a.s_own + k * 16);
     *reinterpret_cast<u32x4 *>(in + r * a.s_in + (2 * t0 + k) * 16) = v;
-    if (xb && r < rows)
-      __builtin_amdgcn_raw_buffer_store_b128(v, rs, (r * CL_LDX + (2 * t0 + k) * 8) * 2, 0, kSc1);
+    if (xb && r < rows) {
+      if (local)
+        __builtin_amdgcn_raw_buffer_store_b128(v, rs, (r * CL_LDX + (2 * t0 + k) * 8) * 2, 0, 0);
+      else
+        __builtin_amdgcn_raw_buffer_store_b128(v, rs, (r * CL_LDX + (2 * t0 + k) * 8) * 2, 0, kSc1);
+    }
   }
 }
 
@@ -281,106 +319,114 @@ __device__ __forceinline__ void cl_out(const ClArgs &a, const char *blk, int t0,
 }
 
 // ---------------------------------------------------------------------------
-// one layer: weight prefetch -> (hand-off wait + peer slices) -> MFMA k loop
+// one layer: the wave's weight fragments are issued right after the previous
+// hand-off was signalled (all k steps at once: they load while the workgroup waits
+// for its peers), then the peers' slices, then the MFMA k loop
 // ---------------------------------------------------------------------------
 
-struct ClWait {  // what to do between the weight prefetch and the k loop
-  unsigned long long *stamp;  // LDS slot stamped once the peers' slices are in (or NULL)
-  unsigned *ctr;
-  unsigned target;  // 0: nothing to wait for (layer 0: x0 is already in IN)
+constexpr int CL_KS = 16;  // k steps of a layer input (widths <= 512)
+
+struct ClWait {  // what to do before the k loop
+  unsigned long long *stamp_poll;  // LDS slots stamped after the poll / the gather (or NULL)
+  unsigned long long *stamp_in;
+  ClSync sy;
+  int hand;         // < 0: nothing to wait for (layer 0: x0 is already in IN)
   const uint16_t *xb;
   int T, t0, t1;
   int64_t row0;
 };
 
 __device__ __forceinline__ void cl_do_wait(const ClArgs &a, const ClWait &w, char *in) {
-  if (w.target == 0) return;
-  cl_wait(a, w.ctr, w.target);
-  cl_gather_peers(a, w.xb, in, w.T, w.t0, w.t1, w.row0);
+  if (w.hand < 0) return;
+  if (!(a.diag & 1)) cl_wait(a, w.sy, static_cast<unsigned>(w.hand));
+  if (w.stamp_poll && threadIdx.x == 0) *w.stamp_poll = wall_clock64();
+  if (!(a.diag & 4)) cl_gather_peers(a, w.xb, in, w.T, w.t0, w.t1, w.row0);
   __syncthreads();
-  if (w.stamp && threadIdx.x == 0) *w.stamp = wall_clock64();
+  if (w.stamp_in && threadIdx.x == 0) *w.stamp_in = wall_clock64();
 }
 
-template <int G, bool ACT>
-__device__ __forceinline__ void cl_mfma_g(const ClArgs &a, f32x4 (&acc)[4],
-                                          __amdgpu_buffer_rsrc_t rsrc, int voff, int img_bytes,
-                                          char *in, int ksteps, int rot, const ClWait &w) {
+// the wave's fragments of output tile `tile` for every k step (rot: the first step)
+__device__ __forceinline__ void cl_issue(bf16x8 (&wfr)[CL_KS], const uint16_t *img, int img_bytes,
+                                         int ksteps, int tile, int rot, bool act, int diag = 0) {
+  if (!act || (diag & 2)) return;
   const int lane = threadIdx.x & 63;
-  const int g = lane >> 4, r16 = lane & 15;
-  bf16x8 wfr[CL_PF];
-  if constexpr (ACT) {
+  const int voff = (tile * ksteps * 512 + lane * 8) * 2;
+  const __amdgpu_buffer_rsrc_t rsrc =
+      __builtin_amdgcn_make_buffer_rsrc(const_cast<uint16_t *>(img), 0, img_bytes, 0x00020000);
 #pragma unroll
-    for (int p = 0; p < CL_PF; ++p) {
-      const int so = p < ksteps ? cl_rot(p, rot, ksteps) * 1024 : img_bytes;
-      wfr[p] = __builtin_bit_cast(bf16x8, __builtin_amdgcn_raw_buffer_load_b128(rsrc, voff, so, 0));
-    }
-  }
-  cl_do_wait(a, w, in);
-  if constexpr (ACT) {
-    const char *brow = in + r16 * a.s_in + g * 16;
-    const int s16 = 16 * a.s_in;
-#pragma unroll
-    for (int s = 0; s < G * CL_PF; ++s) {
-      const int p = s % CL_PF;
-      const int kk = cl_rot(s, rot, ksteps) * 64;
-      bf16x8 b[4];
-#pragma unroll
-      for (int r = 0; r < 4; ++r) b[r] = *reinterpret_cast<const bf16x8 *>(brow + r * s16 + kk);
-#pragma unroll
-      for (int r = 0; r < 4; ++r) acc[r] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wfr[p], b[r], acc[r], 0, 0, 0);
-      const int sn = s + CL_PF;
-      if (sn < G * CL_PF) {
-        const int so = sn < ksteps ? cl_rot(sn, rot, ksteps) * 1024 : img_bytes;
-        wfr[p] = __builtin_bit_cast(bf16x8, __builtin_amdgcn_raw_buffer_load_b128(rsrc, voff, so, 0));
-      }
-      __builtin_amdgcn_sched_barrier(0);
-    }
-  }
+  for (int s = 0; s < CL_KS; ++s)
+    if (s < ksteps)
+      wfr[s] = __builtin_bit_cast(
+          bf16x8, __builtin_amdgcn_raw_buffer_load_b128(rsrc, voff, cl_rot(s, rot, ksteps) * 1024, 0));
 }
 
-// dispatch on the number of PF-step groups (ksteps <= 16)
-template <int G = 1>
-__device__ __forceinline__ void cl_mfma(const ClArgs &a, f32x4 (&acc)[4], __amdgpu_buffer_rsrc_t rsrc,
-                                        int voff, int img_bytes, char *in, int ksteps, int rot,
-                                        const ClWait &w) {
-  if constexpr (G * CL_PF >= 16) {
-    cl_mfma_g<G, true>(a, acc, rsrc, voff, img_bytes, in, ksteps, rot, w);
-  } else {
-    if (ksteps <= G * CL_PF)
-      cl_mfma_g<G, true>(a, acc, rsrc, voff, img_bytes, in, ksteps, rot, w);
-    else
-      cl_mfma<G + 1>(a, acc, rsrc, voff, img_bytes, in, ksteps, rot, w);
+__device__ __forceinline__ int cl_rot_of(const ClArgs &a, int cluster, int ksteps) {
+  return a.rotate ? cluster % ksteps : 0;
+}
+
+// The k loop of one wave's tile over all 4 row tiles: the activation fragments of
+// step s + 1 are read from LDS while step s's MFMAs run (register double buffer)
+template <int KS>
+__device__ __forceinline__ void cl_kloop(f32x4 (&acc)[4], const bf16x8 (&wfr)[CL_KS],
+                                         const char *brow, int s_in, int rot) {
+  const int s16 = 16 * s_in;
+  bf16x8 b[2][4];
+  {
+    const int kk = cl_rot(0, rot, KS) * 64;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) b[0][r] = *reinterpret_cast<const bf16x8 *>(brow + r * s16 + kk);
+  }
+#pragma unroll
+  for (int s = 0; s < KS; ++s) {
+    const int cur = s & 1;
+    if (s + 1 < KS) {
+      const int kk = cl_rot(s + 1, rot, KS) * 64;
+#pragma unroll
+      for (int r = 0; r < 4; ++r)
+        b[cur ^ 1][r] = *reinterpret_cast<const bf16x8 *>(brow + r * s16 + kk);
+    }
+    // fence: the next step's 4 LDS reads stay ahead of this step's 4 MFMAs (the
+    // scheduler otherwise sinks each read to just before its MFMA: 2 in flight)
+    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+    for (int r = 0; r < 4; ++r)
+      acc[r] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wfr[s], b[cur][r], acc[r], 0, 0, 0);
+    __builtin_amdgcn_sched_barrier(0);
   }
 }
 
 // One layer of the slice: out tile t0 + wave (if the slice has it) over all 64
-// rows.  img: fwd image (tiles over out features, ks = ceil(K/32) steps) or bwd
-// image (tiles over in features); `ksteps` = k steps of the input width.
+// rows, from the fragments in wfr (cl_issue: fwd image = tiles over out features,
+// bwd image = tiles over in features; `ksteps` = k steps of the input width).
 // Epilogue into `out` ([64][s_own], local columns): FWD relu(acc + bias) (columns
 // >= width_out -> 0); BWD acc * [mask > 0] (mask may alias out: same element, same
 // lane), columns >= width_out -> 0.
 template <bool BWD>
-__device__ __forceinline__ void cl_layer(const ClArgs &a, const uint16_t *img, int img_bytes,
-                                         int ksteps, int width_out, int t0, int nt, char *in,
-                                         char *out, const float *bias, const char *mask,
-                                         const ClWait &w, int cluster) {
+__device__ __forceinline__ void cl_layer(const ClArgs &a, const bf16x8 (&wfr)[CL_KS], int ksteps,
+                                         int width_out, int t0, int nt, char *in, char *out,
+                                         const float *bias, const char *mask, const ClWait &w,
+                                         int cluster) {
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int g = lane >> 4, r16 = lane & 15;
   const bool act = wave < nt;
   const int t = t0 + wave;
-  const int voff = (t * ksteps * 512 + lane * 8) * 2;
-  const __amdgpu_buffer_rsrc_t rsrc =
-      __builtin_amdgcn_make_buffer_rsrc(const_cast<uint16_t *>(img), 0, img_bytes, 0x00020000);
+  cl_do_wait(a, w, in);
+  if (!act) return;
   f32x4 acc[4];
 #pragma unroll
   for (int r = 0; r < 4; ++r) acc[r] = f32x4{0.f, 0.f, 0.f, 0.f};
-  const int rot = a.rotate ? cluster % ksteps : 0;
-  if (act)
-    cl_mfma(a, acc, rsrc, voff, img_bytes, in, ksteps, rot, w);
-  else
-    cl_mfma_g<1, false>(a, acc, rsrc, voff, img_bytes, in, ksteps, rot, w);
-  if (!act) return;
+  const int rot = cl_rot_of(a, cluster, ksteps);
+  const char *brow = in + r16 * a.s_in + g * 16;
+  switch (ksteps) {  // compile-time k steps: one straight-line, branch-free k loop
+#define CL_KCASE(K) \
+    case K: cl_kloop<K>(acc, wfr, brow, a.s_in, rot); break;
+    CL_KCASE(1) CL_KCASE(2) CL_KCASE(3) CL_KCASE(4) CL_KCASE(5) CL_KCASE(6) CL_KCASE(7)
+    CL_KCASE(8) CL_KCASE(9) CL_KCASE(10) CL_KCASE(11) CL_KCASE(12) CL_KCASE(13) CL_KCASE(14)
+    CL_KCASE(15) CL_KCASE(16)
+#undef CL_KCASE
+    default: break;
+  }
   const int cl0 = 16 * wave + 4 * g;  // local column of acc[r][0]
   const int c0 = 16 * t + 4 * g;      // its global column
 #pragma unroll
@@ -415,16 +461,33 @@ __device__ __forceinline__ void cl_layer(const ClArgs &a, const uint16_t *img, i
     if (a.stamps && tid == 0) s_stamp[(k)] = wall_clock64();                         \
   } while (0)
 
+// stamp slots: 0 start, 1 x0 in; fwd layer l: 2+4l poll, 3+4l peers in, 4+4l done,
+// 5+4l published (L <= 3 fits; deeper towers stamp the first three); 14 z published,
+// 15 z in, 16 dh_L published; bwd step j (layer L-1-j): 17+4j poll, 18+4j in,
+// 19+4j done, 20+4j published; 31 end
 __global__ __launch_bounds__(CL_THREADS) void tower_cl_kernel(ClArgs a) {
   extern __shared__ __attribute__((aligned(16))) char lds[];
   __shared__ unsigned long long s_stamp[32];
   const int tid = threadIdx.x;
   const int lane = tid & 63;
-  const int cluster = static_cast<int>(blockIdx.x) / CL_WG;
-  const int c = static_cast<int>(blockIdx.x) % CL_WG;
+  const int wave = tid >> 6;
+  // cluster of this workgroup: with a grid of whole multiples of 32 the 4 members
+  // are blocks b, b + 8, b + 16, b + 24 (one XCD under the observed round-robin
+  // placement: their hand-offs can stay in its L2), else 4 consecutive blocks
+  const int bid = static_cast<int>(blockIdx.x);
+  const int grid = static_cast<int>(gridDim.x);
+  int cluster, c;
+  if ((grid & 31) == 0) {
+    const int q = bid >> 3;
+    cluster = (bid & 7) * (grid >> 5) + (q >> 2);
+    c = q & 3;
+  } else {
+    cluster = bid >> 2;
+    c = bid & 3;
+  }
   const int64_t row0 = static_cast<int64_t>(cluster) * CL_ROWS;
   const int L = a.L;
-  unsigned *ctr = a.sync + cluster * 32;
+  __shared__ unsigned s_sync[2];  // epoch, local
   char *in = lds + a.off_in;
   float *f_z = reinterpret_cast<float *>(lds + a.off_f);
   float *f_dz = f_z + CL_ROWS;
@@ -434,11 +497,23 @@ __global__ __launch_bounds__(CL_THREADS) void tower_cl_kernel(ClArgs a) {
   float *p_y = p_hw + 128;
   float *p_base = p_y + CL_ROWS;
   float *p_b0 = p_base + CL_ROWS;
+  float *p_ws = p_b0 + 4;             // ns side-linear weights (c == 0)
+  float *p_xs = p_ws + 64;            // [64][ns] side-linear inputs (c == 0)
   const int H = a.width[L];
+  const int ns = c == 0 ? a.ns : 0;
   unsigned long long *stp = a.stamps ? s_stamp : nullptr;
+  auto slot = [&](int k) -> unsigned long long * { return (stp && k < 31) ? stp + k : nullptr; };
   CL_STAMP(0);
+  if (tid == 0) {  // this launch's epoch; announce this member's XCD to the cluster
+    const unsigned ep = __hip_atomic_load(a.epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    s_sync[0] = ep;
+    __hip_atomic_store(a.xcc + cluster * CL_WG + c, ((ep + 1) << 4) | cl_xcc_id(), __ATOMIC_RELAXED,
+                       __HIP_MEMORY_SCOPE_AGENT);
+  }
+  bf16x8 wfr[CL_KS];  // the next layer's weight fragments of this wave's tile
 
-  // ---- prologue: zero IN (pad columns), stage the slice's parameters, x0 -> IN --
+  // ---- prologue: x0 rows and layer 0's weights in flight together; zero IN (pad
+  // columns), stage the slice's parameters, x0 -> IN, x0's k-fragment image ----------
   {
     const int xch = tw_ceil(a.width[0], 8);
     constexpr int XQ = (CL_ROWS * 64) / CL_THREADS;  // <= 64 chunks per row (512 columns)
@@ -455,6 +530,13 @@ __global__ __launch_bounds__(CL_THREADS) void tower_cl_kernel(ClArgs a) {
                                                        : 0x40000000;
       xr[q] = __builtin_amdgcn_raw_buffer_load_b128(xrs, off, 0, 0);
     }
+    {
+      const int T = tw_ceil(a.width[1], 16);
+      const int t0 = cl_t0(T, c);
+      const int ks = tw_ceil(a.width[0], 32);
+      cl_issue(wfr, a.wf[0], a.wf_bytes[0], ks, t0 + wave, cl_rot_of(a, cluster, ks),
+               wave < cl_t0(T, c + 1) - t0, a.diag);
+    }
     float pb[CL_MAXL];
 #pragma unroll
     for (int l = 0; l < CL_MAXL; ++l) {  // own columns of each layer's output (<= 128)
@@ -465,7 +547,7 @@ __global__ __launch_bounds__(CL_THREADS) void tower_cl_kernel(ClArgs a) {
         if (col < a.width[l + 1] && tid < 16 * (cl_t0(T, c + 1) - cl_t0(T, c))) pb[l] = a.bias[l][col];
       }
     }
-    float phw = 0.f, py = 0.f, pbase = 0.f, pb0 = 0.f;
+    float phw = 0.f, py = 0.f, pbase = 0.f, pb0 = 0.f, pws = 0.f;
     {
       const int T = tw_ceil(H, 16);
       const int col = 16 * cl_t0(T, c) + tid;
@@ -476,6 +558,14 @@ __global__ __launch_bounds__(CL_THREADS) void tower_cl_kernel(ClArgs a) {
     py = (yrow && ysrc) ? ysrc[row0 + tid] : 0.f;
     pbase = (yrow && a.base) ? a.base[row0 + tid] : 0.f;
     if (tid == 0) pb0 = (a.head_b ? a.head_b[0] : 0.f) + (a.b2 ? a.b2[0] : 0.f);
+    if (tid < ns) pws = a.ws[tid];
+    float pxs[8];  // [64][ns <= 64] side inputs: 8 per thread
+#pragma unroll
+    for (int q = 0; q < 8; ++q) {
+      const int i = tid + q * CL_THREADS;
+      const int r = ns ? i / ns : 0, j = i - r * ns;
+      pxs[q] = (i < CL_ROWS * ns && row0 + r < a.B) ? a.xs[(row0 + r) * a.ld_xs + j] : 0.f;
+    }
     for (int i = tid * 16; i < CL_ROWS * a.s_in; i += CL_THREADS * 16)
       *reinterpret_cast<uint4 *>(in + i) = make_uint4(0u, 0u, 0u, 0u);
 #pragma unroll
@@ -487,6 +577,12 @@ __global__ __launch_bounds__(CL_THREADS) void tower_cl_kernel(ClArgs a) {
       p_base[tid] = pbase;
     }
     if (tid == 0) p_b0[0] = pb0;
+    if (tid < 64) p_ws[tid] = pws;
+#pragma unroll
+    for (int q = 0; q < 8; ++q) {
+      const int i = tid + q * CL_THREADS;
+      if (i < CL_ROWS * ns) p_xs[i] = pxs[q];
+    }
     __syncthreads();
 #pragma unroll
     for (int q = 0; q < XQ; ++q) {
@@ -495,37 +591,65 @@ __global__ __launch_bounds__(CL_THREADS) void tower_cl_kernel(ClArgs a) {
       if (i < CL_ROWS * xch) *reinterpret_cast<u32x4 *>(in + r * a.s_in + k * 16) = xr[q];
     }
     __syncthreads();
+    CL_STAMP(1);
+    // all 4 members on one XCD?  (their announcements are long out by now)
+    if (tid == 0) {
+      const unsigned want = (s_sync[0] + 1) << 4;
+      const __amdgpu_buffer_rsrc_t rs =
+          __builtin_amdgcn_make_buffer_rsrc(a.xcc + cluster * CL_WG, 0, 16, 0x00020000);
+      unsigned n = 0;
+      u32x4 f;
+      while (true) {
+        f = __builtin_amdgcn_raw_buffer_load_b128(rs, 0, 0, kSc1);
+        if ((f[0] >> 4) == (want >> 4) && (f[1] >> 4) == (want >> 4) && (f[2] >> 4) == (want >> 4) &&
+            (f[3] >> 4) == (want >> 4))
+          break;
+        __builtin_amdgcn_s_sleep(1);
+        if (++n == CL_SPIN_MAX) {
+          __hip_atomic_store(a.err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          break;
+        }
+      }
+      const bool same = f[0] == f[1] && f[1] == f[2] && f[2] == f[3];
+      s_sync[1] = (same && !a.force_sc1) ? 1u : 0u;
+    }
+    __syncthreads();
+    if (a.kfrag && a.x0_img && a.mode != MREC_TOWER_FORWARD) {
+      // x0's k-fragment image (this workgroup's column slice), out while layer 0 runs
+      const int T0 = tw_ceil(a.width[0], 16);
+      const int s0 = cl_t0(T0, c), s1 = cl_t0(T0, c + 1);
+      cl_store_kfrag(a, in + 32 * s0, a.s_in, s0, s1 - s0, a.width[0], a.x0_img, row0);
+    }
   }
-  CL_STAMP(1);
+
+  const ClSync sy{a.flags + cluster * CL_WG, s_sync[0] * 64u, c, static_cast<int>(s_sync[1])};
 
   // ---- forward -------------------------------------------------------------------
-  unsigned hand = 0;  // hand-offs completed (counter target of the next: 4 (hand + 1))
+  int hand = 0;  // hand-offs completed
   for (int l = 0; l < L; ++l) {
     const int w_out = a.width[l + 1];
     const int T = tw_ceil(w_out, 16);
     const int t0 = cl_t0(T, c), t1 = cl_t0(T, c + 1);
     const int Tin = tw_ceil(a.width[l], 16);
-    ClWait w{stp ? stp + 2 + 3 * l : nullptr, ctr, l == 0 ? 0u : CL_WG * hand,
+    ClWait w{slot(2 + 4 * l), slot(3 + 4 * l), sy, l == 0 ? -1 : hand - 1,
              a.xb[(hand - 1) & 1], Tin, cl_t0(Tin, c), cl_t0(Tin, c + 1), row0};
     char *own = lds + a.off_own[l];
-    cl_layer<false>(a, a.wf[l], a.wf_bytes[l], tw_ceil(a.width[l], 32), w_out, t0, t1 - t0, in,
-                    own, prm + l * 128, nullptr, w, cluster);
+    cl_layer<false>(a, wfr, tw_ceil(a.width[l], 32), w_out, t0, t1 - t0, in, own, prm + l * 128,
+                    nullptr, w, cluster);
     __syncthreads();  // OWN[l] complete, IN free
-    CL_STAMP(3 + 3 * l);
-    if (l == 0 && a.kfrag && a.x0_img && a.mode != MREC_TOWER_FORWARD) {
-      // x0's k-fragment image: this workgroup's column slice (IN still holds x0 rows
-      // until the publish below overwrites the own columns of the next input)
-      const int T0 = tw_ceil(a.width[0], 16);
-      const int s0 = cl_t0(T0, c), s1 = cl_t0(T0, c + 1);
-      cl_store_kfrag(a, in + 32 * s0, a.s_in, s0, s1 - s0, a.width[0], a.x0_img, row0);
-      __syncthreads();  // its LDS reads done before IN is overwritten
-    }
+    if (l < 3) CL_STAMP(4 + 4 * l);
     if (l + 1 < L) {
       uint16_t *xb = a.xb[hand & 1];
-      cl_publish(a, own, in, xb, t0, t1 - t0, row0);
-      cl_signal(ctr);
+      cl_publish(a, own, in, xb, t0, t1 - t0, row0, sy.local);
+      cl_signal(sy, static_cast<unsigned>(hand));
       ++hand;
-      CL_STAMP(4 + 3 * l);
+      if (l < 3) CL_STAMP(5 + 4 * l);
+      // the next layer's weights load while this workgroup waits for its peers
+      const int Tn = tw_ceil(a.width[l + 2], 16);
+      const int n0 = cl_t0(Tn, c);
+      const int ks = tw_ceil(w_out, 32);
+      cl_issue(wfr, a.wf[l + 1], a.wf_bytes[l + 1], ks, n0 + wave, cl_rot_of(a, cluster, ks),
+               wave < cl_t0(Tn, c + 1) - n0, a.diag);
       if (a.mode != MREC_TOWER_FORWARD)
         cl_out(a, own, t0, t1 - t0, w_out, a.h_out[l], a.ld_h[l], row0);
     }
@@ -546,19 +670,29 @@ __global__ __launch_bounds__(CL_THREADS) void tower_cl_kernel(ClArgs a) {
 #pragma unroll
       for (int q = 0; q < 8; ++q) dot = fmaf(hf[q], p_hw[k * 8 + q], dot);
     }
-    if (c == 0 && row0 + m < a.B)
-      for (int q = j; q < a.ns; q += 8) dot = fmaf(a.xs[(row0 + m) * a.ld_xs + q], a.ws[q], dot);
+    for (int q = j; q < ns; q += 8) dot = fmaf(p_xs[m * ns + q], p_ws[q], dot);
     dot += __shfl_xor(dot, 1);
     dot += __shfl_xor(dot, 2);
     dot += __shfl_xor(dot, 4);
-    if (j == 0)
-      __hip_atomic_store(a.zx + (static_cast<int64_t>(cluster) * CL_WG + c) * CL_ROWS + m, dot,
-                         __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (j == 0) {
+      float *zd = a.zx + (static_cast<int64_t>(cluster) * CL_WG + c) * CL_ROWS + m;
+      if (sy.local)
+        *reinterpret_cast<volatile float *>(zd) = dot;
+      else
+        __hip_atomic_store(zd, dot, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
   }
-  cl_signal(ctr);
+  cl_signal(sy, static_cast<unsigned>(hand));
   ++hand;
   CL_STAMP(14);
-  cl_wait(a, ctr, CL_WG * hand);
+  if (a.mode != MREC_TOWER_FORWARD) {  // the backward's first weights load meanwhile
+    const int T = tw_ceil(a.width[L - 1], 16);
+    const int t0 = cl_t0(T, c);
+    const int ks = tw_ceil(H, 32);
+    cl_issue(wfr, a.wb[L - 1], a.wb_bytes[L - 1], ks, t0 + wave, cl_rot_of(a, cluster, ks),
+             wave < cl_t0(T, c + 1) - t0, a.diag);
+  }
+  cl_wait(a, sy, static_cast<unsigned>(hand - 1));
   CL_STAMP(15);
   if (tid < CL_ROWS) {
     const float *zp = a.zx + static_cast<int64_t>(cluster) * CL_WG * CL_ROWS + tid;
@@ -581,50 +715,70 @@ __global__ __launch_bounds__(CL_THREADS) void tower_cl_kernel(ClArgs a) {
     f_loss[tid] = lo;
   }
   __syncthreads();
-  const int nfinal = (a.mode == MREC_TOWER_FORWARD ? L : 2 * L) + 1;  // adds per workgroup
   if (a.mode == MREC_TOWER_FORWARD) {
     if (c == 0 && tid < CL_ROWS && row0 + tid < a.B) a.z[row0 + tid] = f_z[tid];
   } else {
-    // z / dz out, loss partials + ticket (c == 0), head-parameter partials: one row
+    // head-parameter partials (registers: h_L is overwritten by dh_L below), one row
     // per 16 rows, [sum_m dz h_L (own columns) | sum dz | sum dz xs] (c == 0: the
     // last two), as the 16-row kernel and mrec_ctr_head_finish lay them out
-    if (c == 0 && tid < CL_ROWS && row0 + tid < a.B) {
-      if (a.dz) a.dz[row0 + tid] = f_dz[tid];
-      if (a.z && a.mode == MREC_TOWER_BCE) a.z[row0 + tid] = f_z[tid];
-    }
-    {
-      const int q = tid >> 7, k = tid & 127;  // 4 quarters x 128 columns
-      const int64_t prow = (row0 >> 4) + q;
-      if (prow * 16 < a.B) {
-        float *pr = a.part + prow * a.ldp;
-        if (k < hcols) {
-          float sacc = 0.f;
+    const int q = tid >> 7, k = tid & 127;  // 4 quarters x 128 columns
+    float hp = 0.f;
+    if (k < hcols) {
 #pragma unroll
-          for (int m = 0; m < 16; ++m)
-            sacc = fmaf(f_dz[16 * q + m],
-                        bf16_to_f32(*reinterpret_cast<const uint16_t *>(hL + (16 * q + m) * a.s_own + k * 2)),
-                        sacc);
-          pr[16 * h0 + k] = sacc;
-        }
+      for (int m = 0; m < 16; ++m)
+        hp = fmaf(f_dz[16 * q + m],
+                  bf16_to_f32(*reinterpret_cast<const uint16_t *>(hL + (16 * q + m) * a.s_own + k * 2)),
+                  hp);
+    }
+    float sp = 0.f;  // c == 0: sum dz (j = 0) / sum dz xs_j (j = 1..ns) of quarter q
+    const int qs = tid / (1 + ns), js = tid - qs * (1 + ns);
+    const bool side = c == 0 && qs < 4;
+    if (side) {
+      if (js == 0) {
+        for (int m = 0; m < 16; ++m) sp += f_dz[16 * qs + m];
+      } else {
+        for (int m = 0; m < 16; ++m) sp = fmaf(f_dz[16 * qs + m], p_xs[(16 * qs + m) * ns + js - 1], sp);
       }
     }
-    if (c == 0) {
-      // sum dz and the side-linear partials: 4 quarters x (1 + ns) values
-      for (int i = tid; i < 4 * (1 + a.ns); i += CL_THREADS) {
-        const int q = i / (1 + a.ns), j = i - q * (1 + a.ns);
-        const int64_t prow = (row0 >> 4) + q;
-        if (prow * 16 >= a.B) continue;
-        float sacc = 0.f;
-        if (j == 0) {
-          for (int m = 0; m < 16; ++m) sacc += f_dz[16 * q + m];
-        } else {
-          for (int m = 0; m < 16; ++m) {
-            const int64_t row = row0 + 16 * q + m;
-            const float xv = row < a.B ? a.xs[row * a.ld_xs + (j - 1)] : 0.f;
-            sacc = fmaf(f_dz[16 * q + m], xv, sacc);
-          }
+    __syncthreads();  // h_L reads done before dh_L overwrites it
+    // dh_L = dz * head_w * [h_L > 0], in place over the own h_L slice
+    {
+      char *g0 = lds + a.off_own[L - 1];
+      const int m = tid >> 3, j = tid & 7;
+      const float d = f_dz[m];
+      for (int kk = j; kk < 2 * (h1 - h0); kk += 8) {
+        const uint4 hv = *reinterpret_cast<const uint4 *>(g0 + m * a.s_own + kk * 16);
+        const uint32_t hwd[4] = {hv.x, hv.y, hv.z, hv.w};
+        float gv[8];
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          const uint32_t hb = (e & 1) ? (hwd[e >> 1] >> 16) : (hwd[e >> 1] & 0xffffu);
+          gv[e] = bf16_pos(hb) ? d * p_hw[kk * 8 + e] : 0.f;  // pad columns: h = 0
         }
-        a.part[prow * a.ldp + H + j] = sacc;
+        *reinterpret_cast<uint4 *>(g0 + m * a.s_own + kk * 16) =
+            make_uint4(pack_bf16x2(gv[0], gv[1]), pack_bf16x2(gv[2], gv[3]),
+                       pack_bf16x2(gv[4], gv[5]), pack_bf16x2(gv[6], gv[7]));
+      }
+    }
+    __syncthreads();
+    {
+      uint16_t *xb = a.xb[hand & 1];
+      cl_publish(a, lds + a.off_own[L - 1], in, xb, h0, h1 - h0, row0, sy.local);
+      cl_signal(sy, static_cast<unsigned>(hand));
+      ++hand;
+      CL_STAMP(16);
+    }
+    // the head's outputs leave behind the hand-off
+    {
+      const int64_t prow = (row0 >> 4) + q;
+      if (k < hcols && prow * 16 < a.B) a.part[prow * a.ldp + 16 * h0 + k] = hp;
+      if (side && (row0 >> 4) + qs < (a.B + 15) / 16)
+        a.part[((row0 >> 4) + qs) * a.ldp + H + js] = sp;
+    }
+    if (c == 0) {
+      if (tid < CL_ROWS && row0 + tid < a.B) {
+        if (a.dz) a.dz[row0 + tid] = f_dz[tid];
+        if (a.z && a.mode == MREC_TOWER_BCE) a.z[row0 + tid] = f_z[tid];
       }
       if (a.mode == MREC_TOWER_BCE && tid < 4) {
         const int64_t prow = (row0 >> 4) + tid;
@@ -635,35 +789,7 @@ __global__ __launch_bounds__(CL_THREADS) void tower_cl_kernel(ClArgs a) {
         }
       }
     }
-    __syncthreads();  // h_L reads (head partials) done before dh_L overwrites it
-    // dh_L = dz * head_w * [h_L > 0], in place over the own h_L slice
-    {
-      char *g0 = lds + a.off_own[L - 1];
-      const int m = tid >> 3, j = tid & 7;
-      const float d = f_dz[m];
-      for (int k = j; k < 2 * (h1 - h0); k += 8) {
-        const uint4 hv = *reinterpret_cast<const uint4 *>(g0 + m * a.s_own + k * 16);
-        const uint32_t hwd[4] = {hv.x, hv.y, hv.z, hv.w};
-        float gv[8];
-#pragma unroll
-        for (int q = 0; q < 8; ++q) {
-          const uint32_t hb = (q & 1) ? (hwd[q >> 1] >> 16) : (hwd[q >> 1] & 0xffffu);
-          gv[q] = bf16_pos(hb) ? d * p_hw[k * 8 + q] : 0.f;  // pad columns: h = 0
-        }
-        *reinterpret_cast<uint4 *>(g0 + m * a.s_own + k * 16) =
-            make_uint4(pack_bf16x2(gv[0], gv[1]), pack_bf16x2(gv[2], gv[3]),
-                       pack_bf16x2(gv[4], gv[5]), pack_bf16x2(gv[6], gv[7]));
-      }
-    }
-    __syncthreads();
-    {
-      uint16_t *xb = a.xb[hand & 1];
-      cl_publish(a, lds + a.off_own[L - 1], in, xb, h0, h1 - h0, row0);
-      cl_signal(ctr);
-      ++hand;
-      CL_STAMP(16);
-      cl_out(a, lds + a.off_own[L - 1], h0, h1 - h0, H, a.dh_out[L - 1], a.ld_dh[L - 1], row0);
-    }
+    cl_out(a, lds + a.off_own[L - 1], h0, h1 - h0, H, a.dh_out[L - 1], a.ld_dh[L - 1], row0);
 
     // ---- backward: dh_l = (dh_{l+1} W_l) * [h_l > 0] (own columns of width[l]) ----
     for (int l = L - 1; l >= 0; --l) {
@@ -671,21 +797,26 @@ __global__ __launch_bounds__(CL_THREADS) void tower_cl_kernel(ClArgs a) {
       const int T = tw_ceil(w_out, 16);
       const int t0 = cl_t0(T, c), t1 = cl_t0(T, c + 1);
       const int Tin = tw_ceil(a.width[l + 1], 16);
-      const int sb = 17 + 3 * (L - 1 - l);
-      ClWait w{stp ? stp + sb : nullptr, ctr, CL_WG * hand, a.xb[(hand - 1) & 1], Tin,
+      const int sb = 17 + 4 * (L - 1 - l);
+      ClWait w{slot(sb), slot(sb + 1), sy, hand - 1, a.xb[(hand - 1) & 1], Tin,
                cl_t0(Tin, c), cl_t0(Tin, c + 1), row0};
       // output: in place over the mask h_l (OWN[l-1]); dx0 (l == 0) into OWN[L-1]
       char *out = lds + (l > 0 ? a.off_own[l - 1] : a.off_own[L - 1]);
-      cl_layer<true>(a, a.wb[l], a.wb_bytes[l], tw_ceil(a.width[l + 1], 32), w_out, t0, t1 - t0,
-                     in, out, nullptr, l > 0 ? out : nullptr, w, cluster);
+      cl_layer<true>(a, wfr, tw_ceil(a.width[l + 1], 32), w_out, t0, t1 - t0, in, out, nullptr,
+                     l > 0 ? out : nullptr, w, cluster);
       __syncthreads();
-      CL_STAMP(sb + 1);
+      CL_STAMP(min(sb + 2, 30));
       if (l > 0) {
         uint16_t *xb = a.xb[hand & 1];
-        cl_publish(a, out, in, xb, t0, t1 - t0, row0);
-        cl_signal(ctr);
+        cl_publish(a, out, in, xb, t0, t1 - t0, row0, sy.local);
+        cl_signal(sy, static_cast<unsigned>(hand));
         ++hand;
-        CL_STAMP(sb + 2);
+        CL_STAMP(min(sb + 3, 30));
+        const int Tn = tw_ceil(a.width[l - 1], 16);
+        const int n0 = cl_t0(Tn, c);
+        const int ks = tw_ceil(w_out, 32);
+        cl_issue(wfr, a.wb[l - 1], a.wb_bytes[l - 1], ks, n0 + wave, cl_rot_of(a, cluster, ks),
+                 wave < cl_t0(Tn, c + 1) - n0, a.diag);
         cl_out(a, out, t0, t1 - t0, w_out, a.dh_out[l - 1], a.ld_dh[l - 1], row0);
       } else {
         cl_store_rows(a, out, a.s_own, t0, t1 - t0, w_out, a.dx0, a.ld_dx0, row0);
@@ -694,7 +825,7 @@ __global__ __launch_bounds__(CL_THREADS) void tower_cl_kernel(ClArgs a) {
   }
 
   // ---- teardown: the loss (last ticket holder, fixed order) and the counter reset --
-  CL_STAMP(29);
+  CL_STAMP(31);
   if (a.stamps && tid < 32) a.stamps[blockIdx.x * 32 + tid] = s_stamp[tid];
   __shared__ unsigned s_last;
   if (tid == 0) {
@@ -705,11 +836,15 @@ __global__ __launch_bounds__(CL_THREADS) void tower_cl_kernel(ClArgs a) {
                                                   __HIP_MEMORY_SCOPE_AGENT);
       s_last = old == static_cast<unsigned>(a.nclus) - 1 ? 1u : 0u;
     }
-    // every workgroup's last add; the last of the cluster's 4 resets its counter
+    // the last workgroup of the launch advances the epoch (the next launch's flags)
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    const unsigned old = __hip_atomic_fetch_add(ctr, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    if (old == static_cast<unsigned>(CL_WG * nfinal) - 1)
-      __hip_atomic_store(ctr, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const unsigned old = __hip_atomic_fetch_add(a.gticket, 1u, __ATOMIC_RELAXED,
+                                                __HIP_MEMORY_SCOPE_AGENT);
+    if (old == static_cast<unsigned>(grid) - 1) {
+      __hip_atomic_store(a.gticket, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_store(a.epoch, (s_sync[0] + 1) & 0x3ffffffu, __ATOMIC_RELAXED,
+                         __HIP_MEMORY_SCOPE_AGENT);
+    }
   }
   __syncthreads();
   if (!s_last) return;
@@ -739,18 +874,19 @@ unsigned long long *tower_debug_stamps();  // tower.hip (mrec_tower_debug_stamps
 
 int64_t cl_nclus(int64_t B) { return (B + CL_ROWS - 1) / CL_ROWS; }
 
-// workspace layout: [err | pad 128 B][counters nclus x 128 B][zx nclus x 4 x 64 f32]
-// [xb0 B x 512 bf16][xb1], every part 256-B aligned
+// workspace layout: [err, epoch, gticket | pad to 256 B][flags nclus x 16 B]
+// [xcc nclus x 16 B][zx nclus x 4 x 64 f32][xb0 B x 512 bf16][xb1], parts 256-B aligned
 struct ClWs {
-  int64_t off_sync, off_zx, off_xb0, off_xb1, bytes;
+  int64_t off_flags, off_xcc, off_zx, off_xb0, off_xb1, bytes;
 };
 
 ClWs cl_ws_layout(int64_t B) {
   auto al = [](int64_t x) { return (x + 255) / 256 * 256; };
   ClWs w{};
   const int64_t n = cl_nclus(B);
-  w.off_sync = 256;
-  w.off_zx = al(w.off_sync + n * 128);
+  w.off_flags = 256;
+  w.off_xcc = al(w.off_flags + n * 16);
+  w.off_zx = al(w.off_xcc + n * 16);
   w.off_xb0 = al(w.off_zx + n * CL_WG * CL_ROWS * 4);
   w.off_xb1 = al(w.off_xb0 + B * CL_LDX * 2);
   w.bytes = al(w.off_xb1 + B * CL_LDX * 2);
@@ -850,13 +986,26 @@ bool tower_cluster_launch(const mrec_tower_args &s, hipStream_t st, mrec_status 
   }();
   a.rotate = rot_env;
   a.stamps = tower_debug_stamps();
+  static const int diag_env = [] {
+    const char *e = getenv("MREC_TOWER_CL_DIAG");
+    return e ? atoi(e) : 0;
+  }();
+  a.diag = diag_env;
+  static const int sc1_env = [] {
+    const char *e = getenv("MREC_TOWER_CL_SC1");
+    return (e && e[0] == '1') ? 1 : 0;
+  }();
+  a.force_sc1 = sc1_env;
   if (a.mode == MREC_TOWER_FORWARD) {
     a.x0_img = nullptr;
     for (int l = 0; l < L; ++l) a.h_out[l] = nullptr;
   }
   char *base = static_cast<char *>(s.cl_ws);
   a.err = reinterpret_cast<unsigned *>(base);
-  a.sync = reinterpret_cast<unsigned *>(base + ws.off_sync);
+  a.epoch = reinterpret_cast<unsigned *>(base) + 1;
+  a.gticket = reinterpret_cast<unsigned *>(base) + 2;
+  a.flags = reinterpret_cast<unsigned *>(base + ws.off_flags);
+  a.xcc = reinterpret_cast<unsigned *>(base + ws.off_xcc);
   a.zx = reinterpret_cast<float *>(base + ws.off_zx);
   a.xb[0] = reinterpret_cast<uint16_t *>(base + ws.off_xb0);
   a.xb[1] = reinterpret_cast<uint16_t *>(base + ws.off_xb1);
@@ -875,7 +1024,7 @@ bool tower_cluster_launch(const mrec_tower_args &s, hipStream_t st, mrec_status 
   a.off_f = off;
   off += 3 * CL_ROWS * 4;
   a.off_p = off;
-  off += (CL_MAXL * 128 + 128 + 2 * CL_ROWS + 4) * 4;
+  off += (CL_MAXL * 128 + 128 + 2 * CL_ROWS + 4 + 64 + CL_ROWS * std::max(0, s.ns)) * 4;
   a.lds_bytes = (off + 15) / 16 * 16;
   constexpr int kMaxDyn = 160 * 1024 - 256;
   if (a.lds_bytes > kMaxDyn) return false;

@@ -122,14 +122,16 @@ torch.cuda.synchronize()
 t = st.cpu().double() * 10.0 / 1e3  # 100 MHz ticks -> us
 t0 = t[:, 0].min()
 if cluster:
-    names = {0: "start", 1: "x0 loaded"}
-    for l in range(L):
-        names.update({2 + 3 * l: f"fwd{l} peers in", 3 + 3 * l: f"fwd{l} done",
-                      4 + 3 * l: f"fwd{l} published"})
-    names.update({14: "z published", 15: "z peers in", 16: "dh_L published", 29: "end"})
+    names = {0: "start", 1: "x0 in"}
+    for l in range(min(L, 3)):
+        names.update({2 + 4 * l: f"fwd{l} poll", 3 + 4 * l: f"fwd{l} peers in",
+                      4 + 4 * l: f"fwd{l} done", 5 + 4 * l: f"fwd{l} published"})
+    names.update({14: "z published", 15: "z peers in", 16: "dh_L published", 31: "end"})
     for j, l in enumerate(range(L - 1, -1, -1)):
-        sb = 17 + 3 * j
-        names.update({sb: f"bwd{l} peers in", sb + 1: f"bwd{l} done", sb + 2: f"bwd{l} published"})
+        sb = 17 + 4 * j
+        names.update({sb: f"bwd{l} poll", sb + 1: f"bwd{l} peers in", sb + 2: f"bwd{l} done",
+                      sb + 3: f"bwd{l} published"})
+    names = {k: v for k, v in names.items() if k < 32}
     order = sorted(names)
 else:
     names = {0: "start", 1: "x0 loaded", 2: "fwd1", 3: "fwd2", 4: "fwd3", 5: "head dot",

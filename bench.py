@@ -67,6 +67,11 @@ def parse():
                         "(uniform ids), min(batch, 8192 / W) with --zipf")
     p.add_argument("--force-collectives", action="store_true",
                    help="issue the all-to-alls / all-reduce even at N=1 (RCCL capture check)")
+    p.add_argument("--table-dtype", default="bf16", choices=["bf16", "fp32"],
+                   help="embedding tables (DeepFM / DCN-v2); the tower computes in bf16 either way")
+    p.add_argument("--exchange", default="auto", choices=["auto", "compact", "slot"],
+                   help="row-sharded exchange: auto = compact at N>1, slot at N=1; compact = "
+                        "one record per distinct id even at N=1; slot = one row per lookup")
     p.add_argument("--stub-step", action="store_true",
                    help="launcher check without a GPU: each rank's step is one gloo all-reduce")
     args = p.parse_args()
@@ -134,6 +139,10 @@ def launch(args) -> int:
 # workload
 # ----------------------------------------------------------------------------
 
+def _table_dtype(args):
+    return torch.float32 if getattr(args, "table_dtype", "bf16") == "fp32" else torch.bfloat16
+
+
 def build_deepfm(args, device, comm=None):
     """C2 DeepFM; with ``comm`` the tables are row-sharded over its ranks (each rank
     allocates only its shard) and the dense tower is data-parallel."""
@@ -152,9 +161,12 @@ def build_deepfm(args, device, comm=None):
            else contextlib.nullcontext())
     with ctx:
         model = DeepFM(sparse, dense, label, emb_size=16, layers=(400, 400, 400), dropout=0.0,
-                       emb_dtype=torch.bfloat16, device=device, random_seed=2020)
+                       emb_dtype=_table_dtype(args), device=device, random_seed=2020)
     if comm is not None:
         model.distribute(comm)
+        ex = getattr(args, "exchange", "auto")
+        for b in model.embedding_banks():
+            b.compact = {"auto": True, "compact": "always", "slot": False}[ex]
     return model, sparse, dense, label
 
 
@@ -170,7 +182,7 @@ def build_dcnv2(args, device, comm=None):
     dense = [NumericColumn(f"c_n_I{j + 1}") for j in range(CRITEO_DENSE)]
     label = CategoricalColumnWithIdentity(2, "label")
     model = DCNv2(sparse, dense, label, emb_size=16, cross_layers=3, layers=(400, 400),
-                  emb_dtype=torch.bfloat16, device=device, random_seed=2020)
+                  emb_dtype=_table_dtype(args), device=device, random_seed=2020)
     return model, sparse, dense, label
 
 
@@ -273,12 +285,13 @@ def time_launches(fn, reps=100):
     return e0.elapsed_time(e1) / reps * 1e-3  # seconds per launch
 
 
-def alg_bytes_per_sample(F, D, n_dense, first_order):
-    """SURVEY.md §8(d) algorithmic bytes per sample, bf16 weights, int32 ids:
-    fwd = ids F*4 + useful row bytes F*(D+w)*2 + dense n_dense*4 + label 4;
-    bwd = ids F*4 + row-sparse read-modify-write 2*F*(D+w)*2.
+def alg_bytes_per_sample(F, D, n_dense, first_order, es=2):
+    """SURVEY.md §8(d) algorithmic bytes per sample, bf16 weights (es = 2; fp32
+    tables es = 4), int32 ids:
+    fwd = ids F*4 + useful row bytes F*(D+w)*es + dense n_dense*4 + label 4;
+    bwd = ids F*4 + row-sparse read-modify-write 2*F*(D+w)*es.
     C2 DeepFM: 1,044 + 1,872 = 2,916; C3 DCN-v2 (no w): 992 + 1,768 = 2,760."""
-    row = (D + (1 if first_order else 0)) * 2
+    row = (D + (1 if first_order else 0)) * es
     return F * 4 + F * row + n_dense * 4 + 4, F * 4 + 2 * F * row
 
 
@@ -299,7 +312,7 @@ def kernel_rooflines(model, data, args):
         # full C5 bank would not fit beside the shard)
         world = max(1, int(os.environ.get("WORLD_SIZE", "1")))
         bank = E.EmbeddingBank([max(1, args.rows_per_table // world)] * CRITEO_FIELDS, 16,
-                               with_first_order=first_order, dtype=torch.bfloat16, device=dev)
+                               with_first_order=first_order, dtype=_table_dtype(args), device=dev)
         E.init_bank_(bank, generator=torch.Generator(device=dev).manual_seed(5))
         bank.use_fused_sgd(args.lr)
         bank.check_ids = False
@@ -309,7 +322,8 @@ def kernel_rooflines(model, data, args):
     B, F, D = args.batch, bank.n_tables, bank.dim
     ids = model._ids(data)
     dense = model._dense(data)
-    alg_fwd, alg_bwd = alg_bytes_per_sample(F, D, CRITEO_DENSE, first_order)
+    es = bank.weight.element_size()
+    alg_fwd, alg_bwd = alg_bytes_per_sample(F, D, CRITEO_DENSE, first_order, es)
     w = 1 if first_order else 0
     out = {}
     with torch.no_grad():
@@ -322,7 +336,7 @@ def kernel_rooflines(model, data, args):
         # as implemented, bytes/sample: ids F*4 + useful row bytes F*(D+w)*2 + dense
         # 13*4 + x0 write x0_cols*2 + logit 4 + fm_sum D*4; plan: ids F*4 again + per
         # lookup one 12-B workspace entry (row table / descriptor / permutation)
-        impl_fwd = (F * 4 + F * (D + w) * 2 + CRITEO_DENSE * 4 + model.x0_cols * 2 + 4
+        impl_fwd = (F * 4 + F * (D + w) * es + CRITEO_DENSE * 4 + model.x0_cols * 2 + 4
                     + (D * 4 if fm else 0) + F * 4 + F * 12)
         t = time_launches(fwd)
         out["mrec_interact_fwd_ex"] = (t, alg_fwd * B, impl_fwd * B)
@@ -342,7 +356,7 @@ def kernel_rooflines(model, data, args):
         t = time_launches(apply)
         # as implemented, per lookup: perm/row table 4 + dx D*2 (+ v re-read D*2 for
         # the FM term) + row read+write 2*(D+w)*2; per sample: fm_sum D*4 + dlogit 4
-        impl_bwd = (F * (4 + D * 2 + (D * 2 if fm else 0) + 2 * (D + w) * 2)
+        impl_bwd = (F * (4 + D * 2 + (D * 2 if fm else 0) + 2 * (D + w) * es)
                     + ((D * 4 + 4) if fm else 0))
         out["mrec_emb_bwd_apply"] = (t, alg_bwd * B, impl_bwd * B)
     return out
@@ -466,7 +480,8 @@ def end_to_end(args, per_gpu_samples_s):
         fwd = DIN_L * 2 * (128 * 80 + 80 * 40 + 40) + 2 * (64 * 200 + 200 * 80 + 80)
     else:
         fo = args.model == "deepfm"
-        f, b = alg_bytes_per_sample(CRITEO_FIELDS, 16, CRITEO_DENSE, fo)
+        f, b = alg_bytes_per_sample(CRITEO_FIELDS, 16, CRITEO_DENSE, fo,
+                                    4 if getattr(args, "table_dtype", "bf16") == "fp32" else 2)
         nbytes = f + b
         d0 = CRITEO_FIELDS * 16 + CRITEO_DENSE
         if fo:
@@ -795,11 +810,13 @@ def main():
         "higher_is_better": True,
         "scaling": "weak",
         "vs_baseline": None,
-        "dtype": "bf16",
+        "dtype": "bf16" if args.table_dtype == "bf16" or args.model == "din" else
+                 "bf16 tower, fp32 tables",
         "data": data_desc,
         "config": {"workload": workloads[args.model],
                    "global_batch": args.batch * world, "batch_per_gpu": args.batch,
                    "parallelism": (f"dp{world}+rowshard{world}" if sharded else "single"),
+                   "exchange": (_exchange_desc(model, args) if sharded else None),
                    "hip_graph": not args.no_graph,
                    "steps_per_graph": G if graphs is not None else 0},
     }
@@ -872,6 +889,23 @@ def main():
               flush=True)
     if torch.distributed.is_initialized():
         torch.distributed.destroy_process_group()
+
+
+def _exchange_desc(model, args):
+    """The row-sharded exchange the bank ran and its bytes per rank and direction
+    (rows forward / gradients backward; ids are 4 B per slot)."""
+    b = model.embeddings
+    compact = b.use_compact(args.batch)
+    W = b.world
+    if compact:
+        per = b.cap_rows * b.wire_bytes()
+        return {"kind": "compact (one record per distinct id)", "cap": b.cap,
+                "cap_rows": b.cap_rows, "record_bytes": b.wire_bytes(),
+                "bytes_per_rank_each_way": W * per, "remote_bytes_each_way": (W - 1) * per}
+    rows = W * b.n_tables * b.cap
+    return {"kind": "slot (one row per lookup)", "cap": b.cap,
+            "bytes_rows_fwd": rows * b.row_stride * b.weight.element_size(),
+            "bytes_grads_bwd": rows * b.g_ld * 4}
 
 
 def release_graphs() -> int:

@@ -32,7 +32,7 @@
 extern "C" {
 #endif
 
-#define MREC_ABI_VERSION 19
+#define MREC_ABI_VERSION 20
 #define MREC_MAX_TABLES 64      /* tables per table bank / per call */
 #define MREC_BWD_MAX_BATCH 8192  /* lookups per table per plan/apply call */
 #define MREC_BWD_HASH_MAX_BATCH 4096  /* batches up to this use the hash plan */
@@ -295,6 +295,26 @@ mrec_status mrec_emb_bwd_large_apply(const mrec_table_bank *bank, int64_t batch,
                                      int64_t x0_ld, const float *dw, mrec_bwd_mode mode, float lr,
                                      uint64_t seed, const uint64_t *d_step, void *grad,
                                      mrec_stream stream);
+/*
+ * mrec_emb_bwd_large_plan + mrec_emb_bwd_large_apply in one call (ABI 20).  For
+ * batches of <= 2M lookups over banks whose rows hash into at most 512 per bucket
+ * (NB = batch * n_tables / 256 buckets, a power of two <= 8192), the BUCKETED plan
+ * runs: lookups are partitioned by a multiplicative hash of their row (bucket
+ * histograms per 8192-lookup chunk, per-bucket prefix, scatter: no per-row global
+ * atomics), then one workgroup per bucket groups its rows in LDS and updates them
+ * in place — rows hit <= 16 times summed in ascending sample order by one worker,
+ * 17..2048 times in 64-bit fixed point by a wave (the same arithmetic, hence the
+ * same bits, as the two-call path), and longer segments through the chunked
+ * fixed-point kernels.  Otherwise (or with MREC_LG_ATOMIC_PLAN set) it is the
+ * two calls.  Same arguments as the two calls; same workspace.
+ */
+mrec_status mrec_emb_bwd_large_fused(const mrec_table_bank *bank, const mrec_ids *ids,
+                                     int64_t batch, void *workspace, size_t ws_bytes,
+                                     int32_t *d_oob_flag, const void *dx, mrec_dtype dx_dtype,
+                                     int64_t dx_ld, const float *dfm, const float *fm_sum,
+                                     const void *x0, mrec_dtype x0_dtype, int64_t x0_ld,
+                                     const float *dw, mrec_bwd_mode mode, float lr, uint64_t seed,
+                                     const uint64_t *d_step, void *grad, mrec_stream stream);
 
 struct mrec_gemm_call_s; /* mrec_gemm_call, defined with the GEMM entry points below */
 

@@ -9,6 +9,11 @@
 //       blocksum -> scan (segment starts, ascending unique-row list, long-segment
 //       work list) -> place (lookup indices into their row's segment; the order
 //       inside a segment follows the atomics, so it is NOT used for arithmetic).
+//       Batches of <= 4M lookups take the BUCKETED plan instead (4 launches, a
+//       handful of global atomics per workgroup): lookups are partitioned into NB
+//       buckets by a hash of their row (so hot rows and small tables spread over
+//       all buckets), then one workgroup per bucket groups its rows in an LDS hash
+//       table and emits the same segment lists (see bk_hist_kernel).
 // apply (3 launches): a segment of <= 16 lookups is sorted by a register network
 //       and summed in ascending sample order (identical arithmetic to the batched
 //       path).  A longer (hot) segment is split into chunks summed in parallel in
@@ -18,6 +23,7 @@
 //       result does not depend on the order, and it is exact up to the one
 //       rounding of each term to 2^-S (relative 2^-45 of the largest term).
 #include <algorithm>
+#include <cstdlib>
 
 #include "common.h"
 #include "emb_apply.h"
@@ -27,6 +33,7 @@ namespace mrec {
 constexpr int kLgRowsPerBlock = 4096;  // scan block: 256 threads x 16 rows
 constexpr int kLgChunk = 2048;         // lookups per long-segment work item
 constexpr int kLgShort = 16;           // segments up to this: register sort
+constexpr int kLgHuge = kLgChunk;      // longer: chunked fixed-point kernels (else one wave)
 constexpr int64_t kLgMaxRows = int64_t(1) << 24;
 constexpr int kLgApplyBlocks = 2048;   // grid-stride launches (device-side counts)
 
@@ -45,27 +52,88 @@ struct LgWs {
   int2 *chunks;     // [C] (L, chunk)
   uint32_t *segmax; // [U] max |g| bits of long segment L (zero on entry, left zero)
   long long *acc;   // [U * stride] fixed-point sums (zero on entry, left zero)
+  int32_t *bhist;   // bucketed plan: [G][NB] lookups per (chunk, bucket), then their offsets
+  int32_t *bstart;  // bucketed plan: [NB + 1] first entry of every bucket
+  int2 *ent;        // bucketed plan: [N] (row, b) grouped by bucket
 };
 
+// bucketed plan geometry: NB buckets (a power of two, ~256 lookups each), G chunks
+// of kBkChunk lookups, one 1024-thread workgroup each
+constexpr int kBkThreads = 1024;
+#ifndef MREC_BK_PER
+#define MREC_BK_PER 4
+#endif
+constexpr int kBkPer = MREC_BK_PER;  // lookups per thread of the chunk kernels
+constexpr int64_t kBkChunk = kBkThreads * kBkPer;
+constexpr int kBkMaxNB = 8192;
+constexpr int64_t kBkMaxN = int64_t(kBkMaxNB) * 256;  // <= 2M lookups
+constexpr int kBkSlotBits = 11;
+constexpr int kBkSlots = 1 << kBkSlotBits;  // LDS hash slots per bucket workgroup
+
+#ifndef MREC_BK_PER_BUCKET
+#define MREC_BK_PER_BUCKET 1024
+#endif
+constexpr int kBkPerBucket = MREC_BK_PER_BUCKET;  // lookups per bucket (power of two)
+
+__host__ __device__ inline int bk_buckets(int64_t N) {
+  int nb = 64;
+  while (nb < kBkMaxNB && int64_t(nb) * kBkPerBucket < N) nb *= 2;
+  return nb;
+}
+// chunks of the bucketed plan, 0 = the atomic plan.  The row hash spreads the R
+// consecutive global rows evenly over the buckets (Fibonacci hashing), so with R
+// <= NB * kBkSlots / 2 no bucket's LDS hash can fill up.
+__host__ __device__ inline int bk_groups(int64_t R, int64_t N) {
+  if (N <= 0 || N > kBkMaxN || R > int64_t(bk_buckets(N)) * (kBkSlots / 2)) return 0;
+  return static_cast<int>((N + kBkChunk - 1) / kBkChunk);
+}
+
 __host__ __device__ inline int64_t lg_align(int64_t x) { return (x + 255) & ~int64_t(255); }
+
+// list capacities: U unique rows (the atomic plan: min(R, N) compact; the bucketed
+// plan: N, bucket k's rows at its entry range), UL long-segment slots (bucketed:
+// ceil(lo_k / 2049) + j for bucket k, disjoint because a long segment has > 2048
+// lookups), C chunk slots (bucketed: ceil(lo_k / 2049) + ceil(lo_k / 2048) + j)
+struct LgCaps {
+  int64_t U, UL, C;
+};
+__host__ __device__ inline LgCaps lg_caps(int64_t R, int64_t N) {
+  const int64_t u = R < N ? R : N;
+  LgCaps c{u, u, N / kLgChunk + u + 1};
+  if (bk_groups(R, N) > 0) {
+    const int64_t ul = (N + kLgHuge) / (kLgHuge + 1) + 1;
+    const int64_t cc = ul + (N + kLgChunk - 1) / kLgChunk + 2;
+    c.U = N;
+    c.UL = ul > c.UL ? ul : c.UL;
+    c.C = cc > c.C ? cc : c.C;
+  }
+  return c;
+}
 
 __host__ __device__ inline int64_t lg_ws_bytes(int64_t R, int64_t N, int stride, LgWs *w,
                                                char *base) {
   const int64_t nblk = (R + kLgRowsPerBlock - 1) / kLgRowsPerBlock;
-  const int64_t U = R < N ? R : N;
-  const int64_t C = N / kLgChunk + U + 1;
+  const LgCaps cp = lg_caps(R, N);
+  const int64_t U = cp.U, UL = cp.UL, C = cp.C;
   int64_t o = 0;
   auto take = [&](int64_t bytes) {
     const int64_t at = o;
     o = lg_align(o + bytes);
     return at;
   };
-  const int64_t o_hdr = take(32), o_segmax = take(4 * U), o_acc = take(8 * U * stride);
+  const int64_t o_hdr = take(32), o_segmax = take(4 * UL), o_acc = take(8 * UL * stride);
   const int64_t o_cnt = take(4 * R), o_start = take(4 * R), o_blk = take(8 * nblk);
   const int64_t o_uniq = take(4 * U), o_ustart = take(4 * U), o_ulen = take(4 * U);
-  const int64_t o_ulong = take(4 * U), o_perm = take(4 * N), o_longs = take(4 * U);
+  const int64_t o_ulong = take(4 * U), o_perm = take(4 * N), o_longs = take(4 * UL);
   const int64_t o_chunks = take(8 * C);
+  const int G = bk_groups(R, N), NB = bk_buckets(N);
+  const int64_t o_bhist = take(G ? 4 * (int64_t(G + 1) * NB + 1) : 0);
+  const int64_t o_bstart = take(G ? 4 * (NB + 1) : 0);
+  const int64_t o_ent = take(G ? 8 * N : 0);
   if (w) {
+    w->bhist = G ? reinterpret_cast<int32_t *>(base + o_bhist) : nullptr;
+    w->bstart = G ? reinterpret_cast<int32_t *>(base + o_bstart) : nullptr;
+    w->ent = G ? reinterpret_cast<int2 *>(base + o_ent) : nullptr;
     w->hdr = reinterpret_cast<int32_t *>(base + o_hdr);
     w->segmax = reinterpret_cast<uint32_t *>(base + o_segmax);
     w->acc = reinterpret_cast<long long *>(base + o_acc);
@@ -85,8 +153,8 @@ __host__ __device__ inline int64_t lg_ws_bytes(int64_t R, int64_t N, int stride,
 
 // bytes that must be zero before the first call (every apply leaves them zero)
 __host__ inline int64_t lg_zero_bytes(int64_t R, int64_t N, int stride) {
-  const int64_t U = R < N ? R : N;
-  return lg_align(32) + lg_align(4 * U) + lg_align(8 * U * stride);
+  const int64_t UL = lg_caps(R, N).UL;
+  return lg_align(32) + lg_align(4 * UL) + lg_align(8 * UL * stride);
 }
 
 __device__ __forceinline__ int table_of_row(const BankArgs &bank, int64_t grow) {
@@ -124,8 +192,10 @@ __device__ __forceinline__ int32_t lookup_row(const BankArgs &bank, const IdsArg
                                               int64_t i, int64_t total, int64_t *b_out,
                                               int32_t *__restrict__ oob) {
   if (i >= total) return -1;
-  const int f = static_cast<int>(i / n);
-  const int64_t b = i - f * n;
+  // (total = batch * n_tables < 2^31, checked by lg_setup: 32-bit division)
+  const uint32_t ui = static_cast<uint32_t>(i), un = static_cast<uint32_t>(n);
+  const int f = static_cast<int>(ui / un);
+  const int64_t b = static_cast<int64_t>(ui - static_cast<uint32_t>(f) * un);
   *b_out = b;
   const int64_t id = load_id(ids, f, b);
   if (id >= 0 && id < bank.rows[f]) return static_cast<int32_t>(bank.row_offset[f] + id);
@@ -223,6 +293,7 @@ __global__ __launch_bounds__(256) void lg_blocksum_kernel(int64_t R, LgWs w) {
   }
 }
 
+template <int RPT>
 __global__ __launch_bounds__(256) void lg_scan_kernel(int64_t R, int nblk, LgWs w) {
   __shared__ int2 red[4];
   __shared__ int2 wex[4];
@@ -237,11 +308,11 @@ __global__ __launch_bounds__(256) void lg_scan_kernel(int64_t R, int nblk, LgWs 
   const int2 p = block_sum2(ps, pn, red);
   if (tid == 0) base = p;
   __syncthreads();
-  const int64_t r0 = static_cast<int64_t>(blockIdx.x) * kLgRowsPerBlock + tid * 16;
-  int c[16];
+  const int64_t r0 = static_cast<int64_t>(blockIdx.x) * (256 * RPT) + tid * RPT;
+  int c[RPT];
   int s = 0, nz = 0;
 #pragma unroll
-  for (int j = 0; j < 16; ++j) {
+  for (int j = 0; j < RPT; ++j) {
     c[j] = r0 + j < R ? w.cnt[r0 + j] : 0;
     s += c[j];
     nz += c[j] > 0;
@@ -267,8 +338,8 @@ __global__ __launch_bounds__(256) void lg_scan_kernel(int64_t R, int nblk, LgWs 
   // the two list counters serialised ~10^3 atomics on one address at C4)
   int nl = 0, nc = 0;
 #pragma unroll
-  for (int j = 0; j < 16; ++j)
-    if (c[j] > kLgShort) {
+  for (int j = 0; j < RPT; ++j)
+    if (c[j] > kLgHuge) {
       ++nl;
       nc += (c[j] + kLgChunk - 1) / kLgChunk;
     }
@@ -289,7 +360,7 @@ __global__ __launch_bounds__(256) void lg_scan_kernel(int64_t R, int nblk, LgWs 
   int L = __shfl(bl, 63) + il - nl;
   int cb = __shfl(bc, 63) + ic - nc;
 #pragma unroll
-  for (int j = 0; j < 16; ++j) {
+  for (int j = 0; j < RPT; ++j) {
     const int64_t r = r0 + j;
     if (r >= R) break;
     w.start[r] = es;
@@ -298,7 +369,7 @@ __global__ __launch_bounds__(256) void lg_scan_kernel(int64_t R, int nblk, LgWs 
       w.ustart[en] = es;
       w.ulen[en] = c[j];
       int32_t myL = -1;
-      if (c[j] > kLgShort) {
+      if (c[j] > kLgHuge) {
         myL = L++;
         w.longs[myL] = en;
         const int nch = (c[j] + kLgChunk - 1) / kLgChunk;
@@ -364,6 +435,269 @@ __global__ __launch_bounds__(256) void lg_place_kernel(BankArgs bank, IdsArgs id
   }
 }
 
+// ---- bucketed plan -------------------------------------------------------------
+// bucket of a row: the top bits of a multiplicative hash (rows of one table, a hot
+// row's neighbours, a small table: all spread over the buckets)
+__device__ __forceinline__ int bk_of(int32_t r, int lognb) {
+  return static_cast<int>((static_cast<uint32_t>(r) * 2654435761u) >> (32 - lognb));
+}
+
+// chunk g: lookups [g * kBkChunk, ...) -> per-bucket counts, stored densely [g][NB]
+__global__ __launch_bounds__(kBkThreads) void bk_hist_kernel(BankArgs bank, IdsArgs ids, int64_t n,
+                                                             int lognb, LgWs w,
+                                                             int32_t *__restrict__ oob) {
+  __shared__ int32_t h[kBkMaxNB];
+  const int NB = 1 << lognb;
+  if (blockIdx.x == 0 && threadIdx.x < 8) w.hdr[threadIdx.x] = 0;
+  for (int k = threadIdx.x; k < NB; k += kBkThreads) h[k] = 0;
+  __syncthreads();
+  const int64_t total = n * bank.n_tables;
+  const int64_t i0 = static_cast<int64_t>(blockIdx.x) * kBkChunk + threadIdx.x;
+  int32_t rr[kBkPer];
+#pragma unroll
+  for (int u = 0; u < kBkPer; ++u) {
+    int64_t b;
+    rr[u] = lookup_row(bank, ids, n, i0 + u * kBkThreads, total, &b, oob);
+  }
+#pragma unroll
+  for (int u = 0; u < kBkPer; ++u)
+    if (rr[u] >= 0) atomicAdd(&h[bk_of(rr[u], lognb)], 1);
+  __syncthreads();
+  int32_t *dst = w.bhist + static_cast<int64_t>(blockIdx.x) * NB;
+  for (int k = threadIdx.x; k < NB; k += kBkThreads) dst[k] = h[k];
+}
+
+// per bucket (one thread each, 256 per workgroup): every chunk's count becomes its
+// first position inside the bucket (chunk order), and the bucket's total
+__global__ __launch_bounds__(256) void bk_scan_kernel(int G, int lognb, LgWs w) {
+  const int NB = 1 << lognb;
+  const int k = blockIdx.x * 256 + threadIdx.x;
+  if (k >= NB) return;
+  int tot = 0;
+  for (int g0 = 0; g0 < G; g0 += 16) {
+    int32_t c[16];
+#pragma unroll
+    for (int u = 0; u < 16; ++u)
+      c[u] = g0 + u < G ? w.bhist[static_cast<int64_t>(g0 + u) * NB + k] : 0;
+#pragma unroll
+    for (int u = 0; u < 16; ++u) {
+      if (g0 + u < G) w.bhist[static_cast<int64_t>(g0 + u) * NB + k] = tot;
+      tot += c[u];
+    }
+  }
+  w.bstart[k] = tot;  // the total for now: bk_scatter_kernel scans the totals
+}
+
+// exclusive scan of the NB bucket totals (bstart) into LDS base[]; returns the sum
+__device__ int bk_bucket_base(const int32_t *tot, int NB, int32_t *base, int32_t *wsum) {
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  constexpr int KPT = kBkMaxNB / kBkThreads;  // consecutive buckets per thread
+  int v[KPT], mine = 0;
+#pragma unroll
+  for (int q = 0; q < KPT; ++q) {
+    const int k = tid * KPT + q;
+    v[q] = k < NB ? tot[k] : 0;
+    mine += v[q];
+  }
+  int incl = mine;
+#pragma unroll
+  for (int off = 1; off < 64; off <<= 1) {
+    const int t = __shfl_up(incl, off);
+    if (lane >= off) incl += t;
+  }
+  if (lane == 63) wsum[wid] = incl;
+  __syncthreads();
+  int at = incl - mine, all = 0;
+  for (int k = 0; k < kBkThreads / 64; ++k) {
+    at += k < wid ? wsum[k] : 0;
+    all += wsum[k];
+  }
+#pragma unroll
+  for (int q = 0; q < KPT; ++q) {
+    const int k = tid * KPT + q;
+    if (k < NB) base[k] = at;
+    at += v[q];
+  }
+  __syncthreads();
+  return all;
+}
+
+// the same chunks as bk_hist_kernel: every valid lookup -> (row, b) at its
+// bucket's next position (LDS cursors; the order inside a bucket is not used for
+// arithmetic).  Workgroup 0 also publishes the bucket starts (bstart, written
+// after every workgroup has read the totals: bk_group_kernel reads them) -- so the
+// starts go to bhist's spare row G and bk_group_kernel reads them there.
+__global__ __launch_bounds__(kBkThreads) void bk_scatter_kernel(BankArgs bank, IdsArgs ids, int64_t n,
+                                                                int G, int lognb, LgWs w,
+                                                                int fused) {
+  __shared__ int32_t cur[kBkMaxNB];
+  __shared__ int32_t wsum[kBkThreads / 64];
+  const int NB = 1 << lognb;
+  const int64_t total = n * bank.n_tables;
+  const int64_t i0 = static_cast<int64_t>(blockIdx.x) * kBkChunk + threadIdx.x;
+  int32_t rr[kBkPer], bb[kBkPer];
+#pragma unroll
+  for (int u = 0; u < kBkPer; ++u) {
+    int64_t b = 0;
+    rr[u] = lookup_row(bank, ids, n, i0 + u * kBkThreads, total, &b, nullptr);
+    bb[u] = static_cast<int32_t>(b);
+  }
+  const int all = bk_bucket_base(w.bstart, NB, cur, wsum);
+  const int32_t *src = w.bhist + static_cast<int64_t>(blockIdx.x) * NB;
+  int32_t *pub = w.bhist + static_cast<int64_t>(G) * NB;  // spare row: bucket starts
+  for (int k = threadIdx.x; k < NB; k += kBkThreads) {
+    const int b0 = cur[k];
+    if (blockIdx.x == 0) pub[k] = b0;
+    cur[k] = b0 + src[k];
+  }
+  if (blockIdx.x == 0 && threadIdx.x == 0) {
+    pub[NB] = all;
+    // bucketed lists: entries with holes; the apply walks every slot (fused: only
+    // the huge segments, at their long slots)
+    w.hdr[0] = fused ? (all + kLgHuge) / (kLgHuge + 1) + 1 : all;
+    w.hdr[2] = (all + kLgHuge) / (kLgHuge + 1) + 1 + (all + kLgChunk - 1) / kLgChunk + 2;
+  }
+  __syncthreads();
+  const int lane = threadIdx.x & 63;
+#pragma unroll
+  for (int u = 0; u < kBkPer; ++u) {
+    const int32_t r = rr[u];
+    const int k = r >= 0 ? bk_of(r, lognb) : -1;
+    const Run x = lane_run(k);  // equal buckets in consecutive lanes: one atomic
+    int at = 0;
+    if (x.r >= 0 && x.head == lane) at = atomicAdd(&cur[x.r], x.len);
+    at = __shfl(at, x.head) + (lane - x.head);
+    if (r >= 0) w.ent[at] = make_int2(r, bb[u]);
+  }
+}
+
+// block-wide exclusive scan of one int per thread (256 threads); returns the total
+__device__ __forceinline__ int bk_scan256(int v, int *excl, int *red) {
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  int incl = v;
+#pragma unroll
+  for (int off = 1; off < 64; off <<= 1) {
+    const int t = __shfl_up(incl, off);
+    if (lane >= off) incl += t;
+  }
+  __syncthreads();  // red is free
+  if (lane == 63) red[wid] = incl;
+  __syncthreads();
+  int base = 0, tot = 0;
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    base += k < wid ? red[k] : 0;
+    tot += red[k];
+  }
+  *excl = base + incl - v;
+  return tot;
+}
+
+// one workgroup per bucket: its rows in an LDS hash (kBkSlots), per-row counts ->
+// segments inside the bucket's entry range [lo, hi), and the segment lists at
+// slots only this bucket uses: unique rows at [lo, lo + nu) (ulen 0 marks the
+// holes up to hi), huge segments (> kLgHuge lookups) at ceil(lo / 2049) + j, their
+// chunks at ceil(lo / 2049) + ceil(lo / 2048) + j (x = -1 marks holes) -- no
+// global atomics.
+__global__ __launch_bounds__(256) void bk_group_kernel(LgWs w, int G, int lognb,
+                                                       int32_t *__restrict__ err) {
+  __shared__ uint32_t key[kBkSlots];
+  __shared__ int32_t cnt[kBkSlots];
+  __shared__ int red[4];
+  constexpr int SPT = kBkSlots / 256;  // slots per thread
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int NB = 1 << lognb;
+  const int32_t *pub = w.bhist + static_cast<int64_t>(G) * NB;
+  const int lo = pub[blockIdx.x], hi = pub[blockIdx.x + 1];
+  for (int k = tid; k < kBkSlots; k += 256) {
+    key[k] = kLgEmpty;
+    cnt[k] = 0;
+  }
+  __syncthreads();
+  auto find = [&](int32_t r, bool insert) -> int {
+    // the hash bits below the bucket's (its top lognb bits are the same for all rows)
+    uint32_t hsh = ((static_cast<uint32_t>(r) * 2654435761u) << lognb) >> (32 - kBkSlotBits);
+    for (int p = 0; p < kBkSlots; ++p) {
+      const uint32_t k = insert ? atomicCAS(&key[hsh], kLgEmpty, static_cast<uint32_t>(r))
+                                : key[hsh];
+      if (k == static_cast<uint32_t>(r) || (insert && k == kLgEmpty)) return static_cast<int>(hsh);
+      hsh = (hsh + 1) & (kBkSlots - 1);
+    }
+    return -1;
+  };
+  // (entries of one chunk and bucket are contiguous: a hot row comes in runs)
+  for (int j0 = lo; j0 < hi; j0 += 256) {
+    const int j = j0 + tid;
+    const int32_t r = j < hi ? w.ent[j].x : -1;
+    const Run x = lane_run(r);
+    if (x.r >= 0 && x.head == lane) {
+      const int s = find(x.r, true);
+      if (s >= 0)
+        atomicAdd(&cnt[s], x.len);
+      else if (err)
+        *err = 1;  // more distinct rows in one bucket than slots (excluded by bk_groups)
+    }
+  }
+  __syncthreads();
+  // per slot: segment offset, unique / long / chunk index inside the bucket
+  int c[SPT], so = 0, su = 0, sl = 0, sc = 0;
+#pragma unroll
+  for (int q = 0; q < SPT; ++q) {
+    c[q] = cnt[tid * SPT + q];
+    so += c[q];
+    su += c[q] > 0;
+    sl += c[q] > kLgHuge;
+    sc += c[q] > kLgHuge ? (c[q] + kLgChunk - 1) / kLgChunk : 0;
+  }
+  int eo, eu, el, ec;
+  bk_scan256(so, &eo, red);
+  const int nu = bk_scan256(su, &eu, red);
+  bk_scan256(sl, &el, red);
+  const int nc = bk_scan256(sc, &ec, red);
+  const int l0 = (lo + kLgHuge) / (kLgHuge + 1);
+  const int c0 = l0 + (lo + kLgChunk - 1) / kLgChunk;
+  const int c1 = (hi + kLgHuge) / (kLgHuge + 1) + (hi + kLgChunk - 1) / kLgChunk;
+  int u = lo + eu, L = l0 + el, cb = c0 + ec, at = lo + eo;
+#pragma unroll
+  for (int q = 0; q < SPT; ++q) {
+    const int k = tid * SPT + q;
+    if (c[q] > 0) {
+      w.uniq[u] = static_cast<int32_t>(key[k]);
+      w.ustart[u] = at;
+      w.ulen[u] = c[q];
+      int32_t myL = -1;
+      if (c[q] > kLgHuge) {
+        myL = L++;
+        w.longs[myL] = u;
+        const int nch = (c[q] + kLgChunk - 1) / kLgChunk;
+        for (int t = 0; t < nch; ++t) w.chunks[cb + t] = make_int2(myL, t);
+        cb += nch;
+      }
+      w.ulong[u] = myL;
+      ++u;
+    }
+    cnt[k] = at;  // the slot's cursor
+    at += c[q];
+  }
+  for (int v = lo + nu + tid; v < hi; v += 256) w.ulen[v] = 0;
+  for (int v = c0 + nc + tid; v < c1; v += 256) w.chunks[v] = make_int2(-1, 0);
+  if (blockIdx.x == NB - 1)  // chunk slots past the last bucket's range
+    for (int v = c1 + tid; v < w.hdr[2]; v += 256) w.chunks[v] = make_int2(-1, 0);
+  __syncthreads();
+  for (int j0 = lo; j0 < hi; j0 += 256) {
+    const int j = j0 + tid;
+    const int2 e = j < hi ? w.ent[j] : make_int2(-1, 0);
+    const Run x = lane_run(e.x);
+    int p = 0;
+    if (x.r >= 0 && x.head == lane) {
+      const int s = find(x.r, false);
+      p = s >= 0 ? atomicAdd(&cnt[s], x.len) : -1;
+    }
+    p = __shfl(p, x.head);
+    if (e.x >= 0 && p >= 0) w.perm[p + (lane - x.head)] = e.y;
+  }
+}
+
 // ---- apply -------------------------------------------------------------------
 // pass 1 over the long segments' chunks: max |g| per segment (bits of a
 // non-negative float order like the float)
@@ -378,6 +712,7 @@ __global__ __launch_bounds__(256) void lg_longmax_kernel(BankArgs bank, int64_t 
   const int nchunks = w.hdr[2];
   for (int j = blockIdx.x; j < nchunks; j += gridDim.x) {
     const int2 ch = w.chunks[j];
+    if (ch.x < 0) continue;  // a hole (bucketed plan)
     const int u = w.longs[ch.x];
     const int f = table_of_row(bank, w.uniq[u]);
     const int s0 = w.ustart[u] + ch.y * kLgChunk;
@@ -419,6 +754,7 @@ __global__ __launch_bounds__(256) void lg_longacc_kernel(BankArgs bank, int64_t 
   const int nchunks = w.hdr[2];
   for (int j = blockIdx.x; j < nchunks; j += gridDim.x) {
     const int2 ch = w.chunks[j];
+    if (ch.x < 0) continue;  // a hole (bucketed plan; uniform over the workgroup)
     const int u = w.longs[ch.x];
     const int f = table_of_row(bank, w.uniq[u]);
     const int s0 = w.ustart[u] + ch.y * kLgChunk;
@@ -455,35 +791,52 @@ __global__ __launch_bounds__(256) void lg_longacc_kernel(BankArgs bank, int64_t 
   }
 }
 
-// one update per unique row
+// one update per unique row.  A wave takes 64 / LPR consecutive unique rows, one
+// per worker (LPR lanes): a segment of <= 16 lookups is sorted and summed in
+// ascending sample order by its worker; a segment of 17..kLgHuge lookups by the
+// whole wave in fixed point (max |g| over the segment, then the int64 sum of every
+// term scaled by 2^S: the arithmetic of the chunked kernels, so the same bits); a
+// longer one from the chunked kernels' accumulator.
 template <typename T, int LPR>
 __global__ __launch_bounds__(256) void lg_apply_kernel(BankArgs bank, int64_t n, LgWs w,
                                                        ApplyArgs a, int stride) {
   constexpr int EPL = Vec<T>::EPL;
-  constexpr int WPB = 256 / LPR;
+  constexpr int WPB = 256 / LPR;  // workers per workgroup
+  constexpr int WPW = 64 / LPR;   // workers per wave
   if (a.d_step) a.seed += *a.d_step * 0x9e3779b97f4a7c15ull;
-  const int worker = threadIdx.x / LPR, l = threadIdx.x % LPR, e0 = l * EPL;
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  const int wk = lane / LPR, l = lane % LPR, e0 = l * EPL;
   const int D = bank.dim;
   const bool v_lane = e0 + EPL <= D, w_lane = bank.has_w && e0 == D;
   const bool live = v_lane || w_lane;
-  // (lanes without a live element stay: a fused row-wise optimizer reduces
-  // across the worker's lanes)
-  if (!live && a.mode != MREC_BWD_ROWWISE_ADAGRAD) return;
   const int nu = w.hdr[0];
-  for (int u = blockIdx.x * WPB + worker; u < nu; u += gridDim.x * WPB) {
-    const int64_t grow = w.uniq[u];
-    const int f = table_of_row(bank, grow);
-    const int64_t row = grow - bank.row_offset[f];
-    const int len = w.ulen[u];
+  for (int u0 = blockIdx.x * WPB + wid * WPW; u0 < nu; u0 += gridDim.x * WPB) {
+    const int u = u0 + wk;
+    const int len = u < nu ? w.ulen[u] : 0;  // 0: past the end, or a hole (bucketed plan)
+    int64_t grow = 0;
+    int f = 0, L = -1, us = 0;
+    if (len > 0) {
+      grow = w.uniq[u];
+      f = table_of_row(bank, grow);
+      L = w.ulong[u];
+      us = w.ustart[u];
+    }
     float acc[EPL];
 #pragma unroll
     for (int q = 0; q < EPL; ++q) acc[q] = 0.f;
-    const int L = w.ulong[u];
-    if (!live) {
-    } else if (L < 0) {
+    if (len > 0 && live && L >= 0) {
+      const int S = lg_scale(__uint_as_float(w.segmax[L]), len);
+      long long *src = w.acc + static_cast<int64_t>(L) * stride + e0;
+#pragma unroll
+      for (int q = 0; q < EPL; ++q) {
+        acc[q] = static_cast<float>(ldexp(static_cast<double>(src[q]), -S));
+        src[q] = 0;  // left zero for the next call
+      }
+      if (l == 0) w.segmax[L] = 0u;
+    } else if (len > 0 && live && len <= kLgShort) {
       int r[kLgShort];
 #pragma unroll
-      for (int j = 0; j < kLgShort; ++j) r[j] = j < len ? w.perm[w.ustart[u] + j] : INT_MAX;
+      for (int j = 0; j < kLgShort; ++j) r[j] = j < len ? w.perm[us + j] : INT_MAX;
       if (len <= 4)
         bitonic_sort<4>(r);
       else if (len <= 8)
@@ -493,20 +846,244 @@ __global__ __launch_bounds__(256) void lg_apply_kernel(BankArgs bank, int64_t n,
 #pragma unroll
       for (int j = 0; j < kLgShort; ++j)
         if (j < len) add_lookup_grad<EPL>(a, r[j], f, D, e0, v_lane, w_lane, acc);
-    } else {
-      const int S = lg_scale(__uint_as_float(w.segmax[L]), len);
-      long long *src = w.acc + static_cast<int64_t>(L) * stride + e0;
+    }
+    // medium segments: the whole wave, one at a time (wave-uniform loop)
+    uint64_t med = __ballot(l == 0 && len > kLgShort && L < 0);
+    while (med) {
+      const int src = __ffsll(static_cast<unsigned long long>(med)) - 1;
+      med &= med - 1;
+      const int mlen = __shfl(len, src), ms = __shfl(us, src), mf = __shfl(f, src);
+      float m = 0.f;
+      if (live) {
+#pragma unroll 1
+        for (int j = wk; j < mlen; j += WPW) {
+          float g[EPL];
+          lookup_grad<EPL>(a, w.perm[ms + j], mf, D, e0, v_lane, w_lane, g);
 #pragma unroll
-      for (int q = 0; q < EPL; ++q) {
-        acc[q] = static_cast<float>(ldexp(static_cast<double>(src[q]), -S));
-        src[q] = 0;  // left zero for the next call
+          for (int q = 0; q < EPL; ++q) m = fmaxf(m, fabsf(g[q]));
+        }
       }
-      if (l == 0) w.segmax[L] = 0u;
+#pragma unroll
+      for (int off = 32; off > 0; off >>= 1) m = fmaxf(m, __shfl_xor(m, off));
+      const int S = lg_scale(m, mlen);
+      long long sa[EPL];
+#pragma unroll
+      for (int q = 0; q < EPL; ++q) sa[q] = 0;
+      if (live) {
+#pragma unroll 1
+        for (int j = wk; j < mlen; j += WPW) {
+          float g[EPL];
+          lookup_grad<EPL>(a, w.perm[ms + j], mf, D, e0, v_lane, w_lane, g);
+#pragma unroll
+          for (int q = 0; q < EPL; ++q) sa[q] += llrint(ldexp(static_cast<double>(g[q]), S));
+        }
+      }
+#pragma unroll
+      for (int off = LPR; off < 64; off <<= 1)
+#pragma unroll
+        for (int q = 0; q < EPL; ++q) sa[q] += __shfl_xor(sa[q], off);
+      if (wk == src / LPR)
+#pragma unroll
+        for (int q = 0; q < EPL; ++q) acc[q] = static_cast<float>(ldexp(static_cast<double>(sa[q]), -S));
+    }
+    if (len > 0) {
+      uint4 raw = make_uint4(0u, 0u, 0u, 0u);
+      if (live) raw = *reinterpret_cast<const uint4 *>(row_ptr_g<T>(bank, a, grow, e0));
+      row_update<T, LPR, -1>(bank, a, grow, e0, v_lane, w_lane, live, acc, raw);
+    }
+  }
+}
+
+// ---- fused bucketed plan + apply (mrec_emb_bwd_large_fused) ---------------------
+// bk_group_kernel's grouping, then the bucket's own rows are updated right there:
+// a segment of <= 16 lookups by one worker (sorted, ascending sample order), one of
+// 17..kLgHuge lookups by a whole wave in fixed point (the chunked kernels'
+// arithmetic: the same bits as the unfused apply); only huge segments (> kLgHuge)
+// go to the lists, indexed by their long slot, for the chunked kernels that follow.
+constexpr int kBkLdsPerm = 4096;  // a bucket's placed lookups stay in LDS up to this
+
+template <typename T, int LPR>
+__global__ __launch_bounds__(256) void bk_apply_kernel(BankArgs bank, LgWs w, ApplyArgs a, int G,
+                                                       int lognb) {
+  __shared__ uint32_t key[kBkSlots];
+  __shared__ int32_t cur[kBkSlots];   // counts, then placement cursors (end = start + count)
+  __shared__ int32_t seg[kBkSlots];   // segment start inside the bucket
+  __shared__ int32_t rowl[kBkSlots];  // short rows, then (from the top) medium rows: slots
+  __shared__ int32_t lperm[kBkLdsPerm];
+  __shared__ int red[4];
+  __shared__ int nshort_s, nmed_s;
+  constexpr int EPL = Vec<T>::EPL;
+  constexpr int WPB = 256 / LPR, WPW = 64 / LPR;
+  constexpr int SPT = kBkSlots / 256;
+  if (a.d_step) a.seed += *a.d_step * 0x9e3779b97f4a7c15ull;
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int NB = 1 << lognb;
+  const int32_t *pub = w.bhist + static_cast<int64_t>(G) * NB;
+  const int lo = pub[blockIdx.x], hi = pub[blockIdx.x + 1];
+  for (int k = tid; k < kBkSlots; k += 256) {
+    key[k] = kLgEmpty;
+    cur[k] = 0;
+  }
+  __syncthreads();
+  auto find = [&](int32_t r, bool insert) -> int {
+    uint32_t hsh = ((static_cast<uint32_t>(r) * 2654435761u) << lognb) >> (32 - kBkSlotBits);
+    for (int p = 0; p < kBkSlots; ++p) {
+      const uint32_t k = insert ? atomicCAS(&key[hsh], kLgEmpty, static_cast<uint32_t>(r))
+                                : key[hsh];
+      if (k == static_cast<uint32_t>(r) || (insert && k == kLgEmpty)) return static_cast<int>(hsh);
+      hsh = (hsh + 1) & (kBkSlots - 1);
+    }
+    return -1;
+  };
+  for (int j0 = lo; j0 < hi; j0 += 256) {
+    const int j = j0 + tid;
+    const int32_t r = j < hi ? w.ent[j].x : -1;
+    const Run x = lane_run(r);
+    if (x.r >= 0 && x.head == lane) {
+      const int s = find(x.r, true);
+      if (s >= 0) atomicAdd(&cur[s], x.len);
+    }
+  }
+  __syncthreads();
+  int c[SPT], so = 0, ss = 0, sm = 0, sl = 0, sc = 0;
+#pragma unroll
+  for (int q = 0; q < SPT; ++q) {
+    c[q] = cur[tid * SPT + q];
+    so += c[q];
+    ss += c[q] > 0 && c[q] <= kLgShort;
+    sm += c[q] > kLgShort && c[q] <= kLgHuge;
+    sl += c[q] > kLgHuge;
+    sc += c[q] > kLgHuge ? (c[q] + kLgChunk - 1) / kLgChunk : 0;
+  }
+  int eo, es, em, el, ec;
+  bk_scan256(so, &eo, red);
+  const int ns = bk_scan256(ss, &es, red);
+  const int nm = bk_scan256(sm, &em, red);
+  const int nl = bk_scan256(sl, &el, red);
+  const int nc = bk_scan256(sc, &ec, red);
+  const bool in_lds = nl == 0 && hi - lo <= kBkLdsPerm;
+  int32_t *P = in_lds ? lperm : w.perm + lo;  // the bucket's placed lookups
+  const int l0 = (lo + kLgHuge) / (kLgHuge + 1), l1 = (hi + kLgHuge) / (kLgHuge + 1);
+  const int c0 = l0 + (lo + kLgChunk - 1) / kLgChunk;
+  const int c1 = l1 + (hi + kLgChunk - 1) / kLgChunk;
+  int L = l0 + el, cb = c0 + ec, at = eo;
+#pragma unroll
+  for (int q = 0; q < SPT; ++q) {
+    const int k = tid * SPT + q;
+    if (c[q] > 0 && c[q] <= kLgShort) rowl[es++] = k;
+    if (c[q] > kLgShort && c[q] <= kLgHuge) rowl[kBkSlots - 1 - em++] = k;
+    if (c[q] > kLgHuge) {  // huge: the lists, at its long slot (u = L)
+      w.uniq[L] = static_cast<int32_t>(key[k]);
+      w.ustart[L] = lo + at;
+      w.ulen[L] = c[q];
+      w.ulong[L] = L;
+      w.longs[L] = L;
+      const int nch = (c[q] + kLgChunk - 1) / kLgChunk;
+      for (int t = 0; t < nch; ++t) w.chunks[cb + t] = make_int2(L, t);
+      cb += nch;
+      ++L;
+    }
+    seg[k] = at;
+    cur[k] = at;
+    at += c[q];
+  }
+  if (tid == 0) {
+    nshort_s = ns;
+    nmed_s = nm;
+  }
+  for (int v = l0 + nl + tid; v < l1; v += 256) w.ulen[v] = 0;
+  for (int v = c0 + nc + tid; v < c1; v += 256) w.chunks[v] = make_int2(-1, 0);
+  if (blockIdx.x == NB - 1) {  // slots past the last bucket's ranges
+    for (int v = l1 + tid; v < w.hdr[0]; v += 256) w.ulen[v] = 0;
+    for (int v = c1 + tid; v < w.hdr[2]; v += 256) w.chunks[v] = make_int2(-1, 0);
+  }
+  __syncthreads();
+  for (int j0 = lo; j0 < hi; j0 += 256) {
+    const int j = j0 + tid;
+    const int2 e = j < hi ? w.ent[j] : make_int2(-1, 0);
+    const Run x = lane_run(e.x);
+    int p = 0;
+    if (x.r >= 0 && x.head == lane) {
+      const int s = find(x.r, false);
+      p = s >= 0 ? atomicAdd(&cur[s], x.len) : -1;
+    }
+    p = __shfl(p, x.head);
+    if (e.x >= 0 && p >= 0) P[p + (lane - x.head)] = e.y;
+  }
+  __syncthreads();
+  // ---- the bucket's updates
+  const int wk = lane / LPR, l = lane % LPR, e0 = l * EPL;
+  const int worker = tid / LPR;
+  const int D = bank.dim;
+  const bool v_lane = e0 + EPL <= D, w_lane = bank.has_w && e0 == D;
+  const bool live = v_lane || w_lane;
+  const int nsh = nshort_s, nmd = nmed_s;
+  for (int r0 = 0; r0 < nsh; r0 += WPB) {  // short rows: one per worker
+    const int r = r0 + worker;
+    if (r >= nsh) break;
+    const int k = rowl[r];
+    const int len = cur[k] - seg[k];
+    const int64_t grow = key[k];
+    const int f = table_of_row(bank, grow);
+    float acc[EPL];
+#pragma unroll
+    for (int q = 0; q < EPL; ++q) acc[q] = 0.f;
+    if (live) {
+      int rr[kLgShort];
+#pragma unroll
+      for (int j = 0; j < kLgShort; ++j) rr[j] = j < len ? P[seg[k] + j] : INT_MAX;
+      if (len <= 4)
+        bitonic_sort<4>(rr);
+      else if (len <= 8)
+        bitonic_sort<8>(rr);
+      else
+        bitonic_sort<16>(rr);
+#pragma unroll
+      for (int j = 0; j < kLgShort; ++j)
+        if (j < len) add_lookup_grad<EPL>(a, rr[j], f, D, e0, v_lane, w_lane, acc);
     }
     uint4 raw = make_uint4(0u, 0u, 0u, 0u);
     if (live) raw = *reinterpret_cast<const uint4 *>(row_ptr_g<T>(bank, a, grow, e0));
     row_update<T, LPR, -1>(bank, a, grow, e0, v_lane, w_lane, live, acc, raw);
-    (void)row;
+  }
+  for (int m = wid; m < nmd; m += 4) {  // medium rows: one per wave (wave-uniform)
+    const int k = rowl[kBkSlots - 1 - m];
+    const int ms = seg[k], mlen = cur[k] - seg[k];
+    const int64_t grow = key[k];
+    const int f = table_of_row(bank, grow);
+    float mx = 0.f;
+    if (live)
+      for (int j = wk; j < mlen; j += WPW) {
+        float g[EPL];
+        lookup_grad<EPL>(a, P[ms + j], f, D, e0, v_lane, w_lane, g);
+#pragma unroll
+        for (int q = 0; q < EPL; ++q) mx = fmaxf(mx, fabsf(g[q]));
+      }
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) mx = fmaxf(mx, __shfl_xor(mx, off));
+    const int S = lg_scale(mx, mlen);
+    long long sa[EPL];
+#pragma unroll
+    for (int q = 0; q < EPL; ++q) sa[q] = 0;
+    if (live)
+      for (int j = wk; j < mlen; j += WPW) {
+        float g[EPL];
+        lookup_grad<EPL>(a, P[ms + j], f, D, e0, v_lane, w_lane, g);
+#pragma unroll
+        for (int q = 0; q < EPL; ++q) sa[q] += llrint(ldexp(static_cast<double>(g[q]), S));
+      }
+#pragma unroll
+    for (int off = LPR; off < 64; off <<= 1)
+#pragma unroll
+      for (int q = 0; q < EPL; ++q) sa[q] += __shfl_xor(sa[q], off);
+    if (wk == 0) {
+      float acc[EPL];
+#pragma unroll
+      for (int q = 0; q < EPL; ++q) acc[q] = static_cast<float>(ldexp(static_cast<double>(sa[q]), -S));
+      uint4 raw = make_uint4(0u, 0u, 0u, 0u);
+      if (live) raw = *reinterpret_cast<const uint4 *>(row_ptr_g<T>(bank, a, grow, e0));
+      row_update<T, LPR, -1>(bank, a, grow, e0, v_lane, w_lane, live, acc, raw);
+    }
   }
 }
 
@@ -564,32 +1141,37 @@ mrec_status mrec_emb_bwd_large_plan(const mrec_table_bank *bank, const mrec_ids 
   if ((st = make_ids_args(ids, ba.n_tables, &ia)) != MREC_OK) return st;
   hipStream_t s = static_cast<hipStream_t>(stream);
   if (batch == 0) return MREC_OK;  // (apply returns early for batch 0 as well)
+  const int64_t total = batch * ba.n_tables;
+  const int G = bk_groups(R, total);
+  if (G > 0 && !std::getenv("MREC_LG_ATOMIC_PLAN")) {
+    const int NB = bk_buckets(total);
+    int lognb = 0;
+    while ((1 << lognb) < NB) ++lognb;
+    bk_hist_kernel<<<dim3(G), kBkThreads, 0, s>>>(ba, ia, batch, lognb, w, d_oob_flag);
+    bk_scan_kernel<<<dim3((NB + 255) / 256), 256, 0, s>>>(G, lognb, w);
+    bk_scatter_kernel<<<dim3(G), kBkThreads, 0, s>>>(ba, ia, batch, G, lognb, w, 0);
+    bk_group_kernel<<<dim3(NB), 256, 0, s>>>(w, G, lognb, d_oob_flag);
+    return launch_status("mrec_emb_bwd_large_plan");
+  }
   if (hipMemsetAsync(w.cnt, 0, static_cast<size_t>(R) * 4, s) != hipSuccess)
     return launch_status("mrec_emb_bwd_large_plan (memset)");
-  const int64_t total = batch * ba.n_tables;
   const int nblk = static_cast<int>((R + kLgRowsPerBlock - 1) / kLgRowsPerBlock);
   const unsigned gl = static_cast<unsigned>((total + 256 * kLgIter - 1) / (256 * kLgIter));
   lg_count_kernel<<<dim3(gl), 256, 0, s>>>(ba, ia, batch, w, d_oob_flag);
   lg_blocksum_kernel<<<dim3(nblk), 256, 0, s>>>(R, w);
-  lg_scan_kernel<<<dim3(nblk), 256, 0, s>>>(R, nblk, w);
+  lg_scan_kernel<16><<<dim3(nblk), 256, 0, s>>>(R, nblk, w);
   lg_place_kernel<<<dim3(gl), 256, 0, s>>>(ba, ia, batch, w);
   return launch_status("mrec_emb_bwd_large_plan");
 }
 
-mrec_status mrec_emb_bwd_large_apply(const mrec_table_bank *bank, int64_t batch,
-                                     const void *workspace, size_t ws_bytes, const void *dx,
-                                     mrec_dtype dx_dtype, int64_t dx_ld, const float *dfm,
-                                     const float *fm_sum, const void *x0, mrec_dtype x0_dtype,
-                                     int64_t x0_ld, const float *dw, mrec_bwd_mode mode, float lr,
-                                     uint64_t seed, const uint64_t *d_step, void *grad,
-                                     mrec_stream stream) {
-  BankArgs ba;
-  int lpr;
-  int64_t R;
-  LgWs w;
-  mrec_status st = lg_setup(bank, batch, const_cast<void *>(workspace), ws_bytes, &ba, &lpr, &R,
-                            &w);
-  if (st != MREC_OK) return st;
+}  // extern "C"
+
+// the apply arguments, checked (shared by mrec_emb_bwd_large_apply / _fused)
+static mrec_status lg_apply_args(const mrec_table_bank *bank, const BankArgs &ba, const void *dx,
+                                 mrec_dtype dx_dtype, int64_t dx_ld, const float *dfm,
+                                 const float *fm_sum, const void *x0, mrec_dtype x0_dtype,
+                                 int64_t x0_ld, const float *dw, mrec_bwd_mode mode, float lr,
+                                 uint64_t seed, const uint64_t *d_step, void *grad, ApplyArgs *out) {
   MREC_CHECK_ARG(mode >= MREC_BWD_DENSE_GRAD && mode <= MREC_BWD_ADAM, "bad mode");
   OptArgs opt{};
   {
@@ -631,17 +1213,27 @@ mrec_status mrec_emb_bwd_large_apply(const mrec_table_bank *bank, int64_t batch,
   a.d_step = d_step;
   a.opt = opt;
   a.grad = grad;
-  if (batch == 0) return MREC_OK;
-  hipStream_t s = static_cast<hipStream_t>(stream);
-  const int stride = ba.row_stride;
+  *out = a;
+  return MREC_OK;
+}
+
+// the chunked kernels and the per-row apply (fused: the bucket kernel first, the
+// per-row apply then walks only the huge segments' slots)
+template <typename T, int L>
+static void lg_launch_apply(const BankArgs &ba, int64_t batch, const LgWs &w, const ApplyArgs &a,
+                            int stride, int fused_nb, int G, int lognb, hipStream_t s) {
+  if (fused_nb) bk_apply_kernel<T, L><<<dim3(fused_nb), 256, 0, s>>>(ba, w, a, G, lognb);
   const dim3 g(kLgApplyBlocks);
-#define MREC_LG(T, L)                                                         \
-  do {                                                                        \
-    lg_longmax_kernel<T, L><<<g, 256, 0, s>>>(ba, batch, w, a);               \
-    lg_longacc_kernel<T, L><<<g, 256, 0, s>>>(ba, batch, w, a, stride);       \
-    lg_apply_kernel<T, L><<<g, 256, 0, s>>>(ba, batch, w, a, stride);         \
-  } while (0)
-  if (bank->dtype == MREC_BF16) {
+  lg_longmax_kernel<T, L><<<g, 256, 0, s>>>(ba, batch, w, a);
+  lg_longacc_kernel<T, L><<<g, 256, 0, s>>>(ba, batch, w, a, stride);
+  lg_apply_kernel<T, L><<<g, 256, 0, s>>>(ba, batch, w, a, stride);
+}
+
+static void lg_dispatch_apply(mrec_dtype dtype, int lpr, const BankArgs &ba, int64_t batch,
+                              const LgWs &w, const ApplyArgs &a, int stride, int fused_nb, int G,
+                              int lognb, hipStream_t s) {
+#define MREC_LG(T, L) lg_launch_apply<T, L>(ba, batch, w, a, stride, fused_nb, G, lognb, s)
+  if (dtype == MREC_BF16) {
     switch (lpr) {
       case 1: MREC_LG(uint16_t, 1); break;
       case 2: MREC_LG(uint16_t, 2); break;
@@ -659,7 +1251,72 @@ mrec_status mrec_emb_bwd_large_apply(const mrec_table_bank *bank, int64_t batch,
     }
   }
 #undef MREC_LG
+}
+
+extern "C" {
+
+mrec_status mrec_emb_bwd_large_apply(const mrec_table_bank *bank, int64_t batch,
+                                     const void *workspace, size_t ws_bytes, const void *dx,
+                                     mrec_dtype dx_dtype, int64_t dx_ld, const float *dfm,
+                                     const float *fm_sum, const void *x0, mrec_dtype x0_dtype,
+                                     int64_t x0_ld, const float *dw, mrec_bwd_mode mode, float lr,
+                                     uint64_t seed, const uint64_t *d_step, void *grad,
+                                     mrec_stream stream) {
+  BankArgs ba;
+  int lpr;
+  int64_t R;
+  LgWs w;
+  mrec_status st = lg_setup(bank, batch, const_cast<void *>(workspace), ws_bytes, &ba, &lpr, &R,
+                            &w);
+  if (st != MREC_OK) return st;
+  ApplyArgs a;
+  st = lg_apply_args(bank, ba, dx, dx_dtype, dx_ld, dfm, fm_sum, x0, x0_dtype, x0_ld, dw, mode,
+                     lr, seed, d_step, grad, &a);
+  if (st != MREC_OK) return st;
+  if (batch == 0) return MREC_OK;
+  lg_dispatch_apply(bank->dtype, lpr, ba, batch, w, a, ba.row_stride, 0, 0, 0,
+                    static_cast<hipStream_t>(stream));
   return launch_status("mrec_emb_bwd_large_apply");
+}
+
+mrec_status mrec_emb_bwd_large_fused(const mrec_table_bank *bank, const mrec_ids *ids,
+                                     int64_t batch, void *workspace, size_t ws_bytes,
+                                     int32_t *d_oob_flag, const void *dx, mrec_dtype dx_dtype,
+                                     int64_t dx_ld, const float *dfm, const float *fm_sum,
+                                     const void *x0, mrec_dtype x0_dtype, int64_t x0_ld,
+                                     const float *dw, mrec_bwd_mode mode, float lr, uint64_t seed,
+                                     const uint64_t *d_step, void *grad, mrec_stream stream) {
+  BankArgs ba;
+  IdsArgs ia;
+  int lpr;
+  int64_t R;
+  LgWs w;
+  mrec_status st = lg_setup(bank, batch, workspace, ws_bytes, &ba, &lpr, &R, &w);
+  if (st != MREC_OK) return st;
+  if ((st = make_ids_args(ids, ba.n_tables, &ia)) != MREC_OK) return st;
+  ApplyArgs a;
+  st = lg_apply_args(bank, ba, dx, dx_dtype, dx_ld, dfm, fm_sum, x0, x0_dtype, x0_ld, dw, mode,
+                     lr, seed, d_step, grad, &a);
+  if (st != MREC_OK) return st;
+  if (batch == 0) return MREC_OK;
+  const int64_t total = batch * ba.n_tables;
+  const int G = bk_groups(R, total);
+  if (G == 0 || std::getenv("MREC_LG_ATOMIC_PLAN")) {  // the two-call path
+    st = mrec_emb_bwd_large_plan(bank, ids, batch, workspace, ws_bytes, d_oob_flag, stream);
+    if (st != MREC_OK) return st;
+    return mrec_emb_bwd_large_apply(bank, batch, workspace, ws_bytes, dx, dx_dtype, dx_ld, dfm,
+                                    fm_sum, x0, x0_dtype, x0_ld, dw, mode, lr, seed, d_step, grad,
+                                    stream);
+  }
+  hipStream_t s = static_cast<hipStream_t>(stream);
+  const int NB = bk_buckets(total);
+  int lognb = 0;
+  while ((1 << lognb) < NB) ++lognb;
+  bk_hist_kernel<<<dim3(G), kBkThreads, 0, s>>>(ba, ia, batch, lognb, w, d_oob_flag);
+  bk_scan_kernel<<<dim3((NB + 255) / 256), 256, 0, s>>>(G, lognb, w);
+  bk_scatter_kernel<<<dim3(G), kBkThreads, 0, s>>>(ba, ia, batch, G, lognb, w, 1);
+  lg_dispatch_apply(bank->dtype, lpr, ba, batch, w, a, ba.row_stride, NB, G, lognb, s);
+  return launch_status("mrec_emb_bwd_large_fused");
 }
 
 }  // extern "C"

@@ -276,8 +276,16 @@ __global__ __launch_bounds__(kBT) void bucketize_dedup_kernel(IdsArgs ids, RowsA
 // dim 16 + w: 36 B, against 64 B per slot), part p of a wire buffer holds cap_rows
 // records; table f's entries of part p start at prefix_p(f) = sum_{g<f} count_p(g)
 // (the counts of the header of `hdr`, W parts of n_tables*cap + n_tables int32).
-// One 256-thread workgroup per (part, table), one thread per record, dword copies.
+// The kernels below walk one part's records as a FLAT element space (record x
+// dword): a workgroup takes kWireElems consecutive elements, so lanes touch
+// consecutive dwords of the wire (coalesced) and every workgroup has the same
+// amount of work whatever the per-table counts; an element's table comes from a
+// binary search of the part's count prefix, kept in LDS.
 // ---------------------------------------------------------------------------
+
+constexpr int kWireThreads = 256;
+constexpr int kWirePer = 8;  // elements per thread
+constexpr int kWireElems = kWireThreads * kWirePer;
 
 struct WireArgs {
   const int32_t *hdr;  // W parts of F*cap + F (counts at F*cap + f)
@@ -286,98 +294,156 @@ struct WireArgs {
   int32_t *overflow;
 };
 
-// prefix of table f in part p, and its count; flags (and clips to) cap_rows
-__device__ __forceinline__ void wire_span(const WireArgs &w, int p, int f, int *base, int *cnt) {
-  const int32_t *h = w.hdr + static_cast<int64_t>(p) * (static_cast<int64_t>(w.F) * w.cap + w.F) +
-                     static_cast<int64_t>(w.F) * w.cap;
-  int pre = 0;
-  for (int g = 0; g < f; ++g) pre += h[g];
-  int c = h[f];
-  if (pre + c > w.cap_rows) {
-    if (w.overflow && threadIdx.x == 0) *w.overflow = 1;
-    c = max(0, w.cap_rows - pre);
+// exclusive prefix of part p's per-table counts into pre[0..F]; returns the part's
+// record total, clipped to cap_rows (and flags the overflow)
+__device__ __forceinline__ int wire_prefix(const WireArgs &w, int p, int *pre) {
+  if (threadIdx.x < 64) {
+    const int lane = threadIdx.x;
+    const int32_t *h = w.hdr + static_cast<int64_t>(p) * (static_cast<int64_t>(w.F) * w.cap + w.F) +
+                       static_cast<int64_t>(w.F) * w.cap;
+    int s = lane < w.F ? h[lane] : 0;
+#pragma unroll
+    for (int off = 1; off < 64; off <<= 1) {
+      const int t = __shfl_up(s, off);
+      if (lane >= off) s += t;
+    }
+    if (lane < w.F) pre[lane + 1] = s;
+    if (lane == 0) pre[0] = 0;
   }
-  *base = p * w.cap_rows + pre;
-  *cnt = c;
+  __syncthreads();
+  int tot = pre[w.F];
+  if (tot > w.cap_rows) {
+    if (w.overflow && threadIdx.x == 0) *w.overflow = 1;
+    tot = w.cap_rows;
+  }
+  return tot;
 }
 
-// owner: local bank rows of part p's received ids -> wire records
-__global__ __launch_bounds__(256) void gather_wire_kernel(BankArgs bank, WireArgs w,
-                                                          const int32_t *__restrict__ recv,
-                                                          uint32_t *__restrict__ wire) {
-  const int p = blockIdx.x / w.F, f = blockIdx.x % w.F;
-  int base, cnt;
-  wire_span(w, p, f, &base, &cnt);
-  const int32_t *ids = recv + static_cast<int64_t>(p) * (static_cast<int64_t>(w.F) * w.cap + w.F) +
-                       static_cast<int64_t>(f) * w.cap;
-  for (int j = threadIdx.x; j < cnt; j += 256) {
-    const int64_t id = ids[j];
-    uint32_t *dst = wire + static_cast<int64_t>(base + j) * w.rec_dw;
-    if (id < 0 || id >= bank.rows[f]) {
-      for (int k = 0; k < w.rec_dw; ++k) dst[k] = 0u;
-      continue;
+// the table holding record r (< the part's total): the largest f with pre[f] <= r
+__device__ __forceinline__ int wire_table(const int *pre, int F, int r) {
+  int lo = 0, hi = F;  // pre[lo] <= r < pre[hi]
+  while (hi - lo > 1) {
+    const int mid = (lo + hi) >> 1;
+    if (pre[mid] <= r)
+      lo = mid;
+    else
+      hi = mid;
+  }
+  return lo;
+}
+
+// owner: local bank rows of part p's received ids -> wire records (grid: chunks x W)
+__global__ __launch_bounds__(kWireThreads) void gather_wire_kernel(BankArgs bank, WireArgs w,
+                                                                   const int32_t *__restrict__ recv,
+                                                                   uint32_t *__restrict__ wire) {
+  __shared__ int pre[MREC_MAX_TABLES + 1];
+  __shared__ int64_t roff[MREC_MAX_TABLES], nrows[MREC_MAX_TABLES];
+  const int p = blockIdx.y;
+  if (threadIdx.x < w.F) {
+    roff[threadIdx.x] = bank.row_offset[threadIdx.x];
+    nrows[threadIdx.x] = bank.rows[threadIdx.x];
+  }
+  const int tot = wire_prefix(w, p, pre);  // (its barrier covers roff / nrows too)
+  const int64_t n = static_cast<int64_t>(tot) * w.rec_dw;
+  const int64_t e0 = static_cast<int64_t>(blockIdx.x) * kWireElems + threadIdx.x;
+  if (e0 - threadIdx.x >= n) return;
+  const int32_t *ids = recv + static_cast<int64_t>(p) * (static_cast<int64_t>(w.F) * w.cap + w.F);
+  const uint32_t *data = reinterpret_cast<const uint32_t *>(bank.data);
+  const int row_dw = bank.lpr * 4;
+  int64_t src[kWirePer];
+#pragma unroll
+  for (int it = 0; it < kWirePer; ++it) {  // every id load first
+    const int64_t e = e0 + it * kWireThreads;
+    src[it] = -1;
+    if (e < n) {
+      const int r = static_cast<int>(e / w.rec_dw), k = static_cast<int>(e - int64_t(r) * w.rec_dw);
+      const int f = wire_table(pre, w.F, r);
+      const int64_t id = ids[static_cast<int64_t>(f) * w.cap + (r - pre[f])];
+      if (id >= 0 && id < nrows[f]) src[it] = (roff[f] + id) * row_dw + k;
     }
-    const uint32_t *src = reinterpret_cast<const uint32_t *>(bank.data) +
-                          (bank.row_offset[f] + id) * (bank.lpr * 4);
-    uint32_t v[18];
+  }
+  uint32_t v[kWirePer];
 #pragma unroll
-    for (int k = 0; k < 18; ++k)
-      if (k < w.rec_dw) v[k] = src[k];
+  for (int it = 0; it < kWirePer; ++it) v[it] = src[it] >= 0 ? data[src[it]] : 0u;
+  uint32_t *dst = wire + static_cast<int64_t>(p) * w.cap_rows * w.rec_dw;
 #pragma unroll
-    for (int k = 0; k < 18; ++k)
-      if (k < w.rec_dw) dst[k] = v[k];
+  for (int it = 0; it < kWirePer; ++it) {
+    const int64_t e = e0 + it * kWireThreads;
+    if (e < n) dst[e] = v[it];
   }
 }
 
 // wire records <-> slot rows [(p * F + f) * cap + j] of `slots` (row pitch slot_dw
-// dwords).  unpack: the record into the slot row (dwords past the record zeroed;
-// with to_f32 the bf16 record is widened to fp32: dwords of fp32 = 2 x record
-// elements), and optionally zero `zero_dw` dwords of the same row of `zero`;
-// pack: the slot row's first rec_dw dwords into the record.
+// dwords).  unpack (elements = record x max(slot_dw, zero_dw)): the record into
+// the slot row (dwords past the record zeroed; with to_f32 the bf16 record is
+// widened to fp32: dwords of fp32 = 2 x record elements), and zero the first
+// zero_dw dwords of the same row of `zero` when given; pack (elements = record x
+// rec_dw): the slot row's first rec_dw dwords into the record.  Grid: chunks x W.
 template <bool UNPACK, bool TO_F32>
-__global__ __launch_bounds__(256) void wire_move_kernel(WireArgs w, uint32_t *__restrict__ wire,
-                                                        uint32_t *__restrict__ slots, int slot_dw,
-                                                        uint32_t *__restrict__ zero, int zero_dw) {
-  const int p = blockIdx.x / w.F, f = blockIdx.x % w.F;
-  int base, cnt;
-  wire_span(w, p, f, &base, &cnt);
-  for (int j = threadIdx.x; j < cnt; j += 256) {
-    uint32_t *rec = wire + static_cast<int64_t>(base + j) * w.rec_dw;
-    const int64_t srow = (static_cast<int64_t>(p) * w.F + f) * w.cap + j;
-    uint32_t *row = slots + srow * slot_dw;
-    if constexpr (UNPACK) {
-      uint32_t v[18];
+__global__ __launch_bounds__(kWireThreads) void wire_move_kernel(WireArgs w,
+                                                                 uint32_t *__restrict__ wire,
+                                                                 uint32_t *__restrict__ slots,
+                                                                 int slot_dw,
+                                                                 uint32_t *__restrict__ zero,
+                                                                 int zero_dw) {
+  __shared__ int pre[MREC_MAX_TABLES + 1];
+  const int p = blockIdx.y;
+  const int tot = wire_prefix(w, p, pre);
+  const int epr = UNPACK ? max(slot_dw, zero ? zero_dw : 0) : w.rec_dw;
+  const int64_t n = static_cast<int64_t>(tot) * epr;
+  const int64_t e0 = static_cast<int64_t>(blockIdx.x) * kWireElems + threadIdx.x;
+  if (e0 - threadIdx.x >= n) return;
+  uint32_t *rec0 = wire + static_cast<int64_t>(p) * w.cap_rows * w.rec_dw;
+  int64_t srow[kWirePer];
+  int kk[kWirePer], rr[kWirePer];
 #pragma unroll
-      for (int k = 0; k < 18; ++k)
-        if (k < w.rec_dw) v[k] = rec[k];
-      if constexpr (TO_F32) {  // bf16 pairs -> two fp32
-#pragma unroll
-        for (int k = 0; k < 18; ++k)
-          if (k < w.rec_dw && 2 * k + 1 < slot_dw) {
-            row[2 * k] = v[k] << 16;
-            row[2 * k + 1] = v[k] & 0xffff0000u;
-          }
-        for (int k = 2 * w.rec_dw; k < slot_dw; ++k) row[k] = 0u;
-      } else {
-#pragma unroll
-        for (int k = 0; k < 18; ++k)
-          if (k < w.rec_dw) row[k] = v[k];
-        for (int k = w.rec_dw; k < slot_dw; ++k) row[k] = 0u;
-      }
-      if (zero) {
-        uint32_t *z = zero + srow * zero_dw;
-        for (int k = 0; k < zero_dw; ++k) z[k] = 0u;
-      }
-    } else {
-      uint32_t v[18];
-#pragma unroll
-      for (int k = 0; k < 18; ++k)
-        if (k < w.rec_dw) v[k] = row[k];
-#pragma unroll
-      for (int k = 0; k < 18; ++k)
-        if (k < w.rec_dw) rec[k] = v[k];
+  for (int it = 0; it < kWirePer; ++it) {
+    const int64_t e = e0 + it * kWireThreads;
+    srow[it] = -1;
+    kk[it] = 0;
+    rr[it] = 0;
+    if (e < n) {
+      const int r = static_cast<int>(e / epr);
+      const int f = wire_table(pre, w.F, r);
+      srow[it] = (static_cast<int64_t>(p) * w.F + f) * w.cap + (r - pre[f]);
+      kk[it] = static_cast<int>(e - int64_t(r) * epr);
+      rr[it] = r;
     }
   }
+  if constexpr (UNPACK) {
+    uint32_t v[kWirePer];
+#pragma unroll
+    for (int it = 0; it < kWirePer; ++it) {
+      const int k = kk[it];
+      const int src = TO_F32 ? (k >> 1) : k;
+      v[it] = (srow[it] >= 0 && src < w.rec_dw && (!TO_F32 || k < 2 * w.rec_dw))
+                  ? rec0[static_cast<int64_t>(rr[it]) * w.rec_dw + src]
+                  : 0u;
+    }
+#pragma unroll
+    for (int it = 0; it < kWirePer; ++it) {
+      if (srow[it] < 0) continue;
+      const int k = kk[it];
+      uint32_t x = v[it];
+      if constexpr (TO_F32) x = (k & 1) ? (x & 0xffff0000u) : (x << 16);  // bf16 pair -> fp32
+      if (k < slot_dw) slots[srow[it] * slot_dw + k] = x;
+      if (zero && k < zero_dw) zero[srow[it] * zero_dw + k] = 0u;
+    }
+  } else {
+    uint32_t v[kWirePer];
+#pragma unroll
+    for (int it = 0; it < kWirePer; ++it)
+      v[it] = srow[it] >= 0 ? slots[srow[it] * slot_dw + kk[it]] : 0u;
+#pragma unroll
+    for (int it = 0; it < kWirePer; ++it)
+      if (srow[it] >= 0) rec0[static_cast<int64_t>(rr[it]) * w.rec_dw + kk[it]] = v[it];
+  }
+}
+
+static dim3 wire_grid(const WireArgs &w, int elems_per_record) {
+  const int64_t chunks = (static_cast<int64_t>(w.cap_rows) * elems_per_record + kWireElems - 1) /
+                         kWireElems;
+  return dim3(static_cast<unsigned>(chunks), static_cast<unsigned>(w.W));
 }
 
 template <int LPR, typename T = uint16_t, bool ADAM = false>
@@ -658,8 +724,9 @@ mrec_status mrec_shard_gather_wire(const mrec_table_bank *local, const int32_t *
   WireArgs w;
   st = wire_args(recv_ids, world, ba.n_tables, cap, cap_rows, rec, d_overflow, &w);
   if (st != MREC_OK) return st;
-  gather_wire_kernel<<<dim3(world * ba.n_tables), 256, 0, static_cast<hipStream_t>(stream)>>>(
-      ba, w, recv_ids, static_cast<uint32_t *>(wire));
+  gather_wire_kernel<<<wire_grid(w, w.rec_dw), kWireThreads, 0,
+                       static_cast<hipStream_t>(stream)>>>(ba, w, recv_ids,
+                                                           static_cast<uint32_t *>(wire));
   return launch_status("mrec_shard_gather_wire");
 }
 
@@ -675,19 +742,16 @@ mrec_status mrec_shard_wire_unpack(const void *wire, int32_t rec_bytes, const in
                  "row pitches must be multiples of 4 bytes");
   MREC_CHECK_ARG(slot_bytes >= (to_f32 ? 2 : 1) * rec_bytes, "slot rows narrower than the record");
   MREC_CHECK_ARG(!zero || zero_bytes > 0, "zero rows need their pitch");
-  const dim3 g(static_cast<unsigned>(world * n_tables));
+  const int slot_dw = static_cast<int>(slot_bytes / 4), zero_dw = static_cast<int>(zero_bytes / 4);
+  const dim3 g = wire_grid(w, std::max(slot_dw, zero ? zero_dw : 0));
   hipStream_t s = static_cast<hipStream_t>(stream);
   uint32_t *wp = static_cast<uint32_t *>(const_cast<void *>(wire));
   if (to_f32)
-    wire_move_kernel<true, true><<<g, 256, 0, s>>>(w, wp, static_cast<uint32_t *>(slots),
-                                                   static_cast<int>(slot_bytes / 4),
-                                                   static_cast<uint32_t *>(zero),
-                                                   static_cast<int>(zero_bytes / 4));
+    wire_move_kernel<true, true><<<g, kWireThreads, 0, s>>>(
+        w, wp, static_cast<uint32_t *>(slots), slot_dw, static_cast<uint32_t *>(zero), zero_dw);
   else
-    wire_move_kernel<true, false><<<g, 256, 0, s>>>(w, wp, static_cast<uint32_t *>(slots),
-                                                    static_cast<int>(slot_bytes / 4),
-                                                    static_cast<uint32_t *>(zero),
-                                                    static_cast<int>(zero_bytes / 4));
+    wire_move_kernel<true, false><<<g, kWireThreads, 0, s>>>(
+        w, wp, static_cast<uint32_t *>(slots), slot_dw, static_cast<uint32_t *>(zero), zero_dw);
   return launch_status("mrec_shard_wire_unpack");
 }
 
@@ -700,7 +764,7 @@ mrec_status mrec_shard_wire_pack(const void *slots, int64_t slot_bytes, int32_t 
   if (st != MREC_OK) return st;
   MREC_CHECK_ARG(wire && slots, "NULL pointer");
   MREC_CHECK_ARG(slot_bytes % 4 == 0 && slot_bytes >= rec_bytes, "bad slot pitch");
-  wire_move_kernel<false, false><<<dim3(static_cast<unsigned>(world * n_tables)), 256, 0,
+  wire_move_kernel<false, false><<<wire_grid(w, w.rec_dw), kWireThreads, 0,
                                    static_cast<hipStream_t>(stream)>>>(
       w, static_cast<uint32_t *>(wire), static_cast<uint32_t *>(const_cast<void *>(slots)),
       static_cast<int>(slot_bytes / 4), nullptr, 0);

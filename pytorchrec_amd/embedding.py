@@ -346,6 +346,8 @@ def _chunks(batch: int):
 LARGE_MAX_ROWS = 1 << 24  # banks up to this many rows take the large-batch path
 # MREC_LARGE_BATCH=0: chunked plan/apply pairs instead (one SGD step per chunk)
 LARGE_BATCH = os.environ.get("MREC_LARGE_BATCH", "1") == "1"
+# MREC_LARGE_FUSED=0: the plan / apply pair instead of mrec_emb_bwd_large_fused
+LARGE_FUSED = os.environ.get("MREC_LARGE_FUSED", "1") == "1"
 
 
 def _large_ws(bank: EmbeddingBank, batch: int) -> torch.Tensor:
@@ -362,18 +364,30 @@ def _large_ws(bank: EmbeddingBank, batch: int) -> torch.Tensor:
 def _backward_large(bank: EmbeddingBank, ids, batch, grad, dx=None, dfm=None, fm_sum=None,
                     x0=None, dw=None):
     """One device-wide plan + ONE update per row for batches beyond a plan
-    workgroup (DIN's B x L history lookups): emb_bwd_large.hip."""
+    workgroup (DIN's B x L history lookups): emb_bwd_large.hip, one call
+    (mrec_emb_bwd_large_fused: the bucketed plan with the updates in the bucket
+    kernel; the plan / apply pair when the batch is too large for it)."""
     ws = _large_ws(bank, batch)
-    _mrec.call("mrec_emb_bwd_large_plan", bank.desc().ref(), _ids_desc(ids).ref(), batch,
-               ws.data_ptr(), ws.numel(), None, _mrec.stream_handle())
     mode, lr = bank.apply_mode()
-    _mrec.call("mrec_emb_bwd_large_apply", bank.desc().ref(), batch, ws.data_ptr(), ws.numel(),
-               _mrec.ptr(dx), _mrec.dtype_code(dx.dtype) if dx is not None else _mrec.F32,
-               dx.stride(0) if dx is not None else 0, _mrec.ptr(dfm), _mrec.ptr(fm_sum),
-               _mrec.ptr(x0), _mrec.dtype_code(x0.dtype) if x0 is not None else _mrec.F32,
-               x0.stride(0) if x0 is not None else 0, _mrec.ptr(dw), mode, float(lr),
-               bank.next_seed(), bank.step_counter().data_ptr(), _mrec.ptr(grad),
-               _mrec.stream_handle())
+    if not LARGE_FUSED:
+        _mrec.call("mrec_emb_bwd_large_plan", bank.desc().ref(), _ids_desc(ids).ref(), batch,
+                   ws.data_ptr(), ws.numel(), None, _mrec.stream_handle())
+        _mrec.call("mrec_emb_bwd_large_apply", bank.desc().ref(), batch, ws.data_ptr(),
+                   ws.numel(), *_large_apply_args(bank, grad, dx, dfm, fm_sum, x0, dw, mode, lr))
+        return
+    _mrec.call("mrec_emb_bwd_large_fused", bank.desc().ref(), _ids_desc(ids).ref(), batch,
+               ws.data_ptr(), ws.numel(), None,
+               *_large_apply_args(bank, grad, dx, dfm, fm_sum, x0, dw, mode, lr))
+
+
+def _large_apply_args(bank, grad, dx, dfm, fm_sum, x0, dw, mode, lr):
+    """The apply arguments of mrec_emb_bwd_large_apply / _fused after the workspace."""
+    return (_mrec.ptr(dx), _mrec.dtype_code(dx.dtype) if dx is not None else _mrec.F32,
+            dx.stride(0) if dx is not None else 0, _mrec.ptr(dfm), _mrec.ptr(fm_sum),
+            _mrec.ptr(x0), _mrec.dtype_code(x0.dtype) if x0 is not None else _mrec.F32,
+            x0.stride(0) if x0 is not None else 0, _mrec.ptr(dw), mode, float(lr),
+            bank.next_seed(), bank.step_counter().data_ptr(), _mrec.ptr(grad),
+            _mrec.stream_handle())
 
 
 def _backward_into_bank(bank: EmbeddingBank, ids, batch, plan_ws, dx=None, dfm=None,

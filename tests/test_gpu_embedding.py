@@ -415,6 +415,47 @@ def test_backward_large_batch_dense_grad(gpu, B, nums):
         assert np.all(err <= 2 ** -24 * np.abs(want[hot]) + 1e-12 * mag[hot] + 1e-30), f
 
 
+@pytest.mark.parametrize("B,hot", [(20000, 0.3), (150000, 0.7)])
+@pytest.mark.parametrize("update", ["dense", "sgd"])
+def test_bucketed_plan_matches_atomic_plan(gpu, B, hot, update, monkeypatch):
+    """Batches of <= 2M lookups take the bucketed plan (lookups partitioned by a hash
+    of their row, one workgroup per bucket groups its rows in LDS), fused with the
+    updates (mrec_emb_bwd_large_fused) or as the plan / apply pair.  Every path sums
+    a row's lookups with the same arithmetic (ascending sample order up to 16,
+    order-free fixed point beyond), so the results are bitwise those of the atomic
+    plan (MREC_LG_ATOMIC_PLAN=1) -- also across many chunks (B=150000: 37 chunks)
+    and for a row hit > 2^16 times (2048+: the chunked kernels)."""
+    from pytorchrec_amd import embedding as E
+    rng = np.random.default_rng(B)
+    nums, D = [63002, 802], 16
+    ids_np = np.stack([rng.integers(0, n, B) for n in nums], 1)
+    ids_np[rng.random(B) < hot, 0] = 0
+    ids = [torch.from_numpy(ids_np[:, f].astype(np.int32)).to(gpu) for f in range(2)]
+    dy = torch.from_numpy((rng.standard_normal((B, 2 * D)) * 1e-3).astype(np.float32)).to(gpu)
+    dtype = torch.float32 if update == "dense" else torch.bfloat16
+    tabs = [(rng.standard_normal((n, D)) * 0.1).astype(np.float32) for n in nums]
+    got = {}
+    for path in ("fused", "pair", "atomic"):
+        monkeypatch.setattr(E, "LARGE_FUSED", path == "fused")
+        if path == "atomic":
+            monkeypatch.setenv("MREC_LG_ATOMIC_PLAN", "1")
+        bank = _bank(nums, D, False, dtype, update=update)
+        if update == "sgd":
+            bank.use_fused_sgd(0.5)
+            bank.stochastic_rounding = False
+        _fill(bank, tabs)
+        E.gather(bank, ids, out_dtype=torch.float32).backward(dy)
+        res = bank.weight.grad if update == "dense" else bank.weight
+        got[path] = _bits(res[:, :D])
+    monkeypatch.delenv("MREC_LG_ATOMIC_PLAN")
+    assert (ids_np[:, 0] == 0).sum() > (1 << 16) or B < 100000
+    assert np.array_equal(got["fused"], got["atomic"])
+    assert np.array_equal(got["pair"], got["atomic"])
+    if update == "dense":
+        want = ref.dense_grad(nums[0], ids_np[:, 0], dy[:, :D].cpu().numpy().astype(np.float64))
+        assert np.allclose(got["fused"].view(np.float32)[:nums[0]], want, rtol=1e-5, atol=1e-7)
+
+
 def test_backward_large_batch_sgd_one_update_per_row(gpu):
     """Fused SGD at B > MREC_BWD_MAX_BATCH updates every touched row exactly once:
     new = RNE_bf16(old - lr * sum g), equal to the fp64 oracle's sum rounded once

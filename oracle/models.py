@@ -176,8 +176,11 @@ def criteo_batch(category_nums, batch: int, n_dense: int = 13, seed: int = 0, zi
     import numpy as np
     F = len(category_nums)
     rng = np.random.default_rng(seed)
-    if zipf:
-        ids = np.stack([np.minimum(rng.zipf(zipf, batch) - 1, n - 1) for n in category_nums], 1)
+    if zipf:  # truncated Zipf over each table's rows (inverse CDF), as bench.zipf_ids
+        def trunc(n):
+            cdf = np.cumsum(np.arange(1, n + 1, dtype=np.float64) ** -zipf)
+            return np.minimum(np.searchsorted(cdf / cdf[-1], rng.random(batch), side="right"), n - 1)
+        ids = np.stack([trunc(n) for n in category_nums], 1)
     else:
         ids = np.stack([rng.integers(0, n, batch) for n in category_nums], 1)
     dense = np.random.default_rng(seed + 2).random((batch, n_dense), dtype=np.float32)

@@ -219,6 +219,13 @@ __global__ __launch_bounds__(kPlanThreads) void plan_hash_kernel(BankArgs bank, 
 // workgroups of the apply launch: independent of the embedding update, and a
 // launch of their own would cost a kernel boundary on the step's serial path
 constexpr int kMaxCoReduce = 4;
+// hot segments (> short_seg lookups) of a (table, bucket) are spread over kHotPer
+// workgroups of their own (segment k by workgroup k % kHotPer), so a bucket's hot
+// rows are summed in parallel instead of one after another by its segment block
+#ifndef MREC_HOT_PER
+#define MREC_HOT_PER 4
+#endif
+constexpr int kHotPer = MREC_HOT_PER;
 struct CoReduce {
   int n;
   int nblk[kMaxCoReduce];
@@ -244,8 +251,10 @@ template <typename T, int LPR>
 struct HotSeg {
   static constexpr int EPL = Vec<T>::EPL;
   static constexpr int WPB = 256 / LPR;
+  static constexpr int kHotChunk = 1024;  // ranks expanded per pass (a multiple of WPB)
   uint32_t bits[kHashMaxEntries / 32];
   uint32_t pre[kHashMaxEntries / 32];
+  int32_t srt[kHotChunk];
   float red[4][LPR * EPL];
   uint32_t wsum[4];
 
@@ -283,25 +292,52 @@ struct HotSeg {
     float acc[EPL];
 #pragma unroll
     for (int j = 0; j < EPL; ++j) acc[j] = 0.f;
-    if (live) {
+    // ranks -> samples, kHotChunk ranks at a time: thread t expands its bitmap word
+    // into srt[rank - c0]; worker w then takes ranks w, w + WPB, ... (ascending, as
+    // always), KB of them per round with every gradient load issued first
+#ifndef MREC_HOT_KB
+#define MREC_HOT_KB 2
+#endif
+    constexpr int KB = MREC_HOT_KB;
 #pragma unroll 1
-      for (int i = worker; i < sn; i += WPB) {
-        int lo = 0, hi = nwords - 1;  // last word with pre <= i
-        while (lo < hi) {
-          const int mid = (lo + hi + 1) >> 1;
-          if (static_cast<int>(pre[mid]) <= i) lo = mid; else hi = mid - 1;
+    for (int c0 = 0; c0 < sn; c0 += kHotChunk) {
+      if (tid < nwords) {
+        uint32_t wb = bits[tid];
+        int r = static_cast<int>(pre[tid]);
+        while (wb && r < c0 + kHotChunk) {
+          if (r >= c0) srt[r - c0] = tid * 32 + __ffs(wb) - 1;
+          wb &= wb - 1;
+          ++r;
         }
-        uint32_t w = bits[lo];
-        for (int k = i - static_cast<int>(pre[lo]); k > 0; --k) w &= w - 1;
-        const int b = lo * 32 + __ffs(w) - 1;
-        float g[EPL];
-        if constexpr (ROW_V)
-          lookup_grad_v<EPL>(a, b, f, D, e0, v_lane, w_lane, v, g);
-        else
-          lookup_grad<EPL>(a, b, f, D, e0, v_lane, w_lane, g);
-#pragma unroll
-        for (int j = 0; j < EPL; ++j) acc[j] += g[j];
       }
+      __syncthreads();
+      const int c1 = min(sn, c0 + kHotChunk);
+      if (live) {
+#pragma unroll 1
+        for (int i0 = c0 + worker; i0 < c1; i0 += WPB * KB) {
+          int bs[KB];
+#pragma unroll
+          for (int u = 0; u < KB; ++u) {
+            const int i = i0 + u * WPB;
+            bs[u] = i < c1 ? srt[i - c0] : -1;
+          }
+          float g[KB][EPL];
+#pragma unroll
+          for (int u = 0; u < KB; ++u) {
+            const int b = bs[u] < 0 ? bs[0] : bs[u];  // (a repeat of a valid one; not added)
+            if constexpr (ROW_V)
+              lookup_grad_v<EPL>(a, b, f, D, e0, v_lane, w_lane, v, g[u]);
+            else
+              lookup_grad<EPL>(a, b, f, D, e0, v_lane, w_lane, g[u]);
+          }
+#pragma unroll
+          for (int u = 0; u < KB; ++u)
+            if (bs[u] >= 0)
+#pragma unroll
+              for (int j = 0; j < EPL; ++j) acc[j] += g[u][j];
+        }
+      }
+      __syncthreads();  // srt is rewritten by the next chunk
     }
 #pragma unroll
     for (int off = LPR; off < 64; off <<= 1)
@@ -425,7 +461,7 @@ __global__ __launch_bounds__(256, MREC_APPLY_WAVES) void apply_hash_kernel(BankA
   // embedding update, they start first instead of trailing it
 #if MREC_APPLY_EXP == 13  // (diagnostic: reductions trailing the apply blocks)
   const int co_blocks = 0;
-  if (static_cast<int>(blockIdx.x) >= seg_blocks + sm_blocks) {
+  if (static_cast<int>(blockIdx.x) >= seg_blocks * (1 + kHotPer) + sm_blocks) {
     co_reduce(co, blockIdx.x - seg_blocks - sm_blocks);
     return;
   }
@@ -470,13 +506,21 @@ __global__ __launch_bounds__(256, MREC_APPLY_WAVES) void apply_hash_kernel(BankA
           apply_segment<T, LPR, MODE>(bank, a, t, f, toff_f, d, l, e0, v_lane, w_lane, live);
       }
     }
-    if (nl == 0) return;  // uniform
+    return;
+  }
+  if (blk < seg_blocks * (1 + kHotPer)) {  // uniform: hot segments k = h, h + kHotPer, ...
 #if MREC_APPLY_EXP == 10
     return;
 #endif
-    __syncthreads();
+    const int q = blk - seg_blocks;
+    const int fr = q / kHotPer, h = q - fr * kHotPer;
+    const int f = fr / kPlanBuckets, r = fr - f * kPlanBuckets;
+    const BucketWs t = bucket_ws(ws, f, r, B);
+    const int nl = t.hdr[2];
+    if (h >= nl) return;  // uniform
+    const int64_t toff_f = bank.row_offset[f];
     __shared__ HotSeg<T, LPR> hot;
-    for (int k = 0; k < nl; ++k) {
+    for (int k = h; k < nl; k += kHotPer) {
       const int4 d = t.desc[t.longl[k]];
       float v[EPL];
 #pragma unroll
@@ -496,7 +540,7 @@ __global__ __launch_bounds__(256, MREC_APPLY_WAVES) void apply_hash_kernel(BankA
   }
 
   // a row hit once: one lookup, one update
-  const int64_t q = static_cast<int64_t>(blk - seg_blocks) * WPB + worker;
+  const int64_t q = static_cast<int64_t>(blk - seg_blocks * (1 + kHotPer)) * WPB + worker;
   if (q >= B * F) return;  // whole workers
   const bool rowwise = MODE < 0 && a.mode == MREC_BWD_ROWWISE_ADAGRAD;
   if (!live && !rowwise) return;
@@ -905,7 +949,8 @@ static mrec_status apply_impl(const mrec_table_bank *bank, int64_t batch, const 
                               : static_cast<int>((batch + wpb - 1) / wpb);
   const int64_t sm_blocks = hash ? (batch * F + wpb - 1) / wpb : 0;
   const int apply_blocks =
-      static_cast<int>(hash ? seg_blocks + sm_blocks : static_cast<int64_t>(seg_blocks) * F);
+      static_cast<int>(hash ? seg_blocks * (1 + kHotPer) + sm_blocks
+                           : static_cast<int64_t>(seg_blocks) * F);
   CoReduce co = {};
   int co_blocks = 0;
   MREC_CHECK_ARG(n_reduce >= 0 && n_reduce <= kMaxCoReduce && (n_reduce == 0 || reduce),

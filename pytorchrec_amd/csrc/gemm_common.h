@@ -177,14 +177,21 @@ __device__ __forceinline__ void splitk_reduce_body(const GemmArgs &g, int64_t bi
   const int64_t M4 = blk4 ? g.M / 4 * 4 : 0;
   const int64_t N4 = blk4 ? g.N / 4 : 0;  // whole column fours inside W
   if (blk4) {
+    // one row of a block per lane (4 lanes per block: a quarter of the dependent slab
+    // loads per thread), the block gathered by the first of the 4 lanes
     const int64_t tot4 = (M4 / 4) * N4;
-    for (int64_t i = bid * 256 + threadIdx.x; i < tot4; i += nblk * 256) {
-      const int64_t m0 = (i / N4) * 4, n = (i % N4) * 4;
+    const int base = (threadIdx.x & 63) & ~3;
+    for (int64_t i = bid * 256 + threadIdx.x; i < tot4 * 4; i += nblk * 256) {
+      const int64_t j = i >> 2;
+      const int r = static_cast<int>(i & 3);
+      const int64_t m0 = (j / N4) * 4, n = (j % N4) * 4;
+      const float4 mine = splitk_sum4<DEEP>(g.ws + (m0 + r) * g.ldws + n, slab, g.split_k);
       float4 v[4];
 #pragma unroll
-      for (int r = 0; r < 4; ++r)
-        v[r] = splitk_sum4<DEEP>(g.ws + (m0 + r) * g.ldws + n, slab, g.split_k);
-      update_block4_tower(g, m0, n, v);
+      for (int rr = 0; rr < 4; ++rr)
+        v[rr] = make_float4(__shfl(mine.x, base + rr), __shfl(mine.y, base + rr),
+                            __shfl(mine.z, base + rr), __shfl(mine.w, base + rr));
+      if (r == 0) update_block4_tower(g, m0, n, v);
     }
   }
   const int64_t total = g.M * q;

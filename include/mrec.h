@@ -32,7 +32,7 @@
 extern "C" {
 #endif
 
-#define MREC_ABI_VERSION 20
+#define MREC_ABI_VERSION 21
 #define MREC_MAX_TABLES 64      /* tables per table bank / per call */
 #define MREC_BWD_MAX_BATCH 8192  /* lookups per table per plan/apply call */
 #define MREC_BWD_HASH_MAX_BATCH 4096  /* batches up to this use the hash plan */
@@ -465,10 +465,13 @@ mrec_status mrec_shard_bucketize_dedup(const mrec_ids *ids, int32_t n_tables, co
                                        int32_t *d_oob_flag, mrec_stream stream);
 /* bytes of one wire record: round4((dim + has_w) * element bytes) */
 int32_t mrec_shard_wire_bytes(int32_t dim, int32_t has_w, mrec_dtype dtype);
-/* owner: rows of the received ids (header = recv_ids) -> wire (no lazy-Adam banks) */
+/* owner: rows of the received ids (header = recv_ids) -> wire (no lazy-Adam banks);
+ * plan (may be NULL, ABI 21): the owner's backward hash plan over the same received
+ * ids (an exchange view, mrec_plan_job) run by leading workgroups of this launch */
 mrec_status mrec_shard_gather_wire(const mrec_table_bank *local, const int32_t *recv_ids,
                                    int32_t world, int32_t cap, int32_t cap_rows, void *wire,
-                                   int32_t *d_overflow, mrec_stream stream);
+                                   int32_t *d_overflow, const mrec_plan_job *plan,
+                                   mrec_stream stream);
 /* wire records -> slot rows [(p * n_tables + f) * cap + j] (pitch slot_bytes; to_f32:
  * bf16 records widened to fp32); zero (may be NULL): zero_bytes of the same rows of a
  * second buffer are cleared (the sender's gradient sums) */

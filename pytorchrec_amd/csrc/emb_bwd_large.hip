@@ -1222,11 +1222,19 @@ static mrec_status lg_apply_args(const mrec_table_bank *bank, const BankArgs &ba
 template <typename T, int L>
 static void lg_launch_apply(const BankArgs &ba, int64_t batch, const LgWs &w, const ApplyArgs &a,
                             int stride, int fused_nb, int G, int lognb, hipStream_t s) {
-  if (fused_nb) bk_apply_kernel<T, L><<<dim3(fused_nb), 256, 0, s>>>(ba, w, a, G, lognb);
-  const dim3 g(kLgApplyBlocks);
-  lg_longmax_kernel<T, L><<<g, 256, 0, s>>>(ba, batch, w, a);
-  lg_longacc_kernel<T, L><<<g, 256, 0, s>>>(ba, batch, w, a, stride);
-  lg_apply_kernel<T, L><<<g, 256, 0, s>>>(ba, batch, w, a, stride);
+  dim3 gc(kLgApplyBlocks), gu(kLgApplyBlocks);
+  if (fused_nb) {
+    bk_apply_kernel<T, L><<<dim3(fused_nb), 256, 0, s>>>(ba, w, a, G, lognb);
+    // only huge segments are left: as many workgroups as their slots (mostly holes)
+    const int64_t N = batch * ba.n_tables;
+    const int64_t ul = (N + kLgHuge) / (kLgHuge + 1) + 1;
+    const int64_t cc = ul + (N + kLgChunk - 1) / kLgChunk + 2;
+    gc = dim3(static_cast<unsigned>(std::min<int64_t>(cc, kLgApplyBlocks)));
+    gu = dim3(static_cast<unsigned>(std::min<int64_t>((ul + 256 / L - 1) / (256 / L), kLgApplyBlocks)));
+  }
+  lg_longmax_kernel<T, L><<<gc, 256, 0, s>>>(ba, batch, w, a);
+  lg_longacc_kernel<T, L><<<gc, 256, 0, s>>>(ba, batch, w, a, stride);
+  lg_apply_kernel<T, L><<<gu, 256, 0, s>>>(ba, batch, w, a, stride);
 }
 
 static void lg_dispatch_apply(mrec_dtype dtype, int lpr, const BankArgs &ba, int64_t batch,

@@ -14,6 +14,7 @@
 #include <algorithm>
 
 #include "common.h"
+#include "emb_plan.h"
 
 namespace mrec {
 
@@ -156,7 +157,7 @@ __global__ __launch_bounds__(kBT) void bucketize_kernel(IdsArgs ids, RowsArg row
 // (the header every wire kernel reads).
 // ---------------------------------------------------------------------------
 
-constexpr uint32_t kEmpty = 0xffffffffu;
+// (kEmpty: emb_plan.h)
 
 __device__ __forceinline__ uint32_t id_hash(uint32_t x, uint32_t mask) {
   return (x * 2654435761u) & mask;
@@ -283,8 +284,8 @@ __global__ __launch_bounds__(kBT) void bucketize_dedup_kernel(IdsArgs ids, RowsA
 // binary search of the part's count prefix, kept in LDS.
 // ---------------------------------------------------------------------------
 
-constexpr int kWireThreads = 256;
-constexpr int kWirePer = 8;  // elements per thread
+constexpr int kWireThreads = 1024;
+constexpr int kWirePer = 2;  // elements per thread
 constexpr int kWireElems = kWireThreads * kWirePer;
 
 struct WireArgs {
@@ -332,20 +333,35 @@ __device__ __forceinline__ int wire_table(const int *pre, int F, int r) {
   return lo;
 }
 
-// owner: local bank rows of part p's received ids -> wire records (grid: chunks x W)
+// owner: local bank rows of part p's received ids -> wire records (grid: chunks x W,
+// flattened: blockIdx.x = p * chunks + chunk after `plan_blocks` leading workgroups
+// that run the owner's backward hash plan over the same received ids, PLAN)
+template <bool PLAN>
 __global__ __launch_bounds__(kWireThreads) void gather_wire_kernel(BankArgs bank, WireArgs w,
                                                                    const int32_t *__restrict__ recv,
-                                                                   uint32_t *__restrict__ wire) {
+                                                                   uint32_t *__restrict__ wire,
+                                                                   int chunks, PlanJob plan,
+                                                                   int plan_blocks) {
+  if constexpr (PLAN) {
+    if (static_cast<int>(blockIdx.x) < plan_blocks) {  // uniform: (table, bucket) plans
+      __shared__ __attribute__((aligned(16))) uint32_t smem[2 * kHashSlots + 2];
+      plan_hash_body<kWireThreads, kHashSlots>(plan.bank, plan.ids, plan.B, plan.ws, plan.oob,
+                                               plan.d_step, blockIdx.x / kPlanBuckets,
+                                               blockIdx.x % kPlanBuckets, smem);
+      return;
+    }
+  }
   __shared__ int pre[MREC_MAX_TABLES + 1];
   __shared__ int64_t roff[MREC_MAX_TABLES], nrows[MREC_MAX_TABLES];
-  const int p = blockIdx.y;
+  const int gb = static_cast<int>(blockIdx.x) - (PLAN ? plan_blocks : 0);
+  const int p = gb / chunks, cx = gb - p * chunks;
   if (threadIdx.x < w.F) {
     roff[threadIdx.x] = bank.row_offset[threadIdx.x];
     nrows[threadIdx.x] = bank.rows[threadIdx.x];
   }
   const int tot = wire_prefix(w, p, pre);  // (its barrier covers roff / nrows too)
   const int64_t n = static_cast<int64_t>(tot) * w.rec_dw;
-  const int64_t e0 = static_cast<int64_t>(blockIdx.x) * kWireElems + threadIdx.x;
+  const int64_t e0 = static_cast<int64_t>(cx) * kWireElems + threadIdx.x;
   if (e0 - threadIdx.x >= n) return;
   const int32_t *ids = recv + static_cast<int64_t>(p) * (static_cast<int64_t>(w.F) * w.cap + w.F);
   const uint32_t *data = reinterpret_cast<const uint32_t *>(bank.data);
@@ -710,7 +726,8 @@ static mrec_status wire_args(const int32_t *hdr, int32_t world, int32_t n_tables
 
 mrec_status mrec_shard_gather_wire(const mrec_table_bank *local, const int32_t *recv_ids,
                                    int32_t world, int32_t cap, int32_t cap_rows, void *wire,
-                                   int32_t *d_overflow, mrec_stream stream) {
+                                   int32_t *d_overflow, const mrec_plan_job *plan,
+                                   mrec_stream stream) {
   BankArgs ba;
   int eb, lpr;
   mrec_status st = make_bank_args(local, &ba, &eb, &lpr);
@@ -724,9 +741,24 @@ mrec_status mrec_shard_gather_wire(const mrec_table_bank *local, const int32_t *
   WireArgs w;
   st = wire_args(recv_ids, world, ba.n_tables, cap, cap_rows, rec, d_overflow, &w);
   if (st != MREC_OK) return st;
-  gather_wire_kernel<<<wire_grid(w, w.rec_dw), kWireThreads, 0,
-                       static_cast<hipStream_t>(stream)>>>(ba, w, recv_ids,
-                                                           static_cast<uint32_t *>(wire));
+  const dim3 g = wire_grid(w, w.rec_dw);
+  const int chunks = static_cast<int>(g.x);
+  PlanJob job{};
+  int pb = 0;
+  if (plan) {
+    if ((st = build_plan_job(plan, &job)) != MREC_OK) return st;
+    pb = job.bank.n_tables * kPlanBuckets;
+  }
+  const dim3 gf(static_cast<unsigned>(pb + chunks * world));
+  hipStream_t s = static_cast<hipStream_t>(stream);
+  if (plan)
+    gather_wire_kernel<true><<<gf, kWireThreads, 0, s>>>(ba, w, recv_ids,
+                                                         static_cast<uint32_t *>(wire), chunks,
+                                                         job, pb);
+  else
+    gather_wire_kernel<false><<<gf, kWireThreads, 0, s>>>(ba, w, recv_ids,
+                                                          static_cast<uint32_t *>(wire), chunks,
+                                                          job, 0);
   return launch_status("mrec_shard_gather_wire");
 }
 

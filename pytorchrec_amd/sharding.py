@@ -413,13 +413,17 @@ def shard_bucketize_dedup(bank: ShardedEmbeddingBank, ids: Sequence[torch.Tensor
     return send, pos
 
 
-def shard_gather_wire(bank: ShardedEmbeddingBank, recv_ids: torch.Tensor) -> torch.Tensor:
-    """Owner: one record per received distinct id -> [W, cap_rows * record] bytes."""
+def shard_gather_wire(bank: ShardedEmbeddingBank, recv_ids: torch.Tensor,
+                      plan_job=None) -> torch.Tensor:
+    """Owner: one record per received distinct id -> [W, cap_rows * record] bytes.
+    ``plan_job`` (owner_plan_job) runs the owner's backward plan over the same ids in
+    leading workgroups of the launch."""
     W, rb = bank.world, bank.wire_bytes()
     wire = torch.empty(W, bank.cap_rows * rb, dtype=torch.uint8, device=bank.weight.device)
     fl = bank.flags()
     _mrec.call("mrec_shard_gather_wire", bank.desc().ref(), recv_ids.data_ptr(), W, bank.cap,
-               bank.cap_rows, wire.data_ptr(), fl.data_ptr(), _mrec.stream_handle())
+               bank.cap_rows, wire.data_ptr(), fl.data_ptr(),
+               ctypes.byref(plan_job) if plan_job is not None else None, _mrec.stream_handle())
     return wire
 
 
@@ -627,10 +631,15 @@ class _CompactInteractFn(torch.autograd.Function):
         comm = bank.comm
         send, pos = shard_bucketize_dedup(bank, ids)
         recv = comm.exchange(send)
-        wire = comm.exchange(shard_gather_wire(bank, recv))
+        train = trigger is not None
+        # the owner's backward plan rides in the gather launch (same received ids)
+        ojob_ok = train and bank.world * bank.cap <= _mrec.BWD_MAX_BATCH
+        ojob, oplan, okeep = (owner_plan_job(bank, recv, bank.part) if ojob_ok
+                              else (None, None, None))
+        wire = comm.exchange(shard_gather_wire(bank, recv, plan_job=ojob))
+        del okeep
         n = bank.world * bank.n_tables * bank.cap
         rows_recv = torch.empty(n, bank.row_stride, dtype=bank.weight.dtype, device=dev)
-        train = trigger is not None
         gsum = torch.empty_like(rows_recv) if train else None
         shard_wire_unpack(bank, wire, send, rows_recv, zero=gsum)
         fuse = train and B <= _mrec.BWD_HASH_MAX_BATCH
@@ -641,7 +650,8 @@ class _CompactInteractFn(torch.autograd.Function):
         del keep
         if train and not fuse:
             splan = sender_plan(bank, rows_recv, pos)
-        oplan = owner_plan(bank, recv, bank.part) if train else None
+        if train and oplan is None:
+            oplan = owner_plan(bank, recv, bank.part)
         if bank.check_ids:
             bank.check_flags()
         ctx.bank, ctx.B = bank, B

@@ -447,3 +447,103 @@ def test_compact_exchange_simulated_bit_exact(gpu, W, zipf, B):
     slot = W * F * banks[0].cap * banks[0].row_stride * 2
     assert compact < slot
 
+
+
+def test_c5_sized_tables_compact_exchange_w8(gpu):
+    """C5's 100,000,000-row tables on the row-sharded path: W = 8
+    ranks simulated in one process, 2 tables x 1e8 rows (each rank's shard 12.5 M
+    rows per table, byte offsets past 2^31), B = 4096 uniform ids per rank over the
+    whole range plus the last rows.  Compact exchange: every record the sender
+    unpacks is bit-exactly the owner's row; the senders' per-slot gradient sums
+    (dx only) equal the fp32 sum of the rank's lookups in ascending sample order,
+    rounded once to bf16; the owners' fused SGD moves each touched row to
+    w - lr * (rank-order fp32 sum of those) within one bf16 ulp."""
+    from pytorchrec_amd import sharding as S
+    W, B, R, F = 8, 4096, 100_000_000, 2
+    rows_g = [R, R]
+    banks = []
+    for r in range(W):
+        b = S.ShardedEmbeddingBank(rows_g, D, S.ShardComm(world=W, rank=r), with_first_order=True,
+                                   dtype=torch.bfloat16, max_batch=B, device=gpu)
+        with torch.no_grad():
+            b.weight.copy_(torch.randn(b.weight.shape, device=gpu,
+                                       generator=torch.Generator(device=gpu).manual_seed(r)))
+        b.stochastic_rounding = False
+        assert b.use_compact(B)
+        banks.append(b)
+    g = torch.Generator().manual_seed(5)
+    ids = []
+    for r in range(W):
+        t = [torch.randint(0, R, (B,), generator=g, dtype=torch.int32) for _ in range(F)]
+        t[0][:W] = torch.arange(R - W, R, dtype=torch.int32)  # the last row of every shard
+        ids.append([x.to(gpu) for x in t])
+    sends, poss = zip(*[S.shard_bucketize_dedup(banks[r], ids[r]) for r in range(W)])
+    recvs = _exchange(list(sends), W)
+    ojobs = [S.owner_plan_job(banks[r], recvs[r], banks[r].part) for r in range(W)]
+    wires = _exchange([S.shard_gather_wire(banks[r], recvs[r], plan_job=ojobs[r][0])
+                       for r in range(W)], W)
+    n = W * F * banks[0].cap
+    rows, gsums = [], []
+    for r in range(W):
+        rr = torch.empty(n, banks[r].row_stride, dtype=torch.bfloat16, device=gpu)
+        gs = torch.empty_like(rr)
+        S.shard_wire_unpack(banks[r], wires[r], sends[r], rr, zero=gs)
+        rows.append(rr)
+        gsums.append(gs)
+        banks[r].check_flags()
+        for f in range(F):
+            idl = ids[r][f].long()
+            own, loc = idl % W, idl // W
+            want = torch.empty(B, D + 1, dtype=torch.bfloat16, device=gpu)
+            for o in range(W):
+                m = own == o
+                want[m] = banks[o].weight[banks[o].row_offset[f] + loc[m], :D + 1]
+            assert torch.equal(rows[r][poss[r][f].long(), :D + 1], want), (r, f)
+    # backward: dx only (gradient of lookup (b, f) = dx0[b, 16 f .. 16 f + 16], w: 0)
+    x0_cols = F * D
+    dx0 = [torch.randn(B, x0_cols, device=gpu).to(torch.bfloat16) for _ in range(W)]
+    tot = {}  # global (f, id) -> fp32 rank-order sum of the ranks' bf16 sums
+    for r in range(W):
+        plan = S.sender_plan(banks[r], rows[r], poss[r])
+        S.sender_grad_sums(banks[r], rows[r], poss[r], plan, gsums[r], dx=dx0[r])
+        dxr = dx0[r].float().cpu().numpy()
+        for f in range(F):
+            idr = ids[r][f].cpu().numpy()
+            order = np.argsort(idr, kind="stable")
+            uniq, start = np.unique(idr[order], return_index=True)
+            ends = np.append(start[1:], len(order))
+            pos_r = poss[r][f].cpu().numpy()
+            got = gsums[r][torch.from_numpy(pos_r[order[start]]).long().to(gpu), :D].float().cpu().numpy()
+            for k, (s0, s1) in enumerate(zip(start, ends)):
+                acc = np.zeros(D, np.float32)
+                for b in order[s0:s1]:  # ascending sample order
+                    acc += dxr[b, f * D:(f + 1) * D]
+                want = torch.from_numpy(acc).to(torch.bfloat16).float().numpy()
+                assert np.array_equal(got[k], want), (r, f, uniq[k])
+                key = (f, int(uniq[k]))
+                tot[key] = tot.get(key, np.zeros(D, np.float32)) + want
+    wire_g = _exchange([S.shard_wire_pack(banks[r], gsums[r], sends[r]) for r in range(W)], W)
+    lr = 0.5
+    for r in range(W):
+        g_recv = torch.empty(n, banks[r].g_ld, dtype=torch.float32, device=gpu)
+        S.shard_wire_unpack(banks[r], wire_g[r], recvs[r], g_recv, to_f32=True)
+        before = banks[r].weight.detach().clone()
+        S.owner_apply(banks[r], ojobs[r][1], g_recv, lr)
+        banks[r].check_flags()
+        keys = [k for k in tot if k[1] % W == r]
+        idx = torch.tensor([banks[r].row_offset[f] + i // W for f, i in keys], device=gpu)
+        w0 = before[idx, :D].double()
+        want = w0 - lr * torch.from_numpy(np.stack([tot[k] for k in keys])).double().to(gpu)
+        got = banks[r].weight[idx, :D].double()
+        ulp = torch.from_numpy(np.spacing(np.abs(want.cpu().numpy()).astype(np.float32))
+                               .astype(np.float64)).to(gpu) * 2 ** 16
+        assert bool(((got - want).abs() <= ulp * 1.0001 + 1e-30).all()), r
+        # rows nobody looked up (a sample of them) keep their bits
+        probe = torch.randint(0, banks[r].weight.shape[0], (4096,), device=gpu)
+        touched = torch.zeros(banks[r].weight.shape[0], dtype=torch.bool, device=gpu)
+        touched[idx] = True
+        keep = probe[~touched[probe]]
+        assert torch.equal(banks[r].weight[keep], before[keep]), r
+        del before
+    del banks, rows, gsums
+    torch.cuda.empty_cache()

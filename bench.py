@@ -72,6 +72,12 @@ def parse():
     p.add_argument("--exchange", default="auto", choices=["auto", "compact", "slot"],
                    help="row-sharded exchange: auto = compact at N>1, slot at N=1; compact = "
                         "one record per distinct id even at N=1; slot = one row per lookup")
+    p.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
+                   help="N > 1 collectives: nccl (= RCCL, the measured path) or gloo (a "
+                        "rehearsal of the process-level protocol: eager, staged via host)")
+    p.add_argument("--same-gpu", action="store_true",
+                   help="rehearsal on a one-GPU box: every rank on cuda:0 (needs "
+                        "--dist-backend gloo; RCCL refuses two ranks on one device)")
     p.add_argument("--stub-step", action="store_true",
                    help="launcher check without a GPU: each rank's step is one gloo all-reduce")
     args = p.parse_args()
@@ -688,6 +694,12 @@ def main():
     if args.stub_step:
         return stub_main(args, json_out, world, rank)
     sharded = world > 1 or args.shard
+    if args.same_gpu:
+        if args.dist_backend != "gloo":
+            raise SystemExit("bench.py: --same-gpu needs --dist-backend gloo")
+        local = 0
+    if args.dist_backend == "gloo":
+        args.no_graph = True  # gloo collectives are host-driven: nothing to capture
     if world > 1 or args.force_collectives:
         import torch.distributed as dist
         torch.cuda.set_device(local)
@@ -695,7 +707,10 @@ def main():
         os.environ.setdefault("MASTER_PORT", "29561")
         os.environ.setdefault("RANK", "0")
         os.environ.setdefault("WORLD_SIZE", "1")
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if args.dist_backend == "gloo":
+            dist.init_process_group("gloo")
+        else:
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
     device = torch.device("cuda", local)
     torch.cuda.set_device(device)
 
@@ -832,6 +847,9 @@ def main():
         "config": {"workload": workloads[args.model],
                    "global_batch": args.batch * world, "batch_per_gpu": args.batch,
                    "parallelism": (f"dp{world}+rowshard{world}" if sharded else "single"),
+                   "collectives": (("gloo rehearsal, every rank on one GPU" if args.same_gpu
+                                    else args.dist_backend) if world > 1 or
+                                   args.force_collectives else None),
                    "exchange": (_exchange_desc(model, args) if sharded else None),
                    "hip_graph": not args.no_graph,
                    "steps_per_graph": G if graphs is not None else 0},

@@ -25,6 +25,8 @@
 // B[k .. + 8][n = l % 16]; so every operand buffer is stored "row = output index,
 // contiguous along k" and the reductions over history rows read transposed copies
 // ([feature][row]) written beside the row-major ones.
+#include <cstdlib>
+
 #include "common.h"
 
 namespace mrec {
@@ -55,7 +57,16 @@ struct DinAttArgs {
   int64_t ld_drows;
   float *part;  // [gridDim.x][P] weight-gradient partials
   int64_t P;
+  unsigned long long *stamps;  // diagnostics: workgroup 0's phase clocks (NULL: off)
 };
+
+// diagnostics: s_memtime stamps of workgroup 0 (thread 0) at the backward's phase
+// boundaries, samples 0..5: [0] start, [1] weights staged, then 8 per sample
+#define DA_STAMP(k)                                                   \
+  do {                                                                \
+    if (p.stamps && blockIdx.x == 0 && tid == 0 && (k) < 64)          \
+      p.stamps[(k)] = __builtin_amdgcn_s_memtime();                   \
+  } while (0)
 
 __device__ __forceinline__ da_bf16x8 da_frag(const uint16_t *base, int ld, int r0, int k0,
                                              int lane) {
@@ -321,8 +332,6 @@ __global__ __launch_bounds__(DA_THREADS) void din_att_fwd_kernel(DinAttArgs p) {
   DaRaw cur = {};
   if (blockIdx.x < p.batch) cur = da_load<E, false>(p, blockIdx.x, task, lane);
   for (int64_t b = blockIdx.x; b < p.batch; b += gridDim.x) {
-    DaRaw nxt = {};
-    if (b + gridDim.x < p.batch) nxt = da_load<E, false>(p, b + gridDim.x, task, lane);
     if (task.on) {
       float qv[8], kv[8];
       da_build_x<S, E, false>(p, cur, task, sm, qv, kv);
@@ -331,6 +340,10 @@ __global__ __launch_bounds__(DA_THREADS) void din_att_fwd_kernel(DinAttArgs p) {
     // row tiles skip the MLP (wave-uniform: every wave holds all 64 validity bits)
     const uint64_t vm = __ballot(cur.valid);
     const bool act = 16 * rt < (vm ? 64 - __clzll(vm) : 0);
+    // the next sample's inputs, issued once this sample's are consumed (issued before
+    // the X build, the build's wait covered them too)
+    DaRaw nxt = {};
+    if (b + gridDim.x < p.batch) nxt = da_load<E, false>(p, b + gridDim.x, task, lane);
     __syncthreads();
     {
       da_f32x4 acc[J1];
@@ -436,10 +449,13 @@ __global__ __launch_bounds__(DA_THREADS) void din_att_bwd_kernel(DinAttArgs p) {
   float *sg = sdu + E;       // g_j = du . k_j [64]
   float *sdq = sg + DA_ROWS;  // per-row-tile dq parts [4][E]
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, rt = w >> 1, cg = w & 1;
+  DA_STAMP(0);
   da_zero_lds(da_lds, S::bwd_end * 2);
   __syncthreads();
   da_stage_weights<S, true>(p, sm, sb1, sb2, sw3);
   const DaTask<E> task(tid);
+  int sidx = 0;
+  DA_STAMP(1);
 
   da_f32x4 gw1[NW1], gw2[NW2];
 #pragma unroll
@@ -486,6 +502,7 @@ __global__ __launch_bounds__(DA_THREADS) void din_att_bwd_kernel(DinAttArgs p) {
     const bool act = 16 * rt < nv;
     const int kk = nv > 32 ? 2 : 1;
     __syncthreads();
+    DA_STAMP(2 + 8 * sidx + 0);
     // ---- phase 1: ds (every wave, lane = row), layer 1 -> H1, H1^T ----
     const float gj = sg[lane];
     const float ag = sum_wave(aj * gj);
@@ -510,6 +527,7 @@ __global__ __launch_bounds__(DA_THREADS) void din_att_bwd_kernel(DinAttArgs p) {
       }
     }
     __syncthreads();
+    DA_STAMP(2 + 8 * sidx + 1);
     // ---- phase 2: layer 2, dZ2 = ds w3 relu'(z2) -> dZ2 (over H1), dZ2^T ----
     {
       da_f32x4 acc[J2];
@@ -536,6 +554,7 @@ __global__ __launch_bounds__(DA_THREADS) void din_att_bwd_kernel(DinAttArgs p) {
       }
     }
     __syncthreads();
+    DA_STAMP(2 + 8 * sidx + 2);
     // ---- phase 3: dH1 = dZ2 W2, dZ1 = dH1 relu'(H1) -> dZ1 (over X), dZ1^T; dW2 ----
     {
       da_f32x4 acc[J1];
@@ -582,6 +601,7 @@ __global__ __launch_bounds__(DA_THREADS) void din_att_bwd_kernel(DinAttArgs p) {
       }
     }
     __syncthreads();
+    DA_STAMP(2 + 8 * sidx + 3);
     // ---- phase 4: dX = dZ1 W1 -> d rows (dk per row, dq parts); dW1 ----
     {
       // the wave's X column tiles: blocks q / k / q-k / q*k of column tiles c16 = cg + DA_CG jx
@@ -641,12 +661,15 @@ __global__ __launch_bounds__(DA_THREADS) void din_att_bwd_kernel(DinAttArgs p) {
       }
     }
     __syncthreads();
+    DA_STAMP(2 + 8 * sidx + 4);
     if (tid < E) {
       const float v = bf16_to_f32(p.dtop[b * p.lddt + tid]) + sdq[tid] + sdq[E + tid] +
                       sdq[2 * E + tid] + sdq[3 * E + tid];
       p.drows[b * p.ld_drows + tid] = f32_to_bf16_rne(v);
     }
     cur = nxt;
+    DA_STAMP(2 + 8 * sidx + 5);
+    ++sidx;
   }
 
   // ---- weight-gradient partials of this workgroup ----
@@ -712,20 +735,440 @@ __global__ __launch_bounds__(DA_THREADS) void din_att_bwd_kernel(DinAttArgs p) {
   if (tid == 0) pb3[0] = gb3;
 }
 
-// fixed-order sum of the workgroup partials; grads (flat, P) or SGD in place.
-// Block: 64 columns x 4 slices of the partials (each slice summed in order with 4
-// loads in flight), the 4 slice sums added in slice order.
-__global__ __launch_bounds__(256) void din_att_wgrad_kernel(
+// ---------------------------------------------------------------------------
+// backward, two samples in flight per workgroup (the default): waves 0-3 take one
+// sample, waves 4-7 the next, each wave one 16-row tile of its sample with ALL
+// column tiles.  No transposed copies: the operands whose k runs along history
+// rows (dW1 = dZ1^T X, dW2 = dZ2^T H1) and the weights' transposed uses (dH1 =
+// dZ2 W2, dX = dZ1 W1) are read with ds_read_b64_tr_b16 from the row-major
+// buffers, which leaves LDS for two samples' X / H1 / dZ2 / dZ1.  A wave's layer 1
+// -> layer 2 -> dH1 chain only touches its own rows, so a pair of samples takes 3
+// workgroup barriers (X built; all rows' dZ2 / H1 / dZ1 for the weight gradients;
+// the pair done) where the one-sample kernel took 6 per sample.
+// ---------------------------------------------------------------------------
+template <int E, int H1T, int H1K, int H2T, int H2K>
+struct DaShape2 : DaShape<E, H1T, H1K, H2T, H2K> {
+  using B = DaShape<E, H1T, H1K, H2T, H2K>;
+  static constexpr int LDZ2 = B::H2P + 8;
+  static constexpr int oW1 = 0;                       // W1 [H1P][LDX] (rows >= H1 zero)
+  static constexpr int oW2 = oW1 + B::H1P * B::LDX;   // W2 [H2P][LDH] (rows >= H2 zero)
+  static constexpr int oS = oW2 + B::H2P * B::LDH;    // two slots of:
+  static constexpr int sX = 0;                        //   X [64][LDX]
+  static constexpr int sH1 = sX + DA_ROWS * B::LDX;   //   H1 [64][LDH]
+  static constexpr int sZ2 = sH1 + DA_ROWS * B::LDH;  //   dZ2 [64][LDZ2]
+  static constexpr int sZ1 = sZ2 + DA_ROWS * LDZ2;    //   dZ1 [64][LDH]
+  static constexpr int slot_elems = sZ1 + DA_ROWS * B::LDH;
+  static constexpr int bf_end = oS + 2 * slot_elems;
+  // fp32 tail: b1 [H1N], b2 [H2N], w3 [H2N], then per slot q [E], du [E], g [64], dq [4][E]
+  static constexpr int nslot32 = 2 * E + DA_ROWS + 4 * E;
+  static constexpr int nf32 = B::H1N + 2 * B::H2N + 2 * nslot32;
+  static constexpr size_t bytes = bf_end * 2 + nf32 * 4;
+  // after the loop: column partials [8][H1N + 2 H2N] | b3 [2]
+  static constexpr size_t red_bytes = (8 * (B::H1N + 2 * B::H2N) + 2) * 4;
+  static_assert(red_bytes <= bytes, "the end reduction reuses the workgroup's LDS");
+};
+
+// MFMA operand fragment with k running down the rows of a row-major bf16 buffer:
+// lane l gets column c0 + l % 16, rows r0 + 8 (l / 16) .. + 8 (two
+// ds_read_b64_tr_b16: each 16-lane group addresses 4 rows x 4 column quads)
+__device__ __forceinline__ da_bf16x8 da_frag_tr(const uint16_t *base, int ld, int c0, int r0,
+                                                int lane) {
+  typedef short v4s_t __attribute__((ext_vector_type(4)));
+  typedef __attribute__((address_space(3))) v4s_t lds_v4s_t;
+  const int i = lane & 15, g = lane >> 4;
+  const uint16_t *q = base + (r0 + 8 * g + (i >> 2)) * ld + c0 + 4 * (i & 3);
+  const v4s_t lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4s_t *)(q));
+  const v4s_t hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4s_t *)(q + 4 * ld));
+  return da_bf16x8{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+}
+
+// X rows of one sample, row-major only: [q | k | q - k | q * k] (rows >= L zero)
+template <int E, int LDX>
+__device__ __forceinline__ void da_build_x_rm(const DinAttArgs &p, const DaRaw &raw,
+                                              const DaTask<E> &t, uint16_t *X, float (&qv)[8],
+                                              float (&kv)[8]) {
+  const uint4 qraw = raw.q, kraw = raw.k;
+  const bool real = t.j < p.L;
+  Vec<uint16_t>::to_f32(qraw, qv);
+  Vec<uint16_t>::to_f32(kraw, kv);
+  float d[8], m[8];
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    d[i] = qv[i] - kv[i];
+    m[i] = qv[i] * kv[i];
+  }
+  uint4 dq = make_uint4(pack_bf16x2(d[0], d[1]), pack_bf16x2(d[2], d[3]), pack_bf16x2(d[4], d[5]),
+                        pack_bf16x2(d[6], d[7]));
+  uint4 mq = make_uint4(pack_bf16x2(m[0], m[1]), pack_bf16x2(m[2], m[3]), pack_bf16x2(m[4], m[5]),
+                        pack_bf16x2(m[6], m[7]));
+  uint4 qq = qraw;
+  if (!real) qq = dq = mq = make_uint4(0, 0, 0, 0);
+  uint16_t *x = X + t.j * LDX + t.c;
+  *reinterpret_cast<uint4 *>(x) = qq;
+  *reinterpret_cast<uint4 *>(x + E) = kraw;
+  *reinterpret_cast<uint4 *>(x + 2 * E) = dq;
+  *reinterpret_cast<uint4 *>(x + 3 * E) = mq;
+}
+
+template <int E, int H1T, int H1K, int H2T, int H2K>
+__global__ __launch_bounds__(DA_THREADS) void din_att_bwd2_kernel(DinAttArgs p) {
+  using S = DaShape2<E, H1T, H1K, H2T, H2K>;
+  constexpr int NTX = S::NTX, EC = E / 16, LDX = S::LDX, LDH = S::LDH, LDZ2 = S::LDZ2;
+  constexpr int NWV = DA_THREADS / 64;
+  constexpr int NW1 = (H1T * NTX + NWV - 1) / NWV;  // dW1 tiles per wave (over both slots' rows)
+  constexpr int NW2 = (H2T * H1T + NWV - 1) / NWV;  // dW2 tiles per wave
+  extern __shared__ __attribute__((aligned(16))) char da_lds[];
+  uint16_t *sm = reinterpret_cast<uint16_t *>(da_lds);
+  float *sb1 = reinterpret_cast<float *>(da_lds + S::bf_end * 2);
+  float *sb2 = sb1 + S::H1N;
+  float *sw3 = sb2 + S::H2N;
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, slot = w >> 2, rt = w & 3;
+  float *sq = sw3 + S::H2N + slot * S::nslot32;  // this slot's q [E]
+  float *sdu = sq + E;                           // du [E]
+  float *sg = sdu + E;                           // g_j = du . k_j [64]
+  float *sdq = sg + DA_ROWS;                     // per-row-tile dq parts [4][E]
+  uint16_t *X = sm + S::oS + slot * S::slot_elems + S::sX;
+  uint16_t *Hb = sm + S::oS + slot * S::slot_elems + S::sH1;
+  uint16_t *Z2 = sm + S::oS + slot * S::slot_elems + S::sZ2;
+  uint16_t *Z1 = sm + S::oS + slot * S::slot_elems + S::sZ1;
+  const uint16_t *W1 = sm + S::oW1, *W2 = sm + S::oW2;
+  const uint16_t *slots = sm + S::oS;
+  __shared__ int snv[2];  // per slot: rows up to the last one with a_j != 0
+  DA_STAMP(0);
+  da_zero_lds(da_lds, S::bf_end * 2);
+  __syncthreads();
+  da_stage_weights<S, false>(p, sm, sb1, sb2, sw3);
+  const DaTask<E> task(tid & 255);  // X chunk tasks of this thread's slot
+  int sidx = 0;
+  DA_STAMP(1);
+
+  da_f32x4 gw1[NW1], gw2[NW2];
+#pragma unroll
+  for (int i = 0; i < NW1; ++i) gw1[i] = da_f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int i = 0; i < NW2; ++i) gw2[i] = da_f32x4{0.f, 0.f, 0.f, 0.f};
+  float gb1[H1T], gb2[H2T], gw3[H2T];  // per-lane column partials (column 16 n + lane % 16)
+#pragma unroll
+  for (int n = 0; n < H1T; ++n) gb1[n] = 0.f;
+#pragma unroll
+  for (int n = 0; n < H2T; ++n) gb2[n] = gw3[n] = 0.f;
+  float gb3 = 0.f;
+
+  const int64_t G = gridDim.x;
+  int64_t b = blockIdx.x + G * slot;  // this slot's sample (samples blockIdx + G i: i even / odd)
+  DaRaw cur = {};
+  uint16_t dtq = 0;  // dtop[b, lane] (q part, raw bf16) for the dq tail (waves rt == 0)
+  if (b < p.batch) {
+    cur = da_load<E, true>(p, b, task, lane);
+    if (rt == 0 && lane < E) dtq = p.dtop[b * p.lddt + lane];
+  }
+  // the dq tail of a pair runs in the next iteration (after its first barrier): a
+  // store just before the loop's end made the iteration wait for its write
+  int64_t tb = -1;     // pending tail: this slot's sample
+  uint16_t tdq = 0;
+  for (int64_t b0 = blockIdx.x; b0 < p.batch; b0 += 2 * G, b += 2 * G) {
+    const bool have = b < p.batch;  // uniform per slot (slot 1 may be idle in the last pair)
+    // ---- X, q, du, g_j = du . k_j ----
+    if (task.on) {
+      float qv[8], kv[8], dv[8];
+      da_build_x_rm<E, LDX>(p, cur, task, X, qv, kv);
+      Vec<uint16_t>::to_f32(cur.du, dv);
+      float g = 0.f;
+#pragma unroll
+      for (int i = 0; i < 8; ++i) g = fmaf(dv[i], kv[i], g);
+#pragma unroll
+      for (int off = 1; off < DaTask<E>::CH; off <<= 1) g += __shfl_xor(g, off);
+      if (task.c == 0) sg[task.j] = g;
+      if (task.j == 0) {
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+          sq[task.c + i] = qv[i];
+          sdu[task.c + i] = dv[i];
+        }
+      }
+    }
+    const float aj = cur.a;  // lane = history row (0 when this slot is idle)
+    // the next pair's inputs, issued once this pair's are consumed: loaded at the top
+    // of the iteration they made the X build wait for them (one vmcnt for both)
+    DaRaw nxt = {};
+    uint16_t dtq_n = 0;
+    if (b + 2 * G < p.batch) {
+      nxt = da_load<E, true>(p, b + 2 * G, task, lane);
+      if (rt == 0 && lane < E) dtq_n = p.dtop[(b + 2 * G) * p.lddt + lane];
+    }
+    const uint64_t am = __ballot(aj != 0.f);
+    const int nv = am ? 64 - __clzll(am) : 0;
+    const bool act = 16 * rt < nv;
+    if (rt == 0 && lane == 0) snv[slot] = nv;
+    __syncthreads();
+    DA_STAMP(2 + 8 * sidx + 0);
+    // the weight gradients' k steps per slot: rows past 32 add nothing when no row
+    // there carries a gradient
+    const int kk0 = snv[0] > 32 ? 2 : 1, kk1 = snv[1] > 32 ? 2 : 1;
+    if (tb >= 0 && rt == 0 && lane < E) {  // the previous pair's dq (sdq is rewritten after B2)
+      const float v = bf16_to_f32(tdq) + sdq[lane] + sdq[E + lane] + sdq[2 * E + lane] +
+                      sdq[3 * E + lane];
+      p.drows[tb * p.ld_drows + lane] = f32_to_bf16_rne(v);
+    }
+    // ---- ds; layer 1 -> H1 (own rows) ----
+    const float gj = sg[lane];
+    const float ag = sum_wave(aj * gj);
+    const float dsj = aj * (gj - ag);
+    if (rt == 0) gb3 += sum_wave(dsj);
+    {
+      da_f32x4 acc[H1T];
+#pragma unroll
+      for (int n = 0; n < H1T; ++n) acc[n] = da_f32x4{0.f, 0.f, 0.f, 0.f};
+      if (act) {
+#pragma unroll
+        for (int s = 0; s < S::KT1; ++s) {
+          const da_bf16x8 a = da_frag(X, LDX, 16 * rt, 32 * s, lane);
+#pragma unroll
+          for (int n = 0; n < H1T; ++n) acc[n] = da_mfma(a, da_frag(W1, LDX, 16 * n, 32 * s, lane), acc[n]);
+        }
+      }
+#pragma unroll
+      for (int n = 0; n < H1T; ++n) {
+        const int col = 16 * n + (lane & 15);
+        const float bias = sb1[col];
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const int r = 16 * rt + 4 * (lane >> 4) + i;
+          Hb[r * LDH + col] = f32_to_bf16_rne(fmaxf(acc[n][i] + bias, 0.f));
+        }
+      }
+    }
+    // ---- layer 2, dZ2 = ds w3 relu'(z2) -> dZ2 (own rows) ----
+    {
+      da_f32x4 acc[H2T];
+#pragma unroll
+      for (int n = 0; n < H2T; ++n) acc[n] = da_f32x4{0.f, 0.f, 0.f, 0.f};
+      if (act) {
+#pragma unroll
+        for (int s = 0; s < H1K; ++s) {
+          const da_bf16x8 a = da_frag(Hb, LDH, 16 * rt, 32 * s, lane);
+#pragma unroll
+          for (int n = 0; n < H2T; ++n) acc[n] = da_mfma(a, da_frag(W2, LDH, 16 * n, 32 * s, lane), acc[n]);
+        }
+      }
+#pragma unroll
+      for (int n = 0; n < H2T; ++n) {
+        const int col = 16 * n + (lane & 15);
+        const float bias = sb2[col], wv = sw3[col];
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const int r = 16 * rt + 4 * (lane >> 4) + i;
+          const float dsr = __shfl(dsj, r);
+          const float h2 = fmaxf(acc[n][i] + bias, 0.f);
+          const float dz = h2 > 0.f ? dsr * wv : 0.f;
+          gw3[n] = fmaf(dsr, h2, gw3[n]);
+          gb2[n] += dz;
+          Z2[r * LDZ2 + col] = f32_to_bf16_rne(dz);
+        }
+      }
+    }
+    // ---- dH1 = dZ2 W2, dZ1 = dH1 relu'(H1) -> dZ1 (own rows) ----
+    {
+      da_f32x4 acc[H1T];
+#pragma unroll
+      for (int n = 0; n < H1T; ++n) acc[n] = da_f32x4{0.f, 0.f, 0.f, 0.f};
+      if (act) {
+#pragma unroll
+        for (int s = 0; s < H2K; ++s) {
+          const da_bf16x8 a = da_frag(Z2, LDZ2, 16 * rt, 32 * s, lane);
+#pragma unroll
+          for (int n = 0; n < H1T; ++n)
+            acc[n] = da_mfma(a, da_frag_tr(W2, LDH, 16 * n, 32 * s, lane), acc[n]);
+        }
+      }
+#pragma unroll
+      for (int n = 0; n < H1T; ++n) {
+        const int col = 16 * n + (lane & 15);
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const int r = 16 * rt + 4 * (lane >> 4) + i;
+          const uint16_t h = Hb[r * LDH + col];
+          const float dz = (h != 0 && !(h & 0x8000u)) ? acc[n][i] : 0.f;
+          gb1[n] += dz;
+          Z1[r * LDH + col] = f32_to_bf16_rne(dz);
+        }
+      }
+    }
+    __syncthreads();
+    DA_STAMP(2 + 8 * sidx + 1);
+    // ---- dW2 += dZ2^T H1 over both slots' rows (k = history rows) ----
+#pragma unroll
+    for (int sl = 0; sl < 2; ++sl) {
+      const uint16_t *z2 = slots + sl * S::slot_elems + S::sZ2;
+      const uint16_t *h1 = slots + sl * S::slot_elems + S::sH1;
+      const int kks = sl ? kk1 : kk0;
+#pragma unroll 1
+      for (int s = 0; s < kks; ++s) {
+#pragma unroll
+        for (int i = 0; i < NW2; ++i) {
+          const int t = w + NWV * i;
+          if (t < H2T * H1T) {
+            const int m = t / H1T, n = t - m * H1T;
+            gw2[i] = da_mfma(da_frag_tr(z2, LDZ2, 16 * m, 32 * s, lane),
+                             da_frag_tr(h1, LDH, 16 * n, 32 * s, lane), gw2[i]);
+          }
+        }
+      }
+    }
+    // ---- dX = dZ1 W1 -> d rows (dk per row, dq parts), one 16-column chunk of
+    // q / k / q-k / q*k at a time (registers) ----
+#pragma unroll 1
+    for (int c16 = 0; c16 < EC; ++c16) {
+      da_f32x4 acc[4];
+#pragma unroll
+      for (int blk = 0; blk < 4; ++blk) acc[blk] = da_f32x4{0.f, 0.f, 0.f, 0.f};
+      if (act) {
+#pragma unroll
+        for (int s = 0; s < H1K; ++s) {
+          const da_bf16x8 a = da_frag(Z1, LDH, 16 * rt, 32 * s, lane);
+#pragma unroll
+          for (int blk = 0; blk < 4; ++blk)
+            acc[blk] = da_mfma(a, da_frag_tr(W1, LDX, 16 * (blk * EC + c16), 32 * s, lane), acc[blk]);
+        }
+      }
+      const int e = 16 * c16 + (lane & 15);
+      const float qe = sq[e], due = sdu[e];
+      float dqp = 0.f;
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int r = 16 * rt + 4 * (lane >> 4) + i;
+        const float dfq = acc[0][i], dfk = acc[1][i];
+        const float dfd = acc[2][i], dfm = acc[3][i];
+        const float ke = bf16_to_f32(X[r * LDX + E + e]);
+        const float ar = __shfl(aj, r);
+        const float dk = fmaf(ar, due, dfk - dfd + dfm * qe);
+        if (have && r < p.L)
+          p.drows[(p.batch + b * p.L + r) * p.ld_drows + e] = f32_to_bf16_rne(dk);
+        dqp += dfq + dfd + dfm * ke;
+      }
+      dqp = swap32_sum(swap16_sum(dqp));  // the 4 row groups of column e
+      if (lane < 16) sdq[rt * E + e] = dqp;
+    }
+    // ---- dW1 += dZ1^T X over both slots' rows ----
+#pragma unroll
+    for (int sl = 0; sl < 2; ++sl) {
+      const uint16_t *z1 = slots + sl * S::slot_elems + S::sZ1;
+      const uint16_t *x = slots + sl * S::slot_elems + S::sX;
+      const int kks = sl ? kk1 : kk0;
+#pragma unroll 1
+      for (int s = 0; s < kks; ++s) {
+#pragma unroll
+        for (int i = 0; i < NW1; ++i) {
+          const int t = w + NWV * i;
+          if (t < H1T * NTX) {
+            const int m = t / NTX, n = t - m * NTX;
+            gw1[i] = da_mfma(da_frag_tr(z1, LDH, 16 * m, 32 * s, lane),
+                             da_frag_tr(x, LDX, 16 * n, 32 * s, lane), gw1[i]);
+          }
+        }
+      }
+    }
+    tb = have ? b : -1;
+    tdq = dtq;
+    cur = nxt;
+    dtq = dtq_n;
+    __syncthreads();
+    DA_STAMP(2 + 8 * sidx + 2);
+    ++sidx;
+  }
+  if (tb >= 0 && rt == 0 && lane < E) {  // the last pair's dq
+    const float v = bf16_to_f32(tdq) + sdq[lane] + sdq[E + lane] + sdq[2 * E + lane] +
+                    sdq[3 * E + lane];
+    p.drows[tb * p.ld_drows + lane] = f32_to_bf16_rne(v);
+  }
+
+  // ---- weight-gradient partials of this workgroup ----
+  float *part = p.part + static_cast<int64_t>(blockIdx.x) * p.P;
+  const int E4 = S::E4, H1 = p.H1, H2 = p.H2;
+  float *pw2 = part + H1 * E4, *pb1 = pw2 + H2 * H1, *pb2 = pb1 + H1, *pw3 = pb2 + H2,
+        *pb3 = pw3 + H2;
+#pragma unroll
+  for (int i = 0; i < NW1; ++i) {
+    const int t = w + NWV * i;
+    if (t < H1T * NTX) {
+      const int m = t / NTX, n = t - m * NTX;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int h = 16 * m + 4 * (lane >> 4) + j;
+        if (h < H1) part[h * E4 + 16 * n + (lane & 15)] = gw1[i][j];
+      }
+    }
+  }
+#pragma unroll
+  for (int i = 0; i < NW2; ++i) {
+    const int t = w + NWV * i;
+    if (t < H2T * H1T) {
+      const int m = t / H1T, n = t - m * H1T;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int h2 = 16 * m + 4 * (lane >> 4) + j, h1 = 16 * n + (lane & 15);
+        if (h2 < H2 && h1 < H1) pw2[h2 * H1 + h1] = gw2[i][j];
+      }
+    }
+  }
+  // column partials: the 4 row groups of a lane column, then the 8 (slot, row tile)
+  // waves in fixed order
+  constexpr int RW = S::H1N + 2 * S::H2N;
+  float *red = reinterpret_cast<float *>(da_lds);  // [8][RW] | b3 [2]
+  float *rb3 = red + 8 * RW;
+  __syncthreads();  // the LDS buffers are dead
+#pragma unroll
+  for (int n = 0; n < H1T; ++n) {
+    const float v = swap32_sum(swap16_sum(gb1[n]));
+    if (lane < 16) red[w * RW + 16 * n + lane] = v;
+  }
+#pragma unroll
+  for (int n = 0; n < H2T; ++n) {
+    const float v = swap32_sum(swap16_sum(gb2[n])), u = swap32_sum(swap16_sum(gw3[n]));
+    if (lane < 16) {
+      red[w * RW + S::H1N + 16 * n + lane] = v;
+      red[w * RW + S::H1N + S::H2N + 16 * n + lane] = u;
+    }
+  }
+  if (rt == 0 && lane == 0) rb3[slot] = gb3;
+  __syncthreads();
+  for (int c = tid; c < RW; c += DA_THREADS) {
+    float v = red[c];
+#pragma unroll
+    for (int q = 1; q < 8; ++q) v += red[q * RW + c];
+    if (c < S::H1N) {
+      if (c < H1) pb1[c] = v;
+    } else if (c < S::H1N + S::H2N) {
+      if (c - S::H1N < H2) pb2[c - S::H1N] = v;
+    } else if (c - S::H1N - S::H2N < H2) {
+      pw3[c - S::H1N - S::H2N] = v;
+    }
+  }
+  if (tid == 0) pb3[0] = rb3[0] + rb3[1];
+}
+
+__global__ __launch_bounds__(1024) void din_att_wgrad_kernel(
     const float *__restrict__ part, int parts, int64_t P, int E4, int H1, int H2, float *grads,
     float lr, float *w1, int64_t ldw1, float *b1, float *w2, int64_t ldw2, float *b2, float *w3,
     float *b3) {
-  __shared__ float red[4][64];
+  // 16 waves per 64 parameters, each summing its slice of the partials with every
+  // load of the slice in flight (parts <= 256: <= 16 per wave), then the 16 slice
+  // sums in slice order: a fixed order, deterministic run to run
+  constexpr int NS = 16;
+  __shared__ float red[NS][64];
   const int cl = threadIdx.x & 63, sl = threadIdx.x >> 6;
   const int64_t i = static_cast<int64_t>(blockIdx.x) * 64 + cl;
-  const int per = (parts + 3) / 4, g0 = sl * per, g1 = min(parts, g0 + per);
+  const int per = (parts + NS - 1) / NS, g0 = sl * per, g1 = min(parts, g0 + per);
   float v = 0.f;
   if (i < P) {
     int g = g0;
+    for (; g + 16 <= g1; g += 16) {
+      float x[16];
+#pragma unroll
+      for (int u = 0; u < 16; ++u) x[u] = part[(g + u) * P + i];
+#pragma unroll
+      for (int u = 0; u < 16; ++u) v += x[u];
+    }
     for (; g + 4 <= g1; g += 4) {
       const float x0 = part[(g + 0) * P + i], x1 = part[(g + 1) * P + i];
       const float x2 = part[(g + 2) * P + i], x3 = part[(g + 3) * P + i];
@@ -739,7 +1182,9 @@ __global__ __launch_bounds__(256) void din_att_wgrad_kernel(
   red[sl][cl] = v;
   __syncthreads();
   if (sl != 0 || i >= P) return;
-  v = red[0][cl] + red[1][cl] + red[2][cl] + red[3][cl];
+  v = red[0][cl];
+#pragma unroll
+  for (int q = 1; q < NS; ++q) v += red[q][cl];
   if (grads) {
     grads[i] = v;
     return;
@@ -804,7 +1249,19 @@ void da_set_attrs() {
   (void)hipFuncSetAttribute(reinterpret_cast<const void *>(din_att_bwd_kernel<E, H1T, H1K, H2T, H2K>),
                             hipFuncAttributeMaxDynamicSharedMemorySize,
                             static_cast<int>(S::bwd_bytes));
+  (void)hipFuncSetAttribute(reinterpret_cast<const void *>(din_att_bwd2_kernel<E, H1T, H1K, H2T, H2K>),
+                            hipFuncAttributeMaxDynamicSharedMemorySize,
+                            static_cast<int>(DaShape2<E, H1T, H1K, H2T, H2K>::bytes));
   (void)hipGetLastError();
+}
+
+// MREC_DIN_BWD_ONE=1: the one-sample-per-workgroup backward (A/B and parity yardstick)
+bool da_one_sample() {
+  static const bool v = [] {
+    const char *e = std::getenv("MREC_DIN_BWD_ONE");
+    return e && e[0] == '1';
+  }();
+  return v;
 }
 
 bool da_supported(int E, int H1, int H2) {
@@ -817,7 +1274,12 @@ bool da_supported(int E, int H1, int H2) {
 
 }  // namespace
 
+static unsigned long long *g_da_stamps = nullptr;
+
 extern "C" {
+
+// diagnostics (not in mrec.h): phase clocks of the next backward launches (NULL: off)
+void mrec_din_att_debug_stamps(void *buf) { g_da_stamps = static_cast<unsigned long long *>(buf); }
 
 int32_t mrec_din_att_supported(int32_t E, int32_t H1, int32_t H2) {
   return da_supported(E, H1, H2) ? 1 : 0;
@@ -915,14 +1377,20 @@ mrec_status mrec_din_att_bwd(const void *rows, int64_t ld_rows, int64_t batch, i
   p.ld_drows = ld_drows;
   p.part = part;
   p.P = mrec_din_att_param_count(E, H1, H2);
+  p.stamps = g_da_stamps;
   hipStream_t s = static_cast<hipStream_t>(stream);
 #define X(e, h1t, h1k, h2t, h2k)                                                              \
   if (da_match<e, h1t, h1k, h2t, h2k>(E, H1, H2)) {                                         \
     static const int once = (da_set_attrs<e, h1t, h1k, h2t, h2k>(), 1);                     \
     (void)once;                                                                             \
-    din_att_bwd_kernel<e, h1t, h1k, h2t, h2k>                                               \
-        <<<dim3(static_cast<unsigned>(parts)), DA_THREADS,                                  \
-           DaShape<e, h1t, h1k, h2t, h2k>::bwd_bytes, s>>>(p);                              \
+    if (da_one_sample())                                                                    \
+      din_att_bwd_kernel<e, h1t, h1k, h2t, h2k>                                             \
+          <<<dim3(static_cast<unsigned>(parts)), DA_THREADS,                                \
+             DaShape<e, h1t, h1k, h2t, h2k>::bwd_bytes, s>>>(p);                            \
+    else                                                                                    \
+      din_att_bwd2_kernel<e, h1t, h1k, h2t, h2k>                                            \
+          <<<dim3(static_cast<unsigned>(parts)), DA_THREADS,                                \
+             DaShape2<e, h1t, h1k, h2t, h2k>::bytes, s>>>(p);                               \
     return launch_status("mrec_din_att_bwd");                                               \
   }
   MREC_DA_SHAPES(X)
@@ -937,7 +1405,7 @@ mrec_status mrec_din_att_wgrad(const float *part, int64_t parts, int32_t E, int3
   MREC_CHECK_ARG(part && parts >= 1, "NULL pointer / no partials");
   MREC_CHECK_ARG(grads || (w1 && b1 && w2 && b2 && w3 && b3), "need grads or the parameters");
   const int64_t P = mrec_din_att_param_count(E, H1, H2);
-  din_att_wgrad_kernel<<<dim3(static_cast<unsigned>((P + 63) / 64)), 256, 0,
+  din_att_wgrad_kernel<<<dim3(static_cast<unsigned>((P + 63) / 64)), 1024, 0,
                          static_cast<hipStream_t>(stream)>>>(
       part, static_cast<int>(parts), P, 4 * E, H1, H2, grads, lr, w1, ldw1, b1, w2, ldw2, b2, w3,
       b3);

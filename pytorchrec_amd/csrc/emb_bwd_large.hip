@@ -469,23 +469,49 @@ __global__ __launch_bounds__(kBkThreads) void bk_hist_kernel(BankArgs bank, IdsA
 
 // per bucket (one thread each, 256 per workgroup): every chunk's count becomes its
 // first position inside the bucket (chunk order), and the bucket's total
+// per bucket, the chunks' exclusive prefix: a workgroup takes 16 consecutive buckets
+// (64-B row segments of bhist) x 16 groups of consecutive chunks; every load of a
+// thread is in flight before any is added, the 16 group sums are prefixed through
+// LDS, then each thread rewrites its chunks with the running offset
 __global__ __launch_bounds__(256) void bk_scan_kernel(int G, int lognb, LgWs w) {
+  constexpr int BW = 16, CG = 16, U = 8;
+  __shared__ int32_t gs[CG][BW];
   const int NB = 1 << lognb;
-  const int k = blockIdx.x * 256 + threadIdx.x;
-  if (k >= NB) return;
-  int tot = 0;
-  for (int g0 = 0; g0 < G; g0 += 16) {
-    int32_t c[16];
+  const int j = threadIdx.x % BW, c = threadIdx.x / BW;
+  const int k = blockIdx.x * BW + j;
+  const int per = (G + CG - 1) / CG, g0 = c * per, g1 = min(G, g0 + per);
+  int sum = 0;
+  if (k < NB) {
+    for (int g = g0; g < g1; g += U) {
+      int32_t v[U];
 #pragma unroll
-    for (int u = 0; u < 16; ++u)
-      c[u] = g0 + u < G ? w.bhist[static_cast<int64_t>(g0 + u) * NB + k] : 0;
+      for (int u = 0; u < U; ++u)
+        v[u] = g + u < g1 ? w.bhist[static_cast<int64_t>(g + u) * NB + k] : 0;
 #pragma unroll
-    for (int u = 0; u < 16; ++u) {
-      if (g0 + u < G) w.bhist[static_cast<int64_t>(g0 + u) * NB + k] = tot;
-      tot += c[u];
+      for (int u = 0; u < U; ++u) sum += v[u];
     }
   }
-  w.bstart[k] = tot;  // the total for now: bk_scatter_kernel scans the totals
+  gs[c][j] = sum;
+  __syncthreads();
+  int tot = 0, all = 0;
+#pragma unroll
+  for (int q = 0; q < CG; ++q) {
+    tot += q < c ? gs[q][j] : 0;
+    all += gs[q][j];
+  }
+  if (k >= NB) return;
+  for (int g = g0; g < g1; g += U) {
+    int32_t v[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u)
+      v[u] = g + u < g1 ? w.bhist[static_cast<int64_t>(g + u) * NB + k] : 0;
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      if (g + u < g1) w.bhist[static_cast<int64_t>(g + u) * NB + k] = tot;
+      tot += v[u];
+    }
+  }
+  if (c == 0) w.bstart[k] = all;  // the total for now: bk_scatter_kernel scans the totals
 }
 
 // exclusive scan of the NB bucket totals (bstart) into LDS base[]; returns the sum
@@ -702,7 +728,7 @@ __global__ __launch_bounds__(256) void bk_group_kernel(LgWs w, int G, int lognb,
 // pass 1 over the long segments' chunks: max |g| per segment (bits of a
 // non-negative float order like the float)
 template <typename T, int LPR>
-__global__ __launch_bounds__(256) void lg_longmax_kernel(BankArgs bank, int64_t n, LgWs w,
+__device__ __forceinline__ void lg_longmax_body(BankArgs bank, int64_t n, LgWs w,
                                                          ApplyArgs a) {
   constexpr int EPL = Vec<T>::EPL;
   constexpr int WPB = 256 / LPR;
@@ -743,7 +769,7 @@ __device__ __forceinline__ int lg_scale(float mx, int len) {
 
 // pass 2: fixed-point chunk sums added into the segment's int64 accumulator
 template <typename T, int LPR>
-__global__ __launch_bounds__(256) void lg_longacc_kernel(BankArgs bank, int64_t n, LgWs w,
+__device__ __forceinline__ void lg_longacc_body(BankArgs bank, int64_t n, LgWs w,
                                                          ApplyArgs a, int stride) {
   constexpr int EPL = Vec<T>::EPL;
   constexpr int WPB = 256 / LPR;
@@ -798,7 +824,7 @@ __global__ __launch_bounds__(256) void lg_longacc_kernel(BankArgs bank, int64_t 
 // term scaled by 2^S: the arithmetic of the chunked kernels, so the same bits); a
 // longer one from the chunked kernels' accumulator.
 template <typename T, int LPR>
-__global__ __launch_bounds__(256) void lg_apply_kernel(BankArgs bank, int64_t n, LgWs w,
+__device__ __forceinline__ void lg_apply_body(BankArgs bank, int64_t n, LgWs w,
                                                        ApplyArgs a, int stride) {
   constexpr int EPL = Vec<T>::EPL;
   constexpr int WPB = 256 / LPR;  // workers per workgroup
@@ -894,6 +920,70 @@ __global__ __launch_bounds__(256) void lg_apply_kernel(BankArgs bank, int64_t n,
   }
 }
 
+template <typename T, int LPR>
+__global__ __launch_bounds__(256) void lg_longmax_kernel(BankArgs bank, int64_t n, LgWs w,
+                                                         ApplyArgs a) {
+  lg_longmax_body<T, LPR>(bank, n, w, a);
+}
+
+template <typename T, int LPR>
+__global__ __launch_bounds__(256) void lg_longacc_kernel(BankArgs bank, int64_t n, LgWs w,
+                                                         ApplyArgs a, int stride) {
+  lg_longacc_body<T, LPR>(bank, n, w, a, stride);
+}
+
+template <typename T, int LPR>
+__global__ __launch_bounds__(256) void lg_apply_kernel(BankArgs bank, int64_t n, LgWs w,
+                                                       ApplyArgs a, int stride) {
+  lg_apply_body<T, LPR>(bank, n, w, a, stride);
+}
+
+// grid-wide barrier of the huge-segment kernel (every workgroup co-resident: the
+// grid is sized by the occupancy query): stores drained, one agent-scope arrival
+// per workgroup, a bounded poll (an error flag, never a hang), acquire fence.
+__device__ __forceinline__ void lg_grid_sync(int32_t *ctr, int target) {
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+    __hip_atomic_fetch_add(ctr, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    int spins = 0;
+    while (__hip_atomic_load(ctr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < target) {
+      __builtin_amdgcn_s_sleep(2);
+      if (++spins > (1 << 26)) {  // seconds: a workgroup never arrived
+        __hip_atomic_store(ctr + 2, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        break;
+      }
+    }
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+  }
+  __syncthreads();
+}
+
+// the fused path's huge segments (> kLgHuge lookups of one row): max |g|, the
+// fixed-point chunk sums and the per-row update as three phases of ONE launch
+// (grid barriers between them).  The bucket kernel counts the huge segments in
+// hdr[3]; with none (the common case: DIN's padding slots skip the PAD row) every
+// workgroup leaves at once, so the step pays one empty launch instead of three.
+// hdr[4] counts arrivals (2 barriers + 1 exit per workgroup; the last exit resets
+// it), hdr[6] is the barrier's time-out flag.
+template <typename T, int LPR>
+__global__ __launch_bounds__(256) void lg_huge_kernel(BankArgs bank, int64_t n, LgWs w,
+                                                      ApplyArgs a, int stride) {
+  if (__hip_atomic_load(w.hdr + 3, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0) return;
+  const int G = static_cast<int>(gridDim.x);
+  lg_longmax_body<T, LPR>(bank, n, w, a);
+  lg_grid_sync(w.hdr + 4, G);
+  lg_longacc_body<T, LPR>(bank, n, w, a, stride);
+  lg_grid_sync(w.hdr + 4, 2 * G);
+  lg_apply_body<T, LPR>(bank, n, w, a, stride);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (threadIdx.x == 0 &&
+      __hip_atomic_fetch_add(w.hdr + 4, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 3 * G - 1)
+    __hip_atomic_store(w.hdr + 4, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
 // ---- fused bucketed plan + apply (mrec_emb_bwd_large_fused) ---------------------
 // bk_group_kernel's grouping, then the bucket's own rows are updated right there:
 // a segment of <= 16 lookups by one worker (sorted, ascending sample order), one of
@@ -961,6 +1051,7 @@ __global__ __launch_bounds__(256) void bk_apply_kernel(BankArgs bank, LgWs w, Ap
   const int nm = bk_scan256(sm, &em, red);
   const int nl = bk_scan256(sl, &el, red);
   const int nc = bk_scan256(sc, &ec, red);
+  if (tid == 0 && nl > 0) __hip_atomic_fetch_add(w.hdr + 3, nl, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   const bool in_lds = nl == 0 && hi - lo <= kBkLdsPerm;
   int32_t *P = in_lds ? lperm : w.perm + lo;  // the bucket's placed lookups
   const int l0 = (lo + kLgHuge) / (kLgHuge + 1), l1 = (hi + kLgHuge) / (kLgHuge + 1);
@@ -1148,7 +1239,7 @@ mrec_status mrec_emb_bwd_large_plan(const mrec_table_bank *bank, const mrec_ids 
     int lognb = 0;
     while ((1 << lognb) < NB) ++lognb;
     bk_hist_kernel<<<dim3(G), kBkThreads, 0, s>>>(ba, ia, batch, lognb, w, d_oob_flag);
-    bk_scan_kernel<<<dim3((NB + 255) / 256), 256, 0, s>>>(G, lognb, w);
+    bk_scan_kernel<<<dim3((NB + 15) / 16), 256, 0, s>>>(G, lognb, w);
     bk_scatter_kernel<<<dim3(G), kBkThreads, 0, s>>>(ba, ia, batch, G, lognb, w, 0);
     bk_group_kernel<<<dim3(NB), 256, 0, s>>>(w, G, lognb, d_oob_flag);
     return launch_status("mrec_emb_bwd_large_plan");
@@ -1231,6 +1322,18 @@ static void lg_launch_apply(const BankArgs &ba, int64_t batch, const LgWs &w, co
     const int64_t cc = ul + (N + kLgChunk - 1) / kLgChunk + 2;
     gc = dim3(static_cast<unsigned>(std::min<int64_t>(cc, kLgApplyBlocks)));
     gu = dim3(static_cast<unsigned>(std::min<int64_t>((ul + 256 / L - 1) / (256 / L), kLgApplyBlocks)));
+    static const int resident = [] {  // workgroups the grid barrier may count on
+      int dev = 0, cus = 0, per = 0;
+      (void)hipGetDevice(&dev);
+      (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+      (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, lg_huge_kernel<T, L>, 256, 0);
+      (void)hipGetLastError();
+      return std::max(1, cus) * std::max(1, std::min(per, 2));
+    }();
+    const int64_t need = std::max<int64_t>(gc.x, gu.x);
+    lg_huge_kernel<T, L><<<dim3(static_cast<unsigned>(std::min<int64_t>(need, resident))), 256, 0, s>>>(
+        ba, batch, w, a, stride);
+    return;
   }
   lg_longmax_kernel<T, L><<<gc, 256, 0, s>>>(ba, batch, w, a);
   lg_longacc_kernel<T, L><<<gc, 256, 0, s>>>(ba, batch, w, a, stride);
@@ -1321,7 +1424,7 @@ mrec_status mrec_emb_bwd_large_fused(const mrec_table_bank *bank, const mrec_ids
   int lognb = 0;
   while ((1 << lognb) < NB) ++lognb;
   bk_hist_kernel<<<dim3(G), kBkThreads, 0, s>>>(ba, ia, batch, lognb, w, d_oob_flag);
-  bk_scan_kernel<<<dim3((NB + 255) / 256), 256, 0, s>>>(G, lognb, w);
+  bk_scan_kernel<<<dim3((NB + 15) / 16), 256, 0, s>>>(G, lognb, w);
   bk_scatter_kernel<<<dim3(G), kBkThreads, 0, s>>>(ba, ia, batch, G, lognb, w, 1);
   lg_dispatch_apply(bank->dtype, lpr, ba, batch, w, a, ba.row_stride, NB, G, lognb, s);
   return launch_status("mrec_emb_bwd_large_fused");

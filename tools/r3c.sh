@@ -1,0 +1,12 @@
+# C4 changes: merged huge-segment launch, wider DIN wgrad reduce; DIN phase clocks
+set -e
+cd $GRAFT_REPO_ROOT
+R=$GRAFT_REPO_ROOT
+O=$R/gpurun_out/r3c
+mkdir -p $O
+timeout -k 10 600 python -u -m pytest tests/test_gpu_embedding.py tests/test_gpu_din.py -x -q --timeout 300 --timeout-method thread > $O/tests.log 2>&1
+timeout -k 10 120 python tools/din_stamps.py > $O/din_stamps.txt 2>&1
+timeout -k 10 200 python bench.py --model din --no-cpu-baseline > $O/bench_din.json 2> $O/din.err
+cd /tmp && export TMPDIR=/tmp
+timeout -k 10 240 rocprofv3 --kernel-trace --stats --output-format csv -d $O/prof_din -o run -- python3 $R/bench.py --model din --no-cpu-baseline --no-roofline --steps 20 > $O/prof_din.log 2>&1
+echo OK

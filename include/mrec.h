@@ -32,7 +32,7 @@
 extern "C" {
 #endif
 
-#define MREC_ABI_VERSION 21
+#define MREC_ABI_VERSION 22
 #define MREC_MAX_TABLES 64      /* tables per table bank / per call */
 #define MREC_BWD_MAX_BATCH 8192  /* lookups per table per plan/apply call */
 #define MREC_BWD_HASH_MAX_BATCH 4096  /* batches up to this use the hash plan */
@@ -899,6 +899,22 @@ mrec_status mrec_din_lookup_ids(const void *iid, const void *cid, const void *hi
                                 const void *hcat, int64_t ld_hcat, int32_t ids_dtype,
                                 int64_t batch, int32_t L, int32_t *out_item, int32_t *out_cate,
                                 mrec_stream stream);
+
+/*
+ * mrec_din_lookup_ids and mrec_emb_gather_fwd (pad_negative) in ONE launch (ABI 22):
+ * writes the same out_item / out_cate ids (for the embedding backward) and gathers
+ * the rows of both tables into out [batch (L + 1), 2 dim] (item | category; a
+ * padding slot is a zero row).  bank: the two tables (item, category), not under
+ * the lazy fused Adam.  An invalid id sets *d_oob_flag (the caller raises
+ * IndexError, as for nn.Embedding).  Replaces, with the ids builder, the
+ * reference's nn.Embedding lookups of target and history ids (SASRec.py:85-86 idiom;
+ * torchrec has no DIN).
+ */
+mrec_status mrec_din_gather(const mrec_table_bank *bank, const void *iid, const void *cid,
+                            const void *his, int64_t ld_his, const void *hcat, int64_t ld_hcat,
+                            int32_t ids_dtype, int64_t batch, int32_t L, int32_t *out_item,
+                            int32_t *out_cate, void *out, mrec_dtype out_dtype, int64_t out_ld,
+                            int32_t *d_oob_flag, mrec_stream stream);
 
 /*
  * Fused DIN attention unit (ABI 17): one launch each way replaces

@@ -20,7 +20,7 @@ import torch  # noqa: F401  (must precede the dlopen, see module docstring)
 LIB_DIR = os.path.join(os.path.dirname(os.path.abspath(__file__)), "lib")
 LIB_PATH = os.environ.get("MREC_LIB_PATH") or os.path.join(LIB_DIR, "libmrec.so")
 
-ABI_VERSION = 21
+ABI_VERSION = 22
 MAX_TABLES = 64
 BWD_MAX_BATCH = 8192
 BWD_HASH_MAX_BATCH = 4096  # batches up to this use the hash plan (fusable into a GEMM launch)
@@ -280,6 +280,8 @@ SIGNATURES = {
                                               _i32, _vp, _i64, _vp, _i64, _vp]),
     "mrec_din_lookup_ids": (ctypes.c_int, [_vp, _vp, _vp, _i64, _vp, _i64, _i32, _i64, _i32, _vp,
                                            _vp, _vp]),
+    "mrec_din_gather": (ctypes.c_int, [_bank_p, _vp, _vp, _vp, _i64, _vp, _i64, _i32, _i64, _i32,
+                                        _vp, _vp, _vp, _i32, _i64, _vp, _vp]),
     "mrec_din_att_supported": (ctypes.c_int32, [_i32, _i32, _i32]),
     "mrec_din_att_parts": (ctypes.c_int64, [_i64]),
     "mrec_din_att_param_count": (ctypes.c_int64, [_i32, _i32, _i32]),

@@ -239,6 +239,112 @@ __global__ __launch_bounds__(256) void din_ids_kernel(const I *__restrict__ iid,
   out_c[B + b * L + j] = (pad && c >= 0) ? -1 : din_narrow_id(c);
 }
 
+// mrec_din_gather: the lookup ids of din_ids_kernel built in the gather itself (one
+// launch instead of two): worker (i, f) over the N = B (L + 1) lookup positions and
+// the two tables; its lane 0 also writes the id for the embedding backward.  A
+// padding slot (-1) gathers a zero row; an invalid id (INT32_MAX) sets the OOB flag.
+template <typename I, typename T, typename O, int LPR>
+__global__ __launch_bounds__(256) void din_gather_kernel(BankArgs bank, const I *__restrict__ iid,
+                                                         const I *__restrict__ cid,
+                                                         const I *__restrict__ his, int64_t ldh,
+                                                         const I *__restrict__ hcat, int64_t ldc,
+                                                         int64_t B, int L, int32_t *__restrict__ out_i,
+                                                         int32_t *__restrict__ out_c,
+                                                         O *__restrict__ out, int64_t out_ld,
+                                                         int32_t *__restrict__ oob) {
+  constexpr int EPL = Vec<T>::EPL;
+  constexpr int WPB = 256 / LPR;
+  const int64_t g = static_cast<int64_t>(blockIdx.x) * WPB + threadIdx.x / LPR;
+  const int l = threadIdx.x % LPR;
+  const int64_t N = B * (L + 1);
+  if (g >= 2 * N) return;
+  const int64_t i = g >> 1;
+  const int f = static_cast<int>(g & 1);
+  int32_t id;
+  if (i < B) {
+    id = din_narrow_id(f ? cid[i] : iid[i]);
+  } else {
+    const int64_t bb = (i - B) / L;
+    const int j = static_cast<int>(i - B - bb * L);
+    const I h = his[bb * ldh + j];
+    const bool pad = j > 0 && h == 0;  // masked (h < 0 is an error wherever it sits)
+    if (f == 0) {
+      id = pad ? -1 : din_narrow_id(h);
+    } else {
+      const I c = hcat[bb * ldc + j];
+      id = (pad && c >= 0) ? -1 : din_narrow_id(c);
+    }
+  }
+  if (l == 0) (f ? out_c : out_i)[i] = id;
+  const bool ok = id >= 0 && id < bank.rows[f];
+  uint4 raw = make_uint4(0, 0, 0, 0);
+  if (ok) {
+    const T *row = reinterpret_cast<const T *>(bank.data) +
+                   (bank.row_offset[f] + id) * static_cast<int64_t>(bank.row_stride);
+    raw = *reinterpret_cast<const uint4 *>(row + l * EPL);
+  } else if (l == 0 && oob && id >= 0) {
+    *oob = 1;
+  }
+  const int D = bank.dim;
+  const int e0 = l * EPL;
+  if (e0 + EPL > D) return;
+  O *dst = out + i * out_ld + static_cast<int64_t>(f) * D + e0;
+  if constexpr (sizeof(O) == sizeof(T)) {
+    *reinterpret_cast<uint4 *>(dst) = raw;  // bit copy
+  } else {
+    float v[EPL];
+    Vec<T>::to_f32(raw, v);
+    if constexpr (sizeof(O) == 4) {
+#pragma unroll
+      for (int q = 0; q < EPL; q += 4)
+        *reinterpret_cast<float4 *>(dst + q) = make_float4(v[q], v[q + 1], v[q + 2], v[q + 3]);
+    } else {
+      *reinterpret_cast<uint2 *>(dst) = make_uint2(pack_bf16x2(v[0], v[1]), pack_bf16x2(v[2], v[3]));
+    }
+  }
+}
+
+template <typename I, typename T, typename O>
+static void din_gather_launch(int lpr, const BankArgs &ba, const void *iid, const void *cid,
+                              const void *his, int64_t ldh, const void *hcat, int64_t ldc,
+                              int64_t B, int L, int32_t *oi, int32_t *oc, void *out,
+                              int64_t out_ld, int32_t *oob, hipStream_t s) {
+  const int64_t work = 2 * B * (L + 1);
+  const int wpb = 256 / lpr;
+  const dim3 grid(static_cast<unsigned>((work + wpb - 1) / wpb));
+  const I *a = static_cast<const I *>(iid), *c = static_cast<const I *>(cid);
+  const I *h = static_cast<const I *>(his), *hc = static_cast<const I *>(hcat);
+  O *o = static_cast<O *>(out);
+#define MREC_DG(LP) \
+  din_gather_kernel<I, T, O, LP><<<grid, 256, 0, s>>>(ba, a, c, h, ldh, hc, ldc, B, L, oi, oc, o, out_ld, oob)
+  switch (lpr) {
+    case 1: MREC_DG(1); break;
+    case 2: MREC_DG(2); break;
+    case 4: MREC_DG(4); break;
+    case 8: MREC_DG(8); break;
+    default: MREC_DG(16); break;
+  }
+#undef MREC_DG
+}
+
+template <typename I>
+static void din_gather_dispatch(mrec_dtype bank_dt, mrec_dtype out_dt, int lpr, const BankArgs &ba,
+                                const void *iid, const void *cid, const void *his, int64_t ldh,
+                                const void *hcat, int64_t ldc, int64_t B, int L, int32_t *oi,
+                                int32_t *oc, void *out, int64_t out_ld, int32_t *oob, hipStream_t s) {
+  if (bank_dt == MREC_BF16) {
+    if (out_dt == MREC_BF16)
+      din_gather_launch<I, uint16_t, uint16_t>(lpr, ba, iid, cid, his, ldh, hcat, ldc, B, L, oi, oc, out, out_ld, oob, s);
+    else
+      din_gather_launch<I, uint16_t, float>(lpr, ba, iid, cid, his, ldh, hcat, ldc, B, L, oi, oc, out, out_ld, oob, s);
+  } else {
+    if (out_dt == MREC_BF16)
+      din_gather_launch<I, float, uint16_t>(lpr, ba, iid, cid, his, ldh, hcat, ldc, B, L, oi, oc, out, out_ld, oob, s);
+    else
+      din_gather_launch<I, float, float>(lpr, ba, iid, cid, his, ldh, hcat, ldc, B, L, oi, oc, out, out_ld, oob, s);
+  }
+}
+
 static bool a16(const void *p, int64_t ld) {
   return (reinterpret_cast<uintptr_t>(p) & 15) == 0 && ld % 8 == 0;
 }
@@ -271,6 +377,39 @@ mrec_status mrec_din_lookup_ids(const void *iid, const void *cid, const void *hi
         static_cast<const int64_t *>(his), ld_his, static_cast<const int64_t *>(hcat), ld_hcat,
         batch, L, out_item, out_cate);
   return launch_status("mrec_din_lookup_ids");
+}
+
+mrec_status mrec_din_gather(const mrec_table_bank *bank, const void *iid, const void *cid,
+                            const void *his, int64_t ld_his, const void *hcat, int64_t ld_hcat,
+                            int32_t ids_dtype, int64_t batch, int32_t L, int32_t *out_item,
+                            int32_t *out_cate, void *out, mrec_dtype out_dtype, int64_t out_ld,
+                            int32_t *d_oob_flag, mrec_stream stream) {
+  BankArgs ba;
+  int eb, lpr;
+  mrec_status st = make_bank_args(bank, &ba, &eb, &lpr);
+  if (st != MREC_OK) return st;
+  MREC_CHECK_ARG(ba.n_tables == 2, "the DIN bank has two tables (item, category)");
+  MREC_CHECK_ARG(!ba.adam.kind, "a lazily updated Adam bank reads rows through mrec_emb_gather_fwd");
+  MREC_CHECK_ARG(iid && cid && his && hcat && out_item && out_cate && out, "NULL pointer");
+  MREC_CHECK_ARG(batch >= 0 && L >= 1 && ld_his >= L && ld_hcat >= L, "bad shape / strides");
+  MREC_CHECK_ARG(ids_dtype == MREC_I32 || ids_dtype == MREC_I64, "ids must be int32 or int64");
+  MREC_CHECK_ARG(out_dtype == MREC_F32 || out_dtype == MREC_BF16, "out dtype must be F32/BF16");
+  const int ob = out_dtype == MREC_F32 ? 4 : 2;
+  MREC_CHECK_ARG(out_ld >= 2 * ba.dim, "out_ld < 2 * dim");
+  MREC_CHECK_ARG((reinterpret_cast<uintptr_t>(out) & 15) == 0 && (out_ld * ob) % 16 == 0 &&
+                     (ba.dim * ob) % 16 == 0,
+                 "out must be 16B aligned with 16B-multiple rows");
+  MREC_CHECK_ARG(ba.rows[0] < INT32_MAX && ba.rows[1] < INT32_MAX,
+                 "DIN padded lookups need tables of fewer than 2^31 - 1 rows");
+  if (batch == 0) return MREC_OK;
+  hipStream_t s = static_cast<hipStream_t>(stream);
+  if (ids_dtype == MREC_I32)
+    din_gather_dispatch<int32_t>(bank->dtype, out_dtype, lpr, ba, iid, cid, his, ld_his, hcat,
+                                 ld_hcat, batch, L, out_item, out_cate, out, out_ld, d_oob_flag, s);
+  else
+    din_gather_dispatch<int64_t>(bank->dtype, out_dtype, lpr, ba, iid, cid, his, ld_his, hcat,
+                                 ld_hcat, batch, L, out_item, out_cate, out, out_ld, d_oob_flag, s);
+  return launch_status("mrec_din_gather");
 }
 
 mrec_status mrec_din_feat_fwd(const void *q, int64_t ldq, const void *k, int64_t ldk,

@@ -428,14 +428,22 @@ def _needs_backward(bank: EmbeddingBank) -> bool:
 class _GatherFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, weight, trigger, bank: EmbeddingBank, ids: List[torch.Tensor], out_dtype,
-                want_w: bool, need_bwd: bool):
+                want_w: bool, need_bwd: bool, din_src=None):
         B = ids[0].shape[0]
         F, D = bank.n_tables, bank.dim
         dev = weight.device
         out = torch.empty(B, F * D, dtype=out_dtype, device=dev)
         w_out = torch.empty(B, F, dtype=torch.float32, device=dev) if want_w else None
         flag = _oob_flag(bank, dev)
-        if B:
+        if B and din_src is not None:  # DIN: the ids are built by the gather launch itself
+            iid, cid, his, hcat = din_src
+            _mrec.call("mrec_din_gather", bank.desc().ref(), iid.data_ptr(), cid.data_ptr(),
+                       his.data_ptr(), his.stride(0), hcat.data_ptr(), hcat.stride(0),
+                       _mrec.dtype_code(his.dtype), his.shape[0], his.shape[1],
+                       ids[0].data_ptr(), ids[1].data_ptr(), out.data_ptr(),
+                       _mrec.dtype_code(out_dtype), out.stride(0), _mrec.ptr(flag),
+                       _mrec.stream_handle())
+        elif B:
             _mrec.call("mrec_emb_gather_fwd", bank.desc().ref(), _ids_desc(ids).ref(), B,
                        out.data_ptr(), _mrec.dtype_code(out_dtype), out.stride(0),
                        _mrec.ptr(w_out), _mrec.ptr(flag), _mrec.stream_handle())
@@ -459,15 +467,17 @@ class _GatherFn(torch.autograd.Function):
                                           "per call; use interact() for multi-field models")
             dw = dw_out.reshape(-1).contiguous().float()
         grad = _backward_into_bank(bank, ctx.ids, ctx.B, ctx.plan_ws, dx=dx, dw=dw)
-        return grad, None, None, None, None, None, None
+        return grad, None, None, None, None, None, None, None
 
 
 def gather(bank: EmbeddingBank, ids: Sequence[torch.Tensor], out_dtype=None, with_w=False,
-           pad_negative: bool = False):
+           pad_negative: bool = False, din_src=None):
     """out[b, f*D:(f+1)*D] = table_f[ids[f][b]] — F ``nn.Embedding`` lookups.
 
     Returns [B, F*D] (and [B, F] first-order weights if ``with_w``).  With
     ``pad_negative`` a negative id is a padding slot: a zero row, no gradient.
+    ``din_src`` = (iid, cid, his, hcat): ``ids`` are int32 output buffers that the
+    launch fills with DIN's padded lookup ids (mrec_din_gather; GPU only).
     """
     ids = PaddedIds(ids) if pad_negative else list(ids)
     if len(ids) != bank.n_tables:
@@ -479,7 +489,7 @@ def gather(bank: EmbeddingBank, ids: Sequence[torch.Tensor], out_dtype=None, wit
     # (grad mode is off inside Function.forward: decide here whether a backward
     # will run, so the plan can be queued ahead of it)
     return _GatherFn.apply(bank.weight, trigger, bank, ids, out_dtype, with_w,
-                           _needs_backward(bank))
+                           _needs_backward(bank), din_src)
 
 
 _TRIGGERS = {}

@@ -52,6 +52,27 @@ def din_lookup_ids(iid: Tensor, cid: Tensor, his: Tensor, hcat: Tensor, rows=Non
     return out_i, out_c
 
 
+def din_id_buffers(his: Tensor):
+    """int32 [B (L + 1)] item / category lookup-id buffers for mrec_din_gather."""
+    B, L = his.shape
+    out_i = torch.empty(B * (L + 1), dtype=torch.int32, device=his.device)
+    return [out_i, torch.empty_like(out_i)]
+
+
+def din_sources(iid: Tensor, cid: Tensor, his: Tensor, hcat: Tensor, rows=None):
+    """(iid, cid, his, hcat) of one id dtype, rows contiguous (mrec_din_gather's inputs)."""
+    if rows is not None and max(rows) >= 2 ** 31 - 1:
+        raise ValueError("DIN padded lookups need tables of fewer than 2^31 - 1 rows")
+    dt = his.dtype
+    iid, cid = iid.reshape(-1).to(dt).contiguous(), cid.reshape(-1).to(dt).contiguous()
+    hcat = hcat.to(dt)
+    if his.stride(1) != 1:
+        his = his.contiguous()
+    if hcat.stride(1) != 1:
+        hcat = hcat.contiguous()
+    return iid, cid, his, hcat
+
+
 class DIN(IModel):
     # GPU: masked history positions are padding slots of the lookup (see _top);
     # False keeps the plain [target | history] ids (A/B, parity tests)
@@ -120,8 +141,12 @@ class DIN(IModel):
             # masked history positions (softmax weight 0: an exactly zero gradient)
             # become padding slots (-1): zero rows forward, skipped by the backward, so
             # the PAD row is not a ~B L / 2-lookup hot row of every step's update
-            ids_i, ids_c = din_lookup_ids(iid, cid, his, hcat, bank.category_nums)
-            rows = gather(bank, [ids_i, ids_c], out_dtype=act_dtype, pad_negative=True)
+            if bank.update == "adam":  # rows are caught up on read: the plain gather
+                ids_i, ids_c = din_lookup_ids(iid, cid, his, hcat, bank.category_nums)
+                rows = gather(bank, [ids_i, ids_c], out_dtype=act_dtype, pad_negative=True)
+            else:  # ids built inside the gather launch (mrec_din_gather)
+                rows = gather(bank, din_id_buffers(his), out_dtype=act_dtype, pad_negative=True,
+                              din_src=din_sources(iid, cid, his, hcat, bank.category_nums))
             return dense_ops.din_attention_top_rows(rows, B, his, self.att_mlp, self.att_out)
         rows = gather(bank, [torch.cat([iid.reshape(-1), his.reshape(-1).to(iid.dtype)]),
                              torch.cat([cid.reshape(-1), hcat.reshape(-1).to(cid.dtype)])],

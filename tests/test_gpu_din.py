@@ -399,3 +399,36 @@ def test_din_padded_lookups_still_raise_on_bad_ids(gpu, monkeypatch, what):
         torch.cuda.synchronize()
     # the unmodified batch runs
     model(bench.din_batch(A, 0, gpu))
+
+
+@pytest.mark.parametrize("ids64,table_dtype,out_dtype", [(False, torch.bfloat16, torch.bfloat16),
+                                                         (True, torch.float32, torch.float32),
+                                                         (False, torch.float32, torch.bfloat16)])
+def test_din_gather_equals_lookup_ids_then_gather(gpu, ids64, table_dtype, out_dtype):
+    """mrec_din_gather (ids built inside the gather launch) writes exactly the ids of
+    mrec_din_lookup_ids and gathers exactly the rows of mrec_emb_gather_fwd with
+    padding slots (bit-exact), at a batch that is not a multiple of the launch's
+    workgroup and with masked positions everywhere but position 0."""
+    import bench
+    from pytorchrec_amd.embedding import EmbeddingBank, gather, init_bank_
+    from pytorchrec_amd.model.DIN import din_id_buffers, din_lookup_ids, din_sources
+
+    class A:
+        batch, lr = 333, 0.05
+    d = bench.din_batch(A, 3, gpu)
+    if ids64:
+        d = {k: (v.long() if v.dtype == torch.int32 else v) for k, v in d.items()}
+    bank = EmbeddingBank([bench.DIN_ITEMS, bench.DIN_CATES], 16, dtype=table_dtype, device=gpu)
+    init_bank_(bank, generator=torch.Generator(device=gpu).manual_seed(2))
+    iid, cid, his, hcat = d["iid"], d["cid"], d["pos_his"], d["pos_his_cate"]
+    with torch.no_grad():
+        ref_i, ref_c = din_lookup_ids(iid, cid, his, hcat, bank.category_nums)
+        ref = gather(bank, [ref_i, ref_c], out_dtype=out_dtype, pad_negative=True)
+        bufs = din_id_buffers(his)
+        got = gather(bank, bufs, out_dtype=out_dtype, pad_negative=True,
+                     din_src=din_sources(iid, cid, his, hcat, bank.category_nums))
+    torch.cuda.synchronize()
+    assert torch.equal(bufs[0], ref_i) and torch.equal(bufs[1], ref_c)
+    assert (ref_i < 0).any()  # masked positions exist
+    assert torch.equal(got.view(torch.int16 if out_dtype == torch.bfloat16 else torch.int32),
+                       ref.view(torch.int16 if out_dtype == torch.bfloat16 else torch.int32))

@@ -164,31 +164,6 @@ class _Call:
 
 _PENDING = []  # deferred split-K reductions (fused SGD of a layer's W, b and images)
 
-# MREC_DW_SIDE=1: mrec_tower_dw on a side stream (a parallel branch of a captured
-# graph) so the embedding backward overlaps it; its reductions then run after the
-# join instead of inside the embedding apply launch
-_DW_SIDE = os.environ.get("MREC_DW_SIDE", "0") == "1"
-_JOIN = []  # events the deferred reductions wait for
-_SIDE = {}
-
-
-def _dw_on_side_stream(fn, dev):
-    main = torch.cuda.current_stream(dev)
-    side = _SIDE.get(dev)
-    if side is None:
-        side = _SIDE[dev] = torch.cuda.Stream(dev)
-    side.wait_stream(main)
-    with torch.cuda.stream(side):
-        fn()
-        ev = torch.cuda.Event()
-        ev.record(side)
-    _JOIN.append(ev)
-
-
-def _join_side():
-    while _JOIN:
-        torch.cuda.current_stream().wait_event(_JOIN.pop(0))
-
 
 def launch_multi(calls):
     """Run ``calls`` plus the pending deferred reductions in as few launches as
@@ -196,8 +171,6 @@ def launch_multi(calls):
     flushed first)."""
     global _PENDING
     pend = _PENDING
-    if pend:
-        _join_side()
     reads = set().union(*[c.reads for c in calls]) if calls else set()
     if any(p.writes & reads for p in pend):
         _run(pend)
@@ -264,7 +237,6 @@ def flush_pending():
     pending)."""
     global _PENDING
     pend, _PENDING = _PENDING, []
-    _join_side()
     for i in range(0, len(pend), 4):
         _run(pend[i:i + 4])
     _flush_finish()
@@ -274,8 +246,6 @@ def take_pending(n: int):
     """Remove and return up to ``n`` deferred reductions, for a launch that runs
     them beside its own work (``mrec_emb_bwd_apply_ex``)."""
     global _PENDING
-    if _JOIN:  # their slabs come from a side-stream launch: they run after the join
-        return []
     jobs, _PENDING = _PENDING[:n], _PENDING[n:]
     return jobs
 
@@ -1418,12 +1388,7 @@ def _tower_param_grads(widths, Ws, bs, imgs, head, B: int, H: int, ns: int, x0, 
                    g.data_ptr(), 0, 0.0, None, None, None, None, dW_h.data_ptr(),
                    _mrec.ptr(db_h), _mrec.ptr(dws), _mrec.ptr(db2), _mrec.stream_handle())
     if calls and tdw:
-        if _DW_SIDE and (lr is not None or dpg is not None):
-            # the weight-gradient launch on a side stream, joined before its deferred
-            # reductions: the embedding backward that follows runs beside it
-            _dw_on_side_stream(lambda: _tower_dw(calls, dhs, xin, widths, B, tdw), dev)
-        else:
-            _tower_dw(calls, dhs, xin, widths, B, tdw)
+        _tower_dw(calls, dhs, xin, widths, B, tdw)
         if lr is None and dpg is None:
             _run([c.with_phase(_mrec.GEMM_REDUCE) for c in calls])
         else:

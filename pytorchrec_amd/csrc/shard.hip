@@ -285,7 +285,10 @@ __global__ __launch_bounds__(kBT) void bucketize_dedup_kernel(IdsArgs ids, RowsA
 // ---------------------------------------------------------------------------
 
 constexpr int kWireThreads = 1024;
-constexpr int kWirePer = 2;  // elements per thread
+#ifndef MREC_WIRE_PER
+#define MREC_WIRE_PER 2
+#endif
+constexpr int kWirePer = MREC_WIRE_PER;  // elements per thread
 constexpr int kWireElems = kWireThreads * kWirePer;
 
 struct WireArgs {
@@ -360,19 +363,21 @@ __global__ __launch_bounds__(kWireThreads) void gather_wire_kernel(BankArgs bank
     nrows[threadIdx.x] = bank.rows[threadIdx.x];
   }
   const int tot = wire_prefix(w, p, pre);  // (its barrier covers roff / nrows too)
-  const int64_t n = static_cast<int64_t>(tot) * w.rec_dw;
-  const int64_t e0 = static_cast<int64_t>(cx) * kWireElems + threadIdx.x;
+  // element indices fit 32 bits (checked on the host): 32-bit divisions, not 64-bit
+  const uint32_t n = static_cast<uint32_t>(tot) * static_cast<uint32_t>(w.rec_dw);
+  const uint32_t e0 = static_cast<uint32_t>(cx) * kWireElems + threadIdx.x;
   if (e0 - threadIdx.x >= n) return;
+  const uint32_t rdw = static_cast<uint32_t>(w.rec_dw);
   const int32_t *ids = recv + static_cast<int64_t>(p) * (static_cast<int64_t>(w.F) * w.cap + w.F);
   const uint32_t *data = reinterpret_cast<const uint32_t *>(bank.data);
   const int row_dw = bank.lpr * 4;
   int64_t src[kWirePer];
 #pragma unroll
   for (int it = 0; it < kWirePer; ++it) {  // every id load first
-    const int64_t e = e0 + it * kWireThreads;
+    const uint32_t e = e0 + it * kWireThreads;
     src[it] = -1;
     if (e < n) {
-      const int r = static_cast<int>(e / w.rec_dw), k = static_cast<int>(e - int64_t(r) * w.rec_dw);
+      const int r = static_cast<int>(e / rdw), k = static_cast<int>(e - r * rdw);
       const int f = wire_table(pre, w.F, r);
       const int64_t id = ids[static_cast<int64_t>(f) * w.cap + (r - pre[f])];
       if (id >= 0 && id < nrows[f]) src[it] = (roff[f] + id) * row_dw + k;
@@ -384,7 +389,7 @@ __global__ __launch_bounds__(kWireThreads) void gather_wire_kernel(BankArgs bank
   uint32_t *dst = wire + static_cast<int64_t>(p) * w.cap_rows * w.rec_dw;
 #pragma unroll
   for (int it = 0; it < kWirePer; ++it) {
-    const int64_t e = e0 + it * kWireThreads;
+    const uint32_t e = e0 + it * kWireThreads;
     if (e < n) dst[e] = v[it];
   }
 }
@@ -406,24 +411,26 @@ __global__ __launch_bounds__(kWireThreads) void wire_move_kernel(WireArgs w,
   const int p = blockIdx.y;
   const int tot = wire_prefix(w, p, pre);
   const int epr = UNPACK ? max(slot_dw, zero ? zero_dw : 0) : w.rec_dw;
-  const int64_t n = static_cast<int64_t>(tot) * epr;
-  const int64_t e0 = static_cast<int64_t>(blockIdx.x) * kWireElems + threadIdx.x;
+  // element indices fit 32 bits (checked on the host): 32-bit divisions, not 64-bit
+  const uint32_t n = static_cast<uint32_t>(tot) * static_cast<uint32_t>(epr);
+  const uint32_t e0 = blockIdx.x * kWireElems + threadIdx.x;
   if (e0 - threadIdx.x >= n) return;
+  const uint32_t uepr = static_cast<uint32_t>(epr);
   uint32_t *rec0 = wire + static_cast<int64_t>(p) * w.cap_rows * w.rec_dw;
   int64_t srow[kWirePer];
   int kk[kWirePer], rr[kWirePer];
 #pragma unroll
   for (int it = 0; it < kWirePer; ++it) {
-    const int64_t e = e0 + it * kWireThreads;
+    const uint32_t e = e0 + it * kWireThreads;
     srow[it] = -1;
     kk[it] = 0;
     rr[it] = 0;
     if (e < n) {
-      const int r = static_cast<int>(e / epr);
-      const int f = wire_table(pre, w.F, r);
-      srow[it] = (static_cast<int64_t>(p) * w.F + f) * w.cap + (r - pre[f]);
-      kk[it] = static_cast<int>(e - int64_t(r) * epr);
-      rr[it] = r;
+      const uint32_t r = e / uepr;
+      const int f = wire_table(pre, w.F, static_cast<int>(r));
+      srow[it] = (static_cast<int64_t>(p) * w.F + f) * w.cap + (static_cast<int>(r) - pre[f]);
+      kk[it] = static_cast<int>(e - r * uepr);
+      rr[it] = static_cast<int>(r);
     }
   }
   if constexpr (UNPACK) {
@@ -714,6 +721,8 @@ static mrec_status wire_args(const int32_t *hdr, int32_t world, int32_t n_tables
                      cap_rows >= 1, "bad world / tables / cap");
   MREC_CHECK_ARG(rec_bytes % 4 == 0 && rec_bytes >= 4 && rec_bytes <= 72,
                  "record bytes must be a multiple of 4 in [4, 72]");
+  // the wire kernels index a part's elements (records x <= 64 dwords) in 32 bits
+  MREC_CHECK_ARG(static_cast<int64_t>(cap_rows) * 64 < (int64_t(1) << 31), "cap_rows too large");
   w->hdr = hdr;
   w->W = world;
   w->F = n_tables;
@@ -773,6 +782,7 @@ mrec_status mrec_shard_wire_unpack(const void *wire, int32_t rec_bytes, const in
   MREC_CHECK_ARG(slot_bytes % 4 == 0 && zero_bytes % 4 == 0 && zero_bytes >= 0,
                  "row pitches must be multiples of 4 bytes");
   MREC_CHECK_ARG(slot_bytes >= (to_f32 ? 2 : 1) * rec_bytes, "slot rows narrower than the record");
+  MREC_CHECK_ARG(slot_bytes <= 256 && zero_bytes <= 256, "slot / zero rows wider than 256 B");
   MREC_CHECK_ARG(!zero || zero_bytes > 0, "zero rows need their pitch");
   const int slot_dw = static_cast<int>(slot_bytes / 4), zero_dw = static_cast<int>(zero_bytes / 4);
   const dim3 g = wire_grid(w, std::max(slot_dw, zero ? zero_dw : 0));

@@ -307,6 +307,44 @@ def time_launches(fn, reps=100):
     return e0.elapsed_time(e1) / reps * 1e-3  # seconds per launch
 
 
+def tower_rooflines(model, step, datas, widths, B, steps=20):
+    """The dense tower's two launches timed INSIDE eager training steps (HIP events
+    around each launch on its stream, dense.KERNEL_EVENTS): the fused tower
+    (forward + input-gradient backward, 2 x 2 B sum_l n_l n_(l+1) flops) and the
+    weight gradients (2 B sum_l n_(l+1) (n_l + 1)).  The tower streams every layer's
+    bf16 weight images (forward + transposed) through each CU once: its bound is
+    the per-CU L2 read rate, reported beside the MFMA fraction."""
+    from pytorchrec_amd import dense as D
+    D.KERNEL_EVENTS = {}
+    try:
+        for i in range(steps):
+            step(datas[i % len(datas)])
+        torch.cuda.synchronize()
+        ev = D.KERNEL_EVENTS
+    finally:
+        D.KERNEL_EVENTS = None
+    L = len(widths) - 1
+    mm = sum(widths[l] * widths[l + 1] for l in range(L))
+    wimg = 2 * 2 * mm  # bf16 forward + transposed images
+    out = {}
+    for name, fl in (("mrec_tower_fwd_bwd", 2 * 2 * B * mm),
+                     ("mrec_tower_dw", 2 * B * sum(widths[l + 1] * (widths[l] + 1) for l in range(L)))):
+        pairs = ev.get(name, [])
+        if not pairs:
+            continue
+        ts = sorted(a.elapsed_time(b) * 1e-3 for a, b in pairs)
+        t = ts[len(ts) // 2]  # median over the eager steps
+        d = {"avg_us": round(t * 1e6, 3), "launches": len(ts), "flop": fl,
+             "TFLOP/s": round(fl / t / 1e12, 1), "frac_of_mfma_peak": round(fl / t / 1e12 / MFMA_PEAK_TFLOPS, 4),
+             "timing": "in-step (eager steps, HIP events around the launch, median)"}
+        if name == "mrec_tower_fwd_bwd":
+            d["weight_bytes_per_workgroup"] = wimg
+            d["per_CU_L2_GB/s"] = round(wimg / t / 1e9, 1)
+            d["bound"] = "per-CU L2 read rate (~70 GB/s per CU, MI355X_MICROARCH.md indexed-rows table)"
+        out[name] = d
+    return out
+
+
 def alg_bytes_per_sample(F, D, n_dense, first_order, es=2):
     """SURVEY.md §8(d) algorithmic bytes per sample, bf16 weights (es = 2; fp32
     tables es = 4), int32 ids:
@@ -881,6 +919,14 @@ def main():
                                           "GB/s": round(v[1] / v[0] / 1e9, 1),
                                           "as_implemented_bytes": v[2]}
                                       for k, v in ks.items()}
+    if rank == 0 and not args.no_roofline and args.model == "deepfm":
+        try:
+            lins = [m for m in model.mlp.modules() if isinstance(m, torch.nn.Linear)]
+            widths = [lins[0].in_features] + [m.out_features for m in lins]
+            result.setdefault("roofline_kernels", {}).update(
+                tower_rooflines(model, step, datas, widths, args.batch))
+        except Exception as e:  # a measurement aid: never fail the bench line
+            print(f"bench: tower timing skipped ({type(e).__name__}: {e})", file=sys.stderr)
     if rank == 0 and not args.no_roofline and args.model == "din":
         ks = din_rooflines(model, datas[0], args)
         name = max(ks, key=lambda k: ks[k][0])  # the dominant kernel

@@ -164,6 +164,32 @@ class _Call:
 
 _PENDING = []  # deferred split-K reductions (fused SGD of a layer's W, b and images)
 
+# measurement hook (bench.py): when a dict, the tower launches of eager steps are
+# bracketed by HIP events on their stream: {name: [(start, end), ...]}
+KERNEL_EVENTS = None
+
+
+class _timed:
+    def __init__(self, name):
+        self.name = name
+
+    def __enter__(self):
+        if KERNEL_EVENTS is not None:
+            # keep the queue busy (~80 us spin) so the start event and the launch are
+            # both queued when the GPU reaches them: the host's launch latency of an
+            # eager step is then outside the bracket
+            torch.cuda._sleep(200000)
+            self.e0 = torch.cuda.Event(enable_timing=True)
+            self.e0.record()
+        return self
+
+    def __exit__(self, *exc):
+        if KERNEL_EVENTS is not None:
+            e1 = torch.cuda.Event(enable_timing=True)
+            e1.record()
+            KERNEL_EVENTS.setdefault(self.name, []).append((self.e0, e1))
+        return False
+
 
 def launch_multi(calls):
     """Run ``calls`` plus the pending deferred reductions in as few launches as
@@ -1291,7 +1317,8 @@ class _TowerBCEFn(torch.autograd.Function):
         a.part, a.ldp = part.data_ptr(), ldp
         a.loss_part, a.ticket, a.loss = loss_part.data_ptr(), _ticket(dev).data_ptr(), loss.data_ptr()
         _set_cluster_ws(a, dev, B)
-        _mrec.call("mrec_tower_fwd_bwd", ctypes.byref(a), _mrec.stream_handle())
+        with _timed("mrec_tower_fwd_bwd"):
+            _mrec.call("mrec_tower_fwd_bwd", ctypes.byref(a), _mrec.stream_handle())
         ctx.save_for_backward(x0 if x0_img is None else x0_img, dz, part, dx0, *hs, *dhs)
         ctx.L, ctx.B, ctx.H, ctx.ns, ctx.widths = L, B, H, ns, widths
         ctx.tdw = tdw
@@ -1426,8 +1453,9 @@ def _tower_dw(calls, dhs, xin, widths, B: int, splits: int):
         a.dy_img[l], a.x_img[l] = dhs[l].data_ptr(), xin[l].data_ptr()
         a.ws[l], a.ldws[l] = c.ws.data_ptr(), (widths[l] + 1 + 7) // 8 * 8
     fin = _FINISH.pop(0) if _FINISH else None
-    _mrec.call("mrec_tower_dw", ctypes.byref(a), ctypes.byref(fin.struct) if fin else None,
-               _mrec.stream_handle())
+    with _timed("mrec_tower_dw"):
+        _mrec.call("mrec_tower_dw", ctypes.byref(a), ctypes.byref(fin.struct) if fin else None,
+                   _mrec.stream_handle())
     pend = _PENDING
     _PENDING = []
     for i in range(0, len(pend), 4):

@@ -563,6 +563,9 @@ class _Ctx:
     def save_for_backward(self, *a):
         pass
 
+    def set_materialize_grads(self, value):
+        pass
+
 
 # ----------------------------------------------------------------------------
 # PCIe-inclusive rate: the same step fed from host memory by the columnar loader

@@ -555,6 +555,9 @@ class _InteractFn(torch.autograd.Function):
         _raise_if_oob(flag)
         ctx.bank, ctx.ids, ctx.B, ctx.plan_ws = bank, ids, B, plan_ws
         ctx.fm2, ctx.first_order = fm2, first_order
+        # an output the model does not use (DCN-v2's logit) gets None, not a zero
+        # tensor autograd would fill with a kernel of its own every step
+        ctx.set_materialize_grads(False)
         ctx.save_for_backward(x0, fm_sum, dense)
         ctx.has_dense_w = dense_w is not None
         ctx.has_bias = bias is not None

@@ -32,7 +32,7 @@
 extern "C" {
 #endif
 
-#define MREC_ABI_VERSION 22
+#define MREC_ABI_VERSION 23
 #define MREC_MAX_TABLES 64      /* tables per table bank / per call */
 #define MREC_BWD_MAX_BATCH 8192  /* lookups per table per plan/apply call */
 #define MREC_BWD_HASH_MAX_BATCH 4096  /* batches up to this use the hash plan */
@@ -353,6 +353,20 @@ mrec_status mrec_emb_bwd_apply_given(const mrec_table_bank *bank, int64_t batch,
                                      mrec_bwd_mode mode, float lr, uint64_t seed,
                                      const uint64_t *d_step, void *grad, int32_t n_reduce,
                                      const struct mrec_gemm_call_s *reduce, mrec_stream stream);
+/* The owner's apply reading the received gradient RECORDS in place (ABI 23): no
+ * unpack to fp32 slots.  Entry j of part p (exchange view: b = p * chunk + j,
+ * chunk = cap, chunk_stride = the int32 per part of the ids message) of table f has
+ * its gradient in record p * cap_rows + pref[p * n_tables + f] + j of `wire`
+ * (rec_bytes each, wire_dtype BF16 or F32, 4-B aligned; pref from
+ * mrec_shard_gather_wire_ex).  Same sums, order and update as mrec_emb_bwd_apply_given
+ * on the unpacked slots (bit-identical). */
+mrec_status mrec_emb_bwd_apply_wire(const mrec_table_bank *bank, int64_t batch,
+                                    const void *workspace, size_t ws_bytes, const void *wire,
+                                    int32_t rec_bytes, mrec_dtype wire_dtype, const int32_t *pref,
+                                    int32_t cap_rows, int64_t chunk, int64_t chunk_stride,
+                                    mrec_bwd_mode mode, float lr, uint64_t seed,
+                                    const uint64_t *d_step, void *grad, int32_t n_reduce,
+                                    const struct mrec_gemm_call_s *reduce, mrec_stream stream);
 
 /* ------------------------------------------------------------------------- */
 /* Communicator (RCCL over xGMI) for the row-sharded exchange                  */
@@ -472,6 +486,14 @@ mrec_status mrec_shard_gather_wire(const mrec_table_bank *local, const int32_t *
                                    int32_t world, int32_t cap, int32_t cap_rows, void *wire,
                                    int32_t *d_overflow, const mrec_plan_job *plan,
                                    mrec_stream stream);
+/* the same, also writing pref [world][n_tables] int32: part p's table prefixes (record
+ * of entry j of table f in part p = p * cap_rows + pref[p][f] + j).  The gradient
+ * records the senders return have the layout of the ids they sent, so pref also
+ * addresses them for mrec_emb_bwd_apply_wire (ABI 23) */
+mrec_status mrec_shard_gather_wire_ex(const mrec_table_bank *local, const int32_t *recv_ids,
+                                      int32_t world, int32_t cap, int32_t cap_rows, void *wire,
+                                      int32_t *pref, int32_t *d_overflow,
+                                      const mrec_plan_job *plan, mrec_stream stream);
 /* wire records -> slot rows [(p * n_tables + f) * cap + j] (pitch slot_bytes; to_f32:
  * bf16 records widened to fp32); zero (may be NULL): zero_bytes of the same rows of a
  * second buffer are cleared (the sender's gradient sums) */

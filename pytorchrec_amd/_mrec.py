@@ -20,7 +20,7 @@ import torch  # noqa: F401  (must precede the dlopen, see module docstring)
 LIB_DIR = os.path.join(os.path.dirname(os.path.abspath(__file__)), "lib")
 LIB_PATH = os.environ.get("MREC_LIB_PATH") or os.path.join(LIB_DIR, "libmrec.so")
 
-ABI_VERSION = 22
+ABI_VERSION = 23
 MAX_TABLES = 64
 BWD_MAX_BATCH = 8192
 BWD_HASH_MAX_BATCH = 4096  # batches up to this use the hash plan (fusable into a GEMM launch)
@@ -233,6 +233,10 @@ SIGNATURES = {
                                                 _i64, _vp, _vp, _i64, _i64, _i64, ctypes.c_int,
                                                 _f32, ctypes.c_uint64, _vp, _vp, _i32,
                                                 ctypes.POINTER(GemmCall), _vp]),
+    "mrec_emb_bwd_apply_wire": (ctypes.c_int, [_bank_p, _i64, _vp, ctypes.c_size_t, _vp, _i32, _i32,
+                                               _vp, _i32, _i64, _i64, ctypes.c_int, _f32,
+                                               ctypes.c_uint64, _vp, _vp, _i32,
+                                               ctypes.POINTER(GemmCall), _vp]),
     "mrec_shard_bucketize": (ctypes.c_int, [_ids_p, _i32, ctypes.POINTER(ctypes.c_int64), _i64,
                                             _i32, _i32, _vp, _vp, _vp, _vp, _vp]),
     "mrec_shard_gather": (ctypes.c_int, [_bank_p, _vp, _i32, _i32, _vp, _vp]),
@@ -306,6 +310,8 @@ SIGNATURES = {
     "mrec_shard_wire_bytes": (_i32, [_i32, _i32, _i32]),
     "mrec_shard_gather_wire": (ctypes.c_int, [_bank_p, _vp, _i32, _i32, _i32, _vp, _vp,
                                               ctypes.POINTER(PlanJob), _vp]),
+    "mrec_shard_gather_wire_ex": (ctypes.c_int, [_bank_p, _vp, _i32, _i32, _i32, _vp, _vp, _vp,
+                                                 ctypes.POINTER(PlanJob), _vp]),
     "mrec_shard_wire_unpack": (ctypes.c_int, [_vp, _i32, _vp, _i32, _i32, _i32, _i32, _vp, _i64,
                                               _i32, _vp, _i64, _vp, _vp]),
     "mrec_shard_wire_pack": (ctypes.c_int, [_vp, _i64, _i32, _vp, _i32, _i32, _i32, _i32, _vp, _vp,

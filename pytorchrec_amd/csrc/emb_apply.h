@@ -28,8 +28,47 @@ struct ApplyArgs {
   int64_t g_ld;
   int64_t chunk;
   int64_t chunk_stride;
+  // or read straight from the received wire records (ABI 23, owner side of the
+  // compact exchange): entry j of part p, table f -> record p * cap_rows +
+  // pref[p * F + f] + j (p = b / chunk, j = b % chunk), pitch g_rec_pitch elements
+  const void *g_rec;
+  int g_rec_bf16;
+  int g_rec_pitch;
+  const int32_t *g_pref;
+  int64_t g_cap_rows;
+  int g_F;
   OptArgs opt;
 };
+
+// a given gradient from a wire record (4-B aligned rows: records are not 16-B)
+template <int EPL>
+__device__ __forceinline__ void wire_grad(const ApplyArgs &a, int64_t b, int f, int D, int e0,
+                                          bool v_lane, bool w_lane, float *g) {
+  const int64_t p = b / a.chunk, j = b - p * a.chunk;
+  const int64_t rec = p * a.g_cap_rows + a.g_pref[p * a.g_F + f] + j;
+  if (a.g_rec_bf16) {
+    const uint16_t *go = static_cast<const uint16_t *>(a.g_rec) + rec * a.g_rec_pitch;
+    if (v_lane) {
+      const uint32_t *q = reinterpret_cast<const uint32_t *>(go + e0);
+#pragma unroll
+      for (int i = 0; i < EPL / 2; ++i) {
+        const uint32_t x = q[i];
+        g[2 * i] = __uint_as_float(x << 16);
+        g[2 * i + 1] = __uint_as_float(x & 0xffff0000u);
+      }
+    } else if (w_lane) {
+      g[0] = __uint_as_float(static_cast<uint32_t>(go[D]) << 16);
+    }
+  } else {
+    const float *go = static_cast<const float *>(a.g_rec) + rec * a.g_rec_pitch;
+    if (v_lane) {
+#pragma unroll
+      for (int i = 0; i < EPL; ++i) g[i] = go[e0 + i];
+    } else if (w_lane) {
+      g[0] = go[D];
+    }
+  }
+}
 
 template <int EPL>
 __device__ __forceinline__ void load_f32xN(const float *p, float *v) {
@@ -62,6 +101,10 @@ __device__ __forceinline__ void lookup_grad(const ApplyArgs &a, int64_t b, int f
                                             bool v_lane, bool w_lane, float *g) {
 #pragma unroll
   for (int j = 0; j < EPL; ++j) g[j] = 0.f;
+  if (a.g_rec) {
+    wire_grad<EPL>(a, b, f, D, e0, v_lane, w_lane, g);
+    return;
+  }
   if (a.g_occ) {
     const int64_t idx = a.chunk ? (b / a.chunk) * a.chunk_stride + f * a.chunk + b % a.chunk : b;
     const float *go = a.g_occ + idx * a.g_ld;
@@ -105,6 +148,10 @@ __device__ __forceinline__ void lookup_grad_v(const ApplyArgs &a, int64_t b, int
                                               bool v_lane, bool w_lane, const float *v, float *g) {
 #pragma unroll
   for (int j = 0; j < EPL; ++j) g[j] = 0.f;
+  if (a.g_rec) {
+    wire_grad<EPL>(a, b, f, D, e0, v_lane, w_lane, g);
+    return;
+  }
   if (a.g_occ) {
     const int64_t idx = a.chunk ? (b / a.chunk) * a.chunk_stride + f * a.chunk + b % a.chunk : b;
     const float *go = a.g_occ + idx * a.g_ld;

@@ -553,7 +553,7 @@ __global__ __launch_bounds__(256, MREC_APPLY_WAVES) void apply_hash_kernel(BankA
   float dfm_c = 0.f;
 #pragma unroll
   for (int j = 0; j < EPL; ++j) gdx[j] = fs[j] = 0.f;
-  const bool pre = live && !a.g_occ;
+  const bool pre = live && !a.g_occ && !a.g_rec;
   if (pre) {
     if (v_lane) {
       const int64_t col = static_cast<int64_t>(f) * D + e0;
@@ -821,6 +821,14 @@ mrec_status mrec_emb_bwd_plan(const mrec_table_bank *bank, const mrec_ids *ids, 
 
 }  // extern "C"
 
+struct GivenWire {  // mrec_emb_bwd_apply_wire: given gradients as wire records
+  const void *wire;
+  int bf16;
+  int pitch;  // elements per record
+  const int32_t *pref;
+  int64_t cap_rows;
+};
+
 static mrec_status apply_impl(const mrec_table_bank *bank, int64_t batch, const void *workspace,
                               size_t ws_bytes, const void *dx, mrec_dtype dx_dtype, int64_t dx_ld,
                               const float *dfm, const float *fm_sum, const void *x0,
@@ -828,7 +836,8 @@ static mrec_status apply_impl(const mrec_table_bank *bank, int64_t batch, const 
                               const float *g_occ, int64_t g_ld, int64_t chunk,
                               int64_t chunk_stride, mrec_bwd_mode mode, float lr, uint64_t seed,
                               const uint64_t *d_step, void *grad, int32_t n_reduce,
-                              const mrec_gemm_call *reduce, mrec_stream stream);
+                              const mrec_gemm_call *reduce, mrec_stream stream,
+                              const GivenWire *gw = nullptr);
 
 extern "C" {
 
@@ -870,6 +879,22 @@ mrec_status mrec_emb_bwd_apply_given(const mrec_table_bank *bank, int64_t batch,
                     grad, n_reduce, reduce, stream);
 }
 
+mrec_status mrec_emb_bwd_apply_wire(const mrec_table_bank *bank, int64_t batch,
+                                    const void *workspace, size_t ws_bytes, const void *wire,
+                                    int32_t rec_bytes, mrec_dtype wire_dtype, const int32_t *pref,
+                                    int32_t cap_rows, int64_t chunk, int64_t chunk_stride,
+                                    mrec_bwd_mode mode, float lr, uint64_t seed,
+                                    const uint64_t *d_step, void *grad, int32_t n_reduce,
+                                    const mrec_gemm_call *reduce, mrec_stream stream) {
+  MREC_CHECK_ARG(wire_dtype == MREC_BF16 || wire_dtype == MREC_F32, "wire dtype must be BF16/F32");
+  const int es = wire_dtype == MREC_BF16 ? 2 : 4;
+  MREC_CHECK_ARG(rec_bytes > 0 && rec_bytes % es == 0 && rec_bytes % 4 == 0, "bad record bytes");
+  const GivenWire gw{wire, wire_dtype == MREC_BF16 ? 1 : 0, rec_bytes / es, pref, cap_rows};
+  return apply_impl(bank, batch, workspace, ws_bytes, nullptr, MREC_F32, 0, nullptr, nullptr,
+                    nullptr, MREC_F32, 0, nullptr, nullptr, 0, chunk, chunk_stride, mode, lr, seed,
+                    d_step, grad, n_reduce, reduce, stream, &gw);
+}
+
 }  // extern "C"
 
 static mrec_status apply_impl(const mrec_table_bank *bank, int64_t batch, const void *workspace,
@@ -879,7 +904,8 @@ static mrec_status apply_impl(const mrec_table_bank *bank, int64_t batch, const 
                               const float *g_occ, int64_t g_ld, int64_t chunk,
                               int64_t chunk_stride, mrec_bwd_mode mode, float lr, uint64_t seed,
                               const uint64_t *d_step, void *grad, int32_t n_reduce,
-                              const mrec_gemm_call *reduce, mrec_stream stream) {
+                              const mrec_gemm_call *reduce, mrec_stream stream,
+                              const GivenWire *gw) {
   BankArgs ba;
   int eb, lpr;
   mrec_status st = make_bank_args(bank, &ba, &eb, &lpr);
@@ -912,6 +938,14 @@ static mrec_status apply_impl(const mrec_table_bank *bank, int64_t batch, const 
                    "x0/fm_sum must be 16B aligned with 16B-multiple rows");
   }
   MREC_CHECK_ARG(dw == nullptr || ba.has_w, "dw given but bank has no w column");
+  if (gw) {
+    MREC_CHECK_ARG(!dx && !dfm && !dw && !g_occ, "wire gradients exclude dx / dfm / dw / g_occ");
+    MREC_CHECK_ARG(gw->wire && gw->pref && gw->cap_rows >= 1, "NULL wire / pref");
+    MREC_CHECK_ARG(gw->pitch >= D + (ba.has_w ? 1 : 0) && (gw->pitch * (gw->bf16 ? 2 : 4)) % 4 == 0 &&
+                       (reinterpret_cast<uintptr_t>(gw->wire) & 3) == 0,
+                   "records: pitch >= dim + has_w elements, 4-B aligned");
+    MREC_CHECK_ARG(chunk >= 1 && chunk_stride >= F * chunk, "bad chunk");
+  }
   if (g_occ) {
     MREC_CHECK_ARG(!dx && !dfm && !dw, "g_occ excludes dx / dfm / dw");
     MREC_CHECK_ARG(g_ld >= D + (ba.has_w ? 1 : 0) && g_ld % 4 == 0 &&
@@ -938,13 +972,19 @@ static mrec_status apply_impl(const mrec_table_bank *bank, int64_t batch, const 
   a.g_ld = g_ld;
   a.chunk = chunk;
   a.chunk_stride = chunk_stride;
+  a.g_rec = gw ? gw->wire : nullptr;
+  a.g_rec_bf16 = gw ? gw->bf16 : 0;
+  a.g_rec_pitch = gw ? gw->pitch : 0;
+  a.g_pref = gw ? gw->pref : nullptr;
+  a.g_cap_rows = gw ? gw->cap_rows : 0;
+  a.g_F = F;
   a.opt = opt;
   hipStream_t s = static_cast<hipStream_t>(stream);
   const int wpb = 256 / lpr;
   // hash layout (batch <= kHashMaxKeys or an exchange view, see mrec_emb_bwd_plan):
   // sample-major blocks + one hot-segment block per (table, bucket); sorted
   // layout: one block per WPB segments of each table
-  const bool hash = hash_layout(batch, g_occ != nullptr);  // given grads: an exchange view
+  const bool hash = hash_layout(batch, g_occ != nullptr || gw != nullptr);  // given: an exchange view
   const int seg_blocks = hash ? (batch > 0 ? F * kPlanBuckets : 0)
                               : static_cast<int>((batch + wpb - 1) / wpb);
   const int64_t sm_blocks = hash ? (batch * F + wpb - 1) / wpb : 0;

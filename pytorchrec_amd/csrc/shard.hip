@@ -294,6 +294,7 @@ constexpr int kWireElems = kWireThreads * kWirePer;
 struct WireArgs {
   const int32_t *hdr;  // W parts of F*cap + F (counts at F*cap + f)
   int W, F, cap, cap_rows;
+  int32_t *pref;  // gather: [W][F] per-part table prefixes written here (NULL: not)
   int rec_dw;          // dwords per record
   int32_t *overflow;
 };
@@ -363,6 +364,7 @@ __global__ __launch_bounds__(kWireThreads) void gather_wire_kernel(BankArgs bank
     nrows[threadIdx.x] = bank.rows[threadIdx.x];
   }
   const int tot = wire_prefix(w, p, pre);  // (its barrier covers roff / nrows too)
+  if (w.pref && cx == 0 && threadIdx.x < w.F) w.pref[p * w.F + threadIdx.x] = pre[threadIdx.x];
   // element indices fit 32 bits (checked on the host): 32-bit divisions, not 64-bit
   const uint32_t n = static_cast<uint32_t>(tot) * static_cast<uint32_t>(w.rec_dw);
   const uint32_t e0 = static_cast<uint32_t>(cx) * kWireElems + threadIdx.x;
@@ -730,6 +732,7 @@ static mrec_status wire_args(const int32_t *hdr, int32_t world, int32_t n_tables
   w->cap_rows = cap_rows;
   w->rec_dw = rec_bytes / 4;
   w->overflow = d_overflow;
+  w->pref = nullptr;
   return MREC_OK;
 }
 
@@ -737,6 +740,14 @@ mrec_status mrec_shard_gather_wire(const mrec_table_bank *local, const int32_t *
                                    int32_t world, int32_t cap, int32_t cap_rows, void *wire,
                                    int32_t *d_overflow, const mrec_plan_job *plan,
                                    mrec_stream stream) {
+  return mrec_shard_gather_wire_ex(local, recv_ids, world, cap, cap_rows, wire, nullptr, d_overflow,
+                                   plan, stream);
+}
+
+mrec_status mrec_shard_gather_wire_ex(const mrec_table_bank *local, const int32_t *recv_ids,
+                                      int32_t world, int32_t cap, int32_t cap_rows, void *wire,
+                                      int32_t *pref, int32_t *d_overflow,
+                                      const mrec_plan_job *plan, mrec_stream stream) {
   BankArgs ba;
   int eb, lpr;
   mrec_status st = make_bank_args(local, &ba, &eb, &lpr);
@@ -750,6 +761,7 @@ mrec_status mrec_shard_gather_wire(const mrec_table_bank *local, const int32_t *
   WireArgs w;
   st = wire_args(recv_ids, world, ba.n_tables, cap, cap_rows, rec, d_overflow, &w);
   if (st != MREC_OK) return st;
+  w.pref = pref;
   const dim3 g = wire_grid(w, w.rec_dw);
   const int chunks = static_cast<int>(g.x);
   PlanJob job{};

@@ -414,15 +414,17 @@ def shard_bucketize_dedup(bank: ShardedEmbeddingBank, ids: Sequence[torch.Tensor
 
 
 def shard_gather_wire(bank: ShardedEmbeddingBank, recv_ids: torch.Tensor,
-                      plan_job=None) -> torch.Tensor:
+                      plan_job=None, pref: Optional[torch.Tensor] = None) -> torch.Tensor:
     """Owner: one record per received distinct id -> [W, cap_rows * record] bytes.
     ``plan_job`` (owner_plan_job) runs the owner's backward plan over the same ids in
-    leading workgroups of the launch."""
+    leading workgroups of the launch; ``pref`` (int32 [W, n_tables]) receives each
+    part's table prefixes (mrec_shard_gather_wire_ex), which address the gradient
+    records the senders return (owner_apply_wire)."""
     W, rb = bank.world, bank.wire_bytes()
     wire = torch.empty(W, bank.cap_rows * rb, dtype=torch.uint8, device=bank.weight.device)
     fl = bank.flags()
-    _mrec.call("mrec_shard_gather_wire", bank.desc().ref(), recv_ids.data_ptr(), W, bank.cap,
-               bank.cap_rows, wire.data_ptr(), fl.data_ptr(),
+    _mrec.call("mrec_shard_gather_wire_ex", bank.desc().ref(), recv_ids.data_ptr(), W, bank.cap,
+               bank.cap_rows, wire.data_ptr(), _mrec.ptr(pref), fl.data_ptr(),
                ctypes.byref(plan_job) if plan_job is not None else None, _mrec.stream_handle())
     return wire
 
@@ -614,6 +616,32 @@ def owner_apply(bank: ShardedEmbeddingBank, plan, g_recv: torch.Tensor,
     del jobs
 
 
+def owner_apply_wire(bank: ShardedEmbeddingBank, plan, wire_g: torch.Tensor, pref: torch.Tensor,
+                     lr: Optional[float] = None, grad: Optional[torch.Tensor] = None):
+    """owner_apply reading the received gradient records in place
+    (mrec_emb_bwd_apply_wire: no unpack to fp32 slots; same sums and update)."""
+    ws, wsb = plan
+    F, W, cap = bank.n_tables, bank.world, bank.cap
+    if grad is not None:
+        mode, lr = _mrec.BWD_DENSE_GRAD, 0.0
+    elif lr is not None:
+        mode = (_mrec.BWD_SGD_SR if (bank.stochastic_rounding and
+                                     bank.weight.dtype == torch.bfloat16) else _mrec.BWD_SGD)
+    else:
+        mode, lr = bank.apply_mode()
+        if mode in (_mrec.BWD_SGD, _mrec.BWD_SGD_SR):
+            lr = lr / W
+    from pytorchrec_amd import dense as dense_ops
+    jobs = dense_ops.take_pending(4)
+    arr = (_mrec.GemmCall * len(jobs))(*[j.struct() for j in jobs]) if jobs else None
+    _mrec.call("mrec_emb_bwd_apply_wire", bank.desc().ref(), W * cap, ws.data_ptr(), wsb,
+               wire_g.data_ptr(), bank.wire_bytes(), _mrec.dtype_code(bank.weight.dtype),
+               pref.data_ptr(), bank.cap_rows, cap, F * cap, mode, float(lr), bank.next_seed(),
+               bank.step_counter().data_ptr(), _mrec.ptr(grad), len(jobs), arr,
+               _mrec.stream_handle())
+    del jobs
+
+
 # ----------------------------------------------------------------------------
 # autograd (GPU)
 # ----------------------------------------------------------------------------
@@ -636,7 +664,9 @@ class _CompactInteractFn(torch.autograd.Function):
         ojob_ok = train and bank.world * bank.cap <= _mrec.BWD_MAX_BATCH
         ojob, oplan, okeep = (owner_plan_job(bank, recv, bank.part) if ojob_ok
                               else (None, None, None))
-        wire = comm.exchange(shard_gather_wire(bank, recv, plan_job=ojob))
+        pref = (torch.empty(bank.world, bank.n_tables, dtype=torch.int32, device=dev)
+                if train else None)
+        wire = comm.exchange(shard_gather_wire(bank, recv, plan_job=ojob, pref=pref))
         del okeep
         n = bank.world * bank.n_tables * bank.cap
         rows_recv = torch.empty(n, bank.row_stride, dtype=bank.weight.dtype, device=dev)
@@ -659,6 +689,7 @@ class _CompactInteractFn(torch.autograd.Function):
         ctx.fm2, ctx.first_order = fm2, first_order
         ctx.has_dense_w, ctx.has_bias = dense_w is not None, bias is not None
         ctx.dense_w, ctx.bias = dense_w, bias
+        ctx.pref = pref
         ctx.save_for_backward(x0, fm_sum, dense, pos, send, recv, rows_recv, gsum)
         if x0 is None:
             return logit
@@ -682,10 +713,8 @@ class _CompactInteractFn(torch.autograd.Function):
             sender_grad_sums(bank, rows_recv, pos, ctx.splan, gsum, dx=dx0, dfm=dfm,
                              fm_sum=fm_sum, x0=x0 if dfm is not None else None, dw=dw)
             wire_g = bank.comm.exchange(shard_wire_pack(bank, gsum, send))
-            g_recv = torch.empty(bank.world * bank.n_tables * bank.cap, bank.g_ld,
-                                 dtype=torch.float32, device=gsum.device)
-            shard_wire_unpack(bank, wire_g, recv, g_recv, to_f32=gsum.dtype != torch.float32)
-            owner_apply(bank, ctx.oplan, g_recv)
+            # the owner reads the gradient records in place (no unpack launch)
+            owner_apply_wire(bank, ctx.oplan, wire_g, ctx.pref)
         g_dense_w, g_bias = _dense_first_order_grads(ctx, dlogit, dense)
         return g_dense_w, g_bias, None, None, None, None, None, None, None, None
 

@@ -370,7 +370,8 @@ def test_compact_exchange_simulated_bit_exact(gpu, W, zipf, B):
         ref_send, ref_pos = S.cpu_bucketize_dedup(banks[r], [t.cpu() for t in ids[r]])
         assert torch.equal(sends[r].cpu(), ref_send) and torch.equal(poss[r].cpu(), ref_pos), r
     recvs = _exchange(list(sends), W)
-    wires = _exchange([S.shard_gather_wire(banks[r], recvs[r]) for r in range(W)], W)
+    prefs = [torch.empty(W, len(ROWS), dtype=torch.int32, device=gpu) for _ in range(W)]
+    wires = _exchange([S.shard_gather_wire(banks[r], recvs[r], pref=prefs[r]) for r in range(W)], W)
     n = W * F * banks[0].cap
     rows, gsums, outs, plans, oplans = [], [], [], [], []
     for r in range(W):
@@ -426,13 +427,23 @@ def test_compact_exchange_simulated_bit_exact(gpu, W, zipf, B):
         own = torch.zeros_like(banks[r].weight)
         S.owner_apply(banks[r], oplans[r], g_recv, grad=own)
         banks[r].check_flags()
+        # the same sums read from the received records in place (no unpack)
+        own_w = torch.zeros_like(banks[r].weight)
+        S.owner_apply_wire(banks[r], oplans[r], wire_g[r], prefs[r], grad=own_w)
+        assert torch.equal(own_w.view(torch.int16), own.view(torch.int16)), r
         for f, (o, cnt) in enumerate(zip(banks[r].row_offset, banks[r].category_nums)):
             want = tot[glob.row_offset[f]:glob.row_offset[f] + ROWS[f]][r::W, :D + 1]
             assert torch.equal(own[o:o + cnt, :D + 1], want.to(torch.bfloat16)), (r, f)
         # fused SGD from the same sums: within one bf16 ulp of w - lr * sum
         lr = 0.5
         before = banks[r].weight.detach().clone()
+        S.owner_apply_wire(banks[r], oplans[r], wire_g[r], prefs[r], lr)
+        after_wire = banks[r].weight.detach().clone()
+        with torch.no_grad():
+            banks[r].weight.copy_(before)
         S.owner_apply(banks[r], oplans[r], g_recv, lr)
+        # bitwise (the shard's pad columns hold uninitialised bits, NaNs included)
+        assert torch.equal(banks[r].weight.view(torch.int16), after_wire.view(torch.int16)), r
         for f, (o, cnt) in enumerate(zip(banks[r].row_offset, banks[r].category_nums)):
             g = tot[glob.row_offset[f]:glob.row_offset[f] + ROWS[f]][r::W, :D + 1].double()
             w0 = before[o:o + cnt, :D + 1].double()

@@ -1221,13 +1221,17 @@ def _tdw_tiles(widths) -> int:
 
 def _tdw_splits(B: int, widths=None) -> int:
     """K slices of mrec_tower_dw (0: not used): about 640 one-wave workgroups (2.5
-    per CU) over the tiles, slices of >= 256 rows, at most 64.  4 for the C2 tower
-    (147 tiles; 8 slices ran no faster and double the slabs the reduction reads), 64
-    for DIN's attention unit (8 tiles over 204,800 rows)."""
+    per CU) over the tiles, slices of >= 256 rows, at most 64 and at most B / 1024
+    (but 4 allowed): the REDUCE that follows reads every slice's slab, and for a small
+    tower it is the longer part.  4 for the C2 tower (147 tiles; 8 slices ran no
+    faster and double the slabs the reduction reads) and for DIN's top tower (16
+    tiles: 16 slices 0.2256-0.2258 ms/step, 8: 0.2245-0.2252, 4: 0.2233-0.2240), 64
+    for DIN's layered attention unit (8 tiles over 204,800 rows)."""
     if os.environ.get("MREC_TOWER_DW", "1") == "0" or B < 256:
         return 0
     env = os.environ.get("MREC_TDW_SPLITS")  # A/B knob
-    want = int(env) if env else (4 if widths is None else max(1, min(64, 640 // _tdw_tiles(widths))))
+    want = int(env) if env else (4 if widths is None else
+                                 max(1, min(64, 640 // _tdw_tiles(widths), max(4, B // 1024))))
     for s in range(want, 1, -1):
         if B // s >= 256 and _eff_split(B, s) == s:
             return s

@@ -32,7 +32,7 @@
 extern "C" {
 #endif
 
-#define MREC_ABI_VERSION 23
+#define MREC_ABI_VERSION 24
 #define MREC_MAX_TABLES 64      /* tables per table bank / per call */
 #define MREC_BWD_MAX_BATCH 8192  /* lookups per table per plan/apply call */
 #define MREC_BWD_HASH_MAX_BATCH 4096  /* batches up to this use the hash plan */
@@ -317,6 +317,23 @@ mrec_status mrec_emb_bwd_large_fused(const mrec_table_bank *bank, const mrec_ids
                                      const uint64_t *d_step, void *grad, mrec_stream stream);
 
 struct mrec_gemm_call_s; /* mrec_gemm_call, defined with the GEMM entry points below */
+
+/*
+ * mrec_emb_bwd_large_fused plus up to 4 deferred split-K weight-gradient reductions
+ * (phase MREC_GEMM_REDUCE, as for mrec_emb_bwd_apply_ex) run by workgroups after
+ * the bucket kernel's own (ABI 24): DIN's top-tower dW reduce + fused SGD leaves
+ * its standalone launch.  They must not touch what the update reads or writes.  On
+ * the two-call path (and for batch 0) they run as one mrec_gemm_multi after it.
+ */
+mrec_status mrec_emb_bwd_large_fused_ex(const mrec_table_bank *bank, const mrec_ids *ids,
+                                        int64_t batch, void *workspace, size_t ws_bytes,
+                                        int32_t *d_oob_flag, const void *dx, mrec_dtype dx_dtype,
+                                        int64_t dx_ld, const float *dfm, const float *fm_sum,
+                                        const void *x0, mrec_dtype x0_dtype, int64_t x0_ld,
+                                        const float *dw, mrec_bwd_mode mode, float lr,
+                                        uint64_t seed, const uint64_t *d_step, void *grad,
+                                        int32_t n_reduce, const struct mrec_gemm_call_s *reduce,
+                                        mrec_stream stream);
 
 /*
  * mrec_emb_bwd_apply plus up to 2 deferred split-K weight-gradient reductions

@@ -20,7 +20,7 @@ import torch  # noqa: F401  (must precede the dlopen, see module docstring)
 LIB_DIR = os.path.join(os.path.dirname(os.path.abspath(__file__)), "lib")
 LIB_PATH = os.environ.get("MREC_LIB_PATH") or os.path.join(LIB_DIR, "libmrec.so")
 
-ABI_VERSION = 23
+ABI_VERSION = 24
 MAX_TABLES = 64
 BWD_MAX_BATCH = 8192
 BWD_HASH_MAX_BATCH = 4096  # batches up to this use the hash plan (fusable into a GEMM launch)
@@ -269,6 +269,11 @@ SIGNATURES = {
                                                 _vp, ctypes.c_int, _i64, _vp, _vp, _vp,
                                                 ctypes.c_int, _i64, _vp, ctypes.c_int, _f32,
                                                 ctypes.c_uint64, _vp, _vp, _vp]),
+    "mrec_emb_bwd_large_fused_ex": (ctypes.c_int, [_bank_p, _ids_p, _i64, _vp, ctypes.c_size_t,
+                                                   _vp, _vp, ctypes.c_int, _i64, _vp, _vp, _vp,
+                                                   ctypes.c_int, _i64, _vp, ctypes.c_int, _f32,
+                                                   ctypes.c_uint64, _vp, _vp, _i32,
+                                                   ctypes.POINTER(GemmCall), _vp]),
     "mrec_head_fwd": (ctypes.c_int, [_vp, _i64, _i64, _i32, _vp, _vp, _vp, _vp, _vp]),
     "mrec_head_bwd": (ctypes.c_int, [_vp, _vp, _i64, _i32, _vp, _i64, _vp, _i64, _vp]),
     "mrec_bce_fwd": (ctypes.c_int, [_vp, _vp, _i64, _vp, _vp]),

@@ -215,10 +215,7 @@ __global__ __launch_bounds__(kPlanThreads) void plan_hash_kernel(BankArgs bank, 
 // ---------------------------------------------------------------------------
 // apply (helpers in emb_apply.h)
 // ---------------------------------------------------------------------------
-// deferred split-K weight-gradient reductions (+ fused SGD) run by trailing
-// workgroups of the apply launch: independent of the embedding update, and a
-// launch of their own would cost a kernel boundary on the step's serial path
-constexpr int kMaxCoReduce = 4;
+// deferred split-K reductions ride in trailing workgroups (CoReduce, gemm_common.h)
 // hot segments (> short_seg lookups) of a (table, bucket) are spread over kHotPer
 // workgroups of their own (segment k by workgroup k % kHotPer), so a bucket's hot
 // rows are summed in parallel instead of one after another by its segment block
@@ -226,21 +223,6 @@ constexpr int kMaxCoReduce = 4;
 #define MREC_HOT_PER 4
 #endif
 constexpr int kHotPer = MREC_HOT_PER;
-struct CoReduce {
-  int n;
-  int nblk[kMaxCoReduce];
-  int start[kMaxCoReduce + 1];  // workgroup offsets after the apply blocks
-  GemmArgs g[kMaxCoReduce];
-};
-
-__device__ __forceinline__ bool co_reduce(const CoReduce &co, int b) {
-  int p = 0;
-  while (p + 1 < co.n && b >= co.start[p + 1]) ++p;
-  const int local = b - co.start[p];
-  if (local < co.nblk[p]) splitk_reduce_body<false>(co.g[p], local, co.nblk[p]);
-  return true;
-}
-
 // One hot segment (> kShortSeg lookups) summed by the whole workgroup, in a
 // fixed order independent of how the plan listed it: the samples go into an LDS
 // bitmap of the batch (<= kHashMaxEntries), worker w sums the w-th, (w + WPB)-th
@@ -993,19 +975,8 @@ static mrec_status apply_impl(const mrec_table_bank *bank, int64_t batch, const 
                            : static_cast<int64_t>(seg_blocks) * F);
   CoReduce co = {};
   int co_blocks = 0;
-  MREC_CHECK_ARG(n_reduce >= 0 && n_reduce <= kMaxCoReduce && (n_reduce == 0 || reduce),
-                 "n_reduce out of [0, 4]");
-  for (int i = 0; i < n_reduce; ++i) {
-    int64_t nb = 0;
-    mrec_status st = build_reduce_job(reduce[i], &co.g[co.n], &nb);
-    if (st != MREC_OK) return st;
-    if (nb == 0) continue;
-    co.nblk[co.n] = static_cast<int>(nb);
-    co.start[co.n] = co_blocks;
-    co_blocks += static_cast<int>(nb);
-    ++co.n;
-  }
-  co.start[co.n] = co_blocks;
+  if (mrec_status st = build_co_reduce(n_reduce, reduce, &co, &co_blocks); st != MREC_OK)
+    return st;
   if (apply_blocks + co_blocks == 0) return MREC_OK;  // (batch 0 still runs the reductions)
   const dim3 grid(static_cast<unsigned>(apply_blocks + co_blocks));
 #define MREC_AKM(T, L, M) \

@@ -27,6 +27,7 @@
 
 #include "common.h"
 #include "emb_apply.h"
+#include "gemm_common.h"
 
 namespace mrec {
 
@@ -994,7 +995,7 @@ constexpr int kBkLdsPerm = 4096;  // a bucket's placed lookups stay in LDS up to
 
 template <typename T, int LPR>
 __global__ __launch_bounds__(256) void bk_apply_kernel(BankArgs bank, LgWs w, ApplyArgs a, int G,
-                                                       int lognb) {
+                                                       int lognb, CoReduce co) {
   __shared__ uint32_t key[kBkSlots];
   __shared__ int32_t cur[kBkSlots];   // counts, then placement cursors (end = start + count)
   __shared__ int32_t seg[kBkSlots];   // segment start inside the bucket
@@ -1008,6 +1009,10 @@ __global__ __launch_bounds__(256) void bk_apply_kernel(BankArgs bank, LgWs w, Ap
   if (a.d_step) a.seed += *a.d_step * 0x9e3779b97f4a7c15ull;
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int NB = 1 << lognb;
+  if (static_cast<int>(blockIdx.x) >= NB) {  // trailing workgroups: deferred MLP reductions
+    co_reduce(co, blockIdx.x - NB);
+    return;
+  }
   const int32_t *pub = w.bhist + static_cast<int64_t>(G) * NB;
   const int lo = pub[blockIdx.x], hi = pub[blockIdx.x + 1];
   for (int k = tid; k < kBkSlots; k += 256) {
@@ -1312,10 +1317,11 @@ static mrec_status lg_apply_args(const mrec_table_bank *bank, const BankArgs &ba
 // per-row apply then walks only the huge segments' slots)
 template <typename T, int L>
 static void lg_launch_apply(const BankArgs &ba, int64_t batch, const LgWs &w, const ApplyArgs &a,
-                            int stride, int fused_nb, int G, int lognb, hipStream_t s) {
+                            int stride, int fused_nb, int G, int lognb, const CoReduce &co,
+                            int co_blocks, hipStream_t s) {
   dim3 gc(kLgApplyBlocks), gu(kLgApplyBlocks);
   if (fused_nb) {
-    bk_apply_kernel<T, L><<<dim3(fused_nb), 256, 0, s>>>(ba, w, a, G, lognb);
+    bk_apply_kernel<T, L><<<dim3(fused_nb + co_blocks), 256, 0, s>>>(ba, w, a, G, lognb, co);
     // only huge segments are left: as many workgroups as their slots (mostly holes)
     const int64_t N = batch * ba.n_tables;
     const int64_t ul = (N + kLgHuge) / (kLgHuge + 1) + 1;
@@ -1342,8 +1348,10 @@ static void lg_launch_apply(const BankArgs &ba, int64_t batch, const LgWs &w, co
 
 static void lg_dispatch_apply(mrec_dtype dtype, int lpr, const BankArgs &ba, int64_t batch,
                               const LgWs &w, const ApplyArgs &a, int stride, int fused_nb, int G,
-                              int lognb, hipStream_t s) {
-#define MREC_LG(T, L) lg_launch_apply<T, L>(ba, batch, w, a, stride, fused_nb, G, lognb, s)
+                              int lognb, hipStream_t s, const CoReduce &co = CoReduce{},
+                              int co_blocks = 0) {
+#define MREC_LG(T, L) \
+  lg_launch_apply<T, L>(ba, batch, w, a, stride, fused_nb, G, lognb, co, co_blocks, s)
   if (dtype == MREC_BF16) {
     switch (lpr) {
       case 1: MREC_LG(uint16_t, 1); break;
@@ -1390,13 +1398,15 @@ mrec_status mrec_emb_bwd_large_apply(const mrec_table_bank *bank, int64_t batch,
   return launch_status("mrec_emb_bwd_large_apply");
 }
 
-mrec_status mrec_emb_bwd_large_fused(const mrec_table_bank *bank, const mrec_ids *ids,
-                                     int64_t batch, void *workspace, size_t ws_bytes,
-                                     int32_t *d_oob_flag, const void *dx, mrec_dtype dx_dtype,
-                                     int64_t dx_ld, const float *dfm, const float *fm_sum,
-                                     const void *x0, mrec_dtype x0_dtype, int64_t x0_ld,
-                                     const float *dw, mrec_bwd_mode mode, float lr, uint64_t seed,
-                                     const uint64_t *d_step, void *grad, mrec_stream stream) {
+mrec_status mrec_emb_bwd_large_fused_ex(const mrec_table_bank *bank, const mrec_ids *ids,
+                                        int64_t batch, void *workspace, size_t ws_bytes,
+                                        int32_t *d_oob_flag, const void *dx, mrec_dtype dx_dtype,
+                                        int64_t dx_ld, const float *dfm, const float *fm_sum,
+                                        const void *x0, mrec_dtype x0_dtype, int64_t x0_ld,
+                                        const float *dw, mrec_bwd_mode mode, float lr,
+                                        uint64_t seed, const uint64_t *d_step, void *grad,
+                                        int32_t n_reduce, const mrec_gemm_call *reduce,
+                                        mrec_stream stream) {
   BankArgs ba;
   IdsArgs ia;
   int lpr;
@@ -1409,15 +1419,21 @@ mrec_status mrec_emb_bwd_large_fused(const mrec_table_bank *bank, const mrec_ids
   st = lg_apply_args(bank, ba, dx, dx_dtype, dx_ld, dfm, fm_sum, x0, x0_dtype, x0_ld, dw, mode,
                      lr, seed, d_step, grad, &a);
   if (st != MREC_OK) return st;
-  if (batch == 0) return MREC_OK;
+  CoReduce co;
+  int co_blocks = 0;
+  if ((st = build_co_reduce(n_reduce, reduce, &co, &co_blocks)) != MREC_OK) return st;
   const int64_t total = batch * ba.n_tables;
-  const int G = bk_groups(R, total);
+  const int G = batch == 0 ? 0 : bk_groups(R, total);
   if (G == 0 || std::getenv("MREC_LG_ATOMIC_PLAN")) {  // the two-call path
-    st = mrec_emb_bwd_large_plan(bank, ids, batch, workspace, ws_bytes, d_oob_flag, stream);
-    if (st != MREC_OK) return st;
-    return mrec_emb_bwd_large_apply(bank, batch, workspace, ws_bytes, dx, dx_dtype, dx_ld, dfm,
+    if (batch > 0) {
+      st = mrec_emb_bwd_large_plan(bank, ids, batch, workspace, ws_bytes, d_oob_flag, stream);
+      if (st != MREC_OK) return st;
+      st = mrec_emb_bwd_large_apply(bank, batch, workspace, ws_bytes, dx, dx_dtype, dx_ld, dfm,
                                     fm_sum, x0, x0_dtype, x0_ld, dw, mode, lr, seed, d_step, grad,
                                     stream);
+      if (st != MREC_OK) return st;
+    }
+    return co.n ? mrec_gemm_multi(n_reduce, reduce, stream) : MREC_OK;
   }
   hipStream_t s = static_cast<hipStream_t>(stream);
   const int NB = bk_buckets(total);
@@ -1426,8 +1442,21 @@ mrec_status mrec_emb_bwd_large_fused(const mrec_table_bank *bank, const mrec_ids
   bk_hist_kernel<<<dim3(G), kBkThreads, 0, s>>>(ba, ia, batch, lognb, w, d_oob_flag);
   bk_scan_kernel<<<dim3((NB + 15) / 16), 256, 0, s>>>(G, lognb, w);
   bk_scatter_kernel<<<dim3(G), kBkThreads, 0, s>>>(ba, ia, batch, G, lognb, w, 1);
-  lg_dispatch_apply(bank->dtype, lpr, ba, batch, w, a, ba.row_stride, NB, G, lognb, s);
+  lg_dispatch_apply(bank->dtype, lpr, ba, batch, w, a, ba.row_stride, NB, G, lognb, s, co,
+                    co_blocks);
   return launch_status("mrec_emb_bwd_large_fused");
+}
+
+mrec_status mrec_emb_bwd_large_fused(const mrec_table_bank *bank, const mrec_ids *ids,
+                                     int64_t batch, void *workspace, size_t ws_bytes,
+                                     int32_t *d_oob_flag, const void *dx, mrec_dtype dx_dtype,
+                                     int64_t dx_ld, const float *dfm, const float *fm_sum,
+                                     const void *x0, mrec_dtype x0_dtype, int64_t x0_ld,
+                                     const float *dw, mrec_bwd_mode mode, float lr, uint64_t seed,
+                                     const uint64_t *d_step, void *grad, mrec_stream stream) {
+  return mrec_emb_bwd_large_fused_ex(bank, ids, batch, workspace, ws_bytes, d_oob_flag, dx,
+                                     dx_dtype, dx_ld, dfm, fm_sum, x0, x0_dtype, x0_ld, dw, mode,
+                                     lr, seed, d_step, grad, 0, nullptr, stream);
 }
 
 }  // extern "C"

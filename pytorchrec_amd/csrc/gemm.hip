@@ -581,6 +581,26 @@ mrec_status build_reduce_job(const mrec_gemm_call &c, GemmArgs *g, int64_t *nblk
   return MREC_OK;
 }
 
+mrec_status build_co_reduce(int32_t n_reduce, const mrec_gemm_call *reduce, CoReduce *co,
+                            int *blocks) {
+  *co = {};
+  *blocks = 0;
+  MREC_CHECK_ARG(n_reduce >= 0 && n_reduce <= kMaxCoReduce && (n_reduce == 0 || reduce),
+                 "n_reduce out of [0, 4]");
+  for (int i = 0; i < n_reduce; ++i) {
+    int64_t nb = 0;
+    mrec_status st = build_reduce_job(reduce[i], &co->g[co->n], &nb);
+    if (st != MREC_OK) return st;
+    if (nb == 0) continue;
+    co->nblk[co->n] = static_cast<int>(nb);
+    co->start[co->n] = *blocks;
+    *blocks += static_cast<int>(nb);
+    ++co->n;
+  }
+  co->start[co->n] = *blocks;
+  return MREC_OK;
+}
+
 }  // namespace mrec
 
 extern "C" {

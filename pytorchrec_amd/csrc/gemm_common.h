@@ -212,4 +212,29 @@ __device__ __forceinline__ void splitk_reduce_body(const GemmArgs &g, int64_t bi
 mrec_status build_reduce_job(const mrec_gemm_call &c, GemmArgs *g, int64_t *nblk);
 int64_t reduce_blocks(const GemmArgs &g);
 
+// deferred split-K weight-gradient reductions (+ fused SGD) run by trailing
+// workgroups of an embedding-update launch (emb_bwd.hip's apply kernels,
+// emb_bwd_large.hip's bucket kernel): independent of the embedding update, and a
+// launch of their own would cost a kernel boundary on the step's serial path
+constexpr int kMaxCoReduce = 4;
+struct CoReduce {
+  int n;
+  int nblk[kMaxCoReduce];
+  int start[kMaxCoReduce + 1];  // workgroup offsets after the host launch's own blocks
+  GemmArgs g[kMaxCoReduce];
+};
+
+__device__ __forceinline__ bool co_reduce(const CoReduce &co, int b) {
+  int p = 0;
+  while (p + 1 < co.n && b >= co.start[p + 1]) ++p;
+  const int local = b - co.start[p];
+  if (local < co.nblk[p]) splitk_reduce_body<false>(co.g[p], local, co.nblk[p]);
+  return true;
+}
+
+// host: validate n_reduce REDUCE-phase calls into *co (jobs with no work dropped);
+// *blocks = the workgroups they take (gemm.hip)
+mrec_status build_co_reduce(int32_t n_reduce, const mrec_gemm_call *reduce, CoReduce *co,
+                            int *blocks);
+
 }  // namespace mrec

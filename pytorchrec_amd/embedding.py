@@ -375,9 +375,14 @@ def _backward_large(bank: EmbeddingBank, ids, batch, grad, dx=None, dfm=None, fm
         _mrec.call("mrec_emb_bwd_large_apply", bank.desc().ref(), batch, ws.data_ptr(),
                    ws.numel(), *_large_apply_args(bank, grad, dx, dfm, fm_sum, x0, dw, mode, lr))
         return
-    _mrec.call("mrec_emb_bwd_large_fused", bank.desc().ref(), _ids_desc(ids).ref(), batch,
-               ws.data_ptr(), ws.numel(), None,
-               *_large_apply_args(bank, grad, dx, dfm, fm_sum, x0, dw, mode, lr))
+    # deferred MLP weight-gradient reductions (DIN's top tower) ride along the bucket kernel
+    from pytorchrec_amd import dense as dense_ops
+    jobs = dense_ops.take_pending(4)
+    arr = (_mrec.GemmCall * len(jobs))(*[j.struct() for j in jobs]) if jobs else None
+    args = _large_apply_args(bank, grad, dx, dfm, fm_sum, x0, dw, mode, lr)
+    _mrec.call("mrec_emb_bwd_large_fused_ex", bank.desc().ref(), _ids_desc(ids).ref(), batch,
+               ws.data_ptr(), ws.numel(), None, *args[:-1], len(jobs), arr, args[-1])
+    del jobs
 
 
 def _large_apply_args(bank, grad, dx, dfm, fm_sum, x0, dw, mode, lr):

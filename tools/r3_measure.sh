@@ -3,7 +3,7 @@
 set -e
 cd $GRAFT_REPO_ROOT
 R=$GRAFT_REPO_ROOT
-O=$R/gpurun_out/r3m2
+O=$R/gpurun_out/r3m3
 mkdir -p $O
 timeout -k 10 900 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread > $O/gputest.log 2>&1
 timeout -k 10 300 python bench.py > $O/bench_deepfm_c2.json 2> $O/bench_deepfm_c2.err

@@ -935,16 +935,18 @@ def main():
         name = max(ks, key=lambda k: ks[k][0])  # the dominant kernel
         t, fl, nb = ks[name]
         ach = fl / t / 1e12
+        traffic, tsrc = pmc_traffic([name], args)
         result["roofline"] = {"bound": "mfma", "kernel": name,
                               "achieved": round(ach, 2), "peak": MFMA_PEAK_TFLOPS,
                               "unit": "TFLOP/s", "frac": round(ach / MFMA_PEAK_TFLOPS, 4),
-                              "traffic": None, "avg_us": round(t * 1e6, 3),
-                              "flop_per_launch": fl,
+                              "traffic": traffic, "traffic_source": tsrc,
+                              "avg_us": round(t * 1e6, 3), "flop_per_launch": fl,
                               "flop_rule": "attention unit 2 L (128*80 + 80*40 + 40) per "
                                            "sample forward, x3 for the backward launch "
                                            "(forward recomputed)",
                               "hbm_GB/s": round(nb / t / 1e9, 1),
-                              "hbm_frac": round(nb / t / 1e9 / HBM_PEAK_GBS, 4)}
+                              "hbm_frac": round(nb / t / 1e9 / HBM_PEAK_GBS, 4),
+                              "alg_bytes_per_launch": nb}
         result["roofline_kernels"] = {k: {"avg_us": round(v[0] * 1e6, 3), "flop": v[1],
                                           "TFLOP/s": round(v[1] / v[0] / 1e12, 2),
                                           "bytes": v[2], "GB/s": round(v[2] / v[0] / 1e9, 1)}

@@ -26,7 +26,8 @@ import subprocess
 import sys
 
 # substring of the kernel name -> bench.py roofline key (first match wins)
-KERNELS = {"interact_plan_kernel": "mrec_interact_fwd_ex", "interact_kernel": "mrec_interact_fwd",
+KERNELS = {"din_att_bwd": "mrec_din_att_bwd", "din_att_fwd": "mrec_din_att_fwd",
+           "bk_apply_kernel": "mrec_emb_bwd_large_fused", "interact_plan_kernel": "mrec_interact_fwd_ex", "interact_kernel": "mrec_interact_fwd",
            "plan_hash_kernel": "mrec_emb_bwd_plan", "apply_hash_kernel": "mrec_emb_bwd_apply",
            "apply_kernel": "mrec_emb_bwd_apply", "tower_kernel": "mrec_tower_fwd_bwd",
            "gemm_dma_kernel": "mrec_gemm", "gemm_multi_kernel": "mrec_gemm_multi",

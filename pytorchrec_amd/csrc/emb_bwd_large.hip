@@ -54,7 +54,8 @@ struct LgWs {
   uint32_t *segmax; // [U] max |g| bits of long segment L (zero on entry, left zero)
   long long *acc;   // [U * stride] fixed-point sums (zero on entry, left zero)
   int32_t *bhist;   // bucketed plan: [G][NB] lookups per (chunk, bucket), then their offsets
-  int32_t *bstart;  // bucketed plan: [NB + 1] first entry of every bucket
+  int32_t *btot;    // bucketed plan: [NB] lookups per bucket (zero on entry, left zero)
+  int32_t *bcur;    // bucketed plan: [NB] next chunk offset inside the bucket (ditto)
   int2 *ent;        // bucketed plan: [N] (row, b) grouped by bucket
 };
 
@@ -122,18 +123,18 @@ __host__ __device__ inline int64_t lg_ws_bytes(int64_t R, int64_t N, int stride,
     o = lg_align(o + bytes);
     return at;
   };
-  const int64_t o_hdr = take(32), o_segmax = take(4 * UL), o_acc = take(8 * UL * stride);
+  const int G = bk_groups(R, N), NB = bk_buckets(N);
+  const int64_t o_hdr = take(32), o_bcnt = take(G ? 8 * NB : 0), o_segmax = take(4 * UL), o_acc = take(8 * UL * stride);
   const int64_t o_cnt = take(4 * R), o_start = take(4 * R), o_blk = take(8 * nblk);
   const int64_t o_uniq = take(4 * U), o_ustart = take(4 * U), o_ulen = take(4 * U);
   const int64_t o_ulong = take(4 * U), o_perm = take(4 * N), o_longs = take(4 * UL);
   const int64_t o_chunks = take(8 * C);
-  const int G = bk_groups(R, N), NB = bk_buckets(N);
   const int64_t o_bhist = take(G ? 4 * (int64_t(G + 1) * NB + 1) : 0);
-  const int64_t o_bstart = take(G ? 4 * (NB + 1) : 0);
   const int64_t o_ent = take(G ? 8 * N : 0);
   if (w) {
     w->bhist = G ? reinterpret_cast<int32_t *>(base + o_bhist) : nullptr;
-    w->bstart = G ? reinterpret_cast<int32_t *>(base + o_bstart) : nullptr;
+    w->btot = G ? reinterpret_cast<int32_t *>(base + o_bcnt) : nullptr;
+    w->bcur = G ? w->btot + NB : nullptr;
     w->ent = G ? reinterpret_cast<int2 *>(base + o_ent) : nullptr;
     w->hdr = reinterpret_cast<int32_t *>(base + o_hdr);
     w->segmax = reinterpret_cast<uint32_t *>(base + o_segmax);
@@ -155,7 +156,8 @@ __host__ __device__ inline int64_t lg_ws_bytes(int64_t R, int64_t N, int stride,
 // bytes that must be zero before the first call (every apply leaves them zero)
 __host__ inline int64_t lg_zero_bytes(int64_t R, int64_t N, int stride) {
   const int64_t UL = lg_caps(R, N).UL;
-  return lg_align(32) + lg_align(4 * UL) + lg_align(8 * UL * stride);
+  const int64_t bcnt = bk_groups(R, N) ? lg_align(8 * bk_buckets(N)) : 0;
+  return lg_align(32) + bcnt + lg_align(4 * UL) + lg_align(8 * UL * stride);
 }
 
 __device__ __forceinline__ int table_of_row(const BankArgs &bank, int64_t grow) {
@@ -465,57 +467,13 @@ __global__ __launch_bounds__(kBkThreads) void bk_hist_kernel(BankArgs bank, IdsA
     if (rr[u] >= 0) atomicAdd(&h[bk_of(rr[u], lognb)], 1);
   __syncthreads();
   int32_t *dst = w.bhist + static_cast<int64_t>(blockIdx.x) * NB;
-  for (int k = threadIdx.x; k < NB; k += kBkThreads) dst[k] = h[k];
+  for (int k = threadIdx.x; k < NB; k += kBkThreads) {
+    dst[k] = h[k];
+    if (h[k]) atomicAdd(&w.btot[k], h[k]);  // the bucket totals (zero on entry)
+  }
 }
 
-// per bucket (one thread each, 256 per workgroup): every chunk's count becomes its
-// first position inside the bucket (chunk order), and the bucket's total
-// per bucket, the chunks' exclusive prefix: a workgroup takes 16 consecutive buckets
-// (64-B row segments of bhist) x 16 groups of consecutive chunks; every load of a
-// thread is in flight before any is added, the 16 group sums are prefixed through
-// LDS, then each thread rewrites its chunks with the running offset
-__global__ __launch_bounds__(256) void bk_scan_kernel(int G, int lognb, LgWs w) {
-  constexpr int BW = 16, CG = 16, U = 8;
-  __shared__ int32_t gs[CG][BW];
-  const int NB = 1 << lognb;
-  const int j = threadIdx.x % BW, c = threadIdx.x / BW;
-  const int k = blockIdx.x * BW + j;
-  const int per = (G + CG - 1) / CG, g0 = c * per, g1 = min(G, g0 + per);
-  int sum = 0;
-  if (k < NB) {
-    for (int g = g0; g < g1; g += U) {
-      int32_t v[U];
-#pragma unroll
-      for (int u = 0; u < U; ++u)
-        v[u] = g + u < g1 ? w.bhist[static_cast<int64_t>(g + u) * NB + k] : 0;
-#pragma unroll
-      for (int u = 0; u < U; ++u) sum += v[u];
-    }
-  }
-  gs[c][j] = sum;
-  __syncthreads();
-  int tot = 0, all = 0;
-#pragma unroll
-  for (int q = 0; q < CG; ++q) {
-    tot += q < c ? gs[q][j] : 0;
-    all += gs[q][j];
-  }
-  if (k >= NB) return;
-  for (int g = g0; g < g1; g += U) {
-    int32_t v[U];
-#pragma unroll
-    for (int u = 0; u < U; ++u)
-      v[u] = g + u < g1 ? w.bhist[static_cast<int64_t>(g + u) * NB + k] : 0;
-#pragma unroll
-    for (int u = 0; u < U; ++u) {
-      if (g + u < g1) w.bhist[static_cast<int64_t>(g + u) * NB + k] = tot;
-      tot += v[u];
-    }
-  }
-  if (c == 0) w.bstart[k] = all;  // the total for now: bk_scatter_kernel scans the totals
-}
-
-// exclusive scan of the NB bucket totals (bstart) into LDS base[]; returns the sum
+// exclusive scan of the NB bucket totals (btot) into LDS base[]; returns the sum
 __device__ int bk_bucket_base(const int32_t *tot, int NB, int32_t *base, int32_t *wsum) {
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   constexpr int KPT = kBkMaxNB / kBkThreads;  // consecutive buckets per thread
@@ -551,9 +509,11 @@ __device__ int bk_bucket_base(const int32_t *tot, int NB, int32_t *base, int32_t
 
 // the same chunks as bk_hist_kernel: every valid lookup -> (row, b) at its
 // bucket's next position (LDS cursors; the order inside a bucket is not used for
-// arithmetic).  Workgroup 0 also publishes the bucket starts (bstart, written
-// after every workgroup has read the totals: bk_group_kernel reads them) -- so the
-// starts go to bhist's spare row G and bk_group_kernel reads them there.
+// arithmetic).  Every workgroup scans the bucket totals bk_hist_kernel summed
+// (btot) itself and reserves its chunk's range in each bucket with one atomic on
+// the bucket's cursor (bcur): no scan launch between the two.  Workgroup 0 also
+// publishes the bucket starts in bhist's spare row G for the bucket kernels, which
+// leave btot / bcur zero again.
 __global__ __launch_bounds__(kBkThreads) void bk_scatter_kernel(BankArgs bank, IdsArgs ids, int64_t n,
                                                                 int G, int lognb, LgWs w,
                                                                 int fused) {
@@ -569,13 +529,15 @@ __global__ __launch_bounds__(kBkThreads) void bk_scatter_kernel(BankArgs bank, I
     rr[u] = lookup_row(bank, ids, n, i0 + u * kBkThreads, total, &b, nullptr);
     bb[u] = static_cast<int32_t>(b);
   }
-  const int all = bk_bucket_base(w.bstart, NB, cur, wsum);
+  const int all = bk_bucket_base(w.btot, NB, cur, wsum);
   const int32_t *src = w.bhist + static_cast<int64_t>(blockIdx.x) * NB;
   int32_t *pub = w.bhist + static_cast<int64_t>(G) * NB;  // spare row: bucket starts
   for (int k = threadIdx.x; k < NB; k += kBkThreads) {
-    const int b0 = cur[k];
+    const int b0 = cur[k], c = src[k];
     if (blockIdx.x == 0) pub[k] = b0;
-    cur[k] = b0 + src[k];
+    // this chunk's range inside the bucket: one atomic per (chunk, bucket) -- the
+    // order of the chunks inside a bucket is not used for arithmetic
+    cur[k] = b0 + (c ? atomicAdd(&w.bcur[k], c) : 0);
   }
   if (blockIdx.x == 0 && threadIdx.x == 0) {
     pub[NB] = all;
@@ -636,6 +598,10 @@ __global__ __launch_bounds__(256) void bk_group_kernel(LgWs w, int G, int lognb,
   const int NB = 1 << lognb;
   const int32_t *pub = w.bhist + static_cast<int64_t>(G) * NB;
   const int lo = pub[blockIdx.x], hi = pub[blockIdx.x + 1];
+  if (tid == 0) {  // the scatter has used them: zero for the next call
+    w.btot[blockIdx.x] = 0;
+    w.bcur[blockIdx.x] = 0;
+  }
   for (int k = tid; k < kBkSlots; k += 256) {
     key[k] = kLgEmpty;
     cnt[k] = 0;
@@ -1015,6 +981,10 @@ __global__ __launch_bounds__(256) void bk_apply_kernel(BankArgs bank, LgWs w, Ap
   }
   const int32_t *pub = w.bhist + static_cast<int64_t>(G) * NB;
   const int lo = pub[blockIdx.x], hi = pub[blockIdx.x + 1];
+  if (tid == 0) {  // the scatter has used them: zero for the next call
+    w.btot[blockIdx.x] = 0;
+    w.bcur[blockIdx.x] = 0;
+  }
   for (int k = tid; k < kBkSlots; k += 256) {
     key[k] = kLgEmpty;
     cur[k] = 0;
@@ -1244,8 +1214,7 @@ mrec_status mrec_emb_bwd_large_plan(const mrec_table_bank *bank, const mrec_ids 
     int lognb = 0;
     while ((1 << lognb) < NB) ++lognb;
     bk_hist_kernel<<<dim3(G), kBkThreads, 0, s>>>(ba, ia, batch, lognb, w, d_oob_flag);
-    bk_scan_kernel<<<dim3((NB + 15) / 16), 256, 0, s>>>(G, lognb, w);
-    bk_scatter_kernel<<<dim3(G), kBkThreads, 0, s>>>(ba, ia, batch, G, lognb, w, 0);
+      bk_scatter_kernel<<<dim3(G), kBkThreads, 0, s>>>(ba, ia, batch, G, lognb, w, 0);
     bk_group_kernel<<<dim3(NB), 256, 0, s>>>(w, G, lognb, d_oob_flag);
     return launch_status("mrec_emb_bwd_large_plan");
   }
@@ -1440,7 +1409,6 @@ mrec_status mrec_emb_bwd_large_fused_ex(const mrec_table_bank *bank, const mrec_
   int lognb = 0;
   while ((1 << lognb) < NB) ++lognb;
   bk_hist_kernel<<<dim3(G), kBkThreads, 0, s>>>(ba, ia, batch, lognb, w, d_oob_flag);
-  bk_scan_kernel<<<dim3((NB + 15) / 16), 256, 0, s>>>(G, lognb, w);
   bk_scatter_kernel<<<dim3(G), kBkThreads, 0, s>>>(ba, ia, batch, G, lognb, w, 1);
   lg_dispatch_apply(bank->dtype, lpr, ba, batch, w, a, ba.row_stride, NB, G, lognb, s, co,
                     co_blocks);

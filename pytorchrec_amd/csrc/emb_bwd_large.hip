@@ -522,6 +522,18 @@ __global__ __launch_bounds__(kBkThreads) void bk_scatter_kernel(BankArgs bank, I
   const int NB = 1 << lognb;
   const int64_t total = n * bank.n_tables;
   const int64_t i0 = static_cast<int64_t>(blockIdx.x) * kBkChunk + threadIdx.x;
+  // this chunk's range inside each bucket: one atomic per (chunk, bucket), issued
+  // first so its round trip overlaps the id loads -- the order of the chunks inside
+  // a bucket is not used for arithmetic
+  constexpr int KQ = kBkMaxNB / kBkThreads;
+  const int32_t *src = w.bhist + static_cast<int64_t>(blockIdx.x) * NB;
+  int32_t resv[KQ];
+#pragma unroll
+  for (int q = 0; q < KQ; ++q) {
+    const int k = threadIdx.x + q * kBkThreads;
+    const int c = k < NB ? src[k] : 0;
+    resv[q] = c ? atomicAdd(&w.bcur[k], c) : 0;
+  }
   int32_t rr[kBkPer], bb[kBkPer];
 #pragma unroll
   for (int u = 0; u < kBkPer; ++u) {
@@ -530,14 +542,14 @@ __global__ __launch_bounds__(kBkThreads) void bk_scatter_kernel(BankArgs bank, I
     bb[u] = static_cast<int32_t>(b);
   }
   const int all = bk_bucket_base(w.btot, NB, cur, wsum);
-  const int32_t *src = w.bhist + static_cast<int64_t>(blockIdx.x) * NB;
   int32_t *pub = w.bhist + static_cast<int64_t>(G) * NB;  // spare row: bucket starts
-  for (int k = threadIdx.x; k < NB; k += kBkThreads) {
-    const int b0 = cur[k], c = src[k];
+#pragma unroll
+  for (int q = 0; q < KQ; ++q) {
+    const int k = threadIdx.x + q * kBkThreads;
+    if (k >= NB) break;
+    const int b0 = cur[k];
     if (blockIdx.x == 0) pub[k] = b0;
-    // this chunk's range inside the bucket: one atomic per (chunk, bucket) -- the
-    // order of the chunks inside a bucket is not used for arithmetic
-    cur[k] = b0 + (c ? atomicAdd(&w.bcur[k], c) : 0);
+    cur[k] = b0 + resv[q];
   }
   if (blockIdx.x == 0 && threadIdx.x == 0) {
     pub[NB] = all;

@@ -39,7 +39,7 @@ C5_ROWS = 100_000_000  # rows per table, SURVEY.md §8(d) C5 (row-sharded over t
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md chip table (spec)
 
 
-def parse():
+def parse(argv=None):
     p = argparse.ArgumentParser()
     p.add_argument("--gpus", type=int, default=1)
     p.add_argument("--steps", type=int, default=50)
@@ -80,7 +80,7 @@ def parse():
                         "--dist-backend gloo; RCCL refuses two ranks on one device)")
     p.add_argument("--stub-step", action="store_true",
                    help="launcher check without a GPU: each rank's step is one gloo all-reduce")
-    args = p.parse_args()
+    args = p.parse_args(argv)
     if args.rows_per_table is None:
         # N = 1: C2 (~1M rows); N > 1: C5, 100M-row tables row-sharded over the ranks
         args.rows_per_table = C5_ROWS if args.gpus > 1 else CRITEO_ROWS

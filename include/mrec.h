@@ -32,7 +32,7 @@
 extern "C" {
 #endif
 
-#define MREC_ABI_VERSION 24
+#define MREC_ABI_VERSION 25
 #define MREC_MAX_TABLES 64      /* tables per table bank / per call */
 #define MREC_BWD_MAX_BATCH 8192  /* lookups per table per plan/apply call */
 #define MREC_BWD_HASH_MAX_BATCH 4096  /* batches up to this use the hash plan */
@@ -315,6 +315,18 @@ mrec_status mrec_emb_bwd_large_fused(const mrec_table_bank *bank, const mrec_ids
                                      const void *x0, mrec_dtype x0_dtype, int64_t x0_ld,
                                      const float *dw, mrec_bwd_mode mode, float lr, uint64_t seed,
                                      const uint64_t *d_step, void *grad, mrec_stream stream);
+
+/*
+ * Byte offset, inside the large-batch workspace, of an int32 STICKY error word
+ * (ABI 25).  The fused path's huge segments (a row hit > 2048 times) are summed in
+ * one launch of three dependent phases whose work items are dequeued in phase
+ * order (no co-residency assumed, so a phase wait always ends); its waits are still
+ * bounded, and a wait that ran out (a hardware stall; or MREC_LG_HUGE_TEST_STALL,
+ * a test-only knob that makes them unreachable) leaves the rows of that launch's
+ * huge segments un-updated and sets this word to non-zero.  No kernel clears it:
+ * the caller reads it at a sync point of its choosing, raises, and zeroes it.
+ */
+size_t mrec_emb_bwd_large_error_offset(void);
 
 struct mrec_gemm_call_s; /* mrec_gemm_call, defined with the GEMM entry points below */
 

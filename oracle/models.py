@@ -159,9 +159,126 @@ class RefDCNv2(nn.Module):
         return (x @ self.out.weight.T + self.out.bias).squeeze(-1)
 
 
+class _RoundBF16Grad(torch.autograd.Function):
+    """Passes the value unrounded, rounds the gradient to bf16 (a pre-activation
+    whose gradient the MI355X path stores as a bf16 MFMA operand while the value
+    itself never leaves fp32 registers)."""
+
+    @staticmethod
+    def forward(ctx, x):
+        return x.view_as(x)
+
+    @staticmethod
+    def backward(ctx, g):
+        return g.to(torch.bfloat16).to(g.dtype)
+
+
+def _rbg(x):
+    return _RoundBF16Grad.apply(x)
+
+
+class RefDIN(nn.Module):
+    """DIN (config C4) the reference way.  The reference has no DIN; this is built
+    from its primitives, which is what a PyTorchRec user would write:
+
+      * an item and a category ``nn.Embedding`` shared by the target and the
+        history (FunkSVD.py:39-41), init normal(0, 0.01) (IModel.py:61-68);
+        q = [item(iid) | cate(cid)], k_j = [item(his_j) | cate(hcat_j)];
+      * history validity ``his > 0`` with position 0 forced valid
+        (``get_valid_his_index``, torchrec/model/utils.py:5-10);
+      * attention unit = reference ``MLP`` (Linear -> ReLU, MLP.py:8-23) over
+        [q, k, q - k, q * k] + Linear(h, 1) -> scores;
+      * masked softmax: -inf on invalid keys, then softmax over the history
+        (``scaled_dot_product_attention``, SASRec.py:14-31; its global-max shift is
+        a no-op for softmax and is kept for fidelity), pooled u = sum_j a_j k_j
+        (the weighted-sum form of SASRec.py:30 / SVDPP.py:49-55);
+      * top = MLP over [q, u] + Linear(last, 1) -> logit (NCF.py:68-74).
+
+    ``bf16_points=True`` is NOT the reference: the same model with every tensor
+    the MI355X path stores in bf16 rounded there: the
+    attention-unit input's q - k and q * k, W1 / W2 as MFMA operands, H1 (value)
+    and the layer-1 / layer-2 pre-activation gradients (dZ1, dZ2), the pooled u
+    (top = [q | u] is a bf16 tensor, and so is its gradient), the top tower as in
+    RefDeepFM, and each gathered row's gradient (one bf16 value per lookup).  H2,
+    the scores, the softmax and w3 stay fp32.  Its distance to the fp64 model is
+    what bf16 storage alone costs; the C4 parity test sizes its bar by it."""
+
+    def __init__(self, item_rows: int, cate_rows: int, emb_size: int = 16, att_layers=(80, 40),
+                 layers=(200, 80), dtype=torch.float32, seed: int = 2020,
+                 bf16_points: bool = False):
+        super().__init__()
+        torch.manual_seed(seed)
+        E = 2 * emb_size
+        self.item = nn.Embedding(item_rows, emb_size)
+        self.cate = nn.Embedding(cate_rows, emb_size)
+        self.att_mlp = _mlp([4 * E, *att_layers])
+        self.att_out = nn.Linear(att_layers[-1], 1)
+        self.mlp = _mlp([2 * E, *layers])
+        self.out = nn.Linear(layers[-1], 1)
+        self.bf16_points = bf16_points
+        self.apply(_reset)
+        self.to(dtype)
+
+    def forward(self, iid, cid, his, hcat):
+        """iid / cid [B], his / hcat [B, L] int64 -> logits [B]."""
+        B, L = his.shape
+        rb = self.bf16_points
+        q = torch.cat([self.item(iid), self.cate(cid)], -1)                   # [B, E]
+        k = torch.cat([self.item(his), self.cate(hcat)], -1)                  # [B, L, E]
+        if rb:  # one bf16 gradient per gathered row
+            q, k = _rb(q), _rb(k)
+        valid = his.gt(0)
+        valid[:, 0] = True
+        qb = q[:, None, :].expand_as(k)
+        if rb:
+            x = torch.cat([qb, k, _rbv(qb - k), _rbv(qb * k)], -1)
+        else:
+            x = torch.cat([qb, k, qb - k, qb * k], -1)
+        lins = [m for m in self.att_mlp if isinstance(m, nn.Linear)]
+        for i, m in enumerate(lins):
+            if not rb:
+                x = torch.relu(m(x))
+                continue
+            z = _rbg(x @ _rbv(m.weight).T + m.bias)
+            x = torch.relu(z)
+            if i + 1 < len(lins):
+                x = _rbv(x)  # H1 is a bf16 MFMA operand; H2 stays fp32
+        s = self.att_out(x).squeeze(-1)                                       # [B, L]
+        # SASRec.py:26 (the shift's gradient is analytically zero; detached so it
+        # does not leak rounding noise into whichever row holds the max)
+        s = s - s.detach().max()
+        a = s.masked_fill(~valid, float("-inf")).softmax(-1)
+        u = (a[..., None] * k).sum(1)
+        top = torch.cat([q, u], -1)
+        if not rb:
+            return self.out(self.mlp(top)).squeeze(-1)
+        x = _rb(top)
+        for m in self.mlp:
+            if isinstance(m, nn.Linear):
+                x = _rb(torch.relu(x @ _rbv(m.weight).T + m.bias))
+        return (x @ self.out.weight.T + self.out.bias).squeeze(-1)
+
+
+def din_batch(item_rows: int, cate_rows: int, batch: int, L: int = 50, seed: int = 0):
+    """SURVEY.md §8(d) C4 synthetic batch (bench.din_batch's recipe): ids uniform
+    over the non-PAD rows, history lengths U{1..L}, tail-padded with 0
+    (interaction_history_list.py:17-29), labels Bernoulli(0.25)."""
+    g = torch.Generator().manual_seed(seed)
+    iid = torch.randint(1, item_rows, (batch,), generator=g)
+    cid = torch.randint(1, cate_rows, (batch,), generator=g)
+    his = torch.randint(1, item_rows, (batch, L), generator=g)
+    hcat = torch.randint(1, cate_rows, (batch, L), generator=g)
+    lens = torch.randint(1, L + 1, (batch, 1), generator=g)
+    pad = torch.arange(L)[None, :] >= lens
+    his[pad] = 0
+    hcat[pad] = 0
+    label = (torch.rand(batch, generator=g) < 0.25).float()
+    return iid, cid, his, hcat, label
+
+
 def sgd_train_step(model: nn.Module, opt: torch.optim.Optimizer, ids, dense, label):
     """``IModel.train_step`` (IModel.py:116-125) with BCEWithLogitsLoss."""
-    logit = model(ids, dense)
+    logit = model(*ids) if isinstance(ids, (tuple, list)) else model(ids, dense)
     loss = torch.nn.functional.binary_cross_entropy_with_logits(logit, label.to(logit.dtype))
     opt.zero_grad()
     loss.backward()

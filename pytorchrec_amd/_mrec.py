@@ -20,7 +20,7 @@ import torch  # noqa: F401  (must precede the dlopen, see module docstring)
 LIB_DIR = os.path.join(os.path.dirname(os.path.abspath(__file__)), "lib")
 LIB_PATH = os.environ.get("MREC_LIB_PATH") or os.path.join(LIB_DIR, "libmrec.so")
 
-ABI_VERSION = 24
+ABI_VERSION = 25
 MAX_TABLES = 64
 BWD_MAX_BATCH = 8192
 BWD_HASH_MAX_BATCH = 4096  # batches up to this use the hash plan (fusable into a GEMM launch)
@@ -259,6 +259,7 @@ SIGNATURES = {
                                                _i64, _vp, _i64, _i32, _vp, _i64, _vp]),
     "mrec_emb_bwd_large_workspace_size": (ctypes.c_size_t, [_bank_p, _i64]),
     "mrec_emb_bwd_large_zero_bytes": (ctypes.c_size_t, [_bank_p, _i64]),
+    "mrec_emb_bwd_large_error_offset": (ctypes.c_size_t, []),
     "mrec_emb_bwd_large_plan": (ctypes.c_int, [_bank_p, _ids_p, _i64, _vp, ctypes.c_size_t, _vp,
                                                _vp]),
     "mrec_emb_bwd_large_apply": (ctypes.c_int, [_bank_p, _i64, _vp, ctypes.c_size_t, _vp,

@@ -40,12 +40,16 @@ struct ApplyArgs {
   OptArgs opt;
 };
 
-// a given gradient from a wire record (4-B aligned rows: records are not 16-B)
+// a given gradient from a wire record (4-B aligned rows: records are not 16-B).
+// An entry past its part's cap_rows records had its record clipped by the sender
+// (the overflow flag is set): zero gradient -- never another entry's record.
 template <int EPL>
 __device__ __forceinline__ void wire_grad(const ApplyArgs &a, int64_t b, int f, int D, int e0,
                                           bool v_lane, bool w_lane, float *g) {
   const int64_t p = b / a.chunk, j = b - p * a.chunk;
-  const int64_t rec = p * a.g_cap_rows + a.g_pref[p * a.g_F + f] + j;
+  const int64_t in_part = a.g_pref[p * a.g_F + f] + j;
+  if (in_part >= a.g_cap_rows) return;  // g stays zero (lookup_grad zeroed it)
+  const int64_t rec = p * a.g_cap_rows + in_part;
   if (a.g_rec_bf16) {
     const uint16_t *go = static_cast<const uint16_t *>(a.g_rec) + rec * a.g_rec_pitch;
     if (v_lane) {

@@ -444,7 +444,7 @@ __global__ __launch_bounds__(256, MREC_APPLY_WAVES) void apply_hash_kernel(BankA
 #if MREC_APPLY_EXP == 13  // (diagnostic: reductions trailing the apply blocks)
   const int co_blocks = 0;
   if (static_cast<int>(blockIdx.x) >= seg_blocks * (1 + kHotPer) + sm_blocks) {
-    co_reduce(co, blockIdx.x - seg_blocks - sm_blocks);
+    co_reduce(co, blockIdx.x - seg_blocks * (1 + kHotPer) - sm_blocks);
     return;
   }
 #else

@@ -40,7 +40,9 @@ constexpr int kLgApplyBlocks = 2048;   // grid-stride launches (device-side coun
 
 // workspace layout (all offsets 256-B aligned)
 struct LgWs {
-  int32_t *hdr;     // [8]: 0 unique rows, 1 long segments, 2 chunks
+  int32_t *hdr;     // [16]: 0 unique rows, 1 long segments, 2 chunks, 3 huge segments,
+                    // 4-6 lg_huge_kernel's queue / done counters ([0..7] zeroed per
+                    // call), 8 sticky error word (kLgErrWord: host-cleared)
   int32_t *cnt;     // [R]
   int32_t *start;   // [R]
   int32_t *blk;     // [2 * nblk]: per scan block (lookups, nonzero rows)
@@ -124,7 +126,7 @@ __host__ __device__ inline int64_t lg_ws_bytes(int64_t R, int64_t N, int stride,
     return at;
   };
   const int G = bk_groups(R, N), NB = bk_buckets(N);
-  const int64_t o_hdr = take(32), o_bcnt = take(G ? 8 * NB : 0), o_segmax = take(4 * UL), o_acc = take(8 * UL * stride);
+  const int64_t o_hdr = take(64), o_bcnt = take(G ? 8 * NB : 0), o_segmax = take(4 * UL), o_acc = take(8 * UL * stride);
   const int64_t o_cnt = take(4 * R), o_start = take(4 * R), o_blk = take(8 * nblk);
   const int64_t o_uniq = take(4 * U), o_ustart = take(4 * U), o_ulen = take(4 * U);
   const int64_t o_ulong = take(4 * U), o_perm = take(4 * N), o_longs = take(4 * UL);
@@ -707,17 +709,15 @@ __global__ __launch_bounds__(256) void bk_group_kernel(LgWs w, int G, int lognb,
 // pass 1 over the long segments' chunks: max |g| per segment (bits of a
 // non-negative float order like the float)
 template <typename T, int LPR>
-__device__ __forceinline__ void lg_longmax_body(BankArgs bank, int64_t n, LgWs w,
-                                                         ApplyArgs a) {
+__device__ __forceinline__ void lg_longmax_chunk(BankArgs bank, LgWs w, ApplyArgs a, int j) {
   constexpr int EPL = Vec<T>::EPL;
   constexpr int WPB = 256 / LPR;
   const int worker = threadIdx.x / LPR, l = threadIdx.x % LPR, e0 = l * EPL;
   const int D = bank.dim;
   const bool v_lane = e0 + EPL <= D, w_lane = bank.has_w && e0 == D;
-  const int nchunks = w.hdr[2];
-  for (int j = blockIdx.x; j < nchunks; j += gridDim.x) {
+  {
     const int2 ch = w.chunks[j];
-    if (ch.x < 0) continue;  // a hole (bucketed plan)
+    if (ch.x < 0) return;  // a hole (bucketed plan)
     const int u = w.longs[ch.x];
     const int f = table_of_row(bank, w.uniq[u]);
     const int s0 = w.ustart[u] + ch.y * kLgChunk;
@@ -736,6 +736,13 @@ __device__ __forceinline__ void lg_longmax_body(BankArgs bank, int64_t n, LgWs w
   }
 }
 
+template <typename T, int LPR>
+__device__ __forceinline__ void lg_longmax_body(BankArgs bank, int64_t n, LgWs w,
+                                                         ApplyArgs a) {
+  const int nchunks = w.hdr[2];
+  for (int j = blockIdx.x; j < nchunks; j += gridDim.x) lg_longmax_chunk<T, LPR>(bank, w, a, j);
+}
+
 // fixed-point scale of long segment L: sum of len terms of |x| <= max stays < 2^62
 __device__ __forceinline__ int lg_scale(float mx, int len) {
   if (!(mx > 0.f)) return 0;
@@ -747,19 +754,19 @@ __device__ __forceinline__ int lg_scale(float mx, int len) {
 }
 
 // pass 2: fixed-point chunk sums added into the segment's int64 accumulator
+// (workgroup-uniform: one chunk per call, LDS reduction with barriers)
 template <typename T, int LPR>
-__device__ __forceinline__ void lg_longacc_body(BankArgs bank, int64_t n, LgWs w,
-                                                         ApplyArgs a, int stride) {
+__device__ __forceinline__ void lg_longacc_chunk(BankArgs bank, LgWs w, ApplyArgs a, int stride,
+                                                 int j) {
   constexpr int EPL = Vec<T>::EPL;
   constexpr int WPB = 256 / LPR;
   __shared__ long long red[WPB][LPR * EPL];
   const int worker = threadIdx.x / LPR, l = threadIdx.x % LPR, e0 = l * EPL;
   const int D = bank.dim;
   const bool v_lane = e0 + EPL <= D, w_lane = bank.has_w && e0 == D;
-  const int nchunks = w.hdr[2];
-  for (int j = blockIdx.x; j < nchunks; j += gridDim.x) {
+  {
     const int2 ch = w.chunks[j];
-    if (ch.x < 0) continue;  // a hole (bucketed plan; uniform over the workgroup)
+    if (ch.x < 0) return;  // a hole (bucketed plan; uniform over the workgroup)
     const int u = w.longs[ch.x];
     const int f = table_of_row(bank, w.uniq[u]);
     const int s0 = w.ustart[u] + ch.y * kLgChunk;
@@ -796,26 +803,37 @@ __device__ __forceinline__ void lg_longacc_body(BankArgs bank, int64_t n, LgWs w
   }
 }
 
+template <typename T, int LPR>
+__device__ __forceinline__ void lg_longacc_body(BankArgs bank, int64_t n, LgWs w,
+                                                         ApplyArgs a, int stride) {
+  const int nchunks = w.hdr[2];
+  for (int j = blockIdx.x; j < nchunks; j += gridDim.x)
+    lg_longacc_chunk<T, LPR>(bank, w, a, stride, j);
+}
+
 // one update per unique row.  A wave takes 64 / LPR consecutive unique rows, one
 // per worker (LPR lanes): a segment of <= 16 lookups is sorted and summed in
 // ascending sample order by its worker; a segment of 17..kLgHuge lookups by the
 // whole wave in fixed point (max |g| over the segment, then the int64 sum of every
 // term scaled by 2^S: the arithmetic of the chunked kernels, so the same bits); a
 // longer one from the chunked kernels' accumulator.
+// (the unique rows [blk * WPB, (blk + 1) * WPB): wave wid takes the WPW from
+// blk * WPB + wid * WPW; a.seed already advanced by the step counter)
 template <typename T, int LPR>
-__device__ __forceinline__ void lg_apply_body(BankArgs bank, int64_t n, LgWs w,
-                                                       ApplyArgs a, int stride) {
+__device__ __forceinline__ void lg_apply_block(BankArgs bank, LgWs w, ApplyArgs a, int stride,
+                                               int blk) {
   constexpr int EPL = Vec<T>::EPL;
   constexpr int WPB = 256 / LPR;  // workers per workgroup
   constexpr int WPW = 64 / LPR;   // workers per wave
-  if (a.d_step) a.seed += *a.d_step * 0x9e3779b97f4a7c15ull;
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
   const int wk = lane / LPR, l = lane % LPR, e0 = l * EPL;
   const int D = bank.dim;
   const bool v_lane = e0 + EPL <= D, w_lane = bank.has_w && e0 == D;
   const bool live = v_lane || w_lane;
   const int nu = w.hdr[0];
-  for (int u0 = blockIdx.x * WPB + wid * WPW; u0 < nu; u0 += gridDim.x * WPB) {
+  {
+    const int u0 = blk * WPB + wid * WPW;
+    if (u0 >= nu) return;  // wave-uniform
     const int u = u0 + wk;
     const int len = u < nu ? w.ulen[u] : 0;  // 0: past the end, or a hole (bucketed plan)
     int64_t grow = 0;
@@ -900,6 +918,16 @@ __device__ __forceinline__ void lg_apply_body(BankArgs bank, int64_t n, LgWs w,
 }
 
 template <typename T, int LPR>
+__device__ __forceinline__ void lg_apply_body(BankArgs bank, int64_t n, LgWs w,
+                                                       ApplyArgs a, int stride) {
+  constexpr int WPB = 256 / LPR;
+  if (a.d_step) a.seed += *a.d_step * 0x9e3779b97f4a7c15ull;
+  const int nblk = (w.hdr[0] + WPB - 1) / WPB;
+  for (int blk = blockIdx.x; blk < nblk; blk += gridDim.x)
+    lg_apply_block<T, LPR>(bank, w, a, stride, blk);
+}
+
+template <typename T, int LPR>
 __global__ __launch_bounds__(256) void lg_longmax_kernel(BankArgs bank, int64_t n, LgWs w,
                                                          ApplyArgs a) {
   lg_longmax_body<T, LPR>(bank, n, w, a);
@@ -917,50 +945,83 @@ __global__ __launch_bounds__(256) void lg_apply_kernel(BankArgs bank, int64_t n,
   lg_apply_body<T, LPR>(bank, n, w, a, stride);
 }
 
-// grid-wide barrier of the huge-segment kernel (every workgroup co-resident: the
-// grid is sized by the occupancy query): stores drained, one agent-scope arrival
-// per workgroup, a bounded poll (an error flag, never a hang), acquire fence.
-__device__ __forceinline__ void lg_grid_sync(int32_t *ctr, int target) {
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-    __hip_atomic_fetch_add(ctr, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    int spins = 0;
-    while (__hip_atomic_load(ctr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < target) {
-      __builtin_amdgcn_s_sleep(2);
-      if (++spins > (1 << 26)) {  // seconds: a workgroup never arrived
-        __hip_atomic_store(ctr + 2, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        break;
-      }
-    }
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+// The fused path's huge segments (> kLgHuge lookups of one row): max |g|, the
+// fixed-point chunk sums and the per-row update, three dependent phases in ONE
+// launch.  The bucket kernel counts the huge segments in hdr[3]; with none (the
+// common case: DIN's padding slots skip the PAD row) every workgroup leaves at once,
+// so the step pays one empty launch instead of three.
+//
+// No co-residency is assumed (a grid barrier would need every workgroup resident,
+// which another stream's kernels -- the batch feed, RCCL -- can break): work items
+// are DEQUEUED in phase order from one counter (hdr[4]): the nc chunks of phase 0,
+// the nc chunks of phase 1, then the apply blocks of phase 2.  A workgroup starting
+// an item of phase p > 0 first waits until every item of phase p - 1 is done
+// (hdr[4 + p] == nc).  Every such item was dequeued before it by a workgroup that is
+// running and never waits while it holds it, so the wait always ends, whatever the
+// number of resident workgroups.  Done counters: vmcnt(0) + barrier + release fence
+// + agent add; the waiter: relaxed polls + acquire fence.  hdr[4..6] are zeroed by
+// the next call's bk_hist_kernel.  The poll is still bounded (a hardware stall, or
+// the test-only stall knob which adds `stall` to the target): the workgroup then sets
+// the sticky error word hdr[kLgErrWord] (never cleared by a kernel; the host reads and
+// clears it: mrec_emb_bwd_large_error_offset) and leaves WITHOUT touching any row --
+// an update is never applied from partial sums.
+constexpr int kLgErrWord = 8;
+
+__device__ __forceinline__ bool lg_wait_done(int32_t *ctr, int target, int bound) {
+  for (int spins = 0; __hip_atomic_load(ctr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < target;) {
+    __builtin_amdgcn_s_sleep(2);
+    if (++spins > bound) return false;
   }
-  __syncthreads();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+  return true;
 }
 
-// the fused path's huge segments (> kLgHuge lookups of one row): max |g|, the
-// fixed-point chunk sums and the per-row update as three phases of ONE launch
-// (grid barriers between them).  The bucket kernel counts the huge segments in
-// hdr[3]; with none (the common case: DIN's padding slots skip the PAD row) every
-// workgroup leaves at once, so the step pays one empty launch instead of three.
-// hdr[4] counts arrivals (2 barriers + 1 exit per workgroup; the last exit resets
-// it), hdr[6] is the barrier's time-out flag.
 template <typename T, int LPR>
 __global__ __launch_bounds__(256) void lg_huge_kernel(BankArgs bank, int64_t n, LgWs w,
-                                                      ApplyArgs a, int stride) {
+                                                      ApplyArgs a, int stride, int stall,
+                                                      int bound) {
+  constexpr int WPB = 256 / LPR;
   if (__hip_atomic_load(w.hdr + 3, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0) return;
-  const int G = static_cast<int>(gridDim.x);
-  lg_longmax_body<T, LPR>(bank, n, w, a);
-  lg_grid_sync(w.hdr + 4, G);
-  lg_longacc_body<T, LPR>(bank, n, w, a, stride);
-  lg_grid_sync(w.hdr + 4, 2 * G);
-  lg_apply_body<T, LPR>(bank, n, w, a, stride);
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();
-  if (threadIdx.x == 0 &&
-      __hip_atomic_fetch_add(w.hdr + 4, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 3 * G - 1)
-    __hip_atomic_store(w.hdr + 4, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  __shared__ int s_item, s_ok;
+  if (a.d_step) a.seed += *a.d_step * 0x9e3779b97f4a7c15ull;
+  const int nc = w.hdr[2];
+  const int n_items = 2 * nc + (w.hdr[0] + WPB - 1) / WPB;
+  int seen = 0;  // phases this workgroup has seen complete
+  for (;;) {
+    if (threadIdx.x == 0)
+      s_item = __hip_atomic_fetch_add(w.hdr + 4, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __syncthreads();
+    const int it = s_item;
+    if (it >= n_items) break;
+    const int ph = it < nc ? 0 : it < 2 * nc ? 1 : 2;
+    if (ph > seen) {
+      if (threadIdx.x == 0) {
+        bool ok = lg_wait_done(w.hdr + 4 + ph, nc + stall, bound);
+        if (!ok) __hip_atomic_store(w.hdr + kLgErrWord, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        s_ok = ok;
+      }
+      __syncthreads();
+      if (!s_ok) break;  // uniform: no partial sums ever reach a row
+      seen = ph;
+    }
+    if (ph == 0)
+      lg_longmax_chunk<T, LPR>(bank, w, a, it);
+    else if (ph == 1)
+      lg_longacc_chunk<T, LPR>(bank, w, a, stride, it - nc);
+    else
+      lg_apply_block<T, LPR>(bank, w, a, stride, it - 2 * nc);
+    if (ph < 2) {  // publish this item's atomics / stores, then count it done
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __syncthreads();
+      if (threadIdx.x == 0) {
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __hip_atomic_fetch_add(w.hdr + 5 + ph, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      }
+    } else {
+      __syncthreads();  // s_item is rewritten by the next dequeue
+    }
+  }
 }
 
 // ---- fused bucketed plan + apply (mrec_emb_bwd_large_fused) ---------------------
@@ -1309,17 +1370,23 @@ static void lg_launch_apply(const BankArgs &ba, int64_t batch, const LgWs &w, co
     const int64_t cc = ul + (N + kLgChunk - 1) / kLgChunk + 2;
     gc = dim3(static_cast<unsigned>(std::min<int64_t>(cc, kLgApplyBlocks)));
     gu = dim3(static_cast<unsigned>(std::min<int64_t>((ul + 256 / L - 1) / (256 / L), kLgApplyBlocks)));
-    static const int resident = [] {  // workgroups the grid barrier may count on
-      int dev = 0, cus = 0, per = 0;
+    // any grid size is correct (dequeued items, no co-residency); enough to fill the
+    // chip when there is work, and every workgroup leaves at once when there is none
+    static const int cus = [] {
+      int dev = 0, c = 0;
       (void)hipGetDevice(&dev);
-      (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
-      (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, lg_huge_kernel<T, L>, 256, 0);
+      (void)hipDeviceGetAttribute(&c, hipDeviceAttributeMultiprocessorCount, dev);
       (void)hipGetLastError();
-      return std::max(1, cus) * std::max(1, std::min(per, 2));
+      return std::max(1, c);
     }();
     const int64_t need = std::max<int64_t>(gc.x, gu.x);
-    lg_huge_kernel<T, L><<<dim3(static_cast<unsigned>(std::min<int64_t>(need, resident))), 256, 0, s>>>(
-        ba, batch, w, a, stride);
+    int stall = 0, bound = 1 << 26;  // ~seconds of 128-cycle sleeps
+    if (const char *e = std::getenv("MREC_LG_HUGE_TEST_STALL")) {  // test-only: force the time-out
+      stall = std::atoi(e);
+      if (stall) bound = 1 << 14;
+    }
+    lg_huge_kernel<T, L><<<dim3(static_cast<unsigned>(std::min<int64_t>(need, 2 * cus))), 256, 0, s>>>(
+        ba, batch, w, a, stride, stall, bound);
     return;
   }
   lg_longmax_kernel<T, L><<<gc, 256, 0, s>>>(ba, batch, w, a);
@@ -1354,6 +1421,8 @@ static void lg_dispatch_apply(mrec_dtype dtype, int lpr, const BankArgs &ba, int
 }
 
 extern "C" {
+
+size_t mrec_emb_bwd_large_error_offset(void) { return kLgErrWord * sizeof(int32_t); }
 
 mrec_status mrec_emb_bwd_large_apply(const mrec_table_bank *bank, int64_t batch,
                                      const void *workspace, size_t ws_bytes, const void *dx,

@@ -130,7 +130,7 @@ __global__ __launch_bounds__(kBT) void bucketize_kernel(IdsArgs ids, RowsArg row
     }
     const uint32_t slot = hist[d * G + r * kBWaves + wid] + __popcll(m & lt) - hist[d * G];
     if (slot >= static_cast<uint32_t>(cap)) {
-      if (overflow) *overflow = 1;
+      if (overflow) atomicOr(overflow, 1);  // bit 0: a table's `cap` slots
       pos[f * B + i] = -1;
       continue;
     }
@@ -239,7 +239,7 @@ __global__ __launch_bounds__(kBT) void bucketize_dedup_kernel(IdsArgs ids, RowsA
     if (d == static_cast<uint32_t>(W)) continue;
     uint32_t slot = hist[d * G + r * kBWaves + wid] + __popcll(m & lt) - hist[d * G];
     if (slot >= static_cast<uint32_t>(cap)) {
-      if (overflow) *overflow = 1;
+      if (overflow) atomicOr(overflow, 1);  // bit 0: a table's `cap` slots
       slot = 0xffffu;
     } else {
       send_ids[d * P + static_cast<int64_t>(f) * cap + slot] =
@@ -318,7 +318,7 @@ __device__ __forceinline__ int wire_prefix(const WireArgs &w, int p, int *pre) {
   __syncthreads();
   int tot = pre[w.F];
   if (tot > w.cap_rows) {
-    if (w.overflow && threadIdx.x == 0) *w.overflow = 1;
+    if (w.overflow && threadIdx.x == 0) atomicOr(w.overflow, 2);  // bit 1: `cap_rows` records
     tot = w.cap_rows;
   }
   return tot;

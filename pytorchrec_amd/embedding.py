@@ -211,6 +211,24 @@ class EmbeddingBank(torch.nn.Module):
         self._seed = (self._seed * 6364136223846793005 + 1442695040888963407) & (2 ** 64 - 1)
         return self._seed
 
+    def check_flags(self):
+        """Raise if a large-batch backward since the last check could not finish its
+        huge-segment phases (the workspace's sticky error word, ABI 25: those rows were
+        left un-updated, never updated from partial sums).  Syncs once; clears the
+        word.  IModel.fit calls it at the end of every epoch, the id-checking mode
+        after every large backward."""
+        cache = getattr(self, "_large_ws_cache", None)
+        if cache is None:
+            return
+        off = int(_mrec.lib().mrec_emb_bwd_large_error_offset())
+        word = cache[1][off:off + 4].view(torch.int32)
+        err = int(word.item())
+        if err:
+            word.zero_()
+            raise RuntimeError("embedding backward: the huge-segment phases of a large-batch "
+                               "update timed out waiting for each other (a stalled GPU); the "
+                               "rows hit > 2048 times in that step were not updated")
+
     # -- table views (for checkpoints / tests) ----------------------------------
     def table(self, f: int) -> torch.Tensor:
         o = self.row_offset[f]
@@ -383,6 +401,8 @@ def _backward_large(bank: EmbeddingBank, ids, batch, grad, dx=None, dfm=None, fm
     _mrec.call("mrec_emb_bwd_large_fused_ex", bank.desc().ref(), _ids_desc(ids).ref(), batch,
                ws.data_ptr(), ws.numel(), None, *args[:-1], len(jobs), arr, args[-1])
     del jobs
+    if bank.check_ids and not torch.cuda.is_current_stream_capturing():
+        bank.check_flags()
 
 
 def _large_apply_args(bank, grad, dx, dfm, fm_sum, x0, dw, mode, lr):

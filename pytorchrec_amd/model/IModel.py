@@ -420,6 +420,7 @@ class IModel(Module, IWithArguments, ABC):
             for data in self._loader(dataset, batch_size, shuffle, workers, drop_last):
                 logs = self.train_step(data)
             epoch_logs = {k: float(v.detach() if torch.is_tensor(v) else v) for k, v in logs.items()}
+            self.check_embedding_flags()
             if dev_dataset is not None and (epoch + 1) % dev_freq == 0:
                 epoch_logs.update(self.evaluate(dev_dataset, dev_batch_size or batch_size,
                                                 verbose=verbose, workers=workers))
@@ -451,6 +452,15 @@ class IModel(Module, IWithArguments, ABC):
         preds = [self.predict_step(d).detach().float().cpu().numpy()
                  for d in self._loader(dataset, batch_size, workers=workers)]
         return np.concatenate(preds) if preds else np.zeros(0)
+
+    def check_embedding_flags(self):
+        """Raise any sticky device-side error of the model's embedding banks (exchange
+        overflow / out-of-range ids of a row-sharded bank, an unfinished huge-segment
+        update of a large-batch backward).  One sync per bank."""
+        for bank in self.embedding_banks():
+            chk = getattr(bank, "check_flags", None)
+            if chk is not None:
+                chk()
 
     def _assert_compile_was_called(self):
         if not self._is_compiled:

@@ -257,9 +257,14 @@ class ShardedEmbeddingBank(EmbeddingBank):
         return int(_mrec.lib().mrec_shard_wire_bytes(self.dim, int(self.has_w), dt))
 
     def use_compact(self, batch: int) -> bool:
+        """The compact exchange when it is on and mrec_shard_bucketize_dedup takes the
+        shape: B <= 8192 (16-bit sample index), cap < 65535, and its per-(owner,
+        wave-group) histogram (world + 1) * ceil(B / 1024) * 16 <= 2048 entries
+        (e.g. W >= 16 at B = 8192 falls back to the slot exchange)."""
         on = self.compact == "always" or (bool(self.compact) and self.world > 1)
+        groups = max(1, -(-int(batch) // 1024) * 16)
         return (on and self.update != "adam" and batch <= _mrec.BWD_MAX_BATCH
-                and self.cap < 65535)
+                and self.cap < 65535 and (self.world + 1) * groups <= 2048)
 
     @property
     def g_ld(self) -> int:
@@ -276,11 +281,19 @@ class ShardedEmbeddingBank(EmbeddingBank):
         f = self.flags()
         ov, oob = (int(x) for x in f.tolist())
         f.zero_()
-        if ov:  # (overflowed lookups also read slot -1, which sets the OOB flag)
+        if ov & 1:  # (overflowed lookups also read slot -1, which sets the OOB flag)
             raise RuntimeError(f"row-sharded exchange overflow: more than cap={self.cap} ids of "
-                               "one table for one owner in a batch; raise cap")
+                               "one table for one owner in a batch; raise `cap` "
+                               "(sharded_tables(cap=...))")
+        if ov & 2:
+            raise RuntimeError(f"row-sharded compact exchange overflow: more than cap_rows="
+                               f"{self.cap_rows} distinct ids for one owner over all tables in a "
+                               "batch (their rows were not exchanged and got no update); raise "
+                               "`cap_rows` (ShardedEmbeddingBank.cap_rows, default "
+                               "default_cap_rows: mean + 8 sd)")
         if oob:
             raise IndexError("index out of range in self")
+        super().check_flags()
 
     # -- global <-> shard ------------------------------------------------------
     @torch.no_grad()

@@ -456,6 +456,64 @@ def test_bucketed_plan_matches_atomic_plan(gpu, B, hot, update, monkeypatch):
         assert np.allclose(got["fused"].view(np.float32)[:nums[0]], want, rtol=1e-5, atol=1e-7)
 
 
+def test_huge_segment_wait_timeout_raises_and_leaves_rows_untouched(gpu, monkeypatch):
+    """The fused large-batch path sums rows hit > 2048 times in one launch of three
+    dependent phases (max |g|, fixed-point chunk sums, the update) whose work items
+    are dequeued in phase order: no co-residency is assumed, so a phase wait always
+    ends.  Its waits are still bounded; MREC_LG_HUGE_TEST_STALL=1 (test-only) makes
+    them unreachable.  Then the backward raises RuntimeError (the workspace's sticky
+    error word, read by EmbeddingBank.check_flags), the huge rows keep their bits
+    (never an update from partial sums), every other row gets exactly the update of
+    a normal run, and the next normal call is clean and bitwise equal to the atomic
+    plan."""
+    from pytorchrec_amd import embedding as E
+    rng = np.random.default_rng(77)
+    nums, D, B = [63002, 802], 16, 20000
+    ids_np = np.stack([rng.integers(0, n, B) for n in nums], 1)
+    ids_np[rng.random(B) < 0.3, 0] = 5   # row 5 of table 0: ~6000 lookups (huge)
+    ids_np[rng.random(B) < 0.2, 1] = 3   # row 3 of table 1: ~4000 lookups (huge)
+    ids = [torch.from_numpy(ids_np[:, f].astype(np.int32)).to(gpu) for f in range(2)]
+    dy = torch.from_numpy((rng.standard_normal((B, 2 * D)) * 1e-2).astype(np.float32)).to(gpu)
+    tabs = [ref.f32_to_bf16_bits((rng.standard_normal((n, D)) * 0.1).astype(np.float32))
+            for n in nums]
+    def run(stall, atomic=False):
+        if stall:
+            monkeypatch.setenv("MREC_LG_HUGE_TEST_STALL", "1")
+        if atomic:
+            monkeypatch.setenv("MREC_LG_ATOMIC_PLAN", "1")
+        bank = _bank(nums, D, False, torch.bfloat16, update="sgd")
+        bank.use_fused_sgd(0.5)
+        bank.stochastic_rounding = False
+        _fill(bank, tabs)
+        b0 = _bits(bank.weight[:, :D])
+        out = E.gather(bank, ids, out_dtype=torch.float32)
+        err = None
+        try:
+            out.backward(dy)
+            torch.cuda.synchronize()
+        except RuntimeError as e:
+            err = e
+        monkeypatch.delenv("MREC_LG_HUGE_TEST_STALL", raising=False)
+        monkeypatch.delenv("MREC_LG_ATOMIC_PLAN", raising=False)
+        return bank, b0, _bits(bank.weight[:, :D]), err
+
+    monkeypatch.setattr(E, "LARGE_FUSED", True)
+    bank_s, before, stalled, err = run(True)
+    huge = [bank_s.row_offset[0] + 5, bank_s.row_offset[1] + 3]
+    assert err is not None and "huge-segment" in str(err), err
+    bank_s.check_flags()  # the word was cleared by the raise
+    _, _, normal, err2 = run(False)
+    assert err2 is None
+    _, _, atomic, _ = run(False, atomic=True)
+    assert np.array_equal(normal, atomic)
+    for r in huge:
+        assert np.array_equal(stalled[r], before[r]), r      # untouched, not half-updated
+        assert not np.array_equal(normal[r], before[r]), r   # a normal run does move them
+    keep = np.ones(stalled.shape[0], bool)
+    keep[huge] = False
+    assert np.array_equal(stalled[keep], normal[keep])
+
+
 def test_backward_large_batch_sgd_one_update_per_row(gpu):
     """Fused SGD at B > MREC_BWD_MAX_BATCH updates every touched row exactly once:
     new = RNE_bf16(old - lr * sum g), equal to the fp64 oracle's sum rounded once

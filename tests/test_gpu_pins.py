@@ -72,7 +72,7 @@ def test_c3_cross_net_at_config_shape(gpu):
         check(bg[i].grad, grads[i][1], f"db{i}")
 
 
-def _dcnv2_pair(gpu, rows, B, scale_cross=8.0, scale_mlp=6.0):
+def _dcnv2_pair(gpu, rows, B, scale_cross=8.0, scale_mlp=6.0, emb_dtype=torch.float32):
     import torch.nn as nn
     from oracle.models import RefDCNv2
     from pytorchrec_amd.feature_column import CategoricalColumnWithIdentity, NumericColumn
@@ -82,7 +82,8 @@ def _dcnv2_pair(gpu, rows, B, scale_cross=8.0, scale_mlp=6.0):
     dense = [NumericColumn(f"c_n_I{j + 1}") for j in range(13)]
     lab = CategoricalColumnWithIdentity(2, "label")
     m = DCNv2(sparse, dense, lab, emb_size=16, cross_layers=3, layers=(400, 400),
-              emb_dtype=torch.float32, device=gpu, random_seed=2020)
+              emb_dtype=emb_dtype, device=gpu, random_seed=2020)
+    m.embeddings.stochastic_rounding = False
     with torch.no_grad():  # weights large enough that every layer matters
         for c in m.cross:
             c.weight.mul_(scale_cross)
@@ -102,13 +103,16 @@ def _dcnv2_pair(gpu, rows, B, scale_cross=8.0, scale_mlp=6.0):
     return m, r, sparse, dense, nums
 
 
-def test_c3_dcnv2_train_step_matches_oracle_model(gpu):
+@pytest.mark.parametrize("emb_dtype", [torch.float32, torch.bfloat16], ids=["fp32", "bf16"])
+def test_c3_dcnv2_train_step_matches_oracle_model(gpu, emb_dtype):
     """One DCN-v2 train step at the C3 shape (26 x 38,462 rows, D = 16, 13 dense,
     3 cross layers of 429, deep 400-400, B = 4096, plain SGD fused into every
     backward kernel) against RefDCNv2 (the reference-path torch model, fp64) from
-    identical weights: the loss and every parameter's UPDATE.  Tables are fp32
-    here so the update is not hidden by bf16 table rounding; x0 and the towers are
-    bf16.  At this shape bf16 storage alone moves the gradients by several percent
+    identical weights: the loss and every parameter's UPDATE.  Tables fp32 (the
+    reference's dtype: the update is not hidden by table rounding) and bf16 (what
+    the C3 bench line runs: RNE table rounding, lr 1e4 so the table updates are
+    tens of bf16 ulps and the emulation's tables are rounded the same way); x0 and
+    the towers are bf16.  At this shape bf16 storage alone moves the gradients by several percent
     (the 400-wide ReLU layers sum ~400 terms with heavy cancellation): the same
     model in torch fp32 with bf16 rounding at the build's storage points
     (``RefDCNv2(bf16_points=True)``, run here on the GPU) is 5-8 % (L2) and
@@ -119,8 +123,11 @@ def test_c3_dcnv2_train_step_matches_oracle_model(gpu):
     import torch.nn as nn
     from oracle.models import RefDCNv2, criteo_batch, sgd_train_step
     from pytorchrec_amd.loss import BCEWithLogitsLoss
-    B, lr = 4096, 1.0  # updates well above the fp32 resolution of the tables
-    m, r, sparse, dense, nums = _dcnv2_pair(gpu, 38462, B)
+    bf16 = emb_dtype == torch.bfloat16
+    # table updates well above the tables' resolution (bf16: ~40 ulps median)
+    B, lr = 4096, (1e4 if bf16 else 1.0)
+    m, r, sparse, dense, nums = _dcnv2_pair(gpu, 38462, B, emb_dtype=emb_dtype)
+    assert m.embeddings.weight.dtype == emb_dtype
     ids, dn, label = criteo_batch(nums, B, seed=0)
     data = {c.feature_name: ids[:, f].to(torch.int32).to(gpu) for f, c in enumerate(sparse)}
     data.update({c.feature_name: dn[:, j].to(gpu) for j, c in enumerate(dense)})
@@ -152,8 +159,9 @@ def test_c3_dcnv2_train_step_matches_oracle_model(gpu):
             eg, ee = norm(dg - dw), norm(de - dw)
             assert eg <= 1.5 * ee + 0.01 * norm(dw), (name, eg / norm(dw), ee / norm(dw))
 
+    rnd = (lambda t: t.detach().to(torch.bfloat16)) if bf16 else (lambda t: t.detach())  # noqa: E731
     for f in range(26):
-        upd_close(m.embeddings.table(f).detach(), e.emb[f].weight.detach(),
+        upd_close(m.embeddings.table(f).detach(), rnd(e.emb[f].weight),
                   r.emb[f].weight.detach(), before_t[f], f"table{f}")
     ml = list(m.cross) + [x for x in m.mlp.modules() if isinstance(x, nn.Linear)] + [m.prediction]
     for i, (a, b_, c_) in enumerate(zip(ml, rl, el)):
@@ -558,3 +566,131 @@ def test_columns_on_cuda_match_reference_g8(gpu):
         got = num.get_feature_data(xb, mode)
         assert got.is_cuda and got.dtype == torch.float32
         assert np.array_equal(got.cpu().numpy().view(np.uint32), g[key].view(np.uint32)), key
+
+
+# ---------------------------------------------------------------------------
+# C4: the composed DIN train step at the config shape
+# ---------------------------------------------------------------------------
+
+def test_c4_din_train_step_matches_oracle_model(gpu, monkeypatch):
+    """One DIN train step at the C4 shape (item 63,001 + PAD / category 801 + PAD
+    bf16 tables, D = 16, L = 50 with lengths U{1..50}, attention MLP 80-40-1, top
+    MLP 200-80-1, B = 4096, plain SGD, RNE table rounding) on the PRODUCT path --
+    ``mrec_din_gather`` (lookup ids with padding slots built in the gather launch),
+    the fused attention unit (``mrec_din_att_fwd`` / ``_bwd`` / ``_wgrad`` with the
+    fused SGD of the attention MLP), the fused top tower with its deferred dW
+    reductions riding in the bucketed embedding-backward launch
+    (``mrec_emb_bwd_large_fused_ex`` with jobs), and the bucketed fused SGD of the
+    tables -- against RefDIN (the reference-path torch model, fp64) from identical
+    weights: the loss and every parameter's UPDATE.
+
+    The bar is the C2 / C3 one: ``RefDIN(bf16_points=True)`` in fp32 on the GPU
+    (bf16 at the build's storage points, its tables rounded to bf16 after the step
+    like the bank's) sets what bf16 storage alone costs (tables 3-6 % L2, the
+    attention MLP 1-3 %, the top tower 0.1-1 %); the kernels' error against fp64
+    may not exceed 1.5x the emulation's + 1 % of the update.  Scales: attention
+    weights x40 and rows x10 (scores spread ~1.6 std: a peaked, not uniform,
+    softmax, so every term of the unit's backward matters), top tower x6, lr 1e5
+    (table updates ~20 bf16 ulps median).  The attention output bias gets an
+    analytically zero gradient (sum_j ds_j = 0): its update is bounded by 1e-4 of
+    the score weights' update."""
+    import torch.nn as nn
+    from oracle.models import RefDIN, din_batch, sgd_train_step
+    from pytorchrec_amd import _mrec
+    from pytorchrec_amd import dense as D
+    from pytorchrec_amd.feature_column import CategoricalColumnWithIdentity
+    from pytorchrec_amd.loss import BCEWithLogitsLoss
+    from pytorchrec_amd.model import DIN
+    B, L, lr, ITEMS, CATES = 4096, 50, 1e5, 63002, 802
+    cols = [CategoricalColumnWithIdentity(ITEMS, "iid"), CategoricalColumnWithIdentity(CATES, "cid"),
+            CategoricalColumnWithIdentity(ITEMS, "pos_his"),
+            CategoricalColumnWithIdentity(CATES, "pos_his_cate")]
+    m = DIN(*cols, CategoricalColumnWithIdentity(2, "label"), emb_size=16, att_layers=(80, 40),
+            layers=(200, 80), emb_dtype=torch.bfloat16, device=gpu, random_seed=2020)
+    m.embeddings.stochastic_rounding = False
+    r = RefDIN(ITEMS, CATES, 16, (80, 40), (200, 80), dtype=torch.float64)
+    with torch.no_grad():
+        for p in list(r.att_mlp.parameters()) + list(r.att_out.parameters()):
+            p.mul_(40.0)
+        for p in list(r.mlp.parameters()) + [r.out.weight]:
+            p.mul_(6.0)
+        for t in (r.item, r.cate):  # bf16-representable tables shared by all three models
+            t.weight.copy_((t.weight * 10.0).to(torch.bfloat16).double())
+        m.embeddings.table(0).copy_(r.item.weight.to(gpu))
+        m.embeddings.table(1).copy_(r.cate.weight.to(gpu))
+    pairs = [(a, b_) for a, b_ in zip(
+        [x for x in m.att_mlp.modules() if isinstance(x, nn.Linear)] + [m.att_out]
+        + [x for x in m.mlp.modules() if isinstance(x, nn.Linear)] + [m.prediction],
+        [x for x in r.att_mlp.modules() if isinstance(x, nn.Linear)] + [r.att_out]
+        + [x for x in r.mlp.modules() if isinstance(x, nn.Linear)] + [r.out])]
+    assert len(pairs) == 6
+    with torch.no_grad():
+        for a, b_ in pairs:
+            a.weight.copy_(b_.weight.to(gpu))
+            a.bias.copy_(b_.bias.to(gpu))
+    before_state = [v.clone() for v in r.state_dict().values()]
+    before_t = [r.item.weight.detach().clone(), r.cate.weight.detach().clone()]
+    before_l = [(b_.weight.detach().clone(), b_.bias.detach().clone()) for _, b_ in pairs]
+    iid, cid, his, hcat, label = din_batch(ITEMS, CATES, B, L, seed=0)
+    data = {"iid": iid.to(torch.int32).to(gpu), "cid": cid.to(torch.int32).to(gpu),
+            "pos_his": his.to(torch.int32).to(gpu), "pos_his_cate": hcat.to(torch.int32).to(gpu),
+            "label": label.to(gpu)}
+    m.compile(torch.optim.SGD(m.get_parameters(), lr=lr), BCEWithLogitsLoss(), [], gpu)
+    assert m.embeddings.update == "sgd" and m.embeddings.weight.dtype == torch.bfloat16
+    assert D.DIN_FUSED and D.din_att_supported(32, m.att_mlp, m.att_out)
+    calls = []
+    real_call = _mrec.call
+
+    def spy(name, *args):
+        calls.append((name, args))
+        return real_call(name, *args)
+
+    monkeypatch.setattr(_mrec, "call", spy)
+    loss = float(m.train_step(data)["loss"].detach())
+    torch.cuda.synchronize()
+    monkeypatch.setattr(_mrec, "call", real_call)
+    names = [n for n, _ in calls]
+    for want in ("mrec_din_gather", "mrec_din_att_fwd", "mrec_din_att_bwd", "mrec_din_att_wgrad",
+                 "mrec_emb_bwd_large_fused_ex"):
+        assert want in names, (want, names)
+    ex = [a for n, a in calls if n == "mrec_emb_bwd_large_fused_ex"]
+    assert len(ex) == 1 and ex[0][-3] > 0, "the top tower's dW reductions must ride in the bucket launch"
+    # the attention MLP took its fused SGD in place (no gradient handed back)
+    wg = [a for n, a in calls if n == "mrec_din_att_wgrad"]
+    assert wg[0][5] is None and wg[0][6] == lr
+    rloss = float(sgd_train_step(r, torch.optim.SGD(r.parameters(), lr=lr),
+                                 (iid, cid, his, hcat), None, label.double()).detach())
+    assert abs(loss - rloss) <= 2e-3 * max(1.0, abs(rloss)), (loss, rloss)
+    e = RefDIN(ITEMS, CATES, 16, (80, 40), (200, 80), dtype=torch.float32, bf16_points=True)
+    e.load_state_dict(dict(zip(e.state_dict(), before_state)))
+    e = e.to(gpu)
+    sgd_train_step(e, torch.optim.SGD(e.parameters(), lr=lr),
+                   tuple(t.to(gpu) for t in (iid, cid, his, hcat)), None, label.to(gpu))
+
+    def upd_close(got_after, emu_after, want_after, before, name):
+        dg = got_after.double().cpu() - before
+        de = emu_after.double().cpu() - before
+        dw = want_after.double() - before
+        assert torch.isfinite(dg).all(), name
+        assert float(dw.abs().max()) > 0, name
+        for norm in (lambda t: float(t.norm()), lambda t: float(t.abs().max())):
+            eg, ee = norm(dg - dw), norm(de - dw)
+            assert eg <= 1.5 * ee + 0.01 * norm(dw), (name, eg / norm(dw), ee / norm(dw))
+
+    rnd = lambda t: t.detach().to(torch.bfloat16)  # noqa: E731  the bank's rounding
+    upd_close(m.embeddings.table(0).detach(), rnd(e.item.weight), r.item.weight.detach(),
+              before_t[0], "item")
+    upd_close(m.embeddings.table(1).detach(), rnd(e.cate.weight), r.cate.weight.detach(),
+              before_t[1], "cate")
+    # PAD rows (id 0) only ever sit at masked positions here (lengths >= 1): no update
+    assert torch.equal(m.embeddings.table(0)[0].double().cpu(), before_t[0][0])
+    el = ([x for x in e.att_mlp.modules() if isinstance(x, nn.Linear)] + [e.att_out]
+          + [x for x in e.mlp.modules() if isinstance(x, nn.Linear)] + [e.out])
+    for i, ((a, b_), c_) in enumerate(zip(pairs, el)):
+        upd_close(a.weight.detach(), c_.weight.detach(), b_.weight.detach(), before_l[i][0], f"W{i}")
+        if i == 2:  # score bias: sum_j ds_j = 0
+            db = float((a.bias.detach().double().cpu() - before_l[i][1]).abs().max())
+            dw3 = float((b_.weight.detach() - before_l[i][0]).abs().max())
+            assert db <= 1e-4 * dw3, (db, dw3)
+            continue
+        upd_close(a.bias.detach(), c_.bias.detach(), b_.bias.detach(), before_l[i][1], f"b{i}")

@@ -240,3 +240,39 @@ def test_g9_full_size_c2_hash_and_checksum():
     sums, head = m.c2_checksum(z)
     np.testing.assert_allclose(sums, g["c2_fm_sums"], rtol=1e-10)
     np.testing.assert_allclose(head, g["c2_fm_head"], rtol=1e-12)
+
+
+def test_refdin_model_agrees_with_numpy_oracle_and_bf16_emulation_is_close():
+    """oracle.models.RefDIN (the C4 step oracle, fp64) against the numpy
+    restatement ``ref.din_attention_pool`` (pinned to the reference's masked
+    softmax by G5 above) and the reference MLP (``ref.mlp_fwd``, pinned by G6): the
+    same logits on a small seeded batch with ragged histories, PAD positions
+    included.  Its ``bf16_points`` twin stays within a few percent of it (that
+    distance sizes the C4 GPU test's bar)."""
+    import torch
+    from oracle.models import RefDIN, din_batch
+    r = RefDIN(501, 37, 16, (80, 40), (200, 80), dtype=torch.float64)
+    with torch.no_grad():
+        for p in list(r.att_mlp.parameters()) + list(r.att_out.parameters()):
+            p.mul_(40.0)
+        for t in (r.item, r.cate):
+            t.weight.mul_(10.0)
+    iid, cid, his, hcat, _ = din_batch(501, 37, 64, 50, seed=4)
+    assert (his == 0).any() and (his[:, 0] > 0).all()
+    with torch.no_grad():
+        got = r(iid, cid, his, hcat).numpy()
+        q = torch.cat([r.item(iid), r.cate(cid)], -1).numpy()
+        k = torch.cat([r.item(his), r.cate(hcat)], -1).numpy()
+        lin = lambda ms: [(m.weight.numpy(), m.bias.numpy()) for m in ms  # noqa: E731
+                          if isinstance(m, torch.nn.Linear)]
+        u, a, s = ref.din_attention_pool(q, k, ref.valid_his_index(his.numpy()), lin(r.att_mlp),
+                                         (r.att_out.weight.numpy(), r.att_out.bias.numpy()))
+        assert np.all(a[ref.valid_his_index(his.numpy()) == 0] == 0)
+        h = ref.mlp_fwd(np.concatenate([q, u], 1), lin(r.mlp))[-1]
+        want = ref.linear(h, r.out.weight.numpy(), r.out.bias.numpy())[:, 0]
+    np.testing.assert_allclose(got, want, rtol=1e-12, atol=1e-12)
+    e = RefDIN(501, 37, 16, (80, 40), (200, 80), dtype=torch.float32, bf16_points=True)
+    e.load_state_dict({k_: v.float() for k_, v in r.state_dict().items()})
+    with torch.no_grad():
+        emu = e(iid, cid, his, hcat).double().numpy()
+    assert np.abs(emu - got).max() <= 0.05 * np.abs(got).max()

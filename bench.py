@@ -58,6 +58,8 @@ def parse(argv=None):
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--cpu-seconds", type=float, default=12.0)
     p.add_argument("--no-roofline", action="store_true")
+    p.add_argument("--standalone-roofline", action="store_true",
+                   help="also time the embedding kernels launched alone (frac_standalone)")
     p.add_argument("--no-h2d", action="store_true",
                    help="skip the PCIe-inclusive (host-fed columnar loader) measurement")
     p.add_argument("--shard", action="store_true",
@@ -109,6 +111,13 @@ def launch(args) -> int:
         procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + sys.argv[1:],
                                       env=env, stdout=subprocess.PIPE if r == 0 else
                                       subprocess.DEVNULL))
+    # rank 0's stdout is drained while the ranks run (a reader thread), so a child
+    # that prints more than a pipe buffer never blocks on a full pipe
+    import threading
+    out_chunks = []
+    reader = threading.Thread(target=lambda: out_chunks.extend(iter(
+        lambda: procs[0].stdout.read1(65536), b"")), daemon=True)
+    reader.start()
     rc = 0
     try:
         while True:
@@ -131,7 +140,8 @@ def launch(args) -> int:
         for q in procs:
             if q.poll() is None:
                 q.kill()
-    out0 = procs[0].stdout.read() if procs[0].stdout is not None else b""
+    reader.join(timeout=30)
+    out0 = b"".join(out_chunks)
     lines = [ln for ln in out0.decode(errors="replace").splitlines() if ln.startswith("{")]
     if rc == 0 and lines:
         print(lines[-1], flush=True)
@@ -307,41 +317,291 @@ def time_launches(fn, reps=100):
     return e0.elapsed_time(e1) / reps * 1e-3  # seconds per launch
 
 
-def tower_rooflines(model, step, datas, widths, B, steps=20):
-    """The dense tower's two launches timed INSIDE eager training steps (HIP events
-    around each launch on its stream, dense.KERNEL_EVENTS): the fused tower
-    (forward + input-gradient backward, 2 x 2 B sum_l n_l n_(l+1) flops) and the
-    weight gradients (2 B sum_l n_(l+1) (n_l + 1)).  The tower streams every layer's
-    bf16 weight images (forward + transposed) through each CU once: its bound is
-    the per-CU L2 read rate, reported beside the MFMA fraction."""
-    from pytorchrec_amd import dense as D
-    D.KERNEL_EVENTS = {}
+class GraphKernelTimer:
+    """Times chosen kernel launches INSIDE a captured HIP graph.  While a graph is
+    captured (torch.cuda.CUDAGraph(keep_graph=True)), ``begin()`` / ``end(tag)``
+    around a launch remember the capture's tail node before it and the last node it
+    added (hipStreamGetCaptureInfo_v2).  ``arm(graph)`` then splices an event-record
+    node behind each (hipGraphAddEventRecordNode, the outgoing edges rewired
+    through it) before the graph is instantiated; every
+    replay re-records the events, so ``elapsed(i)`` is kernel i's device time in the
+    replayed step.  (torch refuses ``Event(external=True)`` on ROCm, and a plain
+    event recorded during capture becomes a dependency, not a node.)  Uses the HIP
+    runtime torch loaded (ctypes on the same libamdhip64)."""
+    _hip = None
+
+    @classmethod
+    def hip(cls):
+        if cls._hip is None:
+            import ctypes
+            import glob
+            c = ctypes
+            cands = glob.glob(os.path.join(os.path.dirname(torch.__file__), "lib", "libamdhip64.so*"))
+            h = c.CDLL(cands[0] if cands else "libamdhip64.so")
+            vp, sz = c.c_void_p, c.c_size_t
+            h.hipStreamGetCaptureInfo_v2.argtypes = [vp, c.POINTER(c.c_int), c.POINTER(c.c_ulonglong),
+                                                     c.POINTER(vp), c.POINTER(c.POINTER(vp)),
+                                                     c.POINTER(sz)]
+            h.hipGraphNodeGetDependencies.argtypes = [vp, c.POINTER(vp), c.POINTER(sz)]
+            h.hipGraphNodeGetDependentNodes.argtypes = [vp, c.POINTER(vp), c.POINTER(sz)]
+            h.hipGraphRemoveDependencies.argtypes = [vp, c.POINTER(vp), c.POINTER(vp), sz]
+            h.hipGraphAddDependencies.argtypes = [vp, c.POINTER(vp), c.POINTER(vp), sz]
+            h.hipGraphAddEventRecordNode.argtypes = [c.POINTER(vp), vp, c.POINTER(vp), sz, vp]
+            h.hipEventCreateWithFlags.argtypes = [c.POINTER(vp), c.c_uint]
+            h.hipEventElapsedTime.argtypes = [c.POINTER(c.c_float), vp, vp]
+            h.hipEventDestroy.argtypes = [vp]
+            cls._hip = h
+        return cls._hip
+
+    @staticmethod
+    def _ok(rc, what):
+        if rc != 0:
+            raise RuntimeError(f"{what}: hipError {rc}")
+
+    def __init__(self):
+        self.nodes = []   # (tag, node before the span or None, last node of the span)
+        self.events = []  # (ev0, ev1) per span, after arm()
+        self._open = None
+
+    def _tail(self):
+        import ctypes as c
+        h = self.hip()
+        st, cid, graph = c.c_int(), c.c_ulonglong(), c.c_void_p()
+        deps, nd = c.POINTER(c.c_void_p)(), c.c_size_t()
+        self._ok(h.hipStreamGetCaptureInfo_v2(c.c_void_p(torch.cuda.current_stream().cuda_stream),
+                                              c.byref(st), c.byref(cid), c.byref(graph),
+                                              c.byref(deps), c.byref(nd)), "capture info")
+        if st.value != 1 or nd.value > 1:  # an active capture of a linear chain
+            raise RuntimeError(f"GraphKernelTimer: capture status {st.value}, {nd.value} tails")
+        return c.c_void_p(deps[0]) if nd.value else None
+
+    def begin(self):
+        """Call right before the launch(es) to time, on the capturing stream."""
+        self._open = self._tail()
+
+    def end(self, tag):
+        """Call right after them: the span from the first to the last node they added."""
+        last = self._tail()
+        if last is None or (self._open is not None and last.value == self._open.value):
+            raise RuntimeError("GraphKernelTimer: no node was captured for " + tag)
+        self.nodes.append((tag, self._open, last))
+
+    def _edges(self, fn, node):
+        import ctypes as c
+        n = c.c_size_t(0)
+        self._ok(fn(node, None, c.byref(n)), "node edges")
+        arr = (c.c_void_p * max(1, n.value))()
+        self._ok(fn(node, arr, c.byref(n)), "node edges")
+        return [c.c_void_p(arr[i]) for i in range(n.value)]
+
+    def arm(self, graph_handle):
+        """Splice the event nodes into the captured graph (before instantiate): ev0 on
+        every edge leaving the node before the span (or in front of the graph's roots
+        when the span starts the graph), ev1 on every edge leaving its last node."""
+        import ctypes as c
+        h = self.hip()
+        g = c.c_void_p(graph_handle)
+
+        def arr(xs):
+            return (c.c_void_p * max(1, len(xs)))(*[x.value for x in xs])
+
+        def splice_after(node, ev):
+            """event node right behind ``node`` (None: in front of the roots)."""
+            n = c.c_void_p()
+            if node is None:
+                roots = self._roots(g)
+                self._ok(h.hipGraphAddEventRecordNode(c.byref(n), g, None, 0, ev), "event node")
+                for r in roots:
+                    self._ok(h.hipGraphAddDependencies(g, arr([n]), arr([r]), 1), "add dep")
+                return
+            succs = self._edges(h.hipGraphNodeGetDependentNodes, node)
+            for y in succs:
+                self._ok(h.hipGraphRemoveDependencies(g, arr([node]), arr([y]), 1), "rm dep")
+            self._ok(h.hipGraphAddEventRecordNode(c.byref(n), g, arr([node]), 1, ev), "event node")
+            for y in succs:
+                self._ok(h.hipGraphAddDependencies(g, arr([n]), arr([y]), 1), "add dep")
+
+        for _, before, last in self.nodes:
+            evs = []
+            for _ in range(2):
+                e = c.c_void_p()
+                self._ok(h.hipEventCreateWithFlags(c.byref(e), 0), "event create")
+                evs.append(e)
+            splice_after(before, evs[0])
+            splice_after(last, evs[1])
+            self.events.append(tuple(evs))
+
+    def _roots(self, g):
+        import ctypes as c
+        h = self.hip()
+        h.hipGraphGetRootNodes.argtypes = [c.c_void_p, c.POINTER(c.c_void_p), c.POINTER(c.c_size_t)]
+        n = c.c_size_t(0)
+        self._ok(h.hipGraphGetRootNodes(g, None, c.byref(n)), "roots")
+        a = (c.c_void_p * max(1, n.value))()
+        self._ok(h.hipGraphGetRootNodes(g, a, c.byref(n)), "roots")
+        return [c.c_void_p(a[i]) for i in range(n.value)]
+
+    def elapsed(self, i) -> float:
+        """Seconds between kernel i's two event nodes in the last replay."""
+        import ctypes as c
+        ms = c.c_float()
+        self._ok(self.hip().hipEventElapsedTime(c.byref(ms), *self.events[i]), "elapsed")
+        return ms.value * 1e-3
+
+    def close(self):
+        h = self.hip()
+        for e0, e1 in self.events:
+            h.hipEventDestroy(e0)
+            h.hipEventDestroy(e1)
+        self.events = []
+
+
+def instep_kernel_times(step, datas, names, steps=4, replays=30, strip_coreduce=False):
+    """Device time of every launch of the named libmrec entry points INSIDE the
+    graph-replayed training step: ``steps`` train steps (batch i % len(datas)) are
+    captured in one HIP graph; each such launch gets an event-record node before
+    and after it (GraphKernelTimer); the graph is replayed ``replays`` times.
+    ``strip_coreduce``: the deferred MLP weight-gradient reductions do not ride in
+    the embedding apply (they run as their own launch at the end of the backward)
+    -- the apply's CoReduce share is the difference.  Returns {name: median
+    seconds per launch}."""
+    from pytorchrec_amd import _mrec, dense as D
+    timer = GraphKernelTimer()
+    real_call, real_take = _mrec.call, D.take_pending
+    capturing = [False]
+
+    def spy(name, *a):
+        if not (capturing[0] and name in names):
+            return real_call(name, *a)
+        timer.begin()
+        r = real_call(name, *a)
+        timer.end(name)
+        return r
+
+    _mrec.call = spy
+    if strip_coreduce:
+        D.take_pending = lambda n=0: []
     try:
-        for i in range(steps):
-            step(datas[i % len(datas)])
-        torch.cuda.synchronize()
-        ev = D.KERNEL_EVENTS
+        s = torch.cuda.Stream()
+        s.wait_stream(torch.cuda.current_stream())
+        with torch.cuda.stream(s):
+            for i in range(2):
+                step(datas[i % len(datas)])
+        torch.cuda.current_stream().wait_stream(s)
+        g = torch.cuda.CUDAGraph(keep_graph=True)
+        capturing[0] = True
+        with torch.cuda.graph(g, capture_error_mode="thread_local"):
+            for i in range(steps):
+                step(datas[i % len(datas)])
+        capturing[0] = False
     finally:
-        D.KERNEL_EVENTS = None
-    L = len(widths) - 1
-    mm = sum(widths[l] * widths[l + 1] for l in range(L))
-    wimg = 2 * 2 * mm  # bf16 forward + transposed images
+        _mrec.call, D.take_pending = real_call, real_take
+    timer.arm(g.raw_cuda_graph())
+    g.instantiate()
+    times = {n: [] for n in names}
+    for _ in range(replays):
+        g.replay()
+        torch.cuda.synchronize()
+        for i, (tag, _, _) in enumerate(timer.nodes):
+            times[tag].append(timer.elapsed(i))
+    g.reset()
+    timer.close()
     out = {}
-    for name, fl in (("mrec_tower_fwd_bwd", 2 * 2 * B * mm),
-                     ("mrec_tower_dw", 2 * B * sum(widths[l + 1] * (widths[l] + 1) for l in range(L)))):
-        pairs = ev.get(name, [])
-        if not pairs:
-            continue
-        ts = sorted(a.elapsed_time(b) * 1e-3 for a, b in pairs)
-        t = ts[len(ts) // 2]  # median over the eager steps
-        d = {"avg_us": round(t * 1e6, 3), "launches": len(ts), "flop": fl,
-             "TFLOP/s": round(fl / t / 1e12, 1), "frac_of_mfma_peak": round(fl / t / 1e12 / MFMA_PEAK_TFLOPS, 4),
-             "timing": "in-step (eager steps, HIP events around the launch, median)"}
-        if name == "mrec_tower_fwd_bwd":
-            d["weight_bytes_per_workgroup"] = wimg
-            d["per_CU_L2_GB/s"] = round(wimg / t / 1e9, 1)
-            d["bound"] = "per-CU L2 read rate (~70 GB/s per CU, MI355X_MICROARCH.md indexed-rows table)"
-        out[name] = d
+    for n, ts in times.items():
+        if ts:
+            ts.sort()
+            out[n] = ts[len(ts) // 2]
+    return out
+
+
+EMB_PAIR = ("mrec_interact_fwd_ex", "mrec_emb_bwd_apply_ex")
+TOWER_PAIR = ("mrec_tower_fwd_bwd", "mrec_tower_dw")
+
+
+def embedding_roofline(model, step, datas, args, in_step=True):
+    """The bench line's ``roofline`` (HBM-bound embedding path) and
+    ``roofline_kernels``.  ``achieved`` = SURVEY.md §8(d) algorithmic bytes of the
+    step's two embedding launches (interaction + plan; apply) / their durations
+    INSIDE the graph-replayed training step (instep_kernel_times: what rocprof's
+    in-step kernel table shows, the apply including the MLP's deferred split-K
+    reductions that ride in it -- their share is reported as
+    ``apply_coreduce_us``, measured as the apply with them moved out).  With
+    --standalone-roofline the kernels launched alone back to back are reported
+    too (``frac_standalone``).  The dense tower's launches (MFMA) are timed in the
+    same captured steps."""
+    D = model.embeddings.dim
+    first_order = bool(model.embeddings.has_w)
+    es = model.embeddings.weight.element_size()
+    F = model.embeddings.n_tables
+    alg_fwd, alg_bwd = alg_bytes_per_sample(F, D, CRITEO_DENSE, first_order, es)
+    nbytes = (alg_fwd + alg_bwd) * args.batch
+    out = {}
+    rk = {}
+    if in_step:
+        t = instep_kernel_times(step, datas, EMB_PAIR + TOWER_PAIR)
+        t_strip = instep_kernel_times(step, datas, EMB_PAIR[1:], strip_coreduce=True)
+        t_pair = t[EMB_PAIR[0]] + t[EMB_PAIR[1]]
+        ach = nbytes / t_pair / 1e9
+        t_emb = t[EMB_PAIR[0]] + t_strip[EMB_PAIR[1]]
+        traffic, tsrc = pmc_traffic([EMB_PAIR[0], "mrec_emb_bwd_apply"], args)
+        out["roofline"] = {
+            "bound": "hbm", "kernel": "embedding path: " + " + ".join(EMB_PAIR),
+            "achieved": round(ach, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+            "frac": round(ach / HBM_PEAK_GBS, 4), "traffic": traffic,
+            "avg_us": round(t_pair * 1e6, 3), "bytes_per_launch": nbytes,
+            "bytes_rule": "SURVEY.md §8(d) algorithmic bytes per sample x batch",
+            "timing": "in-step: HIP event-record nodes around each launch inside the "
+                      "graph-replayed train steps (median over 4 steps x 30 replays)",
+            "apply_coreduce_us": round((t[EMB_PAIR[1]] - t_strip[EMB_PAIR[1]]) * 1e6, 3),
+            "frac_embedding_only": round(nbytes / t_emb / 1e9 / HBM_PEAK_GBS, 4),
+            "traffic_source": tsrc}
+        for k in EMB_PAIR:
+            rk[k] = {"avg_us": round(t[k] * 1e6, 3), "timing": "in-step"}
+        rk[EMB_PAIR[1]]["avg_us_without_coreduce"] = round(t_strip[EMB_PAIR[1]] * 1e6, 3)
+        if args.model == "deepfm":
+            lins = [m for m in model.mlp.modules() if isinstance(m, torch.nn.Linear)]
+            widths = [lins[0].in_features] + [m.out_features for m in lins]
+            L = len(widths) - 1
+            mm = sum(widths[l] * widths[l + 1] for l in range(L))
+            for name, fl in ((TOWER_PAIR[0], 2 * 2 * args.batch * mm),
+                             (TOWER_PAIR[1], 2 * args.batch * sum(widths[l + 1] * (widths[l] + 1)
+                                                                  for l in range(L)))):
+                if name in t:
+                    d = {"avg_us": round(t[name] * 1e6, 3), "flop": fl,
+                         "TFLOP/s": round(fl / t[name] / 1e12, 1),
+                         "frac_of_mfma_peak": round(fl / t[name] / 1e12 / MFMA_PEAK_TFLOPS, 4),
+                         "timing": "in-step"}
+                    if name == TOWER_PAIR[0]:
+                        wimg = 2 * 2 * mm  # bf16 forward + transposed images
+                        d["weight_bytes_per_workgroup"] = wimg
+                        d["per_CU_L2_GB/s"] = round(wimg / t[name] / 1e9, 1)
+                        d["bound"] = ("per-CU L2 read rate (~70 GB/s per CU, MI355X_MICROARCH.md "
+                                      "indexed-rows table)")
+                    rk[name] = d
+    if args.standalone_roofline or not in_step:
+        ks = kernel_rooflines(model, datas[0], args)
+        ts = sum(v[0] for v in ks.values())
+        impl = sum(v[2] for v in ks.values())
+        if "roofline" not in out:
+            ach = nbytes / ts / 1e9
+            traffic, tsrc = pmc_traffic(list(ks), args)
+            out["roofline"] = {"bound": "hbm", "kernel": "embedding path: " + " + ".join(ks),
+                               "achieved": round(ach, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                               "frac": round(ach / HBM_PEAK_GBS, 4), "traffic": traffic,
+                               "avg_us": round(ts * 1e6, 3), "bytes_per_launch": nbytes,
+                               "bytes_rule": "SURVEY.md §8(d) algorithmic bytes per sample x batch",
+                               "timing": "standalone: each kernel launched alone back to back",
+                               "traffic_source": tsrc}
+        out["roofline"]["frac_standalone"] = round(nbytes / ts / 1e9 / HBM_PEAK_GBS, 4)
+        out["roofline"]["as_implemented_bytes_per_launch"] = impl
+        for k, v in ks.items():
+            rk.setdefault(k, {})["standalone_avg_us"] = round(v[0] * 1e6, 3)
+            rk[k]["as_implemented_bytes"] = v[2]
+    att = attainable()
+    if att:
+        out["roofline"]["attainable"] = att
+        out["roofline"]["frac_of_attainable"] = round(out["roofline"]["achieved"] / att["GB/s"], 4)
+    out["roofline_kernels"] = rk
     return out
 
 
@@ -896,40 +1156,8 @@ def main():
                    "steps_per_graph": G if graphs is not None else 0},
     }
     if rank == 0 and not args.no_roofline and args.model in ("deepfm", "dcnv2"):
-        ks = kernel_rooflines(model, datas[0], args)
-        # achieved = sum of the algorithmic bytes of the HBM-bound
-        # embedding-path kernels / sum of their measured launch durations
-        t = sum(v[0] for v in ks.values())
-        nbytes = sum(v[1] for v in ks.values())
-        impl = sum(v[2] for v in ks.values())
-        ach = nbytes / t / 1e9
-        traffic, tsrc = pmc_traffic(list(ks), args)
-        result["roofline"] = {"bound": "hbm",
-                              "kernel": "embedding path: " + " + ".join(ks),
-                              "achieved": round(ach, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                              "frac": round(ach / HBM_PEAK_GBS, 4),
-                              "traffic": traffic,
-                              "avg_us": round(t * 1e6, 3), "bytes_per_launch": nbytes,
-                              "bytes_rule": "SURVEY.md §8(d) algorithmic bytes per sample x batch",
-                              "as_implemented_bytes_per_launch": impl,
-                              "as_implemented_GB/s": round(impl / t / 1e9, 1),
-                              "traffic_source": tsrc}
-        att = attainable()
-        if att:
-            result["roofline"]["attainable"] = att
-            result["roofline"]["frac_of_attainable"] = round(ach / att["GB/s"], 4)
-        result["roofline_kernels"] = {k: {"avg_us": round(v[0] * 1e6, 3), "bytes": v[1],
-                                          "GB/s": round(v[1] / v[0] / 1e9, 1),
-                                          "as_implemented_bytes": v[2]}
-                                      for k, v in ks.items()}
-    if rank == 0 and not args.no_roofline and args.model == "deepfm":
-        try:
-            lins = [m for m in model.mlp.modules() if isinstance(m, torch.nn.Linear)]
-            widths = [lins[0].in_features] + [m.out_features for m in lins]
-            result.setdefault("roofline_kernels", {}).update(
-                tower_rooflines(model, step, datas, widths, args.batch))
-        except Exception as e:  # a measurement aid: never fail the bench line
-            print(f"bench: tower timing skipped ({type(e).__name__}: {e})", file=sys.stderr)
+        result.update(embedding_roofline(model, step, datas, args,
+                                         in_step=graphs is not None and not sharded))
     if rank == 0 and not args.no_roofline and args.model == "din":
         ks = din_rooflines(model, datas[0], args)
         name = max(ks, key=lambda k: ks[k][0])  # the dominant kernel

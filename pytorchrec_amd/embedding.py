@@ -83,8 +83,10 @@ class EmbeddingBank(torch.nn.Module):
             acc += n
         self.row_offset = offs
         self.total_rows = acc
+        # zeros: the pad columns past [v | w] stay zero (never read by a kernel, but
+        # they travel into state_dict / checkpoints, so no uninitialised bits)
         self.weight = torch.nn.Parameter(
-            torch.empty(acc, self.row_stride, dtype=dtype, device=device),
+            torch.zeros(acc, self.row_stride, dtype=dtype, device=device),
             requires_grad=(update == "dense"))
         self.update = update
         self.sgd_lr: Optional[float] = None
@@ -210,6 +212,14 @@ class EmbeddingBank(torch.nn.Module):
     def next_seed(self) -> int:
         self._seed = (self._seed * 6364136223846793005 + 1442695040888963407) & (2 ** 64 - 1)
         return self._seed
+
+    @torch.no_grad()
+    def zero_pad_(self):
+        """Zero the row-pitch pad columns (after an init that wrote whole rows)."""
+        used = self.dim + (1 if self.has_w else 0)
+        if used < self.row_stride:
+            self.weight[:, used:].zero_()
+        return self
 
     def check_flags(self):
         """Raise if a large-batch backward since the last check could not finish its
@@ -692,7 +702,7 @@ def init_bank_(bank: EmbeddingBank, std: float = 0.01, generator=None, chunk_row
         w = bank.weight
         for s in range(0, w.shape[0], chunk_rows):
             w[s:s + chunk_rows].normal_(0.0, std, generator=generator)
-    return bank
+    return bank.zero_pad_()
 
 
 def rows_to_bytes(bank: EmbeddingBank) -> int:

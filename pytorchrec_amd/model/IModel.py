@@ -70,6 +70,8 @@ class IModel(Module, IWithArguments, ABC):
         elif "Embedding" in str(type(m)):
             with torch.no_grad():
                 torch.nn.init.normal_(m.weight, mean=0.0, std=0.01)
+                if hasattr(m, "zero_pad_"):  # an EmbeddingBank's row-pitch pad columns
+                    m.zero_pad_()
 
     def _reset_weights(self):
         self.apply(self._reset_weights_fn)

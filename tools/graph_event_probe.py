@@ -1,13 +1,18 @@
-"""Can a kernel INSIDE a replayed HIP graph be timed with events?  torch's
-``Event(external=True)`` records become event-record nodes of the captured graph
-(cudaEventRecordExternal semantics).  Captures [a | b | c] with external timing
-events around b, replays it, and prints the per-replay event interval next to b's
-duration when b runs alone -- run under rocprofv3 --kernel-trace --stats to compare
-with the profiler's in-graph duration of b.  (the roofline must
-be the in-step figure.)"""
+"""Can a kernel INSIDE a replayed HIP graph be timed with events?  bench.py's
+GraphKernelTimer splices event-record nodes around chosen kernel nodes of a
+captured graph (torch refuses Event(external=True) on ROCm).  Captures [a | b | c],
+times b inside the replayed graph, and prints it next to b's duration when b runs
+alone -- run under rocprofv3 --kernel-trace --stats to compare with the profiler's
+in-graph duration of b.  (the roofline must be the in-step
+figure.)"""
 import json
+import os
+import sys
 
 import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+from bench import GraphKernelTimer  # noqa: E402
 
 
 def main():
@@ -16,16 +21,15 @@ def main():
     y = torch.randn(4096, 4096, device=dev, dtype=torch.bfloat16)
     z = torch.empty(4096, 4096, device=dev, dtype=torch.bfloat16)
     big = torch.empty(64 << 20, device=dev, dtype=torch.float32)
-    e0 = torch.cuda.Event(enable_timing=True, external=True)
-    e1 = torch.cuda.Event(enable_timing=True, external=True)
+    timer = GraphKernelTimer()
 
     def body(timed):
         big.fill_(1.0)                      # a
         if timed:
-            e0.record()
+            timer.begin()
         torch.mm(x, y, out=z)               # b (the timed kernel)
         if timed:
-            e1.record()
+            timer.end("mm")
         big.mul_(0.5)                       # c
 
     s = torch.cuda.Stream()
@@ -33,14 +37,16 @@ def main():
     with torch.cuda.stream(s):
         body(False)
     torch.cuda.current_stream().wait_stream(s)
-    g = torch.cuda.CUDAGraph()
+    g = torch.cuda.CUDAGraph(keep_graph=True)
     with torch.cuda.graph(g):
         body(True)
+    timer.arm(g.raw_cuda_graph())
+    g.instantiate()
     ins = []
     for _ in range(30):
         g.replay()
         torch.cuda.synchronize()
-        ins.append(e0.elapsed_time(e1) * 1e3)
+        ins.append(timer.elapsed(0) * 1e6)
     a0 = torch.cuda.Event(enable_timing=True)
     a1 = torch.cuda.Event(enable_timing=True)
     alone = []

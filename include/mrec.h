@@ -787,20 +787,7 @@ typedef struct {
    * backward as for BCE (dh_out, dx0, head partials, images). */
   int32_t mode;
   const float *dz_in;        /* [batch] for MREC_TOWER_GIVEN_DZ */
-  /* ABI 18: workspace of the cluster kernel (mrec_tower_cluster_ws_bytes(batch)
-   * bytes, 256-B aligned, ZEROED before its first use, left as found).  With it, and
-   * when 4 workgroups per 64 rows fit the device's CUs at once (batch <= 4096 on
-   * MI355X), every 64-row block is computed by 4 workgroups that each own a quarter
-   * of every layer's output columns and swap their slices through the workspace
-   * (pytorchrec_amd/csrc/tower_cl.hip): a quarter of the weight traffic per
-   * workgroup.  NULL: one workgroup per 16 rows.  Word 0 of the workspace becomes
-   * non-zero if a workgroup ever waited ~seconds for its cluster (results invalid). */
-  void *cl_ws;
-  int64_t cl_ws_bytes;
 } mrec_tower_args;
-
-/* bytes of mrec_tower_args.cl_ws for a batch */
-int64_t mrec_tower_cluster_ws_bytes(int64_t batch);
 
 enum { MREC_TOWER_BCE = 0, MREC_TOWER_FORWARD = 1, MREC_TOWER_GIVEN_DZ = 2 };
 

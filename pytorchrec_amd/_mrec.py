@@ -162,8 +162,7 @@ class TowerArgs(ctypes.Structure):
                 ("part", ctypes.c_void_p), ("ldp", ctypes.c_int64),
                 ("loss_part", ctypes.c_void_p), ("ticket", ctypes.c_void_p),
                 ("loss", ctypes.c_void_p), ("kfrag", ctypes.c_int32), ("x0_img", ctypes.c_void_p),
-                ("mode", ctypes.c_int32), ("dz_in", ctypes.c_void_p),
-                ("cl_ws", ctypes.c_void_p), ("cl_ws_bytes", ctypes.c_int64)]
+                ("mode", ctypes.c_int32), ("dz_in", ctypes.c_void_p)]
 
 
 class TowerDwArgs(ctypes.Structure):
@@ -323,7 +322,6 @@ SIGNATURES = {
     "mrec_shard_wire_pack": (ctypes.c_int, [_vp, _i64, _i32, _vp, _i32, _i32, _i32, _i32, _vp, _vp,
                                             _vp]),
     "mrec_tower_fwd_bwd": (ctypes.c_int, [ctypes.POINTER(TowerArgs), _vp]),
-    "mrec_tower_cluster_ws_bytes": (_i64, [_i64]),
     "mrec_tower_image_elems": (ctypes.c_int64, [_i64, _i64, _i32]),
     "mrec_tower_weight_prep": (ctypes.c_int, [_vp, _i64, _i64, _i64, _vp, _vp, _vp]),
 }

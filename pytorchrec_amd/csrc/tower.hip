@@ -606,8 +606,6 @@ static unsigned long long *g_tower_stamps = nullptr;  // mrec_tower_debug_stamps
 
 unsigned long long *tower_debug_stamps() { return g_tower_stamps; }
 
-// tower_cl.hip: the cluster kernel (false: not applicable, run the 16-row kernel)
-bool tower_cluster_launch(const mrec_tower_args &s, hipStream_t st, mrec_status *status);
 
 static bool al16(const void *p, int64_t ld) {
   return p && (reinterpret_cast<uintptr_t>(p) & 15) == 0 && ld % 8 == 0;
@@ -803,10 +801,6 @@ mrec_status mrec_tower_fwd_bwd(const mrec_tower_args *p, mrec_stream stream) {
     return (v == 6 || v == 8) ? v : 4;
   }();
   hipStream_t st = static_cast<hipStream_t>(stream);
-  {
-    mrec_status cs = MREC_OK;  // 64-row clusters of 4 workgroups when they fit (tower_cl.hip)
-    if (tower_cluster_launch(s, st, &cs)) return cs;
-  }
   const int64_t grid = (s.batch + TW_ROWS - 1) / TW_ROWS;
   const dim3 gd(static_cast<unsigned>(grid));
   if (pf_env == 8)

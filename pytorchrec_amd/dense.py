@@ -1031,41 +1031,6 @@ def _ticket(dev) -> torch.Tensor:
     return t
 
 
-_CLUSTER_WS = {}
-TOWER_CLUSTER = os.environ.get("MREC_TOWER_CLUSTER", "0") != "0"
-
-
-def tower_cluster_ws(dev, B: int):
-    """Workspace of the cluster tower kernel (tower_cl.hip: exchange buffers and one
-    counter per 64-row cluster), zeroed once and left zero by every launch; one per
-    (device, batch), kept alive for captured graphs.  None disables the cluster
-    kernel (MREC_TOWER_CLUSTER=0)."""
-    if not TOWER_CLUSTER:
-        return None
-    key = (dev, int(B))
-    t = _CLUSTER_WS.get(key)
-    if t is None:
-        n = int(_mrec.lib().mrec_tower_cluster_ws_bytes(int(B)))
-        t = torch.zeros(n + 256, dtype=torch.uint8, device=dev)
-        off = (-t.data_ptr()) % 256  # 256-B aligned start
-        t = t[off:off + n]
-        _CLUSTER_WS[key] = t
-    return t
-
-
-def tower_cluster_error(dev) -> bool:
-    """True if a cluster tower launch on ``dev`` ever gave up waiting for its peers
-    (workspace word 0; the results of that launch are invalid)."""
-    return any(int(t[:4].view(torch.int32).item()) != 0
-               for (d, _), t in _CLUSTER_WS.items() if d == dev)
-
-
-def _set_cluster_ws(a, dev, B: int):
-    ws = tower_cluster_ws(dev, B)
-    if ws is not None:
-        a.cl_ws, a.cl_ws_bytes = ws.data_ptr(), ws.numel()
-
-
 def grad_one(dev) -> torch.Tensor:
     """Persistent scalar 1.0 used as the loss gradient (no fill kernel per step, and
     lets the fused head skip scaling its stashed gradients)."""
@@ -1320,7 +1285,6 @@ class _TowerBCEFn(torch.autograd.Function):
         a.z, a.dz = None, dz.data_ptr()
         a.part, a.ldp = part.data_ptr(), ldp
         a.loss_part, a.ticket, a.loss = loss_part.data_ptr(), _ticket(dev).data_ptr(), loss.data_ptr()
-        _set_cluster_ws(a, dev, B)
         with _timed("mrec_tower_fwd_bwd"):
             _mrec.call("mrec_tower_fwd_bwd", ctypes.byref(a), _mrec.stream_handle())
         ctx.save_for_backward(x0 if x0_img is None else x0_img, dz, part, dx0, *hs, *dhs)
@@ -1499,7 +1463,6 @@ class _ScoreTowerFn(torch.autograd.Function):
             a.w_fwd[l], a.w_bwd[l] = imgs[l][0].data_ptr(), imgs[l][1].data_ptr()
             a.bias[l] = _mrec.ptr(bsd[l])
         a.head_w, a.head_b = hw.data_ptr(), _mrec.ptr(hb)
-        _set_cluster_ws(a, x0.device, x0.shape[0])
         return a
 
     @staticmethod

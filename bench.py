@@ -172,7 +172,8 @@ def build_deepfm(args, device, comm=None):
     label = CategoricalColumnWithIdentity(2, "label")
     cap = args.shard_cap
     if cap is None and args.zipf > 0 and comm is not None:
-        cap = min(args.batch, 8192 // comm.world)  # skewed ids: no tight capacity
+        cap = args.batch  # skewed ids: no tight capacity (a large W * cap takes the
+        # owner's large-batch path, sharding.owner_apply_large)
     ctx = (sharded_tables(comm, cap=cap, max_batch=args.batch) if comm is not None
            else contextlib.nullcontext())
     with ctx:

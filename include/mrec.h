@@ -317,13 +317,38 @@ mrec_status mrec_emb_bwd_large_fused(const mrec_table_bank *bank, const mrec_ids
                                      const uint64_t *d_step, void *grad, mrec_stream stream);
 
 /*
+ * Per-lookup gradients GIVEN by the caller instead of computed from dx / dfm (the
+ * owner side of the row-sharded exchange).  The lookups are an
+ * exchange view (mrec_ids with chunk = the entries per part): entry b of table f
+ * sits in part p = b / chunk at j = b % chunk.  Exactly one source:
+ *   g_occ: fp32 rows [.., g_ld], entry (p, f, j) at row p * chunk_stride + f * chunk
+ *          + j (the slot exchange's received gradient slots);
+ *   wire:  records of rec_bytes (wire_dtype BF16 / F32), entry (p, f, j) at record
+ *          p * cap_rows + pref[p * n_tables + f] + j (the compact exchange; an entry
+ *          past its part's cap_rows records gets a zero gradient).
+ */
+typedef struct {
+  const float *g_occ;
+  int64_t g_ld;
+  int64_t chunk;
+  int64_t chunk_stride;
+  const void *wire;
+  int32_t rec_bytes;
+  mrec_dtype wire_dtype;
+  const int32_t *pref;
+  int32_t cap_rows;
+} mrec_given_grads;
+
+/*
  * Byte offset, inside the large-batch workspace, of an int32 STICKY error word
  * (ABI 25).  The fused path's huge segments (a row hit > 2048 times) are summed in
  * one launch of three dependent phases whose work items are dequeued in phase
  * order (no co-residency assumed, so a phase wait always ends); its waits are still
  * bounded, and a wait that ran out (a hardware stall; or MREC_LG_HUGE_TEST_STALL,
  * a test-only knob that makes them unreachable) leaves the rows of that launch's
- * huge segments un-updated and sets this word to non-zero.  No kernel clears it:
+ * huge segments un-updated and sets this word to 1; a bank of more than 2^24 rows
+ * (only the bucketed plan) whose bucket holds more distinct rows than its LDS hash
+ * sets 2 (those rows un-updated).  No kernel clears it:
  * the caller reads it at a sync point of its choosing, raises, and zeroes it.
  */
 size_t mrec_emb_bwd_large_error_offset(void);
@@ -346,6 +371,21 @@ mrec_status mrec_emb_bwd_large_fused_ex(const mrec_table_bank *bank, const mrec_
                                         uint64_t seed, const uint64_t *d_step, void *grad,
                                         int32_t n_reduce, const struct mrec_gemm_call_s *reduce,
                                         mrec_stream stream);
+
+/*
+ * mrec_emb_bwd_large_fused_ex over GIVEN per-lookup gradients (ABI 25; the owner
+ * side of the row-sharded exchange when an exchange view exceeds the hash plan's
+ * MREC_BWD_MAX_BATCH entries per table: large W * cap, Zipf).  `ids` is the exchange
+ * view of the received ids (pad_negative: padding slots skipped), `batch` its
+ * entries per table.  Same sums and update arithmetic as every large-batch path.
+ */
+mrec_status mrec_emb_bwd_large_fused_given(const mrec_table_bank *bank, const mrec_ids *ids,
+                                           int64_t batch, void *workspace, size_t ws_bytes,
+                                           int32_t *d_oob_flag, const mrec_given_grads *given,
+                                           mrec_bwd_mode mode, float lr, uint64_t seed,
+                                           const uint64_t *d_step, void *grad, int32_t n_reduce,
+                                           const struct mrec_gemm_call_s *reduce,
+                                           mrec_stream stream);
 
 /*
  * mrec_emb_bwd_apply plus up to 2 deferred split-K weight-gradient reductions

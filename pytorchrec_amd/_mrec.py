@@ -125,6 +125,14 @@ class PlanJob(ctypes.Structure):
                 ("d_step", ctypes.c_void_p)]
 
 
+class GivenGrads(ctypes.Structure):
+    """mrec_given_grads (include/mrec.h)."""
+    _fields_ = [("g_occ", ctypes.c_void_p), ("g_ld", ctypes.c_int64), ("chunk", ctypes.c_int64),
+                ("chunk_stride", ctypes.c_int64), ("wire", ctypes.c_void_p),
+                ("rec_bytes", ctypes.c_int32), ("wire_dtype", ctypes.c_int),
+                ("pref", ctypes.c_void_p), ("cap_rows", ctypes.c_int32)]
+
+
 class HeadFinishJob(ctypes.Structure):
     _fields_ = [("part", ctypes.c_void_p), ("ldp", ctypes.c_int64), ("batch", ctypes.c_int64),
                 ("H", ctypes.c_int32), ("ns", ctypes.c_int32), ("g", ctypes.c_void_p),
@@ -269,6 +277,10 @@ SIGNATURES = {
                                                 _vp, ctypes.c_int, _i64, _vp, _vp, _vp,
                                                 ctypes.c_int, _i64, _vp, ctypes.c_int, _f32,
                                                 ctypes.c_uint64, _vp, _vp, _vp]),
+    "mrec_emb_bwd_large_fused_given": (ctypes.c_int, [_bank_p, _ids_p, _i64, _vp, ctypes.c_size_t,
+                                                      _vp, ctypes.POINTER(GivenGrads), ctypes.c_int,
+                                                      _f32, ctypes.c_uint64, _vp, _vp, _i32,
+                                                      ctypes.POINTER(GemmCall), _vp]),
     "mrec_emb_bwd_large_fused_ex": (ctypes.c_int, [_bank_p, _ids_p, _i64, _vp, ctypes.c_size_t,
                                                    _vp, _vp, ctypes.c_int, _i64, _vp, _vp, _vp,
                                                    ctypes.c_int, _i64, _vp, ctypes.c_int, _f32,

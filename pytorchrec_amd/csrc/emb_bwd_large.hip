@@ -36,6 +36,10 @@ constexpr int kLgChunk = 2048;         // lookups per long-segment work item
 constexpr int kLgShort = 16;           // segments up to this: register sort
 constexpr int kLgHuge = kLgChunk;      // longer: chunked fixed-point kernels (else one wave)
 constexpr int64_t kLgMaxRows = int64_t(1) << 24;
+// the workspace header's sticky error word (never cleared by a kernel; the host reads
+// and clears it, mrec_emb_bwd_large_error_offset): 1 a huge-segment phase wait ran
+// out, 2 a bucket's distinct rows overflowed its LDS hash
+constexpr int kLgErrWord = 8;
 constexpr int kLgApplyBlocks = 2048;   // grid-stride launches (device-side counts)
 
 // workspace layout (all offsets 256-B aligned)
@@ -86,9 +90,14 @@ __host__ __device__ inline int bk_buckets(int64_t N) {
 }
 // chunks of the bucketed plan, 0 = the atomic plan.  The row hash spreads the R
 // consecutive global rows evenly over the buckets (Fibonacci hashing), so with R
-// <= NB * kBkSlots / 2 no bucket's LDS hash can fill up.
+// <= NB * kBkSlots / 2 no bucket's LDS hash can fill up.  Banks past kLgMaxRows rows
+// (the row-sharded owner's shard of 100M-row tables) have no atomic plan (its
+// per-row arrays would be GBs) and always take the bucketed one: a bucket holds at
+// most its lookups' distinct rows (~N / NB = 128-256 on average), and a bucket whose
+// distinct rows do not fit its LDS hash sets the sticky error word, never silently.
 __host__ __device__ inline int bk_groups(int64_t R, int64_t N) {
-  if (N <= 0 || N > kBkMaxN || R > int64_t(bk_buckets(N)) * (kBkSlots / 2)) return 0;
+  if (N <= 0 || N > kBkMaxN) return 0;
+  if (R <= kLgMaxRows && R > int64_t(bk_buckets(N)) * (kBkSlots / 2)) return 0;
   return static_cast<int>((N + kBkChunk - 1) / kBkChunk);
 }
 
@@ -127,7 +136,8 @@ __host__ __device__ inline int64_t lg_ws_bytes(int64_t R, int64_t N, int stride,
   };
   const int G = bk_groups(R, N), NB = bk_buckets(N);
   const int64_t o_hdr = take(64), o_bcnt = take(G ? 8 * NB : 0), o_segmax = take(4 * UL), o_acc = take(8 * UL * stride);
-  const int64_t o_cnt = take(4 * R), o_start = take(4 * R), o_blk = take(8 * nblk);
+  const int64_t Ra = R <= kLgMaxRows ? R : 0;  // the atomic plan's per-row arrays
+  const int64_t o_cnt = take(4 * Ra), o_start = take(4 * Ra), o_blk = take(8 * (Ra ? nblk : 0));
   const int64_t o_uniq = take(4 * U), o_ustart = take(4 * U), o_ulen = take(4 * U);
   const int64_t o_ulong = take(4 * U), o_perm = take(4 * N), o_longs = take(4 * UL);
   const int64_t o_chunks = take(8 * C);
@@ -965,7 +975,6 @@ __global__ __launch_bounds__(256) void lg_apply_kernel(BankArgs bank, int64_t n,
 // the sticky error word hdr[kLgErrWord] (never cleared by a kernel; the host reads and
 // clears it: mrec_emb_bwd_large_error_offset) and leaves WITHOUT touching any row --
 // an update is never applied from partial sums.
-constexpr int kLgErrWord = 8;
 
 __device__ __forceinline__ bool lg_wait_done(int32_t *ctr, int target, int bound) {
   for (int spins = 0; __hip_atomic_load(ctr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < target;) {
@@ -1079,7 +1088,10 @@ __global__ __launch_bounds__(256) void bk_apply_kernel(BankArgs bank, LgWs w, Ap
     const Run x = lane_run(r);
     if (x.r >= 0 && x.head == lane) {
       const int s = find(x.r, true);
-      if (s >= 0) atomicAdd(&cur[s], x.len);
+      if (s >= 0)
+        atomicAdd(&cur[s], x.len);
+      else  // more distinct rows than the LDS hash (a bank past kLgMaxRows rows only)
+        __hip_atomic_store(w.hdr + kLgErrWord, 2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
   }
   __syncthreads();
@@ -1257,7 +1269,9 @@ static mrec_status lg_setup(const mrec_table_bank *bank, int64_t batch, void *ws
   MREC_CHECK_ARG(ws != nullptr, "workspace is NULL");
   *R = 0;
   for (int f = 0; f < ba->n_tables; ++f) *R += ba->rows[f];
-  MREC_CHECK_ARG(*R <= kLgMaxRows, "total rows must be <= 2^24 for the large-batch path");
+  MREC_CHECK_ARG(*R < (int64_t(1) << 31), "total rows must be < 2^31");
+  MREC_CHECK_ARG(*R <= kLgMaxRows || bk_groups(*R, batch * ba->n_tables) > 0,
+                 "banks of more than 2^24 rows need the bucketed plan: batch * n_tables <= 2M");
   const int64_t need = lg_ws_bytes(*R, batch * ba->n_tables, ba->row_stride, w,
                                    static_cast<char *>(ws));
   if (ws_bytes < static_cast<size_t>(need)) {
@@ -1448,6 +1462,49 @@ mrec_status mrec_emb_bwd_large_apply(const mrec_table_bank *bank, int64_t batch,
   return launch_status("mrec_emb_bwd_large_apply");
 }
 
+}  // extern "C"
+
+// fused plan + apply with the apply arguments already built (own gradients, or
+// given ones: the owner side of a row-sharded exchange)
+static mrec_status lg_fused_impl(const mrec_table_bank *bank, const mrec_ids *ids, int64_t batch,
+                                 void *workspace, size_t ws_bytes, int32_t *d_oob_flag,
+                                 const ApplyArgs &a, int32_t n_reduce,
+                                 const mrec_gemm_call *reduce, mrec_stream stream) {
+  BankArgs ba;
+  IdsArgs ia;
+  int lpr;
+  int64_t R;
+  LgWs w;
+  mrec_status st = lg_setup(bank, batch, workspace, ws_bytes, &ba, &lpr, &R, &w);
+  if (st != MREC_OK) return st;
+  if ((st = make_ids_args(ids, ba.n_tables, &ia)) != MREC_OK) return st;
+  CoReduce co;
+  int co_blocks = 0;
+  if ((st = build_co_reduce(n_reduce, reduce, &co, &co_blocks)) != MREC_OK) return st;
+  const int64_t total = batch * ba.n_tables;
+  const int G = batch == 0 ? 0 : bk_groups(R, total);
+  hipStream_t s = static_cast<hipStream_t>(stream);
+  if (G == 0 || std::getenv("MREC_LG_ATOMIC_PLAN")) {  // the two-call path
+    if (batch > 0) {
+      st = mrec_emb_bwd_large_plan(bank, ids, batch, workspace, ws_bytes, d_oob_flag, stream);
+      if (st != MREC_OK) return st;
+      lg_dispatch_apply(bank->dtype, lpr, ba, batch, w, a, ba.row_stride, 0, 0, 0, s);
+      if ((st = launch_status("mrec_emb_bwd_large_apply")) != MREC_OK) return st;
+    }
+    return co.n ? mrec_gemm_multi(n_reduce, reduce, stream) : MREC_OK;
+  }
+  const int NB = bk_buckets(total);
+  int lognb = 0;
+  while ((1 << lognb) < NB) ++lognb;
+  bk_hist_kernel<<<dim3(G), kBkThreads, 0, s>>>(ba, ia, batch, lognb, w, d_oob_flag);
+  bk_scatter_kernel<<<dim3(G), kBkThreads, 0, s>>>(ba, ia, batch, G, lognb, w, 1);
+  lg_dispatch_apply(bank->dtype, lpr, ba, batch, w, a, ba.row_stride, NB, G, lognb, s, co,
+                    co_blocks);
+  return launch_status("mrec_emb_bwd_large_fused");
+}
+
+extern "C" {
+
 mrec_status mrec_emb_bwd_large_fused_ex(const mrec_table_bank *bank, const mrec_ids *ids,
                                         int64_t batch, void *workspace, size_t ws_bytes,
                                         int32_t *d_oob_flag, const void *dx, mrec_dtype dx_dtype,
@@ -1457,43 +1514,64 @@ mrec_status mrec_emb_bwd_large_fused_ex(const mrec_table_bank *bank, const mrec_
                                         uint64_t seed, const uint64_t *d_step, void *grad,
                                         int32_t n_reduce, const mrec_gemm_call *reduce,
                                         mrec_stream stream) {
+  MREC_CHECK_ARG(bank != nullptr, "NULL bank");
   BankArgs ba;
-  IdsArgs ia;
-  int lpr;
-  int64_t R;
-  LgWs w;
-  mrec_status st = lg_setup(bank, batch, workspace, ws_bytes, &ba, &lpr, &R, &w);
+  int es = 0, lpr = 0;
+  mrec_status st = make_bank_args(bank, &ba, &es, &lpr);
   if (st != MREC_OK) return st;
-  if ((st = make_ids_args(ids, ba.n_tables, &ia)) != MREC_OK) return st;
   ApplyArgs a;
   st = lg_apply_args(bank, ba, dx, dx_dtype, dx_ld, dfm, fm_sum, x0, x0_dtype, x0_ld, dw, mode,
                      lr, seed, d_step, grad, &a);
   if (st != MREC_OK) return st;
-  CoReduce co;
-  int co_blocks = 0;
-  if ((st = build_co_reduce(n_reduce, reduce, &co, &co_blocks)) != MREC_OK) return st;
-  const int64_t total = batch * ba.n_tables;
-  const int G = batch == 0 ? 0 : bk_groups(R, total);
-  if (G == 0 || std::getenv("MREC_LG_ATOMIC_PLAN")) {  // the two-call path
-    if (batch > 0) {
-      st = mrec_emb_bwd_large_plan(bank, ids, batch, workspace, ws_bytes, d_oob_flag, stream);
-      if (st != MREC_OK) return st;
-      st = mrec_emb_bwd_large_apply(bank, batch, workspace, ws_bytes, dx, dx_dtype, dx_ld, dfm,
-                                    fm_sum, x0, x0_dtype, x0_ld, dw, mode, lr, seed, d_step, grad,
-                                    stream);
-      if (st != MREC_OK) return st;
-    }
-    return co.n ? mrec_gemm_multi(n_reduce, reduce, stream) : MREC_OK;
+  return lg_fused_impl(bank, ids, batch, workspace, ws_bytes, d_oob_flag, a, n_reduce, reduce,
+                       stream);
+}
+
+mrec_status mrec_emb_bwd_large_fused_given(const mrec_table_bank *bank, const mrec_ids *ids,
+                                           int64_t batch, void *workspace, size_t ws_bytes,
+                                           int32_t *d_oob_flag, const mrec_given_grads *given,
+                                           mrec_bwd_mode mode, float lr, uint64_t seed,
+                                           const uint64_t *d_step, void *grad, int32_t n_reduce,
+                                           const mrec_gemm_call *reduce, mrec_stream stream) {
+  MREC_CHECK_ARG(bank != nullptr && given != nullptr, "NULL bank / given");
+  const mrec_given_grads &g = *given;
+  MREC_CHECK_ARG((g.g_occ != nullptr) != (g.wire != nullptr), "exactly one of g_occ / wire");
+  MREC_CHECK_ARG(g.chunk >= 1, "chunk (entries per exchange part) must be >= 1");
+  BankArgs ba;
+  int es = 0, lpr = 0;
+  mrec_status st = make_bank_args(bank, &ba, &es, &lpr);
+  if (st != MREC_OK) return st;
+  ApplyArgs a;
+  st = lg_apply_args(bank, ba, nullptr, MREC_F32, 0, nullptr, nullptr, nullptr, MREC_F32, 0,
+                     nullptr, mode, lr, seed, d_step, grad, &a);
+  if (st != MREC_OK) return st;
+  a.chunk = g.chunk;
+  if (g.g_occ) {
+    MREC_CHECK_ARG(g.g_ld >= ba.dim + (ba.has_w ? 1 : 0) && g.g_ld % 4 == 0 &&
+                       (reinterpret_cast<uintptr_t>(g.g_occ) & 15) == 0,
+                   "g_occ rows: >= dim (+w) floats, 16-B aligned");
+    MREC_CHECK_ARG(g.chunk_stride >= static_cast<int64_t>(ba.n_tables) * g.chunk,
+                   "chunk_stride < n_tables * chunk");
+    a.g_occ = g.g_occ;
+    a.g_ld = g.g_ld;
+    a.chunk_stride = g.chunk_stride;
+  } else {
+    MREC_CHECK_ARG(g.wire_dtype == MREC_BF16 || g.wire_dtype == MREC_F32,
+                   "wire dtype must be BF16/F32");
+    const int wes = g.wire_dtype == MREC_BF16 ? 2 : 4;
+    MREC_CHECK_ARG(g.rec_bytes > 0 && g.rec_bytes % wes == 0 && g.rec_bytes % 4 == 0 &&
+                       g.rec_bytes >= (ba.dim + (ba.has_w ? 1 : 0)) * wes,
+                   "bad record bytes");
+    MREC_CHECK_ARG(g.pref != nullptr && g.cap_rows >= 1, "NULL pref / cap_rows < 1");
+    a.g_rec = g.wire;
+    a.g_rec_bf16 = g.wire_dtype == MREC_BF16;
+    a.g_rec_pitch = g.rec_bytes / wes;
+    a.g_pref = g.pref;
+    a.g_cap_rows = g.cap_rows;
   }
-  hipStream_t s = static_cast<hipStream_t>(stream);
-  const int NB = bk_buckets(total);
-  int lognb = 0;
-  while ((1 << lognb) < NB) ++lognb;
-  bk_hist_kernel<<<dim3(G), kBkThreads, 0, s>>>(ba, ia, batch, lognb, w, d_oob_flag);
-  bk_scatter_kernel<<<dim3(G), kBkThreads, 0, s>>>(ba, ia, batch, G, lognb, w, 1);
-  lg_dispatch_apply(bank->dtype, lpr, ba, batch, w, a, ba.row_stride, NB, G, lognb, s, co,
-                    co_blocks);
-  return launch_status("mrec_emb_bwd_large_fused");
+  a.g_F = ba.n_tables;
+  return lg_fused_impl(bank, ids, batch, workspace, ws_bytes, d_oob_flag, a, n_reduce, reduce,
+                       stream);
 }
 
 mrec_status mrec_emb_bwd_large_fused(const mrec_table_bank *bank, const mrec_ids *ids,

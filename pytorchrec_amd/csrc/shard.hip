@@ -339,8 +339,10 @@ __device__ __forceinline__ int wire_table(const int *pre, int F, int r) {
 
 // owner: local bank rows of part p's received ids -> wire records (grid: chunks x W,
 // flattened: blockIdx.x = p * chunks + chunk after `plan_blocks` leading workgroups
-// that run the owner's backward hash plan over the same received ids, PLAN)
-template <bool PLAN>
+// that run the owner's backward hash plan over the same received ids, PLAN).  ADAM:
+// a lazily updated Adam bank's rows go out as of the current step (adam_current on
+// the 16-B chunk holding the dword, as mrec_shard_gather does for the slot rows).
+template <bool PLAN, typename T = uint16_t, bool ADAM = false>
 __global__ __launch_bounds__(kWireThreads) void gather_wire_kernel(BankArgs bank, WireArgs w,
                                                                    const int32_t *__restrict__ recv,
                                                                    uint32_t *__restrict__ wire,
@@ -387,7 +389,23 @@ __global__ __launch_bounds__(kWireThreads) void gather_wire_kernel(BankArgs bank
   }
   uint32_t v[kWirePer];
 #pragma unroll
-  for (int it = 0; it < kWirePer; ++it) v[it] = src[it] >= 0 ? data[src[it]] : 0u;
+  for (int it = 0; it < kWirePer; ++it) {
+    if constexpr (ADAM) {
+      constexpr int EPL = Vec<T>::EPL;
+      v[it] = 0u;
+      if (src[it] >= 0) {
+        const int64_t grow = src[it] / row_dw;
+        const int k = static_cast<int>(src[it] - grow * row_dw), c = k >> 2;
+        uint4 raw = reinterpret_cast<const uint4 *>(bank.data)[grow * bank.lpr + c];
+        raw = adam_current<T>(bank, grow, c * EPL, live_elems(bank, c * EPL, EPL), raw,
+                              *bank.adam.d_t);
+        const uint32_t q[4] = {raw.x, raw.y, raw.z, raw.w};
+        v[it] = q[k & 3];
+      }
+    } else {
+      v[it] = src[it] >= 0 ? data[src[it]] : 0u;
+    }
+  }
   uint32_t *dst = wire + static_cast<int64_t>(p) * w.cap_rows * w.rec_dw;
 #pragma unroll
   for (int it = 0; it < kWirePer; ++it) {
@@ -752,8 +770,6 @@ mrec_status mrec_shard_gather_wire_ex(const mrec_table_bank *local, const int32_
   int eb, lpr;
   mrec_status st = make_bank_args(local, &ba, &eb, &lpr);
   if (st != MREC_OK) return st;
-  MREC_CHECK_ARG(!ba.adam.kind, "the wire gather does not catch up lazy Adam rows: "
-                                "use mrec_shard_gather");
   MREC_CHECK_ARG(recv_ids && wire, "NULL pointer");
   MREC_CHECK_ARG((reinterpret_cast<uintptr_t>(wire) & 3) == 0, "wire not 4-B aligned");
   const int rec = mrec_shard_wire_bytes(ba.dim, ba.has_w, local->dtype);
@@ -772,14 +788,25 @@ mrec_status mrec_shard_gather_wire_ex(const mrec_table_bank *local, const int32_
   }
   const dim3 gf(static_cast<unsigned>(pb + chunks * world));
   hipStream_t s = static_cast<hipStream_t>(stream);
-  if (plan)
-    gather_wire_kernel<true><<<gf, kWireThreads, 0, s>>>(ba, w, recv_ids,
-                                                         static_cast<uint32_t *>(wire), chunks,
-                                                         job, pb);
-  else
-    gather_wire_kernel<false><<<gf, kWireThreads, 0, s>>>(ba, w, recv_ids,
-                                                          static_cast<uint32_t *>(wire), chunks,
-                                                          job, 0);
+  uint32_t *wd = static_cast<uint32_t *>(wire);
+#define MREC_GW(P, T, A) gather_wire_kernel<P, T, A><<<gf, kWireThreads, 0, s>>>(ba, w, recv_ids, wd, chunks, job, pb)
+  if (!ba.adam.kind) {
+    if (plan)
+      MREC_GW(true, uint16_t, false);
+    else
+      MREC_GW(false, uint16_t, false);
+  } else if (local->dtype == MREC_BF16) {  // a lazily updated Adam bank
+    if (plan)
+      MREC_GW(true, uint16_t, true);
+    else
+      MREC_GW(false, uint16_t, true);
+  } else {
+    if (plan)
+      MREC_GW(true, float, true);
+    else
+      MREC_GW(false, float, true);
+  }
+#undef MREC_GW
   return launch_status("mrec_shard_gather_wire");
 }
 

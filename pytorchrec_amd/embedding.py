@@ -235,6 +235,10 @@ class EmbeddingBank(torch.nn.Module):
         err = int(word.item())
         if err:
             word.zero_()
+            if err == 2:
+                raise RuntimeError("embedding backward: a bucket of the large-batch plan held "
+                                   "more distinct rows than its LDS hash (a bank of more than "
+                                   "2^24 rows); some rows of that step were not updated")
             raise RuntimeError("embedding backward: the huge-segment phases of a large-batch "
                                "update timed out waiting for each other (a stalled GPU); the "
                                "rows hit > 2048 times in that step were not updated")

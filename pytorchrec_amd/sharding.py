@@ -24,9 +24,12 @@ compact exchange, include/mrec.h ABI 19):
 
 so the bytes on xGMI per rank and direction are ~cap_rows x 36 B per peer (one
 record per distinct id; bf16, D = 16 + w) instead of n_tables x cap x 64 B rows
-and 80-B fp32 gradients.  Banks under a fused lazy Adam (whose reads must catch
-rows up) keep the slot exchange of ABI 14 (one 64-B row / fp32 gradient per
-lookup).
+and 80-B fp32 gradients.  Banks under a fused lazy Adam take the same path: the
+owner's wire gather catches each row up to the current step as it packs it
+(ABI 25).  ``compact = False`` keeps the slot exchange of ABI 14 (one 64-B row /
+fp32 gradient per lookup).  An owner whose exchange view (W * cap entries per
+table) exceeds one plan workgroup sums the received gradients with the large-batch
+bucketed plan (owner_apply_large).
 
 Every exchange buffer has W equal parts, so all collectives are equal-split: no
 host sync, capturable in a HIP graph.  An overflow (more distinct ids of one table
@@ -178,7 +181,8 @@ def default_cap(batch: int, world: int, rows: Optional[Sequence[int]] = None,
     table) — at W = 8, B = 4096 that is 688 slots for a mean of 512, where a 2x
     share would move 1.5x the bytes over xGMI in each of the three all-to-alls.
     Skewed ids (Zipf) need a larger ``cap`` (an overflow is raised, never dropped).
-    Bounded so the owner's per-table plan stays within MREC_BWD_MAX_BATCH entries."""
+    An owner whose exchange view (W * cap entries per table) exceeds one plan
+    workgroup's MREC_BWD_MAX_BATCH takes the large-batch path (owner_apply_large)."""
     batch, world = int(batch), int(world)
     if world <= 1:
         cap = batch
@@ -187,7 +191,7 @@ def default_cap(batch: int, world: int, rows: Optional[Sequence[int]] = None,
         p = max(shares + [1.0 / world])
         sd = math.sqrt(batch * p * (1.0 - p))
         cap = (int(math.ceil(batch * p + sigmas * sd)) + 7) // 8 * 8
-    return max(1, min(batch, cap, _mrec.BWD_MAX_BATCH // world))
+    return max(1, min(batch, cap))
 
 
 def default_cap_rows(batch: int, world: int, rows: Sequence[int], cap: int,
@@ -235,13 +239,13 @@ class ShardedEmbeddingBank(EmbeddingBank):
         self.world, self.rank = W, r
         self.cap = (int(cap) if cap is not None
                     else default_cap(max_batch, W, self.global_rows))
-        if W * self.cap > _mrec.BWD_MAX_BATCH:
-            raise ValueError(f"world * cap = {W * self.cap} exceeds MREC_BWD_MAX_BATCH")
+        if self.cap < 1:
+            raise ValueError(f"cap = {self.cap} must be >= 1")
         self._flags = None  # device int32 [2] = {overflow, oob}, sticky until checked
         self._global_rows_arr = (ctypes.c_int64 * len(self.global_rows))(*self.global_rows)
         # the compact exchange (one record per distinct id, ABI 19) at world > 1
-        # ("always": at world 1 too); False: one slot row per lookup (ABI 14) -- always
-        # for a fused lazy Adam bank.  At world 1 nothing crosses xGMI and the slot
+        # ("always": at world 1 too); False: one slot row per lookup (ABI 14).  At
+        # world 1 nothing crosses xGMI and the slot
         # path keeps the step bit-identical to the unsharded bank (the compact path
         # rounds each rank's gradient sum of a bf16 row to bf16 on the wire).
         self.compact = True
@@ -263,7 +267,7 @@ class ShardedEmbeddingBank(EmbeddingBank):
         (e.g. W >= 16 at B = 8192 falls back to the slot exchange)."""
         on = self.compact == "always" or (bool(self.compact) and self.world > 1)
         groups = max(1, -(-int(batch) // 1024) * 16)
-        return (on and self.update != "adam" and batch <= _mrec.BWD_MAX_BATCH
+        return (on and batch <= _mrec.BWD_MAX_BATCH
                 and self.cap < 65535 and (self.world + 1) * groups <= 2048)
 
     @property
@@ -635,15 +639,7 @@ def owner_apply_wire(bank: ShardedEmbeddingBank, plan, wire_g: torch.Tensor, pre
     (mrec_emb_bwd_apply_wire: no unpack to fp32 slots; same sums and update)."""
     ws, wsb = plan
     F, W, cap = bank.n_tables, bank.world, bank.cap
-    if grad is not None:
-        mode, lr = _mrec.BWD_DENSE_GRAD, 0.0
-    elif lr is not None:
-        mode = (_mrec.BWD_SGD_SR if (bank.stochastic_rounding and
-                                     bank.weight.dtype == torch.bfloat16) else _mrec.BWD_SGD)
-    else:
-        mode, lr = bank.apply_mode()
-        if mode in (_mrec.BWD_SGD, _mrec.BWD_SGD_SR):
-            lr = lr / W
+    mode, lr = _owner_mode(bank, lr, grad)
     from pytorchrec_amd import dense as dense_ops
     jobs = dense_ops.take_pending(4)
     arr = (_mrec.GemmCall * len(jobs))(*[j.struct() for j in jobs]) if jobs else None
@@ -653,6 +649,67 @@ def owner_apply_wire(bank: ShardedEmbeddingBank, plan, wire_g: torch.Tensor, pre
                bank.step_counter().data_ptr(), _mrec.ptr(grad), len(jobs), arr,
                _mrec.stream_handle())
     del jobs
+
+
+def _owner_mode(bank: ShardedEmbeddingBank, lr, grad):
+    if grad is not None:
+        return _mrec.BWD_DENSE_GRAD, 0.0
+    if lr is not None:
+        return (_mrec.BWD_SGD_SR if (bank.stochastic_rounding and
+                                     bank.weight.dtype == torch.bfloat16) else _mrec.BWD_SGD), lr
+    mode, lr = bank.apply_mode()
+    if mode in (_mrec.BWD_SGD, _mrec.BWD_SGD_SR):
+        lr = lr / bank.world
+    return mode, lr
+
+
+def owner_view_fits_hash(bank: ShardedEmbeddingBank) -> bool:
+    """The owner's exchange view (W * cap entries per table) fits the hash / sorted
+    plan of one workgroup per table; larger views (big W * cap: Zipf ids, large
+    batches) take the large-batch path with given gradients (owner_apply_large)."""
+    return bank.world * bank.cap <= _mrec.BWD_MAX_BATCH
+
+
+def owner_apply_large(bank: ShardedEmbeddingBank, recv_ids: torch.Tensor, part: int,
+                      g_occ: Optional[torch.Tensor] = None, wire_g: Optional[torch.Tensor] = None,
+                      pref: Optional[torch.Tensor] = None, lr: Optional[float] = None,
+                      grad: Optional[torch.Tensor] = None):
+    """Owner: the large-batch bucketed plan over the received ids' exchange view
+    (W * cap entries per table, padding skipped) and one update per row from the
+    GIVEN gradients -- the slot exchange's fp32 slots (``g_occ``) or the compact
+    exchange's records (``wire_g`` + ``pref``) -- in ONE call
+    (mrec_emb_bwd_large_fused_given, ABI 25).  Rows hit <= 16 times are summed in
+    entry order (= sender rank order, as the hash path), hotter rows in the
+    order-free 64-bit fixed point."""
+    F, W, cap = bank.n_tables, bank.world, bank.cap
+    n = W * cap
+    mode, lr = _owner_mode(bank, lr, grad)
+    ws = _large_ws_for(bank, n)
+    idd = _mrec.IdsDesc.exchange_view(recv_ids, F, cap, part)
+    g = _mrec.GivenGrads()
+    g.chunk = cap
+    if g_occ is not None:
+        g.g_occ, g.g_ld, g.chunk_stride = g_occ.data_ptr(), g_occ.shape[1], F * cap
+    else:
+        g.wire, g.rec_bytes = wire_g.data_ptr(), bank.wire_bytes()
+        g.wire_dtype, g.pref, g.cap_rows = (_mrec.dtype_code(bank.weight.dtype), pref.data_ptr(),
+                                            bank.cap_rows)
+    from pytorchrec_amd import dense as dense_ops
+    jobs = dense_ops.take_pending(4)
+    arr = (_mrec.GemmCall * len(jobs))(*[j.struct() for j in jobs]) if jobs else None
+    fl = bank.flags()
+    _mrec.call("mrec_emb_bwd_large_fused_given", bank.desc().ref(), idd.ref(), n, ws.data_ptr(),
+               ws.numel(), fl.data_ptr() + 4, ctypes.byref(g), mode, float(lr), bank.next_seed(),
+               bank.step_counter().data_ptr(), _mrec.ptr(grad), len(jobs), arr,
+               _mrec.stream_handle())
+    del jobs
+
+
+def _large_ws_for(bank: ShardedEmbeddingBank, n: int) -> torch.Tensor:
+    """The bank's large-batch workspace for exchange views of n entries per table
+    (zeroed once; every call leaves its zero region zero)."""
+    from pytorchrec_amd.embedding import _large_ws
+    return _large_ws(bank, n)
 
 
 # ----------------------------------------------------------------------------
@@ -673,8 +730,9 @@ class _CompactInteractFn(torch.autograd.Function):
         send, pos = shard_bucketize_dedup(bank, ids)
         recv = comm.exchange(send)
         train = trigger is not None
-        # the owner's backward plan rides in the gather launch (same received ids)
-        ojob_ok = train and bank.world * bank.cap <= _mrec.BWD_MAX_BATCH
+        # the owner's backward plan rides in the gather launch (same received ids);
+        # a view past one plan workgroup takes the large path in the backward
+        ojob_ok = train and owner_view_fits_hash(bank)
         ojob, oplan, okeep = (owner_plan_job(bank, recv, bank.part) if ojob_ok
                               else (None, None, None))
         pref = (torch.empty(bank.world, bank.n_tables, dtype=torch.int32, device=dev)
@@ -693,7 +751,7 @@ class _CompactInteractFn(torch.autograd.Function):
         del keep
         if train and not fuse:
             splan = sender_plan(bank, rows_recv, pos)
-        if train and oplan is None:
+        if train and oplan is None and owner_view_fits_hash(bank):
             oplan = owner_plan(bank, recv, bank.part)
         if bank.check_ids:
             bank.check_flags()
@@ -727,14 +785,18 @@ class _CompactInteractFn(torch.autograd.Function):
                              fm_sum=fm_sum, x0=x0 if dfm is not None else None, dw=dw)
             wire_g = bank.comm.exchange(shard_wire_pack(bank, gsum, send))
             # the owner reads the gradient records in place (no unpack launch)
-            owner_apply_wire(bank, ctx.oplan, wire_g, ctx.pref)
+            if ctx.oplan is not None:
+                owner_apply_wire(bank, ctx.oplan, wire_g, ctx.pref)
+            else:
+                owner_apply_large(bank, recv, bank.part, wire_g=wire_g, pref=ctx.pref)
         g_dense_w, g_bias = _dense_first_order_grads(ctx, dlogit, dense)
         return g_dense_w, g_bias, None, None, None, None, None, None, None, None
 
 
 class _ShardedInteractFn(torch.autograd.Function):
-    """The slot exchange of ABI 14 (one row / fp32 gradient per lookup): banks under
-    a fused lazy Adam, and ``ShardedEmbeddingBank.compact = False``."""
+    """The slot exchange of ABI 14 (one row / fp32 gradient per lookup):
+    ``ShardedEmbeddingBank.compact = False`` (and shapes the compact bucketize
+    does not take, ShardedEmbeddingBank.use_compact)."""
 
     @staticmethod
     def forward(ctx, dense_w, bias, trigger, bank: ShardedEmbeddingBank, ids, dense, fm2: bool,
@@ -745,14 +807,18 @@ class _ShardedInteractFn(torch.autograd.Function):
         send_ids, pos = shard_bucketize(bank, ids)
         recv_ids = comm.exchange(send_ids)
         rows_recv = comm.exchange(shard_gather(bank, recv_ids))
-        job, plan, keep = (owner_plan_job(bank, recv_ids) if trigger is not None
+        train = trigger is not None
+        # the owner's plan rides in the interaction launch when its exchange view fits
+        # one plan workgroup per table; else the large path in the backward
+        job, plan, keep = (owner_plan_job(bank, recv_ids) if train and owner_view_fits_hash(bank)
                            else (None, None, None))
         x0, logit, fm_sum = shard_interact(bank, rows_recv, pos, dense, dense_w, bias, fm2,
                                            first_order, x0_cols, x0_dtype, plan_job=job)
         del keep
         if bank.check_ids:
             bank.check_flags()
-        ctx.bank, ctx.B, ctx.plan = bank, B, plan
+        ctx.bank, ctx.B, ctx.plan, ctx.train = bank, B, plan, train
+        ctx.recv_ids = recv_ids if train and plan is None else None
         ctx.fm2, ctx.first_order = fm2, first_order
         ctx.has_dense_w, ctx.has_bias = dense_w is not None, bias is not None
         ctx.dense_w, ctx.bias = dense_w, bias
@@ -775,11 +841,14 @@ class _ShardedInteractFn(torch.autograd.Function):
         dw = dlogit if (ctx.first_order and dlogit is not None) else None
         if dx0 is not None:
             dx0 = dx0.contiguous()
-        if ctx.plan is not None:
+        if ctx.train:
             g_send = shard_lookup_grad(bank, pos, ctx.B, dx=dx0, dfm=dfm, fm_sum=fm_sum,
                                        x0=x0 if dfm is not None else None, dw=dw)
             g_recv = bank.comm.exchange(g_send)
-            owner_apply(bank, ctx.plan, g_recv)
+            if ctx.plan is not None:
+                owner_apply(bank, ctx.plan, g_recv)
+            else:
+                owner_apply_large(bank, ctx.recv_ids, 0, g_occ=g_recv)
         g_dense_w, g_bias = _dense_first_order_grads(ctx, dlogit, dense)
         return g_dense_w, g_bias, None, None, None, None, None, None, None, None
 

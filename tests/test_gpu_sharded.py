@@ -132,7 +132,7 @@ def test_sharded_overflow_is_raised(gpu):
         bank.check_flags()
 
 
-def _deepfm(gpu, sharded):
+def _deepfm(gpu, sharded, emb_dtype=torch.bfloat16):
     from pytorchrec_amd.feature_column import CategoricalColumnWithIdentity, NumericColumn
     from pytorchrec_amd.model import DeepFM
     from pytorchrec_amd.sharding import ShardComm, sharded_tables
@@ -142,10 +142,10 @@ def _deepfm(gpu, sharded):
     torch.manual_seed(3)
     if sharded:
         with sharded_tables(ShardComm(world=1, rank=0), max_batch=256):
-            m = DeepFM(sparse, dense, label, emb_size=D, layers=(64, 32), emb_dtype=torch.bfloat16,
+            m = DeepFM(sparse, dense, label, emb_size=D, layers=(64, 32), emb_dtype=emb_dtype,
                        random_seed=5, device=gpu)
     else:
-        m = DeepFM(sparse, dense, label, emb_size=D, layers=(64, 32), emb_dtype=torch.bfloat16,
+        m = DeepFM(sparse, dense, label, emb_size=D, layers=(64, 32), emb_dtype=emb_dtype,
                    random_seed=5, device=gpu)
     return m
 
@@ -197,6 +197,42 @@ def test_world1_sharded_fused_optimizers_equal_unsharded(gpu, opt):
     assert a.embeddings.update == kind and b.embeddings.update == kind
     la = [float(a.train_step(d)["loss"].detach()) for d in batches]
     lb = [float(b.train_step(d)["loss"].detach()) for d in batches]
+    np.testing.assert_allclose(la, lb, rtol=1e-6)
+    sa, sb = a.state_dict(), b.state_dict()
+    for k in sa:
+        torch.testing.assert_close(sa[k].float(), sb[k].float(), rtol=1e-5, atol=1e-6)
+
+
+@pytest.mark.parametrize("opt", ["adam", "adamw"])
+def test_world1_compact_exchange_lazy_adam_equals_unsharded(gpu, opt):
+    """A fused lazy Adam bank on the COMPACT exchange (ABI 25: the owner's wire
+    gather catches every row up to the current step as it packs the record; the
+    owner's apply reads the gradient records in place and steps Adam): at W = 1
+    with fp32 tables (fp32 records: the wire is exact) the sharded model equals the
+    unsharded one over batches that leave rows out for a step, i.e. the forward
+    reads the caught-up rows and the updates replay the missed steps the same way."""
+    from pytorchrec_amd.loss import BCEWithLogitsLoss
+    from pytorchrec_amd.optim import AdamW
+    a, b = _deepfm(gpu, False, torch.float32), _deepfm(gpu, True, torch.float32)
+    b.load_state_dict(a.state_dict())
+    b.embeddings.compact = "always"
+    batches = []
+    for s in range(4):
+        data = {f"c_c_C{i}": t for i, t in enumerate(_ids(gpu, 256, 60 + s))}
+        g = torch.Generator().manual_seed(70 + s)
+        for i in range(13):
+            data[f"c_n_I{i}"] = torch.rand(256, generator=g).to(gpu)
+        data["label"] = (torch.rand(256, generator=g) < 0.25).to(torch.int32).to(gpu)
+        batches.append(data)
+    make = {"adam": lambda p: torch.optim.Adam(p, lr=0.01, weight_decay=0.01),
+            "adamw": lambda p: AdamW(p, lr=0.01, weight_decay=0.01)}[opt]
+    for m in (a, b):
+        m.compile(make(m.get_parameters()), BCEWithLogitsLoss(), [], gpu)
+    assert a.embeddings.update == "adam" and b.embeddings.update == "adam"
+    assert b.embeddings.use_compact(256)
+    la = [float(a.train_step(d)["loss"].detach()) for d in batches]
+    lb = [float(b.train_step(d)["loss"].detach()) for d in batches]
+    b.embeddings.check_flags()
     np.testing.assert_allclose(la, lb, rtol=1e-6)
     sa, sb = a.state_dict(), b.state_dict()
     for k in sa:
@@ -332,9 +368,11 @@ def test_sgd_multi_matches_torch_and_weight_prep(gpu):
 # compact exchange (ABI 19): distinct ids, 36-B records, summed gradients
 # ---------------------------------------------------------------------------
 
-@pytest.mark.parametrize("W,zipf,B", [(2, False, 512), (4, True, 512), (8, False, 1024),
-                                      (3, True, 4096), (8, True, 4096), (2, False, 8192)])
-def test_compact_exchange_simulated_bit_exact(gpu, W, zipf, B):
+@pytest.mark.parametrize("W,zipf,B,big", [(2, False, 512, False), (4, True, 512, False),
+                                          (8, False, 1024, False), (3, True, 4096, False),
+                                          (8, True, 4096, False), (2, False, 8192, False),
+                                          (8, True, 4096, True), (4, False, 8192, True)])
+def test_compact_exchange_simulated_bit_exact(gpu, W, zipf, B, big):
     """W ranks simulated in one process (all-to-alls by slicing), every stage checked:
       * bucketize_dedup == its CPU restatement (cpu_bucketize_dedup): the distinct
         ids per (owner, table) in first-lookup order, every lookup's slot, counts;
@@ -346,6 +384,10 @@ def test_compact_exchange_simulated_bit_exact(gpu, W, zipf, B):
       * the owner's sum over the senders (DENSE_GRAD) == the fp32 sum of the ranks'
         bf16 gradients in rank order, rounded once (bit-exact);
       * with fused SGD the owners' rows are within 1 bf16 ulp of that sum applied.
+    ``big``: cap = B, so the owner's exchange view (W * cap entries per table, up to
+    32,768) exceeds one plan workgroup and the owner takes the large-batch bucketed
+    path over the received records / fp32 slots (owner_apply_large, ABI 25): the
+    same sums (a row has <= W entries, summed in sender order), bit-exact.
     Per-rank bytes on the wire are checked against the slot exchange."""
     from pytorchrec_amd import embedding as E
     from pytorchrec_amd import sharding as S
@@ -354,7 +396,7 @@ def test_compact_exchange_simulated_bit_exact(gpu, W, zipf, B):
     for r in range(W):
         b = S.ShardedEmbeddingBank(ROWS, D, S.ShardComm(world=W, rank=r), with_first_order=True,
                                    dtype=torch.bfloat16, max_batch=B, device=gpu,
-                                   cap=min(B, 8192 // W) if zipf else None)
+                                   cap=B if big else (min(B, 8192 // W) if zipf else None))
         b.load_global_(_tables(glob))
         b.stochastic_rounding = False
         assert b.use_compact(B)
@@ -386,7 +428,8 @@ def test_compact_exchange_simulated_bit_exact(gpu, W, zipf, B):
                                      x0_cols, torch.bfloat16, plan_job=job))
         del keep
         plans.append(sp if fuse else S.sender_plan(banks[r], rr, poss[r]))
-        oplans.append(S.owner_plan(banks[r], recvs[r], banks[r].part))
+        assert S.owner_view_fits_hash(banks[r]) != big
+        oplans.append(None if big else S.owner_plan(banks[r], recvs[r], banks[r].part))
     for r in range(W):
         banks[r].check_flags()
         gw = glob.weight
@@ -425,11 +468,16 @@ def test_compact_exchange_simulated_bit_exact(gpu, W, zipf, B):
         g_recv = torch.empty(n, banks[r].g_ld, dtype=torch.float32, device=gpu)
         S.shard_wire_unpack(banks[r], wire_g[r], recvs[r], g_recv, to_f32=True)
         own = torch.zeros_like(banks[r].weight)
-        S.owner_apply(banks[r], oplans[r], g_recv, grad=own)
-        banks[r].check_flags()
-        # the same sums read from the received records in place (no unpack)
         own_w = torch.zeros_like(banks[r].weight)
-        S.owner_apply_wire(banks[r], oplans[r], wire_g[r], prefs[r], grad=own_w)
+        if big:  # the large-batch path over the slots, then over the records in place
+            S.owner_apply_large(banks[r], recvs[r], banks[r].part, g_occ=g_recv, grad=own)
+            S.owner_apply_large(banks[r], recvs[r], banks[r].part, wire_g=wire_g[r],
+                                pref=prefs[r], grad=own_w)
+        else:
+            S.owner_apply(banks[r], oplans[r], g_recv, grad=own)
+            # the same sums read from the received records in place (no unpack)
+            S.owner_apply_wire(banks[r], oplans[r], wire_g[r], prefs[r], grad=own_w)
+        banks[r].check_flags()
         assert torch.equal(own_w.view(torch.int16), own.view(torch.int16)), r
         for f, (o, cnt) in enumerate(zip(banks[r].row_offset, banks[r].category_nums)):
             want = tot[glob.row_offset[f]:glob.row_offset[f] + ROWS[f]][r::W, :D + 1]
@@ -437,12 +485,20 @@ def test_compact_exchange_simulated_bit_exact(gpu, W, zipf, B):
         # fused SGD from the same sums: within one bf16 ulp of w - lr * sum
         lr = 0.5
         before = banks[r].weight.detach().clone()
-        S.owner_apply_wire(banks[r], oplans[r], wire_g[r], prefs[r], lr)
+        if big:
+            S.owner_apply_large(banks[r], recvs[r], banks[r].part, wire_g=wire_g[r],
+                                pref=prefs[r], lr=lr)
+        else:
+            S.owner_apply_wire(banks[r], oplans[r], wire_g[r], prefs[r], lr)
         after_wire = banks[r].weight.detach().clone()
         with torch.no_grad():
             banks[r].weight.copy_(before)
-        S.owner_apply(banks[r], oplans[r], g_recv, lr)
-        # bitwise (the shard's pad columns hold uninitialised bits, NaNs included)
+        if big:
+            S.owner_apply_large(banks[r], recvs[r], banks[r].part, g_occ=g_recv, lr=lr)
+        else:
+            S.owner_apply(banks[r], oplans[r], g_recv, lr)
+        banks[r].check_flags()
+        # bitwise, pad columns included (zeroed at allocation)
         assert torch.equal(banks[r].weight.view(torch.int16), after_wire.view(torch.int16)), r
         for f, (o, cnt) in enumerate(zip(banks[r].row_offset, banks[r].category_nums)):
             g = tot[glob.row_offset[f]:glob.row_offset[f] + ROWS[f]][r::W, :D + 1].double()

@@ -546,9 +546,24 @@ mrec_status mrec_shard_bucketize_dedup(const mrec_ids *ids, int32_t n_tables, co
                                        int64_t batch, int32_t world, int32_t cap,
                                        int32_t *send_ids, int32_t *pos, int32_t *d_overflow,
                                        int32_t *d_oob_flag, mrec_stream stream);
+/*
+ * Batches past one workgroup's hash (ABI 25): the sender's batch is cut into
+ * C = ceil(batch / chunk_batch) chunks (chunk_batch <= 8192), each its own
+ * sub-sender -- part d * C + c of send_ids holds chunk c's distinct ids for owner d
+ * (owner d's C parts contiguous, so the equal-split all-to-all moves W parts of
+ * C * (n_tables*cap + n_tables) int32), pos addresses slot rows of W * C parts, and
+ * every other compact-exchange call takes world = W * C.  An id repeated across
+ * chunks takes a slot in each; the owner sums its entries in part order.
+ */
+mrec_status mrec_shard_bucketize_dedup_ex(const mrec_ids *ids, int32_t n_tables,
+                                          const int64_t *rows, int64_t batch, int32_t world,
+                                          int32_t cap, int64_t chunk_batch, int32_t *send_ids,
+                                          int32_t *pos, int32_t *d_overflow, int32_t *d_oob_flag,
+                                          mrec_stream stream);
 /* bytes of one wire record: round4((dim + has_w) * element bytes) */
 int32_t mrec_shard_wire_bytes(int32_t dim, int32_t has_w, mrec_dtype dtype);
-/* owner: rows of the received ids (header = recv_ids) -> wire (no lazy-Adam banks);
+/* owner: rows of the received ids (header = recv_ids) -> wire (a lazy-Adam bank's
+ * rows caught up to the current step, ABI 25); 
  * plan (may be NULL, ABI 21): the owner's backward hash plan over the same received
  * ids (an exchange view, mrec_plan_job) run by leading workgroups of this launch */
 mrec_status mrec_shard_gather_wire(const mrec_table_bank *local, const int32_t *recv_ids,

@@ -324,6 +324,9 @@ SIGNATURES = {
                                    _f32, _vp]),
     "mrec_shard_bucketize_dedup": (ctypes.c_int, [_ids_p, _i32, ctypes.POINTER(ctypes.c_int64),
                                                   _i64, _i32, _i32, _vp, _vp, _vp, _vp, _vp]),
+    "mrec_shard_bucketize_dedup_ex": (ctypes.c_int, [_ids_p, _i32, ctypes.POINTER(ctypes.c_int64),
+                                                     _i64, _i32, _i32, _i64, _vp, _vp, _vp, _vp,
+                                                     _vp]),
     "mrec_shard_wire_bytes": (_i32, [_i32, _i32, _i32]),
     "mrec_shard_gather_wire": (ctypes.c_int, [_bank_p, _vp, _i32, _i32, _i32, _vp, _vp,
                                               ctypes.POINTER(PlanJob), _vp]),

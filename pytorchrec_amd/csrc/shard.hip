@@ -163,12 +163,17 @@ __device__ __forceinline__ uint32_t id_hash(uint32_t x, uint32_t mask) {
   return (x * 2654435761u) & mask;
 }
 
-__global__ __launch_bounds__(kBT) void bucketize_dedup_kernel(IdsArgs ids, RowsArg rows, int64_t B,
+// Batches past one workgroup's hash (8192 samples) are cut into C chunks of cb
+// samples (grid y): chunk c of the batch is its own "sub-sender", part d * C + c of
+// send_ids (owner d's C parts contiguous, so the equal-split all-to-all still moves
+// W parts of C * P); an id repeated across chunks takes a slot in each.
+__global__ __launch_bounds__(kBT) void bucketize_dedup_kernel(IdsArgs ids, RowsArg rows, int64_t Btot,
                                                               int W, int cap, int F, int hs,
                                                               int32_t *__restrict__ send_ids,
                                                               int32_t *__restrict__ pos,
                                                               int32_t *__restrict__ overflow,
-                                                              int32_t *__restrict__ oob) {
+                                                              int32_t *__restrict__ oob, int C,
+                                                              int64_t cb) {
   __shared__ uint32_t hist[kBHist];
   __shared__ uint32_t wtot[kBWaves];
   extern __shared__ uint32_t hash_lds[];  // keys [hs] | (first << 16 | slot) [hs]
@@ -176,6 +181,9 @@ __global__ __launch_bounds__(kBT) void bucketize_dedup_kernel(IdsArgs ids, RowsA
   uint32_t *fs = hash_lds + hs;
   const uint32_t hmask = static_cast<uint32_t>(hs - 1);
   const int f = blockIdx.x;
+  const int c = blockIdx.y;
+  const int64_t s0 = static_cast<int64_t>(c) * cb;
+  const int64_t B = min(cb, Btot - s0);  // this chunk's samples
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int64_t rows_f = rows.v[f];
   const int rounds = static_cast<int>((B + kBT - 1) / kBT);  // <= 8 (B <= 8192)
@@ -189,7 +197,7 @@ __global__ __launch_bounds__(kBT) void bucketize_dedup_kernel(IdsArgs ids, RowsA
 #pragma unroll
   for (int r = 0; r < kR; ++r) {
     const int64_t i = static_cast<int64_t>(r) * kBT + tid;
-    idv[r] = (r < rounds && i < B) ? load_id(ids, f, i) : -2;
+    idv[r] = (r < rounds && i < B) ? load_id(ids, f, s0 + i) : -2;
   }
   for (int i = tid; i < nh; i += kBT) hist[i] = 0u;
   for (int i = tid; i < hs; i += kBT) {
@@ -242,7 +250,7 @@ __global__ __launch_bounds__(kBT) void bucketize_dedup_kernel(IdsArgs ids, RowsA
       if (overflow) atomicOr(overflow, 1);  // bit 0: a table's `cap` slots
       slot = 0xffffu;
     } else {
-      send_ids[d * P + static_cast<int64_t>(f) * cap + slot] =
+      send_ids[(static_cast<int64_t>(d) * C + c) * P + static_cast<int64_t>(f) * cap + slot] =
           static_cast<int32_t>(static_cast<uint32_t>(idv[r]) / static_cast<uint32_t>(W));
     }
     fs[hpos[r]] = (static_cast<uint32_t>(r * kBT + tid) << 16) | slot;
@@ -256,19 +264,22 @@ __global__ __launch_bounds__(kBT) void bucketize_dedup_kernel(IdsArgs ids, RowsA
     const int64_t id = idv[r];
     if (hpos[r] == kEmpty) {
       if (oob && id != -2) *oob = 1;
-      pos[f * B + i] = -1;
+      pos[f * Btot + s0 + i] = -1;
       continue;
     }
     const uint32_t slot = fs[hpos[r]] & 0xffffu;
     const uint32_t d = static_cast<uint32_t>(id) % static_cast<uint32_t>(W);
-    pos[f * B + i] = slot == 0xffffu ? -1 : static_cast<int32_t>((static_cast<int64_t>(d) * F + f) * cap + slot);
+    pos[f * Btot + s0 + i] =
+        slot == 0xffffu ? -1
+                        : static_cast<int32_t>(((static_cast<int64_t>(d) * C + c) * F + f) * cap + slot);
   }
   // 4. counts header and padding slots of every owner part
   for (int d = 0; d < W; ++d) {
     const uint32_t cnt = min(static_cast<uint32_t>(cap), hist[(d + 1) * G] - hist[d * G]);
-    int32_t *part = send_ids + d * P + static_cast<int64_t>(f) * cap;
+    const int64_t pd = (static_cast<int64_t>(d) * C + c) * P;
+    int32_t *part = send_ids + pd + static_cast<int64_t>(f) * cap;
     for (int s = static_cast<int>(cnt) + tid; s < cap; s += kBT) part[s] = -1;
-    if (tid == 0) send_ids[d * P + static_cast<int64_t>(F) * cap + f] = static_cast<int32_t>(cnt);
+    if (tid == 0) send_ids[pd + static_cast<int64_t>(F) * cap + f] = static_cast<int32_t>(cnt);
   }
 }
 
@@ -694,27 +705,34 @@ mrec_status mrec_shard_lookup_grad(int64_t batch, int32_t n_tables, int32_t dim,
 
 // ---- compact exchange (ABI 19) ----------------------------------------------
 
-mrec_status mrec_shard_bucketize_dedup(const mrec_ids *ids, int32_t n_tables, const int64_t *rows,
-                                       int64_t batch, int32_t world, int32_t cap,
-                                       int32_t *send_ids, int32_t *pos, int32_t *d_overflow,
-                                       int32_t *d_oob_flag, mrec_stream stream) {
+mrec_status mrec_shard_bucketize_dedup_ex(const mrec_ids *ids, int32_t n_tables,
+                                          const int64_t *rows, int64_t batch, int32_t world,
+                                          int32_t cap, int64_t chunk_batch, int32_t *send_ids,
+                                          int32_t *pos, int32_t *d_overflow, int32_t *d_oob_flag,
+                                          mrec_stream stream) {
   MREC_CHECK_ARG(n_tables >= 1 && n_tables <= MREC_MAX_TABLES, "n_tables out of range");
   MREC_CHECK_ARG(rows != nullptr && send_ids && pos, "NULL pointer");
-  MREC_CHECK_ARG(world >= 1 && cap >= 1 && cap < 65535 && batch >= 0 && batch <= 8192,
-                 "bad world / cap / batch (batch <= 8192, cap < 65535)");
+  MREC_CHECK_ARG(world >= 1 && cap >= 1 && cap < 65535 && batch >= 0,
+                 "bad world / cap / batch (cap < 65535)");
+  MREC_CHECK_ARG(chunk_batch >= 1 && chunk_batch <= 8192, "chunk_batch must be in [1, 8192]");
+  const int64_t C = batch > 0 ? (batch + chunk_batch - 1) / chunk_batch : 1;
+  MREC_CHECK_ARG(C <= 65535 && batch * n_tables < (int64_t(1) << 31) &&
+                     int64_t(world) * C * n_tables * cap < (int64_t(1) << 31),
+                 "batch / chunks too large for int32 slots");
   IdsArgs ia;
   mrec_status st = make_ids_args(ids, n_tables, &ia);
   if (st != MREC_OK) return st;
-  const int64_t groups = (batch + kBT - 1) / kBT * kBWaves;
+  const int64_t cb = std::min<int64_t>(chunk_batch, std::max<int64_t>(batch, 1));
+  const int64_t groups = (cb + kBT - 1) / kBT * kBWaves;
   MREC_CHECK_ARG((world + 1) * std::max<int64_t>(groups, 1) <= kBHist,
-                 "(world + 1) * ceil(batch / 64) must be <= 2048");
+                 "(world + 1) * ceil(chunk_batch / 64) must be <= 2048");
   RowsArg ra;
   for (int f = 0; f < MREC_MAX_TABLES; ++f) {
     ra.v[f] = f < n_tables ? rows[f] : 0;
     MREC_CHECK_ARG(ra.v[f] >= 0 && ra.v[f] < (int64_t(1) << 31), "rows per table must be < 2^31");
   }
   int hs = 1024;
-  while (hs < 2 * batch) hs *= 2;  // load factor <= 1/2
+  while (hs < 2 * cb) hs *= 2;  // load factor <= 1/2
   const size_t lds = static_cast<size_t>(hs) * 8;
   static int attr = [] {
     (void)hipFuncSetAttribute(reinterpret_cast<const void *>(bucketize_dedup_kernel),
@@ -723,9 +741,22 @@ mrec_status mrec_shard_bucketize_dedup(const mrec_ids *ids, int32_t n_tables, co
     return 1;
   }();
   (void)attr;
-  bucketize_dedup_kernel<<<dim3(n_tables), kBT, lds, static_cast<hipStream_t>(stream)>>>(
-      ia, ra, batch, world, cap, n_tables, hs, send_ids, pos, d_overflow, d_oob_flag);
+  bucketize_dedup_kernel<<<dim3(n_tables, static_cast<unsigned>(C)), kBT, lds,
+                           static_cast<hipStream_t>(stream)>>>(
+      ia, ra, batch, world, cap, n_tables, hs, send_ids, pos, d_overflow, d_oob_flag,
+      static_cast<int>(C), cb);
   return launch_status("mrec_shard_bucketize_dedup");
+}
+
+mrec_status mrec_shard_bucketize_dedup(const mrec_ids *ids, int32_t n_tables, const int64_t *rows,
+                                       int64_t batch, int32_t world, int32_t cap,
+                                       int32_t *send_ids, int32_t *pos, int32_t *d_overflow,
+                                       int32_t *d_oob_flag, mrec_stream stream) {
+  MREC_CHECK_ARG(batch >= 0 && batch <= 8192, "batch must be <= 8192 (mrec_shard_bucketize_dedup_ex "
+                                              "takes larger batches in chunks)");
+  return mrec_shard_bucketize_dedup_ex(ids, n_tables, rows, batch, world, cap,
+                                       std::max<int64_t>(batch, 1), send_ids, pos, d_overflow,
+                                       d_oob_flag, stream);
 }
 
 int32_t mrec_shard_wire_bytes(int32_t dim, int32_t has_w, mrec_dtype dtype) {

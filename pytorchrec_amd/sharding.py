@@ -237,8 +237,8 @@ class ShardedEmbeddingBank(EmbeddingBank):
         self.global_rows = [int(n) for n in category_nums]
         self.comm = comm
         self.world, self.rank = W, r
-        self.cap = (int(cap) if cap is not None
-                    else default_cap(max_batch, W, self.global_rows))
+        self.cap = (int(cap) if cap is not None  # slots per (owner, table[, chunk])
+                    else default_cap(min(int(max_batch), self.chunk_batch), W, self.global_rows))
         if self.cap < 1:
             raise ValueError(f"cap = {self.cap} must be >= 1")
         self._flags = None  # device int32 [2] = {overflow, oob}, sticky until checked
@@ -249,26 +249,37 @@ class ShardedEmbeddingBank(EmbeddingBank):
         # path keeps the step bit-identical to the unsharded bank (the compact path
         # rounds each rank's gradient sum of a bf16 row to bf16 on the wire).
         self.compact = True
-        self.cap_rows = default_cap_rows(max_batch, W, self.global_rows, self.cap)
+        self.cap_rows = default_cap_rows(min(int(max_batch), self.chunk_batch), W,
+                                         self.global_rows, self.cap)
 
     @property
     def part(self) -> int:
         """int32 per owner part of the compact ids message: slots, then counts."""
         return self.n_tables * self.cap + self.n_tables
 
+    # a sender's batch past one bucketize workgroup (8192 samples) goes out in
+    # chunks, each its own sub-sender: W * chunks parts on the compact exchange
+    chunk_batch = 8192
+
+    def chunks(self, batch: int) -> int:
+        return max(1, -(-int(batch) // self.chunk_batch))
+
+    def parts(self, batch: int) -> int:
+        """Parts of the compact exchange's messages for a batch: world x chunks."""
+        return self.world * self.chunks(batch)
+
     def wire_bytes(self) -> int:
         dt = _mrec.dtype_code(self.weight.dtype)
         return int(_mrec.lib().mrec_shard_wire_bytes(self.dim, int(self.has_w), dt))
 
     def use_compact(self, batch: int) -> bool:
-        """The compact exchange when it is on and mrec_shard_bucketize_dedup takes the
-        shape: B <= 8192 (16-bit sample index), cap < 65535, and its per-(owner,
-        wave-group) histogram (world + 1) * ceil(B / 1024) * 16 <= 2048 entries
-        (e.g. W >= 16 at B = 8192 falls back to the slot exchange)."""
+        """The compact exchange when it is on and mrec_shard_bucketize_dedup_ex takes
+        the shape: cap < 65535 and its per-(owner, wave-group) histogram (world + 1)
+        * ceil(chunk / 1024) * 16 <= 2048 entries (e.g. W >= 16 at 8192-sample chunks
+        falls back to the slot exchange).  Batches past 8192 go out in chunks."""
         on = self.compact == "always" or (bool(self.compact) and self.world > 1)
-        groups = max(1, -(-int(batch) // 1024) * 16)
-        return (on and batch <= _mrec.BWD_MAX_BATCH
-                and self.cap < 65535 and (self.world + 1) * groups <= 2048)
+        groups = max(1, -(-min(int(batch), self.chunk_batch) // 1024) * 16)
+        return on and self.cap < 65535 and (self.world + 1) * groups <= 2048
 
     @property
     def g_ld(self) -> int:
@@ -416,31 +427,34 @@ def shard_gather(bank: ShardedEmbeddingBank, recv_ids: torch.Tensor) -> torch.Te
 
 
 def shard_bucketize_dedup(bank: ShardedEmbeddingBank, ids: Sequence[torch.Tensor]):
-    """-> (send_ids [W, F*cap + F] int32: distinct ids per (owner, table) + counts,
-    pos [F, B] int32: the slot of every lookup)."""
+    """-> (send_ids [W, C * (F*cap + F)] int32: distinct ids per (owner, table) +
+    counts for each of the C chunks of the batch (bank.chunks), pos [F, B] int32:
+    the slot of every lookup in the W * C parts' slot rows)."""
     F, W, cap = bank.n_tables, bank.world, bank.cap
     B = ids[0].shape[0]
+    C = bank.chunks(B)
     dev = bank.weight.device
-    send = torch.empty(W, bank.part, dtype=torch.int32, device=dev)
+    send = torch.empty(W, C * bank.part, dtype=torch.int32, device=dev)
     pos = torch.empty(F, B, dtype=torch.int32, device=dev)
     fl = bank.flags()
-    _mrec.call("mrec_shard_bucketize_dedup", _mrec.IdsDesc(ids).ref(), F, bank._global_rows_arr,
-               B, W, cap, send.data_ptr(), pos.data_ptr(), fl.data_ptr(), fl.data_ptr() + 4,
-               _mrec.stream_handle())
+    _mrec.call("mrec_shard_bucketize_dedup_ex", _mrec.IdsDesc(ids).ref(), F,
+               bank._global_rows_arr, B, W, cap, bank.chunk_batch, send.data_ptr(),
+               pos.data_ptr(), fl.data_ptr(), fl.data_ptr() + 4, _mrec.stream_handle())
     return send, pos
 
 
 def shard_gather_wire(bank: ShardedEmbeddingBank, recv_ids: torch.Tensor,
-                      plan_job=None, pref: Optional[torch.Tensor] = None) -> torch.Tensor:
+                      plan_job=None, pref: Optional[torch.Tensor] = None,
+                      parts: Optional[int] = None) -> torch.Tensor:
     """Owner: one record per received distinct id -> [W, cap_rows * record] bytes.
     ``plan_job`` (owner_plan_job) runs the owner's backward plan over the same ids in
     leading workgroups of the launch; ``pref`` (int32 [W, n_tables]) receives each
     part's table prefixes (mrec_shard_gather_wire_ex), which address the gradient
-    records the senders return (owner_apply_wire)."""
-    W, rb = bank.world, bank.wire_bytes()
-    wire = torch.empty(W, bank.cap_rows * rb, dtype=torch.uint8, device=bank.weight.device)
+    records the senders return (owner_apply_wire).  ``parts``: W * chunks."""
+    P, rb = parts or bank.world, bank.wire_bytes()
+    wire = torch.empty(P, bank.cap_rows * rb, dtype=torch.uint8, device=bank.weight.device)
     fl = bank.flags()
-    _mrec.call("mrec_shard_gather_wire_ex", bank.desc().ref(), recv_ids.data_ptr(), W, bank.cap,
+    _mrec.call("mrec_shard_gather_wire_ex", bank.desc().ref(), recv_ids.data_ptr(), P, bank.cap,
                bank.cap_rows, wire.data_ptr(), _mrec.ptr(pref), fl.data_ptr(),
                ctypes.byref(plan_job) if plan_job is not None else None, _mrec.stream_handle())
     return wire
@@ -448,25 +462,26 @@ def shard_gather_wire(bank: ShardedEmbeddingBank, recv_ids: torch.Tensor,
 
 def shard_wire_unpack(bank: ShardedEmbeddingBank, wire: torch.Tensor, hdr: torch.Tensor,
                       slots: torch.Tensor, to_f32: bool = False,
-                      zero: Optional[torch.Tensor] = None):
+                      zero: Optional[torch.Tensor] = None, parts: Optional[int] = None):
     """Records -> slot rows [W*F*cap, ...] (``hdr``: the ids message whose counts
     describe ``wire``); ``zero``: the same rows of a second buffer are cleared."""
     fl = bank.flags()
     _mrec.call("mrec_shard_wire_unpack", wire.data_ptr(), bank.wire_bytes(), hdr.data_ptr(),
-               bank.world, bank.n_tables, bank.cap, bank.cap_rows, slots.data_ptr(),
+               parts or bank.world, bank.n_tables, bank.cap, bank.cap_rows, slots.data_ptr(),
                slots.stride(0) * slots.element_size(), int(to_f32), _mrec.ptr(zero),
                zero.stride(0) * zero.element_size() if zero is not None else 0, fl.data_ptr(),
                _mrec.stream_handle())
     return slots
 
 
-def shard_wire_pack(bank: ShardedEmbeddingBank, slots: torch.Tensor, hdr: torch.Tensor):
-    """Slot rows (the table dtype) -> records [W, cap_rows * record] bytes."""
-    W, rb = bank.world, bank.wire_bytes()
-    wire = torch.empty(W, bank.cap_rows * rb, dtype=torch.uint8, device=bank.weight.device)
+def shard_wire_pack(bank: ShardedEmbeddingBank, slots: torch.Tensor, hdr: torch.Tensor,
+                    parts: Optional[int] = None):
+    """Slot rows (the table dtype) -> records [W * chunks, cap_rows * record] bytes."""
+    P, rb = parts or bank.world, bank.wire_bytes()
+    wire = torch.empty(P, bank.cap_rows * rb, dtype=torch.uint8, device=bank.weight.device)
     fl = bank.flags()
     _mrec.call("mrec_shard_wire_pack", slots.data_ptr(), slots.stride(0) * slots.element_size(),
-               rb, hdr.data_ptr(), W, bank.n_tables, bank.cap, bank.cap_rows, wire.data_ptr(),
+               rb, hdr.data_ptr(), P, bank.n_tables, bank.cap, bank.cap_rows, wire.data_ptr(),
                fl.data_ptr(), _mrec.stream_handle())
     return wire
 
@@ -500,6 +515,18 @@ def sender_plan(bank: ShardedEmbeddingBank, rows_recv: torch.Tensor, pos: torch.
     return ws, wsb
 
 
+def sender_plans(bank: ShardedEmbeddingBank, rows_recv: torch.Tensor, pos: torch.Tensor):
+    """sender_plan per chunk of bank.chunk_batch samples (a chunk's lookups address
+    only its own parts' slots, so each is summed on its own) -> [(s0, n, plan)]."""
+    B = pos.shape[1]
+    cb = bank.chunk_batch
+    out = []
+    for s0 in range(0, B, cb):
+        n = min(cb, B - s0)
+        out.append((s0, n, sender_plan(bank, rows_recv, pos[:, s0:s0 + n])))
+    return out or [(0, 0, sender_plan(bank, rows_recv, pos))]
+
+
 def sender_grad_sums(bank: ShardedEmbeddingBank, rows_recv: torch.Tensor, pos: torch.Tensor,
                      plan, gsum: torch.Tensor, dx=None, dfm=None, fm_sum=None, x0=None, dw=None):
     """Sender: per slot, the sum of its lookups' gradient rows (fp32, ascending
@@ -530,12 +557,13 @@ def remote_desc(bank: ShardedEmbeddingBank, rows_recv: torch.Tensor) -> _mrec.Ba
     return _mrec.BankDesc(rows_recv, [0] * F, [n] * F, bank.dim, bank.has_w)
 
 
-def owner_plan_job(bank: ShardedEmbeddingBank, recv_ids: torch.Tensor, part: int = 0):
+def owner_plan_job(bank: ShardedEmbeddingBank, recv_ids: torch.Tensor, part: int = 0,
+                   parts: Optional[int] = None):
     """The owner's backward plan as a job for the interaction launch (hash layout
     over the padded exchange view, <= MREC_BWD_MAX_BATCH entries; ``part``: int32
     per owner part of the ids message, 0 = n_tables * cap) ->
     (job, (ws, ws_bytes), keep-alive)."""
-    F, W, cap = bank.n_tables, bank.world, bank.cap
+    F, W, cap = bank.n_tables, parts or bank.world, bank.cap
     n = W * cap
     wsb = _mrec.lib().mrec_emb_bwd_workspace_size(F, n)
     ws = torch.empty(wsb, dtype=torch.uint8, device=bank.weight.device)
@@ -575,10 +603,11 @@ def shard_interact(bank: ShardedEmbeddingBank, rows_recv: torch.Tensor, pos: tor
     return x0, logit, fm_sum
 
 
-def owner_plan(bank: ShardedEmbeddingBank, recv_ids: torch.Tensor, part: int = 0):
+def owner_plan(bank: ShardedEmbeddingBank, recv_ids: torch.Tensor, part: int = 0,
+               parts: Optional[int] = None):
     """Sorted-segment plan of the owner's received ids (padding skipped; ``part``
     as in owner_plan_job)."""
-    F, W, cap = bank.n_tables, bank.world, bank.cap
+    F, W, cap = bank.n_tables, parts or bank.world, bank.cap
     n = W * cap
     wsb = _mrec.lib().mrec_emb_bwd_workspace_size(F, n)
     ws = torch.empty(wsb, dtype=torch.uint8, device=bank.weight.device)
@@ -634,11 +663,12 @@ def owner_apply(bank: ShardedEmbeddingBank, plan, g_recv: torch.Tensor,
 
 
 def owner_apply_wire(bank: ShardedEmbeddingBank, plan, wire_g: torch.Tensor, pref: torch.Tensor,
-                     lr: Optional[float] = None, grad: Optional[torch.Tensor] = None):
+                     lr: Optional[float] = None, grad: Optional[torch.Tensor] = None,
+                     parts: Optional[int] = None):
     """owner_apply reading the received gradient records in place
     (mrec_emb_bwd_apply_wire: no unpack to fp32 slots; same sums and update)."""
     ws, wsb = plan
-    F, W, cap = bank.n_tables, bank.world, bank.cap
+    F, W, cap = bank.n_tables, parts or bank.world, bank.cap
     mode, lr = _owner_mode(bank, lr, grad)
     from pytorchrec_amd import dense as dense_ops
     jobs = dense_ops.take_pending(4)
@@ -663,17 +693,18 @@ def _owner_mode(bank: ShardedEmbeddingBank, lr, grad):
     return mode, lr
 
 
-def owner_view_fits_hash(bank: ShardedEmbeddingBank) -> bool:
-    """The owner's exchange view (W * cap entries per table) fits the hash / sorted
-    plan of one workgroup per table; larger views (big W * cap: Zipf ids, large
-    batches) take the large-batch path with given gradients (owner_apply_large)."""
-    return bank.world * bank.cap <= _mrec.BWD_MAX_BATCH
+def owner_view_fits_hash(bank: ShardedEmbeddingBank, parts: Optional[int] = None) -> bool:
+    """The owner's exchange view (parts x cap entries per table, parts = W x chunks)
+    fits the hash / sorted plan of one workgroup per table; larger views (big W *
+    cap: Zipf ids, large batches) take the large-batch path with given gradients
+    (owner_apply_large)."""
+    return (parts or bank.world) * bank.cap <= _mrec.BWD_MAX_BATCH
 
 
 def owner_apply_large(bank: ShardedEmbeddingBank, recv_ids: torch.Tensor, part: int,
                       g_occ: Optional[torch.Tensor] = None, wire_g: Optional[torch.Tensor] = None,
                       pref: Optional[torch.Tensor] = None, lr: Optional[float] = None,
-                      grad: Optional[torch.Tensor] = None):
+                      grad: Optional[torch.Tensor] = None, parts: Optional[int] = None):
     """Owner: the large-batch bucketed plan over the received ids' exchange view
     (W * cap entries per table, padding skipped) and one update per row from the
     GIVEN gradients -- the slot exchange's fp32 slots (``g_occ``) or the compact
@@ -681,7 +712,7 @@ def owner_apply_large(bank: ShardedEmbeddingBank, recv_ids: torch.Tensor, part: 
     (mrec_emb_bwd_large_fused_given, ABI 25).  Rows hit <= 16 times are summed in
     entry order (= sender rank order, as the hash path), hotter rows in the
     order-free 64-bit fixed point."""
-    F, W, cap = bank.n_tables, bank.world, bank.cap
+    F, W, cap = bank.n_tables, parts or bank.world, bank.cap
     n = W * cap
     mode, lr = _owner_mode(bank, lr, grad)
     ws = _large_ws_for(bank, n)
@@ -719,7 +750,9 @@ def _large_ws_for(bank: ShardedEmbeddingBank, n: int) -> torch.Tensor:
 
 class _CompactInteractFn(torch.autograd.Function):
     """The compact exchange (module docstring): distinct ids out, one record per
-    distinct row back, one summed gradient per distinct row to the owners."""
+    distinct row back, one summed gradient per distinct row to the owners.  A batch
+    past 8192 samples goes out as C chunks (sub-senders): every message has W * C
+    parts, the sender plans and sums each chunk's lookups on their own."""
 
     @staticmethod
     def forward(ctx, dense_w, bias, trigger, bank: ShardedEmbeddingBank, ids, dense, fm2: bool,
@@ -727,36 +760,38 @@ class _CompactInteractFn(torch.autograd.Function):
         B = ids[0].shape[0]
         dev = bank.weight.device
         comm = bank.comm
+        P = bank.parts(B)
         send, pos = shard_bucketize_dedup(bank, ids)
         recv = comm.exchange(send)
         train = trigger is not None
         # the owner's backward plan rides in the gather launch (same received ids);
         # a view past one plan workgroup takes the large path in the backward
-        ojob_ok = train and owner_view_fits_hash(bank)
-        ojob, oplan, okeep = (owner_plan_job(bank, recv, bank.part) if ojob_ok
+        ojob_ok = train and owner_view_fits_hash(bank, P)
+        ojob, oplan, okeep = (owner_plan_job(bank, recv, bank.part, P) if ojob_ok
                               else (None, None, None))
-        pref = (torch.empty(bank.world, bank.n_tables, dtype=torch.int32, device=dev)
+        pref = (torch.empty(P, bank.n_tables, dtype=torch.int32, device=dev)
                 if train else None)
-        wire = comm.exchange(shard_gather_wire(bank, recv, plan_job=ojob, pref=pref))
+        wire = comm.exchange(shard_gather_wire(bank, recv, plan_job=ojob, pref=pref, parts=P))
         del okeep
-        n = bank.world * bank.n_tables * bank.cap
+        n = P * bank.n_tables * bank.cap
         rows_recv = torch.empty(n, bank.row_stride, dtype=bank.weight.dtype, device=dev)
         gsum = torch.empty_like(rows_recv) if train else None
-        shard_wire_unpack(bank, wire, send, rows_recv, zero=gsum)
+        shard_wire_unpack(bank, wire, send, rows_recv, zero=gsum, parts=P)
         fuse = train and B <= _mrec.BWD_HASH_MAX_BATCH
         job, splan, keep = (sender_plan_job(bank, rows_recv, pos) if fuse
                             else (None, None, None))
         x0, logit, fm_sum = shard_interact(bank, rows_recv, pos, dense, dense_w, bias, fm2,
                                            first_order, x0_cols, x0_dtype, plan_job=job)
         del keep
+        splans = [(0, B, splan)] if fuse else None
         if train and not fuse:
-            splan = sender_plan(bank, rows_recv, pos)
-        if train and oplan is None and owner_view_fits_hash(bank):
-            oplan = owner_plan(bank, recv, bank.part)
+            splans = sender_plans(bank, rows_recv, pos)
+        if train and oplan is None and owner_view_fits_hash(bank, P):
+            oplan = owner_plan(bank, recv, bank.part, P)
         if bank.check_ids:
             bank.check_flags()
-        ctx.bank, ctx.B = bank, B
-        ctx.splan, ctx.oplan = splan, oplan
+        ctx.bank, ctx.B, ctx.P = bank, B, P
+        ctx.splans, ctx.oplan = splans, oplan
         ctx.fm2, ctx.first_order = fm2, first_order
         ctx.has_dense_w, ctx.has_bias = dense_w is not None, bias is not None
         ctx.dense_w, ctx.bias = dense_w, bias
@@ -780,15 +815,19 @@ class _CompactInteractFn(torch.autograd.Function):
         dw = dlogit if (ctx.first_order and dlogit is not None) else None
         if dx0 is not None:
             dx0 = dx0.contiguous()
-        if ctx.splan is not None:
-            sender_grad_sums(bank, rows_recv, pos, ctx.splan, gsum, dx=dx0, dfm=dfm,
-                             fm_sum=fm_sum, x0=x0 if dfm is not None else None, dw=dw)
-            wire_g = bank.comm.exchange(shard_wire_pack(bank, gsum, send))
+        if ctx.splans is not None:
+            for s0, n_c, splan in ctx.splans:  # each chunk's lookups (disjoint slots)
+                sl = (lambda t: None if t is None else t[s0:s0 + n_c])  # noqa: E731
+                sender_grad_sums(bank, rows_recv, pos[:, s0:s0 + n_c], splan, gsum, dx=sl(dx0),
+                                 dfm=sl(dfm), fm_sum=sl(fm_sum),
+                                 x0=sl(x0) if dfm is not None else None, dw=sl(dw))
+            wire_g = bank.comm.exchange(shard_wire_pack(bank, gsum, send, parts=ctx.P))
             # the owner reads the gradient records in place (no unpack launch)
             if ctx.oplan is not None:
-                owner_apply_wire(bank, ctx.oplan, wire_g, ctx.pref)
+                owner_apply_wire(bank, ctx.oplan, wire_g, ctx.pref, parts=ctx.P)
             else:
-                owner_apply_large(bank, recv, bank.part, wire_g=wire_g, pref=ctx.pref)
+                owner_apply_large(bank, recv, bank.part, wire_g=wire_g, pref=ctx.pref,
+                                  parts=ctx.P)
         g_dense_w, g_bias = _dense_first_order_grads(ctx, dlogit, dense)
         return g_dense_w, g_bias, None, None, None, None, None, None, None, None
 
@@ -882,44 +921,55 @@ def cpu_bucketize(bank: ShardedEmbeddingBank, ids: Sequence[torch.Tensor]):
 
 
 def cpu_bucketize_dedup(bank: ShardedEmbeddingBank, ids: Sequence[torch.Tensor]):
-    """CPU restatement of mrec_shard_bucketize_dedup: per (owner, table) the
+    """CPU restatement of mrec_shard_bucketize_dedup(_ex): per (owner, table) the
     distinct ids in the order of their first lookup, every lookup's slot, the
-    counts header -> (send [W, F*cap + F] int32, pos [F, B] int32)."""
+    counts header, for each chunk of bank.chunk_batch samples (sub-sender c of owner
+    o's part o * C + c) -> (send [W, C * (F*cap + F)] int32, pos [F, B] int32)."""
     F, W, cap = bank.n_tables, bank.world, bank.cap
     B = ids[0].shape[0]
-    send = torch.full((W, bank.part), -1, dtype=torch.int32)
+    C = bank.chunks(B)
+    send = torch.full((W, C, bank.part), -1, dtype=torch.int32)
     pos = torch.empty(F, B, dtype=torch.int32)
-    ar = torch.arange(B)
-    for f, t in enumerate(ids):
-        t = t.long()
-        if t.numel() and (int(t.min()) < 0 or int(t.max()) >= bank.global_rows[f]):
-            raise IndexError("index out of range in self")
-        owner = t % W
-        uniq, inv = torch.unique(t, return_inverse=True)
-        first = torch.full((uniq.numel(),), B, dtype=torch.long)
-        first.scatter_reduce_(0, inv, ar, reduce="amin")
-        rep = first[inv] == ar
-        slot_u = torch.empty(uniq.numel(), dtype=torch.long)
+    for c in range(C):
+        s0 = c * bank.chunk_batch
+        n = min(bank.chunk_batch, B - s0)
+        ar = torch.arange(n)
+        for f, t in enumerate(ids):
+            t = t[s0:s0 + n].long()
+            if t.numel() and (int(t.min()) < 0 or int(t.max()) >= bank.global_rows[f]):
+                raise IndexError("index out of range in self")
+            owner = t % W
+            uniq, inv = torch.unique(t, return_inverse=True)
+            first = torch.full((uniq.numel(),), n, dtype=torch.long)
+            first.scatter_reduce_(0, inv, ar, reduce="amin")
+            rep = first[inv] == ar
+            slot_u = torch.empty(uniq.numel(), dtype=torch.long)
+            for o in range(W):
+                r = torch.nonzero(rep & (owner == o)).reshape(-1)  # ascending sample order
+                if r.numel() > cap:
+                    raise RuntimeError(f"row-sharded exchange overflow: more than cap={cap} ids "
+                                       "of one table for one owner in a batch; raise cap")
+                slot_u[inv[r]] = torch.arange(r.numel())
+                send[o, c, f * cap:f * cap + r.numel()] = (t[r] // W).to(torch.int32)
+                send[o, c, F * cap + f] = r.numel()
+            pos[f, s0:s0 + n] = (((owner * C + c) * F + f) * cap + slot_u[inv]).to(torch.int32)
         for o in range(W):
-            r = torch.nonzero(rep & (owner == o)).reshape(-1)  # ascending sample order
-            if r.numel() > cap:
-                raise RuntimeError(f"row-sharded exchange overflow: more than cap={cap} ids of "
-                                   "one table for one owner in a batch; raise cap")
-            slot_u[inv[r]] = torch.arange(r.numel())
-            send[o, f * cap:f * cap + r.numel()] = (t[r] // W).to(torch.int32)
-            send[o, F * cap + f] = r.numel()
-        pos[f] = ((owner * F + f) * cap + slot_u[inv]).to(torch.int32)
-    for o in range(W):
-        if int(send[o, F * cap:].sum()) > bank.cap_rows:
-            raise RuntimeError(f"row-sharded exchange overflow: more than cap_rows="
-                               f"{bank.cap_rows} distinct ids for one owner in a batch")
-    return send, pos
+            if int(send[o, c, F * cap:].sum()) > bank.cap_rows:
+                raise RuntimeError(f"row-sharded exchange overflow: more than cap_rows="
+                                   f"{bank.cap_rows} distinct ids for one owner in a batch")
+    return send.reshape(W, C * bank.part), pos
+
+
+def _cpu_slots(bank: ShardedEmbeddingBank, recv: torch.Tensor, compact: bool) -> torch.Tensor:
+    """The slot ids of a received ids message ([parts, F * cap]): the compact message
+    carries the counts behind each part (and W * chunks parts)."""
+    if compact:
+        return recv.reshape(-1, bank.part)[:, :bank.n_tables * bank.cap]
+    return recv
 
 
 def _cpu_owner_rows(bank: ShardedEmbeddingBank, recv: torch.Tensor) -> torch.Tensor:
     F, cap = bank.n_tables, bank.cap
-    if recv.shape[-1] == bank.part:  # the compact ids message: slots, then the counts
-        recv = recv[:, :F * cap]
     flat = recv.reshape(-1).long()
     f_of = (torch.arange(flat.numel()) // cap) % F
     offs = torch.tensor(bank.row_offset, dtype=torch.long)[f_of]
@@ -935,6 +985,7 @@ class _CpuExchangeRowsFn(torch.autograd.Function):
 
     @staticmethod
     def forward(ctx, trigger, bank: ShardedEmbeddingBank, recv):
+        # (recv: the slot ids, [parts, F * cap], _cpu_slots)
         rows, offs, valid = _cpu_owner_rows(bank, recv)
         ctx.bank, ctx.recv, ctx.offs, ctx.valid = bank, recv, offs, valid
         return bank.comm.exchange(rows.float())
@@ -943,10 +994,7 @@ class _CpuExchangeRowsFn(torch.autograd.Function):
     def backward(ctx, g):
         bank = ctx.bank
         g_recv = bank.comm.exchange(g.contiguous())
-        recv = ctx.recv
-        if recv.shape[-1] == bank.part:
-            recv = recv[:, :bank.n_tables * bank.cap]
-        flat = recv.reshape(-1).long()
+        flat = ctx.recv.reshape(-1).long()
         idx = (ctx.offs + flat)[ctx.valid]
         cols = bank.dim + (1 if bank.has_w else 0)
         upd = g_recv[ctx.valid][:, :cols].to(bank.weight.dtype)
@@ -965,9 +1013,9 @@ def cpu_sharded_interact(bank: ShardedEmbeddingBank, ids, dense, dense_w, bias, 
                          first_order: bool, x0_cols: int, x0_dtype):
     from pytorchrec_amd import cpu_path
     B = ids[0].shape[0]
-    send, pos = (cpu_bucketize_dedup(bank, ids) if bank.use_compact(B)
-                 else cpu_bucketize(bank, ids))
-    recv = bank.comm.exchange(send)
+    compact = bank.use_compact(B)
+    send, pos = cpu_bucketize_dedup(bank, ids) if compact else cpu_bucketize(bank, ids)
+    recv = _cpu_slots(bank, bank.comm.exchange(send), compact)
     trig = torch.zeros(0, requires_grad=True) if torch.is_grad_enabled() else None
     rows = _CpuExchangeRowsFn.apply(trig, bank, recv)
     g = [rows.index_select(0, pos[f].long()) for f in range(bank.n_tables)]

@@ -371,7 +371,8 @@ def test_sgd_multi_matches_torch_and_weight_prep(gpu):
 @pytest.mark.parametrize("W,zipf,B,big", [(2, False, 512, False), (4, True, 512, False),
                                           (8, False, 1024, False), (3, True, 4096, False),
                                           (8, True, 4096, False), (2, False, 8192, False),
-                                          (8, True, 4096, True), (4, False, 8192, True)])
+                                          (8, True, 4096, True), (4, False, 8192, True),
+                                          (8, True, 16384, True)])
 def test_compact_exchange_simulated_bit_exact(gpu, W, zipf, B, big):
     """W ranks simulated in one process (all-to-alls by slicing), every stage checked:
       * bucketize_dedup == its CPU restatement (cpu_bucketize_dedup): the distinct
@@ -388,6 +389,10 @@ def test_compact_exchange_simulated_bit_exact(gpu, W, zipf, B, big):
     32,768) exceeds one plan workgroup and the owner takes the large-batch bucketed
     path over the received records / fp32 slots (owner_apply_large, ABI 25): the
     same sums (a row has <= W entries, summed in sender order), bit-exact.
+    B = 16,384 per rank (Zipf, W = 8): each rank's batch goes out as 2 chunks of
+    8,192 (sub-senders: every message has W x 2 parts, mrec_shard_bucketize_dedup_ex);
+    each chunk's slot sums == the dense gradient of that chunk alone, and the owner's
+    sum runs over (rank, chunk) in that order.
     Per-rank bytes on the wire are checked against the slot exchange."""
     from pytorchrec_amd import embedding as E
     from pytorchrec_amd import sharding as S
@@ -396,7 +401,7 @@ def test_compact_exchange_simulated_bit_exact(gpu, W, zipf, B, big):
     for r in range(W):
         b = S.ShardedEmbeddingBank(ROWS, D, S.ShardComm(world=W, rank=r), with_first_order=True,
                                    dtype=torch.bfloat16, max_batch=B, device=gpu,
-                                   cap=B if big else (min(B, 8192 // W) if zipf else None))
+                                   cap=min(B, 8192) if big else (min(B, 8192 // W) if zipf else None))
         b.load_global_(_tables(glob))
         b.stochastic_rounding = False
         assert b.use_compact(B)
@@ -412,14 +417,19 @@ def test_compact_exchange_simulated_bit_exact(gpu, W, zipf, B, big):
         ref_send, ref_pos = S.cpu_bucketize_dedup(banks[r], [t.cpu() for t in ids[r]])
         assert torch.equal(sends[r].cpu(), ref_send) and torch.equal(poss[r].cpu(), ref_pos), r
     recvs = _exchange(list(sends), W)
-    prefs = [torch.empty(W, len(ROWS), dtype=torch.int32, device=gpu) for _ in range(W)]
-    wires = _exchange([S.shard_gather_wire(banks[r], recvs[r], pref=prefs[r]) for r in range(W)], W)
-    n = W * F * banks[0].cap
+    P = banks[0].parts(B)  # W x chunks
+    CB = banks[0].chunk_batch
+    chunks = [(s0, min(CB, B - s0)) for s0 in range(0, B, CB)]
+    assert P == W * len(chunks)
+    prefs = [torch.empty(P, len(ROWS), dtype=torch.int32, device=gpu) for _ in range(W)]
+    wires = _exchange([S.shard_gather_wire(banks[r], recvs[r], pref=prefs[r], parts=P)
+                       for r in range(W)], W)
+    n = P * F * banks[0].cap
     rows, gsums, outs, plans, oplans = [], [], [], [], []
     for r in range(W):
         rr = torch.empty(n, banks[r].row_stride, dtype=torch.bfloat16, device=gpu)
         gs = torch.empty_like(rr)
-        S.shard_wire_unpack(banks[r], wires[r], sends[r], rr, zero=gs)
+        S.shard_wire_unpack(banks[r], wires[r], sends[r], rr, zero=gs, parts=P)
         rows.append(rr)
         gsums.append(gs)
         fuse = B <= 4096
@@ -427,9 +437,9 @@ def test_compact_exchange_simulated_bit_exact(gpu, W, zipf, B, big):
         outs.append(S.shard_interact(banks[r], rr, poss[r], dense[r], dense_w, bias, True, True,
                                      x0_cols, torch.bfloat16, plan_job=job))
         del keep
-        plans.append(sp if fuse else S.sender_plan(banks[r], rr, poss[r]))
-        assert S.owner_view_fits_hash(banks[r]) != big
-        oplans.append(None if big else S.owner_plan(banks[r], recvs[r], banks[r].part))
+        plans.append([(0, B, sp)] if fuse else S.sender_plans(banks[r], rr, poss[r]))
+        assert S.owner_view_fits_hash(banks[r], P) != big
+        oplans.append(None if big else S.owner_plan(banks[r], recvs[r], banks[r].part, P))
     for r in range(W):
         banks[r].check_flags()
         gw = glob.weight
@@ -444,39 +454,46 @@ def test_compact_exchange_simulated_bit_exact(gpu, W, zipf, B, big):
     # ---- backward
     dx0 = [torch.randn(B, x0_cols, device=gpu).to(torch.bfloat16) for _ in range(W)]
     dl = [torch.randn(B, device=gpu) for _ in range(W)]
-    rank_grads = []
+    rank_grads = []  # (rank, chunk) order = the owners' summation order
     for r in range(W):
-        S.sender_grad_sums(banks[r], rows[r], poss[r], plans[r], gsums[r], dx=dx0[r], dfm=dl[r],
-                           fm_sum=outs[r][2], x0=outs[r][0], dw=dl[r])
-        # reference: rank r's dense gradient of the unsharded bank (bf16, same kernels)
-        ref = E.EmbeddingBank(ROWS, D, with_first_order=True, dtype=torch.bfloat16,
-                              update="dense", device=gpu)
-        with torch.no_grad():
-            ref.weight.copy_(glob.weight)
-        gref = E._backward_into_bank(ref, ids[r], B, None, dx=dx0[r], dfm=dl[r],
-                                     fm_sum=outs[r][2], x0=outs[r][0], dw=dl[r])
-        rank_grads.append(gref)
-        for f in range(F):
-            p = poss[r][f].long()
-            want = gref[glob.row_offset[f] + ids[r][f].long(), :D + 1]
-            assert torch.equal(gsums[r][p, :D + 1], want), (r, f)
-    wire_g = _exchange([S.shard_wire_pack(banks[r], gsums[r], sends[r]) for r in range(W)], W)
+        for s0, nc in chunks:
+            sl = (lambda t: t[s0:s0 + nc])  # noqa: E731
+            sp = [p_ for p_ in plans[r] if p_[0] == s0][0][2]
+            S.sender_grad_sums(banks[r], rows[r], poss[r][:, s0:s0 + nc], sp, gsums[r],
+                               dx=sl(dx0[r]), dfm=sl(dl[r]), fm_sum=sl(outs[r][2]),
+                               x0=sl(outs[r][0]), dw=sl(dl[r]))
+            # reference: the chunk's dense gradient of the unsharded bank (bf16, same kernels)
+            ref = E.EmbeddingBank(ROWS, D, with_first_order=True, dtype=torch.bfloat16,
+                                  update="dense", device=gpu)
+            with torch.no_grad():
+                ref.weight.copy_(glob.weight)
+            ids_c = [sl(t) for t in ids[r]]
+            gref = E._backward_into_bank(ref, ids_c, nc, None, dx=sl(dx0[r]), dfm=sl(dl[r]),
+                                         fm_sum=sl(outs[r][2]), x0=sl(outs[r][0]), dw=sl(dl[r]))
+            rank_grads.append(gref)
+            for f in range(F):
+                p = poss[r][f, s0:s0 + nc].long()
+                want = gref[glob.row_offset[f] + ids_c[f].long(), :D + 1]
+                assert torch.equal(gsums[r][p, :D + 1], want), (r, s0, f)
+    wire_g = _exchange([S.shard_wire_pack(banks[r], gsums[r], sends[r], parts=P)
+                        for r in range(W)], W)
     tot = torch.zeros_like(rank_grads[0], dtype=torch.float32)
     for g in rank_grads:  # the owners' order: source rank 0, 1, ...
         tot += g.float()
     for r in range(W):
         g_recv = torch.empty(n, banks[r].g_ld, dtype=torch.float32, device=gpu)
-        S.shard_wire_unpack(banks[r], wire_g[r], recvs[r], g_recv, to_f32=True)
+        S.shard_wire_unpack(banks[r], wire_g[r], recvs[r], g_recv, to_f32=True, parts=P)
         own = torch.zeros_like(banks[r].weight)
         own_w = torch.zeros_like(banks[r].weight)
         if big:  # the large-batch path over the slots, then over the records in place
-            S.owner_apply_large(banks[r], recvs[r], banks[r].part, g_occ=g_recv, grad=own)
+            S.owner_apply_large(banks[r], recvs[r], banks[r].part, g_occ=g_recv, grad=own,
+                                parts=P)
             S.owner_apply_large(banks[r], recvs[r], banks[r].part, wire_g=wire_g[r],
-                                pref=prefs[r], grad=own_w)
+                                pref=prefs[r], grad=own_w, parts=P)
         else:
             S.owner_apply(banks[r], oplans[r], g_recv, grad=own)
             # the same sums read from the received records in place (no unpack)
-            S.owner_apply_wire(banks[r], oplans[r], wire_g[r], prefs[r], grad=own_w)
+            S.owner_apply_wire(banks[r], oplans[r], wire_g[r], prefs[r], grad=own_w, parts=P)
         banks[r].check_flags()
         assert torch.equal(own_w.view(torch.int16), own.view(torch.int16)), r
         for f, (o, cnt) in enumerate(zip(banks[r].row_offset, banks[r].category_nums)):
@@ -487,14 +504,14 @@ def test_compact_exchange_simulated_bit_exact(gpu, W, zipf, B, big):
         before = banks[r].weight.detach().clone()
         if big:
             S.owner_apply_large(banks[r], recvs[r], banks[r].part, wire_g=wire_g[r],
-                                pref=prefs[r], lr=lr)
+                                pref=prefs[r], lr=lr, parts=P)
         else:
-            S.owner_apply_wire(banks[r], oplans[r], wire_g[r], prefs[r], lr)
+            S.owner_apply_wire(banks[r], oplans[r], wire_g[r], prefs[r], lr, parts=P)
         after_wire = banks[r].weight.detach().clone()
         with torch.no_grad():
             banks[r].weight.copy_(before)
         if big:
-            S.owner_apply_large(banks[r], recvs[r], banks[r].part, g_occ=g_recv, lr=lr)
+            S.owner_apply_large(banks[r], recvs[r], banks[r].part, g_occ=g_recv, lr=lr, parts=P)
         else:
             S.owner_apply(banks[r], oplans[r], g_recv, lr)
         banks[r].check_flags()

@@ -59,13 +59,15 @@ def _train(model, batches):
     return [float(model.train_step(b)["loss"].detach()) for b in batches]
 
 
-def _worker(rank, world, port, out_dir, steps):
+def _worker(rank, world, port, out_dir, steps, chunk_batch=None):
     import torch.distributed as dist
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
         from pytorchrec_amd.model import DeepFM
-        from pytorchrec_amd.sharding import ShardComm, sharded_tables
+        from pytorchrec_amd.sharding import ShardComm, ShardedEmbeddingBank, sharded_tables
+        if chunk_batch:  # the batch goes out as chunks (sub-senders) of this many samples
+            ShardedEmbeddingBank.chunk_batch = chunk_batch
         comm = ShardComm()
         ref = _reference_model()  # same init on every rank: the global tables to shard
         sparse, dense, label = _columns()
@@ -103,12 +105,16 @@ def _worker(rank, world, port, out_dir, steps):
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("steps", [2])
-def test_two_rank_sharded_deepfm_matches_single_process(steps):
+@pytest.mark.parametrize("steps,chunk_batch", [(2, None), (2, 12)])
+def test_two_rank_sharded_deepfm_matches_single_process(steps, chunk_batch):
+    """``chunk_batch`` 12: each rank's 32-sample batch goes out as 3 chunks (the
+    compact exchange's sub-senders, as a batch past 8192 samples does on the GPU):
+    an id repeated across chunks is sent once per chunk and summed by its owner."""
     import torch.multiprocessing as mp
     world = 2
     with tempfile.TemporaryDirectory() as d:
-        mp.spawn(_worker, args=(world, _free_port(), d, steps), nprocs=world, join=True)
+        mp.spawn(_worker, args=(world, _free_port(), d, steps, chunk_batch), nprocs=world,
+                 join=True)
         res = [dict(np.load(os.path.join(d, f"rank{r}.npz"))) for r in range(world)]
     ref = _reference_model()
     ref_losses = _train(ref, [_batch(100 + s, B * world) for s in range(steps)])

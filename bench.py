@@ -318,165 +318,34 @@ def time_launches(fn, reps=100):
     return e0.elapsed_time(e1) / reps * 1e-3  # seconds per launch
 
 
-class GraphKernelTimer:
-    """Times chosen kernel launches INSIDE a captured HIP graph.  While a graph is
-    captured (torch.cuda.CUDAGraph(keep_graph=True)), ``begin()`` / ``end(tag)``
-    around a launch remember the capture's tail node before it and the last node it
-    added (hipStreamGetCaptureInfo_v2).  ``arm(graph)`` then splices an event-record
-    node behind each (hipGraphAddEventRecordNode, the outgoing edges rewired
-    through it) before the graph is instantiated; every
-    replay re-records the events, so ``elapsed(i)`` is kernel i's device time in the
-    replayed step.  (torch refuses ``Event(external=True)`` on ROCm, and a plain
-    event recorded during capture becomes a dependency, not a node.)  Uses the HIP
-    runtime torch loaded (ctypes on the same libamdhip64)."""
-    _hip = None
-
-    @classmethod
-    def hip(cls):
-        if cls._hip is None:
-            import ctypes
-            import glob
-            c = ctypes
-            cands = glob.glob(os.path.join(os.path.dirname(torch.__file__), "lib", "libamdhip64.so*"))
-            h = c.CDLL(cands[0] if cands else "libamdhip64.so")
-            vp, sz = c.c_void_p, c.c_size_t
-            h.hipStreamGetCaptureInfo_v2.argtypes = [vp, c.POINTER(c.c_int), c.POINTER(c.c_ulonglong),
-                                                     c.POINTER(vp), c.POINTER(c.POINTER(vp)),
-                                                     c.POINTER(sz)]
-            h.hipGraphNodeGetDependencies.argtypes = [vp, c.POINTER(vp), c.POINTER(sz)]
-            h.hipGraphNodeGetDependentNodes.argtypes = [vp, c.POINTER(vp), c.POINTER(sz)]
-            h.hipGraphRemoveDependencies.argtypes = [vp, c.POINTER(vp), c.POINTER(vp), sz]
-            h.hipGraphAddDependencies.argtypes = [vp, c.POINTER(vp), c.POINTER(vp), sz]
-            h.hipGraphAddEventRecordNode.argtypes = [c.POINTER(vp), vp, c.POINTER(vp), sz, vp]
-            h.hipEventCreateWithFlags.argtypes = [c.POINTER(vp), c.c_uint]
-            h.hipEventElapsedTime.argtypes = [c.POINTER(c.c_float), vp, vp]
-            h.hipEventDestroy.argtypes = [vp]
-            cls._hip = h
-        return cls._hip
-
-    @staticmethod
-    def _ok(rc, what):
-        if rc != 0:
-            raise RuntimeError(f"{what}: hipError {rc}")
-
-    def __init__(self):
-        self.nodes = []   # (tag, node before the span or None, last node of the span)
-        self.events = []  # (ev0, ev1) per span, after arm()
-        self._open = None
-
-    def _tail(self):
-        import ctypes as c
-        h = self.hip()
-        st, cid, graph = c.c_int(), c.c_ulonglong(), c.c_void_p()
-        deps, nd = c.POINTER(c.c_void_p)(), c.c_size_t()
-        self._ok(h.hipStreamGetCaptureInfo_v2(c.c_void_p(torch.cuda.current_stream().cuda_stream),
-                                              c.byref(st), c.byref(cid), c.byref(graph),
-                                              c.byref(deps), c.byref(nd)), "capture info")
-        if st.value != 1 or nd.value > 1:  # an active capture of a linear chain
-            raise RuntimeError(f"GraphKernelTimer: capture status {st.value}, {nd.value} tails")
-        return c.c_void_p(deps[0]) if nd.value else None
-
-    def begin(self):
-        """Call right before the launch(es) to time, on the capturing stream."""
-        self._open = self._tail()
-
-    def end(self, tag):
-        """Call right after them: the span from the first to the last node they added."""
-        last = self._tail()
-        if last is None or (self._open is not None and last.value == self._open.value):
-            raise RuntimeError("GraphKernelTimer: no node was captured for " + tag)
-        self.nodes.append((tag, self._open, last))
-
-    def _edges(self, fn, node):
-        import ctypes as c
-        n = c.c_size_t(0)
-        self._ok(fn(node, None, c.byref(n)), "node edges")
-        arr = (c.c_void_p * max(1, n.value))()
-        self._ok(fn(node, arr, c.byref(n)), "node edges")
-        return [c.c_void_p(arr[i]) for i in range(n.value)]
-
-    def arm(self, graph_handle):
-        """Splice the event nodes into the captured graph (before instantiate): ev0 on
-        every edge leaving the node before the span (or in front of the graph's roots
-        when the span starts the graph), ev1 on every edge leaving its last node."""
-        import ctypes as c
-        h = self.hip()
-        g = c.c_void_p(graph_handle)
-
-        def arr(xs):
-            return (c.c_void_p * max(1, len(xs)))(*[x.value for x in xs])
-
-        def splice_after(node, ev):
-            """event node right behind ``node`` (None: in front of the roots)."""
-            n = c.c_void_p()
-            if node is None:
-                roots = self._roots(g)
-                self._ok(h.hipGraphAddEventRecordNode(c.byref(n), g, None, 0, ev), "event node")
-                for r in roots:
-                    self._ok(h.hipGraphAddDependencies(g, arr([n]), arr([r]), 1), "add dep")
-                return
-            succs = self._edges(h.hipGraphNodeGetDependentNodes, node)
-            for y in succs:
-                self._ok(h.hipGraphRemoveDependencies(g, arr([node]), arr([y]), 1), "rm dep")
-            self._ok(h.hipGraphAddEventRecordNode(c.byref(n), g, arr([node]), 1, ev), "event node")
-            for y in succs:
-                self._ok(h.hipGraphAddDependencies(g, arr([n]), arr([y]), 1), "add dep")
-
-        for _, before, last in self.nodes:
-            evs = []
-            for _ in range(2):
-                e = c.c_void_p()
-                self._ok(h.hipEventCreateWithFlags(c.byref(e), 0), "event create")
-                evs.append(e)
-            splice_after(before, evs[0])
-            splice_after(last, evs[1])
-            self.events.append(tuple(evs))
-
-    def _roots(self, g):
-        import ctypes as c
-        h = self.hip()
-        h.hipGraphGetRootNodes.argtypes = [c.c_void_p, c.POINTER(c.c_void_p), c.POINTER(c.c_size_t)]
-        n = c.c_size_t(0)
-        self._ok(h.hipGraphGetRootNodes(g, None, c.byref(n)), "roots")
-        a = (c.c_void_p * max(1, n.value))()
-        self._ok(h.hipGraphGetRootNodes(g, a, c.byref(n)), "roots")
-        return [c.c_void_p(a[i]) for i in range(n.value)]
-
-    def elapsed(self, i) -> float:
-        """Seconds between kernel i's two event nodes in the last replay."""
-        import ctypes as c
-        ms = c.c_float()
-        self._ok(self.hip().hipEventElapsedTime(c.byref(ms), *self.events[i]), "elapsed")
-        return ms.value * 1e-3
-
-    def close(self):
-        h = self.hip()
-        for e0, e1 in self.events:
-            h.hipEventDestroy(e0)
-            h.hipEventDestroy(e1)
-        self.events = []
-
-
 def instep_kernel_times(step, datas, names, steps=4, replays=30, strip_coreduce=False):
     """Device time of every launch of the named libmrec entry points INSIDE the
     graph-replayed training step: ``steps`` train steps (batch i % len(datas)) are
-    captured in one HIP graph; each such launch gets an event-record node before
-    and after it (GraphKernelTimer); the graph is replayed ``replays`` times.
-    ``strip_coreduce``: the deferred MLP weight-gradient reductions do not ride in
-    the embedding apply (they run as their own launch at the end of the backward)
-    -- the apply's CoReduce share is the difference.  Returns {name: median
-    seconds per launch}."""
+    captured in one HIP graph with the kernel clock on (mrec_kernel_clock: the hot
+    kernels record their first workgroup's start and last wave's end, s_memrealtime
+    at 100 MHz, into the slot each launch took at capture); the graph is replayed
+    ``replays`` times.  (HIP event-record nodes spliced into the graph were tried
+    first: each added 12-14 us to a 10-15 us kernel, so the in-step figure comes
+    from the kernels' own clock.)  ``strip_coreduce``: the deferred MLP
+    weight-gradient reductions do not ride in the embedding apply (they run as their
+    own launch at the end of the backward) -- the apply's CoReduce share is the
+    difference.  Returns {name: median seconds per launch}."""
+    import numpy as np
     from pytorchrec_amd import _mrec, dense as D
-    timer = GraphKernelTimer()
+    lib = _mrec.lib()
+    dev = torch.device("cuda", torch.cuda.current_device())
+    n_slots = 64
+    buf = torch.empty(n_slots, 64, 2, dtype=torch.int64, device=dev)
+    tags = []
     real_call, real_take = _mrec.call, D.take_pending
     capturing = [False]
 
     def spy(name, *a):
-        if not (capturing[0] and name in names):
+        if not capturing[0]:
             return real_call(name, *a)
-        timer.begin()
+        before = int(lib.mrec_kernel_clock_used())
         r = real_call(name, *a)
-        timer.end(name)
+        tags.extend([name] * (int(lib.mrec_kernel_clock_used()) - before))
         return r
 
     _mrec.call = spy
@@ -489,24 +358,31 @@ def instep_kernel_times(step, datas, names, steps=4, replays=30, strip_coreduce=
             for i in range(2):
                 step(datas[i % len(datas)])
         torch.cuda.current_stream().wait_stream(s)
-        g = torch.cuda.CUDAGraph(keep_graph=True)
+        g = torch.cuda.CUDAGraph()
+        lib.mrec_kernel_clock(buf.data_ptr(), n_slots)
         capturing[0] = True
-        with torch.cuda.graph(g, capture_error_mode="thread_local"):
-            for i in range(steps):
-                step(datas[i % len(datas)])
-        capturing[0] = False
+        try:
+            with torch.cuda.graph(g, capture_error_mode="thread_local"):
+                for i in range(steps):
+                    step(datas[i % len(datas)])
+        finally:
+            capturing[0] = False
+            lib.mrec_kernel_clock(None, 0)
     finally:
         _mrec.call, D.take_pending = real_call, real_take
-    timer.arm(g.raw_cuda_graph())
-    g.instantiate()
     times = {n: [] for n in names}
     for _ in range(replays):
+        buf[..., 0].fill_(-1)  # starts: all ones (u64 max)
+        buf[..., 1].zero_()
         g.replay()
         torch.cuda.synchronize()
-        for i, (tag, _, _) in enumerate(timer.nodes):
-            times[tag].append(timer.elapsed(i))
+        u = buf.cpu().numpy().view(np.uint64)
+        for i, tag in enumerate(tags):
+            if tag in times:
+                t0, t1 = u[i, :, 0].min(), u[i, :, 1].max()
+                if t1 > t0 > 0:
+                    times[tag].append(float(t1 - t0) * 1e-8)  # 100 MHz ticks
     g.reset()
-    timer.close()
     out = {}
     for n, ts in times.items():
         if ts:
@@ -551,8 +427,9 @@ def embedding_roofline(model, step, datas, args, in_step=True):
             "frac": round(ach / HBM_PEAK_GBS, 4), "traffic": traffic,
             "avg_us": round(t_pair * 1e6, 3), "bytes_per_launch": nbytes,
             "bytes_rule": "SURVEY.md §8(d) algorithmic bytes per sample x batch",
-            "timing": "in-step: HIP event-record nodes around each launch inside the "
-                      "graph-replayed train steps (median over 4 steps x 30 replays)",
+            "timing": "in-step: the kernels' own clock (mrec_kernel_clock: first workgroup "
+                      "start to last wave end, s_memrealtime) inside the graph-replayed train "
+                      "steps (median over 4 steps x 30 replays)",
             "apply_coreduce_us": round((t[EMB_PAIR[1]] - t_strip[EMB_PAIR[1]]) * 1e6, 3),
             "frac_embedding_only": round(nbytes / t_emb / 1e9 / HBM_PEAK_GBS, 4),
             "traffic_source": tsrc}

@@ -317,6 +317,20 @@ mrec_status mrec_emb_bwd_large_fused(const mrec_table_bank *bank, const mrec_ids
                                      const uint64_t *d_step, void *grad, mrec_stream stream);
 
 /*
+ * Kernel clock (ABI 25, measurement only: bench.py's in-step roofline).  With a
+ * buffer set, every launch of the step's hot kernels -- mrec_interact_fwd_ex,
+ * mrec_emb_bwd_apply(_ex), mrec_tower_fwd_bwd, mrec_tower_dw -- takes the next
+ * slot (in launch order; a HIP graph captured meanwhile keeps its slots) and
+ * records the first workgroup's start and the last wave's end: buf[slot][64][2]
+ * u64 = {min start, max end} of s_memrealtime (100 MHz ticks) per shard (block %
+ * 64).  The caller fills starts with ~0 and ends with 0 before each run, and
+ * reduces min / max over the shards.  NULL turns it off (the default).  Not
+ * thread-safe; host-side counter only.
+ */
+void mrec_kernel_clock(void *buf, int32_t n_slots);
+int32_t mrec_kernel_clock_used(void);
+
+/*
  * Per-lookup gradients GIVEN by the caller instead of computed from dx / dfm (the
  * owner side of the row-sharded exchange).  The lookups are an
  * exchange view (mrec_ids with chunk = the entries per part): entry b of table f

@@ -267,6 +267,8 @@ SIGNATURES = {
     "mrec_emb_bwd_large_workspace_size": (ctypes.c_size_t, [_bank_p, _i64]),
     "mrec_emb_bwd_large_zero_bytes": (ctypes.c_size_t, [_bank_p, _i64]),
     "mrec_emb_bwd_large_error_offset": (ctypes.c_size_t, []),
+    "mrec_kernel_clock": (None, [_vp, _i32]),
+    "mrec_kernel_clock_used": (_i32, []),
     "mrec_emb_bwd_large_plan": (ctypes.c_int, [_bank_p, _ids_p, _i64, _vp, ctypes.c_size_t, _vp,
                                                _vp]),
     "mrec_emb_bwd_large_apply": (ctypes.c_int, [_bank_p, _i64, _vp, ctypes.c_size_t, _vp,

@@ -26,6 +26,32 @@ void set_error(const std::string &msg);
 mrec_status launch_status(const char *what);  // hipGetLastError -> status
 
 // ---------------------------------------------------------------------------
+// Kernel clock (measurement only, mrec_kernel_clock): the step's hot launches
+// (interaction, apply, tower, tower_dw) record their first workgroup's start and
+// every wave's end (s_memrealtime, 100 MHz) into slot `slot` of a caller buffer of
+// [slots][64 shards][2] u64 (min start, max end; shard = block % 64 keeps the
+// atomics off one address).  buf == NULL (the default): one uniform branch.
+// ---------------------------------------------------------------------------
+struct KClock {
+  unsigned long long *buf;
+  int slot;
+};
+KClock kclock_take();  // host: the next slot when the clock is on, else {NULL, 0}
+
+__device__ __forceinline__ void kc_begin(const KClock &kc) {
+  if (kc.buf && threadIdx.x == 0)
+    atomicMin(kc.buf + (static_cast<int64_t>(kc.slot) * 64 + (blockIdx.x & 63)) * 2,
+              static_cast<unsigned long long>(__builtin_amdgcn_s_memrealtime()));
+}
+__device__ __forceinline__ void kc_end(const KClock &kc) {
+  if (kc.buf && (threadIdx.x & 63) == 0) {
+    __builtin_amdgcn_s_waitcnt(0);  // this wave's stores acknowledged
+    atomicMax(kc.buf + (static_cast<int64_t>(kc.slot) * 64 + (blockIdx.x & 63)) * 2 + 1,
+              static_cast<unsigned long long>(__builtin_amdgcn_s_memrealtime()));
+  }
+}
+
+// ---------------------------------------------------------------------------
 // kernel argument blocks (passed by value; <= 4 KiB kernarg segment)
 // ---------------------------------------------------------------------------
 // fused optimizer of the update (mrec_optim); kind = the apply's mode

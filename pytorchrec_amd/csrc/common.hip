@@ -113,9 +113,25 @@ mrec_status make_ids_args(const mrec_ids *ids, int n_tables, IdsArgs *out) {
   return MREC_OK;
 }
 
+static unsigned long long *g_kclock_buf = nullptr;
+static int g_kclock_slots = 0, g_kclock_next = 0;
+
+KClock kclock_take() {
+  if (!g_kclock_buf || g_kclock_next >= g_kclock_slots) return KClock{nullptr, 0};
+  return KClock{g_kclock_buf, g_kclock_next++};
+}
+
 }  // namespace mrec
 
 extern "C" {
+
+void mrec_kernel_clock(void *buf, int32_t n_slots) {
+  mrec::g_kclock_buf = static_cast<unsigned long long *>(buf);
+  mrec::g_kclock_slots = buf ? n_slots : 0;
+  mrec::g_kclock_next = 0;
+}
+
+int32_t mrec_kernel_clock_used(void) { return mrec::g_kclock_next; }
 
 int mrec_abi_version(void) { return MREC_ABI_VERSION; }
 

@@ -80,6 +80,7 @@ struct InteractArgs {
   float *logit;
   float *fm_sum;
   int32_t *oob;
+  KClock kc;  // measurement only (mrec_kernel_clock)
 };
 
 #ifdef MREC_INTERACT_PROF
@@ -277,9 +278,10 @@ __device__ __forceinline__ void interact_sample(const BankArgs &bank, const IdsA
 template <typename T, int LPR, bool X0_BF16, bool ADAM>
 __global__ __launch_bounds__(256) void interact_kernel(BankArgs bank, IdsArgs ids, int64_t B,
                                                        InteractArgs ia) {
+  kc_begin(ia.kc);
   const int64_t b = static_cast<int64_t>(blockIdx.x) * 4 + (threadIdx.x >> 6);
-  if (b >= B) return;
-  interact_sample<T, LPR, X0_BF16, ADAM>(bank, ids, ia, b, threadIdx.x & 63);
+  if (b < B) interact_sample<T, LPR, X0_BF16, ADAM>(bank, ids, ia, b, threadIdx.x & 63);
+  kc_end(ia.kc);
 }
 
 // the interaction (16 samples per 1024-thread workgroup) with the embedding-
@@ -290,14 +292,15 @@ __global__ __launch_bounds__(1024) void interact_plan_kernel(BankArgs bank, IdsA
                                                              InteractArgs ia, PlanJob plan,
                                                              int plan_blocks) {
   __shared__ __attribute__((aligned(16))) uint32_t smem[2 * kHashSlots + 2];
+  kc_begin(ia.kc);
   if (static_cast<int>(blockIdx.x) < plan_blocks) {  // uniform: (table, bucket) plans
     plan_hash_body<1024, kHashSlots>(plan.bank, plan.ids, plan.B, plan.ws, plan.oob, plan.d_step,
                                      blockIdx.x / kPlanBuckets, blockIdx.x % kPlanBuckets, smem);
-    return;
+  } else {
+    const int64_t b = static_cast<int64_t>(blockIdx.x - plan_blocks) * 16 + (threadIdx.x >> 6);
+    if (b < B) interact_sample<T, LPR, X0_BF16, ADAM>(bank, ids, ia, b, threadIdx.x & 63);
   }
-  const int64_t b = static_cast<int64_t>(blockIdx.x - plan_blocks) * 16 + (threadIdx.x >> 6);
-  if (b >= B) return;
-  interact_sample<T, LPR, X0_BF16, ADAM>(bank, ids, ia, b, threadIdx.x & 63);
+  kc_end(ia.kc);
 }
 
 // ---------------------------------------------------------------------------
@@ -368,7 +371,8 @@ static void launch_gather(int lpr, const BankArgs &ba, const IdsArgs &ia, int64_
 
 template <typename T, bool XB>
 static void launch_interact(int lpr, const BankArgs &ba, const IdsArgs &ids, int64_t B,
-                            const InteractArgs &ia, const PlanJob *plan, hipStream_t s) {
+                            InteractArgs ia, const PlanJob *plan, hipStream_t s) {
+  ia.kc = kclock_take();
   const int pb = plan ? plan->bank.n_tables * kPlanBuckets : 0;
   const dim3 grid(static_cast<unsigned>((B + 3) / 4));
   const dim3 grid_p(static_cast<unsigned>(pb + (B + 15) / 16));

@@ -92,6 +92,7 @@ struct TowerArgs {
   uint16_t *x0_img;
   int mode;        // MREC_TOWER_BCE / _FORWARD / _GIVEN_DZ
   const float *dz_in;
+  KClock kc;  // measurement only (mrec_kernel_clock)
 };
 
 
@@ -331,8 +332,7 @@ __device__ __forceinline__ void tower_out(const TowerArgs &a, const char *blk, i
   } while (0)
 
 template <int TW_PF>
-__global__ __launch_bounds__(TW_THREADS) void tower_kernel(TowerArgs a) {
-  extern __shared__ __attribute__((aligned(16))) char lds[];
+__device__ __forceinline__ void tower_body(const TowerArgs &a, char *lds) {
   const int tid = threadIdx.x, lane = tid & 63;
   __shared__ unsigned long long s_stamp[16];
   TW_STAMP(0);
@@ -587,6 +587,14 @@ __global__ __launch_bounds__(TW_THREADS) void tower_kernel(TowerArgs a) {
   }
 }
 
+template <int TW_PF>
+__global__ __launch_bounds__(TW_THREADS) void tower_kernel(TowerArgs a) {
+  extern __shared__ __attribute__((aligned(16))) char lds[];
+  kc_begin(a.kc);
+  tower_body<TW_PF>(a, lds);
+  kc_end(a.kc);
+}
+
 // ---------------------------------------------------------------------------
 // image prep: fp32 W [N, K] -> tower fwd / bwd images (real elements only)
 // ---------------------------------------------------------------------------
@@ -803,6 +811,7 @@ mrec_status mrec_tower_fwd_bwd(const mrec_tower_args *p, mrec_stream stream) {
   hipStream_t st = static_cast<hipStream_t>(stream);
   const int64_t grid = (s.batch + TW_ROWS - 1) / TW_ROWS;
   const dim3 gd(static_cast<unsigned>(grid));
+  a.kc = kclock_take();
   if (pf_env == 8)
     tower_kernel<8><<<gd, TW_THREADS, a.lds_bytes, st>>>(a);
   else if (pf_env == 6)

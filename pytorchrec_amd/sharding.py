@@ -173,7 +173,7 @@ class MrecComm:
 
 
 def default_cap(batch: int, world: int, rows: Optional[Sequence[int]] = None,
-                sigmas: float = 8.0) -> int:
+                sigmas: float = 8.0, dedup: bool = False) -> int:
     """Slots per (owner, table), sized for ids spread uniformly over each table: the
     count of a table's ids owned by one rank is Binomial(batch, p) with p the
     largest owner share of the table's rows (ceil(n / W) / n, 1/W for big tables),
@@ -185,12 +185,27 @@ def default_cap(batch: int, world: int, rows: Optional[Sequence[int]] = None,
     workgroup's MREC_BWD_MAX_BATCH takes the large-batch path (owner_apply_large)."""
     batch, world = int(batch), int(world)
     if world <= 1:
-        cap = batch
-    else:
-        shares = [-(-int(n) // world) / int(n) for n in (rows or []) if int(n) > 0]
+        return max(1, batch)
+    # ``dedup`` (the compact exchange): slots hold DISTINCT ids, so a table's bound is
+    # also its owner's expected distinct rows hit (m = ceil(n / W) owned rows, each
+    # hit with q = 1 - (1 - 1/n)^B: mean m q + 8 sd) and m itself -- a 1-row table
+    # needs one slot, not B
+    ns = [int(n) for n in (rows or []) if int(n) > 0]
+    if not dedup or not ns:
+        shares = [-(-n // world) / n for n in ns]
         p = max(shares + [1.0 / world])
         sd = math.sqrt(batch * p * (1.0 - p))
-        cap = (int(math.ceil(batch * p + sigmas * sd)) + 7) // 8 * 8
+        cap = int(math.ceil(batch * p + sigmas * sd))
+    else:
+        cap = 0
+        for n in ns:
+            m = -(-n // world)
+            p = m / n
+            look = batch * p + sigmas * math.sqrt(batch * p * (1.0 - p))
+            q = -math.expm1(batch * math.log1p(-1.0 / n)) if n > 1 else 1.0
+            dist = m * q + sigmas * math.sqrt(m * q * (1.0 - q))
+            cap = max(cap, int(math.ceil(min(look, dist, m))))
+    cap = (cap + 7) // 8 * 8
     return max(1, min(batch, cap))
 
 
@@ -237,8 +252,13 @@ class ShardedEmbeddingBank(EmbeddingBank):
         self.global_rows = [int(n) for n in category_nums]
         self.comm = comm
         self.world, self.rank = W, r
-        self.cap = (int(cap) if cap is not None  # slots per (owner, table[, chunk])
-                    else default_cap(min(int(max_batch), self.chunk_batch), W, self.global_rows))
+        # slots per (owner, table[, chunk]): distinct ids on the compact exchange,
+        # lookups on the slot exchange (the `compact` setter switches a defaulted cap)
+        mb = min(int(max_batch), self.chunk_batch)
+        self._caps = None if cap is not None else (
+            default_cap(mb, W, self.global_rows, dedup=True), default_cap(mb, W, self.global_rows))
+        self._max_batch = mb
+        self.cap = int(cap) if cap is not None else self._caps[0]
         if self.cap < 1:
             raise ValueError(f"cap = {self.cap} must be >= 1")
         self._flags = None  # device int32 [2] = {overflow, oob}, sticky until checked
@@ -248,9 +268,22 @@ class ShardedEmbeddingBank(EmbeddingBank):
         # world 1 nothing crosses xGMI and the slot
         # path keeps the step bit-identical to the unsharded bank (the compact path
         # rounds each rank's gradient sum of a bf16 row to bf16 on the wire).
-        self.compact = True
-        self.cap_rows = default_cap_rows(min(int(max_batch), self.chunk_batch), W,
-                                         self.global_rows, self.cap)
+        self._compact = True
+        self.cap_rows = default_cap_rows(mb, W, self.global_rows, self.cap)
+
+    @property
+    def compact(self):
+        return self._compact
+
+    @compact.setter
+    def compact(self, value):
+        """True / "always" / False (see __init__); a defaulted cap follows it."""
+        self._compact = value
+        if self._caps is not None:
+            on = value == "always" or (bool(value) and self.world > 1)
+            self.cap = self._caps[0] if on else self._caps[1]
+            self.cap_rows = default_cap_rows(self._max_batch, self.world, self.global_rows,
+                                             self.cap)
 
     @property
     def part(self) -> int:

@@ -438,8 +438,9 @@ def test_compact_exchange_simulated_bit_exact(gpu, W, zipf, B, big):
                                      x0_cols, torch.bfloat16, plan_job=job))
         del keep
         plans.append([(0, B, sp)] if fuse else S.sender_plans(banks[r], rr, poss[r]))
-        assert S.owner_view_fits_hash(banks[r], P) != big
-        oplans.append(None if big else S.owner_plan(banks[r], recvs[r], banks[r].part, P))
+        large = not S.owner_view_fits_hash(banks[r], P)  # W * cap entries past one plan
+        assert large or not big
+        oplans.append(None if large else S.owner_plan(banks[r], recvs[r], banks[r].part, P))
     for r in range(W):
         banks[r].check_flags()
         gw = glob.weight
@@ -485,7 +486,7 @@ def test_compact_exchange_simulated_bit_exact(gpu, W, zipf, B, big):
         S.shard_wire_unpack(banks[r], wire_g[r], recvs[r], g_recv, to_f32=True, parts=P)
         own = torch.zeros_like(banks[r].weight)
         own_w = torch.zeros_like(banks[r].weight)
-        if big:  # the large-batch path over the slots, then over the records in place
+        if oplans[r] is None:  # the large-batch path over the slots, then the records in place
             S.owner_apply_large(banks[r], recvs[r], banks[r].part, g_occ=g_recv, grad=own,
                                 parts=P)
             S.owner_apply_large(banks[r], recvs[r], banks[r].part, wire_g=wire_g[r],
@@ -502,7 +503,7 @@ def test_compact_exchange_simulated_bit_exact(gpu, W, zipf, B, big):
         # fused SGD from the same sums: within one bf16 ulp of w - lr * sum
         lr = 0.5
         before = banks[r].weight.detach().clone()
-        if big:
+        if oplans[r] is None:
             S.owner_apply_large(banks[r], recvs[r], banks[r].part, wire_g=wire_g[r],
                                 pref=prefs[r], lr=lr, parts=P)
         else:
@@ -510,7 +511,7 @@ def test_compact_exchange_simulated_bit_exact(gpu, W, zipf, B, big):
         after_wire = banks[r].weight.detach().clone()
         with torch.no_grad():
             banks[r].weight.copy_(before)
-        if big:
+        if oplans[r] is None:
             S.owner_apply_large(banks[r], recvs[r], banks[r].part, g_occ=g_recv, lr=lr, parts=P)
         else:
             S.owner_apply(banks[r], oplans[r], g_recv, lr)

@@ -321,21 +321,31 @@ def time_launches(fn, reps=100):
 def instep_kernel_times(step, datas, names, steps=4, replays=30, strip_coreduce=False):
     """Device time of every launch of the named libmrec entry points INSIDE the
     graph-replayed training step: ``steps`` train steps (batch i % len(datas)) are
-    captured in one HIP graph with the kernel clock on (mrec_kernel_clock: the hot
-    kernels record their first workgroup's start and last wave's end, s_memrealtime
-    at 100 MHz, into the slot each launch took at capture); the graph is replayed
-    ``replays`` times.  (HIP event-record nodes spliced into the graph were tried
-    first: each added 12-14 us to a 10-15 us kernel, so the in-step figure comes
-    from the kernels' own clock.)  ``strip_coreduce``: the deferred MLP
-    weight-gradient reductions do not ride in the embedding apply (they run as their
-    own launch at the end of the backward) -- the apply's CoReduce share is the
-    difference.  Returns {name: median seconds per launch}."""
+    captured in one HIP graph with the kernel clock on (mrec_kernel_clock: clocked
+    instantiations of the hot kernels whose waves record their start and end,
+    s_memrealtime at 100 MHz, into the slot each launch took at capture); the graph
+    is replayed ``replays`` times.  (HIP event-record nodes spliced into the graph
+    were tried first: each added 12-14 us to a 10-15 us kernel.)
+
+    A launch's in-step time is its first wave's start to the NEXT clocked launch's
+    first wave's start: the graph runs the step's kernels back to back, so this is
+    the launch's share of the step -- dispatch, its waves, and the end-of-kernel
+    cache write-back before the next kernel's waves can start -- which is what
+    rocprof's per-kernel duration inside the replayed graph shows (its kernels
+    abut).  The last launch of the graph has no successor and gives no sample.
+    ``span`` is the waves' own first start to last end (the part the kernel's code
+    controls).  ``strip_coreduce``: the deferred MLP weight-gradient reductions do
+    not ride in the embedding apply (they run as their own launch at the end of
+    the backward) -- the apply's CoReduce share is the difference.
+
+    Returns ({name: median in-step seconds}, {name: median span seconds},
+    median seconds from the first clocked start to the last clocked end / steps)."""
     import numpy as np
     from pytorchrec_amd import _mrec, dense as D
     lib = _mrec.lib()
     dev = torch.device("cuda", torch.cuda.current_device())
     n_slots = 64
-    buf = torch.empty(n_slots, 64, 2, dtype=torch.int64, device=dev)
+    buf = torch.empty(n_slots, 4096, 16, dtype=torch.int64, device=dev)  # mrec.h MREC_KCLOCK_*
     tags = []
     real_call, real_take = _mrec.call, D.take_pending
     capturing = [False]
@@ -370,25 +380,30 @@ def instep_kernel_times(step, datas, names, steps=4, replays=30, strip_coreduce=
             lib.mrec_kernel_clock(None, 0)
     finally:
         _mrec.call, D.take_pending = real_call, real_take
-    times = {n: [] for n in names}
+    share = {n: [] for n in names}
+    span = {n: [] for n in names}
+    whole = []
+    n = len(tags)
     for _ in range(replays):
         buf[..., 0].fill_(-1)  # starts: all ones (u64 max)
         buf[..., 1].zero_()
         g.replay()
         torch.cuda.synchronize()
-        u = buf.cpu().numpy().view(np.uint64)
+        u = buf[:n, :, :2].cpu().numpy().view(np.uint64)
+        t0, t1 = u[:, :, 0].min(axis=1), u[:, :, 1].max(axis=1)
+        if n == 0 or not (t1 > t0).all():
+            continue
+        whole.append(float(t1[-1] - t0[0]) * 1e-8 / steps)
         for i, tag in enumerate(tags):
-            if tag in times:
-                t0, t1 = u[i, :, 0].min(), u[i, :, 1].max()
-                if t1 > t0 > 0:
-                    times[tag].append(float(t1 - t0) * 1e-8)  # 100 MHz ticks
+            if tag in share:
+                span[tag].append(float(t1[i] - t0[i]) * 1e-8)  # 100 MHz ticks
+                if i + 1 < n:
+                    share[tag].append(float(t0[i + 1] - t0[i]) * 1e-8)
     g.reset()
-    out = {}
-    for n, ts in times.items():
-        if ts:
-            ts.sort()
-            out[n] = ts[len(ts) // 2]
-    return out
+
+    def med(d):
+        return {k: sorted(v)[len(v) // 2] for k, v in d.items() if v}
+    return med(share), med(span), (sorted(whole)[len(whole) // 2] if whole else None)
 
 
 EMB_PAIR = ("mrec_interact_fwd_ex", "mrec_emb_bwd_apply_ex")
@@ -415,8 +430,12 @@ def embedding_roofline(model, step, datas, args, in_step=True):
     out = {}
     rk = {}
     if in_step:
-        t = instep_kernel_times(step, datas, EMB_PAIR + TOWER_PAIR)
-        t_strip = instep_kernel_times(step, datas, EMB_PAIR[1:], strip_coreduce=True)
+        t, t_span, clocked_step = instep_kernel_times(step, datas, EMB_PAIR + TOWER_PAIR)
+        # the stripped step runs the reductions as a launch of their own right after the
+        # apply, so the apply's share there is not comparable: the co-reduce's cost is
+        # the difference of the apply's wave spans with and without it
+        span_strip = instep_kernel_times(step, datas, EMB_PAIR[1:], strip_coreduce=True)[1]
+        t_strip = {EMB_PAIR[1]: t[EMB_PAIR[1]] - (t_span[EMB_PAIR[1]] - span_strip[EMB_PAIR[1]])}
         t_pair = t[EMB_PAIR[0]] + t[EMB_PAIR[1]]
         ach = nbytes / t_pair / 1e9
         t_emb = t[EMB_PAIR[0]] + t_strip[EMB_PAIR[1]]
@@ -427,14 +446,17 @@ def embedding_roofline(model, step, datas, args, in_step=True):
             "frac": round(ach / HBM_PEAK_GBS, 4), "traffic": traffic,
             "avg_us": round(t_pair * 1e6, 3), "bytes_per_launch": nbytes,
             "bytes_rule": "SURVEY.md §8(d) algorithmic bytes per sample x batch",
-            "timing": "in-step: the kernels' own clock (mrec_kernel_clock: first workgroup "
-                      "start to last wave end, s_memrealtime) inside the graph-replayed train "
-                      "steps (median over 4 steps x 30 replays)",
+            "timing": "in-step: the kernels' own clock (mrec_kernel_clock, s_memrealtime) "
+                      "inside the graph-replayed train steps, each launch's first wave start "
+                      "to the next launch's (its share of the step, as rocprof's abutting "
+                      "in-graph durations count it); median over 4 steps x 30 replays",
+            "clocked_step_us": round(clocked_step * 1e6, 3) if clocked_step else None,
             "apply_coreduce_us": round((t[EMB_PAIR[1]] - t_strip[EMB_PAIR[1]]) * 1e6, 3),
             "frac_embedding_only": round(nbytes / t_emb / 1e9 / HBM_PEAK_GBS, 4),
             "traffic_source": tsrc}
         for k in EMB_PAIR:
-            rk[k] = {"avg_us": round(t[k] * 1e6, 3), "timing": "in-step"}
+            rk[k] = {"avg_us": round(t[k] * 1e6, 3), "timing": "in-step",
+                     "wave_span_us": round(t_span[k] * 1e6, 3)}
         rk[EMB_PAIR[1]]["avg_us_without_coreduce"] = round(t_strip[EMB_PAIR[1]] * 1e6, 3)
         if args.model == "deepfm":
             lins = [m for m in model.mlp.modules() if isinstance(m, torch.nn.Linear)]
@@ -448,7 +470,7 @@ def embedding_roofline(model, step, datas, args, in_step=True):
                     d = {"avg_us": round(t[name] * 1e6, 3), "flop": fl,
                          "TFLOP/s": round(fl / t[name] / 1e12, 1),
                          "frac_of_mfma_peak": round(fl / t[name] / 1e12 / MFMA_PEAK_TFLOPS, 4),
-                         "timing": "in-step"}
+                         "timing": "in-step", "wave_span_us": round(t_span[name] * 1e6, 3)}
                     if name == TOWER_PAIR[0]:
                         wimg = 2 * 2 * mm  # bf16 forward + transposed images
                         d["weight_bytes_per_workgroup"] = wimg

@@ -318,15 +318,21 @@ mrec_status mrec_emb_bwd_large_fused(const mrec_table_bank *bank, const mrec_ids
 
 /*
  * Kernel clock (ABI 25, measurement only: bench.py's in-step roofline).  With a
- * buffer set, every launch of the step's hot kernels -- mrec_interact_fwd_ex,
- * mrec_emb_bwd_apply(_ex), mrec_tower_fwd_bwd, mrec_tower_dw -- takes the next
- * slot (in launch order; a HIP graph captured meanwhile keeps its slots) and
- * records the first workgroup's start and the last wave's end: buf[slot][64][2]
- * u64 = {min start, max end} of s_memrealtime (100 MHz ticks) per shard (block %
- * 64).  The caller fills starts with ~0 and ends with 0 before each run, and
- * reduces min / max over the shards.  NULL turns it off (the default).  Not
- * thread-safe; host-side counter only.
+ * buffer set, every launch of the step's hot kernels -- mrec_interact_fwd_ex (the
+ * plan-fused launch), mrec_emb_bwd_apply(_ex) (hash layout), mrec_tower_fwd_bwd,
+ * mrec_tower_dw -- takes the next slot (in launch order; a HIP graph captured
+ * meanwhile keeps its slots) and runs a clocked instantiation of its kernel
+ * (the production instantiations carry no clock code).  Every wave records its
+ * start and its end (after its stores are acknowledged) into shard
+ * (global wave index % MREC_KCLOCK_SHARDS) of its slot:
+ * buf[slot][MREC_KCLOCK_SHARDS][MREC_KCLOCK_SHARD_U64] u64, element 0 = min start,
+ * element 1 = max end, s_memrealtime (100 MHz ticks); one 128-B line per shard
+ * keeps the waves' atomics apart.  The caller fills starts with ~0 and ends with
+ * 0 before each run and reduces min / max over the shards.  NULL turns it off
+ * (the default).  Not thread-safe; host-side counter only.
  */
+#define MREC_KCLOCK_SHARDS 4096
+#define MREC_KCLOCK_SHARD_U64 16
 void mrec_kernel_clock(void *buf, int32_t n_slots);
 int32_t mrec_kernel_clock_used(void);
 

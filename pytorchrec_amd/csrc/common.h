@@ -26,11 +26,14 @@ void set_error(const std::string &msg);
 mrec_status launch_status(const char *what);  // hipGetLastError -> status
 
 // ---------------------------------------------------------------------------
-// Kernel clock (measurement only, mrec_kernel_clock): the step's hot launches
-// (interaction, apply, tower, tower_dw) record their first workgroup's start and
-// every wave's end (s_memrealtime, 100 MHz) into slot `slot` of a caller buffer of
-// [slots][64 shards][2] u64 (min start, max end; shard = block % 64 keeps the
-// atomics off one address).  buf == NULL (the default): one uniform branch.
+// Kernel clock (measurement only, mrec_kernel_clock; layout in mrec.h).
+// The clocked kernels are a separate instantiation (template flag KC), launched
+// only while the clock is on: KcScope<false> is empty, so the production kernels
+// compile exactly as they would without it; KcScope<true> reads the clock on entry
+// (a uniform value, kept in scalar registers) and writes both stamps on every
+// return path of the wave, after the wave's own stores are acknowledged, into the
+// wave's own shard line (waves sharing an address serialise their atomics: 64
+// shards per slot cost the 16-wave interaction workgroups ~15 us).
 // ---------------------------------------------------------------------------
 struct KClock {
   unsigned long long *buf;
@@ -38,18 +41,29 @@ struct KClock {
 };
 KClock kclock_take();  // host: the next slot when the clock is on, else {NULL, 0}
 
-__device__ __forceinline__ void kc_begin(const KClock &kc) {
-  if (kc.buf && threadIdx.x == 0)
-    atomicMin(kc.buf + (static_cast<int64_t>(kc.slot) * 64 + (blockIdx.x & 63)) * 2,
-              static_cast<unsigned long long>(__builtin_amdgcn_s_memrealtime()));
-}
-__device__ __forceinline__ void kc_end(const KClock &kc) {
-  if (kc.buf && (threadIdx.x & 63) == 0) {
-    __builtin_amdgcn_s_waitcnt(0);  // this wave's stores acknowledged
-    atomicMax(kc.buf + (static_cast<int64_t>(kc.slot) * 64 + (blockIdx.x & 63)) * 2 + 1,
-              static_cast<unsigned long long>(__builtin_amdgcn_s_memrealtime()));
+template <bool ON>
+struct KcScope {
+  __device__ explicit KcScope(const KClock &) {}
+};
+template <>
+struct KcScope<true> {
+  KClock kc;
+  unsigned long long t0;
+  __device__ explicit KcScope(const KClock &k) : kc(k), t0(__builtin_amdgcn_s_memrealtime()) {}
+  __device__ ~KcScope() {
+    if ((threadIdx.x & 63) == 0) {
+#ifndef MREC_KC_NOWAIT  // (diagnostic: stamp at the last issue, not the last acknowledgement)
+      __builtin_amdgcn_s_waitcnt(0);
+#endif
+      const unsigned wave = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
+      unsigned long long *p =
+          kc.buf + (static_cast<int64_t>(kc.slot) * MREC_KCLOCK_SHARDS + (wave % MREC_KCLOCK_SHARDS)) *
+                       MREC_KCLOCK_SHARD_U64;
+      atomicMin(p, t0);
+      atomicMax(p + 1, static_cast<unsigned long long>(__builtin_amdgcn_s_memrealtime()));
+    }
   }
-}
+};
 
 // ---------------------------------------------------------------------------
 // kernel argument blocks (passed by value; <= 4 KiB kernarg segment)

@@ -38,7 +38,6 @@ struct ApplyArgs {
   int64_t g_cap_rows;
   int g_F;
   OptArgs opt;
-  KClock kc;  // measurement only (mrec_kernel_clock)
 };
 
 // a given gradient from a wire record (4-B aligned rows: records are not 16-B).

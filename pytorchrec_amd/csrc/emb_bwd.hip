@@ -434,10 +434,12 @@ __device__ __forceinline__ void apply_segment(const BankArgs &bank, const ApplyA
   row_update<T, LPR, MODE>(bank, a, grow, e0, v_lane, w_lane, live, acc, raw);
 }
 
-template <typename T, int LPR, int MODE>
-__device__ __forceinline__ void apply_hash_body(const BankArgs &bank, int64_t B, const void *ws,
-                                                ApplyArgs a, int seg_blocks, int sm_blocks,
-                                                const CoReduce &co) {
+template <typename T, int LPR, int MODE, bool KC>
+__global__ __launch_bounds__(256, MREC_APPLY_WAVES) void apply_hash_kernel(BankArgs bank, int64_t B,
+                                                                           const void *ws, ApplyArgs a,
+                                                                           int seg_blocks, int sm_blocks,
+                                                                           CoReduce co, KClock kc) {
+  KcScope<KC> kc_scope(kc);
   // the co-launched reductions take the leading workgroups: independent of the
   // embedding update, they start first instead of trailing it
 #if MREC_APPLY_EXP == 13  // (diagnostic: reductions trailing the apply blocks)
@@ -584,16 +586,6 @@ __device__ __forceinline__ void apply_hash_body(const BankArgs &bank, int64_t B,
   return;
 #endif
   row_update<T, LPR, MODE>(bank, a, grow, e0, v_lane, w_lane, live, acc, raw);
-}
-
-template <typename T, int LPR, int MODE>
-__global__ __launch_bounds__(256, MREC_APPLY_WAVES) void apply_hash_kernel(BankArgs bank, int64_t B,
-                                                                           const void *ws, ApplyArgs a,
-                                                                           int seg_blocks, int sm_blocks,
-                                                                           CoReduce co) {
-  kc_begin(a.kc);
-  apply_hash_body<T, LPR, MODE>(bank, B, ws, a, seg_blocks, sm_blocks, co);
-  kc_end(a.kc);
 }
 
 // ---------------------------------------------------------------------------
@@ -987,10 +979,17 @@ static mrec_status apply_impl(const mrec_table_bank *bank, int64_t batch, const 
   if (mrec_status st = build_co_reduce(n_reduce, reduce, &co, &co_blocks); st != MREC_OK)
     return st;
   if (apply_blocks + co_blocks == 0) return MREC_OK;  // (batch 0 still runs the reductions)
-  if (hash) a.kc = kclock_take();
   const dim3 grid(static_cast<unsigned>(apply_blocks + co_blocks));
-#define MREC_AKM(T, L, M) \
-  apply_hash_kernel<T, L, M><<<grid, 256, 0, s>>>(ba, batch, workspace, a, seg_blocks, static_cast<int>(sm_blocks), co)
+  const KClock kc = hash ? kclock_take() : KClock{nullptr, 0};
+#define MREC_AKM(T, L, M)                                                                         \
+  do {                                                                                            \
+    if (kc.buf)                                                                                   \
+      apply_hash_kernel<T, L, M, true><<<grid, 256, 0, s>>>(ba, batch, workspace, a, seg_blocks,  \
+                                                            static_cast<int>(sm_blocks), co, kc); \
+    else                                                                                          \
+      apply_hash_kernel<T, L, M, false><<<grid, 256, 0, s>>>(ba, batch, workspace, a, seg_blocks, \
+                                                             static_cast<int>(sm_blocks), co, kc); \
+  } while (0)
 #define MREC_AK(T, L)                                                                            \
   do {                                                                                           \
     if (hash) {                                                                                  \

@@ -80,7 +80,6 @@ struct InteractArgs {
   float *logit;
   float *fm_sum;
   int32_t *oob;
-  KClock kc;  // measurement only (mrec_kernel_clock)
 };
 
 #ifdef MREC_INTERACT_PROF
@@ -278,29 +277,28 @@ __device__ __forceinline__ void interact_sample(const BankArgs &bank, const IdsA
 template <typename T, int LPR, bool X0_BF16, bool ADAM>
 __global__ __launch_bounds__(256) void interact_kernel(BankArgs bank, IdsArgs ids, int64_t B,
                                                        InteractArgs ia) {
-  kc_begin(ia.kc);
   const int64_t b = static_cast<int64_t>(blockIdx.x) * 4 + (threadIdx.x >> 6);
-  if (b < B) interact_sample<T, LPR, X0_BF16, ADAM>(bank, ids, ia, b, threadIdx.x & 63);
-  kc_end(ia.kc);
+  if (b >= B) return;
+  interact_sample<T, LPR, X0_BF16, ADAM>(bank, ids, ia, b, threadIdx.x & 63);
 }
 
 // the interaction (16 samples per 1024-thread workgroup) with the embedding-
 // backward hash plan in the leading workgroups: a HIP graph runs the step's
 // kernels one after another, so the plan would otherwise cost a kernel of its own
-template <typename T, int LPR, bool X0_BF16, bool ADAM>
+template <typename T, int LPR, bool X0_BF16, bool ADAM, bool KC>
 __global__ __launch_bounds__(1024) void interact_plan_kernel(BankArgs bank, IdsArgs ids, int64_t B,
                                                              InteractArgs ia, PlanJob plan,
-                                                             int plan_blocks) {
+                                                             int plan_blocks, KClock kc) {
   __shared__ __attribute__((aligned(16))) uint32_t smem[2 * kHashSlots + 2];
-  kc_begin(ia.kc);
+  KcScope<KC> kc_scope(kc);
   if (static_cast<int>(blockIdx.x) < plan_blocks) {  // uniform: (table, bucket) plans
     plan_hash_body<1024, kHashSlots>(plan.bank, plan.ids, plan.B, plan.ws, plan.oob, plan.d_step,
                                      blockIdx.x / kPlanBuckets, blockIdx.x % kPlanBuckets, smem);
-  } else {
-    const int64_t b = static_cast<int64_t>(blockIdx.x - plan_blocks) * 16 + (threadIdx.x >> 6);
-    if (b < B) interact_sample<T, LPR, X0_BF16, ADAM>(bank, ids, ia, b, threadIdx.x & 63);
+    return;
   }
-  kc_end(ia.kc);
+  const int64_t b = static_cast<int64_t>(blockIdx.x - plan_blocks) * 16 + (threadIdx.x >> 6);
+  if (b >= B) return;
+  interact_sample<T, LPR, X0_BF16, ADAM>(bank, ids, ia, b, threadIdx.x & 63);
 }
 
 // ---------------------------------------------------------------------------
@@ -371,15 +369,19 @@ static void launch_gather(int lpr, const BankArgs &ba, const IdsArgs &ia, int64_
 
 template <typename T, bool XB>
 static void launch_interact(int lpr, const BankArgs &ba, const IdsArgs &ids, int64_t B,
-                            InteractArgs ia, const PlanJob *plan, hipStream_t s) {
-  ia.kc = kclock_take();
+                            const InteractArgs &ia, const PlanJob *plan, hipStream_t s) {
   const int pb = plan ? plan->bank.n_tables * kPlanBuckets : 0;
   const dim3 grid(static_cast<unsigned>((B + 3) / 4));
   const dim3 grid_p(static_cast<unsigned>(pb + (B + 15) / 16));
+  const KClock kc = plan ? kclock_take() : KClock{nullptr, 0};  // (the fused step's launch)
 #define MREC_IKA(L, A)                                                                      \
   do {                                                                                      \
-    if (plan)                                                                               \
-      interact_plan_kernel<T, L, XB, A><<<grid_p, 1024, 0, s>>>(ba, ids, B, ia, *plan, pb); \
+    if (plan && kc.buf)                                                                     \
+      interact_plan_kernel<T, L, XB, A, true><<<grid_p, 1024, 0, s>>>(ba, ids, B, ia, *plan, \
+                                                                      pb, kc);              \
+    else if (plan)                                                                          \
+      interact_plan_kernel<T, L, XB, A, false><<<grid_p, 1024, 0, s>>>(ba, ids, B, ia,      \
+                                                                       *plan, pb, kc);      \
     else                                                                                    \
       interact_kernel<T, L, XB, A><<<grid, 256, 0, s>>>(ba, ids, B, ia);                    \
   } while (0)

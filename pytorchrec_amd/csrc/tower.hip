@@ -92,7 +92,6 @@ struct TowerArgs {
   uint16_t *x0_img;
   int mode;        // MREC_TOWER_BCE / _FORWARD / _GIVEN_DZ
   const float *dz_in;
-  KClock kc;  // measurement only (mrec_kernel_clock)
 };
 
 
@@ -331,8 +330,10 @@ __device__ __forceinline__ void tower_out(const TowerArgs &a, const char *blk, i
     if (a.stamps && tid == 0) s_stamp[(k)] = wall_clock64();                         \
   } while (0)
 
-template <int TW_PF>
-__device__ __forceinline__ void tower_body(const TowerArgs &a, char *lds) {
+template <int TW_PF, bool KC>
+__global__ __launch_bounds__(TW_THREADS) void tower_kernel(TowerArgs a, KClock kc) {
+  KcScope<KC> kc_scope(kc);
+  extern __shared__ __attribute__((aligned(16))) char lds[];
   const int tid = threadIdx.x, lane = tid & 63;
   __shared__ unsigned long long s_stamp[16];
   TW_STAMP(0);
@@ -587,14 +588,6 @@ __device__ __forceinline__ void tower_body(const TowerArgs &a, char *lds) {
   }
 }
 
-template <int TW_PF>
-__global__ __launch_bounds__(TW_THREADS) void tower_kernel(TowerArgs a) {
-  extern __shared__ __attribute__((aligned(16))) char lds[];
-  kc_begin(a.kc);
-  tower_body<TW_PF>(a, lds);
-  kc_end(a.kc);
-}
-
 // ---------------------------------------------------------------------------
 // image prep: fp32 W [N, K] -> tower fwd / bwd images (real elements only)
 // ---------------------------------------------------------------------------
@@ -795,9 +788,10 @@ mrec_status mrec_tower_fwd_bwd(const mrec_tower_args *p, mrec_stream stream) {
   constexpr int kMaxDyn = 160 * 1024 - 256;  // the kernel's static LDS (s_last) is on top
   MREC_CHECK_ARG(a.lds_bytes <= kMaxDyn, "activation blocks exceed the 160 KiB LDS");
   static int attr_set = [] {
-    for (const void *k : {reinterpret_cast<const void *>(tower_kernel<4>),
-                          reinterpret_cast<const void *>(tower_kernel<6>),
-                          reinterpret_cast<const void *>(tower_kernel<8>)})
+    for (const void *k : {reinterpret_cast<const void *>(tower_kernel<4, false>),
+                          reinterpret_cast<const void *>(tower_kernel<6, false>),
+                          reinterpret_cast<const void *>(tower_kernel<8, false>),
+                          reinterpret_cast<const void *>(tower_kernel<TW_PF_DEFAULT, true>)})
       (void)hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, kMaxDyn);
     (void)hipGetLastError();  // a refused attribute must not read as a failed launch
     return 1;
@@ -811,13 +805,15 @@ mrec_status mrec_tower_fwd_bwd(const mrec_tower_args *p, mrec_stream stream) {
   hipStream_t st = static_cast<hipStream_t>(stream);
   const int64_t grid = (s.batch + TW_ROWS - 1) / TW_ROWS;
   const dim3 gd(static_cast<unsigned>(grid));
-  a.kc = kclock_take();
-  if (pf_env == 8)
-    tower_kernel<8><<<gd, TW_THREADS, a.lds_bytes, st>>>(a);
+  const KClock kc = kclock_take();
+  if (kc.buf)  // (the clocked instantiation is the default prefetch depth's)
+    tower_kernel<TW_PF_DEFAULT, true><<<gd, TW_THREADS, a.lds_bytes, st>>>(a, kc);
+  else if (pf_env == 8)
+    tower_kernel<8, false><<<gd, TW_THREADS, a.lds_bytes, st>>>(a, kc);
   else if (pf_env == 6)
-    tower_kernel<6><<<gd, TW_THREADS, a.lds_bytes, st>>>(a);
+    tower_kernel<6, false><<<gd, TW_THREADS, a.lds_bytes, st>>>(a, kc);
   else
-    tower_kernel<4><<<gd, TW_THREADS, a.lds_bytes, st>>>(a);
+    tower_kernel<4, false><<<gd, TW_THREADS, a.lds_bytes, st>>>(a, kc);
   return launch_status("mrec_tower_fwd_bwd");
 }
 

@@ -61,12 +61,12 @@ struct DwArgs {
   DwLayer lay[DW_MAXL];
   int fin_blocks;
   HeadFinishArgs fin;
-  KClock kc;  // measurement only (mrec_kernel_clock)
 };
 
 // One wave per workgroup, one 64 x 64 output tile (4 x 4 MFMA tiles) per wave.
-template <int PF>
-__device__ __forceinline__ void tower_dw_body(const DwArgs &a) {
+template <int PF, bool KC>
+__global__ __launch_bounds__(64) void tower_dw_kernel(DwArgs a, KClock kc) {
+  KcScope<KC> kc_scope(kc);
   __shared__ __attribute__((aligned(16))) float tile[64 * 68];  // epilogue transpose
   if (static_cast<int>(blockIdx.x) < a.fin_blocks) {  // uniform
     if (static_cast<int>(blockIdx.x) < head_finish_blocks(a.fin.H, a.fin.ns))
@@ -184,13 +184,6 @@ __device__ __forceinline__ void tower_dw_body(const DwArgs &a) {
   }
 }
 
-template <int PF>
-__global__ __launch_bounds__(64) void tower_dw_kernel(DwArgs a) {
-  kc_begin(a.kc);
-  tower_dw_body<PF>(a);
-  kc_end(a.kc);
-}
-
 // row-major bf16 [rows, cols] (row stride ld) -> k-fragment image (pad rows /
 // columns zero); one thread per 16-B lane slot of the image
 __global__ __launch_bounds__(256) void kfrag_pack_kernel(const uint16_t *__restrict__ x, int64_t rows,
@@ -283,9 +276,13 @@ mrec_status mrec_tower_dw(const mrec_tower_dw_args *p, const mrec_head_finish_jo
   }
   const int grid = a.fin_blocks + blocks;
   if (grid == 0) return MREC_OK;
-  a.kc = kclock_take();
-  tower_dw_kernel<DW_PF><<<dim3(static_cast<unsigned>(grid)), 64, 0,
-                           static_cast<hipStream_t>(stream)>>>(a);
+  const KClock kc = kclock_take();
+  if (kc.buf)
+    tower_dw_kernel<DW_PF, true><<<dim3(static_cast<unsigned>(grid)), 64, 0,
+                                   static_cast<hipStream_t>(stream)>>>(a, kc);
+  else
+    tower_dw_kernel<DW_PF, false><<<dim3(static_cast<unsigned>(grid)), 64, 0,
+                                    static_cast<hipStream_t>(stream)>>>(a, kc);
   return launch_status("mrec_tower_dw");
 }
 

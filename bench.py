@@ -334,7 +334,9 @@ def instep_kernel_times(step, datas, names, steps=4, replays=30, strip_coreduce=
     rocprof's per-kernel duration inside the replayed graph shows (its kernels
     abut).  The last launch of the graph has no successor and gives no sample.
     ``span`` is the waves' own first start to last end (the part the kernel's code
-    controls).  ``strip_coreduce``: the deferred MLP weight-gradient reductions do
+    controls); a launch whose next libmrec call is not a clocked launch (work the
+    clock does not see follows it) reports its span as its in-step time.
+    ``strip_coreduce``: the deferred MLP weight-gradient reductions do
     not ride in the embedding apply (they run as their own launch at the end of
     the backward) -- the apply's CoReduce share is the difference.
 
@@ -346,7 +348,8 @@ def instep_kernel_times(step, datas, names, steps=4, replays=30, strip_coreduce=
     dev = torch.device("cuda", torch.cuda.current_device())
     n_slots = 64
     buf = torch.empty(n_slots, 4096, 16, dtype=torch.int64, device=dev)  # mrec.h MREC_KCLOCK_*
-    tags = []
+    tags, at_call = [], []  # per clock slot: entry point, index of the libmrec call
+    calls = [0]
     real_call, real_take = _mrec.call, D.take_pending
     capturing = [False]
 
@@ -355,7 +358,10 @@ def instep_kernel_times(step, datas, names, steps=4, replays=30, strip_coreduce=
             return real_call(name, *a)
         before = int(lib.mrec_kernel_clock_used())
         r = real_call(name, *a)
-        tags.extend([name] * (int(lib.mrec_kernel_clock_used()) - before))
+        k = int(lib.mrec_kernel_clock_used()) - before
+        tags.extend([name] * k)
+        at_call.extend([calls[0]] * k)
+        calls[0] += 1
         return r
 
     _mrec.call = spy
@@ -382,6 +388,7 @@ def instep_kernel_times(step, datas, names, steps=4, replays=30, strip_coreduce=
         _mrec.call, D.take_pending = real_call, real_take
     share = {n: [] for n in names}
     span = {n: [] for n in names}
+    unclocked = set()
     whole = []
     n = len(tags)
     for _ in range(replays):
@@ -395,18 +402,34 @@ def instep_kernel_times(step, datas, names, steps=4, replays=30, strip_coreduce=
             continue
         whole.append(float(t1[-1] - t0[0]) * 1e-8 / steps)
         for i, tag in enumerate(tags):
+            if CAT_SPANS is not None and tag == EMB_PAIR[1]:  # (diagnostic build, MREC_KC_CAT)
+                for c in range(4):
+                    cs, ce = u[i, c * 1024:(c + 1) * 1024, 0].min(), u[i, c * 1024:(c + 1) * 1024, 1].max()
+                    if ce > cs:
+                        CAT_SPANS.setdefault(c, []).append(
+                            (float(cs - t0[i]) * 1e-8, float(ce - t0[i]) * 1e-8))
             if tag in share:
                 span[tag].append(float(t1[i] - t0[i]) * 1e-8)  # 100 MHz ticks
-                if i + 1 < n:
+                # the share needs the next clocked launch to be the next libmrec call
+                # (DCN-v2's cross layers run between its interaction and tower)
+                if i + 1 < n and at_call[i + 1] == at_call[i] + 1:
                     share[tag].append(float(t0[i + 1] - t0[i]) * 1e-8)
+                elif i + 1 < n:
+                    unclocked.add(tag)
     g.reset()
 
     def med(d):
         return {k: sorted(v)[len(v) // 2] for k, v in d.items() if v}
-    return med(share), med(span), (sorted(whole)[len(whole) // 2] if whole else None)
+    ms, mp = med(share), med(span)
+    for k in unclocked:  # a launch followed by unclocked work: its own waves only
+        ms[k] = mp[k]
+    return ms, mp, (sorted(whole)[len(whole) // 2] if whole else None)
 
 
 EMB_PAIR = ("mrec_interact_fwd_ex", "mrec_emb_bwd_apply_ex")
+# MREC_BENCH_KC_CAT=1 with a library built with -DMREC_KC_CAT: the apply's block kinds
+# (co-reduce, segment, hot-segment, single-lookup blocks) clocked apart
+CAT_SPANS = {} if os.environ.get("MREC_BENCH_KC_CAT") == "1" else None
 TOWER_PAIR = ("mrec_tower_fwd_bwd", "mrec_tower_dw")
 
 
@@ -458,6 +481,12 @@ def embedding_roofline(model, step, datas, args, in_step=True):
             rk[k] = {"avg_us": round(t[k] * 1e6, 3), "timing": "in-step",
                      "wave_span_us": round(t_span[k] * 1e6, 3)}
         rk[EMB_PAIR[1]]["avg_us_without_coreduce"] = round(t_strip[EMB_PAIR[1]] * 1e6, 3)
+        if CAT_SPANS:
+            rk[EMB_PAIR[1]]["block_kinds_us"] = {
+                ("co_reduce", "segments", "hot", "singles")[c]: [
+                    round(sorted(x[0] for x in v)[len(v) // 2] * 1e6, 2),
+                    round(sorted(x[1] for x in v)[len(v) // 2] * 1e6, 2)]
+                for c, v in sorted(CAT_SPANS.items())}
         if args.model == "deepfm":
             lins = [m for m in model.mlp.modules() if isinstance(m, torch.nn.Linear)]
             widths = [lins[0].in_features] + [m.out_features for m in lins]

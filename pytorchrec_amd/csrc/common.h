@@ -44,21 +44,24 @@ KClock kclock_take();  // host: the next slot when the clock is on, else {NULL, 
 template <bool ON>
 struct KcScope {
   __device__ explicit KcScope(const KClock &) {}
+  __device__ KcScope(const KClock &, int) {}
 };
 template <>
 struct KcScope<true> {
   KClock kc;
   unsigned long long t0;
+  int cat = -1;  // (diagnostic builds: a block category owns shards [cat * 1024, + 1024))
   __device__ explicit KcScope(const KClock &k) : kc(k), t0(__builtin_amdgcn_s_memrealtime()) {}
+  __device__ KcScope(const KClock &k, int c) : kc(k), t0(__builtin_amdgcn_s_memrealtime()), cat(c) {}
   __device__ ~KcScope() {
     if ((threadIdx.x & 63) == 0) {
 #ifndef MREC_KC_NOWAIT  // (diagnostic: stamp at the last issue, not the last acknowledgement)
       __builtin_amdgcn_s_waitcnt(0);
 #endif
       const unsigned wave = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
+      const unsigned shard = cat < 0 ? wave % MREC_KCLOCK_SHARDS : cat * 1024 + (wave & 1023);
       unsigned long long *p =
-          kc.buf + (static_cast<int64_t>(kc.slot) * MREC_KCLOCK_SHARDS + (wave % MREC_KCLOCK_SHARDS)) *
-                       MREC_KCLOCK_SHARD_U64;
+          kc.buf + (static_cast<int64_t>(kc.slot) * MREC_KCLOCK_SHARDS + shard) * MREC_KCLOCK_SHARD_U64;
       atomicMin(p, t0);
       atomicMax(p + 1, static_cast<unsigned long long>(__builtin_amdgcn_s_memrealtime()));
     }

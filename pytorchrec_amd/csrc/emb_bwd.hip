@@ -23,7 +23,7 @@
 namespace mrec {
 
 #ifndef MREC_APPLY_EXP
-#define MREC_APPLY_EXP 0  // microbenchmark variants (tools/bench_apply.py); 0 = product
+#define MREC_APPLY_EXP 0  // microbenchmark variants (tools/bench_apply.py, tools/r4_apply_exp.sh); 0 = product
 #endif
 
 constexpr int kMaxPlanKeys = 8192;
@@ -360,7 +360,10 @@ struct HotSeg {
 #ifndef MREC_APPLY_WAVES
 #define MREC_APPLY_WAVES 6  // waves per SIMD: every sample-major block of C2 resident at once
 #endif
-constexpr int kSegBatch = 1;  // gradient loads in flight per segment step
+#ifndef MREC_SEG_BATCH
+#define MREC_SEG_BATCH 1
+#endif
+constexpr int kSegBatch = MREC_SEG_BATCH;  // gradient loads in flight per segment step
 
 template <typename T, int LPR, int MODE>
 __device__ __forceinline__ void apply_segment(const BankArgs &bank, const ApplyArgs &a,
@@ -439,7 +442,12 @@ __global__ __launch_bounds__(256, MREC_APPLY_WAVES) void apply_hash_kernel(BankA
                                                                            const void *ws, ApplyArgs a,
                                                                            int seg_blocks, int sm_blocks,
                                                                            CoReduce co, KClock kc) {
+#ifdef MREC_KC_CAT  // (diagnostic: clock shards per block kind: co-reduce, segments, hot, singles)
+  const int cb_ = co.start[co.n], bb_ = static_cast<int>(blockIdx.x) - cb_;
+  KcScope<KC> kc_scope(kc, bb_ < 0 ? 0 : bb_ < seg_blocks ? 1 : bb_ < seg_blocks * (1 + kHotPer) ? 2 : 3);
+#else
   KcScope<KC> kc_scope(kc);
+#endif
   // the co-launched reductions take the leading workgroups: independent of the
   // embedding update, they start first instead of trailing it
 #if MREC_APPLY_EXP == 13  // (diagnostic: reductions trailing the apply blocks)
@@ -472,7 +480,7 @@ __global__ __launch_bounds__(256, MREC_APPLY_WAVES) void apply_hash_kernel(BankA
   const int64_t *__restrict__ toff = table_offsets(ws, F, B);
 
   if (blk < seg_blocks) {  // uniform: the repeated rows of one (table, bucket)
-#if MREC_APPLY_EXP == 8
+#if MREC_APPLY_EXP == 8 || MREC_APPLY_EXP == 14
     return;
 #endif
     const int f = blk / kPlanBuckets, r = blk - f * kPlanBuckets;
@@ -492,7 +500,7 @@ __global__ __launch_bounds__(256, MREC_APPLY_WAVES) void apply_hash_kernel(BankA
     return;
   }
   if (blk < seg_blocks * (1 + kHotPer)) {  // uniform: hot segments k = h, h + kHotPer, ...
-#if MREC_APPLY_EXP == 10
+#if MREC_APPLY_EXP == 10 || MREC_APPLY_EXP == 14
     return;
 #endif
     const int q = blk - seg_blocks;
@@ -523,6 +531,9 @@ __global__ __launch_bounds__(256, MREC_APPLY_WAVES) void apply_hash_kernel(BankA
   }
 
   // a row hit once: one lookup, one update
+#if MREC_APPLY_EXP == 15
+  return;
+#endif
   const int64_t q = static_cast<int64_t>(blk - seg_blocks * (1 + kHotPer)) * WPB + worker;
   if (q >= B * F) return;  // whole workers
   const bool rowwise = MODE < 0 && a.mode == MREC_BWD_ROWWISE_ADAGRAD;

@@ -22,6 +22,7 @@ import datetime
 import glob
 import json
 import os
+import re
 import subprocess
 import sys
 
@@ -34,11 +35,16 @@ KERNELS = {"din_att_bwd": "mrec_din_att_bwd", "din_att_fwd": "mrec_din_att_fwd",
            "gather_kernel": "mrec_emb_gather_fwd"}
 
 
+# the kernel clock's instantiations (template flag KC = true, the last template
+# argument) run only in bench.py's in-step timing graphs: not the product kernels
+_CLOCKED = re.compile(r"(interact_plan_kernel|apply_hash_kernel|tower_kernel|tower_dw_kernel)<[^()]*true>\(")
+
+
 def per_kernel(d, counter):
     f = glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True)[0]
     agg = collections.defaultdict(list)
     for r in csv.DictReader(open(f)):
-        if r["Counter_Name"] != counter:
+        if r["Counter_Name"] != counter or _CLOCKED.search(r["Kernel_Name"]):
             continue
         for k, v in KERNELS.items():
             if k in r["Kernel_Name"]:

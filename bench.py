@@ -404,10 +404,18 @@ def instep_kernel_times(step, datas, names, steps=4, replays=30, strip_coreduce=
         for i, tag in enumerate(tags):
             if CAT_SPANS is not None and tag == EMB_PAIR[1]:  # (diagnostic build, MREC_KC_CAT)
                 for c in range(4):
-                    cs, ce = u[i, c * 1024:(c + 1) * 1024, 0].min(), u[i, c * 1024:(c + 1) * 1024, 1].max()
+                    st_, en_ = u[i, c * 1024:(c + 1) * 1024, 0], u[i, c * 1024:(c + 1) * 1024, 1]
+                    cs, ce = st_.min(), en_.max()
                     if ce > cs:
+                        ok = en_ > 0
+                        # per-wave shards (waves of one kind < 1024): start / duration
+                        # quantiles over the kind's waves
+                        ws_ = (st_[ok] - t0[i]).astype(np.float64) * 1e-8
+                        wd_ = (en_[ok] - st_[ok]).astype(np.float64) * 1e-8
+                        q = [float(x) for x in np.quantile(ws_, [0.5, 0.9, 1.0])] + \
+                            [float(x) for x in np.quantile(wd_, [0.5, 0.9, 1.0])]
                         CAT_SPANS.setdefault(c, []).append(
-                            (float(cs - t0[i]) * 1e-8, float(ce - t0[i]) * 1e-8))
+                            (float(cs - t0[i]) * 1e-8, float(ce - t0[i]) * 1e-8, q))
             if tag in share:
                 span[tag].append(float(t1[i] - t0[i]) * 1e-8)  # 100 MHz ticks
                 # the share needs the next clocked launch to be the next libmrec call
@@ -483,9 +491,13 @@ def embedding_roofline(model, step, datas, args, in_step=True):
         rk[EMB_PAIR[1]]["avg_us_without_coreduce"] = round(t_strip[EMB_PAIR[1]] * 1e6, 3)
         if CAT_SPANS:
             rk[EMB_PAIR[1]]["block_kinds_us"] = {
-                ("co_reduce", "segments", "hot", "singles")[c]: [
-                    round(sorted(x[0] for x in v)[len(v) // 2] * 1e6, 2),
-                    round(sorted(x[1] for x in v)[len(v) // 2] * 1e6, 2)]
+                ("co_reduce", "segments", "hot", "singles")[c]: {
+                    "span": [round(sorted(x[0] for x in v)[len(v) // 2] * 1e6, 2),
+                             round(sorted(x[1] for x in v)[len(v) // 2] * 1e6, 2)],
+                    "wave_start_p50_p90_max": [round(v[len(v) // 2][2][j] * 1e6, 2)
+                                               for j in range(3)],
+                    "wave_dur_p50_p90_max": [round(v[len(v) // 2][2][j] * 1e6, 2)
+                                             for j in range(3, 6)]}
                 for c, v in sorted(CAT_SPANS.items())}
         if args.model == "deepfm":
             lins = [m for m in model.mlp.modules() if isinstance(m, torch.nn.Linear)]

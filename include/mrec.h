@@ -32,7 +32,7 @@
 extern "C" {
 #endif
 
-#define MREC_ABI_VERSION 25
+#define MREC_ABI_VERSION 26
 #define MREC_MAX_TABLES 64      /* tables per table bank / per call */
 #define MREC_BWD_MAX_BATCH 8192  /* lookups per table per plan/apply call */
 #define MREC_BWD_HASH_MAX_BATCH 4096  /* batches up to this use the hash plan */
@@ -456,6 +456,28 @@ mrec_status mrec_emb_bwd_apply_wire(const mrec_table_bank *bank, int64_t batch,
                                     mrec_bwd_mode mode, float lr, uint64_t seed,
                                     const uint64_t *d_step, void *grad, int32_t n_reduce,
                                     const struct mrec_gemm_call_s *reduce, mrec_stream stream);
+/* The sender's DENSE_GRAD sums written straight as wire RECORDS (ABI 26): the
+ * bank is the slot rows the interaction read (ids = pos, slot s = (p * n_tables +
+ * f) * cap + j); slot s's sum goes to record p * cap_rows + pref[p * n_tables + f]
+ * + j of `wire` (rec_bytes each, the table dtype, 4-B aligned; pref from
+ * mrec_shard_wire_unpack_ex) -- the bytes mrec_shard_wire_pack would produce from
+ * a zeroed sum buffer (bit-identical), without that buffer, its zeroing or the pack
+ * launch.  Entries past a part's cap_rows are dropped (the unpack flagged them).
+ * Hash layout only (batch <= MREC_BWD_HASH_MAX_BATCH). */
+typedef struct {
+  void *wire;
+  int32_t rec_bytes;
+  const int32_t *pref;
+  int32_t cap;
+  int32_t cap_rows;
+} mrec_grad_records;
+mrec_status mrec_emb_bwd_apply_rec(const mrec_table_bank *bank, int64_t batch,
+                                   const void *workspace, size_t ws_bytes, const void *dx,
+                                   mrec_dtype dx_dtype, int64_t dx_ld, const float *dfm,
+                                   const float *fm_sum, const void *x0, mrec_dtype x0_dtype,
+                                   int64_t x0_ld, const float *dw, const mrec_grad_records *out,
+                                   int32_t n_reduce, const struct mrec_gemm_call_s *reduce,
+                                   mrec_stream stream);
 
 /* ------------------------------------------------------------------------- */
 /* Communicator (RCCL over xGMI) for the row-sharded exchange                  */
@@ -605,6 +627,14 @@ mrec_status mrec_shard_wire_unpack(const void *wire, int32_t rec_bytes, const in
                                    int32_t world, int32_t n_tables, int32_t cap, int32_t cap_rows,
                                    void *slots, int64_t slot_bytes, int32_t to_f32, void *zero,
                                    int64_t zero_bytes, int32_t *d_overflow, mrec_stream stream);
+/* the same, also writing pref [world][n_tables] int32 (may be NULL, ABI 26): part
+ * p's table prefixes of hdr_ids' counts -- the sender's own record layout, which
+ * mrec_emb_bwd_apply_rec writes the gradient records in */
+mrec_status mrec_shard_wire_unpack_ex(const void *wire, int32_t rec_bytes, const int32_t *hdr_ids,
+                                      int32_t world, int32_t n_tables, int32_t cap,
+                                      int32_t cap_rows, void *slots, int64_t slot_bytes,
+                                      int32_t to_f32, void *zero, int64_t zero_bytes,
+                                      int32_t *pref, int32_t *d_overflow, mrec_stream stream);
 /* slot rows -> wire records (the first rec_bytes of each row) */
 mrec_status mrec_shard_wire_pack(const void *slots, int64_t slot_bytes, int32_t rec_bytes,
                                  const int32_t *hdr_ids, int32_t world, int32_t n_tables,

@@ -20,7 +20,7 @@ import torch  # noqa: F401  (must precede the dlopen, see module docstring)
 LIB_DIR = os.path.join(os.path.dirname(os.path.abspath(__file__)), "lib")
 LIB_PATH = os.environ.get("MREC_LIB_PATH") or os.path.join(LIB_DIR, "libmrec.so")
 
-ABI_VERSION = 25
+ABI_VERSION = 26
 MAX_TABLES = 64
 BWD_MAX_BATCH = 8192
 BWD_HASH_MAX_BATCH = 4096  # batches up to this use the hash plan (fusable into a GEMM launch)
@@ -133,6 +133,12 @@ class GivenGrads(ctypes.Structure):
                 ("pref", ctypes.c_void_p), ("cap_rows", ctypes.c_int32)]
 
 
+class GradRecords(ctypes.Structure):
+    """mrec_grad_records (include/mrec.h, ABI 26)."""
+    _fields_ = [("wire", ctypes.c_void_p), ("rec_bytes", ctypes.c_int32), ("pref", ctypes.c_void_p),
+                ("cap", ctypes.c_int32), ("cap_rows", ctypes.c_int32)]
+
+
 class HeadFinishJob(ctypes.Structure):
     _fields_ = [("part", ctypes.c_void_p), ("ldp", ctypes.c_int64), ("batch", ctypes.c_int64),
                 ("H", ctypes.c_int32), ("ns", ctypes.c_int32), ("g", ctypes.c_void_p),
@@ -240,6 +246,10 @@ SIGNATURES = {
                                                 _i64, _vp, _vp, _i64, _i64, _i64, ctypes.c_int,
                                                 _f32, ctypes.c_uint64, _vp, _vp, _i32,
                                                 ctypes.POINTER(GemmCall), _vp]),
+    "mrec_emb_bwd_apply_rec": (ctypes.c_int, [_bank_p, _i64, _vp, ctypes.c_size_t, _vp,
+                                              ctypes.c_int, _i64, _vp, _vp, _vp, ctypes.c_int,
+                                              _i64, _vp, ctypes.POINTER(GradRecords), _i32,
+                                              ctypes.POINTER(GemmCall), _vp]),
     "mrec_emb_bwd_apply_wire": (ctypes.c_int, [_bank_p, _i64, _vp, ctypes.c_size_t, _vp, _i32, _i32,
                                                _vp, _i32, _i64, _i64, ctypes.c_int, _f32,
                                                ctypes.c_uint64, _vp, _vp, _i32,
@@ -336,6 +346,8 @@ SIGNATURES = {
                                                  ctypes.POINTER(PlanJob), _vp]),
     "mrec_shard_wire_unpack": (ctypes.c_int, [_vp, _i32, _vp, _i32, _i32, _i32, _i32, _vp, _i64,
                                               _i32, _vp, _i64, _vp, _vp]),
+    "mrec_shard_wire_unpack_ex": (ctypes.c_int, [_vp, _i32, _vp, _i32, _i32, _i32, _i32, _vp,
+                                                 _i64, _i32, _vp, _i64, _vp, _vp, _vp]),
     "mrec_shard_wire_pack": (ctypes.c_int, [_vp, _i64, _i32, _vp, _i32, _i32, _i32, _i32, _vp, _vp,
                                             _vp]),
     "mrec_tower_fwd_bwd": (ctypes.c_int, [ctypes.POINTER(TowerArgs), _vp]),

@@ -38,6 +38,14 @@ struct ApplyArgs {
   int64_t g_cap_rows;
   int g_F;
   OptArgs opt;
+  // DENSE_GRAD straight into wire records (ABI 26, sender side of the compact
+  // exchange, mrec_emb_bwd_apply_rec): slot row s = (p * F + f) * cap + j -> record
+  // p * cap_rows + o_pref[p * F + f] + j (o_rec_dw dwords); no wire pack launch
+  uint32_t *o_rec;
+  int o_rec_dw;
+  const int32_t *o_pref;
+  int o_F, o_cap;
+  int64_t o_cap_rows;
 };
 
 // a given gradient from a wire record (4-B aligned rows: records are not 16-B).
@@ -224,12 +232,53 @@ __device__ __forceinline__ T *row_ptr(const BankArgs &bank, const ApplyArgs &a, 
   return row_ptr_g<T>(bank, a, bank.row_offset[f] + row, e0);
 }
 
+// DENSE_GRAD into a wire record (a.o_rec): the sums the slot row would hold after
+// the zeroed buffer's `0 + acc`, rounded to the table dtype as there; the record's
+// dwords only (a w lane: its one dword, element D and the zero pad beside it).  An
+// entry past its part's cap_rows records is dropped (the unpack flagged it).
+template <typename T>
+__device__ __forceinline__ void rec_out(const ApplyArgs &a, int64_t grow, int e0, bool v_lane,
+                                        const float *acc) {
+  constexpr int EPL = Vec<T>::EPL;
+  const int64_t fc = static_cast<int64_t>(a.o_F) * a.o_cap;
+  const int64_t p = grow / fc, rem = grow - p * fc;
+  const int f = static_cast<int>(rem / a.o_cap);
+  const int64_t j = rem - static_cast<int64_t>(f) * a.o_cap;
+  const int64_t in_part = a.o_pref[p * a.o_F + f] + j;
+  if (in_part >= a.o_cap_rows) return;
+  uint32_t *dst = a.o_rec + (p * a.o_cap_rows + in_part) * a.o_rec_dw +
+                  e0 * static_cast<int>(sizeof(T)) / 4;
+  if constexpr (sizeof(T) == 4) {
+    if (v_lane) {
+#pragma unroll
+      for (int k = 0; k < EPL; ++k) dst[k] = __float_as_uint(0.f + acc[k]);
+    } else {
+      dst[0] = __float_as_uint(0.f + acc[0]);
+    }
+  } else {
+    if (v_lane) {
+#pragma unroll
+      for (int k = 0; k < EPL / 2; ++k)
+        dst[k] = static_cast<uint32_t>(f32_to_bf16_rne(0.f + acc[2 * k])) |
+                 (static_cast<uint32_t>(f32_to_bf16_rne(0.f + acc[2 * k + 1])) << 16);
+    } else {
+      dst[0] = static_cast<uint32_t>(f32_to_bf16_rne(0.f + acc[0]));
+    }
+  }
+}
+
 // new value of this lane's 16 bytes of global row `grow` from its old contents `raw`
 template <typename T, int MODE = -1>
 __device__ __forceinline__ void apply_row_raw_g(const BankArgs &bank, const ApplyArgs &a,
                                                 int64_t grow, int e0, bool v_lane,
                                                 const float *acc, const uint4 raw) {
   constexpr int EPL = Vec<T>::EPL;
+  if constexpr (MODE == MREC_BWD_DENSE_GRAD) {
+    if (a.o_rec) {  // uniform
+      rec_out<T>(a, grow, e0, v_lane, acc);
+      return;
+    }
+  }
   const int mode = MODE >= 0 ? MODE : a.mode;
   T *p = row_ptr_g<T, MODE>(bank, a, grow, e0);
   float old[EPL];

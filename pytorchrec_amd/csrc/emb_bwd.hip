@@ -822,6 +822,13 @@ struct GivenWire {  // mrec_emb_bwd_apply_wire: given gradients as wire records
   const int32_t *pref;
   int64_t cap_rows;
 };
+struct RecOut {  // mrec_emb_bwd_apply_rec: DENSE_GRAD sums into wire records
+  void *wire;
+  int rec_dw;
+  const int32_t *pref;
+  int cap;
+  int64_t cap_rows;
+};
 
 static mrec_status apply_impl(const mrec_table_bank *bank, int64_t batch, const void *workspace,
                               size_t ws_bytes, const void *dx, mrec_dtype dx_dtype, int64_t dx_ld,
@@ -831,7 +838,7 @@ static mrec_status apply_impl(const mrec_table_bank *bank, int64_t batch, const 
                               int64_t chunk_stride, mrec_bwd_mode mode, float lr, uint64_t seed,
                               const uint64_t *d_step, void *grad, int32_t n_reduce,
                               const mrec_gemm_call *reduce, mrec_stream stream,
-                              const GivenWire *gw = nullptr);
+                              const GivenWire *gw = nullptr, const RecOut *ro = nullptr);
 
 extern "C" {
 
@@ -873,6 +880,21 @@ mrec_status mrec_emb_bwd_apply_given(const mrec_table_bank *bank, int64_t batch,
                     grad, n_reduce, reduce, stream);
 }
 
+mrec_status mrec_emb_bwd_apply_rec(const mrec_table_bank *bank, int64_t batch,
+                                   const void *workspace, size_t ws_bytes, const void *dx,
+                                   mrec_dtype dx_dtype, int64_t dx_ld, const float *dfm,
+                                   const float *fm_sum, const void *x0, mrec_dtype x0_dtype,
+                                   int64_t x0_ld, const float *dw, const mrec_grad_records *out,
+                                   int32_t n_reduce, const mrec_gemm_call *reduce,
+                                   mrec_stream stream) {
+  MREC_CHECK_ARG(out != nullptr, "out is NULL");
+  MREC_CHECK_ARG(out->rec_bytes > 0 && out->rec_bytes % 4 == 0, "bad record bytes");
+  const RecOut ro{out->wire, out->rec_bytes / 4, out->pref, out->cap, out->cap_rows};
+  return apply_impl(bank, batch, workspace, ws_bytes, dx, dx_dtype, dx_ld, dfm, fm_sum, x0,
+                    x0_dtype, x0_ld, dw, nullptr, 0, 0, 0, MREC_BWD_DENSE_GRAD, 0.f, 0, nullptr,
+                    nullptr, n_reduce, reduce, stream, nullptr, &ro);
+}
+
 mrec_status mrec_emb_bwd_apply_wire(const mrec_table_bank *bank, int64_t batch,
                                     const void *workspace, size_t ws_bytes, const void *wire,
                                     int32_t rec_bytes, mrec_dtype wire_dtype, const int32_t *pref,
@@ -899,7 +921,7 @@ static mrec_status apply_impl(const mrec_table_bank *bank, int64_t batch, const 
                               int64_t chunk_stride, mrec_bwd_mode mode, float lr, uint64_t seed,
                               const uint64_t *d_step, void *grad, int32_t n_reduce,
                               const mrec_gemm_call *reduce, mrec_stream stream,
-                              const GivenWire *gw) {
+                              const GivenWire *gw, const RecOut *ro) {
   BankArgs ba;
   int eb, lpr;
   mrec_status st = make_bank_args(bank, &ba, &eb, &lpr);
@@ -911,7 +933,17 @@ static mrec_status apply_impl(const mrec_table_bank *bank, int64_t batch, const 
     return MREC_ENOSPC;
   }
   MREC_CHECK_ARG(mode >= MREC_BWD_DENSE_GRAD && mode <= MREC_BWD_ADAM, "bad mode");
-  MREC_CHECK_ARG(mode != MREC_BWD_DENSE_GRAD || grad != nullptr, "DENSE_GRAD needs grad");
+  MREC_CHECK_ARG(mode != MREC_BWD_DENSE_GRAD || grad != nullptr || ro != nullptr,
+                 "DENSE_GRAD needs grad");
+  if (ro) {
+    MREC_CHECK_ARG(mode == MREC_BWD_DENSE_GRAD && grad == nullptr, "records take DENSE_GRAD sums");
+    MREC_CHECK_ARG(hash_layout(batch, false), "record output needs the hash layout (batch <= 4096)");
+    MREC_CHECK_ARG(ro->wire && ro->pref && ro->cap >= 1 && ro->cap_rows >= 1 &&
+                       (reinterpret_cast<uintptr_t>(ro->wire) & 3) == 0,
+                   "records: NULL wire / pref, bad cap");
+    MREC_CHECK_ARG(ro->rec_dw * 4 >= (ba.dim + (ba.has_w ? 1 : 0)) * eb, "record narrower than a row");
+    grad = bank->data;  // (the raw loads of the old sums read the rows: never used)
+  }
   OptArgs opt{};
   if ((st = make_opt_args(bank, mode, &opt)) != MREC_OK) return st;
   const int F = ba.n_tables, D = ba.dim;
@@ -973,6 +1005,12 @@ static mrec_status apply_impl(const mrec_table_bank *bank, int64_t batch, const 
   a.g_cap_rows = gw ? gw->cap_rows : 0;
   a.g_F = F;
   a.opt = opt;
+  a.o_rec = ro ? static_cast<uint32_t *>(ro->wire) : nullptr;
+  a.o_rec_dw = ro ? ro->rec_dw : 0;
+  a.o_pref = ro ? ro->pref : nullptr;
+  a.o_F = F;
+  a.o_cap = ro ? ro->cap : 1;
+  a.o_cap_rows = ro ? ro->cap_rows : 0;
   hipStream_t s = static_cast<hipStream_t>(stream);
   const int wpb = 256 / lpr;
   // hash layout (batch <= kHashMaxKeys or an exchange view, see mrec_emb_bwd_plan):

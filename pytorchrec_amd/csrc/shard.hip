@@ -441,6 +441,9 @@ __global__ __launch_bounds__(kWireThreads) void wire_move_kernel(WireArgs w,
   __shared__ int pre[MREC_MAX_TABLES + 1];
   const int p = blockIdx.y;
   const int tot = wire_prefix(w, p, pre);
+  // unpack: the part's table prefixes for the sender's gradient records (ABI 26)
+  if (UNPACK && w.pref && blockIdx.x == 0 && threadIdx.x < w.F)
+    w.pref[p * w.F + threadIdx.x] = pre[threadIdx.x];
   const int epr = UNPACK ? max(slot_dw, zero ? zero_dw : 0) : w.rec_dw;
   // element indices fit 32 bits (checked on the host): 32-bit divisions, not 64-bit
   const uint32_t n = static_cast<uint32_t>(tot) * static_cast<uint32_t>(epr);
@@ -845,9 +848,20 @@ mrec_status mrec_shard_wire_unpack(const void *wire, int32_t rec_bytes, const in
                                    int32_t world, int32_t n_tables, int32_t cap, int32_t cap_rows,
                                    void *slots, int64_t slot_bytes, int32_t to_f32, void *zero,
                                    int64_t zero_bytes, int32_t *d_overflow, mrec_stream stream) {
+  return mrec_shard_wire_unpack_ex(wire, rec_bytes, hdr_ids, world, n_tables, cap, cap_rows, slots,
+                                   slot_bytes, to_f32, zero, zero_bytes, nullptr, d_overflow,
+                                   stream);
+}
+
+mrec_status mrec_shard_wire_unpack_ex(const void *wire, int32_t rec_bytes, const int32_t *hdr_ids,
+                                      int32_t world, int32_t n_tables, int32_t cap,
+                                      int32_t cap_rows, void *slots, int64_t slot_bytes,
+                                      int32_t to_f32, void *zero, int64_t zero_bytes,
+                                      int32_t *pref, int32_t *d_overflow, mrec_stream stream) {
   WireArgs w;
   mrec_status st = wire_args(hdr_ids, world, n_tables, cap, cap_rows, rec_bytes, d_overflow, &w);
   if (st != MREC_OK) return st;
+  w.pref = pref;
   MREC_CHECK_ARG(wire && slots, "NULL pointer");
   MREC_CHECK_ARG(slot_bytes % 4 == 0 && zero_bytes % 4 == 0 && zero_bytes >= 0,
                  "row pitches must be multiples of 4 bytes");

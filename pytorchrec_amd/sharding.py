@@ -11,16 +11,19 @@ compact exchange, include/mrec.h ABI 19):
   owner   rows of the received ids -> one 36-B record per        mrec_shard_gather_wire
           distinct row, packed per owner over all tables
           all_to_all records back                                (equal split)
-  sender  records -> slot rows (+ zero the gradient sums)        mrec_shard_wire_unpack
+  sender  records -> slot rows, the part prefixes of its own     mrec_shard_wire_unpack_ex
+          record layout
           interaction on the slot rows, with the sender's        mrec_interact_fwd_ex
           backward plan over pos in the same launch
   ---- backward ----
-  sender  gradient sum of each slot's lookups (fixed ascending   mrec_emb_bwd_apply_ex
-          order, DENSE_GRAD into the slot rows)                  (DENSE_GRAD)
-          -> one record per distinct row, table dtype            mrec_shard_wire_pack
+  sender  gradient sum of each slot's lookups (fixed ascending   mrec_emb_bwd_apply_rec
+          order) written straight as one record per distinct     (ABI 26; batches past
+          row, table dtype                                       4096: DENSE_GRAD sums
+                                                                 + mrec_shard_wire_pack)
           all_to_all records to the owners                       (equal split)
-  owner   records -> fp32 slots; plan over the received ids;     mrec_shard_wire_unpack,
-          fixed-order sums over the senders + fused SGD          mrec_emb_bwd_apply_given
+  owner   plan over the received ids (in the gather launch);     mrec_emb_bwd_apply_wire
+          fixed-order sums over the senders read from the
+          records in place + fused SGD
 
 so the bytes on xGMI per rank and direction are ~cap_rows x 36 B per peer (one
 record per distinct id; bf16, D = 16 + w) instead of n_tables x cap x 64 B rows
@@ -495,15 +498,18 @@ def shard_gather_wire(bank: ShardedEmbeddingBank, recv_ids: torch.Tensor,
 
 def shard_wire_unpack(bank: ShardedEmbeddingBank, wire: torch.Tensor, hdr: torch.Tensor,
                       slots: torch.Tensor, to_f32: bool = False,
-                      zero: Optional[torch.Tensor] = None, parts: Optional[int] = None):
+                      zero: Optional[torch.Tensor] = None, parts: Optional[int] = None,
+                      pref: Optional[torch.Tensor] = None):
     """Records -> slot rows [W*F*cap, ...] (``hdr``: the ids message whose counts
-    describe ``wire``); ``zero``: the same rows of a second buffer are cleared."""
+    describe ``wire``); ``zero``: the same rows of a second buffer are cleared;
+    ``pref`` (int32 [parts, n_tables]) receives each part's table prefixes -- the
+    record layout sender_grad_records writes the gradients in."""
     fl = bank.flags()
-    _mrec.call("mrec_shard_wire_unpack", wire.data_ptr(), bank.wire_bytes(), hdr.data_ptr(),
+    _mrec.call("mrec_shard_wire_unpack_ex", wire.data_ptr(), bank.wire_bytes(), hdr.data_ptr(),
                parts or bank.world, bank.n_tables, bank.cap, bank.cap_rows, slots.data_ptr(),
                slots.stride(0) * slots.element_size(), int(to_f32), _mrec.ptr(zero),
-               zero.stride(0) * zero.element_size() if zero is not None else 0, fl.data_ptr(),
-               _mrec.stream_handle())
+               zero.stride(0) * zero.element_size() if zero is not None else 0, _mrec.ptr(pref),
+               fl.data_ptr(), _mrec.stream_handle())
     return slots
 
 
@@ -580,6 +586,33 @@ def sender_grad_sums(bank: ShardedEmbeddingBank, rows_recv: torch.Tensor, pos: t
                0, None, gsum.data_ptr(), len(jobs), arr, _mrec.stream_handle())
     del jobs
     return gsum
+
+
+def sender_grad_records(bank: ShardedEmbeddingBank, rows_recv: torch.Tensor, pos: torch.Tensor,
+                        plan, spref: torch.Tensor, parts: Optional[int] = None, dx=None, dfm=None,
+                        fm_sum=None, x0=None, dw=None) -> torch.Tensor:
+    """sender_grad_sums + shard_wire_pack in ONE launch (mrec_emb_bwd_apply_rec, ABI
+    26): each slot's sum goes straight into its wire record (``spref``: the part
+    prefixes shard_wire_unpack wrote) -> [parts, cap_rows * record] bytes, the same
+    bytes the pack of a zeroed sum buffer gives.  Hash-layout plans only (B <=
+    MREC_BWD_HASH_MAX_BATCH); the deferred MLP reductions ride along."""
+    ws, wsb = plan
+    B = pos.shape[1]
+    P, rb = parts or bank.world, bank.wire_bytes()
+    wire = torch.empty(P, bank.cap_rows * rb, dtype=torch.uint8, device=bank.weight.device)
+    out = _mrec.GradRecords(wire.data_ptr(), rb, spref.data_ptr(), bank.cap, bank.cap_rows)
+    from pytorchrec_amd import dense as dense_ops
+    jobs = dense_ops.take_pending(4)
+    arr = (_mrec.GemmCall * len(jobs))(*[j.struct() for j in jobs]) if jobs else None
+    rdesc = remote_desc(bank, rows_recv)
+    _mrec.call("mrec_emb_bwd_apply_rec", rdesc.ref(), B, ws.data_ptr(), wsb,
+               _mrec.ptr(dx), _mrec.dtype_code(dx.dtype) if dx is not None else _mrec.F32,
+               dx.stride(0) if dx is not None else 0, _mrec.ptr(dfm), _mrec.ptr(fm_sum),
+               _mrec.ptr(x0), _mrec.dtype_code(x0.dtype) if x0 is not None else _mrec.F32,
+               x0.stride(0) if x0 is not None else 0, _mrec.ptr(dw), ctypes.byref(out),
+               len(jobs), arr, _mrec.stream_handle())
+    del jobs
+    return wire
 
 
 def remote_desc(bank: ShardedEmbeddingBank, rows_recv: torch.Tensor) -> _mrec.BankDesc:
@@ -808,9 +841,12 @@ class _CompactInteractFn(torch.autograd.Function):
         del okeep
         n = P * bank.n_tables * bank.cap
         rows_recv = torch.empty(n, bank.row_stride, dtype=bank.weight.dtype, device=dev)
-        gsum = torch.empty_like(rows_recv) if train else None
-        shard_wire_unpack(bank, wire, send, rows_recv, zero=gsum, parts=P)
         fuse = train and B <= _mrec.BWD_HASH_MAX_BATCH
+        # one chunk in the hash layout: the backward writes the gradient records
+        # directly (sender_grad_records); else sums into zeroed slot rows + a pack
+        spref = torch.empty(P, bank.n_tables, dtype=torch.int32, device=dev) if fuse else None
+        gsum = torch.empty_like(rows_recv) if train and not fuse else None
+        shard_wire_unpack(bank, wire, send, rows_recv, zero=gsum, parts=P, pref=spref)
         job, splan, keep = (sender_plan_job(bank, rows_recv, pos) if fuse
                             else (None, None, None))
         x0, logit, fm_sum = shard_interact(bank, rows_recv, pos, dense, dense_w, bias, fm2,
@@ -828,7 +864,7 @@ class _CompactInteractFn(torch.autograd.Function):
         ctx.fm2, ctx.first_order = fm2, first_order
         ctx.has_dense_w, ctx.has_bias = dense_w is not None, bias is not None
         ctx.dense_w, ctx.bias = dense_w, bias
-        ctx.pref = pref
+        ctx.pref, ctx.spref = pref, spref
         ctx.save_for_backward(x0, fm_sum, dense, pos, send, recv, rows_recv, gsum)
         if x0 is None:
             return logit
@@ -849,12 +885,19 @@ class _CompactInteractFn(torch.autograd.Function):
         if dx0 is not None:
             dx0 = dx0.contiguous()
         if ctx.splans is not None:
-            for s0, n_c, splan in ctx.splans:  # each chunk's lookups (disjoint slots)
-                sl = (lambda t: None if t is None else t[s0:s0 + n_c])  # noqa: E731
-                sender_grad_sums(bank, rows_recv, pos[:, s0:s0 + n_c], splan, gsum, dx=sl(dx0),
-                                 dfm=sl(dfm), fm_sum=sl(fm_sum),
-                                 x0=sl(x0) if dfm is not None else None, dw=sl(dw))
-            wire_g = bank.comm.exchange(shard_wire_pack(bank, gsum, send, parts=ctx.P))
+            if ctx.spref is not None:  # one hash-layout chunk: records written directly
+                (_, _, splan), = ctx.splans
+                wire_g = sender_grad_records(bank, rows_recv, pos, splan, ctx.spref, parts=ctx.P,
+                                             dx=dx0, dfm=dfm, fm_sum=fm_sum,
+                                             x0=x0 if dfm is not None else None, dw=dw)
+            else:
+                for s0, n_c, splan in ctx.splans:  # each chunk's lookups (disjoint slots)
+                    sl = (lambda t: None if t is None else t[s0:s0 + n_c])  # noqa: E731
+                    sender_grad_sums(bank, rows_recv, pos[:, s0:s0 + n_c], splan, gsum,
+                                     dx=sl(dx0), dfm=sl(dfm), fm_sum=sl(fm_sum),
+                                     x0=sl(x0) if dfm is not None else None, dw=sl(dw))
+                wire_g = shard_wire_pack(bank, gsum, send, parts=ctx.P)
+            wire_g = bank.comm.exchange(wire_g)
             # the owner reads the gradient records in place (no unpack launch)
             if ctx.oplan is not None:
                 owner_apply_wire(bank, ctx.oplan, wire_g, ctx.pref, parts=ctx.P)

@@ -40,6 +40,12 @@ def _ids(gpu, B, seed, zipf=False):
     return out
 
 
+def prefs_own(send, P, F, cap):
+    """The sender's part prefixes of its table counts (int32 [P, F], exclusive)."""
+    c = send.view(P, -1)[:, F * cap:F * cap + F].long()
+    return (torch.cumsum(c, 1) - c).to(torch.int32)
+
+
 def _exchange(sends, W):
     """all_to_all for W simulated ranks: out[r] = concat_s send[s] part r."""
     parts = [s.reshape(W, -1, *s.shape[1:]) if s.dim() > 1 else s.reshape(W, -1) for s in sends]
@@ -426,11 +432,12 @@ def test_compact_exchange_simulated_bit_exact(gpu, W, zipf, B, big):
     wires = _exchange([S.shard_gather_wire(banks[r], recvs[r], pref=prefs[r], parts=P)
                        for r in range(W)], W)
     n = P * F * banks[0].cap
-    rows, gsums, outs, plans, oplans = [], [], [], [], []
+    rows, gsums, outs, plans, oplans, sprefs = [], [], [], [], [], []
     for r in range(W):
         rr = torch.empty(n, banks[r].row_stride, dtype=torch.bfloat16, device=gpu)
         gs = torch.empty_like(rr)
-        S.shard_wire_unpack(banks[r], wires[r], sends[r], rr, zero=gs, parts=P)
+        sprefs.append(torch.empty(P, F, dtype=torch.int32, device=gpu))
+        S.shard_wire_unpack(banks[r], wires[r], sends[r], rr, zero=gs, parts=P, pref=sprefs[r])
         rows.append(rr)
         gsums.append(gs)
         fuse = B <= 4096
@@ -477,8 +484,19 @@ def test_compact_exchange_simulated_bit_exact(gpu, W, zipf, B, big):
                 p = poss[r][f, s0:s0 + nc].long()
                 want = gref[glob.row_offset[f] + ids_c[f].long(), :D + 1]
                 assert torch.equal(gsums[r][p, :D + 1], want), (r, s0, f)
-    wire_g = _exchange([S.shard_wire_pack(banks[r], gsums[r], sends[r], parts=P)
-                        for r in range(W)], W)
+    packed = [S.shard_wire_pack(banks[r], gsums[r], sends[r], parts=P) for r in range(W)]
+    if B <= 4096:  # one hash-layout chunk: the sums written straight as records (ABI 26)
+        rb = banks[0].wire_bytes()
+        for r in range(W):
+            recs = S.sender_grad_records(banks[r], rows[r], poss[r], plans[r][0][2], sprefs[r],
+                                         parts=P, dx=dx0[r], dfm=dl[r], fm_sum=outs[r][2],
+                                         x0=outs[r][0], dw=dl[r])
+            cnt = sends[r].view(P, -1)[:, F * banks[r].cap:].sum(1).clamp(max=banks[r].cap_rows)
+            for p_ in range(P):
+                k = int(cnt[p_]) * rb
+                assert torch.equal(recs[p_, :k], packed[r][p_, :k]), (r, p_)
+            assert torch.equal(sprefs[r], prefs_own(sends[r], P, F, banks[r].cap)), r
+    wire_g = _exchange(packed, W)
     tot = torch.zeros_like(rank_grads[0], dtype=torch.float32)
     for g in rank_grads:  # the owners' order: source rank 0, 1, ...
         tot += g.float()

@@ -294,7 +294,11 @@ struct HotSeg {
       }
       __syncthreads();
       const int c1 = min(sn, c0 + kHotChunk);
+#if MREC_APPLY_EXP == 17  // (diagnostic: no hot-segment gradient loads)
+      if (live && sn < 0) {
+#else
       if (live) {
+#endif
 #pragma unroll 1
         for (int i0 = c0 + worker; i0 < c1; i0 += WPB * KB) {
           int bs[KB];
@@ -407,6 +411,9 @@ __device__ __forceinline__ void apply_segment(const BankArgs &bank, const ApplyA
 #pragma unroll
     for (int i = 0; i < PER; ++i) p[i] = l + i * LPR < n ? t.perm[d.z + l + i * LPR] : INT_MAX;
     int last = -1;
+#if MREC_APPLY_EXP == 16  // (diagnostic: no segment gradient loop)
+    if (n < 0)
+#endif
 #pragma unroll 1
     for (int k0 = 0; k0 < n; k0 += kSegBatch) {
       int sb[kSegBatch];

@@ -90,7 +90,10 @@ constexpr int kHashSlots = 8192;       // per workgroup: any bucket fits at load
 #define MREC_PLAN_BUCKETS_LOG2 3
 #endif
 constexpr int kPlanBuckets = 1 << MREC_PLAN_BUCKETS_LOG2;  // workgroups per table
-constexpr int kShortSeg = 16;          // longer segments: the bucket's long list
+#ifndef MREC_SHORT_SEG
+#define MREC_SHORT_SEG 16
+#endif
+constexpr int kShortSeg = MREC_SHORT_SEG;  // longer segments: the bucket's long list
 constexpr uint32_t kEmpty = 0xffffffffu;
 
 // segments up to this many lookups are summed by one wave of the apply (one

@@ -23,7 +23,7 @@
 namespace mrec {
 
 #ifndef MREC_APPLY_EXP
-#define MREC_APPLY_EXP 0  // microbenchmark variants (tools/bench_apply.py, tools/r4_apply_exp.sh); 0 = product
+#define MREC_APPLY_EXP 0  // microbenchmark variants (tools/bench_apply.py, tools/gpu_apply_exp.sh); 0 = product
 #endif
 
 constexpr int kMaxPlanKeys = 8192;

@@ -1,4 +1,4 @@
-"""Print ms/step and the in-step apply time of tools/r4_apply_exp.sh outputs."""
+"""Print ms/step and the in-step apply time of tools/gpu_apply_exp.sh outputs."""
 import glob
 import json
 import os

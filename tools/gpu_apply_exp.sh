@@ -1,6 +1,6 @@
 # In-step apply time (kernel clock) for apply-experiment builds (tools/build_variant.py
 # NAME emb_bwd.hip -D...), Zipf C2 ids and uniform C2 ids.
-#   bash tools/r4_apply_exp.sh OUTDIR variant [variant ...]   (base = the product build)
+#   bash tools/gpu_apply_exp.sh OUTDIR variant [variant ...]   (base = the product build)
 export TMPDIR=/tmp
 o=gpurun_out/$1
 shift

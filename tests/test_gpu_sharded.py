@@ -651,3 +651,46 @@ def test_c5_sized_tables_compact_exchange_w8(gpu):
         del before
     del banks, rows, gsums
     torch.cuda.empty_cache()
+
+
+def test_compact_cap_rows_overflow_raised_and_clipped_rows_untouched(gpu):
+    """ADVICE r3: a part whose distinct ids exceed cap_rows has its records clipped;
+    the overflow is raised (its own message), and the owner's apply reading the
+    gradient records in place gives the clipped entries a zero gradient -- their rows
+    stay unchanged, never another entry's record (emb_apply.h wire_grad)."""
+    from pytorchrec_amd import sharding as S
+    n_rows, B = 1000, 64
+    bank = S.ShardedEmbeddingBank([n_rows], D, S.ShardComm(world=1, rank=0), dtype=torch.float32,
+                                  max_batch=B, cap=B, device=gpu)
+    with torch.no_grad():
+        bank.weight.copy_(torch.randn_like(bank.weight))
+    bank.cap_rows = 8  # 40 distinct ids below: entries 8.. are clipped
+    ids = [torch.arange(40, dtype=torch.int32, device=gpu).repeat(2)[:B] * 7]
+    send, pos = S.shard_bucketize_dedup(bank, ids)
+    recv = send  # world 1
+    pref = torch.empty(1, 1, dtype=torch.int32, device=gpu)
+    wire = S.shard_gather_wire(bank, recv, pref=pref, parts=1)
+    rows = torch.empty(bank.cap, bank.row_stride, dtype=torch.float32, device=gpu)
+    S.shard_wire_unpack(bank, wire, send, rows, parts=1)
+    with pytest.raises(RuntimeError, match="cap_rows"):
+        bank.check_flags()
+    # gradient records: every valid record carries 1.0 in every element
+    wire_g = torch.ones(1, bank.cap_rows * bank.wire_bytes() // 4, dtype=torch.float32,
+                        device=gpu).view(torch.uint8)
+    before = bank.weight.detach().clone()
+    plan = S.owner_plan(bank, recv, bank.part, 1)
+    S.owner_apply_wire(bank, plan, wire_g, pref, lr=0.5, parts=1)
+    bank.check_flags()
+    torch.cuda.synchronize()
+    slot_ids = send.view(-1)[:bank.cap].long()  # the distinct ids in slot order
+    cols = D + 1 if bank.has_w else D
+    for j in range(40):
+        r = int(slot_ids[j])
+        got, old = bank.weight[r, :D], before[r, :D]
+        if j < bank.cap_rows:
+            assert torch.equal(got, old - 0.5), j  # one record: gradient 1.0
+        else:
+            assert torch.equal(got, old), j  # clipped: zero gradient
+    untouched = torch.ones(n_rows, dtype=torch.bool, device=gpu)
+    untouched[slot_ids[:40]] = False
+    assert torch.equal(bank.weight[untouched, :cols], before[untouched, :cols])

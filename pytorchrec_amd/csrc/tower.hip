@@ -36,7 +36,7 @@ constexpr int TW_THREADS = 512;
 constexpr int TW_WAVES = TW_THREADS / 64;
 constexpr int TW_MAXL = 4;
 constexpr int TW_MAXW = 512;
-constexpr int TW_PF_DEFAULT = 4;         // k steps of weight fragments in flight per wave
+constexpr int TW_PF_DEFAULT = 8;         // k steps of weight fragments in flight per wave (r04: 8 over 4, -0.5 % step)
 constexpr int TW_TPW = 4;                // output tiles per wave (<= 32 tiles = 512 wide)
 constexpr int TW_MAXNS = 64;             // side-linear width
 
@@ -800,7 +800,7 @@ mrec_status mrec_tower_fwd_bwd(const mrec_tower_args *p, mrec_stream stream) {
   static const int pf_env = [] {  // MREC_TOWER_PF: weight k steps in flight per wave
     const char *e = getenv("MREC_TOWER_PF");
     const int v = e ? atoi(e) : TW_PF_DEFAULT;
-    return (v == 6 || v == 8) ? v : 4;
+    return (v == 4 || v == 6) ? v : 8;
   }();
   hipStream_t st = static_cast<hipStream_t>(stream);
   const int64_t grid = (s.batch + TW_ROWS - 1) / TW_ROWS;

@@ -42,8 +42,8 @@ HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md chip table (spec)
 def parse(argv=None):
     p = argparse.ArgumentParser()
     p.add_argument("--gpus", type=int, default=1)
-    p.add_argument("--steps", type=int, default=50)
-    p.add_argument("--warmup", type=int, default=10)
+    p.add_argument("--steps", type=int, default=200)
+    p.add_argument("--warmup", type=int, default=20)
     p.add_argument("--model", default="deepfm", choices=["deepfm", "dcnv2", "din"])
     p.add_argument("--batch", type=int, default=4096)
     p.add_argument("--rows-per-table", type=int, default=None,

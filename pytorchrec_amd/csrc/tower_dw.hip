@@ -34,7 +34,10 @@ namespace mrec {
 #ifndef MREC_TDW_EXP
 #define MREC_TDW_EXP 0
 #endif
-constexpr int DW_PF = 4;       // k steps of fragments in flight per wave
+#ifndef MREC_DW_PF
+#define MREC_DW_PF 4
+#endif
+constexpr int DW_PF = MREC_DW_PF;  // k steps of fragments in flight per wave
 constexpr int DW_MAXL = 4;
 constexpr int DW_TILE = 64;    // output tile edge of one wave (4 MFMA tiles)
 constexpr int DW_OOB = 1 << 30;  // a voffset past every image: the load returns zeros

@@ -32,7 +32,7 @@
 extern "C" {
 #endif
 
-#define MREC_ABI_VERSION 26
+#define MREC_ABI_VERSION 27
 #define MREC_MAX_TABLES 64      /* tables per table bank / per call */
 #define MREC_BWD_MAX_BATCH 8192  /* lookups per table per plan/apply call */
 #define MREC_BWD_HASH_MAX_BATCH 4096  /* batches up to this use the hash plan */
@@ -892,6 +892,24 @@ typedef struct {
    * backward as for BCE (dh_out, dx0, head partials, images). */
   int32_t mode;
   const float *dz_in;        /* [batch] for MREC_TOWER_GIVEN_DZ */
+  /* ABI 27: a DCN-v2 cross network ahead of the MLP (the
+   * layers are nn.Linear(d, d) as the reference's Linear init, IModel.py:61-66),
+   * n_cross layers of width d = width[0], run in the same launch on the x0 block:
+   *   x_0 = x0;  z_c = x_c Wc_c^T + bc_c;  x_{c+1} = x0 * z_c + x_c;  the MLP reads
+   *   x_{n_cross} (its h_0);
+   * backward (G_{n_cross} = the MLP's input gradient):
+   *   dz_c = G_{c+1} * x0;  G_c = dz_c Wc_c + G_{c+1};
+   *   dx0 = G_0 + sum_c G_{c+1} * z_c   (fp32 sum, one rounding, written to dx0).
+   * With kfrag: x0_img receives x_0's image, cross_x_img[c] the image of x_{c+1}
+   * (cross_x_img[n_cross - 1] is the MLP's first-layer X operand) and
+   * cross_dz_img[c] that of dz_c: with them mrec_tower_dw computes dWc_c =
+   * dz_c^T [x_c | 1].  z_c stays on chip (bf16) from the forward to the backward. */
+  int32_t n_cross;           /* 0..3 */
+  const void *cross_w_fwd[3];  /* tower images of Wc_c [d, d] */
+  const void *cross_w_bwd[3];
+  const float *cross_bias[3];  /* [d] (NULL: no bias) */
+  void *cross_x_img[3];
+  void *cross_dz_img[3];
 } mrec_tower_args;
 
 enum { MREC_TOWER_BCE = 0, MREC_TOWER_FORWARD = 1, MREC_TOWER_GIVEN_DZ = 2 };
@@ -914,13 +932,13 @@ mrec_status mrec_tower_fwd_bwd(const mrec_tower_args *a, mrec_stream stream);
  * reference MLP (MLP.py:8-23, Dense.py:12-24) for the tower path.
  */
 typedef struct {
-  int32_t n_layers;          /* 1..4 */
+  int32_t n_layers;          /* 1..8 (ABI 27: 8, the cross layers + the MLP) */
   int64_t batch;
-  int32_t n_out[4], n_in[4];
-  const void *dy_img[4];     /* bf16 k-fragment image of dY_l [batch, n_out] */
-  const void *x_img[4];      /* bf16 k-fragment image of X_l [batch, n_in] */
-  float *ws[4];              /* splits x n_out x ldws fp32 */
-  int64_t ldws[4];           /* >= n_in + 1 (mrec_gemm's slab stride: round8(n_in + 1)) */
+  int32_t n_out[8], n_in[8];
+  const void *dy_img[8];     /* bf16 k-fragment image of dY_l [batch, n_out] */
+  const void *x_img[8];      /* bf16 k-fragment image of X_l [batch, n_in] */
+  float *ws[8];              /* splits x n_out x ldws fp32 */
+  int64_t ldws[8];           /* >= n_in + 1 (mrec_gemm's slab stride: round8(n_in + 1)) */
   int32_t splits;
 } mrec_tower_dw_args;
 

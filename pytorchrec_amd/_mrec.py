@@ -20,7 +20,7 @@ import torch  # noqa: F401  (must precede the dlopen, see module docstring)
 LIB_DIR = os.path.join(os.path.dirname(os.path.abspath(__file__)), "lib")
 LIB_PATH = os.environ.get("MREC_LIB_PATH") or os.path.join(LIB_DIR, "libmrec.so")
 
-ABI_VERSION = 26
+ABI_VERSION = 27
 MAX_TABLES = 64
 BWD_MAX_BATCH = 8192
 BWD_HASH_MAX_BATCH = 4096  # batches up to this use the hash plan (fusable into a GEMM launch)
@@ -176,15 +176,18 @@ class TowerArgs(ctypes.Structure):
                 ("part", ctypes.c_void_p), ("ldp", ctypes.c_int64),
                 ("loss_part", ctypes.c_void_p), ("ticket", ctypes.c_void_p),
                 ("loss", ctypes.c_void_p), ("kfrag", ctypes.c_int32), ("x0_img", ctypes.c_void_p),
-                ("mode", ctypes.c_int32), ("dz_in", ctypes.c_void_p)]
+                ("mode", ctypes.c_int32), ("dz_in", ctypes.c_void_p),
+                ("n_cross", ctypes.c_int32), ("cross_w_fwd", ctypes.c_void_p * 3),
+                ("cross_w_bwd", ctypes.c_void_p * 3), ("cross_bias", ctypes.c_void_p * 3),
+                ("cross_x_img", ctypes.c_void_p * 3), ("cross_dz_img", ctypes.c_void_p * 3)]
 
 
 class TowerDwArgs(ctypes.Structure):
     """mrec_tower_dw_args (include/mrec.h)."""
     _fields_ = [("n_layers", ctypes.c_int32), ("batch", ctypes.c_int64),
-                ("n_out", ctypes.c_int32 * 4), ("n_in", ctypes.c_int32 * 4),
-                ("dy_img", ctypes.c_void_p * 4), ("x_img", ctypes.c_void_p * 4),
-                ("ws", ctypes.c_void_p * 4), ("ldws", ctypes.c_int64 * 4),
+                ("n_out", ctypes.c_int32 * 8), ("n_in", ctypes.c_int32 * 8),
+                ("dy_img", ctypes.c_void_p * 8), ("x_img", ctypes.c_void_p * 8),
+                ("ws", ctypes.c_void_p * 8), ("ldws", ctypes.c_int64 * 8),
                 ("splits", ctypes.c_int32)]
 
 

@@ -39,6 +39,7 @@ constexpr int TW_MAXW = 512;
 constexpr int TW_PF_DEFAULT = 8;         // k steps of weight fragments in flight per wave (r04: 8 over 4, -0.5 % step)
 constexpr int TW_TPW = 4;                // output tiles per wave (<= 32 tiles = 512 wide)
 constexpr int TW_MAXNS = 64;             // side-linear width
+constexpr int TW_MAXC = 3;               // DCN-v2 cross layers ahead of the MLP (ABI 27)
 
 typedef short bf16x8 __attribute__((ext_vector_type(8)));
 typedef float f32x4 __attribute__((ext_vector_type(4)));
@@ -92,6 +93,16 @@ struct TowerArgs {
   uint16_t *x0_img;
   int mode;        // MREC_TOWER_BCE / _FORWARD / _GIVEN_DZ
   const float *dz_in;
+  // DCN-v2 cross network (ABI 27): C layers of width d = width[0] ahead of the MLP
+  int C;
+  const uint16_t *cwf[TW_MAXC];
+  const uint16_t *cwb[TW_MAXC];
+  const float *cbias[TW_MAXC];
+  int cw_bytes;    // fwd and bwd images of a [d, d] weight have the same size
+  uint16_t *cx_img[TW_MAXC];   // k-fragment images of x_1 .. x_C
+  uint16_t *cdz_img[TW_MAXC];  // k-fragment images of dz_0 .. dz_{C-1}
+  int off_xc[2];               // ping-pong x_c blocks (stride s_x); off_xc[0] is G in the backward
+  int p_cbias[TW_MAXC];
 };
 
 
@@ -167,16 +178,15 @@ __device__ __forceinline__ void tower_mfma(f32x4 (&acc)[TW_TPW], __amdgpu_buffer
 //   BWD: acc, times [mask[m][c] > 0] when mask != NULL.
 // Tiles in [ntiles, 2 ceil(width_out / 32)) are written as zeros (the next
 // layer reads whole k steps of 32).
-template <bool BWD, int TW_PF>
-__device__ __forceinline__ void tower_layer(const uint16_t *__restrict__ img, int img_bytes,
-                                            int ksteps, int width_out, const char *in, int s_in, char *out,
-                                            int s_out, const float *__restrict__ bias,
-                                            const char *mask, int s_mask, int rotate) {
+// The MFMA phase of a layer: acc[i] = the wave's output tile t = wave + 8 i (lane l:
+// rows 16 t + 4 (l / 16) .. + 4 of batch row l % 16).
+template <int TW_PF>
+__device__ __forceinline__ void tower_layer_acc(f32x4 (&acc)[TW_TPW], const uint16_t *__restrict__ img,
+                                                int img_bytes, int ksteps, int ntiles, const char *in,
+                                                int s_in, int rotate) {
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int g = lane >> 4, r16 = lane & 15;
-  const int ntiles = tw_ceil(width_out, 16);
-  const int ztiles = 2 * tw_ceil(width_out, 32);
   int nreal = 0;
 #pragma unroll
   for (int i = 0; i < TW_TPW; ++i) nreal += (wave + TW_WAVES * i < ntiles) ? 1 : 0;
@@ -187,7 +197,6 @@ __device__ __forceinline__ void tower_layer(const uint16_t *__restrict__ img, in
   const __amdgpu_buffer_rsrc_t rsrc =
       __builtin_amdgcn_make_buffer_rsrc(const_cast<uint16_t *>(img), 0, img_bytes, 0x00020000);
 
-  f32x4 acc[TW_TPW];
 #pragma unroll
   for (int i = 0; i < TW_TPW; ++i) acc[i] = f32x4{0.f, 0.f, 0.f, 0.f};
 
@@ -200,6 +209,20 @@ __device__ __forceinline__ void tower_layer(const uint16_t *__restrict__ img, in
     case 1: tower_mfma<1, TW_PF>(acc, rsrc, voff, img_bytes, brow, ksteps, rot); break;
     default: break;
   }
+}
+
+template <bool BWD, int TW_PF>
+__device__ __forceinline__ void tower_layer(const uint16_t *__restrict__ img, int img_bytes,
+                                            int ksteps, int width_out, const char *in, int s_in, char *out,
+                                            int s_out, const float *__restrict__ bias,
+                                            const char *mask, int s_mask, int rotate) {
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int g = lane >> 4, r16 = lane & 15;
+  const int ntiles = tw_ceil(width_out, 16);
+  const int ztiles = 2 * tw_ceil(width_out, 32);
+  f32x4 acc[TW_TPW];
+  tower_layer_acc<TW_PF>(acc, img, img_bytes, ksteps, ntiles, in, s_in, rotate);
 
   // epilogue: lane holds rows c = 16 t + 4 g + r (r = 0..3) of column m = r16
 #pragma unroll
@@ -228,6 +251,142 @@ __device__ __forceinline__ void tower_layer(const uint16_t *__restrict__ img, in
     }
     *reinterpret_cast<uint2 *>(out + r16 * s_out + c0 * 2) =
         make_uint2(pack_bf16x2(v[0], v[1]), pack_bf16x2(v[2], v[3]));
+  }
+}
+
+__device__ __forceinline__ void unpack_bf16x4(uint2 v, float (&f)[4]) {
+  f[0] = __uint_as_float(v.x << 16);
+  f[1] = __uint_as_float(v.x & 0xffff0000u);
+  f[2] = __uint_as_float(v.y << 16);
+  f[3] = __uint_as_float(v.y & 0xffff0000u);
+}
+__device__ __forceinline__ uint2 pack_bf16x4(const float (&f)[4]) {
+  return make_uint2(pack_bf16x2(f[0], f[1]), pack_bf16x2(f[2], f[3]));
+}
+
+// ---- DCN-v2 cross network inside the tower (ABI 27) -------------------------------
+// Layer c: z_c = x_c Wc_c^T + b_c, x_{c+1} = x0 * z_c + x_c (d = width[0] wide, the
+// x0 block stays in LDS).  The epilogue lane mapping is the same for the forward and
+// the backward of a layer (d outputs both ways), so z_c stays in the lane's registers
+// as bf16 (4 x 8 B per layer) from the forward to the backward instead of crossing
+// HBM.  Rounding points as the layered path (mrec_gemm's mul / add / aux epilogue):
+// z and x_{c+1} are bf16, x_{c+1} is computed from the fp32 z.
+template <int TW_PF>
+__device__ __forceinline__ void tower_cross_fwd(const uint16_t *__restrict__ img, int img_bytes, int d,
+                                                const char *x0b, const char *in, int s_x, char *out,
+                                                const float *bias, int rotate, uint2 (&zq)[TW_TPW]) {
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int g = lane >> 4, r16 = lane & 15;
+  const int ntiles = tw_ceil(d, 16), ztiles = 2 * tw_ceil(d, 32);
+  f32x4 acc[TW_TPW];
+  tower_layer_acc<TW_PF>(acc, img, img_bytes, tw_ceil(d, 32), ntiles, in, s_x, rotate);
+#pragma unroll
+  for (int i = 0; i < TW_TPW; ++i) {
+    const int t = wave + TW_WAVES * i;
+    zq[i] = make_uint2(0u, 0u);
+    if (t >= ztiles) continue;  // uniform
+    const int c0 = 16 * t + 4 * g;
+    float v[4] = {0.f, 0.f, 0.f, 0.f};
+    if (t < ntiles) {
+      float x0f[4], xlf[4], z[4] = {0.f, 0.f, 0.f, 0.f};
+      unpack_bf16x4(*reinterpret_cast<const uint2 *>(x0b + r16 * s_x + c0 * 2), x0f);
+      unpack_bf16x4(*reinterpret_cast<const uint2 *>(in + r16 * s_x + c0 * 2), xlf);
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        if (c0 + r < d) {
+          z[r] = acc[i][r] + bias[c0 + r];
+          v[r] = z[r] * x0f[r] + xlf[r];
+        }
+      }
+      zq[i] = pack_bf16x4(z);
+    }
+    *reinterpret_cast<uint2 *>(out + r16 * s_x + c0 * 2) = pack_bf16x4(v);
+  }
+}
+
+// The MLP's first layer backward when a cross network precedes it: acc = dx_C tile
+// -> G block = bf16(dx_C) (the cross backward's running G), dz_{C-1} = bf16(G x0) ->
+// dzo (the next MFMA operand).
+template <int TW_PF>
+__device__ __forceinline__ void tower_cross_handoff(const uint16_t *__restrict__ img, int img_bytes,
+                                                    int ksteps, int d, const char *gin, int s_g,
+                                                    const char *x0b, char *G, int s_x, char *dzo,
+                                                    int rotate) {
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int g = lane >> 4, r16 = lane & 15;
+  const int ntiles = tw_ceil(d, 16), ztiles = 2 * tw_ceil(d, 32);
+  f32x4 acc[TW_TPW];
+  tower_layer_acc<TW_PF>(acc, img, img_bytes, ksteps, ntiles, gin, s_g, rotate);
+#pragma unroll
+  for (int i = 0; i < TW_TPW; ++i) {
+    const int t = wave + TW_WAVES * i;
+    if (t >= ztiles) continue;  // uniform
+    const int c0 = 16 * t + 4 * g;
+    uint2 gq = make_uint2(0u, 0u), dq = make_uint2(0u, 0u);
+    if (t < ntiles) {
+      float gv[4] = {acc[i][0], acc[i][1], acc[i][2], acc[i][3]}, x0f[4], gr[4], dz[4];
+      gq = pack_bf16x4(gv);
+      unpack_bf16x4(gq, gr);
+      unpack_bf16x4(*reinterpret_cast<const uint2 *>(x0b + r16 * s_x + c0 * 2), x0f);
+#pragma unroll
+      for (int r = 0; r < 4; ++r) dz[r] = gr[r] * x0f[r];
+      dq = pack_bf16x4(dz);
+    }
+    *reinterpret_cast<uint2 *>(G + r16 * s_x + c0 * 2) = gq;
+    *reinterpret_cast<uint2 *>(dzo + r16 * s_g + c0 * 2) = dq;
+  }
+}
+
+// Cross layer c backward, G_{c+1} in the G block, dz_c = G_{c+1} x0 in dzi:
+//   G_c = dz_c Wc_c + G_{c+1},  dacc += G_{c+1} z_c (fp32, the x0-multiplier gradient);
+// LAST (c = 0): G block = bf16(G_0 + dacc) = dx0; else G block = bf16(G_c) and
+// dz_{c-1} = bf16(G_c x0) -> dzo.  Every lane reads and writes only its own G
+// elements (the MFMA operand is dzi), so G is updated in place.
+template <int TW_PF>
+__device__ __forceinline__ void tower_cross_bwd(const uint16_t *__restrict__ img, int img_bytes, int d,
+                                                const char *x0b, char *G, int s_x, const char *dzi,
+                                                char *dzo, int s_g, int rotate, const uint2 (&zq)[TW_TPW],
+                                                f32x4 (&dacc)[TW_TPW], bool last) {
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int g = lane >> 4, r16 = lane & 15;
+  const int ntiles = tw_ceil(d, 16), ztiles = 2 * tw_ceil(d, 32);
+  f32x4 acc[TW_TPW];
+  tower_layer_acc<TW_PF>(acc, img, img_bytes, tw_ceil(d, 32), ntiles, dzi, s_g, rotate);
+#pragma unroll
+  for (int i = 0; i < TW_TPW; ++i) {
+    const int t = wave + TW_WAVES * i;
+    if (t >= ztiles) continue;  // uniform
+    const int c0 = 16 * t + 4 * g;
+    char *gp = G + r16 * s_x + c0 * 2;
+    uint2 gq = make_uint2(0u, 0u), dq = make_uint2(0u, 0u);
+    if (t < ntiles) {  // pad columns: G, z, x0 and the weights are zero there
+      float go[4], zf[4], gn[4];
+      unpack_bf16x4(*reinterpret_cast<const uint2 *>(gp), go);
+      unpack_bf16x4(zq[i], zf);
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        gn[r] = acc[i][r] + go[r];
+        dacc[i][r] = fmaf(go[r], zf[r], dacc[i][r]);
+      }
+      if (last) {
+#pragma unroll
+        for (int r = 0; r < 4; ++r) gn[r] += dacc[i][r];
+        gq = pack_bf16x4(gn);
+      } else {
+        float x0f[4], gr[4], dz[4];
+        gq = pack_bf16x4(gn);
+        unpack_bf16x4(gq, gr);
+        unpack_bf16x4(*reinterpret_cast<const uint2 *>(x0b + r16 * s_x + c0 * 2), x0f);
+#pragma unroll
+        for (int r = 0; r < 4; ++r) dz[r] = gr[r] * x0f[r];
+        dq = pack_bf16x4(dz);
+      }
+    }
+    *reinterpret_cast<uint2 *>(gp) = gq;
+    if (!last) *reinterpret_cast<uint2 *>(dzo + r16 * s_g + c0 * 2) = dq;
   }
 }
 
@@ -330,7 +489,7 @@ __device__ __forceinline__ void tower_out(const TowerArgs &a, const char *blk, i
     if (a.stamps && tid == 0) s_stamp[(k)] = wall_clock64();                         \
   } while (0)
 
-template <int TW_PF, bool KC>
+template <int TW_PF, bool KC, bool CROSS>
 __global__ __launch_bounds__(TW_THREADS) void tower_kernel(TowerArgs a, KClock kc) {
   KcScope<KC> kc_scope(kc);
   extern __shared__ __attribute__((aligned(16))) char lds[];
@@ -374,12 +533,23 @@ __global__ __launch_bounds__(TW_THREADS) void tower_kernel(TowerArgs a, KClock k
     pxs[q] = (i < TW_ROWS * a.ns && row0 + r < a.B) ? a.xs[(row0 + r) * a.ld_xs + j] : 0.f;
   }
   const float pb0 = tid == 0 ? (a.head_b ? a.head_b[0] : 0.f) + (a.b2 ? a.b2[0] : 0.f) : 0.f;
+  float pcb[TW_MAXC];
+  if constexpr (CROSS) {
+#pragma unroll
+    for (int c = 0; c < TW_MAXC; ++c)
+      pcb[c] = (c < a.C && tid < a.width[0] && a.cbias[c]) ? a.cbias[c][tid] : 0.f;
+  }
   for (int i = tid * 16; i < a.off_p; i += TW_THREADS * 16)
     *reinterpret_cast<uint4 *>(lds + i) = make_uint4(0u, 0u, 0u, 0u);
   float *prm = reinterpret_cast<float *>(lds + a.off_p);
 #pragma unroll
   for (int l = 0; l < TW_MAXL; ++l)
     if (l < L && tid < a.width[l + 1]) prm[a.p_bias[l] + tid] = pb[l];
+  if constexpr (CROSS) {
+#pragma unroll
+    for (int c = 0; c < TW_MAXC; ++c)
+      if (c < a.C && tid < a.width[0]) prm[a.p_cbias[c] + tid] = pcb[c];
+  }
   if (tid < (H + 7) / 8 * 8) prm[a.p_hw + tid] = phw;  // zero past H: whole chunks
   if (tid < a.ns) prm[a.p_ws + tid] = pws;
   if (tid == 0) prm[a.p_b0] = pb0;
@@ -403,9 +573,42 @@ __global__ __launch_bounds__(TW_THREADS) void tower_kernel(TowerArgs a, KClock k
   __syncthreads();
   TW_STAMP(1);
 
+  // ---- cross network (CROSS): x_{c+1} = x0 * (x_c Wc_c^T + b_c) + x_c ------------
+  // z_c as bf16 in a shift register of the lane's registers: pushed here, popped in
+  // reverse layer order by the backward (compile-time indices, a runtime layer loop)
+  uint2 zs[CROSS ? TW_MAXC : 1][TW_TPW];
+#pragma unroll
+  for (int k = 0; k < (CROSS ? TW_MAXC : 1); ++k)
+#pragma unroll
+    for (int i = 0; i < TW_TPW; ++i) zs[k][i] = make_uint2(0u, 0u);
+  int off_in0 = a.off_x;
+  if constexpr (CROSS) {
+    const int d = a.width[0];
+    for (int c = 0; c < a.C; ++c) {
+      const char *in = lds + (c == 0 ? a.off_x : a.off_xc[(c - 1) & 1]);
+      char *out = lds + a.off_xc[c & 1];
+      uint2 zq[TW_TPW];
+      tower_cross_fwd<TW_PF>(a.cwf[c], a.cw_bytes, d, lds + a.off_x, in, a.s_x, out,
+                             prm + a.p_cbias[c], a.rotate, zq);
+#pragma unroll
+      for (int i = 0; i < TW_TPW; ++i) {
+#pragma unroll
+        for (int k = TW_MAXC - 1; k > 0; --k) zs[k][i] = zs[k - 1][i];
+        zs[0][i] = zq[i];
+      }
+      __syncthreads();
+      if (a.kfrag) {  // the cross weight gradients' X operands: x_0 = x0, x_{c+1}
+        if (c == 0)
+          tower_store_kfrag(lds + a.off_x, a.s_x, d, a.x0_img, a.nsteps, row0, a.B, a.store_mode);
+        tower_store_kfrag(out, a.s_x, d, a.cx_img[c], a.nsteps, row0, a.B, a.store_mode);
+      }
+    }
+    off_in0 = a.off_xc[(a.C - 1) & 1];
+  }
+
   // ---- forward: h_l = relu(h_{l-1} W_l^T + b_l) --------------------------------
   for (int l = 0; l < L; ++l) {
-    const char *in = lds + (l == 0 ? a.off_x : a.off_h[l - 1]);
+    const char *in = lds + (l == 0 ? off_in0 : a.off_h[l - 1]);
     const int s_in = l == 0 ? a.s_x : a.s_h[l - 1];
     tower_layer<false, TW_PF>(a.wf[l], a.wf_bytes[l], tw_ceil(a.width[l], 32), a.width[l + 1], in, s_in,
                        lds + a.off_h[l], a.s_h[l], prm + a.p_bias[l], nullptr, 0, a.rotate);
@@ -413,7 +616,7 @@ __global__ __launch_bounds__(TW_THREADS) void tower_kernel(TowerArgs a, KClock k
     TW_STAMP(2 + l);
     // x0's k-fragment image leaves behind layer 1 (x0's block stays in LDS): issued
     // before it, its stores delayed the first weight fragments by ~1 us
-    if (l == 0 && a.kfrag)
+    if (!CROSS && l == 0 && a.kfrag)
       tower_store_kfrag(lds + a.off_x, a.s_x, a.width[0], a.x0_img, a.nsteps, row0, a.B,
                         a.store_mode);
     if (l + 1 < L) tower_out(a, lds + a.off_h[l], a.s_h[l], a.width[l + 1], a.h_out[l], a.ld_h[l], row0);
@@ -535,12 +738,30 @@ __global__ __launch_bounds__(TW_THREADS) void tower_kernel(TowerArgs a, KClock k
     char *gout = lds + a.off_g[cur ^ 1];
     const char *mask = l > 0 ? lds + a.off_h[l - 1] : nullptr;
     const int s_mask = l > 0 ? a.s_h[l - 1] : 0;
-    tower_layer<true, TW_PF>(a.wb[l], a.wb_bytes[l], tw_ceil(a.width[l + 1], 32), a.width[l], gin, a.s_g, gout, a.s_g,
-                      nullptr, mask, s_mask, a.rotate);
+    if (CROSS && l == 0)  // dx_C -> G (off_xc[0], free in the backward), dz_{C-1} -> gout
+      tower_cross_handoff<TW_PF>(a.wb[0], a.wb_bytes[0], tw_ceil(a.width[1], 32), a.width[0], gin,
+                                 a.s_g, lds + a.off_x, lds + a.off_xc[0], a.s_x, gout, a.rotate);
+    else
+      tower_layer<true, TW_PF>(a.wb[l], a.wb_bytes[l], tw_ceil(a.width[l + 1], 32), a.width[l], gin,
+                               a.s_g, gout, a.s_g, nullptr, mask, s_mask, a.rotate);
     __syncthreads();
     TW_STAMP(7 + (L - 1 - l));
     if (l > 0) {
       tower_out(a, gout, a.s_g, a.width[l], a.dh_out[l - 1], a.ld_dh[l - 1], row0);
+    } else if (CROSS) {
+      if (tid == 0 && a.mode != MREC_TOWER_BCE) s_last = 0u;
+      if (tid == 0 && a.mode == MREC_TOWER_BCE) {
+        float lp = 0.f;
+        for (int m = 0; m < TW_ROWS; ++m) lp += f_loss[m];
+        __hip_atomic_store(a.loss_part + blockIdx.x, lp, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        const unsigned old = __hip_atomic_fetch_add(a.ticket, 1u, __ATOMIC_RELAXED,
+                                                    __HIP_MEMORY_SCOPE_AGENT);
+        s_last = old == gridDim.x - 1 ? 1u : 0u;
+      }
+      if (a.kfrag)
+        tower_store_kfrag(gout, a.s_g, a.width[0], a.cdz_img[a.C - 1], a.nsteps, row0, a.B,
+                          a.store_mode);
     } else {
       // the loss: this workgroup's partial as a write-through granule + a relaxed
       // agent ticket (cdna_hip_programming.md §6 G16), before the dx0 stores so the
@@ -558,6 +779,35 @@ __global__ __launch_bounds__(TW_THREADS) void tower_kernel(TowerArgs a, KClock k
       tower_store(gout, a.s_g, a.width[0], a.dx0, a.ld_dx0, row0, a.B, a.store_mode);
     }
     cur ^= 1;
+  }
+
+  // ---- cross backward (CROSS): dz_c in off_g[cur], G_{c+1} in off_xc[0] ------------
+  if constexpr (CROSS) {
+    const int d = a.width[0];
+    char *G = lds + a.off_xc[0];
+    f32x4 dacc[TW_TPW];
+#pragma unroll
+    for (int i = 0; i < TW_TPW; ++i) dacc[i] = f32x4{0.f, 0.f, 0.f, 0.f};
+    for (int c = a.C - 1; c >= 0; --c) {
+      uint2 zq[TW_TPW];
+#pragma unroll
+      for (int i = 0; i < TW_TPW; ++i) {  // pop z_c
+        zq[i] = zs[0][i];
+#pragma unroll
+        for (int k = 0; k + 1 < TW_MAXC; ++k) zs[k][i] = zs[k + 1][i];
+      }
+      char *dzo = lds + a.off_g[cur ^ 1];
+      tower_cross_bwd<TW_PF>(a.cwb[c], a.cw_bytes, d, lds + a.off_x, G, a.s_x, lds + a.off_g[cur],
+                             dzo, a.s_g, a.rotate, zq, dacc, c == 0);
+      __syncthreads();
+      if (c > 0) {
+        if (a.kfrag)
+          tower_store_kfrag(dzo, a.s_g, d, a.cdz_img[c - 1], a.nsteps, row0, a.B, a.store_mode);
+      } else {
+        tower_store(G, a.s_x, d, a.dx0, a.ld_dx0, row0, a.B, a.store_mode);
+      }
+      cur ^= 1;
+    }
   }
 
   // ---- the last ticket holder sums the loss partials (fixed order) ------------------
@@ -684,6 +934,15 @@ mrec_status mrec_tower_fwd_bwd(const mrec_tower_args *p, mrec_stream stream) {
   MREC_CHECK_ARG(s.ns >= 0 && s.ns <= TW_MAXNS && (s.ns == 0 || (s.xs && s.ws)),
                  "side linear: ns in [0, 64] with xs and ws");
   MREC_CHECK_ARG(s.ldp >= s.width[L] + 1 + s.ns, "ldp < N_L + 1 + ns");
+  const int C = s.n_cross;
+  MREC_CHECK_ARG(C >= 0 && C <= TW_MAXC, "n_cross must be in [0, 3]");
+  for (int c = 0; c < C; ++c) {
+    MREC_CHECK_ARG(s.cross_w_fwd[c] && s.cross_w_bwd[c], "NULL cross weight image");
+    if (kf && !fwd_only)
+      MREC_CHECK_ARG(al(s.cross_x_img[c]) && al(s.cross_dz_img[c]) && al(s.x0_img),
+                     "cross layers with kfrag need x0_img, cross_x_img and cross_dz_img "
+                     "(16-B aligned)");
+  }
   if (s.batch == 0) return MREC_OK;
 
   TowerArgs a{};
@@ -740,14 +999,28 @@ mrec_status mrec_tower_fwd_bwd(const mrec_tower_args *p, mrec_stream stream) {
   a.x0_img = kf ? static_cast<uint16_t *>(s.x0_img) : nullptr;
   a.mode = s.mode;
   a.dz_in = s.dz_in;
+  a.C = C;
+  a.cw_bytes = static_cast<int>(tower_img_elems_fwd(s.width[0], s.width[0]) * 2);
+  for (int c = 0; c < C; ++c) {
+    a.cwf[c] = static_cast<const uint16_t *>(s.cross_w_fwd[c]);
+    a.cwb[c] = static_cast<const uint16_t *>(s.cross_w_bwd[c]);
+    a.cbias[c] = s.cross_bias[c];
+    a.cx_img[c] = kf ? static_cast<uint16_t *>(s.cross_x_img[c]) : nullptr;
+    a.cdz_img[c] = kf ? static_cast<uint16_t *>(s.cross_dz_img[c]) : nullptr;
+  }
   if (a.mode == MREC_TOWER_FORWARD) {  // nothing leaves but z
     a.x0_img = nullptr;
     for (int l = 0; l < L; ++l) a.h_out[l] = nullptr;
+    a.kfrag = 0;  // (the cross images)
   }
   int off = 0;
   a.off_x = off;
   a.s_x = tw_stride(s.width[0]);
   off += TW_ROWS * a.s_x;
+  for (int q = 0; q < (C > 0 ? 2 : 0); ++q) {  // x_c ping-pong (G in the backward)
+    a.off_xc[q] = off;
+    off += TW_ROWS * a.s_x;
+  }
   for (int l = 0; l < L; ++l) {
     a.off_h[l] = off;
     a.s_h[l] = tw_stride(s.width[l + 1]);
@@ -783,15 +1056,22 @@ mrec_status mrec_tower_fwd_bwd(const mrec_tower_args *p, mrec_stream stream) {
   np += TW_ROWS;
   a.p_part = np;
   np += s.width[L] + 1 + s.ns;
+  for (int c = 0; c < C; ++c) {
+    np = (np + 3) / 4 * 4;
+    a.p_cbias[c] = np;
+    np += s.width[0];
+  }
   off += np * 4;
   a.lds_bytes = (off + 15) / 16 * 16;
   constexpr int kMaxDyn = 160 * 1024 - 256;  // the kernel's static LDS (s_last) is on top
   MREC_CHECK_ARG(a.lds_bytes <= kMaxDyn, "activation blocks exceed the 160 KiB LDS");
   static int attr_set = [] {
-    for (const void *k : {reinterpret_cast<const void *>(tower_kernel<4, false>),
-                          reinterpret_cast<const void *>(tower_kernel<6, false>),
-                          reinterpret_cast<const void *>(tower_kernel<8, false>),
-                          reinterpret_cast<const void *>(tower_kernel<TW_PF_DEFAULT, true>)})
+    for (const void *k : {reinterpret_cast<const void *>(tower_kernel<4, false, false>),
+                          reinterpret_cast<const void *>(tower_kernel<6, false, false>),
+                          reinterpret_cast<const void *>(tower_kernel<8, false, false>),
+                          reinterpret_cast<const void *>(tower_kernel<TW_PF_DEFAULT, true, false>),
+                          reinterpret_cast<const void *>(tower_kernel<TW_PF_DEFAULT, false, true>),
+                          reinterpret_cast<const void *>(tower_kernel<TW_PF_DEFAULT, true, true>)})
       (void)hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, kMaxDyn);
     (void)hipGetLastError();  // a refused attribute must not read as a failed launch
     return 1;
@@ -806,14 +1086,20 @@ mrec_status mrec_tower_fwd_bwd(const mrec_tower_args *p, mrec_stream stream) {
   const int64_t grid = (s.batch + TW_ROWS - 1) / TW_ROWS;
   const dim3 gd(static_cast<unsigned>(grid));
   const KClock kc = kclock_take();
-  if (kc.buf)  // (the clocked instantiation is the default prefetch depth's)
-    tower_kernel<TW_PF_DEFAULT, true><<<gd, TW_THREADS, a.lds_bytes, st>>>(a, kc);
-  else if (pf_env == 8)
-    tower_kernel<8, false><<<gd, TW_THREADS, a.lds_bytes, st>>>(a, kc);
-  else if (pf_env == 6)
-    tower_kernel<6, false><<<gd, TW_THREADS, a.lds_bytes, st>>>(a, kc);
-  else
-    tower_kernel<4, false><<<gd, TW_THREADS, a.lds_bytes, st>>>(a, kc);
+  if (C > 0) {  // the cross network runs at the default prefetch depth
+    if (kc.buf)
+      tower_kernel<TW_PF_DEFAULT, true, true><<<gd, TW_THREADS, a.lds_bytes, st>>>(a, kc);
+    else
+      tower_kernel<TW_PF_DEFAULT, false, true><<<gd, TW_THREADS, a.lds_bytes, st>>>(a, kc);
+  } else if (kc.buf) {  // (the clocked instantiation is the default prefetch depth's)
+    tower_kernel<TW_PF_DEFAULT, true, false><<<gd, TW_THREADS, a.lds_bytes, st>>>(a, kc);
+  } else if (pf_env == 8) {
+    tower_kernel<8, false, false><<<gd, TW_THREADS, a.lds_bytes, st>>>(a, kc);
+  } else if (pf_env == 6) {
+    tower_kernel<6, false, false><<<gd, TW_THREADS, a.lds_bytes, st>>>(a, kc);
+  } else {
+    tower_kernel<4, false, false><<<gd, TW_THREADS, a.lds_bytes, st>>>(a, kc);
+  }
   return launch_status("mrec_tower_fwd_bwd");
 }
 

@@ -38,7 +38,7 @@ namespace mrec {
 #define MREC_DW_PF 4
 #endif
 constexpr int DW_PF = MREC_DW_PF;  // k steps of fragments in flight per wave
-constexpr int DW_MAXL = 4;
+constexpr int DW_MAXL = 8;
 constexpr int DW_TILE = 64;    // output tile edge of one wave (4 MFMA tiles)
 constexpr int DW_OOB = 1 << 30;  // a voffset past every image: the load returns zeros
 
@@ -231,7 +231,7 @@ mrec_status mrec_tower_dw(const mrec_tower_dw_args *p, const mrec_head_finish_jo
                           mrec_stream stream) {
   MREC_CHECK_ARG(p != nullptr, "NULL args");
   const mrec_tower_dw_args &s = *p;
-  MREC_CHECK_ARG(s.n_layers >= 1 && s.n_layers <= DW_MAXL, "n_layers must be in [1, 4]");
+  MREC_CHECK_ARG(s.n_layers >= 1 && s.n_layers <= DW_MAXL, "n_layers must be in [1, 8]");
   MREC_CHECK_ARG(s.batch >= 0, "negative batch");
   MREC_CHECK_ARG(s.splits >= 1 && s.splits <= 64, "splits out of [1, 64]");
   {  // the split count the REDUCE jobs use (mrec_gemm_workspace_size(.., K = batch, splits))

@@ -1144,15 +1144,32 @@ def ctr_head_bce(h: torch.Tensor, weight: torch.Tensor, bias: Optional[torch.Ten
 
 TOWER = os.environ.get("MREC_TOWER", "1") == "1"
 TOWER_MAXL, TOWER_MAXW = 4, 512
+# DCN-v2 cross layers inside the tower launch (MREC_TOWER_CROSS=0: the layered
+# cross network of _CrossNetFn ahead of the tower)
+TOWER_CROSS = os.environ.get("MREC_TOWER_CROSS", "1") == "1"
+TOWER_MAXC = 3
 
 
 def _mlp_linears(mlp) -> list:
     return [m.linear for m in mlp.mlp] if hasattr(mlp, "mlp") else list(mlp)
 
 
-def tower_supported(x0: torch.Tensor, mlp, head: torch.nn.Linear, xs=None) -> bool:
+def tower_supported(x0: torch.Tensor, mlp, head: torch.nn.Linear, xs=None, cross=None) -> bool:
     """The fused tower covers the reference MLP (Linear -> ReLU per layer,
-    Dense.py:4-24) with dropout 0 (or eval) + Linear(N_L, 1) + BCE on the GPU."""
+    Dense.py:4-24) with dropout 0 (or eval) + Linear(N_L, 1) + BCE on the GPU, and
+    up to 3 DCN-v2 cross layers (``nn.Linear(d, d)``, d = the MLP's input width)
+    ahead of it when the batch takes mrec_tower_dw."""
+    if cross:
+        lins = _mlp_linears(mlp) if (hasattr(mlp, "mlp") and mlp.mlp) else None
+        if not TOWER_CROSS or not lins or len(cross) > TOWER_MAXC:
+            return False
+        d = lins[0].in_features
+        if any(c.in_features != d or c.out_features != d or c.weight.dtype != torch.float32
+               or not c.weight.is_contiguous() for c in cross):
+            return False
+        widths = [d] * len(cross) + [d] + [l.out_features for l in lins]
+        if not _tdw_splits(x0.shape[0], widths):
+            return False
     if not (TOWER and x0.is_cuda and torch.is_grad_enabled() and x0.dtype == _BF16):
         return False
     dense_layers = list(mlp.mlp) if hasattr(mlp, "mlp") else None
@@ -1223,23 +1240,32 @@ class _TowerBCEFn(torch.autograd.Function):
     plain SGD, the split-K reductions ride in the next launch)."""
 
     @staticmethod
-    def forward(ctx, x0, base, xs, y, n_layers, *params):
-        L = n_layers
+    def forward(ctx, x0, base, xs, y, n_layers, n_cross, *params):
+        L, C = n_layers, n_cross
         Ws, bs = params[:L], params[L:2 * L]
         head_w, head_b, ws, b2 = params[2 * L:2 * L + 4]
+        cWs, cbs = params[2 * L + 4:2 * L + 4 + C], params[2 * L + 4 + C:2 * L + 4 + 2 * C]
         B = x0.shape[0]
         dev = x0.device
         widths = [Ws[0].shape[1]] + [W.shape[0] for W in Ws]
         imgs = [tower_images(W) for W in Ws]
+        cimgs = [tower_images(W) for W in cWs]
         # the weight gradients' operands: k-fragment images for mrec_tower_dw (the
         # tower writes them, x0's too), else row-major for the generic GEMM
-        tdw = _tdw_splits(B, widths) if any(ctx.needs_input_grad[5:5 + 2 * L]) else 0
+        need_w = any(ctx.needs_input_grad[6:6 + 2 * L]) or any(
+            ctx.needs_input_grad[6 + 2 * L + 4:6 + 2 * L + 4 + 2 * C])
+        tdw = _tdw_splits(B, [widths[0]] * C + widths) if need_w else 0
+        if C and need_w and not tdw:
+            raise ValueError("cross layers in the tower need mrec_tower_dw (tower_supported)")
+        cx_imgs, cdz_imgs = [], []
         if tdw:
             kf = lambda n: torch.empty(int(_mrec.lib().mrec_kfrag_elems(B, n)), dtype=_BF16,  # noqa: E731
                                        device=dev)
             hs = [kf(widths[l + 1]) for l in range(L - 1)]
             dhs = [kf(widths[l + 1]) for l in range(L)]
             x0_img = kf(widths[0])
+            cx_imgs = [kf(widths[0]) for _ in range(C)]
+            cdz_imgs = [kf(widths[0]) for _ in range(C)]
         else:
             hs = [_alloc(B, widths[l + 1], _BF16, dev) for l in range(L - 1)]
             dhs = [_alloc(B, widths[l + 1], _BF16, dev) for l in range(L)]
@@ -1278,6 +1304,13 @@ class _TowerBCEFn(torch.autograd.Function):
             if l < L - 1:
                 a.h_out[l], a.ld_h[l] = hs[l].data_ptr(), hs[l].stride(0)
         a.kfrag, a.x0_img = int(bool(tdw)), _mrec.ptr(x0_img)
+        cbsd = [f32(b) for b in cbs]
+        a.n_cross = C
+        for c in range(C):
+            a.cross_w_fwd[c], a.cross_w_bwd[c] = cimgs[c][0].data_ptr(), cimgs[c][1].data_ptr()
+            a.cross_bias[c] = _mrec.ptr(cbsd[c])
+            if tdw:
+                a.cross_x_img[c], a.cross_dz_img[c] = cx_imgs[c].data_ptr(), cdz_imgs[c].data_ptr()
         a.head_w, a.head_b, a.base = hw.data_ptr(), _mrec.ptr(hb), _mrec.ptr(base_c)
         a.xs, a.ld_xs, a.ns = _mrec.ptr(xs), xs.stride(0) if xs is not None else 0, ns
         a.ws, a.b2, a.y = _mrec.ptr(wsd), _mrec.ptr(b2d), yc.data_ptr()
@@ -1287,10 +1320,12 @@ class _TowerBCEFn(torch.autograd.Function):
         a.loss_part, a.ticket, a.loss = loss_part.data_ptr(), _ticket(dev).data_ptr(), loss.data_ptr()
         with _timed("mrec_tower_fwd_bwd"):
             _mrec.call("mrec_tower_fwd_bwd", ctypes.byref(a), _mrec.stream_handle())
-        ctx.save_for_backward(x0 if x0_img is None else x0_img, dz, part, dx0, *hs, *dhs)
-        ctx.L, ctx.B, ctx.H, ctx.ns, ctx.widths = L, B, H, ns, widths
+        ctx.save_for_backward(x0 if x0_img is None else x0_img, dz, part, dx0, *hs, *dhs, *cx_imgs,
+                              *cdz_imgs)
+        ctx.L, ctx.C, ctx.B, ctx.H, ctx.ns, ctx.widths = L, C, B, H, ns, widths
         ctx.tdw = tdw
         ctx.Ws, ctx.bs, ctx.imgs = Ws, bs, imgs
+        ctx.cWs, ctx.cbs, ctx.cimgs = cWs, cbs, cimgs
         ctx.head = (head_w, head_b, ws, b2)
         ctx.has_base = base is not None
         ctx.mark_non_differentiable(dz)
@@ -1298,10 +1333,12 @@ class _TowerBCEFn(torch.autograd.Function):
 
     @staticmethod
     def backward(ctx, gloss):
-        L, B = ctx.L, ctx.B
+        L, C, B = ctx.L, ctx.C, ctx.B
         saved = ctx.saved_tensors
         x0, dz, part, dx0 = saved[:4]
-        hs, dhs = list(saved[4:4 + L - 1]), list(saved[4 + L - 1:])
+        hs, dhs = list(saved[4:4 + L - 1]), list(saved[4 + L - 1:4 + 2 * L - 1])
+        cx_imgs = list(saved[4 + 2 * L - 1:4 + 2 * L - 1 + C]) if ctx.tdw else []
+        cdz_imgs = list(saved[4 + 2 * L - 1 + C:]) if ctx.tdw else []
         dev = part.device
         g = gloss.detach().float().reshape(1).contiguous()
         one = g.data_ptr() == grad_one(dev).data_ptr()
@@ -1311,29 +1348,49 @@ class _TowerBCEFn(torch.autograd.Function):
             dx0 = (dx0.float() * g).to(_BF16) if dx0 is not None else None
             dhs = [(d.float() * g).to(_BF16) if tdw else _bf16_rows((d.float() * g).to(_BF16))
                    for d in dhs]
+            cdz_imgs = [(d.float() * g).to(_BF16) for d in cdz_imgs]
+        cross = None
+        if C:  # cross layer c: dW = dz_c^T [x_c | 1]; the MLP's first X is x_C
+            d = ctx.widths[0]
+            cross = (ctx.cWs, ctx.cbs, ctx.cimgs, [(d, d)] * C, cdz_imgs, [x0] + cx_imgs[:-1])
+            if tdw:
+                x0 = cx_imgs[-1]
+        need_w = any(ctx.needs_input_grad[6:6 + 2 * L]) or any(
+            ctx.needs_input_grad[6 + 2 * L + 4:6 + 2 * L + 4 + 2 * C])
         grads = _tower_param_grads(ctx.widths, ctx.Ws, ctx.bs, ctx.imgs, ctx.head, B, ctx.H, ctx.ns,
-                                   x0, hs, dhs, part, g, one, tdw,
-                                   any(ctx.needs_input_grad[5:5 + 2 * L]))
-        dWs, dbs, (dW_h, db_h, dws, db2) = grads
-        return (dx0, dz if ctx.has_base else None, None, None, None, *dWs, *dbs,
-                dW_h, db_h, dws, db2)
+                                   x0, hs, dhs, part, g, one, tdw, need_w, cross=cross)
+        dWs, dbs, (dW_h, db_h, dws, db2), (cdWs, cdbs) = grads
+        return (dx0, dz if ctx.has_base else None, None, None, None, None, *dWs, *dbs,
+                dW_h, db_h, dws, db2, *cdWs, *cdbs)
 
 
 def _tower_param_grads(widths, Ws, bs, imgs, head, B: int, H: int, ns: int, x0, hs, dhs, part, g,
-                       one: bool, tdw: int, need_w: bool):
+                       one: bool, tdw: int, need_w: bool, cross=None):
     """The weight-gradient tail of a fused tower (BCE and given-dz modes): the L
     layers' dW = dh^T [h | 1] (mrec_tower_dw from the k-fragment images, else the
     generic split-K GEMMs) + the head parameters from the tower's partials; fused
-    SGD / flat DP buffer / returned gradients as the parameters ask.  ->
-    (dWs, dbs, (dW_h, db_h, dws, db2)), None where not returned."""
+    SGD / flat DP buffer / returned gradients as the parameters ask.  ``cross``
+    (Ws, bs, imgs, dims, dys, xs): the cross layers ahead of the MLP, their dW =
+    dz^T [x | 1] in the same mrec_tower_dw launch (tdw required).  ->
+    (dWs, dbs, (dW_h, db_h, dws, db2), (cross dWs, cross dbs)), None where not
+    returned."""
     head_w, head_b, ws, b2 = head
     L = len(Ws)
     dev = part.device
     xin = ([x0] if tdw else [x0[:, :widths[0]]]) + hs
-    # --- weight gradients of the L layers: one launch ---
-    lr = sgd_lr(*Ws, *bs)
-    dpg = dp_grads(*Ws, *bs) if lr is None else None
-    dWs, dbs = [None] * L, [None] * L
+    # every layer of the launch: (W, b, images, N, K, dY, X); cross layers first
+    lay = []
+    if cross is not None:
+        cW, cb, cim, cdims, cdy, cx = cross
+        lay += [(cW[c], cb[c], cim[c], cdims[c][0], cdims[c][1], cdy[c] if tdw else None,
+                 cx[c] if tdw else None) for c in range(len(cW))]
+    C = len(lay)
+    lay += [(Ws[l], bs[l], imgs[l], widths[l + 1], widths[l], dhs[l], xin[l]) for l in range(L)]
+    # --- weight gradients of the layers: one launch ---
+    lr = sgd_lr(*[t[0] for t in lay], *[t[1] for t in lay])
+    dpg = dp_grads(*[t[0] for t in lay], *[t[1] for t in lay]) if lr is None else None
+    n = len(lay)
+    dWs, dbs = [None] * n, [None] * n
     calls = []
     if need_w:
         sk = tdw or _split_tower(widths, B)
@@ -1341,26 +1398,23 @@ def _tower_param_grads(widths, Ws, bs, imgs, head, B: int, H: int, ns: int, x0, 
         # with mrec_tower_dw the calls below only carry the REDUCE phase's
         # arguments (its operands are never read: k-fragment images as stand-ins)
         opnd = (lambda t: t.view(-1, 8)) if tdw else (lambda t: t)  # noqa: E731
-        for l in range(L):
-            N, K = widths[l + 1], widths[l]
-            bias_l = bs[l]
+        for i, (W, bias_l, img, N, K, dy, xx) in enumerate(lay):
             if lr is not None:
-                c = _Call(opnd(dhs[l]), _mrec.LAYOUT_COL, opnd(xin[l]), _mrec.LAYOUT_COL, N, K, B, ph,
+                c = _Call(opnd(dy), _mrec.LAYOUT_COL, opnd(xx), _mrec.LAYOUT_COL, N, K, B, ph,
                           ones_out=bias_l.detach() if bias_l is not None else None,
-                          out=Ws[l].detach(), out_dtype=torch.float32, split_k=sk, sgd_lr=lr,
-                          img_row=imgs[l][0], img_tr=imgs[l][1],
-                          img_kind=_mrec.IMG_TOWER)
-                images_updated(Ws[l], "tower")
+                          out=W.detach(), out_dtype=torch.float32, split_k=sk, sgd_lr=lr,
+                          img_row=img[0], img_tr=img[1], img_kind=_mrec.IMG_TOWER)
+                images_updated(W, "tower")
             elif dpg is not None:
-                c = _Call(opnd(dhs[l]), _mrec.LAYOUT_COL, opnd(xin[l]), _mrec.LAYOUT_COL, N, K, B, ph,
-                          ones_out=dpg[L + l], out=dpg[l], out_dtype=torch.float32,
+                c = _Call(opnd(dy), _mrec.LAYOUT_COL, opnd(xx), _mrec.LAYOUT_COL, N, K, B, ph,
+                          ones_out=dpg[n + i], out=dpg[i], out_dtype=torch.float32,
                           split_k=sk)
             else:
-                dWs[l] = torch.empty(N, K, dtype=torch.float32, device=dev)
-                dbs[l] = (torch.empty(N, dtype=torch.float32, device=dev)
+                dWs[i] = torch.empty(N, K, dtype=torch.float32, device=dev)
+                dbs[i] = (torch.empty(N, dtype=torch.float32, device=dev)
                           if bias_l is not None else None)
-                c = _Call(opnd(dhs[l]), _mrec.LAYOUT_COL, opnd(xin[l]), _mrec.LAYOUT_COL, N, K, B, ph,
-                          ones_out=dbs[l], out=dWs[l], out_dtype=torch.float32, split_k=sk)
+                c = _Call(opnd(dy), _mrec.LAYOUT_COL, opnd(xx), _mrec.LAYOUT_COL, N, K, B, ph,
+                          ones_out=dbs[i], out=dWs[i], out_dtype=torch.float32, split_k=sk)
             calls.append(c)
     # --- the head's parameters (w, b, ws, b2): fixed-order partial sums ---
     hlr = sgd_lr(head_w, head_b, ws, b2)
@@ -1383,9 +1437,10 @@ def _tower_param_grads(widths, Ws, bs, imgs, head, B: int, H: int, ns: int, x0, 
                    g.data_ptr(), 0, 0.0, None, None, None, None, dW_h.data_ptr(),
                    _mrec.ptr(db_h), _mrec.ptr(dws), _mrec.ptr(db2), _mrec.stream_handle())
     if calls and tdw:
-        _tower_dw(calls, dhs, xin, widths, B, tdw)
+        _tower_dw(calls, [t[5] for t in lay], [t[6] for t in lay], [(t[3], t[4]) for t in lay], B,
+                  tdw)
         if lr is None and dpg is None:
-            _run([c.with_phase(_mrec.GEMM_REDUCE) for c in calls])
+            _run_all([c.with_phase(_mrec.GEMM_REDUCE) for c in calls])
         else:
             for c in calls:
                 _defer(c)
@@ -1395,52 +1450,58 @@ def _tower_param_grads(widths, Ws, bs, imgs, head, B: int, H: int, ns: int, x0, 
             if lr is None and dpg is None:
                 # returned gradients: autograd may copy them on return, so they must
                 # be complete before this backward returns
-                _run([c.with_phase(_mrec.GEMM_REDUCE) for c in calls])
+                _run_all([c.with_phase(_mrec.GEMM_REDUCE) for c in calls])
             else:  # in-place SGD / flat DP buffer: ride in the next launches
                 for c in calls:
                     _defer(c)
     else:
         _flush_finish()
-    return dWs, dbs, (dW_h, db_h, dws, db2)
+    return dWs[C:], dbs[C:], (dW_h, db_h, dws, db2), (dWs[:C], dbs[:C])
 
 
-def _tower_dw(calls, dhs, xin, widths, B: int, splits: int):
+def _run_all(jobs):
+    for i in range(0, len(jobs), 4):
+        _run(jobs[i:i + 4])
+
+
+def _tower_dw(calls, dys, xins, dims, B: int, splits: int):
     """The tower's weight-gradient partial slabs by mrec_tower_dw from the
     k-fragment images (+ the deferred CTR head finish in the same launch); the
     split-K REDUCE of each call (fused SGD / flat DP buffer / returned gradient)
     follows as usual.  Pending reductions that write what this reads run first."""
     global _PENDING
-    reads = {t.data_ptr() for t in list(dhs) + list(xin)}
+    reads = {t.data_ptr() for t in list(dys) + list(xins)}
     if any(p.writes & reads for p in _PENDING):
-        _run(_PENDING)
+        _run_all(_PENDING)
         _PENDING = []
     a = _mrec.TowerDwArgs()
     a.n_layers, a.batch, a.splits = len(calls), B, splits
     for l, c in enumerate(calls):
-        a.n_out[l], a.n_in[l] = widths[l + 1], widths[l]
-        a.dy_img[l], a.x_img[l] = dhs[l].data_ptr(), xin[l].data_ptr()
-        a.ws[l], a.ldws[l] = c.ws.data_ptr(), (widths[l] + 1 + 7) // 8 * 8
+        a.n_out[l], a.n_in[l] = dims[l]
+        a.dy_img[l], a.x_img[l] = dys[l].data_ptr(), xins[l].data_ptr()
+        a.ws[l], a.ldws[l] = c.ws.data_ptr(), (dims[l][1] + 1 + 7) // 8 * 8
     fin = _FINISH.pop(0) if _FINISH else None
     with _timed("mrec_tower_dw"):
         _mrec.call("mrec_tower_dw", ctypes.byref(a), ctypes.byref(fin.struct) if fin else None,
                    _mrec.stream_handle())
     pend = _PENDING
     _PENDING = []
-    for i in range(0, len(pend), 4):
-        _run(pend[i:i + 4])
+    _run_all(pend)
 
 
 def tower_bce(x0: torch.Tensor, mlp, head: torch.nn.Linear, base: Optional[torch.Tensor],
               y: torch.Tensor, xs: Optional[torch.Tensor] = None, ws: Optional[torch.Tensor] = None,
-              b2: Optional[torch.Tensor] = None) -> torch.Tensor:
+              b2: Optional[torch.Tensor] = None, cross=None) -> torch.Tensor:
     """Training loss of a CTR model's deep part: mean BCE-with-logits of
     MLP(x0) . head.weight + head.bias + base (+ xs . ws + b2) — the reference MLP
     (MLP.py:8-23) and Linear(N_L, 1) — as one fused tower launch (caller checks
-    ``tower_supported``)."""
+    ``tower_supported``).  ``cross``: DCN-v2 cross layers (``nn.Linear(d, d)``)
+    applied to x0 ahead of the MLP in the same launch (mrec_tower_args.n_cross)."""
     lins = _mlp_linears(mlp)
+    cross = list(cross or [])
     params = ([l.weight for l in lins] + [l.bias for l in lins] +
-              [head.weight, head.bias, ws, b2])
-    return _TowerBCEFn.apply(x0, base, xs, y, len(lins), *params)
+              [head.weight, head.bias, ws, b2] + [c.weight for c in cross] + [c.bias for c in cross])
+    return _TowerBCEFn.apply(x0, base, xs, y, len(lins), len(cross), *params)
 
 
 class _ScoreTowerFn(torch.autograd.Function):
@@ -1525,7 +1586,7 @@ class _ScoreTowerFn(torch.autograd.Function):
         a.mode, a.dz_in = _mrec.TOWER_GIVEN_DZ, ds.data_ptr()
         _mrec.call("mrec_tower_fwd_bwd", ctypes.byref(a), _mrec.stream_handle())
         g = grad_one(dev)
-        dWs, dbs, (dW_h, db_h, _, _) = _tower_param_grads(
+        dWs, dbs, (dW_h, db_h, _, _), _ = _tower_param_grads(
             widths, ctx.Ws, ctx.bs, ctx.imgs, ctx.head, B, H, 0, x0_img if tdw else x0, hs, dhs,
             part, g, True, tdw, need_w)
         return (dx0, None, *dWs, *dbs, dW_h, db_h)

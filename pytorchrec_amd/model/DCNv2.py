@@ -68,11 +68,15 @@ class DCNv2(_CTRBase):
             for m in (self.cross, self.mlp, self.prediction):
                 m.to(dev)
 
-    def _cross(self, data: Dict[str, Tensor]):
+    def _x0(self, data: Dict[str, Tensor]):
         x0, _ = interact(self.embeddings, self._ids(data), self._dense(data), None, None,
                          fm2=False, first_order=False, x0_cols=self.x0_cols,
                          x0_dtype=self._x0_dtype())
-        return dense_ops.cross_net(x0, [c.weight for c in self.cross], [c.bias for c in self.cross])
+        return x0
+
+    def _cross(self, data: Dict[str, Tensor]):
+        return dense_ops.cross_net(self._x0(data), [c.weight for c in self.cross],
+                                   [c.bias for c in self.cross])
 
     def _deep(self, data: Dict[str, Tensor]):
         return self.mlp(self._cross(data))
@@ -82,9 +86,16 @@ class DCNv2(_CTRBase):
         return dense_ops.head(h, self.prediction.weight, self.prediction.bias), self._target(data)
 
     def fused_bce_loss(self, data: Dict[str, Tensor]):
-        """Training loss (BCE with logits, mean): the deep MLP, the output layer and the
-        loss as one fused tower launch (or the output layer fused into the loss)."""
-        x = self._cross(data)
+        """Training loss (BCE with logits, mean): the cross network, the deep MLP, the
+        output layer and the loss as one fused tower launch (cross layers as tower
+        layers with the x0 * (W x + b) + x epilogue, mrec_tower_args.n_cross), else
+        the layered cross network ahead of the tower / the output layer fused into
+        the loss."""
+        x0 = self._x0(data)
+        if dense_ops.tower_supported(x0, self.mlp, self.prediction, cross=list(self.cross)):
+            return dense_ops.tower_bce(x0, self.mlp, self.prediction, None, self._target(data),
+                                       cross=list(self.cross))
+        x = dense_ops.cross_net(x0, [c.weight for c in self.cross], [c.bias for c in self.cross])
         if dense_ops.tower_supported(x, self.mlp, self.prediction):
             return dense_ops.tower_bce(x, self.mlp, self.prediction, None, self._target(data))
         loss, _ = dense_ops.ctr_head_bce(self.mlp(x), self.prediction.weight,

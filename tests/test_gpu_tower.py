@@ -258,3 +258,93 @@ def test_score_tower_matches_layered_path_and_fp64(gpu, widths, B):
         close(got[f"db{l}"], wb, f"db{l}")
     close(got["dW_head"].reshape(-1), acts[-1].T @ dz, "dW_head")
     close(got["db_head"], np.array([dz.sum()]), "db_head")
+
+
+@pytest.mark.parametrize("d,mlp_w,C,B", [(429, (400, 400), 3, 4096), (45, (70, 33), 2, 1000),
+                                         (100, (64,), 1, 513), (16, (48, 32, 17), 3, 600)])
+def test_cross_tower_matches_layered_path_and_fp64(gpu, d, mlp_w, C, B):
+    """DCN-v2 cross layers inside the tower launch (mrec_tower_args.n_cross: x_{c+1} =
+    x0 * (x_c W_c^T + b_c) + x_c on the x0 block, z_c kept on chip, the cross dW
+    from the tower's k-fragment images in the same mrec_tower_dw launch) against
+
+      * the layered path (dense.cross_net: one mrec_gemm per layer + the
+        mrec_dcn_cross_bwd_prep elementwise stage, then the MLP tower): the same
+        bf16 rounding points except dx0, which the fused path rounds once (fp32
+        sum of G_0 and every G_{c+1} z_c) -- loss within 1e-6, every gradient within
+        0.1 % of its magnitude on average, 99.9 % of the elements within 1 %
+        (dx0: 0.3 % / 3 %, bias gradients 0.4 % / 4 %), the loss within 1e-5;
+      * the fp64 oracle (ref.dcn_cross_fwd / _bwd + ref.mlp_fwd / _bwd) on the same
+        bf16 x0 and bf16-rounded weights: l2 within 8e-2, as the MLP tower's test."""
+    from pytorchrec_amd import dense as D
+    widths = (d,) + tuple(mlp_w)
+    mlp, head = _mlp(widths, gpu, seed=B + C)
+    torch.manual_seed(B + 11)
+    cross = [torch.nn.Linear(d, d).to(gpu) for _ in range(C)]
+    with torch.no_grad():
+        for c in cross:
+            c.weight.normal_(0, 1.0 / np.sqrt(d))
+            c.bias.normal_(0, 0.1)
+    x0 = _x0(B, d, gpu, seed=B + 12)
+    g = torch.Generator().manual_seed(B + 13)
+    y = (torch.rand(B, generator=g) < 0.3).float().to(gpu)
+    lins = [l.linear for l in mlp.mlp]
+    params = list(mlp.parameters()) + list(head.parameters()) + [p for c in cross for p in c.parameters()]
+
+    xg = x0.detach().requires_grad_()
+    assert D.tower_supported(xg, mlp, head, cross=cross)
+    loss = D.tower_bce(xg, mlp, head, None, y, cross=cross)
+    loss.backward()
+    got = {"dx0": xg.grad.clone()}
+    for i, l in enumerate(cross + lins):
+        got[f"dW{i}"], got[f"db{i}"] = l.weight.grad.clone(), l.bias.grad.clone()
+    got["dW_head"], got["db_head"] = head.weight.grad.clone(), head.bias.grad.clone()
+
+    for p in params:
+        p.grad = None
+    xl = x0.detach().requires_grad_()
+    x = D.cross_net(xl, [c.weight for c in cross], [c.bias for c in cross])
+    loss2, _ = D.ctr_head_bce(mlp(x), head.weight, head.bias, None, y)
+    loss2.backward()
+    # the k steps of a layer are summed in a per-workgroup rotated order in the tower
+    # (the GEMM's is fixed): a 1-ulp flip of an x_c element feeds every later layer
+    # through both the product and the residual, so the loss bar is 1e-5 here
+    assert abs(float(loss) - float(loss2)) <= 1e-5 * abs(float(loss2)) + 1e-7
+    want = {"dx0": xl.grad}
+    for i, l in enumerate(cross + lins):
+        want[f"dW{i}"], want[f"db{i}"] = l.weight.grad, l.bias.grad
+    want["dW_head"], want["db_head"] = head.weight.grad, head.bias.grad
+    for name in want:
+        a, b = got[name].double().cpu(), want[name].double().cpu().reshape(got[name].shape)
+        mag = float(b.abs().max()) + 1e-30
+        err = (a - b).abs()
+        # dx0 is rounded once here (three times on the layered path); the bias
+        # gradients sum B terms with heavy cancellation, so a few 1-ulp flips of
+        # dz (the rotated k order) move them by ~2^-9 of their magnitude (the score
+        # tower's bar)
+        k = 3.0 if name == "dx0" else (4.0 if name.startswith("db") else 1.0)
+        assert float(err.mean()) <= k * 1e-3 * mag, (name, float(err.mean()) / mag)
+        assert float((err > k * 1e-2 * mag).double().mean()) <= 1e-3, name
+
+    clay = [(ref.bf16_round(c.weight.detach().cpu().numpy()), c.bias.detach().cpu().numpy())
+            for c in cross]
+    layers = [(ref.bf16_round(l.weight.detach().cpu().numpy()), l.bias.detach().cpu().numpy())
+              for l in lins]
+    xs, zs = ref.dcn_cross_fwd(x0.detach().float().cpu().numpy(), clay)
+    acts = ref.mlp_fwd(xs[-1], layers)
+    hw = head.weight.detach().cpu().numpy().reshape(-1)
+    z = acts[-1] @ hw + float(head.bias)
+    want_loss, dz = ref.bce_with_logits(z, y.cpu().numpy())
+    assert abs(float(loss) - want_loss) <= 3e-3 * abs(want_loss), (float(loss), want_loss)
+    dxc, lgr = ref.mlp_bwd(acts, layers, dz[:, None] * hw[None, :])
+    dx0, cgr = ref.dcn_cross_bwd(xs, zs, clay, dxc)
+
+    def close(a, w, name):
+        a = a.detach().double().cpu().numpy().reshape(w.shape)
+        l2 = np.linalg.norm(a - w) / (np.linalg.norm(w) + 1e-30)
+        assert l2 <= 8e-2, (name, l2)
+
+    close(got["dx0"], dx0, "dx0")
+    for i, (wW, wb) in enumerate(cgr + lgr):
+        close(got[f"dW{i}"], wW, f"dW{i}")
+        close(got[f"db{i}"], wb, f"db{i}")
+    close(got["dW_head"].reshape(-1), acts[-1].T @ dz, "dW_head")

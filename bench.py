@@ -499,14 +499,17 @@ def embedding_roofline(model, step, datas, args, in_step=True):
                     "wave_dur_p50_p90_max": [round(v[len(v) // 2][2][j] * 1e6, 2)
                                              for j in range(3, 6)]}
                 for c, v in sorted(CAT_SPANS.items())}
-        if args.model == "deepfm":
+        if args.model in ("deepfm", "dcnv2"):
             lins = [m for m in model.mlp.modules() if isinstance(m, torch.nn.Linear)]
+            # DCN-v2: the cross layers (d x d) run in the same tower / tower_dw launches
+            cross = list(getattr(model, "cross", []))
             widths = [lins[0].in_features] + [m.out_features for m in lins]
-            L = len(widths) - 1
-            mm = sum(widths[l] * widths[l + 1] for l in range(L))
+            dims = [(c.out_features, c.in_features) for c in cross] + \
+                [(widths[l + 1], widths[l]) for l in range(len(widths) - 1)]
+            mm = sum(n * k for n, k in dims)
+            mm_c = sum(c.out_features * c.in_features for c in cross)
             for name, fl in ((TOWER_PAIR[0], 2 * 2 * args.batch * mm),
-                             (TOWER_PAIR[1], 2 * args.batch * sum(widths[l + 1] * (widths[l] + 1)
-                                                                  for l in range(L)))):
+                             (TOWER_PAIR[1], 2 * args.batch * sum(n * (k + 1) for n, k in dims))):
                 if name in t:
                     d = {"avg_us": round(t[name] * 1e6, 3), "flop": fl,
                          "TFLOP/s": round(fl / t[name] / 1e12, 1),
@@ -518,6 +521,24 @@ def embedding_roofline(model, step, datas, args, in_step=True):
                         d["per_CU_L2_GB/s"] = round(wimg / t[name] / 1e9, 1)
                         d["bound"] = ("per-CU L2 read rate (~70 GB/s per CU, MI355X_MICROARCH.md "
                                       "indexed-rows table)")
+                        if cross:
+                            ph = tower_cross_phases(step, datas[0], args.batch, len(lins))
+                            if ph:
+                                frac = (ph["cross_fwd_us"] + ph["cross_bwd_us"]) / ph["wave_us"]
+                                tc = t[name] * frac
+                                fc = 2 * 2 * args.batch * mm_c
+                                d["cross"] = {
+                                    "layers": len(cross), "flop": fc,
+                                    "in_step_us": round(tc * 1e6, 3),
+                                    "TFLOP/s": round(fc / tc / 1e12, 1),
+                                    "frac_of_mfma_peak": round(fc / tc / 1e12 / MFMA_PEAK_TFLOPS, 4),
+                                    "timing": "the tower's in-step time x the cross phases' share "
+                                              "of the workgroups' wall clock (phase stamps of an "
+                                              "eager step, medians over workgroups)",
+                                    "phases_us": ph}
+                                dw = 2 * args.batch * sum(n * (k + 1) for n, k in dims[:len(cross)])
+                                rk.setdefault("cross_dw_share_of_tower_dw_flop", round(
+                                    dw / (2 * args.batch * sum(n * (k + 1) for n, k in dims)), 4))
                     rk[name] = d
     if args.standalone_roofline or not in_step:
         ks = kernel_rooflines(model, datas[0], args)
@@ -544,6 +565,34 @@ def embedding_roofline(model, step, datas, args, in_step=True):
         out["roofline"]["frac_of_attainable"] = round(out["roofline"]["achieved"] / att["GB/s"], 4)
     out["roofline_kernels"] = rk
     return out
+
+
+def tower_cross_phases(step, data, B, L):
+    """Per-workgroup phase stamps of the fused tower (mrec_tower_debug_stamps, 100
+    MHz wall clock) over one eager train step: the cross network's forward (stamp 1
+    -> 15) and backward (the MLP's last backward layer -> stamp 11) against the
+    workgroup's whole span (0 -> 12), medians over the workgroups, in us."""
+    from pytorchrec_amd import _mrec
+    import ctypes
+    dev = torch.device("cuda", torch.cuda.current_device())
+    grid = (B + 15) // 16
+    st = torch.zeros(grid, 16, dtype=torch.int64, device=dev)
+    fn = _mrec.lib().mrec_tower_debug_stamps
+    fn.argtypes, fn.restype = [ctypes.c_void_p], None
+    torch.cuda.synchronize()
+    fn(st.data_ptr())
+    try:
+        step(data)
+    finally:
+        fn(None)
+    torch.cuda.synchronize()
+    t = st.cpu().double() * 1e-2  # us
+    last_mlp = 7 + (L - 1)  # stamp 7 + (L - 1 - l) at the MLP's first layer (l = 0)
+    if not bool((st[:, [0, 1, 15, last_mlp, 11, 12]] != 0).all()):
+        return None
+    med = lambda x: round(float(x.median()), 3)  # noqa: E731
+    return {"cross_fwd_us": med(t[:, 15] - t[:, 1]), "cross_bwd_us": med(t[:, 11] - t[:, last_mlp]),
+            "wave_us": med(t[:, 12] - t[:, 0])}
 
 
 def alg_bytes_per_sample(F, D, n_dense, first_order, es=2):
@@ -747,8 +796,8 @@ def end_to_end(args, per_gpu_samples_s):
         d0 = CRITEO_FIELDS * 16 + CRITEO_DENSE
         if fo:
             fwd = 2 * (d0 * 400 + 400 * 400 + 400 * 400 + 400)
-        else:  # 3 cross layers d0 x d0 + deep 400-400 + head over [x_3 | h_2]
-            fwd = 2 * (3 * d0 * d0 + d0 * 400 + 400 * 400 + (d0 + 400))
+        else:  # 3 cross layers d0 x d0 + deep 400-400 + Linear(400, 1) (stacked DCN-v2)
+            fwd = 2 * (3 * d0 * d0 + d0 * 400 + 400 * 400 + 400)
     flops = 3 * fwd
     hbm = HBM_PEAK_GBS * 1e9 / nbytes
     mfma = MFMA_PEAK_TFLOPS * 1e12 / flops

@@ -212,6 +212,17 @@ __global__ __launch_bounds__(kPlanThreads) void plan_hash_kernel(BankArgs bank, 
                                            blockIdx.x % kPlanBuckets, smem);
 }
 
+// diagnostics (mrec_diag_plan_hash_variant): the plan body at other workgroup sizes /
+// slot counts than the production launches use (the 512-thread body)
+template <int THREADS, int SLOTS, int MAXB>
+__global__ __launch_bounds__(THREADS) void plan_hash_variant_kernel(BankArgs bank, IdsArgs ids,
+                                                                    int64_t B, void *ws,
+                                                                    int32_t *__restrict__ oob) {
+  __shared__ __attribute__((aligned(16))) uint32_t smem[2 * SLOTS + 2];
+  plan_hash_body<THREADS, SLOTS, MAXB>(bank, ids, B, ws, oob, nullptr, blockIdx.x / kPlanBuckets,
+                                       blockIdx.x % kPlanBuckets, smem);
+}
+
 // ---------------------------------------------------------------------------
 // apply (helpers in emb_apply.h)
 // ---------------------------------------------------------------------------
@@ -818,6 +829,39 @@ mrec_status mrec_emb_bwd_plan(const mrec_table_bank *bank, const mrec_ids *ids, 
   plan_kernel<<<dim3(ba.n_tables), kPlanThreads, 0, static_cast<hipStream_t>(stream)>>>(
       ba, ia, batch, rounds < 1 ? 1 : rounds, workspace, d_oob_flag, d_step);
   return launch_status("mrec_emb_bwd_plan");
+}
+
+// diagnostics (not in mrec.h): the hash plan of mrec_emb_bwd_plan run by the plan body
+// instantiated for `threads` threads and `slots` LDS slots (variants: 1024 / 8192 --
+// the production instantiation --, 512 / 8192, 256 / 8192, 512 / 4096 for batches <=
+// 4096).  The workspace it leaves drives mrec_emb_bwd_apply like the standalone plan's.
+mrec_status mrec_diag_plan_hash_variant(const mrec_table_bank *bank, const mrec_ids *ids,
+                                        int64_t batch, void *workspace, size_t ws_bytes,
+                                        int32_t threads, int32_t slots, int32_t *d_oob_flag,
+                                        mrec_stream stream) {
+  BankArgs ba;
+  IdsArgs ia;
+  int eb, lpr;
+  mrec_status st = make_bank_args(bank, &ba, &eb, &lpr);
+  if (st != MREC_OK) return st;
+  if ((st = make_ids_args(ids, ba.n_tables, &ia)) != MREC_OK) return st;
+  MREC_CHECK_ARG(batch >= 1 && hash_layout(batch, ia.pad_negative != 0),
+                 "the batch must take the hash layout");
+  MREC_CHECK_ARG(workspace && ws_bytes >= static_cast<size_t>(mrec_emb_bwd_workspace_size(ba.n_tables, batch)),
+                 "workspace too small");
+  const dim3 grid(ba.n_tables * kPlanBuckets);
+  hipStream_t s = static_cast<hipStream_t>(stream);
+  if (threads == 1024 && slots == 8192)
+    plan_hash_variant_kernel<1024, 8192, kHashMaxEntries><<<grid, 1024, 0, s>>>(ba, ia, batch, workspace, d_oob_flag);
+  else if (threads == 512 && slots == 8192)
+    plan_hash_variant_kernel<512, 8192, kHashMaxEntries><<<grid, 512, 0, s>>>(ba, ia, batch, workspace, d_oob_flag);
+  else if (threads == 256 && slots == 8192)
+    plan_hash_variant_kernel<256, 8192, kHashMaxEntries><<<grid, 256, 0, s>>>(ba, ia, batch, workspace, d_oob_flag);
+  else if (threads == 512 && slots == 4096 && batch <= 4096)
+    plan_hash_variant_kernel<512, 4096, 4096><<<grid, 512, 0, s>>>(ba, ia, batch, workspace, d_oob_flag);
+  else
+    MREC_CHECK_ARG(false, "no such plan variant");
+  return launch_status("mrec_diag_plan_hash_variant");
 }
 
 }  // extern "C"

@@ -1296,7 +1296,10 @@ mrec_status mrec_emb_bwd_large_plan(const mrec_table_bank *bank, const mrec_ids 
   if (batch == 0) return MREC_OK;  // (apply returns early for batch 0 as well)
   const int64_t total = batch * ba.n_tables;
   const int G = bk_groups(R, total);
-  if (G > 0 && !std::getenv("MREC_LG_ATOMIC_PLAN")) {
+  // MREC_LG_ATOMIC_PLAN (diagnostics): the atomic plan's per-row arrays exist only for
+  // banks up to kLgMaxRows rows (lg_ws_bytes); past that the knob is ignored
+  const bool atomic_knob = std::getenv("MREC_LG_ATOMIC_PLAN") != nullptr && R <= kLgMaxRows;
+  if (G > 0 && !atomic_knob) {
     const int NB = bk_buckets(total);
     int lognb = 0;
     while ((1 << lognb) < NB) ++lognb;
@@ -1305,6 +1308,7 @@ mrec_status mrec_emb_bwd_large_plan(const mrec_table_bank *bank, const mrec_ids 
     bk_group_kernel<<<dim3(NB), 256, 0, s>>>(w, G, lognb, d_oob_flag);
     return launch_status("mrec_emb_bwd_large_plan");
   }
+  MREC_CHECK_ARG(R <= kLgMaxRows, "the atomic large-batch plan needs a bank of <= 2^24 rows");
   if (hipMemsetAsync(w.cnt, 0, static_cast<size_t>(R) * 4, s) != hipSuccess)
     return launch_status("mrec_emb_bwd_large_plan (memset)");
   const int nblk = static_cast<int>((R + kLgRowsPerBlock - 1) / kLgRowsPerBlock);
@@ -1484,7 +1488,7 @@ static mrec_status lg_fused_impl(const mrec_table_bank *bank, const mrec_ids *id
   const int64_t total = batch * ba.n_tables;
   const int G = batch == 0 ? 0 : bk_groups(R, total);
   hipStream_t s = static_cast<hipStream_t>(stream);
-  if (G == 0 || std::getenv("MREC_LG_ATOMIC_PLAN")) {  // the two-call path
+  if (G == 0 || (std::getenv("MREC_LG_ATOMIC_PLAN") && R <= kLgMaxRows)) {  // the two-call path
     if (batch > 0) {
       st = mrec_emb_bwd_large_plan(bank, ids, batch, workspace, ws_bytes, d_oob_flag, stream);
       if (st != MREC_OK) return st;

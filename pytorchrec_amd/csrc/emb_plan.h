@@ -167,6 +167,11 @@ __device__ __forceinline__ void plan_hash_body(const BankArgs &bank, const IdsAr
                                                void *ws, int32_t *__restrict__ oob,
                                                uint64_t *__restrict__ d_step, int f, int r,
                                                uint32_t *smem) {
+  // every entry in [0, B) is one thread's k-th round: B <= MAXB (host-checked) and
+  // MAXB a multiple of THREADS; SLOTS >= MAXB bounds the linear probing (a bucket
+  // holds at most B distinct keys, so an empty slot always exists)
+  static_assert(THREADS % 64 == 0 && MAXB % THREADS == 0, "whole waves, whole rounds");
+  static_assert(SLOTS >= MAXB, "the probe loop needs a free slot for every distinct key");
   constexpr int kRounds = MAXB / THREADS;
   uint32_t *hkey = smem;          // [SLOTS] row id; after the claim: (segment << 16) | start
   uint32_t *hcnt = smem + SLOTS;  // [SLOTS] (tickets << 16) | lookups

@@ -604,6 +604,7 @@ __global__ __launch_bounds__(TW_THREADS) void tower_kernel(TowerArgs a, KClock k
       }
     }
     off_in0 = a.off_xc[(a.C - 1) & 1];
+    TW_STAMP(15);  // diagnostics: the cross forward's end (the backward's is stamp 11)
   }
 
   // ---- forward: h_l = relu(h_{l-1} W_l^T + b_l) --------------------------------

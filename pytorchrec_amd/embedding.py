@@ -387,6 +387,8 @@ def _large_ws(bank: EmbeddingBank, batch: int) -> torch.Tensor:
     allocation, every mrec_emb_bwd_large_apply leaves its zero region zero."""
     cache = getattr(bank, "_large_ws_cache", None)
     if cache is None or cache[0] != batch or cache[1].device != bank.weight.device:
+        if cache is not None and not torch.cuda.is_current_stream_capturing():
+            bank.check_flags()  # an earlier step's sticky error word must not be dropped
         nbytes = _mrec.lib().mrec_emb_bwd_large_workspace_size(bank.desc().ref(), batch)
         cache = (batch, torch.zeros(nbytes, dtype=torch.uint8, device=bank.weight.device))
         bank._large_ws_cache = cache

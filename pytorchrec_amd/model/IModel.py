@@ -26,6 +26,7 @@ MI355X additions (documented deviations):
 from __future__ import annotations
 
 import copy
+import os
 from abc import ABC, abstractmethod
 from typing import Dict, List, Optional
 
@@ -48,6 +49,7 @@ class IModel(Module, IWithArguments, ABC):
         super().__init__()
         self.stop_training = False
         self.best_state_dict = None
+        self._weights_version = 0  # bumped by every train step / load (save_best_weights)
         self.history: Optional[list] = None
         self._is_compiled = False
         self.compiled_optimizers: Optional[Optimizer] = None
@@ -78,60 +80,81 @@ class IModel(Module, IWithArguments, ABC):
 
     # -- checkpoints (IModel.py:73-81, 314-321) --------------------------------
     def load_weights(self, filepath: str, device: torch.device):
-        state_dict = torch.load(filepath, map_location=device, weights_only=True)
-        self.load_state_dict(state_dict)
+        """Restore a checkpoint written by ``save_weights``: a single-file state dict
+        (the reference's format) or a row-sharded checkpoint (index file + per-rank
+        shard files, checkpoint.py) -- into this model sharded at any world size or
+        unsharded; every bank reads only its own rows."""
+        from pytorchrec_amd import checkpoint
+        state = torch.load(filepath, map_location="cpu", weights_only=True)
+        checkpoint.load_into(self, state, os.path.abspath(filepath))
         self.to(device)
+        self._weights_version += 1
 
     def save_weights(self, filepath: str):
-        # the reference pickles with HIGHEST_PROTOCOL (IModel.py:79-81); torch >= 2.6
-        # loads with weights_only=True, whose unpickler rejects protocol >= 4 frames,
-        # so the default protocol keeps the file loadable safely (here and by the
-        # reference's own torch.load on a current torch)
-        torch.save(self.state_dict(), filepath)
+        """The reference's ``torch.save(state_dict)``; a model with row-sharded banks
+        writes the row-sharded checkpoint instead (collective: every rank calls it;
+        checkpoint.save_sharded), which never assembles a bank anywhere."""
+        from pytorchrec_amd import checkpoint
+        if checkpoint.has_sharded_banks(self):
+            checkpoint.save_sharded(self, filepath)
+        else:
+            # the reference pickles with HIGHEST_PROTOCOL (IModel.py:79-81); torch >= 2.6
+            # loads with weights_only=True, whose unpickler rejects protocol >= 4 frames,
+            # so the default protocol keeps the file loadable safely (here and by the
+            # reference's own torch.load on a current torch)
+            checkpoint.save_file(self.state_dict(), filepath)
+        self._last_saved = (os.path.abspath(filepath), self._weights_version)
 
     # -- row-sharded checkpoints (SURVEY.md §8(f) rank 4) -------------------------
-    def global_state_dict(self) -> Dict:
+    def global_state_dict(self, dst: Optional[int] = None) -> Dict:
         """``state_dict()`` with every row-sharded bank replaced by the full bank in
-        the unsharded layout, so the keys and shapes are exactly those of the same
-        model built without sharding (and of the reference's per-field tables via
-        ``EmbeddingBank.table``).  Collective over the shard group."""
+        the unsharded layout (host memory, assembled chunk by chunk: the GPUs never
+        hold more than their shard + one chunk), so the keys and shapes are exactly
+        those of the same model built without sharding (and of the reference's
+        per-field tables via ``EmbeddingBank.table``).  ``dst``: only that rank
+        receives the banks (the others get None for them).  Collective over the
+        shard group.  For banks larger than one host's memory use ``save_weights``."""
         from pytorchrec_amd.sharding import ShardedEmbeddingBank
         sd = self.state_dict()
         for name, m in self.named_modules():
             if isinstance(m, ShardedEmbeddingBank):
-                sd[(name + "." if name else "") + "weight"] = m.gather_global()
+                sd[(name + "." if name else "") + "weight"] = m.gather_global(dst=dst)
         return sd
 
     def load_global_state_dict(self, state_dict: Dict, strict: bool = True):
         """Load a checkpoint in the unsharded layout (``global_state_dict`` or a
         single-GPU ``state_dict``); each row-sharded bank keeps its own rows."""
-        from pytorchrec_amd.sharding import ShardedEmbeddingBank
-        sd = dict(state_dict)
-        bank_keys, missing = set(), []
-        for name, m in self.named_modules():
-            if isinstance(m, ShardedEmbeddingBank):
-                key = (name + "." if name else "") + "weight"
-                bank_keys.add(key)
-                w = sd.pop(key, None)
-                if w is None:
-                    missing.append(key)
-                else:
-                    m.load_global_bank_(w)
-        res = self.load_state_dict(sd, strict=False)
-        missing += [k for k in res.missing_keys if k not in bank_keys]
-        unexpected = list(res.unexpected_keys)
-        if strict and (missing or unexpected):
-            raise RuntimeError(f"Error(s) in loading state_dict for {type(self).__name__}: "
-                               f"missing keys {missing}, unexpected keys {unexpected}")
+        from pytorchrec_amd import checkpoint
+        checkpoint.load_into(self, state_dict, None, strict=strict)
+        self._weights_version += 1
         return self
 
     def save_best_weights(self):
+        """The reference deep-copies the state dict to host memory (IModel.py:314-317).
+        ModelCheckpoint calls this right after ``save_weights`` (ModelCheckpoint.py:
+        82-91): when nothing trained since that save, the files just written ARE the
+        best state, kept as hard links under ``<file>.best`` (no copy; a later save
+        replaces the live files' inodes, checkpoint.py) -- a row-sharded bank is never
+        copied to any host.  Else a host copy of this rank's state (its own shard of
+        a sharded bank, never the whole bank).  Every rank calls it."""
+        from pytorchrec_amd import checkpoint
+        saved = getattr(self, "_last_saved", None)
+        if saved is not None and saved[1] == self._weights_version:
+            snap = saved[0] + ".best"
+            checkpoint.link_snapshot(self, saved[0], snap)
+            self.best_state_dict = {"__mrec_best_file__": snap}
+            return
         self.best_state_dict = copy.deepcopy(tensor_to_device(self.state_dict(), torch.device("cpu")))
 
     def load_best_weights(self):
         assert self.best_state_dict is not None
+        path = self.best_state_dict.get("__mrec_best_file__")
+        if path is not None:
+            self.load_weights(path, self.compiled_device)
+            return
         self.load_state_dict(self.best_state_dict)
         self.to(self.compiled_device)
+        self._weights_version += 1
 
     def get_parameters(self):
         weight_p, bias_p = [], []
@@ -345,6 +368,7 @@ class IModel(Module, IWithArguments, ABC):
     # -- steps ------------------------------------------------------------------
     def train_step(self, data: Dict):
         self.train()
+        self._weights_version += 1
         data = tensor_to_device(data, self.compiled_device)
         fused = self._fused_loss_fn()
         if fused is not None:

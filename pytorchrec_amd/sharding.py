@@ -255,13 +255,23 @@ class ShardedEmbeddingBank(EmbeddingBank):
         self.global_rows = [int(n) for n in category_nums]
         self.comm = comm
         self.world, self.rank = W, r
-        # slots per (owner, table[, chunk]): distinct ids on the compact exchange,
-        # lookups on the slot exchange (the `compact` setter switches a defaulted cap)
+        # the compact exchange's chunks: its per-(owner, wave-group) rank histogram
+        # holds (W + 1) * ceil(chunk / 1024) * 16 <= 2048 entries, so large worlds take
+        # smaller chunks (W = 16: 7,168 samples; W >= 127 is not supported)
+        if W + 1 > 128:
+            raise ValueError(f"row sharding supports world sizes up to 127, not {W}")
+        self.chunk_batch = min(int(type(self).chunk_batch), 1024 * (128 // (W + 1)))
+        # slots per (owner, table[, chunk]): distinct ids of one chunk on the compact
+        # exchange, lookups of the whole batch on the slot exchange (which does not
+        # chunk); the `compact` setter switches a defaulted cap
         mb = min(int(max_batch), self.chunk_batch)
         self._caps = None if cap is not None else (
-            default_cap(mb, W, self.global_rows, dedup=True), default_cap(mb, W, self.global_rows))
+            default_cap(mb, W, self.global_rows, dedup=True),
+            default_cap(int(max_batch), W, self.global_rows))
         self._max_batch = mb
-        self.cap = int(cap) if cap is not None else self._caps[0]
+        self._compact = True
+        on = W > 1  # the default exchange: compact at W > 1 (see `compact`)
+        self.cap = int(cap) if cap is not None else self._caps[0 if on else 1]
         if self.cap < 1:
             raise ValueError(f"cap = {self.cap} must be >= 1")
         self._flags = None  # device int32 [2] = {overflow, oob}, sticky until checked
@@ -271,8 +281,20 @@ class ShardedEmbeddingBank(EmbeddingBank):
         # world 1 nothing crosses xGMI and the slot
         # path keeps the step bit-identical to the unsharded bank (the compact path
         # rounds each rank's gradient sum of a bf16 row to bf16 on the wire).
-        self._compact = True
-        self.cap_rows = default_cap_rows(mb, W, self.global_rows, self.cap)
+        self._cap_rows = default_cap_rows(mb, W, self.global_rows, self._caps[0]
+                                          if self._caps is not None else self.cap)
+        self._cap_rows_user = False
+
+    @property
+    def cap_rows(self) -> int:
+        """Records per owner part of the compact exchange (default_cap_rows); an
+        assigned value is kept when ``compact`` is toggled later."""
+        return self._cap_rows
+
+    @cap_rows.setter
+    def cap_rows(self, value):
+        self._cap_rows = int(value)
+        self._cap_rows_user = True
 
     @property
     def compact(self):
@@ -280,13 +302,15 @@ class ShardedEmbeddingBank(EmbeddingBank):
 
     @compact.setter
     def compact(self, value):
-        """True / "always" / False (see __init__); a defaulted cap follows it."""
+        """True / "always" / False (see __init__); a defaulted cap follows it (and a
+        defaulted cap_rows follows the cap)."""
         self._compact = value
         if self._caps is not None:
             on = value == "always" or (bool(value) and self.world > 1)
             self.cap = self._caps[0] if on else self._caps[1]
-            self.cap_rows = default_cap_rows(self._max_batch, self.world, self.global_rows,
-                                             self.cap)
+            if not self._cap_rows_user:
+                self._cap_rows = default_cap_rows(self._max_batch, self.world, self.global_rows,
+                                                  self._caps[0])
 
     @property
     def part(self) -> int:
@@ -310,12 +334,20 @@ class ShardedEmbeddingBank(EmbeddingBank):
 
     def use_compact(self, batch: int) -> bool:
         """The compact exchange when it is on and mrec_shard_bucketize_dedup_ex takes
-        the shape: cap < 65535 and its per-(owner, wave-group) histogram (world + 1)
-        * ceil(chunk / 1024) * 16 <= 2048 entries (e.g. W >= 16 at 8192-sample chunks
-        falls back to the slot exchange).  Batches past 8192 go out in chunks."""
+        the shape: cap < 65535 (its per-(owner, wave-group) histogram always fits:
+        ``chunk_batch`` shrinks with the world size).  Batches past ``chunk_batch``
+        go out in chunks.  The slot exchange (compact off) does not chunk: its batch
+        must keep (world + 1) * ceil(batch / 1024) * 16 <= 2048 (checked, raised)."""
         on = self.compact == "always" or (bool(self.compact) and self.world > 1)
-        groups = max(1, -(-min(int(batch), self.chunk_batch) // 1024) * 16)
-        return on and self.cap < 65535 and (self.world + 1) * groups <= 2048
+        return on and self.cap < 65535
+
+    def check_slot_batch(self, batch: int):
+        groups = -(-int(batch) // 1024) * 16
+        if (self.world + 1) * groups > 2048:
+            raise ValueError(
+                f"the slot exchange (compact off) takes at most {2048 // 16 // (self.world + 1)}"
+                f" x 1024 samples per rank at world {self.world}, not {batch}: use the compact "
+                "exchange (ShardedEmbeddingBank.compact = True) or smaller batches")
 
     @property
     def g_ld(self) -> int:
@@ -362,29 +394,42 @@ class ShardedEmbeddingBank(EmbeddingBank):
         return self
 
     @torch.no_grad()
-    def gather_global(self) -> torch.Tensor:
+    def gather_global(self, dst: Optional[int] = None,
+                      chunk_rows: int = 1 << 22) -> Optional[torch.Tensor]:
         """The full bank in the UNSHARDED layout (``EmbeddingBank(global_rows)``:
-        tables concatenated, same row pitch), assembled on every rank: per table one
-        all_gather of the shards padded to ceil(rows / W) rows, then global row i =
-        row i // W of rank i % W.  Collective: every rank must call it."""
+        tables concatenated, same row pitch), in HOST memory on rank ``dst`` (every
+        rank when None; the others return None).  Per table, chunks of ``chunk_rows``
+        global rows: one all_gather of each rank's rows of the chunk, then global row
+        i = row i // W of rank i % W -- the GPUs hold one chunk beside their shard,
+        never the bank.  Collective: every rank must call it.  (Banks too large for
+        one host: IModel.save_weights writes per-rank shard files, checkpoint.py.)"""
         W = self.world
-        full = torch.empty(sum(self.global_rows), self.row_stride, dtype=self.weight.dtype,
-                           device=self.weight.device)
+        keep = dst is None or dst == self.rank
+        full = (torch.empty(sum(self.global_rows), self.row_stride, dtype=self.weight.dtype)
+                if keep else None)
         g_off = 0
+        per_chunk = max(1, chunk_rows // W)  # local rows per rank and chunk
         for f, n in enumerate(self.global_rows):
             per = -(-n // W)
             local = self.weight[self.row_offset[f]:self.row_offset[f] + self.category_nums[f]]
-            if W == 1:
-                full[g_off:g_off + n] = local
-            else:
-                pad = torch.zeros(per, self.row_stride, dtype=self.weight.dtype,
+            for a in range(0, per, per_chunk):
+                b = min(per, a + per_chunk)
+                if W == 1:
+                    if keep:
+                        full[g_off + a:g_off + b] = local[a:b].cpu()
+                    continue
+                pad = torch.zeros(b - a, self.row_stride, dtype=self.weight.dtype,
                                   device=self.weight.device)
-                pad[:local.shape[0]] = local
+                mine = local[a:min(b, local.shape[0])]
+                pad[:mine.shape[0]] = mine
                 parts = [torch.empty_like(pad) for _ in range(W)]
                 dist.all_gather(parts, pad, group=self.comm.group)
-                # [W, per, stride] -> [per, W, stride]: row j of rank r is global j*W + r
-                inter = torch.stack(parts, 1).reshape(per * W, self.row_stride)
-                full[g_off:g_off + n] = inter[:n]
+                if keep:
+                    # [W, c, stride] -> [c, W, stride]: row j of rank r is global j*W + r
+                    inter = torch.stack(parts, 1).reshape((b - a) * W, self.row_stride)
+                    lo, hi = a * W, min(n, b * W)
+                    full[g_off + lo:g_off + hi] = inter[:hi - lo].cpu()
+                del parts, pad
             g_off += n
         return full
 
@@ -1105,7 +1150,10 @@ def sharded_interact(bank: ShardedEmbeddingBank, ids, dense, dense_w, bias, fm2:
         return cpu_sharded_interact(bank, ids, dense, dense_w, bias, fm2, first_order, x0_cols,
                                     x0_dtype)
     trigger = _trigger(bank)
-    fn = _CompactInteractFn if bank.use_compact(ids[0].shape[0]) else _ShardedInteractFn
+    compact = bank.use_compact(ids[0].shape[0])
+    if not compact:
+        bank.check_slot_batch(ids[0].shape[0])
+    fn = _CompactInteractFn if compact else _ShardedInteractFn
     return fn.apply(dense_w, bias, trigger, bank, ids, dense, fm2, first_order, int(x0_cols),
                     x0_dtype)
 

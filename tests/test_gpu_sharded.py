@@ -139,7 +139,7 @@ def test_sharded_overflow_is_raised(gpu):
         bank.check_flags()
 
 
-def _deepfm(gpu, sharded, emb_dtype=torch.bfloat16):
+def _deepfm(gpu, sharded, emb_dtype=torch.bfloat16, max_batch=256):
     from pytorchrec_amd.feature_column import CategoricalColumnWithIdentity, NumericColumn
     from pytorchrec_amd.model import DeepFM
     from pytorchrec_amd.sharding import ShardComm, sharded_tables
@@ -148,7 +148,7 @@ def _deepfm(gpu, sharded, emb_dtype=torch.bfloat16):
     label = CategoricalColumnWithIdentity(2, "label")
     torch.manual_seed(3)
     if sharded:
-        with sharded_tables(ShardComm(world=1, rank=0), max_batch=256):
+        with sharded_tables(ShardComm(world=1, rank=0), max_batch=max_batch):
             m = DeepFM(sparse, dense, label, emb_size=D, layers=(64, 32), emb_dtype=emb_dtype,
                        random_seed=5, device=gpu)
     else:
@@ -171,6 +171,32 @@ def test_world1_sharded_deepfm_step_equals_unsharded(gpu):
         m.compile(opt, BCEWithLogitsLoss(), [], gpu)
     la = [float(a.train_step(data)["loss"].detach()) for _ in range(2)]
     lb = [float(b.train_step(data)["loss"].detach()) for _ in range(2)]
+    assert la == lb
+    for (k, va), vb in zip(a.state_dict().items(), b.state_dict().values()):
+        assert torch.equal(va, vb), k
+
+
+def test_world1_sharded_large_batch_default_cap_equals_unsharded(gpu):
+    """a world-1 sharded bank built for B = 16,384 takes the slot exchange
+    with a defaulted cap sized for the WHOLE batch (the slot bucketize does not
+    chunk), so nothing overflows and the owner's view (W * cap > 8,192 entries)
+    takes the large-batch owner apply: two steps bit-identical to the unsharded
+    model."""
+    from pytorchrec_amd.loss import BCEWithLogitsLoss
+    B = 16384
+    a, b = _deepfm(gpu, False), _deepfm(gpu, True, max_batch=B)
+    assert b.embeddings.cap >= B and not b.embeddings.use_compact(B)
+    b.load_state_dict(a.state_dict())
+    data = {f"c_c_C{i}": t for i, t in enumerate(_ids(gpu, B, 5))}
+    g = torch.Generator().manual_seed(6)
+    for i in range(13):
+        data[f"c_n_I{i}"] = torch.rand(B, generator=g).to(gpu)
+    data["label"] = (torch.rand(B, generator=g) < 0.25).to(torch.int32).to(gpu)
+    for m in (a, b):
+        m.compile(torch.optim.SGD(m.get_parameters(), lr=0.05), BCEWithLogitsLoss(), [], gpu)
+    la = [float(a.train_step(data)["loss"].detach()) for _ in range(2)]
+    lb = [float(b.train_step(data)["loss"].detach()) for _ in range(2)]
+    b.embeddings.check_flags()
     assert la == lb
     for (k, va), vb in zip(a.state_dict().items(), b.state_dict().values()):
         assert torch.equal(va, vb), k
@@ -694,3 +720,72 @@ def test_compact_cap_rows_overflow_raised_and_clipped_rows_untouched(gpu):
     untouched = torch.ones(n_rows, dtype=torch.bool, device=gpu)
     untouched[slot_ids[:40]] = False
     assert torch.equal(bank.weight[untouched, :cols], before[untouched, :cols])
+
+
+def test_sharded_checkpoint_world1_gpu_bit_exact_and_memory_bounded(gpu, tmp_path):
+    """Row-sharded checkpoint on the GPU (checkpoint.py): a
+    world-1 sharded DeepFM of 26 x 10^6-row bf16 tables (1.66 GB bank) trained one
+    step, then ``save_weights`` (the shard streamed device -> host -> file in chunks)
+    and ``load_weights`` into a fresh sharded replica and into an unsharded model:
+    every row bit-identical to the trained bank, dense entries equal, and the
+    unsharded model's own single-file checkpoint loads back into a sharded replica
+    bit-identically.  Peak GPU memory above the model's during save and load stays
+    below one shard (the whole never exists twice: < 2x the shard in total)."""
+    from pytorchrec_amd.embedding import init_bank_
+    from pytorchrec_amd.feature_column import CategoricalColumnWithIdentity, NumericColumn
+    from pytorchrec_amd.loss import BCEWithLogitsLoss
+    from pytorchrec_amd.model import DeepFM
+    from pytorchrec_amd.sharding import ShardComm, sharded_tables
+    rows = [1_000_000] * 26
+    sparse = [CategoricalColumnWithIdentity(n, f"c_c_C{i}") for i, n in enumerate(rows)]
+    dense = [NumericColumn(f"c_n_I{i}") for i in range(13)]
+    label = CategoricalColumnWithIdentity(2, "label")
+
+    def build(sharded, seed):
+        mk = lambda: DeepFM(sparse, dense, label, emb_size=16, layers=(64, 32),  # noqa: E731
+                            emb_dtype=torch.bfloat16, random_seed=seed, device=gpu)
+        if not sharded:
+            return mk()
+        with sharded_tables(ShardComm(world=1, rank=0), max_batch=512):
+            return mk()
+
+    m = build(True, 5)
+    init_bank_(m.embeddings, generator=torch.Generator(device=gpu).manual_seed(9))
+    m.compile(torch.optim.SGD(m.get_parameters(), lr=0.05), BCEWithLogitsLoss(), [], gpu)
+    g = torch.Generator().manual_seed(4)
+    data = {f"c_c_C{i}": torch.randint(0, n, (512,), generator=g, dtype=torch.int32).to(gpu)
+            for i, n in enumerate(rows)}
+    for i in range(13):
+        data[f"c_n_I{i}"] = torch.rand(512, generator=g).to(gpu)
+    data["label"] = (torch.rand(512, generator=g) < 0.25).to(torch.int32).to(gpu)
+    m.train_step(data)
+    shard_bytes = m.embeddings.weight.numel() * m.embeddings.weight.element_size()
+    path = str(tmp_path / "c5like.pt")
+    torch.cuda.synchronize()
+    base = torch.cuda.memory_allocated()
+    torch.cuda.reset_peak_memory_stats()
+    m.save_weights(path)
+    torch.cuda.synchronize()
+    assert torch.cuda.max_memory_allocated() - base < shard_bytes, "save materialised the bank"
+    want = m.embeddings.weight.detach().view(torch.int16)
+    fresh = build(True, 77)
+    torch.cuda.synchronize()
+    base = torch.cuda.memory_allocated()
+    torch.cuda.reset_peak_memory_stats()
+    fresh.load_weights(path, gpu)
+    torch.cuda.synchronize()
+    assert torch.cuda.max_memory_allocated() - base < shard_bytes, "load materialised the bank"
+    assert torch.equal(fresh.embeddings.weight.detach().view(torch.int16), want)
+    for k, v in m.state_dict().items():
+        if k != "embeddings.weight":
+            assert torch.equal(fresh.state_dict()[k], v), k
+    del fresh
+    u = build(False, 78)  # unsharded EmbeddingBank: the same rows at world 1
+    u.load_weights(path, gpu)
+    assert torch.equal(u.embeddings.weight.detach().view(torch.int16), want)
+    single = str(tmp_path / "single.pt")
+    u.save_weights(single)  # the reference's single-file format
+    del u
+    back = build(True, 79)
+    back.load_weights(single, gpu)
+    assert torch.equal(back.embeddings.weight.detach().view(torch.int16), want)

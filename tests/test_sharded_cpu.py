@@ -100,6 +100,18 @@ def _worker(rank, world, port, out_dir, steps, chunk_batch=None):
             if not k.startswith("embeddings"):
                 same = same and torch.equal(fresh.state_dict()[k], v)
         out["reload_ok"] = np.array(bool(same))
+        # the row-sharded checkpoint (checkpoint.py): collective save_weights writes
+        # per-rank shard files + rank 0's index; a fresh replica reads its own file
+        ck = os.path.join(out_dir, "ckpt.pt")
+        model.save_weights(ck)
+        with sharded_tables(comm, cap=B):
+            fresh2 = DeepFM(sparse, dense, label, emb_size=DIM, layers=LAYERS, random_seed=123)
+        fresh2.load_weights(ck, torch.device("cpu"))
+        same2 = torch.equal(fresh2.embeddings.weight[:, :cols], model.embeddings.weight[:, :cols])
+        for k, v in model.state_dict().items():
+            if not k.startswith("embeddings"):
+                same2 = same2 and torch.equal(fresh2.state_dict()[k], v)
+        out["ckpt_reload_ok"] = np.array(bool(same2))
         np.savez(os.path.join(out_dir, f"rank{rank}.npz"), **out)
     finally:
         dist.destroy_process_group()
@@ -116,6 +128,10 @@ def test_two_rank_sharded_deepfm_matches_single_process(steps, chunk_batch):
         mp.spawn(_worker, args=(world, _free_port(), d, steps, chunk_batch), nprocs=world,
                  join=True)
         res = [dict(np.load(os.path.join(d, f"rank{r}.npz"))) for r in range(world)]
+        # the world-2 checkpoint into ONE unsharded model: the global tables
+        unsharded = _reference_model()
+        unsharded.load_weights(os.path.join(d, "ckpt.pt"), torch.device("cpu"))
+        ckpt_bank = unsharded.embeddings.weight.detach().numpy()
     ref = _reference_model()
     ref_losses = _train(ref, [_batch(100 + s, B * world) for s in range(steps)])
     # the global loss is the mean of the ranks' (equal-size) batch means
@@ -132,9 +148,11 @@ def test_two_rank_sharded_deepfm_matches_single_process(steps, chunk_batch):
     cols = bank.dim + 1
     for r in range(world):
         assert bool(res[r]["reload_ok"]), f"rank {r}: load_global_state_dict did not restore"
+        assert bool(res[r]["ckpt_reload_ok"]), f"rank {r}: load_weights did not restore"
         assert res[r]["global_bank"].shape == tuple(bank.weight.shape)
         np.testing.assert_allclose(res[r]["global_bank"][:, :cols],
                                    bank.weight.detach()[:, :cols].numpy(), rtol=1e-5, atol=1e-6)
+    np.testing.assert_array_equal(ckpt_bank[:, :cols], res[0]["global_bank"][:, :cols])
     for r in range(world):
         w = res[r]["embeddings__weight"]
         o_local = 0

@@ -824,12 +824,15 @@ class _Ctx:
 def pcie_inclusive(step, args, sparse, dense_cols, label_col, device):
     """Train steps whose batches start in HOST memory: ``ColumnarLoader`` packs the
     epoch into pinned memory (outside the timed region, as a real epoch would be
-    prepared ahead), then each batch crosses PCIe as one copy kernel enqueued
-    ``depth - 1`` batches ahead on the step's stream (one HIP graph per loader
-    slot).  Reported beside ``value``, never as it."""
+    prepared ahead), then each batch crosses PCIe as one copy kernel reading the
+    pinned record, on a branch of the step's HIP graph beside the step's kernels,
+    ``depth - 1`` batches ahead (ColumnarLoader.capture_steps: one graph of
+    ``depth`` steps, the record index a device cursor).  Reported beside ``value``
+    (DESIGN.md §5), never as it."""
     from pytorchrec_amd.loader import ColumnarDataset, ColumnarLoader
     B = args.batch
-    n_batches = max(args.steps, 12)
+    depth = 4
+    n_batches = -(-max(args.steps, 12) // depth) * depth
     N = B * n_batches
     g = torch.Generator().manual_seed(7)
     cols = {c.feature_name: torch.randint(0, c.category_num, (N,), generator=g,
@@ -838,30 +841,27 @@ def pcie_inclusive(step, args, sparse, dense_cols, label_col, device):
         cols[c.feature_name] = torch.rand(N, generator=g)
     cols[label_col.feature_name] = (torch.rand(N, generator=g) < 0.25).float()
     ds = ColumnarDataset(cols, dense_group=[c.feature_name for c in dense_cols])
-    ld = ColumnarLoader(ds, B, device, depth=3)
+    ld = ColumnarLoader(ds, B, device, depth=depth)
     for s, _ in ld.iter_slots():  # eager epoch: warms the model and fills every slot
         step(ld.slot_views(s))
     torch.cuda.synchronize()
-    graphs = []
-    for k in range(ld.depth):
-        gr = torch.cuda.CUDAGraph()
-        with torch.cuda.graph(gr, capture_error_mode="thread_local"):
-            step(ld.slot_views(k))
-        graphs.append(gr)
+    ge = ld.capture_steps(step)
+    for _ in ge.replays():  # one untimed graph epoch
+        pass
     ld.prepare_epoch()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     n = 0
-    for s, _ in ld.iter_slots():
-        graphs[s].replay()
-        n += 1
+    for _ in ge.replays():
+        n += depth
     torch.cuda.synchronize()
     el = time.perf_counter() - t0
     return {"value": round(n * B / el, 1), "unit": "samples/s", "steps": n,
             "ms_per_step": round(el / n * 1e3, 4), "h2d_bytes_per_step": ld.layout.slot_bytes,
-            "feed": "ColumnarLoader (pytorchrec_amd/loader.py), depth 3: one packed pinned "
-                    "record per batch copied by mrec_batch_stage (kernel reading the host "
-                    "record over PCIe), enqueued ahead on the step stream, one HIP graph per slot"}
+            "feed": f"ColumnarLoader (pytorchrec_amd/loader.py), depth {depth}: one packed pinned "
+                    "record per batch copied by mrec_batch_stage_cursor (kernel reading the "
+                    "host record over PCIe) on a branch of the step's HIP graph, depth - 1 "
+                    "batches ahead; one graph of depth steps replayed (capture_steps)"}
 
 
 # ----------------------------------------------------------------------------

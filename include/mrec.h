@@ -975,6 +975,15 @@ mrec_status mrec_tower_weight_prep(const float *W, int64_t N, int64_t K, int64_t
  * SimpleDataReader.__getitem__ (torchrec/data/SimpleDataReader.py:323-331). */
 mrec_status mrec_batch_stage(void *dst, const void *host_src, int64_t bytes, mrec_stream stream);
 
+/* ABI 27: the record at a DEVICE cursor of a pinned epoch buffer (n_records records
+ * of record_bytes each, one pinned allocation): copies record d_state[0] (nothing
+ * when it is past the last) into dst, then advances d_state[0] by one (d_state[1]:
+ * a ticket word, zero before the first call, left zero).  Captured into a HIP graph
+ * on a branch beside the train step, every replay stages the next batch while the
+ * step runs (no host work per step; loader.py ColumnarLoader.capture_steps). */
+mrec_status mrec_batch_stage_cursor(void *dst, const void *host_base, int64_t record_bytes,
+                                    int64_t n_records, uint64_t *d_state, mrec_stream stream);
+
 /* ------------------------------------------------------------------------- */
 /* CTR head and loss                                                          */
 /* ------------------------------------------------------------------------- */

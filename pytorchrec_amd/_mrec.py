@@ -275,6 +275,7 @@ SIGNATURES = {
     "mrec_weight_prep": (ctypes.c_int, [_vp, _i64, _i64, _i64, _vp, _i64, _vp, _i64, _vp]),
     "mrec_sgd_multi": (ctypes.c_int, [_i32, ctypes.POINTER(SgdJob), _vp]),
     "mrec_batch_stage": (ctypes.c_int, [_vp, _vp, _i64, _vp]),
+    "mrec_batch_stage_cursor": (ctypes.c_int, [_vp, _vp, _i64, _i64, _vp, _vp]),
     "mrec_dcn_cross_bwd_prep": (ctypes.c_int, [_i64, _i64, _vp, _i64, _vp, _i64, _vp, _i64, _vp,
                                                _i64, _vp, _i64, _i32, _vp, _i64, _vp]),
     "mrec_emb_bwd_large_workspace_size": (ctypes.c_size_t, [_bank_p, _i64]),

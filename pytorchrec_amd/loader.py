@@ -292,6 +292,39 @@ class ColumnarLoader:
         finally:
             self._iterating = False
 
+    # -- graph-captured steps, the H2D copy on a branch of the graph (ABI 27) ------
+    def capture_steps(self, step) -> "GraphEpoch":
+        """Capture ONE HIP graph of ``depth`` train steps ``step(batch_dict)``: step j
+        reads device slot j while a branch of the graph stages the record ``depth - 1``
+        batches ahead into the slot step j - 1 read (``mrec_batch_stage_cursor``: the
+        record index is a device cursor, so every replay stages the next records with
+        no host work and the copy runs beside the step's kernels instead of before
+        them).  Call ``step`` eagerly on ``slot_views`` first (warm-up).  Epochs are
+        then run by ``GraphEpoch.replays()``; they need full batches in a multiple of
+        ``depth``."""
+        if self.device.type != "cuda" or self.copy != "kernel":
+            raise RuntimeError("capture_steps needs a cuda device and copy='kernel'")
+        self.prepare_epoch()  # the pinned epoch buffer the graph reads (fixed address)
+        self._ensure_slots()
+        state = torch.zeros(2, dtype=torch.int64, device=self.device)
+        main = torch.cuda.current_stream(self.device)
+        side = torch.cuda.Stream(device=self.device)
+        g = torch.cuda.CUDAGraph()
+        host = self._host
+        with torch.cuda.graph(g, capture_error_mode="thread_local"):
+            cap = torch.cuda.current_stream(self.device)
+            for j in range(self.depth):
+                side.wait_stream(cap)
+                with torch.cuda.stream(side):
+                    _mrec.call("mrec_batch_stage_cursor",
+                               self._slots[(j + self.depth - 1) % self.depth].data_ptr(),
+                               host.data_ptr(), self.layout.slot_bytes, host.shape[0],
+                               state.data_ptr(), _mrec.stream_handle(self.device))
+                step(self.layout.views(self._slots[j], self.batch_size))
+                cap.wait_stream(side)
+        del main
+        return GraphEpoch(self, g, state, host)
+
     def __iter__(self) -> Iterator[Dict[str, Tensor]]:
         if self.device.type == "cuda":
             for s, n in self.iter_slots():
@@ -304,3 +337,38 @@ class ColumnarLoader:
                     yield self.layout.views(self._host[j], n)
             finally:
                 self._iterating = False
+
+
+class GraphEpoch:
+    """Epochs of a ``ColumnarLoader`` run by replaying the graph ``capture_steps``
+    captured (``depth`` steps per replay)."""
+
+    def __init__(self, loader: ColumnarLoader, graph, state: Tensor, host: Tensor):
+        self.loader, self.graph, self.state, self.host = loader, graph, state, host
+
+    def replays(self) -> Iterator[int]:
+        """Run one epoch: stage its first ``depth - 1`` batches, then replay the
+        graph len / depth times (yielding the first batch index of each replay)."""
+        ld = self.loader
+        sizes = ld._take_epoch()
+        d = ld.depth
+        if ld._host.data_ptr() != self.host.data_ptr():
+            raise RuntimeError("the loader's host buffer moved since capture_steps")
+        if any(n != ld.batch_size for n in sizes) or len(sizes) % d:
+            raise ValueError(f"graph epochs need full batches in a multiple of depth={d} "
+                             f"(got {len(sizes)} batches)")
+        ld._iterating = True
+        try:
+            for j in range(min(d - 1, len(sizes))):
+                _mrec.call("mrec_batch_stage", ld._slots[j].data_ptr(), ld._host[j].data_ptr(),
+                           ld.layout.slot_bytes, _mrec.stream_handle(ld.device))
+            self.state.zero_()
+            self.state[0] = d - 1
+            for r in range(len(sizes) // d):
+                self.graph.replay()
+                yield r * d
+            if ld._reading is None:
+                ld._reading = torch.cuda.Event()
+            ld._reading.record(torch.cuda.current_stream(ld.device))
+        finally:
+            ld._iterating = False

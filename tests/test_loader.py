@@ -231,3 +231,38 @@ def _check_training(cols, n, batch, gpu):
     assert losses[0] == losses[2]
     for k in losses[1]:
         assert torch.equal(losses[1][k], losses[3][k]), k
+
+
+@pytest.mark.gpu
+def test_gpu_graph_epochs_stage_on_a_branch_bit_exact(gpu):
+    """ColumnarLoader.capture_steps: one HIP graph of ``depth`` steps, the H2D copy of
+    the batch depth - 1 ahead on a branch beside each step (mrec_batch_stage_cursor,
+    device cursor): over two shuffled epochs every step sees exactly its batch, with
+    a slow step (the copy of the next batches must not overtake it)."""
+    n, batch, depth = 1536, 128, 4  # 12 batches: 3 replays per epoch
+    cols = _columns(n, seed=3)
+    ds = _dataset(n, seed=3)
+    ld = ColumnarLoader(ds, batch, device=gpu, shuffle=True, seed=31, depth=depth)
+    seen = torch.zeros(depth, batch, dtype=torch.int32, device=gpu)
+    dense = torch.zeros(depth, batch, ds.dense.shape[1], dtype=torch.float32, device=gpu)
+    calls = [0]
+
+    def step(b):
+        j = calls[0] % depth
+        calls[0] += 1
+        torch.cuda._sleep(1_000_000)
+        seen[j].copy_(b["c_c_C0"])
+        dense[j].copy_(b["__dense__"])
+
+    for s, _ in ld.iter_slots():  # eager warm-up epoch
+        step(ld.slot_views(s))
+    ge = ld.capture_steps(step)
+    for e in range(2):
+        order = torch.randperm(n, generator=torch.Generator().manual_seed(31 + 1 + e))
+        for first in ge.replays():
+            torch.cuda.synchronize()
+            for j in range(depth):
+                want = _expected(cols, order[(first + j) * batch:(first + j + 1) * batch])
+                assert torch.equal(seen[j].cpu(), want["c_c_C0"]), (e, first, j)
+                wd = torch.stack([want[f"c_n_I{k}"] for k in range(N_DENSE)], 1)
+                assert torch.equal(dense[j].cpu(), wd), (e, first, j)

@@ -376,7 +376,7 @@ size_t mrec_emb_bwd_large_error_offset(void);
 struct mrec_gemm_call_s; /* mrec_gemm_call, defined with the GEMM entry points below */
 
 /*
- * mrec_emb_bwd_large_fused plus up to 4 deferred split-K weight-gradient reductions
+ * mrec_emb_bwd_large_fused plus up to 6 deferred split-K weight-gradient reductions
  * (phase MREC_GEMM_REDUCE, as for mrec_emb_bwd_apply_ex) run by workgroups after
  * the bucket kernel's own (ABI 24): DIN's top-tower dW reduce + fused SGD leaves
  * its standalone launch.  They must not touch what the update reads or writes.  On
@@ -408,7 +408,7 @@ mrec_status mrec_emb_bwd_large_fused_given(const mrec_table_bank *bank, const mr
                                            mrec_stream stream);
 
 /*
- * mrec_emb_bwd_apply plus up to 2 deferred split-K weight-gradient reductions
+ * mrec_emb_bwd_apply plus up to 6 deferred split-K weight-gradient reductions
  * (mrec_gemm_call with phase MREC_GEMM_REDUCE, e.g. the first MLP layer's dW +
  * fused SGD) run by extra workgroups of the same launch.  They must not touch
  * what the apply reads or writes.  A HIP graph runs the step's kernels one after
@@ -431,7 +431,7 @@ mrec_status mrec_emb_bwd_apply_ex(const mrec_table_bank *bank, int64_t batch,
  * else (b / chunk) * chunk_stride + f * chunk + b % chunk — the receive buffer of
  * mrec_shard_lookup_grad rows after the reverse all-to-all (fp32, g_ld % 4 == 0).
  * The owner side of a row-sharded table (SURVEY.md §8e backward).  Like
- * mrec_emb_bwd_apply_ex, up to 2 deferred weight-gradient reductions may ride along.
+ * mrec_emb_bwd_apply_ex, up to 6 deferred weight-gradient reductions may ride along.
  */
 mrec_status mrec_emb_bwd_apply_given(const mrec_table_bank *bank, int64_t batch,
                                      const void *workspace, size_t ws_bytes, const void *dx,
@@ -944,6 +944,11 @@ typedef struct {
 
 mrec_status mrec_tower_dw(const mrec_tower_dw_args *args, const mrec_head_finish_job *finish,
                           mrec_stream stream);
+/* ABI 27: + the batch feed's copy of the next record in extra workgroups (feed may be
+ * NULL; see mrec_feed_job) */
+struct mrec_feed_job_s; /* mrec_feed_job, defined with the batch feed below */
+mrec_status mrec_tower_dw_ex(const mrec_tower_dw_args *args, const mrec_head_finish_job *finish,
+                             const struct mrec_feed_job_s *feed, mrec_stream stream);
 
 /* elements of the k-fragment image of a [rows, cols] matrix: one 1 KiB block per 16
  * columns x 32 rows, block (c / 16) * ceil(rows / 32) + r / 32, lane
@@ -983,6 +988,17 @@ mrec_status mrec_batch_stage(void *dst, const void *host_src, int64_t bytes, mre
  * step runs (no host work per step; loader.py ColumnarLoader.capture_steps). */
 mrec_status mrec_batch_stage_cursor(void *dst, const void *host_base, int64_t record_bytes,
                                     int64_t n_records, uint64_t *d_state, mrec_stream stream);
+
+/* The same copy as a job another launch runs in extra workgroups (ABI 27:
+ * mrec_tower_dw_ex), so the PCIe reads overlap that launch's work instead of taking
+ * their own ~15 us on the step's critical path. */
+typedef struct mrec_feed_job_s {
+  void *dst;                 /* the device slot (16-B aligned) */
+  const void *host_base;     /* the pinned epoch buffer: n_records x record_bytes */
+  int64_t record_bytes;
+  int64_t n_records;
+  uint64_t *d_state;         /* [0] cursor (the record to copy, advanced by one), [1] ticket */
+} mrec_feed_job;
 
 /* ------------------------------------------------------------------------- */
 /* CTR head and loss                                                          */

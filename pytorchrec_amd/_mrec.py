@@ -191,6 +191,13 @@ class TowerDwArgs(ctypes.Structure):
                 ("splits", ctypes.c_int32)]
 
 
+class FeedJob(ctypes.Structure):
+    """mrec_feed_job (include/mrec.h, ABI 27)."""
+    _fields_ = [("dst", ctypes.c_void_p), ("host_base", ctypes.c_void_p),
+                ("record_bytes", ctypes.c_int64), ("n_records", ctypes.c_int64),
+                ("d_state", ctypes.c_void_p)]
+
+
 LAYOUT_ROW, LAYOUT_COL = 0, 1
 ACT_NONE, ACT_RELU = 0, 1
 
@@ -268,6 +275,8 @@ SIGNATURES = {
                                  _vp, ctypes.c_int, _i64, _i32, _vp, ctypes.c_size_t, _vp]),
     "mrec_gemm_multi": (ctypes.c_int, [_i32, ctypes.POINTER(GemmCall), _vp]),
     "mrec_tower_dw": (ctypes.c_int, [ctypes.POINTER(TowerDwArgs), ctypes.POINTER(HeadFinishJob), _vp]),
+    "mrec_tower_dw_ex": (ctypes.c_int, [ctypes.POINTER(TowerDwArgs), ctypes.POINTER(HeadFinishJob),
+                                        ctypes.POINTER(FeedJob), _vp]),
     "mrec_kfrag_elems": (_i64, [_i64, _i64]),
     "mrec_kfrag_pack": (ctypes.c_int, [_vp, _i64, _i64, _i64, _vp, _vp]),
     "mrec_gemm_multi_ex": (ctypes.c_int, [_i32, ctypes.POINTER(GemmCall), ctypes.POINTER(PlanJob),

@@ -762,7 +762,13 @@ struct DaShape2 : DaShape<E, H1T, H1K, H2T, H2K> {
   // fp32 tail: b1 [H1N], b2 [H2N], w3 [H2N], then per slot q [E], du [E], g [64], dq [4][E]
   static constexpr int nslot32 = 2 * E + DA_ROWS + 4 * E;
   static constexpr int nf32 = B::H1N + 2 * B::H2N + 2 * nslot32;
-  static constexpr size_t bytes = bf_end * 2 + nf32 * 4;
+  static constexpr size_t core_bytes = bf_end * 2 + nf32 * 4;
+  // per wave: its 16 rows' bf16 gradient staged in LDS so that the rows leave as
+  // whole 16-B pieces (one 2-B store per lane wrote 32-B row pieces: 2x the HBM writes)
+  static constexpr int SP = E + 8;  // staging row pitch (elements)
+  static constexpr size_t stage_off = (core_bytes + 15) / 16 * 16;
+  static constexpr size_t bytes = stage_off + (DA_THREADS / 64) * 16 * SP * 2;
+  static_assert(bytes <= 160 * 1024, "LDS");
   // after the loop: column partials [8][H1N + 2 H2N] | b3 [2]
   static constexpr size_t red_bytes = (8 * (B::H1N + 2 * B::H2N) + 2) * 4;
   static_assert(red_bytes <= bytes, "the end reduction reuses the workgroup's LDS");
@@ -833,6 +839,7 @@ __global__ __launch_bounds__(DA_THREADS) void din_att_bwd2_kernel(DinAttArgs p) 
   uint16_t *Z1 = sm + S::oS + slot * S::slot_elems + S::sZ1;
   const uint16_t *W1 = sm + S::oW1, *W2 = sm + S::oW2;
   const uint16_t *slots = sm + S::oS;
+  uint16_t *stg = reinterpret_cast<uint16_t *>(da_lds + S::stage_off) + w * 16 * S::SP;
   __shared__ int snv[2];  // per slot: rows up to the last one with a_j != 0
   DA_STAMP(0);
   da_zero_lds(da_lds, S::bf_end * 2);
@@ -1042,12 +1049,25 @@ __global__ __launch_bounds__(DA_THREADS) void din_att_bwd2_kernel(DinAttArgs p) 
         const float ke = bf16_to_f32(X[r * LDX + E + e]);
         const float ar = __shfl(aj, r);
         const float dk = fmaf(ar, due, dfk - dfd + dfm * qe);
-        if (have && r < p.L)
-          p.drows[(p.batch + b * p.L + r) * p.ld_drows + e] = f32_to_bf16_rne(dk);
+        stg[(r - 16 * rt) * S::SP + e] = f32_to_bf16_rne(dk);
         dqp += dfq + dfd + dfm * ke;
       }
       dqp = swap32_sum(swap16_sum(dqp));  // the 4 row groups of column e
       if (lane < 16) sdq[rt * E + e] = dqp;
+    }
+    // the wave's 16 rows of dk leave as 16-B pieces (its own staging rows: a wave-local
+    // LDS round trip, no barrier)
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_wave_barrier();
+    if (have) {
+      constexpr int QPR = E / 8;  // 16-B pieces per row
+#pragma unroll
+      for (int idx = lane; idx < 16 * QPR; idx += 64) {
+        const int rr = idx / QPR, q = idx - rr * QPR, r = 16 * rt + rr;
+        if (r < p.L)
+          *reinterpret_cast<uint4 *>(p.drows + (p.batch + b * p.L + r) * p.ld_drows + 8 * q) =
+              *reinterpret_cast<const uint4 *>(stg + rr * S::SP + 8 * q);
+      }
     }
     // ---- dW1 += dZ1^T X over both slots' rows ----
 #pragma unroll
@@ -1361,7 +1381,8 @@ mrec_status mrec_din_att_bwd(const void *rows, int64_t ld_rows, int64_t batch, i
   MREC_CHECK_ARG(a && dtop && d_rows && part, "NULL pointer");
   MREC_CHECK_ARG((reinterpret_cast<uintptr_t>(dtop) & 15) == 0 && lddt % 8 == 0 && lddt >= 2 * E,
                  "dtop must be 16-byte aligned bf16 rows of >= 2E elements");
-  MREC_CHECK_ARG(ld_drows >= E, "bad d_rows stride");
+  MREC_CHECK_ARG(ld_drows >= E && ld_drows % 8 == 0 && (reinterpret_cast<uintptr_t>(d_rows) & 15) == 0,
+                 "d_rows must be 16-byte aligned bf16 rows (ld_drows a multiple of 8, >= E)");
   MREC_CHECK_ARG(parts == mrec_din_att_parts(batch), "parts must be mrec_din_att_parts(batch)");
   if (batch == 0) return MREC_OK;
   DinAttArgs p{};

@@ -10,6 +10,7 @@
 #include <algorithm>
 
 #include "common.h"
+#include "feed_common.h"
 
 namespace mrec {
 
@@ -28,44 +29,50 @@ __global__ __launch_bounds__(256) void batch_stage_kernel(const uint4 *__restric
   for (; i < n16; i += stride) dst[i] = src[i];
 }
 
-// the record at the device cursor (state[0]) of a pinned epoch buffer; the last
-// workgroup to finish (ticket state[1]) advances the cursor, so a HIP graph that
-// contains this launch stages the NEXT record on every replay
-__global__ __launch_bounds__(256) void batch_stage_cursor_kernel(const char *__restrict__ base,
-                                                                 int64_t record_bytes,
-                                                                 int64_t n_records,
-                                                                 uint4 *__restrict__ dst,
-                                                                 unsigned long long *state) {
+__global__ __launch_bounds__(256) void batch_stage_cursor_kernel(FeedCopy fc) {
   __shared__ long long s_rec;
-  if (threadIdx.x == 0)
-    s_rec = static_cast<long long>(__hip_atomic_load(state, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
-  __syncthreads();
-  const long long rec = s_rec;
-  if (rec >= 0 && rec < n_records) {
-    const uint4 *src = reinterpret_cast<const uint4 *>(base + rec * record_bytes);
-    const int64_t n16 = record_bytes / 16;
-    constexpr int U = 4;
-    const int64_t stride = static_cast<int64_t>(gridDim.x) * 256;
-    int64_t i = static_cast<int64_t>(blockIdx.x) * 256 + threadIdx.x;
-    for (; i + (U - 1) * stride < n16; i += U * stride) {
-      uint4 v[U];
-#pragma unroll
-      for (int u = 0; u < U; ++u) v[u] = src[i + u * stride];
-#pragma unroll
-      for (int u = 0; u < U; ++u) dst[i + u * stride] = v[u];
-    }
-    for (; i < n16; i += stride) dst[i] = src[i];
+  feed_copy_body<256>(fc, blockIdx.x, &s_rec);
+}
+
+mrec_status build_feed_copy(const mrec_feed_job *job, int threads, FeedCopy *out) {
+  *out = FeedCopy{};
+  MREC_CHECK_ARG(job != nullptr, "NULL feed job");
+  const mrec_feed_job &j = *job;
+  MREC_CHECK_ARG(j.record_bytes > 0 && j.n_records >= 0, "bad record size / count");
+  MREC_CHECK_ARG(j.dst && j.host_base && j.d_state, "NULL pointer");
+  MREC_CHECK_ARG(j.record_bytes % 16 == 0 && (reinterpret_cast<uintptr_t>(j.dst) & 15) == 0 &&
+                     (reinterpret_cast<uintptr_t>(j.host_base) & 15) == 0 &&
+                     (reinterpret_cast<uintptr_t>(j.d_state) & 7) == 0,
+                 "dst / host_base must be 16-B aligned, record_bytes a multiple of 16");
+  // the whole epoch buffer must be ONE pinned, device-visible host allocation
+  hipPointerAttribute_t attr;
+  if (hipPointerGetAttributes(&attr, j.host_base) != hipSuccess || attr.type != hipMemoryTypeHost ||
+      attr.devicePointer == nullptr) {
+    (void)hipGetLastError();
+    set_error("feed job: host_base is not pinned (hipHostMalloc) host memory");
+    return MREC_EINVAL;
   }
-  __syncthreads();  // every thread of this workgroup has read the cursor (s_rec)
-  if (threadIdx.x == 0) {
-    const unsigned long long t =
-        __hip_atomic_fetch_add(state + 1, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    if (t == gridDim.x - 1) {  // the last arriver: every workgroup read the cursor already
-      __hip_atomic_store(state + 1, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      __hip_atomic_store(state, static_cast<unsigned long long>(rec + 1), __ATOMIC_RELAXED,
-                         __HIP_MEMORY_SCOPE_AGENT);
+  const char *dev_base = static_cast<const char *>(attr.devicePointer);
+  if (j.n_records > 0) {
+    const char *last = static_cast<const char *>(j.host_base) + j.n_records * j.record_bytes - 1;
+    hipPointerAttribute_t attr2;
+    if (hipPointerGetAttributes(&attr2, last) != hipSuccess || attr2.type != hipMemoryTypeHost ||
+        static_cast<const char *>(attr2.devicePointer) !=
+            dev_base + (last - static_cast<const char *>(j.host_base))) {
+      (void)hipGetLastError();
+      set_error("feed job: the epoch buffer is not one pinned allocation");
+      return MREC_EINVAL;
     }
   }
+  out->src = dev_base;
+  out->record_bytes = j.record_bytes;
+  out->n_records = j.n_records;
+  out->dst = static_cast<uint4 *>(j.dst);
+  out->state = reinterpret_cast<unsigned long long *>(j.d_state);
+  const int64_t n16 = j.record_bytes / 16;
+  out->blocks = static_cast<int>(std::max<int64_t>(
+      std::min<int64_t>((n16 + 4 * threads - 1) / (4 * threads), 1024), 1));
+  return MREC_OK;
 }
 
 }  // namespace mrec
@@ -101,36 +108,11 @@ mrec_status mrec_batch_stage(void *dst, const void *host_src, int64_t bytes, mre
 
 mrec_status mrec_batch_stage_cursor(void *dst, const void *host_base, int64_t record_bytes,
                                     int64_t n_records, uint64_t *d_state, mrec_stream stream) {
-  MREC_CHECK_ARG(record_bytes > 0 && n_records >= 0, "bad record size / count");
-  MREC_CHECK_ARG(dst && host_base && d_state, "NULL pointer");
-  MREC_CHECK_ARG(record_bytes % 16 == 0 && (reinterpret_cast<uintptr_t>(dst) & 15) == 0 &&
-                     (reinterpret_cast<uintptr_t>(host_base) & 15) == 0 &&
-                     (reinterpret_cast<uintptr_t>(d_state) & 7) == 0,
-                 "dst / host_base must be 16-B aligned, record_bytes a multiple of 16");
-  // the whole epoch buffer must be pinned, device-visible host memory
-  hipPointerAttribute_t attr;
-  const char *last = static_cast<const char *>(host_base) +
-                     (n_records > 0 ? n_records * record_bytes - 1 : 0);
-  if (hipPointerGetAttributes(&attr, host_base) != hipSuccess || attr.type != hipMemoryTypeHost ||
-      attr.devicePointer == nullptr) {
-    (void)hipGetLastError();
-    set_error("mrec_batch_stage_cursor: host_base is not pinned (hipHostMalloc) host memory");
-    return MREC_EINVAL;
-  }
-  const char *dev_base = static_cast<const char *>(attr.devicePointer);
-  hipPointerAttribute_t attr2;
-  if (hipPointerGetAttributes(&attr2, last) != hipSuccess || attr2.type != hipMemoryTypeHost ||
-      static_cast<const char *>(attr2.devicePointer) != dev_base + (last - static_cast<const char *>(host_base))) {
-    (void)hipGetLastError();
-    set_error("mrec_batch_stage_cursor: the epoch buffer is not one pinned allocation");
-    return MREC_EINVAL;
-  }
-  const int64_t n16 = record_bytes / 16;
-  const int64_t blocks = std::max<int64_t>(std::min<int64_t>((n16 + 1023) / 1024, 1024), 1);
-  batch_stage_cursor_kernel<<<dim3(static_cast<unsigned>(blocks)), 256, 0,
-                              static_cast<hipStream_t>(stream)>>>(
-      dev_base, record_bytes, n_records, static_cast<uint4 *>(dst),
-      reinterpret_cast<unsigned long long *>(d_state));
+  const mrec_feed_job job{dst, host_base, record_bytes, n_records, d_state};
+  FeedCopy fc;
+  if (mrec_status st = build_feed_copy(&job, 256, &fc); st != MREC_OK) return st;
+  batch_stage_cursor_kernel<<<dim3(static_cast<unsigned>(fc.blocks)), 256, 0,
+                              static_cast<hipStream_t>(stream)>>>(fc);
   return launch_status("mrec_batch_stage_cursor");
 }
 

@@ -1,0 +1,62 @@
+// The batch feed's copy of one pinned host record into its device slot, as a body
+// any launch can run in some of its workgroups (feed.hip's own kernels; the tower's
+// weight-gradient launch, tower_dw.hip, where the PCIe reads overlap the L2-bound
+// MFMA work instead of taking their own ~15 us on the step's critical path).
+//
+// The record index is a device cursor (state[0]); the workgroups that copy it count
+// themselves on a ticket (state[1]) and the last one advances the cursor, so a HIP
+// graph holding the launch stages the next record on every replay.
+#pragma once
+#include "common.h"
+
+namespace mrec {
+
+struct FeedCopy {
+  const char *src;            // device address of the pinned epoch buffer
+  int64_t record_bytes;
+  int64_t n_records;
+  uint4 *dst;                 // the device slot
+  unsigned long long *state;  // [0] cursor, [1] ticket
+  int blocks;                 // workgroups of the launch that copy (0: none)
+};
+
+// run by workgroup `b` of the `fc.blocks` copying ones (THREADS threads each)
+template <int THREADS>
+__device__ __forceinline__ void feed_copy_body(const FeedCopy &fc, int b, long long *s_rec) {
+  if (threadIdx.x == 0)
+    *s_rec = static_cast<long long>(
+        __hip_atomic_load(fc.state, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+  __syncthreads();
+  const long long rec = *s_rec;
+  if (rec >= 0 && rec < fc.n_records) {
+    const uint4 *src = reinterpret_cast<const uint4 *>(fc.src + rec * fc.record_bytes);
+    const int64_t n16 = fc.record_bytes / 16;
+    constexpr int U = 4;  // independent 16-B loads per lane per trip
+    const int64_t stride = static_cast<int64_t>(fc.blocks) * THREADS;
+    int64_t i = static_cast<int64_t>(b) * THREADS + threadIdx.x;
+    for (; i + (U - 1) * stride < n16; i += U * stride) {
+      uint4 v[U];
+#pragma unroll
+      for (int u = 0; u < U; ++u) v[u] = src[i + u * stride];
+#pragma unroll
+      for (int u = 0; u < U; ++u) fc.dst[i + u * stride] = v[u];
+    }
+    for (; i < n16; i += stride) fc.dst[i] = src[i];
+  }
+  __syncthreads();  // every thread of this workgroup has read the cursor
+  if (threadIdx.x == 0) {
+    const unsigned long long t =
+        __hip_atomic_fetch_add(fc.state + 1, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (t == static_cast<unsigned long long>(fc.blocks) - 1) {  // every workgroup read it
+      __hip_atomic_store(fc.state + 1, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_store(fc.state, static_cast<unsigned long long>(rec + 1), __ATOMIC_RELAXED,
+                         __HIP_MEMORY_SCOPE_AGENT);
+    }
+  }
+}
+
+// host (feed.hip): validate a mrec_feed_job and fill *out (blocks: the copying
+// workgroups of THREADS threads)
+mrec_status build_feed_copy(const mrec_feed_job *job, int threads, FeedCopy *out);
+
+}  // namespace mrec

@@ -586,7 +586,7 @@ mrec_status build_co_reduce(int32_t n_reduce, const mrec_gemm_call *reduce, CoRe
   *co = {};
   *blocks = 0;
   MREC_CHECK_ARG(n_reduce >= 0 && n_reduce <= kMaxCoReduce && (n_reduce == 0 || reduce),
-                 "n_reduce out of [0, 4]");
+                 "n_reduce out of [0, 6]");
   for (int i = 0; i < n_reduce; ++i) {
     int64_t nb = 0;
     mrec_status st = build_reduce_job(reduce[i], &co->g[co->n], &nb);

@@ -216,7 +216,7 @@ int64_t reduce_blocks(const GemmArgs &g);
 // workgroups of an embedding-update launch (emb_bwd.hip's apply kernels,
 // emb_bwd_large.hip's bucket kernel): independent of the embedding update, and a
 // launch of their own would cost a kernel boundary on the step's serial path
-constexpr int kMaxCoReduce = 4;
+constexpr int kMaxCoReduce = 6;  // (C3: 3 cross + 2 MLP layers; kernel args stay < 4 KB)
 struct CoReduce {
   int n;
   int nblk[kMaxCoReduce];

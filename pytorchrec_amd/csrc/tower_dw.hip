@@ -26,6 +26,7 @@
 #include <cstdlib>
 
 #include "common.h"
+#include "feed_common.h"
 #include "head_common.h"
 #include "tower_common.h"
 
@@ -64,6 +65,7 @@ struct DwArgs {
   DwLayer lay[DW_MAXL];
   int fin_blocks;
   HeadFinishArgs fin;
+  FeedCopy feed;   // the batch feed's copy in workgroups [fin_blocks, fin_blocks + feed.blocks)
 };
 
 // One wave per workgroup, one 64 x 64 output tile (4 x 4 MFMA tiles) per wave.
@@ -76,7 +78,11 @@ __global__ __launch_bounds__(64) void tower_dw_kernel(DwArgs a, KClock kc) {
       ctr_head_finish_body<64>(a.fin, blockIdx.x, reinterpret_cast<float (*)[9]>(tile));
     return;
   }
-  const int b = blockIdx.x - a.fin_blocks;
+  if (static_cast<int>(blockIdx.x) < a.fin_blocks + a.feed.blocks) {  // uniform
+    feed_copy_body<64>(a.feed, blockIdx.x - a.fin_blocks, reinterpret_cast<long long *>(tile));
+    return;
+  }
+  const int b = blockIdx.x - a.fin_blocks - a.feed.blocks;
   int l = 0;
   while (l + 1 < a.L && b >= a.lay[l + 1].start) ++l;  // uniform
   const DwLayer &y = a.lay[l];
@@ -229,6 +235,11 @@ mrec_status mrec_kfrag_pack(const void *x, int64_t rows, int64_t cols, int64_t l
 
 mrec_status mrec_tower_dw(const mrec_tower_dw_args *p, const mrec_head_finish_job *finish,
                           mrec_stream stream) {
+  return mrec_tower_dw_ex(p, finish, nullptr, stream);
+}
+
+mrec_status mrec_tower_dw_ex(const mrec_tower_dw_args *p, const mrec_head_finish_job *finish,
+                             const mrec_feed_job *feed, mrec_stream stream) {
   MREC_CHECK_ARG(p != nullptr, "NULL args");
   const mrec_tower_dw_args &s = *p;
   MREC_CHECK_ARG(s.n_layers >= 1 && s.n_layers <= DW_MAXL, "n_layers must be in [1, 8]");
@@ -277,7 +288,10 @@ mrec_status mrec_tower_dw(const mrec_tower_dw_args *p, const mrec_head_finish_jo
     y.start = blocks;
     blocks += y.nbn * y.nbk * s.splits;
   }
-  const int grid = a.fin_blocks + blocks;
+  if (feed) {
+    if (mrec_status st = build_feed_copy(feed, 64, &a.feed); st != MREC_OK) return st;
+  }
+  const int grid = a.fin_blocks + a.feed.blocks + blocks;
   if (grid == 0) return MREC_OK;
   const KClock kc = kclock_take();
   if (kc.buf)

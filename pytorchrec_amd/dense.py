@@ -163,6 +163,7 @@ class _Call:
 
 
 _PENDING = []  # deferred split-K reductions (fused SGD of a layer's W, b and images)
+CO_REDUCE_MAX = 6  # reductions one embedding-update launch takes along (gemm_common.h kMaxCoReduce)
 
 # measurement hook (bench.py): when a dict, the tower launches of eager steps are
 # bracketed by HIP events on their stream: {name: [(start, end), ...]}
@@ -189,6 +190,22 @@ class _timed:
             e1.record()
             KERNEL_EVENTS.setdefault(self.name, []).append((self.e0, e1))
         return False
+
+
+# the batch feed's copy of a later batch (an mrec_feed_job, loader.capture_steps),
+# taken by the next mrec_tower_dw launch: its PCIe reads then run in extra workgroups
+# beside the L2-bound weight-gradient tiles instead of on the step's critical path
+_FEED_JOB = []
+
+
+def set_feed_job(job):
+    _FEED_JOB[:] = [job]
+
+
+def take_feed_job():
+    job = _FEED_JOB[0] if _FEED_JOB else None
+    _FEED_JOB.clear()
+    return job
 
 
 def launch_multi(calls):
@@ -1481,9 +1498,10 @@ def _tower_dw(calls, dys, xins, dims, B: int, splits: int):
         a.dy_img[l], a.x_img[l] = dys[l].data_ptr(), xins[l].data_ptr()
         a.ws[l], a.ldws[l] = c.ws.data_ptr(), (dims[l][1] + 1 + 7) // 8 * 8
     fin = _FINISH.pop(0) if _FINISH else None
+    feed = take_feed_job()
     with _timed("mrec_tower_dw"):
-        _mrec.call("mrec_tower_dw", ctypes.byref(a), ctypes.byref(fin.struct) if fin else None,
-                   _mrec.stream_handle())
+        _mrec.call("mrec_tower_dw_ex", ctypes.byref(a), ctypes.byref(fin.struct) if fin else None,
+                   ctypes.byref(feed) if feed is not None else None, _mrec.stream_handle())
     pend = _PENDING
     _PENDING = []
     _run_all(pend)

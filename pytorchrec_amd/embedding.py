@@ -359,7 +359,7 @@ def _apply(bank: EmbeddingBank, ws, ws_bytes, count, dx=None, dfm=None, fm_sum=N
     x0_dt = _mrec.dtype_code(x0.dtype) if x0 is not None else _mrec.F32
     # deferred MLP weight-gradient reductions (+ fused SGD) ride along this launch
     from pytorchrec_amd import dense as dense_ops
-    jobs = dense_ops.take_pending(4)
+    jobs = dense_ops.take_pending(dense_ops.CO_REDUCE_MAX)
     arr = (_mrec.GemmCall * len(jobs))(*[j.struct() for j in jobs]) if jobs else None
     _mrec.call("mrec_emb_bwd_apply_ex", bank.desc().ref(), count, ws.data_ptr(), ws_bytes,
                _mrec.ptr(dx), dx_dt, dx.stride(0) if dx is not None else 0,
@@ -411,7 +411,7 @@ def _backward_large(bank: EmbeddingBank, ids, batch, grad, dx=None, dfm=None, fm
         return
     # deferred MLP weight-gradient reductions (DIN's top tower) ride along the bucket kernel
     from pytorchrec_amd import dense as dense_ops
-    jobs = dense_ops.take_pending(4)
+    jobs = dense_ops.take_pending(dense_ops.CO_REDUCE_MAX)
     arr = (_mrec.GemmCall * len(jobs))(*[j.struct() for j in jobs]) if jobs else None
     args = _large_apply_args(bank, grad, dx, dfm, fm_sum, x0, dw, mode, lr)
     _mrec.call("mrec_emb_bwd_large_fused_ex", bank.desc().ref(), _ids_desc(ids).ref(), batch,

@@ -292,38 +292,39 @@ class ColumnarLoader:
         finally:
             self._iterating = False
 
-    # -- graph-captured steps, the H2D copy on a branch of the graph (ABI 27) ------
+    # -- graph-captured steps, the H2D copy inside the step (ABI 27) ---------------
     def capture_steps(self, step) -> "GraphEpoch":
         """Capture ONE HIP graph of ``depth`` train steps ``step(batch_dict)``: step j
-        reads device slot j while a branch of the graph stages the record ``depth - 1``
-        batches ahead into the slot step j - 1 read (``mrec_batch_stage_cursor``: the
-        record index is a device cursor, so every replay stages the next records with
-        no host work and the copy runs beside the step's kernels instead of before
-        them).  Call ``step`` eagerly on ``slot_views`` first (warm-up).  Epochs are
-        then run by ``GraphEpoch.replays()``; they need full batches in a multiple of
-        ``depth``."""
+        reads device slot j while the record ``depth - 1`` batches ahead is copied into
+        the slot step j - 1 read (``mrec_feed_job``: the record index is a device
+        cursor, so every replay stages the next records with no host work).  The copy
+        runs in extra workgroups of the step's fused-tower weight-gradient launch
+        (``mrec_tower_dw_ex``: PCIe reads beside L2-bound tiles; a graph branch on a
+        side stream was serialised by the graph executor), or after the step when the
+        model has none (``mrec_batch_stage_cursor``).  Call ``step`` eagerly on
+        ``slot_views`` first (warm-up).  Epochs are then run by
+        ``GraphEpoch.replays()``; they need full batches in a multiple of ``depth``."""
         if self.device.type != "cuda" or self.copy != "kernel":
             raise RuntimeError("capture_steps needs a cuda device and copy='kernel'")
+        from pytorchrec_amd import dense as dense_ops
         self.prepare_epoch()  # the pinned epoch buffer the graph reads (fixed address)
         self._ensure_slots()
         state = torch.zeros(2, dtype=torch.int64, device=self.device)
-        main = torch.cuda.current_stream(self.device)
-        side = torch.cuda.Stream(device=self.device)
         g = torch.cuda.CUDAGraph()
         host = self._host
+        jobs = [_mrec.FeedJob(self._slots[(j + self.depth - 1) % self.depth].data_ptr(),
+                              host.data_ptr(), self.layout.slot_bytes, host.shape[0],
+                              state.data_ptr()) for j in range(self.depth)]
         with torch.cuda.graph(g, capture_error_mode="thread_local"):
-            cap = torch.cuda.current_stream(self.device)
             for j in range(self.depth):
-                side.wait_stream(cap)
-                with torch.cuda.stream(side):
-                    _mrec.call("mrec_batch_stage_cursor",
-                               self._slots[(j + self.depth - 1) % self.depth].data_ptr(),
-                               host.data_ptr(), self.layout.slot_bytes, host.shape[0],
-                               state.data_ptr(), _mrec.stream_handle(self.device))
+                dense_ops.set_feed_job(jobs[j])
                 step(self.layout.views(self._slots[j], self.batch_size))
-                cap.wait_stream(side)
-        del main
-        return GraphEpoch(self, g, state, host)
+                left = dense_ops.take_feed_job()
+                if left is not None:  # no tower weight-gradient launch in this step
+                    _mrec.call("mrec_batch_stage_cursor", left.dst, left.host_base,
+                               left.record_bytes, left.n_records, left.d_state,
+                               _mrec.stream_handle(self.device))
+        return GraphEpoch(self, g, state, host, jobs)
 
     def __iter__(self) -> Iterator[Dict[str, Tensor]]:
         if self.device.type == "cuda":
@@ -343,8 +344,9 @@ class GraphEpoch:
     """Epochs of a ``ColumnarLoader`` run by replaying the graph ``capture_steps``
     captured (``depth`` steps per replay)."""
 
-    def __init__(self, loader: ColumnarLoader, graph, state: Tensor, host: Tensor):
+    def __init__(self, loader: ColumnarLoader, graph, state: Tensor, host: Tensor, jobs):
         self.loader, self.graph, self.state, self.host = loader, graph, state, host
+        self.jobs = jobs  # (the captured kernels' argument blocks point at these buffers)
 
     def replays(self) -> Iterator[int]:
         """Run one epoch: stage its first ``depth - 1`` batches, then replay the

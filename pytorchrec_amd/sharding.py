@@ -620,7 +620,7 @@ def sender_grad_sums(bank: ShardedEmbeddingBank, rows_recv: torch.Tensor, pos: t
     ws, wsb = plan
     B = pos.shape[1]
     from pytorchrec_amd import dense as dense_ops
-    jobs = dense_ops.take_pending(4)
+    jobs = dense_ops.take_pending(dense_ops.CO_REDUCE_MAX)
     arr = (_mrec.GemmCall * len(jobs))(*[j.struct() for j in jobs]) if jobs else None
     rdesc = remote_desc(bank, rows_recv)
     _mrec.call("mrec_emb_bwd_apply_ex", rdesc.ref(), B, ws.data_ptr(), wsb,
@@ -647,7 +647,7 @@ def sender_grad_records(bank: ShardedEmbeddingBank, rows_recv: torch.Tensor, pos
     wire = torch.empty(P, bank.cap_rows * rb, dtype=torch.uint8, device=bank.weight.device)
     out = _mrec.GradRecords(wire.data_ptr(), rb, spref.data_ptr(), bank.cap, bank.cap_rows)
     from pytorchrec_amd import dense as dense_ops
-    jobs = dense_ops.take_pending(4)
+    jobs = dense_ops.take_pending(dense_ops.CO_REDUCE_MAX)
     arr = (_mrec.GemmCall * len(jobs))(*[j.struct() for j in jobs]) if jobs else None
     rdesc = remote_desc(bank, rows_recv)
     _mrec.call("mrec_emb_bwd_apply_rec", rdesc.ref(), B, ws.data_ptr(), wsb,
@@ -763,7 +763,7 @@ def owner_apply(bank: ShardedEmbeddingBank, plan, g_recv: torch.Tensor,
             lr = lr / W
     # deferred MLP weight-gradient reductions ride along this launch
     from pytorchrec_amd import dense as dense_ops
-    jobs = dense_ops.take_pending(4)
+    jobs = dense_ops.take_pending(dense_ops.CO_REDUCE_MAX)
     arr = (_mrec.GemmCall * len(jobs))(*[j.struct() for j in jobs]) if jobs else None
     _mrec.call("mrec_emb_bwd_apply_given", bank.desc().ref(), W * cap, ws.data_ptr(), wsb,
                None, _mrec.F32, 0, None, None, None, _mrec.F32, 0, None, g_recv.data_ptr(),
@@ -782,7 +782,7 @@ def owner_apply_wire(bank: ShardedEmbeddingBank, plan, wire_g: torch.Tensor, pre
     F, W, cap = bank.n_tables, parts or bank.world, bank.cap
     mode, lr = _owner_mode(bank, lr, grad)
     from pytorchrec_amd import dense as dense_ops
-    jobs = dense_ops.take_pending(4)
+    jobs = dense_ops.take_pending(dense_ops.CO_REDUCE_MAX)
     arr = (_mrec.GemmCall * len(jobs))(*[j.struct() for j in jobs]) if jobs else None
     _mrec.call("mrec_emb_bwd_apply_wire", bank.desc().ref(), W * cap, ws.data_ptr(), wsb,
                wire_g.data_ptr(), bank.wire_bytes(), _mrec.dtype_code(bank.weight.dtype),
@@ -837,7 +837,7 @@ def owner_apply_large(bank: ShardedEmbeddingBank, recv_ids: torch.Tensor, part: 
         g.wire_dtype, g.pref, g.cap_rows = (_mrec.dtype_code(bank.weight.dtype), pref.data_ptr(),
                                             bank.cap_rows)
     from pytorchrec_amd import dense as dense_ops
-    jobs = dense_ops.take_pending(4)
+    jobs = dense_ops.take_pending(dense_ops.CO_REDUCE_MAX)
     arr = (_mrec.GemmCall * len(jobs))(*[j.struct() for j in jobs]) if jobs else None
     fl = bank.flags()
     _mrec.call("mrec_emb_bwd_large_fused_given", bank.desc().ref(), idd.ref(), n, ws.data_ptr(),

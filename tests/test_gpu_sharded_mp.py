@@ -187,10 +187,13 @@ def test_two_process_sharded_step_on_gpu_matches_single_process(gpu, case):
                 assert np.all(diff <= 2.0 ** -7 * np.abs(rows) + 1e-6), f"rank {r} table {f}"
                 assert np.mean(diff > 0) < 0.01, f"rank {r} table {f}: {np.mean(diff > 0)}"
             else:  # lazy Adam, bf16: each rank's row-gradient sum crosses the wire rounded
-                # to bf16 once, and Adam's normalised step turns that into up to ~one bf16
-                # ulp of the row per step: 3 steps -> within 2^-6 relative (+ 1e-5), and
-                # most rows identical
+                # to bf16 once (and is summed per rank first).  Adam's step is normalised:
+                # where a gradient element is tiny against that rounding its sign can flip,
+                # moving the element by up to 2 lr per step -- so: every element within
+                # 2 lr x steps (+ 2^-6 relative), and at most 2 % beyond one bf16 ulp
                 diff = np.abs(got_rows - rows)
-                assert np.all(diff <= 2.0 ** -6 * np.abs(rows) + 1e-5), f"rank {r} table {f}"
-                assert np.mean(diff > 0) < 0.05, f"rank {r} table {f}: {np.mean(diff > 0)}"
+                lim = 2 * 1e-3 * sp["steps"] + 2.0 ** -6 * np.abs(rows)
+                far = float(np.mean(diff > 2.0 ** -7 * np.abs(rows) + 1e-6)) if diff.size else 0.0
+                assert np.all(diff <= lim), (r, f, float((diff / lim).max()), far)
+                assert far < 0.02, (r, f, far, float(np.mean(diff > 0)))
             o_local += rows.shape[0]

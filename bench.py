@@ -304,7 +304,9 @@ def time_launches(fn, reps=100):
     with torch.cuda.stream(s):
         fn()
         g = torch.cuda.CUDAGraph()
-        with torch.cuda.graph(g, stream=s):
+        # thread_local: the RCCL watchdog thread queries its events during the capture
+        # (a sharded model's process group); "global" mode made that query fail and abort
+        with torch.cuda.graph(g, stream=s, capture_error_mode="thread_local"):
             for _ in range(reps):
                 fn()
         g.replay()

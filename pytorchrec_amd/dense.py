@@ -1229,8 +1229,10 @@ def _tdw_splits(B: int, widths=None) -> int:
     if os.environ.get("MREC_TOWER_DW", "1") == "0" or B < 256:
         return 0
     env = os.environ.get("MREC_TDW_SPLITS")  # A/B knob
+    # at least 4 (C3's 245 tiles: 2 slices 0.1243 ms/step, 4: 0.1194; 3 and 5 slower,
+    # tools/gpu_ab_splits.sh)
     want = int(env) if env else (4 if widths is None else
-                                 max(1, min(64, 640 // _tdw_tiles(widths), max(4, B // 1024))))
+                                 max(4, min(64, 640 // _tdw_tiles(widths), max(4, B // 1024))))
     for s in range(want, 1, -1):
         if B // s >= 256 and _eff_split(B, s) == s:
             return s

@@ -440,7 +440,7 @@ EMB_PAIR = ("mrec_interact_fwd_ex", "mrec_emb_bwd_apply_ex")
 # MREC_BENCH_KC_CAT=1 with a library built with -DMREC_KC_CAT: the apply's block kinds
 # (co-reduce, segment, hot-segment, single-lookup blocks) clocked apart
 CAT_SPANS = {} if os.environ.get("MREC_BENCH_KC_CAT") == "1" else None
-TOWER_PAIR = ("mrec_tower_fwd_bwd", "mrec_tower_dw")
+TOWER_PAIR = ("mrec_tower_fwd_bwd", "mrec_tower_dw_ex")
 
 
 def embedding_roofline(model, step, datas, args, in_step=True):

@@ -11,7 +11,7 @@ import sys
 KERNELS = {"interact_plan_kernel": "mrec_interact_fwd_ex",
            "apply_hash_kernel": "mrec_emb_bwd_apply_ex",
            "tower_kernel": "mrec_tower_fwd_bwd",
-           "tower_dw_kernel": "mrec_tower_dw"}
+           "tower_dw_kernel": "mrec_tower_dw_ex"}
 
 
 def main(bench_json, stats_csv):

@@ -201,7 +201,11 @@ __device__ __forceinline__ void tower_layer_acc(f32x4 (&acc)[TW_TPW], const uint
   for (int i = 0; i < TW_TPW; ++i) acc[i] = f32x4{0.f, 0.f, 0.f, 0.f};
 
   const char *brow = in + r16 * s_in + g * 16;
-  const int rot = rotate ? static_cast<int>(blockIdx.x % static_cast<unsigned>(ksteps)) : 0;
+  // rotate 1: blockIdx % ksteps; 2: (blockIdx / 8) % ksteps -- workgroups are dealt to the
+  // 8 XCDs round-robin, so this spreads the 32 workgroups of one XCD (one L2) over all
+  // k steps where mode 1 gives only ksteps / gcd(8, ksteps) distinct starts
+  const unsigned bq = rotate == 2 ? blockIdx.x >> 3 : blockIdx.x;
+  const int rot = rotate ? static_cast<int>(bq % static_cast<unsigned>(ksteps)) : 0;
   switch (nreal) {  // uniform per wave
     case 4: tower_mfma<4, TW_PF>(acc, rsrc, voff, img_bytes, brow, ksteps, rot); break;
     case 3: tower_mfma<3, TW_PF>(acc, rsrc, voff, img_bytes, brow, ksteps, rot); break;
@@ -984,9 +988,9 @@ mrec_status mrec_tower_fwd_bwd(const mrec_tower_args *p, mrec_stream stream) {
   a.ticket = s.ticket;
   a.loss = s.loss;
   a.invB = 1.f / static_cast<float>(s.batch);
-  static const int rot_env = [] {
+  static const int rot_env = [] {  // MREC_TOWER_ROT: 0 off, 1 blockIdx, 2 per-XCD index
     const char *e = getenv("MREC_TOWER_ROT");
-    return (e && e[0] == '0') ? 0 : 1;
+    return e ? atoi(e) : 1;
   }();
   a.rotate = rot_env;
   a.stamps = g_tower_stamps;

@@ -53,6 +53,7 @@ from __future__ import annotations
 import contextlib
 import ctypes
 import math
+import os
 from typing import List, Optional, Sequence
 
 import torch
@@ -260,7 +261,8 @@ class ShardedEmbeddingBank(EmbeddingBank):
         # smaller chunks (W = 16: 7,168 samples; W >= 127 is not supported)
         if W + 1 > 128:
             raise ValueError(f"row sharding supports world sizes up to 127, not {W}")
-        self.chunk_batch = min(int(type(self).chunk_batch), 1024 * (128 // (W + 1)))
+        cb = int(os.environ.get("MREC_SHARD_CHUNK", type(self).chunk_batch))  # (A/B knob)
+        self.chunk_batch = min(cb, 1024 * (128 // (W + 1)))
         # slots per (owner, table[, chunk]): distinct ids of one chunk on the compact
         # exchange, lookups of the whole batch on the slot exchange (which does not
         # chunk); the `compact` setter switches a defaulted cap

@@ -144,16 +144,34 @@ __device__ __forceinline__ float sum_quad(float v) {
 }
 // sum over all 64 lanes
 __device__ __forceinline__ float sum_wave(float v) { return sum_mod4_lanes(sum_quad(v)); }
+// max over all 64 lanes (every lane gets it; order-free, so equal to any other order)
+__device__ __forceinline__ float max_wave(float v) {
+  v = fmaxf(v, dpp_f32<0xb1>(v));   // quad_perm [1, 0, 3, 2]
+  v = fmaxf(v, dpp_f32<0x4e>(v));   // quad_perm [2, 3, 0, 1]
+  v = fmaxf(v, dpp_f32<0x124>(v));  // row_ror:4
+  v = fmaxf(v, dpp_f32<0x128>(v));  // row_ror:8
+  const auto r16 = __builtin_amdgcn_permlane16_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+  v = fmaxf(__uint_as_float(r16[0]), __uint_as_float(r16[1]));
+  const auto r32 = __builtin_amdgcn_permlane32_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+  return fmaxf(__uint_as_float(r32[0]), __uint_as_float(r32[1]));
+}
 
 __device__ __forceinline__ float bf16_to_f32(uint16_t h) {
   return __uint_as_float(static_cast<uint32_t>(h) << 16);
 }
 
-// round-to-nearest-even, NaN kept NaN (quiet bit set)
+// round-to-nearest-even with v_cvt_pk_bf16_f32 (the kernels' f32 mode: RNE,
+// denormals kept; NaN stays NaN).  The integer form -- (u + 0x7fff + lsb) >> 16 with
+// a NaN test -- gives the same bits on every non-NaN input and cost ~5 VALU ops per
+// value: the DIN attention backward's ~70 conversions per lane and sample were
+// ~14 us of C4's step (r05).
+__device__ __forceinline__ uint32_t pack_bf16x2(float lo, float hi) {
+  typedef float f32x2_t __attribute__((ext_vector_type(2)));
+  typedef __bf16 bf16x2_t __attribute__((ext_vector_type(2)));
+  return __builtin_bit_cast(uint32_t, __builtin_convertvector((f32x2_t{lo, hi}), bf16x2_t));
+}
 __device__ __forceinline__ uint16_t f32_to_bf16_rne(float f) {
-  uint32_t u = __float_as_uint(f);
-  if ((u & 0x7fffffffu) > 0x7f800000u) return static_cast<uint16_t>((u >> 16) | 0x40u);
-  return static_cast<uint16_t>((u + 0x7fffu + ((u >> 16) & 1u)) >> 16);
+  return static_cast<uint16_t>(pack_bf16x2(f, 0.f));
 }
 
 // stochastic rounding with 16 random bits (unbiased: E[result] = f)
@@ -208,10 +226,6 @@ struct Vec<float> {
   }
 };
 
-__device__ __forceinline__ uint32_t pack_bf16x2(float lo, float hi) {
-  return static_cast<uint32_t>(f32_to_bf16_rne(lo)) |
-         (static_cast<uint32_t>(f32_to_bf16_rne(hi)) << 16);
-}
 
 // Per-step scalars of Adam / AdamW at step s (b1p = beta1^s, b2p = beta2^s, in
 // double like the host-side scalars of the dense optimizers).

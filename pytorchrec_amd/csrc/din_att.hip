@@ -139,20 +139,22 @@ __device__ void da_stage_weights(const DinAttArgs &p, uint16_t *sm, float *sb1, 
   constexpr int Q1 = S::H1N * S::E4 / 4, N1 = (Q1 + DA_THREADS - 1) / DA_THREADS;
   constexpr int Q2 = S::H2N * S::H1N / 4, N2 = (Q2 + DA_THREADS - 1) / DA_THREADS;
   float4 v1[N1], v2[N2];
+  // unconditional loads (padding reads element 0, zeroed at the conversion): a
+  // conditional load's value is copied out of its branch and that copy waits for it
+  bool ok1[N1], ok2[N2];
 #pragma unroll
   for (int it = 0; it < N1; ++it) {
     const int i = (tid + it * DA_THREADS) * 4, n = i / S::E4, k = i - n * S::E4;
-    v1[it] = (i < S::H1N * S::E4 && n < p.H1)
-                 ? *reinterpret_cast<const float4 *>(p.w1 + n * p.ldw1 + k)
-                 : make_float4(0.f, 0.f, 0.f, 0.f);
+    ok1[it] = i < S::H1N * S::E4 && n < p.H1;
+    v1[it] = *reinterpret_cast<const float4 *>(p.w1 + (ok1[it] ? n * p.ldw1 + k : 0));
   }
 #pragma unroll
   for (int it = 0; it < N2; ++it) {
     const int i = (tid + it * DA_THREADS) * 4, n = i / S::H1N, k = i - n * S::H1N;
-    v2[it] = (i < S::H2N * S::H1N && n < p.H2 && k < p.H1)
-                 ? *reinterpret_cast<const float4 *>(p.w2 + n * p.ldw2 + k)
-                 : make_float4(0.f, 0.f, 0.f, 0.f);
+    ok2[it] = i < S::H2N * S::H1N && n < p.H2 && k < p.H1;
+    v2[it] = *reinterpret_cast<const float4 *>(p.w2 + (ok2[it] ? n * p.ldw2 + k : 0));
   }
+  DA_STAMP(61);
   for (int i = tid; i < S::H1N; i += DA_THREADS) sb1[i] = i < p.H1 ? p.b1[i] : 0.f;
   for (int i = tid; i < S::H2N; i += DA_THREADS) {
     sb2[i] = i < p.H2 ? p.b2[i] : 0.f;
@@ -162,6 +164,7 @@ __device__ void da_stage_weights(const DinAttArgs &p, uint16_t *sm, float *sb1, 
   for (int it = 0; it < N1; ++it) {
     const int i = (tid + it * DA_THREADS) * 4, n = i / S::E4, k = i - n * S::E4;
     if (i >= S::H1N * S::E4) continue;
+    if (!ok1[it]) v1[it] = make_float4(0.f, 0.f, 0.f, 0.f);
     const uint16_t h[4] = {f32_to_bf16_rne(v1[it].x), f32_to_bf16_rne(v1[it].y),
                            f32_to_bf16_rne(v1[it].z), f32_to_bf16_rne(v1[it].w)};
     *reinterpret_cast<uint2 *>(sm + S::oW1 + n * S::LDX + k) =
@@ -172,10 +175,12 @@ __device__ void da_stage_weights(const DinAttArgs &p, uint16_t *sm, float *sb1, 
       for (int c = 0; c < 4; ++c) sm[S::oW1T + (k + c) * S::LDH + n] = h[c];
     }
   }
+  DA_STAMP(62);
 #pragma unroll
   for (int it = 0; it < N2; ++it) {
     const int i = (tid + it * DA_THREADS) * 4, n = i / S::H1N, k = i - n * S::H1N;
     if (i >= S::H2N * S::H1N) continue;
+    if (!ok2[it]) v2[it] = make_float4(0.f, 0.f, 0.f, 0.f);
     const uint16_t h[4] = {f32_to_bf16_rne(v2[it].x), f32_to_bf16_rne(v2[it].y),
                            f32_to_bf16_rne(v2[it].z), f32_to_bf16_rne(v2[it].w)};
     *reinterpret_cast<uint2 *>(sm + S::oW2 + n * S::LDH + k) =
@@ -422,6 +427,261 @@ __global__ __launch_bounds__(DA_THREADS) void din_att_fwd_kernel(DinAttArgs p) {
     for (int c = 2 * E + tid; c < p.ldt; c += DA_THREADS) p.top[b * p.ldt + c] = 0;
     cur = nxt;
     __syncthreads();  // the next sample's X build overwrites X, read by the pooled sum
+  }
+}
+
+// ---------------------------------------------------------------------------
+// forward, one wave per sample: no workgroup barrier after the weights are staged.
+//
+// The attention MLP is row-independent, so a wave can take a sample's 64 history
+// rows as 4 row tiles of its own: layer 1's A operand is built in registers straight
+// from the lane's 16-B q / k chunks (lane l holds X[row l % 16][k = 8 (l / 16) .. + 8]
+// of each 32-wide k step, and with E >= 16 that is one block of [q | k | q - k | q k]
+// at column offset 8 (l / 16) mod E), layer 1's B fragments live in VGPRs for the
+// launch, and only H1 (one 16-row tile), the scores, a and the pooling parts pass
+// through the wave's own LDS scratch.  Every sum runs in the order of
+// din_att_fwd_kernel (k steps ascending, score parts of column group 0 then 1, the
+// pooled sum's DA_THREADS / E parts in part order), so the two kernels agree
+// bitwise (tests/test_gpu_din_att.py).  The one-workgroup-per-sample kernel spent
+// ~4.6 us per sample on barriers and LDS round trips (37 us at C4); the MFMA work of
+// a sample is 116 16x16x32 steps (~1.9k cycles).
+// ---------------------------------------------------------------------------
+template <int E, int H1T, int H1K, int H2T, int H2K>
+struct DaShapeF : DaShape<E, H1T, H1K, H2T, H2K> {
+  using B = DaShape<E, H1T, H1K, H2T, H2K>;
+  static constexpr int WAVES = DA_THREADS / 64;
+  static constexpr int G = DA_THREADS / E;  // pooling parts (din_att_fwd_kernel's order)
+  // bf16 elements: the weights, shared by the workgroup's waves while they load
+  // their fragments
+  static constexpr int oW1 = 0;
+  static constexpr int oW2 = B::H1N * B::LDX;
+  static constexpr int w_end = oW2 + B::H2N * B::LDH;
+  static constexpr size_t fp_off = static_cast<size_t>(w_end) * 2;  // b1, b2, w3 fp32
+  static constexpr size_t scratch_off = (fp_off + (B::H1N + 2 * B::H2N) * 4 + 15) / 16 * 16;
+  // per wave: H [16][LDH] bf16; score parts [2][64], a [64], pooling parts [G][E] fp32
+  static constexpr int s_end = 16 * B::LDH;
+  static constexpr size_t wave_bytes =
+      static_cast<size_t>(s_end) * 2 + (3 * DA_ROWS + G * E) * 4;
+  static constexpr size_t bytes = scratch_off + WAVES * wave_bytes;
+  static_assert(E == 16 || E == 32, "a lane's k-step chunk is one block of X at offset 8 g mod E");
+  static_assert((s_end * 2) % 16 == 0 && wave_bytes % 16 == 0, "16-B aligned scratch");
+  static_assert(bytes <= 160 * 1024, "LDS budget");
+};
+
+// Loaded unconditionally from clamped addresses (sample min(b, batch - 1), row
+// min(j, L - 1), position min(lane, L - 1)) and masked where used: a conditional
+// load's value is copied out of its branch, and that copy waits for the load -- the
+// prologue's first-sample loads then stalled the weight staging behind them.
+struct DaRawW {
+  uint4 q;     // q chunk (bf16 x 8) at column offset 8 (lane / 16) mod E
+  uint4 k[4];  // k chunk of history row min(16 rt + lane % 16, L - 1)
+  int hv;      // his[b, min(lane, L - 1)]
+};
+
+template <int E>
+__device__ __forceinline__ DaRawW da_load_w(const DinAttArgs &p, int64_t b, int lane, int off) {
+  DaRawW r;
+  b = b < p.batch ? b : p.batch - 1;
+  r.q = *reinterpret_cast<const uint4 *>(p.rows + b * p.ld_rows + off);
+#pragma unroll
+  for (int rt = 0; rt < 4; ++rt) {
+    const int j = min(16 * rt + (lane & 15), p.L - 1);
+    r.k[rt] = *reinterpret_cast<const uint4 *>(p.rows + (p.batch + b * p.L + j) * p.ld_rows + off);
+  }
+  r.hv = p.his[b * p.ld_his + min(lane, p.L - 1)];
+  return r;
+}
+
+// compiler + wave-order fence for a wave-local LDS round trip (the LDS executes one
+// wave's instructions in order; this keeps the compiler from moving them)
+#define DA_WAVE_SYNC()                                  \
+  do {                                                  \
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); \
+    __builtin_amdgcn_wave_barrier();                    \
+  } while (0)
+
+template <int E, int H1T, int H1K, int H2T, int H2K>
+__global__ __launch_bounds__(DA_THREADS, 1) void din_att_fwd_wave_kernel(DinAttArgs p) {
+  using S = DaShapeF<E, H1T, H1K, H2T, H2K>;
+  constexpr int KT1 = S::KT1, G = S::G, LDH = S::LDH;
+  constexpr int PPL = G / 16;  // pooling parts per lane: rows j = 16 rt + lane % 16 -> j mod G
+  extern __shared__ __attribute__((aligned(16))) char da_lds[];
+  uint16_t *sm = reinterpret_cast<uint16_t *>(da_lds);
+  float *sb1 = reinterpret_cast<float *>(da_lds + S::fp_off);
+  float *sb2 = sb1 + S::H1N;
+  float *sw3 = sb2 + S::H2N;
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, g = lane >> 4, r16 = lane & 15;
+  char *ws = da_lds + S::scratch_off + w * S::wave_bytes;
+  uint16_t *sHt = reinterpret_cast<uint16_t *>(ws);
+  float *sSC = reinterpret_cast<float *>(ws + S::s_end * 2);
+  float *sA = sSC + 2 * DA_ROWS;
+  float *sP = sA + DA_ROWS;
+  DA_STAMP(0);
+  const int off = (8 * g) % E;
+  const int64_t nw = static_cast<int64_t>(gridDim.x) * S::WAVES;
+  int64_t b = blockIdx.x + static_cast<int64_t>(gridDim.x) * w;
+  DaRawW cur = da_load_w<E>(p, b, lane, off);  // loads while the weights are staged
+  // zero what is read but never written: W2's and H's padded k columns
+  da_zero_lds(da_lds, S::scratch_off);
+  for (int o = lane * 16; o < S::s_end * 2; o += 64 * 16)
+    *reinterpret_cast<uint4 *>(ws + o) = make_uint4(0, 0, 0, 0);
+  __syncthreads();
+  DA_STAMP(60);
+  da_stage_weights<S, false>(p, sm, sb1, sb2, sw3);
+  __syncthreads();
+  DA_STAMP(1);
+  // layer 1's B fragments in VGPRs (80 at C4); layer 2's are read from the staged
+  // copy per use (in VGPRs too they spill at 256)
+  da_bf16x8 w1f[H1T][KT1];
+  float b1v[H1T][4], b2v[H2T], w3v[H2T];
+#pragma unroll
+  for (int n = 0; n < H1T; ++n) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) b1v[n][i] = sb1[16 * n + 4 * g + i];
+#pragma unroll
+    for (int s = 0; s < KT1; ++s) w1f[n][s] = da_frag(sm + S::oW1, S::LDX, 16 * n, 32 * s, lane);
+  }
+#pragma unroll
+  for (int n = 0; n < H2T; ++n) {
+    b2v[n] = sb2[16 * n + r16];
+    w3v[n] = sw3[16 * n + r16];
+  }
+  const float b3 = p.b3[0];
+  int sidx = 0;
+  for (; b < p.batch; b += nw) {
+    const DaRawW nxt = da_load_w<E>(p, b + nw, lane, off);
+    DA_WAVE_SYNC();  // the previous sample's pooling reads are done
+    DA_STAMP(2 + 8 * sidx);
+    const bool valid = lane < p.L && (lane == 0 || cur.hv > 0);
+    const uint64_t vm = __ballot(valid);
+    const int nact = vm ? 64 - __clzll(vm) : 0;
+    float qv[8];
+    Vec<uint16_t>::to_f32(cur.q, qv);
+#pragma unroll
+    for (int rt = 0; rt < 4; ++rt) {
+      if (16 * rt >= nact) continue;  // rows past the last valid position: masked
+      const bool real = 16 * rt + r16 < p.L;
+      const uint4 kk = real ? cur.k[rt] : make_uint4(0, 0, 0, 0);
+      uint4 qq = cur.q, dq, mq;
+      {
+        float kv[8], d[8], m[8];
+        Vec<uint16_t>::to_f32(kk, kv);
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+          d[i] = qv[i] - kv[i];
+          m[i] = qv[i] * kv[i];
+        }
+        dq = make_uint4(pack_bf16x2(d[0], d[1]), pack_bf16x2(d[2], d[3]),
+                        pack_bf16x2(d[4], d[5]), pack_bf16x2(d[6], d[7]));
+        mq = make_uint4(pack_bf16x2(m[0], m[1]), pack_bf16x2(m[2], m[3]),
+                        pack_bf16x2(m[4], m[5]), pack_bf16x2(m[6], m[7]));
+      }
+      if (!real) qq = dq = mq = make_uint4(0, 0, 0, 0);
+      da_f32x4 acc[H1T];
+#pragma unroll
+      for (int n = 0; n < H1T; ++n) acc[n] = da_f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int s = 0; s < KT1; ++s) {
+        const int blk = (32 * s + 8 * g) / E;
+        const uint4 xv = blk == 0 ? qq : blk == 1 ? kk : blk == 2 ? dq : mq;
+        const da_bf16x8 a = __builtin_bit_cast(da_bf16x8, xv);
+#pragma unroll
+        for (int n = 0; n < H1T; ++n) acc[n] = da_mfma(w1f[n][s], a, acc[n]);
+      }
+      // (operands swapped: acc[n] is H1^T, lane l holds row l % 16's outputs
+      // 16 n + 4 (l / 16) .. + 3 -- the same products and k order, one 8-B store each)
+      DA_WAVE_SYNC();  // the previous tile's H reads are done
+#pragma unroll
+      for (int n = 0; n < H1T; ++n) {
+        float h[4];
+#pragma unroll
+        for (int i = 0; i < 4; ++i) h[i] = fmaxf(acc[n][i] + b1v[n][i], 0.f);
+        *reinterpret_cast<uint2 *>(sHt + r16 * LDH + 16 * n + 4 * g) =
+            make_uint2(pack_bf16x2(h[0], h[1]), pack_bf16x2(h[2], h[3]));
+      }
+      DA_WAVE_SYNC();
+      da_f32x4 acc2[H2T];
+#pragma unroll
+      for (int n = 0; n < H2T; ++n) acc2[n] = da_f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int s = 0; s < H1K; ++s) {
+        const da_bf16x8 a = da_frag(sHt, LDH, 0, 32 * s, lane);
+#pragma unroll
+        for (int n = 0; n < H2T; ++n)
+          acc2[n] = da_mfma(a, da_frag(sm + S::oW2, LDH, 16 * n, 32 * s, lane), acc2[n]);
+      }
+      float part[DA_CG][4] = {};
+#pragma unroll
+      for (int n = 0; n < H2T; ++n)
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+          part[n % DA_CG][i] = fmaf(fmaxf(acc2[n][i] + b2v[n], 0.f), w3v[n], part[n % DA_CG][i]);
+#pragma unroll
+      for (int cg = 0; cg < DA_CG; ++cg)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const float v = da_sum16(part[cg][i]);
+          if (r16 == 0) sSC[cg * DA_ROWS + 16 * rt + 4 * g + i] = v;
+        }
+    }
+    DA_WAVE_SYNC();
+    DA_STAMP(3 + 8 * sidx);
+    // masked softmax over history positions (lane j)
+    {
+      float sc = b3;
+#pragma unroll
+      for (int cg = 0; cg < DA_CG; ++cg) sc += sSC[cg * DA_ROWS + lane];
+      const float sj = valid ? sc : -INFINITY;
+      const float m = max_wave(sj);
+      const float e = valid ? __expf(sj - m) : 0.f;
+      const float a = e / sum_wave(e);
+      sA[lane] = a;
+      if (lane < p.L) p.a[b * p.L + lane] = a;
+    }
+    DA_WAVE_SYNC();
+    DA_STAMP(4 + 8 * sidx);
+    // pooling parts from the lane's own k chunks: part gp = sum over rows j = gp mod G
+    // in ascending j (= ascending row tile), columns off .. off + 7
+    {
+      float pu[PPL][8] = {};
+#pragma unroll
+      for (int rt = 0; rt < 4; ++rt) {
+        const int j = 16 * rt + r16;
+        if (j >= p.L) continue;
+        const float aj = sA[j];
+        float kv[8];
+        Vec<uint16_t>::to_f32(cur.k[rt], kv);
+#pragma unroll
+        for (int i = 0; i < 8; ++i) pu[rt % PPL][i] = fmaf(aj, kv[i], pu[rt % PPL][i]);
+      }
+      if (8 * g < E) {  // (E = 16: lanes g and g + 2 hold the same chunk)
+#pragma unroll
+        for (int t = 0; t < PPL; ++t) {
+          float4 *dst = reinterpret_cast<float4 *>(sP + (16 * t + r16) * E + off);
+          dst[0] = make_float4(pu[t][0], pu[t][1], pu[t][2], pu[t][3]);
+          dst[1] = make_float4(pu[t][4], pu[t][5], pu[t][6], pu[t][7]);
+        }
+      }
+    }
+    DA_WAVE_SYNC();
+    DA_STAMP(5 + 8 * sidx);
+    uint16_t *tp = p.top + b * p.ldt;
+    if (lane < E) {
+      float u = 0.f;
+#pragma unroll 8
+      for (int gp = 0; gp < G; ++gp) u += sP[gp * E + lane];
+      tp[E + lane] = f32_to_bf16_rne(u);
+    }
+    if (r16 == 0 && 8 * g < E) {  // q (row 0's q block: zero iff L == 0)
+      const uint32_t qw[4] = {cur.q.x, cur.q.y, cur.q.z, cur.q.w};
+#pragma unroll
+      for (int i = 0; i < 8; ++i)
+        tp[8 * g + i] = p.L > 0 ? static_cast<uint16_t>(qw[i >> 1] >> (16 * (i & 1))) : 0;
+    }
+    for (int c = 2 * E + lane; c < p.ldt; c += 64) tp[c] = 0;
+    DA_STAMP(6 + 8 * sidx);
+    ++sidx;
+    cur = nxt;
   }
 }
 
@@ -1272,7 +1532,18 @@ void da_set_attrs() {
   (void)hipFuncSetAttribute(reinterpret_cast<const void *>(din_att_bwd2_kernel<E, H1T, H1K, H2T, H2K>),
                             hipFuncAttributeMaxDynamicSharedMemorySize,
                             static_cast<int>(DaShape2<E, H1T, H1K, H2T, H2K>::bytes));
+  (void)hipFuncSetAttribute(
+      reinterpret_cast<const void *>(din_att_fwd_wave_kernel<E, H1T, H1K, H2T, H2K>),
+      hipFuncAttributeMaxDynamicSharedMemorySize,
+      static_cast<int>(DaShapeF<E, H1T, H1K, H2T, H2K>::bytes));
   (void)hipGetLastError();
+}
+
+// MREC_DIN_FWD_WG=1: the one-workgroup-per-sample forward (A/B and parity yardstick;
+// read per call so a test can switch it)
+bool da_fwd_wg() {
+  const char *e = std::getenv("MREC_DIN_FWD_WG");
+  return e && e[0] == '1';
 }
 
 // MREC_DIN_BWD_ONE=1: the one-sample-per-workgroup backward (A/B and parity yardstick)
@@ -1295,6 +1566,12 @@ bool da_supported(int E, int H1, int H2) {
 }  // namespace
 
 static unsigned long long *g_da_stamps = nullptr;
+
+// MREC_DA_STAMP_FWD=1: the debug stamps go to the wave forward, not the backward
+static bool da_stamp_fwd() {
+  const char *e = std::getenv("MREC_DA_STAMP_FWD");
+  return e && e[0] == '1';
+}
 
 extern "C" {
 
@@ -1353,15 +1630,24 @@ mrec_status mrec_din_att_fwd(const void *rows, int64_t ld_rows, const int32_t *h
   p.a = a;
   p.top = static_cast<uint16_t *>(top);
   p.ldt = ldt;
-  const int64_t grid = std::min<int64_t>(batch, 2 * static_cast<int64_t>(da_cus()));
+  p.stamps = da_stamp_fwd() ? g_da_stamps : nullptr;
+  const bool wg = da_fwd_wg();
+  // one workgroup (8 sample waves) per CU, or one sample per workgroup
+  const int64_t grid = wg ? std::min<int64_t>(batch, 2 * static_cast<int64_t>(da_cus()))
+                          : std::min<int64_t>((batch + 7) / 8, da_cus());
   hipStream_t s = static_cast<hipStream_t>(stream);
 #define X(e, h1t, h1k, h2t, h2k)                                                              \
   if (da_match<e, h1t, h1k, h2t, h2k>(E, H1, H2)) {                                         \
     static const int once = (da_set_attrs<e, h1t, h1k, h2t, h2k>(), 1);                     \
     (void)once;                                                                             \
-    din_att_fwd_kernel<e, h1t, h1k, h2t, h2k>                                               \
-        <<<dim3(static_cast<unsigned>(grid)), DA_THREADS,                                   \
-           DaShape<e, h1t, h1k, h2t, h2k>::fwd_bytes, s>>>(p);                              \
+    if (wg)                                                                                 \
+      din_att_fwd_kernel<e, h1t, h1k, h2t, h2k>                                             \
+          <<<dim3(static_cast<unsigned>(grid)), DA_THREADS,                                 \
+             DaShape<e, h1t, h1k, h2t, h2k>::fwd_bytes, s>>>(p);                            \
+    else                                                                                    \
+      din_att_fwd_wave_kernel<e, h1t, h1k, h2t, h2k>                                        \
+          <<<dim3(static_cast<unsigned>(grid)), DA_THREADS,                                 \
+             DaShapeF<e, h1t, h1k, h2t, h2k>::bytes, s>>>(p);                               \
     return launch_status("mrec_din_att_fwd");                                               \
   }
   MREC_DA_SHAPES(X)
@@ -1398,7 +1684,7 @@ mrec_status mrec_din_att_bwd(const void *rows, int64_t ld_rows, int64_t batch, i
   p.ld_drows = ld_drows;
   p.part = part;
   p.P = mrec_din_att_param_count(E, H1, H2);
-  p.stamps = g_da_stamps;
+  p.stamps = da_stamp_fwd() ? nullptr : g_da_stamps;
   hipStream_t s = static_cast<hipStream_t>(stream);
 #define X(e, h1t, h1k, h2t, h2k)                                                              \
   if (da_match<e, h1t, h1k, h2t, h2k>(E, H1, H2)) {                                         \

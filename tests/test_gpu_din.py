@@ -257,6 +257,34 @@ def test_din_fused_unit_matches_fp64_reference(gpu, monkeypatch, B, L, E, H1, H2
         assert fmean <= max(3e-3, 1.5 * lmean), (name, fmean, lmean)
 
 
+@pytest.mark.parametrize("B,L,E,H1,H2,full", [(4096, 50, 32, 80, 40, False),
+                                              (300, 50, 32, 80, 40, False),
+                                              (48, 64, 32, 80, 40, True),
+                                              (37, 1, 32, 80, 40, True),
+                                              (2100, 37, 16, 24, 12, False)])
+def test_din_wave_forward_equals_workgroup_forward_bitwise(gpu, monkeypatch, B, L, E, H1, H2, full):
+    """The one-wave-per-sample forward (din_att_fwd_wave_kernel, the default) and the
+    one-workgroup-per-sample forward (MREC_DIN_FWD_WG=1) sum in the same order: top
+    and the saved softmax weights a are equal bit for bit, with interior masked
+    history positions as well as masked tails (rows past the last valid position
+    skip the MLP in both)."""
+    from pytorchrec_amd import dense as D
+    att, out, q, k, his = _block_shape(gpu, B, L, E, H1, H2, seed=5 + B, full_len=full)
+    g = torch.Generator().manual_seed(B)
+    hole = torch.rand(B, L, generator=g) < 0.2
+    his = his.masked_fill(hole.to(gpu), 0)
+    res = {}
+    for wg in ("1", "0"):
+        monkeypatch.setenv("MREC_DIN_FWD_WG", wg)
+        rows = torch.cat([q, k]).detach().clone().requires_grad_()
+        top = D.din_attention_top_rows(rows, B, his, att, out)
+        assert "DinAtt" in type(top.grad_fn).__name__
+        torch.cuda.synchronize()
+        res[wg] = (top.detach().clone(), top.grad_fn.saved_tensors[1].clone())
+    assert torch.equal(res["1"][0].view(torch.int16), res["0"][0].view(torch.int16))
+    assert torch.equal(res["1"][1].view(torch.int32), res["0"][1].view(torch.int32))
+
+
 def test_din_fused_close_to_layered_path(gpu, monkeypatch):
     """Fused and layered GPU paths agree (same bf16 operand roundings; different
     summation orders and the fused path keeps H2 / dX in fp32)."""

@@ -1,5 +1,5 @@
 """Phase clocks of the fused DIN attention backward (workgroup 0, s_memtime) in a
-C4 train step: python tools/din_stamps.py.  Prints per-sample phase durations in
+C4 train step: python tools/din_stamps.py (MREC_DA_STAMP_FWD=1: the wave forward's).  Prints per-sample phase durations in
 clock cycles and the step's samples-per-workgroup count."""
 import ctypes
 import os
@@ -35,6 +35,21 @@ def main():
     fn(None)
     st = buf.cpu().tolist()
     print("stage weights:", st[1] - st[0])
+    if st[60]:
+        print("  zero", st[60] - st[0], " loads issued", st[61] - st[60], " W1 converted",
+              st[62] - st[61], " W2 + sync", st[1] - st[62])
+    if os.environ.get("MREC_DA_STAMP_FWD") == "1":  # the wave forward (wave 0's samples)
+        names = ["loads+K", "row tiles", "softmax", "pool parts", "top"]
+        prev = st[1]
+        for k in range(7):
+            base = 2 + 8 * k
+            if st[base + 4] == 0:
+                break
+            row = [st[base] - prev] + [st[base + j] - st[base + j - 1] for j in range(1, 5)]
+            prev = st[base + 4]
+            print(f"sample {k}: " + "  ".join(f"{n}={v}" for n, v in zip(names, row)),
+                  " total", sum(row))
+        return
     if os.environ.get("MREC_DIN_BWD_ONE") == "1":  # one sample per iteration, 6 stamps
         names = ["ph0 X/g", "ph1 L1", "ph2 L2/dZ2", "ph3 dH1/dW2", "ph4 dX/dW1", "dq+next"]
     else:  # two samples per iteration, 3 stamps

@@ -200,6 +200,52 @@ __device__ __forceinline__ int64_t load_id(const IdsArgs &ids, int f, int64_t b)
   return static_cast<int64_t>(static_cast<const int32_t *>(ids.ptr[f])[off]);
 }
 
+// ids of table f at samples i_k = base + k * step (k < N); `fill` for i_k >= limit.
+// Every load is issued before any is used: unconditional loads from clamped indices
+// (sample 0 past `limit`), masked afterwards.  A load inside `i < B ? load_id(..) : -1`
+// has its value copied out of the branch, and that copy waits for it: the compiler
+// serialised such loops into one memory round trip per id (r05: the hash plan's 8
+// rounds per thread were ~8 us of its 9).  The layout branches (is64, chunk) are
+// uniform and taken once, outside the loads.
+template <int N>
+__device__ __forceinline__ void load_ids_batch(const IdsArgs &ids, int f, int64_t base, int64_t step,
+                                               int64_t limit, int64_t fill, int64_t (&out)[N]) {
+  if (limit <= 0) {
+#pragma unroll
+    for (int k = 0; k < N; ++k) out[k] = fill;
+    return;
+  }
+  if (ids.chunk) {  // chunked sender views: the per-element path
+#pragma unroll
+    for (int k = 0; k < N; ++k) {
+      const int64_t i = base + k * step;
+      out[k] = i < limit ? load_id(ids, f, i) : fill;
+    }
+    return;
+  }
+  if (ids.is64) {
+    const int64_t *p = static_cast<const int64_t *>(ids.ptr[f]);
+    int64_t v[N];
+#pragma unroll
+    for (int k = 0; k < N; ++k) {
+      const int64_t i = base + k * step;
+      v[k] = p[(i < limit ? i : 0) * ids.stride];
+    }
+#pragma unroll
+    for (int k = 0; k < N; ++k) out[k] = base + k * step < limit ? v[k] : fill;
+  } else {
+    const int32_t *p = static_cast<const int32_t *>(ids.ptr[f]);
+    int32_t v[N];
+#pragma unroll
+    for (int k = 0; k < N; ++k) {
+      const int64_t i = base + k * step;
+      v[k] = p[(i < limit ? i : 0) * ids.stride];
+    }
+#pragma unroll
+    for (int k = 0; k < N; ++k) out[k] = base + k * step < limit ? static_cast<int64_t>(v[k]) : fill;
+  }
+}
+
 // 16 bytes of a row as floats: EPL = 8 (bf16) or 4 (f32)
 template <typename T>
 struct Vec;

@@ -218,6 +218,57 @@ __device__ __forceinline__ int32_t lookup_row(const BankArgs &bank, const IdsArg
   return -1;
 }
 
+// lookup_row for the N lookups i_k = i0 + k * step of a thread, every load issued
+// before any is used (common.h load_ids_batch): the per-lane kernel-argument reads
+// (ids.ptr[f], rows[f], row_offset[f]) first, then the ids, unconditionally from
+// clamped indices.  As N calls of lookup_row the compiler chained ~4 dependent round
+// trips per lookup (each loaded value copied out of its branch waits for it).
+// b_out[k] = the lookup's sample (0 past `total`).
+template <int N>
+__device__ __forceinline__ void lookup_rows_batch(const BankArgs &bank, const IdsArgs &ids,
+                                                  int64_t n, int64_t i0, int64_t step, int64_t total,
+                                                  int32_t (&row)[N], int64_t (&b_out)[N],
+                                                  int32_t *__restrict__ oob) {
+  // (total = batch * n_tables < 2^31, checked by lg_setup: 32-bit division)
+  const uint32_t un = static_cast<uint32_t>(n);
+  int fk[N];
+  const void *fp[N];
+  int64_t nrow[N], roff[N], id[N];
+#pragma unroll
+  for (int k = 0; k < N; ++k) {
+    const int64_t i = i0 + k * step;
+    const uint32_t ui = static_cast<uint32_t>(i < total ? i : 0);
+    fk[k] = static_cast<int>(ui / un);
+    b_out[k] = static_cast<int64_t>(ui - static_cast<uint32_t>(fk[k]) * un);
+  }
+  __builtin_amdgcn_sched_barrier(0);  // the index math first: no register reuse waits
+#pragma unroll
+  for (int k = 0; k < N; ++k) {
+    fp[k] = ids.ptr[fk[k]];
+    nrow[k] = bank.rows[fk[k]];
+    roff[k] = bank.row_offset[fk[k]];
+  }
+  if (ids.chunk) {  // (uniform) chunked views: the per-element path
+#pragma unroll
+    for (int k = 0; k < N; ++k) id[k] = load_id(ids, fk[k], b_out[k]);
+  } else if (ids.is64) {
+#pragma unroll
+    for (int k = 0; k < N; ++k) id[k] = static_cast<const int64_t *>(fp[k])[b_out[k] * ids.stride];
+  } else {
+#pragma unroll
+    for (int k = 0; k < N; ++k) id[k] = static_cast<const int32_t *>(fp[k])[b_out[k] * ids.stride];
+  }
+#pragma unroll
+  for (int k = 0; k < N; ++k) {
+    row[k] = -1;
+    if (i0 + k * step >= total) continue;
+    if (id[k] >= 0 && id[k] < nrow[k])
+      row[k] = static_cast<int32_t>(roff[k] + id[k]);
+    else if (oob && !(ids.pad_negative && id[k] < 0))
+      *oob = 1;
+  }
+}
+
 // Runs are further combined per workgroup in an LDS hash (a row's runs from
 // different samples, e.g. one PAD run per history): a workgroup covers
 // kLgIter * 256 consecutive lookups and pays ONE global atomic per distinct row
@@ -252,10 +303,9 @@ __global__ __launch_bounds__(256) void lg_count_kernel(BankArgs bank, IdsArgs id
   const int64_t base = static_cast<int64_t>(blockIdx.x) * 256 * kLgIter;
   // every id load of this thread first (one memory round trip, not kLgIter)
   int32_t rr[kLgIter];
-#pragma unroll
-  for (int it = 0; it < kLgIter; ++it) {
-    int64_t b;
-    rr[it] = lookup_row(bank, ids, n, base + it * 256 + threadIdx.x, total, &b, oob);
+  {
+    int64_t bq[kLgIter];
+    lookup_rows_batch<kLgIter>(bank, ids, n, base + threadIdx.x, 256, total, rr, bq, oob);
   }
 #pragma unroll
   for (int it = 0; it < kLgIter; ++it) {
@@ -415,11 +465,11 @@ __global__ __launch_bounds__(256) void lg_place_kernel(BankArgs bank, IdsArgs id
   const int64_t total = n * bank.n_tables;
   const int64_t base = static_cast<int64_t>(blockIdx.x) * 256 * kLgIter;
   int32_t row[kLgIter], bb[kLgIter], slot[kLgIter], off[kLgIter];
+  {  // every id load first (one memory round trip)
+    int64_t bq[kLgIter];
+    lookup_rows_batch<kLgIter>(bank, ids, n, base + threadIdx.x, 256, total, row, bq, nullptr);
 #pragma unroll
-  for (int it = 0; it < kLgIter; ++it) {  // every id load first (one memory round trip)
-    int64_t b = 0;
-    row[it] = lookup_row(bank, ids, n, base + it * 256 + threadIdx.x, total, &b, nullptr);
-    bb[it] = static_cast<int32_t>(b);
+    for (int it = 0; it < kLgIter; ++it) bb[it] = static_cast<int32_t>(bq[it]);
   }
 #pragma unroll
   for (int it = 0; it < kLgIter; ++it) {
@@ -469,10 +519,9 @@ __global__ __launch_bounds__(kBkThreads) void bk_hist_kernel(BankArgs bank, IdsA
   const int64_t total = n * bank.n_tables;
   const int64_t i0 = static_cast<int64_t>(blockIdx.x) * kBkChunk + threadIdx.x;
   int32_t rr[kBkPer];
-#pragma unroll
-  for (int u = 0; u < kBkPer; ++u) {
-    int64_t b;
-    rr[u] = lookup_row(bank, ids, n, i0 + u * kBkThreads, total, &b, oob);
+  {
+    int64_t bq[kBkPer];
+    lookup_rows_batch<kBkPer>(bank, ids, n, i0, kBkThreads, total, rr, bq, oob);
   }
 #pragma unroll
   for (int u = 0; u < kBkPer; ++u)
@@ -547,11 +596,11 @@ __global__ __launch_bounds__(kBkThreads) void bk_scatter_kernel(BankArgs bank, I
     resv[q] = c ? atomicAdd(&w.bcur[k], c) : 0;
   }
   int32_t rr[kBkPer], bb[kBkPer];
+  {
+    int64_t bq[kBkPer];
+    lookup_rows_batch<kBkPer>(bank, ids, n, i0, kBkThreads, total, rr, bq, nullptr);
 #pragma unroll
-  for (int u = 0; u < kBkPer; ++u) {
-    int64_t b = 0;
-    rr[u] = lookup_row(bank, ids, n, i0 + u * kBkThreads, total, &b, nullptr);
-    bb[u] = static_cast<int32_t>(b);
+    for (int u = 0; u < kBkPer; ++u) bb[u] = static_cast<int32_t>(bq[u]);
   }
   const int all = bk_bucket_base(w.btot, NB, cur, wsum);
   int32_t *pub = w.bhist + static_cast<int64_t>(G) * NB;  // spare row: bucket starts

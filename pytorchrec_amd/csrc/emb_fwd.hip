@@ -142,23 +142,53 @@ __device__ __forceinline__ void interact_sample(const BankArgs &bank, const IdsA
     IA_STAMP(1, static_cast<int>(id0));
   }
 #endif
+  // The lane's field metadata (kernel-argument arrays indexed per lane: vector loads),
+  // then its ids, then its rows, each group issued unconditionally (a clamped field /
+  // row, masked afterwards): under `if (valid)` every loaded value was copied out of
+  // its branch and the copy waited for it, which chained ~5 round trips per field.
   uint4 raw[MAXIT];
+  const void *fptr[MAXIT];
+  int64_t frows[MAXIT], foff[MAXIT], idv[MAXIT];
+  bool okv[MAXIT];
+  // (iterations past the last field load table F - 1's id again: no branch per
+  // iteration, whose join would wait for the load)
+#pragma unroll
+  for (int it = 0; it < MAXIT; ++it) {
+    const int fc = min(it * WPW + worker, F - 1);
+    fptr[it] = ids.ptr[fc];
+    frows[it] = bank.rows[fc];
+    foff[it] = bank.row_offset[fc];
+  }
+  if (ids.chunk) {  // (uniform) chunked views: the per-element path
+#pragma unroll
+    for (int it = 0; it < MAXIT; ++it) idv[it] = load_id(ids, min(it * WPW + worker, F - 1), b);
+  } else if (ids.is64) {
+#pragma unroll
+    for (int it = 0; it < MAXIT; ++it) idv[it] = static_cast<const int64_t *>(fptr[it])[b * ids.stride];
+  } else {
+#pragma unroll
+    for (int it = 0; it < MAXIT; ++it) idv[it] = static_cast<const int32_t *>(fptr[it])[b * ids.stride];
+  }
 #pragma unroll
   for (int it = 0; it < MAXIT; ++it) {
     raw[it] = make_uint4(0, 0, 0, 0);
+    okv[it] = false;
+    if (it * WPW >= F) continue;  // uniform
+    okv[it] = it * WPW + worker < F && idv[it] >= 0 && idv[it] < frows[it];
+    const int64_t grow = okv[it] ? foff[it] + idv[it] : 0;
+    raw[it] = *reinterpret_cast<const uint4 *>(reinterpret_cast<const T *>(bank.data) +
+                                               grow * static_cast<int64_t>(bank.row_stride) + e0);
+  }
+#pragma unroll
+  for (int it = 0; it < MAXIT; ++it) {
+    if (it * WPW >= F) continue;  // uniform
     const int f = it * WPW + worker;
-    if (it * WPW < F && f < F) {
-      const int64_t id = load_id(ids, f, b);
-      if (id >= 0 && id < bank.rows[f]) {
-        const T *row = reinterpret_cast<const T *>(bank.data) +
-                       (bank.row_offset[f] + id) * static_cast<int64_t>(bank.row_stride);
-        raw[it] = *reinterpret_cast<const uint4 *>(row + e0);
-        if constexpr (ADAM)  // a lazily updated Adam bank: the row as of the last step
-          raw[it] = adam_current<T>(bank, bank.row_offset[f] + id, e0, live_elems(bank, e0, EPL),
-                                    raw[it], *bank.adam.d_t);
-      } else if (l == 0 && oob) {
-        *oob = 1;
-      }
+    if (!okv[it]) {
+      raw[it] = make_uint4(0, 0, 0, 0);
+      if (f < F && l == 0 && oob) *oob = 1;
+    } else if constexpr (ADAM) {  // a lazily updated Adam bank: the row as of the last step
+      raw[it] = adam_current<T>(bank, foff[it] + idv[it], e0, live_elems(bank, e0, EPL), raw[it],
+                                *bank.adam.d_t);
     }
   }
 

@@ -186,11 +186,7 @@ __device__ __forceinline__ void plan_hash_body(const BankArgs &bank, const IdsAr
   PLAN_STAMP(0);
   // ids of this thread's lookups, loads issued before anything waits on them
   int64_t id[kRounds];
-#pragma unroll
-  for (int k = 0; k < kRounds; ++k) {
-    const int i = k * THREADS + tid;
-    id[k] = i < B ? load_id(ids, f, i) : -1;
-  }
+  load_ids_batch<kRounds>(ids, f, tid, THREADS, B, -1, id);
   static_assert(SLOTS % (4 * THREADS) == 0, "16-B LDS init");
   for (int i = 4 * tid; i < SLOTS; i += 4 * THREADS) {
     *reinterpret_cast<uint4 *>(hkey + i) = make_uint4(kEmpty, kEmpty, kEmpty, kEmpty);

@@ -90,11 +90,7 @@ __global__ __launch_bounds__(kBT) void bucketize_kernel(IdsArgs ids, RowsArg row
   // one per round); ids < rows < 2^31, so owner / local row use 32-bit division
   constexpr int kPre = 8;
   int64_t pre[kPre];
-#pragma unroll
-  for (int r = 0; r < kPre; ++r) {
-    const int64_t i = static_cast<int64_t>(r) * kBT + tid;
-    pre[r] = (r < rounds && i < B) ? load_id(ids, f, i) : -1;
-  }
+  load_ids_batch<kPre>(ids, f, tid, kBT, B, -1, pre);
   auto id_of = [&](int r, int64_t i) -> int64_t {
     if (i >= B) return -1;
     if (r < kPre) {
@@ -194,11 +190,7 @@ __global__ __launch_bounds__(kBT) void bucketize_dedup_kernel(IdsArgs ids, RowsA
   const int64_t P = static_cast<int64_t>(F) * cap + F;  // int32 per owner part
   constexpr int kR = 8;
   int64_t idv[kR];
-#pragma unroll
-  for (int r = 0; r < kR; ++r) {
-    const int64_t i = static_cast<int64_t>(r) * kBT + tid;
-    idv[r] = (r < rounds && i < B) ? load_id(ids, f, s0 + i) : -2;
-  }
+  load_ids_batch<kR>(ids, f, s0 + tid, kBT, s0 + B, -2, idv);
   for (int i = tid; i < nh; i += kBT) hist[i] = 0u;
   for (int i = tid; i < hs; i += kBT) {
     keys[i] = kEmpty;

@@ -1,0 +1,7 @@
+export TMPDIR=/tmp
+mkdir -p gpurun_out/ldab
+timeout -k 10 700 python3 -u -m pytest tests/test_gpu_embedding.py tests/test_gpu_pins.py tests/test_gpu_din.py tests/test_gpu_sharded.py -x -q --timeout 120 --timeout-method thread > gpurun_out/ldab/t.log 2>&1; tail -2 gpurun_out/ldab/t.log
+H=$GRAFT_REPO_ROOT/pytorchrec_amd/lib/libmrec_head.so
+for m in "--model deepfm" "--model din" "--shard --force-collectives --exchange compact"; do
+  AB="MREC_LIB_PATH=$H - MREC_LIB_PATH=$H -" ARGS="$m" REP=1 OUT=ldab/x bash tools/gpu_ab_env.sh || exit 1
+done

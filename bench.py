@@ -861,8 +861,8 @@ def pcie_inclusive(step, args, sparse, dense_cols, label_col, device):
     return {"value": round(n * B / el, 1), "unit": "samples/s", "steps": n,
             "ms_per_step": round(el / n * 1e3, 4), "h2d_bytes_per_step": ld.layout.slot_bytes,
             "feed": f"ColumnarLoader (pytorchrec_amd/loader.py), depth {depth}: one packed pinned "
-                    "record per batch copied by mrec_batch_stage_cursor (kernel reading the "
-                    "host record over PCIe) on a branch of the step's HIP graph, depth - 1 "
+                    "record per batch read over PCIe by copy workgroups of the step's "
+                    "mrec_tower_dw_ex launch (mrec_feed_job, a device cursor), depth - 1 "
                     "batches ahead; one graph of depth steps replayed (capture_steps)"}
 
 

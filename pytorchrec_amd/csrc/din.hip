@@ -260,30 +260,49 @@ __global__ __launch_bounds__(256) void din_gather_kernel(BankArgs bank, const I 
   if (g >= 2 * N) return;
   const int64_t i = g >> 1;
   const int f = static_cast<int>(g & 1);
-  int32_t id;
-  if (i < B) {
-    id = din_narrow_id(f ? cid[i] : iid[i]);
-  } else {
-    const int64_t bb = (i - B) / L;
-    const int j = static_cast<int>(i - B - bb * L);
-    const I h = his[bb * ldh + j];
-    const bool pad = j > 0 && h == 0;  // masked (h < 0 is an error wherever it sits)
-    if (f == 0) {
-      id = pad ? -1 : din_narrow_id(h);
+  // Every id source is loaded before any is used, from clamped indices (a target
+  // lookup reads his[0] / hcat[0], a history one iid[0] / cid[0], and drops them), and
+  // the two tables' bounds come from the kernel arguments by constant index: as
+  // written before, his -> hcat -> rows[f] -> row_offset[f] -> row ran as ~5 dependent
+  // round trips (a loaded value copied out of a branch waits for its load).
+  const bool tgt = i < B;
+  int64_t bb = 0;
+  int j = 0;
+  if (!tgt) {
+    const int64_t r = i - B;
+    if (N < (int64_t(1) << 31)) {  // (uniform) 32-bit division
+      const uint32_t q = static_cast<uint32_t>(r) / static_cast<uint32_t>(L);
+      bb = q;
+      j = static_cast<int>(static_cast<uint32_t>(r) - q * static_cast<uint32_t>(L));
     } else {
-      const I c = hcat[bb * ldc + j];
-      id = (pad && c >= 0) ? -1 : din_narrow_id(c);
+      bb = r / L;
+      j = static_cast<int>(r - bb * L);
     }
   }
+  const I tv = (f ? cid : iid)[tgt ? i : 0];
+  const I h = his[bb * ldh + j];
+  const I c = hcat[bb * ldc + j];
+  // (an empty use of all three: the compiler would otherwise sink each load into the
+  // branch that consumes it, one round trip after the other)
+  asm volatile("" ::"v"(tv), "v"(h), "v"(c));
+  int32_t id;
+  if (tgt) {
+    id = din_narrow_id(tv);
+  } else {
+    const bool pad = j > 0 && h == 0;  // masked (h < 0 is an error wherever it sits)
+    id = f == 0 ? (pad ? -1 : din_narrow_id(h)) : ((pad && c >= 0) ? -1 : din_narrow_id(c));
+  }
   if (l == 0) (f ? out_c : out_i)[i] = id;
-  const bool ok = id >= 0 && id < bank.rows[f];
-  uint4 raw = make_uint4(0, 0, 0, 0);
-  if (ok) {
-    const T *row = reinterpret_cast<const T *>(bank.data) +
-                   (bank.row_offset[f] + id) * static_cast<int64_t>(bank.row_stride);
-    raw = *reinterpret_cast<const uint4 *>(row + l * EPL);
-  } else if (l == 0 && oob && id >= 0) {
-    *oob = 1;
+  const int64_t nrow = f ? bank.rows[1] : bank.rows[0];
+  const int64_t roff = f ? bank.row_offset[1] : bank.row_offset[0];
+  const bool ok = id >= 0 && id < nrow;
+  uint4 raw = *reinterpret_cast<const uint4 *>(reinterpret_cast<const T *>(bank.data) +
+                                               (ok ? roff + id : 0) *
+                                                   static_cast<int64_t>(bank.row_stride) +
+                                               l * EPL);
+  if (!ok) {
+    raw = make_uint4(0, 0, 0, 0);
+    if (l == 0 && oob && id >= 0) *oob = 1;
   }
   const int D = bank.dim;
   const int e0 = l * EPL;

@@ -378,19 +378,37 @@ __global__ __launch_bounds__(kWireThreads) void gather_wire_kernel(BankArgs bank
   const int32_t *ids = recv + static_cast<int64_t>(p) * (static_cast<int64_t>(w.F) * w.cap + w.F);
   const uint32_t *data = reinterpret_cast<const uint32_t *>(bank.data);
   const int row_dw = bank.lpr * 4;
+  // every id load first, unconditionally (element 0 past n) and pinned by an empty
+  // use: under `if (e < n)` each load waited on its own (one round trip per element)
   int64_t src[kWirePer];
+  int32_t idv[kWirePer];
+  int fr[kWirePer], kr[kWirePer];
 #pragma unroll
-  for (int it = 0; it < kWirePer; ++it) {  // every id load first
+  for (int it = 0; it < kWirePer; ++it) {
     const uint32_t e = e0 + it * kWireThreads;
-    src[it] = -1;
-    if (e < n) {
-      const int r = static_cast<int>(e / rdw), k = static_cast<int>(e - r * rdw);
-      const int f = wire_table(pre, w.F, r);
-      const int64_t id = ids[static_cast<int64_t>(f) * w.cap + (r - pre[f])];
-      if (id >= 0 && id < nrows[f]) src[it] = (roff[f] + id) * row_dw + k;
-    }
+    const uint32_t ec = e < n ? e : 0u;
+    const int r = static_cast<int>(ec / rdw);
+    kr[it] = static_cast<int>(ec - r * rdw);
+    fr[it] = wire_table(pre, w.F, r);
+    idv[it] = ids[static_cast<int64_t>(fr[it]) * w.cap + (r - pre[fr[it]])];
+  }
+#pragma unroll
+  for (int it = 0; it < kWirePer; ++it) asm volatile("" ::"v"(idv[it]));
+#pragma unroll
+  for (int it = 0; it < kWirePer; ++it) {
+    const int64_t id = idv[it];
+    const int f = fr[it];
+    src[it] = (e0 + it * kWireThreads < n && id >= 0 && id < nrows[f])
+                  ? (roff[f] + id) * row_dw + kr[it]
+                  : -1;
   }
   uint32_t v[kWirePer];
+  if constexpr (!ADAM) {  // the row dwords the same way
+#pragma unroll
+    for (int it = 0; it < kWirePer; ++it) v[it] = data[src[it] >= 0 ? src[it] : 0];
+#pragma unroll
+    for (int it = 0; it < kWirePer; ++it) asm volatile("" ::"v"(v[it]));
+  }
 #pragma unroll
   for (int it = 0; it < kWirePer; ++it) {
     if constexpr (ADAM) {
@@ -406,7 +424,7 @@ __global__ __launch_bounds__(kWireThreads) void gather_wire_kernel(BankArgs bank
         v[it] = q[k & 3];
       }
     } else {
-      v[it] = src[it] >= 0 ? data[src[it]] : 0u;
+      v[it] = src[it] >= 0 ? v[it] : 0u;
     }
   }
   uint32_t *dst = wire + static_cast<int64_t>(p) * w.cap_rows * w.rec_dw;

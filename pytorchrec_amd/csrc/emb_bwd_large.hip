@@ -1228,6 +1228,9 @@ __global__ __launch_bounds__(256) void bk_apply_kernel(BankArgs bank, LgWs w, Ap
     float acc[EPL];
 #pragma unroll
     for (int q = 0; q < EPL; ++q) acc[q] = 0.f;
+    // the row first: it does not depend on the lookups' gradients
+    uint4 raw = make_uint4(0u, 0u, 0u, 0u);
+    if (live) raw = *reinterpret_cast<const uint4 *>(row_ptr_g<T>(bank, a, grow, e0));
     if (live) {
       int rr[kLgShort];
 #pragma unroll
@@ -1238,12 +1241,41 @@ __global__ __launch_bounds__(256) void bk_apply_kernel(BankArgs bank, LgWs w, Ap
         bitonic_sort<8>(rr);
       else
         bitonic_sort<16>(rr);
+      // plain bf16 gradient rows (DIN's gathered-row gradient): the lookups' 16-B
+      // pieces 4 at a time, issued together (clamped to the first lookup, pinned by
+      // an empty use) and added in the same ascending order: the per-lookup loop
+      // waited for each load in turn
+      bool fast = false;
+      if constexpr (EPL == 8)
+        fast = v_lane && !a.g_rec && !a.g_occ && !a.dfm && a.dx && a.dx_bf16;
+      if (fast) {
+        const uint16_t *dxb = static_cast<const uint16_t *>(a.dx) + static_cast<int64_t>(f) * D + e0;
 #pragma unroll
-      for (int j = 0; j < kLgShort; ++j)
-        if (j < len) add_lookup_grad<EPL>(a, rr[j], f, D, e0, v_lane, w_lane, acc);
+        for (int j0 = 0; j0 < kLgShort; j0 += 4) {
+          if (j0 >= len) break;
+          uint4 q4[4];
+#pragma unroll
+          for (int u = 0; u < 4; ++u) {
+            const int b = j0 + u < len ? rr[j0 + u] : rr[0];
+            q4[u] = *reinterpret_cast<const uint4 *>(dxb + static_cast<int64_t>(b) * a.dx_ld);
+          }
+          asm volatile("" ::"v"(q4[0].x), "v"(q4[1].x), "v"(q4[2].x), "v"(q4[3].x));
+#pragma unroll
+          for (int u = 0; u < 4; ++u) {
+            if (j0 + u < len) {
+              float g[EPL];
+              Vec<uint16_t>::to_f32(q4[u], g);
+#pragma unroll
+              for (int q = 0; q < EPL; ++q) acc[q] += g[q];
+            }
+          }
+        }
+      } else {
+#pragma unroll
+        for (int j = 0; j < kLgShort; ++j)
+          if (j < len) add_lookup_grad<EPL>(a, rr[j], f, D, e0, v_lane, w_lane, acc);
+      }
     }
-    uint4 raw = make_uint4(0u, 0u, 0u, 0u);
-    if (live) raw = *reinterpret_cast<const uint4 *>(row_ptr_g<T>(bank, a, grow, e0));
     row_update<T, LPR, -1>(bank, a, grow, e0, v_lane, w_lane, live, acc, raw);
   }
   for (int m = wid; m < nmd; m += 4) {  // medium rows: one per wave (wave-uniform)

@@ -1278,32 +1278,83 @@ __global__ __launch_bounds__(256) void bk_apply_kernel(BankArgs bank, LgWs w, Ap
     }
     row_update<T, LPR, -1>(bank, a, grow, e0, v_lane, w_lane, live, acc, raw);
   }
+  // plain bf16 gradient rows: a worker's lookups 4 at a time, their permutation
+  // entries then their 16-B gradient pieces issued together (each pinned by an empty
+  // use); the max and the fixed-point sums do not depend on the order (DIN's category
+  // table puts all of its rows here, ~130 lookups each at C4)
+  bool mfast = false;
+  if constexpr (EPL == 8) mfast = v_lane && !a.g_rec && !a.g_occ && !a.dfm && a.dx && a.dx_bf16;
   for (int m = wid; m < nmd; m += 4) {  // medium rows: one per wave (wave-uniform)
     const int k = rowl[kBkSlots - 1 - m];
     const int ms = seg[k], mlen = cur[k] - seg[k];
     const int64_t grow = key[k];
     const int f = table_of_row(bank, grow);
+    uint4 raw = make_uint4(0u, 0u, 0u, 0u);  // the row, for the update (issued first)
+    if (live && wk == 0) raw = *reinterpret_cast<const uint4 *>(row_ptr_g<T>(bank, a, grow, e0));
+    const uint16_t *dxb = mfast ? static_cast<const uint16_t *>(a.dx) + static_cast<int64_t>(f) * D + e0
+                                : nullptr;
+    auto grads4 = [&](int j0, uint4 (&q4)[4]) {
+      int idx[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const int j = j0 + u * WPW;
+        idx[u] = P[ms + (j < mlen ? j : 0)];
+      }
+      asm volatile("" ::"v"(idx[0]), "v"(idx[1]), "v"(idx[2]), "v"(idx[3]));
+#pragma unroll
+      for (int u = 0; u < 4; ++u)
+        q4[u] = *reinterpret_cast<const uint4 *>(dxb + static_cast<int64_t>(idx[u]) * a.dx_ld);
+      asm volatile("" ::"v"(q4[0].x), "v"(q4[1].x), "v"(q4[2].x), "v"(q4[3].x));
+    };
     float mx = 0.f;
-    if (live)
+    if (mfast) {
+      for (int j0 = wk; j0 < mlen; j0 += 4 * WPW) {
+        uint4 q4[4];
+        grads4(j0, q4);
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+          if (j0 + u * WPW >= mlen) continue;
+          float g[EPL];
+          Vec<uint16_t>::to_f32(q4[u], g);
+#pragma unroll
+          for (int q = 0; q < EPL; ++q) mx = fmaxf(mx, fabsf(g[q]));
+        }
+      }
+    } else if (live) {
       for (int j = wk; j < mlen; j += WPW) {
         float g[EPL];
         lookup_grad<EPL>(a, P[ms + j], f, D, e0, v_lane, w_lane, g);
 #pragma unroll
         for (int q = 0; q < EPL; ++q) mx = fmaxf(mx, fabsf(g[q]));
       }
+    }
 #pragma unroll
     for (int off = 32; off > 0; off >>= 1) mx = fmaxf(mx, __shfl_xor(mx, off));
     const int S = lg_scale(mx, mlen);
     long long sa[EPL];
 #pragma unroll
     for (int q = 0; q < EPL; ++q) sa[q] = 0;
-    if (live)
+    if (mfast) {
+      for (int j0 = wk; j0 < mlen; j0 += 4 * WPW) {
+        uint4 q4[4];
+        grads4(j0, q4);
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+          if (j0 + u * WPW >= mlen) continue;
+          float g[EPL];
+          Vec<uint16_t>::to_f32(q4[u], g);
+#pragma unroll
+          for (int q = 0; q < EPL; ++q) sa[q] += llrint(ldexp(static_cast<double>(g[q]), S));
+        }
+      }
+    } else if (live) {
       for (int j = wk; j < mlen; j += WPW) {
         float g[EPL];
         lookup_grad<EPL>(a, P[ms + j], f, D, e0, v_lane, w_lane, g);
 #pragma unroll
         for (int q = 0; q < EPL; ++q) sa[q] += llrint(ldexp(static_cast<double>(g[q]), S));
       }
+    }
 #pragma unroll
     for (int off = LPR; off < 64; off <<= 1)
 #pragma unroll
@@ -1312,8 +1363,6 @@ __global__ __launch_bounds__(256) void bk_apply_kernel(BankArgs bank, LgWs w, Ap
       float acc[EPL];
 #pragma unroll
       for (int q = 0; q < EPL; ++q) acc[q] = static_cast<float>(ldexp(static_cast<double>(sa[q]), -S));
-      uint4 raw = make_uint4(0u, 0u, 0u, 0u);
-      if (live) raw = *reinterpret_cast<const uint4 *>(row_ptr_g<T>(bank, a, grow, e0));
       row_update<T, LPR, -1>(bank, a, grow, e0, v_lane, w_lane, live, acc, raw);
     }
   }

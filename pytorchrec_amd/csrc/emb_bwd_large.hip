@@ -203,26 +203,13 @@ __device__ __forceinline__ Run lane_run(int32_t r) {
   return out;
 }
 
-__device__ __forceinline__ int32_t lookup_row(const BankArgs &bank, const IdsArgs &ids, int64_t n,
-                                              int64_t i, int64_t total, int64_t *b_out,
-                                              int32_t *__restrict__ oob) {
-  if (i >= total) return -1;
-  // (total = batch * n_tables < 2^31, checked by lg_setup: 32-bit division)
-  const uint32_t ui = static_cast<uint32_t>(i), un = static_cast<uint32_t>(n);
-  const int f = static_cast<int>(ui / un);
-  const int64_t b = static_cast<int64_t>(ui - static_cast<uint32_t>(f) * un);
-  *b_out = b;
-  const int64_t id = load_id(ids, f, b);
-  if (id >= 0 && id < bank.rows[f]) return static_cast<int32_t>(bank.row_offset[f] + id);
-  if (oob && !(ids.pad_negative && id < 0)) *oob = 1;
-  return -1;
-}
-
-// lookup_row for the N lookups i_k = i0 + k * step of a thread, every load issued
+// The rows of the N lookups i_k = i0 + k * step of a thread (lookup i: table
+// i / n, sample i % n; -1 for an invalid id or i >= total), every load issued
 // before any is used (common.h load_ids_batch): the per-lane kernel-argument reads
 // (ids.ptr[f], rows[f], row_offset[f]) first, then the ids, unconditionally from
-// clamped indices.  As N calls of lookup_row the compiler chained ~4 dependent round
-// trips per lookup (each loaded value copied out of its branch waits for it).
+// clamped indices.  As N calls of a one-lookup helper the compiler chained ~4
+// dependent round trips per lookup (each loaded value copied out of its branch
+// waits for it).
 // b_out[k] = the lookup's sample (0 past `total`).
 template <int N>
 __device__ __forceinline__ void lookup_rows_batch(const BankArgs &bank, const IdsArgs &ids,

@@ -10,6 +10,8 @@
 #include <algorithm>
 
 #include "common.h"
+#include <cstdlib>
+
 #include "feed_common.h"
 
 namespace mrec {
@@ -70,8 +72,15 @@ mrec_status build_feed_copy(const mrec_feed_job *job, int threads, FeedCopy *out
   out->dst = static_cast<uint4 *>(j.dst);
   out->state = reinterpret_cast<unsigned long long *>(j.d_state);
   const int64_t n16 = j.record_bytes / 16;
+  // 32 loads in flight per lane (MREC_FEED_UNROLL=4|16|32): fewer copying workgroups
+  static const int unroll = [] {
+    const char *e = std::getenv("MREC_FEED_UNROLL");
+    const int u = e ? std::atoi(e) : 32;
+    return u == 4 || u == 16 ? u : 32;
+  }();
+  out->unroll = unroll;
   out->blocks = static_cast<int>(std::max<int64_t>(
-      std::min<int64_t>((n16 + 4 * threads - 1) / (4 * threads), 1024), 1));
+      std::min<int64_t>((n16 + unroll * threads - 1) / (unroll * threads), 1024), 1));
   return MREC_OK;
 }
 

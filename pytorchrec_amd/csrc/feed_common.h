@@ -18,11 +18,13 @@ struct FeedCopy {
   uint4 *dst;                 // the device slot
   unsigned long long *state;  // [0] cursor, [1] ticket
   int blocks;                 // workgroups of the launch that copy (0: none)
+  int unroll;                 // 16-B loads in flight per lane: 4, 16 or 32 (fewer copying
+                              // workgroups, so fewer CUs with host loads in flight)
 };
 
 // run by workgroup `b` of the `fc.blocks` copying ones (THREADS threads each)
-template <int THREADS>
-__device__ __forceinline__ void feed_copy_body(const FeedCopy &fc, int b, long long *s_rec) {
+template <int THREADS, int U = 4>
+__device__ __forceinline__ void feed_copy_body_u(const FeedCopy &fc, int b, long long *s_rec) {
   if (threadIdx.x == 0)
     *s_rec = static_cast<long long>(
         __hip_atomic_load(fc.state, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
@@ -31,7 +33,6 @@ __device__ __forceinline__ void feed_copy_body(const FeedCopy &fc, int b, long l
   if (rec >= 0 && rec < fc.n_records) {
     const uint4 *src = reinterpret_cast<const uint4 *>(fc.src + rec * fc.record_bytes);
     const int64_t n16 = fc.record_bytes / 16;
-    constexpr int U = 4;  // independent 16-B loads per lane per trip
     const int64_t stride = static_cast<int64_t>(fc.blocks) * THREADS;
     int64_t i = static_cast<int64_t>(b) * THREADS + threadIdx.x;
     for (; i + (U - 1) * stride < n16; i += U * stride) {
@@ -53,6 +54,16 @@ __device__ __forceinline__ void feed_copy_body(const FeedCopy &fc, int b, long l
                          __HIP_MEMORY_SCOPE_AGENT);
     }
   }
+}
+
+template <int THREADS>
+__device__ __forceinline__ void feed_copy_body(const FeedCopy &fc, int b, long long *s_rec) {
+  if (fc.unroll == 32)  // uniform
+    feed_copy_body_u<THREADS, 32>(fc, b, s_rec);
+  else if (fc.unroll == 16)
+    feed_copy_body_u<THREADS, 16>(fc, b, s_rec);
+  else
+    feed_copy_body_u<THREADS, 4>(fc, b, s_rec);
 }
 
 // host (feed.hip): validate a mrec_feed_job and fill *out (blocks: the copying

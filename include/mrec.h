@@ -32,7 +32,7 @@
 extern "C" {
 #endif
 
-#define MREC_ABI_VERSION 27
+#define MREC_ABI_VERSION 28
 #define MREC_MAX_TABLES 64      /* tables per table bank / per call */
 #define MREC_BWD_MAX_BATCH 8192  /* lookups per table per plan/apply call */
 #define MREC_BWD_HASH_MAX_BATCH 4096  /* batches up to this use the hash plan */
@@ -219,9 +219,26 @@ size_t mrec_emb_bwd_workspace_size(int32_t n_tables, int64_t batch);
  * Plan of the embedding backward: per table the lookups are grouped by row (an
  * LDS hash table for batch <= MREC_BWD_HASH_MAX_BATCH, a stable LDS radix sort
  * up to MREC_BWD_MAX_BATCH).  Depends only on the ids, so it can run as soon as
- * the batch is resident (or inside a GEMM launch: mrec_gemm_multi_ex).  If
- * d_step (device uint64, may be NULL) is given the plan increments it once, so a
- * graph replayed step after step still draws fresh stochastic-rounding bits.
+ * the batch is resident (or inside another launch: mrec_interact_fwd_ex,
+ * mrec_shard_gather_wire).  If d_step (device uint64, may be NULL) is given the plan
+ * increments it once, so a graph replayed step after step still draws fresh
+ * stochastic-rounding bits.
+ *
+ * Workspace layout rule (ABI 28).  The plan writes the HASH layout when batch <=
+ * MREC_BWD_HASH_MAX_BATCH, or when the ids are a padded exchange view
+ * (mrec_ids.pad_negative) of batch <= MREC_BWD_MAX_BATCH entries; else the SORTED
+ * layout.  An apply reads the hash layout when batch <= MREC_BWD_HASH_MAX_BATCH or
+ * when its gradients are given (mrec_emb_bwd_apply_given with g_occ, _wire), else
+ * the sorted one.  So a padded plan of more than MREC_BWD_HASH_MAX_BATCH entries is
+ * consumed only by the given-gradient applies.  Every plan entry (this one, the
+ * mrec_plan_job of mrec_interact_fwd_ex / mrec_shard_gather_wire(_ex)) records
+ * {layout, batch, n_tables} for its workspace address when it is issued (host side;
+ * the same tag, (batch << 2) | layout, is stamped into the device headers), and every
+ * apply (mrec_emb_bwd_apply, _ex, _given, _rec, _wire) returns MREC_EINVAL, with
+ * mrec_last_error naming both layouts, when the workspace's last plan wrote another
+ * layout, batch or table count, or when no plan was issued into it.  Batch 0 reads
+ * nothing and is not checked.  (The reference's autograd backward cannot be
+ * mis-paired: IModel.py:123; misuse raises: IModel.py:101-108.)
  */
 mrec_status mrec_emb_bwd_plan(const mrec_table_bank *bank, const mrec_ids *ids, int64_t batch,
                               void *workspace, size_t ws_bytes, int32_t *d_oob_flag,

@@ -19,6 +19,15 @@ that single tensor cannot be assembled anywhere, so a sharded model writes:
 Every file is written under a temporary name and renamed into place, so a new save
 never modifies the inode of an earlier one (``link_snapshot`` relies on it).
 
+Crash consistency: a save draws one random ``save_id`` (rank 0's, shared by an
+all-reduce), written into the index and beside every shard file (``{shard}.id``);
+rank 0 writes the main file only after a barrier that follows every rank's renames.
+Loading checks each shard's id against the index, so a crash mid-save (new index,
+some shards of the previous save: same shapes) raises instead of restoring rows of
+two different steps.  The main file is read by every rank (``load_weights``), so
+it must live on a filesystem all ranks see; at the same world size each rank then
+reads only its own shard files (those may be node-local).
+
 Loading reads only the rows the loading rank owns, straight from the shard files
 (numpy memory maps, ``allow_pickle=False``): same world size -> its own file, chunk
 by chunk; any other world size (including an unsharded ``EmbeddingBank``, world 1)
@@ -87,6 +96,29 @@ def _barrier(comm, device):
     comm.allreduce_sum_(torch.zeros(1, device=device))
 
 
+def _shared_save_id(comm, rank: int, device) -> int:
+    """A random 48-bit id drawn by rank 0 and summed to every rank (three 16-bit
+    parts: exact in fp32, whatever the communicator reduces in)."""
+    parts = torch.zeros(3, device=device)
+    if rank == 0:
+        parts.copy_(torch.from_numpy(np.frombuffer(os.urandom(6), dtype=np.uint16)
+                                     .astype(np.float32)))
+    comm.allreduce_sum_(parts)
+    a, b, c = (int(v) for v in parts.cpu().tolist())
+    return (a << 32) | (b << 16) | c
+
+
+def id_file(shard_path: str) -> str:
+    return shard_path + ".id"
+
+
+def _write_text(path: str, text: str) -> None:
+    tmp = path + ".tmp"
+    with open(tmp, "w") as f:
+        f.write(text)
+    os.replace(tmp, path)
+
+
 @torch.no_grad()
 def save_sharded(model, filepath: str, chunk_rows: int = CHUNK_ROWS) -> None:
     """Write ``model`` (with row-sharded banks) as described in the module
@@ -96,6 +128,8 @@ def save_sharded(model, filepath: str, chunk_rows: int = CHUNK_ROWS) -> None:
     sharded = [(k, m) for k, m in banks if _is_sharded(m)]
     comm = sharded[0][1].comm
     rank, world = sharded[0][1].rank, sharded[0][1].world
+    dev = sharded[0][1].weight.device
+    save_id = _shared_save_id(comm, rank, dev)
     index = {}
     for key, m in sharded:
         dt = "bfloat16" if m.weight.dtype == torch.bfloat16 else "float32"
@@ -109,15 +143,18 @@ def save_sharded(model, filepath: str, chunk_rows: int = CHUNK_ROWS) -> None:
         arr.flush()
         del arr
         os.replace(tmp, path)
+        _write_text(id_file(path), f"{save_id}\n")
         index[key] = {"world": m.world, "global_rows": list(m.global_rows),
                       "row_stride": m.row_stride, "dim": m.dim, "has_w": bool(m.has_w),
-                      "dtype": dt, "files": [shard_suffix(key, r, m.world) for r in range(m.world)]}
+                      "dtype": dt, "files": [shard_suffix(key, r, m.world) for r in range(m.world)],
+                      "save_id": save_id}
+    _barrier(comm, dev)  # every rank's shards and ids are in place before the index
     if rank == 0:
         keys = {k for k, _ in sharded}
         out = {k: v for k, v in sd.items() if k not in keys}
         out[INDEX_KEY] = index
         save_file(out, filepath)
-    _barrier(comm, sharded[0][1].weight.device)
+    _barrier(comm, dev)
 
 
 def save_file(obj, filepath: str) -> None:
@@ -152,6 +189,15 @@ def load_bank_from_shards(m, meta: Dict, filepath: str, chunk_rows: int = CHUNK_
             continue  # same world size: only this rank's own file has its rows (and only
             # it needs to be visible to this rank: node-local disks work)
         path = filepath + meta["files"][s]
+        if "save_id" in meta:  # (checkpoints before r06 carry none)
+            try:
+                with open(id_file(path)) as f:
+                    got = int(f.read().strip())
+            except (OSError, ValueError):
+                got = None
+            if got != int(meta["save_id"]):
+                raise RuntimeError(f"{path}: shard of another save (id {got}, the index says "
+                                   f"{meta['save_id']}): the checkpoint is incomplete")
         mm = np.load(path, mmap_mode="r", allow_pickle=False)
         n_s, offs_s = _shard_layout(grows, W, s)
         if mm.shape[0] != sum(n_s) or mm.shape[1] != int(meta["row_stride"]):
@@ -229,7 +275,8 @@ def checkpoint_files(model, filepath: str) -> List[str]:
     if not sharded:
         return [filepath]
     r, W = sharded[0][1].rank, sharded[0][1].world
-    return ([filepath] if r == 0 else []) + [shard_file(filepath, k, r, W) for k, _ in sharded]
+    shards = [shard_file(filepath, k, r, W) for k, _ in sharded]
+    return ([filepath] if r == 0 else []) + shards + [id_file(p) for p in shards]
 
 
 def link_snapshot(model, filepath: str, snapshot: str) -> None:
@@ -249,7 +296,8 @@ def remove_checkpoint(filepath: str, state: Optional[Dict] = None) -> None:
         state = torch.load(filepath, map_location="cpu", weights_only=True)
     for meta in state.get(INDEX_KEY, {}).values():
         for suf in meta["files"]:
-            if os.path.exists(filepath + suf):
-                os.remove(filepath + suf)
+            for p in (filepath + suf, id_file(filepath + suf)):
+                if os.path.exists(p):
+                    os.remove(p)
     if os.path.exists(filepath):
         os.remove(filepath)

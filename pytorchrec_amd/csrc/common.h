@@ -26,6 +26,27 @@ void set_error(const std::string &msg);
 mrec_status launch_status(const char *what);  // hipGetLastError -> status
 
 // ---------------------------------------------------------------------------
+// Embedding-backward workspace layout tags (ABI 28).  A plan decides the layout
+// (sorted or hash) from its batch and whether its ids are a padded exchange view;
+// an apply decides it from its batch and whether the gradients are given.  The two
+// can disagree (a padded plan of 4096 < B <= 8192 entries followed by a plain
+// apply), and the apply would then read the workspace in the wrong layout.  So
+// every plan records {layout, batch, tables} per workspace address on the host when
+// it is issued (and stamps the same tag into the device headers, ws_layout_tag),
+// and every apply entry checks its own expectation against the record before it
+// launches: a mismatch, or a workspace no plan was issued for, is MREC_EINVAL.
+// Host-only (no device read, no sync): graph capture records the plan first too.
+// ---------------------------------------------------------------------------
+constexpr int kLayoutSorted = 0;  // emb_plan.h describes both layouts
+constexpr int kLayoutHash = 1;
+__host__ __device__ inline int32_t ws_layout_tag(int layout, int64_t batch) {
+  return static_cast<int32_t>((batch << 2) | layout);
+}
+void ws_layout_record(const void *ws, int layout, int64_t batch, int n_tables, bool padded);
+mrec_status ws_layout_check(const void *ws, int layout, int64_t batch, int n_tables,
+                            const char *who);
+
+// ---------------------------------------------------------------------------
 // Kernel clock (measurement only, mrec_kernel_clock; layout in mrec.h).
 // The clocked kernels are a separate instantiation (template flag KC), launched
 // only while the clock is on: KcScope<false> is empty, so the production kernels

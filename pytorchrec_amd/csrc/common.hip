@@ -1,6 +1,9 @@
 // Host-side helpers and the ABI identity functions of libmrec.
 #include "common.h"
 
+#include <mutex>
+#include <unordered_map>
+
 namespace mrec {
 
 static thread_local std::string g_last_error;
@@ -12,6 +15,58 @@ mrec_status launch_status(const char *what) {
   if (e != hipSuccess) {
     set_error(std::string(what) + ": " + hipGetErrorString(e));
     return MREC_EHIP;
+  }
+  return MREC_OK;
+}
+
+// workspace layout records (common.h): address -> the last plan issued into it
+namespace {
+struct WsRecord {
+  int layout;
+  int64_t batch;
+  int n_tables;
+  bool padded;
+  uint64_t seq;
+};
+std::mutex g_ws_mu;
+std::unordered_map<uintptr_t, WsRecord> g_ws_records;
+uint64_t g_ws_seq = 0;
+constexpr size_t kWsRecordsMax = 1 << 14;
+const char *layout_name(int layout) { return layout == kLayoutHash ? "hash" : "sorted"; }
+}  // namespace
+
+void ws_layout_record(const void *ws, int layout, int64_t batch, int n_tables, bool padded) {
+  std::lock_guard<std::mutex> lk(g_ws_mu);
+  if (g_ws_records.size() >= kWsRecordsMax &&
+      g_ws_records.find(reinterpret_cast<uintptr_t>(ws)) == g_ws_records.end()) {
+    auto oldest = g_ws_records.begin();  // (only a process with 16 k live workspaces gets here)
+    for (auto it = g_ws_records.begin(); it != g_ws_records.end(); ++it)
+      if (it->second.seq < oldest->second.seq) oldest = it;
+    g_ws_records.erase(oldest);
+  }
+  g_ws_records[reinterpret_cast<uintptr_t>(ws)] = WsRecord{layout, batch, n_tables, padded, ++g_ws_seq};
+}
+
+mrec_status ws_layout_check(const void *ws, int layout, int64_t batch, int n_tables,
+                            const char *who) {
+  if (batch == 0) return MREC_OK;  // nothing is read
+  std::lock_guard<std::mutex> lk(g_ws_mu);
+  auto it = g_ws_records.find(reinterpret_cast<uintptr_t>(ws));
+  if (it == g_ws_records.end()) {
+    set_error(std::string(who) + ": no embedding-backward plan was issued into this workspace");
+    return MREC_EINVAL;
+  }
+  const WsRecord &r = it->second;
+  if (r.layout != layout || r.batch != batch || r.n_tables != n_tables) {
+    set_error(std::string(who) + ": workspace layout mismatch: the plan wrote the " +
+              layout_name(r.layout) + " layout for " + std::to_string(r.batch) + " entries x " +
+              std::to_string(r.n_tables) + " tables" + (r.padded ? " (padded exchange view)" : "") +
+              ", this apply reads the " + layout_name(layout) + " layout for " +
+              std::to_string(batch) + " x " + std::to_string(n_tables) +
+              (layout == kLayoutHash ? "" :
+               " (a padded plan past MREC_BWD_HASH_MAX_BATCH entries takes the hash layout: "
+               "apply it with mrec_emb_bwd_apply_given / _wire)"));
+    return MREC_EINVAL;
   }
   return MREC_OK;
 }

@@ -194,7 +194,7 @@ __global__ __launch_bounds__(kPlanThreads) void plan_kernel(BankArgs bank, IdsAr
   sort_and_segment(keyA, keyB, payA, payB, rounds, rows, hist, wtot, t, &s_total, &s_nvalid);
   if (tid == 0) {
     t.hdr[2] = 0;
-    t.hdr[3] = kLayoutSorted;
+    t.hdr[3] = ws_layout_tag(kLayoutSorted, B);
     if (d_step && f == 0) *d_step += 1;
   }
 }
@@ -732,6 +732,8 @@ mrec_status build_plan_job(const mrec_plan_job *plan, PlanJob *out) {
   }
   for (int f = 0; f < out->bank.n_tables; ++f)
     MREC_CHECK_ARG(out->bank.rows[f] < (int64_t(1) << 31), "rows per table must be < 2^31");
+  ws_layout_record(plan->workspace, kLayoutHash, plan->batch, out->bank.n_tables,
+                   out->ids.pad_negative != 0);
   out->B = plan->batch;
   out->ws = plan->workspace;
   out->oob = plan->d_oob_flag;
@@ -820,7 +822,10 @@ mrec_status mrec_emb_bwd_plan(const mrec_table_bank *bank, const mrec_ids *ids, 
   for (int f = 0; f < ba.n_tables; ++f)
     MREC_CHECK_ARG(ba.rows[f] < (int64_t(1) << 31), "rows per table must be < 2^31");
   const int rounds = static_cast<int>((batch + kPlanThreads - 1) / kPlanThreads);
-  if (batch >= 1 && hash_layout(batch, ia.pad_negative != 0)) {
+  const bool hash = batch >= 1 && hash_layout(batch, ia.pad_negative != 0);
+  ws_layout_record(workspace, hash ? kLayoutHash : kLayoutSorted, batch, ba.n_tables,
+                   ia.pad_negative != 0);
+  if (hash) {
     plan_hash_kernel<<<dim3(ba.n_tables * kPlanBuckets), kPlanThreads, 0,
                        static_cast<hipStream_t>(stream)>>>(
         ba, ia, batch, workspace, d_oob_flag, d_step);
@@ -851,6 +856,7 @@ mrec_status mrec_diag_plan_hash_variant(const mrec_table_bank *bank, const mrec_
                  "workspace too small");
   const dim3 grid(ba.n_tables * kPlanBuckets);
   hipStream_t s = static_cast<hipStream_t>(stream);
+  ws_layout_record(workspace, kLayoutHash, batch, ba.n_tables, ia.pad_negative != 0);
   if (threads == 1024 && slots == 8192)
     plan_hash_variant_kernel<1024, 8192, kHashMaxEntries><<<grid, 1024, 0, s>>>(ba, ia, batch, workspace, d_oob_flag);
   else if (threads == 512 && slots == 8192)
@@ -984,6 +990,15 @@ static mrec_status apply_impl(const mrec_table_bank *bank, int64_t batch, const 
     return MREC_ENOSPC;
   }
   MREC_CHECK_ARG(mode >= MREC_BWD_DENSE_GRAD && mode <= MREC_BWD_ADAM, "bad mode");
+  // the layout this apply reads (hash: batch <= 4096, or an exchange view's given
+  // gradients up to 8192 entries) must be the one the workspace's plan wrote
+  const bool hash = hash_layout(batch, g_occ != nullptr || gw != nullptr);
+  if ((st = ws_layout_check(workspace, hash ? kLayoutHash : kLayoutSorted, batch, ba.n_tables,
+                            gw ? "mrec_emb_bwd_apply_wire"
+                               : ro ? "mrec_emb_bwd_apply_rec"
+                                    : g_occ ? "mrec_emb_bwd_apply_given" : "mrec_emb_bwd_apply")) !=
+      MREC_OK)
+    return st;
   MREC_CHECK_ARG(mode != MREC_BWD_DENSE_GRAD || grad != nullptr || ro != nullptr,
                  "DENSE_GRAD needs grad");
   if (ro) {
@@ -1067,7 +1082,6 @@ static mrec_status apply_impl(const mrec_table_bank *bank, int64_t batch, const 
   // hash layout (batch <= kHashMaxKeys or an exchange view, see mrec_emb_bwd_plan):
   // sample-major blocks + one hot-segment block per (table, bucket); sorted
   // layout: one block per WPB segments of each table
-  const bool hash = hash_layout(batch, g_occ != nullptr || gw != nullptr);  // given: an exchange view
   const int seg_blocks = hash ? (batch > 0 ? F * kPlanBuckets : 0)
                               : static_cast<int>((batch + wpb - 1) / wpb);
   const int64_t sm_blocks = hash ? (batch * F + wpb - 1) / wpb : 0;

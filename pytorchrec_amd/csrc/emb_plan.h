@@ -20,8 +20,7 @@ struct TableWs {  // per-table workspace view of the sorted layout
 // layout 1 (hash plan, batch <= MREC_BWD_HASH_MAX_BATCH or a padded exchange view):
 //   per (table, bucket) descriptors of the rows hit more than once, and the
 //   sample-major lookup table lut[b][f] (below, BucketWs / lookup_table).
-constexpr int kLayoutSorted = 0;
-constexpr int kLayoutHash = 1;
+// (kLayoutSorted / kLayoutHash: common.h)
 
 __host__ __device__ inline int64_t pad4(int64_t x) { return (x + 3) & ~int64_t(3); }
 
@@ -298,7 +297,7 @@ __device__ __forceinline__ void plan_hash_body(const BankArgs &bank, const IdsAr
     t.hdr[0] = static_cast<int32_t>(s_tot >> 16);
     t.hdr[1] = static_cast<int32_t>(s_tot & 0xffffu);
     t.hdr[2] = static_cast<int32_t>(s_long);
-    t.hdr[3] = kLayoutHash;
+    t.hdr[3] = ws_layout_tag(kLayoutHash, B);
     if (r == 0) table_offsets(ws, F, B)[f] = bank.row_offset[f];
     if (d_step && f == 0 && r == 0) *d_step += 1;
   }

@@ -31,18 +31,23 @@ __device__ __forceinline__ void feed_copy_body_u(const FeedCopy &fc, int b, long
   __syncthreads();
   const long long rec = *s_rec;
   if (rec >= 0 && rec < fc.n_records) {
-    const uint4 *src = reinterpret_cast<const uint4 *>(fc.src + rec * fc.record_bytes);
+    // the clang vector type, not HIP's uint4 struct: an array of the struct stayed a
+    // stack object (ScratchSize 528 B/lane at U = 32, every value through scratch);
+    // the vector array is promoted to registers (U loads in flight, no scratch)
+    typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+    const u32x4 *src = reinterpret_cast<const u32x4 *>(fc.src + rec * fc.record_bytes);
+    u32x4 *dst = reinterpret_cast<u32x4 *>(fc.dst);
     const int64_t n16 = fc.record_bytes / 16;
     const int64_t stride = static_cast<int64_t>(fc.blocks) * THREADS;
     int64_t i = static_cast<int64_t>(b) * THREADS + threadIdx.x;
     for (; i + (U - 1) * stride < n16; i += U * stride) {
-      uint4 v[U];
+      u32x4 v[U];
 #pragma unroll
       for (int u = 0; u < U; ++u) v[u] = src[i + u * stride];
 #pragma unroll
-      for (int u = 0; u < U; ++u) fc.dst[i + u * stride] = v[u];
+      for (int u = 0; u < U; ++u) dst[i + u * stride] = v[u];
     }
-    for (; i < n16; i += stride) fc.dst[i] = src[i];
+    for (; i < n16; i += stride) dst[i] = src[i];
   }
   __syncthreads();  // every thread of this workgroup has read the cursor
   if (threadIdx.x == 0) {

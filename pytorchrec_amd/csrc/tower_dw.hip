@@ -69,7 +69,12 @@ struct DwArgs {
 };
 
 // One wave per workgroup, one 64 x 64 output tile (4 x 4 MFMA tiles) per wave.
-template <int PF, bool KC>
+// FEED: the launch also hosts the batch feed's copy (mrec_tower_dw_ex with a feed
+// job).  Only that instantiation carries the copy body: its 32 loads in flight per
+// lane cost 39 VGPRs, which every wave of the launch would reserve (164 -> 203
+// VGPRs + 90 AGPRs: 2 -> 1 waves/SIMD; C3's ~980 dW tiles ran 19.5 -> 24.8 us
+// without any feed job).
+template <int PF, bool KC, bool FEED>
 __global__ __launch_bounds__(64) void tower_dw_kernel(DwArgs a, KClock kc) {
   KcScope<KC> kc_scope(kc);
   __shared__ __attribute__((aligned(16))) float tile[64 * 68];  // epilogue transpose
@@ -78,9 +83,11 @@ __global__ __launch_bounds__(64) void tower_dw_kernel(DwArgs a, KClock kc) {
       ctr_head_finish_body<64>(a.fin, blockIdx.x, reinterpret_cast<float (*)[9]>(tile));
     return;
   }
-  if (static_cast<int>(blockIdx.x) < a.fin_blocks + a.feed.blocks) {  // uniform
-    feed_copy_body<64>(a.feed, blockIdx.x - a.fin_blocks, reinterpret_cast<long long *>(tile));
-    return;
+  if constexpr (FEED) {
+    if (static_cast<int>(blockIdx.x) < a.fin_blocks + a.feed.blocks) {  // uniform
+      feed_copy_body<64>(a.feed, blockIdx.x - a.fin_blocks, reinterpret_cast<long long *>(tile));
+      return;
+    }
   }
   const int b = blockIdx.x - a.fin_blocks - a.feed.blocks;
   int l = 0;
@@ -294,12 +301,19 @@ mrec_status mrec_tower_dw_ex(const mrec_tower_dw_args *p, const mrec_head_finish
   const int grid = a.fin_blocks + a.feed.blocks + blocks;
   if (grid == 0) return MREC_OK;
   const KClock kc = kclock_take();
-  if (kc.buf)
-    tower_dw_kernel<DW_PF, true><<<dim3(static_cast<unsigned>(grid)), 64, 0,
-                                   static_cast<hipStream_t>(stream)>>>(a, kc);
-  else
-    tower_dw_kernel<DW_PF, false><<<dim3(static_cast<unsigned>(grid)), 64, 0,
-                                    static_cast<hipStream_t>(stream)>>>(a, kc);
+  const dim3 g(static_cast<unsigned>(grid));
+  hipStream_t st = static_cast<hipStream_t>(stream);
+  if (a.feed.blocks > 0) {
+    if (kc.buf)
+      tower_dw_kernel<DW_PF, true, true><<<g, 64, 0, st>>>(a, kc);
+    else
+      tower_dw_kernel<DW_PF, false, true><<<g, 64, 0, st>>>(a, kc);
+  } else {
+    if (kc.buf)
+      tower_dw_kernel<DW_PF, true, false><<<g, 64, 0, st>>>(a, kc);
+    else
+      tower_dw_kernel<DW_PF, false, false><<<g, 64, 0, st>>>(a, kc);
+  }
   return launch_status("mrec_tower_dw");
 }
 

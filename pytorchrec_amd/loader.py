@@ -315,15 +315,20 @@ class ColumnarLoader:
         jobs = [_mrec.FeedJob(self._slots[(j + self.depth - 1) % self.depth].data_ptr(),
                               host.data_ptr(), self.layout.slot_bytes, host.shape[0],
                               state.data_ptr()) for j in range(self.depth)]
-        with torch.cuda.graph(g, capture_error_mode="thread_local"):
-            for j in range(self.depth):
-                dense_ops.set_feed_job(jobs[j])
-                step(self.layout.views(self._slots[j], self.batch_size))
-                left = dense_ops.take_feed_job()
-                if left is not None:  # no tower weight-gradient launch in this step
-                    _mrec.call("mrec_batch_stage_cursor", left.dst, left.host_base,
-                               left.record_bytes, left.n_records, left.d_state,
-                               _mrec.stream_handle(self.device))
+        try:
+            with torch.cuda.graph(g, capture_error_mode="thread_local"):
+                for j in range(self.depth):
+                    dense_ops.set_feed_job(jobs[j])
+                    step(self.layout.views(self._slots[j], self.batch_size))
+                    left = dense_ops.take_feed_job()
+                    if left is not None:  # no tower weight-gradient launch in this step
+                        _mrec.call("mrec_batch_stage_cursor", left.dst, left.host_base,
+                                   left.record_bytes, left.n_records, left.d_state,
+                                   _mrec.stream_handle(self.device))
+        finally:
+            # a step that raised mid-capture leaves its job set: the next eager
+            # tower_dw would take it and copy through this (freed) cursor
+            dense_ops.take_feed_job()
         return GraphEpoch(self, g, state, host, jobs)
 
     def __iter__(self) -> Iterator[Dict[str, Tensor]]:

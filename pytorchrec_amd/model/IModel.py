@@ -139,11 +139,15 @@ class IModel(Module, IWithArguments, ABC):
         a sharded bank, never the whole bank).  Every rank calls it."""
         from pytorchrec_amd import checkpoint
         saved = getattr(self, "_last_saved", None)
-        if saved is not None and saved[1] == self._weights_version:
+        if (saved is not None and saved[1] == self._weights_version
+                and checkpoint.has_sharded_banks(self)):  # unsharded: the reference's copy
             snap = saved[0] + ".best"
-            checkpoint.link_snapshot(self, saved[0], snap)
-            self.best_state_dict = {"__mrec_best_file__": snap}
-            return
+            try:
+                checkpoint.link_snapshot(self, saved[0], snap)
+                self.best_state_dict = {"__mrec_best_file__": snap}
+                return
+            except OSError:  # no hard links here (or across devices): the host copy below
+                pass
         self.best_state_dict = copy.deepcopy(tensor_to_device(self.state_dict(), torch.device("cpu")))
 
     def load_best_weights(self):

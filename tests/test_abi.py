@@ -91,6 +91,29 @@ def test_invalid_arguments_return_einval(lib):
     assert b"NULL" in lib.mrec_last_error()
 
 
+def test_apply_refuses_a_workspace_no_plan_was_issued_into(lib):
+    """ABI 28 layout rule (mrec.h, above mrec_emb_bwd_plan): every embedding-backward
+    apply checks the layout its workspace's last plan recorded, on the host, before
+    any launch -- here no plan was ever issued into that address, so each apply entry
+    refuses with MREC_EINVAL (the GPU suite covers the padded-plan / plain-apply
+    mismatch, test_plan_body_instantiations_match_standalone)."""
+    from pytorchrec_amd import _mrec
+    rows = (ctypes.c_int64 * 1)(100)
+    offs = (ctypes.c_int64 * 1)(0)
+    bank = _mrec.TableBank(64, offs, rows, 1, 16, 32, 1, _mrec.BF16)
+    ws_addr, B = 1 << 20, 100
+    wsb = lib.mrec_emb_bwd_workspace_size(1, B)
+    st = lib.mrec_emb_bwd_apply(ctypes.byref(bank), B, ws_addr, wsb, None, _mrec.F32, 0, None,
+                                None, None, _mrec.F32, 0, None, _mrec.BWD_SGD, 0.1, 0, None, None,
+                                None)
+    assert st == _mrec.EINVAL
+    assert b"no embedding-backward plan" in lib.mrec_last_error()
+    st = lib.mrec_emb_bwd_apply_wire(ctypes.byref(bank), B, ws_addr, wsb, 256, 36, _mrec.BF16, 512,
+                                     8, 1, 1, _mrec.BWD_SGD, 0.1, 0, None, None, 0, None, None)
+    assert st == _mrec.EINVAL
+    assert b"mrec_emb_bwd_apply_wire" in lib.mrec_last_error()
+
+
 def test_product_path_has_no_cpu_fallback_for_gpu_tensors():
     """The HIP ops raise MrecUnavailable (never fall back) when the library is gone."""
     from pytorchrec_amd import _mrec

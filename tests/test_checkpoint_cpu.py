@@ -25,12 +25,21 @@ DIM = 8
 
 
 class _LocalComm:
-    """A ShardComm stand-in for (world, rank) with no-op collectives."""
+    """A ShardComm stand-in for (world, rank) with no-op collectives -- except that
+    the ranks of one simulated save (saved one after another, rank 0 first) share
+    rank 0's contribution to a 3-element all-reduce, as the save id's sum would."""
+
+    _rank0_sum = None
 
     def __init__(self, world, rank):
         self.world, self.rank, self.group, self.force = world, rank, None, False
 
     def allreduce_sum_(self, t):
+        if t.numel() == 3:
+            if self.rank == 0:
+                _LocalComm._rank0_sum = t.clone()
+            else:
+                t.copy_(_LocalComm._rank0_sum)
         return t
 
 
@@ -84,8 +93,8 @@ def test_sharded_checkpoint_reshards_bitwise(dtype):
         path = os.path.join(d, "ckpt.pt")
         src = _save_world(path, 4, dtype, tables)
         files = sorted(os.listdir(d))
-        assert files == sorted(["ckpt.pt"] + [f"ckpt.pt.embeddings.weight.r{r}of4.npy"
-                                              for r in range(4)]), files
+        assert files == sorted(["ckpt.pt"] + [f"ckpt.pt.embeddings.weight.r{r}of4.npy{x}"
+                                              for r in range(4) for x in ("", ".id")]), files
         state = torch.load(path, map_location="cpu", weights_only=True)
         assert "embeddings.weight" not in state and checkpoint.INDEX_KEY in state
         # the dense entries are saved under their unsharded keys
@@ -135,15 +144,14 @@ def test_unsharded_state_dict_loads_into_sharded_and_best_weights_link():
             m = _model(3, r, seed=99)
             m.load_weights(path, torch.device("cpu"))
             _check_rows(m, tables, 3, r)
-        # save_best_weights right after a save: hard links, unchanged by a later save
+        # save_best_weights of an unsharded model: the reference's host copy
+        # (IModel.py:314-315), no file
         u.save_best_weights()
-        best = path + ".best"
-        assert os.path.samefile(best, path)
+        assert not os.path.exists(path + ".best")
         with torch.no_grad():
             u.embeddings.weight.add_(1.0)
         u._weights_version += 1
         u.save_weights(path)
-        assert not os.path.samefile(best, path)
         u.compiled_device = torch.device("cpu")
         u.load_best_weights()
         _check_rows(u, tables, 1, 0)
@@ -163,3 +171,33 @@ def test_unsharded_state_dict_loads_into_sharded_and_best_weights_link():
         assert not any(n.startswith("sh.pt.embeddings") for n in os.listdir(d))
         assert np.all([os.path.exists(os.path.join(d, f"sh.pt.best.embeddings.weight.r{r}of2.npy"))
                        for r in range(2)])
+
+
+def test_sharded_checkpoint_with_a_shard_of_another_save_is_refused():
+    """a crash between the shards' renames and the index leaves a new
+    index beside shard files of the previous save (same shapes).  The save id in the
+    index and beside every shard makes the load raise instead of mixing two steps."""
+    import shutil
+    from pytorchrec_amd import checkpoint
+    tables = _global_tables(torch.float32)
+    with tempfile.TemporaryDirectory() as d:
+        path = os.path.join(d, "c.pt")
+        _save_world(path, 2, torch.float32, tables)
+        old = checkpoint.shard_file(path, "embeddings.weight", 1, 2)
+        shutil.copy(old, old + ".prev")
+        shutil.copy(checkpoint.id_file(old), old + ".prev.id")
+        newer = [t + 1 for t in tables]
+        _save_world(path, 2, torch.float32, newer)
+        state = torch.load(path, map_location="cpu", weights_only=True)
+        ids = {meta["save_id"] for meta in state[checkpoint.INDEX_KEY].values()}
+        assert len(ids) == 1
+        m = _model(2, 1, seed=5)
+        checkpoint.load_into(m, state, path)
+        _check_rows(m, newer, 2, 1)
+        os.replace(old + ".prev", old)  # rank 1 "crashed" before its rename
+        os.replace(old + ".prev.id", checkpoint.id_file(old))
+        with pytest.raises(RuntimeError, match="another save"):
+            checkpoint.load_into(_model(2, 1, seed=5), state, path)
+        os.remove(checkpoint.id_file(old))  # or before it wrote its id
+        with pytest.raises(RuntimeError, match="another save"):
+            checkpoint.load_into(_model(2, 1, seed=5), state, path)

@@ -650,6 +650,17 @@ def test_plan_body_instantiations_match_standalone(gpu, threads, slots):
                 _mrec.call("mrec_emb_bwd_plan", bank.desc().ref(), idd.ref(), B, ws.data_ptr(), wsb,
                            oob.data_ptr(), None, _mrec.stream_handle())
             grad = torch.zeros_like(bank.weight)
+            if padded and B > 4096:
+                # r5b: a padded plan past 4096 entries wrote the hash layout; the plain
+                # apply would read it as the sorted one (silently wrong gradients in r05).
+                # ABI 28 refuses the pair before launching anything (mrec.h layout rule).
+                with pytest.raises(_mrec.MrecError, match="layout mismatch"):
+                    _mrec.call("mrec_emb_bwd_apply", bank.desc().ref(), B, ws.data_ptr(), wsb,
+                               dy.data_ptr(), _mrec.F32, dy.stride(0), None, None, None,
+                               _mrec.F32, 0, None, _mrec.BWD_DENSE_GRAD, 0.0, 0, None,
+                               grad.data_ptr(), _mrec.stream_handle())
+                torch.cuda.synchronize()
+                assert not grad.any(), "a refused apply must not launch"
             if padded:  # an exchange view's apply: the per-entry gradients given (fp32 [B, 16])
                 _mrec.call("mrec_emb_bwd_apply_given", bank.desc().ref(), B, ws.data_ptr(), wsb,
                            None, _mrec.F32, 0, None, None, None, _mrec.F32, 0, None, g_occ.data_ptr(),

@@ -739,28 +739,52 @@ PMC_FILE = os.path.join(PROFILES, "pmc_traffic.json")
 CEIL_FILE = os.path.join(PROFILES, "ceilings.json")
 
 
+def pmc_workload(args):
+    """The workload key a PMC stamp must match (tools/pmc_traffic.py writes the same)."""
+    return {"model": args.model, "batch": args.batch, "rows_per_table": args.rows_per_table,
+            "zipf": float(args.zipf or 0.0), "shard": bool(args.shard or args.gpus > 1),
+            "exchange": args.exchange if (args.shard or args.gpus > 1) else None}
+
+
+def lib_digest():
+    """The source digest libmrec.so was built from (pytorchrec_amd/build.py stamp)."""
+    try:
+        with open(os.path.join(ROOT, "pytorchrec_amd", "lib", "libmrec.so.sha256")) as fh:
+            return fh.read().strip()
+    except OSError:
+        return None
+
+
 def pmc_traffic(kernels, args):
     """HBM bytes per launch summed over ``kernels`` from the committed PMC passes
     (tools/gpu_pmc.sh: rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE in separate runs of
-    this bench, corrected by the calibration tools/pmc_traffic.py applies), with the
-    run they came from.  rocprof cannot count the run it is printed by, so the
-    stamp names the profiled run; the traffic is only reported when that run had
-    this workload (same model, batch, rows per table).  Returns (bytes | None, stamp)."""
+    this bench, corrected by the calibration tools/pmc_traffic.py applies).  rocprof
+    cannot count the run it is printed by, so a stamp names its profiled run: the
+    traffic is reported only when that run had THIS workload (model, batch, rows per
+    table, Zipf alpha, sharding / exchange) AND this library (the source digest of
+    libmrec.so, i.e. the same kernels); otherwise ``traffic`` is null and the source
+    says why.  Returns (bytes | None, source)."""
+    src = {"file": "profiles/pmc_traffic.json"}
     try:
         with open(PMC_FILE) as fh:
             pmc = json.load(fh)
-        want = {"model": args.model, "batch": args.batch, "rows_per_table": args.rows_per_table}
-        runs = [r for r in pmc.get("runs", [pmc.get("run", {})])
-                if all(r.get(k) == v for k, v in want.items())]
-        if not runs:
-            return None, {"file": "profiles/pmc_traffic.json", "no_run_for": want}
-        run = runs[0]
-        per = pmc["kernels"][args.model]
-        return int(sum(per[k]["hbm_bytes_per_launch"] for k in kernels)), {
-            "file": "profiles/pmc_traffic.json", "run": run,
-            "correction": pmc.get("correction")}
-    except (OSError, KeyError, ValueError, TypeError):
-        return None, None
+    except (OSError, ValueError):
+        return None, dict(src, missing=True)
+    want, lib = pmc_workload(args), lib_digest()
+    runs = [r for r in pmc.get("runs", []) if r.get("workload") == want]
+    if not runs:
+        return None, dict(src, no_run_for=want)
+    run = runs[-1]
+    if run.get("lib") != lib:
+        return None, dict(src, stale={"stamped_lib": run.get("lib"), "this_lib": lib,
+                                      "stamped_commit": run.get("commit")})
+    try:
+        per = run["kernels"]
+        nbytes = int(sum(per[k]["hbm_bytes_per_launch"] for k in kernels))
+    except (KeyError, TypeError):
+        return None, dict(src, missing_kernels=[k for k in kernels if k not in run.get("kernels", {})])
+    return nbytes, dict(src, run={k: run[k] for k in ("workload", "commit", "lib", "utc")},
+                        kernels={k: per[k] for k in kernels}, correction=pmc.get("correction"))
 
 
 def attainable():
@@ -1147,6 +1171,8 @@ def main():
                    "hip_graph": not args.no_graph,
                    "steps_per_graph": G if graphs is not None else 0},
     }
+    # what a PMC pass of this run stamps (tools/pmc_traffic.py reads it from the line)
+    result["stamp"] = {"lib": lib_digest(), "workload": pmc_workload(args)}
     if rank == 0 and not args.no_roofline and args.model in ("deepfm", "dcnv2"):
         result.update(embedding_roofline(model, step, datas, args,
                                          in_step=graphs is not None and not sharded))

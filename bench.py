@@ -320,7 +320,8 @@ def time_launches(fn, reps=100):
     return e0.elapsed_time(e1) / reps * 1e-3  # seconds per launch
 
 
-def instep_kernel_times(step, datas, names, steps=4, replays=30, strip_coreduce=False):
+def instep_kernel_times(step, datas, names, steps=4, replays=30, strip_coreduce=False,
+                        comm=None):
     """Device time of every launch of the named libmrec entry points INSIDE the
     graph-replayed training step: ``steps`` train steps (batch i % len(datas)) are
     captured in one HIP graph with the kernel clock on (mrec_kernel_clock: clocked
@@ -340,7 +341,10 @@ def instep_kernel_times(step, datas, names, steps=4, replays=30, strip_coreduce=
     clock does not see follows it) reports its span as its in-step time.
     ``strip_coreduce``: the deferred MLP weight-gradient reductions do
     not ride in the embedding apply (they run as their own launch at the end of
-    the backward) -- the apply's CoReduce share is the difference.
+    the backward) -- the apply's CoReduce share is the difference.  ``comm``: the
+    row-sharded step's communicator -- its collectives (RCCL all-to-all /
+    all-reduce) count as calls, so a launch followed by one reports its own waves'
+    span and the collective's time stays out of every launch's share.
 
     Returns ({name: median in-step seconds}, {name: median span seconds},
     median seconds from the first clocked start to the last clocked end / steps)."""
@@ -367,6 +371,20 @@ def instep_kernel_times(step, datas, names, steps=4, replays=30, strip_coreduce=
         return r
 
     _mrec.call = spy
+    wrapped = []
+    if comm is not None:
+        for meth in ("exchange", "allreduce_sum_", "allreduce_mean_"):
+            orig = getattr(comm, meth, None)
+            if orig is None:
+                continue
+
+            def counted(*a, _o=orig, **k):
+                r = _o(*a, **k)
+                if capturing[0]:
+                    calls[0] += 1
+                return r
+            setattr(comm, meth, counted)
+            wrapped.append(meth)
     if strip_coreduce:
         D.take_pending = lambda n=0: []
     try:
@@ -388,6 +406,8 @@ def instep_kernel_times(step, datas, names, steps=4, replays=30, strip_coreduce=
             lib.mrec_kernel_clock(None, 0)
     finally:
         _mrec.call, D.take_pending = real_call, real_take
+        for meth in wrapped:
+            delattr(comm, meth)  # (the instance attribute shadowed the method)
     share = {n: [] for n in names}
     span = {n: [] for n in names}
     unclocked = set()
@@ -567,6 +587,62 @@ def embedding_roofline(model, step, datas, args, in_step=True):
         out["roofline"]["frac_of_attainable"] = round(out["roofline"]["achieved"] / att["GB/s"], 4)
     out["roofline_kernels"] = rk
     return out
+
+
+SHARD_EMB = ("mrec_shard_bucketize_dedup_ex", "mrec_shard_gather_wire_ex",
+             "mrec_shard_wire_unpack_ex", "mrec_interact_fwd_ex", "mrec_emb_bwd_apply_rec",
+             "mrec_emb_bwd_apply_wire")
+
+
+def sharded_roofline(model, step, datas, args):
+    """The row-sharded (compact exchange) line's ``roofline``, IN-STEP: the same
+    SURVEY.md §8(d) algorithmic bytes as the unsharded step (the exchange adds no
+    algorithmic bytes: it only moves the same rows between ranks) over the summed
+    in-step time of every embedding-path launch of the step -- the sender's
+    bucketize / dedup, the owner's record gather (+ its backward plan), the sender's
+    unpack, the interaction (+ the sender's plan), the sender's gradient sums into
+    records and the owner's apply -- each timed by its clocked instantiation inside
+    the graph-replayed step (mrec_kernel_clock); the RCCL collectives are counted as
+    calls, so no launch's share includes one.  The collectives' own time is the
+    step's remainder (``collectives_us``)."""
+    D = model.embeddings.dim
+    first_order = bool(model.embeddings.has_w)
+    es = model.embeddings.weight.element_size()
+    F = model.embeddings.n_tables
+    alg_fwd, alg_bwd = alg_bytes_per_sample(F, D, CRITEO_DENSE, first_order, es)
+    nbytes = (alg_fwd + alg_bwd) * args.batch
+    names = SHARD_EMB + TOWER_PAIR + ("mrec_sgd_multi",)
+    t, t_span, clocked_step = instep_kernel_times(step, datas, names, comm=model.embeddings.comm)
+    emb = [k for k in SHARD_EMB if k in t]
+    t_emb = sum(t[k] for k in emb)
+    ach = nbytes / t_emb / 1e9
+    traffic, tsrc = pmc_traffic(sorted({KERNEL_OF[k] for k in emb if k in KERNEL_OF}), args)
+    out = {"roofline": {
+        "bound": "hbm", "kernel": "row-sharded embedding path: " + " + ".join(emb),
+        "achieved": round(ach, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+        "frac": round(ach / HBM_PEAK_GBS, 4), "traffic": traffic, "traffic_source": tsrc,
+        "avg_us": round(t_emb * 1e6, 3), "bytes_per_launch": nbytes,
+        "bytes_rule": "SURVEY.md §8(d) algorithmic bytes per sample x batch (the exchange "
+                      "adds none)",
+        "timing": "in-step: the kernels' own clock inside the graph-replayed train steps "
+                  "(each launch's first wave start to the next libmrec launch's; a launch "
+                  "followed by a collective: its own waves' span); median over 4 steps x 30 "
+                  "replays",
+        "clocked_step_us": round(clocked_step * 1e6, 3) if clocked_step else None}}
+    if clocked_step:
+        out["roofline"]["collectives_us"] = round((clocked_step - sum(t.values())) * 1e6, 3)
+    out["roofline_kernels"] = {k: {"avg_us": round(t[k] * 1e6, 3), "timing": "in-step",
+                                   "wave_span_us": round(t_span[k] * 1e6, 3)} for k in t}
+    return out
+
+
+# bench entry point -> the PMC stamp's kernel key (tools/pmc_traffic.py KERNELS)
+KERNEL_OF = {"mrec_shard_bucketize_dedup_ex": "mrec_shard_bucketize_dedup",
+             "mrec_shard_gather_wire_ex": "mrec_shard_gather_wire",
+             "mrec_shard_wire_unpack_ex": "mrec_shard_wire_move",
+             "mrec_interact_fwd_ex": "mrec_interact_fwd_ex",
+             "mrec_emb_bwd_apply_rec": "mrec_emb_bwd_apply",
+             "mrec_emb_bwd_apply_wire": "mrec_emb_bwd_apply"}
 
 
 def tower_cross_phases(step, data, B, L):
@@ -1173,7 +1249,10 @@ def main():
     }
     # what a PMC pass of this run stamps (tools/pmc_traffic.py reads it from the line)
     result["stamp"] = {"lib": lib_digest(), "workload": pmc_workload(args)}
-    if rank == 0 and not args.no_roofline and args.model in ("deepfm", "dcnv2"):
+    if (rank == 0 and not args.no_roofline and args.model == "deepfm" and sharded
+            and graphs is not None and model.embeddings.use_compact(args.batch)):
+        result.update(sharded_roofline(model, step, datas, args))
+    elif rank == 0 and not args.no_roofline and args.model in ("deepfm", "dcnv2"):
         result.update(embedding_roofline(model, step, datas, args,
                                          in_step=graphs is not None and not sharded))
     if rank == 0 and not args.no_roofline and args.model == "din":

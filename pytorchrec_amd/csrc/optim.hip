@@ -33,7 +33,9 @@ struct SgdArgs {
 
 // one 32x32 tile of one job per workgroup: w -= lr * g, images from the new w
 // (the transposed image goes through an LDS tile so both writes are coalesced)
-__global__ __launch_bounds__(256) void sgd_multi_kernel(SgdArgs a) {
+template <bool KC>
+__global__ __launch_bounds__(256) void sgd_multi_kernel(SgdArgs a, KClock kc) {
+  KcScope<KC> kc_scope(kc);
   __shared__ float tile[kTile][kTile + 1];
   int j = 0;
   while (j + 1 < a.n && static_cast<int>(blockIdx.x) >= a.job[j + 1].first) ++j;  // uniform
@@ -115,8 +117,13 @@ mrec_status mrec_sgd_multi(int32_t n, const mrec_sgd_job *jobs, mrec_stream stre
     ++a.n;
   }
   if (total == 0) return MREC_OK;
-  sgd_multi_kernel<<<dim3(static_cast<unsigned>(total)), 256, 0,
-                     static_cast<hipStream_t>(stream)>>>(a);
+  const KClock kc = kclock_take();
+  if (kc.buf)
+    sgd_multi_kernel<true><<<dim3(static_cast<unsigned>(total)), 256, 0,
+                             static_cast<hipStream_t>(stream)>>>(a, kc);
+  else
+    sgd_multi_kernel<false><<<dim3(static_cast<unsigned>(total)), 256, 0,
+                              static_cast<hipStream_t>(stream)>>>(a, kc);
   return launch_status("mrec_sgd_multi");
 }
 

@@ -163,13 +163,15 @@ __device__ __forceinline__ uint32_t id_hash(uint32_t x, uint32_t mask) {
 // samples (grid y): chunk c of the batch is its own "sub-sender", part d * C + c of
 // send_ids (owner d's C parts contiguous, so the equal-split all-to-all still moves
 // W parts of C * P); an id repeated across chunks takes a slot in each.
+template <bool KC>
 __global__ __launch_bounds__(kBT) void bucketize_dedup_kernel(IdsArgs ids, RowsArg rows, int64_t Btot,
                                                               int W, int cap, int F, int hs,
                                                               int32_t *__restrict__ send_ids,
                                                               int32_t *__restrict__ pos,
                                                               int32_t *__restrict__ overflow,
                                                               int32_t *__restrict__ oob, int C,
-                                                              int64_t cb) {
+                                                              int64_t cb, KClock kc) {
+  KcScope<KC> kc_scope(kc);  // (clocked instantiation: bench.py in-step times)
   __shared__ uint32_t hist[kBHist];
   __shared__ uint32_t wtot[kBWaves];
   extern __shared__ uint32_t hash_lds[];  // keys [hs] | (first << 16 | slot) [hs]
@@ -345,12 +347,13 @@ __device__ __forceinline__ int wire_table(const int *pre, int F, int r) {
 // that run the owner's backward hash plan over the same received ids, PLAN).  ADAM:
 // a lazily updated Adam bank's rows go out as of the current step (adam_current on
 // the 16-B chunk holding the dword, as mrec_shard_gather does for the slot rows).
-template <bool PLAN, typename T = uint16_t, bool ADAM = false>
+template <bool PLAN, typename T = uint16_t, bool ADAM = false, bool KC = false>
 __global__ __launch_bounds__(kWireThreads) void gather_wire_kernel(BankArgs bank, WireArgs w,
                                                                    const int32_t *__restrict__ recv,
                                                                    uint32_t *__restrict__ wire,
                                                                    int chunks, PlanJob plan,
-                                                                   int plan_blocks) {
+                                                                   int plan_blocks, KClock kc) {
+  KcScope<KC> kc_scope(kc);
   if constexpr (PLAN) {
     if (static_cast<int>(blockIdx.x) < plan_blocks) {  // uniform: (table, bucket) plans
       __shared__ __attribute__((aligned(16))) uint32_t smem[2 * kHashSlots + 2];
@@ -441,13 +444,14 @@ __global__ __launch_bounds__(kWireThreads) void gather_wire_kernel(BankArgs bank
 // widened to fp32: dwords of fp32 = 2 x record elements), and zero the first
 // zero_dw dwords of the same row of `zero` when given; pack (elements = record x
 // rec_dw): the slot row's first rec_dw dwords into the record.  Grid: chunks x W.
-template <bool UNPACK, bool TO_F32>
+template <bool UNPACK, bool TO_F32, bool KC = false>
 __global__ __launch_bounds__(kWireThreads) void wire_move_kernel(WireArgs w,
                                                                  uint32_t *__restrict__ wire,
                                                                  uint32_t *__restrict__ slots,
                                                                  int slot_dw,
                                                                  uint32_t *__restrict__ zero,
-                                                                 int zero_dw) {
+                                                                 int zero_dw, KClock kc) {
+  KcScope<KC> kc_scope(kc);
   __shared__ int pre[MREC_MAX_TABLES + 1];
   const int p = blockIdx.y;
   const int tot = wire_prefix(w, p, pre);
@@ -748,16 +752,25 @@ mrec_status mrec_shard_bucketize_dedup_ex(const mrec_ids *ids, int32_t n_tables,
   while (hs < 2 * cb) hs *= 2;  // load factor <= 1/2
   const size_t lds = static_cast<size_t>(hs) * 8;
   static int attr = [] {
-    (void)hipFuncSetAttribute(reinterpret_cast<const void *>(bucketize_dedup_kernel),
+    (void)hipFuncSetAttribute(reinterpret_cast<const void *>(bucketize_dedup_kernel<false>),
+                              hipFuncAttributeMaxDynamicSharedMemorySize, 16384 * 8);
+    (void)hipFuncSetAttribute(reinterpret_cast<const void *>(bucketize_dedup_kernel<true>),
                               hipFuncAttributeMaxDynamicSharedMemorySize, 16384 * 8);
     (void)hipGetLastError();
     return 1;
   }();
   (void)attr;
-  bucketize_dedup_kernel<<<dim3(n_tables, static_cast<unsigned>(C)), kBT, lds,
-                           static_cast<hipStream_t>(stream)>>>(
-      ia, ra, batch, world, cap, n_tables, hs, send_ids, pos, d_overflow, d_oob_flag,
-      static_cast<int>(C), cb);
+  const KClock kc = kclock_take();
+  const dim3 grid(n_tables, static_cast<unsigned>(C));
+  hipStream_t s = static_cast<hipStream_t>(stream);
+  if (kc.buf)
+    bucketize_dedup_kernel<true><<<grid, kBT, lds, s>>>(ia, ra, batch, world, cap, n_tables, hs,
+                                                        send_ids, pos, d_overflow, d_oob_flag,
+                                                        static_cast<int>(C), cb, kc);
+  else
+    bucketize_dedup_kernel<false><<<grid, kBT, lds, s>>>(ia, ra, batch, world, cap, n_tables, hs,
+                                                         send_ids, pos, d_overflow, d_oob_flag,
+                                                         static_cast<int>(C), cb, kc);
   return launch_status("mrec_shard_bucketize_dedup");
 }
 
@@ -833,7 +846,16 @@ mrec_status mrec_shard_gather_wire_ex(const mrec_table_bank *local, const int32_
   const dim3 gf(static_cast<unsigned>(pb + chunks * world));
   hipStream_t s = static_cast<hipStream_t>(stream);
   uint32_t *wd = static_cast<uint32_t *>(wire);
-#define MREC_GW(P, T, A) gather_wire_kernel<P, T, A><<<gf, kWireThreads, 0, s>>>(ba, w, recv_ids, wd, chunks, job, pb)
+  const KClock kc = kclock_take();
+#define MREC_GW(P, T, A)                                                                          \
+  do {                                                                                            \
+    if (kc.buf)                                                                                   \
+      gather_wire_kernel<P, T, A, true><<<gf, kWireThreads, 0, s>>>(ba, w, recv_ids, wd, chunks,  \
+                                                                    job, pb, kc);                 \
+    else                                                                                          \
+      gather_wire_kernel<P, T, A, false><<<gf, kWireThreads, 0, s>>>(ba, w, recv_ids, wd, chunks, \
+                                                                     job, pb, kc);                \
+  } while (0)
   if (!ba.adam.kind) {
     if (plan)
       MREC_GW(true, uint16_t, false);
@@ -882,12 +904,14 @@ mrec_status mrec_shard_wire_unpack_ex(const void *wire, int32_t rec_bytes, const
   const dim3 g = wire_grid(w, std::max(slot_dw, zero ? zero_dw : 0));
   hipStream_t s = static_cast<hipStream_t>(stream);
   uint32_t *wp = static_cast<uint32_t *>(const_cast<void *>(wire));
+  const KClock kc = to_f32 ? KClock{nullptr, 0} : kclock_take();  // (the slot exchange: unclocked)
+  uint32_t *sl = static_cast<uint32_t *>(slots), *zr = static_cast<uint32_t *>(zero);
   if (to_f32)
-    wire_move_kernel<true, true><<<g, kWireThreads, 0, s>>>(
-        w, wp, static_cast<uint32_t *>(slots), slot_dw, static_cast<uint32_t *>(zero), zero_dw);
+    wire_move_kernel<true, true><<<g, kWireThreads, 0, s>>>(w, wp, sl, slot_dw, zr, zero_dw, kc);
+  else if (kc.buf)
+    wire_move_kernel<true, false, true><<<g, kWireThreads, 0, s>>>(w, wp, sl, slot_dw, zr, zero_dw, kc);
   else
-    wire_move_kernel<true, false><<<g, kWireThreads, 0, s>>>(
-        w, wp, static_cast<uint32_t *>(slots), slot_dw, static_cast<uint32_t *>(zero), zero_dw);
+    wire_move_kernel<true, false><<<g, kWireThreads, 0, s>>>(w, wp, sl, slot_dw, zr, zero_dw, kc);
   return launch_status("mrec_shard_wire_unpack");
 }
 
@@ -903,7 +927,7 @@ mrec_status mrec_shard_wire_pack(const void *slots, int64_t slot_bytes, int32_t 
   wire_move_kernel<false, false><<<wire_grid(w, w.rec_dw), kWireThreads, 0,
                                    static_cast<hipStream_t>(stream)>>>(
       w, static_cast<uint32_t *>(wire), static_cast<uint32_t *>(const_cast<void *>(slots)),
-      static_cast<int>(slot_bytes / 4), nullptr, 0);
+      static_cast<int>(slot_bytes / 4), nullptr, 0, KClock{nullptr, 0});
   return launch_status("mrec_shard_wire_pack");
 }
 

@@ -269,6 +269,38 @@ mrec_status mrec_interact_fwd_ex(const mrec_table_bank *bank, const mrec_ids *id
                                  mrec_stream stream);
 
 /*
+ * The compact exchange's received rows as wire records (ABI 28): record
+ * p * cap_rows + pref[p][f] + j answers slot (p * n_tables + f) * cap + j of the ids
+ * message `hdr` (parts x (n_tables * cap + n_tables) int32, the per-table counts
+ * last; pref[p][f] = the running sum of part p's counts of the tables before f).
+ */
+typedef struct {
+  const void *wire;     /* [parts][cap_rows] records of rec_bytes (4-B multiple, bf16 row + w) */
+  int32_t rec_bytes;
+  const int32_t *hdr;   /* the ids message the sender sent (mrec_shard_bucketize_dedup) */
+  int32_t parts, cap, cap_rows;
+  int32_t *pref;        /* out, nullable: [parts][n_tables] prefixes (mrec_emb_bwd_apply_rec) */
+  int32_t *d_overflow;  /* nullable: bit 1 set when a part's counts exceed cap_rows */
+} mrec_wire_rows;
+
+/*
+ * mrec_interact_fwd_ex over the compact exchange's received records without the
+ * unpack launch: `bank` is the sender's slot rows (every table = the whole
+ * parts x n_tables x cap slot range, row offset 0; bf16, 64-B rows) and `ids` the
+ * lookups' slots (mrec_shard_bucketize_dedup pos).  Each lookup's row is read from its
+ * record and also written into its slot row -- the bytes mrec_shard_wire_unpack_ex
+ * writes there (the record, zeros past it), which the sender's backward reads -- and
+ * the launch writes the parts' prefixes to rows->pref.  Same outputs as
+ * mrec_shard_wire_unpack_ex followed by mrec_interact_fwd_ex.  (ABI 28)
+ */
+mrec_status mrec_interact_fwd_rec(const mrec_table_bank *bank, const mrec_ids *ids, int64_t batch,
+                                  const float *dense, int32_t n_dense, int64_t dense_ld,
+                                  const float *dense_w, const float *bias, int32_t flags, void *x0,
+                                  mrec_dtype x0_dtype, int64_t x0_ld, int32_t x0_cols, float *logit,
+                                  float *fm_sum, int32_t *d_oob_flag, const mrec_plan_job *plan,
+                                  const mrec_wire_rows *rows, mrec_stream stream);
+
+/*
  * Gradient sources of lookup (b, f) (each may be NULL = 0):
  *   g_v[d] = dx[b, f*dim + d]                                (dx: F32/BF16, row stride dx_ld)
  *          + dfm[b] * (fm_sum[b, d] - v[b, f*dim + d])      (FM2 backward; v read from x0)

@@ -139,6 +139,13 @@ class GradRecords(ctypes.Structure):
                 ("cap", ctypes.c_int32), ("cap_rows", ctypes.c_int32)]
 
 
+class WireRows(ctypes.Structure):
+    """mrec_wire_rows (include/mrec.h, ABI 28)."""
+    _fields_ = [("wire", ctypes.c_void_p), ("rec_bytes", ctypes.c_int32), ("hdr", ctypes.c_void_p),
+                ("parts", ctypes.c_int32), ("cap", ctypes.c_int32), ("cap_rows", ctypes.c_int32),
+                ("pref", ctypes.c_void_p), ("d_overflow", ctypes.c_void_p)]
+
+
 class HeadFinishJob(ctypes.Structure):
     _fields_ = [("part", ctypes.c_void_p), ("ldp", ctypes.c_int64), ("batch", ctypes.c_int64),
                 ("H", ctypes.c_int32), ("ns", ctypes.c_int32), ("g", ctypes.c_void_p),
@@ -239,6 +246,9 @@ SIGNATURES = {
     "mrec_interact_fwd_ex": (ctypes.c_int, [_bank_p, _ids_p, _i64, _vp, _i32, _i64, _vp, _vp, _i32,
                                             _vp, ctypes.c_int, _i64, _i32, _vp, _vp, _vp,
                                             ctypes.POINTER(PlanJob), _vp]),
+    "mrec_interact_fwd_rec": (ctypes.c_int, [_bank_p, _ids_p, _i64, _vp, _i32, _i64, _vp, _vp, _i32,
+                                             _vp, ctypes.c_int, _i64, _i32, _vp, _vp, _vp,
+                                             ctypes.POINTER(PlanJob), ctypes.POINTER(WireRows), _vp]),
     "mrec_fm2_fwd": (ctypes.c_int, [_vp, _i64, _i32, _i32, _vp, _vp]),
     "mrec_fm2_bwd": (ctypes.c_int, [_vp, _vp, _i64, _i32, _i32, _vp, _vp]),
     "mrec_emb_bwd_workspace_size": (ctypes.c_size_t, [_i32, _i64]),

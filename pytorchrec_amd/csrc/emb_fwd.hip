@@ -80,6 +80,12 @@ struct InteractArgs {
   float *logit;
   float *fm_sum;
   int32_t *oob;
+  // REC (mrec_interact_fwd_rec): rows from the compact exchange's wire records
+  const uint32_t *rec_wire;  // [parts][cap_rows] records of rec_dw dwords
+  const int32_t *rec_hdr;    // the ids message they answer: parts x (F * cap + F), counts last
+  int rec_dw, rec_cap, rec_cap_rows, rec_parts;
+  int32_t *rec_pref;         // out (nullable): [parts][F] table prefixes
+  int32_t *rec_overflow;     // nullable: bit 1 = a part holds more than cap_rows records
 };
 
 #ifdef MREC_INTERACT_PROF
@@ -99,10 +105,17 @@ __device__ uint64_t g_interact_prof[8192][5];
   } while (0)
 #endif
 
-// sample b, by the wave whose lane this is
-template <typename T, int LPR, bool X0_BF16, bool ADAM>
+// sample b, by the wave whose lane this is.  REC: the bank is the sender's slot rows
+// [(p * F + f) * cap + j] (ids = those slots), which are NOT filled yet: each row comes
+// from its wire record p * cap_rows + pref[p][f] + j (s_pref: the parts' table
+// prefixes in LDS) by dword loads (records are 4-B aligned), and is also written into
+// its slot row -- the bytes mrec_shard_wire_unpack_ex would have written there (the
+// record, zeros past it), which the sender's backward reads -- so the unpack launch
+// is gone.  Lookups of one slot store the same bytes.
+template <typename T, int LPR, bool X0_BF16, bool ADAM, bool REC = false>
 __device__ __forceinline__ void interact_sample(const BankArgs &bank, const IdsArgs &ids,
-                                                const InteractArgs &ia, int64_t b, int lane) {
+                                                const InteractArgs &ia, int64_t b, int lane,
+                                                const int32_t *s_pref = nullptr) {
   constexpr int EPL = Vec<T>::EPL;
   constexpr int WPW = 64 / LPR;                             // rows per wave-instruction
   constexpr int MAXIT = (MREC_MAX_TABLES + WPW - 1) / WPW;  // field iterations
@@ -175,9 +188,29 @@ __device__ __forceinline__ void interact_sample(const BankArgs &bank, const IdsA
     okv[it] = false;
     if (it * WPW >= F) continue;  // uniform
     okv[it] = it * WPW + worker < F && idv[it] >= 0 && idv[it] < frows[it];
-    const int64_t grow = okv[it] ? foff[it] + idv[it] : 0;
-    raw[it] = *reinterpret_cast<const uint4 *>(reinterpret_cast<const T *>(bank.data) +
-                                               grow * static_cast<int64_t>(bank.row_stride) + e0);
+    if constexpr (REC) {
+      // slot s of table fc -> its record; dwords 4 l .. 4 l + 3 of the row (past the
+      // record: zeros), every load from a clamped index, masked below
+      const int fc = min(it * WPW + worker, F - 1);
+      const uint32_t sl = okv[it] ? static_cast<uint32_t>(idv[it]) : 0u;
+      const uint32_t fcap = static_cast<uint32_t>(F) * static_cast<uint32_t>(ia.rec_cap);
+      const uint32_t pp = sl / fcap;
+      const int32_t j = static_cast<int32_t>(sl - (pp * F + fc) * static_cast<uint32_t>(ia.rec_cap));
+      const int32_t r = s_pref[pp * F + fc] + j;
+      okv[it] = okv[it] && j >= 0 && j < ia.rec_cap && r < ia.rec_cap_rows;
+      const uint32_t *src = ia.rec_wire + (static_cast<int64_t>(pp) * ia.rec_cap_rows + (okv[it] ? r : 0)) *
+                                              ia.rec_dw;
+      uint32_t w4[4];
+#pragma unroll
+      for (int k = 0; k < 4; ++k) w4[k] = src[min(4 * l + k, ia.rec_dw - 1)];
+#pragma unroll
+      for (int k = 0; k < 4; ++k) w4[k] = 4 * l + k < ia.rec_dw ? w4[k] : 0u;
+      raw[it] = make_uint4(w4[0], w4[1], w4[2], w4[3]);
+    } else {
+      const int64_t grow = okv[it] ? foff[it] + idv[it] : 0;
+      raw[it] = *reinterpret_cast<const uint4 *>(reinterpret_cast<const T *>(bank.data) +
+                                                 grow * static_cast<int64_t>(bank.row_stride) + e0);
+    }
   }
 #pragma unroll
   for (int it = 0; it < MAXIT; ++it) {
@@ -189,6 +222,15 @@ __device__ __forceinline__ void interact_sample(const BankArgs &bank, const IdsA
     } else if constexpr (ADAM) {  // a lazily updated Adam bank: the row as of the last step
       raw[it] = adam_current<T>(bank, foff[it] + idv[it], e0, live_elems(bank, e0, EPL), raw[it],
                                 *bank.adam.d_t);
+    }
+  }
+  if constexpr (REC) {  // the slot rows the backward reads (the unpack's bytes)
+#pragma unroll
+    for (int it = 0; it < MAXIT; ++it) {
+      if (it * WPW >= F) continue;  // uniform
+      if (okv[it])
+        *reinterpret_cast<uint4 *>(reinterpret_cast<T *>(bank.data) +
+                                   idv[it] * static_cast<int64_t>(bank.row_stride) + e0) = raw[it];
     }
   }
 
@@ -329,6 +371,52 @@ __global__ __launch_bounds__(1024) void interact_plan_kernel(BankArgs bank, IdsA
   const int64_t b = static_cast<int64_t>(blockIdx.x - plan_blocks) * 16 + (threadIdx.x >> 6);
   if (b >= B) return;
   interact_sample<T, LPR, X0_BF16, ADAM>(bank, ids, ia, b, threadIdx.x & 63);
+}
+
+// the same launch over the compact exchange's wire records (interact_sample REC):
+// every sample workgroup first builds the parts' table prefixes in LDS (the running
+// sums of the counts the ids message carries, as the unpack did); the first one also
+// writes them out for the sender's gradient records (mrec_emb_bwd_apply_rec)
+template <typename T, int LPR, bool X0_BF16, bool KC>
+__global__ __launch_bounds__(1024) void interact_rec_kernel(BankArgs bank, IdsArgs ids, int64_t B,
+                                                            InteractArgs ia, PlanJob plan,
+                                                            int plan_blocks, KClock kc) {
+  __shared__ __attribute__((aligned(16))) uint32_t smem[2 * kHashSlots + 2];
+  KcScope<KC> kc_scope(kc);
+  if (static_cast<int>(blockIdx.x) < plan_blocks) {  // uniform: (table, bucket) plans
+    plan_hash_body<1024, kHashSlots>(plan.bank, plan.ids, plan.B, plan.ws, plan.oob, plan.d_step,
+                                     blockIdx.x / kPlanBuckets, blockIdx.x % kPlanBuckets, smem);
+    return;
+  }
+  const int F = bank.n_tables;
+  int32_t *s_pref = reinterpret_cast<int32_t *>(smem);  // [parts][F] (host: parts * F <= 8192)
+  {
+    // one thread per part: its F counts loaded together, then summed in table order
+    const int p = threadIdx.x;
+    if (p < ia.rec_parts) {
+      const int32_t *h = ia.rec_hdr + static_cast<int64_t>(p) * (static_cast<int64_t>(F) * ia.rec_cap + F) +
+                         static_cast<int64_t>(F) * ia.rec_cap;
+      int32_t c[MREC_MAX_TABLES];
+#pragma unroll
+      for (int f = 0; f < MREC_MAX_TABLES; ++f) c[f] = h[min(f, F - 1)];
+      int32_t run = 0;
+#pragma unroll
+      for (int f = 0; f < MREC_MAX_TABLES; ++f) {
+        if (f < F) {
+          s_pref[p * F + f] = run;
+          run += c[f];
+        }
+      }
+      const bool first = static_cast<int>(blockIdx.x) == plan_blocks;
+      if (first && ia.rec_pref)
+        for (int f = 0; f < F; ++f) ia.rec_pref[p * F + f] = s_pref[p * F + f];
+      if (first && run > ia.rec_cap_rows && ia.rec_overflow) atomicOr(ia.rec_overflow, 2);
+    }
+  }
+  __syncthreads();
+  const int64_t b = static_cast<int64_t>(blockIdx.x - plan_blocks) * 16 + (threadIdx.x >> 6);
+  if (b >= B) return;
+  interact_sample<T, LPR, X0_BF16, false, true>(bank, ids, ia, b, threadIdx.x & 63, s_pref);
 }
 
 // ---------------------------------------------------------------------------
@@ -488,6 +576,17 @@ mrec_status mrec_interact_fwd_ex(const mrec_table_bank *bank, const mrec_ids *id
                                  mrec_dtype x0_dtype, int64_t x0_ld, int32_t x0_cols, float *logit,
                                  float *fm_sum, int32_t *d_oob_flag, const mrec_plan_job *plan,
                                  mrec_stream stream) {
+  return mrec_interact_fwd_rec(bank, ids, batch, dense, n_dense, dense_ld, dense_w, bias, flags,
+                               x0, x0_dtype, x0_ld, x0_cols, logit, fm_sum, d_oob_flag, plan,
+                               nullptr, stream);
+}
+
+mrec_status mrec_interact_fwd_rec(const mrec_table_bank *bank, const mrec_ids *ids, int64_t batch,
+                                  const float *dense, int32_t n_dense, int64_t dense_ld,
+                                  const float *dense_w, const float *bias, int32_t flags, void *x0,
+                                  mrec_dtype x0_dtype, int64_t x0_ld, int32_t x0_cols, float *logit,
+                                  float *fm_sum, int32_t *d_oob_flag, const mrec_plan_job *plan,
+                                  const mrec_wire_rows *rec, mrec_stream stream) {
   BankArgs ba;
   IdsArgs ia;
   int eb, lpr;
@@ -518,9 +617,65 @@ mrec_status mrec_interact_fwd_ex(const mrec_table_bank *bank, const mrec_ids *id
   if (batch == 0) return MREC_OK;
   hipStream_t s = static_cast<hipStream_t>(stream);
   const bool xb16 = x0 && x0_dtype == MREC_BF16;
-  const InteractArgs args{dense, n_dense, dense_ld, dense_w, bias,   flags,
-                          x0,    x0_ld,   x0_cols,  logit,   fm_sum, d_oob_flag};
+  InteractArgs args{};
+  args.dense = dense;
+  args.n_dense = n_dense;
+  args.dense_ld = dense_ld;
+  args.dense_w = dense_w;
+  args.bias = bias;
+  args.flags = flags;
+  args.x0v = x0;
+  args.x0_ld = x0_ld;
+  args.x0_cols = x0_cols;
+  args.logit = logit;
+  args.fm_sum = fm_sum;
+  args.oob = d_oob_flag;
   const PlanJob *pp = plan ? &pj : nullptr;
+  if (rec) {
+    MREC_CHECK_ARG(bank->dtype == MREC_BF16 && lpr == 4 && !ba.adam.kind,
+                   "records: bf16 slot rows of 64 B, no Adam catch-up (else unpack them)");
+    MREC_CHECK_ARG(rec->wire && rec->hdr, "records: NULL wire / hdr");
+    MREC_CHECK_ARG(rec->rec_bytes >= 4 && rec->rec_bytes % 4 == 0 &&
+                       rec->rec_bytes <= ba.row_stride * eb &&
+                       (reinterpret_cast<uintptr_t>(rec->wire) & 3) == 0,
+                   "records: 4-B multiple no wider than a slot row, 4-B aligned wire");
+    MREC_CHECK_ARG(rec->parts >= 1 && rec->cap >= 1 && rec->cap_rows >= 1 &&
+                       static_cast<int64_t>(rec->parts) * ba.n_tables <= 8192 &&
+                       rec->parts <= 1024,
+                   "records: parts in [1, 1024], parts * n_tables <= 8192, cap / cap_rows >= 1");
+    for (int f = 0; f < ba.n_tables; ++f)
+      MREC_CHECK_ARG(ba.row_offset[f] == 0 &&
+                         ba.rows[f] == static_cast<int64_t>(rec->parts) * ba.n_tables * rec->cap,
+                     "records: the bank must be the slot rows (every table = all parts x tables x cap)");
+    args.rec_wire = static_cast<const uint32_t *>(rec->wire);
+    args.rec_hdr = rec->hdr;
+    args.rec_dw = rec->rec_bytes / 4;
+    args.rec_cap = rec->cap;
+    args.rec_cap_rows = rec->cap_rows;
+    args.rec_parts = rec->parts;
+    args.rec_pref = rec->pref;
+    args.rec_overflow = rec->d_overflow;
+    const int pb = pp ? pp->bank.n_tables * kPlanBuckets : 0;
+    const dim3 grid(static_cast<unsigned>(pb + (batch + 15) / 16));
+    const KClock kc = kclock_take();
+    PlanJob none{};
+    const PlanJob &job = pp ? *pp : none;
+#define MREC_IRK(XB)                                                                          \
+  do {                                                                                        \
+    if (kc.buf)                                                                               \
+      interact_rec_kernel<uint16_t, 4, XB, true><<<grid, 1024, 0, s>>>(ba, ia, batch, args,   \
+                                                                      job, pb, kc);           \
+    else                                                                                      \
+      interact_rec_kernel<uint16_t, 4, XB, false><<<grid, 1024, 0, s>>>(ba, ia, batch, args,  \
+                                                                       job, pb, kc);          \
+  } while (0)
+    if (xb16)
+      MREC_IRK(true);
+    else
+      MREC_IRK(false);
+#undef MREC_IRK
+    return launch_status("mrec_interact_fwd_rec");
+  }
   if (bank->dtype == MREC_BF16) {
     if (xb16)
       launch_interact<uint16_t, true>(lpr, ba, ia, batch, args, pp, s);

@@ -689,12 +689,23 @@ def owner_plan_job(bank: ShardedEmbeddingBank, recv_ids: torch.Tensor, part: int
     return job, (ws, wsb), (desc, idd, recv_ids)
 
 
+def records_direct(bank: ShardedEmbeddingBank) -> bool:
+    """Whether the interaction reads the received records itself
+    (mrec_interact_fwd_rec: bf16 64-B slot rows; a lazy-Adam bank's rows were caught
+    up by the owner's gather) instead of after an unpack launch; MREC_SHARD_UNPACK=1
+    forces the unpack (A/B)."""
+    return (bank.weight.dtype == torch.bfloat16 and bank.row_stride * 2 == 64
+            and os.environ.get("MREC_SHARD_UNPACK") != "1")
+
+
 def shard_interact(bank: ShardedEmbeddingBank, rows_recv: torch.Tensor, pos: torch.Tensor,
                    dense, dense_w, bias, fm2: bool, first_order: bool, x0_cols: int, x0_dtype,
-                   plan_job=None):
+                   plan_job=None, rec=None):
     """Sender: mrec_interact_fwd over the received rows (ids = slots) ->
     (x0 or None, logit, fm_sum or None).  ``plan_job`` (owner_plan_job) runs the
-    owner's backward plan in leading workgroups of the same launch."""
+    owner's backward plan in leading workgroups of the same launch.  ``rec``: a
+    WireRows -- the rows come from the received records (mrec_interact_fwd_rec),
+    which the same launch also writes into ``rows_recv`` (the unpack's bytes)."""
     B = pos.shape[1]
     dev = bank.weight.device
     rdesc = remote_desc(bank, rows_recv)
@@ -705,14 +716,16 @@ def shard_interact(bank: ShardedEmbeddingBank, rows_recv: torch.Tensor, pos: tor
     fm_sum = torch.empty(B, bank.dim, dtype=torch.float32, device=dev) if fm2 else None
     fl = bank.flags()
     if B:
-        _mrec.call("mrec_interact_fwd_ex", rdesc.ref(),
-                   _mrec.IdsDesc([pos[f] for f in range(bank.n_tables)]).ref(), B,
-                   _mrec.ptr(dense), n_dense, dense.stride(0) if dense is not None else 0,
-                   _mrec.ptr(dense_w), _mrec.ptr(bias), flags, _mrec.ptr(x0),
-                   _mrec.dtype_code(x0_dtype), x0.stride(0) if x0 is not None else 0,
-                   int(x0_cols), logit.data_ptr(), _mrec.ptr(fm_sum), fl.data_ptr() + 4,
-                   ctypes.byref(plan_job) if plan_job is not None else None,
-                   _mrec.stream_handle())
+        args = (rdesc.ref(), _mrec.IdsDesc([pos[f] for f in range(bank.n_tables)]).ref(), B,
+                _mrec.ptr(dense), n_dense, dense.stride(0) if dense is not None else 0,
+                _mrec.ptr(dense_w), _mrec.ptr(bias), flags, _mrec.ptr(x0),
+                _mrec.dtype_code(x0_dtype), x0.stride(0) if x0 is not None else 0,
+                int(x0_cols), logit.data_ptr(), _mrec.ptr(fm_sum), fl.data_ptr() + 4,
+                ctypes.byref(plan_job) if plan_job is not None else None)
+        if rec is not None:
+            _mrec.call("mrec_interact_fwd_rec", *args, ctypes.byref(rec), _mrec.stream_handle())
+        else:
+            _mrec.call("mrec_interact_fwd_ex", *args, _mrec.stream_handle())
     return x0, logit, fm_sum
 
 
@@ -893,11 +906,19 @@ class _CompactInteractFn(torch.autograd.Function):
         # directly (sender_grad_records); else sums into zeroed slot rows + a pack
         spref = torch.empty(P, bank.n_tables, dtype=torch.int32, device=dev) if fuse else None
         gsum = torch.empty_like(rows_recv) if train and not fuse else None
-        shard_wire_unpack(bank, wire, send, rows_recv, zero=gsum, parts=P, pref=spref)
+        # the interaction reads the records itself (and leaves the unpack's slot rows
+        # behind for the backward) unless a zeroed sum buffer is needed too
+        direct = gsum is None and records_direct(bank) and P * bank.n_tables <= 8192
+        rec = None
+        if direct:
+            rec = _mrec.WireRows(wire.data_ptr(), bank.wire_bytes(), send.data_ptr(), P, bank.cap,
+                                 bank.cap_rows, _mrec.ptr(spref), bank.flags().data_ptr())
+        else:
+            shard_wire_unpack(bank, wire, send, rows_recv, zero=gsum, parts=P, pref=spref)
         job, splan, keep = (sender_plan_job(bank, rows_recv, pos) if fuse
                             else (None, None, None))
         x0, logit, fm_sum = shard_interact(bank, rows_recv, pos, dense, dense_w, bias, fm2,
-                                           first_order, x0_cols, x0_dtype, plan_job=job)
+                                           first_order, x0_cols, x0_dtype, plan_job=job, rec=rec)
         del keep
         splans = [(0, B, splan)] if fuse else None
         if train and not fuse:

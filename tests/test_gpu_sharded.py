@@ -427,6 +427,7 @@ def test_compact_exchange_simulated_bit_exact(gpu, W, zipf, B, big):
     each chunk's slot sums == the dense gradient of that chunk alone, and the owner's
     sum runs over (rank, chunk) in that order.
     Per-rank bytes on the wire are checked against the slot exchange."""
+    from pytorchrec_amd import _mrec
     from pytorchrec_amd import embedding as E
     from pytorchrec_amd import sharding as S
     glob = _global_bank(gpu)
@@ -471,6 +472,24 @@ def test_compact_exchange_simulated_bit_exact(gpu, W, zipf, B, big):
         outs.append(S.shard_interact(banks[r], rr, poss[r], dense[r], dense_w, bias, True, True,
                                      x0_cols, torch.bfloat16, plan_job=job))
         del keep
+        if fuse and S.records_direct(banks[r]):
+            # ABI 28: the interaction over the received records itself (no unpack) --
+            # same outputs, the same slot rows left behind, the same part prefixes
+            rr2 = torch.empty_like(rr)
+            sp2 = torch.full((P, F), -7, dtype=torch.int32, device=gpu)
+            rec = _mrec.WireRows(wires[r].data_ptr(), banks[r].wire_bytes(), sends[r].data_ptr(), P,
+                                 banks[r].cap, banks[r].cap_rows, sp2.data_ptr(),
+                                 banks[r].flags().data_ptr())
+            job2, _, keep2 = S.sender_plan_job(banks[r], rr2, poss[r])
+            out2 = S.shard_interact(banks[r], rr2, poss[r], dense[r], dense_w, bias, True, True,
+                                    x0_cols, torch.bfloat16, plan_job=job2, rec=rec)
+            del keep2
+            for a_, b_ in zip(out2, outs[-1]):
+                assert torch.equal(a_, b_), r
+            looked = poss[r].reshape(-1).long()
+            looked = looked[looked >= 0]
+            assert torch.equal(rr2[looked].view(torch.int16), rr[looked].view(torch.int16)), r
+            assert torch.equal(sp2, sprefs[r]), r
         plans.append([(0, B, sp)] if fuse else S.sender_plans(banks[r], rr, poss[r]))
         large = not S.owner_view_fits_hash(banks[r], P)  # W * cap entries past one plan
         assert large or not big

@@ -590,8 +590,8 @@ def embedding_roofline(model, step, datas, args, in_step=True):
 
 
 SHARD_EMB = ("mrec_shard_bucketize_dedup_ex", "mrec_shard_gather_wire_ex",
-             "mrec_shard_wire_unpack_ex", "mrec_interact_fwd_ex", "mrec_emb_bwd_apply_rec",
-             "mrec_emb_bwd_apply_wire")
+             "mrec_shard_wire_unpack_ex", "mrec_interact_fwd_ex", "mrec_interact_fwd_rec",
+             "mrec_emb_bwd_apply_rec", "mrec_emb_bwd_apply_wire")
 
 
 def sharded_roofline(model, step, datas, args):
@@ -641,6 +641,7 @@ KERNEL_OF = {"mrec_shard_bucketize_dedup_ex": "mrec_shard_bucketize_dedup",
              "mrec_shard_gather_wire_ex": "mrec_shard_gather_wire",
              "mrec_shard_wire_unpack_ex": "mrec_shard_wire_move",
              "mrec_interact_fwd_ex": "mrec_interact_fwd_ex",
+             "mrec_interact_fwd_rec": "mrec_interact_fwd_ex",
              "mrec_emb_bwd_apply_rec": "mrec_emb_bwd_apply",
              "mrec_emb_bwd_apply_wire": "mrec_emb_bwd_apply"}
 

@@ -391,26 +391,27 @@ __global__ __launch_bounds__(1024) void interact_rec_kernel(BankArgs bank, IdsAr
   const int F = bank.n_tables;
   int32_t *s_pref = reinterpret_cast<int32_t *>(smem);  // [parts][F] (host: parts * F <= 8192)
   {
-    // one thread per part: its F counts loaded together, then summed in table order
-    const int p = threadIdx.x;
-    if (p < ia.rec_parts) {
+    // one wave per part (lane = table, F <= 64): the counts by one load per lane, the
+    // exclusive prefix by a shuffle scan (a per-thread array of 64 counts cost 64
+    // VGPRs: 6 instead of 8 waves per SIMD, half the workgroups resident)
+    const int lane = threadIdx.x & 63;
+    const bool first = static_cast<int>(blockIdx.x) == plan_blocks;
+    for (int p = threadIdx.x >> 6; p < ia.rec_parts; p += 16) {
       const int32_t *h = ia.rec_hdr + static_cast<int64_t>(p) * (static_cast<int64_t>(F) * ia.rec_cap + F) +
                          static_cast<int64_t>(F) * ia.rec_cap;
-      int32_t c[MREC_MAX_TABLES];
+      const int32_t c = lane < F ? h[lane] : 0;
+      int32_t incl = c;
 #pragma unroll
-      for (int f = 0; f < MREC_MAX_TABLES; ++f) c[f] = h[min(f, F - 1)];
-      int32_t run = 0;
-#pragma unroll
-      for (int f = 0; f < MREC_MAX_TABLES; ++f) {
-        if (f < F) {
-          s_pref[p * F + f] = run;
-          run += c[f];
-        }
+      for (int off = 1; off < 64; off <<= 1) {
+        const int32_t t = __shfl_up(incl, off);
+        if (lane >= off) incl += t;
       }
-      const bool first = static_cast<int>(blockIdx.x) == plan_blocks;
-      if (first && ia.rec_pref)
-        for (int f = 0; f < F; ++f) ia.rec_pref[p * F + f] = s_pref[p * F + f];
-      if (first && run > ia.rec_cap_rows && ia.rec_overflow) atomicOr(ia.rec_overflow, 2);
+      if (lane < F) {
+        s_pref[p * F + lane] = incl - c;
+        if (first && ia.rec_pref) ia.rec_pref[p * F + lane] = incl - c;
+      }
+      if (first && lane == 63 && incl > ia.rec_cap_rows && ia.rec_overflow)
+        atomicOr(ia.rec_overflow, 2);
     }
   }
   __syncthreads();

@@ -34,7 +34,8 @@ import sys
 # substring of the kernel name -> bench.py roofline key (first match wins)
 KERNELS = {"din_att_bwd": "mrec_din_att_bwd", "din_att_fwd": "mrec_din_att_fwd",
            "bk_apply_kernel": "mrec_emb_bwd_large_fused",
-           "interact_plan_kernel": "mrec_interact_fwd_ex", "interact_kernel": "mrec_interact_fwd",
+           "interact_plan_kernel": "mrec_interact_fwd_ex", "interact_rec_kernel": "mrec_interact_fwd_ex",
+           "interact_kernel": "mrec_interact_fwd",
            "plan_hash_kernel": "mrec_emb_bwd_plan", "apply_hash_kernel": "mrec_emb_bwd_apply",
            "apply_kernel": "mrec_emb_bwd_apply", "tower_dw_kernel": "mrec_tower_dw_ex",
            "tower_kernel": "mrec_tower_fwd_bwd", "gemm_dma_kernel": "mrec_gemm",
@@ -46,7 +47,7 @@ KERNELS = {"din_att_bwd": "mrec_din_att_bwd", "din_att_fwd": "mrec_din_att_fwd",
 # the kernel clock's instantiations (template flag KC = true, the last template
 # argument; wire_move<true, true> is the slot exchange's fp32 unpack, not clocked and
 # not on the compact path) run only in bench.py's in-step timing graphs
-_CLOCKED = re.compile(r"(interact_plan_kernel|apply_hash_kernel|tower_kernel|tower_dw_kernel|"
+_CLOCKED = re.compile(r"(interact_plan_kernel|interact_rec_kernel|apply_hash_kernel|tower_kernel|tower_dw_kernel|"
                       r"bucketize_dedup_kernel|gather_wire_kernel|wire_move_kernel|sgd_multi_kernel)<[^()]*true>\(")
 
 

@@ -390,20 +390,6 @@ __global__ __launch_bounds__(1024) void interact_rec_kernel(BankArgs bank, IdsAr
   }
   const int F = bank.n_tables;
   int32_t *s_pref = reinterpret_cast<int32_t *>(smem);  // [parts][F] (host: parts * F <= 8192)
-  // the wave's slots (pos) requested before the prefix phase: the barrier's fence waits
-  // for them together with the header (one round trip), interact_sample reads them
-  // again from the cache; the values are kept alive past the barrier by an empty use
-  int32_t pv[(MREC_MAX_TABLES + 15) / 16];
-  {
-    const int64_t bp = min(static_cast<int64_t>(blockIdx.x - plan_blocks) * 16 + (threadIdx.x >> 6),
-                           B - 1);
-    const int worker = (threadIdx.x & 63) / 4;
-#pragma unroll
-    for (int it = 0; it < (MREC_MAX_TABLES + 15) / 16; ++it)
-      pv[it] = ids.is64 || ids.chunk ? 0
-                                     : static_cast<const int32_t *>(ids.ptr[min(it * 16 + worker, F - 1)])
-                                           [bp * ids.stride];
-  }
   {
     // one wave per part (lane = table, F <= 64): the counts by one load per lane, the
     // exclusive prefix by a shuffle scan (a per-thread array of 64 counts cost 64
@@ -429,8 +415,6 @@ __global__ __launch_bounds__(1024) void interact_rec_kernel(BankArgs bank, IdsAr
     }
   }
   __syncthreads();
-#pragma unroll
-  for (int it = 0; it < (MREC_MAX_TABLES + 15) / 16; ++it) asm volatile("" ::"v"(pv[it]));
   const int64_t b = static_cast<int64_t>(blockIdx.x - plan_blocks) * 16 + (threadIdx.x >> 6);
   if (b >= B) return;
   interact_sample<T, LPR, X0_BF16, false, true>(bank, ids, ia, b, threadIdx.x & 63, s_pref);

@@ -503,14 +503,19 @@ __global__ __launch_bounds__(256, MREC_APPLY_WAVES) void apply_hash_kernel(BankA
 #endif
     const int f = blk / kPlanBuckets, r = blk - f * kPlanBuckets;
     const BucketWs t = bucket_ws(ws, f, r, B);
+    // the first pass's descriptor is loaded beside the header (unconditionally, from
+    // a clamped slot; used only when the header says it is a segment): one memory
+    // round trip less on the block's chain (header -> descriptor -> gradients -> row)
+    const int64_t scap = seg_cap(B);
+    const int4 dpre = t.desc[worker < scap ? worker : 0];
     const int nseg = t.hdr[0];
-    const int nl = t.hdr[2];
+    asm volatile("" ::"v"(dpre.x), "v"(dpre.y), "v"(dpre.z), "v"(dpre.w));  // (not sunk below)
     const int64_t toff_f = bank.row_offset[f];
     const int sshort = short_seg(LPR);
     for (int s0 = 0; s0 < nseg; s0 += WPB) {  // uniform
       const int s = s0 + worker;
       if (s < nseg) {
-        const int4 d = t.desc[s];
+        const int4 d = s0 == 0 ? dpre : t.desc[s];
         if (d.y <= sshort)
           apply_segment<T, LPR, MODE>(bank, a, t, f, toff_f, d, l, e0, v_lane, w_lane, live);
       }

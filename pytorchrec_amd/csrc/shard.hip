@@ -193,12 +193,37 @@ __global__ __launch_bounds__(kBT) void bucketize_dedup_kernel(IdsArgs ids, RowsA
   constexpr int kR = 8;
   int64_t idv[kR];
   load_ids_batch<kR>(ids, f, s0 + tid, kBT, s0 + B, -2, idv);
+#ifndef MREC_BKT_EXP
+#define MREC_BKT_EXP 0
+#endif
+#if MREC_BKT_EXP  // (diagnostics: phases skipped; the message left empty: no slot, no count)
+  auto diag_exit = [&](bool keep) {
+    if (keep) *oob = 7;
+    for (int r = 0; r < kR; ++r) {
+      const int64_t i = static_cast<int64_t>(r) * kBT + tid;
+      if (i < B) pos[f * Btot + s0 + i] = -1;
+    }
+    for (int d = 0; d < W; ++d) {
+      const int64_t pd = (static_cast<int64_t>(d) * C + c) * P;
+      for (int s = tid; s < cap; s += kBT) send_ids[pd + static_cast<int64_t>(f) * cap + s] = -1;
+      if (tid == 0) send_ids[pd + static_cast<int64_t>(F) * cap + f] = 0;
+    }
+  };
+#endif
+#if MREC_BKT_EXP == 1  // (diagnostic: the id loads only)
+  diag_exit(idv[0] == -12345 && idv[kR - 1] == -12345);
+  return;
+#endif
   for (int i = tid; i < nh; i += kBT) hist[i] = 0u;
   for (int i = tid; i < hs; i += kBT) {
     keys[i] = kEmpty;
     fs[i] = kEmpty;
   }
   __syncthreads();
+#if MREC_BKT_EXP == 2  // (diagnostic: + the LDS init)
+  diag_exit(idv[0] == -12345 && idv[kR - 1] == -12345 && keys[tid] == 5u);
+  return;
+#endif
   // 1. distinct ids: insert, keep the first sample index of each
   uint32_t hpos[kR];
 #pragma unroll
@@ -218,6 +243,10 @@ __global__ __launch_bounds__(kBT) void bucketize_dedup_kernel(IdsArgs ids, RowsA
     }
   }
   __syncthreads();
+#if MREC_BKT_EXP == 3  // (diagnostic: + the inserts)
+  diag_exit(hpos[0] == 12345u);
+  return;
+#endif
   // 2. stable per-owner ranks of the first lookups (owner W = no slot)
   uint32_t dv[kR];
 #pragma unroll
@@ -233,6 +262,10 @@ __global__ __launch_bounds__(kBT) void bucketize_dedup_kernel(IdsArgs ids, RowsA
   }
   __syncthreads();
   scan_2048(hist, nh, wtot);
+#if MREC_BKT_EXP == 4  // (diagnostic: + the ranks and the scan)
+  diag_exit(hist[tid] == 12345u);
+  return;
+#endif
 #pragma unroll
   for (int r = 0; r < kR; ++r) {
     if (r >= rounds) continue;

@@ -505,6 +505,18 @@ mrec_status mrec_emb_bwd_apply_wire(const mrec_table_bank *bank, int64_t batch,
                                     mrec_bwd_mode mode, float lr, uint64_t seed,
                                     const uint64_t *d_step, void *grad, int32_t n_reduce,
                                     const struct mrec_gemm_call_s *reduce, mrec_stream stream);
+/* mrec_emb_bwd_apply_wire plus the data-parallel dense SGD of an
+ * mrec_sgd_table_build table (device copy; sgd_blocks workgroups) in the same
+ * launch (ABI 28) */
+mrec_status mrec_emb_bwd_apply_wire_sgd(const mrec_table_bank *bank, int64_t batch,
+                                        const void *workspace, size_t ws_bytes, const void *wire,
+                                        int32_t rec_bytes, mrec_dtype wire_dtype,
+                                        const int32_t *pref, int32_t cap_rows, int64_t chunk,
+                                        int64_t chunk_stride, mrec_bwd_mode mode, float lr,
+                                        uint64_t seed, const uint64_t *d_step, void *grad,
+                                        int32_t n_reduce, const struct mrec_gemm_call_s *reduce,
+                                        const void *sgd_table, int32_t sgd_blocks,
+                                        mrec_stream stream);
 /* The sender's DENSE_GRAD sums written straight as wire RECORDS (ABI 26): the
  * bank is the slot rows the interaction read (ids = pos, slot s = (p * n_tables +
  * f) * cap + j); slot s's sum goes to record p * cap_rows + pref[p * n_tables + f]
@@ -875,6 +887,19 @@ typedef struct {
 } mrec_sgd_job;
 
 mrec_status mrec_sgd_multi(int32_t n, const mrec_sgd_job *jobs, mrec_stream stream);
+
+/*
+ * The same jobs as a table another launch runs (ABI 28): mrec_sgd_table_build
+ * validates them and writes the table (mrec_sgd_table_bytes() bytes, host memory)
+ * and its workgroup count; the caller copies it to a 16-B aligned device buffer once
+ * (it holds pointers and lr, not data) and passes that to
+ * mrec_emb_bwd_apply_wire_sgd, which runs the SGD tiles beside the owner's
+ * embedding update -- after the flat gradient's all-reduce, instead of a
+ * mrec_sgd_multi launch of its own.  Same arithmetic, same bits.
+ */
+size_t mrec_sgd_table_bytes(void);
+mrec_status mrec_sgd_table_build(int32_t n, const mrec_sgd_job *jobs, void *out, size_t out_bytes,
+                                 int32_t *blocks);
 
 /*
  * Fused MLP tower + CTR head + BCE loss, forward AND the input-gradient half of

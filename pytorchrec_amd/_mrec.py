@@ -274,6 +274,10 @@ SIGNATURES = {
                                                _vp, _i32, _i64, _i64, ctypes.c_int, _f32,
                                                ctypes.c_uint64, _vp, _vp, _i32,
                                                ctypes.POINTER(GemmCall), _vp]),
+    "mrec_emb_bwd_apply_wire_sgd": (ctypes.c_int, [_bank_p, _i64, _vp, ctypes.c_size_t, _vp, _i32,
+                                                   _i32, _vp, _i32, _i64, _i64, ctypes.c_int, _f32,
+                                                   ctypes.c_uint64, _vp, _vp, _i32,
+                                                   ctypes.POINTER(GemmCall), _vp, _i32, _vp]),
     "mrec_shard_bucketize": (ctypes.c_int, [_ids_p, _i32, ctypes.POINTER(ctypes.c_int64), _i64,
                                             _i32, _i32, _vp, _vp, _vp, _vp, _vp]),
     "mrec_shard_gather": (ctypes.c_int, [_bank_p, _vp, _i32, _i32, _vp, _vp]),
@@ -293,6 +297,9 @@ SIGNATURES = {
                                           ctypes.POINTER(HeadFinishJob), _vp]),
     "mrec_weight_prep": (ctypes.c_int, [_vp, _i64, _i64, _i64, _vp, _i64, _vp, _i64, _vp]),
     "mrec_sgd_multi": (ctypes.c_int, [_i32, ctypes.POINTER(SgdJob), _vp]),
+    "mrec_sgd_table_bytes": (ctypes.c_size_t, []),
+    "mrec_sgd_table_build": (ctypes.c_int, [_i32, ctypes.POINTER(SgdJob), _vp, ctypes.c_size_t,
+                                            ctypes.POINTER(ctypes.c_int32)]),
     "mrec_batch_stage": (ctypes.c_int, [_vp, _vp, _i64, _vp]),
     "mrec_batch_stage_cursor": (ctypes.c_int, [_vp, _vp, _i64, _i64, _vp, _vp]),
     "mrec_dcn_cross_bwd_prep": (ctypes.c_int, [_i64, _i64, _vp, _i64, _vp, _i64, _vp, _i64, _vp,

@@ -46,6 +46,10 @@ struct ApplyArgs {
   const int32_t *o_pref;
   int o_F, o_cap;
   int64_t o_cap_rows;
+  // data-parallel dense SGD tiles riding in this launch (ABI 28,
+  // mrec_emb_bwd_apply_wire_sgd): a device-resident SgdArgs (optim_common.h)
+  const struct SgdArgs *sgd;
+  int sgd_blocks;
 };
 
 // a given gradient from a wire record (4-B aligned rows: records are not 16-B).

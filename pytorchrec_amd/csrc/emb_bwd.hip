@@ -18,6 +18,7 @@
 #include "common.h"
 #include "emb_apply.h"
 #include "emb_plan.h"
+#include "optim_common.h"
 #include "gemm_common.h"
 
 namespace mrec {
@@ -475,13 +476,19 @@ __global__ __launch_bounds__(256, MREC_APPLY_WAVES) void apply_hash_kernel(BankA
     return;
   }
 #else
-  const int co_blocks = co.start[co.n];
-  if (static_cast<int>(blockIdx.x) < co_blocks) {  // uniform
+  const int co_blocks0 = co.start[co.n];
+  if (static_cast<int>(blockIdx.x) < co_blocks0) {  // uniform
 #if MREC_APPLY_EXP != 12
     co_reduce(co, blockIdx.x);
 #endif
     return;
   }
+  // the data-parallel dense SGD tiles (independent of the embedding update)
+  if (static_cast<int>(blockIdx.x) < co_blocks0 + a.sgd_blocks) {  // uniform
+    sgd_tile(*a.sgd, static_cast<int>(blockIdx.x) - co_blocks0);
+    return;
+  }
+  const int co_blocks = co_blocks0 + a.sgd_blocks;
 #endif
   if (a.d_step) a.seed += *a.d_step * 0x9e3779b97f4a7c15ull;
   constexpr int EPL = Vec<T>::EPL;
@@ -900,7 +907,8 @@ static mrec_status apply_impl(const mrec_table_bank *bank, int64_t batch, const 
                               int64_t chunk_stride, mrec_bwd_mode mode, float lr, uint64_t seed,
                               const uint64_t *d_step, void *grad, int32_t n_reduce,
                               const mrec_gemm_call *reduce, mrec_stream stream,
-                              const GivenWire *gw = nullptr, const RecOut *ro = nullptr);
+                              const GivenWire *gw = nullptr, const RecOut *ro = nullptr,
+                              const void *sgd_table = nullptr, int32_t sgd_blocks = 0);
 
 extern "C" {
 
@@ -973,6 +981,26 @@ mrec_status mrec_emb_bwd_apply_wire(const mrec_table_bank *bank, int64_t batch,
                     d_step, grad, n_reduce, reduce, stream, &gw);
 }
 
+mrec_status mrec_emb_bwd_apply_wire_sgd(const mrec_table_bank *bank, int64_t batch,
+                                        const void *workspace, size_t ws_bytes, const void *wire,
+                                        int32_t rec_bytes, mrec_dtype wire_dtype,
+                                        const int32_t *pref, int32_t cap_rows, int64_t chunk,
+                                        int64_t chunk_stride, mrec_bwd_mode mode, float lr,
+                                        uint64_t seed, const uint64_t *d_step, void *grad,
+                                        int32_t n_reduce, const mrec_gemm_call *reduce,
+                                        const void *sgd_table, int32_t sgd_blocks,
+                                        mrec_stream stream) {
+  MREC_CHECK_ARG(wire_dtype == MREC_BF16 || wire_dtype == MREC_F32, "wire dtype must be BF16/F32");
+  const int es = wire_dtype == MREC_BF16 ? 2 : 4;
+  MREC_CHECK_ARG(rec_bytes > 0 && rec_bytes % es == 0 && rec_bytes % 4 == 0, "bad record bytes");
+  MREC_CHECK_ARG(sgd_table == nullptr || (reinterpret_cast<uintptr_t>(sgd_table) & 15) == 0,
+                 "sgd table not 16-B aligned");
+  const GivenWire gw{wire, wire_dtype == MREC_BF16 ? 1 : 0, rec_bytes / es, pref, cap_rows};
+  return apply_impl(bank, batch, workspace, ws_bytes, nullptr, MREC_F32, 0, nullptr, nullptr,
+                    nullptr, MREC_F32, 0, nullptr, nullptr, 0, chunk, chunk_stride, mode, lr, seed,
+                    d_step, grad, n_reduce, reduce, stream, &gw, nullptr, sgd_table, sgd_blocks);
+}
+
 }  // extern "C"
 
 static mrec_status apply_impl(const mrec_table_bank *bank, int64_t batch, const void *workspace,
@@ -983,7 +1011,8 @@ static mrec_status apply_impl(const mrec_table_bank *bank, int64_t batch, const 
                               int64_t chunk_stride, mrec_bwd_mode mode, float lr, uint64_t seed,
                               const uint64_t *d_step, void *grad, int32_t n_reduce,
                               const mrec_gemm_call *reduce, mrec_stream stream,
-                              const GivenWire *gw, const RecOut *ro) {
+                              const GivenWire *gw, const RecOut *ro, const void *sgd_table,
+                              int32_t sgd_blocks) {
   BankArgs ba;
   int eb, lpr;
   mrec_status st = make_bank_args(bank, &ba, &eb, &lpr);
@@ -1050,7 +1079,7 @@ static mrec_status apply_impl(const mrec_table_bank *bank, int64_t batch, const 
                    "g_occ rows must be 16B aligned, g_ld >= dim + has_w, g_ld % 4 == 0");
     MREC_CHECK_ARG(chunk >= 0 && (chunk == 0 || chunk_stride >= F * chunk), "bad chunk");
   }
-  ApplyArgs a;
+  ApplyArgs a{};
   a.dx = dx;
   a.dx_ld = dx_ld;
   a.dx_bf16 = dx_dtype == MREC_BF16;
@@ -1082,6 +1111,10 @@ static mrec_status apply_impl(const mrec_table_bank *bank, int64_t batch, const 
   a.o_F = F;
   a.o_cap = ro ? ro->cap : 1;
   a.o_cap_rows = ro ? ro->cap_rows : 0;
+  MREC_CHECK_ARG(sgd_blocks >= 0 && (sgd_blocks == 0 || sgd_table != nullptr),
+                 "sgd_blocks > 0 needs the table");
+  a.sgd = static_cast<const SgdArgs *>(sgd_table);
+  a.sgd_blocks = sgd_blocks;
   hipStream_t s = static_cast<hipStream_t>(stream);
   const int wpb = 256 / lpr;
   // hash layout (batch <= kHashMaxKeys or an exchange view, see mrec_emb_bwd_plan):
@@ -1097,6 +1130,8 @@ static mrec_status apply_impl(const mrec_table_bank *bank, int64_t batch, const 
   int co_blocks = 0;
   if (mrec_status st = build_co_reduce(n_reduce, reduce, &co, &co_blocks); st != MREC_OK)
     return st;
+  co_blocks += sgd_blocks;  // (the SGD tiles follow the reductions, hash layout only)
+  MREC_CHECK_ARG(sgd_blocks == 0 || hash, "SGD tiles ride in the hash-layout apply only");
   if (apply_blocks + co_blocks == 0) return MREC_OK;  // (batch 0 still runs the reductions)
   const dim3 grid(static_cast<unsigned>(apply_blocks + co_blocks));
   const KClock kc = hash ? kclock_take() : KClock{nullptr, 0};

@@ -1573,7 +1573,7 @@ mrec_status mrec_emb_bwd_large_apply(const mrec_table_bank *bank, int64_t batch,
   mrec_status st = lg_setup(bank, batch, const_cast<void *>(workspace), ws_bytes, &ba, &lpr, &R,
                             &w);
   if (st != MREC_OK) return st;
-  ApplyArgs a;
+  ApplyArgs a{};
   st = lg_apply_args(bank, ba, dx, dx_dtype, dx_ld, dfm, fm_sum, x0, x0_dtype, x0_ld, dw, mode,
                      lr, seed, d_step, grad, &a);
   if (st != MREC_OK) return st;
@@ -1640,7 +1640,7 @@ mrec_status mrec_emb_bwd_large_fused_ex(const mrec_table_bank *bank, const mrec_
   int es = 0, lpr = 0;
   mrec_status st = make_bank_args(bank, &ba, &es, &lpr);
   if (st != MREC_OK) return st;
-  ApplyArgs a;
+  ApplyArgs a{};
   st = lg_apply_args(bank, ba, dx, dx_dtype, dx_ld, dfm, fm_sum, x0, x0_dtype, x0_ld, dw, mode,
                      lr, seed, d_step, grad, &a);
   if (st != MREC_OK) return st;
@@ -1662,7 +1662,7 @@ mrec_status mrec_emb_bwd_large_fused_given(const mrec_table_bank *bank, const mr
   int es = 0, lpr = 0;
   mrec_status st = make_bank_args(bank, &ba, &es, &lpr);
   if (st != MREC_OK) return st;
-  ApplyArgs a;
+  ApplyArgs a{};
   st = lg_apply_args(bank, ba, nullptr, MREC_F32, 0, nullptr, nullptr, nullptr, MREC_F32, 0,
                      nullptr, mode, lr, seed, d_step, grad, &a);
   if (st != MREC_OK) return st;

@@ -26,6 +26,7 @@ MI355X additions (documented deviations):
 from __future__ import annotations
 
 import copy
+import ctypes
 import os
 from abc import ABC, abstractmethod
 from typing import Dict, List, Optional
@@ -300,14 +301,60 @@ class IModel(Module, IWithArguments, ABC):
             p._mrec_dp_grad = view if p.dim() == 2 else view.reshape(-1)
             p._mrec_dp_group = g
         self._dp_flat = (flat, layout)
+        self._dp_sgd_table = None
+        from pytorchrec_amd.sharding import ShardedEmbeddingBank
+        for b in self.embedding_banks():  # the owner apply runs the dense SGD (ABI 28)
+            if isinstance(b, ShardedEmbeddingBank) and os.environ.get("MREC_DP_INLINE_SGD", "1") == "1":
+                b.dp_inline_sgd = self._dp_inline_sgd
 
     def _dp_flat_step(self):
         """All-reduce the flat gradient buffer (sum) and apply SGD with lr / world to
         every parameter that owns a view of it, plus its cached bf16 images."""
         from pytorchrec_amd import _mrec
+        flat, _ = self._dp_flat
+        self.dp_comm.allreduce_sum_(flat)
+        jobs = self._dp_sgd_jobs()
+        arr = (_mrec.SgdJob * len(jobs))(*jobs)
+        _mrec.call("mrec_sgd_multi", len(jobs), arr, _mrec.stream_handle())
+
+    def _dp_inline_sgd(self):
+        """Called by a row-sharded bank's backward right before its owner apply, when
+        every dense gradient of the step is in the flat buffer (the interaction is the
+        model's first op, so its backward runs last): the flat all-reduce now, and the
+        SGD as a table of tiles the owner's apply launch runs beside the embedding
+        update (mrec_emb_bwd_apply_wire_sgd) instead of a mrec_sgd_multi launch of its
+        own -- the same jobs, the same bits.  train_step then skips _dp_flat_step.
+        -> (device table, workgroups), or None (no flat buffer)."""
+        from pytorchrec_amd import _mrec
+        from pytorchrec_amd import dense as dense_ops
+        if getattr(self, "_dp_flat", None) is None:
+            return None
+        dense_ops.flush_pending()  # (any deferred reduction still writing the flat buffer)
+        flat, _ = self._dp_flat
+        self.dp_comm.allreduce_sum_(flat)
+        jobs = self._dp_sgd_jobs()
+        key = tuple((j.w, j.g, j.N, j.K, j.ldw, j.ldg, j.lr, j.img_row, j.ld_row, j.img_tr,
+                     j.ld_tr, j.img_kind) for j in jobs)
+        cached = getattr(self, "_dp_sgd_table", None)
+        if cached is None or cached[2] != key:
+            lib = _mrec.lib()
+            nb = int(lib.mrec_sgd_table_bytes())
+            host = (ctypes.c_uint8 * nb)()
+            blocks = ctypes.c_int32(0)
+            arr = (_mrec.SgdJob * len(jobs))(*jobs)
+            _mrec.call("mrec_sgd_table_build", len(jobs), arr, ctypes.addressof(host), nb,
+                       ctypes.byref(blocks))
+            table = torch.frombuffer(bytearray(host), dtype=torch.uint8).to(flat.device)
+            cached = (table, int(blocks.value), key)
+            self._dp_sgd_table = cached
+        self._dp_inline_done = True
+        return cached[0], cached[1]
+
+    def _dp_sgd_jobs(self):
+        """The flat buffer's SGD jobs (lr / world), marking the images they re-emit."""
+        from pytorchrec_amd import _mrec
         flat, layout = self._dp_flat
         comm = self.dp_comm
-        comm.allreduce_sum_(flat)
         from pytorchrec_amd.dense import cached_images, images_updated
         jobs = []
         for p, g, n, k, ld, o in layout:
@@ -327,8 +374,7 @@ class IModel(Module, IWithArguments, ABC):
                                      _mrec.IMG_TOWER if packed else _mrec.IMG_ROW_TR))
             if imgs is not None:
                 images_updated(p, kind)
-        arr = (_mrec.SgdJob * len(jobs))(*jobs)
-        _mrec.call("mrec_sgd_multi", len(jobs), arr, _mrec.stream_handle())
+        return jobs
 
     # -- data parallel (one process per GPU) ------------------------
     def distribute(self, comm):
@@ -389,7 +435,9 @@ class IModel(Module, IWithArguments, ABC):
             loss.backward()
         comm = getattr(self, "dp_comm", None)
         if comm is not None and (comm.world > 1 or comm.force):
-            if getattr(self, "_dp_flat", None) is not None:
+            if getattr(self, "_dp_inline_done", False):
+                self._dp_inline_done = False  # done in the owner's apply launch
+            elif getattr(self, "_dp_flat", None) is not None:
                 self._dp_flat_step()
             self._allreduce_dense_grads()  # parameters outside the flat buffer
         self.compiled_optimizers.step(closure=None)

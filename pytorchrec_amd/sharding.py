@@ -790,20 +790,26 @@ def owner_apply(bank: ShardedEmbeddingBank, plan, g_recv: torch.Tensor,
 
 def owner_apply_wire(bank: ShardedEmbeddingBank, plan, wire_g: torch.Tensor, pref: torch.Tensor,
                      lr: Optional[float] = None, grad: Optional[torch.Tensor] = None,
-                     parts: Optional[int] = None):
+                     parts: Optional[int] = None, sgd=None):
     """owner_apply reading the received gradient records in place
-    (mrec_emb_bwd_apply_wire: no unpack to fp32 slots; same sums and update)."""
+    (mrec_emb_bwd_apply_wire: no unpack to fp32 slots; same sums and update).
+    ``sgd``: (device table, workgroups) of mrec_sgd_table_build -- the data-parallel
+    dense SGD rides in the same launch (mrec_emb_bwd_apply_wire_sgd, ABI 28)."""
     ws, wsb = plan
     F, W, cap = bank.n_tables, parts or bank.world, bank.cap
     mode, lr = _owner_mode(bank, lr, grad)
     from pytorchrec_amd import dense as dense_ops
     jobs = dense_ops.take_pending(dense_ops.CO_REDUCE_MAX)
     arr = (_mrec.GemmCall * len(jobs))(*[j.struct() for j in jobs]) if jobs else None
-    _mrec.call("mrec_emb_bwd_apply_wire", bank.desc().ref(), W * cap, ws.data_ptr(), wsb,
-               wire_g.data_ptr(), bank.wire_bytes(), _mrec.dtype_code(bank.weight.dtype),
-               pref.data_ptr(), bank.cap_rows, cap, F * cap, mode, float(lr), bank.next_seed(),
-               bank.step_counter().data_ptr(), _mrec.ptr(grad), len(jobs), arr,
-               _mrec.stream_handle())
+    args = (bank.desc().ref(), W * cap, ws.data_ptr(), wsb, wire_g.data_ptr(), bank.wire_bytes(),
+            _mrec.dtype_code(bank.weight.dtype), pref.data_ptr(), bank.cap_rows, cap, F * cap, mode,
+            float(lr), bank.next_seed(), bank.step_counter().data_ptr(), _mrec.ptr(grad),
+            len(jobs), arr)
+    if sgd is not None:
+        _mrec.call("mrec_emb_bwd_apply_wire_sgd", *args, sgd[0].data_ptr(), int(sgd[1]),
+                   _mrec.stream_handle())
+    else:
+        _mrec.call("mrec_emb_bwd_apply_wire", *args, _mrec.stream_handle())
     del jobs
 
 
@@ -966,9 +972,13 @@ class _CompactInteractFn(torch.autograd.Function):
                                      x0=sl(x0) if dfm is not None else None, dw=sl(dw))
                 wire_g = shard_wire_pack(bank, gsum, send, parts=ctx.P)
             wire_g = bank.comm.exchange(wire_g)
-            # the owner reads the gradient records in place (no unpack launch)
+            # the owner reads the gradient records in place (no unpack launch); a
+            # data-parallel model's dense SGD rides in the same launch when the flat
+            # gradient is complete here (IModel._dp_inline_sgd: its all-reduce first)
             if ctx.oplan is not None:
-                owner_apply_wire(bank, ctx.oplan, wire_g, ctx.pref, parts=ctx.P)
+                hook = getattr(bank, "dp_inline_sgd", None)
+                sgd = hook() if hook is not None else None
+                owner_apply_wire(bank, ctx.oplan, wire_g, ctx.pref, parts=ctx.P, sgd=sgd)
             else:
                 owner_apply_large(bank, recv, bank.part, wire_g=wire_g, pref=ctx.pref,
                                   parts=ctx.P)

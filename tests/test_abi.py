@@ -114,6 +114,26 @@ def test_apply_refuses_a_workspace_no_plan_was_issued_into(lib):
     assert b"mrec_emb_bwd_apply_wire" in lib.mrec_last_error()
 
 
+def test_sgd_table_build_is_host_only_and_validates(lib):
+    """mrec_sgd_table_build (ABI 28) fills a host table and its workgroup count, no
+    device call: 32 x 32 tiles per job; bad jobs fail with MREC_EINVAL."""
+    from pytorchrec_amd import _mrec
+    nb = int(lib.mrec_sgd_table_bytes())
+    assert nb > 16 * 64
+    host = (ctypes.c_uint8 * nb)()
+    blocks = ctypes.c_int32(-1)
+    jobs = (_mrec.SgdJob * 2)(
+        _mrec.SgdJob(64, 128, 400, 429, 429, 432, 0.1, None, 0, None, 0, _mrec.IMG_TOWER),
+        _mrec.SgdJob(256, 512, 1, 400, 400, 400, 0.1, None, 0, None, 0, _mrec.IMG_ROW_TR))
+    assert lib.mrec_sgd_table_build(2, jobs, ctypes.addressof(host), nb, ctypes.byref(blocks)) == _mrec.OK
+    assert blocks.value == 13 * 14 + 1 * 13
+    assert lib.mrec_sgd_table_build(2, jobs, ctypes.addressof(host), nb - 1,
+                                    ctypes.byref(blocks)) == _mrec.EINVAL
+    jobs[0].g = None
+    assert lib.mrec_sgd_table_build(2, jobs, ctypes.addressof(host), nb, ctypes.byref(blocks)) == _mrec.EINVAL
+    assert b"NULL" in lib.mrec_last_error()
+
+
 def test_product_path_has_no_cpu_fallback_for_gpu_tensors():
     """The HIP ops raise MrecUnavailable (never fall back) when the library is gone."""
     from pytorchrec_amd import _mrec

@@ -591,7 +591,7 @@ def embedding_roofline(model, step, datas, args, in_step=True):
 
 SHARD_EMB = ("mrec_shard_bucketize_dedup_ex", "mrec_shard_gather_wire_ex",
              "mrec_shard_wire_unpack_ex", "mrec_interact_fwd_ex", "mrec_interact_fwd_rec",
-             "mrec_emb_bwd_apply_rec", "mrec_emb_bwd_apply_wire")
+             "mrec_emb_bwd_apply_rec", "mrec_emb_bwd_apply_wire", "mrec_emb_bwd_apply_wire_sgd")
 
 
 def sharded_roofline(model, step, datas, args):
@@ -643,7 +643,8 @@ KERNEL_OF = {"mrec_shard_bucketize_dedup_ex": "mrec_shard_bucketize_dedup",
              "mrec_interact_fwd_ex": "mrec_interact_fwd_ex",
              "mrec_interact_fwd_rec": "mrec_interact_fwd_ex",
              "mrec_emb_bwd_apply_rec": "mrec_emb_bwd_apply",
-             "mrec_emb_bwd_apply_wire": "mrec_emb_bwd_apply"}
+             "mrec_emb_bwd_apply_wire": "mrec_emb_bwd_apply",
+             "mrec_emb_bwd_apply_wire_sgd": "mrec_emb_bwd_apply"}
 
 
 def tower_cross_phases(step, data, B, L):

@@ -663,6 +663,26 @@ mrec_status mrec_shard_bucketize_dedup_ex(const mrec_ids *ids, int32_t n_tables,
                                           int32_t cap, int64_t chunk_batch, int32_t *send_ids,
                                           int32_t *pos, int32_t *d_overflow, int32_t *d_oob_flag,
                                           mrec_stream stream);
+
+/*
+ * mrec_shard_bucketize_dedup_ex with `quarters` (a power of two <= 16) workgroups per
+ * table and chunk (ABI 28): workgroup q takes the ids whose quarter
+ * ((id * 0x9e3779b1) mod 2^32) >> (32 - log2 quarters) is q, so each inserts and
+ * ranks a quarter of the distinct ids; a part's slots are quarter-major (quarter 0's
+ * distinct ids in first-lookup order, then quarter 1's, ...) -- the same records and
+ * sums, another slot order.  The quarters of a (table, chunk) meet once through
+ * `scratch` (mrec_shard_dedup_scratch_bytes, zeroed once before first use, then kept
+ * with the caller: it holds monotonic arrival tickets); a wait that times out sets bit
+ * 2 of *d_overflow.  quarters = 1 is mrec_shard_bucketize_dedup_ex.
+ */
+size_t mrec_shard_dedup_scratch_bytes(int32_t n_tables, int64_t chunks, int32_t world,
+                                      int32_t quarters);
+mrec_status mrec_shard_bucketize_dedup_q(const mrec_ids *ids, int32_t n_tables,
+                                         const int64_t *rows, int64_t batch, int32_t world,
+                                         int32_t cap, int64_t chunk_batch, int32_t quarters,
+                                         void *scratch, size_t scratch_bytes, int32_t *send_ids,
+                                         int32_t *pos, int32_t *d_overflow, int32_t *d_oob_flag,
+                                         mrec_stream stream);
 /* bytes of one wire record: round4((dim + has_w) * element bytes) */
 int32_t mrec_shard_wire_bytes(int32_t dim, int32_t has_w, mrec_dtype dtype);
 /* owner: rows of the received ids (header = recv_ids) -> wire (a lazy-Adam bank's

@@ -369,6 +369,10 @@ SIGNATURES = {
     "mrec_shard_bucketize_dedup_ex": (ctypes.c_int, [_ids_p, _i32, ctypes.POINTER(ctypes.c_int64),
                                                      _i64, _i32, _i32, _i64, _vp, _vp, _vp, _vp,
                                                      _vp]),
+    "mrec_shard_dedup_scratch_bytes": (ctypes.c_size_t, [_i32, _i64, _i32, _i32]),
+    "mrec_shard_bucketize_dedup_q": (ctypes.c_int, [_ids_p, _i32, ctypes.POINTER(ctypes.c_int64),
+                                                    _i64, _i32, _i32, _i64, _i32, _vp,
+                                                    ctypes.c_size_t, _vp, _vp, _vp, _vp, _vp]),
     "mrec_shard_wire_bytes": (_i32, [_i32, _i32, _i32]),
     "mrec_shard_gather_wire": (ctypes.c_int, [_bank_p, _vp, _i32, _i32, _i32, _vp, _vp,
                                               ctypes.POINTER(PlanJob), _vp]),

@@ -163,6 +163,21 @@ __device__ __forceinline__ uint32_t id_hash(uint32_t x, uint32_t mask) {
 // samples (grid y): chunk c of the batch is its own "sub-sender", part d * C + c of
 // send_ids (owner d's C parts contiguous, so the equal-split all-to-all still moves
 // W parts of C * P); an id repeated across chunks takes a slot in each.
+// Quarters (ABI 28, mrec_shard_bucketize_dedup_q): H = 2^lgH workgroups per (table,
+// chunk), workgroup h taking the ids whose dedup_quarter is h, so each inserts and
+// ranks ~1/H of the table's distinct ids (the id loads, the LDS hash and the ranks
+// were one workgroup's serial chain: 3.3 + 0.6 + 3.4 + 2.2 + 2.1 us at C2's shape).
+// A part's slots are then quarter-major (quarter 0's distinct ids in first-lookup
+// order, then quarter 1's, ...): each workgroup publishes its per-owner counts and
+// waits for its H - 1 siblings (one agent-scope ticket, bounded spin; the siblings
+// are adjacent workgroups, dispatched together) to place its ids after the lower
+// quarters'.  The slot order changes no arithmetic (one entry per distinct id and
+// owner); cpu_bucketize_dedup restates the same order.
+__host__ __device__ inline uint32_t dedup_quarter(uint32_t key, int lgH) {
+  return lgH ? (key * 0x9e3779b1u) >> (32 - lgH) : 0u;
+}
+constexpr int kDedupMaxW = 128;  // (W + 1) * groups <= 2048 keeps W below this anyway
+
 template <bool KC>
 __global__ __launch_bounds__(kBT) void bucketize_dedup_kernel(IdsArgs ids, RowsArg rows, int64_t Btot,
                                                               int W, int cap, int F, int hs,
@@ -170,15 +185,22 @@ __global__ __launch_bounds__(kBT) void bucketize_dedup_kernel(IdsArgs ids, RowsA
                                                               int32_t *__restrict__ pos,
                                                               int32_t *__restrict__ overflow,
                                                               int32_t *__restrict__ oob, int C,
-                                                              int64_t cb, KClock kc) {
+                                                              int64_t cb, int lgH,
+                                                              int32_t *__restrict__ qcnt,
+                                                              unsigned long long *__restrict__ arrive,
+                                                              int spin_bound, KClock kc) {
   KcScope<KC> kc_scope(kc);  // (clocked instantiation: bench.py in-step times)
   __shared__ uint32_t hist[kBHist];
   __shared__ uint32_t wtot[kBWaves];
+  __shared__ uint32_t s_base[kDedupMaxW], s_tot[kDedupMaxW];
+  __shared__ int s_ok;
   extern __shared__ uint32_t hash_lds[];  // keys [hs] | (first << 16 | slot) [hs]
   uint32_t *keys = hash_lds;
   uint32_t *fs = hash_lds + hs;
   const uint32_t hmask = static_cast<uint32_t>(hs - 1);
-  const int f = blockIdx.x;
+  const int H = 1 << lgH;
+  const int f = blockIdx.x >> lgH;
+  const int qh = blockIdx.x & (H - 1);
   const int c = blockIdx.y;
   const int64_t s0 = static_cast<int64_t>(c) * cb;
   const int64_t B = min(cb, Btot - s0);  // this chunk's samples
@@ -230,7 +252,7 @@ __global__ __launch_bounds__(kBT) void bucketize_dedup_kernel(IdsArgs ids, RowsA
   for (int r = 0; r < kR; ++r) {
     hpos[r] = kEmpty;
     const int64_t id = idv[r];
-    if (id >= 0 && id < rows_f) {
+    if (id >= 0 && id < rows_f && dedup_quarter(static_cast<uint32_t>(id), lgH) == static_cast<uint32_t>(qh)) {
       const uint32_t key = static_cast<uint32_t>(id);
       uint32_t h = id_hash(key, hmask);
       while (true) {
@@ -266,13 +288,61 @@ __global__ __launch_bounds__(kBT) void bucketize_dedup_kernel(IdsArgs ids, RowsA
   diag_exit(hist[tid] == 12345u);
   return;
 #endif
+  // this quarter's slot base per owner (after the lower quarters') and the totals
+  if (H == 1) {
+    if (tid < W) {
+      s_base[tid] = 0u;
+      s_tot[tid] = hist[(tid + 1) * G] - hist[tid * G];
+    }
+  } else {
+    const int64_t q0 = (static_cast<int64_t>(c) * F + f) * H;
+    if (tid < W)
+      __hip_atomic_store(qcnt + (q0 + qh) * W + tid,
+                         static_cast<int32_t>(hist[(tid + 1) * G] - hist[tid * G]),
+                         __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (tid == 0) {
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      unsigned long long *ctr = arrive + static_cast<int64_t>(c) * F + f;
+      // arrivals only grow (H per call): this call's H tickets end at the next multiple
+      const unsigned long long t = __hip_atomic_fetch_add(ctr, 1ull, __ATOMIC_RELAXED,
+                                                          __HIP_MEMORY_SCOPE_AGENT);
+      const unsigned long long target = (t / H + 1) * H;
+      int ok = 1;
+      for (int spins = 0; __hip_atomic_load(ctr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < target;) {
+        __builtin_amdgcn_s_sleep(1);
+        if (++spins > spin_bound) {
+          ok = 0;
+          if (overflow) atomicOr(overflow, 4);  // bit 2: a quarter's wait timed out
+          break;
+        }
+      }
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+      s_ok = ok;
+    }
+    __syncthreads();
+    if (tid < W) {
+      uint32_t base = 0u, tot = 0u;
+      for (int h2 = 0; h2 < H; ++h2) {
+        const uint32_t v = static_cast<uint32_t>(
+            __hip_atomic_load(qcnt + (q0 + h2) * W + tid, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+        if (h2 < qh) base += v;
+        tot += v;
+      }
+      s_base[tid] = s_ok ? base : 0u;
+      s_tot[tid] = s_ok ? tot : 0u;
+    }
+    __syncthreads();
+  }
 #pragma unroll
   for (int r = 0; r < kR; ++r) {
     if (r >= rounds) continue;
     const uint32_t d = dv[r];
     const uint64_t m = same_value_lanes(d, nbits);
     if (d == static_cast<uint32_t>(W)) continue;
-    uint32_t slot = hist[d * G + r * kBWaves + wid] + __popcll(m & lt) - hist[d * G];
+    uint32_t slot = hist[d * G + r * kBWaves + wid] + __popcll(m & lt) - hist[d * G] + s_base[d];
     if (slot >= static_cast<uint32_t>(cap)) {
       if (overflow) atomicOr(overflow, 1);  // bit 0: a table's `cap` slots
       slot = 0xffffu;
@@ -290,8 +360,12 @@ __global__ __launch_bounds__(kBT) void bucketize_dedup_kernel(IdsArgs ids, RowsA
     if (r >= rounds || i >= B) continue;
     const int64_t id = idv[r];
     if (hpos[r] == kEmpty) {
-      if (oob && id != -2) *oob = 1;
-      pos[f * Btot + s0 + i] = -1;
+      const bool valid = id >= 0 && id < rows_f;
+      if (valid) continue;  // another quarter's id: its workgroup writes the slot
+      if (qh == 0) {        // an invalid id: quarter 0 alone flags it
+        if (oob && id != -2) *oob = 1;
+        pos[f * Btot + s0 + i] = -1;
+      }
       continue;
     }
     const uint32_t slot = fs[hpos[r]] & 0xffffu;
@@ -300,13 +374,16 @@ __global__ __launch_bounds__(kBT) void bucketize_dedup_kernel(IdsArgs ids, RowsA
         slot == 0xffffu ? -1
                         : static_cast<int32_t>(((static_cast<int64_t>(d) * C + c) * F + f) * cap + slot);
   }
-  // 4. counts header and padding slots of every owner part
-  for (int d = 0; d < W; ++d) {
-    const uint32_t cnt = min(static_cast<uint32_t>(cap), hist[(d + 1) * G] - hist[d * G]);
-    const int64_t pd = (static_cast<int64_t>(d) * C + c) * P;
-    int32_t *part = send_ids + pd + static_cast<int64_t>(f) * cap;
-    for (int s = static_cast<int>(cnt) + tid; s < cap; s += kBT) part[s] = -1;
-    if (tid == 0) send_ids[pd + static_cast<int64_t>(F) * cap + f] = static_cast<int32_t>(cnt);
+  // 4. counts header and padding slots of every owner part (the last quarter: every
+  // quarter's slots lie below the total)
+  if (qh == H - 1) {
+    for (int d = 0; d < W; ++d) {
+      const uint32_t cnt = min(static_cast<uint32_t>(cap), s_tot[d]);
+      const int64_t pd = (static_cast<int64_t>(d) * C + c) * P;
+      int32_t *part = send_ids + pd + static_cast<int64_t>(f) * cap;
+      for (int s = static_cast<int>(cnt) + tid; s < cap; s += kBT) part[s] = -1;
+      if (tid == 0) send_ids[pd + static_cast<int64_t>(F) * cap + f] = static_cast<int32_t>(cnt);
+    }
   }
 }
 
@@ -755,10 +832,57 @@ mrec_status mrec_shard_lookup_grad(int64_t batch, int32_t n_tables, int32_t dim,
 
 // ---- compact exchange (ABI 19) ----------------------------------------------
 
+static mrec_status bucketize_dedup_launch(const mrec_ids *ids, int32_t n_tables,
+                                          const int64_t *rows, int64_t batch, int32_t world,
+                                          int32_t cap, int64_t chunk_batch, int32_t quarters,
+                                          void *scratch, int32_t *send_ids, int32_t *pos,
+                                          int32_t *d_overflow, int32_t *d_oob_flag,
+                                          mrec_stream stream);
+
+static int64_t dedup_chunks(int64_t batch, int64_t chunk_batch) {
+  return batch > 0 ? (batch + chunk_batch - 1) / chunk_batch : 1;
+}
+
+size_t mrec_shard_dedup_scratch_bytes(int32_t n_tables, int64_t chunks, int32_t world,
+                                      int32_t quarters) {
+  if (n_tables < 1 || chunks < 1 || world < 1 || quarters < 1) return 0;
+  const int64_t arrive = (chunks * n_tables * 8 + 255) / 256 * 256;
+  return static_cast<size_t>(arrive + chunks * n_tables * quarters * world * 4);
+}
+
+mrec_status mrec_shard_bucketize_dedup_q(const mrec_ids *ids, int32_t n_tables,
+                                         const int64_t *rows, int64_t batch, int32_t world,
+                                         int32_t cap, int64_t chunk_batch, int32_t quarters,
+                                         void *scratch, size_t scratch_bytes, int32_t *send_ids,
+                                         int32_t *pos, int32_t *d_overflow, int32_t *d_oob_flag,
+                                         mrec_stream stream) {
+  MREC_CHECK_ARG(quarters >= 1 && quarters <= 16 && (quarters & (quarters - 1)) == 0,
+                 "quarters must be a power of two in [1, 16]");
+  MREC_CHECK_ARG(world <= kDedupMaxW, "world too large for the dedup bucketize");
+  const int64_t C = dedup_chunks(batch, std::max<int64_t>(chunk_batch, 1));
+  if (quarters > 1) {
+    MREC_CHECK_ARG(scratch != nullptr && (reinterpret_cast<uintptr_t>(scratch) & 7) == 0 &&
+                       scratch_bytes >= mrec_shard_dedup_scratch_bytes(n_tables, C, world, quarters),
+                   "quarters > 1 need mrec_shard_dedup_scratch_bytes of zeroed scratch");
+  }
+  return bucketize_dedup_launch(ids, n_tables, rows, batch, world, cap, chunk_batch, quarters,
+                                scratch, send_ids, pos, d_overflow, d_oob_flag, stream);
+}
+
 mrec_status mrec_shard_bucketize_dedup_ex(const mrec_ids *ids, int32_t n_tables,
                                           const int64_t *rows, int64_t batch, int32_t world,
                                           int32_t cap, int64_t chunk_batch, int32_t *send_ids,
                                           int32_t *pos, int32_t *d_overflow, int32_t *d_oob_flag,
+                                          mrec_stream stream) {
+  return bucketize_dedup_launch(ids, n_tables, rows, batch, world, cap, chunk_batch, 1, nullptr,
+                                send_ids, pos, d_overflow, d_oob_flag, stream);
+}
+
+static mrec_status bucketize_dedup_launch(const mrec_ids *ids, int32_t n_tables,
+                                          const int64_t *rows, int64_t batch, int32_t world,
+                                          int32_t cap, int64_t chunk_batch, int32_t quarters,
+                                          void *scratch, int32_t *send_ids, int32_t *pos,
+                                          int32_t *d_overflow, int32_t *d_oob_flag,
                                           mrec_stream stream) {
   MREC_CHECK_ARG(n_tables >= 1 && n_tables <= MREC_MAX_TABLES, "n_tables out of range");
   MREC_CHECK_ARG(rows != nullptr && send_ids && pos, "NULL pointer");
@@ -794,16 +918,25 @@ mrec_status mrec_shard_bucketize_dedup_ex(const mrec_ids *ids, int32_t n_tables,
   }();
   (void)attr;
   const KClock kc = kclock_take();
-  const dim3 grid(n_tables, static_cast<unsigned>(C));
+  int lgH = 0;
+  while ((1 << lgH) < quarters) ++lgH;
+  unsigned long long *arrive = static_cast<unsigned long long *>(scratch);
+  int32_t *qcnt = scratch ? reinterpret_cast<int32_t *>(static_cast<char *>(scratch) +
+                                                        (C * n_tables * 8 + 255) / 256 * 256)
+                          : nullptr;
+  const int spin_bound = 1 << 22;  // ~0.1 s of sleeps: then the overflow word's bit 2
+  const dim3 grid(static_cast<unsigned>(n_tables) << lgH, static_cast<unsigned>(C));
   hipStream_t s = static_cast<hipStream_t>(stream);
   if (kc.buf)
     bucketize_dedup_kernel<true><<<grid, kBT, lds, s>>>(ia, ra, batch, world, cap, n_tables, hs,
                                                         send_ids, pos, d_overflow, d_oob_flag,
-                                                        static_cast<int>(C), cb, kc);
+                                                        static_cast<int>(C), cb, lgH, qcnt, arrive,
+                                                        spin_bound, kc);
   else
     bucketize_dedup_kernel<false><<<grid, kBT, lds, s>>>(ia, ra, batch, world, cap, n_tables, hs,
                                                          send_ids, pos, d_overflow, d_oob_flag,
-                                                         static_cast<int>(C), cb, kc);
+                                                         static_cast<int>(C), cb, lgH, qcnt, arrive,
+                                                         spin_bound, kc);
   return launch_status("mrec_shard_bucketize_dedup");
 }
 

@@ -286,6 +286,19 @@ class ShardedEmbeddingBank(EmbeddingBank):
         self._cap_rows = default_cap_rows(mb, W, self.global_rows, self._caps[0]
                                           if self._caps is not None else self.cap)
         self._cap_rows_user = False
+        # the dedup bucketize's workgroups per table (mrec_shard_bucketize_dedup_q, ABI
+        # 28; a power of two <= 16, 1 = one workgroup per table) and its scratch
+        self.dedup_quarters = int(os.environ.get("MREC_DEDUP_QUARTERS", "4"))
+        self._dedup_scratch = None
+
+    def dedup_scratch(self, chunks: int) -> torch.Tensor:
+        """The quarters' meeting words for ``chunks`` chunks (zeroed once, kept: they
+        hold monotonic arrival tickets)."""
+        nb = int(_mrec.lib().mrec_shard_dedup_scratch_bytes(self.n_tables, max(1, chunks),
+                                                            self.world, self.dedup_quarters))
+        if self._dedup_scratch is None or self._dedup_scratch.numel() < nb:
+            self._dedup_scratch = torch.zeros(nb, dtype=torch.uint8, device=self.weight.device)
+        return self._dedup_scratch
 
     @property
     def cap_rows(self) -> int:
@@ -370,6 +383,10 @@ class ShardedEmbeddingBank(EmbeddingBank):
             raise RuntimeError(f"row-sharded exchange overflow: more than cap={self.cap} ids of "
                                "one table for one owner in a batch; raise `cap` "
                                "(sharded_tables(cap=...))")
+        if ov & 4:
+            raise RuntimeError("row-sharded dedup bucketize: a quarter workgroup's wait for "
+                               "its siblings timed out (slots of that table are not valid); "
+                               "MREC_DEDUP_QUARTERS=1 runs one workgroup per table")
         if ov & 2:
             raise RuntimeError(f"row-sharded compact exchange overflow: more than cap_rows="
                                f"{self.cap_rows} distinct ids for one owner over all tables in a "
@@ -520,9 +537,12 @@ def shard_bucketize_dedup(bank: ShardedEmbeddingBank, ids: Sequence[torch.Tensor
     send = torch.empty(W, C * bank.part, dtype=torch.int32, device=dev)
     pos = torch.empty(F, B, dtype=torch.int32, device=dev)
     fl = bank.flags()
-    _mrec.call("mrec_shard_bucketize_dedup_ex", _mrec.IdsDesc(ids).ref(), F,
-               bank._global_rows_arr, B, W, cap, bank.chunk_batch, send.data_ptr(),
-               pos.data_ptr(), fl.data_ptr(), fl.data_ptr() + 4, _mrec.stream_handle())
+    H = bank.dedup_quarters
+    scratch = bank.dedup_scratch(C) if H > 1 else None
+    _mrec.call("mrec_shard_bucketize_dedup_q", _mrec.IdsDesc(ids).ref(), F,
+               bank._global_rows_arr, B, W, cap, bank.chunk_batch, H, _mrec.ptr(scratch),
+               scratch.numel() if scratch is not None else 0, send.data_ptr(), pos.data_ptr(),
+               fl.data_ptr(), fl.data_ptr() + 4, _mrec.stream_handle())
     return send, pos
 
 
@@ -1074,6 +1094,15 @@ def cpu_bucketize(bank: ShardedEmbeddingBank, ids: Sequence[torch.Tensor]):
     return send, pos
 
 
+def dedup_quarter(ids: torch.Tensor, quarters: int) -> torch.Tensor:
+    """The dedup bucketize's quarter of each id (shard.hip dedup_quarter):
+    ((id * 0x9e3779b1) mod 2^32) >> (32 - log2 quarters)."""
+    lg = max(0, int(quarters).bit_length() - 1)
+    if lg == 0:
+        return torch.zeros_like(ids, dtype=torch.long)
+    return ((ids.long() * 0x9E3779B1) & 0xFFFFFFFF) >> (32 - lg)
+
+
 def cpu_bucketize_dedup(bank: ShardedEmbeddingBank, ids: Sequence[torch.Tensor]):
     """CPU restatement of mrec_shard_bucketize_dedup(_ex): per (owner, table) the
     distinct ids in the order of their first lookup, every lookup's slot, the
@@ -1098,8 +1127,10 @@ def cpu_bucketize_dedup(bank: ShardedEmbeddingBank, ids: Sequence[torch.Tensor])
             first.scatter_reduce_(0, inv, ar, reduce="amin")
             rep = first[inv] == ar
             slot_u = torch.empty(uniq.numel(), dtype=torch.long)
+            quarter = dedup_quarter(t, getattr(bank, "dedup_quarters", 1))
             for o in range(W):
                 r = torch.nonzero(rep & (owner == o)).reshape(-1)  # ascending sample order
+                r = r[torch.argsort(quarter[r], stable=True)]      # quarter-major (ABI 28)
                 if r.numel() > cap:
                     raise RuntimeError(f"row-sharded exchange overflow: more than cap={cap} ids "
                                        "of one table for one owner in a batch; raise cap")
@@ -1196,4 +1227,4 @@ __all__ = ["ShardComm", "ShardedEmbeddingBank", "sharded_tables", "make_bank", "
            "shard_lookup_grad", "shard_bucketize_dedup", "shard_gather_wire", "shard_wire_unpack",
            "shard_wire_pack", "sender_plan_job", "sender_grad_sums", "owner_plan",
            "owner_plan_job", "owner_apply", "remote_desc", "shard_interact", "cpu_bucketize",
-           "cpu_bucketize_dedup"]
+           "cpu_bucketize_dedup", "dedup_quarter"]

@@ -589,7 +589,7 @@ def embedding_roofline(model, step, datas, args, in_step=True):
     return out
 
 
-SHARD_EMB = ("mrec_shard_bucketize_dedup_ex", "mrec_shard_gather_wire_ex",
+SHARD_EMB = ("mrec_shard_bucketize_dedup_ex", "mrec_shard_bucketize_dedup_q", "mrec_shard_gather_wire_ex",
              "mrec_shard_wire_unpack_ex", "mrec_interact_fwd_ex", "mrec_interact_fwd_rec",
              "mrec_emb_bwd_apply_rec", "mrec_emb_bwd_apply_wire", "mrec_emb_bwd_apply_wire_sgd")
 
@@ -638,6 +638,7 @@ def sharded_roofline(model, step, datas, args):
 
 # bench entry point -> the PMC stamp's kernel key (tools/pmc_traffic.py KERNELS)
 KERNEL_OF = {"mrec_shard_bucketize_dedup_ex": "mrec_shard_bucketize_dedup",
+             "mrec_shard_bucketize_dedup_q": "mrec_shard_bucketize_dedup",
              "mrec_shard_gather_wire_ex": "mrec_shard_gather_wire",
              "mrec_shard_wire_unpack_ex": "mrec_shard_wire_move",
              "mrec_interact_fwd_ex": "mrec_interact_fwd_ex",

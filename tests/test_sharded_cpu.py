@@ -270,9 +270,11 @@ def test_compact_exchange_wire_bytes_c5_w8():
 
 def test_cpu_bucketize_dedup_layout():
     """The compact ids message on the CPU: per (owner, table) the distinct ids in
-    first-lookup order (as local ids), -1 padding, the counts header, and every
-    lookup's pos pointing at its id's slot."""
-    from pytorchrec_amd.sharding import ShardComm, ShardedEmbeddingBank, cpu_bucketize_dedup
+    quarter-major, then first-lookup order (as local ids; ABI 28: the GPU bucketize
+    runs one workgroup per quarter of the ids, sharding.dedup_quarter), -1 padding,
+    the counts header, and every lookup's pos pointing at its id's slot."""
+    from pytorchrec_amd.sharding import (ShardComm, ShardedEmbeddingBank, cpu_bucketize_dedup,
+                                         dedup_quarter)
     W, B = 3, 40
     rows = [17, 5, 1000]
     bank = ShardedEmbeddingBank(rows, 8, ShardComm(world=W, rank=0), cap=B, max_batch=B)
@@ -287,6 +289,8 @@ def test_cpu_bucketize_dedup_layout():
                 i = int(t[b])
                 if i % W == o and i not in seen:
                     seen.append(i)
+            q = dedup_quarter(torch.tensor(seen, dtype=torch.long), bank.dedup_quarters).tolist()
+            seen = [i for _, _, i in sorted((qq, k, i) for k, (qq, i) in enumerate(zip(q, seen)))]
             cnt = int(send[o, F * cap + f])
             assert cnt == len(seen)
             assert send[o, f * cap:f * cap + cnt].tolist() == [i // W for i in seen]

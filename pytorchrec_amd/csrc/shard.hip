@@ -300,11 +300,12 @@ __global__ __launch_bounds__(kBT) void bucketize_dedup_kernel(IdsArgs ids, RowsA
       __hip_atomic_store(qcnt + (q0 + qh) * W + tid,
                          static_cast<int32_t>(hist[(tid + 1) * G] - hist[tid * G]),
                          __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    // the counts are agent-scope atomic (write-through) stores, drained before the
+    // ticket and read back by agent-scope atomic loads: no release / acquire fence
+    // (MI355X L1 invalidation ~1.7 us; cdna_hip_programming.md Guideline 16 R1)
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
     if (tid == 0) {
-      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       unsigned long long *ctr = arrive + static_cast<int64_t>(c) * F + f;
       // arrivals only grow (H per call): this call's H tickets end at the next multiple
       const unsigned long long t = __hip_atomic_fetch_add(ctr, 1ull, __ATOMIC_RELAXED,
@@ -319,7 +320,7 @@ __global__ __launch_bounds__(kBT) void bucketize_dedup_kernel(IdsArgs ids, RowsA
           break;
         }
       }
-      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");  // (no instruction: order only)
       s_ok = ok;
     }
     __syncthreads();

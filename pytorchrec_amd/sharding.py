@@ -287,8 +287,10 @@ class ShardedEmbeddingBank(EmbeddingBank):
                                           if self._caps is not None else self.cap)
         self._cap_rows_user = False
         # the dedup bucketize's workgroups per table (mrec_shard_bucketize_dedup_q, ABI
-        # 28; a power of two <= 16, 1 = one workgroup per table) and its scratch
-        self.dedup_quarters = int(os.environ.get("MREC_DEDUP_QUARTERS", "4"))
+        # 28; a power of two <= 16) and its scratch.  1 by default: 2 or 4 quarters
+        # measured no faster at C2's shape (11.9-12.2 us against 11.9 at W = 1; the
+        # launch is a chain of id loads, barriers and stores, not of inserts)
+        self.dedup_quarters = int(os.environ.get("MREC_DEDUP_QUARTERS", "1"))
         self._dedup_scratch = None
 
     def dedup_scratch(self, chunks: int) -> torch.Tensor:

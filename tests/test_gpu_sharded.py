@@ -808,3 +808,22 @@ def test_sharded_checkpoint_world1_gpu_bit_exact_and_memory_bounded(gpu, tmp_pat
     back = build(True, 79)
     back.load_weights(single, gpu)
     assert torch.equal(back.embeddings.weight.detach().view(torch.int16), want)
+
+
+@pytest.mark.parametrize("quarters,W,B", [(4, 8, 4096), (2, 3, 1000), (4, 1, 4096), (16, 2, 300)])
+def test_dedup_bucketize_in_quarters_matches_restatement(gpu, quarters, W, B):
+    """mrec_shard_bucketize_dedup_q (ABI 28): `quarters` workgroups per table, each
+    taking the ids of its quarter and meeting its siblings once through the scratch
+    tickets, give exactly the CPU restatement's quarter-major message and slots, call
+    after call (the tickets only grow); Zipf ids with many repeats included."""
+    from pytorchrec_amd import sharding as S
+    b = S.ShardedEmbeddingBank(ROWS, D, S.ShardComm(world=W, rank=0), with_first_order=True,
+                               dtype=torch.bfloat16, max_batch=B, device=gpu)
+    b.dedup_quarters = quarters
+    for call, zipf in enumerate((False, True, False)):
+        ids = _ids(gpu, B, 70 + call, zipf)
+        send, pos = S.shard_bucketize_dedup(b, ids)
+        ref_send, ref_pos = S.cpu_bucketize_dedup(b, [t.cpu() for t in ids])
+        b.check_flags()
+        assert torch.equal(send.cpu(), ref_send), (quarters, W, call)
+        assert torch.equal(pos.cpu(), ref_pos), (quarters, W, call)

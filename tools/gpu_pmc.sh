@@ -3,7 +3,7 @@
 # gpurun_out/pmc_traffic.json (copy it to profiles/).  Each workload's stamp carries
 # its bench args' workload key and the library digest (bench.py reports the traffic
 # only for its own workload and library).  MREC_COMMIT names the commit (no .git on
-# the box).  WORKLOADS selects: c2 zipf c3 c4 shard (default all).
+# the box).  WORKLOADS selects: c2 zipf c3 c4 shard c5 (default all).
 set -o pipefail
 R=$GRAFT_REPO_ROOT
 O=$R/gpurun_out/pmc
@@ -17,10 +17,11 @@ args_of() {
     c3) echo "--model dcnv2" ;;
     c4) echo "--model din" ;;
     shard) echo "--model deepfm --shard --force-collectives --exchange compact" ;;
+    c5) echo "--model deepfm --rows-per-table 100000000" ;;
   esac
 }
 pairs=""
-for w in ${WORKLOADS:-c2 zipf c3 c4 shard}; do
+for w in ${WORKLOADS:-c2 zipf c3 c4 shard c5}; do
   for c in FETCH_SIZE WRITE_SIZE; do
     timeout -s KILL 240 rocprofv3 --pmc $c -d $O/${w}_$c -o run --output-format csv -- python3 $R/bench.py $(args_of $w) --steps 5 --warmup 3 --no-cpu-baseline --no-h2d > $O/${w}_$c.log 2>&1 || { echo PMC_FAIL $w $c; tail -20 $O/${w}_$c.log; exit 1; }
   done

@@ -500,8 +500,11 @@ __device__ __forceinline__ DaRawW da_load_w(const DinAttArgs &p, int64_t b, int 
     __builtin_amdgcn_wave_barrier();                    \
   } while (0)
 
-template <int E, int H1T, int H1K, int H2T, int H2K>
-__global__ __launch_bounds__(DA_THREADS, 1) void din_att_fwd_wave_kernel(DinAttArgs p) {
+// KC: the clocked instantiation (mrec_kernel_clock, common.h), launched only while
+// the clock is on; the production one carries no clock code
+template <int E, int H1T, int H1K, int H2T, int H2K, bool KC = false>
+__global__ __launch_bounds__(DA_THREADS, 1) void din_att_fwd_wave_kernel(DinAttArgs p, KClock kc) {
+  KcScope<KC> kc_scope(kc);
   using S = DaShapeF<E, H1T, H1K, H2T, H2K>;
   constexpr int KT1 = S::KT1, G = S::G, LDH = S::LDH;
   constexpr int PPL = G / 16;  // pooling parts per lane: rows j = 16 rt + lane % 16 -> j mod G
@@ -1076,8 +1079,9 @@ __device__ __forceinline__ void da_build_x_rm(const DinAttArgs &p, const DaRaw &
   *reinterpret_cast<uint4 *>(x + 3 * E) = mq;
 }
 
-template <int E, int H1T, int H1K, int H2T, int H2K>
-__global__ __launch_bounds__(DA_THREADS) void din_att_bwd2_kernel(DinAttArgs p) {
+template <int E, int H1T, int H1K, int H2T, int H2K, bool KC = false>
+__global__ __launch_bounds__(DA_THREADS) void din_att_bwd2_kernel(DinAttArgs p, KClock kc) {
+  KcScope<KC> kc_scope(kc);
   using S = DaShape2<E, H1T, H1K, H2T, H2K>;
   constexpr int NTX = S::NTX, EC = E / 16, LDX = S::LDX, LDH = S::LDH, LDZ2 = S::LDZ2;
   constexpr int NWV = DA_THREADS / 64;
@@ -1529,13 +1533,14 @@ void da_set_attrs() {
   (void)hipFuncSetAttribute(reinterpret_cast<const void *>(din_att_bwd_kernel<E, H1T, H1K, H2T, H2K>),
                             hipFuncAttributeMaxDynamicSharedMemorySize,
                             static_cast<int>(S::bwd_bytes));
-  (void)hipFuncSetAttribute(reinterpret_cast<const void *>(din_att_bwd2_kernel<E, H1T, H1K, H2T, H2K>),
-                            hipFuncAttributeMaxDynamicSharedMemorySize,
-                            static_cast<int>(DaShape2<E, H1T, H1K, H2T, H2K>::bytes));
-  (void)hipFuncSetAttribute(
-      reinterpret_cast<const void *>(din_att_fwd_wave_kernel<E, H1T, H1K, H2T, H2K>),
-      hipFuncAttributeMaxDynamicSharedMemorySize,
-      static_cast<int>(DaShapeF<E, H1T, H1K, H2T, H2K>::bytes));
+  for (const void *k : {reinterpret_cast<const void *>(din_att_bwd2_kernel<E, H1T, H1K, H2T, H2K, false>),
+                        reinterpret_cast<const void *>(din_att_bwd2_kernel<E, H1T, H1K, H2T, H2K, true>)})
+    (void)hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize,
+                              static_cast<int>(DaShape2<E, H1T, H1K, H2T, H2K>::bytes));
+  for (const void *k : {reinterpret_cast<const void *>(din_att_fwd_wave_kernel<E, H1T, H1K, H2T, H2K, false>),
+                        reinterpret_cast<const void *>(din_att_fwd_wave_kernel<E, H1T, H1K, H2T, H2K, true>)})
+    (void)hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize,
+                              static_cast<int>(DaShapeF<E, H1T, H1K, H2T, H2K>::bytes));
   (void)hipGetLastError();
 }
 
@@ -1644,10 +1649,14 @@ mrec_status mrec_din_att_fwd(const void *rows, int64_t ld_rows, const int32_t *h
       din_att_fwd_kernel<e, h1t, h1k, h2t, h2k>                                             \
           <<<dim3(static_cast<unsigned>(grid)), DA_THREADS,                                 \
              DaShape<e, h1t, h1k, h2t, h2k>::fwd_bytes, s>>>(p);                            \
-    else                                                                                    \
-      din_att_fwd_wave_kernel<e, h1t, h1k, h2t, h2k>                                        \
+    else if (const KClock kc = kclock_take(); kc.buf)                                       \
+      din_att_fwd_wave_kernel<e, h1t, h1k, h2t, h2k, true>                                  \
           <<<dim3(static_cast<unsigned>(grid)), DA_THREADS,                                 \
-             DaShapeF<e, h1t, h1k, h2t, h2k>::bytes, s>>>(p);                               \
+             DaShapeF<e, h1t, h1k, h2t, h2k>::bytes, s>>>(p, kc);                           \
+    else                                                                                    \
+      din_att_fwd_wave_kernel<e, h1t, h1k, h2t, h2k, false>                                 \
+          <<<dim3(static_cast<unsigned>(grid)), DA_THREADS,                                 \
+             DaShapeF<e, h1t, h1k, h2t, h2k>::bytes, s>>>(p, kc);                           \
     return launch_status("mrec_din_att_fwd");                                               \
   }
   MREC_DA_SHAPES(X)
@@ -1694,10 +1703,14 @@ mrec_status mrec_din_att_bwd(const void *rows, int64_t ld_rows, int64_t batch, i
       din_att_bwd_kernel<e, h1t, h1k, h2t, h2k>                                             \
           <<<dim3(static_cast<unsigned>(parts)), DA_THREADS,                                \
              DaShape<e, h1t, h1k, h2t, h2k>::bwd_bytes, s>>>(p);                            \
-    else                                                                                    \
-      din_att_bwd2_kernel<e, h1t, h1k, h2t, h2k>                                            \
+    else if (const KClock kc = kclock_take(); kc.buf)                                       \
+      din_att_bwd2_kernel<e, h1t, h1k, h2t, h2k, true>                                      \
           <<<dim3(static_cast<unsigned>(parts)), DA_THREADS,                                \
-             DaShape2<e, h1t, h1k, h2t, h2k>::bytes, s>>>(p);                               \
+             DaShape2<e, h1t, h1k, h2t, h2k>::bytes, s>>>(p, kc);                           \
+    else                                                                                    \
+      din_att_bwd2_kernel<e, h1t, h1k, h2t, h2k, false>                                     \
+          <<<dim3(static_cast<unsigned>(parts)), DA_THREADS,                                \
+             DaShape2<e, h1t, h1k, h2t, h2k>::bytes, s>>>(p, kc);                           \
     return launch_status("mrec_din_att_bwd");                                               \
   }
   MREC_DA_SHAPES(X)

@@ -1027,7 +1027,8 @@ struct DaShape2 : DaShape<E, H1T, H1K, H2T, H2K> {
   static constexpr int nf32 = B::H1N + 2 * B::H2N + 2 * nslot32;
   static constexpr size_t core_bytes = bf_end * 2 + nf32 * 4;
   // per wave: its 16 rows' bf16 gradient staged in LDS so that the rows leave as
-  // whole 16-B pieces (one 2-B store per lane wrote 32-B row pieces: 2x the HBM writes)
+  // whole 16-B pieces (one 2-B store per lane: 8x the store instructions; the PMC
+  // write count is the same either way, the lines merge before HBM)
   static constexpr int SP = E + 8;  // staging row pitch (elements)
   static constexpr size_t stage_off = (core_bytes + 15) / 16 * 16;
   static constexpr size_t bytes = stage_off + (DA_THREADS / 64) * 16 * SP * 2;

@@ -311,6 +311,44 @@ def test_world1_rccl_dp_sharded_deepfm_step_equals_unsharded(gpu, rccl_world1):
         assert torch.equal(va, vb), k
 
 
+def _batches(gpu, n, B=256, seed=90):
+    out = []
+    for s in range(n):
+        data = {f"c_c_C{i}": t for i, t in enumerate(_ids(gpu, B, seed + s))}
+        g = torch.Generator().manual_seed(seed + 50 + s)
+        for i in range(13):
+            data[f"c_n_I{i}"] = torch.rand(B, generator=g).to(gpu)
+        data["label"] = (torch.rand(B, generator=g) < 0.25).to(torch.int32).to(gpu)
+        out.append(data)
+    return out
+
+
+def test_world1_rccl_compact_inline_dense_sgd_bit_identical(gpu, rccl_world1):
+    """ABI 28: a data-parallel dense tower over the compact exchange all-reduces its
+    flat gradient right before the owner apply, and the dense SGD tiles ride in that
+    launch (IModel._dp_inline_sgd -> mrec_emb_bwd_apply_wire_sgd).  Against the
+    separate mrec_sgd_multi launch after the backward (the hook removed): the same
+    losses and parameters bit for bit over three steps, every collective issued."""
+    from pytorchrec_amd.loss import BCEWithLogitsLoss
+    from pytorchrec_amd.sharding import ShardComm
+    a, b = _deepfm(gpu, True), _deepfm(gpu, True)
+    b.load_state_dict(a.state_dict())
+    for m in (a, b):
+        m.embeddings.compact = "always"
+        m.embeddings.comm = ShardComm(force_collectives=True)
+        m.distribute(ShardComm(force_collectives=True))
+        m.compile(torch.optim.SGD(m.get_parameters(), lr=0.05), BCEWithLogitsLoss(), [], gpu)
+    assert getattr(b.embeddings, "dp_inline_sgd", None) is not None
+    del a.embeddings.dp_inline_sgd  # a: the flat step's own mrec_sgd_multi launch
+    batches = _batches(gpu, 3)
+    la = [float(a.train_step(d)["loss"].detach()) for d in batches]
+    lb = [float(b.train_step(d)["loss"].detach()) for d in batches]
+    assert b._dp_sgd_table is not None and a._dp_sgd_table is None  # b went inline
+    assert la == lb
+    for (k, va), vb in zip(a.state_dict().items(), b.state_dict().values()):
+        assert torch.equal(va, vb), k
+
+
 def test_world1_mrec_comm_sharded_step_equals_unsharded(gpu):
     """The C-ABI communicator (mrec_comm_init / mrec_a2a_* / mrec_allreduce_sum_f32,
     RCCL opened by libmrec, no torch.distributed at all) drives the row-sharded +

@@ -23,7 +23,11 @@ def main():
         ids2 = torch.from_numpy(z.astype(np.int32)).cuda()
     else:
         ids2 = torch.randint(0, rows, (B, 26), dtype=torch.int32, device="cuda")
-    idd = _mrec.IdsDesc(None, stacked=ids2)  # [B, 26] int32, as the models pass them
+    if len(sys.argv) > 4 and sys.argv[4] == "cols":  # per-field [B] columns (bench.py's layout)
+        cols = [ids2[:, f].contiguous() for f in range(26)]
+        idd = _mrec.IdsDesc(cols)
+    else:
+        idd = _mrec.IdsDesc(None, stacked=ids2)  # [B, 26] int32
     wsb = _mrec.lib().mrec_emb_bwd_workspace_size(26, B)
     ws = torch.empty(wsb, dtype=torch.uint8, device="cuda")
 

@@ -44,11 +44,14 @@ KERNELS = {"din_att_bwd": "mrec_din_att_bwd", "din_att_fwd": "mrec_din_att_fwd",
            "gather_wire_kernel": "mrec_shard_gather_wire", "wire_move_kernel": "mrec_shard_wire_move",
            "sgd_multi_kernel": "mrec_sgd_multi"}
 
-# the kernel clock's instantiations (template flag KC = true, the last template
-# argument; wire_move<true, true> is the slot exchange's fp32 unpack, not clocked and
-# not on the compact path) run only in bench.py's in-step timing graphs
-_CLOCKED = re.compile(r"(interact_plan_kernel|interact_rec_kernel|apply_hash_kernel|tower_kernel|tower_dw_kernel|"
-                      r"bucketize_dedup_kernel|gather_wire_kernel|wire_move_kernel|sgd_multi_kernel)<[^()]*true>\(")
+# the kernel clock's instantiations (template flag KC = true: the last template
+# argument, the second of the tower kernels'; wire_move<true, true> is the slot
+# exchange's fp32 unpack, not clocked and not on the compact path) run only in
+# bench.py's in-step timing graphs
+_CLOCKED = re.compile(r"(interact_plan_kernel|interact_rec_kernel|apply_hash_kernel|"
+                      r"bucketize_dedup_kernel|gather_wire_kernel|wire_move_kernel|sgd_multi_kernel|"
+                      r"din_att_bwd2_kernel|din_att_fwd_wave_kernel)<[^()]*true>\(|"
+                      r"(tower_kernel|tower_dw_kernel)<\d+, true")  # (KC second: <PF, KC, CROSS / FEED>)
 
 
 def per_kernel(d, counter):

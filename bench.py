@@ -963,7 +963,7 @@ def pcie_inclusive(step, args, sparse, dense_cols, label_col, device):
     torch.cuda.synchronize()
     el = time.perf_counter() - t0
     return {"value": round(n * B / el, 1), "unit": "samples/s", "steps": n,
-            "ms_per_step": round(el / n * 1e3, 4), "h2d_bytes_per_step": ld.layout.slot_bytes,
+            "ms_per_step": round(el / n * 1e3, 4), "h2d_bytes_per_step": ld.layout.record_bytes,
             "feed": f"ColumnarLoader (pytorchrec_amd/loader.py), depth {depth}: one packed pinned "
                     "record per batch read over PCIe by copy workgroups of the step's "
                     "mrec_tower_dw_ex launch (mrec_feed_job, a device cursor), depth - 1 "

@@ -32,7 +32,7 @@
 extern "C" {
 #endif
 
-#define MREC_ABI_VERSION 28
+#define MREC_ABI_VERSION 29
 #define MREC_MAX_TABLES 64      /* tables per table bank / per call */
 #define MREC_BWD_MAX_BATCH 8192  /* lookups per table per plan/apply call */
 #define MREC_BWD_HASH_MAX_BATCH 4096  /* batches up to this use the hash plan */
@@ -1092,7 +1092,20 @@ typedef struct mrec_feed_job_s {
   int64_t record_bytes;
   int64_t n_records;
   uint64_t *d_state;         /* [0] cursor (the record to copy, advanced by one), [1] ticket */
+  /* ABI 29: the record's first widen_bytes (a multiple of 16) hold uint16 values the
+   * copy writes as int32 (zero-extended): the device slot is record_bytes +
+   * widen_bytes long, the rest of the record lands after the widened prefix.  The
+   * loader packs ids below 65,536 this way (a third less PCIe per C2 batch); 0: a
+   * plain copy */
+  int64_t widen_bytes;
 } mrec_feed_job;
+
+/* ABI 29: mrec_batch_stage with a widened uint16 prefix (see mrec_feed_job) */
+mrec_status mrec_batch_stage_ex(void *dst, const void *host_src, int64_t bytes, int64_t widen_bytes,
+                                mrec_stream stream);
+/* ABI 29: a feed job as a launch of its own (mrec_batch_stage_cursor with the job's
+ * widened prefix) */
+mrec_status mrec_batch_stage_job(const mrec_feed_job *job, mrec_stream stream);
 
 /* ------------------------------------------------------------------------- */
 /* CTR head and loss                                                          */

@@ -20,7 +20,7 @@ import torch  # noqa: F401  (must precede the dlopen, see module docstring)
 LIB_DIR = os.path.join(os.path.dirname(os.path.abspath(__file__)), "lib")
 LIB_PATH = os.environ.get("MREC_LIB_PATH") or os.path.join(LIB_DIR, "libmrec.so")
 
-ABI_VERSION = 28
+ABI_VERSION = 29
 MAX_TABLES = 64
 BWD_MAX_BATCH = 8192
 BWD_HASH_MAX_BATCH = 4096  # batches up to this use the hash plan (fusable into a GEMM launch)
@@ -199,10 +199,10 @@ class TowerDwArgs(ctypes.Structure):
 
 
 class FeedJob(ctypes.Structure):
-    """mrec_feed_job (include/mrec.h, ABI 27)."""
+    """mrec_feed_job (include/mrec.h, ABI 27; widen_bytes ABI 29)."""
     _fields_ = [("dst", ctypes.c_void_p), ("host_base", ctypes.c_void_p),
                 ("record_bytes", ctypes.c_int64), ("n_records", ctypes.c_int64),
-                ("d_state", ctypes.c_void_p)]
+                ("d_state", ctypes.c_void_p), ("widen_bytes", ctypes.c_int64)]
 
 
 LAYOUT_ROW, LAYOUT_COL = 0, 1
@@ -302,6 +302,8 @@ SIGNATURES = {
                                             ctypes.POINTER(ctypes.c_int32)]),
     "mrec_batch_stage": (ctypes.c_int, [_vp, _vp, _i64, _vp]),
     "mrec_batch_stage_cursor": (ctypes.c_int, [_vp, _vp, _i64, _i64, _vp, _vp]),
+    "mrec_batch_stage_ex": (ctypes.c_int, [_vp, _vp, _i64, _i64, _vp]),
+    "mrec_batch_stage_job": (ctypes.c_int, [ctypes.POINTER(FeedJob), _vp]),
     "mrec_dcn_cross_bwd_prep": (ctypes.c_int, [_i64, _i64, _vp, _i64, _vp, _i64, _vp, _i64, _vp,
                                                _i64, _vp, _i64, _i32, _vp, _i64, _vp]),
     "mrec_emb_bwd_large_workspace_size": (ctypes.c_size_t, [_bank_p, _i64]),

@@ -16,19 +16,28 @@
 
 namespace mrec {
 
-__global__ __launch_bounds__(256) void batch_stage_kernel(const uint4 *__restrict__ src,
-                                                          uint4 *__restrict__ dst, int64_t n16) {
+__global__ __launch_bounds__(256) void batch_stage_kernel(const feed_u32x4 *__restrict__ src,
+                                                          feed_u32x4 *__restrict__ dst, int64_t n16,
+                                                          int64_t w16) {
   constexpr int U = 4;  // independent 16-B loads per lane per trip
   const int64_t stride = static_cast<int64_t>(gridDim.x) * 256;
   int64_t i = static_cast<int64_t>(blockIdx.x) * 256 + threadIdx.x;
-  for (; i + (U - 1) * stride < n16; i += U * stride) {
-    uint4 v[U];
+  for (; i < n16; i += U * stride) {  // (as feed_copy_body_u: U loads on every trip)
+    feed_u32x4 v[U];
 #pragma unroll
-    for (int u = 0; u < U; ++u) v[u] = src[i + u * stride];
+    for (int u = 0; u < U; ++u) {
+      const int64_t p = i + u * stride;
+      v[u] = src[p < n16 ? p : n16 - 1];
+    }
 #pragma unroll
-    for (int u = 0; u < U; ++u) dst[i + u * stride] = v[u];
+    for (int u = 0; u < U; ++u) {
+      const int64_t p = i + u * stride;
+      if (p < w16)
+        feed_widen(dst, p, v[u]);
+      else if (p < n16)
+        dst[p + w16] = v[u];
+    }
   }
-  for (; i < n16; i += stride) dst[i] = src[i];
 }
 
 __global__ __launch_bounds__(256) void batch_stage_cursor_kernel(FeedCopy fc) {
@@ -66,6 +75,9 @@ mrec_status build_feed_copy(const mrec_feed_job *job, int threads, FeedCopy *out
       return MREC_EINVAL;
     }
   }
+  MREC_CHECK_ARG(j.widen_bytes >= 0 && j.widen_bytes % 16 == 0 && j.widen_bytes <= j.record_bytes,
+                 "feed job: widen_bytes must be a multiple of 16 within the record");
+  out->w16 = j.widen_bytes / 16;
   out->src = dev_base;
   out->record_bytes = j.record_bytes;
   out->n_records = j.n_records;
@@ -91,7 +103,14 @@ using namespace mrec;
 extern "C" {
 
 mrec_status mrec_batch_stage(void *dst, const void *host_src, int64_t bytes, mrec_stream stream) {
+  return mrec_batch_stage_ex(dst, host_src, bytes, 0, stream);
+}
+
+mrec_status mrec_batch_stage_ex(void *dst, const void *host_src, int64_t bytes, int64_t widen_bytes,
+                                mrec_stream stream) {
   MREC_CHECK_ARG(bytes >= 0, "bytes < 0");
+  MREC_CHECK_ARG(widen_bytes >= 0 && widen_bytes % 16 == 0 && widen_bytes <= bytes,
+                 "widen_bytes must be a multiple of 16 within bytes");
   MREC_CHECK_ARG(bytes == 0 || (dst != nullptr && host_src != nullptr), "NULL pointer");
   MREC_CHECK_ARG(bytes % 16 == 0 && (reinterpret_cast<uintptr_t>(dst) & 15) == 0 &&
                      (reinterpret_cast<uintptr_t>(host_src) & 15) == 0,
@@ -111,18 +130,23 @@ mrec_status mrec_batch_stage(void *dst, const void *host_src, int64_t bytes, mre
   const int64_t blocks = std::min<int64_t>((n16 + 1023) / 1024, 1024);
   batch_stage_kernel<<<dim3(static_cast<unsigned>(std::max<int64_t>(blocks, 1))), 256, 0,
                        static_cast<hipStream_t>(stream)>>>(
-      static_cast<const uint4 *>(host_src), static_cast<uint4 *>(dst), n16);
+      static_cast<const feed_u32x4 *>(host_src), static_cast<feed_u32x4 *>(dst), n16,
+      widen_bytes / 16);
   return launch_status("mrec_batch_stage");
 }
 
 mrec_status mrec_batch_stage_cursor(void *dst, const void *host_base, int64_t record_bytes,
                                     int64_t n_records, uint64_t *d_state, mrec_stream stream) {
-  const mrec_feed_job job{dst, host_base, record_bytes, n_records, d_state};
+  const mrec_feed_job job{dst, host_base, record_bytes, n_records, d_state, 0};
+  return mrec_batch_stage_job(&job, stream);
+}
+
+mrec_status mrec_batch_stage_job(const mrec_feed_job *job, mrec_stream stream) {
   FeedCopy fc;
-  if (mrec_status st = build_feed_copy(&job, 256, &fc); st != MREC_OK) return st;
+  if (mrec_status st = build_feed_copy(job, 256, &fc); st != MREC_OK) return st;
   batch_stage_cursor_kernel<<<dim3(static_cast<unsigned>(fc.blocks)), 256, 0,
                               static_cast<hipStream_t>(stream)>>>(fc);
-  return launch_status("mrec_batch_stage_cursor");
+  return launch_status("mrec_batch_stage_job");
 }
 
 }  // extern "C"

@@ -35,7 +35,9 @@ requested (its slot is then refilled); ``clone()`` what must outlive that.
 """
 from __future__ import annotations
 
+import ctypes
 import math
+import os
 from typing import Dict, Iterator, List, Mapping, Optional, Sequence, Tuple
 
 import numpy as np
@@ -113,23 +115,45 @@ class ColumnarDataset(torch.utils.data.Dataset):
 
 class PackedLayout:
     """Byte layout of one batch record: per column a 256-B aligned segment
-    ``[batch, *trailing]`` of the column's dtype."""
+    ``[batch, *trailing]`` of the column's dtype.
 
-    def __init__(self, dataset: ColumnarDataset, batch: int):
+    ``narrow`` (a kernel-copied GPU loader, ABI 29): the leading int32 ``[N]`` columns
+    whose values all lie in [0, 65536) -- the ids of tables up to 65,536 rows -- are
+    packed as 16-bit values in the HOST record and widened back to int32 by the copy
+    into the device slot (``mrec_feed_job.widen_bytes``): a third less PCIe per C2
+    batch.  Such a column's device segment is twice its host segment, so the widened
+    prefix maps 1:2 and everything after it lands ``widen_bytes`` further on.
+    ``record_bytes``: the host record; ``slot_bytes``: the device slot (the batch
+    dict's views)."""
+
+    def __init__(self, dataset: ColumnarDataset, batch: int, narrow: bool = False):
         self.batch = int(batch)
         self.dense_group = list(dataset.dense_group)
-        self.segments = []  # (name, dtype, trailing shape, byte offset, bytes per sample)
+        # (name, dtype, trailing shape, device byte offset, bytes per sample, narrow)
+        self.segments = []
         off = 0
+        self.widen_bytes = 0
+        prefix = bool(narrow)
         for name, t in dataset.sources():
             per = t.element_size() * int(math.prod(t.shape[1:]))
-            self.segments.append((name, t.dtype, tuple(t.shape[1:]), off, per))
-            off += (per * self.batch + _ALIGN - 1) // _ALIGN * _ALIGN
+            nar = (prefix and t.dtype == torch.int32 and t.dim() == 1 and t.numel() > 0
+                   and int(t.min()) >= 0 and int(t.max()) < 65536)
+            prefix = nar  # only a leading run of columns is widened
+            self.segments.append((name, t.dtype, tuple(t.shape[1:]), off, per, nar))
+            if nar:
+                hseg = (2 * self.batch + _ALIGN - 1) // _ALIGN * _ALIGN
+                self.widen_bytes += hseg
+                off += 2 * hseg
+            else:
+                off += (per * self.batch + _ALIGN - 1) // _ALIGN * _ALIGN
         self.slot_bytes = max(off, _ALIGN)
+        self.record_bytes = max(off - self.widen_bytes, _ALIGN)
 
     def views(self, record: Tensor, n: int) -> Dict[str, Tensor]:
-        """The batch dict over one packed record (uint8 ``[slot_bytes]``), first n samples."""
+        """The batch dict over one DEVICE slot (uint8 ``[slot_bytes]``), first n
+        samples (without narrow columns a host record is the same layout)."""
         out = {}
-        for name, dt, trail, off, per in self.segments:
+        for name, dt, trail, off, per, _ in self.segments:
             out[name] = record[off:off + per * self.batch].view(dt).view(self.batch, *trail)[:n]
         if "__dense__" in out:
             d = out["__dense__"]
@@ -139,15 +163,20 @@ class PackedLayout:
 
     def pack(self, dataset: ColumnarDataset, order: Optional[Tensor], out: Tensor, n_batches: int):
         """Write the dataset (rows in ``order``, or in storage order) batch-major into
-        ``out`` (uint8 ``[>= n_batches, slot_bytes]``).  Bytes past the dataset's
+        ``out`` (uint8 ``[>= n_batches, record_bytes]``).  Bytes past the dataset's
         end in the last record are left as they are (views cut at n)."""
         N, B = dataset.n, self.batch
         full, rem = divmod(min(N, n_batches * B), B)
         srcs = dict(dataset.sources())
-        for name, dt, trail, off, per in self.segments:
+        for name, dt, trail, off, per, nar in self.segments:
             src = srcs[name]
             if order is not None:
                 src = src.index_select(0, order)
+            if nar:  # 16-bit in the host record (the uint16 bit pattern as int16)
+                off, per, dt = off // 2, 2, torch.int16
+                src = torch.where(src >= 32768, src - 65536, src).to(torch.int16)
+            elif self.widen_bytes:
+                off -= self.widen_bytes
             dst = out[:n_batches, off:off + per * B].view(dt).view(n_batches, B, *trail)
             if full:
                 dst[:full].copy_(src[:full * B].view(full, B, *trail))
@@ -185,7 +214,10 @@ class ColumnarLoader:
         self.copy = copy
         self.side_stream = copy == "side"
         self.epoch = 0
-        self.layout = PackedLayout(dataset, self.batch_size)
+        # 16-bit ids in the host records when the copy is a kernel that widens them
+        narrow = (self.device.type == "cuda" and copy == "kernel"
+                  and os.environ.get("MREC_FEED_NARROW", "1") != "0")
+        self.layout = PackedLayout(dataset, self.batch_size, narrow=narrow)
         self._host: Optional[Tensor] = None
         self._packed: Optional[List[int]] = None  # batch sizes of a prepared epoch
         self._slots: Optional[Tensor] = None
@@ -224,7 +256,7 @@ class ColumnarLoader:
             if self._reading is not None:
                 self._reading.synchronize()  # enqueued copies of the last epoch read the buffer
             if self._host is None or self._host.shape[0] < nb:
-                self._host = torch.empty(nb, self.layout.slot_bytes, dtype=torch.uint8,
+                self._host = torch.empty(nb, self.layout.record_bytes, dtype=torch.uint8,
                                          pin_memory=self.device.type == "cuda")
             self.layout.pack(self.dataset, self._order(), self._host, nb)
             self.epoch += 1
@@ -269,9 +301,9 @@ class ColumnarLoader:
                 while issued < min(len(sizes), i + self.depth):
                     s = issued % self.depth
                     if self.copy == "kernel":  # stream order alone protects the slot
-                        _mrec.call("mrec_batch_stage", self._slots[s].data_ptr(),
-                                   host[issued].data_ptr(), self.layout.slot_bytes,
-                                   _mrec.stream_handle(self.device))
+                        _mrec.call("mrec_batch_stage_ex", self._slots[s].data_ptr(),
+                                   host[issued].data_ptr(), self.layout.record_bytes,
+                                   self.layout.widen_bytes, _mrec.stream_handle(self.device))
                         self._reading.record(torch.cuda.current_stream(self.device))
                     elif self.copy == "dma":
                         self._slots[s].copy_(host[issued], non_blocking=True)
@@ -313,8 +345,9 @@ class ColumnarLoader:
         g = torch.cuda.CUDAGraph()
         host = self._host
         jobs = [_mrec.FeedJob(self._slots[(j + self.depth - 1) % self.depth].data_ptr(),
-                              host.data_ptr(), self.layout.slot_bytes, host.shape[0],
-                              state.data_ptr()) for j in range(self.depth)]
+                              host.data_ptr(), self.layout.record_bytes, host.shape[0],
+                              state.data_ptr(), self.layout.widen_bytes)
+                for j in range(self.depth)]
         try:
             with torch.cuda.graph(g, capture_error_mode="thread_local"):
                 for j in range(self.depth):
@@ -322,8 +355,7 @@ class ColumnarLoader:
                     step(self.layout.views(self._slots[j], self.batch_size))
                     left = dense_ops.take_feed_job()
                     if left is not None:  # no tower weight-gradient launch in this step
-                        _mrec.call("mrec_batch_stage_cursor", left.dst, left.host_base,
-                                   left.record_bytes, left.n_records, left.d_state,
+                        _mrec.call("mrec_batch_stage_job", ctypes.byref(left),
                                    _mrec.stream_handle(self.device))
         finally:
             # a step that raised mid-capture leaves its job set: the next eager
@@ -367,8 +399,9 @@ class GraphEpoch:
         ld._iterating = True
         try:
             for j in range(min(d - 1, len(sizes))):
-                _mrec.call("mrec_batch_stage", ld._slots[j].data_ptr(), ld._host[j].data_ptr(),
-                           ld.layout.slot_bytes, _mrec.stream_handle(ld.device))
+                _mrec.call("mrec_batch_stage_ex", ld._slots[j].data_ptr(), ld._host[j].data_ptr(),
+                           ld.layout.record_bytes, ld.layout.widen_bytes,
+                           _mrec.stream_handle(ld.device))
             self.state.zero_()
             self.state[0] = d - 1
             for r in range(len(sizes) // d):

@@ -266,3 +266,39 @@ def test_gpu_graph_epochs_stage_on_a_branch_bit_exact(gpu):
                 assert torch.equal(seen[j].cpu(), want["c_c_C0"]), (e, first, j)
                 wd = torch.stack([want[f"c_n_I{k}"] for k in range(N_DENSE)], 1)
                 assert torch.equal(dense[j].cpu(), wd), (e, first, j)
+
+
+@pytest.mark.parametrize("batch", [32, 130, 4096])
+def test_narrow_record_widened_equals_the_batch(batch):
+    """ABI 29: a kernel-copied GPU loader packs the leading int32 [N] columns whose
+    values fit 16 bits (ids, labels) as 16-bit values in the host record and the copy
+    widens them into the device slot (mrec_feed_job.widen_bytes).  Restated on the
+    CPU: widening the host record's prefix 1:2 (zero-extended) and moving the rest
+    by widen_bytes gives a slot whose views are exactly the batch; ids of 65,535 and
+    a column past 16 bits stay correct (the latter is not narrowed)."""
+    from pytorchrec_amd.loader import PackedLayout
+    n = batch + 7
+    cols = _columns(n, seed=5)
+    cols["c_c_C0"][:3] = torch.tensor([65535, 32768, 0])  # the 16-bit extremes
+    cols["c_c_big"] = torch.randint(0, 1 << 20, (n,), dtype=torch.int64)
+    ds = ColumnarDataset(cols, dense_group=[f"c_n_I{j}" for j in range(N_DENSE)])
+    lay = PackedLayout(ds, batch, narrow=True)
+    wide = PackedLayout(ds, batch, narrow=False)
+    assert 0 < lay.widen_bytes and lay.widen_bytes % 16 == 0
+    assert lay.record_bytes + lay.widen_bytes == lay.slot_bytes
+    assert lay.record_bytes <= wide.slot_bytes
+    host = torch.zeros(1, lay.record_bytes, dtype=torch.uint8)
+    lay.pack(ds, None, host, 1)
+    h = host[0].numpy()
+    w = lay.widen_bytes
+    slot = np.zeros(lay.slot_bytes, dtype=np.uint8)
+    slot[:2 * w].view(np.int32)[:] = h[:w].view(np.uint16).astype(np.int32)
+    slot[2 * w:] = h[w:]
+    got = lay.views(torch.from_numpy(slot), batch)
+    want = _expected(cols, torch.arange(batch))
+    for k, v in want.items():
+        if k.startswith("c_n_I"):
+            continue
+        assert torch.equal(got[k], v), k
+    narrowed = [name for name, *_, nar in lay.segments if nar]
+    assert "c_c_C0" in narrowed and "c_c_big" not in narrowed

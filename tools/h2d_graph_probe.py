@@ -29,7 +29,7 @@ def main():
     for s, _ in ld.iter_slots():
         step(ld.slot_views(s))
     host = ld._host  # packed epoch (pinned)
-    nbytes = ld.layout.slot_bytes
+    nbytes = ld.layout.record_bytes
     staging = torch.empty(2, nbytes, dtype=torch.uint8, pin_memory=True)
     cur = torch.cuda.current_stream()
     side = torch.cuda.Stream()
@@ -41,13 +41,14 @@ def main():
             cs = torch.cuda.current_stream()
             side.wait_stream(cs)
             with torch.cuda.stream(side):  # branch: stage batch j+1 into the other slot
-                _mrec.call("mrec_batch_stage", ld._slots[1 - k].data_ptr(), staging[k].data_ptr(),
-                           nbytes, side.cuda_stream)
+                _mrec.call("mrec_batch_stage_ex", ld._slots[1 - k].data_ptr(),
+                           staging[k].data_ptr(), nbytes, ld.layout.widen_bytes, side.cuda_stream)
             step(ld.slot_views(k))
             cs.wait_stream(side)
         graphs.append(gr)
     done = [torch.cuda.Event(), torch.cuda.Event()]
-    ld._slots[0].copy_(host[0])
+    _mrec.call("mrec_batch_stage_ex", ld._slots[0].data_ptr(), host[0].data_ptr(), nbytes,
+               ld.layout.widen_bytes, cur.cuda_stream)
     torch.cuda.synchronize()
     t = time.perf_counter()
     for j in range(nb):
